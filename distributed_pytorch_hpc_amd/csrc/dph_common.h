@@ -1,0 +1,88 @@
+// Shared device helpers for the CDNA4 (gfx950 / MI355X) kernels of distributed_pytorch_hpc_amd.
+//
+// Conventions used by every kernel in csrc/:
+//   * wave = 64 lanes; all wave-level reductions below are written for 64 lanes.
+//   * bf16 is handled as raw 16-bit storage (`__bf16` arithmetic type of amdclang); loads and stores
+//     are vectorised to 16 B per lane (8 bf16 / 4 fp32), the coalescing sweet spot on CDNA4.
+//   * fp32 accumulation everywhere; fp32 -> bf16 conversion is a plain cast (RNE, NaN preserving,
+//     lowered to v_cvt_pk_bf16_f32).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace dph {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 8-element vector load/store with fp32 conversion, for T in {float, bf16}.
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16> {
+  static __device__ __forceinline__ void load(const bf16* p, float (&o)[8]) {
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (float)v[i];
+  }
+  static __device__ __forceinline__ void store(bf16* p, const float (&o)[8]) {
+    bf16x8 v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (bf16)o[i];
+    *reinterpret_cast<bf16x8*>(p) = v;
+  }
+};
+template <> struct Vec8<float> {
+  static __device__ __forceinline__ void load(const float* p, float (&o)[8]) {
+    f32x4 a = *reinterpret_cast<const f32x4*>(p);
+    f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { o[i] = a[i]; o[i + 4] = b[i]; }
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&o)[8]) {
+    f32x4 a, b;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { a[i] = o[i]; b[i] = o[i + 4]; }
+    *reinterpret_cast<f32x4*>(p) = a;
+    *reinterpret_cast<f32x4*>(p + 4) = b;
+  }
+};
+
+template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T)v; }
+
+__host__ __device__ __forceinline__ int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Grid size for memory-bound grid-stride kernels: enough workgroups to fill 256 CUs x 8 resident.
+__host__ __forceinline__ int stream_grid(int64_t work_items, int per_block) {
+  int64_t g = cdiv(work_items, per_block);
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace dph
+
+#define DPH_DISPATCH_FLOAT(dt, T, ...)                       \
+  do {                                                       \
+    if ((dt) == dph::kBF16) { typedef dph::bf16 T; __VA_ARGS__; } \
+    else { typedef float T; __VA_ARGS__; }                   \
+  } while (0)

@@ -1,0 +1,93 @@
+// Host-side launcher API of the HIP kernels (device code lives in csrc/*.hip).
+// Pointers are device pointers; every launcher enqueues on `stream` and never synchronises, so all
+// of them are safe inside hipGraph capture.  dtype codes: dph::DType (0 = fp32, 1 = bf16).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dph {
+
+enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+
+// ---- RMSNorm (fsdp_tp/llama2_model.py:115-142 semantics: fp32 statistics, eps inside rsqrt) ----
+void rmsnorm_fwd(const void* x, const void* w, const void* residual, void* h_out, void* y, float* rstd,
+                 int64_t rows, int dim, float eps, int x_dtype, int w_dtype, hipStream_t stream);
+// dx (x dtype) and dw_partial (fp32 [nblk, dim]) then dw (w dtype) by a column reduction.
+void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx, float* dw_partial,
+                 void* dw, int nblk, int64_t rows, int dim, int x_dtype, int w_dtype, hipStream_t stream);
+int rmsnorm_bwd_blocks(int64_t rows);
+
+// ---- LayerNorm (nn.LayerNorm semantics, used by ViT / pipeline transformer) ----
+void layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int64_t rows,
+                   int dim, float eps, int x_dtype, int w_dtype, hipStream_t stream);
+void layernorm_bwd(const void* dy, const void* x, const void* w, const float* mean, const float* rstd, void* dx,
+                   float* dwb_partial, void* dw, void* db, int nblk, int64_t rows, int dim, int x_dtype,
+                   int w_dtype, hipStream_t stream);
+
+// ---- RoPE, interleaved pairs (llama2_model.py:74-100), in place on a [B,S,H,hd] strided view ----
+void rope_apply(void* x, const float* cos_t, const float* sin_t, int64_t B, int64_t S, int64_t H, int hd,
+                int64_t sb, int64_t ss, int64_t sh, int64_t pos_offset, int inverse, int dtype, hipStream_t stream);
+
+// ---- SwiGLU on the fused [N, 2F] = [w1 x | w3 x] GEMM output (llama2_model.py:266-267) ----
+void swiglu_fwd(const void* x2, void* y, int64_t n, int64_t f, int64_t ld_x2, int dtype, hipStream_t stream);
+void swiglu_bwd(const void* dy, const void* x2, void* dx2, int64_t n, int64_t f, int64_t ld_x2, int dtype,
+                hipStream_t stream);
+
+// ---- GELU (tanh / erf) fwd/bwd, elementwise ----
+void gelu_fwd(const void* x, void* y, int64_t n, int approximate_tanh, int dtype, hipStream_t stream);
+void gelu_bwd(const void* dy, const void* x, void* dx, int64_t n, int approximate_tanh, int dtype,
+              hipStream_t stream);
+
+// ---- Fused AdamW over flat buffers (torch.optim.AdamW semantics, decoupled weight decay) ----
+//   master/m/v: fp32 [n]; grad: grad_dtype [n]; param_out (optional): param_dtype [n] (rounded copy of master).
+//   grad_scale_ptr (optional device fp32 scalar) multiplies the gradient (global-norm clipping, 1/world).
+void adamw_step(float* master, float* m, float* v, const void* grad, void* param_out, int64_t n, float lr,
+                float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2,
+                const float* grad_scale_ptr, int grad_dtype, int param_dtype, hipStream_t stream);
+// ---- Fused SGD with momentum (torch.optim.SGD semantics) ----
+void sgd_step(float* master, float* momentum_buf, const void* grad, void* param_out, int64_t n, float lr,
+              float momentum, float dampening, float weight_decay, int nesterov, int first_step,
+              const float* grad_scale_ptr, int grad_dtype, int param_dtype, hipStream_t stream);
+// sum of squares of a flat buffer, accumulated (atomically, fp32) into *out (caller zeroes it).
+void sumsq(const void* x, int64_t n, float* out, int dtype, hipStream_t stream);
+
+// ---- Fused softmax cross-entropy over [N, V] logits (mean over non-ignored rows) ----
+//   loss_rows: fp32 [N]; if grad_inplace, logits are overwritten with d(mean loss)/d(logits)
+//   using the device scalar *inv_count (1 / number of non-ignored rows).
+void cross_entropy_fwd(void* logits, const int64_t* target, float* loss_rows, float* lse_rows,
+                       const float* inv_count, int64_t n, int64_t v, int64_t ld, int64_t ignore_index,
+                       int grad_inplace, float label_smoothing, int dtype, hipStream_t stream);
+
+// ---- Flash attention (causal / full, GQA), bf16, head_dim in {32, 64, 128} ----
+//   q: [B, Sq, Hq, D], k/v: [B, Sk, Hkv, D] with arbitrary batch/seq/head strides (last dim contiguous),
+//   o: [B, Sq, Hq, D] contiguous, lse: fp32 [B, Hq, Sq] (natural log, includes the softmax scale).
+struct AttnParams {
+  const void* q; const void* k; const void* v; void* o; float* lse;
+  int64_t q_sb, q_ss, q_sh, k_sb, k_ss, k_sh, v_sb, v_ss, v_sh, o_sb, o_ss, o_sh;
+  int B, Sq, Sk, Hq, Hkv, D;
+  float scale;
+  int causal;
+  // causal offset: query i attends keys j <= i + (Sk - Sq) (bottom-right aligned, as flash-attn).
+};
+void flash_attn_fwd(const AttnParams& p, hipStream_t stream);
+
+struct AttnBwdParams {
+  AttnParams f;
+  const void* dout; int64_t do_sb, do_ss, do_sh;
+  float* delta;          // fp32 [B, Hq, Sq] workspace: rowsum(dO * O)
+  float* dq_accum;       // fp32 [B, Sq, Hq, D] workspace, zeroed by the launcher
+  void* dq; void* dk; void* dv;   // bf16, [B,S,H,D] contiguous; dk/dv are per KV head (GQA summed)
+  float* dk_accum; float* dv_accum; // fp32 [B, Sk, Hkv, D] when Hq != Hkv (GQA), else null
+};
+void flash_attn_bwd(const AttnBwdParams& p, hipStream_t stream);
+
+// ---- Embedding gather / scatter-add backward (vocab-sharded friendly: out-of-range ids -> zero row) ----
+void embedding_fwd(const int64_t* ids, const void* table, void* out, int64_t n, int64_t dim, int64_t vocab_start,
+                   int64_t vocab_local, int dtype, hipStream_t stream);
+void embedding_bwd(const int64_t* ids, const void* dout, float* dtable_f32, int64_t n, int64_t dim,
+                   int64_t vocab_start, int64_t vocab_local, int dtype, hipStream_t stream);
+
+// ---- cast / scale helpers ----
+void cast_copy(const void* src, void* dst, int64_t n, int src_dtype, int dst_dtype, float scale, hipStream_t stream);
+
+}  // namespace dph

@@ -1,0 +1,361 @@
+// PyTorch dispatcher registration of the CDNA4 kernels as `torch.ops.dph.*` (HIP dispatch key = "CUDA"
+// on ROCm builds).  Shape/meta functions live in distributed_pytorch_hpc_amd/ops/_meta.py, autograd in
+// ops/*.py.  Every op validates its operands on the host (shape, dtype, contiguity, alignment) before a
+// launch, so a kernel never sees a layout it was not written for.
+#include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include "kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dt_code(const Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return dph::kBF16;
+  if (t.scalar_type() == at::kFloat) return dph::kF32;
+  TORCH_CHECK(false, "dph: unsupported dtype ", t.scalar_type(), " (fp32 / bf16 only)");
+}
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "dph: ", name, " must be a GPU tensor");
+}
+void check_align16(const Tensor& t, const char* name) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "dph: ", name, " must be 16-byte aligned");
+}
+
+// ------------------------------------------------------------------------------------------------ RMSNorm
+std::tuple<Tensor, Tensor, Tensor> rmsnorm_fwd(const Tensor& x, const Tensor& w, double eps,
+                                               const c10::optional<Tensor>& residual) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "rmsnorm: contiguous operands required");
+  const int64_t D = x.size(-1);
+  TORCH_CHECK(w.numel() == D && D % 8 == 0, "rmsnorm: dim must match weight and be a multiple of 8");
+  const int64_t rows = x.numel() / D;
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  Tensor h;
+  const void* res = nullptr;
+  if (residual.has_value()) {
+    TORCH_CHECK(residual->is_contiguous() && residual->sizes() == x.sizes() &&
+                residual->scalar_type() == x.scalar_type(), "rmsnorm: residual must match x");
+    h = at::empty_like(x);
+    res = residual->data_ptr();
+  } else {
+    h = at::empty({0}, x.options());
+  }
+  check_align16(x, "x");
+  dph::rmsnorm_fwd(x.data_ptr(), w.data_ptr(), res, res ? h.data_ptr() : nullptr, y.data_ptr(),
+                   rstd.data_ptr<float>(), rows, (int)D, (float)eps, dt_code(x), dt_code(w), cur_stream());
+  return {y, rstd, h};
+}
+
+std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& rstd) {
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && w.is_contiguous(), "rmsnorm_bwd: contiguous required");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "rmsnorm_bwd: dy/x dtype mismatch");
+  const int64_t D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  auto dx = at::empty_like(x);
+  auto dw = at::empty_like(w);
+  if (rows == 0) return {dx, dw.zero_()};
+  const int nblk = dph::rmsnorm_bwd_blocks(rows);
+  auto part = at::empty({nblk, D}, x.options().dtype(at::kFloat));
+  dph::rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dx.data_ptr(),
+                   part.data_ptr<float>(), dw.data_ptr(), nblk, rows, (int)D, dt_code(x), dt_code(w), cur_stream());
+  return {dx, dw};
+}
+
+// ------------------------------------------------------------------------------------------------ LayerNorm
+std::tuple<Tensor, Tensor, Tensor> layernorm_fwd(const Tensor& x, const Tensor& w, const Tensor& b, double eps) {
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && b.is_contiguous(), "layernorm: contiguous required");
+  const int64_t D = x.size(-1);
+  TORCH_CHECK(w.numel() == D && b.numel() == D && D % 8 == 0 && D <= 8192, "layernorm: bad dim");
+  TORCH_CHECK(w.scalar_type() == b.scalar_type(), "layernorm: weight/bias dtype mismatch");
+  const int64_t rows = x.numel() / D;
+  auto y = at::empty_like(x);
+  auto mean = at::empty({rows}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  dph::layernorm_fwd(x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), rows, (int)D, (float)eps, dt_code(x), dt_code(w), cur_stream());
+  return {y, mean, rstd};
+}
+
+std::tuple<Tensor, Tensor, Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w,
+                                                 const Tensor& mean, const Tensor& rstd) {
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous(), "layernorm_bwd: contiguous required");
+  const int64_t D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  auto dx = at::empty_like(x);
+  auto dw = at::empty_like(w);
+  auto db = at::empty_like(w);
+  if (rows == 0) return {dx, dw.zero_(), db.zero_()};
+  const int nblk = dph::rmsnorm_bwd_blocks(rows);
+  auto part = at::empty({nblk, 2 * D}, x.options().dtype(at::kFloat));
+  dph::layernorm_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                     dx.data_ptr(), part.data_ptr<float>(), dw.data_ptr(), db.data_ptr(), nblk, rows, (int)D,
+                     dt_code(x), dt_code(w), cur_stream());
+  return {dx, dw, db};
+}
+
+// ------------------------------------------------------------------------------------------------ RoPE
+void rope_(Tensor x, const Tensor& cos_t, const Tensor& sin_t, int64_t pos_offset, bool inverse) {
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.dim() == 4, "rope: x must be [B, S, H, hd]");
+  TORCH_CHECK(x.stride(3) == 1, "rope: head dim must be contiguous");
+  const int64_t hd = x.size(3);
+  TORCH_CHECK(hd % 8 == 0, "rope: head dim must be a multiple of 8");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
+              sin_t.is_contiguous() && cos_t.size(-1) == hd / 2, "rope: tables must be fp32 [S, hd/2]");
+  TORCH_CHECK(pos_offset + x.size(1) <= cos_t.size(0), "rope: position table too short");
+  TORCH_CHECK(x.stride(0) % 8 == 0 && x.stride(1) % 8 == 0 && x.stride(2) % 8 == 0, "rope: strides must be x8");
+  check_align16(x, "x");
+  dph::rope_apply(x.data_ptr(), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), x.size(0), x.size(1), x.size(2),
+                  (int)hd, x.stride(0), x.stride(1), x.stride(2), pos_offset, inverse ? 1 : 0, dt_code(x),
+                  cur_stream());
+}
+
+// ------------------------------------------------------------------------------------------------ SwiGLU
+Tensor swiglu_fwd(const Tensor& x2) {
+  c10::DeviceGuard g(x2.device());
+  TORCH_CHECK(x2.is_contiguous(), "swiglu: contiguous input required");
+  const int64_t two_f = x2.size(-1);
+  TORCH_CHECK(two_f % 16 == 0, "swiglu: hidden must be a multiple of 8");
+  const int64_t f = two_f / 2, n = x2.numel() / two_f;
+  auto sizes = x2.sizes().vec();
+  sizes.back() = f;
+  auto y = at::empty(sizes, x2.options());
+  dph::swiglu_fwd(x2.data_ptr(), y.data_ptr(), n, f, two_f, dt_code(x2), cur_stream());
+  return y;
+}
+Tensor swiglu_bwd(const Tensor& dy, const Tensor& x2) {
+  c10::DeviceGuard g(x2.device());
+  TORCH_CHECK(x2.is_contiguous() && dy.is_contiguous(), "swiglu_bwd: contiguous required");
+  const int64_t two_f = x2.size(-1), f = two_f / 2, n = x2.numel() / two_f;
+  auto dx2 = at::empty_like(x2);
+  dph::swiglu_bwd(dy.data_ptr(), x2.data_ptr(), dx2.data_ptr(), n, f, two_f, dt_code(x2), cur_stream());
+  return dx2;
+}
+
+// ------------------------------------------------------------------------------------------------ GELU
+Tensor gelu_fwd(const Tensor& x, bool tanh_form) {
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 8 == 0, "gelu: contiguous, numel % 8 == 0 required");
+  auto y = at::empty_like(x);
+  dph::gelu_fwd(x.data_ptr(), y.data_ptr(), x.numel(), tanh_form ? 1 : 0, dt_code(x), cur_stream());
+  return y;
+}
+Tensor gelu_bwd(const Tensor& dy, const Tensor& x, bool tanh_form) {
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.is_contiguous() && dy.is_contiguous(), "gelu_bwd: contiguous required");
+  auto dx = at::empty_like(x);
+  dph::gelu_bwd(dy.data_ptr(), x.data_ptr(), dx.data_ptr(), x.numel(), tanh_form ? 1 : 0, dt_code(x), cur_stream());
+  return dx;
+}
+
+// ------------------------------------------------------------------------------------------------ optimizers
+void adamw_step_(Tensor master, Tensor m, Tensor v, const Tensor& grad, const c10::optional<Tensor>& param_out,
+                 double lr, double b1, double b2, double eps, double wd, double bc1, double bc2,
+                 const c10::optional<Tensor>& grad_scale) {
+  c10::DeviceGuard g(master.device());
+  const int64_t n = master.numel();
+  TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
+              "adamw: master/m/v must be fp32");
+  TORCH_CHECK(m.numel() == n && v.numel() == n && grad.numel() == n, "adamw: size mismatch");
+  TORCH_CHECK(master.is_contiguous() && m.is_contiguous() && v.is_contiguous() && grad.is_contiguous(),
+              "adamw: contiguous buffers required");
+  check_align16(master, "master"); check_align16(m, "m"); check_align16(v, "v");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(grad.data_ptr()) % 8 == 0, "adamw: grad must be 8-byte aligned");
+  void* pout = nullptr;
+  int pdt = dph::kBF16;
+  if (param_out.has_value()) {
+    TORCH_CHECK(param_out->numel() == n && param_out->is_contiguous(), "adamw: param_out mismatch");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(param_out->data_ptr()) % 8 == 0, "adamw: param_out alignment");
+    pout = param_out->data_ptr();
+    pdt = dt_code(*param_out);
+  }
+  const float* gs = grad_scale.has_value() ? grad_scale->data_ptr<float>() : nullptr;
+  dph::adamw_step(master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), grad.data_ptr(), pout, n,
+                  (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, gs, dt_code(grad),
+                  pdt, cur_stream());
+}
+
+void sgd_step_(Tensor master, Tensor buf, const Tensor& grad, const c10::optional<Tensor>& param_out, double lr,
+               double momentum, double dampening, double wd, bool nesterov, bool first_step,
+               const c10::optional<Tensor>& grad_scale) {
+  c10::DeviceGuard g(master.device());
+  const int64_t n = master.numel();
+  TORCH_CHECK(master.scalar_type() == at::kFloat && buf.scalar_type() == at::kFloat, "sgd: fp32 master/buf");
+  TORCH_CHECK(grad.numel() == n && master.is_contiguous() && grad.is_contiguous(), "sgd: layout");
+  void* pout = nullptr;
+  int pdt = dph::kBF16;
+  if (param_out.has_value()) {
+    pout = param_out->data_ptr();
+    pdt = dt_code(*param_out);
+  }
+  const float* gs = grad_scale.has_value() ? grad_scale->data_ptr<float>() : nullptr;
+  dph::sgd_step(master.data_ptr<float>(), buf.data_ptr<float>(), grad.data_ptr(), pout, n, (float)lr,
+                (float)momentum, (float)dampening, (float)wd, nesterov ? 1 : 0, first_step ? 1 : 0, gs, dt_code(grad),
+                pdt, cur_stream());
+}
+
+void sumsq_(const Tensor& x, Tensor out) {
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.is_contiguous() && out.scalar_type() == at::kFloat, "sumsq: layout");
+  check_align16(x, "x");
+  dph::sumsq(x.data_ptr(), x.numel(), out.data_ptr<float>(), dt_code(x), cur_stream());
+}
+
+// ------------------------------------------------------------------------------------------------ cross-entropy
+std::tuple<Tensor, Tensor> cross_entropy_fwd(Tensor logits, const Tensor& target, const Tensor& inv_count,
+                                             int64_t ignore_index, bool grad_inplace, double smoothing) {
+  c10::DeviceGuard g(logits.device());
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "xent: logits must be [N, V] row-major");
+  TORCH_CHECK(target.scalar_type() == at::kLong && target.numel() == logits.size(0), "xent: target [N] int64");
+  const int64_t n = logits.size(0), v = logits.size(1);
+  auto loss = at::empty({n}, logits.options().dtype(at::kFloat));
+  auto lse = at::empty({n}, logits.options().dtype(at::kFloat));
+  dph::cross_entropy_fwd(logits.data_ptr(), target.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(),
+                         inv_count.data_ptr<float>(), n, v, logits.stride(0), ignore_index, grad_inplace ? 1 : 0,
+                         (float)smoothing, dt_code(logits), cur_stream());
+  return {loss, lse};
+}
+
+// ------------------------------------------------------------------------------------------------ attention
+void check_attn_operand(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 4, "flash_attn: ", name, " must be [B, S, H, D]");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "flash_attn: ", name, " must be bf16");
+  TORCH_CHECK(t.stride(3) == 1, "flash_attn: ", name, " head dim must be contiguous");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0,
+              "flash_attn: ", name, " strides must be multiples of 8 elements");
+  check_align16(t, name);
+}
+
+dph::AttnParams make_params(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& lse,
+                            double scale, bool causal) {
+  dph::AttnParams p{};
+  p.q = q.data_ptr(); p.k = k.data_ptr(); p.v = v.data_ptr(); p.o = o.data_ptr();
+  p.lse = lse.defined() && lse.numel() ? lse.data_ptr<float>() : nullptr;
+  p.q_sb = q.stride(0); p.q_ss = q.stride(1); p.q_sh = q.stride(2);
+  p.k_sb = k.stride(0); p.k_ss = k.stride(1); p.k_sh = k.stride(2);
+  p.v_sb = v.stride(0); p.v_ss = v.stride(1); p.v_sh = v.stride(2);
+  p.o_sb = o.stride(0); p.o_ss = o.stride(1); p.o_sh = o.stride(2);
+  p.B = (int)q.size(0); p.Sq = (int)q.size(1); p.Hq = (int)q.size(2); p.D = (int)q.size(3);
+  p.Sk = (int)k.size(1); p.Hkv = (int)k.size(2);
+  p.scale = (float)scale;
+  p.causal = causal ? 1 : 0;
+  return p;
+}
+
+std::tuple<Tensor, Tensor> flash_attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, double scale,
+                                          bool causal) {
+  c10::DeviceGuard g(q.device());
+  check_attn_operand(q, "q"); check_attn_operand(k, "k"); check_attn_operand(v, "v");
+  const int64_t D = q.size(3);
+  TORCH_CHECK(D == 32 || D == 64 || D == 128, "flash_attn: head_dim must be 32, 64 or 128");
+  TORCH_CHECK(k.size(3) == D && v.size(3) == D && k.sizes() == v.sizes(), "flash_attn: k/v shape mismatch");
+  TORCH_CHECK(k.size(0) == q.size(0) && q.size(2) % k.size(2) == 0, "flash_attn: batch / GQA heads mismatch");
+  auto o = at::empty({q.size(0), q.size(1), q.size(2), D}, q.options());
+  auto lse = at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
+  auto p = make_params(q, k, v, o, lse, scale, causal);
+  dph::flash_attn_fwd(p, cur_stream());
+  return {o, lse};
+}
+
+std::tuple<Tensor, Tensor, Tensor> flash_attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k,
+                                                  const Tensor& v, const Tensor& o, const Tensor& lse, double scale,
+                                                  bool causal) {
+  c10::DeviceGuard g(q.device());
+  check_attn_operand(q, "q"); check_attn_operand(k, "k"); check_attn_operand(v, "v");
+  check_attn_operand(o, "o"); check_attn_operand(dout, "dout");
+  TORCH_CHECK(dout.sizes() == o.sizes() && o.sizes() == q.sizes(), "flash_attn_bwd: dout/o shape mismatch");
+  const int64_t B = q.size(0), Sq = q.size(1), Hq = q.size(2), D = q.size(3), Sk = k.size(1), Hkv = k.size(2);
+  auto dq = at::empty({B, Sq, Hq, D}, q.options());
+  auto dk = at::empty({B, Sk, Hkv, D}, q.options());
+  auto dv = at::empty({B, Sk, Hkv, D}, q.options());
+  auto delta = at::empty({B, Hq, Sq}, q.options().dtype(at::kFloat));
+  auto dq_acc = at::empty({B, Sq, Hq, D}, q.options().dtype(at::kFloat));
+  dph::AttnBwdParams P{};
+  P.f = make_params(q, k, v, o, lse.contiguous(), scale, causal);
+  P.dout = dout.data_ptr(); P.do_sb = dout.stride(0); P.do_ss = dout.stride(1); P.do_sh = dout.stride(2);
+  P.delta = delta.data_ptr<float>();
+  P.dq_accum = dq_acc.data_ptr<float>();
+  P.dq = dq.data_ptr(); P.dk = dk.data_ptr(); P.dv = dv.data_ptr();
+  dph::flash_attn_bwd(P, cur_stream());
+  return {dq, dk, dv};
+}
+
+// ------------------------------------------------------------------------------------------------ embedding
+Tensor embedding_fwd(const Tensor& ids, const Tensor& table, int64_t vocab_start) {
+  c10::DeviceGuard g(table.device());
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && table.is_contiguous() && table.dim() == 2,
+              "embedding: int64 ids, contiguous [V, D] table");
+  TORCH_CHECK(table.size(1) % 8 == 0, "embedding: dim must be a multiple of 8");
+  auto sizes = ids.sizes().vec();
+  sizes.push_back(table.size(1));
+  auto out = at::empty(sizes, table.options());
+  dph::embedding_fwd(ids.data_ptr<int64_t>(), table.data_ptr(), out.data_ptr(), ids.numel(), table.size(1),
+                     vocab_start, table.size(0), dt_code(table), cur_stream());
+  return out;
+}
+Tensor embedding_bwd(const Tensor& ids, const Tensor& dout, int64_t vocab_local, int64_t vocab_start) {
+  c10::DeviceGuard g(dout.device());
+  TORCH_CHECK(dout.is_contiguous() && ids.is_contiguous(), "embedding_bwd: contiguous required");
+  const int64_t dim = dout.size(-1);
+  auto dtab = at::zeros({vocab_local, dim}, dout.options().dtype(at::kFloat));
+  dph::embedding_bwd(ids.data_ptr<int64_t>(), dout.data_ptr(), dtab.data_ptr<float>(), ids.numel(), dim, vocab_start,
+                     vocab_local, dt_code(dout), cur_stream());
+  return dtab;
+}
+
+}  // namespace
+
+TORCH_LIBRARY(dph, m) {
+  m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps, Tensor? residual=None) -> (Tensor, Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd) -> (Tensor, Tensor)");
+  m.def("layernorm_fwd(Tensor x, Tensor w, Tensor b, float eps) -> (Tensor, Tensor, Tensor)");
+  m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd) -> (Tensor, Tensor, Tensor)");
+  m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, int pos_offset, bool inverse) -> ()");
+  m.def("swiglu_fwd(Tensor x2) -> Tensor");
+  m.def("swiglu_bwd(Tensor dy, Tensor x2) -> Tensor");
+  m.def("gelu_fwd(Tensor x, bool tanh_form) -> Tensor");
+  m.def("gelu_bwd(Tensor dy, Tensor x, bool tanh_form) -> Tensor");
+  m.def("adamw_step_(Tensor(a!) master, Tensor(b!) m, Tensor(c!) v, Tensor grad, Tensor(d!)? param_out, float lr, "
+        "float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, Tensor? grad_scale) -> ()");
+  m.def("sgd_step_(Tensor(a!) master, Tensor(b!) buf, Tensor grad, Tensor(d!)? param_out, float lr, float momentum, "
+        "float dampening, float weight_decay, bool nesterov, bool first_step, Tensor? grad_scale) -> ()");
+  m.def("sumsq_(Tensor x, Tensor(a!) out) -> ()");
+  m.def("cross_entropy_fwd(Tensor(a!) logits, Tensor target, Tensor inv_count, int ignore_index, bool grad_inplace, "
+        "float smoothing) -> (Tensor, Tensor)");
+  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal) -> (Tensor, Tensor)");
+  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal) "
+        "-> (Tensor, Tensor, Tensor)");
+  m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
+  m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
+}
+
+TORCH_LIBRARY_IMPL(dph, CUDA, m) {
+  m.impl("rmsnorm_fwd", &rmsnorm_fwd);
+  m.impl("rmsnorm_bwd", &rmsnorm_bwd);
+  m.impl("layernorm_fwd", &layernorm_fwd);
+  m.impl("layernorm_bwd", &layernorm_bwd);
+  m.impl("rope_", &rope_);
+  m.impl("swiglu_fwd", &swiglu_fwd);
+  m.impl("swiglu_bwd", &swiglu_bwd);
+  m.impl("gelu_fwd", &gelu_fwd);
+  m.impl("gelu_bwd", &gelu_bwd);
+  m.impl("adamw_step_", &adamw_step_);
+  m.impl("sgd_step_", &sgd_step_);
+  m.impl("sumsq_", &sumsq_);
+  m.impl("cross_entropy_fwd", &cross_entropy_fwd);
+  m.impl("flash_attn_fwd", &flash_attn_fwd);
+  m.impl("flash_attn_bwd", &flash_attn_bwd);
+  m.impl("embedding_fwd", &embedding_fwd);
+  m.impl("embedding_bwd", &embedding_bwd);
+}

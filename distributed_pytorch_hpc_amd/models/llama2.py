@@ -1,0 +1,260 @@
+"""Llama-2 decoder for MI355X training (capability parity with fsdp_tp/llama2_model.py:1-462).
+
+Same architecture, hyper-parameters and init scheme as the reference ``Transformer``:
+pre-norm RMSNorm blocks, interleaved-pair RoPE (theta 1e4), causal MHA/GQA attention, SwiGLU FFN with
+hidden = multiple_of * ceil(int(2 * 4 * dim / 3) / multiple_of) (11008 at dim 4096), depth-scaled
+truncated-normal init, fp32 logits from ``forward(tokens)``.
+
+MI355X-first changes (numerically equivalent):
+  * q/k/v and w1/w3 are FUSED projections (``wqkv``, ``w13``): one GEMM each instead of three / two,
+    q/k/v are strided views of the GEMM output fed straight to the flash-attention kernel.
+  * RoPE + attention run as one autograd node (ops.rope_attention), RoPE in place on the QKV buffer.
+  * The residual add after each sub-block is fused into the following RMSNorm (ops.add_rms_norm):
+    a block consumes and produces the pair (residual, pending delta) -- see TransformerBlock.forward.
+  * With targets, ``forward`` returns the mean cross-entropy through the fused CE kernel, which never
+    materialises fp32 logits.
+``convert_reference_state_dict`` maps a reference checkpoint (wq/wk/wv, w1/w3) onto this layout.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field, replace
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .. import ops
+from ..ops.rope import precompute_rope_tables
+
+
+@dataclass
+class ModelArgs:
+    dim: int = 4096
+    n_layers: int = 32
+    n_heads: int = 32
+    n_kv_heads: Optional[int] = None
+    vocab_size: int = -1
+    multiple_of: int = 256
+    ffn_dim_multiplier: Optional[float] = None
+    norm_eps: float = 1e-5
+    max_batch_size: int = 32
+    max_seq_len: int = 32768
+    depth_init: bool = True
+    rope_theta: float = 10000.0
+
+    @property
+    def head_dim(self) -> int:
+        return self.dim // self.n_heads
+
+    @property
+    def kv_heads(self) -> int:
+        return self.n_heads if self.n_kv_heads is None else self.n_kv_heads
+
+    @property
+    def ffn_hidden(self) -> int:
+        h = int(2 * (4 * self.dim) / 3)
+        if self.ffn_dim_multiplier is not None:
+            h = int(self.ffn_dim_multiplier * h)
+        return self.multiple_of * ((h + self.multiple_of - 1) // self.multiple_of)
+
+    def num_params(self) -> int:
+        d, hd = self.dim, self.head_dim
+        attn = d * (self.n_heads + 2 * self.kv_heads) * hd + self.n_heads * hd * d
+        ffn = 3 * d * self.ffn_hidden
+        return self.n_layers * (attn + ffn + 2 * d) + 2 * self.vocab_size * d + d
+
+    def flops_per_token(self, seq_len: int) -> float:
+        """Training FLOPs per token: 6 N (dense) + 6 L S D (causal attention, fwd+bwd, with the 1/2 mask)."""
+        n_dense = self.num_params() - self.vocab_size * self.dim  # embedding gather is not a GEMM
+        return 6.0 * n_dense + 6.0 * self.n_layers * seq_len * self.dim
+
+
+PRESETS = {
+    # the reference toy config (fsdp_tp/fsdp_tp_example.py:134, scripts/06_hybrid_parallelism/01_fsdp_tp_hybrid.py)
+    "toy": ModelArgs(dim=256, n_layers=2, n_heads=16, vocab_size=32000),
+    "tiny": ModelArgs(dim=128, n_layers=2, n_heads=4, vocab_size=512, max_seq_len=512),
+    "llama2-1b": ModelArgs(dim=2048, n_layers=16, n_heads=16, vocab_size=32000, max_seq_len=4096),
+    "llama2-7b": ModelArgs(dim=4096, n_layers=32, n_heads=32, vocab_size=32000, max_seq_len=4096),
+    "llama2-13b": ModelArgs(dim=5120, n_layers=40, n_heads=40, vocab_size=32000, max_seq_len=4096),
+}
+
+
+def get_preset(name: str, **overrides) -> ModelArgs:
+    return replace(PRESETS[name], **overrides)
+
+
+# ---------------------------------------------------------------------------------------------- rope cache
+_ROPE: dict = {}
+
+
+def rope_tables(head_dim: int, max_pos: int, theta: float, device) -> tuple[torch.Tensor, torch.Tensor]:
+    key = (head_dim, max_pos, theta, str(device))
+    t = _ROPE.get(key)
+    if t is None:
+        t = precompute_rope_tables(head_dim, max_pos, theta, device)
+        _ROPE[key] = t
+    return t
+
+
+# ---------------------------------------------------------------------------------------------- modules
+class Attention(nn.Module):
+    def __init__(self, args: ModelArgs):
+        super().__init__()
+        self.n_heads = args.n_heads
+        self.n_kv_heads = args.kv_heads
+        self.head_dim = args.head_dim
+        self.max_pos = 2 * args.max_seq_len
+        self.theta = args.rope_theta
+        self.wqkv = nn.Linear(args.dim, (self.n_heads + 2 * self.n_kv_heads) * self.head_dim, bias=False)
+        self.wo = nn.Linear(self.n_heads * self.head_dim, args.dim, bias=False)
+        # local head counts (changed by the tensor-parallel plan)
+        self.n_local_heads = self.n_heads
+        self.n_local_kv_heads = self.n_kv_heads
+        # optional context-parallel attention implementation (Ulysses / ring), set by parallel.cp
+        self.cp_attention = None
+
+    def init_weights(self, init_std: float):
+        nn.init.trunc_normal_(self.wqkv.weight, mean=0.0, std=0.02)
+        nn.init.trunc_normal_(self.wo.weight, mean=0.0, std=init_std)
+
+    def forward(self, x: torch.Tensor, pos_offset: int = 0) -> torch.Tensor:
+        qkv = self.wqkv(x)
+        cos, sin = rope_tables(self.head_dim, self.max_pos, self.theta, qkv.device)
+        if self.cp_attention is not None:
+            o = self.cp_attention(qkv, cos, sin, self.n_local_heads, self.n_local_kv_heads, self.head_dim)
+        else:
+            o = ops.rope_attention(qkv, cos, sin, self.n_local_heads, self.n_local_kv_heads, self.head_dim,
+                                   causal=True, pos_offset=pos_offset)
+        return self.wo(o)
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim: int, hidden_dim: int):
+        super().__init__()
+        self.hidden_dim = hidden_dim
+        self.w13 = nn.Linear(dim, 2 * hidden_dim, bias=False)   # [w1; w3]
+        self.w2 = nn.Linear(hidden_dim, dim, bias=False)
+
+    def init_weights(self, init_std: float):
+        h = self.hidden_dim
+        with torch.no_grad():
+            nn.init.trunc_normal_(self.w13.weight[:h], mean=0.0, std=0.02)          # w1
+            nn.init.trunc_normal_(self.w13.weight[h:], mean=0.0, std=init_std)      # w3
+        nn.init.trunc_normal_(self.w2.weight, mean=0.0, std=init_std)
+
+    def forward(self, x):
+        return self.w2(ops.swiglu(self.w13(x)))
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, layer_id: int, args: ModelArgs):
+        super().__init__()
+        self.layer_id = layer_id
+        self.attention = Attention(args)
+        self.feed_forward = FeedForward(args.dim, args.ffn_hidden)
+        self.attention_norm = ops.RMSNorm(args.dim, eps=args.norm_eps)
+        self.ffn_norm = ops.RMSNorm(args.dim, eps=args.norm_eps)
+        if args.depth_init:
+            self.weight_init_std = 0.02 / (2 * (layer_id + 1)) ** 0.5
+        else:
+            self.weight_init_std = 0.02 / (2 * args.n_layers) ** 0.5
+
+    def init_weights(self):
+        self.attention_norm.reset_parameters()
+        self.ffn_norm.reset_parameters()
+        self.attention.init_weights(self.weight_init_std)
+        self.feed_forward.init_weights(self.weight_init_std)
+
+    def forward(self, x: torch.Tensor, delta: Optional[torch.Tensor] = None):
+        """Takes the residual stream as (x, delta) with x + delta = reference block input and returns
+        (h, ffn_out) with h + ffn_out = reference block output (the final add is deferred into the next
+        norm).  ``forward(x)`` with delta None is the plain reference input."""
+        if delta is None:
+            r, a = x, self.attention_norm(x)
+        else:
+            r, a = ops.add_rms_norm(x, delta, self.attention_norm.weight, self.attention_norm.eps)
+        h, f = ops.add_rms_norm(r, self.attention(a), self.ffn_norm.weight, self.ffn_norm.eps)
+        return h, self.feed_forward(f)
+
+
+class Transformer(nn.Module):
+    def __init__(self, args: ModelArgs):
+        super().__init__()
+        assert args.vocab_size > 0, "vocab_size must be set"
+        self.model_args = args
+        self.vocab_size = args.vocab_size
+        self.n_layers = args.n_layers
+        self.tok_embeddings = nn.Embedding(args.vocab_size, args.dim)
+        self.layers = nn.ModuleList([TransformerBlock(i, args) for i in range(args.n_layers)])
+        self.norm = ops.RMSNorm(args.dim, eps=args.norm_eps)
+        self.output = nn.Linear(args.dim, args.vocab_size, bias=False)
+        self.init_weights()
+
+    @classmethod
+    def from_model_args(cls, args: ModelArgs) -> "Transformer":
+        return cls(args)
+
+    @torch.no_grad()
+    def init_weights(self):
+        nn.init.normal_(self.tok_embeddings.weight)
+        for layer in self.layers:
+            layer.init_weights()
+        self.norm.reset_parameters()
+        std = self.model_args.dim ** -0.5
+        nn.init.trunc_normal_(self.output.weight, mean=0.0, std=std, a=-3 * std, b=3 * std)
+
+    def embed(self, tokens: torch.Tensor) -> torch.Tensor:
+        return ops.embedding(tokens, self.tok_embeddings.weight)
+
+    def head(self, h: torch.Tensor, delta: Optional[torch.Tensor], targets: Optional[torch.Tensor] = None):
+        if delta is None:
+            x = self.norm(h)
+        else:
+            _, x = ops.add_rms_norm(h, delta, self.norm.weight, self.norm.eps)
+        logits = self.output(x)
+        if targets is None:
+            return logits.float()
+        return ops.fused_cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1))
+
+    def forward(self, tokens: torch.Tensor, targets: Optional[torch.Tensor] = None):
+        """tokens [B, S] -> fp32 logits [B, S, V]; with ``targets`` -> scalar mean cross-entropy."""
+        h, delta = self.embed(tokens), None
+        for layer in self.layers:
+            h, delta = layer(h, delta)
+        return self.head(h, delta, targets)
+
+
+def build_llama(args: ModelArgs | str, device=None, dtype: torch.dtype = torch.bfloat16, seed: int = 0,
+                **overrides) -> Transformer:
+    """Construct and initialise directly on ``device`` (fast for 7B on a GPU), then cast to ``dtype``."""
+    if isinstance(args, str):
+        args = get_preset(args, **overrides)
+    elif overrides:
+        args = replace(args, **overrides)
+    torch.manual_seed(seed)
+    with torch.device(device if device is not None else "cpu"):
+        model = Transformer(args)
+    return model.to(dtype)
+
+
+def convert_reference_state_dict(sd: dict, args: ModelArgs) -> dict:
+    """Map a reference llama2_model.Transformer state dict (wq/wk/wv, w1/w3, freqs_cis) to this layout."""
+    out = {}
+    for k, v in sd.items():
+        if k == "freqs_cis":
+            continue
+        if ".attention.wq." in k:
+            base = k.replace(".wq.", ".")
+            out[base.replace(".attention.", ".attention.wqkv.")] = torch.cat(
+                [v, sd[k.replace(".wq.", ".wk.")], sd[k.replace(".wq.", ".wv.")]], 0)
+        elif ".attention.wk." in k or ".attention.wv." in k:
+            continue
+        elif ".feed_forward.w1." in k:
+            out[k.replace(".w1.", ".w13.")] = torch.cat([v, sd[k.replace(".w1.", ".w3.")]], 0)
+        elif ".feed_forward.w3." in k:
+            continue
+        else:
+            out[k] = v
+    return out

@@ -1,0 +1,99 @@
+"""Fake (meta) implementations of the ``torch.ops.dph`` operators.
+
+They let the custom ops flow through FakeTensor tracing (torch.export / meta-device model
+construction / shape inference) without running a kernel.
+"""
+from __future__ import annotations
+
+import torch
+from torch.library import register_fake
+
+
+@register_fake("dph::rmsnorm_fwd")
+def _rmsnorm_fwd(x, w, eps, residual=None):
+    rows = x.numel() // x.shape[-1]
+    h = torch.empty_like(x) if residual is not None else x.new_empty((0,))
+    return torch.empty_like(x), x.new_empty((rows,), dtype=torch.float32), h
+
+
+@register_fake("dph::rmsnorm_bwd")
+def _rmsnorm_bwd(dy, x, w, rstd):
+    return torch.empty_like(x), torch.empty_like(w)
+
+
+@register_fake("dph::layernorm_fwd")
+def _layernorm_fwd(x, w, b, eps):
+    rows = x.numel() // x.shape[-1]
+    return torch.empty_like(x), x.new_empty((rows,), dtype=torch.float32), x.new_empty((rows,), dtype=torch.float32)
+
+
+@register_fake("dph::layernorm_bwd")
+def _layernorm_bwd(dy, x, w, mean, rstd):
+    return torch.empty_like(x), torch.empty_like(w), torch.empty_like(w)
+
+
+@register_fake("dph::rope_")
+def _rope(x, cos, sin, pos_offset, inverse):
+    return None
+
+
+@register_fake("dph::swiglu_fwd")
+def _swiglu_fwd(x2):
+    return x2.new_empty((*x2.shape[:-1], x2.shape[-1] // 2))
+
+
+@register_fake("dph::swiglu_bwd")
+def _swiglu_bwd(dy, x2):
+    return torch.empty_like(x2)
+
+
+@register_fake("dph::gelu_fwd")
+def _gelu_fwd(x, tanh_form):
+    return torch.empty_like(x)
+
+
+@register_fake("dph::gelu_bwd")
+def _gelu_bwd(dy, x, tanh_form):
+    return torch.empty_like(x)
+
+
+@register_fake("dph::adamw_step_")
+def _adamw(master, m, v, grad, param_out, lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale):
+    return None
+
+
+@register_fake("dph::sgd_step_")
+def _sgd(master, buf, grad, param_out, lr, momentum, dampening, weight_decay, nesterov, first_step, grad_scale):
+    return None
+
+
+@register_fake("dph::sumsq_")
+def _sumsq(x, out):
+    return None
+
+
+@register_fake("dph::cross_entropy_fwd")
+def _xent(logits, target, inv_count, ignore_index, grad_inplace, smoothing):
+    n = logits.shape[0]
+    return logits.new_empty((n,), dtype=torch.float32), logits.new_empty((n,), dtype=torch.float32)
+
+
+@register_fake("dph::flash_attn_fwd")
+def _fa_fwd(q, k, v, scale, causal):
+    b, s, h, d = q.shape
+    return q.new_empty((b, s, h, d)), q.new_empty((b, h, s), dtype=torch.float32)
+
+
+@register_fake("dph::flash_attn_bwd")
+def _fa_bwd(dout, q, k, v, o, lse, scale, causal):
+    return torch.empty_like(q), k.new_empty(k.shape), v.new_empty(v.shape)
+
+
+@register_fake("dph::embedding_fwd")
+def _emb_fwd(ids, table, vocab_start):
+    return table.new_empty((*ids.shape, table.shape[1]))
+
+
+@register_fake("dph::embedding_bwd")
+def _emb_bwd(ids, dout, vocab_local, vocab_start):
+    return dout.new_empty((vocab_local, dout.shape[-1]), dtype=torch.float32)

@@ -1,0 +1,84 @@
+"""Losses: fused softmax cross-entropy (csrc/xent.hip) and the latitude-weighted MSE of the ERA5
+drivers (scripts/01_data_parallel_ddp/multinode_ddp_unet.py:221-229).
+
+``fused_cross_entropy`` computes the mean loss AND writes d(loss)/d(logits) in place over the logits
+during the forward kernel; backward only scales that buffer by the incoming scalar gradient.  This
+removes the reference's fp32 [B, S, V] logits copy (llama2_model.py:447) and a separate softmax pass.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+class _FusedXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, ignore_index, smoothing):
+        valid = (target != ignore_index).sum().clamp_min(1).float()
+        inv = (1.0 / valid).reshape(1)
+        need_grad = ctx.needs_input_grad[0]
+        loss_rows, _ = _lib.ops().cross_entropy_fwd(logits, target, inv, ignore_index, need_grad, smoothing)
+        if need_grad:
+            ctx.mark_dirty(logits)
+            ctx.save_for_backward(logits)
+        return loss_rows.sum() * inv[0], logits
+
+    @staticmethod
+    def backward(ctx, gloss, _glogits):
+        (g,) = ctx.saved_tensors
+        g.mul_(gloss.to(g.dtype))
+        return g, None, None, None
+
+
+def fused_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100,
+                        label_smoothing: float = 0.0, inplace: bool = True) -> torch.Tensor:
+    """Mean cross-entropy over rows of [N, V] logits.  With ``inplace`` (default) the logits buffer is
+    consumed (overwritten by its gradient) -- pass ``inplace=False`` if the caller still needs it."""
+    if logits.dim() != 2:
+        logits = logits.reshape(-1, logits.shape[-1])
+        target = target.reshape(-1)
+    if _lib.use_native(logits) and logits.dtype in (torch.bfloat16, torch.float32):
+        if not inplace:
+            logits = logits.clone()
+        loss, _ = _FusedXentFn.apply(logits, target.contiguous(), ignore_index, float(label_smoothing))
+        return loss
+    return F.cross_entropy(logits.float(), target, ignore_index=ignore_index, label_smoothing=label_smoothing)
+
+
+def latitude_weights(n_lat: int, device=None, dtype=torch.float32) -> torch.Tensor:
+    """cos(latitude) weights over a [90, -90] grid normalised to mean 1 (multinode_ddp_unet.py:221-229)."""
+    lat = torch.linspace(90.0, -90.0, n_lat, dtype=torch.float64)
+    w = torch.cos(lat * math.pi / 180.0)
+    w = w / w.mean()
+    return w.to(device=device, dtype=dtype)
+
+
+def latitude_weighted_mse(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """mean over [B, C, H, W] of w[H] * (pred - target)^2."""
+    w = latitude_weights(pred.shape[-2], pred.device, torch.float32).view(1, 1, -1, 1)
+    return (w * (pred.float() - target.float()).pow(2)).mean()
+
+
+def vocab_parallel_cross_entropy(local_logits: torch.Tensor, target: torch.Tensor, vocab_start: int, group,
+                                 ignore_index: int = -100) -> torch.Tensor:
+    """Cross-entropy over vocab-sharded logits [N, V/tp] without gathering the vocab dim ("loss
+    parallel"): two [N] all-reduces (max, sum-exp) and one [N] all-reduce of the target logit."""
+    from ..comm.functional import all_reduce_autograd_max, all_reduce_autograd_sum
+
+    x = local_logits.float()
+    n, vloc = x.shape
+    m = all_reduce_autograd_max(x.detach().max(dim=-1).values, group)
+    e = torch.exp(x - m[:, None])
+    se = all_reduce_autograd_sum(e.sum(-1), group)
+    local_t = target - vocab_start
+    in_range = (local_t >= 0) & (local_t < vloc)
+    idx = local_t.clamp(0, vloc - 1)
+    tl = x.gather(1, idx[:, None]).squeeze(1) * in_range
+    tl = all_reduce_autograd_sum(tl, group)
+    loss = torch.log(se) + m - tl
+    valid = target != ignore_index
+    return (loss * valid).sum() / valid.sum().clamp_min(1)

@@ -1,0 +1,261 @@
+"""Numerics of every CDNA4 kernel against a plain PyTorch fp32 reference of the same op (GPU only)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_pytorch_hpc_amd import ops
+from distributed_pytorch_hpc_amd.ops import attention as attn_mod
+from distributed_pytorch_hpc_amd.ops import rope as rope_mod
+from distributed_pytorch_hpc_amd.train import optim as optim_mod
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("rows,dim", [(1000, 4096), (257, 256), (64, 12288), (33, 1376)])
+def test_rmsnorm(dph_native, rows, dim):
+    torch.manual_seed(0)
+    x = torch.randn(rows, dim, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(dim, device=DEV)).to(torch.bfloat16).requires_grad_()
+    y = ops.rms_norm(x, w, 1e-5)
+    xr = x.detach().float().requires_grad_()
+    wr = w.detach().float().requires_grad_()
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    assert rel_err(y, yr) < 1e-2
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    assert rel_err(x.grad, xr.grad) < 2e-2
+    assert rel_err(w.grad, wr.grad) < 2e-2
+
+
+def test_add_rmsnorm(dph_native):
+    torch.manual_seed(1)
+    x = torch.randn(300, 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(300, 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = torch.rand(1024, device=DEV, dtype=torch.bfloat16).requires_grad_()
+    h, y = ops.add_rms_norm(x, r, w, 1e-5)
+    xr, rr, wr = (t.detach().float().requires_grad_() for t in (x, r, w))
+    hr = xr + rr
+    yr = hr * torch.rsqrt(hr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    assert rel_err(h, hr) < 1e-2 and rel_err(y, yr) < 1e-2
+    gh, gy = torch.randn_like(h), torch.randn_like(y)
+    (h * gh).sum().add((y * gy).sum()).backward()
+    ((hr * gh.float()).sum() + (yr * gy.float()).sum()).backward()
+    assert rel_err(x.grad, xr.grad) < 2e-2 and rel_err(r.grad, rr.grad) < 2e-2 and rel_err(w.grad, wr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_layernorm(dph_native, dtype):
+    torch.manual_seed(2)
+    x = torch.randn(500, 256, device=DEV, dtype=dtype, requires_grad=True)
+    w = torch.randn(256, device=DEV, dtype=dtype, requires_grad=True)
+    b = torch.randn(256, device=DEV, dtype=dtype, requires_grad=True)
+    y = ops.layer_norm(x, w, b, 1e-5)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = F.layer_norm(xr, (256,), wr, br, 1e-5)
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    assert rel_err(y, yr) < tol
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g.float())
+    assert rel_err(x.grad, xr.grad) < 2 * tol and rel_err(w.grad, wr.grad) < 2 * tol and rel_err(b.grad, br.grad) < 2 * tol
+
+
+def test_rope(dph_native):
+    torch.manual_seed(3)
+    B, S, H, D = 2, 100, 4, 128
+    cos, sin = rope_mod.precompute_rope_tables(D, 512, device=DEV)
+    x = torch.randn(B, S, 3, H, D, device=DEV, dtype=torch.bfloat16)
+    ref = rope_mod.rope_reference(x[:, :, 0].float(), cos, sin, 7)
+    y = x.clone()
+    ops.rope_(y[:, :, 0], cos, sin, 7)
+    assert rel_err(y[:, :, 0], ref) < 1e-2
+    assert torch.equal(y[:, :, 1:], x[:, :, 1:])  # untouched neighbours of the strided view
+    ops.rope_(y[:, :, 0], cos, sin, 7, inverse=True)
+    assert rel_err(y[:, :, 0], x[:, :, 0]) < 1e-2
+    # complex-multiplication formulation of the reference (llama2_model.py:74-100)
+    freqs = 1.0 / (10000.0 ** (torch.arange(0, D, 2, device=DEV)[: D // 2].float() / D))
+    t = torch.arange(512, device=DEV).float()
+    fc = torch.polar(torch.ones(512, D // 2, device=DEV), torch.outer(t, freqs))[7:7 + S]
+    xc = torch.view_as_complex(x[:, :, 0].float().reshape(B, S, H, -1, 2))
+    refc = torch.view_as_real(xc * fc.view(1, S, 1, -1)).flatten(3)
+    assert rel_err(ref, refc) < 1e-5
+
+
+def test_swiglu(dph_native):
+    torch.manual_seed(4)
+    x = torch.randn(257, 2 * 1376, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.swiglu(x)
+    xr = x.detach().float().requires_grad_()
+    g, u = xr.chunk(2, -1)
+    yr = F.silu(g) * u
+    assert rel_err(y, yr) < 1e-2
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    yr.backward(gy.float())
+    assert rel_err(x.grad, xr.grad) < 2e-2
+
+
+@pytest.mark.parametrize("approx", ["none", "tanh"])
+def test_gelu(dph_native, approx):
+    x = torch.randn(4096, device=DEV, requires_grad=True)
+    y = ops.gelu(x, approx)
+    xr = x.detach().requires_grad_()
+    yr = F.gelu(xr, approximate=approx)
+    assert rel_err(y, yr) < 1e-5
+    y.sum().backward()
+    yr.sum().backward()
+    assert rel_err(x.grad, xr.grad) < 1e-4
+
+
+def test_adamw_matches_torch(dph_native):
+    torch.manual_seed(5)
+    p1 = [torch.nn.Parameter(torch.randn(n, device=DEV)) for n in (1000, 37, 4096)]
+    p2 = [torch.nn.Parameter(p.detach().clone()) for p in p1]
+    o1 = optim_mod.FusedAdamW(p1, lr=1e-2, weight_decay=0.1)
+    o2 = torch.optim.AdamW(p2, lr=1e-2, weight_decay=0.1)
+    for _ in range(5):
+        for a, b in zip(p1, p2):
+            g = torch.randn_like(a)
+            a.grad.copy_(g)
+            b.grad = g.clone()
+        o1.step()
+        o2.step()
+    for a, b in zip(p1, p2):
+        assert rel_err(a, b) < 1e-5
+
+
+def test_adamw_bf16_master(dph_native):
+    torch.manual_seed(6)
+    p = torch.nn.Parameter(torch.randn(2048, device=DEV, dtype=torch.bfloat16))
+    ref = torch.nn.Parameter(p.detach().float().clone())
+    o1 = optim_mod.FusedAdamW([p], lr=1e-3)
+    o2 = torch.optim.AdamW([ref], lr=1e-3)
+    for _ in range(3):
+        g = torch.randn(2048, device=DEV)
+        p.grad.copy_(g.bfloat16())
+        ref.grad = g.bfloat16().float()
+        o1.step()
+        o2.step()
+    assert rel_err(o1.flat_states()[0].master, ref) < 1e-6
+    assert rel_err(p, ref) < 1e-2
+
+
+def test_sgd_matches_torch(dph_native):
+    torch.manual_seed(7)
+    p1 = [torch.nn.Parameter(torch.randn(n, device=DEV)) for n in (100, 513)]
+    p2 = [torch.nn.Parameter(p.detach().clone()) for p in p1]
+    o1 = optim_mod.FusedSGD(p1, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    o2 = torch.optim.SGD(p2, lr=0.1, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    for _ in range(4):
+        for a, b in zip(p1, p2):
+            g = torch.randn_like(a)
+            a.grad.copy_(g)
+            b.grad = g.clone()
+        o1.step()
+        o2.step()
+    for a, b in zip(p1, p2):
+        assert rel_err(a, b) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_cross_entropy(dph_native, dtype):
+    torch.manual_seed(8)
+    N, V = 300, 32000
+    logits = (3 * torch.randn(N, V, device=DEV)).to(dtype)
+    tgt = torch.randint(0, V, (N,), device=DEV)
+    tgt[5] = -100
+    lr = logits.detach().float().requires_grad_()
+    ref = F.cross_entropy(lr, tgt, ignore_index=-100)
+    ref.backward()
+    x = logits.clone().requires_grad_()
+    y = x * 1.0  # non-leaf buffer that the fused op may consume
+    loss = ops.fused_cross_entropy(y, tgt)
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1, abs(ref.item()))
+    loss.backward()
+    assert rel_err(x.grad, lr.grad) < 2e-2
+
+
+CASES = [
+    # B, Sq, Sk, Hq, Hkv, D, causal
+    (2, 256, 256, 4, 4, 128, True),
+    (1, 300, 300, 4, 4, 128, False),
+    (2, 200, 200, 8, 2, 64, True),
+    (1, 130, 130, 2, 2, 32, True),
+    (1, 64, 192, 2, 2, 64, True),
+    (1, 520, 520, 2, 1, 128, True),
+]
+
+
+@pytest.mark.parametrize("B,Sq,Sk,Hq,Hkv,D,causal", CASES)
+def test_flash_attention(dph_native, B, Sq, Sk, Hq, Hkv, D, causal):
+    torch.manual_seed(9)
+    q = torch.randn(B, Sq, Hq, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = ops.flash_attention(q, k, v, causal=causal)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = attn_mod.attention_reference(qr, kr, vr, causal, 1.0 / math.sqrt(D))
+    assert rel_err(o, orf) < 2e-2
+    do = torch.randn_like(o)
+    o.backward(do)
+    orf.backward(do.float())
+    assert rel_err(q.grad, qr.grad) < 3e-2
+    assert rel_err(k.grad, kr.grad) < 3e-2
+    assert rel_err(v.grad, vr.grad) < 3e-2
+
+
+def test_flash_attention_padded_head_dim(dph_native):
+    torch.manual_seed(10)
+    q, k, v = (torch.randn(2, 64, 4, 16, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
+    o = ops.flash_attention(q, k, v, causal=True)
+    orf = attn_mod.attention_reference(q.float(), k.float(), v.float(), True, 0.25)
+    assert o.shape == q.shape and rel_err(o, orf) < 2e-2
+    o.sum().backward()
+    assert q.grad.shape == q.shape
+
+
+def test_rope_attention_fused(dph_native):
+    torch.manual_seed(11)
+    B, S, H, KV, D = 2, 128, 4, 2, 64
+    cos, sin = rope_mod.precompute_rope_tables(D, 256, device=DEV)
+    qkv = torch.randn(B, S, (H + 2 * KV) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = ops.rope_attention(qkv * 1.0, cos, sin, H, KV, D)
+    x = qkv.detach().float().requires_grad_()
+    q = x[:, :, : H * D].view(B, S, H, D)
+    k = x[:, :, H * D:(H + KV) * D].view(B, S, KV, D)
+    v = x[:, :, (H + KV) * D:].view(B, S, KV, D)
+    q, k = rope_mod.rope_reference(q, cos, sin), rope_mod.rope_reference(k, cos, sin)
+    orf = attn_mod.attention_reference(q, k, v, True, 1 / math.sqrt(D)).reshape(B, S, -1)
+    assert rel_err(o, orf) < 2e-2
+    g = torch.randn_like(o)
+    o.backward(g)
+    orf.backward(g.float())
+    assert rel_err(qkv.grad, x.grad) < 3e-2
+
+
+def test_embedding(dph_native):
+    torch.manual_seed(12)
+    table = torch.randn(1000, 64, device=DEV, requires_grad=True)
+    ids = torch.randint(0, 1000, (4, 50), device=DEV)
+    out = ops.embedding(ids, table)
+    ref_t = table.detach().clone().requires_grad_()
+    ref = F.embedding(ids, ref_t)
+    assert torch.equal(out, ref)
+    g = torch.randn_like(out)
+    out.backward(g)
+    ref.backward(g)
+    assert rel_err(table.grad, ref_t.grad) < 1e-6
+    # vocab shard [500, 1000)
+    shard = table.detach()[500:].clone()
+    o2 = ops.embedding(ids, shard, vocab_start=500)
+    exp = torch.where((ids >= 500)[..., None], F.embedding(ids, table.detach()), torch.zeros_like(out))
+    assert torch.equal(o2, exp)
