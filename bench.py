@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Llama-2-7B training throughput (tokens/s) on 1..8 MI355X, weak scaling.
+
+Metric and config come from BASELINE.json ("tokens/sec + DDP/FSDP scaling efficiency, Llama-2-7B at
+1/2/4/8 MI355X").  Every rank trains the full Llama-2-7B architecture (random init, synthetic tokens)
+with a fixed per-GPU batch; N > 1 runs the FSDP engine (reduce-scatter gradients overlapped with
+backward, sharded fp32 AdamW state, parameter all-gather overlapped with the next forward) over RCCL.
+The timed region holds EXACTLY --steps full optimizer steps (forward + backward + gradient collectives +
+AdamW + parameter all-gather), bracketed by a barrier and a device synchronize on both sides; the
+reported time is the MAX over ranks; rank 0 prints one JSON line.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+BASELINE_METRIC = "tokens/sec + DDP/FSDP scaling efficiency, Llama-2-7B at 1/2/4/8 MI355X"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="llama2-7b")
+    ap.add_argument("--seq-len", type=int, default=4096)
+    ap.add_argument("--micro-batch", type=int, default=4, help="sequences per GPU per step")
+    ap.add_argument("--parallel", choices=["auto", "fsdp", "ddp"], default="auto",
+                    help="auto: single-GPU engine for N=1, FSDP (sharded optimizer) for N>1")
+    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--json-out", default=None)
+    ap.add_argument("--quiet", action="store_true")
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    from distributed_pytorch_hpc_amd.runtime import env as rt
+
+    if world_env > 1:
+        rank, world, local = rt.init_distributed(verbose=not args.quiet)
+    else:
+        rank, world, local = 0, 1, 0
+        torch.cuda.set_device(0)
+    if world != args.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting n_gpus={world}", file=sys.stderr)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from distributed_pytorch_hpc_amd.models.llama2 import build_llama, get_preset
+    from distributed_pytorch_hpc_amd.ops import _lib
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import (DataParallelEngine, MixedPrecision,
+                                                                    OptimConfig)
+
+    _lib.require()
+    margs = get_preset(args.model, max_seq_len=max(args.seq_len, 4096))
+    model = build_llama(margs, device=dev, dtype=torch.bfloat16, seed=1234)
+    mode = args.parallel
+    if mode == "auto":
+        mode = "fsdp" if world > 1 else "ddp"
+    engine = DataParallelEngine(
+        model, shard=(mode == "fsdp"),
+        mixed_precision=MixedPrecision(param_dtype=torch.bfloat16,
+                                       reduce_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32),
+        bucket_cap_mb=args.bucket_mb)
+    engine.configure_optimizer(OptimConfig(name="adamw", lr=args.lr, betas=(0.9, 0.95), weight_decay=0.1))
+
+    B, S = args.micro_batch, args.seq_len
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    batches = [torch.randint(0, margs.vocab_size, (B, S + 1), device=dev, generator=g) for _ in range(4)]
+
+    def train_step(i):
+        t = batches[i % len(batches)]
+        loss = model(t[:, :-1], t[:, 1:])
+        loss.backward()
+        engine.step()
+        engine.zero_grad()
+        return loss
+
+    def sync_all():
+        torch.cuda.synchronize()
+        if world > 1:
+            rt.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        loss = train_step(i)
+    if args.warmup:
+        first_loss = float(loss)
+    sync_all()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = train_step(args.warmup + i)
+    engine.synchronize()
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    last_loss = float(loss)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    tokens = world * B * S * args.steps
+    tps = tokens / elapsed
+    ms = 1000.0 * elapsed / args.steps
+    flops_tok = margs.flops_per_token(S)
+    mfu = tps / world * flops_tok / 2.5e15
+    peak_gb = torch.cuda.max_memory_allocated() / 1e9
+    if rank == 0:
+        rec = {
+            "metric": BASELINE_METRIC,
+            "value": round(tps, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random tokens, random-init weights)",
+            "config": {
+                "model": "Llama-2-7B" if args.model == "llama2-7b" else args.model,
+                "global_batch": world * B,
+                "seq_len": S,
+                "parallelism": f"{mode}{world}",
+                "micro_batch_per_gpu": B,
+                "tokens_per_step": world * B * S,
+            },
+            "tokens_per_sec_per_gpu": round(tps / world, 2),
+            "mfu_vs_2.5PF_bf16_dense": round(mfu, 4),
+            "peak_hbm_gb": round(peak_gb, 2),
+            "loss_first_warmup": round(first_loss, 4) if args.warmup else None,
+            "loss_last": round(last_loss, 4),
+        }
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as fh:
+                fh.write(line + "\n")
+    if world > 1:
+        rt.cleanup_distributed()
+
+
+if __name__ == "__main__":
+    main()

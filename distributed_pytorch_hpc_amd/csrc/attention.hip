@@ -11,12 +11,14 @@
 // transposed LDS reads.  K/V tiles (64 keys) are register-staged into a double-buffered, XOR-swizzled
 // LDS image (conflict-free for both ds_read_b128 row reads and tr reads), one barrier per tile.
 //
-// Backward: one workgroup = 4 waves (one per SIMD) = 128 keys of one (batch, kv-head); each wave owns 32 keys and keeps
-// dK^T and dV^T in registers while the workgroup sweeps all query heads of the GQA group x 32-row query
-// tiles.  S and dP are computed with the key on the lane, so P and dS are directly the B operands of
-// dV^T += dO^T P and dK^T += Q^T dS; dS crosses LDS once (a [key][q] image) for dQ = dS K, which
-// waves 0..D/32-1 compute for one 32-column d-tile each over all 128 keys and add to an fp32 dQ
-// accumulator with 256-B-per-instruction global atomics (1/320 atomic byte per FLOP).
+// Backward (no atomics, no dS round trip through LDS): two kernels after a delta = rowsum(dO*O) pass.
+//   dK/dV kernel, KV-stationary: a wave keeps its 32 keys' K^T / V^T fragments and dK^T / dV^T in registers
+//   while the workgroup sweeps query tiles; S and dP are computed with the key on the lane so P and dS are
+//   directly the B operands of dV^T += dO^T P and dK^T += Q^T dS.
+//   dQ kernel, Q-stationary (the forward's structure): S^T, dP^T with the query on the lane, dS^T lane-local,
+//   dQ^T += K^T dS^T with dS^T consumed from the accumulator.
+// The split costs 2 extra MFMA products (S, dP recomputed) but removes the fp32 dQ atomics that bound a
+// fused kernel at ~1.3 TB/s of atomic traffic (MI355X_MICROARCH.md 'Global float atomics').
 #include "dph_common.h"
 #include "kernels.h"
 
@@ -47,6 +49,28 @@ __device__ __forceinline__ bf16x8 lds_tr2(const char* base, int off_lo, int off_
   i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + off_hi));
   bf16x4 a = __builtin_bit_cast(bf16x4, lo), b = __builtin_bit_cast(bf16x4, hi);
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// Stage ROWS rows x NC 16-B chunks of a strided bf16 global tile into an img_off-swizzled LDS image by
+// LDS-DMA (global_load_lds_dwordx4: per-lane source address, lane-linear destination).  The swizzle is
+// applied to the SOURCE address (cdna_hip_programming.md rule 21); rows >= nvalid read the last valid row
+// (finite data that the caller masks), so no lane ever reads out of bounds.
+template <int NC, int ROWS, int NT>
+__device__ __forceinline__ void glds_stage(char* img, const bf16* base, int64_t rstride, int row0, int nvalid) {
+  constexpr int CHUNKS = ROWS * NC;
+  const int tid = threadIdx.x, wave = tid >> 6;
+#pragma unroll
+  for (int i = 0; i < (CHUNKS + NT - 1) / NT; ++i) {
+    const int L = tid + NT * i;
+    if (CHUNKS % NT == 0 || L < CHUNKS) {
+      const int line = L >> 4, slot = L & 15;
+      const int F = (line << 4) + (slot ^ (((line & 3) << 2) | ((line >> 2) & 3)));
+      const int row = min(row0 + F / NC, nvalid - 1);
+      const bf16* src = base + (int64_t)row * rstride + (F % NC) * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(img + (wave * 64 + NT * i) * 16),
+                                       16, 0, 0);
+    }
+  }
 }
 
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -80,7 +104,6 @@ template <int HD, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
   constexpr int BM = 128, BN = 64, NC = HD / 8, KS = HD / 16, DT = HD / 32;
   constexpr int TILE = BN * HD * 2;          // bytes of one K (or V) tile image
-  constexpr int CPT = (BN * NC) / 256;       // 16-B chunks per thread per tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
@@ -114,37 +137,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
   float m = -INFINITY, lsum = 0.f;
   const float sl2 = p.scale * 1.4426950408889634f;
 
-  bf16x8 stk[CPT], stv[CPT];
-  auto gload = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int F = threadIdx.x + 256 * i;
-      const int key = t * BN + F / NC, ch = F % NC;
-      if (key < p.Sk) {
-        stk[i] = *reinterpret_cast<const bf16x8*>(kp + (int64_t)key * p.k_ss + ch * 8);
-        stv[i] = *reinterpret_cast<const bf16x8*>(vp + (int64_t)key * p.v_ss + ch * 8);
-      } else {
-        stk[i] = zero8();
-        stv[i] = zero8();
-      }
-    }
-  };
-  auto swrite = [&](int buf) {
+  auto stage = [&](int t, int buf) {
     char* Kl = smem + buf * 2 * TILE;
-    char* Vl = Kl + TILE;
-#pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int F = threadIdx.x + 256 * i;
-      const int o_ = img_off<NC>(F / NC, F % NC);
-      *reinterpret_cast<bf16x8*>(Kl + o_) = stk[i];
-      *reinterpret_cast<bf16x8*>(Vl + o_) = stv[i];
-    }
+    glds_stage<NC, BN, 256>(Kl, kp, p.k_ss, t * BN, p.Sk);
+    glds_stage<NC, BN, 256>(Kl + TILE, vp, p.v_ss, t * BN, p.Sk);
   };
 
-  if (ntiles > 0) {
-    gload(0);
-    swrite(0);
-  }
+  if (ntiles > 0) stage(0, 0);
   __syncthreads();
 
   // per-lane constant parts of the tr-read addresses (A = V^T operand)
@@ -152,7 +151,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
 
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
-    if (t + 1 < ntiles) gload(t + 1);
+    if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
     const char* Kl = smem + buf * 2 * TILE;
     const char* Vl = Kl + TILE;
 
@@ -224,7 +223,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
         o[dt] = mfma32(a, pf[ks], o[dt]);
       }
     }
-    if (t + 1 < ntiles) swrite(buf ^ 1);
     __syncthreads();
   }
 
@@ -276,31 +274,21 @@ __global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ o, 
   }
 }
 
-// dq (bf16, [B,Sq,Hq,D] contiguous) = scale * dq_accum
-__global__ __launch_bounds__(256) void attn_dq_convert_k(const float* __restrict__ acc, bf16* __restrict__ dq,
-                                                         int64_t n8, float scale) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
-    float v[8];
-    Vec8<float>::load(acc + i * 8, v);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] *= scale;
-    Vec8<bf16>::store(dq + i * 8, v);
-  }
-}
-
+// ---- dK / dV: KV-stationary.  One workgroup = 4 waves = 128 keys of one (batch, kv head); one wave =
+// 32 keys whose K^T / V^T B-operand fragments stay in registers.  The workgroup sweeps every query head
+// of the GQA group x 32-row query tiles (double-buffered Q / dO LDS images, one barrier per tile).
+// S and dP are computed with the key on the lane, so P and dS are directly the B operands of
+// dV^T += dO^T P and dK^T += Q^T dS: no LDS round trip, no atomics.
 template <int HD, bool CAUSAL>
-__global__ __launch_bounds__(256, 1) void attn_bwd_k(AttnBwdParams P) {
-  constexpr int NT = 256;                   // 4 waves, one per SIMD: the whole 512-entry register file per wave
-  constexpr int BNK = 128, BMQ = 32, NC = HD / 8, KS = HD / 16, DT = HD / 32;
-  constexpr int KIMG = BNK * HD * 2;        // K image [128 keys][HD]
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
+  constexpr int NT = 256, BNK = 128, BMQ = 32, NC = HD / 8, KS = HD / 16, DT = HD / 32;
   constexpr int QIMG = BMQ * HD * 2;        // Q / dO tile image [32 q][HD]
-  constexpr int SIMG = BNK * BMQ * 2;       // dS image [128 keys][32 q]
-  // smem: K | Q0 | dO0 | Q1 | dO1 | dS | lse[2][32] | delta[2][32]
+  constexpr int KIMG = BNK * HD * 2;        // K image [128 keys][HD] (B operand of S = Q K^T)
+  // smem: K | Q0 | dO0 | Q1 | dO1 | lse[2][32] | delta[2][32]
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Kimg = smem;
-  char* Qbuf = smem + KIMG;                  // Q buf b at Qbuf + b*2*QIMG, dO at +QIMG
-  char* Simg = Qbuf + 4 * QIMG;
-  float* lse_s = reinterpret_cast<float*>(Simg + SIMG);
+  char* Qbuf = smem + KIMG;
+  float* lse_s = reinterpret_cast<float*>(Qbuf + 4 * QIMG);
   float* del_s = lse_s + 2 * BMQ;
 
   const AttnParams& p = P.f;
@@ -310,58 +298,38 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_k(AttnBwdParams P) {
   const int hk = blockIdx.y, b = blockIdx.z;
   const int grp = p.Hq / p.Hkv;
   const int off = p.Sk - p.Sq;
-  const int mykey = kb0 + wid * 32 + l32;
+  const int key0 = kb0 + wid * 32;
+  const int mykey = key0 + l32;
   const float sl2 = p.scale * 1.4426950408889634f;
 
   const bf16* kp = (const bf16*)p.k + (int64_t)b * p.k_sb + (int64_t)hk * p.k_sh;
   const bf16* vp = (const bf16*)p.v + (int64_t)b * p.v_sb + (int64_t)hk * p.v_sh;
-
-  // K image (all BNK keys) in LDS; V^T fragments of this wave's 32 keys in registers.
-#pragma unroll
-  for (int i = 0; i < (BNK * NC) / NT; ++i) {
-    const int F = threadIdx.x + NT * i;
-    const int key = kb0 + F / NC, ch = F % NC;
-    bf16x8 v = key < p.Sk ? *reinterpret_cast<const bf16x8*>(kp + (int64_t)key * p.k_ss + ch * 8) : zero8();
-    *reinterpret_cast<bf16x8*>(Kimg + img_off<NC>(F / NC, ch)) = v;
-  }
+  glds_stage<NC, BNK, NT>(Kimg, kp, p.k_ss, kb0, p.Sk);
   bf16x8 vf[KS];
 #pragma unroll
   for (int kk = 0; kk < KS; ++kk)
-    vf[kk] = mykey < p.Sk ? *reinterpret_cast<const bf16x8*>(vp + (int64_t)mykey * p.v_ss + kk * 16 + 8 * h) : zero8();
-
+    vf[kk] = mykey < p.Sk ? *reinterpret_cast<const bf16x8*>(vp + (int64_t)mykey * p.v_ss + kk * 16 + 8 * h)
+                          : zero8();
   f32x16 dk[DT], dv[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
 
-  // query tiles: causal -> only queries q with q + off >= kb0 can see any key of this block
   int qstart = 0;
   if (CAUSAL) qstart = max(0, kb0 - off) / BMQ * BMQ;
   const int nqt_head = qstart < p.Sq ? (p.Sq - qstart + BMQ - 1) / BMQ : 0;
   const int total = nqt_head * grp;
 
-  // staging registers for the next Q / dO tile (one 16-B chunk each per thread when HD = 128)
-  constexpr int QCPT = (BMQ * NC + NT - 1) / NT;
-  bf16x8 stq[QCPT], sto[QCPT];
   float st_lse = 0.f, st_del = 0.f;
-  auto gload = [&](int it) {
+  auto stage = [&](int it, int buf) {
     const int hq = hk * grp + it / nqt_head;
     const int qt0 = qstart + (it % nqt_head) * BMQ;
     const bf16* qp = (const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
     const bf16* dop = (const bf16*)P.dout + (int64_t)b * P.do_sb + (int64_t)hq * P.do_sh;
-#pragma unroll
-    for (int i = 0; i < QCPT; ++i) {
-      const int F = threadIdx.x + NT * i;
-      const int q = qt0 + F / NC, ch = F % NC;
-      if (F < BMQ * NC && q < p.Sq) {
-        stq[i] = *reinterpret_cast<const bf16x8*>(qp + (int64_t)q * p.q_ss + ch * 8);
-        sto[i] = *reinterpret_cast<const bf16x8*>(dop + (int64_t)q * P.do_ss + ch * 8);
-      } else {
-        stq[i] = zero8();
-        sto[i] = zero8();
-      }
-    }
+    char* Ql = Qbuf + buf * 2 * QIMG;
+    glds_stage<NC, BMQ, NT>(Ql, qp, p.q_ss, qt0, p.Sq);
+    glds_stage<NC, BMQ, NT>(Ql + QIMG, dop, P.do_ss, qt0, p.Sq);
     if (threadIdx.x < BMQ) {
       const int q = qt0 + threadIdx.x;
       const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + q;
@@ -369,18 +337,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_k(AttnBwdParams P) {
       st_del = q < p.Sq ? P.delta[idx] : 0.f;
     }
   };
-  auto swrite = [&](int buf) {
-    char* Ql = Qbuf + buf * 2 * QIMG;
-    char* Ol = Ql + QIMG;
-#pragma unroll
-    for (int i = 0; i < QCPT; ++i) {
-      const int F = threadIdx.x + NT * i;
-      if (F < BMQ * NC) {
-        const int o_ = img_off<NC>(F / NC, F % NC);
-        *reinterpret_cast<bf16x8*>(Ql + o_) = stq[i];
-        *reinterpret_cast<bf16x8*>(Ol + o_) = sto[i];
-      }
-    }
+  auto stage_scalars = [&](int buf) {
     if (threadIdx.x < BMQ) {
       lse_s[buf * BMQ + threadIdx.x] = st_lse;
       del_s[buf * BMQ + threadIdx.x] = st_del;
@@ -388,105 +345,69 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_k(AttnBwdParams P) {
   };
 
   if (total > 0) {
-    gload(0);
-    swrite(0);
+    stage(0, 0);
+    stage_scalars(0);
   }
   __syncthreads();
 
   for (int it = 0; it < total; ++it) {
     const int buf = it & 1;
-    const int hq = hk * grp + it / nqt_head;
     const int qt0 = qstart + (it % nqt_head) * BMQ;
-    if (it + 1 < total) gload(it + 1);
+    if (it + 1 < total) stage(it + 1, buf ^ 1);
     const char* Ql = Qbuf + buf * 2 * QIMG;
     const char* Ol = Ql + QIMG;
-
-    // S = Q K^T and dP = dO V^T with the key on the lane: A = Q / dO rows (LDS), B = K^T / V^T.
-    f32x16 s, dp;
+    // a wave whose 32 keys are all hidden from this query tile by the causal mask skips the tile
+    if (!(CAUSAL && key0 > qt0 + BMQ - 1 + off)) {
+      f32x16 s, dp;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-      const bf16x8 kf = lds_b128(Kimg, img_off<NC>(wid * 32 + l32, kk * 2 + h));
-      const bf16x8 qa = lds_b128(Ql, img_off<NC>(l32, kk * 2 + h));
-      const bf16x8 oa = lds_b128(Ol, img_off<NC>(l32, kk * 2 + h));
-      s = mfma32(qa, kf, s);
-      dp = mfma32(oa, vf[kk], dp);
-    }
-    // P = exp2(S * c - lse), dS = P (dP - delta); rows = queries
-    const bool need_mask = CAUSAL && (kb0 + wid * 32 + 31 > qt0 + off);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int qr = acc_row(r, h);
-      float pv = exp2_(s[r] * sl2 - lse_s[buf * BMQ + qr]);
-      if (qt0 + qr >= p.Sq || mykey >= p.Sk) pv = 0.f;
-      if (need_mask && mykey > qt0 + qr + off) pv = 0.f;
-      s[r] = pv;
-      dp[r] = pv * (dp[r] - del_s[buf * BMQ + qr]);
-    }
-    bf16x8 pb[2], sb[2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        pb[ks][j] = (bf16)s[8 * ks + j];
-        sb[ks][j] = (bf16)dp[8 * ks + j];
+      for (int kk = 0; kk < KS; ++kk) {
+        const bf16x8 qa = lds_b128(Ql, img_off<NC>(l32, kk * 2 + h));
+        const bf16x8 oa = lds_b128(Ol, img_off<NC>(l32, kk * 2 + h));
+        const bf16x8 kf = lds_b128(Kimg, img_off<NC>(wid * 32 + l32, kk * 2 + h));
+        s = mfma32(qa, kf, s);
+        dp = mfma32(oa, vf[kk], dp);
       }
-    // dV^T += dO^T P ; dK^T += Q^T dS   (A via transposed reads, k-order matching the accumulator)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int qrow = ks * 16 + 4 * (g >> 1) + tq;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const int ch = dt * 4 + 2 * (g & 1) + (tp >> 1);
-        const int bo = 8 * (tp & 1);
-        const bf16x8 oa = lds_tr2(Ol, img_off<NC>(qrow, ch) + bo, img_off<NC>(qrow + 8, ch) + bo);
-        dv[dt] = mfma32(oa, pb[ks], dv[dt]);
-        const bf16x8 qa = lds_tr2(Ql, img_off<NC>(qrow, ch) + bo, img_off<NC>(qrow + 8, ch) + bo);
-        dk[dt] = mfma32(qa, sb[ks], dk[dt]);
-      }
-    }
-    // dS -> LDS as a [key][q] image (64-B rows): lane writes 4 consecutive q per group
-#pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      bf16x4 w;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = (bf16)dp[4 * gg + j];
-      *reinterpret_cast<bf16x4*>(Simg + (wid * 32 + l32) * (BMQ * 2) + (8 * gg + 4 * h) * 2) = w;
-    }
-    __syncthreads();
-    // dQ[q][d] += sum_key dS[q][key] K[key][d] for d-tile `wid` (waves 0..DT-1)
-    if (wid < DT) {
-      f32x16 dq;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dq[r] = 0.f;
-#pragma unroll 4
-      for (int kstep = 0; kstep < BNK / 16; ++kstep) {
-        // A = dS [q x key]: lane (q = l32) needs keys 16*kstep + 8h + 0..7 -> tr reads of the [key][q] image
-        const int krow = kstep * 16 + 8 * h + tq;
-        const int qcol = 16 * (g & 1) + 4 * tp;
-        const bf16x8 a = lds_tr2(Simg, krow * (BMQ * 2) + qcol * 2, (krow + 4) * (BMQ * 2) + qcol * 2);
-        // B = K [key x d]: lane (d = l32) needs keys 16*kstep + 8h + 0..7 -> tr reads of the K image
-        const int ch = wid * 4 + 2 * (g & 1) + (tp >> 1);
-        const int bo = 8 * (tp & 1);
-        const bf16x8 kb = lds_tr2(Kimg, img_off<NC>(krow, ch) + bo, img_off<NC>(krow + 4, ch) + bo);
-        dq = mfma32(a, kb, dq);
-      }
-      float* dqp = P.dq_accum + ((int64_t)b * p.Sq) * p.Hq * HD + (int64_t)hq * HD + wid * 32 + l32;
+      const bool need_mask = CAUSAL && (key0 + 31 > qt0 + off);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int q = qt0 + acc_row(r, h);
-        if (q < p.Sq) atomicAdd(dqp + (int64_t)q * p.Hq * HD, dq[r]);
+        const int qr = acc_row(r, h);
+        float pv = exp2_(s[r] * sl2 - lse_s[buf * BMQ + qr]);
+        if (qt0 + qr >= p.Sq || mykey >= p.Sk) pv = 0.f;
+        if (need_mask && mykey > qt0 + qr + off) pv = 0.f;
+        s[r] = pv;
+        dp[r] = pv * (dp[r] - del_s[buf * BMQ + qr]);
+      }
+      bf16x8 pb[2], sb[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pb[ks][j] = (bf16)s[8 * ks + j];
+          sb[ks][j] = (bf16)dp[8 * ks + j];
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int qrow = ks * 16 + 4 * (g >> 1) + tq;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const int ch = dt * 4 + 2 * (g & 1) + (tp >> 1);
+          const int bo = 8 * (tp & 1);
+          const bf16x8 oa = lds_tr2(Ol, img_off<NC>(qrow, ch) + bo, img_off<NC>(qrow + 8, ch) + bo);
+          dv[dt] = mfma32(oa, pb[ks], dv[dt]);
+          const bf16x8 qa = lds_tr2(Ql, img_off<NC>(qrow, ch) + bo, img_off<NC>(qrow + 8, ch) + bo);
+          dk[dt] = mfma32(qa, sb[ks], dk[dt]);
+        }
       }
     }
-    if (it + 1 < total) swrite(buf ^ 1);
+    if (it + 1 < total) stage_scalars(buf ^ 1);
     __syncthreads();
   }
 
-  // epilogue: dK = scale * dK^T^T, dV ; per-kv-head complete (all query heads of the group swept)
   if (mykey < p.Sk) {
-    bf16* dkp = (bf16*)P.dk + (((int64_t)b * p.Sk + mykey) * p.Hkv + hk) * HD;
-    bf16* dvp = (bf16*)P.dv + (((int64_t)b * p.Sk + mykey) * p.Hkv + hk) * HD;
+    bf16* dkp = (bf16*)P.dk + (int64_t)b * P.dk_sb + (int64_t)mykey * P.dk_ss + (int64_t)hk * P.dk_sh;
+    bf16* dvp = (bf16*)P.dv + (int64_t)b * P.dv_sb + (int64_t)mykey * P.dv_ss + (int64_t)hk * P.dv_sh;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -499,6 +420,128 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_k(AttnBwdParams P) {
         }
         *reinterpret_cast<bf16x4*>(dkp + dt * 32 + 8 * gg + 4 * h) = wk;
         *reinterpret_cast<bf16x4*>(dvp + dt * 32 + 8 * gg + 4 * h) = wv;
+      }
+  }
+}
+
+// ---- dQ: Q-stationary, the forward's structure.  One workgroup = 4 waves = 128 queries; a lane owns one
+// query (lane & 31).  Per 64-key tile: S^T = K Q^T and dP^T = V dO^T (A = K / V rows from LDS, B = Q^T / dO^T
+// fragments in registers), P^T = exp2(S^T c - lse) and dS^T = P^T (dP^T - delta) lane-locally (lse and delta
+// are one scalar per lane), then dQ^T += K^T dS^T with dS^T consumed straight from the accumulator.
+template <int HD, bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
+  constexpr int BM = 128, BN = 64, NC = HD / 8, KS = HD / 16, DT = HD / 32;
+  constexpr int TILE = BN * HD * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const AttnParams& p = P.f;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  const int nqb = (p.Sq + BM - 1) / BM;
+  const int qb = CAUSAL ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int hq = blockIdx.y, b = blockIdx.z;
+  const int hk = hq / (p.Hq / p.Hkv);
+  const int q0 = qb * BM;
+  const int myq = q0 + wid * 32 + l32;
+  const int off = p.Sk - p.Sq;
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  const bf16* qp = (const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
+  const bf16* dop = (const bf16*)P.dout + (int64_t)b * P.do_sb + (int64_t)hq * P.do_sh;
+  const bf16* kp = (const bf16*)p.k + (int64_t)b * p.k_sb + (int64_t)hk * p.k_sh;
+  const bf16* vp = (const bf16*)p.v + (int64_t)b * p.v_sb + (int64_t)hk * p.v_sh;
+
+  bf16x8 qf[KS], df[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const bool ok = myq < p.Sq;
+    qf[kk] = ok ? *reinterpret_cast<const bf16x8*>(qp + (int64_t)myq * p.q_ss + kk * 16 + 8 * h) : zero8();
+    df[kk] = ok ? *reinterpret_cast<const bf16x8*>(dop + (int64_t)myq * P.do_ss + kk * 16 + 8 * h) : zero8();
+  }
+  float lse2 = 0.f, delta = 0.f;
+  if (myq < p.Sq) {
+    const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + myq;
+    lse2 = p.lse[idx] * 1.4426950408889634f;
+    delta = P.delta[idx];
+  }
+
+  int kv_end = p.Sk;
+  if (CAUSAL) kv_end = min(p.Sk, q0 + BM + off);
+  const int ntiles = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
+
+  f32x16 dq[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
+
+  auto stage = [&](int t, int buf) {
+    char* Kl = smem + buf * 2 * TILE;
+    glds_stage<NC, BN, 256>(Kl, kp, p.k_ss, t * BN, p.Sk);
+    glds_stage<NC, BN, 256>(Kl + TILE, vp, p.v_ss, t * BN, p.Sk);
+  };
+  if (ntiles > 0) stage(0, 0);
+  __syncthreads();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
+    const char* Kl = smem + buf * 2 * TILE;
+    const char* Vl = Kl + TILE;
+    const int k0 = t * BN;
+    const bool need_mask = (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0 + wid * 32 + off));
+    bf16x8 sf[4];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      f32x16 s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const bf16x8 ka = lds_b128(Kl, img_off<NC>(sub * 32 + l32, kk * 2 + h));
+        const bf16x8 va = lds_b128(Vl, img_off<NC>(sub * 32 + l32, kk * 2 + h));
+        s = mfma32(ka, qf[kk], s);
+        dp = mfma32(va, df[kk], dp);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float pv = exp2_(s[r] * sl2 - lse2);
+        if (need_mask) {
+          const int key = k0 + sub * 32 + acc_row(r, h);
+          if (key >= p.Sk || (CAUSAL && key > myq + off)) pv = 0.f;
+        }
+        s[r] = pv * (dp[r] - delta);
+      }
+#pragma unroll
+      for (int half = 0; half < 2; ++half)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sf[sub * 2 + half][j] = (bf16)s[8 * half + j];
+    }
+    // dQ^T += K^T dS^T
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int krow = ks * 16 + 4 * (g >> 1) + tq;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int ch = dt * 4 + 2 * (g & 1) + (tp >> 1);
+        const int bo = 8 * (tp & 1);
+        const bf16x8 a = lds_tr2(Kl, img_off<NC>(krow, ch) + bo, img_off<NC>(krow + 8, ch) + bo);
+        dq[dt] = mfma32(a, sf[ks], dq[dt]);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (myq < p.Sq) {
+    bf16* dqp = (bf16*)P.dq + (int64_t)b * P.dq_sb + (int64_t)myq * P.dq_ss + (int64_t)hq * P.dq_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        bf16x4 w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) w[j] = (bf16)(dq[dt][4 * gg + j] * p.scale);
+        *reinterpret_cast<bf16x4*>(dqp + dt * 32 + 8 * gg + 4 * h) = w;
       }
   }
 }
@@ -525,36 +568,29 @@ void flash_attn_fwd(const AttnParams& p, hipStream_t st) {
 template <int HD>
 static void bwd_launch(const AttnBwdParams& P, hipStream_t st) {
   const AttnParams& p = P.f;
-  const size_t lds = 128 * HD * 2 + 4 * 32 * HD * 2 + 128 * 32 * 2 + 4 * 32 * 4;
-  static bool attr_set[2] = {false, false};
-  if (!attr_set[p.causal ? 1 : 0]) {
-    if (p.causal) hipFuncSetAttribute((const void*)attn_bwd_k<HD, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    else hipFuncSetAttribute((const void*)attn_bwd_k<HD, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set[p.causal ? 1 : 0] = true;
-  }
-  const dim3 grid((p.Sk + 127) / 128, p.Hkv, p.B);
-  if (p.causal) hipLaunchKernelGGL((attn_bwd_k<HD, true>), grid, dim3(256), lds, st, P);
-  else hipLaunchKernelGGL((attn_bwd_k<HD, false>), grid, dim3(256), lds, st, P);
+  const size_t lds_kv = 128 * HD * 2 + 4 * 32 * HD * 2 + 4 * 32 * 4;
+  const dim3 grid_kv((p.Sk + 127) / 128, p.Hkv, p.B);
+  if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true>), grid_kv, dim3(256), lds_kv, st, P);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false>), grid_kv, dim3(256), lds_kv, st, P);
+  const size_t lds_q = 2 * 2 * 64 * HD * 2;
+  const dim3 grid_q((p.Sq + 127) / 128, p.Hq, p.B);
+  if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true>), grid_q, dim3(256), lds_q, st, P);
+  else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false>), grid_q, dim3(256), lds_q, st, P);
 }
 
 void flash_attn_bwd(const AttnBwdParams& P, hipStream_t st) {
   const AttnParams& p = P.f;
   if (p.B == 0 || p.Sq == 0) return;
-  // delta = rowsum(dO * O)
   const int64_t rows = (int64_t)p.B * p.Hq * p.Sq;
   hipLaunchKernelGGL(attn_delta_k, dim3(stream_grid(rows, 4)), dim3(256), 0, st, (const bf16*)p.o,
                      (const bf16*)P.dout, P.delta, p.B, p.Sq, p.Hq, p.D, p.o_sb, p.o_ss, p.o_sh, P.do_sb, P.do_ss,
                      P.do_sh);
-  const int64_t nq = (int64_t)p.B * p.Sq * p.Hq * p.D;
-  hipMemsetAsync(P.dq_accum, 0, nq * sizeof(float), st);
   switch (p.D) {
     case 32: bwd_launch<32>(P, st); break;
     case 64: bwd_launch<64>(P, st); break;
     case 128: bwd_launch<128>(P, st); break;
     default: break;
   }
-  hipLaunchKernelGGL(attn_dq_convert_k, dim3(stream_grid(nq / 8, 256)), dim3(256), 0, st, P.dq_accum, (bf16*)P.dq,
-                     nq / 8, p.scale);
 }
 
 }  // namespace dph

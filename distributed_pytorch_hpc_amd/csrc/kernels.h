@@ -76,8 +76,8 @@ struct AttnBwdParams {
   const void* dout; int64_t do_sb, do_ss, do_sh;
   float* delta;          // fp32 [B, Hq, Sq] workspace: rowsum(dO * O)
   float* dq_accum;       // fp32 [B, Sq, Hq, D] workspace, zeroed by the launcher
-  void* dq; void* dk; void* dv;   // bf16, [B,S,H,D] contiguous; dk/dv are per KV head (GQA summed)
-  float* dk_accum; float* dv_accum; // fp32 [B, Sk, Hkv, D] when Hq != Hkv (GQA), else null
+  void* dq; void* dk; void* dv;   // bf16 [B,S,H,D] at the strides below; dk/dv per KV head (GQA summed)
+  int64_t dq_sb, dq_ss, dq_sh, dk_sb, dk_ss, dk_sh, dv_sb, dv_ss, dv_sh;
 };
 void flash_attn_bwd(const AttnBwdParams& p, hipStream_t stream);
 

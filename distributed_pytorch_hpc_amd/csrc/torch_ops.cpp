@@ -268,27 +268,44 @@ std::tuple<Tensor, Tensor> flash_attn_fwd(const Tensor& q, const Tensor& k, cons
   return {o, lse};
 }
 
-std::tuple<Tensor, Tensor, Tensor> flash_attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k,
-                                                  const Tensor& v, const Tensor& o, const Tensor& lse, double scale,
-                                                  bool causal) {
+void flash_attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                         const Tensor& lse, double scale, bool causal, Tensor& dq, Tensor& dk, Tensor& dv) {
   c10::DeviceGuard g(q.device());
   check_attn_operand(q, "q"); check_attn_operand(k, "k"); check_attn_operand(v, "v");
   check_attn_operand(o, "o"); check_attn_operand(dout, "dout");
-  TORCH_CHECK(dout.sizes() == o.sizes() && o.sizes() == q.sizes(), "flash_attn_bwd: dout/o shape mismatch");
-  const int64_t B = q.size(0), Sq = q.size(1), Hq = q.size(2), D = q.size(3), Sk = k.size(1), Hkv = k.size(2);
-  auto dq = at::empty({B, Sq, Hq, D}, q.options());
-  auto dk = at::empty({B, Sk, Hkv, D}, q.options());
-  auto dv = at::empty({B, Sk, Hkv, D}, q.options());
+  check_attn_operand(dq, "dq"); check_attn_operand(dk, "dk"); check_attn_operand(dv, "dv");
+  TORCH_CHECK(dout.sizes() == o.sizes() && o.sizes() == q.sizes() && dq.sizes() == q.sizes(),
+              "flash_attn_bwd: dout/o/dq shape mismatch");
+  TORCH_CHECK(dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "flash_attn_bwd: dk/dv shape mismatch");
+  const int64_t B = q.size(0), Sq = q.size(1), Hq = q.size(2), D = q.size(3);
   auto delta = at::empty({B, Hq, Sq}, q.options().dtype(at::kFloat));
   auto dq_acc = at::empty({B, Sq, Hq, D}, q.options().dtype(at::kFloat));
   dph::AttnBwdParams P{};
-  P.f = make_params(q, k, v, o, lse.contiguous(), scale, causal);
+  auto lse_c = lse.contiguous();
+  P.f = make_params(q, k, v, o, lse_c, scale, causal);
   P.dout = dout.data_ptr(); P.do_sb = dout.stride(0); P.do_ss = dout.stride(1); P.do_sh = dout.stride(2);
   P.delta = delta.data_ptr<float>();
   P.dq_accum = dq_acc.data_ptr<float>();
   P.dq = dq.data_ptr(); P.dk = dk.data_ptr(); P.dv = dv.data_ptr();
+  P.dq_sb = dq.stride(0); P.dq_ss = dq.stride(1); P.dq_sh = dq.stride(2);
+  P.dk_sb = dk.stride(0); P.dk_ss = dk.stride(1); P.dk_sh = dk.stride(2);
+  P.dv_sb = dv.stride(0); P.dv_ss = dv.stride(1); P.dv_sh = dv.stride(2);
   dph::flash_attn_bwd(P, cur_stream());
+}
+
+std::tuple<Tensor, Tensor, Tensor> flash_attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k,
+                                                  const Tensor& v, const Tensor& o, const Tensor& lse, double scale,
+                                                  bool causal) {
+  auto dq = at::empty(q.sizes(), q.options());
+  auto dk = at::empty(k.sizes(), k.options());
+  auto dv = at::empty(v.sizes(), v.options());
+  flash_attn_bwd_impl(dout, q, k, v, o, lse, scale, causal, dq, dk, dv);
   return {dq, dk, dv};
+}
+
+void flash_attn_bwd_into(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                         const Tensor& lse, double scale, bool causal, Tensor dq, Tensor dk, Tensor dv) {
+  flash_attn_bwd_impl(dout, q, k, v, o, lse, scale, causal, dq, dk, dv);
 }
 
 // ------------------------------------------------------------------------------------------------ embedding
@@ -336,6 +353,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal) -> (Tensor, Tensor)");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal) "
         "-> (Tensor, Tensor, Tensor)");
+  m.def("flash_attn_bwd_into(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, "
+        "bool causal, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
 }
@@ -356,6 +375,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("cross_entropy_fwd", &cross_entropy_fwd);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
+  m.impl("flash_attn_bwd_into", &flash_attn_bwd_into);
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
 }

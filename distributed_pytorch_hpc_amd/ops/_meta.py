@@ -89,6 +89,11 @@ def _fa_bwd(dout, q, k, v, o, lse, scale, causal):
     return torch.empty_like(q), k.new_empty(k.shape), v.new_empty(v.shape)
 
 
+@register_fake("dph::flash_attn_bwd_into")
+def _fa_bwd_into(dout, q, k, v, o, lse, scale, causal, dq, dk, dv):
+    return None
+
+
 @register_fake("dph::embedding_fwd")
 def _emb_fwd(ids, table, vocab_start):
     return table.new_empty((*ids.shape, table.shape[1]))

@@ -132,10 +132,14 @@ class _RopeFlashAttnFn(torch.autograd.Function):
         q = qkv[:, :, : nh * hd].view(b, s, nh, hd)
         k = qkv[:, :, nh * hd: (nh + nkv) * hd].view(b, s, nkv, hd)
         v = qkv[:, :, (nh + nkv) * hd:].view(b, s, nkv, hd)
-        dq, dk, dv = flash_bwd(do.view(b, s, nh, hd), q, k, v, o, lse, scale, causal)
-        rope_(dq, cos, sin, pos_offset, True)
-        rope_(dk, cos, sin, pos_offset, True)
-        dqkv = torch.cat((dq.view(b, s, -1), dk.view(b, s, -1), dv.view(b, s, -1)), dim=-1)
+        dqkv = torch.empty_like(qkv)
+        dq = dqkv[:, :, : nh * hd].view(b, s, nh, hd)
+        dk = dqkv[:, :, nh * hd: (nh + nkv) * hd].view(b, s, nkv, hd)
+        dv = dqkv[:, :, (nh + nkv) * hd:].view(b, s, nkv, hd)
+        _lib.ops().flash_attn_bwd_into(do.view(b, s, nh, hd).contiguous(), q, k, v, o, lse, scale, causal,
+                                       dq, dk, dv)
+        # inverse rotation of dq and dk in one strided launch ([B, S, Hq + Hkv, hd] view)
+        rope_(dqkv[:, :, : (nh + nkv) * hd].view(b, s, nh + nkv, hd), cos, sin, pos_offset, True)
         if _dqkv_passthrough is not None:
             dqkv = dqkv + _dqkv_passthrough
         return dqkv, None, None, None, None, None, None, None, None

@@ -23,13 +23,15 @@ class _FusedXentFn(torch.autograd.Function):
         need_grad = ctx.needs_input_grad[0]
         loss_rows, _ = _lib.ops().cross_entropy_fwd(logits, target, inv, ignore_index, need_grad, smoothing)
         if need_grad:
-            ctx.mark_dirty(logits)
-            ctx.save_for_backward(logits)
-        return loss_rows.sum() * inv[0], logits
+            # the kernel overwrote the logits buffer with d(loss)/d(logits) (a raw in-place write that the
+            # autograd version counter does not see; nothing else saved these logits for backward)
+            ctx.grad_buf = logits
+        return loss_rows.sum() * inv[0]
 
     @staticmethod
-    def backward(ctx, gloss, _glogits):
-        (g,) = ctx.saved_tensors
+    def backward(ctx, gloss):
+        g = ctx.grad_buf
+        ctx.grad_buf = None
         g.mul_(gloss.to(g.dtype))
         return g, None, None, None
 
@@ -44,8 +46,7 @@ def fused_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index
     if _lib.use_native(logits) and logits.dtype in (torch.bfloat16, torch.float32):
         if not inplace:
             logits = logits.clone()
-        loss, _ = _FusedXentFn.apply(logits, target.contiguous(), ignore_index, float(label_smoothing))
-        return loss
+        return _FusedXentFn.apply(logits, target.contiguous(), ignore_index, float(label_smoothing))
     return F.cross_entropy(logits.float(), target, ignore_index=ignore_index, label_smoothing=label_smoothing)
 
 
