@@ -1,0 +1,217 @@
+"""Autograd-aware collectives (the conjugate pairs every model-parallel layer is built from).
+
+Reference capability: the implicit DTensor redistributions of the TP/SP plan (fsdp_tp/fsdp_tp_example.py:142-184,
+SURVEY.md C6-C11) and the doc-only Ulysses all-to-all / ring P2P (docs/guide/08_sequence_parallel.md).
+Here each redistribution is one explicit RCCL call with its exact adjoint in backward:
+
+    copy_to_group          fwd identity            bwd all-reduce          (Megatron "f")
+    reduce_from_group      fwd all-reduce          bwd identity            (Megatron "g")
+    gather_along_dim       fwd all-gather(dim)     bwd reduce-scatter(dim) (SP: Shard(1) -> Replicate)
+    reduce_scatter_along   fwd reduce-scatter(dim) bwd all-gather(dim)     (SP: Partial -> Shard(1))
+    split_along_dim        fwd take local chunk    bwd all-gather(dim)
+    all_to_all_4d          fwd all-to-all          bwd inverse all-to-all  (Ulysses head<->sequence)
+
+All collectives run on contiguous buffers (a transpose+contiguous at most) so RCCL moves one large
+message per call; on gloo (CPU tests) the same code runs unchanged.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def _ws(group) -> int:
+    return dist.get_world_size(group) if dist.is_initialized() else 1
+
+
+def _rank(group) -> int:
+    return dist.get_rank(group) if dist.is_initialized() else 0
+
+
+# ------------------------------------------------------------------------------------------- raw helpers
+def all_gather_dim(x: torch.Tensor, dim: int, group) -> torch.Tensor:
+    ws = _ws(group)
+    if ws == 1:
+        return x
+    x = x.contiguous()
+    if dim == 0:
+        out = torch.empty((ws * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x, group=group)
+        return out
+    xt = x.movedim(dim, 0).contiguous()
+    out = torch.empty((ws * xt.shape[0], *xt.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, xt, group=group)
+    return out.movedim(0, dim)
+
+
+def reduce_scatter_dim(x: torch.Tensor, dim: int, group) -> torch.Tensor:
+    ws = _ws(group)
+    if ws == 1:
+        return x
+    assert x.shape[dim] % ws == 0, f"reduce_scatter: dim {dim} size {x.shape[dim]} not divisible by {ws}"
+    xt = x.movedim(dim, 0).contiguous()
+    out = torch.empty((xt.shape[0] // ws, *xt.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.reduce_scatter_tensor(out, xt, op=dist.ReduceOp.SUM, group=group)
+    return out.movedim(0, dim)
+
+
+def split_dim(x: torch.Tensor, dim: int, group) -> torch.Tensor:
+    ws = _ws(group)
+    if ws == 1:
+        return x
+    assert x.shape[dim] % ws == 0, f"split: dim {dim} size {x.shape[dim]} not divisible by {ws}"
+    return x.chunk(ws, dim=dim)[_rank(group)].contiguous()
+
+
+def all_reduce_(x: torch.Tensor, group, op=dist.ReduceOp.SUM) -> torch.Tensor:
+    if _ws(group) > 1:
+        dist.all_reduce(x, op=op, group=group)
+    return x
+
+
+# ------------------------------------------------------------------------------------------- autograd
+class _CopyToGroup(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        return all_reduce_(g.contiguous(), ctx.group), None
+
+
+class _ReduceFromGroup(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, group):
+        return all_reduce_(x.contiguous().clone() if _ws(group) > 1 else x, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+class _GatherDim(torch.autograd.Function):
+    """all-gather; adjoint = reduce-scatter (downstream work is partitioned across the group, so each rank
+    holds a PARTIAL gradient of the gathered tensor -- sequence parallelism)."""
+
+    @staticmethod
+    def forward(ctx, x, dim, group):
+        ctx.dim, ctx.group = dim, group
+        return all_gather_dim(x, dim, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return reduce_scatter_dim(g, ctx.dim, ctx.group), None, None
+
+
+class _GatherDimReplicated(torch.autograd.Function):
+    """all-gather; adjoint = take the local chunk (downstream work is REPLICATED on every rank, so each rank
+    already holds the full gradient -- e.g. gathering TP output logits before a replicated loss)."""
+
+    @staticmethod
+    def forward(ctx, x, dim, group):
+        ctx.dim, ctx.group = dim, group
+        return all_gather_dim(x, dim, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return split_dim(g, ctx.dim, ctx.group), None, None
+
+
+class _ReduceScatterDim(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dim, group):
+        ctx.dim, ctx.group = dim, group
+        return reduce_scatter_dim(x, dim, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return all_gather_dim(g, ctx.dim, ctx.group), None, None
+
+
+class _SplitDim(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dim, group):
+        ctx.dim, ctx.group = dim, group
+        return split_dim(x, dim, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return all_gather_dim(g, ctx.dim, ctx.group), None, None
+
+
+def copy_to_group(x, group):
+    return _CopyToGroup.apply(x, group) if _ws(group) > 1 else x
+
+
+def reduce_from_group(x, group):
+    return _ReduceFromGroup.apply(x, group) if _ws(group) > 1 else x
+
+
+def gather_along_dim(x, dim, group):
+    return _GatherDim.apply(x, dim, group) if _ws(group) > 1 else x
+
+
+def gather_replicated_along_dim(x, dim, group):
+    return _GatherDimReplicated.apply(x, dim, group) if _ws(group) > 1 else x
+
+
+def reduce_scatter_along_dim(x, dim, group):
+    return _ReduceScatterDim.apply(x, dim, group) if _ws(group) > 1 else x
+
+
+def split_along_dim(x, dim, group):
+    return _SplitDim.apply(x, dim, group) if _ws(group) > 1 else x
+
+
+# ------------------------------------------------------------------------------------------- all-to-all
+def _a2a(x: torch.Tensor, scatter_dim: int, gather_dim: int, group) -> torch.Tensor:
+    """Split ``x`` into world chunks along scatter_dim, exchange, concatenate along gather_dim."""
+    ws = _ws(group)
+    if ws == 1:
+        return x
+    chunks = [c.contiguous() for c in x.chunk(ws, dim=scatter_dim)]
+    inp = torch.stack(chunks, 0).contiguous()
+    out = torch.empty_like(inp)
+    dist.all_to_all_single(out, inp, group=group)
+    return torch.cat(out.unbind(0), dim=gather_dim)
+
+
+class _AllToAll(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, scatter_dim, gather_dim, group):
+        ctx.dims, ctx.group = (scatter_dim, gather_dim), group
+        return _a2a(x, scatter_dim, gather_dim, group)
+
+    @staticmethod
+    def backward(ctx, g):
+        sd, gd = ctx.dims
+        return _a2a(g, gd, sd, ctx.group), None, None, None
+
+
+def all_to_all(x, scatter_dim: int, gather_dim: int, group):
+    return _AllToAll.apply(x, scatter_dim, gather_dim, group) if _ws(group) > 1 else x
+
+
+# ------------------------------------------------------------------------------------------- reductions for loss-parallel
+class _AllReduceSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return all_reduce_(x.clone(), group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+def all_reduce_autograd_sum(x, group):
+    """sum over ranks; each rank's input contributes to the (replicated) output, so grad is identity."""
+    return _AllReduceSum.apply(x, group) if _ws(group) > 1 else x
+
+
+def all_reduce_autograd_max(x, group):
+    """max over ranks, treated as a constant (used for the numerically-stable softmax shift only)."""
+    x = x.detach().clone()
+    return all_reduce_(x, group, op=dist.ReduceOp.MAX)

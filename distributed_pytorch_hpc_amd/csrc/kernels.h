@@ -13,8 +13,10 @@ enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 void rmsnorm_fwd(const void* x, const void* w, const void* residual, void* h_out, void* y, float* rstd,
                  int64_t rows, int dim, float eps, int x_dtype, int w_dtype, hipStream_t stream);
 // dx (x dtype) and dw_partial (fp32 [nblk, dim]) then dw (w dtype) by a column reduction.
-void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx, float* dw_partial,
-                 void* dw, int nblk, int64_t rows, int dim, int x_dtype, int w_dtype, hipStream_t stream);
+// dres (optional, x dtype): a residual-stream gradient added into dx in the same pass.
+void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, const void* dres, void* dx,
+                 float* dw_partial, void* dw, int nblk, int64_t rows, int dim, int x_dtype, int w_dtype,
+                 hipStream_t stream);
 int rmsnorm_bwd_blocks(int64_t rows);
 
 // ---- LayerNorm (nn.LayerNorm semantics, used by ViT / pipeline transformer) ----

@@ -127,17 +127,27 @@ __global__ __launch_bounds__(256) void ln_bwd_k(const T* __restrict__ dy, const 
 }
 
 template <typename W>
-__global__ __launch_bounds__(256) void ln_col_reduce_k(const float* __restrict__ part, W* __restrict__ dw,
-                                                       W* __restrict__ db, int nblk, int D) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= D) return;
+__global__ __launch_bounds__(1024) void ln_col_reduce_k(const float* __restrict__ part, W* __restrict__ dw,
+                                                        W* __restrict__ db, int nblk, int D) {
+  __shared__ float red[2][16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
   float a = 0.f, c = 0.f;
-  for (int b = 0; b < nblk; ++b) {
-    a += part[(int64_t)b * 2 * D + col];
-    c += part[(int64_t)b * 2 * D + D + col];
+  if (col < D)
+    for (int b = wv; b < nblk; b += 16) {
+      a += part[(int64_t)b * 2 * D + col];
+      c += part[(int64_t)b * 2 * D + D + col];
+    }
+  red[0][wv][lane] = a;
+  red[1][wv][lane] = c;
+  __syncthreads();
+  if (wv == 0 && col < D) {
+    float ta = 0.f, tc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { ta += red[0][k][lane]; tc += red[1][k][lane]; }
+    dw[col] = (W)ta;
+    db[col] = (W)tc;
   }
-  dw[col] = (W)a;
-  db[col] = (W)c;
 }
 
 template <typename T, typename W>
@@ -163,7 +173,7 @@ static void ln_bwd_d(const void* dy, const void* x, const void* w, const float* 
   else if (D <= 8192) L(4);
   else L(8);
 #undef L
-  hipLaunchKernelGGL((ln_col_reduce_k<W>), dim3((int)cdiv(D, 256)), dim3(256), 0, st, part, (W*)dw, (W*)db, nblk, D);
+  hipLaunchKernelGGL((ln_col_reduce_k<W>), dim3((int)cdiv(D, 64)), dim3(1024), 0, st, part, (W*)dw, (W*)db, nblk, D);
 }
 
 void layernorm_fwd(const void* x, const void* w, const void* b, void* y, float* mean, float* rstd, int64_t rows,

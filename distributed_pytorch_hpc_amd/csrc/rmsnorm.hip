@@ -105,8 +105,8 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_big_k(const T* __restrict__ x
 template <typename T, typename W, int CPT>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const W* __restrict__ w, const float* __restrict__ rstd,
-                                                     T* __restrict__ dx, float* __restrict__ dw_partial,
-                                                     int64_t rows, int D) {
+                                                     const T* __restrict__ dres, T* __restrict__ dx,
+                                                     float* __restrict__ dw_partial, int64_t rows, int D) {
   __shared__ float red[2][4];
   float wv[CPT][8], dwacc[CPT][8];
 #pragma unroll
@@ -158,6 +158,12 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, c
           const float xh = xv[c][i] * rs;
           o[i] = rs * (g[c][i] * wv[c][i] - xh * mdot);
         }
+        if (dres) {
+          float d2[8];
+          Vec8<T>::load(dres + r * D + idx, d2);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] += d2[i];
+        }
         Vec8<T>::store(dx + r * D + idx, o);
       }
     }
@@ -169,15 +175,25 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, c
   }
 }
 
-// Column reduction of [nblk, D] fp32 partials -> dw (W dtype).
+// Column reduction of [nblk, D] fp32 partials -> dw (W dtype): one 1024-thread workgroup per 64 columns,
+// each of its 16 waves sums a strided subset of the partial rows (256-B coalesced row segments), then LDS.
 template <typename W>
-__global__ __launch_bounds__(256) void col_reduce_k(const float* __restrict__ part, W* __restrict__ out, int nblk,
-                                                    int D) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= D) return;
+__global__ __launch_bounds__(1024) void col_reduce_k(const float* __restrict__ part, W* __restrict__ out, int nblk,
+                                                     int D) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * D + col];
-  out[col] = (W)s;
+  if (col < D)
+    for (int b = wv; b < nblk; b += 16) s += part[(int64_t)b * D + col];
+  red[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += red[k][lane];
+    if (col < D) out[col] = (W)t;
+  }
 }
 
 template <typename T, typename W>
@@ -219,33 +235,34 @@ void rmsnorm_fwd(const void* x, const void* w, const void* residual, void* h_out
 }
 
 int rmsnorm_bwd_blocks(int64_t rows) {
-  int64_t g = rows < 1024 ? rows : 1024;
+  int64_t g = rows < 512 ? rows : 512;
   return (int)(g < 1 ? 1 : g);
 }
 
 template <typename T, typename W>
-static void bwd_dispatch(const void* dy, const void* x, const void* w, const float* rstd, void* dx, float* part,
-                         void* dw, int nblk, int64_t rows, int D, hipStream_t st) {
+static void bwd_dispatch(const void* dy, const void* x, const void* w, const float* rstd, const void* dres, void* dx,
+                         float* part, void* dw, int nblk, int64_t rows, int D, hipStream_t st) {
   const T* dyp = (const T*)dy; const T* xp = (const T*)x; const W* wp = (const W*)w; T* dxp = (T*)dx;
-#define LAUNCHB(N) hipLaunchKernelGGL((rmsnorm_bwd_k<T, W, N>), dim3(nblk), dim3(256), 0, st, dyp, xp, wp, rstd, dxp, \
-                                      part, rows, D);
+#define LAUNCHB(N) hipLaunchKernelGGL((rmsnorm_bwd_k<T, W, N>), dim3(nblk), dim3(256), 0, st, dyp, xp, wp, rstd, \
+                                      (const T*)dres, dxp, part, rows, D);
   if (D <= 2048) { LAUNCHB(1) }
   else if (D <= 4096) { LAUNCHB(2) }
   else if (D <= 8192) { LAUNCHB(4) }
   else if (D <= 16384) { LAUNCHB(8) }
   else { LAUNCHB(16) }
 #undef LAUNCHB
-  hipLaunchKernelGGL((col_reduce_k<W>), dim3((int)cdiv(D, 256)), dim3(256), 0, st, part, (W*)dw, nblk, D);
+  hipLaunchKernelGGL((col_reduce_k<W>), dim3((int)cdiv(D, 64)), dim3(1024), 0, st, part, (W*)dw, nblk, D);
 }
 
-void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, void* dx, float* dw_partial,
-                 void* dw, int nblk, int64_t rows, int dim, int x_dtype, int w_dtype, hipStream_t stream) {
+void rmsnorm_bwd(const void* dy, const void* x, const void* w, const float* rstd, const void* dres, void* dx,
+                 float* dw_partial, void* dw, int nblk, int64_t rows, int dim, int x_dtype, int w_dtype,
+                 hipStream_t stream) {
   if (x_dtype == kBF16) {
-    if (w_dtype == kBF16) bwd_dispatch<bf16, bf16>(dy, x, w, rstd, dx, dw_partial, dw, nblk, rows, dim, stream);
-    else bwd_dispatch<bf16, float>(dy, x, w, rstd, dx, dw_partial, dw, nblk, rows, dim, stream);
+    if (w_dtype == kBF16) bwd_dispatch<bf16, bf16>(dy, x, w, rstd, dres, dx, dw_partial, dw, nblk, rows, dim, stream);
+    else bwd_dispatch<bf16, float>(dy, x, w, rstd, dres, dx, dw_partial, dw, nblk, rows, dim, stream);
   } else {
-    if (w_dtype == kBF16) bwd_dispatch<float, bf16>(dy, x, w, rstd, dx, dw_partial, dw, nblk, rows, dim, stream);
-    else bwd_dispatch<float, float>(dy, x, w, rstd, dx, dw_partial, dw, nblk, rows, dim, stream);
+    if (w_dtype == kBF16) bwd_dispatch<float, bf16>(dy, x, w, rstd, dres, dx, dw_partial, dw, nblk, rows, dim, stream);
+    else bwd_dispatch<float, float>(dy, x, w, rstd, dres, dx, dw_partial, dw, nblk, rows, dim, stream);
   }
 }
 

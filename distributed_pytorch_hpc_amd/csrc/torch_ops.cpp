@@ -54,7 +54,8 @@ std::tuple<Tensor, Tensor, Tensor> rmsnorm_fwd(const Tensor& x, const Tensor& w,
   return {y, rstd, h};
 }
 
-std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& rstd) {
+std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& w, const Tensor& rstd,
+                                       const c10::optional<Tensor>& dres) {
   c10::DeviceGuard g(x.device());
   TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && w.is_contiguous(), "rmsnorm_bwd: contiguous required");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type(), "rmsnorm_bwd: dy/x dtype mismatch");
@@ -65,7 +66,13 @@ std::tuple<Tensor, Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& x, const 
   if (rows == 0) return {dx, dw.zero_()};
   const int nblk = dph::rmsnorm_bwd_blocks(rows);
   auto part = at::empty({nblk, D}, x.options().dtype(at::kFloat));
-  dph::rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dx.data_ptr(),
+  const void* dr = nullptr;
+  if (dres.has_value()) {
+    TORCH_CHECK(dres->is_contiguous() && dres->sizes() == x.sizes() && dres->scalar_type() == x.scalar_type(),
+                "rmsnorm_bwd: dres must match x");
+    dr = dres->data_ptr();
+  }
+  dph::rmsnorm_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(), dr, dx.data_ptr(),
                    part.data_ptr<float>(), dw.data_ptr(), nblk, rows, (int)D, dt_code(x), dt_code(w), cur_stream());
   return {dx, dw};
 }
@@ -335,7 +342,7 @@ Tensor embedding_bwd(const Tensor& ids, const Tensor& dout, int64_t vocab_local,
 
 TORCH_LIBRARY(dph, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps, Tensor? residual=None) -> (Tensor, Tensor, Tensor)");
-  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd) -> (Tensor, Tensor)");
+  m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None) -> (Tensor, Tensor)");
   m.def("layernorm_fwd(Tensor x, Tensor w, Tensor b, float eps) -> (Tensor, Tensor, Tensor)");
   m.def("layernorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor mean, Tensor rstd) -> (Tensor, Tensor, Tensor)");
   m.def("rope_(Tensor(a!) x, Tensor cos, Tensor sin, int pos_offset, bool inverse) -> ()");

@@ -186,7 +186,11 @@ class Transformer(nn.Module):
         self.model_args = args
         self.vocab_size = args.vocab_size
         self.n_layers = args.n_layers
-        self.tok_embeddings = nn.Embedding(args.vocab_size, args.dim)
+        self.tok_embeddings = ops.Embedding(args.vocab_size, args.dim)
+        # set by parallel.tensor_parallel.parallelize_llama
+        self.tp_group = None
+        self.sequence_parallel = False
+        self.loss_parallel = False
         self.layers = nn.ModuleList([TransformerBlock(i, args) for i in range(args.n_layers)])
         self.norm = ops.RMSNorm(args.dim, eps=args.norm_eps)
         self.output = nn.Linear(args.dim, args.vocab_size, bias=False)
@@ -206,7 +210,7 @@ class Transformer(nn.Module):
         nn.init.trunc_normal_(self.output.weight, mean=0.0, std=std, a=-3 * std, b=3 * std)
 
     def embed(self, tokens: torch.Tensor) -> torch.Tensor:
-        return ops.embedding(tokens, self.tok_embeddings.weight)
+        return self.tok_embeddings(tokens)
 
     def head(self, h: torch.Tensor, delta: Optional[torch.Tensor], targets: Optional[torch.Tensor] = None):
         if delta is None:
@@ -214,6 +218,16 @@ class Transformer(nn.Module):
         else:
             _, x = ops.add_rms_norm(h, delta, self.norm.weight, self.norm.eps)
         logits = self.output(x)
+        if self.loss_parallel and self.tp_group is not None:
+            # vocab-sharded logits [B, S, V/tp] ("loss parallel", no [B, S, V] all-gather)
+            vloc = logits.shape[-1]
+            vstart = torch.distributed.get_rank(self.tp_group) * vloc
+            if targets is None:
+                from ..comm.functional import gather_replicated_along_dim
+
+                return gather_replicated_along_dim(logits, logits.dim() - 1, self.tp_group).float()
+            return ops.vocab_parallel_cross_entropy(logits.reshape(-1, vloc), targets.reshape(-1), vstart,
+                                                    self.tp_group)
         if targets is None:
             return logits.float()
         return ops.fused_cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1))

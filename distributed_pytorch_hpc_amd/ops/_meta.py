@@ -17,7 +17,7 @@ def _rmsnorm_fwd(x, w, eps, residual=None):
 
 
 @register_fake("dph::rmsnorm_bwd")
-def _rmsnorm_bwd(dy, x, w, rstd):
+def _rmsnorm_bwd(dy, x, w, rstd, dres=None):
     return torch.empty_like(x), torch.empty_like(w)
 
 

@@ -59,10 +59,9 @@ class _AddRMSNormFn(torch.autograd.Function):
         h, w, rstd = ctx.saved_tensors
         if dy is None:
             dy = torch.zeros_like(h)
-        dx, dw = _lib.ops().rmsnorm_bwd(dy.reshape(h.shape).contiguous(), h, w.contiguous(), rstd)
+        dres = dh.reshape(h.shape).contiguous() if dh is not None else None
+        dx, dw = _lib.ops().rmsnorm_bwd(dy.reshape(h.shape).contiguous(), h, w.contiguous(), rstd, dres)
         dx = dx.view(ctx.shape)
-        if dh is not None:
-            dx = dx + dh
         return dx, dx, dw, None
 
 

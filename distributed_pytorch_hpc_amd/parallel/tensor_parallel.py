@@ -1,0 +1,211 @@
+"""Tensor parallelism (Megatron 1-D) and sequence parallelism over an explicit TP process group.
+
+Capability parity with the reference's DTensor plans -- ``parallelize_module`` with ``ColwiseParallel``,
+``RowwiseParallel``, ``SequenceParallel`` and ``PrepareModuleInput`` (fsdp_tp/tensor_parallel_example.py:115-122,
+scripts/03_tensor_parallel_tp/tensor_parallel_vit.py:352-361, fsdp_tp/fsdp_tp_example.py:142-184) -- but every
+layout change is one explicit RCCL collective with a hand-written adjoint (comm/functional.py) and the
+parameters stay plain tensors (local shards), so the data-parallel engine, the fused optimizer and the
+HIP kernels see ordinary contiguous buffers.
+
+Styles (applied by ``parallelize_module(module, tp_group, plan)``):
+  ColwiseParallel(sequence_parallel=False, gather_output=False, shard_fn=None)
+      weight [out, in] -> rows out/tp.  Input: replicated (copy_to_group: grad all-reduced) or, with
+      sequence_parallel, seq-sharded [B, S/tp, *] all-gathered along dim 1 (grad reduce-scattered).
+  RowwiseParallel(sequence_parallel=False, shard_fn=None)
+      weight [out, in] -> columns in/tp.  Output: partial sums all-reduced, or reduce-scattered along the
+      sequence (SP).  A bias is added once, after the reduction.
+  VocabParallelEmbedding(sequence_parallel=False)
+      table rows vocab/tp; out-of-shard ids give zero rows (HIP gather kernel), partial embeddings are
+      all-reduced or reduce-scattered along the sequence (SP) -- the reference's
+      RowwiseParallel(input_layouts=Replicate(), output_layouts=Shard(1)) on tok_embeddings.
+  SequenceParallel()
+      replicated weights of a per-token module (norms) that runs on a sequence shard; their gradients
+      are all-reduced over the TP group (partial over the local tokens).
+
+``parallelize_llama(model, tp_group, sequence_parallel=True, loss_parallel=True)`` applies the TorchTitan-style
+plan of the reference (fsdp_tp_example.py:142-184) to models/llama2.Transformer, including the fused
+wqkv / w13 projections (sharded per head / per half) and vocab-parallel cross-entropy ("loss parallel":
+only [N] all-reduces instead of all-gathering [B, S, V] logits).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+from torch import nn
+
+from .. import ops
+from ..comm import functional as cf
+from .linear import linear as _linear
+
+
+def _ws(group):
+    return dist.get_world_size(group) if dist.is_initialized() else 1
+
+
+def _rank(group):
+    return dist.get_rank(group) if dist.is_initialized() else 0
+
+
+def shard_rows(w: torch.Tensor, group) -> torch.Tensor:
+    ws, r = _ws(group), _rank(group)
+    assert w.shape[0] % ws == 0, f"cannot shard {w.shape[0]} rows over {ws} ranks"
+    return w.chunk(ws, 0)[r].contiguous()
+
+
+def shard_cols(w: torch.Tensor, group) -> torch.Tensor:
+    ws, r = _ws(group), _rank(group)
+    assert w.shape[1] % ws == 0, f"cannot shard {w.shape[1]} columns over {ws} ranks"
+    return w.chunk(ws, 1)[r].contiguous()
+
+
+def shard_rows_grouped(w: torch.Tensor, sizes: list[int], group) -> torch.Tensor:
+    """Row-shard each block of a row-concatenated fused weight separately (wqkv = [q; k; v], w13 = [w1; w3])."""
+    parts = torch.split(w, sizes, 0)
+    return torch.cat([shard_rows(p, group) for p in parts], 0).contiguous()
+
+
+class ColwiseParallelLinear(nn.Module):
+    def __init__(self, lin: nn.Linear, group, sequence_parallel: bool = False, gather_output: bool = False,
+                 shard_fn: Optional[Callable] = None, seq_dim: int = 1):
+        super().__init__()
+        self.group, self.sp, self.gather_output, self.seq_dim = group, sequence_parallel, gather_output, seq_dim
+        w = lin.weight.detach()
+        self.weight = nn.Parameter(shard_fn(w, group) if shard_fn else shard_rows(w, group),
+                                   requires_grad=lin.weight.requires_grad)
+        self.bias = None
+        if lin.bias is not None:
+            self.bias = nn.Parameter(shard_rows(lin.bias.detach()[:, None], group)[:, 0].contiguous())
+        self.in_features, self.out_features = lin.in_features, self.weight.shape[0]
+
+    def forward(self, x):
+        x = cf.gather_along_dim(x, self.seq_dim, self.group) if self.sp else cf.copy_to_group(x, self.group)
+        y = _linear(x, self.weight, self.bias)
+        if self.gather_output:
+            y = cf.gather_replicated_along_dim(y, y.dim() - 1, self.group)
+        return y
+
+
+class RowwiseParallelLinear(nn.Module):
+    def __init__(self, lin: nn.Linear, group, sequence_parallel: bool = False, shard_fn: Optional[Callable] = None,
+                 input_is_parallel: bool = True, seq_dim: int = 1):
+        super().__init__()
+        self.group, self.sp, self.input_is_parallel, self.seq_dim = group, sequence_parallel, input_is_parallel, seq_dim
+        w = lin.weight.detach()
+        self.weight = nn.Parameter(shard_fn(w, group) if shard_fn else shard_cols(w, group),
+                                   requires_grad=lin.weight.requires_grad)
+        self.bias = nn.Parameter(lin.bias.detach().clone()) if lin.bias is not None else None
+        self.in_features, self.out_features = self.weight.shape[1], lin.out_features
+
+    def forward(self, x):
+        if not self.input_is_parallel:
+            x = cf.split_along_dim(x, x.dim() - 1, self.group)
+        y = _linear(x, self.weight, None)
+        y = cf.reduce_scatter_along_dim(y, self.seq_dim, self.group) if self.sp else cf.reduce_from_group(y, self.group)
+        if self.bias is not None:
+            y = y + self.bias
+        return y
+
+
+class VocabParallelEmbedding(nn.Module):
+    def __init__(self, emb: nn.Embedding, group, sequence_parallel: bool = False, seq_dim: int = 1):
+        super().__init__()
+        self.group, self.sp, self.seq_dim = group, sequence_parallel, seq_dim
+        ws, r = _ws(group), _rank(group)
+        v = emb.weight.shape[0]
+        assert v % ws == 0, f"vocab {v} not divisible by tp {ws}"
+        self.vocab_start = r * (v // ws)
+        self.weight = nn.Parameter(shard_rows(emb.weight.detach(), group))
+
+    def forward(self, ids):
+        y = ops.embedding(ids, self.weight, self.vocab_start)
+        return cf.reduce_scatter_along_dim(y, self.seq_dim, self.group) if self.sp else cf.reduce_from_group(y, self.group)
+
+
+def mark_sequence_parallel(module: nn.Module, group):
+    """Replicated params of a module that runs on a sequence shard: all-reduce their grads over TP."""
+    if _ws(group) == 1:
+        return module
+    for p in module.parameters(recurse=False):
+        p.register_hook(lambda g, grp=group: cf.all_reduce_(g.contiguous().clone(), grp))
+        p._dph_sequence_parallel = True
+    return module
+
+
+# ------------------------------------------------------------------------------------------- plan API
+@dataclass
+class ColwiseParallel:
+    sequence_parallel: bool = False
+    gather_output: bool = False
+    shard_fn: Optional[Callable] = None
+
+    def apply(self, mod, group):
+        return ColwiseParallelLinear(mod, group, self.sequence_parallel, self.gather_output, self.shard_fn)
+
+
+@dataclass
+class RowwiseParallel:
+    sequence_parallel: bool = False
+    shard_fn: Optional[Callable] = None
+    input_is_parallel: bool = True
+
+    def apply(self, mod, group):
+        if isinstance(mod, nn.Embedding):
+            return VocabParallelEmbedding(mod, group, self.sequence_parallel)
+        return RowwiseParallelLinear(mod, group, self.sequence_parallel, self.shard_fn, self.input_is_parallel)
+
+
+@dataclass
+class SequenceParallel:
+    def apply(self, mod, group):
+        return mark_sequence_parallel(mod, group)
+
+
+def parallelize_module(module: nn.Module, tp_group, plan: dict) -> nn.Module:
+    """Replace submodules named in ``plan`` (dotted paths, relative to ``module``) by their TP versions."""
+    for name, style in plan.items():
+        parent = module
+        *path, leaf = name.split(".")
+        for p in path:
+            parent = getattr(parent, p)
+        child = getattr(parent, leaf)
+        new = style.apply(child, tp_group)
+        if new is not child:
+            setattr(parent, leaf, new)
+    return module
+
+
+# ------------------------------------------------------------------------------------------- Llama plan
+def parallelize_llama(model, tp_group, sequence_parallel: bool = True, loss_parallel: bool = True):
+    """TP(+SP) plan of fsdp_tp/fsdp_tp_example.py:142-184 for models.llama2.Transformer (fused projections)."""
+    tp = _ws(tp_group)
+    args = model.model_args
+    hd, nh, nkv = args.head_dim, args.n_heads, args.kv_heads
+    assert nh % tp == 0 and nkv % tp == 0, f"heads ({nh}, kv {nkv}) must divide by tp={tp}"
+    sp = sequence_parallel
+    qkv_sizes = [nh * hd, nkv * hd, nkv * hd]
+    f = args.ffn_hidden
+    assert f % tp == 0, f"ffn hidden {f} must divide by tp={tp}"
+    for layer in model.layers:
+        a = layer.attention
+        a.wqkv = ColwiseParallelLinear(a.wqkv, tp_group, sp, shard_fn=lambda w, g: shard_rows_grouped(w, qkv_sizes, g))
+        a.wo = RowwiseParallelLinear(a.wo, tp_group, sp)
+        a.n_local_heads, a.n_local_kv_heads = nh // tp, nkv // tp
+        ff = layer.feed_forward
+        ff.w13 = ColwiseParallelLinear(ff.w13, tp_group, sp, shard_fn=lambda w, g: shard_rows_grouped(w, [f, f], g))
+        ff.w2 = RowwiseParallelLinear(ff.w2, tp_group, sp)
+        ff.hidden_dim = f // tp
+        if sp:
+            mark_sequence_parallel(layer.attention_norm, tp_group)
+            mark_sequence_parallel(layer.ffn_norm, tp_group)
+    model.tok_embeddings = VocabParallelEmbedding(model.tok_embeddings, tp_group, sp)
+    if sp:
+        mark_sequence_parallel(model.norm, tp_group)
+    model.output = ColwiseParallelLinear(model.output, tp_group, sp, gather_output=not loss_parallel)
+    model.tp_group = tp_group
+    model.sequence_parallel = sp
+    model.loss_parallel = loss_parallel
+    return model
