@@ -40,6 +40,8 @@ def parse(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=256.0)
     ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--kernels", choices=["dph", "aten"], default="dph",
+                    help="dph: CDNA4 HIP kernels (default); aten: stock PyTorch-ROCm ops (comparator)")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args(argv)
@@ -65,6 +67,8 @@ def main(argv=None):
                                                                     OptimConfig)
 
     _lib.require()
+    if args.kernels == "aten":
+        _lib.set_reference_mode(True)
     margs = get_preset(args.model, max_seq_len=max(args.seq_len, 4096))
     model = build_llama(margs, device=dev, dtype=torch.bfloat16, seed=1234)
     mode = args.parallel
@@ -140,6 +144,8 @@ def main(argv=None):
                 "parallelism": f"{mode}{world}",
                 "micro_batch_per_gpu": B,
                 "tokens_per_step": world * B * S,
+                "kernels": args.kernels,
+                "bucket_mb": args.bucket_mb,
             },
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "mfu_vs_2.5PF_bf16_dense": round(mfu, 4),

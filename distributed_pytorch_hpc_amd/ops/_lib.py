@@ -69,9 +69,26 @@ def ops():
     return torch.ops.dph
 
 
+_reference_mode = False
+
+
+def set_reference_mode(enabled: bool) -> None:
+    """Route GPU tensors through the stock PyTorch-ROCm reference ops instead of the HIP kernels.
+
+    Only for A/B benchmarking (bench.py --kernels aten: the "stock PyTorch" comparator of BASELINE.md) and
+    debugging; never enabled implicitly.
+    """
+    global _reference_mode
+    _reference_mode = bool(enabled)
+
+
+def reference_mode() -> bool:
+    return _reference_mode
+
+
 def use_native(t: torch.Tensor) -> bool:
     """True when ``t`` lives on the GPU (then the HIP kernel MUST be used)."""
-    if t.is_cuda:
+    if t.is_cuda and not _reference_mode:
         require()
         return True
     return False

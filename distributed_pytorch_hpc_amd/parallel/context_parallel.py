@@ -1,0 +1,233 @@
+"""Context (sequence) parallelism for long sequences: DeepSpeed-Ulysses and ring attention.
+
+The reference only DOCUMENTS these (docs/guide/08_sequence_parallel.md:41-142, SURVEY.md S-ULY / S-RING, C21/C22);
+here they are real, tested implementations on top of the CDNA4 flash-attention kernels:
+
+Ulysses (``UlyssesAttention``): the sequence is sharded over the CP group; before attention one all-to-all
+turns [B, S/P, H, D] into [B, S, H/P, D] (heads scattered, sequence gathered), attention runs on the full
+sequence for H/P heads, and a second all-to-all restores the sequence sharding.  4 all-to-alls per layer
+(q/k/v in, o out) map onto the fully connected xGMI mesh: every pair of GPUs is one hop, all 7 links busy.
+Requires heads % P == 0.
+
+Ring (``RingAttention``): each rank keeps its query chunk; K/V chunks rotate around the ring (P-1 hops,
+batch_isend_irecv posted BEFORE the local block so the xGMI transfer overlaps the flash kernel).  Blocks are
+merged with the online-softmax rule on (o, lse) -- the flash forward kernel emits the log-sum-exp.  Backward
+re-runs the ring: per block the flash backward kernel, fed the FINAL (o, lse), yields exact dq/dk/dv
+contributions; dK/dV accumulators travel with their K/V chunk and arrive home after P hops.  With causal
+attention and contiguous chunks, block (q_r, kv_j) is full for j < r, causal for j == r, skipped for j > r.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..comm import functional as cf
+from ..ops import _lib
+from ..ops.rope import rope_, rope_reference
+
+
+def _ws(g):
+    return dist.get_world_size(g) if dist.is_initialized() else 1
+
+
+def _rank(g):
+    return dist.get_rank(g) if dist.is_initialized() else 0
+
+
+def _split_qkv(qkv, nh, nkv, hd):
+    b, s, _ = qkv.shape
+    q = qkv[:, :, : nh * hd].view(b, s, nh, hd)
+    k = qkv[:, :, nh * hd:(nh + nkv) * hd].view(b, s, nkv, hd)
+    v = qkv[:, :, (nh + nkv) * hd:].view(b, s, nkv, hd)
+    return q, k, v
+
+
+# ================================================================================================ Ulysses
+class UlyssesAttention:
+    def __init__(self, group, causal: bool = True):
+        self.group, self.causal = group, causal
+
+    def __call__(self, qkv, cos, sin, nh, nkv, hd):
+        p = _ws(self.group)
+        assert nh % p == 0 and nkv % p == 0, f"Ulysses needs heads ({nh}, kv {nkv}) divisible by cp={p}"
+        b, s_loc, _ = qkv.shape
+        q, k, v = _split_qkv(qkv, nh, nkv, hd)
+        # [B, S/P, H, D] -> [B, S, H/P, D]
+        q = cf.all_to_all(q, 2, 1, self.group)
+        k = cf.all_to_all(k, 2, 1, self.group)
+        v = cf.all_to_all(v, 2, 1, self.group)
+        s = q.shape[1]
+        packed = torch.cat([q.reshape(b, s, -1), k.reshape(b, s, -1), v.reshape(b, s, -1)], dim=-1)
+        o = ops.rope_attention(packed, cos, sin, nh // p, nkv // p, hd, causal=self.causal)
+        o = o.view(b, s, nh // p, hd)
+        o = cf.all_to_all(o, 1, 2, self.group)    # back to [B, S/P, H, D]
+        return o.reshape(b, s_loc, nh * hd)
+
+
+# ================================================================================================ ring
+def _attn_fwd_lse(q, k, v, causal, scale):
+    """(o, lse) for one block; lse natural-log [B, H, S]."""
+    if q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (32, 64, 128):
+        return _lib.ops().flash_attn_fwd(q, k, v, scale, causal)
+    qf, kf, vf = q.float(), k.float(), v.float()
+    hq, hk = q.shape[2], k.shape[2]
+    if hq != hk:
+        kf, vf = kf.repeat_interleave(hq // hk, 2), vf.repeat_interleave(hq // hk, 2)
+    s = torch.einsum("bqhd,bkhd->bhqk", qf, kf) * scale
+    if causal:
+        sq, sk = q.shape[1], k.shape[1]
+        mask = torch.arange(sk)[None, :] <= torch.arange(sq)[:, None] + (sk - sq)
+        s = s.masked_fill(~mask.to(s.device), float("-inf"))
+    lse = torch.logsumexp(s, -1)
+    o = torch.einsum("bhqk,bkhd->bqhd", torch.exp(s - lse[..., None]), vf)
+    return o.to(q.dtype), lse
+
+
+def _attn_bwd(do, q, k, v, o, lse, causal, scale):
+    if q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (32, 64, 128):
+        return _lib.ops().flash_attn_bwd(do.contiguous(), q, k, v, o, lse, scale, causal)
+    qf, kf, vf, dof, of = (t.float() for t in (q, k, v, do, o))
+    hq, hk = q.shape[2], k.shape[2]
+    rep = hq // hk
+    if rep > 1:
+        kf, vf = kf.repeat_interleave(rep, 2), vf.repeat_interleave(rep, 2)
+    s = torch.einsum("bqhd,bkhd->bhqk", qf, kf) * scale
+    if causal:
+        sq, sk = q.shape[1], k.shape[1]
+        mask = torch.arange(sk)[None, :] <= torch.arange(sq)[:, None] + (sk - sq)
+        s = s.masked_fill(~mask.to(s.device), float("-inf"))
+    p = torch.exp(s - lse[..., None])
+    dv = torch.einsum("bhqk,bqhd->bkhd", p, dof)
+    dp = torch.einsum("bqhd,bkhd->bhqk", dof, vf)
+    delta = (dof * of).sum(-1).transpose(1, 2)[..., None]
+    ds = p * (dp - delta) * scale
+    dq = torch.einsum("bhqk,bkhd->bqhd", ds, kf)
+    dk = torch.einsum("bhqk,bqhd->bkhd", ds, qf)
+    if rep > 1:
+        dk = dk.view(*dk.shape[:2], hk, rep, dk.shape[-1]).sum(3)
+        dv = dv.view(*dv.shape[:2], hk, rep, dv.shape[-1]).sum(3)
+    return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
+
+
+def _merge(o, lse, o2, lse2):
+    """Online-softmax merge of two partial attentions (fp32 accumulators)."""
+    new = torch.logaddexp(lse, lse2)
+    w1 = torch.exp(lse - new).transpose(1, 2)[..., None]
+    w2 = torch.exp(lse2 - new).transpose(1, 2)[..., None]
+    return o * w1 + o2.float() * w2, new
+
+
+class _Ring:
+    """Posts the K/V (and optional dK/dV) transfer to the next rank before the local compute."""
+
+    def __init__(self, group):
+        self.group = group
+        ranks = dist.get_process_group_ranks(group)
+        r = _rank(group)
+        p = len(ranks)
+        self.next, self.prev = ranks[(r + 1) % p], ranks[(r - 1) % p]
+
+    def start(self, tensors):
+        bufs = [torch.empty_like(t) for t in tensors]
+        ops_ = []
+        for t, b in zip(tensors, bufs):
+            ops_.append(dist.P2POp(dist.isend, t.contiguous(), self.next, self.group))
+            ops_.append(dist.P2POp(dist.irecv, b, self.prev, self.group))
+        return dist.batch_isend_irecv(ops_), bufs
+
+
+class _RingAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, group, causal, scale):
+        p, r = _ws(group), _rank(group)
+        ring = _Ring(group)
+        o = lse = None
+        kc, vc = k.contiguous(), v.contiguous()
+        for i in range(p):
+            j = (r - i) % p                       # owner of the K/V chunk held at step i
+            works = bufs = None
+            if i < p - 1:
+                works, bufs = ring.start([kc, vc])
+            if not causal or j <= r:
+                ob, lb = _attn_fwd_lse(q, kc, vc, causal and j == r, scale)
+                if o is None:
+                    o, lse = ob.float(), lb
+                else:
+                    o, lse = _merge(o, lse, ob, lb)
+            if works is not None:
+                for w in works:
+                    w.wait()
+                kc, vc = bufs
+        out = o.to(q.dtype)
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.group, ctx.causal, ctx.scale = group, causal, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        group, causal, scale = ctx.group, ctx.causal, ctx.scale
+        p, r = _ws(group), _rank(group)
+        ring = _Ring(group)
+        dq = torch.zeros_like(q, dtype=torch.float32)
+        kc, vc = k.contiguous(), v.contiguous()
+        dkc = torch.zeros_like(k, dtype=torch.float32)
+        dvc = torch.zeros_like(v, dtype=torch.float32)
+        for i in range(p):
+            j = (r - i) % p
+            if not causal or j <= r:
+                dq_i, dk_i, dv_i = _attn_bwd(do, q, kc, vc, o, lse, causal and j == r, scale)
+                dq += dq_i.float()
+                dkc += dk_i.float()
+                dvc += dv_i.float()
+            # move (K, V, dK-acc, dV-acc) one hop; after p hops every accumulator is home
+            if i < p - 1:
+                works, (kc, vc, dkc_n, dvc_n) = ring.start([kc, vc, dkc, dvc])
+            else:
+                works, (dkc_n, dvc_n) = ring.start([dkc, dvc])
+            for w in works:
+                w.wait()
+            dkc, dvc = dkc_n, dvc_n
+        return dq.to(q.dtype), dkc.to(k.dtype), dvc.to(v.dtype), None, None, None
+
+
+def ring_attention(q, k, v, group, causal: bool = True, scale: float | None = None):
+    """Exact attention over a sequence sharded contiguously across ``group``: q/k/v [B, S/P, H, D]."""
+    scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
+    if _ws(group) == 1:
+        return ops.flash_attention(q, k, v, causal, scale)
+    return _RingAttnFn.apply(q, k, v, group, causal, scale)
+
+
+class RingAttention:
+    def __init__(self, group, causal: bool = True):
+        self.group, self.causal = group, causal
+
+    def __call__(self, qkv, cos, sin, nh, nkv, hd):
+        b, s_loc, _ = qkv.shape
+        off = _rank(self.group) * s_loc            # global position of the local chunk
+        q, k, v = _split_qkv(qkv, nh, nkv, hd)
+        if qkv.is_cuda:
+            from ..ops.rope import apply_rope
+
+            q, k = apply_rope(q, cos, sin, off), apply_rope(k, cos, sin, off)
+        else:
+            q, k = rope_reference(q, cos, sin, off), rope_reference(k, cos, sin, off)
+        o = ring_attention(q, k, v.contiguous(), self.group, self.causal)
+        return o.reshape(b, s_loc, nh * hd)
+
+
+def apply_context_parallel(model, cp_group, mode: str = "ulysses"):
+    """Install Ulysses / ring attention in every Attention module of a models.llama2.Transformer.
+
+    The caller shards tokens and targets contiguously along the sequence over ``cp_group`` and includes the cp
+    ranks in the gradient data-parallel group (each rank's loss is a mean over its local tokens).
+    """
+    impl = UlyssesAttention(cp_group) if mode == "ulysses" else RingAttention(cp_group)
+    for layer in model.layers:
+        layer.attention.cp_attention = impl
+    model.cp_group = cp_group
+    return model
