@@ -1,0 +1,146 @@
+"""ResNet-18/34/50/101/152, defined natively (torchvision is not installed in this environment).
+
+Capability parity with the torchvision models the reference trains (scripts/main.py:186-191,249 -- resnet18/50/101/152
+with pretrained=False; scripts/02_fully_sharded_fsdp/resnet_fsdp_training.py:186-191 -- ResNet-18 with the CIFAR stem:
+3x3 stride-1 conv1 and no max-pool).  The module tree and parameter names match torchvision
+(conv1, bn1, layer1..4[i].{conv1..3, bn1..3, downsample.{0,1}}, fc), so torchvision state dicts load directly and
+the parameter counts agree (ResNet-50: 25,557,032).
+
+MI355X-first choices: ``channels_last=True`` keeps activations NHWC (MIOpen's implicit-GEMM layout) end to end,
+BN-ReLU pairs are left adjacent for MIOpen fusion, and ``zero_init_residual`` is available (as torchvision).
+"""
+from __future__ import annotations
+
+from typing import Optional, Type, Union
+
+import torch
+from torch import nn
+
+
+def conv3x3(cin, cout, stride=1):
+    return nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+
+
+def conv1x1(cin, cout, stride=1):
+    return nn.Conv2d(cin, cout, 1, stride, bias=False)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = conv3x3(inplanes, planes, stride)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = conv3x3(planes, planes)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return self.relu(out + idt)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None):
+        super().__init__()
+        self.conv1 = conv1x1(inplanes, planes)
+        self.bn1 = nn.BatchNorm2d(planes)
+        self.conv2 = conv3x3(planes, planes, stride)
+        self.bn2 = nn.BatchNorm2d(planes)
+        self.conv3 = conv1x1(planes, planes * 4)
+        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.relu = nn.ReLU(inplace=True)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        return self.relu(out + idt)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block: Type[Union[BasicBlock, Bottleneck]], layers: list[int], num_classes: int = 1000,
+                 cifar_stem: bool = False, zero_init_residual: bool = False):
+        super().__init__()
+        self.inplanes = 64
+        if cifar_stem:
+            self.conv1 = nn.Conv2d(3, 64, 3, 1, 1, bias=False)
+            self.maxpool = nn.Identity()
+        else:
+            self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+            self.maxpool = nn.MaxPool2d(3, 2, 1)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.layer1 = self._make(block, 64, layers[0])
+        self.layer2 = self._make(block, 128, layers[1], 2)
+        self.layer3 = self._make(block, 256, layers[2], 2)
+        self.layer4 = self._make(block, 512, layers[3], 2)
+        self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
+        self.fc = nn.Linear(512 * block.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+                elif isinstance(m, BasicBlock):
+                    nn.init.zeros_(m.bn2.weight)
+
+    def _make(self, block, planes, blocks, stride=1):
+        down = None
+        if stride != 1 or self.inplanes != planes * block.expansion:
+            down = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
+                                 nn.BatchNorm2d(planes * block.expansion))
+        layers = [block(self.inplanes, planes, stride, down)]
+        self.inplanes = planes * block.expansion
+        layers += [block(self.inplanes, planes) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+    def forward(self, x):
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        return self.fc(torch.flatten(self.avgpool(x), 1))
+
+
+_CFG = {
+    "resnet18": (BasicBlock, [2, 2, 2, 2]),
+    "resnet34": (BasicBlock, [3, 4, 6, 3]),
+    "resnet50": (Bottleneck, [3, 4, 6, 3]),
+    "resnet101": (Bottleneck, [3, 4, 23, 3]),
+    "resnet152": (Bottleneck, [3, 8, 36, 3]),
+}
+
+
+def resnet(arch: str = "resnet50", num_classes: int = 1000, cifar_stem: bool = False, channels_last: bool = False,
+           **kw) -> ResNet:
+    block, layers = _CFG[arch]
+    m = ResNet(block, layers, num_classes=num_classes, cifar_stem=cifar_stem, **kw)
+    return m.to(memory_format=torch.channels_last) if channels_last else m
+
+
+def resnet18(**kw):
+    return resnet("resnet18", **kw)
+
+
+def resnet50(**kw):
+    return resnet("resnet50", **kw)
+
+
+def resnet101(**kw):
+    return resnet("resnet101", **kw)
+
+
+def resnet152(**kw):
+    return resnet("resnet152", **kw)

@@ -1,0 +1,58 @@
+"""SimpleUNet for ERA5-style gridded data (capability parity with
+scripts/01_data_parallel_ddp/multinode_ddp_unet.py:171-214; 7,742,849 parameters at 65 -> 65 channels).
+
+Same modules and names (enc1..3, bottleneck, up1..3, dec1..3, out, pool).  Convolutions run through MIOpen in
+channels-last (NHWC) layout when the model is moved to the GPU with ``to_channels_last`` -- the MI355X-native
+layout for implicit-GEMM convolutions; the odd 181-latitude grid is handled like the reference (bilinear
+resize of each up-sampled map to its skip connection size).  ``halo`` (domain parallelism, parallel/domain.py)
+swaps the 3x3 convolutions for halo-exchanging ones when the latitude axis is sharded across ranks.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+def conv_block(in_ch: int, out_ch: int) -> nn.Sequential:
+    return nn.Sequential(
+        nn.Conv2d(in_ch, out_ch, 3, padding=1), nn.BatchNorm2d(out_ch), nn.ReLU(inplace=True),
+        nn.Conv2d(out_ch, out_ch, 3, padding=1), nn.BatchNorm2d(out_ch), nn.ReLU(inplace=True),
+    )
+
+
+class SimpleUNet(nn.Module):
+    def __init__(self, in_channels: int = 65, out_channels: int = 65, base_dim: int = 64):
+        super().__init__()
+        b = base_dim
+        self.enc1 = conv_block(in_channels, b)
+        self.enc2 = conv_block(b, 2 * b)
+        self.enc3 = conv_block(2 * b, 4 * b)
+        self.bottleneck = conv_block(4 * b, 8 * b)
+        self.up3 = nn.ConvTranspose2d(8 * b, 4 * b, 2, 2)
+        self.dec3 = conv_block(8 * b, 4 * b)
+        self.up2 = nn.ConvTranspose2d(4 * b, 2 * b, 2, 2)
+        self.dec2 = conv_block(4 * b, 2 * b)
+        self.up1 = nn.ConvTranspose2d(2 * b, b, 2, 2)
+        self.dec1 = conv_block(2 * b, b)
+        self.out = nn.Conv2d(b, out_channels, kernel_size=1)
+        self.pool = nn.MaxPool2d(2)
+
+    @staticmethod
+    def _up(x, size):
+        return x if tuple(x.shape[2:]) == tuple(size) else F.interpolate(x, size=size, mode="bilinear",
+                                                                          align_corners=False)
+
+    def forward(self, x):
+        e1 = self.enc1(x)
+        e2 = self.enc2(self.pool(e1))
+        e3 = self.enc3(self.pool(e2))
+        bt = self.bottleneck(self.pool(e3))
+        d3 = self.dec3(torch.cat([self._up(self.up3(bt), e3.shape[2:]), e3], dim=1))
+        d2 = self.dec2(torch.cat([self._up(self.up2(d3), e2.shape[2:]), e2], dim=1))
+        d1 = self.dec1(torch.cat([self._up(self.up1(d2), e1.shape[2:]), e1], dim=1))
+        return self.out(d1)
+
+
+def to_channels_last(model: nn.Module) -> nn.Module:
+    return model.to(memory_format=torch.channels_last)

@@ -1,0 +1,75 @@
+"""Model zoo: parameter counts against the reference and CPU forward/backward shapes."""
+import torch
+
+from distributed_pytorch_hpc_amd import models
+
+
+def n_params(m):
+    return sum(p.numel() for p in m.parameters())
+
+
+def test_llama_param_counts():
+    assert models.get_preset("toy").num_params() == 18_089_216
+    assert models.get_preset("llama2-7b").num_params() == 6_738_415_616
+    m = models.build_llama("toy", device="cpu", dtype=torch.float32)
+    assert n_params(m) == 18_089_216
+    assert models.get_preset("llama2-7b").ffn_hidden == 11008
+
+
+def test_unet_vit_pp_param_counts():
+    assert n_params(models.SimpleUNet(65, 65)) == 7_742_849
+    assert n_params(models.SimpleViT(65, 65, 8, 64, 128)) == 6_906_176
+    assert n_params(models.PipelineTransformer()) == 11_700_736
+    assert n_params(models.FourBlockMLP()) == 1_050_624
+
+
+def test_resnet_param_counts():
+    assert n_params(models.resnet50()) == 25_557_032
+    assert n_params(models.resnet18()) == 11_689_512
+    assert n_params(models.resnet18(num_classes=10, cifar_stem=True)) == 11_173_962
+
+
+def test_forward_shapes_cpu():
+    x = torch.randn(1, 65, 37, 72)
+    assert models.SimpleUNet(65, 65, base_dim=8)(x).shape == x.shape   # odd latitude (reference X: 181)
+    v = models.SimpleViT(65, 65, 8, 64, 128, embed_dim=64, depth=2, num_heads=4)
+    assert v(torch.randn(2, 65, 64, 128)).shape == (2, 65, 64, 128)
+    pp = models.PipelineTransformer(vocab_size=100, dim=32, n_heads=4, layers_per_stage=1)
+    t = torch.randint(0, 100, (2, 16))
+    assert pp(t).shape == (2, 16, 100)
+    st = pp.stage_modules(2)
+    assert st[1](st[0](t)).shape == (2, 16, 100)
+    r = models.resnet18(num_classes=10, cifar_stem=True)
+    out = r(torch.randn(2, 3, 32, 32))
+    out.sum().backward()
+    assert out.shape == (2, 10)
+
+
+def test_llama_logits_and_loss_consistent():
+    m = models.build_llama("tiny", device="cpu", dtype=torch.float32)
+    t = torch.randint(0, 512, (2, 17))
+    logits = m(t[:, :-1])
+    loss = m(t[:, :-1], t[:, 1:])
+    ref = torch.nn.functional.cross_entropy(logits.reshape(-1, 512), t[:, 1:].reshape(-1))
+    assert torch.allclose(loss, ref, atol=1e-5)
+
+
+def test_reference_state_dict_conversion():
+    args = models.get_preset("tiny")
+    m = models.build_llama(args, device="cpu", dtype=torch.float32)
+    sd = m.state_dict()
+    ref = {}
+    hd = args.head_dim
+    for k, v in sd.items():
+        if "wqkv" in k:
+            q, kk, vv = v.split([args.n_heads * hd, args.kv_heads * hd, args.kv_heads * hd])
+            ref[k.replace("wqkv", "wq")], ref[k.replace("wqkv", "wk")], ref[k.replace("wqkv", "wv")] = q, kk, vv
+        elif "w13" in k:
+            a, b = v.chunk(2)
+            ref[k.replace("w13", "w1")], ref[k.replace("w13", "w3")] = a, b
+        else:
+            ref[k] = v
+    back = models.convert_reference_state_dict(ref, args)
+    assert back.keys() == sd.keys()
+    for k in sd:
+        assert torch.equal(back[k], sd[k])
