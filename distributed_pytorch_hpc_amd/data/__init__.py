@@ -1,1 +1,5 @@
+from .sampler import DistributedSampler, dp_dataloader
+from .synthetic import DeviceBatches, ERA5Dataset, MyTrainDataset, SimpleDataset, TokenDataset
 
+__all__ = ["DistributedSampler", "dp_dataloader", "DeviceBatches", "ERA5Dataset", "MyTrainDataset", "SimpleDataset",
+           "TokenDataset"]
