@@ -207,8 +207,25 @@ class _AllReduceSum(torch.autograd.Function):
 
 
 def all_reduce_autograd_sum(x, group):
-    """sum over ranks; each rank's input contributes to the (replicated) output, so grad is identity."""
+    """sum over ranks feeding a REPLICATED downstream (every rank computes the same loss): grad is identity."""
     return _AllReduceSum.apply(x, group) if _ws(group) > 1 else x
+
+
+class _AllReducePartial(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, group):
+        ctx.group = group
+        return all_reduce_(x.clone(), group)
+
+    @staticmethod
+    def backward(ctx, g):
+        return all_reduce_(g.contiguous().clone(), ctx.group), None
+
+
+def all_reduce_sum_partitioned(x, group):
+    """sum over ranks feeding PARTITIONED downstream work (each rank's loss covers its own shard, total loss =
+    sum over ranks): the adjoint is again an all-reduce (e.g. batch statistics of a domain-sharded field)."""
+    return _AllReducePartial.apply(x, group) if _ws(group) > 1 else x
 
 
 def all_reduce_autograd_max(x, group):
