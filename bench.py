@@ -34,7 +34,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--model", default="llama2-7b")
     ap.add_argument("--seq-len", type=int, default=4096)
-    ap.add_argument("--micro-batch", type=int, default=4, help="sequences per GPU per step")
+    ap.add_argument("--micro-batch", type=int, default=8,
+                    help="sequences per GPU per step (8 x 4096 tokens: ~249 GB peak on one 288 GB MI355X)")
     ap.add_argument("--parallel", choices=["auto", "fsdp", "ddp"], default="auto",
                     help="auto: single-GPU engine for N=1, FSDP (sharded optimizer) for N>1")
     ap.add_argument("--bucket-mb", type=float, default=256.0)
@@ -103,7 +104,7 @@ def main(argv=None):
     for i in range(args.warmup):
         loss = train_step(i)
     if args.warmup:
-        first_loss = float(loss)
+        first_loss = float(loss.detach())
     sync_all()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -111,7 +112,7 @@ def main(argv=None):
     engine.synchronize()
     sync_all()
     elapsed = time.perf_counter() - t0
-    last_loss = float(loss)
+    last_loss = float(loss.detach())
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -97,13 +97,96 @@ __device__ __forceinline__ bf16x8 zero8() {
   return z;
 }
 
+// Per-lane plan for one 64-key K/V tile: swizzled LDS offsets of the ds_read_b128 row reads and the
+// ds_read_b64_tr_b16 transposed reads, and the LDS-DMA source offsets of the staging loads.  Computed once
+// per kernel so the tile loop issues loads with immediate offsets instead of recomputing the XOR swizzle.
+// Row offsets repeat with period KP sub-tiles (32 rows) and tr offsets with period TRP k-steps (16 rows):
+// img_off's line permutation depends on (line & 15) only, so advancing 16 lines is a pure byte offset.
+template <int HD>
+struct KVTilePlan {
+  static constexpr int BN = 64, NT = 256, NC = HD / 8, KS = HD / 16, DT = HD / 32, TILE = BN * HD * 2;
+  static constexpr int KP = NC >= 8 ? 1 : 2;
+  static constexpr int TRP = NC >= 16 ? 1 : (NC == 8 ? 2 : 4);
+  static constexpr int NS = BN * NC / NT;
+  static_assert(BN * NC % NT == 0, "tile must split evenly over the workgroup");
+  int kro[KP][KS];
+  int tro[TRP][DT][2];
+  int kgo[NS];  // staging source offsets (elements), valid when K and V share the sequence stride
+
+  __device__ __forceinline__ void init(int lane, int64_t k_ss) {
+    const int h = lane >> 5, l32 = lane & 31, g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+#pragma unroll
+    for (int sp = 0; sp < KP; ++sp)
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) kro[sp][kk] = img_off<NC>(sp * 32 + l32, kk * 2 + h);
+#pragma unroll
+    for (int kp = 0; kp < TRP; ++kp)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int hi = 0; hi < 2; ++hi)
+          tro[kp][dt][hi] = img_off<NC>(kp * 16 + 4 * (g >> 1) + tq + 8 * hi, dt * 4 + 2 * (g & 1) + (tp >> 1)) +
+                            8 * (tp & 1);
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const int L = threadIdx.x + NT * i, line = L >> 4, slot = L & 15;
+      const int F = (line << 4) + (slot ^ (((line & 3) << 2) | ((line >> 2) & 3)));
+      kgo[i] = (F / NC) * (int)k_ss + (F % NC) * 8;
+    }
+  }
+  __device__ __forceinline__ int row(int sub, int kk) const {
+    return KP == 1 ? kro[0][kk] + sub * 32 * NC * 16 : kro[sub][kk];
+  }
+  __device__ __forceinline__ int tr(int ks, int dt, int hi) const {
+    return tro[ks % TRP][dt][hi] + (ks / TRP) * TRP * 16 * NC * 16;
+  }
+  // K and V tile [k0, k0 + 64) -> image pair at img (K) / img + TILE (V).  Full tiles use the hoisted
+  // offsets; the ragged last tile clamps rows to Sk - 1 (finite data the caller masks).
+  __device__ __forceinline__ void stage(char* img, const bf16* kp, const bf16* vp, int64_t k_ss, int64_t v_ss,
+                                        int k0, int Sk) const {
+    if (k0 + BN <= Sk && k_ss == v_ss) {
+      const bf16* kt = kp + (int64_t)k0 * k_ss;
+      const bf16* vt = vp + (int64_t)k0 * v_ss;
+      const int wave = threadIdx.x >> 6;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        auto* dst = (__attribute__((address_space(3))) void*)(img + (wave * 64 + NT * i) * 16);
+        __builtin_amdgcn_global_load_lds((const void*)(kt + kgo[i]), dst, 16, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        auto* dst = (__attribute__((address_space(3))) void*)(img + TILE + (wave * 64 + NT * i) * 16);
+        __builtin_amdgcn_global_load_lds((const void*)(vt + kgo[i]), dst, 16, 0, 0);
+      }
+    } else {
+      glds_stage<NC, BN, NT>(img, kp, k_ss, k0, Sk);
+      glds_stage<NC, BN, NT>(img + TILE, vp, v_ss, k0, Sk);
+    }
+  }
+};
+
+// Number of 64-key tiles a 32-query wave (first query q0w) must visit: causal waves stop at their last
+// visible key; the workgroup still loops to its own end for the shared staging / barriers.
+template <bool CAUSAL>
+__device__ __forceinline__ int wave_tile_count(int ntiles, int q0w, int off) {
+  if (!CAUSAL) return ntiles;
+  const int last = q0w + 31 + off;
+  return last < 0 ? 0 : min(ntiles, last / 64 + 1);
+}
+
 // ==================================================================================================
 // Forward
 // ==================================================================================================
+// Online softmax in log2 units with the 1/sqrt(d) scale folded into one FMA per score:
+//   p = exp2(s * scale*log2e - m).  The running max m is only raised (and O, l rescaled) when some lane's
+// tile max exceeds it by more than RESCALE_THR (FA4-style lazy rescaling): p is then bounded by 2^THR,
+// harmless for the bf16 P operand and the fp32 accumulators, and the exact result is recovered by the
+// final 1/l.  The rescale branch is wave-uniform (ballot), so steady-state tiles skip 16*DT multiplies.
 template <int HD, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
-  constexpr int BM = 128, BN = 64, NC = HD / 8, KS = HD / 16, DT = HD / 32;
-  constexpr int TILE = BN * HD * 2;          // bytes of one K (or V) tile image
+  using Plan = KVTilePlan<HD>;
+  constexpr int BM = 128, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
+  constexpr float RESCALE_THR = 8.f;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
@@ -111,8 +194,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
   const int qb = CAUSAL ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // heaviest causal blocks first
   const int hq = blockIdx.y, b = blockIdx.z;
   const int hk = hq / (p.Hq / p.Hkv);
-  const int q0 = qb * BM;
-  const int myq = q0 + wid * 32 + l32;
+  const int q0 = qb * BM, q0w = q0 + wid * 32;
+  const int myq = q0w + l32;
   const int off = p.Sk - p.Sq;
 
   const bf16* qp = (const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
@@ -128,81 +211,67 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
   int kv_end = p.Sk;
   if (CAUSAL) kv_end = min(p.Sk, q0 + BM + off);
   const int ntiles = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
+  const int wtiles = wave_tile_count<CAUSAL>(ntiles, q0w, off);
+
+  Plan plan;
+  plan.init(lane, p.k_ss);
 
   f32x16 o[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-  float m = -INFINITY, lsum = 0.f;
+  const f32x16 zacc = {};
+  float m = -INFINITY, lsum = 0.f;  // m: running max of s*sl2; lsum: this half-wave's partial row sum
   const float sl2 = p.scale * 1.4426950408889634f;
 
-  auto stage = [&](int t, int buf) {
-    char* Kl = smem + buf * 2 * TILE;
-    glds_stage<NC, BN, 256>(Kl, kp, p.k_ss, t * BN, p.Sk);
-    glds_stage<NC, BN, 256>(Kl + TILE, vp, p.v_ss, t * BN, p.Sk);
-  };
-
-  if (ntiles > 0) stage(0, 0);
+  if (ntiles > 0) plan.stage(smem, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
   __syncthreads();
 
-  // per-lane constant parts of the tr-read addresses (A = V^T operand)
-  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
-
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
-    const char* Kl = smem + buf * 2 * TILE;
-    const char* Vl = Kl + TILE;
-
+  auto tile = [&](const char* Kl, const char* Vl, int k0, bool need_mask) {
     // ---- S^T = K Q^T for two 32-key sub-tiles ----
     f32x16 s[2];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
+      s[sub] = mfma32(lds_b128(Kl, plan.row(sub, 0)), qf[0], zacc);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[sub][r] = 0.f;
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const bf16x8 a = lds_b128(Kl, img_off<NC>(sub * 32 + l32, kk * 2 + h));
-        s[sub] = mfma32(a, qf[kk], s[sub]);
-      }
+      for (int kk = 1; kk < KS; ++kk) s[sub] = mfma32(lds_b128(Kl, plan.row(sub, kk)), qf[kk], s[sub]);
     }
-    // ---- scale, mask, online softmax (lane-local per query) ----
-    const int k0 = t * BN;
-    const bool need_mask = (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0 + wid * 32 + off));
-    float mx = -INFINITY;
+    // phase fences keep the scheduler from hoisting the next phase's LDS reads into this one's live range
+    __builtin_amdgcn_sched_barrier(0);
+    if (need_mask) {  // wave-uniform: only diagonal / ragged tiles pay for the selects
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
+      for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float v = s[sub][r] * sl2;
-        if (need_mask) {
+        for (int r = 0; r < 16; ++r) {
           const int key = k0 + sub * 32 + acc_row(r, h);
-          if (key >= p.Sk || (CAUSAL && key > myq + off)) v = -INFINITY;
+          s[sub][r] = (key >= p.Sk || (CAUSAL && key > myq + off)) ? -INFINITY : s[sub][r];
         }
-        s[sub][r] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = half_max(mx);
-    const float m_new = fmaxf(m, mx);
-    const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-    const float alpha = exp2_(m - m_use);
-    float ls = 0.f;
+    }
+    float mx = fmaxf(s[0][0], s[1][0]);
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s[0][r], s[1][r]));
+    mx = half_max(mx) * sl2;
+    if (__ballot(mx > m + RESCALE_THR)) {
+      const float mn = fmaxf(m, mx);
+      const float alpha = mn == -INFINITY ? 1.f : exp2_(m - mn);
+      lsum *= alpha;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float e = exp2_(s[sub][r] - m_use);
-        s[sub][r] = e;
-        ls += e;
-      }
-    ls = half_sum(ls);
-    lsum = lsum * alpha + ls;
-    m = m_new;
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+      m = mn;
+    }
+    const float mneg = m == -INFINITY ? 0.f : -m;
+    float ls0 = 0.f, ls1 = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+    for (int r = 0; r < 16; ++r) {
+      s[0][r] = exp2_(fmaf(s[0][r], sl2, mneg));
+      s[1][r] = exp2_(fmaf(s[1][r], sl2, mneg));
+      ls0 += s[0][r];
+      ls1 += s[1][r];
+    }
+    lsum += ls0 + ls1;
 
     // ---- P^T as B operand: k-step ks covers keys 16*ks .. 16*ks+15 of the tile ----
     bf16x8 pf[4];
@@ -210,23 +279,29 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
       for (int j = 0; j < 8; ++j) pf[ks][j] = (bf16)s[ks >> 1][8 * (ks & 1) + j];
+    __builtin_amdgcn_sched_barrier(0);
 
     // ---- O^T += V^T P^T ----
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int krow = ks * 16 + 4 * (g >> 1) + tq;
+    for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const int ch = dt * 4 + 2 * (g & 1) + (tp >> 1);
-        const int bo = 8 * (tp & 1);
-        const bf16x8 a = lds_tr2(Vl, img_off<NC>(krow, ch) + bo, img_off<NC>(krow + 8, ch) + bo);
-        o[dt] = mfma32(a, pf[ks], o[dt]);
-      }
+      for (int dt = 0; dt < DT; ++dt)
+        o[dt] = mfma32(lds_tr2(Vl, plan.tr(ks, dt, 0), plan.tr(ks, dt, 1)), pf[ks], o[dt]);
+  };
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) plan.stage(smem + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
+    const char* Kl = smem + buf * 2 * TILE;
+    if (t < wtiles) {
+      const int k0 = t * BN;
+      tile(Kl, Kl + TILE, k0, (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0w + off)));
     }
     __syncthreads();
   }
 
   // ---- epilogue: O = O^T / l, lse ----
+  lsum = half_sum(lsum);
   if (myq < p.Sq) {
     const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     bf16* op = (bf16*)p.o + (int64_t)b * p.o_sb + (int64_t)myq * p.o_ss + (int64_t)hq * p.o_sh;
@@ -430,19 +505,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
 // are one scalar per lane), then dQ^T += K^T dS^T with dS^T consumed straight from the accumulator.
 template <int HD, bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
-  constexpr int BM = 128, BN = 64, NC = HD / 8, KS = HD / 16, DT = HD / 32;
-  constexpr int TILE = BN * HD * 2;
+  using Plan = KVTilePlan<HD>;
+  constexpr int BM = 128, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const AttnParams& p = P.f;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
-  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const int nqb = (p.Sq + BM - 1) / BM;
   const int qb = CAUSAL ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
   const int hq = blockIdx.y, b = blockIdx.z;
   const int hk = hq / (p.Hq / p.Hkv);
-  const int q0 = qb * BM;
-  const int myq = q0 + wid * 32 + l32;
+  const int q0 = qb * BM, q0w = q0 + wid * 32;
+  const int myq = q0w + l32;
   const int off = p.Sk - p.Sq;
   const float sl2 = p.scale * 1.4426950408889634f;
 
@@ -458,76 +532,72 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
     qf[kk] = ok ? *reinterpret_cast<const bf16x8*>(qp + (int64_t)myq * p.q_ss + kk * 16 + 8 * h) : zero8();
     df[kk] = ok ? *reinterpret_cast<const bf16x8*>(dop + (int64_t)myq * P.do_ss + kk * 16 + 8 * h) : zero8();
   }
-  float lse2 = 0.f, delta = 0.f;
+  float nlse2 = 0.f, delta = 0.f;  // -lse in log2 units
   if (myq < p.Sq) {
     const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + myq;
-    lse2 = p.lse[idx] * 1.4426950408889634f;
+    nlse2 = -p.lse[idx] * 1.4426950408889634f;
     delta = P.delta[idx];
   }
 
   int kv_end = p.Sk;
   if (CAUSAL) kv_end = min(p.Sk, q0 + BM + off);
   const int ntiles = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
+  const int wtiles = wave_tile_count<CAUSAL>(ntiles, q0w, off);
+
+  Plan plan;
+  plan.init(lane, p.k_ss);
 
   f32x16 dq[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
+  const f32x16 zacc = {};
 
-  auto stage = [&](int t, int buf) {
-    char* Kl = smem + buf * 2 * TILE;
-    glds_stage<NC, BN, 256>(Kl, kp, p.k_ss, t * BN, p.Sk);
-    glds_stage<NC, BN, 256>(Kl + TILE, vp, p.v_ss, t * BN, p.Sk);
-  };
-  if (ntiles > 0) stage(0, 0);
+  if (ntiles > 0) plan.stage(smem, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
   __syncthreads();
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
-    const char* Kl = smem + buf * 2 * TILE;
-    const char* Vl = Kl + TILE;
-    const int k0 = t * BN;
-    const bool need_mask = (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0 + wid * 32 + off));
+  auto tile = [&](const char* Kl, const char* Vl, int k0, bool need_mask) {
     bf16x8 sf[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      f32x16 s, dp;
+      f32x16 s = mfma32(lds_b128(Kl, plan.row(sub, 0)), qf[0], zacc);
+      f32x16 dp = mfma32(lds_b128(Vl, plan.row(sub, 0)), df[0], zacc);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const bf16x8 ka = lds_b128(Kl, img_off<NC>(sub * 32 + l32, kk * 2 + h));
-        const bf16x8 va = lds_b128(Vl, img_off<NC>(sub * 32 + l32, kk * 2 + h));
-        s = mfma32(ka, qf[kk], s);
-        dp = mfma32(va, df[kk], dp);
+      for (int kk = 1; kk < KS; ++kk) {
+        s = mfma32(lds_b128(Kl, plan.row(sub, kk)), qf[kk], s);
+        dp = mfma32(lds_b128(Vl, plan.row(sub, kk)), df[kk], dp);
       }
+      if (need_mask) {  // wave-uniform; masked scores -> -inf -> p = 0
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float pv = exp2_(s[r] * sl2 - lse2);
-        if (need_mask) {
+        for (int r = 0; r < 16; ++r) {
           const int key = k0 + sub * 32 + acc_row(r, h);
-          if (key >= p.Sk || (CAUSAL && key > myq + off)) pv = 0.f;
+          s[r] = (key >= p.Sk || (CAUSAL && key > myq + off)) ? -INFINITY : s[r];
         }
-        s[r] = pv * (dp[r] - delta);
       }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = exp2_(fmaf(s[r], sl2, nlse2)) * (dp[r] - delta);
 #pragma unroll
       for (int half = 0; half < 2; ++half)
 #pragma unroll
         for (int j = 0; j < 8; ++j) sf[sub * 2 + half][j] = (bf16)s[8 * half + j];
+      __builtin_amdgcn_sched_barrier(0);
     }
     // dQ^T += K^T dS^T
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int krow = ks * 16 + 4 * (g >> 1) + tq;
+    for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const int ch = dt * 4 + 2 * (g & 1) + (tp >> 1);
-        const int bo = 8 * (tp & 1);
-        const bf16x8 a = lds_tr2(Kl, img_off<NC>(krow, ch) + bo, img_off<NC>(krow + 8, ch) + bo);
-        dq[dt] = mfma32(a, sf[ks], dq[dt]);
-      }
+      for (int dt = 0; dt < DT; ++dt)
+        dq[dt] = mfma32(lds_tr2(Kl, plan.tr(ks, dt, 0), plan.tr(ks, dt, 1)), sf[ks], dq[dt]);
+  };
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) plan.stage(smem + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
+    const char* Kl = smem + buf * 2 * TILE;
+    if (t < wtiles) {
+      const int k0 = t * BN;
+      tile(Kl, Kl + TILE, k0, (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0w + off)));
     }
     __syncthreads();
   }

@@ -24,6 +24,9 @@ BUILD_DIR = os.path.join(PKG, "..", "build", "native")
 OUT = os.path.join(PKG, "_C.so")
 ARCH = os.environ.get("DPH_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+# attention: no NaN canonicalisation around fmaxf of MFMA outputs (halves the row-max VALU work);
+# infinities stay honoured (masked scores are -inf)
+PER_FILE_HIP_FLAGS = {"attention.hip": ["-fno-honor-nans"]}
 
 
 def _torch_paths():
@@ -86,6 +89,8 @@ def write_ninja(build_dir: str, verbose_asm: bool = False) -> str:
     for f in hip:
         o = os.path.join(build_dir, f + ".o")
         lines.append(f"build {o}: hipcc {os.path.join(HERE, f)}")
+        if f in PER_FILE_HIP_FLAGS:
+            lines.append("  hipflags = $hipflags " + " ".join(PER_FILE_HIP_FLAGS[f]))
         objs.append(o)
     for f in cpp:
         o = os.path.join(build_dir, f + ".o")

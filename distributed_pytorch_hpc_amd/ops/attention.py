@@ -120,6 +120,9 @@ class _RopeFlashAttnFn(torch.autograd.Function):
         v = qkv[:, :, (n_heads + n_kv_heads) * head_dim:].view(b, s, n_kv_heads, head_dim)
         o, lse = flash_fwd(q, k, v, scale, causal)
         ctx.mark_dirty(qkv)
+        # the second output (the in-place-rotated qkv) is normally unused: do not materialise a zero gradient
+        # for it (a [B, S, (Hq+2Hkv)*hd] fill + add per layer otherwise)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(qkv, o, lse, cos, sin)
         ctx.cfg = (n_heads, n_kv_heads, head_dim, causal, scale, pos_offset)
         return o.view(b, s, n_heads * head_dim), qkv
