@@ -44,6 +44,8 @@ def parse(argv=None):
     ap.add_argument("--kernels", choices=["dph", "aten"], default="dph",
                     help="dph: CDNA4 HIP kernels (default); aten: stock PyTorch-ROCm ops (comparator)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--force-dist", action="store_true",
+                    help="create the RCCL process group even for one rank (exercises the N>1 collective path)")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args(argv)
 
@@ -53,7 +55,7 @@ def main(argv=None):
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     from distributed_pytorch_hpc_amd.runtime import env as rt
 
-    if world_env > 1:
+    if world_env > 1 or args.force_dist:
         rank, world, local = rt.init_distributed(verbose=not args.quiet)
     else:
         rank, world, local = 0, 1, 0
@@ -74,7 +76,7 @@ def main(argv=None):
     model = build_llama(margs, device=dev, dtype=torch.bfloat16, seed=1234)
     mode = args.parallel
     if mode == "auto":
-        mode = "fsdp" if world > 1 else "ddp"
+        mode = "fsdp" if world > 1 or args.force_dist else "ddp"
     engine = DataParallelEngine(
         model, shard=(mode == "fsdp"),
         mixed_precision=MixedPrecision(param_dtype=torch.bfloat16,
@@ -97,7 +99,7 @@ def main(argv=None):
 
     def sync_all():
         torch.cuda.synchronize()
-        if world > 1:
+        if dist.is_initialized():
             rt.barrier()
         torch.cuda.synchronize()
 
@@ -113,7 +115,7 @@ def main(argv=None):
     sync_all()
     elapsed = time.perf_counter() - t0
     last_loss = float(loss.detach())
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -159,7 +161,7 @@ def main(argv=None):
         if args.json_out:
             with open(args.json_out, "w") as fh:
                 fh.write(line + "\n")
-    if world > 1:
+    if dist.is_initialized():
         rt.cleanup_distributed()
 
 

@@ -1,0 +1,123 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 kernel trace: per-kernel and per-category GPU time.
+
+Reads either rocprofv3's SQLite output (``<dir>/<name>_results.db``, the default format) or its CSV
+kernel trace (``--output-format csv`` -> ``*_kernel_trace.csv``).  Optionally restricts to the last
+``--last-ms`` of GPU activity (the timed steps of a bench run) and divides by ``--steps``.
+
+    python benchmarks/prof_summary.py gpurun_out/prof3 --steps 2 --json profiles/x.json
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+import sqlite3
+from collections import defaultdict
+
+CATEGORIES = [
+    ("gemm", re.compile(r"Cijk_|gemm|Gemm|hipblaslt|_MT\d+x\d+", re.I)),
+    ("attn_fwd", re.compile(r"attn_fwd_k")),
+    ("attn_bwd_dkdv", re.compile(r"attn_bwd_dkdv_k")),
+    ("attn_bwd_dq", re.compile(r"attn_bwd_dq_k")),
+    ("attn_delta", re.compile(r"attn_delta_k")),
+    ("rmsnorm", re.compile(r"rmsnorm|col_reduce")),
+    ("swiglu", re.compile(r"swiglu")),
+    ("rope", re.compile(r"rope")),
+    ("xent", re.compile(r"xent|cross_entropy")),
+    ("embedding", re.compile(r"embed")),
+    ("optimizer", re.compile(r"adamw|sgd_k|sumsq")),
+    ("rccl", re.compile(r"ncclDevKernel|rccl|nccl", re.I)),
+    ("copy/fill", re.compile(r"copy|fill|FillFunctor|direct_copy", re.I)),
+    ("elementwise(aten)", re.compile(r"elementwise|vectorized|reduce_kernel", re.I)),
+]
+
+
+def short_name(name: str) -> str:
+    n = name.split("(")[0]
+    if n.startswith("void "):
+        n = n[5:]
+    return n[:120]
+
+
+def category(name: str) -> str:
+    for cat, rx in CATEGORIES:
+        if rx.search(name):
+            return cat
+    return "other"
+
+
+def load_events(path: str):
+    """-> list of (name, start_ns, end_ns)."""
+    dbs = glob.glob(os.path.join(path, "**", "*_results.db"), recursive=True) if os.path.isdir(path) else [path]
+    dbs = [d for d in dbs if d.endswith(".db")]
+    if dbs:
+        ev = []
+        for db in dbs:
+            con = sqlite3.connect(db)
+            ev += list(con.execute("select name, start, end from kernels"))
+            con.close()
+        return ev
+    csvs = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)
+    ev = []
+    for f in csvs:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                ev.append((row["Kernel_Name"], int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+    return ev
+
+
+def summarise(events, last_ms: float | None = None, steps: int = 1):
+    if not events:
+        raise SystemExit("no kernel events found")
+    events.sort(key=lambda e: e[1])
+    if last_ms:
+        t_end = max(e[2] for e in events)
+        events = [e for e in events if e[1] >= t_end - last_ms * 1e6]
+    span = (max(e[2] for e in events) - min(e[1] for e in events)) / 1e6
+    per_k = defaultdict(lambda: [0, 0.0])
+    per_c = defaultdict(float)
+    for name, s, e in events:
+        d = (e - s) / 1e6
+        k = short_name(name)
+        per_k[k][0] += 1
+        per_k[k][1] += d
+        per_c[category(name)] += d
+    busy = sum(per_c.values())
+    return {
+        "steps": steps,
+        "span_ms_per_step": round(span / steps, 3),
+        "kernel_busy_ms_per_step": round(busy / steps, 3),
+        "categories_ms_per_step": {c: round(v / steps, 3) for c, v in sorted(per_c.items(), key=lambda x: -x[1])},
+        "top_kernels": [
+            {"name": k, "calls_per_step": round(c / steps, 2), "ms_per_step": round(t / steps, 3),
+             "pct": round(100 * t / busy, 2)}
+            for k, (c, t) in sorted(per_k.items(), key=lambda x: -x[1][1])[:40]
+        ],
+    }
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("path", help="rocprofv3 output directory, .db file, or CSV directory")
+    ap.add_argument("--steps", type=int, default=1, help="divide totals by this many steps")
+    ap.add_argument("--last-ms", type=float, default=None, help="only the last N ms of GPU activity")
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args(argv)
+    out = summarise(load_events(args.path), args.last_ms, args.steps)
+    print(f"span/step {out['span_ms_per_step']} ms, kernel busy/step {out['kernel_busy_ms_per_step']} ms")
+    for c, v in out["categories_ms_per_step"].items():
+        print(f"  {c:22s} {v:10.3f} ms")
+    print("top kernels:")
+    for k in out["top_kernels"][:25]:
+        print(f"  {k['ms_per_step']:9.3f} ms {k['pct']:6.2f}% x{k['calls_per_step']:<7} {k['name'][:90]}")
+    if args.json:
+        with open(args.json, "w") as fh:
+            json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

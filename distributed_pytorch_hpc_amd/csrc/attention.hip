@@ -323,29 +323,29 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
 // ==================================================================================================
 // Backward
 // ==================================================================================================
-// delta[b, h, q] = sum_d dO[b,q,h,d] * O[b,q,h,d]   (one wave per row, fp32)
+// delta[b, h, q] = sum_d dO[b,q,h,d] * O[b,q,h,d] (fp32).  TPR = D/8 lanes per row, 8 elements per lane;
+// rows are enumerated (b, q, h) so a wave reads 64 * 16 contiguous bytes of each [B, S, H, D] operand.
+template <int TPR>
 __global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ o, const bf16* __restrict__ dout,
-                                                    float* __restrict__ delta, int B, int S, int H, int D,
+                                                    float* __restrict__ delta, int B, int S, int H,
                                                     int64_t o_sb, int64_t o_ss, int64_t o_sh, int64_t d_sb,
                                                     int64_t d_ss, int64_t d_sh) {
-  const int lane = threadIdx.x & 63;
+  constexpr int RPB = 256 / TPR;  // rows per block-iteration
+  const int sub = threadIdx.x % TPR;
   const int64_t rows = (int64_t)B * H * S;
-  for (int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += (int64_t)gridDim.x * 4) {
-    const int q = (int)(r % S);
-    const int64_t bh = r / S;
-    const int hh = (int)(bh % H), bb = (int)(bh / H);
-    const bf16* a = o + bb * o_sb + (int64_t)q * o_ss + hh * o_sh;
-    const bf16* c = dout + bb * d_sb + (int64_t)q * d_ss + hh * d_sh;
-    float s = 0.f;
-    for (int d = lane * 8; d < D; d += 512) {
-      float x[8], y[8];
-      Vec8<bf16>::load(a + d, x);
-      Vec8<bf16>::load(c + d, y);
+  for (int64_t r = (int64_t)blockIdx.x * RPB + threadIdx.x / TPR; r < rows; r += (int64_t)gridDim.x * RPB) {
+    const int hh = (int)(r % H);
+    const int64_t bq = r / H;
+    const int q = (int)(bq % S), bb = (int)(bq / S);
+    float x[8], y[8];
+    Vec8<bf16>::load(o + bb * o_sb + (int64_t)q * o_ss + hh * o_sh + sub * 8, x);
+    Vec8<bf16>::load(dout + bb * d_sb + (int64_t)q * d_ss + hh * d_sh + sub * 8, y);
+    float acc = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s += x[k] * y[k];
-    }
-    s = wave_sum(s);
-    if (lane == 0) delta[r] = s;
+    for (int k = 0; k < 8; ++k) acc += x[k] * y[k];
+#pragma unroll
+    for (int m = TPR / 2; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
+    if (sub == 0) delta[((int64_t)bb * H + hh) * S + q] = acc;
   }
 }
 
@@ -359,7 +359,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
   constexpr int NT = 256, BNK = 128, BMQ = 32, NC = HD / 8, KS = HD / 16, DT = HD / 32;
   constexpr int QIMG = BMQ * HD * 2;        // Q / dO tile image [32 q][HD]
   constexpr int KIMG = BNK * HD * 2;        // K image [128 keys][HD] (B operand of S = Q K^T)
-  // smem: K | Q0 | dO0 | Q1 | dO1 | lse[2][32] | delta[2][32]
+  // img_off's line permutation repeats every 16 lines.  For NC >= 8, rows r and r + 32 are a multiple of 16
+  // lines apart, so the wave's K rows reuse the Q-image offsets plus a constant.
+  constexpr bool KSHARE = NC >= 8;
+  constexpr bool TRADD = NC >= 16;          // +16 rows is a pure byte offset for the transposed reads
+  // smem: K | Q0 | dO0 | Q1 | dO1 | -lse2[2][32] | delta[2][32]
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Kimg = smem;
   char* Qbuf = smem + KIMG;
@@ -390,6 +394,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+  const f32x16 zacc = {};
+
+  // hoisted per-lane LDS offsets
+  int qro[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) qro[kk] = img_off<NC>(l32, kk * 2 + h);
+  auto kofs = [&](int kk) {
+    return KSHARE ? qro[kk] + wid * 32 * NC * 16 : img_off<NC>(wid * 32 + l32, kk * 2 + h);
+  };
+  int tro[TRADD ? 1 : 2][DT][2];
+#pragma unroll
+  for (int ks = 0; ks < (TRADD ? 1 : 2); ++ks)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi)
+        tro[ks][dt][hi] = img_off<NC>(ks * 16 + 4 * (g >> 1) + tq + 8 * hi, dt * 4 + 2 * (g & 1) + (tp >> 1)) +
+                          8 * (tp & 1);
+  auto trofs = [&](int ks, int dt, int hi) {
+    return TRADD ? tro[0][dt][hi] + ks * 16 * NC * 16 : tro[ks][dt][hi];
+  };
 
   int qstart = 0;
   if (CAUSAL) qstart = max(0, kb0 - off) / BMQ * BMQ;
@@ -408,7 +433,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
     if (threadIdx.x < BMQ) {
       const int q = qt0 + threadIdx.x;
       const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + q;
-      st_lse = q < p.Sq ? p.lse[idx] * 1.4426950408889634f : 0.f;  // log2 units
+      st_lse = q < p.Sq ? -p.lse[idx] * 1.4426950408889634f : 0.f;  // -lse in log2 units
       st_del = q < p.Sq ? P.delta[idx] : 0.f;
     }
   };
@@ -433,26 +458,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
     const char* Ol = Ql + QIMG;
     // a wave whose 32 keys are all hidden from this query tile by the causal mask skips the tile
     if (!(CAUSAL && key0 > qt0 + BMQ - 1 + off)) {
-      f32x16 s, dp;
+      f32x16 s = mfma32(lds_b128(Ql, qro[0]), lds_b128(Kimg, kofs(0)), zacc);
+      f32x16 dp = mfma32(lds_b128(Ol, qro[0]), vf[0], zacc);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        const bf16x8 qa = lds_b128(Ql, img_off<NC>(l32, kk * 2 + h));
-        const bf16x8 oa = lds_b128(Ol, img_off<NC>(l32, kk * 2 + h));
-        const bf16x8 kf = lds_b128(Kimg, img_off<NC>(wid * 32 + l32, kk * 2 + h));
-        s = mfma32(qa, kf, s);
-        dp = mfma32(oa, vf[kk], dp);
+      for (int kk = 1; kk < KS; ++kk) {
+        s = mfma32(lds_b128(Ql, qro[kk]), lds_b128(Kimg, kofs(kk)), s);
+        dp = mfma32(lds_b128(Ol, qro[kk]), vf[kk], dp);
       }
-      const bool need_mask = CAUSAL && (key0 + 31 > qt0 + off);
+      // wave-uniform: only diagonal / ragged tiles pay for the selects (masked scores -> -inf -> P = 0)
+      if ((qt0 + BMQ > p.Sq) || (key0 + 32 > p.Sk) || (CAUSAL && key0 + 31 > qt0 + off)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = qt0 + acc_row(r, h);
+          s[r] = (q >= p.Sq || mykey >= p.Sk || (CAUSAL && mykey > q + off)) ? -INFINITY : s[r];
+        }
+      }
+      const float* ls = lse_s + buf * BMQ;
+      const float* ds = del_s + buf * BMQ;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qr = acc_row(r, h);
-        float pv = exp2_(s[r] * sl2 - lse_s[buf * BMQ + qr]);
-        if (qt0 + qr >= p.Sq || mykey >= p.Sk) pv = 0.f;
-        if (need_mask && mykey > qt0 + qr + off) pv = 0.f;
+        const float pv = exp2_(fmaf(s[r], sl2, ls[qr]));
         s[r] = pv;
-        dp[r] = pv * (dp[r] - del_s[buf * BMQ + qr]);
+        dp[r] = pv * (dp[r] - ds[qr]);
       }
       bf16x8 pb[2], sb[2];
 #pragma unroll
@@ -462,19 +490,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
           pb[ks][j] = (bf16)s[8 * ks + j];
           sb[ks][j] = (bf16)dp[8 * ks + j];
         }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int qrow = ks * 16 + 4 * (g >> 1) + tq;
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-          const int ch = dt * 4 + 2 * (g & 1) + (tp >> 1);
-          const int bo = 8 * (tp & 1);
-          const bf16x8 oa = lds_tr2(Ol, img_off<NC>(qrow, ch) + bo, img_off<NC>(qrow + 8, ch) + bo);
-          dv[dt] = mfma32(oa, pb[ks], dv[dt]);
-          const bf16x8 qa = lds_tr2(Ql, img_off<NC>(qrow, ch) + bo, img_off<NC>(qrow + 8, ch) + bo);
-          dk[dt] = mfma32(qa, sb[ks], dk[dt]);
+          const int o0 = trofs(ks, dt, 0), o1 = trofs(ks, dt, 1);
+          dv[dt] = mfma32(lds_tr2(Ol, o0, o1), pb[ks], dv[dt]);
+          dk[dt] = mfma32(lds_tr2(Ql, o0, o1), sb[ks], dk[dt]);
         }
-      }
     }
     if (it + 1 < total) stage_scalars(buf ^ 1);
     __syncthreads();
@@ -652,9 +676,17 @@ void flash_attn_bwd(const AttnBwdParams& P, hipStream_t st) {
   const AttnParams& p = P.f;
   if (p.B == 0 || p.Sq == 0) return;
   const int64_t rows = (int64_t)p.B * p.Hq * p.Sq;
-  hipLaunchKernelGGL(attn_delta_k, dim3(stream_grid(rows, 4)), dim3(256), 0, st, (const bf16*)p.o,
-                     (const bf16*)P.dout, P.delta, p.B, p.Sq, p.Hq, p.D, p.o_sb, p.o_ss, p.o_sh, P.do_sb, P.do_ss,
-                     P.do_sh);
+  auto delta = [&](auto kern, int tpr) {
+    hipLaunchKernelGGL(kern, dim3(stream_grid(rows, 256 / tpr)), dim3(256), 0, st, (const bf16*)p.o,
+                       (const bf16*)P.dout, P.delta, p.B, p.Sq, p.Hq, p.o_sb, p.o_ss, p.o_sh, P.do_sb, P.do_ss,
+                       P.do_sh);
+  };
+  switch (p.D) {
+    case 32: delta(attn_delta_k<4>, 4); break;
+    case 64: delta(attn_delta_k<8>, 8); break;
+    case 128: delta(attn_delta_k<16>, 16); break;
+    default: return;
+  }
   switch (p.D) {
     case 32: bwd_launch<32>(P, st); break;
     case 64: bwd_launch<64>(P, st); break;
