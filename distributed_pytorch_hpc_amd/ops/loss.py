@@ -58,9 +58,15 @@ def latitude_weights(n_lat: int, device=None, dtype=torch.float32) -> torch.Tens
     return w.to(device=device, dtype=dtype)
 
 
-def latitude_weighted_mse(pred: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
-    """mean over [B, C, H, W] of w[H] * (pred - target)^2."""
-    w = latitude_weights(pred.shape[-2], pred.device, torch.float32).view(1, 1, -1, 1)
+def latitude_weighted_mse(pred: torch.Tensor, target: torch.Tensor, n_lat_global: int | None = None,
+                          lat_offset: int = 0) -> torch.Tensor:
+    """mean over [B, C, H, W] of w[H] * (pred - target)^2.
+
+    For a latitude-sharded field (domain parallelism) pass the global latitude count and this shard's first
+    row: the weights are the matching slice of the global cos-latitude profile, so the average of the
+    per-shard losses over equal shards is the global loss."""
+    n = n_lat_global or pred.shape[-2]
+    w = latitude_weights(n, pred.device, torch.float32)[lat_offset:lat_offset + pred.shape[-2]].view(1, 1, -1, 1)
     return (w * (pred.float() - target.float()).pow(2)).mean()
 
 

@@ -428,13 +428,34 @@ class DistributedDataParallel(nn.Module):
     """
 
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: float = 256.0,
-                 mixed_precision: Optional[MixedPrecision] = None, overlap: bool = True, **_ignored):
+                 mixed_precision: Optional[MixedPrecision] = None, overlap: bool = True,
+                 broadcast_buffers: bool = True, **_ignored):
         super().__init__()
         self.module = module
         self.engine = DataParallelEngine(module, process_group, shard=False, mixed_precision=mixed_precision,
                                          bucket_cap_mb=bucket_cap_mb, overlap=overlap)
+        self.process_group = process_group
+        # torch DDP default: module buffers (BatchNorm running stats) follow rank 0 at every training forward
+        self.broadcast_buffers = broadcast_buffers and self.engine.world > 1 and any(True for _ in module.buffers())
+
+    @torch.no_grad()
+    def _sync_buffers(self):
+        """One coalesced broadcast per buffer dtype from rank 0 of the group."""
+        src = dist.get_global_rank(self.process_group, 0) if self.process_group is not None else 0
+        by_dtype: dict = {}
+        for b in self.module.buffers():
+            by_dtype.setdefault(b.dtype, []).append(b)
+        for bufs in by_dtype.values():
+            flat = torch.cat([b.reshape(-1) for b in bufs])
+            dist.broadcast(flat, src=src, group=self.process_group)
+            o = 0
+            for b in bufs:
+                b.copy_(flat[o:o + b.numel()].view_as(b))
+                o += b.numel()
 
     def forward(self, *args, **kwargs):
+        if self.broadcast_buffers and self.module.training:
+            self._sync_buffers()
         return self.module(*args, **kwargs)
 
     def make_optimizer(self, name: str = "adamw", **kw) -> _EngineOptimizer:

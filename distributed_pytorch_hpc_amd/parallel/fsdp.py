@@ -119,6 +119,10 @@ class ZeRO3Engine:
         if mp.param_dtype is not None:
             for p in module.parameters():
                 p.data = p.data.to(mp.param_dtype)
+        if mp.buffer_dtype is not None:
+            for b in module.buffers():
+                if b.is_floating_point():
+                    b.data = b.data.to(mp.buffer_dtype)
         convert_linears_(module)
         units_m = _select_units(module, auto_wrap_policy)
         owned, self.units = set(), []

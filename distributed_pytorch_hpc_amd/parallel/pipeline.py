@@ -152,6 +152,21 @@ class PipelineSchedule:
             return self._gpipe(mbs, tgts)
         return self._1f1b(mbs, tgts)
 
+    @torch.no_grad()
+    def forward(self, inputs: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+        """Forward-only pipelined pass (evaluation / inference); the last stage returns the concatenated
+        outputs of all micro-batches, other stages None."""
+        mbs = list(inputs.chunk(self.m, 0)) if self.is_first else [None] * self.m
+        outs = []
+        for i in range(self.m):
+            x = mbs[i] if self.is_first else self.p2p.recv_forward(i == 0)
+            y = self.module(x)
+            if self.is_last:
+                outs.append(y)
+            else:
+                self.p2p.send_forward(y, i == 0)
+        return torch.cat(outs, 0) if self.is_last else None
+
     def _recv_fwd(self, mbs, i, with_header):
         return mbs[i] if self.is_first else self._input(self.p2p.recv_forward(with_header))
 
@@ -279,3 +294,18 @@ def lm_loss(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     from .. import ops
 
     return ops.fused_cross_entropy(logits.reshape(-1, logits.shape[-1]), target.reshape(-1), inplace=False)
+
+
+def make_lm_loss(tp_group=None, loss_parallel: bool = False) -> Callable:
+    """Last-stage loss for Llama pipelines; with TP loss-parallel the stage emits vocab-sharded logits
+    [mb, S, V/tp] and the loss is the vocab-parallel cross-entropy (no [mb, S, V] all-gather)."""
+    if not (loss_parallel and tp_group is not None):
+        return lm_loss
+    from .. import ops
+
+    def loss(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+        vloc = logits.shape[-1]
+        return ops.vocab_parallel_cross_entropy(logits.reshape(-1, vloc), target.reshape(-1),
+                                                dist.get_rank(tp_group) * vloc, tp_group)
+
+    return loss
