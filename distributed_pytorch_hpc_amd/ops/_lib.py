@@ -69,7 +69,8 @@ def ops():
     return torch.ops.dph
 
 
-_reference_mode = False
+# DPH_KERNELS=aten selects the stock-op comparator for a whole process (explicit opt-in, like --kernels aten)
+_reference_mode = os.environ.get("DPH_KERNELS", "dph").lower() == "aten"
 
 
 def set_reference_mode(enabled: bool) -> None:
