@@ -15,12 +15,24 @@ import torch.nn.functional as F
 from torch import nn
 
 
+def _autocast_dtype(t: torch.Tensor):
+    dev = t.device.type
+    return torch.get_autocast_dtype(dev) if torch.is_autocast_enabled(dev) else None
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
+        # autocast: cast once here and save the low-precision copies, so backward GEMMs see matching dtypes
+        # (the low-precision dW is accumulated into the fp32 main_grad below)
+        dt = _autocast_dtype(x)
+        if dt is not None and x.is_floating_point():
+            x, w = x.to(dt), w.to(dt)
+            b = b.to(dt) if b is not None else None
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
-        return F.linear(x, w, b)
+        with torch.autocast(x.device.type, enabled=False):
+            return F.linear(x, w, b)
 
     @staticmethod
     def backward(ctx, gy):

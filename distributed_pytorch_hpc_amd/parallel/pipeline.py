@@ -37,7 +37,10 @@ class P2P:
     def __init__(self, group, stage: int, n_stages: int, device):
         self.group = group
         self.stage, self.n_stages = stage, n_stages
-        ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
+        if group is not None:
+            ranks = dist.get_process_group_ranks(group)
+        else:
+            ranks = list(range(dist.get_world_size())) if dist.is_initialized() else [0]
         self.prev = ranks[stage - 1] if stage > 0 else None
         self.next = ranks[stage + 1] if stage < n_stages - 1 else None
         self.device = device

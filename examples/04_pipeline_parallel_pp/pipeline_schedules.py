@@ -46,13 +46,15 @@ def main(argv=None):
         for i in range(args.warmup + args.steps):
             if i == args.warmup:
                 sync()
-                dist.barrier()
+                if world > 1:
+                    dist.barrier()
                 t0 = time.perf_counter()
             sched.step(inputs=x)
             for p in stage_mod.parameters():
                 p.grad = None
         sync()
-        dist.barrier()
+        if world > 1:
+            dist.barrier()
         dt = (time.perf_counter() - t0) / args.steps
         results[sched_name] = dt
         if rank == 0:

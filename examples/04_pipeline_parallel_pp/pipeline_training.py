@@ -84,7 +84,8 @@ def main(argv=None):
     step_t = sum(times) / len(times)
     tps = args.batch * args.seq_len * args.dp / step_t
     t = torch.tensor([step_t, last_loss if last_loss is not None else 0.0], device=dev)
-    dist.broadcast(t, src=world - 1)   # a last-stage rank owns the loss
+    if world > 1:
+        dist.broadcast(t, src=world - 1)   # a last-stage rank owns the loss
     if rank == 0:
         print(f"avg step {1000 * step_t:.2f} ms | {tps:,.0f} tokens/s | bubble {100 * sched.bubble:.1f}% "
               f"({args.schedule}, S={pp}, M={args.microbatches})", flush=True)

@@ -82,7 +82,8 @@ def main(argv=None):
         sync()
         times.append(time.perf_counter() - t0)
         lt = torch.stack(mb_losses).mean().float() if mb_losses else torch.zeros((), device=dev)
-        dist.all_reduce(lt)   # only last-stage ranks contribute (tp * dp of them)
+        if world > 1:
+            dist.all_reduce(lt)   # only last-stage ranks contribute (tp * dp of them)
         losses.append(lt.item() / (tp * args.dp))
         if rank == 0:
             print(f"3D iter {i}: loss {losses[-1]:.4f} | {1000 * times[-1]:.1f} ms", flush=True)

@@ -5,7 +5,10 @@ set -euo pipefail
 cd "$(dirname "${BASH_SOURCE[0]}")/.."
 OUT=${OUT:-gpurun_out/examples}
 mkdir -p "$OUT"
-run() { local name=$1; shift; echo "== $name"; timeout -k 10 "${T:-300}" python3 "$@" --json-out "$OUT/$name.json" > "$OUT/$name.log" 2>&1; tail -n 1 "$OUT/$name.log"; }
+run() {
+    local name=$1; shift
+    if [[ -n "${ONLY:-}" && " $ONLY " != *" $name "* ]]; then return 0; fi
+    echo "== $name"; timeout -k 10 "${T:-300}" python3 "$@" --json-out "$OUT/$name.json" > "$OUT/$name.log" 2>&1; tail -n 1 "$OUT/$name.log"; }
 run ddp_unet examples/01_data_parallel_ddp/ddp_unet.py --epochs 2 --steps-per-epoch 10 --amp --channels-last
 run fsdp_resnet examples/02_fully_sharded_fsdp/fsdp_resnet.py --use-amp --epochs 2 --steps-per-epoch 10
 run tp_vit examples/03_tensor_parallel_tp/tensor_parallel_vit.py --tp 1 --epochs 1 --steps-per-epoch 10 --bf16
