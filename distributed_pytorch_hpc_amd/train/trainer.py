@@ -204,6 +204,9 @@ class Trainer:
             "avg_epoch_seconds_excl_first": sum(steady) / max(len(steady), 1),
             "samples_per_sec": (sum(h.samples for h in self.history) / max(sum(times), 1e-9)),
             "samples_per_sec_per_gpu": (sum(h.samples for h in self.history) / max(sum(times), 1e-9)) / self.dp_world,
+            # steady state: epochs after the first (kernel autotuning / allocator warm-up land in epoch 0)
+            "samples_per_sec_excl_first": (sum(h.samples for h in self.history[1:]) / max(sum(steady), 1e-9)
+                                           if len(self.history) > 1 else None),
             "final_loss": self.history[-1].loss if self.history else None,
         }
         if self.rank == 0 and self.history:

@@ -112,13 +112,13 @@ def main(argv=None):
         summary["eval"] = trainer.evaluate(_CL(), max_steps=args.eval_steps)
     summary.update(example="resnet_benchmark", arch=args.arch, params=n_params, world=world,
                    mode="fsdp" if args.use_fsdp else "ddp", amp=args.amp,
-                   images_per_sec=summary["samples_per_sec"])
+                   images_per_sec=summary["samples_per_sec_excl_first"] or summary["samples_per_sec"])
     if rank == 0 and args.logfile:
         with open(args.logfile, "a") as fh:
             fh.write(f"{time.strftime('%Y-%m-%d %H:%M:%S')} {args.arch} world={world} "
                      f"{'fsdp' if args.use_fsdp else 'ddp'} amp={args.amp} bs={args.batch_size} "
                      f"avg_epoch_s(excl 0)={summary['avg_epoch_seconds_excl_first']:.4f} "
-                     f"img/s={summary['samples_per_sec']:.1f} | {env_report(backend)}\n")
+                     f"img/s(excl 0)={summary['images_per_sec']:.1f} | {env_report(backend)}\n")
     finish(args, summary, rank)
 
 
