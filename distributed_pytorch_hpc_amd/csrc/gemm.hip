@@ -1,0 +1,260 @@
+// Weight-gradient GEMM for CDNA4 (gfx950):  C[M, N] (+)= A^T B  with A [K, M] and B [K, N] both row-major
+// (token-major activations / output gradients, K = tokens).  This is dW = dY^T X of every linear layer.
+//
+// hipBLASLt runs this "both operands K-strided" pattern at 0.95-1.2 PFLOP/s on the Llama-2-7B shapes while the
+// K-contiguous pattern reaches 1.5-1.6 PFLOP/s (profiles/gemm_layout_*.json); transposing the operands first
+// costs more than it saves.  Here the transposition happens on the LDS -> register path instead:
+//   * 256 x 256 output tile per workgroup, 8 waves as 2 (M) x 4 (N), each wave 128 x 64 = 4 x 2 MFMA
+//     32x32x16 bf16 tiles (128 fp32 accumulator VGPRs);
+//   * K-steps of 64 tokens: the [64][256] A and B tiles are copied global -> LDS by LDS-DMA
+//     (global_load_lds_dwordx4, 16 B per lane, lane-linear destination, swizzle applied to the SOURCE address),
+//     double-buffered so the copy of step t+1 overlaps the MFMAs of step t;
+//   * MFMA operands (8 consecutive k of one m or n column per lane) come from ds_read_b64_tr_b16 transposed
+//     reads; the LDS image XORs each 16-B slot with (row & 3) << 2, which makes the 4-row x 4-chunk footprint of
+//     a half-wave's transposed read cover all 64 banks exactly once;
+//   * workgroups are remapped so each XCD (blockIdx % 8 under round-robin dispatch) owns a contiguous range of
+//     output tiles, grouped GROUP_M tiles tall, for L2 reuse of the shared A / B column panels.
+// Requirements (checked by the host op): M % 256 == 0, N % 256 == 0, K % 64 == 0, lda / ldb % 8 == 0,
+// 16-B aligned bases.  Other shapes use hipBLASLt.
+#include <type_traits>
+
+#include "dph_common.h"
+#include "kernels.h"
+
+namespace dph {
+
+namespace {
+
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4_g;
+
+constexpr int GBM = 256, GBN = 256, GBK = 64, GNT = 512;
+constexpr int ROWB = GBM * 2;              // bytes per LDS image row (256 bf16)
+constexpr int TILEB = GBK * ROWB;          // 32 KB per operand tile
+constexpr int GROUP_M = 8;
+
+__device__ __forceinline__ bf16x8 tr2(const char* base, int off_lo, int off_hi) {
+  i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_g*)(base + off_lo));
+  i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_g*)(base + off_hi));
+  bf16x4 a = __builtin_bit_cast(bf16x4, lo), b = __builtin_bit_cast(bf16x4, hi);
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// LDS-DMA of 16 B per lane: global (uniform SGPR base `sbase` + per-lane 32-bit byte offset `voff`) -> LDS
+// (lane-linear destination at the wave-uniform LDS byte address `lds`).  Issued from inline asm on purpose:
+// hipcc cannot tell that the transposed ds_reads of OTHER regions do not alias an in-flight DMA and would drain
+// every DMA (vmcnt(0)) before each read; the asm form is invisible to its wait bookkeeping, and completion is
+// counted explicitly (wait_vm<N> + s_barrier) before any region is read.  The SGPR-base form keeps the per-slot
+// address arithmetic scalar.
+__device__ __forceinline__ void glds16(const char* sbase, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds)
+               : "memory");
+}
+
+// s_waitcnt with only the vector-memory counter constrained (LDS-DMA completion), gfx9 encoding.
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// Pipeline: one K-step (64 tokens) = 4 phases of 16 k-rows.  Phase P's operands live in LDS region
+// R = P & 7 (tile parity x 16-row region; A rows at +0, B rows at +8 KB of a 16-KB region) and are filled by DMA
+// "pair P" (one 16-B global_load_lds per thread per operand, inline asm: see glds16).  In slot P every wave
+//   1. waits (counted vmcnt) for its share of pair P+1 and meets the others at a raw s_barrier,
+//   2. issues pair P+4 (same region of the next tile; that region was last read in phase P-4),
+//   3. issues the transposed LDS reads of phase P+1 into the other fragment register set,
+//   4. runs the 8 MFMAs of phase P (operands read one slot earlier) -- the LDS latency of step 3 and the DMA
+//      latency of step 2 hide behind them.
+// DMA pairs are issued in phase order, so the pairs allowed in flight at step 1 are the ones issued after
+// pair P+1: min(NP - P - 2, 2) of them.  Slots are unrolled 8 at a time (two K-steps) so every region index
+// is a compile-time constant.
+#define DPH_GEMM_REGIONS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+
+template <typename OutT, bool ACCUM>
+__global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                     OutT* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                     int64_t ldb, int64_t ldc) {
+  __shared__ __attribute__((aligned(1024))) char lds[8 * 16384];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 2, wn = wid & 3;                          // 2 x 4 waves
+  const int h = lane >> 5, l32 = lane & 31;
+  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+
+  // ---- XCD-aware, grouped tile order ----
+  const int tiles_m = M / GBM, tiles_n = N / GBN, nwg = tiles_m * tiles_n;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int group = lin / (GROUP_M * tiles_n);
+  const int first_m = group * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int tm = first_m + (lin % (GROUP_M * tiles_n)) % gsz;
+  const int tn = (lin % (GROUP_M * tiles_n)) / gsz;
+  const int m0 = tm * GBM, n0 = tn * GBN;
+
+  // ---- per-lane transposed-read offsets within a region (hi half = +8 rows = +4096 bytes) ----
+  const int x = 2 * (g & 1) + (tp >> 1);
+  const int krow = 4 * (g >> 1) + tq;                             // krow & 3 == tq
+  const int base = krow * ROWB + 8 * (tp & 1);
+  int aoff[4], boff[2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) aoff[mt] = base + (wm << 8) + ((4 * (mt ^ tq) + x) << 4);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+    boff[nt] = 8192 + base + ((wn >> 1) << 8) + ((4 * ((((wn & 1) << 1) | nt) ^ tq) + x) << 4);
+
+  // ---- per-lane DMA source offsets: chunk tid of a 16-row region (row tid/32, swizzled slot) ----
+  const int srow = threadIdx.x >> 5, lr = (threadIdx.x >> 4) & 1, sslot = threadIdx.x & 15;
+  const int sch = (lr << 4) | (sslot ^ ((srow & 3) << 2));
+  const unsigned voffA = (unsigned)((srow * lda + sch * 8) * 2), voffB = (unsigned)((srow * ldb + sch * 8) * 2);
+  const char* Ag = reinterpret_cast<const char*>(A + m0);        // uniform
+  const char* Bg = reinterpret_cast<const char*>(B + n0);
+  const int64_t stepA = 16 * lda * 2, stepB = 16 * ldb * 2;       // bytes per 16-row region
+  const unsigned lds_wave = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds + (threadIdx.x >> 6) * 1024);
+
+  auto region = [&](auto RI) -> char* { return lds + decltype(RI)::value * 16384; };
+  auto dma_pair = [&](int P, auto RI) {
+    const unsigned d = lds_wave + decltype(RI)::value * 16384;
+    glds16(Ag + P * stepA, voffA, d);
+    glds16(Bg + P * stepB, voffB, d + 8192);
+  };
+  auto read_phase = [&](auto RI, bf16x8 (&af)[4], bf16x8 (&bfr)[2]) {
+    const char* rg = region(RI);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) af[mt] = tr2(rg, aoff[mt], aoff[mt] + 8 * ROWB);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) bfr[nt] = tr2(rg, boff[nt], boff[nt] + 8 * ROWB);
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.f;
+
+  auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  const int NP = (K / GBK) * 4;
+  // prologue: the first tile (pairs 0..3 -> regions 0..3), then phase 0's fragments
+  dma_pair(0, I0{});
+  dma_pair(1, I1{});
+  dma_pair(2, I2{});
+  dma_pair(3, I3{});
+  wait_vm<6>();
+  __builtin_amdgcn_s_barrier();
+  bf16x8 af0[4], bf0[2], af1[4], bf1[2];
+  read_phase(I0{}, af0, bf0);
+
+  // Slot S of a two-tile super-step (phase P = P0 + S, region S, operands in register set S & 1).  Every
+  // flag is a compile-time constant so the loop body has no branches (the waitcnt pass would otherwise
+  // merge states pessimistically at the joins and wait lgkmcnt(0) before the MFMAs).
+  //   WAIT: vmcnt to wait for (-1: none, last phase), DMA: issue pair P+4, READ: prefetch phase P+1.
+  auto slot = [&](int P0, auto SI, auto WAITI, auto DMAI, auto READI, bf16x8 (&afc)[4], bf16x8 (&bfc)[2],
+                  bf16x8 (&afn)[4], bf16x8 (&bfn)[2]) {
+    constexpr int S = decltype(SI)::value, WAIT = decltype(WAITI)::value;
+    constexpr bool DMA = decltype(DMAI)::value, READ = decltype(READI)::value;
+    if constexpr (WAIT >= 0) {
+      wait_vm<(WAIT >= 0 ? WAIT : 0)>();
+      __builtin_amdgcn_s_barrier();
+    }
+    if constexpr (DMA) dma_pair(P0 + S + 4, std::integral_constant<int, (S + 4) & 7>{});
+    if constexpr (READ) read_phase(std::integral_constant<int, (S + 1) & 7>{}, afn, bfn);
+    mma(afc, bfc);
+    __builtin_amdgcn_sched_barrier(0);   // keep the next slot's reads out of this slot (register pressure)
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  using W4 = std::integral_constant<int, 4>;
+  using W2 = std::integral_constant<int, 2>;
+  using W0 = std::integral_constant<int, 0>;
+  using WN = std::integral_constant<int, -1>;
+#define DPH_S(i) std::integral_constant<int, i>{}
+  int P0 = 0;
+  // steady state: all 8 slots issue their DMA pair (P + 4 < NP) and keep two pairs in flight
+  for (; P0 + 12 <= NP; P0 += 8) {
+    slot(P0, DPH_S(0), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
+    slot(P0, DPH_S(1), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
+    slot(P0, DPH_S(2), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
+    slot(P0, DPH_S(3), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
+    slot(P0, DPH_S(4), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
+    slot(P0, DPH_S(5), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
+    slot(P0, DPH_S(6), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
+    slot(P0, DPH_S(7), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
+  }
+  if (NP - P0 == 8) {   // last two K-steps: DMA only for the final tile, then drain
+    slot(P0, DPH_S(0), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
+    slot(P0, DPH_S(1), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
+    slot(P0, DPH_S(2), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
+    slot(P0, DPH_S(3), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
+    slot(P0, DPH_S(4), W4{}, F_{}, T_{}, af0, bf0, af1, bf1);
+    slot(P0, DPH_S(5), W2{}, F_{}, T_{}, af1, bf1, af0, bf0);
+    slot(P0, DPH_S(6), W0{}, F_{}, T_{}, af0, bf0, af1, bf1);
+    slot(P0, DPH_S(7), WN{}, F_{}, F_{}, af1, bf1, af0, bf0);
+  } else {              // last K-step
+    slot(P0, DPH_S(0), W4{}, F_{}, T_{}, af0, bf0, af1, bf1);
+    slot(P0, DPH_S(1), W2{}, F_{}, T_{}, af1, bf1, af0, bf0);
+    slot(P0, DPH_S(2), W0{}, F_{}, T_{}, af0, bf0, af1, bf1);
+    slot(P0, DPH_S(3), WN{}, F_{}, F_{}, af1, bf1, af0, bf0);
+  }
+#undef DPH_S
+
+  // ---- epilogue: register i of tile (mt, nt) holds C[row (i&3) + 8(i>>2) + 4h][col l32] ----
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const int col = n0 + wn * 64 + nt * 32 + l32;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = m0 + wm * 128 + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        OutT* p = C + (int64_t)row * ldc + col;
+        float v = acc[mt][nt][i];
+        if (ACCUM) v += (float)*p;
+        *p = (OutT)v;
+      }
+    }
+}
+
+}  // namespace
+
+bool gemm_tn_supported(int64_t M, int64_t N, int64_t K) {
+  return M > 0 && N > 0 && K > 0 && M % GBM == 0 && N % GBN == 0 && K % GBK == 0;
+}
+
+void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+             int64_t ldc, int out_dtype, bool accumulate, hipStream_t st) {
+  const int nwg = (int)((M / GBM) * (N / GBN));
+  const size_t lds = 0;   // static: 8 x 16 KB regions
+  const dim3 grid(nwg), block(GNT);
+#define DPH_GEMM_LAUNCH(T, ACC)                                                                             \
+  hipLaunchKernelGGL((gemm_tn_k<T, ACC>), grid, block, lds, st, (const bf16*)A, (const bf16*)B, (T*)C, (int)M, \
+                     (int)N, (int)K, lda, ldb, ldc)
+  if (out_dtype == kBF16) {
+    if (accumulate) DPH_GEMM_LAUNCH(bf16, true);
+    else DPH_GEMM_LAUNCH(bf16, false);
+  } else {
+    if (accumulate) DPH_GEMM_LAUNCH(float, true);
+    else DPH_GEMM_LAUNCH(float, false);
+  }
+#undef DPH_GEMM_LAUNCH
+}
+
+}  // namespace dph

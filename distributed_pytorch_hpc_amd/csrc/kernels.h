@@ -90,6 +90,11 @@ void embedding_bwd(const int64_t* ids, const void* dout, float* dtable_f32, int6
                    int64_t vocab_start, int64_t vocab_local, int dtype, hipStream_t stream);
 
 // ---- cast / scale helpers ----
+// C[M, N] (+)= A^T B, A [K, M] / B [K, N] bf16 row-major (weight gradient); C bf16 or fp32.
+bool gemm_tn_supported(int64_t M, int64_t N, int64_t K);
+void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+             int64_t ldc, int out_dtype, bool accumulate, hipStream_t stream);
+
 void cast_copy(const void* src, void* dst, int64_t n, int src_dtype, int dst_dtype, float scale, hipStream_t stream);
 
 }  // namespace dph

@@ -338,6 +338,25 @@ Tensor embedding_bwd(const Tensor& ids, const Tensor& dout, int64_t vocab_local,
   return dtab;
 }
 
+// ------------------------------------------------------------------------------------------------ wgrad GEMM
+// C[M, N] (+)= A^T B with A [K, M], B [K, N] bf16 row-major (dW = dY^T X).  C bf16 or fp32, row-major.
+void gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate) {
+  check_cuda(A, "A");
+  c10::DeviceGuard g(A.device());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm_tn: 2-D operands required");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_tn: bf16 A / B");
+  const int64_t K = A.size(0), M = A.size(1), N = B.size(1);
+  TORCH_CHECK(B.size(0) == K && C.size(0) == M && C.size(1) == N, "gemm_tn: shape mismatch");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "gemm_tn: row-major operands required");
+  TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0, "gemm_tn: leading dims must be multiples of 8");
+  TORCH_CHECK(dph::gemm_tn_supported(M, N, K), "gemm_tn: need M, N % 256 == 0 and K % 64 == 0 (got ", M, ", ", N,
+              ", ", K, ")");
+  check_align16(A, "A");
+  check_align16(B, "B");
+  dph::gemm_tn(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0), dt_code(C),
+               accumulate, cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dph, m) {
@@ -364,6 +383,7 @@ TORCH_LIBRARY(dph, m) {
         "bool causal, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
+  m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dph, CUDA, m) {
@@ -385,4 +405,5 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("flash_attn_bwd_into", &flash_attn_bwd_into);
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
+  m.impl("gemm_tn_", &gemm_tn_);
 }

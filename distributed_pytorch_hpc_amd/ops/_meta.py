@@ -72,6 +72,11 @@ def _sumsq(x, out):
     return None
 
 
+@register_fake("dph::gemm_tn_")
+def _gemm_tn(C, A, B, accumulate):
+    return None
+
+
 @register_fake("dph::cross_entropy_fwd")
 def _xent(logits, target, inv_count, ignore_index, grad_inplace, smoothing):
     n = logits.shape[0]

@@ -15,6 +15,29 @@ import torch.nn.functional as F
 from torch import nn
 
 
+def _native_wgrad(out: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor, accumulate: bool) -> bool:
+    """out[N_out, N_in] (+)= g2^T x2 on the CDNA4 weight-gradient kernel (csrc/gemm.hip) when the shapes fit
+    its 256 x 256 x 64 tiling; False -> caller uses hipBLASLt."""
+    if not (g2.is_cuda and g2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16):
+        return False
+    from ..ops import _lib
+
+    if _lib.reference_mode():
+        return False
+    T, M = g2.shape
+    N = x2.shape[1]
+    if M % 256 or N % 256 or T % 64 or T == 0:
+        return False
+    if g2.stride(1) != 1 or x2.stride(1) != 1 or g2.stride(0) % 8 or x2.stride(0) % 8:
+        return False
+    if not out.is_contiguous() or out.dtype not in (torch.bfloat16, torch.float32):
+        return False
+    if g2.data_ptr() % 16 or x2.data_ptr() % 16:
+        return False
+    _lib.ops().gemm_tn_(out, g2, x2, accumulate)
+    return True
+
+
 def _autocast_dtype(t: torch.Tensor):
     dev = t.device.type
     return torch.get_autocast_dtype(dev) if torch.is_autocast_enabled(dev) else None
@@ -44,7 +67,10 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             mg = getattr(w, "main_grad", None)
-            if mg is not None and mg.dtype != x2.dtype:
+            if mg is not None and _native_wgrad(mg, g2, x2, getattr(w, "_dph_accum", False)):
+                w._dph_accum = True
+                w._dph_grad_ready()
+            elif mg is not None and mg.dtype != x2.dtype:
                 gw_ = g2.t().mm(x2)
                 if getattr(w, "_dph_accum", False):
                     mg.add_(gw_)
@@ -60,7 +86,9 @@ class _LinearFn(torch.autograd.Function):
                     w._dph_accum = True
                 w._dph_grad_ready()
             else:
-                gw = g2.t().mm(x2)
+                gw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
+                if not _native_wgrad(gw, g2, x2, False):
+                    gw = g2.t().mm(x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = g2.sum(0)
             if getattr(w, "main_grad", None) is not None and gb is not None:
