@@ -44,6 +44,8 @@ def parse(argv=None):
     ap.add_argument("--kernels", choices=["dph", "aten"], default="dph",
                     help="dph: CDNA4 HIP kernels (default); aten: stock PyTorch-ROCm ops (comparator)")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--ac", default="none",
+                    help="activation checkpointing: none | auto (fit 288 GB) | N (every N-th block)")
     ap.add_argument("--force-dist", action="store_true",
                     help="create the RCCL process group even for one rank (exercises the N>1 collective path)")
     ap.add_argument("--quiet", action="store_true")
@@ -74,6 +76,16 @@ def main(argv=None):
         _lib.set_reference_mode(True)
     margs = get_preset(args.model, max_seq_len=max(args.seq_len, 4096))
     model = build_llama(margs, device=dev, dtype=torch.bfloat16, seed=1234)
+    ac_every = 0
+    if args.ac != "none":
+        from distributed_pytorch_hpc_amd.parallel.activation_checkpoint import (apply_llama_checkpointing,
+                                                                                plan_llama_checkpointing)
+
+        n_par = margs.num_params()
+        static_gb = n_par * (4 + (12 / world if world > 1 else 12)) / 1e9
+        ac_every = (plan_llama_checkpointing(margs, args.micro_batch, args.seq_len, static_gb=static_gb)
+                    if args.ac == "auto" else int(args.ac))
+        apply_llama_checkpointing(model, ac_every)
     mode = args.parallel
     if mode == "auto":
         mode = "fsdp" if world > 1 or args.force_dist else "ddp"
@@ -149,6 +161,7 @@ def main(argv=None):
                 "tokens_per_step": world * B * S,
                 "kernels": args.kernels,
                 "bucket_mb": args.bucket_mb,
+                "activation_checkpoint_every": ac_every,
             },
             "tokens_per_sec_per_gpu": round(tps / world, 2),
             "mfu_vs_2.5PF_bf16_dense": round(mfu, 4),

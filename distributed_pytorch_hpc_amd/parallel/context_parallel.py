@@ -14,7 +14,14 @@ batch_isend_irecv posted BEFORE the local block so the xGMI transfer overlaps th
 merged with the online-softmax rule on (o, lse) -- the flash forward kernel emits the log-sum-exp.  Backward
 re-runs the ring: per block the flash backward kernel, fed the FINAL (o, lse), yields exact dq/dk/dv
 contributions; dK/dV accumulators travel with their K/V chunk and arrive home after P hops.  With causal
-attention and contiguous chunks, block (q_r, kv_j) is full for j < r, causal for j == r, skipped for j > r.
+attention and contiguous chunks, block (q_r, kv_j) is full for j < r, causal for j == r, skipped for j > r --
+rank P-1 does P blocks of work while rank 0 does one.
+
+Zig-zag layout (``layout="zigzag"``, load-balanced causal): the sequence is cut into 2P chunks and rank r holds
+chunks r and 2P-1-r.  Against the K/V of rank j every step costs the same half block: j == r is a causal pass
+over the local pair, j < r is (all local queries) x (first K/V chunk, full), j > r is (second query chunk) x (both
+K/V chunks, full).  ``shard_sequence`` / ``unshard_sequence`` map tokens to and from the layout, and RoPE uses
+each chunk's global positions.
 """
 from __future__ import annotations
 
@@ -141,46 +148,72 @@ class _Ring:
 
 class _RingAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, group, causal, scale):
+    def forward(ctx, q, k, v, group, causal, scale, zigzag):
         p, r = _ws(group), _rank(group)
         ring = _Ring(group)
-        o = lse = None
+        c = q.shape[1] // 2
+        o = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
+        lse = torch.full((q.shape[0], q.shape[2], q.shape[1]), float("-inf"), dtype=torch.float32, device=q.device)
+
+        def accumulate(rows, ob, lb):
+            o_r, l_r = o[:, rows], lse[:, :, rows]
+            new_o, new_l = _merge(o_r, l_r, ob, lb)
+            o[:, rows], lse[:, :, rows] = new_o, new_l
+
         kc, vc = k.contiguous(), v.contiguous()
         for i in range(p):
             j = (r - i) % p                       # owner of the K/V chunk held at step i
             works = bufs = None
             if i < p - 1:
                 works, bufs = ring.start([kc, vc])
-            if not causal or j <= r:
-                ob, lb = _attn_fwd_lse(q, kc, vc, causal and j == r, scale)
-                if o is None:
-                    o, lse = ob.float(), lb
-                else:
-                    o, lse = _merge(o, lse, ob, lb)
+            allq = slice(0, q.shape[1])
+            if not causal:
+                accumulate(allq, *_attn_fwd_lse(q, kc, vc, False, scale))
+            elif not zigzag:
+                if j <= r:
+                    accumulate(allq, *_attn_fwd_lse(q, kc, vc, j == r, scale))
+            elif j == r:
+                accumulate(allq, *_attn_fwd_lse(q, kc, vc, True, scale))
+            elif j < r:
+                accumulate(allq, *_attn_fwd_lse(q, kc[:, :c], vc[:, :c], False, scale))
+            else:
+                accumulate(slice(c, 2 * c), *_attn_fwd_lse(q[:, c:], kc, vc, False, scale))
             if works is not None:
                 for w in works:
                     w.wait()
                 kc, vc = bufs
         out = o.to(q.dtype)
         ctx.save_for_backward(q, k, v, out, lse)
-        ctx.group, ctx.causal, ctx.scale = group, causal, scale
+        ctx.group, ctx.causal, ctx.scale, ctx.zigzag = group, causal, scale, zigzag
         return out
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
-        group, causal, scale = ctx.group, ctx.causal, ctx.scale
+        group, causal, scale, zigzag = ctx.group, ctx.causal, ctx.scale, ctx.zigzag
         p, r = _ws(group), _rank(group)
         ring = _Ring(group)
+        c = q.shape[1] // 2
         dq = torch.zeros_like(q, dtype=torch.float32)
         kc, vc = k.contiguous(), v.contiguous()
         dkc = torch.zeros_like(k, dtype=torch.float32)
         dvc = torch.zeros_like(v, dtype=torch.float32)
         for i in range(p):
             j = (r - i) % p
-            if not causal or j <= r:
+            if not causal or (not zigzag and j <= r) or (zigzag and j == r):
                 dq_i, dk_i, dv_i = _attn_bwd(do, q, kc, vc, o, lse, causal and j == r, scale)
                 dq += dq_i.float()
+                dkc += dk_i.float()
+                dvc += dv_i.float()
+            elif zigzag and j < r:     # all queries x first K/V chunk
+                dq_i, dk_i, dv_i = _attn_bwd(do, q, kc[:, :c], vc[:, :c], o, lse, False, scale)
+                dq += dq_i.float()
+                dkc[:, :c] += dk_i.float()
+                dvc[:, :c] += dv_i.float()
+            elif zigzag:               # second query chunk x all K/V
+                dq_i, dk_i, dv_i = _attn_bwd(do[:, c:], q[:, c:], kc, vc, o[:, c:], lse[:, :, c:].contiguous(), False,
+                                             scale)
+                dq[:, c:] += dq_i.float()
                 dkc += dk_i.float()
                 dvc += dv_i.float()
             # move (K, V, dK-acc, dV-acc) one hop; after p hops every accumulator is home
@@ -191,42 +224,85 @@ class _RingAttnFn(torch.autograd.Function):
             for w in works:
                 w.wait()
             dkc, dvc = dkc_n, dvc_n
-        return dq.to(q.dtype), dkc.to(k.dtype), dvc.to(v.dtype), None, None, None
+        return dq.to(q.dtype), dkc.to(k.dtype), dvc.to(v.dtype), None, None, None, None
 
 
-def ring_attention(q, k, v, group, causal: bool = True, scale: float | None = None):
-    """Exact attention over a sequence sharded contiguously across ``group``: q/k/v [B, S/P, H, D]."""
+def ring_attention(q, k, v, group, causal: bool = True, scale: float | None = None, layout: str = "contiguous"):
+    """Exact attention over a sequence sharded across ``group``: q/k/v [B, S/P, H, D] in ``layout``
+    ("contiguous": rank r holds chunk r; "zigzag": chunks r and 2P-1-r, see ``shard_sequence``)."""
     scale = 1.0 / math.sqrt(q.shape[-1]) if scale is None else scale
     if _ws(group) == 1:
         return ops.flash_attention(q, k, v, causal, scale)
-    return _RingAttnFn.apply(q, k, v, group, causal, scale)
+    assert layout in ("contiguous", "zigzag")
+    if layout == "zigzag":
+        assert q.shape[1] % 2 == 0, "zig-zag layout needs an even local sequence length"
+    return _RingAttnFn.apply(q, k, v, group, causal, scale, layout == "zigzag")
+
+
+def zigzag_chunks(rank: int, world: int) -> tuple[int, int]:
+    return rank, 2 * world - 1 - rank
+
+
+def shard_sequence(t: torch.Tensor, group, layout: str = "contiguous", dim: int = 1) -> torch.Tensor:
+    """This rank's share of a full-sequence tensor (tokens, targets, activations) for the given layout."""
+    p, r = _ws(group), _rank(group)
+    if layout == "contiguous":
+        return t.chunk(p, dim)[r].contiguous()
+    ch = t.chunk(2 * p, dim)
+    a, b = zigzag_chunks(r, p)
+    return torch.cat([ch[a], ch[b]], dim).contiguous()
+
+
+def unshard_sequence(parts: list, layout: str = "contiguous", dim: int = 1) -> torch.Tensor:
+    """Inverse of ``shard_sequence`` given every rank's share (rank order)."""
+    if layout == "contiguous":
+        return torch.cat(parts, dim)
+    p = len(parts)
+    chunks = [None] * (2 * p)
+    for r, t in enumerate(parts):
+        x, y = t.chunk(2, dim)
+        a, b = zigzag_chunks(r, p)
+        chunks[a], chunks[b] = x, y
+    return torch.cat(chunks, dim)
 
 
 class RingAttention:
-    def __init__(self, group, causal: bool = True):
-        self.group, self.causal = group, causal
+    def __init__(self, group, causal: bool = True, layout: str = "contiguous"):
+        self.group, self.causal, self.layout = group, causal, layout
+
+    def _rope(self, x, cos, sin, off):
+        if x.is_cuda:
+            from ..ops.rope import apply_rope
+
+            return apply_rope(x, cos, sin, off)
+        return rope_reference(x, cos, sin, off)
 
     def __call__(self, qkv, cos, sin, nh, nkv, hd):
         b, s_loc, _ = qkv.shape
-        off = _rank(self.group) * s_loc            # global position of the local chunk
         q, k, v = _split_qkv(qkv, nh, nkv, hd)
-        if qkv.is_cuda:
-            from ..ops.rope import apply_rope
-
-            q, k = apply_rope(q, cos, sin, off), apply_rope(k, cos, sin, off)
+        p, r = _ws(self.group), _rank(self.group)
+        if self.layout == "zigzag":
+            c = s_loc // 2
+            a, bb = zigzag_chunks(r, p)          # global positions of the two local chunks
+            q = torch.cat([self._rope(q[:, :c], cos, sin, a * c), self._rope(q[:, c:], cos, sin, bb * c)], 1)
+            k = torch.cat([self._rope(k[:, :c], cos, sin, a * c), self._rope(k[:, c:], cos, sin, bb * c)], 1)
         else:
-            q, k = rope_reference(q, cos, sin, off), rope_reference(k, cos, sin, off)
-        o = ring_attention(q, k, v.contiguous(), self.group, self.causal)
+            off = r * s_loc                       # global position of the local chunk
+            q, k = self._rope(q, cos, sin, off), self._rope(k, cos, sin, off)
+        o = ring_attention(q, k, v.contiguous(), self.group, self.causal, layout=self.layout)
         return o.reshape(b, s_loc, nh * hd)
 
 
-def apply_context_parallel(model, cp_group, mode: str = "ulysses"):
+def apply_context_parallel(model, cp_group, mode: str = "ulysses", layout: str = "contiguous"):
     """Install Ulysses / ring attention in every Attention module of a models.llama2.Transformer.
 
-    The caller shards tokens and targets contiguously along the sequence over ``cp_group`` and includes the cp
-    ranks in the gradient data-parallel group (each rank's loss is a mean over its local tokens).
+    The caller shards tokens and targets with ``shard_sequence(t, cp_group, layout)`` (Ulysses: contiguous;
+    ring: contiguous or zigzag) and includes the cp ranks in the gradient data-parallel group (each rank's loss
+    is a mean over its local tokens).
     """
-    impl = UlyssesAttention(cp_group) if mode == "ulysses" else RingAttention(cp_group)
+    if mode == "ulysses":
+        assert layout == "contiguous", "Ulysses gathers the sequence in rank order: contiguous layout only"
+    impl = UlyssesAttention(cp_group) if mode == "ulysses" else RingAttention(cp_group, layout=layout)
     for layer in model.layers:
         layer.attention.cp_attention = impl
     model.cp_group = cp_group

@@ -25,7 +25,7 @@ import torch.distributed as dist  # noqa: E402
 
 from distributed_pytorch_hpc_amd.comm.mesh import Mesh  # noqa: E402
 from distributed_pytorch_hpc_amd.models.llama2 import build_llama, get_preset  # noqa: E402
-from distributed_pytorch_hpc_amd.parallel.context_parallel import apply_context_parallel  # noqa: E402
+from distributed_pytorch_hpc_amd.parallel.context_parallel import apply_context_parallel, shard_sequence  # noqa: E402
 from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig  # noqa: E402
 from distributed_pytorch_hpc_amd.train.cli import common_parser, finish, start  # noqa: E402
 from distributed_pytorch_hpc_amd.utils.metrics import sync  # noqa: E402
@@ -35,6 +35,8 @@ def main(argv=None):
     ap = common_parser(__doc__)
     ap.add_argument("--mode", choices=["ulysses", "ring"], default="ulysses")
     ap.add_argument("--cp", type=int, default=None, help="context-parallel degree (default: world)")
+    ap.add_argument("--layout", choices=["auto", "contiguous", "zigzag"], default="auto",
+                    help="sequence sharding; auto = zigzag (load-balanced causal) for ring, contiguous for Ulysses")
     ap.add_argument("--model", default="toy")
     ap.add_argument("--n-layers", type=int, default=None)
     ap.add_argument("--seq-len", type=int, default=1024, help="GLOBAL sequence length")
@@ -55,7 +57,8 @@ def main(argv=None):
     margs = get_preset(args.model, **over)
     dtype = torch.bfloat16 if dev.type == "cuda" else torch.float32
     model = build_llama(margs, device=dev, dtype=dtype, seed=args.seed)
-    apply_context_parallel(model, mesh.group("cp"), args.mode)
+    layout = args.layout if args.layout != "auto" else ("zigzag" if args.mode == "ring" else "contiguous")
+    apply_context_parallel(model, mesh.group("cp"), args.mode, layout=layout)
     engine = DataParallelEngine(model, None, shard=world > 1 and dev.type == "cuda")
     engine.configure_optimizer(OptimConfig("adamw", lr=args.lr, betas=(0.9, 0.95), weight_decay=0.1))
     s_loc = args.seq_len // cp
@@ -63,8 +66,8 @@ def main(argv=None):
     times = []
     for step in range(args.warmup + args.steps):
         t = torch.randint(0, margs.vocab_size, (args.batch, args.seq_len + 1), device=dev, generator=g)
-        x = t[:, :-1][:, cp_rank * s_loc:(cp_rank + 1) * s_loc]
-        y = t[:, 1:][:, cp_rank * s_loc:(cp_rank + 1) * s_loc]
+        x = shard_sequence(t[:, :-1], mesh.group("cp"), layout)
+        y = shard_sequence(t[:, 1:], mesh.group("cp"), layout)
         sync()
         t0 = time.perf_counter()
         loss = model(x, y)
@@ -82,7 +85,7 @@ def main(argv=None):
     engine.synchronize()
     step_t = sum(times) / len(times)
     tps = args.batch * args.seq_len * (world // cp) / step_t
-    summary = {"example": "context_parallel_llama", "mode": args.mode, "cp": cp, "dp": world // cp,
+    summary = {"example": "context_parallel_llama", "mode": args.mode, "layout": layout, "cp": cp, "dp": world // cp,
                "model": args.model, "seq_len": args.seq_len, "ms_per_step": 1000 * step_t,
                "tokens_per_sec": tps, "final_loss": lt.item() / world}
     finish(args, summary, rank)

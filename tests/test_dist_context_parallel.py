@@ -81,3 +81,65 @@ def test_llama_context_parallel(mode):
     for l, gw in outs:
         assert abs(l - loss.item()) < 1e-5
         assert torch.allclose(gw, ref_g, atol=1e-5, rtol=1e-4)
+
+
+def _zigzag_worker(rank, world):
+    from distributed_pytorch_hpc_amd.parallel.context_parallel import ring_attention, shard_sequence
+
+    q, k, v = _qkv(s=48)
+    g = torch.Generator().manual_seed(9)
+    do = torch.randn(q.shape, generator=g)
+    grp = dist.group.WORLD
+    ql, kl, vl = (shard_sequence(t, grp, "zigzag").requires_grad_() for t in (q, k, v))
+    o = ring_attention(ql, kl, vl, grp, causal=True, layout="zigzag")
+    o.backward(shard_sequence(do, grp, "zigzag"))
+    return o.detach(), ql.grad, kl.grad, vl.grad
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_zigzag_ring_attention_matches_full(world):
+    """Load-balanced causal layout: rank r holds chunks r and 2P-1-r."""
+    from distributed_pytorch_hpc_amd.ops.attention import attention_reference
+    from distributed_pytorch_hpc_amd.parallel.context_parallel import unshard_sequence
+
+    q, k, v = (t.clone().requires_grad_() for t in _qkv(s=48))
+    o = attention_reference(q, k, v, True, 1 / math.sqrt(q.shape[-1]))
+    g = torch.Generator().manual_seed(9)
+    o.backward(torch.randn(o.shape, generator=g))
+    outs = run_distributed(_zigzag_worker, world)
+    for i, ref in enumerate((o.detach(), q.grad, k.grad, v.grad)):
+        got = unshard_sequence([out[i] for out in outs], "zigzag")
+        assert torch.allclose(got, ref, atol=1e-5), (i, (got - ref).abs().max())
+
+
+def _llama_zigzag_worker(rank, world):
+    from distributed_pytorch_hpc_amd.models.llama2 import ModelArgs, build_llama
+    from distributed_pytorch_hpc_amd.parallel.context_parallel import apply_context_parallel, shard_sequence
+
+    m = build_llama(ModelArgs(**PRESET), device="cpu", dtype=torch.float32, seed=3)
+    apply_context_parallel(m, dist.group.WORLD, "ring", layout="zigzag")
+    g = torch.Generator().manual_seed(1)
+    t = torch.randint(0, 128, (2, 33), generator=g)
+    x = shard_sequence(t[:, :-1], dist.group.WORLD, "zigzag")
+    y = shard_sequence(t[:, 1:], dist.group.WORLD, "zigzag")
+    loss = m(x, y)
+    loss.backward()
+    gw = m.layers[0].attention.wqkv.weight.grad.clone()
+    dist.all_reduce(gw)
+    lt = loss.detach().clone()
+    dist.all_reduce(lt)
+    return lt.item() / world, gw / world
+
+
+def test_llama_zigzag_ring_matches_single():
+    from distributed_pytorch_hpc_amd.models.llama2 import ModelArgs, build_llama
+
+    m = build_llama(ModelArgs(**PRESET), device="cpu", dtype=torch.float32, seed=3)
+    g = torch.Generator().manual_seed(1)
+    t = torch.randint(0, 128, (2, 33), generator=g)
+    loss = m(t[:, :-1], t[:, 1:])
+    loss.backward()
+    outs = run_distributed(_llama_zigzag_worker, 2)
+    for lt, gw in outs:
+        assert abs(lt - loss.item()) < 1e-5
+        assert torch.allclose(gw, m.layers[0].attention.wqkv.weight.grad, atol=1e-5)
