@@ -139,13 +139,11 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, 
       for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.f;
 
   auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[2]) {
-    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt)
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
   };
 
   using I0 = std::integral_constant<int, 0>;
@@ -178,6 +176,16 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, 
     if constexpr (DMA) dma_pair(P0 + S + 4, std::integral_constant<int, (S + 4) & 7>{});
     if constexpr (READ) read_phase(std::integral_constant<int, (S + 1) & 7>{}, afn, bfn);
     mma(afc, bfc);
+    if constexpr (READ) {
+      // interleave the 12 prefetch reads with the 8 MFMAs (2 reads per MFMA) instead of issuing all reads
+      // first: a burst of 12 ds_reads from 8 waves backs up the LDS issue queue and delays the MFMAs
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 DS reads
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
     __builtin_amdgcn_sched_barrier(0);   // keep the next slot's reads out of this slot (register pressure)
   };
   using T_ = std::true_type;
