@@ -77,6 +77,9 @@ def main():
             "C.transpose_x": lambda: xt.copy_(x.t()),
             # D: the framework's CDNA4 weight-gradient kernel on the token-major operands (csrc/gemm.hip)
             "D.wgrad": lambda: torch.ops.dph.gemm_tn_(gw_a, gy, x, False),
+            # E: input gradient through a HIP-transposed weight (parallel/linear.py _dgrad)
+            "E.dgrad": lambda: torch.mm(gy, torch.ops.dph.transpose2d(w).t()),
+            "E.transpose_w": lambda: torch.ops.dph.transpose2d(w),
         }
         for k, fn in cases.items():
             ms = timeit(fn)

@@ -357,6 +357,20 @@ void gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate) {
                accumulate, cur_stream());
 }
 
+// ------------------------------------------------------------------------------------------------ transpose
+Tensor transpose2d(const Tensor& x) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kBFloat16 && x.stride(1) == 1, "transpose2d: bf16 [R, C] rows");
+  TORCH_CHECK(x.stride(0) % 8 == 0, "transpose2d: leading dim must be a multiple of 8");
+  check_align16(x, "x");
+  const int64_t R = x.size(0), C = x.size(1);
+  auto out = at::empty({C, R}, x.options());
+  TORCH_CHECK(R % 8 == 0, "transpose2d: rows must be a multiple of 8 (16-B output rows)");
+  dph::transpose2d(x.data_ptr(), out.data_ptr(), R, C, x.stride(0), R, cur_stream());
+  return out;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dph, m) {
@@ -384,6 +398,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
+  m.def("transpose2d(Tensor x) -> Tensor");
 }
 
 TORCH_LIBRARY_IMPL(dph, CUDA, m) {
@@ -406,4 +421,5 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("gemm_tn_", &gemm_tn_);
+  m.impl("transpose2d", &transpose2d);
 }

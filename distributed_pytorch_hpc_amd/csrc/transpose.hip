@@ -1,0 +1,60 @@
+// 2-D transpose of a row-major bf16 matrix, dst[C, R] = src[R, C]^T, at HBM bandwidth.
+// Used to give hipBLASLt the K-contiguous operand pattern it runs fastest (the input-gradient GEMM
+// dX = dY W reads W^T: profiles/gemm_layout_*.json), where torch's strided copy reaches ~1 TB/s.
+// 64 x 64 tiles through LDS (row pitch 66 elements: 33 dwords, so the column-wise reads of the store phase
+// hit 32 different banks); 16-B vector loads and stores on both global sides.
+#include "dph_common.h"
+#include "kernels.h"
+
+namespace dph {
+
+namespace {
+constexpr int TT = 64, PITCH = 66;
+
+__global__ __launch_bounds__(256) void transpose_k(const bf16* __restrict__ src, bf16* __restrict__ dst, int64_t R,
+                                                   int64_t C, int64_t lds_src, int64_t ld_dst) {
+  __shared__ bf16 tile[TT * PITCH];
+  const int64_t r0 = (int64_t)blockIdx.y * TT, c0 = (int64_t)blockIdx.x * TT;
+  const int t = threadIdx.x;
+  // load: 64 rows x 8 chunks of 8 elements; 2 chunks per thread
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = t + 256 * i, row = idx >> 3, ch = idx & 7;
+    const int64_t gr = r0 + row, gc = c0 + ch * 8;
+    bf16x8 v;
+    if (gr < R && gc + 8 <= C) {
+      v = *reinterpret_cast<const bf16x8*>(src + gr * lds_src + gc);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (gr < R && gc + j < C) ? src[gr * lds_src + gc + j] : (bf16)0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[row * PITCH + ch * 8 + j] = v[j];
+  }
+  __syncthreads();
+  // store: dst row = source column (64 of them) x 8 chunks of 8 source rows
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int idx = t + 256 * i, col = idx >> 3, ch = idx & 7;
+    const int64_t gr = c0 + col, gc = r0 + ch * 8;   // dst coordinates
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = tile[(ch * 8 + j) * PITCH + col];
+    if (gr < C && gc + 8 <= R) {
+      *reinterpret_cast<bf16x8*>(dst + gr * ld_dst + gc) = v;
+    } else if (gr < C) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (gc + j < R) dst[gr * ld_dst + gc + j] = v[j];
+    }
+  }
+}
+}  // namespace
+
+void transpose2d(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_src, int64_t ld_dst, hipStream_t st) {
+  if (R == 0 || C == 0) return;
+  const dim3 grid((unsigned)((C + TT - 1) / TT), (unsigned)((R + TT - 1) / TT));
+  hipLaunchKernelGGL(transpose_k, grid, dim3(256), 0, st, (const bf16*)src, (bf16*)dst, R, C, ld_src, ld_dst);
+}
+
+}  // namespace dph

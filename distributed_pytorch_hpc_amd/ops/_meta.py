@@ -72,6 +72,11 @@ def _sumsq(x, out):
     return None
 
 
+@register_fake("dph::transpose2d")
+def _transpose2d(x):
+    return x.new_empty((x.shape[1], x.shape[0]))
+
+
 @register_fake("dph::gemm_tn_")
 def _gemm_tn(C, A, B, accumulate):
     return None

@@ -38,6 +38,20 @@ def _native_wgrad(out: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor, accumul
     return True
 
 
+def _dgrad(gy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dX = dY W.  hipBLASLt runs this 10-15 % faster with a K-contiguous W^T operand (mm(dY, W^T.t()):
+    profiles/gemm_layout_*.json); the HIP transpose makes that copy at HBM speed (~0.04-0.07 ms for 7B weights)
+    and it is freed right after the GEMM."""
+    if (gy.is_cuda and w.dtype == torch.bfloat16 and gy.dtype == torch.bfloat16 and w.dim() == 2
+            and w.is_contiguous() and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and w.numel() >= (1 << 22)):
+        from ..ops import _lib
+
+        if not _lib.reference_mode():
+            wt = _lib.ops().transpose2d(w)
+            return torch.matmul(gy, wt.t())
+    return torch.matmul(gy, w)
+
+
 def _autocast_dtype(t: torch.Tensor):
     dev = t.device.type
     return torch.get_autocast_dtype(dev) if torch.is_autocast_enabled(dev) else None
@@ -63,7 +77,7 @@ class _LinearFn(torch.autograd.Function):
         gx = gw = gb = None
         g2 = gy.reshape(-1, gy.shape[-1])
         if ctx.needs_input_grad[0]:
-            gx = torch.matmul(gy, w)
+            gx = _dgrad(gy, w)
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             mg = getattr(w, "main_grad", None)

@@ -306,3 +306,9 @@ def test_engine_linear_native_wgrad_matches_autograd(dph_native):
         ref(x).float().pow(2).mean().backward()
     for a, b in zip(m.parameters(), ref.parameters()):
         assert rel_err(a.main_grad, b.grad) < 2e-2
+
+
+@pytest.mark.parametrize("R,C", [(4096, 12288), (64, 72), (200, 136), (32000, 4096)])
+def test_transpose2d(dph_native, R, C):
+    x = torch.randn(R, C, device=DEV, dtype=torch.bfloat16)
+    assert torch.equal(torch.ops.dph.transpose2d(x), x.t().contiguous())
