@@ -1,0 +1,380 @@
+// Fused BatchNorm (training statistics) + optional residual add + ReLU for channels-last (NHWC) activations.
+// Replaces the MIOpen BN kernels (mean/var, norm, dscale/dbias, dx) plus the separate ReLU / residual-add
+// passes of a ResNet block (torchvision-style resnet in scripts/main.py; SimpleUNet conv blocks), which cost more
+// than the convolutions themselves in a bf16 channels-last step (profiles/rocprof_resnet50_*).
+//
+// x is viewed as [M, C] rows (M = N*H*W), C a power of two in [8, 2048] so a 256-thread block tiles rows x
+// 8-channel chunks exactly.  Passes over the activation (A = its size):
+//   forward : stats (read x)  +  apply (read x [+ residual], write y)            = 3A (+A)
+//   backward: reduce (read dy, y, x) + dx (read dy, y, x, write dx [+ dres])      = 7A (+A)
+// Statistics are accumulated with a per-thread shift (the thread's first value) and merged across threads and
+// blocks with Chan's parallel-variance formula, so large-mean channels do not lose the variance to fp32
+// cancellation; all reductions go through fixed-order partial buffers (deterministic).
+#include <algorithm>
+
+#include "dph_common.h"
+#include "kernels.h"
+
+namespace dph {
+
+namespace {
+
+constexpr int BN_NT = 256;
+
+struct Stat {   // count, mean, M2 (sum of squared deviations)
+  float n, mean, m2;
+};
+
+__device__ __forceinline__ Stat chan_merge(Stat a, Stat b) {
+  if (a.n == 0.f) return b;
+  if (b.n == 0.f) return a;
+  const float n = a.n + b.n;
+  const float d = b.mean - a.mean;
+  const float f = b.n / n;
+  return {n, a.mean + d * f, a.m2 + b.m2 + d * d * a.n * f};
+}
+
+// Per-block statistics: block b covers rows [b*rows_per_block, ...).  Partials: mean/m2 [G][C], n [G].
+template <typename T>
+__global__ __launch_bounds__(BN_NT) void bn_stats_k(const T* __restrict__ x, float* __restrict__ pmean,
+                                                    float* __restrict__ pm2, float* __restrict__ pn, int64_t M,
+                                                    int C, int64_t rows_per_block) {
+  extern __shared__ float sh[];   // [3][BN_NT][8]
+  const int ch8 = C / 8, rpi = BN_NT / ch8;
+  const int cc = threadIdx.x % ch8, r0 = threadIdx.x / ch8;
+  const int64_t beg = (int64_t)blockIdx.x * rows_per_block, end = min(M, beg + rows_per_block);
+  float k[8], s[8], ss[8], n = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { k[i] = 0.f; s[i] = 0.f; ss[i] = 0.f; }
+  int64_t r = beg + r0;
+  if (r < end) {
+    Vec8<T>::load(x + r * C + cc * 8, k);   // shift = first value
+    n = 1.f;
+    r += rpi;
+  }
+  for (; r < end; r += rpi) {
+    float v[8];
+    Vec8<T>::load(x + r * C + cc * 8, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float d = v[i] - k[i];
+      s[i] += d;
+      ss[i] = fmaf(d, d, ss[i]);
+    }
+    n += 1.f;
+  }
+  float* shn = sh;
+  float* shm = sh + BN_NT * 8;
+  float* shq = sh + 2 * BN_NT * 8;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float mean_d = n > 0.f ? s[i] / n : 0.f;
+    shn[threadIdx.x * 8 + i] = n;
+    shm[threadIdx.x * 8 + i] = k[i] + mean_d;
+    shq[threadIdx.x * 8 + i] = n > 0.f ? fmaxf(ss[i] - s[i] * mean_d, 0.f) : 0.f;
+  }
+  __syncthreads();
+  if (r0 == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      Stat acc = {shn[threadIdx.x * 8 + i], shm[threadIdx.x * 8 + i], shq[threadIdx.x * 8 + i]};
+      for (int g = 1; g < rpi; ++g) {
+        const int t = g * ch8 + cc;
+        acc = chan_merge(acc, {shn[t * 8 + i], shm[t * 8 + i], shq[t * 8 + i]});
+      }
+      pmean[(int64_t)blockIdx.x * C + cc * 8 + i] = acc.mean;
+      pm2[(int64_t)blockIdx.x * C + cc * 8 + i] = acc.m2;
+    }
+    if (cc == 0) pn[blockIdx.x] = (float)(end > beg ? end - beg : 0);
+  }
+}
+
+// Merge G partials per channel; produce mean / invstd, the apply coefficients and the running-stat update.
+// One block per 8-channel chunk: 32 row-groups of 8 lanes each merge a strided slice of the partials (loads
+// issued 4 at a time so the chain is not one memory latency per partial), then a fixed-order LDS tree.
+constexpr int FIN_GROUPS = BN_NT / 8;
+
+template <typename PT, typename RT>
+__global__ __launch_bounds__(BN_NT) void bn_finalize_k(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                                       const float* __restrict__ pn, int G, int C,
+                                                       const PT* __restrict__ w, const PT* __restrict__ b,
+                                                       RT* __restrict__ rmean, RT* __restrict__ rvar, float momentum,
+                                                       float eps, float* __restrict__ mean_out,
+                                                       float* __restrict__ invstd_out, float* __restrict__ scale,
+                                                       float* __restrict__ shift) {
+  __shared__ float sh[3][BN_NT];
+  const int c = blockIdx.x * 8 + (threadIdx.x & 7), grp = threadIdx.x >> 3;
+  Stat acc = {0.f, 0.f, 0.f};
+  for (int g0 = grp; g0 < G; g0 += 4 * FIN_GROUPS) {
+    Stat st[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int g = g0 + u * FIN_GROUPS;
+      st[u] = g < G ? Stat{pn[g], pmean[(int64_t)g * C + c], pm2[(int64_t)g * C + c]} : Stat{0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = chan_merge(acc, st[u]);
+  }
+  sh[0][threadIdx.x] = acc.n;
+  sh[1][threadIdx.x] = acc.mean;
+  sh[2][threadIdx.x] = acc.m2;
+  __syncthreads();
+  for (int half = FIN_GROUPS / 2; half > 0; half >>= 1) {
+    if (grp < half) {
+      const int o = threadIdx.x + half * 8;
+      acc = chan_merge(acc, {sh[0][o], sh[1][o], sh[2][o]});
+      sh[0][threadIdx.x] = acc.n;
+      sh[1][threadIdx.x] = acc.mean;
+      sh[2][threadIdx.x] = acc.m2;
+    }
+    __syncthreads();
+  }
+  if (grp != 0) return;
+  const float var = acc.n > 0.f ? acc.m2 / acc.n : 0.f;
+  const float inv = rsqrtf(var + eps);
+  mean_out[c] = acc.mean;
+  invstd_out[c] = inv;
+  const float gw = w ? (float)w[c] : 1.f, gb = b ? (float)b[c] : 0.f;
+  scale[c] = gw * inv;
+  shift[c] = gb - acc.mean * gw * inv;
+  if (rmean) {
+    const float unb = acc.n > 1.f ? acc.m2 / (acc.n - 1.f) : var;
+    rmean[c] = (RT)((1.f - momentum) * (float)rmean[c] + momentum * acc.mean);
+    rvar[c] = (RT)((1.f - momentum) * (float)rvar[c] + momentum * unb);
+  }
+}
+
+// y = act(x * scale + shift [+ res])
+template <typename T, bool RES, bool RELU>
+__global__ __launch_bounds__(BN_NT) void bn_apply_k(const T* __restrict__ x, const T* __restrict__ res,
+                                                    const float* __restrict__ scale, const float* __restrict__ shift,
+                                                    T* __restrict__ y, int64_t nvec, int ch8) {
+  for (int64_t v = (int64_t)blockIdx.x * BN_NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * BN_NT) {
+    const int c0 = (int)(v % ch8) * 8;
+    float a[8], rr[8];
+    Vec8<T>::load(x + v * 8, a);
+    if (RES) Vec8<T>::load(res + v * 8, rr);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float t = fmaf(a[i], scale[c0 + i], shift[c0 + i]);
+      if (RES) t += rr[i];
+      a[i] = RELU ? fmaxf(t, 0.f) : t;
+    }
+    Vec8<T>::store(y + v * 8, a);
+  }
+}
+
+// Backward reduction: per channel sum(dz) and sum(dz * xhat), dz = dy * [y > 0 when RELU].
+template <typename T, bool RELU>
+__global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_k(const T* __restrict__ dy, const T* __restrict__ y,
+                                                         const T* __restrict__ x, const float* __restrict__ mean,
+                                                         const float* __restrict__ invstd, float* __restrict__ part,
+                                                         int64_t M, int C, int64_t rows_per_block) {
+  extern __shared__ float sh[];   // [2][BN_NT][8]
+  const int ch8 = C / 8, rpi = BN_NT / ch8;
+  const int cc = threadIdx.x % ch8, r0 = threadIdx.x / ch8;
+  const int64_t beg = (int64_t)blockIdx.x * rows_per_block, end = min(M, beg + rows_per_block);
+  float mu[8], is[8], sd[8], sdx[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mu[i] = mean[cc * 8 + i];
+    is[i] = invstd[cc * 8 + i];
+    sd[i] = 0.f;
+    sdx[i] = 0.f;
+  }
+  for (int64_t r = beg + r0; r < end; r += rpi) {
+    float g[8], xv[8], yv[8];
+    Vec8<T>::load(dy + r * C + cc * 8, g);
+    Vec8<T>::load(x + r * C + cc * 8, xv);
+    if (RELU) Vec8<T>::load(y + r * C + cc * 8, yv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float dz = (!RELU || yv[i] > 0.f) ? g[i] : 0.f;
+      sd[i] += dz;
+      sdx[i] = fmaf(dz, (xv[i] - mu[i]) * is[i], sdx[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sh[threadIdx.x * 8 + i] = sd[i];
+    sh[BN_NT * 8 + threadIdx.x * 8 + i] = sdx[i];
+  }
+  __syncthreads();
+  if (r0 == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float a = 0.f, b = 0.f;
+      for (int gq = 0; gq < rpi; ++gq) {
+        const int t = gq * ch8 + cc;
+        a += sh[t * 8 + i];
+        b += sh[BN_NT * 8 + t * 8 + i];
+      }
+      part[(int64_t)blockIdx.x * 2 * C + cc * 8 + i] = a;
+      part[(int64_t)blockIdx.x * 2 * C + C + cc * 8 + i] = b;
+    }
+  }
+}
+
+// Sum the G partials (same block shape as bn_finalize_k); dgamma = sum(dz xhat), dbeta = sum(dz); dx coefficients.
+template <typename PT>
+__global__ __launch_bounds__(BN_NT) void bn_bwd_finalize_k(const float* __restrict__ part, int G, int C, float count,
+                                                           const PT* __restrict__ w, const float* __restrict__ invstd,
+                                                           PT* __restrict__ dw, PT* __restrict__ db,
+                                                           float* __restrict__ coef) {
+  __shared__ float sh[2][BN_NT];
+  const int c = blockIdx.x * 8 + (threadIdx.x & 7), grp = threadIdx.x >> 3;
+  float a = 0.f, b = 0.f;
+  for (int g0 = grp; g0 < G; g0 += 4 * FIN_GROUPS) {
+    float pa[4], pb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int g = g0 + u * FIN_GROUPS;
+      pa[u] = g < G ? part[(int64_t)g * 2 * C + c] : 0.f;
+      pb[u] = g < G ? part[(int64_t)g * 2 * C + C + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a += pa[u];
+      b += pb[u];
+    }
+  }
+  sh[0][threadIdx.x] = a;
+  sh[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int half = FIN_GROUPS / 2; half > 0; half >>= 1) {
+    if (grp < half) {
+      a += sh[0][threadIdx.x + half * 8];
+      b += sh[1][threadIdx.x + half * 8];
+      sh[0][threadIdx.x] = a;
+      sh[1][threadIdx.x] = b;
+    }
+    __syncthreads();
+  }
+  if (grp != 0) return;
+  if (dw) dw[c] = (PT)b;
+  if (db) db[c] = (PT)a;
+  const float gw = w ? (float)w[c] : 1.f;
+  coef[c] = gw * invstd[c];           // dx = coef * (dz - sum_dz / M - xhat * sum_dzx / M)
+  coef[C + c] = a / count;
+  coef[2 * C + c] = b / count;
+}
+
+template <typename T, bool RELU, bool DRES>
+__global__ __launch_bounds__(BN_NT) void bn_bwd_dx_k(const T* __restrict__ dy, const T* __restrict__ y,
+                                                     const T* __restrict__ x, const float* __restrict__ mean,
+                                                     const float* __restrict__ invstd, const float* __restrict__ coef,
+                                                     T* __restrict__ dx, T* __restrict__ dres, int64_t nvec, int ch8) {
+  const int C = ch8 * 8;
+  for (int64_t v = (int64_t)blockIdx.x * BN_NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * BN_NT) {
+    const int c0 = (int)(v % ch8) * 8;
+    float g[8], xv[8], yv[8], o[8];
+    Vec8<T>::load(dy + v * 8, g);
+    Vec8<T>::load(x + v * 8, xv);
+    if (RELU) Vec8<T>::load(y + v * 8, yv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = c0 + i;
+      const float dz = (!RELU || yv[i] > 0.f) ? g[i] : 0.f;
+      const float xh = (xv[i] - mean[c]) * invstd[c];
+      o[i] = coef[c] * (dz - coef[C + c] - xh * coef[2 * C + c]);
+      g[i] = dz;
+    }
+    Vec8<T>::store(dx + v * 8, o);
+    if (DRES) Vec8<T>::store(dres + v * 8, g);
+  }
+}
+
+int stats_grid(int64_t M, int C, int64_t* rows_per_block) {
+  const int rpi = BN_NT / (C / 8);
+  // ~4 row-iterations per thread minimum, at most 1024 blocks
+  int64_t rpb = std::max<int64_t>((int64_t)rpi * 16, (M + 1023) / 1024);
+  rpb = (rpb + rpi - 1) / rpi * rpi;
+  *rows_per_block = rpb;
+  return (int)((M + rpb - 1) / rpb);
+}
+
+}  // namespace
+
+bool bn_nhwc_supported(int64_t C) { return C >= 8 && C <= 2048 && (C & (C - 1)) == 0; }
+
+int bn_partial_blocks(int64_t M, int64_t C) {
+  int64_t rpb;
+  return stats_grid(M, (int)C, &rpb);
+}
+
+void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const void* b, void* rmean, void* rvar,
+                  float* mean, float* invstd, float* scale, float* shift, float* workspace, int64_t M, int64_t C,
+                  float momentum, float eps, bool relu, int dt, int pdt, int rdt, hipStream_t st) {
+  int64_t rpb;
+  const int G = stats_grid(M, (int)C, &rpb);
+  float* pmean = workspace;
+  float* pm2 = workspace + (int64_t)G * C;
+  float* pn = workspace + 2 * (int64_t)G * C;
+  const size_t shs = 3 * BN_NT * 8 * sizeof(float);
+  DPH_DISPATCH_FLOAT(dt, T, {
+    hipLaunchKernelGGL(bn_stats_k<T>, dim3(G), dim3(BN_NT), shs, st, (const T*)x, pmean, pm2, pn, M, (int)C, rpb);
+  });
+  const dim3 fg((unsigned)(C / 8));
+#define DPH_BN_FIN(PT_, RT_)                                                                                    \
+  hipLaunchKernelGGL((bn_finalize_k<PT_, RT_>), fg, dim3(BN_NT), 0, st, pmean, pm2, pn, G, (int)C, (const PT_*)w, \
+                     (const PT_*)b, (RT_*)rmean, (RT_*)rvar, momentum, eps, mean, invstd, scale, shift)
+  if (pdt == kBF16 && rdt == kBF16) DPH_BN_FIN(bf16, bf16);
+  else if (pdt == kBF16) DPH_BN_FIN(bf16, float);
+  else if (rdt == kBF16) DPH_BN_FIN(float, bf16);
+  else DPH_BN_FIN(float, float);
+#undef DPH_BN_FIN
+  bn_apply(x, res, scale, shift, y, M, C, relu, dt, st);
+}
+
+void bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int64_t M, int64_t C,
+              bool relu, int dt, hipStream_t st) {
+  const int64_t nvec = M * C / 8;
+  const dim3 grid(stream_grid(nvec, BN_NT));
+  DPH_DISPATCH_FLOAT(dt, T, {
+    if (res && relu) hipLaunchKernelGGL((bn_apply_k<T, true, true>), grid, dim3(BN_NT), 0, st, (const T*)x,
+                                        (const T*)res, scale, shift, (T*)y, nvec, (int)(C / 8));
+    else if (res) hipLaunchKernelGGL((bn_apply_k<T, true, false>), grid, dim3(BN_NT), 0, st, (const T*)x,
+                                     (const T*)res, scale, shift, (T*)y, nvec, (int)(C / 8));
+    else if (relu) hipLaunchKernelGGL((bn_apply_k<T, false, true>), grid, dim3(BN_NT), 0, st, (const T*)x,
+                                      (const T*)nullptr, scale, shift, (T*)y, nvec, (int)(C / 8));
+    else hipLaunchKernelGGL((bn_apply_k<T, false, false>), grid, dim3(BN_NT), 0, st, (const T*)x, (const T*)nullptr,
+                            scale, shift, (T*)y, nvec, (int)(C / 8));
+  });
+}
+
+void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
+            void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dt,
+            int pdt, hipStream_t st) {
+  int64_t rpb;
+  const int G = stats_grid(M, (int)C, &rpb);
+  float* part = workspace;                       // [G][2C]
+  float* coef = workspace + 2 * (int64_t)G * C;  // [3C]
+  const size_t shs = 2 * BN_NT * 8 * sizeof(float);
+  DPH_DISPATCH_FLOAT(dt, T, {
+    if (relu) hipLaunchKernelGGL((bn_bwd_reduce_k<T, true>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy, (const T*)y,
+                                 (const T*)x, mean, invstd, part, M, (int)C, rpb);
+    else hipLaunchKernelGGL((bn_bwd_reduce_k<T, false>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy, (const T*)y,
+                            (const T*)x, mean, invstd, part, M, (int)C, rpb);
+  });
+  const dim3 fg((unsigned)(C / 8));
+  if (pdt == kBF16)
+    hipLaunchKernelGGL((bn_bwd_finalize_k<bf16>), fg, dim3(BN_NT), 0, st, part, G, (int)C, (float)M, (const bf16*)w,
+                       invstd, (bf16*)dw, (bf16*)db, coef);
+  else
+    hipLaunchKernelGGL((bn_bwd_finalize_k<float>), fg, dim3(BN_NT), 0, st, part, G, (int)C, (float)M,
+                       (const float*)w, invstd, (float*)dw, (float*)db, coef);
+  const int64_t nvec = M * C / 8;
+  const dim3 grid(stream_grid(nvec, BN_NT));
+#define DPH_BN_DX(R_, D_)                                                                                        \
+  hipLaunchKernelGGL((bn_bwd_dx_k<T, R_, D_>), grid, dim3(BN_NT), 0, st, (const T*)dy, (const T*)y, (const T*)x, \
+                     mean, invstd, coef, (T*)dx, (T*)dres, nvec, (int)(C / 8))
+  DPH_DISPATCH_FLOAT(dt, T, {
+    if (relu && dres) DPH_BN_DX(true, true);
+    else if (relu) DPH_BN_DX(true, false);
+    else if (dres) DPH_BN_DX(false, true);
+    else DPH_BN_DX(false, false);
+  });
+#undef DPH_BN_DX
+}
+
+}  // namespace dph

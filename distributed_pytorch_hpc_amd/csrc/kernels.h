@@ -95,6 +95,20 @@ bool gemm_tn_supported(int64_t M, int64_t N, int64_t K);
 void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
              int64_t ldc, int out_dtype, bool accumulate, hipStream_t stream);
 
+// Fused BatchNorm(train) [+ residual] [+ ReLU] on channels-last [M, C] activations (C power of two, 8..2048).
+// Workspaces (fp32): forward 2*G*C + G, backward 2*G*C + 3*C floats with G = bn_partial_blocks(M, C).
+bool bn_nhwc_supported(int64_t C);
+int bn_partial_blocks(int64_t M, int64_t C);
+void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const void* b, void* rmean, void* rvar,
+                  float* mean, float* invstd, float* scale, float* shift, float* workspace, int64_t M, int64_t C,
+                  float momentum, float eps, bool relu, int dtype, int param_dtype, int running_dtype,
+                  hipStream_t stream);
+void bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int64_t M, int64_t C,
+              bool relu, int dtype, hipStream_t stream);
+void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
+            void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dtype,
+            int param_dtype, hipStream_t stream);
+
 // dst[C, R] = src[R, C]^T (bf16, row-major, leading dims in elements; vector path needs 16-B aligned rows).
 void transpose2d(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_src, int64_t ld_dst,
                  hipStream_t stream);

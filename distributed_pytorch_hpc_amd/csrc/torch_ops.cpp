@@ -371,6 +371,94 @@ Tensor transpose2d(const Tensor& x) {
   return out;
 }
 
+// ------------------------------------------------------------------------------------------------ BatchNorm+act
+// x: channels-last [N, C, H, W] (or contiguous [M, C]); statistics over everything but C.
+int64_t bn_channels(const Tensor& x) {
+  TORCH_CHECK(x.dim() == 4 || x.dim() == 2, "bn_act: [N, C, H, W] channels-last or [M, C] input");
+  if (x.dim() == 4) {
+    TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "bn_act: 4-D input must be channels-last");
+  } else {
+    TORCH_CHECK(x.is_contiguous(), "bn_act: 2-D input must be contiguous");
+  }
+  const int64_t C = x.size(1);
+  TORCH_CHECK(dph::bn_nhwc_supported(C), "bn_act: channels must be a power of two in [8, 2048]");
+  check_align16(x, "x");
+  return C;
+}
+void check_like(const Tensor& a, const Tensor& x, const char* name) {
+  TORCH_CHECK(a.sizes() == x.sizes() && a.scalar_type() == x.scalar_type() && a.strides() == x.strides(),
+              "bn_act: ", name, " must match x (shape, dtype, channels-last layout)");
+}
+
+std::tuple<Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res,
+                                              const c10::optional<Tensor>& w, const c10::optional<Tensor>& b,
+                                              const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
+                                              double momentum, double eps, bool relu) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  const int64_t C = bn_channels(x), M = x.numel() / C;
+  if (res) check_like(*res, x, "residual");
+  TORCH_CHECK(!w || (w->numel() == C && w->is_contiguous()), "bn_act: weight [C]");
+  TORCH_CHECK(!b || (b->numel() == C && b->is_contiguous()), "bn_act: bias [C]");
+  TORCH_CHECK(!w || !b || w->scalar_type() == b->scalar_type(), "bn_act: weight/bias dtype mismatch");
+  TORCH_CHECK((!rmean && !rvar) || (rmean && rvar && rmean->numel() == C && rvar->numel() == C &&
+                                    rmean->scalar_type() == rvar->scalar_type()),
+              "bn_act: running stats [C] (both or none)");
+  auto fopt = x.options().dtype(at::kFloat);
+  auto y = at::empty_like(x);
+  auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
+  auto scale = at::empty({C}, fopt), shift = at::empty({C}, fopt);
+  const int G = dph::bn_partial_blocks(M, C);
+  auto ws = at::empty({2 * (int64_t)G * C + G}, fopt);
+  const int pdt = w ? dt_code(*w) : (b ? dt_code(*b) : dph::kF32);
+  const int rdt = rmean ? dt_code(*rmean) : dph::kF32;
+  dph::bn_fwd_train(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), w ? w->data_ptr() : nullptr,
+                    b ? b->data_ptr() : nullptr, rmean ? rmean->data_ptr() : nullptr,
+                    rvar ? rvar->data_ptr() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                    scale.data_ptr<float>(), shift.data_ptr<float>(), ws.data_ptr<float>(), M, C, (float)momentum,
+                    (float)eps, relu, dt_code(x), pdt, rdt, cur_stream());
+  return {y, mean, invstd};
+}
+
+Tensor bn_act_apply(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& scale, const Tensor& shift,
+                    bool relu) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  const int64_t C = bn_channels(x), M = x.numel() / C;
+  if (res) check_like(*res, x, "residual");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && shift.scalar_type() == at::kFloat && scale.numel() == C &&
+                  shift.numel() == C && scale.is_contiguous() && shift.is_contiguous(),
+              "bn_act_apply: fp32 scale/shift [C]");
+  auto y = at::empty_like(x);
+  dph::bn_apply(x.data_ptr(), res ? res->data_ptr() : nullptr, scale.data_ptr<float>(), shift.data_ptr<float>(),
+                y.data_ptr(), M, C, relu, dt_code(x), cur_stream());
+  return y;
+}
+
+std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Tensor& y, const Tensor& x,
+                                                      const Tensor& mean, const Tensor& invstd,
+                                                      const c10::optional<Tensor>& w, bool relu, bool need_dres,
+                                                      bool need_dwb) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  const int64_t C = bn_channels(x), M = x.numel() / C;
+  check_like(dy, x, "dy");
+  check_like(y, x, "y");
+  auto fopt = x.options().dtype(at::kFloat);
+  auto dx = at::empty_like(x);
+  Tensor dres = need_dres ? at::empty_like(x) : at::empty({0}, x.options());
+  const at::ScalarType pt = w ? w->scalar_type() : at::kFloat;
+  Tensor dw = need_dwb ? at::empty({C}, x.options().dtype(pt)) : at::empty({0}, fopt);
+  Tensor db = need_dwb ? at::empty({C}, x.options().dtype(pt)) : at::empty({0}, fopt);
+  const int G = dph::bn_partial_blocks(M, C);
+  auto ws = at::empty({2 * (int64_t)G * C + 3 * C}, fopt);
+  dph::bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
+              w ? w->data_ptr() : nullptr, dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr,
+              need_dwb ? dw.data_ptr() : nullptr, need_dwb ? db.data_ptr() : nullptr, ws.data_ptr<float>(), M, C, relu,
+              dt_code(x), w ? dt_code(*w) : dph::kF32, cur_stream());
+  return {dx, dres, dw, db};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(dph, m) {
@@ -399,6 +487,11 @@ TORCH_LIBRARY(dph, m) {
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
+  m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
+        "float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor)");
+  m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
+  m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "
+        "bool need_dwb) -> (Tensor, Tensor, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(dph, CUDA, m) {
@@ -422,4 +515,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("gemm_tn_", &gemm_tn_);
   m.impl("transpose2d", &transpose2d);
+  m.impl("bn_act_fwd", &bn_act_fwd);
+  m.impl("bn_act_apply", &bn_act_apply);
+  m.impl("bn_act_bwd", &bn_act_bwd);
 }

@@ -7,7 +7,9 @@ with pretrained=False; scripts/02_fully_sharded_fsdp/resnet_fsdp_training.py:186
 the parameter counts agree (ResNet-50: 25,557,032).
 
 MI355X-first choices: ``channels_last=True`` keeps activations NHWC (MIOpen's implicit-GEMM layout) end to end,
-BN-ReLU pairs are left adjacent for MIOpen fusion, and ``zero_init_residual`` is available (as torchvision).
+every BN -> (+identity) -> ReLU runs as one fused channels-last HIP op (ops.batchnorm.BatchNormAct2d: one stats
+pass + one apply pass forward, the residual's gradient produced by the BN backward), and ``zero_init_residual`` is
+available (as torchvision).  ``BatchNormAct2d`` subclasses ``nn.BatchNorm2d``, so the state-dict keys are unchanged.
 """
 from __future__ import annotations
 
@@ -15,6 +17,8 @@ from typing import Optional, Type, Union
 
 import torch
 from torch import nn
+
+from ..ops.batchnorm import BatchNormAct2d
 
 
 def conv3x3(cin, cout, stride=1):
@@ -31,17 +35,15 @@ class BasicBlock(nn.Module):
     def __init__(self, inplanes, planes, stride=1, downsample=None):
         super().__init__()
         self.conv1 = conv3x3(inplanes, planes, stride)
-        self.bn1 = nn.BatchNorm2d(planes)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BatchNormAct2d(planes)                  # relu(bn1(.))
         self.conv2 = conv3x3(planes, planes)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = BatchNormAct2d(planes)                  # relu(bn2(.) + identity)
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x))
+        return self.bn2(self.conv2(out), idt)
 
 
 class Bottleneck(nn.Module):
@@ -50,20 +52,18 @@ class Bottleneck(nn.Module):
     def __init__(self, inplanes, planes, stride=1, downsample=None):
         super().__init__()
         self.conv1 = conv1x1(inplanes, planes)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = BatchNormAct2d(planes)
         self.conv2 = conv3x3(planes, planes, stride)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = BatchNormAct2d(planes)
         self.conv3 = conv1x1(planes, planes * 4)
-        self.bn3 = nn.BatchNorm2d(planes * 4)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn3 = BatchNormAct2d(planes * 4)              # relu(bn3(.) + identity)
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return self.relu(out + idt)
+        out = self.bn1(self.conv1(x))
+        out = self.bn2(self.conv2(out))
+        return self.bn3(self.conv3(out), idt)
 
 
 class ResNet(nn.Module):
@@ -77,8 +77,7 @@ class ResNet(nn.Module):
         else:
             self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
             self.maxpool = nn.MaxPool2d(3, 2, 1)
-        self.bn1 = nn.BatchNorm2d(64)
-        self.relu = nn.ReLU(inplace=True)
+        self.bn1 = BatchNormAct2d(64)
         self.layer1 = self._make(block, 64, layers[0])
         self.layer2 = self._make(block, 128, layers[1], 2)
         self.layer3 = self._make(block, 256, layers[2], 2)
@@ -102,14 +101,14 @@ class ResNet(nn.Module):
         down = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             down = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
-                                 nn.BatchNorm2d(planes * block.expansion))
+                                 BatchNormAct2d(planes * block.expansion, act=False))
         layers = [block(self.inplanes, planes, stride, down)]
         self.inplanes = planes * block.expansion
         layers += [block(self.inplanes, planes) for _ in range(1, blocks)]
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

@@ -72,6 +72,25 @@ def _sumsq(x, out):
     return None
 
 
+@register_fake("dph::bn_act_fwd")
+def _bn_act_fwd(x, res, w, b, rm, rv, momentum, eps, relu):
+    c = x.shape[1]
+    return torch.empty_like(x), x.new_empty((c,), dtype=torch.float32), x.new_empty((c,), dtype=torch.float32)
+
+
+@register_fake("dph::bn_act_apply")
+def _bn_act_apply(x, res, scale, shift, relu):
+    return torch.empty_like(x)
+
+
+@register_fake("dph::bn_act_bwd")
+def _bn_act_bwd(dy, y, x, mean, invstd, w, relu, need_dres, need_dwb):
+    c = x.shape[1]
+    pdt = w.dtype if w is not None else torch.float32
+    return (torch.empty_like(x), torch.empty_like(x) if need_dres else x.new_empty((0,)),
+            x.new_empty((c,) if need_dwb else (0,), dtype=pdt), x.new_empty((c,) if need_dwb else (0,), dtype=pdt))
+
+
 @register_fake("dph::transpose2d")
 def _transpose2d(x):
     return x.new_empty((x.shape[1], x.shape[0]))

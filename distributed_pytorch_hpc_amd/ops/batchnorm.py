@@ -1,0 +1,99 @@
+"""Fused BatchNorm + residual add + ReLU for channels-last activations (csrc/batchnorm.hip).
+
+``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` (same parameters, buffers and state-dict keys) whose
+``forward(x, residual=None)`` computes ``act(bn(x) + residual)``.  On an MI355X with a channels-last input whose
+channel count is a power of two in [8, 2048] it runs the fused HIP kernels (one statistics pass + one apply pass
+forward; one reduction pass + one dx pass backward, which also emits the residual's gradient); otherwise the
+stock ``F.batch_norm`` + add + ReLU path.  The reference trains torchvision ResNets (scripts/main.py:249,
+resnet_fsdp_training.py:186-191) whose conv -> BN -> ReLU (+ identity) blocks this fuses.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import _lib
+
+
+def _pow2_channels(c: int) -> bool:
+    return 8 <= c <= 2048 and (c & (c - 1)) == 0
+
+
+def _native_ok(x: torch.Tensor, residual) -> bool:
+    if not (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)):
+        return False
+    if not _lib.use_native(x):
+        return False
+    if not (_pow2_channels(x.shape[1]) and x.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    if x.data_ptr() % 16:
+        return False
+    if residual is not None and (residual.shape != x.shape or residual.dtype != x.dtype
+                                 or residual.stride() != x.stride()):
+        return False
+    return True
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
+        y, mean, invstd = _lib.ops().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, momentum, eps,
+                                                relu)
+        ctx.save_for_backward(x, y, mean, invstd, weight)
+        ctx.relu, ctx.has_res = relu, residual is not None
+        ctx.has_wb = weight is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, invstd, weight = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        need_wb = ctx.has_wb and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        dx, dres, dw, db = _lib.ops().bn_act_bwd(dy, y, x, mean, invstd, weight if ctx.has_wb else None, ctx.relu,
+                                                 ctx.has_res, need_wb)
+        return (dx, dw if need_wb else None, db if need_wb else None, None, None, dres if ctx.has_res else None,
+                None, None, None)
+
+
+def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
+                   residual=None, relu: bool = True):
+    """act(batch_norm(x) + residual) with the fused kernels when eligible."""
+    if _native_ok(x, residual):
+        if training:
+            return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, relu)
+        with torch.no_grad():
+            inv = torch.rsqrt(running_var.float() + eps)
+            scale = inv * (weight.float() if weight is not None else 1.0)
+            shift = (bias.float() if bias is not None else 0.0) - running_mean.float() * scale
+        if not torch.is_grad_enabled() or not x.requires_grad:
+            return _lib.ops().bn_act_apply(x, residual, scale.contiguous(), shift.contiguous(), relu)
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``act(BatchNorm2d(x) + residual)``; ``act=False`` gives plain BatchNorm2d (+ residual)."""
+
+    def __init__(self, num_features: int, eps: float = 1e-5, momentum: float = 0.1, affine: bool = True,
+                 track_running_stats: bool = True, act: bool = True, **kw):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats, **kw)
+        self.act = act
+
+    def forward(self, x, residual=None):
+        training = self.training or not self.track_running_stats
+        momentum = self.momentum
+        if self.training and self.track_running_stats:
+            self.num_batches_tracked.add_(1)
+            if momentum is None:   # cumulative moving average, as nn.BatchNorm2d
+                momentum = 1.0 / float(self.num_batches_tracked)
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        if training and rm is not None and not self.training:
+            rm = rv = None
+        return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual, self.act)
+
+    def extra_repr(self):
+        return super().extra_repr() + f", act={'relu' if self.act else 'none'}"

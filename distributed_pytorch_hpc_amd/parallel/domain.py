@@ -113,10 +113,18 @@ class DomainBatchNorm2d(nn.BatchNorm2d):
         super().__init__(bn.num_features, bn.eps, bn.momentum, bn.affine, bn.track_running_stats)
         self.load_state_dict(bn.state_dict())
         self.group = group
+        self.act = getattr(bn, "act", False)   # ops.batchnorm.BatchNormAct2d: act(bn(x) + residual)
 
-    def forward(self, x):
+    def forward(self, x, residual=None):
         if not self.training:
-            return super().forward(x)
+            y = super().forward(x)
+        else:
+            y = self._train_forward(x)
+        if residual is not None:
+            y = y + residual
+        return torch.relu(y) if self.act else y
+
+    def _train_forward(self, x):
         n = torch.tensor(float(x.numel() // x.shape[1]), device=x.device)
         s = all_reduce_sum_partitioned(x.sum((0, 2, 3)), self.group)
         ss = all_reduce_sum_partitioned((x * x).sum((0, 2, 3)), self.group)

@@ -73,3 +73,32 @@ def test_reference_state_dict_conversion():
     assert back.keys() == sd.keys()
     for k in sd:
         assert torch.equal(back[k], sd[k])
+
+
+def test_bn_act_module_cpu_matches_batchnorm():
+    """BatchNormAct2d on CPU == BatchNorm2d (+ residual) (+ ReLU), incl. running stats and eval."""
+    from torch import nn
+    from distributed_pytorch_hpc_amd.ops import BatchNormAct2d
+
+    torch.manual_seed(0)
+    for act in (True, False):
+        fused, ref = BatchNormAct2d(16, act=act), nn.BatchNorm2d(16)
+        with torch.no_grad():
+            fused.weight.normal_(1, 0.3)
+            fused.bias.normal_(0, 0.3)
+        ref.load_state_dict(fused.state_dict())
+        x, r = torch.randn(4, 16, 6, 6), torch.randn(4, 16, 6, 6)
+        want = ref(x) + r
+        want = torch.relu(want) if act else want
+        torch.testing.assert_close(fused(x, r), want)
+        torch.testing.assert_close(fused.running_mean, ref.running_mean)
+        fused.eval(), ref.eval()
+        want = torch.relu(ref(x)) if act else ref(x)
+        torch.testing.assert_close(fused(x), want)
+
+
+def test_resnet_state_dict_keys_torchvision_compatible():
+    keys = set(models.resnet18().state_dict())
+    assert "bn1.running_var" in keys and "layer2.0.downsample.1.weight" in keys
+    assert not any("relu" in k for k in keys)
+    assert len(keys) == 122
