@@ -29,14 +29,29 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributed_pytorch_hpc_amd.runtime import env as rt  # noqa: E402
 
-BUSBW = {"all_reduce": lambda n: 2 * (n - 1) / n, "all_gather": lambda n: (n - 1) / n,
+BUSBW = {"all_reduce": lambda n: 2 * (n - 1) / n, "custom_all_reduce": lambda n: 2 * (n - 1) / n, "all_gather": lambda n: (n - 1) / n,
          "reduce_scatter": lambda n: (n - 1) / n, "all_to_all": lambda n: (n - 1) / n,
          "broadcast": lambda n: 1.0, "send_recv": lambda n: 1.0}
+
+
+_CAR = {}
+
+
+def _custom(world):
+    """XgmiAllReduce over the world group (comm/custom_allreduce.py), created once."""
+    if "car" not in _CAR:
+        from distributed_pytorch_hpc_amd.comm.custom_allreduce import XgmiAllReduce
+
+        _CAR["car"] = XgmiAllReduce(None, max_bytes=int(os.environ.get("CAR_MAX_BYTES", str(64 << 20))),
+                                    max_blocks=int(os.environ.get("CAR_BLOCKS", "64")))
+    return _CAR["car"]
 
 
 def run_op(op, x, out, world, rank, group=None):
     if op == "all_reduce":
         dist.all_reduce(x, group=group)
+    elif op == "custom_all_reduce":   # direct peer reads over xGMI (one-shot / two-shot), in place
+        _custom(world).all_reduce(x)
     elif op == "broadcast":
         dist.broadcast(x, src=0, group=group)
     elif op == "all_gather":
@@ -54,6 +69,12 @@ def run_op(op, x, out, world, rank, group=None):
 def bench_one(op, numel, dtype, device, iters, warmup):
     world, rank = dist.get_world_size(), dist.get_rank()
     numel = max(world, numel // world * world)
+    if op == "custom_all_reduce":
+        if device.type != "cuda":
+            return None
+        numel = max(8, numel // 8 * 8)
+        if numel * torch.empty((), dtype=dtype).element_size() > _custom(world).max_bytes:
+            return None
     x = torch.ones(numel, dtype=dtype, device=device)
     if op == "all_gather":
         out = torch.empty(numel * world, dtype=dtype, device=device)
@@ -104,7 +125,8 @@ def env_header() -> dict:
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("--ops", default="broadcast,all_reduce,all_gather,reduce_scatter,all_to_all,send_recv")
+    ap.add_argument("--ops", default="broadcast,all_reduce,all_gather,reduce_scatter,all_to_all,send_recv",
+                    help="comma list; 'custom_all_reduce' adds the direct-peer-read xGMI all-reduce (GPU only)")
     ap.add_argument("--sizes", default="1e3,1e4,1e5,1e6,1e7,1e8", help="elements per rank (comma list)")
     ap.add_argument("--dtype", default="float32", choices=["float32", "bfloat16"])
     ap.add_argument("--iters", type=int, default=20)
@@ -120,6 +142,8 @@ def main(argv=None):
     for op in args.ops.split(","):
         for s in args.sizes.split(","):
             r = bench_one(op, int(float(s)), dtype, device, args.iters, args.warmup)
+            if r is None:   # custom all-reduce: CPU run or message above its staging buffer
+                continue
             rows.append(r)
             if rank == 0:
                 print(f"{op:15s} {r['bytes'] / 1e6:11.3f} MB  {r['time_us']:11.1f} us  algbw {r['algbw_GBps']:8.2f} GB/s"

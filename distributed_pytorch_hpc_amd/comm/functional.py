@@ -19,6 +19,10 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from .custom_allreduce import custom_allreduce_enabled as _custom_ar_enabled
+from .custom_allreduce import custom_allreduce_max_bytes as _custom_ar_max_bytes
+from .custom_allreduce import get_custom_allreduce as _get_custom_ar
+
 
 def _ws(group) -> int:
     return dist.get_world_size(group) if dist.is_initialized() else 1
@@ -64,7 +68,16 @@ def split_dim(x: torch.Tensor, dim: int, group) -> torch.Tensor:
 
 
 def all_reduce_(x: torch.Tensor, group, op=dist.ReduceOp.SUM) -> torch.Tensor:
+    """In-place all-reduce.  With ``DPH_CUSTOM_ALLREDUCE=1``, SUM messages up to
+    ``DPH_CUSTOM_ALLREDUCE_MAX_BYTES`` on a single-node RCCL group take the direct-peer-read xGMI kernel
+    (comm/custom_allreduce.py); everything else goes to RCCL."""
     if _ws(group) > 1:
+        if op == dist.ReduceOp.SUM and x.is_cuda and _custom_ar_enabled() and \
+                x.numel() * x.element_size() <= _custom_ar_max_bytes():
+            car = _get_custom_ar(group)
+            if car is not None and car.supports(x):
+                car.all_reduce(x)
+                return x
         dist.all_reduce(x, op=op, group=group)
     return x
 

@@ -115,4 +115,14 @@ void transpose2d(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_sr
 
 void cast_copy(const void* src, void* dst, int64_t n, int src_dtype, int dst_dtype, float scale, hipStream_t stream);
 
+// Single-node all-reduce over IPC-mapped peer buffers (csrc/custom_allreduce.hip).  ctx is an opaque handle.
+int64_t car_create(int rank, int world, int64_t max_bytes, double timeout_s);
+void car_ipc_handle(int64_t ctx, void* out64);
+void car_open(int64_t ctx, const void* handles);
+int64_t car_max_bytes(int64_t ctx);
+void car_allreduce(int64_t ctx, const void* in, void* out, int64_t bytes, int dtype, int algo, float scale,
+                   int max_blocks, hipStream_t stream);
+int64_t car_status(int64_t ctx);
+void car_destroy(int64_t ctx);
+
 }  // namespace dph

@@ -459,6 +459,39 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Te
   return {dx, dres, dw, db};
 }
 
+// ------------------------------------------------------------------------------ custom xGMI all-reduce
+int64_t car_create_op(int64_t rank, int64_t world, int64_t max_bytes, double timeout_s) {
+  return dph::car_create((int)rank, (int)world, max_bytes, timeout_s);
+}
+Tensor car_ipc_handle_op(int64_t ctx) {
+  auto h = at::zeros({64}, at::TensorOptions().dtype(at::kByte));
+  dph::car_ipc_handle(ctx, h.data_ptr());
+  return h;
+}
+void car_open_op(int64_t ctx, const Tensor& handles) {
+  TORCH_CHECK(!handles.is_cuda() && handles.scalar_type() == at::kByte && handles.dim() == 2 &&
+                  handles.size(1) == 64 && handles.is_contiguous(),
+              "car_open: handles must be a contiguous CPU uint8 [world, 64] tensor");
+  dph::car_open(ctx, handles.data_ptr());
+}
+void car_allreduce_op(int64_t ctx, const Tensor& inp, Tensor& out, int64_t algo, double scale, int64_t max_blocks) {
+  check_cuda(inp, "inp");
+  c10::DeviceGuard g(inp.device());
+  TORCH_CHECK(inp.is_contiguous() && out.is_contiguous() && inp.sizes() == out.sizes() &&
+                  inp.scalar_type() == out.scalar_type(),
+              "car_allreduce: contiguous inp/out of equal shape and dtype");
+  check_align16(inp, "inp");
+  check_align16(out, "out");
+  const int64_t bytes = inp.numel() * inp.element_size();
+  TORCH_CHECK(bytes % 16 == 0 && bytes <= dph::car_max_bytes(ctx), "car_allreduce: ", bytes,
+              " B is not a multiple of 16 or exceeds the staging buffer");
+  TORCH_CHECK(algo >= 0 && algo <= 2, "car_allreduce: algo 0 (auto), 1 (one-shot) or 2 (two-shot)");
+  dph::car_allreduce(ctx, inp.data_ptr(), out.data_ptr(), bytes, dt_code(inp), (int)algo, (float)scale,
+                     (int)max_blocks, cur_stream());
+}
+int64_t car_status_op(int64_t ctx) { return dph::car_status(ctx); }
+void car_destroy_op(int64_t ctx) { dph::car_destroy(ctx); }
+
 }  // namespace
 
 TORCH_LIBRARY(dph, m) {
@@ -492,6 +525,13 @@ TORCH_LIBRARY(dph, m) {
   m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "
         "bool need_dwb) -> (Tensor, Tensor, Tensor, Tensor)");
+  // custom all-reduce: resource management ops carry no device tensor, so they get catch-all kernels
+  m.def("car_create(int rank, int world, int max_bytes, float timeout_s) -> int", &car_create_op);
+  m.def("car_ipc_handle(int ctx) -> Tensor", &car_ipc_handle_op);
+  m.def("car_open(int ctx, Tensor handles) -> ()", &car_open_op);
+  m.def("car_status(int ctx) -> int", &car_status_op);
+  m.def("car_destroy(int ctx) -> ()", &car_destroy_op);
+  m.def("car_allreduce(int ctx, Tensor inp, Tensor(a!) out, int algo, float scale, int max_blocks) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(dph, CUDA, m) {
@@ -518,4 +558,5 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("bn_act_fwd", &bn_act_fwd);
   m.impl("bn_act_apply", &bn_act_apply);
   m.impl("bn_act_bwd", &bn_act_bwd);
+  m.impl("car_allreduce", &car_allreduce_op);
 }
