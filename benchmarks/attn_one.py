@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Run the flash-attention kernels on one Llama-2-7B shape a few times (for rocprofv3 counter collection)
+and print their TFLOP/s."""
+import argparse
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_pytorch_hpc_amd import ops  # noqa: E402
+from distributed_pytorch_hpc_amd.ops import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--b", type=int, default=8)
+    ap.add_argument("--s", type=int, default=4096)
+    ap.add_argument("--h", type=int, default=32)
+    ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--which", default="fwd,bwd")
+    ap.add_argument("--noncausal", action="store_true")
+    a = ap.parse_args()
+    _lib.require()
+    causal = not a.noncausal
+    q, k, v = (torch.randn(a.b, a.s, a.h, a.d, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    do = torch.randn_like(q)
+    scale = 1 / math.sqrt(a.d)
+    o, lse = ops.flash_fwd(q, k, v, scale, causal)
+    flops = 4 * a.b * a.h * a.s * a.s * a.d * (0.5 if causal else 1.0)
+    for which in a.which.split(","):
+        fn = (lambda: ops.flash_fwd(q, k, v, scale, causal)) if which == "fwd" else \
+            (lambda: _lib.ops().flash_attn_bwd(do, q, k, v, o, lse, scale, causal))
+        fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / a.iters
+        f = flops * (2.5 if which == "bwd" else 1.0)
+        print(f"{which}: {ms:.3f} ms  {f / ms / 1e9:.1f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

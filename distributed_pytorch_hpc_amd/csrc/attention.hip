@@ -165,6 +165,19 @@ struct KVTilePlan {
   }
 };
 
+// Logical (x, y, z) of a workgroup launched on a 1-D grid of nx*ny*nz blocks.  The hardware deals block ids
+// round-robin over the 8 XCDs (ids congruent mod 8 share one L2), so XCD k is given the contiguous logical range
+// [k*n/8, (k+1)*n/8) with x fastest: the workgroups of one (batch, head) -- which all stream the same K/V (or
+// Q/dO) -- run on one XCD and share its L2 instead of every XCD fetching every head (bijective for any n).
+__device__ __forceinline__ void xcd_block(int nx, int ny, int& x, int& y, int& z, int n) {
+  const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
+  const int base = n >> 3, rem = n & 7;
+  const int logical = xcd * base + min(xcd, rem) + slot;
+  x = logical % nx;
+  y = (logical / nx) % ny;
+  z = logical / (nx * ny);
+}
+
 // Number of 64-key tiles a 32-query wave (first query q0w) must visit: causal waves stop at their last
 // visible key; the workgroup still loops to its own end for the shared staging / barriers.
 template <bool CAUSAL>
@@ -191,8 +204,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int nqb = (p.Sq + BM - 1) / BM;
-  const int qb = CAUSAL ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;  // heaviest causal blocks first
-  const int hq = blockIdx.y, b = blockIdx.z;
+  int bx, hq, b;
+  xcd_block(nqb, p.Hq, bx, hq, b, nqb * p.Hq * p.B);
+  const int qb = CAUSAL ? nqb - 1 - bx : bx;  // heaviest causal blocks first
   const int hk = hq / (p.Hq / p.Hkv);
   const int q0 = qb * BM, q0w = q0 + wid * 32;
   const int myq = q0w + l32;
@@ -373,8 +387,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
   const AttnParams& p = P.f;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
-  const int kb0 = blockIdx.x * BNK;
-  const int hk = blockIdx.y, b = blockIdx.z;
+  const int nkb = (p.Sk + BNK - 1) / BNK;
+  int kbx, hk, b;
+  xcd_block(nkb, p.Hkv, kbx, hk, b, nkb * p.Hkv * p.B);
+  const int kb0 = kbx * BNK;   // ascending = heaviest causal key blocks first
   const int grp = p.Hq / p.Hkv;
   const int off = p.Sk - p.Sq;
   const int key0 = kb0 + wid * 32;
@@ -536,8 +552,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
   const AttnParams& p = P.f;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
   const int nqb = (p.Sq + BM - 1) / BM;
-  const int qb = CAUSAL ? nqb - 1 - (int)blockIdx.x : (int)blockIdx.x;
-  const int hq = blockIdx.y, b = blockIdx.z;
+  int bx, hq, b;
+  xcd_block(nqb, p.Hq, bx, hq, b, nqb * p.Hq * p.B);
+  const int qb = CAUSAL ? nqb - 1 - bx : bx;
   const int hk = hq / (p.Hq / p.Hkv);
   const int q0 = qb * BM, q0w = q0 + wid * 32;
   const int myq = q0w + l32;
@@ -643,7 +660,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
 // ==================================================================================================
 template <int HD>
 static void fwd_launch(const AttnParams& p, hipStream_t st) {
-  const dim3 grid((p.Sq + 127) / 128, p.Hq, p.B);
+  const dim3 grid((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));   // 1-D: xcd_block() maps it
   const size_t lds = 2 * 2 * 64 * HD * 2;
   if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true>), grid, dim3(256), lds, st, p);
   else hipLaunchKernelGGL((attn_fwd_k<HD, false>), grid, dim3(256), lds, st, p);
@@ -663,11 +680,11 @@ template <int HD>
 static void bwd_launch(const AttnBwdParams& P, hipStream_t st) {
   const AttnParams& p = P.f;
   const size_t lds_kv = 128 * HD * 2 + 4 * 32 * HD * 2 + 4 * 32 * 4;
-  const dim3 grid_kv((p.Sk + 127) / 128, p.Hkv, p.B);
+  const dim3 grid_kv((unsigned)((p.Sk + 127) / 128 * p.Hkv * p.B));
   if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true>), grid_kv, dim3(256), lds_kv, st, P);
   else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false>), grid_kv, dim3(256), lds_kv, st, P);
   const size_t lds_q = 2 * 2 * 64 * HD * 2;
-  const dim3 grid_q((p.Sq + 127) / 128, p.Hq, p.B);
+  const dim3 grid_q((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
   if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true>), grid_q, dim3(256), lds_q, st, P);
   else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false>), grid_q, dim3(256), lds_q, st, P);
 }
