@@ -86,8 +86,8 @@ void flash_attn_bwd(const AttnBwdParams& p, hipStream_t stream);
 // ---- Embedding gather / scatter-add backward (vocab-sharded friendly: out-of-range ids -> zero row) ----
 void embedding_fwd(const int64_t* ids, const void* table, void* out, int64_t n, int64_t dim, int64_t vocab_start,
                    int64_t vocab_local, int dtype, hipStream_t stream);
-void embedding_bwd(const int64_t* ids, const void* dout, float* dtable_f32, int64_t n, int64_t dim,
-                   int64_t vocab_start, int64_t vocab_local, int dtype, hipStream_t stream);
+void embedding_bwd(const int64_t* sorted_ids, const int64_t* perm, const void* dout, float* dtable_f32, int64_t n,
+                   int64_t dim, int64_t vocab_start, int64_t vocab_local, int dtype, hipStream_t stream);
 
 // ---- cast / scale helpers ----
 // C[M, N] (+)= A^T B, A [K, M] / B [K, N] bf16 row-major (weight gradient); C bf16 or fp32.
@@ -114,6 +114,13 @@ void transpose2d(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_sr
                  hipStream_t stream);
 
 void cast_copy(const void* src, void* dst, int64_t n, int src_dtype, int dst_dtype, float scale, hipStream_t stream);
+
+// Latitude-weighted MSE over [B, C, H, W] (csrc/latmse.hip).  Forward workspace: latmse_partial_blocks(n) floats.
+int latmse_partial_blocks(int64_t n);
+void latmse_fwd(const void* pred, const void* target, float* partial, float* out, int64_t n, int64_t H, int64_t W,
+                int64_t n_global, int64_t lat_offset, int dtype, hipStream_t stream);
+void latmse_bwd(const void* pred, const void* target, const float* gloss, void* dpred, void* dtarget, int64_t n,
+                int64_t H, int64_t W, int64_t n_global, int64_t lat_offset, int dtype, hipStream_t stream);
 
 // Single-node all-reduce over IPC-mapped peer buffers (csrc/custom_allreduce.hip).  ctx is an opaque handle.
 int64_t car_create(int rank, int world, int64_t max_bytes, double timeout_s);

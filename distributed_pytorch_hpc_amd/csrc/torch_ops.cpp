@@ -332,9 +332,13 @@ Tensor embedding_bwd(const Tensor& ids, const Tensor& dout, int64_t vocab_local,
   c10::DeviceGuard g(dout.device());
   TORCH_CHECK(dout.is_contiguous() && ids.is_contiguous(), "embedding_bwd: contiguous required");
   const int64_t dim = dout.size(-1);
+  TORCH_CHECK(dim % 8 == 0, "embedding_bwd: dim must be a multiple of 8");
+  check_align16(dout, "dout");
   auto dtab = at::zeros({vocab_local, dim}, dout.options().dtype(at::kFloat));
-  dph::embedding_bwd(ids.data_ptr<int64_t>(), dout.data_ptr(), dtab.data_ptr<float>(), ids.numel(), dim, vocab_start,
-                     vocab_local, dt_code(dout), cur_stream());
+  auto sorted = at::sort(ids.reshape({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
+  const Tensor sids = std::get<0>(sorted).contiguous(), perm = std::get<1>(sorted).contiguous();
+  dph::embedding_bwd(sids.data_ptr<int64_t>(), perm.data_ptr<int64_t>(), dout.data_ptr(), dtab.data_ptr<float>(),
+                     ids.numel(), dim, vocab_start, vocab_local, dt_code(dout), cur_stream());
   return dtab;
 }
 
@@ -459,6 +463,43 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Te
   return {dx, dres, dw, db};
 }
 
+// ------------------------------------------------------------------------------ latitude-weighted MSE
+// Row step of the latitude axis in the flat storage order: W (NCHW) or W*C (channels-last).
+int64_t latmse_check(const Tensor& p, const Tensor& t) {
+  check_cuda(p, "pred");
+  TORCH_CHECK(p.dim() == 4 && p.sizes() == t.sizes() && p.strides() == t.strides() &&
+                  p.scalar_type() == t.scalar_type(),
+              "latmse: [B, C, H, W] pred / target of equal shape, layout and dtype");
+  check_align16(p, "pred");
+  check_align16(t, "target");
+  if (p.is_contiguous()) return p.size(3);
+  TORCH_CHECK(p.is_contiguous(at::MemoryFormat::ChannelsLast), "latmse: NCHW- or channels-last-contiguous operands");
+  return p.size(3) * p.size(1);
+}
+Tensor latmse_fwd(const Tensor& p, const Tensor& t, int64_t n_global, int64_t lat_offset) {
+  const int64_t step = latmse_check(p, t);
+  c10::DeviceGuard g(p.device());
+  const int64_t n = p.numel();
+  auto fopt = p.options().dtype(at::kFloat);
+  auto out = at::empty({}, fopt);
+  auto part = at::empty({dph::latmse_partial_blocks(n)}, fopt);
+  dph::latmse_fwd(p.data_ptr(), t.data_ptr(), part.data_ptr<float>(), out.data_ptr<float>(), n, p.size(2), step,
+                  n_global, lat_offset, dt_code(p), cur_stream());
+  return out;
+}
+std::tuple<Tensor, Tensor> latmse_bwd(const Tensor& gloss, const Tensor& p, const Tensor& t, int64_t n_global,
+                                      int64_t lat_offset, bool need_dtarget) {
+  const int64_t step = latmse_check(p, t);
+  c10::DeviceGuard g(p.device());
+  TORCH_CHECK(gloss.is_cuda() && gloss.scalar_type() == at::kFloat && gloss.numel() == 1, "latmse_bwd: fp32 scalar grad");
+  auto dp = at::empty_like(p);
+  Tensor dtg = need_dtarget ? at::empty_like(t) : at::empty({0}, p.options());
+  dph::latmse_bwd(p.data_ptr(), t.data_ptr(), gloss.contiguous().data_ptr<float>(), dp.data_ptr(),
+                  need_dtarget ? dtg.data_ptr() : nullptr, p.numel(), p.size(2), step, n_global, lat_offset,
+                  dt_code(p), cur_stream());
+  return {dp, dtg};
+}
+
 // ------------------------------------------------------------------------------ custom xGMI all-reduce
 int64_t car_create_op(int64_t rank, int64_t world, int64_t max_bytes, double timeout_s) {
   return dph::car_create((int)rank, (int)world, max_bytes, timeout_s);
@@ -525,6 +566,9 @@ TORCH_LIBRARY(dph, m) {
   m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "
         "bool need_dwb) -> (Tensor, Tensor, Tensor, Tensor)");
+  m.def("latmse_fwd(Tensor pred, Tensor target, int n_global, int lat_offset) -> Tensor");
+  m.def("latmse_bwd(Tensor gloss, Tensor pred, Tensor target, int n_global, int lat_offset, bool need_dtarget) -> "
+        "(Tensor, Tensor)");
   // custom all-reduce: resource management ops carry no device tensor, so they get catch-all kernels
   m.def("car_create(int rank, int world, int max_bytes, float timeout_s) -> int", &car_create_op);
   m.def("car_ipc_handle(int ctx) -> Tensor", &car_ipc_handle_op);
@@ -559,4 +603,6 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("bn_act_apply", &bn_act_apply);
   m.impl("bn_act_bwd", &bn_act_bwd);
   m.impl("car_allreduce", &car_allreduce_op);
+  m.impl("latmse_fwd", &latmse_fwd);
+  m.impl("latmse_bwd", &latmse_bwd);
 }

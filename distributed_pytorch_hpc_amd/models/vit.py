@@ -10,18 +10,32 @@ Head counts are taken from the (possibly TP-sharded) projection width, as the re
 from __future__ import annotations
 
 import torch
+import torch.nn.functional as F
 from torch import nn
 
 from .. import ops
 
 
 class PatchEmbed(nn.Module):
+    """Non-overlapping k = s = p patch projection (tensor_parallel_vit.py:82-90) computed as ONE GEMM: patches are
+    disjoint, so the "convolution" is a reshape of the image into [B, N_patches, C*p*p] rows times the flattened
+    [E, C*p*p] kernel -- no im2col, no implicit-GEMM convolution search.  The parameter stays a
+    Conv2d weight so state dicts match the reference."""
+
     def __init__(self, in_channels: int, embed_dim: int, patch_size: int):
         super().__init__()
+        self.patch = patch_size
         self.proj = nn.Conv2d(in_channels, embed_dim, kernel_size=patch_size, stride=patch_size)
 
     def forward(self, x):
-        return self.proj(x).flatten(2).transpose(1, 2)
+        b, c, h, w = x.shape
+        p = self.patch
+        hp, wp = h // p, w // p
+        if h != hp * p or w != wp * p:   # Conv2d drops the remainder rows / columns
+            x = x[:, :, :hp * p, :wp * p]
+        rows = x.reshape(b, c, hp, p, wp, p).permute(0, 2, 4, 1, 3, 5).reshape(b, hp * wp, c * p * p)
+        wt = self.proj.weight.reshape(self.proj.out_channels, c * p * p)
+        return F.linear(rows, wt, self.proj.bias)
 
 
 class Attention(nn.Module):

@@ -131,3 +131,13 @@ def _emb_fwd(ids, table, vocab_start):
 @register_fake("dph::embedding_bwd")
 def _emb_bwd(ids, dout, vocab_local, vocab_start):
     return dout.new_empty((vocab_local, dout.shape[-1]), dtype=torch.float32)
+
+
+@register_fake("dph::latmse_fwd")
+def _latmse_fwd(pred, target, n_global, lat_offset):
+    return pred.new_empty((), dtype=torch.float32)
+
+
+@register_fake("dph::latmse_bwd")
+def _latmse_bwd(gloss, pred, target, n_global, lat_offset, need_dtarget):
+    return torch.empty_like(pred), (torch.empty_like(target) if need_dtarget else pred.new_empty((0,)))

@@ -58,14 +58,38 @@ def latitude_weights(n_lat: int, device=None, dtype=torch.float32) -> torch.Tens
     return w.to(device=device, dtype=dtype)
 
 
+class _LatMseFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, target, n_global, lat_offset):
+        ctx.save_for_backward(pred, target)
+        ctx.n_global, ctx.lat_offset = n_global, lat_offset
+        return _lib.ops().latmse_fwd(pred, target, n_global, lat_offset)
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, target = ctx.saved_tensors
+        need_t = ctx.needs_input_grad[1]
+        dp, dt = _lib.ops().latmse_bwd(g.float().reshape(1), pred, target, ctx.n_global, ctx.lat_offset, need_t)
+        return dp, (dt if need_t else None), None, None
+
+
 def latitude_weighted_mse(pred: torch.Tensor, target: torch.Tensor, n_lat_global: int | None = None,
                           lat_offset: int = 0) -> torch.Tensor:
     """mean over [B, C, H, W] of w[H] * (pred - target)^2.
 
     For a latitude-sharded field (domain parallelism) pass the global latitude count and this shard's first
     row: the weights are the matching slice of the global cos-latitude profile, so the average of the
-    per-shard losses over equal shards is the global loss."""
+    per-shard losses over equal shards is the global loss.  GPU tensors run csrc/latmse.hip (weights computed
+    in-kernel from the row index, one reduction pass, deterministic); CPU tensors the PyTorch expression."""
     n = n_lat_global or pred.shape[-2]
+    if (pred.dim() == 4 and _lib.use_native(pred) and pred.dtype in (torch.bfloat16, torch.float32)
+            and target.dtype == pred.dtype and target.shape == pred.shape):
+        fmt = (torch.channels_last if pred.is_contiguous(memory_format=torch.channels_last)
+               and not pred.is_contiguous() else torch.contiguous_format)
+        p, t = pred.contiguous(memory_format=fmt), target.contiguous(memory_format=fmt)
+        p = p if p.data_ptr() % 16 == 0 else p.clone(memory_format=fmt)
+        t = t if t.data_ptr() % 16 == 0 else t.clone(memory_format=fmt)
+        return _LatMseFn.apply(p, t, int(n), int(lat_offset))
     w = latitude_weights(n, pred.device, torch.float32)[lat_offset:lat_offset + pred.shape[-2]].view(1, 1, -1, 1)
     return (w * (pred.float() - target.float()).pow(2)).mean()
 

@@ -404,3 +404,72 @@ def test_resnet50_fused_bn_training_step(dph_native):
         grads.append(torch.cat([p.grad.flatten() for p in m.parameters()]))
     assert rel_err(logits[0], logits[1]) < 1e-4
     assert rel_err(grads[0], grads[1]) < 5e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 5, 181, 360), (3, 4, 16, 13)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_latitude_weighted_mse(dph_native, shape, dtype, channels_last):
+    from distributed_pytorch_hpc_amd.ops.loss import latitude_weighted_mse, latitude_weights
+
+    torch.manual_seed(0)
+    fmt = torch.channels_last if channels_last else torch.contiguous_format
+    p = torch.randn(shape, device=DEV).to(dtype).to(memory_format=fmt).requires_grad_()
+    t = torch.randn(shape, device=DEV).to(dtype).to(memory_format=fmt).requires_grad_()
+    loss = latitude_weighted_mse(p, t)
+    w = latitude_weights(shape[2], DEV).view(1, 1, -1, 1)
+    pr, tr = p.detach().float().requires_grad_(), t.detach().float().requires_grad_()
+    ref = (w * (pr - tr) ** 2).mean()
+    assert abs(loss.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    loss.backward(torch.tensor(1.7, device=DEV))
+    ref.backward(torch.tensor(1.7, device=DEV))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert rel_err(p.grad, pr.grad) < tol and rel_err(t.grad, tr.grad) < tol
+    # a latitude shard of the global grid: rows [40, 80) of 181
+    ps, ts = p.detach()[:, :, 40:80].contiguous(), t.detach()[:, :, 40:80].contiguous()
+    if shape[2] >= 80:
+        got = latitude_weighted_mse(ps, ts, n_lat_global=shape[2], lat_offset=40)
+        ws = latitude_weights(shape[2], DEV)[40:80].view(1, 1, -1, 1)
+        want = (ws * (ps.float() - ts.float()) ** 2).mean()
+        assert abs(got.item() - want.item()) <= 1e-5 * abs(want.item())
+
+
+@pytest.mark.parametrize("case", ["embedding_bwd", "attention_bwd", "bn_bwd", "xent", "latmse", "gemm_tn"])
+def test_kernels_bitwise_deterministic(dph_native, case):
+    """Run each reduction-bearing kernel twice on identical inputs: outputs must be bit-identical
+    (no atomics-order nondeterminism in any HIP kernel)."""
+    torch.manual_seed(0)
+
+    def run():
+        if case == "embedding_bwd":
+            ids = torch.randint(0, 64, (4096,), device=DEV)
+            dout = torch.randn(4096, 256, device=DEV, dtype=torch.bfloat16)
+            return [torch.ops.dph.embedding_bwd(ids, dout, 64, 0)]
+        if case == "attention_bwd":
+            q, k, v = (torch.randn(2, 512, 4, 128, device=DEV, dtype=torch.bfloat16) for _ in range(3))
+            o, lse = ops.flash_fwd(q, k, v, 0.088, True)
+            do = torch.randn_like(q)
+            return list(torch.ops.dph.flash_attn_bwd(do, q, k, v, o, lse, 0.088, True))
+        if case == "bn_bwd":
+            x = torch.randn(8, 64, 28, 28, device=DEV).to(memory_format=torch.channels_last)
+            w = torch.ones(64, device=DEV)
+            y, mean, inv = torch.ops.dph.bn_act_fwd(x, None, w, None, None, None, 0.1, 1e-5, True)
+            return [y, mean, inv] + list(torch.ops.dph.bn_act_bwd(torch.randn_like(x), y, x, mean, inv, w, True,
+                                                                  False, True))
+        if case == "xent":
+            logits = torch.randn(512, 32000, device=DEV, dtype=torch.bfloat16)
+            return [ops.fused_cross_entropy(logits, torch.randint(0, 32000, (512,), device=DEV)), logits]
+        if case == "latmse":
+            a, b = torch.randn(2, 8, 181, 360, device=DEV), torch.randn(2, 8, 181, 360, device=DEV)
+            return [torch.ops.dph.latmse_fwd(a, b, 181, 0)]
+        a = torch.randn(4096, 512, device=DEV, dtype=torch.bfloat16)
+        b = torch.randn(4096, 256, device=DEV, dtype=torch.bfloat16)
+        c = torch.empty(512, 256, device=DEV, dtype=torch.float32)
+        torch.ops.dph.gemm_tn_(c, a, b, False)
+        return [c]
+
+    first = [t.clone() for t in run()]
+    torch.manual_seed(0)
+    second = run()
+    for x, y in zip(first, second):
+        assert torch.equal(x, y)

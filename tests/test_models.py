@@ -102,3 +102,26 @@ def test_resnet_state_dict_keys_torchvision_compatible():
     assert "bn1.running_var" in keys and "layer2.0.downsample.1.weight" in keys
     assert not any("relu" in k for k in keys)
     assert len(keys) == 122
+
+
+def test_vit_patch_embed_gemm_matches_conv():
+    from distributed_pytorch_hpc_amd.models.vit import PatchEmbed
+
+    torch.manual_seed(0)
+    m = PatchEmbed(65, 64, 8)
+    for shape in [(2, 65, 64, 128), (1, 65, 67, 130)]:
+        x = torch.randn(shape)
+        torch.testing.assert_close(m(x), m.proj(x).flatten(2).transpose(1, 2), rtol=1e-5, atol=1e-5)
+
+
+def test_latitude_weighted_mse_cpu_reference():
+    from distributed_pytorch_hpc_amd.ops.loss import latitude_weighted_mse, latitude_weights
+
+    p, t = torch.randn(2, 3, 181, 36), torch.randn(2, 3, 181, 36)
+    w = latitude_weights(181).view(1, 1, -1, 1)
+    torch.testing.assert_close(latitude_weighted_mse(p, t), (w * (p - t) ** 2).mean())
+    # equal latitude shards average to the global loss
+    parts = [latitude_weighted_mse(p[:, :, i:i + 60], t[:, :, i:i + 60], 180, i) for i in (0, 60, 120)]
+    pg, tg = p[:, :, :180], t[:, :, :180]
+    wg = latitude_weights(180).view(1, 1, -1, 1)
+    torch.testing.assert_close(sum(parts) / 3, (wg * (pg - tg) ** 2).mean())
