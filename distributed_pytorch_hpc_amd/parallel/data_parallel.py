@@ -17,9 +17,9 @@ resnet_fsdp_training.py:193-212).  The design here is MI355X-first rather than a
     reduce-scatter reach their plateau bus bandwidth well below that, and a 7B model still gets ~50
     buckets to pipeline against the backward pass (benchmarks/comm_bench.py measures the curve).
   * The optimizer (fused AdamW / SGD kernels, csrc/optim.hip) runs per bucket on the rank's shard:
-    wait(reduce-scatter_b) -> adamw(shard_b) -> all-gather_b (async).  The next forward only waits for
-    the all-gather of the bucket a module actually needs (forward pre-hook), so parameter all-gathers
-    overlap the next step's forward.
+    wait(reduce-scatter_b) -> adamw(shard_b) -> all-gather_b (async), buckets taken in forward order.  The next
+    forward only waits for the all-gather of the bucket a module actually needs (forward pre-hook), so parameter
+    all-gathers overlap the next step's forward.
   * 1/world averaging and optional global-norm clipping are folded into the optimizer kernel through a
     device scalar: no extra pass, no host sync.
 """
@@ -326,7 +326,11 @@ class DataParallelEngine:
         native = _lib.use_native(self.master)
         b1, b2 = cfg.betas
         bc1, bc2 = 1 - b1 ** self.step_count, 1 - b2 ** self.step_count
-        for b in self.buckets:
+        # Sharded: update and re-gather in FORWARD order (buckets are laid out in backward order).  RCCL runs the
+        # all-gathers in issue order, so the first layers' parameters arrive first and the next forward waits
+        # for one bucket's all-gather instead of the whole chain.
+        order = list(reversed(self.buckets)) if self.shard else self.buckets
+        for b in order:
             self._wait_reduce(b)
             master = self.master_view(b)
             grad = self.grad_shard_view(b)
