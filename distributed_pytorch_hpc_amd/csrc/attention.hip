@@ -19,6 +19,8 @@
 //   dQ^T += K^T dS^T with dS^T consumed from the accumulator.
 // The split costs 2 extra MFMA products (S, dP recomputed) but removes the fp32 dQ atomics that bound a
 // fused kernel at ~1.3 TB/s of atomic traffic (MI355X_MICROARCH.md 'Global float atomics').
+#include <cstdlib>
+
 #include "dph_common.h"
 #include "kernels.h"
 
@@ -102,9 +104,9 @@ __device__ __forceinline__ bf16x8 zero8() {
 // per kernel so the tile loop issues loads with immediate offsets instead of recomputing the XOR swizzle.
 // Row offsets repeat with period KP sub-tiles (32 rows) and tr offsets with period TRP k-steps (16 rows):
 // img_off's line permutation depends on (line & 15) only, so advancing 16 lines is a pure byte offset.
-template <int HD>
+template <int HD, int NT_ = 256>
 struct KVTilePlan {
-  static constexpr int BN = 64, NT = 256, NC = HD / 8, KS = HD / 16, DT = HD / 32, TILE = BN * HD * 2;
+  static constexpr int BN = 64, NT = NT_, NC = HD / 8, KS = HD / 16, DT = HD / 32, TILE = BN * HD * 2;
   static constexpr int KP = NC >= 8 ? 1 : 2;
   static constexpr int TRP = NC >= 16 ? 1 : (NC == 8 ? 2 : 4);
   static constexpr int NS = BN * NC / NT;
@@ -195,10 +197,10 @@ __device__ __forceinline__ int wave_tile_count(int ntiles, int q0w, int off) {
 // tile max exceeds it by more than RESCALE_THR (FA4-style lazy rescaling): p is then bounded by 2^THR,
 // harmless for the bf16 P operand and the fp32 accumulators, and the exact result is recovered by the
 // final 1/l.  The rescale branch is wave-uniform (ballot), so steady-state tiles skip 16*DT multiplies.
-template <int HD, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
-  using Plan = KVTilePlan<HD>;
-  constexpr int BM = 128, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
+template <int HD, bool CAUSAL, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
+  using Plan = KVTilePlan<HD, 64 * NW>;
+  constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
   constexpr float RESCALE_THR = 8.f;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -368,9 +370,9 @@ __global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ o, 
 // of the GQA group x 32-row query tiles (double-buffered Q / dO LDS images, one barrier per tile).
 // S and dP are computed with the key on the lane, so P and dS are directly the B operands of
 // dV^T += dO^T P and dK^T += Q^T dS: no LDS round trip, no atomics.
-template <int HD, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
-  constexpr int NT = 256, BNK = 128, BMQ = 32, NC = HD / 8, KS = HD / 16, DT = HD / 32;
+template <int HD, bool CAUSAL, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams P) {
+  constexpr int NT = 64 * NW, BNK = 32 * NW, BMQ = 32, NC = HD / 8, KS = HD / 16, DT = HD / 32;
   constexpr int QIMG = BMQ * HD * 2;        // Q / dO tile image [32 q][HD]
   constexpr int KIMG = BNK * HD * 2;        // K image [128 keys][HD] (B operand of S = Q K^T)
   // img_off's line permutation repeats every 16 lines.  For NC >= 8, rows r and r + 32 are a multiple of 16
@@ -543,10 +545,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
 // query (lane & 31).  Per 64-key tile: S^T = K Q^T and dP^T = V dO^T (A = K / V rows from LDS, B = Q^T / dO^T
 // fragments in registers), P^T = exp2(S^T c - lse) and dS^T = P^T (dP^T - delta) lane-locally (lse and delta
 // are one scalar per lane), then dQ^T += K^T dS^T with dS^T consumed straight from the accumulator.
-template <int HD, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
-  using Plan = KVTilePlan<HD>;
-  constexpr int BM = 128, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
+template <int HD, bool CAUSAL, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P) {
+  using Plan = KVTilePlan<HD, 64 * NW>;
+  constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const AttnParams& p = P.f;
@@ -658,12 +660,30 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
 }
 
 // ==================================================================================================
+// Waves per workgroup (4 or 8; DPH_ATTN_WAVES overrides, for A/B runs).  8 waves = 256 query rows (or keys) share
+// every staged K/V (or Q/dO) tile: half the LDS fill traffic per MFMA of 4 waves, one workgroup per CU.
+static int attn_waves(int fallback) {
+  static const int w = [] {
+    const char* e = getenv("DPH_ATTN_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  return (w == 4 || w == 8) ? w : fallback;
+}
+
+template <int HD, int NW>
+static void fwd_launch_nw(const AttnParams& p, hipStream_t st) {
+  const dim3 grid((unsigned)((p.Sq + 32 * NW - 1) / (32 * NW) * p.Hq * p.B));   // 1-D: xcd_block() maps it
+  const size_t lds = 2 * 2 * 64 * HD * 2;
+  if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, NW>), grid, dim3(64 * NW), lds, st, p);
+  else hipLaunchKernelGGL((attn_fwd_k<HD, false, NW>), grid, dim3(64 * NW), lds, st, p);
+}
+
 template <int HD>
 static void fwd_launch(const AttnParams& p, hipStream_t st) {
-  const dim3 grid((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));   // 1-D: xcd_block() maps it
-  const size_t lds = 2 * 2 * 64 * HD * 2;
-  if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true>), grid, dim3(256), lds, st, p);
-  else hipLaunchKernelGGL((attn_fwd_k<HD, false>), grid, dim3(256), lds, st, p);
+  if constexpr (HD >= 64) {   // a 64-key tile of HD = 32 has fewer 16-B chunks than 8 waves have lanes
+    if (attn_waves(4) == 8) return fwd_launch_nw<HD, 8>(p, st);
+  }
+  fwd_launch_nw<HD, 4>(p, st);
 }
 
 void flash_attn_fwd(const AttnParams& p, hipStream_t st) {
@@ -676,17 +696,26 @@ void flash_attn_fwd(const AttnParams& p, hipStream_t st) {
   }
 }
 
+template <int HD, int NW>
+static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
+  const AttnParams& p = P.f;
+  constexpr int BNK = 32 * NW;
+  const size_t lds_kv = BNK * HD * 2 + 4 * 32 * HD * 2 + 4 * 32 * 4;
+  const dim3 grid_kv((unsigned)((p.Sk + BNK - 1) / BNK * p.Hkv * p.B));
+  if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, NW>), grid_kv, dim3(64 * NW), lds_kv, st, P);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, NW>), grid_kv, dim3(64 * NW), lds_kv, st, P);
+  const size_t lds_q = 2 * 2 * 64 * HD * 2;
+  const dim3 grid_q((unsigned)((p.Sq + 32 * NW - 1) / (32 * NW) * p.Hq * p.B));
+  if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW>), grid_q, dim3(64 * NW), lds_q, st, P);
+  else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW>), grid_q, dim3(64 * NW), lds_q, st, P);
+}
+
 template <int HD>
 static void bwd_launch(const AttnBwdParams& P, hipStream_t st) {
-  const AttnParams& p = P.f;
-  const size_t lds_kv = 128 * HD * 2 + 4 * 32 * HD * 2 + 4 * 32 * 4;
-  const dim3 grid_kv((unsigned)((p.Sk + 127) / 128 * p.Hkv * p.B));
-  if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true>), grid_kv, dim3(256), lds_kv, st, P);
-  else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false>), grid_kv, dim3(256), lds_kv, st, P);
-  const size_t lds_q = 2 * 2 * 64 * HD * 2;
-  const dim3 grid_q((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
-  if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true>), grid_q, dim3(256), lds_q, st, P);
-  else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false>), grid_q, dim3(256), lds_q, st, P);
+  if constexpr (HD >= 64) {
+    if (attn_waves(4) == 8) return bwd_launch_nw<HD, 8>(P, st);
+  }
+  bwd_launch_nw<HD, 4>(P, st);
 }
 
 void flash_attn_bwd(const AttnBwdParams& P, hipStream_t st) {
