@@ -174,8 +174,8 @@ class TransformerBlock(nn.Module):
         if delta is None:
             r, a = x, self.attention_norm(x)
         else:
-            r, a = ops.add_rms_norm(x, delta, self.attention_norm.weight, self.attention_norm.eps)
-        h, f = ops.add_rms_norm(r, self.attention(a), self.ffn_norm.weight, self.ffn_norm.eps)
+            r, a = self.attention_norm(x, delta)
+        h, f = self.ffn_norm(r, self.attention(a))
         return h, self.feed_forward(f)
 
 
@@ -216,7 +216,7 @@ class Transformer(nn.Module):
         if delta is None:
             x = self.norm(h)
         else:
-            _, x = ops.add_rms_norm(h, delta, self.norm.weight, self.norm.eps)
+            _, x = self.norm(h, delta)
         logits = self.output(x)
         if self.loss_parallel and self.tp_group is not None:
             # vocab-sharded logits [B, S, V/tp] ("loss parallel", no [B, S, V] all-gather)

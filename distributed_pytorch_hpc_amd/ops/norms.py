@@ -87,8 +87,13 @@ class RMSNorm(nn.Module):
         self.eps = eps
         self.weight = nn.Parameter(torch.ones(dim))
 
-    def forward(self, x):
-        return rms_norm(x, self.weight, self.eps)
+    def forward(self, x, residual: "torch.Tensor | None" = None):
+        """``norm(x)``; with ``residual`` the fused pre-norm step ``(x + residual, norm(x + residual))``.
+        Models call the module (not the functional op on ``.weight``) so parameter-gathering forward
+        pre-hooks (sharded data parallel, FSDP units) see every use of the weight."""
+        if residual is None:
+            return rms_norm(x, self.weight, self.eps)
+        return add_rms_norm(x, residual, self.weight, self.eps)
 
     def reset_parameters(self):
         nn.init.ones_(self.weight)

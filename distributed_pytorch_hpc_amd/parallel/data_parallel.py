@@ -365,7 +365,13 @@ class DataParallelEngine:
             self._gscale.fill_(1.0 / self.world)
 
     def _wait_ag(self, ids, module=None, args=None):
-        for i in ids:
+        # Wait for the module's buckets AND every bucket before them in forward order (higher index): the
+        # all-gathers were issued in that order, so on RCCL this costs nothing extra, and a parameter that some
+        # earlier module reads functionally (outside its own forward) is covered as well.
+        ids = list(ids)
+        if not ids:
+            return
+        for i in range(len(self.buckets) - 1, min(ids) - 1, -1):
             b = self.buckets[i]
             if b.ag_work is not None:
                 b.ag_work.wait()

@@ -272,12 +272,10 @@ class LlamaStage(nn.Module):
         for layer in self.layers:
             h, delta = layer(h, delta)
         if self.last:
-            from .. import ops
-
             if delta is None:
                 y = self.norm(h)
             else:
-                _, y = ops.add_rms_norm(h, delta, self.norm.weight, self.norm.eps)
+                _, y = self.norm(h, delta)
             return self.output(y)
         return h if delta is None else h + delta
 
