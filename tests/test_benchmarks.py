@@ -1,0 +1,56 @@
+"""Communication microbenchmarks run end-to-end on gloo (the reference runs its tests/*.py by hand under PBS:
+SURVEY.md T-bench / T-ar / T-sr / T-p2p).  Tiny sizes; checks the JSON/log outputs they produce."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _torchrun(script, nproc, args, cwd):
+    env = dict(os.environ, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1", CUDA_VISIBLE_DEVICES="",
+               HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, script)] + args
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=cwd)
+    assert p.returncode == 0, f"{script} failed:\n{p.stdout[-3000:]}\n{p.stderr[-3000:]}"
+    return p.stdout
+
+
+def test_all_reduce_test_gloo(tmp_path):
+    log = tmp_path / "bench.log"
+    out = _torchrun("benchmarks/all_reduce_test.py", 2, ["--backend", "gloo", "--tensor-sizes", "1000,20000",
+                                                         "--iters", "3", "--log-file", str(log),
+                                                         "--json", str(tmp_path / "ar.json")], str(tmp_path))
+    lines = log.read_text().splitlines()
+    assert len(lines) == 4 and all("GB/s" in ln for ln in lines)          # 2 ops x 2 sizes (sizes honoured)
+    rows = json.loads((tmp_path / "ar.json").read_text())["rows"]
+    assert {r["numel"] for r in rows} == {1000, 20000}
+    assert all(r["busbw_GBps"] > 0 for r in rows)
+    assert '"benchmark": "all_reduce_test"' in out
+
+
+def test_comm_bench_gloo(tmp_path):
+    _torchrun("benchmarks/comm_bench.py", 2, ["--backend", "gloo", "--sizes", "1e3,1e4", "--iters", "2",
+                                              "--warmup", "1", "--json", str(tmp_path / "c.json"),
+                                              "--csv", str(tmp_path / "c.csv")], str(tmp_path))
+    res = json.loads((tmp_path / "c.json").read_text())["results"]
+    ops = {r["op"] for r in res}
+    assert {"broadcast", "all_reduce", "all_gather", "reduce_scatter", "all_to_all", "send_recv"} <= ops
+    assert (tmp_path / "c.csv").read_text().startswith("#")
+
+
+def test_send_recv_smoke_gloo(tmp_path):
+    _torchrun("benchmarks/send_recv_test.py", 3, ["--backend", "gloo", "--smoke", "--numel", "1000", "--iters", "2",
+                                                  "--json", str(tmp_path / "s.json")], str(tmp_path))
+    res = json.loads((tmp_path / "s.json").read_text())
+    assert res["smoke"] == "ok" and res["world"] == 3 and res["fanout_s"] > 0

@@ -25,6 +25,7 @@ CASES = [
     ("03_tensor_parallel_tp/device_mesh_basics.py", 4, []),
     ("03_tensor_parallel_tp/basic_tensor_parallel.py", 2, ["--iters", "3"]),
     ("03_tensor_parallel_tp/tensor_parallel_toy.py", 4, ["--dp", "2", "--iters", "3"]),
+    ("03_tensor_parallel_tp/tensor_parallel_2d.py", 4, ["--iters", "3", "--dim", "64", "--tokens", "64"]),
     ("03_tensor_parallel_tp/tensor_parallel_vit.py", 2, ["--tp", "2", "--steps-per-epoch", "2", "--epochs", "1",
                                                          "--channels", "3", "--depth", "2"]),
     ("04_pipeline_parallel_pp/manual_model_split.py", 2, ["--train", "--steps", "2"]),
