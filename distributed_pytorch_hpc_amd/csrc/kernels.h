@@ -92,6 +92,10 @@ void embedding_bwd(const int64_t* sorted_ids, const int64_t* perm, const void* d
 // ---- cast / scale helpers ----
 // C[M, N] (+)= A^T B, A [K, M] / B [K, N] bf16 row-major (weight gradient); C bf16 or fp32.
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K);
+// MFMA shape of the wgrad kernel: 16 (v_mfma_f32_16x16x32_bf16) or 32 (v_mfma_f32_32x32x16_bf16); env DPH_WGRAD_MFMA
+constexpr int kGemmTnDefaultMfma = 32;
+int gemm_tn_mfma();
+void gemm_tn_set_mfma(int shape);
 void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
              int64_t ldc, int out_dtype, bool accumulate, hipStream_t stream);
 

@@ -361,6 +361,12 @@ void gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate) {
                accumulate, cur_stream());
 }
 
+// Select the wgrad kernel's MFMA shape (16 or 32; anything else re-reads DPH_WGRAD_MFMA); returns the active shape.
+int64_t gemm_tn_mfma_(int64_t shape) {
+  if (shape != -1) dph::gemm_tn_set_mfma((int)shape);
+  return dph::gemm_tn_mfma();
+}
+
 // ------------------------------------------------------------------------------------------------ transpose
 Tensor transpose2d(const Tensor& x) {
   check_cuda(x, "x");
@@ -560,6 +566,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
+  m.def("gemm_tn_mfma_(int shape) -> int", &gemm_tn_mfma_);   // no tensor argument: catch-all kernel
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
         "float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor)");

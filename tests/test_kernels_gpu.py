@@ -263,15 +263,22 @@ def test_embedding(dph_native):
 
 @pytest.mark.parametrize("K,M,N,out_dtype,accumulate",
                          [(512, 256, 256, torch.float32, False), (1024, 512, 768, torch.bfloat16, False),
-                          (2048, 768, 512, torch.bfloat16, True), (64, 256, 512, torch.float32, True)])
-def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate):
-    """C (+)= A^T B with token-major A [K, M], B [K, N] (weight gradient dW = dY^T X)."""
+                          (2048, 768, 512, torch.bfloat16, True), (64, 256, 512, torch.float32, True),
+                          (192, 256, 256, torch.float32, False), (128, 512, 256, torch.float32, True)])
+@pytest.mark.parametrize("mfma", [16, 32])
+def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate, mfma):
+    """C (+)= A^T B with token-major A [K, M], B [K, N] (weight gradient dW = dY^T X), both MFMA-shape kernels
+    (K = 64 / 128 / 192 exercise the one- and two-K-step tails of the pipeline)."""
+    torch.ops.dph.gemm_tn_mfma_(mfma)
     torch.manual_seed(0)
     a = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
     b = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
     c0 = torch.randn(M, N, device=DEV, dtype=out_dtype)
     c = c0.clone()
-    torch.ops.dph.gemm_tn_(c, a, b, accumulate)
+    try:
+        torch.ops.dph.gemm_tn_(c, a, b, accumulate)
+    finally:
+        torch.ops.dph.gemm_tn_mfma_(0)   # back to the default / DPH_WGRAD_MFMA
     ref = a.float().t() @ b.float() + (c0.float() if accumulate else 0)
     assert rel_err(c, ref) < (1e-5 if out_dtype == torch.float32 else 8e-3)
 
