@@ -38,7 +38,8 @@ def parse(argv=None):
                     help="sequences per GPU per step (8 x 4096 tokens: ~249 GB peak on one 288 GB MI355X)")
     ap.add_argument("--parallel", choices=["auto", "fsdp", "ddp"], default="auto",
                     help="auto: single-GPU engine for N=1, FSDP (sharded optimizer) for N>1")
-    ap.add_argument("--bucket-mb", type=float, default=256.0)
+    ap.add_argument("--bucket-mb", default="256",
+                    help="gradient bucket size in MiB, or 'auto' (alpha-beta fit of comm/cost_model.py, $DPH_COMM_FIT)")
     ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--lr", type=float, default=3e-4)
     ap.add_argument("--kernels", choices=["dph", "aten"], default="dph",
@@ -93,7 +94,7 @@ def main(argv=None):
         model, shard=(mode == "fsdp"),
         mixed_precision=MixedPrecision(param_dtype=torch.bfloat16,
                                        reduce_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32),
-        bucket_cap_mb=args.bucket_mb)
+        bucket_cap_mb=args.bucket_mb if args.bucket_mb == "auto" else float(args.bucket_mb))
     engine.configure_optimizer(OptimConfig(name="adamw", lr=args.lr, betas=(0.9, 0.95), weight_decay=0.1))
 
     B, S = args.micro_batch, args.seq_len
@@ -160,7 +161,7 @@ def main(argv=None):
                 "micro_batch_per_gpu": B,
                 "tokens_per_step": world * B * S,
                 "kernels": args.kernels,
-                "bucket_mb": args.bucket_mb,
+                "bucket_mb": round(engine.bucket_cap_mb, 1),
                 "activation_checkpoint_every": ac_every,
             },
             "tokens_per_sec_per_gpu": round(tps / world, 2),

@@ -102,7 +102,8 @@ def bench_one(op, numel, dtype, device, iters, warmup):
     tt = torch.tensor([t], dtype=torch.float64, device=device)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     t = tt.item()
-    nbytes = numel * x.element_size()
+    # message size as in rccl-tests: all-gather counts the gathered output, every other op its input
+    nbytes = numel * x.element_size() * (world if op == "all_gather" else 1)
     algbw = nbytes / t / 1e9
     return {"op": op, "numel": numel, "bytes": nbytes, "dtype": str(dtype).replace("torch.", ""), "world": world,
             "time_us": t * 1e6, "algbw_GBps": algbw, "busbw_GBps": algbw * BUSBW[op](world)}
@@ -134,6 +135,9 @@ def main(argv=None):
     ap.add_argument("--backend", default=None)
     ap.add_argument("--csv", default=None)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--fit", default=None,
+                    help="write per-op alpha-beta fits (comm/cost_model.py) here; DPH_COMM_FIT=<file> makes the "
+                         "data-parallel engine size its buckets from them (bucket_cap_mb='auto')")
     args = ap.parse_args(argv)
     rank, world, local = rt.init_distributed(backend=args.backend, verbose=False)
     device = rt.device_for(local, dist.get_backend())
@@ -160,6 +164,19 @@ def main(argv=None):
         if args.json:
             with open(args.json, "w") as fh:
                 json.dump({"env": env_header(), "results": rows}, fh, indent=1)
+        if args.fit:
+            from distributed_pytorch_hpc_amd.comm.cost_model import BUS_FACTOR, fit_alpha_beta, save_fits
+
+            fits = {}
+            for op in {r["op"] for r in rows}:
+                if op not in BUS_FACTOR:
+                    continue
+                samples = [(r["bytes"], r["time_us"] * 1e-6) for r in rows if r["op"] == op]
+                if len(samples) >= 2:
+                    fits[op] = fit_alpha_beta(op, world, samples)
+                    print(f"fit {op:15s} alpha {fits[op].alpha_s * 1e6:9.2f} us  "
+                          f"beta_bus {fits[op].beta_bus_Bps / 1e9:9.2f} GB/s", flush=True)
+            save_fits(fits, args.fit)
     rt.cleanup_distributed()
 
 

@@ -115,6 +115,12 @@ class DataParallelEngine:
         self.is_gloo = dist.is_initialized() and dist.get_backend(process_group) == "gloo"
 
         # ---- bucket assignment (reverse registration order ~ gradient production order) ----
+        if bucket_cap_mb == "auto":   # alpha-beta fit of the collective (comm/cost_model.py, $DPH_COMM_FIT)
+            from ..comm.cost_model import auto_bucket_mb
+
+            grad_bytes = sum(p.numel() for p in params) * torch.empty((), dtype=self.grad_dtype).element_size()
+            bucket_cap_mb = auto_bucket_mb(grad_bytes, self.world, self.shard)
+        self.bucket_cap_mb = float(bucket_cap_mb)
         cap = max(int(bucket_cap_mb * 2 ** 20 / params[0].element_size()), 1)
         pad = ALIGN * self.world
         buckets, cur, cur_n = [], _Bucket(0), 0

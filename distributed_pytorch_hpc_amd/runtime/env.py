@@ -9,7 +9,10 @@ module.  Differences, by design for a single 8-GPU xGMI node:
   * the backend defaults to "nccl" (= RCCL on ROCm) with a GPU, "gloo" without one -- the device
     binding follows the backend, so the gloo path is genuinely CPU-only (reference defect X5);
   * ``init_process_group`` gets a timeout and eager ``device_id`` (communicators created up front, so
-    a broken rank fails at init rather than at the first collective).
+    a broken rank fails at init rather than at the first collective);
+  * RCCL failure detection is on by default: ``TORCH_NCCL_ASYNC_ERROR_HANDLING=1`` (a rank whose
+    collective times out or errors tears the process down instead of hanging the gang) and the c10d watchdog
+    heartbeat ``TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC`` (600 s); user-set values win.
 """
 from __future__ import annotations
 
@@ -95,6 +98,11 @@ def device_for(local_rank: int, backend: str | None = None) -> torch.device:
     return torch.device("cpu")
 
 
+# c10d (ProcessGroupNCCL = RCCL on ROCm) failure detection: async error handling + watchdog heartbeat
+RCCL_FAILURE_ENV = {"TORCH_NCCL_ASYNC_ERROR_HANDLING": "1", "TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC": "600",
+                    "TORCH_NCCL_ENABLE_MONITORING": "1"}
+
+
 def init_distributed(backend: str | None = None, verbose: bool = True, timeout_s: float = 1800.0,
                      eager: bool = True):
     """Bind the device and create the default process group.
@@ -112,6 +120,9 @@ def init_distributed(backend: str | None = None, verbose: bool = True, timeout_s
     dev = device_for(info.local_rank, backend)
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
+    if backend == "nccl":
+        for k, v in RCCL_FAILURE_ENV.items():
+            os.environ.setdefault(k, v)
     if not dist.is_initialized():
         kwargs = dict(backend=backend, init_method="env://", rank=info.rank, world_size=info.world_size,
                       timeout=datetime.timedelta(seconds=timeout_s))
