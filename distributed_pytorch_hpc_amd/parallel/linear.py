@@ -52,6 +52,38 @@ def _dgrad(gy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return torch.matmul(gy, w)
 
 
+def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
+    """dW = g2^T x2 for weight ``w`` ([N, K] from g2 [T, N], x2 [T, K]).  When the data-parallel engine owns ``w``
+    (``w.main_grad``), dW is written / accumulated straight into the flat gradient bucket (CDNA4 wgrad kernel when
+    the shape fits, else hipBLASLt), the engine is notified, and None is returned; otherwise dW is returned."""
+    mg = getattr(w, "main_grad", None)
+    if mg is not None and _native_wgrad(mg, g2, x2, getattr(w, "_dph_accum", False)):
+        w._dph_accum = True
+        w._dph_grad_ready()
+        return None
+    if mg is not None and mg.dtype != x2.dtype:
+        gw_ = g2.t().mm(x2)
+        if getattr(w, "_dph_accum", False):
+            mg.add_(gw_)
+        else:
+            mg.copy_(gw_)
+            w._dph_accum = True
+        w._dph_grad_ready()
+        return None
+    if mg is not None:
+        if getattr(w, "_dph_accum", False):
+            mg.addmm_(g2.t(), x2)
+        else:
+            torch.mm(g2.t(), x2, out=mg)
+            w._dph_accum = True
+        w._dph_grad_ready()
+        return None
+    gw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
+    if not _native_wgrad(gw, g2, x2, False):
+        gw = g2.t().mm(x2)
+    return gw
+
+
 def _autocast_dtype(t: torch.Tensor):
     dev = t.device.type
     return torch.get_autocast_dtype(dev) if torch.is_autocast_enabled(dev) else None
@@ -79,30 +111,7 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = _dgrad(gy, w)
         if ctx.needs_input_grad[1]:
-            x2 = x.reshape(-1, x.shape[-1])
-            mg = getattr(w, "main_grad", None)
-            if mg is not None and _native_wgrad(mg, g2, x2, getattr(w, "_dph_accum", False)):
-                w._dph_accum = True
-                w._dph_grad_ready()
-            elif mg is not None and mg.dtype != x2.dtype:
-                gw_ = g2.t().mm(x2)
-                if getattr(w, "_dph_accum", False):
-                    mg.add_(gw_)
-                else:
-                    mg.copy_(gw_)
-                    w._dph_accum = True
-                w._dph_grad_ready()
-            elif mg is not None:
-                if getattr(w, "_dph_accum", False):
-                    mg.addmm_(g2.t(), x2)
-                else:
-                    torch.mm(g2.t(), x2, out=mg)
-                    w._dph_accum = True
-                w._dph_grad_ready()
-            else:
-                gw = torch.empty(w.shape, dtype=w.dtype, device=w.device)
-                if not _native_wgrad(gw, g2, x2, False):
-                    gw = g2.t().mm(x2)
+            gw = weight_grad(w, g2, x.reshape(-1, x.shape[-1]))
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = g2.sum(0)
             if getattr(w, "main_grad", None) is not None and gb is not None:

@@ -39,6 +39,7 @@ from torch import nn
 
 from .. import ops
 from ..comm import functional as cf
+from .async_tp import ag_matmul, matmul_reduce_scatter
 from .linear import linear as _linear
 
 
@@ -80,10 +81,14 @@ class ColwiseParallelLinear(nn.Module):
         if lin.bias is not None:
             self.bias = nn.Parameter(shard_rows(lin.bias.detach()[:, None], group)[:, 0].contiguous())
         self.in_features, self.out_features = lin.in_features, self.weight.shape[0]
+        self.async_chunks = 0   # > 0: sequence all-gather pipelined against the GEMM (parallel/async_tp.py)
 
     def forward(self, x):
-        x = cf.gather_along_dim(x, self.seq_dim, self.group) if self.sp else cf.copy_to_group(x, self.group)
-        y = _linear(x, self.weight, self.bias)
+        if self.sp and self.async_chunks and self.seq_dim == 1 and x.dim() == 3 and _ws(self.group) > 1:
+            y = ag_matmul(x, self.weight, self.bias, self.group, self.async_chunks)
+        else:
+            x = cf.gather_along_dim(x, self.seq_dim, self.group) if self.sp else cf.copy_to_group(x, self.group)
+            y = _linear(x, self.weight, self.bias)
         if self.gather_output:
             y = cf.gather_replicated_along_dim(y, y.dim() - 1, self.group)
         return y
@@ -99,12 +104,17 @@ class RowwiseParallelLinear(nn.Module):
                                    requires_grad=lin.weight.requires_grad)
         self.bias = nn.Parameter(lin.bias.detach().clone()) if lin.bias is not None else None
         self.in_features, self.out_features = self.weight.shape[1], lin.out_features
+        self.async_chunks = 0   # > 0: GEMM pipelined against the sequence reduce-scatter (parallel/async_tp.py)
 
     def forward(self, x):
         if not self.input_is_parallel:
             x = cf.split_along_dim(x, x.dim() - 1, self.group)
-        y = _linear(x, self.weight, None)
-        y = cf.reduce_scatter_along_dim(y, self.seq_dim, self.group) if self.sp else cf.reduce_from_group(y, self.group)
+        if self.sp and self.async_chunks and self.seq_dim == 1 and x.dim() == 3 and _ws(self.group) > 1:
+            y = matmul_reduce_scatter(x, self.weight, self.group, self.async_chunks)
+        else:
+            y = _linear(x, self.weight, None)
+            y = cf.reduce_scatter_along_dim(y, self.seq_dim, self.group) if self.sp else \
+                cf.reduce_from_group(y, self.group)
         if self.bias is not None:
             y = y + self.bias
         return y
@@ -179,8 +189,11 @@ def parallelize_module(module: nn.Module, tp_group, plan: dict) -> nn.Module:
 
 
 # ------------------------------------------------------------------------------------------- Llama plan
-def parallelize_llama(model, tp_group, sequence_parallel: bool = True, loss_parallel: bool = True):
-    """TP(+SP) plan of fsdp_tp/fsdp_tp_example.py:142-184 for models.llama2.Transformer (fused projections)."""
+def parallelize_llama(model, tp_group, sequence_parallel: bool = True, loss_parallel: bool = True,
+                      async_tp: int = 0):
+    """TP(+SP) plan of fsdp_tp/fsdp_tp_example.py:142-184 for models.llama2.Transformer (fused projections).
+    ``async_tp`` = k > 0 (needs sequence_parallel) pipelines each block's sequence all-gathers / reduce-scatters
+    against the wqkv / wo / w13 / w2 GEMMs in k micro-collectives (parallel/async_tp.py)."""
     tp = _ws(tp_group)
     args = model.model_args
     hd, nh, nkv = args.head_dim, args.n_heads, args.kv_heads
@@ -198,6 +211,9 @@ def parallelize_llama(model, tp_group, sequence_parallel: bool = True, loss_para
         ff.w13 = ColwiseParallelLinear(ff.w13, tp_group, sp, shard_fn=lambda w, g: shard_rows_grouped(w, [f, f], g))
         ff.w2 = RowwiseParallelLinear(ff.w2, tp_group, sp)
         ff.hidden_dim = f // tp
+        if sp and async_tp:
+            for lin in (a.wqkv, a.wo, ff.w13, ff.w2):
+                lin.async_chunks = int(async_tp)
         if sp:
             mark_sequence_parallel(layer.attention_norm, tp_group)
             mark_sequence_parallel(layer.ffn_norm, tp_group)

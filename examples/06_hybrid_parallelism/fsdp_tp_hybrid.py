@@ -46,6 +46,9 @@ def main(argv=None):
     ap.add_argument("--loss", choices=["ce", "sum"], default="ce")
     ap.add_argument("--no-sp", action="store_true", help="disable sequence parallelism")
     ap.add_argument("--no-loss-parallel", action="store_true")
+    ap.add_argument("--async-tp", type=int, default=0,
+                    help="k > 0: pipeline the SP all-gathers / reduce-scatters against the projection GEMMs in k "
+                         "micro-collectives (parallel/async_tp.py)")
     ap.add_argument("--no-shard", action="store_true", help="replicated optimizer state over dp (plain DDP)")
     args = ap.parse_args(argv)
     rank, world, local, dev = start(args)
@@ -62,7 +65,8 @@ def main(argv=None):
     model = build_llama(margs, device=dev, dtype=dtype, seed=args.seed)
     n_params = sum(p.numel() for p in model.parameters())
     parallelize_llama(model, mesh.tp_group, sequence_parallel=not args.no_sp,
-                      loss_parallel=not args.no_loss_parallel and args.loss == "ce")
+                      loss_parallel=not args.no_loss_parallel and args.loss == "ce",
+                      async_tp=0 if args.no_sp else args.async_tp)
     engine = DataParallelEngine(model, mesh.dp_group, shard=not args.no_shard and dp > 1,
                                 mixed_precision=MixedPrecision(reduce_dtype=dtype))
     engine.configure_optimizer(OptimConfig("adamw", lr=args.lr, betas=(0.9, 0.95), weight_decay=0.1))

@@ -82,14 +82,14 @@ def test_fsdp_sharded_optimizer_matches_single_process():
         _check(ref, o)
 
 
-def _tp_worker(rank, world, dp, sp, loss_parallel):
+def _tp_worker(rank, world, dp, sp, loss_parallel, async_tp=0):
     from distributed_pytorch_hpc_amd.comm.mesh import DeviceMesh2D
     from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig
     from distributed_pytorch_hpc_amd.parallel.tensor_parallel import parallelize_llama
 
     mesh = DeviceMesh2D(dp, world // dp)
     m = _model()
-    parallelize_llama(m, mesh.tp_group, sequence_parallel=sp, loss_parallel=loss_parallel)
+    parallelize_llama(m, mesh.tp_group, sequence_parallel=sp, loss_parallel=loss_parallel, async_tp=async_tp)
     eng = DataParallelEngine(m, process_group=mesh.dp_group, shard=dp > 1, bucket_cap_mb=0.02)
     eng.configure_optimizer(OptimConfig(lr=1e-2, weight_decay=0.1))
     losses = []
@@ -144,3 +144,17 @@ def test_hybrid_fsdp2_x_tp2_matches_single_process():
     ref = _reference()
     outs = run_distributed(_tp_worker, 4, 2, True, True)
     _check_tp(ref, outs, 2)
+
+
+def test_async_tp_matches_single_process():
+    """Sequence all-gathers / reduce-scatters pipelined against the projection GEMMs (parallel/async_tp.py)."""
+    ref = _reference()
+    outs = run_distributed(_tp_worker, 2, 1, True, True, 2)
+    _check_tp(ref, outs, 2)
+
+
+def test_async_tp_tp4_uneven_chunks_matches_single_process():
+    # local sequence 16 / 4 = 4 tokens, 3 requested micro-chunks -> falls back to a divisor (2)
+    ref = _reference()
+    outs = run_distributed(_tp_worker, 4, 1, True, True, 3)
+    _check_tp(ref, outs, 4)

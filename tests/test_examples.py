@@ -38,6 +38,8 @@ CASES = [
                                                                    "--steps", "2", "--model", "tiny"]),
     ("06_hybrid_parallelism/fsdp_tp_hybrid.py", 4, ["--tp", "2", "--iters", "2", "--batch", "2", "--seq-len",
                                                     "32", "--model", "tiny"]),
+    ("06_hybrid_parallelism/fsdp_tp_hybrid.py", 4, ["--tp", "2", "--iters", "2", "--batch", "2", "--seq-len",
+                                                    "32", "--model", "tiny", "--async-tp", "2"]),
     ("06_hybrid_parallelism/three_d_parallel.py", 4, ["--pp", "2", "--tp", "2", "--iters", "2", "--batch", "4",
                                                       "--seq-len", "32", "--model", "tiny"]),
     ("07_domain_parallel/domain_parallel_unet.py", 2, ["--lat", "32", "--lon", "32", "--channels", "3",
