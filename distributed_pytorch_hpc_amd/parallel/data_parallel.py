@@ -38,7 +38,7 @@ from torch import nn
 from ..ops import _lib
 from ..train import optim as optim_ref
 from ..utils.flat import ALIGN, align_up
-from .linear import convert_linears_
+from .linear import convert_linears_, join_wgrad_stream, wgrad_stream
 
 
 @dataclass
@@ -253,14 +253,33 @@ class DataParallelEngine:
         if self.world == 1:
             return
         g = self.grad_view(b)
-        if self.shard:
-            b.work = dist.reduce_scatter_tensor(self.grad_shard_view(b), g, op=dist.ReduceOp.SUM,
-                                                group=self.group, async_op=True)
-        else:
-            b.work = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        side = wgrad_stream(self.device)
+        # The bucket's weight gradients may still be in flight on the wgrad side stream (parallel/linear.py):
+        # issue the collective from that stream after it has also caught up with the compute stream, so RCCL
+        # waits for both while the compute stream itself never blocks.
+        ctx = contextlib.nullcontext()
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            ctx = torch.cuda.stream(side)
+        with ctx:
+            if self.shard:
+                b.work = dist.reduce_scatter_tensor(self.grad_shard_view(b), g, op=dist.ReduceOp.SUM,
+                                                    group=self.group, async_op=True)
+            else:
+                b.work = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def _join_wgrad_stream(self):
+        join_wgrad_stream(self.device)
 
     def _finalize_backward(self):
         self._callback_queued = False
+        try:
+            self._launch_remaining()
+        finally:
+            # every main_grad write of this backward is ordered before whatever the compute stream does next
+            self._join_wgrad_stream()
+
+    def _launch_remaining(self):
         if not self._sync_enabled:
             for b in self.buckets:
                 b.n_ready = 0

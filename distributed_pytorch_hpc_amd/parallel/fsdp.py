@@ -35,7 +35,7 @@ from ..ops import _lib
 from ..train import optim as optim_ref
 from ..utils.flat import ALIGN, align_up
 from .data_parallel import DataParallelEngine, MixedPrecision, OptimConfig, _EngineOptimizer
-from .linear import convert_linears_
+from .linear import convert_linears_, join_wgrad_stream, wgrad_stream
 
 
 class ShardingStrategy(Enum):
@@ -275,10 +275,16 @@ class ZeRO3Engine:
         if u.n_ready == len(u.params) and self._sync_enabled:
             self._launch(u)
 
+    def _join_wgrad_stream(self):
+        # weight-gradient GEMMs into u.grad_full may run on the wgrad side stream (parallel/linear.py); the unit's
+        # buffer is zero-filled, reduce-scattered and freed on the compute stream, so order it after them
+        join_wgrad_stream(self.device)
+
     def _launch(self, u):
         if u.launched:
             return
         u.launched = True
+        self._join_wgrad_stream()
         with torch.no_grad():
             for p in u.params:
                 if not p._dph_accum:
@@ -293,6 +299,7 @@ class ZeRO3Engine:
 
     def _finalize_backward(self):
         self._callback_queued = False
+        self._join_wgrad_stream()
         if not self._sync_enabled:
             for u in self.units:
                 u.n_ready = 0

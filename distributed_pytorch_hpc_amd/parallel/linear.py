@@ -10,9 +10,43 @@ rest of the backward pass is still running.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
+
+# Opt-in (DPH_WGRAD_STREAM=1): weight-gradient GEMMs on a side stream (per device).  dW is off the backward's
+# critical path, so the CDNA4 wgrad kernel could overlap the next dgrad / attention-backward / norm kernels and
+# fill their tail waves.  The data-parallel engine orders its collectives after this stream and joins it at the
+# end of backward (DataParallelEngine._finalize_backward).  Measured on Llama-2-7B (1 MI355X, B=8 x 4096): 26,642
+# (lag 1) / 26,463 (lag 2) vs 27,288 tokens/s single-stream -- both kernels are sized for the whole chip and
+# contend for CUs / L2 -- so the default is one stream.
+_WGRAD_STREAMS: dict = {}
+# In-flight side-stream wgrads: (event, operands).  Operands stay referenced (instead of record_stream, which keeps
+# the caching allocator from recycling multi-GB blocks and drives it into synchronising cudaFree/retry cycles
+# near the 288 GB limit) and the compute stream waits for the oldest once more than _WGRAD_LAG are in flight.
+_WGRAD_PENDING: list = []
+_WGRAD_LAG = int(os.environ.get("DPH_WGRAD_LAG", "1"))
+
+
+def join_wgrad_stream(device: torch.device):
+    """Order the compute stream after every side-stream wgrad and drop the operands kept alive for them."""
+    side = wgrad_stream(device)
+    if side is not None:
+        torch.cuda.current_stream(device).wait_stream(side)
+    _WGRAD_PENDING.clear()
+
+
+def wgrad_stream(device: torch.device):
+    """The side stream the engine-managed weight-gradient GEMMs use on ``device`` (None: disabled / not CUDA)."""
+    if device.type != "cuda" or os.environ.get("DPH_WGRAD_STREAM", "0") != "1":
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _WGRAD_STREAMS.get(idx)
+    if s is None:
+        s = _WGRAD_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return s
 
 
 def _native_wgrad(out: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor, accumulate: bool) -> bool:
@@ -57,7 +91,22 @@ def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
     (``w.main_grad``), dW is written / accumulated straight into the flat gradient bucket (CDNA4 wgrad kernel when
     the shape fits, else hipBLASLt), the engine is notified, and None is returned; otherwise dW is returned."""
     mg = getattr(w, "main_grad", None)
-    if mg is not None and _native_wgrad(mg, g2, x2, getattr(w, "_dph_accum", False)):
+    side = wgrad_stream(g2.device) if mg is not None else None
+    if side is not None:
+        main = torch.cuda.current_stream(g2.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            launched = _native_wgrad(mg, g2, x2, getattr(w, "_dph_accum", False))
+        if launched:
+            ev = torch.cuda.Event()
+            ev.record(side)
+            _WGRAD_PENDING.append((ev, g2, x2))
+            while len(_WGRAD_PENDING) > _WGRAD_LAG:
+                main.wait_event(_WGRAD_PENDING.pop(0)[0])
+            w._dph_accum = True
+            w._dph_grad_ready()
+            return None
+    elif mg is not None and _native_wgrad(mg, g2, x2, getattr(w, "_dph_accum", False)):
         w._dph_accum = True
         w._dph_grad_ready()
         return None
