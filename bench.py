@@ -50,6 +50,8 @@ def parse(argv=None):
     ap.add_argument("--force-dist", action="store_true",
                     help="create the RCCL process group even for one rank (exercises the N>1 collective path)")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu: gloo + eager reference ops (tests of the N > 1 code path with tiny models only)")
     return ap.parse_args(argv)
 
 
@@ -58,25 +60,30 @@ def main(argv=None):
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     from distributed_pytorch_hpc_amd.runtime import env as rt
 
+    cpu = args.device == "cpu"
     if world_env > 1 or args.force_dist:
-        rank, world, local = rt.init_distributed(verbose=not args.quiet)
+        rank, world, local = rt.init_distributed(backend="gloo" if cpu else None, verbose=not args.quiet)
     else:
         rank, world, local = 0, 1, 0
-        torch.cuda.set_device(0)
+        if not cpu:
+            torch.cuda.set_device(0)
     if world != args.gpus and rank == 0:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting n_gpus={world}", file=sys.stderr)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = torch.device("cpu") if cpu else torch.device("cuda", torch.cuda.current_device())
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
 
     from distributed_pytorch_hpc_amd.models.llama2 import build_llama, get_preset
     from distributed_pytorch_hpc_amd.ops import _lib
     from distributed_pytorch_hpc_amd.parallel.data_parallel import (DataParallelEngine, MixedPrecision,
                                                                     OptimConfig)
 
-    _lib.require()
+    if not cpu:
+        _lib.require()
     if args.kernels == "aten":
         _lib.set_reference_mode(True)
     margs = get_preset(args.model, max_seq_len=max(args.seq_len, 4096))
-    model = build_llama(margs, device=dev, dtype=torch.bfloat16, seed=1234)
+    dtype = torch.float32 if cpu else torch.bfloat16
+    model = build_llama(margs, device=dev, dtype=dtype, seed=1234)
     ac_every = 0
     if args.ac != "none":
         from distributed_pytorch_hpc_amd.parallel.activation_checkpoint import (apply_llama_checkpointing,
@@ -92,8 +99,9 @@ def main(argv=None):
         mode = "fsdp" if world > 1 or args.force_dist else "ddp"
     engine = DataParallelEngine(
         model, shard=(mode == "fsdp"),
-        mixed_precision=MixedPrecision(param_dtype=torch.bfloat16,
-                                       reduce_dtype=torch.bfloat16 if args.grad_dtype == "bf16" else torch.float32),
+        mixed_precision=MixedPrecision(param_dtype=dtype,
+                                       reduce_dtype=torch.bfloat16 if args.grad_dtype == "bf16" and not cpu
+                                       else torch.float32),
         bucket_cap_mb=args.bucket_mb if args.bucket_mb == "auto" else float(args.bucket_mb))
     engine.configure_optimizer(OptimConfig(name="adamw", lr=args.lr, betas=(0.9, 0.95), weight_decay=0.1))
 
@@ -111,10 +119,10 @@ def main(argv=None):
         return loss
 
     def sync_all():
-        torch.cuda.synchronize()
+        sync()
         if dist.is_initialized():
             rt.barrier()
-        torch.cuda.synchronize()
+        sync()
 
     for i in range(args.warmup):
         loss = train_step(i)
@@ -138,7 +146,7 @@ def main(argv=None):
     ms = 1000.0 * elapsed / args.steps
     flops_tok = margs.flops_per_token(S)
     mfu = tps / world * flops_tok / 2.5e15
-    peak_gb = torch.cuda.max_memory_allocated() / 1e9
+    peak_gb = 0.0 if cpu else torch.cuda.max_memory_allocated() / 1e9
     if rank == 0:
         rec = {
             "metric": BASELINE_METRIC,
@@ -151,7 +159,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp32" if cpu else "bf16",
             "data": "synthetic (random tokens, random-init weights)",
             "config": {
                 "model": "Llama-2-7B" if args.model == "llama2-7b" else args.model,
