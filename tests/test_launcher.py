@@ -44,3 +44,13 @@ def test_rank_detection_precedence(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "16")
     monkeypatch.setenv("LOCAL_RANK", "2")
     assert tuple(get_rank_info()) == (2, 16, 2, "torchrun")
+
+
+def test_utils_facade_has_reference_names():
+    """utils/__init__.py of the reference re-exports these; scripts written against it import them by name."""
+    import distributed_pytorch_hpc_amd.utils as u
+
+    for name in ("get_rank_info", "init_distributed", "cleanup_distributed", "is_main_rank", "print_rank0",
+                 "get_logger", "rank_log", "verify_min_gpu_count", "training_profiler", "print_profiler_summary",
+                 "save_checkpoint", "load_checkpoint", "TrainingConfig", "redirect"):
+        assert callable(getattr(u, name)), name
