@@ -49,7 +49,7 @@ def main():
 
     torch.backends.cudnn.benchmark = True
     B, dev, dt = a.batch, "cuda", torch.bfloat16
-    rows, tot_conv, tot_gemm = [], 0.0, 0.0
+    rows, tot_conv, tot_gemm, tot_dph = [], 0.0, 0.0, 0.0
     for cin, cout, k, s, H, cnt in SHAPES:
         x = torch.randn(B, cin, H, H, device=dev, dtype=dt).contiguous(memory_format=torch.channels_last)
         w = (torch.randn(cout, cin, k, k, device=dev, dtype=dt) * 0.05).contiguous(memory_format=torch.channels_last)
@@ -80,11 +80,24 @@ def main():
             t_gemm = timeit(gemm_fb)
             row["gemm_fwd_bwd_ms"] = t_gemm
             tot_gemm += cnt * t_gemm
+            if s == 1:   # the framework's CDNA4 tall-skinny kernels (ops.Conv1x1)
+                from distributed_pytorch_hpc_amd.ops.conv import _Conv1x1Fn
+
+                def dph_fb():
+                    y = _Conv1x1Fn.apply(xr, wr)
+                    torch.autograd.grad(y, (xr, wr), gy)
+
+                row["dph_fwd_bwd_ms"] = timeit(dph_fb)
+                tot_dph += cnt * row["dph_fwd_bwd_ms"]
+            else:
+                tot_dph += cnt * t_conv
         else:
             tot_gemm += cnt * t_conv
+            tot_dph += cnt * t_conv
         rows.append(row)
         print(json.dumps(row), flush=True)
-    res = {"batch": B, "resnet50_conv_ms_miopen": tot_conv, "resnet50_conv_ms_1x1_as_gemm": tot_gemm, "shapes": rows}
+    res = {"batch": B, "resnet50_conv_ms_miopen": tot_conv, "resnet50_conv_ms_1x1_as_gemm": tot_gemm,
+           "resnet50_conv_ms_1x1_dph": tot_dph, "shapes": rows}
     print(json.dumps({k: v for k, v in res.items() if k != "shapes"}))
     if a.json:
         with open(a.json, "w") as fh:

@@ -1,0 +1,302 @@
+// 1x1 convolutions on channels-last activations = tall-skinny GEMMs, for CDNA4 (gfx950).
+//
+// In NHWC a stride-1 1x1 convolution is Y[M, Cout] = X[M, Cin] W[Cout, Cin]^T with M = N*H*W pixels (up to
+// 802,816 for ResNet-50 at B=256) and Cin, Cout in 64..2048: far more rows than columns and memory-bound
+// (benchmarks/conv_bench.py).  hipBLASLt tiles these shapes badly (2-7x slower than MIOpen's NHWC implicit GEMM,
+// profiles/conv_bench_miopen_vs_1x1_gemm.json); these kernels are written for them:
+//
+//   ts_nt_k   C[M, N] = A[M, K] B[N, K]^T  (forward: A = X, B = W;  input gradient: A = dY, B = W^T)
+//             128 x BN tile per workgroup (4 waves x 32 rows, BN = 64 | 128), K-steps of 64, A fragments straight
+//             from HBM into registers (each row is used by exactly one wave -- no LDS round trip), prefetched one
+//             K-step ahead; the small B slab is register-staged into a double-buffered LDS image (144-B rows:
+//             conflict-free ds_read_b128); v_mfma_f32_32x32x16_bf16; the C tile goes back through LDS so the
+//             stores are whole 16-B row segments.  N-tiles of one row block run on one XCD (L2 reuse of A).
+//   ts_tn_k   P[s][N, K] = sum over the s-th pixel chunk of A[m, N]^T B[m, K]  (weight gradient, A = dY, B = X)
+//             64 x 64 output tile per workgroup (4 waves x 32x32), pixels are the reduction dim: 64-pixel slabs
+//             of both operands are register-staged into LDS rows of 192 B (4 consecutive rows cover all 64
+//             banks) and read back transposed with ds_read_b64_tr_b16; split over pixel chunks with fp32
+//             partials, then
+//   ts_reduce_k  dW = sum_s P[s] (+ dW) in the weight's dtype (deterministic: fixed summation order).
+#include <algorithm>
+
+#include "dph_common.h"
+#include "kernels.h"
+
+namespace dph {
+
+namespace {
+
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4_c;
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// bijective XCD-aware remap of a 1-D grid: blocks congruent mod 8 (one XCD) get a contiguous logical range
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+constexpr int TS_BM = 128, TS_BK = 64, TS_NT = 256;
+constexpr int TS_BROW = 72;   // B slab row: 64 bf16 + 8 pad (144 B: 16 consecutive rows hit 16 distinct 16-B slots)
+constexpr int TS_KF = TS_BK / 16;   // MFMA k-steps (A fragments) per K-step
+
+template <int BN>
+__global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                 bf16* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                 int64_t ldb, int64_t ldc) {
+  constexpr int NT = BN / 32;                        // 32-column tiles per wave
+  constexpr int BCH = BN * (TS_BK / 8) / TS_NT;      // 16-B B chunks per thread per K-step (BN=128: 4)
+  constexpr int CROW = BN + 8;                       // epilogue LDS row (bf16)
+  constexpr int LDS_B = 2 * BN * TS_BROW * 2, LDS_C = TS_BM * CROW * 2;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_B > LDS_C ? LDS_B : LDS_C];
+  bf16* Bs = reinterpret_cast<bf16*>(smem);
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l32 = lane & 31, h = lane >> 5;
+  const int ntn = N / BN, nmb = (M + TS_BM - 1) / TS_BM;
+  const int lin = xcd_remap(blockIdx.x, nmb * ntn);
+  const int mb = lin / ntn, nt0 = (lin % ntn) * BN;
+  const int m0 = mb * TS_BM;
+
+  // A: this lane's row (clamped for the ragged last block; its results are not stored)
+  const int arow = min(m0 + wid * 32 + l32, M - 1);
+  const bf16* ap = A + (int64_t)arow * lda + 8 * h;
+  // B staging: chunk c of thread t -> slab row (t*BCH + c) / 8, 16-B column chunk (t*BCH + c) % 8
+  const bf16* bp[BCH];
+  int bdst[BCH];
+#pragma unroll
+  for (int c = 0; c < BCH; ++c) {
+    const int ch = threadIdx.x * BCH + c, row = ch >> 3, col = (ch & 7) * 8;
+    bp[c] = B + (int64_t)(nt0 + row) * ldb + col;
+    bdst[c] = row * TS_BROW + col;
+  }
+
+  f32x16 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+
+  const int nks = K / TS_BK;
+  bf16x8 a[TS_KF];
+#pragma unroll
+  for (int f = 0; f < TS_KF; ++f) a[f] = *reinterpret_cast<const bf16x8*>(ap + 16 * f);
+  bf16x8 bst[BCH];
+#pragma unroll
+  for (int c = 0; c < BCH; ++c) bst[c] = *reinterpret_cast<const bf16x8*>(bp[c]);
+#pragma unroll
+  for (int c = 0; c < BCH; ++c) *reinterpret_cast<bf16x8*>(Bs + bdst[c]) = bst[c];
+  __syncthreads();
+
+  for (int ks = 0; ks < nks; ++ks) {
+    const int cur = ks & 1;
+    bf16x8 na[TS_KF];
+#pragma unroll
+    for (int f = 0; f < TS_KF; ++f) na[f] = a[f];
+    if (ks + 1 < nks) {   // prefetch the next K-step (A into registers, B into staging registers)
+      const int ko = (ks + 1) * TS_BK;
+#pragma unroll
+      for (int f = 0; f < TS_KF; ++f) na[f] = *reinterpret_cast<const bf16x8*>(ap + ko + 16 * f);
+#pragma unroll
+      for (int c = 0; c < BCH; ++c) bst[c] = *reinterpret_cast<const bf16x8*>(bp[c] + ko);
+    }
+    const bf16* bs = Bs + cur * BN * TS_BROW;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const bf16* br = bs + (t * 32 + l32) * TS_BROW + 8 * h;
+#pragma unroll
+      for (int f = 0; f < TS_KF; ++f)
+        acc[t] = mfma32(a[f], *reinterpret_cast<const bf16x8*>(br + 16 * f), acc[t]);
+    }
+    if (ks + 1 < nks) {
+      bf16* nb = Bs + (cur ^ 1) * BN * TS_BROW;
+#pragma unroll
+      for (int c = 0; c < BCH; ++c) *reinterpret_cast<bf16x8*>(nb + bdst[c]) = bst[c];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int f = 0; f < TS_KF; ++f) a[f] = na[f];
+  }
+
+  // ---- epilogue through LDS: register r of tile t holds C[row (r&3) + 8(r>>2) + 4h][col t*32 + l32] ----
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      Cs[(wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CROW + t * 32 + l32] = (bf16)acc[t][r];
+  __syncthreads();
+  constexpr int CPR = BN / 8;   // 16-B chunks per row
+#pragma unroll
+  for (int i = threadIdx.x; i < TS_BM * CPR; i += TS_NT) {
+    const int row = i / CPR, ch = i % CPR;
+    if (m0 + row < M)
+      *reinterpret_cast<bf16x8*>(C + (int64_t)(m0 + row) * ldc + nt0 + ch * 8) =
+          *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
+  }
+}
+
+// ---- weight gradient: P[s][n][k] = sum_{m in chunk s} A[m][n] B[m][k] ----
+constexpr int TW_ROWB = 192;   // LDS row stride in bytes (64 bf16 + 32 pad): rows 4 apart cover all 64 banks
+
+__device__ __forceinline__ bf16x4 tr_read(const char* p) {
+  i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_c*)p);
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+__global__ __launch_bounds__(256) void ts_tn_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                               float* __restrict__ P, int M, int N, int K, int64_t lda,
+                                               int64_t ldb, int chunk) {
+  constexpr int TP = 64;   // pixels per step (rows of the staged slabs)
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TP * TW_ROWB];   // [buf][A|B][64 rows][192 B]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wi = wid >> 1, wj = wid & 1;             // wave's 32x32 sub-tile of the 64x64 output tile
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int tn = N / 64, tk = K / 64;
+  const int nsplit = gridDim.x / (tn * tk);
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  // all output tiles of one pixel chunk are adjacent (same XCD): they read the same dY / X rows, which then come
+  // from that XCD's L2 instead of HBM once per tile
+  const int ntile = tn * tk;
+  const int s = lin / ntile, tile = lin % ntile;
+  const int n0 = (tile / tk) * 64, k0 = (tile % tk) * 64;
+  const int mbeg = s * chunk, mend = min(M, mbeg + chunk);
+
+  // staging: thread t copies 16 B of rows t>>3 and 32 + (t>>3) of the 64-row slab, chunk t&7, for A and B
+  const int srow = threadIdx.x >> 3, sch = threadIdx.x & 7;
+  const int sdst = srow * TW_ROWB + sch * 16;
+  // transposed-read offsets: lane 4q+p of 16-lane group g reads row (r0 + q), columns c0 + 4p .. +3 where the
+  // group's half h = g >> 1 selects rows 8h.. (k-steps) and g & 1 the column half of the 32-wide operand
+  const int hh = g >> 1, c0 = 16 * (g & 1);
+  const int toffA = (8 * hh + q) * TW_ROWB + (wi * 32 + c0 + 4 * p) * 2;
+  const int toffB = (8 * hh + q) * TW_ROWB + (wj * 32 + c0 + 4 * p) * 2;
+
+  f32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+
+  auto load = [&](int m, bf16x8 (&va)[2], bf16x8 (&vb)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int rr = m + srow + 32 * u, row = min(rr, M - 1);
+      va[u] = *reinterpret_cast<const bf16x8*>(A + (int64_t)row * lda + n0 + sch * 8);
+      vb[u] = *reinterpret_cast<const bf16x8*>(B + (int64_t)row * ldb + k0 + sch * 8);
+      if (rr >= mend) {   // rows past this chunk contribute zero
+        va[u] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        vb[u] = va[u];
+      }
+    }
+  };
+  auto stage = [&](char* base, const bf16x8 (&va)[2], const bf16x8 (&vb)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      *reinterpret_cast<bf16x8*>(base + sdst + 32 * u * TW_ROWB) = va[u];
+      *reinterpret_cast<bf16x8*>(base + TP * TW_ROWB + sdst + 32 * u * TW_ROWB) = vb[u];
+    }
+  };
+  bf16x8 va[2], vb[2];
+  load(mbeg, va, vb);
+  stage(smem, va, vb);
+  __syncthreads();
+  int buf = 0;
+  for (int m = mbeg; m < mend; m += TP) {
+    const bool more = m + TP < mend;
+    if (more) load(m + TP, va, vb);
+    const char* As = smem + buf * 2 * TP * TW_ROWB;
+    const char* Bs = As + TP * TW_ROWB;
+#pragma unroll
+    for (int kk = 0; kk < TP / 16; ++kk) {   // 16-pixel MFMA k-steps: rows 16kk + 8h + j
+      const int ro = 16 * kk * TW_ROWB;
+      const bf16x4 alo = tr_read(As + ro + toffA), ahi = tr_read(As + ro + toffA + 4 * TW_ROWB);
+      const bf16x4 blo = tr_read(Bs + ro + toffB), bhi = tr_read(Bs + ro + toffB + 4 * TW_ROWB);
+      acc = mfma32(__builtin_shufflevector(alo, ahi, 0, 1, 2, 3, 4, 5, 6, 7),
+                   __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7), acc);
+    }
+    if (more) stage(smem + (buf ^ 1) * 2 * TP * TW_ROWB, va, vb);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // register r holds P[n0 + wi*32 + (r&3) + 8(r>>2) + 4h][k0 + wj*32 + (lane & 31)]
+  float* out = P + (int64_t)s * N * K;
+  const int h = lane >> 5;
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    out[(int64_t)(n0 + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * K + k0 + wj * 32 + (lane & 31)] = acc[r];
+}
+
+// dW = sum_s P[s] (+ dW).  A workgroup = 16 float4 output columns x 16 split groups; each thread sums every
+// 16th split of its float4 (independent loads in flight), then the 16 partial sums meet in LDS in a fixed order.
+template <typename T, bool ACC>
+__global__ __launch_bounds__(256) void ts_reduce_k(const float* __restrict__ P, T* __restrict__ out, int64_t nk,
+                                                   int nsplit) {
+  __shared__ f32x4 red[16][16];
+  const int c = threadIdx.x & 15, sg = threadIdx.x >> 4;
+  const int64_t i = ((int64_t)blockIdx.x * 16 + c) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (i < nk) {
+#pragma unroll 4
+    for (int j = sg; j < nsplit; j += 16) s += *reinterpret_cast<const f32x4*>(P + (int64_t)j * nk + i);
+  }
+  red[sg][c] = s;
+  __syncthreads();
+  if (sg == 0 && i < nk) {
+#pragma unroll
+    for (int j = 1; j < 16; ++j) s += red[j][c];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = s[e];
+      if (ACC) v += (float)out[i + e];
+      out[i + e] = (T)v;
+    }
+  }
+}
+
+}  // namespace
+
+bool conv1x1_supported(int64_t M, int64_t N, int64_t K) {
+  return M > 0 && N % 64 == 0 && K % 64 == 0 && N >= 64 && K >= 64;
+}
+
+void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                int64_t ldc, hipStream_t st) {
+  const int nmb = (int)cdiv(M, TS_BM);
+  if (N % 128 == 0) {
+    hipLaunchKernelGGL((ts_nt_k<128>), dim3(nmb * (int)(N / 128)), dim3(TS_NT), 0, st, (const bf16*)A,
+                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc);
+  } else {
+    hipLaunchKernelGGL((ts_nt_k<64>), dim3(nmb * (int)(N / 64)), dim3(TS_NT), 0, st, (const bf16*)A,
+                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc);
+  }
+}
+
+int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K) {
+  // ~4 workgroups per CU in total, pixel chunks of at least 1024 rows, at most 256 partials per output
+  const int64_t tiles = (N / 64) * (K / 64);
+  int64_t s = cdiv(256 * 4, tiles);
+  const int64_t max_s = M / 1024;
+  if (s > max_s) s = max_s;
+  if (s > 256) s = 256;
+  if (s < 1) s = 1;
+  return (int)s;
+}
+
+void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
+                int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t st) {
+  const int64_t tiles = (N / 64) * (K / 64);
+  int64_t chunk = cdiv(M, nsplit);
+  chunk = cdiv(chunk, 64) * 64;
+  hipLaunchKernelGGL(ts_tn_k, dim3((int)(tiles * nsplit)), dim3(256), 0, st, (const bf16*)A, (const bf16*)B,
+                     partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk);
+  const int64_t nk = N * K;
+  const dim3 grid((int)cdiv(nk / 4, 16));
+  if (out_dtype == kBF16) {
+    if (accumulate) hipLaunchKernelGGL((ts_reduce_k<bf16, true>), grid, dim3(256), 0, st, partial, (bf16*)C, nk, nsplit);
+    else hipLaunchKernelGGL((ts_reduce_k<bf16, false>), grid, dim3(256), 0, st, partial, (bf16*)C, nk, nsplit);
+  } else {
+    if (accumulate) hipLaunchKernelGGL((ts_reduce_k<float, true>), grid, dim3(256), 0, st, partial, (float*)C, nk, nsplit);
+    else hipLaunchKernelGGL((ts_reduce_k<float, false>), grid, dim3(256), 0, st, partial, (float*)C, nk, nsplit);
+  }
+}
+
+}  // namespace dph

@@ -19,6 +19,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.conv import Conv1x1
 
 
 def conv3x3(cin, cout, stride=1):
@@ -26,7 +27,8 @@ def conv3x3(cin, cout, stride=1):
 
 
 def conv1x1(cin, cout, stride=1):
-    return nn.Conv2d(cin, cout, 1, stride, bias=False)
+    # stride 1: nn.Conv2d-compatible module that runs channels-last bf16 on the CDNA4 GEMM kernels (ops/conv.py)
+    return Conv1x1(cin, cout) if stride == 1 else nn.Conv2d(cin, cout, 1, stride, bias=False)
 
 
 class BasicBlock(nn.Module):

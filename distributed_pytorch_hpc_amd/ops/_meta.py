@@ -101,6 +101,16 @@ def _gemm_tn(C, A, B, accumulate):
     return None
 
 
+@register_fake("dph::ts_gemm_nt")
+def _ts_gemm_nt(A, B):
+    return A.new_empty((A.shape[0], B.shape[0]))
+
+
+@register_fake("dph::ts_gemm_tn_")
+def _ts_gemm_tn(C, A, B, accumulate):
+    return None
+
+
 @register_fake("dph::cross_entropy_fwd")
 def _xent(logits, target, inv_count, ignore_index, grad_inplace, smoothing):
     n = logits.shape[0]

@@ -1,0 +1,83 @@
+"""1x1 convolutions on channels-last activations through the CDNA4 tall-skinny GEMM kernels (csrc/conv1x1.hip).
+
+In NHWC a stride-1, bias-free 1x1 convolution is ``Y[M, Cout] = X[M, Cin] W[Cout, Cin]^T`` with M = N*H*W, and
+its two gradients are ``dX = dY W`` and ``dW = dY^T X`` -- no im2col, no layout change: the channels-last tensor
+IS the row-major [M, C] matrix.  ResNet-50's bottleneck convolutions conv1 / conv3 are of this kind (about 2/3
+of its convolution time, benchmarks/conv_bench.py).  Other convolutions (3x3, strided, the stem) keep MIOpen.
+
+``Conv1x1`` is a drop-in ``nn.Conv2d`` (same parameter, same state dict) that takes the kernel path for bf16
+(or bf16-autocast) channels-last inputs on the GPU with channel counts that are multiples of 64, and falls back
+to ``F.conv2d`` otherwise.  ``DPH_CONV1X1=0`` disables the kernel path (A/B runs).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import _lib
+
+
+def _autocast_bf16(t: torch.Tensor) -> bool:
+    return t.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
+    """[B, C, H, W] (any layout) -> row-major [B*H*W, C] (a view when t is channels-last contiguous)."""
+    return t.permute(0, 2, 3, 1).contiguous().view(-1, t.shape[1])
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        wdtype = w.dtype
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        wb = w.to(torch.bfloat16) if w.dtype != torch.bfloat16 else w
+        B, C, H, W = x.shape
+        x2 = _nhwc2d(x)
+        w2 = wb.view(wb.shape[0], C)
+        y2 = _lib.ops().ts_gemm_nt(x2, w2)                          # [M, Cout]
+        ctx.save_for_backward(x2, w2)
+        ctx.shape, ctx.wdtype = (B, C, H, W), wdtype
+        return y2.view(B, H, W, -1).permute(0, 3, 1, 2)             # channels-last [B, Cout, H, W]
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w2 = ctx.saved_tensors
+        B, C, H, W = ctx.shape
+        dy2 = _nhwc2d(dy.to(torch.bfloat16))                        # [M, Cout]
+        dx = gw = None
+        if ctx.needs_input_grad[0]:
+            dx2 = _lib.ops().ts_gemm_nt(dy2, w2.t().contiguous())    # [M, Cin]
+            dx = dx2.view(B, H, W, C).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            gw = torch.empty((w2.shape[0], C), dtype=ctx.wdtype, device=dy.device)
+            _lib.ops().ts_gemm_tn_(gw, dy2, x2, False)
+            gw = gw.view(w2.shape[0], C, 1, 1)
+        return dx, gw
+
+
+def conv1x1_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    if os.environ.get("DPH_CONV1X1", "1") == "0" or not x.is_cuda or _lib.reference_mode():
+        return False
+    if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)):
+        return False
+    cout, cin = w.shape[0], w.shape[1]
+    return (x.dim() == 4 and cin % 64 == 0 and cout % 64 == 0 and
+            x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0)
+
+
+class Conv1x1(nn.Conv2d):
+    """Stride-1, bias-free 1x1 ``nn.Conv2d`` with the channels-last GEMM kernel path (see module docstring)."""
+
+    def __init__(self, in_channels: int, out_channels: int):
+        super().__init__(in_channels, out_channels, kernel_size=1, stride=1, padding=0, bias=False)
+
+    def forward(self, x):
+        if conv1x1_native_ok(x, self.weight):
+            _lib.require()
+            return _Conv1x1Fn.apply(x, self.weight)
+        return F.conv2d(x, self.weight)
