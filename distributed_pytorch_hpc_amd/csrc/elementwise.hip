@@ -10,27 +10,28 @@ namespace dph {
 // RoPE with interleaved pairs (x[2i], x[2i+1]) rotated by angle pos * theta^(-2i/hd), exactly the
 // view_as_complex formulation of fsdp_tp/llama2_model.py:74-100 (fp32 math, one rounding).
 // Tables cos_t/sin_t are fp32 [S_table, hd/2] precomputed on the host side (no device trig).
-// Each thread rotates 8 consecutive elements = 4 pairs of one (b, s, h) row.
+// One workgroup per (b, s) token row: every head of the row shares one position, so a thread loads its
+// chunk's cos / sin (4 pairs) once and rotates that chunk in H * hd / 8 / 256 heads -- no per-element 64-bit
+// index division (the grid-stride form spent more on index math than on the 16-B loads) and 16-B accesses.
 template <typename T>
 __global__ __launch_bounds__(256) void rope_k(T* __restrict__ x, const float* __restrict__ cos_t,
-                                              const float* __restrict__ sin_t, int64_t B, int64_t S, int64_t H,
-                                              int hd, int64_t sb, int64_t ss, int64_t sh, int64_t pos_offset,
-                                              float sign, int64_t total) {
-  const int cpr = hd >> 3;  // 8-element chunks per head row
+                                              const float* __restrict__ sin_t, int S, int H, int hd, int64_t sb,
+                                              int64_t ss, int64_t sh, int64_t pos_offset, float sign) {
+  const int cpr = hd >> 3;          // 8-element chunks per head row
   const int half = hd >> 1;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int c = (int)(i % cpr);
-    int64_t t = i / cpr;
-    const int64_t h = t % H; t /= H;
-    const int64_t s = t % S;
-    const int64_t b = t / S;
-    T* p = x + b * sb + s * ss + h * sh + c * 8;
-    float v[8];
+  const int row = blockIdx.x;
+  const int b = row / S, s = row - b * S;
+  const int64_t pos = pos_offset + s;
+  T* base = x + (int64_t)b * sb + (int64_t)s * ss;
+  const int n = H * cpr;
+  int c = threadIdx.x % cpr, h = threadIdx.x / cpr;
+  const int hstep = 256 / cpr, cstep = 256 % cpr;
+  f32x4 cs = *reinterpret_cast<const f32x4*>(cos_t + pos * half + c * 4);
+  f32x4 sn = *reinterpret_cast<const f32x4*>(sin_t + pos * half + c * 4);
+  for (int i = threadIdx.x; i < n; i += 256) {
+    T* p = base + (int64_t)h * sh + c * 8;
+    float v[8], o[8];
     Vec8<T>::load(p, v);
-    const int64_t pos = pos_offset + s;
-    const f32x4 cs = *reinterpret_cast<const f32x4*>(cos_t + pos * half + c * 4);
-    const f32x4 sn = *reinterpret_cast<const f32x4*>(sin_t + pos * half + c * 4);
-    float o[8];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float a = v[2 * k], bb = v[2 * k + 1];
@@ -39,22 +40,28 @@ __global__ __launch_bounds__(256) void rope_k(T* __restrict__ x, const float* __
       o[2 * k + 1] = a * sv + bb * cc;
     }
     Vec8<T>::store(p, o);
+    h += hstep;
+    if (cstep) {   // cpr does not divide 256: advance the chunk and reload the table entries
+      c += cstep;
+      if (c >= cpr) { c -= cpr; ++h; }
+      cs = *reinterpret_cast<const f32x4*>(cos_t + pos * half + c * 4);
+      sn = *reinterpret_cast<const f32x4*>(sin_t + pos * half + c * 4);
+    }
   }
 }
 
 void rope_apply(void* x, const float* cos_t, const float* sin_t, int64_t B, int64_t S, int64_t H, int hd,
                 int64_t sb, int64_t ss, int64_t sh, int64_t pos_offset, int inverse, int dtype,
                 hipStream_t stream) {
-  const int64_t total = B * S * H * (hd / 8);
-  if (total == 0) return;
-  const int grid = stream_grid(total, 256);
+  if (B * S * H == 0) return;
   const float sign = inverse ? -1.f : 1.f;
+  const dim3 grid((unsigned)(B * S));
   if (dtype == kBF16)
-    hipLaunchKernelGGL(rope_k<bf16>, dim3(grid), dim3(256), 0, stream, (bf16*)x, cos_t, sin_t, B, S, H, hd, sb, ss,
-                       sh, pos_offset, sign, total);
+    hipLaunchKernelGGL(rope_k<bf16>, grid, dim3(256), 0, stream, (bf16*)x, cos_t, sin_t, (int)S, (int)H, hd, sb,
+                       ss, sh, pos_offset, sign);
   else
-    hipLaunchKernelGGL(rope_k<float>, dim3(grid), dim3(256), 0, stream, (float*)x, cos_t, sin_t, B, S, H, hd, sb,
-                       ss, sh, pos_offset, sign, total);
+    hipLaunchKernelGGL(rope_k<float>, grid, dim3(256), 0, stream, (float*)x, cos_t, sin_t, (int)S, (int)H, hd, sb,
+                       ss, sh, pos_offset, sign);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -122,20 +122,29 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, c
   }
   int buf = 0;
   const float invD = 1.f / (float)D;
-  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
-    const float rs = rstd[r];
-    float xv[CPT][8], g[CPT][8];
-    float dot = 0.f;
+  // rows are software-pipelined: the next row's x / dy loads are issued before this row's block reduction, so
+  // they are in flight across the barrier instead of starting after it
+  auto load_row = [&](int64_t r, float (&xv)[CPT][8], float (&g)[CPT][8], float (&d)[CPT][8]) {
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int idx = (c * 256 + threadIdx.x) * 8;
       if (idx < D) {
         Vec8<T>::load(x + r * D + idx, xv[c]);
         Vec8<T>::load(dy + r * D + idx, g[c]);
+        if (dres) Vec8<T>::load(dres + r * D + idx, d[c]);
       } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) { xv[c][i] = 0.f; g[c][i] = 0.f; }
+        for (int i = 0; i < 8; ++i) { xv[c][i] = 0.f; g[c][i] = 0.f; d[c][i] = 0.f; }
       }
+    }
+  };
+  float xv[CPT][8], g[CPT][8], dr[CPT][8];
+  if ((int64_t)blockIdx.x < rows) load_row(blockIdx.x, xv, g, dr);
+  for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
+    const float rs = rstd[r];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const float xh = xv[c][i] * rs;
@@ -143,6 +152,9 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, c
         dot += g[c][i] * wv[c][i] * xh;
       }
     }
+    float xn[CPT][8], gn[CPT][8], dn[CPT][8];
+    const int64_t rn = r + gridDim.x;
+    if (rn < rows) load_row(rn, xn, gn, dn);
     dot = wave_sum(dot);
     if ((threadIdx.x & 63) == 0) red[buf][threadIdx.x >> 6] = dot;
     __syncthreads();
@@ -159,13 +171,17 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, c
           o[i] = rs * (g[c][i] * wv[c][i] - xh * mdot);
         }
         if (dres) {
-          float d2[8];
-          Vec8<T>::load(dres + r * D + idx, d2);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] += d2[i];
+          for (int i = 0; i < 8; ++i) o[i] += dr[c][i];
         }
         Vec8<T>::store(dx + r * D + idx, o);
       }
+    }
+    if (rn < rows) {
+#pragma unroll
+      for (int c = 0; c < CPT; ++c)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { xv[c][i] = xn[c][i]; g[c][i] = gn[c][i]; dr[c][i] = dn[c][i]; }
     }
   }
 #pragma unroll

@@ -15,7 +15,8 @@ import threading
 import torch
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO_PATH = os.path.join(_PKG, "_C.so")
+# DPH_NATIVE_SO points at another build of the extension (A/B runs of two kernel versions on one box)
+SO_PATH = os.environ.get("DPH_NATIVE_SO") or os.path.join(_PKG, "_C.so")
 
 _lock = threading.Lock()
 _loaded = False
