@@ -93,7 +93,17 @@ def main():
                 tot_dph += cnt * t_conv
         else:
             tot_gemm += cnt * t_conv
-            tot_dph += cnt * t_conv
+            if k == 3 and s == 1:   # implicit-GEMM 3x3 kernels (ops.Conv3x3)
+                from distributed_pytorch_hpc_amd.ops.conv import _Conv3x3Fn
+
+                def dph3_fb():
+                    y = _Conv3x3Fn.apply(xr, wr)
+                    torch.autograd.grad(y, (xr, wr), gy)
+
+                row["dph_fwd_bwd_ms"] = timeit(dph3_fb)
+                tot_dph += cnt * row["dph_fwd_bwd_ms"]
+            else:
+                tot_dph += cnt * t_conv
         rows.append(row)
         print(json.dumps(row), flush=True)
     res = {"batch": B, "resnet50_conv_ms_miopen": tot_conv, "resnet50_conv_ms_1x1_as_gemm": tot_gemm,

@@ -1,4 +1,5 @@
-// 1x1 convolutions on channels-last activations = tall-skinny GEMMs, for CDNA4 (gfx950).
+// 1x1 (and 3x3 / stride 1, as implicit GEMMs) convolutions on channels-last activations = tall-skinny GEMMs,
+// for CDNA4 (gfx950).
 //
 // In NHWC a stride-1 1x1 convolution is Y[M, Cout] = X[M, Cin] W[Cout, Cin]^T with M = N*H*W pixels (up to
 // 802,816 for ResNet-50 at B=256) and Cin, Cout in 64..2048: far more rows than columns and memory-bound
@@ -42,10 +43,14 @@ constexpr int TS_BM = 128, TS_BK = 64, TS_NT = 256;
 constexpr int TS_BROW = 72;   // B slab row: 64 bf16 + 8 pad (144 B: 16 consecutive rows hit 16 distinct 16-B slots)
 constexpr int TS_KF = TS_BK / 16;   // MFMA k-steps (A fragments) per K-step
 
-template <int BN>
+// C3: 3x3 / stride 1 / pad 1 convolution as an implicit GEMM over the channels-last input A [M = N*H*W, Cin]:
+// K = 9 * Cin is tap-major (k = tap * Cin + c), and the A row of output pixel m for tap (dy, dx) is the input
+// pixel m + (dy-1) * W + (dx-1), or zero when that falls outside the image (padding).  A K-step never straddles
+// two taps (Cin % 64 == 0), so the shift is one wave-uniform offset per K-step plus a per-lane bounds check.
+template <int BN, bool C3>
 __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                  bf16* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                 int64_t ldb, int64_t ldc) {
+                                                 int64_t ldb, int64_t ldc, int H, int W, int Cin) {
   constexpr int NT = BN / 32;                        // 32-column tiles per wave
   constexpr int BCH = BN * (TS_BK / 8) / TS_NT;      // 16-B B chunks per thread per K-step (BN=128: 4)
   constexpr int CROW = BN + 8;                       // epilogue LDS row (bf16)
@@ -62,6 +67,24 @@ __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, con
   // A: this lane's row (clamped for the ragged last block; its results are not stored)
   const int arow = min(m0 + wid * 32 + l32, M - 1);
   const bf16* ap = A + (int64_t)arow * lda + 8 * h;
+  int xw = 0, yh = 0;
+  if constexpr (C3) {
+    xw = arow % W;
+    yh = (arow / W) % H;
+  }
+  // A fragment f of the K-step starting at column ko (zero for a padding tap)
+  auto load_a = [&](int ko, int f) -> bf16x8 {
+    if constexpr (!C3) {
+      return *reinterpret_cast<const bf16x8*>(ap + ko + 16 * f);
+    } else {
+      const int tap = ko / Cin, cb = ko - tap * Cin;
+      const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+      const bool ok = (unsigned)(yh + dy) < (unsigned)H && (unsigned)(xw + dx) < (unsigned)W;
+      const bf16* pp = ok ? ap + (int64_t)(dy * W + dx) * lda + cb + 16 * f : ap;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(pp);
+      return ok ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  };
   // B staging: chunk c of thread t -> slab row (t*BCH + c) / 8, 16-B column chunk (t*BCH + c) % 8
   const bf16* bp[BCH];
   int bdst[BCH];
@@ -81,7 +104,7 @@ __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, con
   const int nks = K / TS_BK;
   bf16x8 a[TS_KF];
 #pragma unroll
-  for (int f = 0; f < TS_KF; ++f) a[f] = *reinterpret_cast<const bf16x8*>(ap + 16 * f);
+  for (int f = 0; f < TS_KF; ++f) a[f] = load_a(0, f);
   bf16x8 bst[BCH];
 #pragma unroll
   for (int c = 0; c < BCH; ++c) bst[c] = *reinterpret_cast<const bf16x8*>(bp[c]);
@@ -97,7 +120,7 @@ __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, con
     if (ks + 1 < nks) {   // prefetch the next K-step (A into registers, B into staging registers)
       const int ko = (ks + 1) * TS_BK;
 #pragma unroll
-      for (int f = 0; f < TS_KF; ++f) na[f] = *reinterpret_cast<const bf16x8*>(ap + ko + 16 * f);
+      for (int f = 0; f < TS_KF; ++f) na[f] = load_a(ko, f);
 #pragma unroll
       for (int c = 0; c < BCH; ++c) bst[c] = *reinterpret_cast<const bf16x8*>(bp[c] + ko);
     }
@@ -145,9 +168,12 @@ __device__ __forceinline__ bf16x4 tr_read(const char* p) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
+// C3: 3x3 weight gradient, K = 9 * Cin tap-major; B rows (input pixels) are shifted by the output tile's tap and
+// zero outside the image, A (output-gradient) rows are not shifted.
+template <bool C3>
 __global__ __launch_bounds__(256) void ts_tn_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                float* __restrict__ P, int M, int N, int K, int64_t lda,
-                                               int64_t ldb, int chunk) {
+                                               int64_t ldb, int chunk, int H, int W, int Cin) {
   constexpr int TP = 64;   // pixels per step (rows of the staged slabs)
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TP * TW_ROWB];   // [buf][A|B][64 rows][192 B]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -162,6 +188,13 @@ __global__ __launch_bounds__(256) void ts_tn_k(const bf16* __restrict__ A, const
   const int s = lin / ntile, tile = lin % ntile;
   const int n0 = (tile / tk) * 64, k0 = (tile % tk) * 64;
   const int mbeg = s * chunk, mend = min(M, mbeg + chunk);
+  int bcol = k0, dy = 0, dx = 0;
+  if constexpr (C3) {
+    const int tap = k0 / Cin;
+    bcol = k0 - tap * Cin;
+    dy = tap / 3 - 1;
+    dx = tap - (tap / 3) * 3 - 1;
+  }
 
   // staging: thread t copies 16 B of rows t>>3 and 32 + (t>>3) of the 64-row slab, chunk t&7, for A and B
   const int srow = threadIdx.x >> 3, sch = threadIdx.x & 7;
@@ -181,7 +214,15 @@ __global__ __launch_bounds__(256) void ts_tn_k(const bf16* __restrict__ A, const
     for (int u = 0; u < 2; ++u) {
       const int rr = m + srow + 32 * u, row = min(rr, M - 1);
       va[u] = *reinterpret_cast<const bf16x8*>(A + (int64_t)row * lda + n0 + sch * 8);
-      vb[u] = *reinterpret_cast<const bf16x8*>(B + (int64_t)row * ldb + k0 + sch * 8);
+      bool bok = true;
+      int brow = row;
+      if constexpr (C3) {
+        const int xw = row % W, yh = (row / W) % H;
+        bok = (unsigned)(yh + dy) < (unsigned)H && (unsigned)(xw + dx) < (unsigned)W;
+        brow = bok ? row + dy * W + dx : row;
+      }
+      vb[u] = *reinterpret_cast<const bf16x8*>(B + (int64_t)brow * ldb + bcol + sch * 8);
+      if (!bok) vb[u] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
       if (rr >= mend) {   // rows past this chunk contribute zero
         va[u] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
         vb[u] = va[u];
@@ -259,15 +300,21 @@ bool conv1x1_supported(int64_t M, int64_t N, int64_t K) {
 }
 
 void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, hipStream_t st) {
+                int64_t ldc, hipStream_t st, int H, int W) {
   const int nmb = (int)cdiv(M, TS_BM);
+  const bool c3 = H > 0;
+  const int cin = c3 ? (int)(K / 9) : 0;
+#define DPH_TS_NT(BN_, C3_)                                                                                     \
+  hipLaunchKernelGGL((ts_nt_k<BN_, C3_>), dim3(nmb * (int)(N / BN_)), dim3(TS_NT), 0, st, (const bf16*)A,       \
+                     (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin)
   if (N % 128 == 0) {
-    hipLaunchKernelGGL((ts_nt_k<128>), dim3(nmb * (int)(N / 128)), dim3(TS_NT), 0, st, (const bf16*)A,
-                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc);
+    if (c3) DPH_TS_NT(128, true);
+    else DPH_TS_NT(128, false);
   } else {
-    hipLaunchKernelGGL((ts_nt_k<64>), dim3(nmb * (int)(N / 64)), dim3(TS_NT), 0, st, (const bf16*)A,
-                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc);
+    if (c3) DPH_TS_NT(64, true);
+    else DPH_TS_NT(64, false);
   }
+#undef DPH_TS_NT
 }
 
 int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K) {
@@ -282,12 +329,16 @@ int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K) {
 }
 
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
-                int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t st) {
+                int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t st, int H, int W) {
   const int64_t tiles = (N / 64) * (K / 64);
   int64_t chunk = cdiv(M, nsplit);
   chunk = cdiv(chunk, 64) * 64;
-  hipLaunchKernelGGL(ts_tn_k, dim3((int)(tiles * nsplit)), dim3(256), 0, st, (const bf16*)A, (const bf16*)B,
-                     partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk);
+  if (H > 0)
+    hipLaunchKernelGGL((ts_tn_k<true>), dim3((int)(tiles * nsplit)), dim3(256), 0, st, (const bf16*)A,
+                       (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, H, W, (int)(K / 9));
+  else
+    hipLaunchKernelGGL((ts_tn_k<false>), dim3((int)(tiles * nsplit)), dim3(256), 0, st, (const bf16*)A,
+                       (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0, 0);
   const int64_t nk = N * K;
   const dim3 grid((int)cdiv(nk / 4, 16));
   if (out_dtype == kBF16) {

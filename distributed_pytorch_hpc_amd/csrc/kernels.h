@@ -103,11 +103,13 @@ void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_
 // ts_gemm_nt: C[M, N] = A[M, K] B[N, K]^T (N, K % 64 == 0).  ts_gemm_tn: C[N, K] (+)= A[M, N]^T B[M, K] through
 // fp32 partials over nsplit pixel chunks (partial: nsplit * N * K floats; ts_gemm_tn_splits picks nsplit).
 bool conv1x1_supported(int64_t M, int64_t N, int64_t K);
+// H, W > 0: 3x3 / stride-1 / pad-1 implicit GEMM over a channels-last [M = n*H*W, K/9] input (K tap-major).
 void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, hipStream_t stream);
+                int64_t ldc, hipStream_t stream, int H = 0, int W = 0);
 int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K);
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
-                int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t stream);
+                int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t stream, int H = 0,
+                int W = 0);
 
 // Fused BatchNorm(train) [+ residual] [+ ReLU] on channels-last [M, C] activations (C power of two, 8..2048).
 // Workspaces (fp32): forward 2*G*C + G, backward 2*G*C + 3*C floats with G = bn_partial_blocks(M, C).

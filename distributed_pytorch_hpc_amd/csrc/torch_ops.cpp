@@ -363,13 +363,17 @@ void gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate) {
 
 // ------------------------------------------------------------------------------------------------ 1x1 conv GEMMs
 // C[M, N] = A[M, K] B[N, K]^T, bf16, row-major (channels-last 1x1 convolution forward / input gradient).
-Tensor ts_gemm_nt(const Tensor& A, const Tensor& B) {
+// H, W > 0: 3x3 / stride-1 / pad-1 convolution as implicit GEMM, A = channels-last input [n*H*W, Cin],
+// B = weights [Cout, 9 * Cin] (tap-major).
+Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W) {
   check_cuda(A, "A");
   c10::DeviceGuard g(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "ts_gemm_nt: 2-D operands required");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "ts_gemm_nt: bf16 operands");
-  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  const int64_t M = A.size(0), N = B.size(0);
+  const int64_t K = H > 0 ? 9 * A.size(1) : A.size(1);
   TORCH_CHECK(B.size(1) == K, "ts_gemm_nt: K mismatch");
+  TORCH_CHECK(H == 0 || (W > 0 && M % (H * W) == 0), "ts_gemm_nt: rows must be a multiple of H * W");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
               "ts_gemm_nt: row-major operands with 16-B aligned rows required");
   TORCH_CHECK(dph::conv1x1_supported(M, N, K), "ts_gemm_nt: need N, K % 64 == 0 (got ", N, ", ", K, ")");
@@ -377,18 +381,20 @@ Tensor ts_gemm_nt(const Tensor& A, const Tensor& B) {
   check_align16(B, "B");
   Tensor C = at::empty({M, N}, A.options());
   dph::ts_gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
-                  cur_stream());
+                  cur_stream(), (int)H, (int)W);
   return C;
 }
 
 // C[N, K] (+)= A[M, N]^T B[M, K] (1x1 convolution weight gradient, split over pixel chunks).
-void ts_gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate) {
+// H, W > 0: 3x3 weight gradient, C [N, 9 * K_in] tap-major, B = channels-last input [n*H*W, K_in].
+void ts_gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate, int64_t H, int64_t W) {
   check_cuda(A, "A");
   c10::DeviceGuard g(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "ts_gemm_tn: 2-D operands required");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "ts_gemm_tn: bf16 A / B");
-  const int64_t M = A.size(0), N = A.size(1), K = B.size(1);
+  const int64_t M = A.size(0), N = A.size(1), K = H > 0 ? 9 * B.size(1) : B.size(1);
   TORCH_CHECK(B.size(0) == M && C.size(0) == N && C.size(1) == K && C.is_contiguous(), "ts_gemm_tn: shape mismatch");
+  TORCH_CHECK(H == 0 || (W > 0 && M % (H * W) == 0), "ts_gemm_tn: rows must be a multiple of H * W");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
               "ts_gemm_tn: row-major operands with 16-B aligned rows required");
   TORCH_CHECK(dph::conv1x1_supported(M, N, K), "ts_gemm_tn: need N, K % 64 == 0 (got ", N, ", ", K, ")");
@@ -398,7 +404,7 @@ void ts_gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate) {
   const int ns = dph::ts_gemm_tn_splits(M, N, K);
   Tensor part = at::empty({(int64_t)ns * N * K}, A.options().dtype(at::kFloat));
   dph::ts_gemm_tn(A.data_ptr(), B.data_ptr(), part.data_ptr<float>(), C.data_ptr(), M, N, K, A.stride(0),
-                  B.stride(0), ns, dt_code(C), accumulate, cur_stream());
+                  B.stride(0), ns, dt_code(C), accumulate, cur_stream(), (int)H, (int)W);
 }
 
 // Select the wgrad kernel's MFMA shape (16 or 32; anything else re-reads DPH_WGRAD_MFMA); returns the active shape.
@@ -607,8 +613,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
   m.def("gemm_tn_mfma_(int shape) -> int", &gemm_tn_mfma_);   // no tensor argument: catch-all kernel
-  m.def("ts_gemm_nt(Tensor A, Tensor B) -> Tensor");
-  m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
+  m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0) -> Tensor");
+  m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
         "float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor)");

@@ -19,11 +19,12 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import Conv1x1
+from ..ops.conv import Conv1x1, Conv3x3
 
 
 def conv3x3(cin, cout, stride=1):
-    return nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+    # stride 1: channels-last implicit-GEMM kernel path (ops/conv.py); strided 3x3 convolutions stay on MIOpen
+    return Conv3x3(cin, cout) if stride == 1 else nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
 
 
 def conv1x1(cin, cout, stride=1):

@@ -102,12 +102,12 @@ def _gemm_tn(C, A, B, accumulate):
 
 
 @register_fake("dph::ts_gemm_nt")
-def _ts_gemm_nt(A, B):
+def _ts_gemm_nt(A, B, H=0, W=0):
     return A.new_empty((A.shape[0], B.shape[0]))
 
 
 @register_fake("dph::ts_gemm_tn_")
-def _ts_gemm_tn(C, A, B, accumulate):
+def _ts_gemm_tn(C, A, B, accumulate, H=0, W=0):
     return None
 
 

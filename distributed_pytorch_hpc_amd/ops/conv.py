@@ -1,13 +1,22 @@
-"""1x1 convolutions on channels-last activations through the CDNA4 tall-skinny GEMM kernels (csrc/conv1x1.hip).
+"""1x1 and 3x3 convolutions on channels-last activations through the CDNA4 tall-skinny GEMM kernels
+(csrc/conv1x1.hip).
 
 In NHWC a stride-1, bias-free 1x1 convolution is ``Y[M, Cout] = X[M, Cin] W[Cout, Cin]^T`` with M = N*H*W, and
 its two gradients are ``dX = dY W`` and ``dW = dY^T X`` -- no im2col, no layout change: the channels-last tensor
 IS the row-major [M, C] matrix.  ResNet-50's bottleneck convolutions conv1 / conv3 are of this kind (about 2/3
-of its convolution time, benchmarks/conv_bench.py).  Other convolutions (3x3, strided, the stem) keep MIOpen.
+of its convolution time, benchmarks/conv_bench.py).  Strided convolutions and the 7x7 stem keep MIOpen.
 
 ``Conv1x1`` is a drop-in ``nn.Conv2d`` (same parameter, same state dict) that takes the kernel path for bf16
 (or bf16-autocast) channels-last inputs on the GPU with channel counts that are multiples of 64, and falls back
 to ``F.conv2d`` otherwise.  ``DPH_CONV1X1=0`` disables the kernel path (A/B runs).
+
+``Conv3x3`` does the same for stride-1 / padding-1 3x3 convolutions as implicit GEMMs (K = 9 * Cin, tap-major,
+input rows shifted per tap with zero padding in the kernel): forward and input gradient on the same kernel
+(the input gradient is a 3x3 convolution of dY with the spatially flipped, channel-transposed weight), weight
+gradient on the split-pixel kernel with the input shifted per output tap.  It is opt-in (``DPH_CONV3X3=1``):
+measured 0.51-0.63 ms vs MIOpen's 0.38-0.53 ms per ResNet-50 shape (fwd + bwd, B=256,
+profiles/conv_bench_with_3x3.json) -- the one-barrier-per-K-step structure tops out near 0.5 PFLOP/s on these
+compute-heavier shapes, so MIOpen keeps the 3x3 convolutions by default.
 """
 from __future__ import annotations
 
@@ -58,6 +67,63 @@ class _Conv1x1Fn(torch.autograd.Function):
             _lib.ops().ts_gemm_tn_(gw, dy2, x2, False)
             gw = gw.view(w2.shape[0], C, 1, 1)
         return dx, gw
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        wdtype = w.dtype
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        wb = w.to(torch.bfloat16)
+        B, C, H, W = x.shape
+        cout = wb.shape[0]
+        x2 = _nhwc2d(x)
+        wk = wb.permute(0, 2, 3, 1).reshape(cout, 9 * C)             # [Cout, (kh, kw, Cin)]
+        y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W)
+        ctx.save_for_backward(x2, wb)
+        ctx.shape, ctx.wdtype = (B, C, H, W), wdtype
+        return y2.view(B, H, W, cout).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wb = ctx.saved_tensors
+        B, C, H, W = ctx.shape
+        cout = wb.shape[0]
+        dy2 = _nhwc2d(dy.to(torch.bfloat16))
+        dx = gw = None
+        if ctx.needs_input_grad[0]:
+            # dX = conv3x3(dY, W') with W'[ci, (kh, kw), co] = W[co, ci, 2 - kh, 2 - kw]
+            wf = wb.flip(2, 3).permute(1, 2, 3, 0).reshape(C, 9 * cout)
+            dx = _lib.ops().ts_gemm_nt(dy2, wf, H, W).view(B, H, W, C).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            gk = torch.empty((cout, 9 * C), dtype=ctx.wdtype, device=dy.device)
+            _lib.ops().ts_gemm_tn_(gk, dy2, x2, False, H, W)
+            gw = gk.view(cout, 3, 3, C).permute(0, 3, 1, 2).contiguous()
+        return dx, gw
+
+
+def conv3x3_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    if os.environ.get("DPH_CONV3X3", "0") != "1" or not x.is_cuda or _lib.reference_mode():
+        return False
+    if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)):
+        return False
+    cout, cin = w.shape[0], w.shape[1]
+    return (x.dim() == 4 and cin % 64 == 0 and cout % 64 == 0 and
+            x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0)
+
+
+class Conv3x3(nn.Conv2d):
+    """Stride-1, padding-1, bias-free 3x3 ``nn.Conv2d`` with the channels-last implicit-GEMM kernel path."""
+
+    def __init__(self, in_channels: int, out_channels: int):
+        super().__init__(in_channels, out_channels, kernel_size=3, stride=1, padding=1, bias=False)
+
+    def forward(self, x):
+        if conv3x3_native_ok(x, self.weight):
+            _lib.require()
+            return _Conv3x3Fn.apply(x, self.weight)
+        return F.conv2d(x, self.weight, padding=1)
 
 
 def conv1x1_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:

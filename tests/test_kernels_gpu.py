@@ -568,3 +568,31 @@ def test_bottleneck_conv1x1_path_matches_miopen_gradients(dph_native, monkeypatc
 
     e_miopen, e_dph = err(g0), err(g1)
     assert e_dph < 1.5 * e_miopen + 1e-3, (e_dph, e_miopen)
+
+
+@pytest.mark.parametrize("B,C,Co,H,W", [(2, 64, 64, 14, 14), (3, 128, 64, 7, 9), (1, 64, 192, 5, 5)])
+@pytest.mark.parametrize("autocast", [False, True])
+def test_conv3x3_module_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W, autocast):
+    """ops.Conv3x3 (implicit-GEMM kernels, zero padding at every image border) vs F.conv2d in fp32: output,
+    input gradient and weight gradient; images smaller than a 128-row tile and non-square."""
+    from distributed_pytorch_hpc_amd.ops.conv import Conv3x3, conv3x3_native_ok
+
+    monkeypatch.setenv("DPH_CONV3X3", "1")   # opt-in path
+    torch.manual_seed(5)
+    conv = Conv3x3(C, Co).to(DEV)
+    if not autocast:
+        conv = conv.to(torch.bfloat16)
+    x = torch.randn(B, C, H, W, device=DEV, dtype=torch.float32 if autocast else torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        assert conv3x3_native_ok(x, conv.weight)
+        y = conv(x)
+    g = torch.randn_like(y.float())
+    y.float().backward(g)
+    xr = x.detach().to(torch.bfloat16).float().requires_grad_()
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_()
+    yr = torch.nn.functional.conv2d(xr, wr, padding=1)
+    yr.backward(g)
+    assert rel_err(y, yr) < 8e-3
+    assert rel_err(x.grad, xr.grad) < 1e-2
+    assert rel_err(conv.weight.grad, wr.grad) < 1e-2
