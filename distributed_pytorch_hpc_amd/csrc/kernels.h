@@ -43,13 +43,14 @@ void gelu_bwd(const void* dy, const void* x, void* dx, int64_t n, int approximat
 // ---- Fused AdamW over flat buffers (torch.optim.AdamW semantics, decoupled weight decay) ----
 //   master/m/v: fp32 [n]; grad: grad_dtype [n]; param_out (optional): param_dtype [n] (rounded copy of master).
 //   grad_scale_ptr (optional device fp32 scalar) multiplies the gradient (global-norm clipping, 1/world).
+//   hyper (optional device fp32 [lr, step]) overrides lr and the bias corrections (HIP-graph capturable steps).
 void adamw_step(float* master, float* m, float* v, const void* grad, void* param_out, int64_t n, float lr,
                 float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2,
-                const float* grad_scale_ptr, int grad_dtype, int param_dtype, hipStream_t stream);
+                const float* grad_scale_ptr, const float* hyper, int grad_dtype, int param_dtype, hipStream_t stream);
 // ---- Fused SGD with momentum (torch.optim.SGD semantics) ----
 void sgd_step(float* master, float* momentum_buf, const void* grad, void* param_out, int64_t n, float lr,
               float momentum, float dampening, float weight_decay, int nesterov, int first_step,
-              const float* grad_scale_ptr, int grad_dtype, int param_dtype, hipStream_t stream);
+              const float* grad_scale_ptr, const float* hyper, int grad_dtype, int param_dtype, hipStream_t stream);
 // sum of squares of a flat buffer, accumulated (atomically, fp32) into *out (caller zeroes it).
 void sumsq(const void* x, int64_t n, float* out, int dtype, hipStream_t stream);
 

@@ -4,6 +4,11 @@
 // Each thread handles 4 consecutive elements per iteration: 16-B fp32 loads/stores for master/m/v,
 // 8-B loads for bf16 grads and 8-B stores of the bf16 working copy of the parameter.
 // Per element AdamW moves 2 (g) + 12 (p,m,v in) + 12 (out) + 2 (bf16 param) = 28 B: HBM bound.
+//
+// Graph-capturable form: with `hyper` (device fp32 [lr, step]) the learning rate and the step count are read from
+// device memory instead of kernel arguments, so one captured HIP graph replays every optimizer step (the bias
+// corrections 1 - beta^step are formed here; the step is incremented on the device by the caller's captured
+// add, the learning rate written by the host before each replay -- runtime/graphs.py).
 #include "dph_common.h"
 #include "kernels.h"
 
@@ -39,8 +44,13 @@ __global__ __launch_bounds__(256) void adamw_k(float* __restrict__ master, float
                                                float* __restrict__ v, const G* __restrict__ grad,
                                                P* __restrict__ pout, int64_t n, float lr, float b1, float b2,
                                                float eps, float wd, float bc1, float bc2,
-                                               const float* __restrict__ gscale) {
+                                               const float* __restrict__ gscale, const float* __restrict__ hyper) {
   const float gs = gscale ? *gscale : 1.f;
+  if (hyper) {
+    lr = hyper[0];
+    bc1 = 1.f - powf(b1, hyper[1]);
+    bc2 = 1.f - powf(b2, hyper[1]);
+  }
   const float decay = 1.f - lr * wd;
   const float step_size = lr / bc1;
   const float inv_bc2_sqrt = 1.f / sqrtf(bc2);
@@ -82,8 +92,12 @@ template <typename G, typename P, bool HAS_OUT>
 __global__ __launch_bounds__(256) void sgd_k(float* __restrict__ master, float* __restrict__ buf,
                                              const G* __restrict__ grad, P* __restrict__ pout, int64_t n, float lr,
                                              float mom, float damp, float wd, int nesterov, int first,
-                                             const float* __restrict__ gscale) {
+                                             const float* __restrict__ gscale, const float* __restrict__ hyper) {
   const float gs = gscale ? *gscale : 1.f;
+  if (hyper) {
+    lr = hyper[0];
+    first = hyper[1] == 1.f;
+  }
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     float p = master[i];
     float d = (float)grad[i] * gs + wd * p;
@@ -121,12 +135,12 @@ __global__ __launch_bounds__(256) void sumsq_k(const T* __restrict__ x, int64_t 
 
 void adamw_step(float* master, float* m, float* v, const void* grad, void* param_out, int64_t n, float lr,
                 float beta1, float beta2, float eps, float wd, float bc1, float bc2, const float* gscale,
-                int grad_dtype, int param_dtype, hipStream_t stream) {
+                const float* hyper, int grad_dtype, int param_dtype, hipStream_t stream) {
   if (n == 0) return;
   const int grid = stream_grid((n + 3) / 4, 256);
 #define AD(G, P, OUT)                                                                                  \
   hipLaunchKernelGGL((adamw_k<G, P, OUT>), dim3(grid), dim3(256), 0, stream, master, m, v, (const G*)grad, \
-                     (P*)param_out, n, lr, beta1, beta2, eps, wd, bc1, bc2, gscale)
+                     (P*)param_out, n, lr, beta1, beta2, eps, wd, bc1, bc2, gscale, hyper)
   if (grad_dtype == kBF16) {
     if (!param_out) AD(bf16, bf16, false);
     else if (param_dtype == kBF16) AD(bf16, bf16, true);
@@ -140,13 +154,13 @@ void adamw_step(float* master, float* m, float* v, const void* grad, void* param
 }
 
 void sgd_step(float* master, float* buf, const void* grad, void* param_out, int64_t n, float lr, float mom,
-              float damp, float wd, int nesterov, int first, const float* gscale, int grad_dtype, int param_dtype,
-              hipStream_t stream) {
+              float damp, float wd, int nesterov, int first, const float* gscale, const float* hyper,
+              int grad_dtype, int param_dtype, hipStream_t stream) {
   if (n == 0) return;
   const int grid = stream_grid(n, 256);
 #define SG(G, P, OUT)                                                                                  \
   hipLaunchKernelGGL((sgd_k<G, P, OUT>), dim3(grid), dim3(256), 0, stream, master, buf, (const G*)grad, \
-                     (P*)param_out, n, lr, mom, damp, wd, nesterov, first, gscale)
+                     (P*)param_out, n, lr, mom, damp, wd, nesterov, first, gscale, hyper)
   if (grad_dtype == kBF16) {
     if (!param_out) SG(bf16, bf16, false);
     else if (param_dtype == kBF16) SG(bf16, bf16, true);

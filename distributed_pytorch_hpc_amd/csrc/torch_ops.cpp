@@ -167,9 +167,18 @@ Tensor gelu_bwd(const Tensor& dy, const Tensor& x, bool tanh_form) {
 }
 
 // ------------------------------------------------------------------------------------------------ optimizers
+// device [lr, step] of a graph-capturable optimizer step (nullptr: the scalar arguments apply)
+static const float* hyper_ptr(const c10::optional<Tensor>& hyper, const Tensor& master) {
+  if (!hyper.has_value()) return nullptr;
+  TORCH_CHECK(hyper->scalar_type() == at::kFloat && hyper->numel() >= 2 && hyper->is_contiguous() &&
+                  hyper->device() == master.device(),
+              "optimizer hyper: fp32 [lr, step] on the parameters' device expected");
+  return hyper->data_ptr<float>();
+}
+
 void adamw_step_(Tensor master, Tensor m, Tensor v, const Tensor& grad, const c10::optional<Tensor>& param_out,
                  double lr, double b1, double b2, double eps, double wd, double bc1, double bc2,
-                 const c10::optional<Tensor>& grad_scale) {
+                 const c10::optional<Tensor>& grad_scale, const c10::optional<Tensor>& hyper) {
   c10::DeviceGuard g(master.device());
   const int64_t n = master.numel();
   TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
@@ -188,14 +197,15 @@ void adamw_step_(Tensor master, Tensor m, Tensor v, const Tensor& grad, const c1
     pdt = dt_code(*param_out);
   }
   const float* gs = grad_scale.has_value() ? grad_scale->data_ptr<float>() : nullptr;
+  const float* hp = hyper_ptr(hyper, master);
   dph::adamw_step(master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), grad.data_ptr(), pout, n,
-                  (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, gs, dt_code(grad),
-                  pdt, cur_stream());
+                  (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (float)bc1, (float)bc2, gs, hp,
+                  dt_code(grad), pdt, cur_stream());
 }
 
 void sgd_step_(Tensor master, Tensor buf, const Tensor& grad, const c10::optional<Tensor>& param_out, double lr,
                double momentum, double dampening, double wd, bool nesterov, bool first_step,
-               const c10::optional<Tensor>& grad_scale) {
+               const c10::optional<Tensor>& grad_scale, const c10::optional<Tensor>& hyper) {
   c10::DeviceGuard g(master.device());
   const int64_t n = master.numel();
   TORCH_CHECK(master.scalar_type() == at::kFloat && buf.scalar_type() == at::kFloat, "sgd: fp32 master/buf");
@@ -207,9 +217,10 @@ void sgd_step_(Tensor master, Tensor buf, const Tensor& grad, const c10::optiona
     pdt = dt_code(*param_out);
   }
   const float* gs = grad_scale.has_value() ? grad_scale->data_ptr<float>() : nullptr;
+  const float* hp = hyper_ptr(hyper, master);
   dph::sgd_step(master.data_ptr<float>(), buf.data_ptr<float>(), grad.data_ptr(), pout, n, (float)lr,
-                (float)momentum, (float)dampening, (float)wd, nesterov ? 1 : 0, first_step ? 1 : 0, gs, dt_code(grad),
-                pdt, cur_stream());
+                (float)momentum, (float)dampening, (float)wd, nesterov ? 1 : 0, first_step ? 1 : 0, gs, hp,
+                dt_code(grad), pdt, cur_stream());
 }
 
 void sumsq_(const Tensor& x, Tensor out) {
@@ -598,9 +609,11 @@ TORCH_LIBRARY(dph, m) {
   m.def("gelu_fwd(Tensor x, bool tanh_form) -> Tensor");
   m.def("gelu_bwd(Tensor dy, Tensor x, bool tanh_form) -> Tensor");
   m.def("adamw_step_(Tensor(a!) master, Tensor(b!) m, Tensor(c!) v, Tensor grad, Tensor(d!)? param_out, float lr, "
-        "float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, Tensor? grad_scale) -> ()");
+        "float beta1, float beta2, float eps, float weight_decay, float bc1, float bc2, Tensor? grad_scale, "
+        "Tensor? hyper=None) -> ()");
   m.def("sgd_step_(Tensor(a!) master, Tensor(b!) buf, Tensor grad, Tensor(d!)? param_out, float lr, float momentum, "
-        "float dampening, float weight_decay, bool nesterov, bool first_step, Tensor? grad_scale) -> ()");
+        "float dampening, float weight_decay, bool nesterov, bool first_step, Tensor? grad_scale, "
+        "Tensor? hyper=None) -> ()");
   m.def("sumsq_(Tensor x, Tensor(a!) out) -> ()");
   m.def("cross_entropy_fwd(Tensor(a!) logits, Tensor target, Tensor inv_count, int ignore_index, bool grad_inplace, "
         "float smoothing) -> (Tensor, Tensor)");

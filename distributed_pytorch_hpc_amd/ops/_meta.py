@@ -58,12 +58,13 @@ def _gelu_bwd(dy, x, tanh_form):
 
 
 @register_fake("dph::adamw_step_")
-def _adamw(master, m, v, grad, param_out, lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale):
+def _adamw(master, m, v, grad, param_out, lr, beta1, beta2, eps, weight_decay, bc1, bc2, grad_scale, hyper=None):
     return None
 
 
 @register_fake("dph::sgd_step_")
-def _sgd(master, buf, grad, param_out, lr, momentum, dampening, weight_decay, nesterov, first_step, grad_scale):
+def _sgd(master, buf, grad, param_out, lr, momentum, dampening, weight_decay, nesterov, first_step, grad_scale,
+         hyper=None):
     return None
 
 

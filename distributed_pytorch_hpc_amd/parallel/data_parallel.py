@@ -60,6 +60,48 @@ class OptimConfig:
     dampening: float = 0.0
     nesterov: bool = False
     max_grad_norm: Optional[float] = None
+    # read lr / step from device memory (HIP-graph capturable step; runtime/graphs.py turns it on)
+    capturable: bool = False
+
+
+class StepHyper:
+    """Device-resident ``[lr, step]`` read by the fused optimizer kernels in capturable mode (csrc/optim.hip
+    ``hyper``): a HIP graph captured around ``engine.step()`` then replays the right learning rate and bias
+    corrections every step.  Eagerly the host writes both values (two tiny fills, no sync); inside a capture
+    only the device-side ``step += 1`` is recorded, and the host sets the learning rate before each replay."""
+
+    def __init__(self, device):
+        self.t = torch.zeros(2, dtype=torch.float32, device=device)
+
+    def advance(self, lr: float, step: int):
+        if self.t.is_cuda and torch.cuda.is_current_stream_capturing():
+            self.t[1:2].add_(1.0)
+        else:
+            self.t[0:1].fill_(lr)
+            self.t[1:2].fill_(float(step))
+
+    def set_lr(self, lr: float):
+        self.t[0:1].fill_(lr)
+
+
+def _hyper_for(engine, native: bool):
+    """The engine's StepHyper tensor (advanced for this step) when its optimizer is capturable and native."""
+    cfg = engine.opt_cfg
+    if not (cfg.capturable and native):
+        return None
+    if engine._hyper is None:
+        engine._hyper = StepHyper(engine.device)
+    engine._hyper.advance(cfg.lr, engine.step_count)
+    return engine._hyper.t
+
+
+def graph_replay_prologue(engine, lr: Optional[float] = None):
+    """Host side of one replayed step: the learning rate goes to device memory, the host step count follows."""
+    if lr is not None:
+        engine.opt_cfg.lr = lr
+    if engine._hyper is not None:
+        engine._hyper.set_lr(engine.opt_cfg.lr)
+    engine.step_count += 1
 
 
 class _Bucket:
@@ -178,6 +220,7 @@ class DataParallelEngine:
         self.opt_state: list[torch.Tensor] = []
         self.opt_cfg: Optional[OptimConfig] = None
         self.step_count = 0
+        self._hyper: Optional[StepHyper] = None
         self._sync_enabled = True
         self._next_launch = 0
         self._callback_queued = False
@@ -349,6 +392,7 @@ class DataParallelEngine:
             self._gscale.copy_(torch.clamp(cfg.max_grad_norm / (norm + 1e-6), max=1.0) / self.world)
             self.last_grad_norm = norm
         native = _lib.use_native(self.master)
+        hyper = _hyper_for(self, native)
         b1, b2 = cfg.betas
         bc1, bc2 = 1 - b1 ** self.step_count, 1 - b2 ** self.step_count
         # Sharded: update and re-gather in FORWARD order (buckets are laid out in backward order).  RCCL runs the
@@ -366,7 +410,7 @@ class DataParallelEngine:
                 m, v = self.opt_state[0][sl], self.opt_state[1][sl]
                 if native:
                     _lib.ops().adamw_step_(master, m, v, grad, pout, cfg.lr, b1, b2, cfg.eps, cfg.weight_decay,
-                                           bc1, bc2, self._gscale)
+                                           bc1, bc2, self._gscale, hyper=hyper)
                 else:
                     optim_ref.adamw_reference_(master, m, v, grad, cfg.lr, b1, b2, cfg.eps, cfg.weight_decay, bc1,
                                                bc2, self._gscale)
@@ -375,7 +419,8 @@ class DataParallelEngine:
                 buf = self.opt_state[0][sl] if cfg.momentum else self.opt_state[0]
                 if native:
                     _lib.ops().sgd_step_(master, buf, grad, pout, cfg.lr, cfg.momentum, cfg.dampening,
-                                         cfg.weight_decay, cfg.nesterov, self.step_count == 1, self._gscale)
+                                         cfg.weight_decay, cfg.nesterov, self.step_count == 1, self._gscale,
+                                         hyper=hyper)
                 else:
                     optim_ref.sgd_reference_(master, buf, grad, cfg.lr, cfg.momentum, cfg.dampening,
                                              cfg.weight_decay, cfg.nesterov, self.step_count == 1, self._gscale)

@@ -34,7 +34,7 @@ from torch import nn
 from ..ops import _lib
 from ..train import optim as optim_ref
 from ..utils.flat import ALIGN, align_up
-from .data_parallel import DataParallelEngine, MixedPrecision, OptimConfig, _EngineOptimizer
+from .data_parallel import DataParallelEngine, MixedPrecision, OptimConfig, _EngineOptimizer, _hyper_for
 from .linear import convert_linears_, join_wgrad_stream, wgrad_stream
 
 
@@ -175,6 +175,7 @@ class ZeRO3Engine:
         self.opt_state: list[torch.Tensor] = []
         self.opt_cfg: Optional[OptimConfig] = None
         self.step_count = 0
+        self._hyper = None
         self._gscale = torch.full((1,), 1.0 / self._dp_world(), dtype=torch.float32, device=self.device)
         self._sync_enabled = True
         self._callback_queued = False
@@ -354,13 +355,14 @@ class ZeRO3Engine:
             norm = sq.sqrt() / self._dp_world()
             self._gscale.copy_(torch.clamp(cfg.max_grad_norm / (norm + 1e-6), max=1.0) / self._dp_world())
         native = _lib.use_native(self.master)
+        hyper = _hyper_for(self, native)
         b1, b2 = cfg.betas
         bc1, bc2 = 1 - b1 ** self.step_count, 1 - b2 ** self.step_count
         if cfg.name == "adamw":
             m, v = self.opt_state
             if native:
                 _lib.ops().adamw_step_(self.master, m, v, self.grad_shard, self.param_shard, cfg.lr, b1, b2, cfg.eps,
-                                       cfg.weight_decay, bc1, bc2, self._gscale)
+                                       cfg.weight_decay, bc1, bc2, self._gscale, hyper=hyper)
             else:
                 optim_ref.adamw_reference_(self.master, m, v, self.grad_shard, cfg.lr, b1, b2, cfg.eps,
                                            cfg.weight_decay, bc1, bc2, self._gscale)
@@ -369,7 +371,8 @@ class ZeRO3Engine:
             buf = self.opt_state[0]
             if native:
                 _lib.ops().sgd_step_(self.master, buf, self.grad_shard, self.param_shard, cfg.lr, cfg.momentum,
-                                     cfg.dampening, cfg.weight_decay, cfg.nesterov, self.step_count == 1, self._gscale)
+                                     cfg.dampening, cfg.weight_decay, cfg.nesterov, self.step_count == 1, self._gscale,
+                                     hyper=hyper)
             else:
                 optim_ref.sgd_reference_(self.master, buf, self.grad_shard, cfg.lr, cfg.momentum, cfg.dampening,
                                          cfg.weight_decay, cfg.nesterov, self.step_count == 1, self._gscale)

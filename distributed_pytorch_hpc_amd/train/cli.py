@@ -25,6 +25,9 @@ def common_parser(description: str) -> argparse.ArgumentParser:
     ap.add_argument("--log-dir", default=None, help="per-rank stdout/stderr files (utils/redirect.py)")
     ap.add_argument("--metrics-file", default=None, help="JSONL metrics sink (rank 0)")
     ap.add_argument("--json-out", default=None, help="write the final summary JSON here (rank 0)")
+    ap.add_argument("--cuda-graph", action="store_true",
+                    help="replay each training step as one captured HIP graph after 3 eager warm-up steps "
+                         "(runtime/graphs.py; single GPU, fixed shapes)")
     return ap
 
 

@@ -69,7 +69,8 @@ class Trainer:
                  sampler=None, snapshot_path: Optional[str] = None, save_every: int = 0, log_every: int = 10,
                  max_steps_per_epoch: Optional[int] = None, dp_world: Optional[int] = None,
                  autocast_dtype: Optional[torch.dtype] = None, grad_clip: Optional[float] = None,
-                 scheduler=None, metrics_file: Optional[str] = None, profiler=None):
+                 scheduler=None, metrics_file: Optional[str] = None, profiler=None, cuda_graph: bool = False,
+                 graph_warmup: int = 3):
         self.model = model
         self.optimizer = optimizer
         self.loader = train_loader
@@ -88,6 +89,10 @@ class Trainer:
         self.scheduler = scheduler
         self.metrics = MetricsLogger(metrics_file, self.rank)
         self.profiler = profiler
+        # whole-step HIP graph (runtime/graphs.py): eager for `graph_warmup` steps, then capture + replay
+        self.cuda_graph = bool(cuda_graph) and self.device.type == "cuda"
+        self.graph_warmup = graph_warmup
+        self._graphed = None
         self.epochs_run = 0
         self.global_step = 0
         self.history: list[EpochStats] = []
@@ -126,9 +131,11 @@ class Trainer:
     def _autocast(self):
         if self.autocast_dtype is None:
             return contextlib.nullcontext()
-        return torch.autocast(device_type=self.device.type, dtype=self.autocast_dtype)
+        # a captured step must not keep autocast's per-step weight-cast cache (it would pin the capture's copies)
+        return torch.autocast(device_type=self.device.type, dtype=self.autocast_dtype,
+                              cache_enabled=not self.cuda_graph)
 
-    def _run_batch(self, source, targets) -> torch.Tensor:
+    def _step_body(self, source, targets) -> torch.Tensor:
         self.optimizer.zero_grad(set_to_none=True)
         with self._autocast():
             output = self.model(source)
@@ -137,10 +144,22 @@ class Trainer:
         if self.grad_clip is not None and self.engine is None:
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip)
         self.optimizer.step()
+        return loss.detach()
+
+    def _run_batch(self, source, targets) -> torch.Tensor:
+        if self.cuda_graph and torch.is_tensor(source) and torch.is_tensor(targets):
+            if self._graphed is None:
+                from ..runtime.graphs import GraphedStep
+
+                self._graphed = GraphedStep(self._step_body, optimizer=self.optimizer, warmup=self.graph_warmup)
+            lr = self.optimizer.param_groups[0]["lr"] if hasattr(self.optimizer, "param_groups") else None
+            loss = self._graphed(source, targets, lr=lr if isinstance(lr, float) else None)
+        else:
+            loss = self._step_body(source, targets)
         if self.scheduler is not None:
             self.scheduler.step()
         self.global_step += 1
-        return loss.detach()
+        return loss
 
     def _run_epoch(self, epoch: int) -> EpochStats:
         if self.sampler is not None and hasattr(self.sampler, "set_epoch"):

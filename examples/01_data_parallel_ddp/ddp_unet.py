@@ -58,7 +58,8 @@ def main(argv=None):
     trainer = Trainer(ddp, opt, data, latitude_weighted_mse, dev, max_steps_per_epoch=args.steps_per_epoch,
                       log_every=max(args.steps_per_epoch // 4, 1),
                       autocast_dtype=torch.bfloat16 if args.amp else None, snapshot_path=args.snapshot_path,
-                      save_every=args.save_every, metrics_file=args.metrics_file)
+                      save_every=args.save_every, metrics_file=args.metrics_file,
+                      cuda_graph=args.cuda_graph)
     summary = trainer.train(args.epochs)
     summary.update(example="ddp_unet", world=world, params=sum(p.numel() for p in model.parameters()))
     finish(args, summary, rank)

@@ -67,7 +67,8 @@ def main(argv=None):
         return F.cross_entropy(out.float(), y)
 
     trainer = Trainer(fsdp, opt, train, loss_fn, dev, max_steps_per_epoch=args.steps_per_epoch,
-                      log_every=max(args.steps_per_epoch // 2, 1), metrics_file=args.metrics_file)
+                      log_every=max(args.steps_per_epoch // 2, 1), metrics_file=args.metrics_file,
+                      cuda_graph=args.cuda_graph)
     for epoch in range(args.epochs):
         st = trainer._run_epoch(epoch)
         trainer.history.append(st)

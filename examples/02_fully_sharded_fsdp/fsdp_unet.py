@@ -50,7 +50,8 @@ def main(argv=None):
                          lat=args.lat, lon=args.lon, dtype=torch.bfloat16 if args.bf16 else torch.float32)
     trainer = Trainer(fsdp, opt, data, lambda o, t: latitude_weighted_mse(o.float(), t.float()), dev,
                       max_steps_per_epoch=args.steps_per_epoch, log_every=max(args.steps_per_epoch // 4, 1),
-                      metrics_file=args.metrics_file)
+                      metrics_file=args.metrics_file,
+                      cuda_graph=args.cuda_graph)
     summary = trainer.train(args.epochs)
     if args.checkpoint:
         sd = fsdp.full_state_dict(rank0_only=True, offload_to_cpu=True)

@@ -102,7 +102,8 @@ def main(argv=None):
     trainer = Trainer(wrapped, opt, _CL(), loss_fn, dev, max_steps_per_epoch=args.steps_syn,
                       log_every=max(args.steps_syn // 2, 1), autocast_dtype=autocast,
                       snapshot_path=args.resume if not args.use_fsdp else None,
-                      save_every=1 if args.resume and not args.use_fsdp else 0, metrics_file=args.metrics_file)
+                      save_every=1 if args.resume and not args.use_fsdp else 0, metrics_file=args.metrics_file,
+                      cuda_graph=args.cuda_graph)
     if rank == 0:
         print(f"[resnet_benchmark] {args.arch} {n_params:,} params | world {world} | "
               f"{'FSDP' if args.use_fsdp else 'DDP'} | per-rank batch {args.batch_size} | {env_report(backend)}",

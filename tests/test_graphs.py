@@ -1,0 +1,225 @@
+"""Whole-step HIP graphs (runtime/graphs.py) and the capturable optimizer mode (csrc/optim.hip ``hyper``).
+
+GPU tests compare a graphed training run against the same run done eagerly: parameters after N steps must
+agree (the graph replays the same kernels on the same data, so the match is near bit-exact).  CPU tests cover
+the host-side logic.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_pytorch_hpc_amd.parallel.data_parallel import (DataParallelEngine, MixedPrecision, OptimConfig,
+                                                                StepHyper, graph_replay_prologue)
+
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+# ------------------------------------------------------------------------------------------------ CPU
+def test_step_hyper_eager_writes_lr_and_step():
+    h = StepHyper("cpu")
+    h.advance(0.25, 3)
+    assert h.t.tolist() == [0.25, 3.0]
+    h.set_lr(0.5)
+    assert h.t.tolist() == [0.5, 3.0]
+
+
+def test_graph_replay_prologue_advances_host_state():
+    m = torch.nn.Linear(8, 4)
+    eng = DataParallelEngine(m)
+    eng.configure_optimizer(OptimConfig("adamw", lr=1e-3, capturable=True))
+    eng._hyper = StepHyper("cpu")
+    graph_replay_prologue(eng, 0.125)
+    assert eng.step_count == 1 and eng.opt_cfg.lr == 0.125 and eng._hyper.t[0].item() == 0.125
+
+
+def test_capturable_engine_on_cpu_matches_default():
+    """Off the GPU the capturable flag changes nothing (reference optimizer path, host scalars)."""
+    torch.manual_seed(0)
+    a, b = torch.nn.Linear(16, 8), torch.nn.Linear(16, 8)
+    b.load_state_dict(a.state_dict())
+    ea, eb = DataParallelEngine(a), DataParallelEngine(b)
+    ea.configure_optimizer(OptimConfig("adamw", lr=1e-2))
+    eb.configure_optimizer(OptimConfig("adamw", lr=1e-2, capturable=True))
+    x = torch.randn(4, 16)
+    for _ in range(3):
+        for m, e in ((a, ea), (b, eb)):
+            e.zero_grad()
+            m(x).pow(2).mean().backward()
+            e.step()
+    assert torch.equal(a.weight, b.weight)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU error")
+def test_graphed_step_needs_gpu():
+    from distributed_pytorch_hpc_amd.runtime.graphs import GraphedStep
+
+    with pytest.raises(RuntimeError, match="GPU"):
+        GraphedStep(lambda x: x)
+
+
+# ------------------------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["adamw", "sgd"])
+def test_optimizer_hyper_matches_scalars(dph_native, name):
+    """Device [lr, step] gives the same update as the host-scalar arguments, step after step."""
+    torch.manual_seed(0)
+    n = 10_003
+    p0 = torch.randn(n, device=DEV)
+    st = [[torch.zeros(n, device=DEV) for _ in range(2)] for _ in range(2)]
+    ps = [p0.clone(), p0.clone()]
+    hyper = torch.zeros(2, device=DEV)
+    lr, b1, b2 = 3e-3, 0.9, 0.95
+    for step in range(1, 5):
+        g = torch.randn(n, device=DEV, dtype=torch.bfloat16)
+        hyper.copy_(torch.tensor([lr, float(step)]))
+        if name == "adamw":
+            dph_native.adamw_step_(ps[0], st[0][0], st[0][1], g, None, lr, b1, b2, 1e-8, 0.1, 1 - b1 ** step,
+                                   1 - b2 ** step, None)
+            dph_native.adamw_step_(ps[1], st[1][0], st[1][1], g, None, 123.0, b1, b2, 1e-8, 0.1, 0.5, 0.5, None,
+                                   hyper=hyper)
+        else:
+            dph_native.sgd_step_(ps[0], st[0][0], g, None, lr, 0.9, 0.0, 1e-4, False, step == 1, None)
+            dph_native.sgd_step_(ps[1], st[1][0], g, None, 123.0, 0.9, 0.0, 1e-4, False, False, None, hyper=hyper)
+    assert rel_err(ps[1], ps[0]) < 1e-6
+
+
+def _run(model, opt_cfg, batches, graphed, warmup=2, fsdp=False, autocast=None):
+    from distributed_pytorch_hpc_amd.runtime.graphs import GraphedStep
+
+    if fsdp:
+        from distributed_pytorch_hpc_amd.parallel.fsdp import FSDP
+
+        wrapped = FSDP(model, mixed_precision=MixedPrecision(torch.bfloat16, torch.bfloat16, torch.bfloat16))
+        opt = wrapped.make_optimizer(opt_cfg.name, lr=opt_cfg.lr, momentum=opt_cfg.momentum,
+                                     weight_decay=opt_cfg.weight_decay)
+        eng = opt.engine
+    else:
+        eng = DataParallelEngine(model)
+        eng.configure_optimizer(opt_cfg)
+        wrapped = model
+
+        class _O:
+            engine = eng
+            param_groups = [{"lr": opt_cfg.lr}]
+
+            def zero_grad(self, set_to_none=True):
+                eng.zero_grad()
+
+            def step(self):
+                eng.step(lr=self.param_groups[0]["lr"])
+
+        opt = _O()
+
+    def step_fn(x, y):
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=autocast, enabled=autocast is not None, cache_enabled=False):
+            out = wrapped(x)
+        loss = F.cross_entropy(out.float().reshape(-1, out.shape[-1]), y.reshape(-1))
+        loss.backward()
+        opt.step()
+        return loss.detach()
+
+    runner = GraphedStep(step_fn, optimizer=opt, warmup=warmup) if graphed else None
+    losses = []
+    for i, (x, y) in enumerate(batches):
+        lr = opt_cfg.lr * (1.0 - 0.05 * i)   # a schedule: the graph must pick up the host's lr every replay
+        if graphed:
+            losses.append(runner(x, y, lr=lr).clone())
+        else:
+            opt.param_groups[0]["lr"] = lr
+            if fsdp:
+                eng.opt_cfg.lr = lr
+            losses.append(step_fn(x, y))
+    torch.cuda.synchronize()
+    if graphed:
+        assert runner.captured
+    return [p.detach().float().clone() for p in model.parameters()], torch.stack(losses), eng
+
+
+@pytest.mark.gpu
+def test_graphed_mlp_adamw_matches_eager(dph_native):
+    def make():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.GELU(), torch.nn.Linear(512, 64)).to(DEV)
+
+    torch.manual_seed(1)
+    batches = [(torch.randn(128, 256, device=DEV), torch.randint(0, 64, (128,), device=DEV)) for _ in range(7)]
+    cfg = lambda: OptimConfig("adamw", lr=1e-3, weight_decay=0.01)   # noqa: E731
+    pe, le, ee = _run(make(), cfg(), batches, graphed=False)
+    pg, lg, eg = _run(make(), cfg(), batches, graphed=True)
+    assert eg.step_count == ee.step_count == len(batches)
+    assert eg._hyper is not None and eg._hyper.t[1].item() == len(batches)
+    for a, b in zip(pg, pe):
+        assert rel_err(a, b) < 1e-5
+    assert rel_err(lg, le) < 1e-5
+
+
+@pytest.mark.gpu
+def test_graphed_llama_tiny_matches_eager(dph_native):
+    from distributed_pytorch_hpc_amd.models.llama2 import build_llama
+
+    torch.manual_seed(2)
+    batches = []
+    for _ in range(6):
+        t = torch.randint(0, 512, (2, 129), device=DEV)
+        batches.append((t[:, :-1].contiguous(), t[:, 1:].contiguous()))
+    cfg = lambda: OptimConfig("adamw", lr=3e-4, weight_decay=0.1)   # noqa: E731
+    pe, le, _ = _run(build_llama("tiny", device=DEV), cfg(), batches, graphed=False)
+    pg, lg, _ = _run(build_llama("tiny", device=DEV), cfg(), batches, graphed=True)
+    for a, b in zip(pg, pe):
+        assert rel_err(a, b) < 1e-3
+    assert rel_err(lg, le) < 1e-3
+
+
+@pytest.mark.gpu
+def test_graphed_resnet_fsdp_bf16_matches_eager(dph_native):
+    """FSDP units (world 1) + bf16 channels-last ResNet: MIOpen and framework conv / batch-norm kernels, SGD."""
+    from distributed_pytorch_hpc_amd.models import resnet
+
+    def make():
+        torch.manual_seed(0)
+        return resnet("resnet18", num_classes=10, cifar_stem=True).to(DEV).to(memory_format=torch.channels_last)
+
+    torch.manual_seed(3)
+    batches = [(torch.randn(16, 3, 32, 32, device=DEV, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last), torch.randint(0, 10, (16,), device=DEV)) for _ in range(6)]
+    cfg = lambda: OptimConfig("sgd", lr=0.002, momentum=0.9, weight_decay=1e-4)   # noqa: E731
+    # MIOpen's bf16 convolutions are not bit-reproducible run to run: two eager runs set the noise floor
+    pe, le, _ = _run(make(), cfg(), batches, graphed=False, fsdp=True)
+    pe2, le2, _ = _run(make(), cfg(), batches, graphed=False, fsdp=True)
+    pg, lg, _ = _run(make(), cfg(), batches, graphed=True, fsdp=True)
+    floor = max(rel_err(a, b) for a, b in zip(pe2, pe))
+    assert max(rel_err(a, b) for a, b in zip(pg, pe)) < max(3 * floor, 2e-2)
+    assert rel_err(lg, le) < max(3 * rel_err(le2, le), 1e-2)
+
+
+@pytest.mark.gpu
+def test_trainer_cuda_graph(dph_native):
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import DDP
+    from distributed_pytorch_hpc_amd.train import Trainer
+
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.ReLU(), torch.nn.Linear(128, 10)).to(DEV)
+    ddp = DDP(model)
+    opt = ddp.make_optimizer("adamw", lr=1e-2)
+    x = torch.randn(32, 64, device=DEV)
+    y = torch.randint(0, 10, (32,), device=DEV)
+
+    class _L:
+        def __iter__(self):
+            return self
+
+        def __next__(self):
+            return x, y
+
+    tr = Trainer(ddp, opt, _L(), F.cross_entropy, DEV, max_steps_per_epoch=10, log_every=0, cuda_graph=True,
+                 graph_warmup=2)
+    tr.train(2)
+    assert tr._graphed is not None and tr._graphed.captured
+    assert ddp.engine.step_count == 20
+    assert tr.history[-1].loss < tr.history[0].loss
