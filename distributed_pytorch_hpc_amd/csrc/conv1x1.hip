@@ -14,11 +14,13 @@
 //             stores are whole 16-B row segments.  N-tiles of one row block run on one XCD (L2 reuse of A).
 //   ts_tn_k   P[s][N, K] = sum over the s-th pixel chunk of A[m, N]^T B[m, K]  (weight gradient, A = dY, B = X)
 //             64 x 64 output tile per workgroup (4 waves x 32x32), pixels are the reduction dim: 64-pixel slabs
-//             of both operands are register-staged into LDS rows of 192 B (4 consecutive rows cover all 64
-//             banks) and read back transposed with ds_read_b64_tr_b16; split over pixel chunks with fp32
-//             partials, then
+//             of both operands are register-staged into unpadded 128-B LDS rows whose 16-B chunks are XOR-
+//             swizzled by bit 1 of the row (the 4-row x 64-B footprint of a half-wave's transposed read then
+//             covers all 64 banks once) and read back with ds_read_b64_tr_b16 (32 KB of LDS per workgroup); split
+//             over pixel chunks sized to fill one resident round of workgroups, fp32 partials, then
 //   ts_reduce_k  dW = sum_s P[s] (+ dW) in the weight's dtype (deterministic: fixed summation order).
 #include <algorithm>
+#include <cstdlib>
 
 #include "dph_common.h"
 #include "kernels.h"
@@ -161,7 +163,10 @@ __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, con
 }
 
 // ---- weight gradient: P[s][n][k] = sum_{m in chunk s} A[m][n] B[m][k] ----
-constexpr int TW_ROWB = 192;   // LDS row stride in bytes (64 bf16 + 32 pad): rows 4 apart cover all 64 banks
+constexpr int TW_ROWB = 128;   // LDS row: 64 bf16, 16-B chunks XOR-swizzled by tw_swz(row)
+
+// chunk swizzle of LDS row r: rows 2 apart (same bank half) read complementary 64-B halves
+__device__ __forceinline__ int tw_swz(int r) { return ((r >> 1) & 1) << 2; }
 
 __device__ __forceinline__ bf16x4 tr_read(const char* p) {
   i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_c*)p);
@@ -175,7 +180,7 @@ __global__ __launch_bounds__(256) void ts_tn_k(const bf16* __restrict__ A, const
                                                float* __restrict__ P, int M, int N, int K, int64_t lda,
                                                int64_t ldb, int chunk, int H, int W, int Cin) {
   constexpr int TP = 64;   // pixels per step (rows of the staged slabs)
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TP * TW_ROWB];   // [buf][A|B][64 rows][192 B]
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TP * TW_ROWB];   // [buf][A|B][64 rows][128 B]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wi = wid >> 1, wj = wid & 1;             // wave's 32x32 sub-tile of the 64x64 output tile
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
@@ -198,12 +203,14 @@ __global__ __launch_bounds__(256) void ts_tn_k(const bf16* __restrict__ A, const
 
   // staging: thread t copies 16 B of rows t>>3 and 32 + (t>>3) of the 64-row slab, chunk t&7, for A and B
   const int srow = threadIdx.x >> 3, sch = threadIdx.x & 7;
-  const int sdst = srow * TW_ROWB + sch * 16;
+  const int sdst = srow * TW_ROWB + (sch ^ tw_swz(srow)) * 16;   // row srow + 32 has the same swizzle
   // transposed-read offsets: lane 4q+p of 16-lane group g reads row (r0 + q), columns c0 + 4p .. +3 where the
-  // group's half h = g >> 1 selects rows 8h.. (k-steps) and g & 1 the column half of the 32-wide operand
-  const int hh = g >> 1, c0 = 16 * (g & 1);
-  const int toffA = (8 * hh + q) * TW_ROWB + (wi * 32 + c0 + 4 * p) * 2;
-  const int toffB = (8 * hh + q) * TW_ROWB + (wj * 32 + c0 + 4 * p) * 2;
+  // group's half h = g >> 1 selects rows 8h.. (k-steps) and g & 1 the column half of the 32-wide operand; the
+  // rows read (16kk + 8h + q, +4) all swizzle like q
+  const int hh = g >> 1;
+  const int tch = 2 * (g & 1) + (p >> 1), tin = 8 * (p & 1);
+  const int toffA = (8 * hh + q) * TW_ROWB + (((wi * 4 + tch) ^ tw_swz(q)) << 4) + tin;
+  const int toffB = (8 * hh + q) * TW_ROWB + (((wj * 4 + tch) ^ tw_swz(q)) << 4) + tin;
 
   f32x16 acc;
 #pragma unroll
@@ -318,14 +325,32 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 }
 
 int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K) {
-  // ~4 workgroups per CU in total, pixel chunks of at least 1024 rows, at most 256 partials per output
+  // Pick the number of pixel chunks s by a small cost model in units of one 64-pixel step:
+  //   rounds(s) * (steps per chunk + 2)  +  s * N * K / 9e5
+  // rounds = ceil(tiles * s / R) resident rounds of workgroups (R = 4 per CU x 256 CUs; a 1026-workgroup grid
+  // runs a second, nearly empty round -- measured 1.4x slower than 1017), +2 steps of per-workgroup prologue /
+  // epilogue, and the fp32 partials written here and re-read by ts_reduce_k (~1.5 us per 8 MB at the measured
+  // 1.47 us per step).  Chunks of at least 1024 rows, partial buffers of at most max(256 splits, 64 MB).
+  // DPH_TS_TN_WGS overrides R.
+  static const int R = [] {
+    const char* e = getenv("DPH_TS_TN_WGS");
+    return e ? atoi(e) : 256 * 4;
+  }();
   const int64_t tiles = (N / 64) * (K / 64);
-  int64_t s = cdiv(256 * 4, tiles);
-  const int64_t max_s = M / 1024;
-  if (s > max_s) s = max_s;
-  if (s > 256) s = 256;
-  if (s < 1) s = 1;
-  return (int)s;
+  const int64_t smax = std::max<int64_t>(1, std::min<int64_t>(M / 1024,
+                                                              std::max<int64_t>(256, (int64_t(64) << 20) / (N * K * 4))));
+  int64_t best_s = 1;
+  double best = 1e300;
+  for (int64_t s = 1; s <= smax; ++s) {
+    const int64_t steps = cdiv(cdiv(M, s), 64);
+    const int64_t rounds = cdiv(tiles * s, (int64_t)R);
+    const double cost = (double)rounds * (double)(steps + 2) + (double)s * (double)(N * K) / 9e5;
+    if (cost < best) {
+      best = cost;
+      best_s = s;
+    }
+  }
+  return (int)best_s;
 }
 
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
