@@ -314,7 +314,14 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 #define DPH_TS_NT(BN_, C3_)                                                                                     \
   hipLaunchKernelGGL((ts_nt_k<BN_, C3_>), dim3(nmb * (int)(N / BN_)), dim3(TS_NT), 0, st, (const bf16*)A,       \
                      (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin)
-  if (N % 128 == 0) {
+  // 128-wide column tiles whenever N allows: 64-wide tiles double the workgroup count of the short-grid 14x14 / 7x7
+  // layers but measured 1.1-1.4x slower there too (profiles/conv_nt_bn_ab.log).  DPH_TS_NT_BN=64 forces them.
+  static const int force_bn = [] {
+    const char* e = getenv("DPH_TS_NT_BN");
+    return e ? atoi(e) : 0;
+  }();
+  const bool wide = N % 128 == 0 && force_bn != 64;
+  if (wide) {
     if (c3) DPH_TS_NT(128, true);
     else DPH_TS_NT(128, false);
   } else {
