@@ -19,6 +19,12 @@
 //   dQ^T += K^T dS^T with dS^T consumed from the accumulator.
 // The split costs 2 extra MFMA products (S, dP recomputed) but removes the fp32 dQ atomics that bound a
 // fused kernel at ~1.3 TB/s of atomic traffic (MI355X_MICROARCH.md 'Global float atomics').
+//
+// Dropout (DROP instantiations, 4-wave workgroups): the keep decision of element (query, key) is a counter hash,
+// so the forward and both backward kernels regenerate the same mask without storing it: the forward drops
+// P after the row sum (the softmax normaliser is the undropped one) and scales O by 1/(1-p); dK/dV uses the
+// dropped, rescaled P for dV and dS = P (Z dP / (1-p) - delta) for dK; dQ the same dS.  This is the
+// nn.MultiheadAttention(dropout=...) path of the pipeline transformer (03_pipeline_training.py:57-58,70).
 #include <cstdlib>
 
 #include "dph_common.h"
@@ -29,6 +35,26 @@ namespace dph {
 typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
 
 __device__ __forceinline__ float exp2_(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// 32-bit integer mix (lowbias32 finalizer)
+__device__ __forceinline__ unsigned attn_mix(unsigned x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+// per-(seed, batch*head, query) row key, then keep(query, key) = mix(row_key ^ key * C) >= threshold
+__device__ __forceinline__ unsigned attn_row_key(unsigned seed, unsigned bh, unsigned q) {
+  return attn_mix(seed ^ attn_mix(bh * 0x9e3779b1u + q * 0x85ebca77u));
+}
+__device__ __forceinline__ bool attn_keep(unsigned row_key, unsigned key, unsigned thr) {
+  return attn_mix(row_key ^ (key * 0xc2b2ae3du)) >= thr;
+}
+__device__ __forceinline__ unsigned attn_drop_thr(float p) {
+  return (unsigned)fminf(p * 4294967296.f, 4294967040.f);
+}
 
 // Byte offset of 16-B chunk `ch` of row `row` in an LDS image whose rows hold NC 16-B chunks.
 // Rows are packed into 256-B lines; chunk slots are XOR-permuted per line so that (a) 32 lanes reading
@@ -197,7 +223,7 @@ __device__ __forceinline__ int wave_tile_count(int ntiles, int q0w, int off) {
 // tile max exceeds it by more than RESCALE_THR (FA4-style lazy rescaling): p is then bounded by 2^THR,
 // harmless for the bf16 P operand and the fp32 accumulators, and the exact result is recovered by the
 // final 1/l.  The rescale branch is wave-uniform (ballot), so steady-state tiles skip 16*DT multiplies.
-template <int HD, bool CAUSAL, int NW>
+template <int HD, bool CAUSAL, int NW, bool DROP = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
   using Plan = KVTilePlan<HD, 64 * NW>;
   constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
@@ -240,6 +266,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
   const f32x16 zacc = {};
   float m = -INFINITY, lsum = 0.f;  // m: running max of s*sl2; lsum: this half-wave's partial row sum
   const float sl2 = p.scale * 1.4426950408889634f;
+  const unsigned drk = DROP ? attn_row_key(p.drop_seed, (unsigned)(b * p.Hq + hq), (unsigned)myq) : 0u;
+  const unsigned dthr = DROP ? attn_drop_thr(p.drop_p) : 0u;
 
   if (ntiles > 0) plan.stage(smem, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
   __syncthreads();
@@ -288,6 +316,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
       ls1 += s[1][r];
     }
     lsum += ls0 + ls1;
+    if constexpr (DROP) {   // after the row sum: the normaliser is the undropped softmax's
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (!attn_keep(drk, (unsigned)(k0 + sub * 32 + acc_row(r, h)), dthr)) s[sub][r] = 0.f;
+    }
 
     // ---- P^T as B operand: k-step ks covers keys 16*ks .. 16*ks+15 of the tile ----
     bf16x8 pf[4];
@@ -319,7 +354,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
   // ---- epilogue: O = O^T / l, lse ----
   lsum = half_sum(lsum);
   if (myq < p.Sq) {
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    const float inv = lsum > 0.f ? (DROP ? 1.f / (1.f - p.drop_p) : 1.f) / lsum : 0.f;
     bf16* op = (bf16*)p.o + (int64_t)b * p.o_sb + (int64_t)myq * p.o_ss + (int64_t)hq * p.o_sh;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
@@ -370,7 +405,7 @@ __global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ o, 
 // of the GQA group x 32-row query tiles (double-buffered Q / dO LDS images, one barrier per tile).
 // S and dP are computed with the key on the lane, so P and dS are directly the B operands of
 // dV^T += dO^T P and dK^T += Q^T dS: no LDS round trip, no atomics.
-template <int HD, bool CAUSAL, int NW>
+template <int HD, bool CAUSAL, int NW, bool DROP = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams P) {
   constexpr int NT = 64 * NW, BNK = 32 * NW, BMQ = 32, NC = HD / 8, KS = HD / 16, DT = HD / 32;
   constexpr int QIMG = BMQ * HD * 2;        // Q / dO tile image [32 q][HD]
@@ -379,12 +414,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
   // lines apart, so the wave's K rows reuse the Q-image offsets plus a constant.
   constexpr bool KSHARE = NC >= 8;
   constexpr bool TRADD = NC >= 16;          // +16 rows is a pure byte offset for the transposed reads
-  // smem: K | Q0 | dO0 | Q1 | dO1 | -lse2[2][32] | delta[2][32]
+  // smem: K | Q0 | dO0 | Q1 | dO1 | -lse2[2][32] | delta[2][32] | dropout row keys[2][32]
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Kimg = smem;
   char* Qbuf = smem + KIMG;
   float* lse_s = reinterpret_cast<float*>(Qbuf + 4 * QIMG);
   float* del_s = lse_s + 2 * BMQ;
+  unsigned* rk_s = reinterpret_cast<unsigned*>(del_s + 2 * BMQ);
 
   const AttnParams& p = P.f;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
@@ -440,6 +476,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
   const int total = nqt_head * grp;
 
   float st_lse = 0.f, st_del = 0.f;
+  unsigned st_rk = 0u;
+  const unsigned dthr = DROP ? attn_drop_thr(p.drop_p) : 0u;
+  const float drs = DROP ? 1.f / (1.f - p.drop_p) : 1.f;
   auto stage = [&](int it, int buf) {
     const int hq = hk * grp + it / nqt_head;
     const int qt0 = qstart + (it % nqt_head) * BMQ;
@@ -453,12 +492,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
       const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + q;
       st_lse = q < p.Sq ? -p.lse[idx] * 1.4426950408889634f : 0.f;  // -lse in log2 units
       st_del = q < p.Sq ? P.delta[idx] : 0.f;
+      if constexpr (DROP) st_rk = attn_row_key(p.drop_seed, (unsigned)(b * p.Hq + hq), (unsigned)q);
     }
   };
   auto stage_scalars = [&](int buf) {
     if (threadIdx.x < BMQ) {
       lse_s[buf * BMQ + threadIdx.x] = st_lse;
       del_s[buf * BMQ + threadIdx.x] = st_del;
+      if constexpr (DROP) rk_s[buf * BMQ + threadIdx.x] = st_rk;
     }
   };
 
@@ -497,8 +538,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
       for (int r = 0; r < 16; ++r) {
         const int qr = acc_row(r, h);
         const float pv = exp2_(fmaf(s[r], sl2, ls[qr]));
-        s[r] = pv;
-        dp[r] = pv * (dp[r] - ds[qr]);
+        if constexpr (DROP) {   // dV from the dropped, rescaled P; dS = P (Z dP / (1-p) - delta)
+          const bool keep = attn_keep(rk_s[buf * BMQ + qr], (unsigned)mykey, dthr);
+          s[r] = keep ? pv * drs : 0.f;
+          dp[r] = pv * ((keep ? dp[r] * drs : 0.f) - ds[qr]);
+        } else {
+          s[r] = pv;
+          dp[r] = pv * (dp[r] - ds[qr]);
+        }
       }
       bf16x8 pb[2], sb[2];
 #pragma unroll
@@ -545,7 +592,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
 // query (lane & 31).  Per 64-key tile: S^T = K Q^T and dP^T = V dO^T (A = K / V rows from LDS, B = Q^T / dO^T
 // fragments in registers), P^T = exp2(S^T c - lse) and dS^T = P^T (dP^T - delta) lane-locally (lse and delta
 // are one scalar per lane), then dQ^T += K^T dS^T with dS^T consumed straight from the accumulator.
-template <int HD, bool CAUSAL, int NW>
+template <int HD, bool CAUSAL, int NW, bool DROP = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P) {
   using Plan = KVTilePlan<HD, 64 * NW>;
   constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
@@ -586,6 +633,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
   if (CAUSAL) kv_end = min(p.Sk, q0 + BM + off);
   const int ntiles = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
   const int wtiles = wave_tile_count<CAUSAL>(ntiles, q0w, off);
+  const unsigned drk = DROP ? attn_row_key(p.drop_seed, (unsigned)(b * p.Hq + hq), (unsigned)myq) : 0u;
+  const unsigned dthr = DROP ? attn_drop_thr(p.drop_p) : 0u;
+  const float drs = DROP ? 1.f / (1.f - p.drop_p) : 1.f;
 
   Plan plan;
   plan.init(lane, p.k_ss);
@@ -618,8 +668,16 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
           s[r] = (key >= p.Sk || (CAUSAL && key > myq + off)) ? -INFINITY : s[r];
         }
       }
+      if constexpr (DROP) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s[r] = exp2_(fmaf(s[r], sl2, nlse2)) * (dp[r] - delta);
+        for (int r = 0; r < 16; ++r) {
+          const bool keep = attn_keep(drk, (unsigned)(k0 + sub * 32 + acc_row(r, h)), dthr);
+          s[r] = exp2_(fmaf(s[r], sl2, nlse2)) * ((keep ? dp[r] * drs : 0.f) - delta);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = exp2_(fmaf(s[r], sl2, nlse2)) * (dp[r] - delta);
+      }
 #pragma unroll
       for (int half = 0; half < 2; ++half)
 #pragma unroll
@@ -680,6 +738,13 @@ static void fwd_launch_nw(const AttnParams& p, hipStream_t st) {
 
 template <int HD>
 static void fwd_launch(const AttnParams& p, hipStream_t st) {
+  if (p.drop_p > 0.f) {   // dropout: 4-wave instantiations only
+    const dim3 grid((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
+    const size_t lds = 2 * 2 * 64 * HD * 2;
+    if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, 4, true>), grid, dim3(256), lds, st, p);
+    else hipLaunchKernelGGL((attn_fwd_k<HD, false, 4, true>), grid, dim3(256), lds, st, p);
+    return;
+  }
   if constexpr (HD >= 64) {   // a 64-key tile of HD = 32 has fewer 16-B chunks than 8 waves have lanes
     if (attn_waves(4) == 8) return fwd_launch_nw<HD, 8>(p, st);
   }
@@ -700,7 +765,7 @@ template <int HD, int NW>
 static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
   const AttnParams& p = P.f;
   constexpr int BNK = 32 * NW;
-  const size_t lds_kv = BNK * HD * 2 + 4 * 32 * HD * 2 + 4 * 32 * 4;
+  const size_t lds_kv = BNK * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
   const dim3 grid_kv((unsigned)((p.Sk + BNK - 1) / BNK * p.Hkv * p.B));
   if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, NW>), grid_kv, dim3(64 * NW), lds_kv, st, P);
   else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, NW>), grid_kv, dim3(64 * NW), lds_kv, st, P);
@@ -712,6 +777,18 @@ static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
 
 template <int HD>
 static void bwd_launch(const AttnBwdParams& P, hipStream_t st) {
+  const AttnParams& p = P.f;
+  if (p.drop_p > 0.f) {   // dropout: 4-wave instantiations only
+    const size_t lds_kv = 128 * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
+    const dim3 grid_kv((unsigned)((p.Sk + 127) / 128 * p.Hkv * p.B));
+    if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, 4, true>), grid_kv, dim3(256), lds_kv, st, P);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, 4, true>), grid_kv, dim3(256), lds_kv, st, P);
+    const size_t lds_q = 2 * 2 * 64 * HD * 2;
+    const dim3 grid_q((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
+    if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, 4, true>), grid_q, dim3(256), lds_q, st, P);
+    else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, 4, true>), grid_q, dim3(256), lds_q, st, P);
+    return;
+  }
   if constexpr (HD >= 64) {
     if (attn_waves(4) == 8) return bwd_launch_nw<HD, 8>(P, st);
   }

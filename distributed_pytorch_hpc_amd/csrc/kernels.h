@@ -71,6 +71,10 @@ struct AttnParams {
   float scale;
   int causal;
   // causal offset: query i attends keys j <= i + (Sk - Sq) (bottom-right aligned, as flash-attn).
+  // Attention dropout (training): probability drop_p, keep mask regenerated bit-identically in the forward and
+  // both backward kernels from a counter hash of (drop_seed, b * Hq + hq, query, key) -- see attn_keep().
+  float drop_p;
+  unsigned drop_seed;
 };
 void flash_attn_fwd(const AttnParams& p, hipStream_t stream);
 

@@ -256,7 +256,7 @@ void check_attn_operand(const Tensor& t, const char* name) {
 }
 
 dph::AttnParams make_params(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& lse,
-                            double scale, bool causal) {
+                            double scale, bool causal, double dropout_p = 0.0, int64_t seed = 0) {
   dph::AttnParams p{};
   p.q = q.data_ptr(); p.k = k.data_ptr(); p.v = v.data_ptr(); p.o = o.data_ptr();
   p.lse = lse.defined() && lse.numel() ? lse.data_ptr<float>() : nullptr;
@@ -268,11 +268,14 @@ dph::AttnParams make_params(const Tensor& q, const Tensor& k, const Tensor& v, c
   p.Sk = (int)k.size(1); p.Hkv = (int)k.size(2);
   p.scale = (float)scale;
   p.causal = causal ? 1 : 0;
+  TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "flash_attn: dropout_p must be in [0, 1)");
+  p.drop_p = (float)dropout_p;
+  p.drop_seed = (unsigned)(seed & 0xffffffff);
   return p;
 }
 
 std::tuple<Tensor, Tensor> flash_attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, double scale,
-                                          bool causal) {
+                                          bool causal, double dropout_p, int64_t seed) {
   c10::DeviceGuard g(q.device());
   check_attn_operand(q, "q"); check_attn_operand(k, "k"); check_attn_operand(v, "v");
   const int64_t D = q.size(3);
@@ -281,13 +284,14 @@ std::tuple<Tensor, Tensor> flash_attn_fwd(const Tensor& q, const Tensor& k, cons
   TORCH_CHECK(k.size(0) == q.size(0) && q.size(2) % k.size(2) == 0, "flash_attn: batch / GQA heads mismatch");
   auto o = at::empty({q.size(0), q.size(1), q.size(2), D}, q.options());
   auto lse = at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
-  auto p = make_params(q, k, v, o, lse, scale, causal);
+  auto p = make_params(q, k, v, o, lse, scale, causal, dropout_p, seed);
   dph::flash_attn_fwd(p, cur_stream());
   return {o, lse};
 }
 
 void flash_attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
-                         const Tensor& lse, double scale, bool causal, Tensor& dq, Tensor& dk, Tensor& dv) {
+                         const Tensor& lse, double scale, bool causal, Tensor& dq, Tensor& dk, Tensor& dv,
+                         double dropout_p, int64_t seed) {
   c10::DeviceGuard g(q.device());
   check_attn_operand(q, "q"); check_attn_operand(k, "k"); check_attn_operand(v, "v");
   check_attn_operand(o, "o"); check_attn_operand(dout, "dout");
@@ -300,7 +304,7 @@ void flash_attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, c
   auto dq_acc = at::empty({B, Sq, Hq, D}, q.options().dtype(at::kFloat));
   dph::AttnBwdParams P{};
   auto lse_c = lse.contiguous();
-  P.f = make_params(q, k, v, o, lse_c, scale, causal);
+  P.f = make_params(q, k, v, o, lse_c, scale, causal, dropout_p, seed);
   P.dout = dout.data_ptr(); P.do_sb = dout.stride(0); P.do_ss = dout.stride(1); P.do_sh = dout.stride(2);
   P.delta = delta.data_ptr<float>();
   P.dq_accum = dq_acc.data_ptr<float>();
@@ -313,17 +317,18 @@ void flash_attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, c
 
 std::tuple<Tensor, Tensor, Tensor> flash_attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k,
                                                   const Tensor& v, const Tensor& o, const Tensor& lse, double scale,
-                                                  bool causal) {
+                                                  bool causal, double dropout_p, int64_t seed) {
   auto dq = at::empty(q.sizes(), q.options());
   auto dk = at::empty(k.sizes(), k.options());
   auto dv = at::empty(v.sizes(), v.options());
-  flash_attn_bwd_impl(dout, q, k, v, o, lse, scale, causal, dq, dk, dv);
+  flash_attn_bwd_impl(dout, q, k, v, o, lse, scale, causal, dq, dk, dv, dropout_p, seed);
   return {dq, dk, dv};
 }
 
 void flash_attn_bwd_into(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
-                         const Tensor& lse, double scale, bool causal, Tensor dq, Tensor dk, Tensor dv) {
-  flash_attn_bwd_impl(dout, q, k, v, o, lse, scale, causal, dq, dk, dv);
+                         const Tensor& lse, double scale, bool causal, Tensor dq, Tensor dk, Tensor dv,
+                         double dropout_p, int64_t seed) {
+  flash_attn_bwd_impl(dout, q, k, v, o, lse, scale, causal, dq, dk, dv, dropout_p, seed);
 }
 
 // ------------------------------------------------------------------------------------------------ embedding
@@ -617,11 +622,12 @@ TORCH_LIBRARY(dph, m) {
   m.def("sumsq_(Tensor x, Tensor(a!) out) -> ()");
   m.def("cross_entropy_fwd(Tensor(a!) logits, Tensor target, Tensor inv_count, int ignore_index, bool grad_inplace, "
         "float smoothing) -> (Tensor, Tensor)");
-  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal) -> (Tensor, Tensor)");
-  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal) "
-        "-> (Tensor, Tensor, Tensor)");
+  m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, float dropout_p=0., int seed=0) "
+        "-> (Tensor, Tensor)");
+  m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, "
+        "float dropout_p=0., int seed=0) -> (Tensor, Tensor, Tensor)");
   m.def("flash_attn_bwd_into(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, "
-        "bool causal, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv) -> ()");
+        "bool causal, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float dropout_p=0., int seed=0) -> ()");
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");

@@ -4,8 +4,8 @@
 Token + learned positional embedding, four named stages (``stage0..stage3``) of pre-LN encoder blocks, final
 LayerNorm and a bias-free vocabulary projection.  The multi-head attention keeps nn.MultiheadAttention's packed
 parameters (``in_proj_weight/in_proj_bias``, ``out_proj``) but runs the CDNA4 flash kernel (non-causal, like the
-reference) when attention dropout is inactive; with dropout > 0 in training it uses ATen SDPA (the flash
-kernel has no in-kernel dropout RNG).  ``stage_modules()`` yields the per-stage callables for parallel.pipeline.
+reference), attention dropout included (in-kernel counter-hash mask, ops/attention.py).  ``stage_modules()``
+yields the per-stage callables for parallel.pipeline.
 """
 from __future__ import annotations
 
@@ -30,11 +30,7 @@ class PackedMHA(nn.Module):
         b, s, d = x.shape
         qkv = F.linear(x, self.in_proj_weight, self.in_proj_bias).view(b, s, 3, -1, self.head_dim)
         q, k, v = qkv.unbind(2)
-        if self.training and self.dropout > 0:
-            o = F.scaled_dot_product_attention(q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2),
-                                               dropout_p=self.dropout).transpose(1, 2)
-        else:
-            o = ops.flash_attention(q, k, v, causal=False)
+        o = ops.flash_attention(q, k, v, causal=False, dropout_p=self.dropout if self.training else 0.0)
         return self.out_proj(o.reshape(b, s, d))
 
 

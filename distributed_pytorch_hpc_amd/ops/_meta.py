@@ -119,18 +119,18 @@ def _xent(logits, target, inv_count, ignore_index, grad_inplace, smoothing):
 
 
 @register_fake("dph::flash_attn_fwd")
-def _fa_fwd(q, k, v, scale, causal):
+def _fa_fwd(q, k, v, scale, causal, dropout_p=0.0, seed=0):
     b, s, h, d = q.shape
     return q.new_empty((b, s, h, d)), q.new_empty((b, h, s), dtype=torch.float32)
 
 
 @register_fake("dph::flash_attn_bwd")
-def _fa_bwd(dout, q, k, v, o, lse, scale, causal):
+def _fa_bwd(dout, q, k, v, o, lse, scale, causal, dropout_p=0.0, seed=0):
     return torch.empty_like(q), k.new_empty(k.shape), v.new_empty(v.shape)
 
 
 @register_fake("dph::flash_attn_bwd_into")
-def _fa_bwd_into(dout, q, k, v, o, lse, scale, causal, dq, dk, dv):
+def _fa_bwd_into(dout, q, k, v, o, lse, scale, causal, dq, dk, dv, dropout_p=0.0, seed=0):
     return None
 
 

@@ -8,6 +8,11 @@ the fused QKV GEMM output [B, S, (Hq + 2 Hkv) * D] -- no transposes, no copies. 
 Head dims 32/64/128 run natively; 16/48/96 are zero-padded to the next native size (exact: padding the
 contraction dim with zeros leaves QK^T unchanged, padded V columns are sliced off).  Larger head dims
 fall back to ATen SDPA with a one-time warning.
+
+Attention dropout (``dropout_p > 0``, the pipeline transformer's nn.MultiheadAttention(dropout=0.1),
+03_pipeline_training.py:57-58) runs in the same kernels: the keep mask of element (query, key) is a counter hash
+of (seed, batch*head, query, key) regenerated in the backward kernels, never stored; ``dropout_mask`` rebuilds
+it for tests.  The seed comes from torch's CPU generator (``torch.manual_seed`` makes runs reproducible).
 """
 from __future__ import annotations
 
@@ -54,39 +59,72 @@ def _pad_last(t: torch.Tensor, d: int) -> torch.Tensor:
     return F.pad(t, (0, d - t.shape[-1]))
 
 
-def flash_fwd(q, k, v, scale: float, causal: bool):
+def flash_fwd(q, k, v, scale: float, causal: bool, dropout_p: float = 0.0, seed: int = 0):
     """Raw native forward: returns (o [B,S,Hq,D] bf16, lse fp32 [B,Hq,S]).  No autograd."""
-    return _lib.ops().flash_attn_fwd(q, k, v, scale, causal)
+    return _lib.ops().flash_attn_fwd(q, k, v, scale, causal, dropout_p, seed)
 
 
-def flash_bwd(do, q, k, v, o, lse, scale: float, causal: bool):
+def flash_bwd(do, q, k, v, o, lse, scale: float, causal: bool, dropout_p: float = 0.0, seed: int = 0):
     """Raw native backward: returns (dq, dk, dv)."""
-    return _lib.ops().flash_attn_bwd(do.contiguous(), q, k, v, o, lse, scale, causal)
+    return _lib.ops().flash_attn_bwd(do.contiguous(), q, k, v, o, lse, scale, causal, dropout_p, seed)
+
+
+_M32 = 0xFFFFFFFF
+
+
+def _mix(x: torch.Tensor) -> torch.Tensor:
+    """csrc/attention.hip attn_mix on int64 tensors holding uint32 values."""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def dropout_mask(b: int, h: int, sq: int, sk: int, dropout_p: float, seed: int, device=None) -> torch.Tensor:
+    """The kernels' keep mask as a bool [B, H, Sq, Sk] tensor (reference / tests)."""
+    bh = torch.arange(b * h, device=device, dtype=torch.int64).view(b, h, 1, 1)
+    q = torch.arange(sq, device=device, dtype=torch.int64).view(1, 1, sq, 1)
+    k = torch.arange(sk, device=device, dtype=torch.int64).view(1, 1, 1, sk)
+    row = _mix((seed & _M32) ^ _mix((bh * 0x9E3779B1 + q * 0x85EBCA77) & _M32))
+    hsh = _mix(row ^ ((k * 0xC2B2AE3D) & _M32))
+    thr = min(int(dropout_p * 4294967296.0), 4294967040)
+    return hsh >= thr
 
 
 class _FlashAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, causal, scale):
-        o, lse = flash_fwd(q, k, v, scale, causal)
+    def forward(ctx, q, k, v, causal, scale, dropout_p=0.0, seed=0):
+        o, lse = flash_fwd(q, k, v, scale, causal, dropout_p, seed)
         ctx.save_for_backward(q, k, v, o, lse)
-        ctx.causal, ctx.scale = causal, scale
+        ctx.causal, ctx.scale, ctx.dropout_p, ctx.seed = causal, scale, dropout_p, seed
         return o
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse = ctx.saved_tensors
-        dq, dk, dv = flash_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal)
-        return dq, dk, dv, None, None
+        dq, dk, dv = flash_bwd(do, q, k, v, o, lse, ctx.scale, ctx.causal, ctx.dropout_p, ctx.seed)
+        return dq, dk, dv, None, None, None, None
 
 
 def _native_ok(q: torch.Tensor) -> bool:
     return q.dtype == torch.bfloat16 and _lib.use_native(q)
 
 
-def flash_attention(q, k, v, causal: bool = True, scale: float | None = None) -> torch.Tensor:
-    """softmax(q k^T * scale [+ causal mask]) v on [B, S, H, D] tensors (GQA: Hq % Hkv == 0)."""
+def _sdpa_dropout(q, k, v, causal, scale, dropout_p):
+    qt, kt, vt = (t.transpose(1, 2) for t in (q, k, v))
+    return F.scaled_dot_product_attention(qt, kt, vt, is_causal=causal, scale=scale,
+                                          dropout_p=dropout_p).transpose(1, 2)
+
+
+def flash_attention(q, k, v, causal: bool = True, scale: float | None = None, dropout_p: float = 0.0,
+                    seed: int | None = None) -> torch.Tensor:
+    """softmax(q k^T * scale [+ causal mask]) v on [B, S, H, D] tensors (GQA: Hq % Hkv == 0), with attention
+    dropout ``dropout_p`` (pass it only in training)."""
     d = q.shape[-1]
     scale = 1.0 / math.sqrt(d) if scale is None else scale
+    if dropout_p > 0.0 and not (_native_ok(q) and _padded_dim(d) is not None):
+        return _sdpa_dropout(q, k, v, causal, scale, dropout_p)
     if not _native_ok(q):
         return attention_reference(q, k, v, causal, scale)
     dp = _padded_dim(d)
@@ -99,7 +137,9 @@ def flash_attention(q, k, v, causal: bool = True, scale: float | None = None) ->
         q, k, v = _pad_last(q, dp), _pad_last(k, dp), _pad_last(v, dp)
     q, k, v = (t if t.stride(-1) == 1 and all(s % 8 == 0 for s in t.stride()[:3]) else t.contiguous()
                for t in (q, k, v))
-    o = _FlashAttnFn.apply(q, k, v, causal, scale)
+    if dropout_p > 0.0 and seed is None:
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+    o = _FlashAttnFn.apply(q, k, v, causal, scale, float(dropout_p), int(seed or 0))
     return o[..., :d] if dp != d else o
 
 
