@@ -7,6 +7,8 @@
 // 8-channel chunks exactly.  Passes over the activation (A = its size):
 //   forward : stats (read x)  +  apply (read x [+ residual], write y)            = 3A (+A)
 //   backward: reduce (read dy, y, x) + dx (read dy, y, x, write dx [+ dres])      = 7A (+A)
+//             ReLU without residual: the mask [x * scale + shift > 0] is recomputed from x with the forward's
+//             own fp32 scale / shift (bit-identical to y > 0), so y is not read:  5A
 // Statistics are accumulated with a per-thread shift (the thread's first value) and merged across threads and
 // blocks with Chan's parallel-variance formula, so large-mean channels do not lose the variance to fp32
 // cancellation; all reductions go through fixed-order partial buffers (deterministic).
@@ -165,20 +167,24 @@ __global__ __launch_bounds__(BN_NT) void bn_apply_k(const T* __restrict__ x, con
 }
 
 // Backward reduction: per channel sum(dz) and sum(dz * xhat), dz = dy * [y > 0 when RELU].
-template <typename T, bool RELU>
+// XMASK: the ReLU mask comes from x * scale + shift (ss = [scale | shift], the forward's values) instead of y.
+template <typename T, bool RELU, bool XMASK>
 __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_k(const T* __restrict__ dy, const T* __restrict__ y,
                                                          const T* __restrict__ x, const float* __restrict__ mean,
-                                                         const float* __restrict__ invstd, float* __restrict__ part,
+                                                         const float* __restrict__ invstd,
+                                                         const float* __restrict__ ss, float* __restrict__ part,
                                                          int64_t M, int C, int64_t rows_per_block) {
   extern __shared__ float sh[];   // [2][BN_NT][8]
   const int ch8 = C / 8, rpi = BN_NT / ch8;
   const int cc = threadIdx.x % ch8, r0 = threadIdx.x / ch8;
   const int64_t beg = (int64_t)blockIdx.x * rows_per_block, end = min(M, beg + rows_per_block);
-  float mu[8], is[8], sd[8], sdx[8];
+  float mu[8], is[8], sd[8], sdx[8], xs[8], xb[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     mu[i] = mean[cc * 8 + i];
     is[i] = invstd[cc * 8 + i];
+    xs[i] = XMASK ? ss[cc * 8 + i] : 0.f;
+    xb[i] = XMASK ? ss[C + cc * 8 + i] : 0.f;
     sd[i] = 0.f;
     sdx[i] = 0.f;
   }
@@ -186,10 +192,11 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_k(const T* __restrict__ d
     float g[8], xv[8], yv[8];
     Vec8<T>::load(dy + r * C + cc * 8, g);
     Vec8<T>::load(x + r * C + cc * 8, xv);
-    if (RELU) Vec8<T>::load(y + r * C + cc * 8, yv);
+    if (RELU && !XMASK) Vec8<T>::load(y + r * C + cc * 8, yv);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float dz = (!RELU || yv[i] > 0.f) ? g[i] : 0.f;
+      const bool on = XMASK ? fmaf(xv[i], xs[i], xb[i]) > 0.f : (!RELU || yv[i] > 0.f);
+      const float dz = on ? g[i] : 0.f;
       sd[i] += dz;
       sdx[i] = fmaf(dz, (xv[i] - mu[i]) * is[i], sdx[i]);
     }
@@ -259,22 +266,24 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_finalize_k(const float* __restri
   coef[2 * C + c] = b / count;
 }
 
-template <typename T, bool RELU, bool DRES>
+template <typename T, bool RELU, bool DRES, bool XMASK>
 __global__ __launch_bounds__(BN_NT) void bn_bwd_dx_k(const T* __restrict__ dy, const T* __restrict__ y,
                                                      const T* __restrict__ x, const float* __restrict__ mean,
                                                      const float* __restrict__ invstd, const float* __restrict__ coef,
-                                                     T* __restrict__ dx, T* __restrict__ dres, int64_t nvec, int ch8) {
+                                                     const float* __restrict__ ss, T* __restrict__ dx,
+                                                     T* __restrict__ dres, int64_t nvec, int ch8) {
   const int C = ch8 * 8;
   for (int64_t v = (int64_t)blockIdx.x * BN_NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * BN_NT) {
     const int c0 = (int)(v % ch8) * 8;
     float g[8], xv[8], yv[8], o[8];
     Vec8<T>::load(dy + v * 8, g);
     Vec8<T>::load(x + v * 8, xv);
-    if (RELU) Vec8<T>::load(y + v * 8, yv);
+    if (RELU && !XMASK) Vec8<T>::load(y + v * 8, yv);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int c = c0 + i;
-      const float dz = (!RELU || yv[i] > 0.f) ? g[i] : 0.f;
+      const bool on = XMASK ? fmaf(xv[i], ss[c], ss[C + c]) > 0.f : (!RELU || yv[i] > 0.f);
+      const float dz = on ? g[i] : 0.f;
       const float xh = (xv[i] - mean[c]) * invstd[c];
       o[i] = coef[c] * (dz - coef[C + c] - xh * coef[2 * C + c]);
       g[i] = dz;
@@ -344,17 +353,20 @@ void bn_apply(const void* x, const void* res, const float* scale, const float* s
 
 void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
             void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dt,
-            int pdt, hipStream_t st) {
+            int pdt, hipStream_t st, const float* xmask_ss) {
+  const bool xm = relu && xmask_ss != nullptr;
   int64_t rpb;
   const int G = stats_grid(M, (int)C, &rpb);
   float* part = workspace;                       // [G][2C]
   float* coef = workspace + 2 * (int64_t)G * C;  // [3C]
   const size_t shs = 2 * BN_NT * 8 * sizeof(float);
   DPH_DISPATCH_FLOAT(dt, T, {
-    if (relu) hipLaunchKernelGGL((bn_bwd_reduce_k<T, true>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy, (const T*)y,
-                                 (const T*)x, mean, invstd, part, M, (int)C, rpb);
-    else hipLaunchKernelGGL((bn_bwd_reduce_k<T, false>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy, (const T*)y,
-                            (const T*)x, mean, invstd, part, M, (int)C, rpb);
+    if (xm) hipLaunchKernelGGL((bn_bwd_reduce_k<T, true, true>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy,
+                               (const T*)y, (const T*)x, mean, invstd, xmask_ss, part, M, (int)C, rpb);
+    else if (relu) hipLaunchKernelGGL((bn_bwd_reduce_k<T, true, false>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy,
+                                      (const T*)y, (const T*)x, mean, invstd, nullptr, part, M, (int)C, rpb);
+    else hipLaunchKernelGGL((bn_bwd_reduce_k<T, false, false>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy,
+                            (const T*)y, (const T*)x, mean, invstd, nullptr, part, M, (int)C, rpb);
   });
   const dim3 fg((unsigned)(C / 8));
   if (pdt == kBF16)
@@ -365,14 +377,16 @@ void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, con
                        (const float*)w, invstd, (float*)dw, (float*)db, coef);
   const int64_t nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, BN_NT));
-#define DPH_BN_DX(R_, D_)                                                                                        \
-  hipLaunchKernelGGL((bn_bwd_dx_k<T, R_, D_>), grid, dim3(BN_NT), 0, st, (const T*)dy, (const T*)y, (const T*)x, \
-                     mean, invstd, coef, (T*)dx, (T*)dres, nvec, (int)(C / 8))
+#define DPH_BN_DX(R_, D_, X_)                                                                                     \
+  hipLaunchKernelGGL((bn_bwd_dx_k<T, R_, D_, X_>), grid, dim3(BN_NT), 0, st, (const T*)dy, (const T*)y,           \
+                     (const T*)x, mean, invstd, coef, xmask_ss, (T*)dx, (T*)dres, nvec, (int)(C / 8))
   DPH_DISPATCH_FLOAT(dt, T, {
-    if (relu && dres) DPH_BN_DX(true, true);
-    else if (relu) DPH_BN_DX(true, false);
-    else if (dres) DPH_BN_DX(false, true);
-    else DPH_BN_DX(false, false);
+    if (xm && dres) DPH_BN_DX(true, true, true);
+    else if (xm) DPH_BN_DX(true, false, true);
+    else if (relu && dres) DPH_BN_DX(true, true, false);
+    else if (relu) DPH_BN_DX(true, false, false);
+    else if (dres) DPH_BN_DX(false, true, false);
+    else DPH_BN_DX(false, false, false);
   });
 #undef DPH_BN_DX
 }

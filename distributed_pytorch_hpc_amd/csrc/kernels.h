@@ -126,9 +126,10 @@ void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const 
                   hipStream_t stream);
 void bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int64_t M, int64_t C,
               bool relu, int dtype, hipStream_t stream);
+// xmask_ss (optional, fp32 [scale | shift] of the forward): ReLU mask from x instead of reading y.
 void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
             void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dtype,
-            int param_dtype, hipStream_t stream);
+            int param_dtype, hipStream_t stream, const float* xmask_ss = nullptr);
 
 // dst[C, R] = src[R, C]^T (bf16, row-major, leading dims in elements; vector path needs 16-B aligned rows).
 void transpose2d(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_src, int64_t ld_dst,

@@ -462,7 +462,7 @@ void check_like(const Tensor& a, const Tensor& x, const char* name) {
               "bn_act: ", name, " must match x (shape, dtype, channels-last layout)");
 }
 
-std::tuple<Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res,
+std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res,
                                               const c10::optional<Tensor>& w, const c10::optional<Tensor>& b,
                                               const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
                                               double momentum, double eps, bool relu) {
@@ -479,7 +479,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10::option
   auto fopt = x.options().dtype(at::kFloat);
   auto y = at::empty_like(x);
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
-  auto scale = at::empty({C}, fopt), shift = at::empty({C}, fopt);
+  auto ss = at::empty({2 * C}, fopt);   // [scale | shift]: the backward recomputes the ReLU mask from them
   const int G = dph::bn_partial_blocks(M, C);
   auto ws = at::empty({2 * (int64_t)G * C + G}, fopt);
   const int pdt = w ? dt_code(*w) : (b ? dt_code(*b) : dph::kF32);
@@ -487,9 +487,9 @@ std::tuple<Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10::option
   dph::bn_fwd_train(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), w ? w->data_ptr() : nullptr,
                     b ? b->data_ptr() : nullptr, rmean ? rmean->data_ptr() : nullptr,
                     rvar ? rvar->data_ptr() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                    scale.data_ptr<float>(), shift.data_ptr<float>(), ws.data_ptr<float>(), M, C, (float)momentum,
+                    ss.data_ptr<float>(), ss.data_ptr<float>() + C, ws.data_ptr<float>(), M, C, (float)momentum,
                     (float)eps, relu, dt_code(x), pdt, rdt, cur_stream());
-  return {y, mean, invstd};
+  return {y, mean, invstd, ss};
 }
 
 Tensor bn_act_apply(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& scale, const Tensor& shift,
@@ -510,12 +510,18 @@ Tensor bn_act_apply(const Tensor& x, const c10::optional<Tensor>& res, const Ten
 std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Tensor& y, const Tensor& x,
                                                       const Tensor& mean, const Tensor& invstd,
                                                       const c10::optional<Tensor>& w, bool relu, bool need_dres,
-                                                      bool need_dwb) {
+                                                      bool need_dwb, const c10::optional<Tensor>& xmask_ss) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
   const int64_t C = bn_channels(x), M = x.numel() / C;
   check_like(dy, x, "dy");
-  check_like(y, x, "y");
+  const bool xm = relu && xmask_ss.has_value();
+  if (xm) {
+    TORCH_CHECK(xmask_ss->scalar_type() == at::kFloat && xmask_ss->numel() == 2 * C && xmask_ss->is_contiguous(),
+                "bn_act_bwd: xmask_ss must be the forward's fp32 [scale | shift]");
+  } else {
+    check_like(y, x, "y");
+  }
   auto fopt = x.options().dtype(at::kFloat);
   auto dx = at::empty_like(x);
   Tensor dres = need_dres ? at::empty_like(x) : at::empty({0}, x.options());
@@ -527,7 +533,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Te
   dph::bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
               w ? w->data_ptr() : nullptr, dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr,
               need_dwb ? dw.data_ptr() : nullptr, need_dwb ? db.data_ptr() : nullptr, ws.data_ptr<float>(), M, C, relu,
-              dt_code(x), w ? dt_code(*w) : dph::kF32, cur_stream());
+              dt_code(x), w ? dt_code(*w) : dph::kF32, cur_stream(), xm ? xmask_ss->data_ptr<float>() : nullptr);
   return {dx, dres, dw, db};
 }
 
@@ -636,10 +642,10 @@ TORCH_LIBRARY(dph, m) {
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-        "float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor)");
+        "float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "
-        "bool need_dwb) -> (Tensor, Tensor, Tensor, Tensor)");
+        "bool need_dwb, Tensor? xmask_ss=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("latmse_fwd(Tensor pred, Tensor target, int n_global, int lat_offset) -> Tensor");
   m.def("latmse_bwd(Tensor gloss, Tensor pred, Tensor target, int n_global, int lat_offset, bool need_dtarget) -> "
         "(Tensor, Tensor)");

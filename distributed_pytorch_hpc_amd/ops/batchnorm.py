@@ -3,7 +3,8 @@
 ``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` (same parameters, buffers and state-dict keys) whose
 ``forward(x, residual=None)`` computes ``act(bn(x) + residual)``.  On an MI355X with a channels-last input whose
 channel count is a power of two in [8, 2048] it runs the fused HIP kernels (one statistics pass + one apply pass
-forward; one reduction pass + one dx pass backward, which also emits the residual's gradient); otherwise the
+forward; one reduction pass + one dx pass backward, which also emits the residual's gradient; for ReLU without a
+residual the backward takes the mask from x and the forward's scale / shift instead of reading y); otherwise the
 stock ``F.batch_norm`` + add + ReLU path.  The reference trains torchvision ResNets (scripts/main.py:249,
 resnet_fsdp_training.py:186-191) whose conv -> BN -> ReLU (+ identity) blocks this fuses.
 """
@@ -38,20 +39,24 @@ def _native_ok(x: torch.Tensor, residual) -> bool:
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
-        y, mean, invstd = _lib.ops().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, momentum, eps,
-                                                relu)
-        ctx.save_for_backward(x, y, mean, invstd, weight)
+        y, mean, invstd, ss = _lib.ops().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, momentum,
+                                                    eps, relu)
+        # ReLU without residual: the backward recomputes the mask from x with the forward's scale / shift and
+        # never reads y (one activation-sized read less in each backward pass)
+        ctx.xmask = relu and residual is None
+        ctx.save_for_backward(x, ss if ctx.xmask else y, mean, invstd, weight)
         ctx.relu, ctx.has_res = relu, residual is not None
         ctx.has_wb = weight is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, mean, invstd, weight = ctx.saved_tensors
+        x, y_or_ss, mean, invstd, weight = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         need_wb = ctx.has_wb and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        y, ss = (x, y_or_ss) if ctx.xmask else (y_or_ss, None)
         dx, dres, dw, db = _lib.ops().bn_act_bwd(dy, y, x, mean, invstd, weight if ctx.has_wb else None, ctx.relu,
-                                                 ctx.has_res, need_wb)
+                                                 ctx.has_res, need_wb, ss)
         return (dx, dw if need_wb else None, db if need_wb else None, None, None, dres if ctx.has_res else None,
                 None, None, None)
 

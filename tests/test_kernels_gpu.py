@@ -364,6 +364,22 @@ def test_bn_act_train(dph_native, N, C, H, W, dtype, residual, relu):
         assert rel_err(rs[0].grad, rs[1].grad) < tol
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_bn_relu_mask_from_x_matches_y(dph_native, dtype):
+    """ReLU-only backward with the mask recomputed from x and the forward's [scale | shift] is bit-identical to the
+    y-masked backward."""
+    torch.manual_seed(5)
+    x = (torch.randn(16, 128, 14, 14, device=DEV) * 3 + 0.5).to(dtype).contiguous(memory_format=torch.channels_last)
+    w = (1 + 0.2 * torch.randn(128, device=DEV)).to(dtype)
+    b = (0.1 * torch.randn(128, device=DEV)).to(dtype)
+    y, mean, inv, ss = torch.ops.dph.bn_act_fwd(x, None, w, b, None, None, 0.1, 1e-5, True)
+    dy = torch.randn_like(x)
+    ref = torch.ops.dph.bn_act_bwd(dy, y, x, mean, inv, w, True, False, True)
+    got = torch.ops.dph.bn_act_bwd(dy, x, x, mean, inv, w, True, False, True, ss)
+    for a, r in zip(got, ref):
+        assert torch.equal(a, r)
+
+
 def test_bn_act_module_native_matches_torch(dph_native):
     """BatchNormAct2d (fused kernels) == nn.BatchNorm2d + add + ReLU, train and eval, incl. running stats."""
     from distributed_pytorch_hpc_amd.ops import BatchNormAct2d
@@ -462,9 +478,9 @@ def test_kernels_bitwise_deterministic(dph_native, case):
         if case == "bn_bwd":
             x = torch.randn(8, 64, 28, 28, device=DEV).to(memory_format=torch.channels_last)
             w = torch.ones(64, device=DEV)
-            y, mean, inv = torch.ops.dph.bn_act_fwd(x, None, w, None, None, None, 0.1, 1e-5, True)
+            y, mean, inv, ss = torch.ops.dph.bn_act_fwd(x, None, w, None, None, None, 0.1, 1e-5, True)
             return [y, mean, inv] + list(torch.ops.dph.bn_act_bwd(torch.randn_like(x), y, x, mean, inv, w, True,
-                                                                  False, True))
+                                                                  False, True, ss))
         if case == "xent":
             logits = torch.randn(512, 32000, device=DEV, dtype=torch.bfloat16)
             return [ops.fused_cross_entropy(logits, torch.randint(0, 32000, (512,), device=DEV)), logits]
