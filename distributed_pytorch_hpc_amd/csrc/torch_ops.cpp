@@ -510,7 +510,9 @@ Tensor bn_act_apply(const Tensor& x, const c10::optional<Tensor>& res, const Ten
 std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Tensor& y, const Tensor& x,
                                                       const Tensor& mean, const Tensor& invstd,
                                                       const c10::optional<Tensor>& w, bool relu, bool need_dres,
-                                                      bool need_dwb, const c10::optional<Tensor>& xmask_ss) {
+                                                      bool need_dwb, const c10::optional<Tensor>& xmask_ss,
+                                                      const c10::optional<Tensor>& dw_out,
+                                                      const c10::optional<Tensor>& db_out) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
   const int64_t C = bn_channels(x), M = x.numel() / C;
@@ -526,8 +528,18 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Te
   auto dx = at::empty_like(x);
   Tensor dres = need_dres ? at::empty_like(x) : at::empty({0}, x.options());
   const at::ScalarType pt = w ? w->scalar_type() : at::kFloat;
-  Tensor dw = need_dwb ? at::empty({C}, x.options().dtype(pt)) : at::empty({0}, fopt);
-  Tensor db = need_dwb ? at::empty({C}, x.options().dtype(pt)) : at::empty({0}, fopt);
+  // dw_out / db_out: write the parameter gradients straight into caller buffers (the engine's gradient bucket)
+  auto out_or_new = [&](const c10::optional<Tensor>& o, const char* name) {
+    if (!need_dwb) return at::empty({0}, fopt);
+    if (o.has_value()) {
+      TORCH_CHECK(o->numel() == C && o->is_contiguous() && o->scalar_type() == pt && o->device() == x.device(),
+                  "bn_act_bwd: ", name, " must be a contiguous [C] tensor of the weight dtype");
+      return *o;
+    }
+    return at::empty({C}, x.options().dtype(pt));
+  };
+  Tensor dw = out_or_new(dw_out, "dw_out");
+  Tensor db = out_or_new(db_out, "db_out");
   const int G = dph::bn_partial_blocks(M, C);
   auto ws = at::empty({2 * (int64_t)G * C + 3 * C}, fopt);
   dph::bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
@@ -645,7 +657,8 @@ TORCH_LIBRARY(dph, m) {
         "float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "
-        "bool need_dwb, Tensor? xmask_ss=None) -> (Tensor, Tensor, Tensor, Tensor)");
+        "bool need_dwb, Tensor? xmask_ss=None, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) "
+        "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("latmse_fwd(Tensor pred, Tensor target, int n_global, int lat_offset) -> Tensor");
   m.def("latmse_bwd(Tensor gloss, Tensor pred, Tensor target, int n_global, int lat_offset, bool need_dtarget) -> "
         "(Tensor, Tensor)");

@@ -86,7 +86,7 @@ def _bn_act_apply(x, res, scale, shift, relu):
 
 
 @register_fake("dph::bn_act_bwd")
-def _bn_act_bwd(dy, y, x, mean, invstd, w, relu, need_dres, need_dwb, xmask_ss=None):
+def _bn_act_bwd(dy, y, x, mean, invstd, w, relu, need_dres, need_dwb, xmask_ss=None, dw_out=None, db_out=None):
     c = x.shape[1]
     pdt = w.dtype if w is not None else torch.float32
     return (torch.empty_like(x), torch.empty_like(x) if need_dres else x.new_empty((0,)),

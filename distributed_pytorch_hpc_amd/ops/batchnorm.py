@@ -15,6 +15,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
+from .conv import _DIRECT
 
 
 def _pow2_channels(c: int) -> bool:
@@ -47,6 +48,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.save_for_backward(x, ss if ctx.xmask else y, mean, invstd, weight)
         ctx.relu, ctx.has_res = relu, residual is not None
         ctx.has_wb = weight is not None
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
@@ -55,8 +57,20 @@ class _BNActFn(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         need_wb = ctx.has_wb and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         y, ss = (x, y_or_ss) if ctx.xmask else (y_or_ss, None)
+        # engine-owned parameters (parallel/data_parallel.py main_grad views) on their first gradient of the step:
+        # the kernel writes dgamma / dbeta straight into the gradient bucket, autograd gets None
+        wp, bp = ctx.params
+        direct = (need_wb and bp is not None and _DIRECT and all(
+            getattr(p, "main_grad", None) is not None and not getattr(p, "_dph_accum", True)
+            and p.main_grad.is_contiguous() and p.main_grad.dtype == p.dtype for p in (wp, bp)))
         dx, dres, dw, db = _lib.ops().bn_act_bwd(dy, y, x, mean, invstd, weight if ctx.has_wb else None, ctx.relu,
-                                                 ctx.has_res, need_wb, ss)
+                                                 ctx.has_res, need_wb, ss, wp.main_grad if direct else None,
+                                                 bp.main_grad if direct else None)
+        if direct:
+            for p in (wp, bp):
+                p._dph_accum = True
+                p._dph_grad_ready()
+            dw = db = None
         return (dx, dw if need_wb else None, db if need_wb else None, None, None, dres if ctx.has_res else None,
                 None, None, None)
 

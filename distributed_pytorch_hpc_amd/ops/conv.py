@@ -28,6 +28,16 @@ from torch import nn
 
 from . import _lib
 
+# DPH_DIRECT_MAIN_GRAD=0: return weight gradients to autograd (engine copies them) instead of writing the bucket
+_DIRECT = os.environ.get("DPH_DIRECT_MAIN_GRAD", "1") != "0"
+
+# Set by runtime/graphs.GraphedStep around its warm-up and capture: the convolutions take MIOpen inside
+# whole-step HIP graphs.  Known issue: a captured ResNet-50 step (B=64, 224^2) with the 14x14 1x1 convolutions
+# on these kernels diverges from the second replay on when other GPU work runs between replays, while the same
+# kernels replay correctly in isolation (single layers and blocks of every ResNet-50 shape, guard-region checks
+# clean) -- unresolved, so graphed steps do not use them.
+_GRAPHED_STEP = False
+
 
 def _autocast_bf16(t: torch.Tensor) -> bool:
     return t.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
@@ -36,6 +46,27 @@ def _autocast_bf16(t: torch.Tensor) -> bool:
 def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
     """[B, C, H, W] (any layout) -> row-major [B*H*W, C] (a view when t is channels-last contiguous)."""
     return t.permute(0, 2, 3, 1).contiguous().view(-1, t.shape[1])
+
+
+def _main_grad_target(w: torch.Tensor, shape):
+    """The engine-owned gradient buffer of parameter ``w`` viewed as ``shape`` (parallel/data_parallel.py keeps
+    ``main_grad`` views into its flat bucket), or None when the weight gradient has to be returned to autograd."""
+    mg = getattr(w, "main_grad", None)
+    if mg is None or not _DIRECT or not mg.is_contiguous() or mg.data_ptr() % 16:
+        return None
+    return mg.view(shape)
+
+
+def _wgrad_into_main(w: torch.Tensor, shape, launch) -> bool:
+    """Run ``launch(out, accumulate)`` straight into the engine's gradient bucket and notify the engine (no
+    autograd gradient, no post-accumulate copy).  False when ``w`` has no engine-owned buffer."""
+    mg = _main_grad_target(w, shape)
+    if mg is None:
+        return False
+    launch(mg, bool(getattr(w, "_dph_accum", False)))
+    w._dph_accum = True
+    w._dph_grad_ready()
+    return True
 
 
 class _Conv1x1Fn(torch.autograd.Function):
@@ -50,7 +81,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         w2 = wb.view(wb.shape[0], C)
         y2 = _lib.ops().ts_gemm_nt(x2, w2)                          # [M, Cout]
         ctx.save_for_backward(x2, w2)
-        ctx.shape, ctx.wdtype = (B, C, H, W), wdtype
+        ctx.shape, ctx.wdtype, ctx.param = (B, C, H, W), wdtype, w
         return y2.view(B, H, W, -1).permute(0, 3, 1, 2)             # channels-last [B, Cout, H, W]
 
     @staticmethod
@@ -63,9 +94,11 @@ class _Conv1x1Fn(torch.autograd.Function):
             dx2 = _lib.ops().ts_gemm_nt(dy2, w2.t().contiguous())    # [M, Cin]
             dx = dx2.view(B, H, W, C).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
-            gw = torch.empty((w2.shape[0], C), dtype=ctx.wdtype, device=dy.device)
-            _lib.ops().ts_gemm_tn_(gw, dy2, x2, False)
-            gw = gw.view(w2.shape[0], C, 1, 1)
+            cout = w2.shape[0]
+            if not _wgrad_into_main(ctx.param, (cout, C), lambda out, acc: _lib.ops().ts_gemm_tn_(out, dy2, x2, acc)):
+                gw = torch.empty((cout, C), dtype=ctx.wdtype, device=dy.device)
+                _lib.ops().ts_gemm_tn_(gw, dy2, x2, False)
+                gw = gw.view(cout, C, 1, 1)
         return dx, gw
 
 
@@ -104,7 +137,7 @@ class _Conv3x3Fn(torch.autograd.Function):
 
 
 def conv3x3_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    if os.environ.get("DPH_CONV3X3", "0") != "1" or not x.is_cuda or _lib.reference_mode():
+    if os.environ.get("DPH_CONV3X3", "0") != "1" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
         return False
     if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)):
         return False
@@ -127,7 +160,7 @@ class Conv3x3(nn.Conv2d):
 
 
 def conv1x1_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    if os.environ.get("DPH_CONV1X1", "1") == "0" or not x.is_cuda or _lib.reference_mode():
+    if os.environ.get("DPH_CONV1X1", "1") == "0" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
         return False
     if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)):
         return False

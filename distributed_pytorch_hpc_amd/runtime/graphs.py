@@ -22,9 +22,13 @@ next replay): consume or clone it before the next call.
 
 Multi-rank steps would capture their RCCL collectives into the graph too; that path is off unless
 ``allow_collectives=True`` (not exercised on the 1-GPU test box).
+
+Inside graphed steps the channels-last 1x1 / 3x3 convolutions run on MIOpen (ops/conv.py ``_GRAPHED_STEP``: an
+unresolved divergence of replayed ResNet-50 steps with the 14x14 1x1 convolutions on the framework kernels).
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -33,6 +37,18 @@ import torch.distributed as dist
 
 def _engine_of(optimizer):
     return getattr(optimizer, "engine", None)
+
+
+@contextlib.contextmanager
+def _graph_safe_ops():
+    from ..ops import conv
+
+    old = conv._GRAPHED_STEP
+    conv._GRAPHED_STEP = True
+    try:
+        yield
+    finally:
+        conv._GRAPHED_STEP = old
 
 
 class GraphedStep:
@@ -94,7 +110,7 @@ class GraphedStep:
         self._set_lr(lr)
         cur = torch.cuda.current_stream()
         self._side.wait_stream(cur)
-        with torch.cuda.stream(self._side):
+        with torch.cuda.stream(self._side), _graph_safe_ops():
             out = self.step_fn(*self.static_in)
         cur.wait_stream(self._side)
         return out
@@ -105,7 +121,7 @@ class GraphedStep:
         saved = self.engine.step_count if self.engine is not None else None
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, pool=self.pool):
+        with _graph_safe_ops(), torch.cuda.graph(self.graph, pool=self.pool):
             self.static_out = self.step_fn(*self.static_in)
         if self.engine is not None:
             self.engine.step_count = saved

@@ -177,24 +177,30 @@ def test_graphed_llama_tiny_matches_eager(dph_native):
 
 
 @pytest.mark.gpu
-def test_graphed_resnet_fsdp_bf16_matches_eager(dph_native):
-    """FSDP units (world 1) + bf16 channels-last ResNet: MIOpen and framework conv / batch-norm kernels, SGD."""
+@pytest.mark.parametrize("arch", ["resnet18", "resnet50"])
+def test_graphed_resnet_fsdp_bf16_matches_eager(dph_native, arch):
+    """FSDP units (world 1) + bf16 channels-last ResNet: MIOpen and framework conv (1x1 bottleneck convolutions
+    for resnet50) / batch-norm kernels writing their weight gradients into the gradient bucket, SGD."""
     from distributed_pytorch_hpc_amd.models import resnet
 
     def make():
         torch.manual_seed(0)
-        return resnet("resnet18", num_classes=10, cifar_stem=True).to(DEV).to(memory_format=torch.channels_last)
+        return resnet(arch, num_classes=10, cifar_stem=True).to(DEV).to(memory_format=torch.channels_last)
 
     torch.manual_seed(3)
     batches = [(torch.randn(16, 3, 32, 32, device=DEV, dtype=torch.bfloat16).contiguous(
         memory_format=torch.channels_last), torch.randint(0, 10, (16,), device=DEV)) for _ in range(6)]
     cfg = lambda: OptimConfig("sgd", lr=0.002, momentum=0.9, weight_decay=1e-4)   # noqa: E731
-    # MIOpen's bf16 convolutions are not bit-reproducible run to run: two eager runs set the noise floor
+    p0 = [p.detach().float().clone() for p in make().parameters()]
+    # MIOpen's bf16 convolutions are not bit-reproducible run to run: two eager runs set the noise floor.  Compare
+    # the parameter UPDATES (a frozen or stale parameter shows up there, not in the parameters themselves)
     pe, le, _ = _run(make(), cfg(), batches, graphed=False, fsdp=True)
     pe2, le2, _ = _run(make(), cfg(), batches, graphed=False, fsdp=True)
     pg, lg, _ = _run(make(), cfg(), batches, graphed=True, fsdp=True)
-    floor = max(rel_err(a, b) for a, b in zip(pe2, pe))
-    assert max(rel_err(a, b) for a, b in zip(pg, pe)) < max(3 * floor, 2e-2)
+    de, de2, dg = ([a - b for a, b in zip(ps, p0)] for ps in (pe, pe2, pg))
+    floor = max(rel_err(a, b) for a, b in zip(de2, de))
+    worst = max(rel_err(a, b) for a, b in zip(dg, de))
+    assert worst < max(3 * floor, 5e-2), (worst, floor)
     assert rel_err(lg, le) < max(3 * rel_err(le2, le), 1e-2)
 
 

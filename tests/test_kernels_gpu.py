@@ -380,6 +380,35 @@ def test_bn_relu_mask_from_x_matches_y(dph_native, dtype):
         assert torch.equal(a, r)
 
 
+def test_conv1x1_bn_main_grad_direct(dph_native):
+    """Under the data-parallel engine the 1x1-conv weight gradient and BN dgamma / dbeta go straight into the
+    flat gradient bucket (no autograd gradient, no copy); two accumulated micro-steps match plain autograd."""
+    from distributed_pytorch_hpc_amd.ops.batchnorm import BatchNormAct2d
+    from distributed_pytorch_hpc_amd.ops.conv import Conv1x1
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, MixedPrecision, OptimConfig
+
+    def make():
+        torch.manual_seed(0)
+        return torch.nn.Sequential(Conv1x1(64, 128), BatchNormAct2d(128)).to(DEV).to(torch.bfloat16).to(
+            memory_format=torch.channels_last)
+
+    m, ref = make(), make()
+    eng = DataParallelEngine(m, mixed_precision=MixedPrecision(reduce_dtype=torch.bfloat16), convert_linears=False)
+    eng.configure_optimizer(OptimConfig("sgd", lr=0.0))
+    xs = [torch.randn(8, 64, 16, 16, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+          for _ in range(2)]
+    gs = [torch.randn(8, 128, 16, 16, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+          for _ in range(2)]
+    with eng.no_sync():
+        m(xs[0]).backward(gs[0])
+    m(xs[1]).backward(gs[1])
+    for x, g in zip(xs, gs):
+        ref(x).backward(g)
+    for p, r in zip(m.parameters(), ref.parameters()):
+        assert p.grad is None
+        assert rel_err(p.main_grad, r.grad) < 2e-2
+
+
 def test_bn_act_module_native_matches_torch(dph_native):
     """BatchNormAct2d (fused kernels) == nn.BatchNorm2d + add + ReLU, train and eval, incl. running stats."""
     from distributed_pytorch_hpc_amd.ops import BatchNormAct2d
