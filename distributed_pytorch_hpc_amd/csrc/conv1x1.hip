@@ -49,10 +49,13 @@ constexpr int TS_KF = TS_BK / 16;   // MFMA k-steps (A fragments) per K-step
 // K = 9 * Cin is tap-major (k = tap * Cin + c), and the A row of output pixel m for tap (dy, dx) is the input
 // pixel m + (dy-1) * W + (dx-1), or zero when that falls outside the image (padding).  A K-step never straddles
 // two taps (Cin % 64 == 0), so the shift is one wave-uniform offset per K-step plus a per-lane bounds check.
-template <int BN, bool C3>
+// ADD: C = A B^T + D (D [M, N] bf16 with C's leading dimension), the sum rounded once like an unfused add of
+// the two bf16 tensors -- merges a residual branch's input gradient into the 1x1 convolution's dgrad.
+template <int BN, bool C3, bool ADD = false>
 __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                  bf16* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                 int64_t ldb, int64_t ldc, int H, int W, int Cin) {
+                                                 int64_t ldb, int64_t ldc, int H, int W, int Cin,
+                                                 const bf16* __restrict__ D = nullptr) {
   constexpr int NT = BN / 32;                        // 32-column tiles per wave
   constexpr int BCH = BN * (TS_BK / 8) / TS_NT;      // 16-B B chunks per thread per K-step (BN=128: 4)
   constexpr int CROW = BN + 8;                       // epilogue LDS row (bf16)
@@ -156,9 +159,16 @@ __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, con
 #pragma unroll
   for (int i = threadIdx.x; i < TS_BM * CPR; i += TS_NT) {
     const int row = i / CPR, ch = i % CPR;
-    if (m0 + row < M)
-      *reinterpret_cast<bf16x8*>(C + (int64_t)(m0 + row) * ldc + nt0 + ch * 8) =
-          *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
+    if (m0 + row < M) {
+      const int64_t o = (int64_t)(m0 + row) * ldc + nt0 + ch * 8;
+      bf16x8 v = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
+      if constexpr (ADD) {
+        const bf16x8 d = *reinterpret_cast<const bf16x8*>(D + o);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)d[j]);
+      }
+      *reinterpret_cast<bf16x8*>(C + o) = v;
+    }
   }
 }
 
@@ -307,7 +317,7 @@ bool conv1x1_supported(int64_t M, int64_t N, int64_t K) {
 }
 
 void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, hipStream_t st, int H, int W) {
+                int64_t ldc, hipStream_t st, int H, int W, const void* D) {
   const int nmb = (int)cdiv(M, TS_BM);
   const bool c3 = H > 0;
   const int cin = c3 ? (int)(K / 9) : 0;
@@ -321,6 +331,15 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     return e ? atoi(e) : 0;
   }();
   const bool wide = N % 128 == 0 && force_bn != 64;
+  if (D != nullptr && !c3) {   // fused residual-gradient add (1x1 only)
+    if (wide)
+      hipLaunchKernelGGL((ts_nt_k<128, false, true>), dim3(nmb * (int)(N / 128)), dim3(TS_NT), 0, st, (const bf16*)A,
+                         (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, (const bf16*)D);
+    else
+      hipLaunchKernelGGL((ts_nt_k<64, false, true>), dim3(nmb * (int)(N / 64)), dim3(TS_NT), 0, st, (const bf16*)A,
+                         (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, (const bf16*)D);
+    return;
+  }
   if (wide) {
     if (c3) DPH_TS_NT(128, true);
     else DPH_TS_NT(128, false);

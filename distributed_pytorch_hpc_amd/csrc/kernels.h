@@ -110,7 +110,8 @@ void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_
 bool conv1x1_supported(int64_t M, int64_t N, int64_t K);
 // H, W > 0: 3x3 / stride-1 / pad-1 implicit GEMM over a channels-last [M = n*H*W, K/9] input (K tap-major).
 void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, hipStream_t stream, int H = 0, int W = 0);
+                int64_t ldc, hipStream_t stream, int H = 0, int W = 0,
+                const void* D = nullptr);
 int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K);
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
                 int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t stream, int H = 0,

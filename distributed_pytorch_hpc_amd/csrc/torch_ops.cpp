@@ -381,7 +381,8 @@ void gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate) {
 // C[M, N] = A[M, K] B[N, K]^T, bf16, row-major (channels-last 1x1 convolution forward / input gradient).
 // H, W > 0: 3x3 / stride-1 / pad-1 convolution as implicit GEMM, A = channels-last input [n*H*W, Cin],
 // B = weights [Cout, 9 * Cin] (tap-major).
-Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W) {
+// add (optional): C = A B^T + add, add [M, N] bf16 row-major (a residual branch's gradient merged in the epilogue)
+Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W, const c10::optional<Tensor>& add) {
   check_cuda(A, "A");
   c10::DeviceGuard g(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "ts_gemm_nt: 2-D operands required");
@@ -396,8 +397,17 @@ Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W) {
   check_align16(A, "A");
   check_align16(B, "B");
   Tensor C = at::empty({M, N}, A.options());
+  const void* D = nullptr;
+  if (add.has_value()) {
+    TORCH_CHECK(H == 0, "ts_gemm_nt: add is supported for 1x1 (H = 0) only");
+    TORCH_CHECK(add->scalar_type() == at::kBFloat16 && add->dim() == 2 && add->size(0) == M && add->size(1) == N &&
+                    add->is_contiguous() && add->device() == A.device(),
+                "ts_gemm_nt: add must be a contiguous bf16 [M, N] tensor");
+    check_align16(*add, "add");
+    D = add->data_ptr();
+  }
   dph::ts_gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
-                  cur_stream(), (int)H, (int)W);
+                  cur_stream(), (int)H, (int)W, D);
   return C;
 }
 
@@ -650,7 +660,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
   m.def("gemm_tn_mfma_(int shape) -> int", &gemm_tn_mfma_);   // no tensor argument: catch-all kernel
-  m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0) -> Tensor");
+  m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0, Tensor? add=None) -> Tensor");
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "

@@ -19,7 +19,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import Conv1x1, Conv3x3
+from ..ops.conv import Conv1x1, Conv3x3, GradSlot
 
 
 def conv3x3(cin, cout, stride=1):
@@ -63,10 +63,14 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
+        # identity blocks: conv1's input-gradient kernel also adds bn3's residual gradient (ops.conv.GradSlot)
+        slot = None
+        if self.downsample is None and isinstance(self.conv1, Conv1x1) and x.requires_grad and torch.is_grad_enabled():
+            slot = GradSlot()
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
+        out = self.bn1(self.conv1(x, grad_slot=slot) if slot is not None else self.conv1(x))
         out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), idt)
+        return self.bn3(self.conv3(out), idt, residual_grad_slot=slot)
 
 
 class ResNet(nn.Module):

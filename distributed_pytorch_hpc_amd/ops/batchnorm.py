@@ -39,7 +39,7 @@ def _native_ok(x: torch.Tensor, residual) -> bool:
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, slot=None):
         y, mean, invstd, ss = _lib.ops().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, momentum,
                                                     eps, relu)
         # ReLU without residual: the backward recomputes the mask from x with the forward's scale / shift and
@@ -49,6 +49,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.relu, ctx.has_res = relu, residual is not None
         ctx.has_wb = weight is not None
         ctx.params = (weight, bias)
+        ctx.slot = slot
         return y
 
     @staticmethod
@@ -71,15 +72,24 @@ class _BNActFn(torch.autograd.Function):
                 p._dph_accum = True
                 p._dph_grad_ready()
             dw = db = None
+        if ctx.slot is not None and ctx.has_res:   # the residual's gradient goes to the consuming 1x1 conv
+            ctx.slot.t = dres
+            dres = None
         return (dx, dw if need_wb else None, db if need_wb else None, None, None, dres if ctx.has_res else None,
-                None, None, None)
+                None, None, None, None)
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
-                   residual=None, relu: bool = True):
-    """act(batch_norm(x) + residual) with the fused kernels when eligible."""
+                   residual=None, relu: bool = True, residual_grad_slot=None):
+    """act(batch_norm(x) + residual) with the fused kernels when eligible.  ``residual_grad_slot``
+    (ops.conv.GradSlot): hand the residual's gradient to the 1x1 convolution that consumes the same input."""
     if _native_ok(x, residual):
         if training:
+            slot = residual_grad_slot
+            if slot is not None and residual is not None and slot.consumer and torch.is_grad_enabled():
+                slot.armed = True
+                return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual.detach(), momentum, eps,
+                                      relu, slot)
             return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, relu)
         with torch.no_grad():
             inv = torch.rsqrt(running_var.float() + eps)
@@ -101,7 +111,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         super().__init__(num_features, eps, momentum, affine, track_running_stats, **kw)
         self.act = act
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, residual_grad_slot=None):
         training = self.training or not self.track_running_stats
         momentum = self.momentum
         if self.training and self.track_running_stats:
@@ -112,7 +122,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         if training and rm is not None and not self.training:
             rm = rv = None
-        return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual, self.act)
+        return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual, self.act,
+                              residual_grad_slot)
 
     def extra_repr(self):
         return super().extra_repr() + f", act={'relu' if self.act else 'none'}"

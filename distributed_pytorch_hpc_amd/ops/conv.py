@@ -69,9 +69,26 @@ def _wgrad_into_main(w: torch.Tensor, shape, launch) -> bool:
     return True
 
 
+class GradSlot:
+    """Hand-off of a residual branch's input gradient into a 1x1 convolution's input-gradient epilogue.
+
+    In an identity ResNet bottleneck the block input x feeds conv1 and the residual add of bn3; autograd would sum
+    the two gradients of x with a separate add kernel (2 reads + 1 write of x's size).  With a slot, conv1 (on the
+    kernel path) marks itself the ``consumer``, bn3 takes the residual detached, ``arms`` the slot and leaves its
+    residual gradient in ``t`` -- bn3's backward runs before conv1's -- and conv1's dgrad kernel adds it in its
+    epilogue (``ts_gemm_nt(..., add=)``), so x receives one gradient."""
+
+    __slots__ = ("consumer", "armed", "t")
+
+    def __init__(self):
+        self.consumer = False
+        self.armed = False
+        self.t = None
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w):
+    def forward(ctx, x, w, slot=None):
         wdtype = w.dtype
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -81,7 +98,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         w2 = wb.view(wb.shape[0], C)
         y2 = _lib.ops().ts_gemm_nt(x2, w2)                          # [M, Cout]
         ctx.save_for_backward(x2, w2)
-        ctx.shape, ctx.wdtype, ctx.param = (B, C, H, W), wdtype, w
+        ctx.shape, ctx.wdtype, ctx.param, ctx.slot = (B, C, H, W), wdtype, w, slot
         return y2.view(B, H, W, -1).permute(0, 3, 1, 2)             # channels-last [B, Cout, H, W]
 
     @staticmethod
@@ -90,8 +107,15 @@ class _Conv1x1Fn(torch.autograd.Function):
         B, C, H, W = ctx.shape
         dy2 = _nhwc2d(dy.to(torch.bfloat16))                        # [M, Cout]
         dx = gw = None
+        slot = ctx.slot
         if ctx.needs_input_grad[0]:
-            dx2 = _lib.ops().ts_gemm_nt(dy2, w2.t().contiguous())    # [M, Cin]
+            add = None
+            if slot is not None and slot.armed:
+                if slot.t is None:
+                    raise RuntimeError("Conv1x1: residual gradient slot armed but empty (backward order)")
+                add = _nhwc2d(slot.t.to(torch.bfloat16))
+                slot.t = None
+            dx2 = _lib.ops().ts_gemm_nt(dy2, w2.t().contiguous(), 0, 0, add)    # [M, Cin] (+ residual grad)
             dx = dx2.view(B, H, W, C).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             cout = w2.shape[0]
@@ -99,7 +123,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 gw = torch.empty((cout, C), dtype=ctx.wdtype, device=dy.device)
                 _lib.ops().ts_gemm_tn_(gw, dy2, x2, False)
                 gw = gw.view(cout, C, 1, 1)
-        return dx, gw
+        return dx, gw, None
 
 
 class _Conv3x3Fn(torch.autograd.Function):
@@ -175,8 +199,10 @@ class Conv1x1(nn.Conv2d):
     def __init__(self, in_channels: int, out_channels: int):
         super().__init__(in_channels, out_channels, kernel_size=1, stride=1, padding=0, bias=False)
 
-    def forward(self, x):
+    def forward(self, x, grad_slot: GradSlot | None = None):
         if conv1x1_native_ok(x, self.weight):
             _lib.require()
-            return _Conv1x1Fn.apply(x, self.weight)
+            if grad_slot is not None:
+                grad_slot.consumer = True
+            return _Conv1x1Fn.apply(x, self.weight, grad_slot)
         return F.conv2d(x, self.weight)

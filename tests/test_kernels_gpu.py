@@ -615,6 +615,48 @@ def test_bottleneck_conv1x1_path_matches_miopen_gradients(dph_native, monkeypatc
     assert e_dph < 1.5 * e_miopen + 1e-3, (e_dph, e_miopen)
 
 
+def test_bottleneck_residual_grad_slot(dph_native, monkeypatch):
+    """Identity bottleneck: bn3's residual gradient is added inside conv1's input-gradient kernel (ops.conv.GradSlot)
+    instead of by autograd; input and parameter gradients match the MIOpen path (autograd add)."""
+    import importlib
+
+    from distributed_pytorch_hpc_amd.ops.conv import GradSlot
+
+    resnet_mod = importlib.import_module("distributed_pytorch_hpc_amd.models.resnet")   # (the package exports a
+    # function of the same name)
+
+    made = []
+
+    class _Spy(GradSlot):
+        __slots__ = ()
+
+        def __init__(self):
+            super().__init__()
+            made.append(self)
+
+    monkeypatch.setattr(resnet_mod, "GradSlot", _Spy)
+    torch.manual_seed(0)
+    block = resnet_mod.Bottleneck(256, 64).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(8, 256, 16, 16, device=DEV, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+
+    def run(flag):
+        monkeypatch.setenv("DPH_CONV1X1", flag)
+        block.zero_grad(set_to_none=True)
+        x.grad = None
+        made.clear()
+        block(x).float().pow(2).mean().backward()
+        return x.grad.float().clone(), {n: p.grad.float().clone() for n, p in block.named_parameters()}
+
+    gx1, g1 = run("1")
+    assert made and made[0].armed and made[0].t is None     # handed over and consumed
+    gx0, g0 = run("0")
+    assert not made[0].armed                                # MIOpen path: autograd adds the residual gradient
+    assert rel_err(gx1, gx0) < 2e-2
+    for n in g0:
+        assert rel_err(g1[n], g0[n]) < 5e-2, n
+
+
 @pytest.mark.parametrize("B,C,Co,H,W", [(2, 64, 64, 14, 14), (3, 128, 64, 7, 9), (1, 64, 192, 5, 5)])
 @pytest.mark.parametrize("autocast", [False, True])
 def test_conv3x3_module_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W, autocast):
