@@ -146,6 +146,40 @@ __global__ __launch_bounds__(BN_NT) void bn_finalize_k(const float* __restrict__
   }
 }
 
+// Merge G (large) statistics partials into gridDim.y segment partials: block (channel chunk, segment s) Chan-merges
+// partials [s*G/S, (s+1)*G/S) of its 8 channels (32 thread groups, then an LDS tree), so bn_finalize_k sees few
+// partials.  Used when the partials come per 128-row block from the 1x1 convolution epilogue (thousands of them).
+__global__ __launch_bounds__(BN_NT) void bn_merge_k(const float* __restrict__ pmean, const float* __restrict__ pm2,
+                                                    const float* __restrict__ pn, int G, int C,
+                                                    float* __restrict__ omean, float* __restrict__ om2,
+                                                    float* __restrict__ on) {
+  __shared__ float sh[3][BN_NT];
+  const int c = blockIdx.x * 8 + (threadIdx.x & 7), grp = threadIdx.x >> 3;
+  const int S = gridDim.y, sgm = blockIdx.y;
+  const int g_beg = (int)((int64_t)G * sgm / S), g_end = (int)((int64_t)G * (sgm + 1) / S);
+  Stat acc = {0.f, 0.f, 0.f};
+  for (int g = g_beg + grp; g < g_end; g += FIN_GROUPS)
+    acc = chan_merge(acc, Stat{pn[g], pmean[(int64_t)g * C + c], pm2[(int64_t)g * C + c]});
+  sh[0][threadIdx.x] = acc.n;
+  sh[1][threadIdx.x] = acc.mean;
+  sh[2][threadIdx.x] = acc.m2;
+  __syncthreads();
+  for (int half = FIN_GROUPS / 2; half > 0; half >>= 1) {
+    if (grp < half) {
+      const int o = threadIdx.x + half * 8;
+      acc = chan_merge(acc, {sh[0][o], sh[1][o], sh[2][o]});
+      sh[0][threadIdx.x] = acc.n;
+      sh[1][threadIdx.x] = acc.mean;
+      sh[2][threadIdx.x] = acc.m2;
+    }
+    __syncthreads();
+  }
+  if (grp != 0) return;
+  omean[(int64_t)sgm * C + c] = acc.mean;
+  om2[(int64_t)sgm * C + c] = acc.m2;
+  if (c == 0) on[sgm] = acc.n;
+}
+
 // y = act(x * scale + shift [+ res])
 template <typename T, bool RES, bool RELU>
 __global__ __launch_bounds__(BN_NT) void bn_apply_k(const T* __restrict__ x, const T* __restrict__ res,
@@ -313,16 +347,32 @@ int bn_partial_blocks(int64_t M, int64_t C) {
 
 void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const void* b, void* rmean, void* rvar,
                   float* mean, float* invstd, float* scale, float* shift, float* workspace, int64_t M, int64_t C,
-                  float momentum, float eps, bool relu, int dt, int pdt, int rdt, hipStream_t st) {
+                  float momentum, float eps, bool relu, int dt, int pdt, int rdt, hipStream_t st,
+                  const float* pre_stats, int pre_groups) {
   int64_t rpb;
-  const int G = stats_grid(M, (int)C, &rpb);
-  float* pmean = workspace;
-  float* pm2 = workspace + (int64_t)G * C;
-  float* pn = workspace + 2 * (int64_t)G * C;
-  const size_t shs = 3 * BN_NT * 8 * sizeof(float);
-  DPH_DISPATCH_FLOAT(dt, T, {
-    hipLaunchKernelGGL(bn_stats_k<T>, dim3(G), dim3(BN_NT), shs, st, (const T*)x, pmean, pm2, pn, M, (int)C, rpb);
-  });
+  int G = stats_grid(M, (int)C, &rpb);
+  const float* pmean = workspace;
+  const float* pm2 = workspace + (int64_t)G * C;
+  const float* pn = workspace + 2 * (int64_t)G * C;
+  if (pre_stats) {   // partials from the producing 1x1 convolution's epilogue, merged down to <= G segments
+    const int S = std::min(G, 64);
+    float* om = workspace;
+    float* o2 = workspace + (int64_t)S * C;
+    float* on = workspace + 2 * (int64_t)S * C;
+    hipLaunchKernelGGL(bn_merge_k, dim3((unsigned)(C / 8), (unsigned)S), dim3(BN_NT), 0, st, pre_stats,
+                       pre_stats + (int64_t)pre_groups * C, pre_stats + 2 * (int64_t)pre_groups * C, pre_groups,
+                       (int)C, om, o2, on);
+    G = S;
+    pmean = om;
+    pm2 = o2;
+    pn = on;
+  } else {
+    const size_t shs = 3 * BN_NT * 8 * sizeof(float);
+    DPH_DISPATCH_FLOAT(dt, T, {
+      hipLaunchKernelGGL(bn_stats_k<T>, dim3(G), dim3(BN_NT), shs, st, (const T*)x, workspace,
+                         workspace + (int64_t)G * C, workspace + 2 * (int64_t)G * C, M, (int)C, rpb);
+    });
+  }
   const dim3 fg((unsigned)(C / 8));
 #define DPH_BN_FIN(PT_, RT_)                                                                                    \
   hipLaunchKernelGGL((bn_finalize_k<PT_, RT_>), fg, dim3(BN_NT), 0, st, pmean, pm2, pn, G, (int)C, (const PT_*)w, \

@@ -51,11 +51,16 @@ constexpr int TS_KF = TS_BK / 16;   // MFMA k-steps (A fragments) per K-step
 // two taps (Cin % 64 == 0), so the shift is one wave-uniform offset per K-step plus a per-lane bounds check.
 // ADD: C = A B^T + D (D [M, N] bf16 with C's leading dimension), the sum rounded once like an unfused add of
 // the two bf16 tensors -- merges a residual branch's input gradient into the 1x1 convolution's dgrad.
-template <int BN, bool C3, bool ADD = false>
+// STATS: also emit per-row-block BatchNorm statistics of the bf16 output (the values BN will read): for row block
+// mb and column n, stats[mb * N + n] = mean, stats[nmb * N + mb * N + n] = M2 (sum of squared deviations),
+// stats[2 * nmb * N + mb] = rows -- the partial layout bn_finalize_k merges (Chan), so the BN that follows a
+// 1x1 convolution skips its own statistics pass over the activation.
+template <int BN, bool C3, bool ADD = false, bool STATS = false>
 __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                  bf16* __restrict__ C, int M, int N, int K, int64_t lda,
                                                  int64_t ldb, int64_t ldc, int H, int W, int Cin,
-                                                 const bf16* __restrict__ D = nullptr) {
+                                                 const bf16* __restrict__ D = nullptr,
+                                                 float* __restrict__ stats = nullptr) {
   constexpr int NT = BN / 32;                        // 32-column tiles per wave
   constexpr int BCH = BN * (TS_BK / 8) / TS_NT;      // 16-B B chunks per thread per K-step (BN=128: 4)
   constexpr int CROW = BN + 8;                       // epilogue LDS row (bf16)
@@ -168,6 +173,45 @@ __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, con
         for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)d[j]);
       }
       *reinterpret_cast<bf16x8*>(C + o) = v;
+    }
+  }
+  if constexpr (STATS) {
+    // thread -> column c, row group rg of RG = TS_NT / BN groups; two passes over its rows (mean, then M2), then
+    // a Chan merge of the RG partials through LDS
+    constexpr int RG = TS_NT / BN, RPG = TS_BM / RG;
+    __shared__ float sred[3][TS_NT];
+    const int c = threadIdx.x % BN, rg = threadIdx.x / BN;
+    const int valid = min(TS_BM, M - m0);
+    const int r0 = rg * RPG, r1 = min(r0 + RPG, valid);
+    float sum = 0.f;
+    for (int r = r0; r < r1; ++r) sum += (float)Cs[r * CROW + c];
+    const float n = (float)max(r1 - r0, 0);
+    const float mean = n > 0.f ? sum / n : 0.f;
+    float m2 = 0.f;
+    for (int r = r0; r < r1; ++r) {
+      const float d = (float)Cs[r * CROW + c] - mean;
+      m2 = fmaf(d, d, m2);
+    }
+    sred[0][threadIdx.x] = n;
+    sred[1][threadIdx.x] = mean;
+    sred[2][threadIdx.x] = m2;
+    __syncthreads();
+    if (rg == 0) {
+      float an = n, am = mean, a2 = m2;
+#pragma unroll
+      for (int g = 1; g < RG; ++g) {
+        const int t = g * BN + c;
+        const float bn_ = sred[0][t];
+        if (bn_ == 0.f) continue;
+        const float tot = an + bn_, d = sred[1][t] - am, f = bn_ / tot;
+        am += d * f;
+        a2 += sred[2][t] + d * d * an * f;
+        an = tot;
+      }
+      const int nmb = (M + TS_BM - 1) / TS_BM;
+      stats[(int64_t)mb * N + nt0 + c] = am;
+      stats[(int64_t)nmb * N + (int64_t)mb * N + nt0 + c] = a2;
+      if (c == 0 && nt0 == 0) stats[2 * (int64_t)nmb * N + mb] = (float)valid;
     }
   }
 }
@@ -317,7 +361,7 @@ bool conv1x1_supported(int64_t M, int64_t N, int64_t K) {
 }
 
 void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, hipStream_t st, int H, int W, const void* D) {
+                int64_t ldc, hipStream_t st, int H, int W, const void* D, float* stats) {
   const int nmb = (int)cdiv(M, TS_BM);
   const bool c3 = H > 0;
   const int cin = c3 ? (int)(K / 9) : 0;
@@ -331,6 +375,17 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     return e ? atoi(e) : 0;
   }();
   const bool wide = N % 128 == 0 && force_bn != 64;
+  if (stats != nullptr && !c3) {   // BatchNorm statistics of the output (1x1 forward only)
+    if (wide)
+      hipLaunchKernelGGL((ts_nt_k<128, false, false, true>), dim3(nmb * (int)(N / 128)), dim3(TS_NT), 0, st,
+                         (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin,
+                         (const bf16*)nullptr, stats);
+    else
+      hipLaunchKernelGGL((ts_nt_k<64, false, false, true>), dim3(nmb * (int)(N / 64)), dim3(TS_NT), 0, st,
+                         (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin,
+                         (const bf16*)nullptr, stats);
+    return;
+  }
   if (D != nullptr && !c3) {   // fused residual-gradient add (1x1 only)
     if (wide)
       hipLaunchKernelGGL((ts_nt_k<128, false, true>), dim3(nmb * (int)(N / 128)), dim3(TS_NT), 0, st, (const bf16*)A,

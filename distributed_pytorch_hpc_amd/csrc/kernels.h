@@ -111,7 +111,7 @@ bool conv1x1_supported(int64_t M, int64_t N, int64_t K);
 // H, W > 0: 3x3 / stride-1 / pad-1 implicit GEMM over a channels-last [M = n*H*W, K/9] input (K tap-major).
 void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, hipStream_t stream, int H = 0, int W = 0,
-                const void* D = nullptr);
+                const void* D = nullptr, float* stats = nullptr);
 int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K);
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
                 int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t stream, int H = 0,
@@ -121,10 +121,12 @@ void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M
 // Workspaces (fp32): forward 2*G*C + G, backward 2*G*C + 3*C floats with G = bn_partial_blocks(M, C).
 bool bn_nhwc_supported(int64_t C);
 int bn_partial_blocks(int64_t M, int64_t C);
+// pre_stats (optional): per-row-block partials [mean G*C | M2 G*C | rows G] already computed by the producer of x
+// (ts_gemm_nt with stats), G = pre_groups: the statistics pass is skipped.
 void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const void* b, void* rmean, void* rvar,
                   float* mean, float* invstd, float* scale, float* shift, float* workspace, int64_t M, int64_t C,
                   float momentum, float eps, bool relu, int dtype, int param_dtype, int running_dtype,
-                  hipStream_t stream);
+                  hipStream_t stream, const float* pre_stats = nullptr, int pre_groups = 0);
 void bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int64_t M, int64_t C,
               bool relu, int dtype, hipStream_t stream);
 // xmask_ss (optional, fp32 [scale | shift] of the forward): ReLU mask from x instead of reading y.

@@ -411,6 +411,27 @@ Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W, const 
   return C;
 }
 
+// C = A B^T plus the BatchNorm statistics partials of C per 128-row block ([mean | M2 | rows], see conv1x1.hip).
+std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B) {
+  check_cuda(A, "A");
+  c10::DeviceGuard g(A.device());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
+              "ts_gemm_nt_stats: bf16 2-D operands");
+  const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+  TORCH_CHECK(B.size(1) == K, "ts_gemm_nt_stats: K mismatch");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
+              "ts_gemm_nt_stats: row-major operands with 16-B aligned rows required");
+  TORCH_CHECK(dph::conv1x1_supported(M, N, K), "ts_gemm_nt_stats: need N, K % 64 == 0");
+  check_align16(A, "A");
+  check_align16(B, "B");
+  const int64_t nmb = (M + 127) / 128;
+  Tensor C = at::empty({M, N}, A.options());
+  Tensor st = at::empty({2 * nmb * N + nmb}, A.options().dtype(at::kFloat));
+  dph::ts_gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
+                  cur_stream(), 0, 0, nullptr, st.data_ptr<float>());
+  return {C, st};
+}
+
 // C[N, K] (+)= A[M, N]^T B[M, K] (1x1 convolution weight gradient, split over pixel chunks).
 // H, W > 0: 3x3 weight gradient, C [N, 9 * K_in] tap-major, B = channels-last input [n*H*W, K_in].
 void ts_gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate, int64_t H, int64_t W) {
@@ -475,7 +496,8 @@ void check_like(const Tensor& a, const Tensor& x, const char* name) {
 std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10::optional<Tensor>& res,
                                               const c10::optional<Tensor>& w, const c10::optional<Tensor>& b,
                                               const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
-                                              double momentum, double eps, bool relu) {
+                                              double momentum, double eps, bool relu,
+                                              const c10::optional<Tensor>& pre_stats) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
   const int64_t C = bn_channels(x), M = x.numel() / C;
@@ -490,6 +512,14 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
   auto y = at::empty_like(x);
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
   auto ss = at::empty({2 * C}, fopt);   // [scale | shift]: the backward recomputes the ReLU mask from them
+  const Tensor* pre = pre_stats.has_value() ? &*pre_stats : nullptr;
+  int pre_groups = 0;
+  if (pre) {
+    TORCH_CHECK(pre->scalar_type() == at::kFloat && pre->is_contiguous() && pre->numel() % (2 * C + 1) == 0 &&
+                    pre->device() == x.device(),
+                "bn_act_fwd: pre_stats must be fp32 [mean G*C | M2 G*C | rows G]");
+    pre_groups = (int)(pre->numel() / (2 * C + 1));
+  }
   const int G = dph::bn_partial_blocks(M, C);
   auto ws = at::empty({2 * (int64_t)G * C + G}, fopt);
   const int pdt = w ? dt_code(*w) : (b ? dt_code(*b) : dph::kF32);
@@ -498,7 +528,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
                     b ? b->data_ptr() : nullptr, rmean ? rmean->data_ptr() : nullptr,
                     rvar ? rvar->data_ptr() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                     ss.data_ptr<float>(), ss.data_ptr<float>() + C, ws.data_ptr<float>(), M, C, (float)momentum,
-                    (float)eps, relu, dt_code(x), pdt, rdt, cur_stream());
+                    (float)eps, relu, dt_code(x), pdt, rdt, cur_stream(), pre ? pre->data_ptr<float>() : nullptr,
+                    pre_groups);
   return {y, mean, invstd, ss};
 }
 
@@ -661,10 +692,11 @@ TORCH_LIBRARY(dph, m) {
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
   m.def("gemm_tn_mfma_(int shape) -> int", &gemm_tn_mfma_);   // no tensor argument: catch-all kernel
   m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0, Tensor? add=None) -> Tensor");
+  m.def("ts_gemm_nt_stats(Tensor A, Tensor B) -> (Tensor, Tensor)");
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-        "float momentum, float eps, bool relu) -> (Tensor, Tensor, Tensor, Tensor)");
+        "float momentum, float eps, bool relu, Tensor? pre_stats=None) -> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "
         "bool need_dwb, Tensor? xmask_ss=None, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) "
@@ -702,6 +734,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("gemm_tn_", &gemm_tn_);
   m.impl("ts_gemm_nt", &ts_gemm_nt);
+  m.impl("ts_gemm_nt_stats", &ts_gemm_nt_stats);
   m.impl("ts_gemm_tn_", &ts_gemm_tn_);
   m.impl("transpose2d", &transpose2d);
   m.impl("bn_act_fwd", &bn_act_fwd);

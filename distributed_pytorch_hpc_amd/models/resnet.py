@@ -19,7 +19,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import Conv1x1, Conv3x3, GradSlot
+from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot
 
 
 def conv3x3(cin, cout, stride=1):
@@ -67,10 +67,13 @@ class Bottleneck(nn.Module):
         slot = None
         if self.downsample is None and isinstance(self.conv1, Conv1x1) and x.requires_grad and torch.is_grad_enabled():
             slot = GradSlot()
+        # training-mode BN after a 1x1 convolution takes its statistics from the convolution's epilogue
+        s1 = StatsSlot() if self.bn1.training and isinstance(self.conv1, Conv1x1) else None
+        s3 = StatsSlot() if self.bn3.training and isinstance(self.conv3, Conv1x1) else None
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x, grad_slot=slot) if slot is not None else self.conv1(x))
+        out = self.bn1(self.conv1(x, grad_slot=slot, stats_slot=s1), stats_slot=s1)
         out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out), idt, residual_grad_slot=slot)
+        return self.bn3(self.conv3(out, stats_slot=s3), idt, residual_grad_slot=slot, stats_slot=s3)
 
 
 class ResNet(nn.Module):

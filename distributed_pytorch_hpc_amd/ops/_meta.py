@@ -74,7 +74,7 @@ def _sumsq(x, out):
 
 
 @register_fake("dph::bn_act_fwd")
-def _bn_act_fwd(x, res, w, b, rm, rv, momentum, eps, relu):
+def _bn_act_fwd(x, res, w, b, rm, rv, momentum, eps, relu, pre_stats=None):
     c = x.shape[1]
     return (torch.empty_like(x), x.new_empty((c,), dtype=torch.float32), x.new_empty((c,), dtype=torch.float32),
             x.new_empty((2 * c,), dtype=torch.float32))
@@ -101,6 +101,13 @@ def _transpose2d(x):
 @register_fake("dph::gemm_tn_")
 def _gemm_tn(C, A, B, accumulate):
     return None
+
+
+@register_fake("dph::ts_gemm_nt_stats")
+def _ts_gemm_nt_stats(A, B):
+    m, n = A.shape[0], B.shape[0]
+    nmb = (m + 127) // 128
+    return A.new_empty((m, n)), A.new_empty((2 * nmb * n + nmb,), dtype=torch.float32)
 
 
 @register_fake("dph::ts_gemm_nt")

@@ -39,9 +39,10 @@ def _native_ok(x: torch.Tensor, residual) -> bool:
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, slot=None):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, slot=None,
+                pre_stats=None):
         y, mean, invstd, ss = _lib.ops().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, momentum,
-                                                    eps, relu)
+                                                    eps, relu, pre_stats)
         # ReLU without residual: the backward recomputes the mask from x with the forward's scale / shift and
         # never reads y (one activation-sized read less in each backward pass)
         ctx.xmask = relu and residual is None
@@ -76,21 +77,24 @@ class _BNActFn(torch.autograd.Function):
             ctx.slot.t = dres
             dres = None
         return (dx, dw if need_wb else None, db if need_wb else None, None, None, dres if ctx.has_res else None,
-                None, None, None, None)
+                None, None, None, None, None)
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
-                   residual=None, relu: bool = True, residual_grad_slot=None):
+                   residual=None, relu: bool = True, residual_grad_slot=None, stats_slot=None):
     """act(batch_norm(x) + residual) with the fused kernels when eligible.  ``residual_grad_slot``
     (ops.conv.GradSlot): hand the residual's gradient to the 1x1 convolution that consumes the same input."""
     if _native_ok(x, residual):
         if training:
+            # statistics already computed by the producing 1x1 convolution (ops.conv.StatsSlot)
+            pre = stats_slot.take(x.numel() // x.shape[1], x.shape[1]) if stats_slot is not None else None
             slot = residual_grad_slot
             if slot is not None and residual is not None and slot.consumer and torch.is_grad_enabled():
                 slot.armed = True
                 return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual.detach(), momentum, eps,
-                                      relu, slot)
-            return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, relu)
+                                      relu, slot, pre)
+            return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, None,
+                                  pre)
         with torch.no_grad():
             inv = torch.rsqrt(running_var.float() + eps)
             scale = inv * (weight.float() if weight is not None else 1.0)
@@ -111,7 +115,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         super().__init__(num_features, eps, momentum, affine, track_running_stats, **kw)
         self.act = act
 
-    def forward(self, x, residual=None, residual_grad_slot=None):
+    def forward(self, x, residual=None, residual_grad_slot=None, stats_slot=None):
         training = self.training or not self.track_running_stats
         momentum = self.momentum
         if self.training and self.track_running_stats:
@@ -123,7 +127,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         if training and rm is not None and not self.training:
             rm = rv = None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual, self.act,
-                              residual_grad_slot)
+                              residual_grad_slot, stats_slot)
 
     def extra_repr(self):
         return super().extra_repr() + f", act={'relu' if self.act else 'none'}"

@@ -86,9 +86,25 @@ class GradSlot:
         self.t = None
 
 
+class StatsSlot:
+    """BatchNorm statistics of a 1x1 convolution's output, computed in the convolution's epilogue
+    (``ts_gemm_nt_stats``: per-128-row-block [mean | M2 | rows] partials) and consumed by the BatchNorm that
+    follows, which then skips its own statistics pass over the activation."""
+
+    __slots__ = ("stats", "rows", "cols")
+
+    def __init__(self):
+        self.stats = None
+        self.rows = self.cols = 0
+
+    def take(self, rows: int, cols: int):
+        st, self.stats = self.stats, None
+        return st if st is not None and (self.rows, self.cols) == (rows, cols) else None
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, slot=None):
+    def forward(ctx, x, w, slot=None, stats_slot=None):
         wdtype = w.dtype
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -96,7 +112,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         B, C, H, W = x.shape
         x2 = _nhwc2d(x)
         w2 = wb.view(wb.shape[0], C)
-        y2 = _lib.ops().ts_gemm_nt(x2, w2)                          # [M, Cout]
+        if stats_slot is not None:
+            y2, stats_slot.stats = _lib.ops().ts_gemm_nt_stats(x2, w2)   # [M, Cout] + BN partials
+            stats_slot.rows, stats_slot.cols = y2.shape
+        else:
+            y2 = _lib.ops().ts_gemm_nt(x2, w2)                      # [M, Cout]
         ctx.save_for_backward(x2, w2)
         ctx.shape, ctx.wdtype, ctx.param, ctx.slot = (B, C, H, W), wdtype, w, slot
         return y2.view(B, H, W, -1).permute(0, 3, 1, 2)             # channels-last [B, Cout, H, W]
@@ -123,7 +143,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                 gw = torch.empty((cout, C), dtype=ctx.wdtype, device=dy.device)
                 _lib.ops().ts_gemm_tn_(gw, dy2, x2, False)
                 gw = gw.view(cout, C, 1, 1)
-        return dx, gw, None
+        return dx, gw, None, None
 
 
 class _Conv3x3Fn(torch.autograd.Function):
@@ -199,10 +219,10 @@ class Conv1x1(nn.Conv2d):
     def __init__(self, in_channels: int, out_channels: int):
         super().__init__(in_channels, out_channels, kernel_size=1, stride=1, padding=0, bias=False)
 
-    def forward(self, x, grad_slot: GradSlot | None = None):
+    def forward(self, x, grad_slot: GradSlot | None = None, stats_slot: StatsSlot | None = None):
         if conv1x1_native_ok(x, self.weight):
             _lib.require()
             if grad_slot is not None:
                 grad_slot.consumer = True
-            return _Conv1x1Fn.apply(x, self.weight, grad_slot)
+            return _Conv1x1Fn.apply(x, self.weight, grad_slot, stats_slot)
         return F.conv2d(x, self.weight)

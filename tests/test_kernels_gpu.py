@@ -615,6 +615,28 @@ def test_bottleneck_conv1x1_path_matches_miopen_gradients(dph_native, monkeypatc
     assert e_dph < 1.5 * e_miopen + 1e-3, (e_dph, e_miopen)
 
 
+@pytest.mark.parametrize("M,K,N", [(8 * 28 * 28, 128, 512), (1000, 64, 64), (257, 256, 128)])
+def test_conv_epilogue_bn_stats(dph_native, M, K, N):
+    """ts_gemm_nt_stats: the per-128-row-block BatchNorm partials of the bf16 output drive bn_act_fwd to the same
+    output / mean / invstd / running statistics as its own statistics pass (ragged last row block included)."""
+    torch.manual_seed(M)
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = (torch.randn(N, K, device=DEV) * 0.1 + 0.02).to(torch.bfloat16)
+    y, st = torch.ops.dph.ts_gemm_nt_stats(a, b)
+    assert torch.equal(y, torch.ops.dph.ts_gemm_nt(a, b))
+    w = (1 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    bias = (0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    rm0, rv0 = torch.zeros(N, device=DEV), torch.ones(N, device=DEV)
+    rm1, rv1 = rm0.clone(), rv0.clone()
+    ref = torch.ops.dph.bn_act_fwd(y, None, w, bias, rm0, rv0, 0.1, 1e-5, True)
+    got = torch.ops.dph.bn_act_fwd(y, None, w, bias, rm1, rv1, 0.1, 1e-5, True, st)
+    for a_, r_ in zip(got, ref):
+        assert rel_err(a_, r_) < 1e-4
+    assert rel_err(rm1, rm0) < 1e-4 and rel_err(rv1, rv0) < 1e-4
+    yf = y.float()
+    assert rel_err(got[1], yf.mean(0)) < 1e-4
+
+
 def test_bottleneck_residual_grad_slot(dph_native, monkeypatch):
     """Identity bottleneck: bn3's residual gradient is added inside conv1's input-gradient kernel (ops.conv.GradSlot)
     instead of by autograd; input and parameter gradients match the MIOpen path (autograd add)."""
