@@ -64,7 +64,7 @@ __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, con
   constexpr int NT = BN / 32;                        // 32-column tiles per wave
   constexpr int BCH = BN * (TS_BK / 8) / TS_NT;      // 16-B B chunks per thread per K-step (BN=128: 4)
   constexpr int CROW = BN + 8;                       // epilogue LDS row (bf16)
-  constexpr int LDS_B = 2 * BN * TS_BROW * 2, LDS_C = TS_BM * CROW * 2;
+  constexpr int LDS_B = 2 * BN * TS_BROW * 2, LDS_C = TS_BM * CROW * 2 + (STATS ? 4 * BN * 4 : 0);
   __shared__ __attribute__((aligned(16))) char smem[LDS_B > LDS_C ? LDS_B : LDS_C];
   bf16* Bs = reinterpret_cast<bf16*>(smem);
 
@@ -176,42 +176,54 @@ __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, con
     }
   }
   if constexpr (STATS) {
-    // thread -> column c, row group rg of RG = TS_NT / BN groups; two passes over its rows (mean, then M2), then
-    // a Chan merge of the RG partials through LDS
-    constexpr int RG = TS_NT / BN, RPG = TS_BM / RG;
-    __shared__ float sred[3][TS_NT];
-    const int c = threadIdx.x % BN, rg = threadIdx.x / BN;
+    // from the accumulator registers (rounded to bf16, the values BN will read): register r of tile t is row
+    // wid*32 + (r&3) + 8(r>>2) + 4h of column t*32 + l32.  Pass 1 column sums, pass 2 squared deviations from the
+    // tile mean; the lane halves (h) meet by a cross-half shuffle, the 4 waves in a [4][BN] LDS block behind the
+    // C tile (it fits in the K-loop's staging footprint for BN = 128).
+    float* sred = reinterpret_cast<float*>(smem + TS_BM * CROW * 2);
     const int valid = min(TS_BM, M - m0);
-    const int r0 = rg * RPG, r1 = min(r0 + RPG, valid);
-    float sum = 0.f;
-    for (int r = r0; r < r1; ++r) sum += (float)Cs[r * CROW + c];
-    const float n = (float)max(r1 - r0, 0);
-    const float mean = n > 0.f ? sum / n : 0.f;
-    float m2 = 0.f;
-    for (int r = r0; r < r1; ++r) {
-      const float d = (float)Cs[r * CROW + c] - mean;
-      m2 = fmaf(d, d, m2);
-    }
-    sred[0][threadIdx.x] = n;
-    sred[1][threadIdx.x] = mean;
-    sred[2][threadIdx.x] = m2;
-    __syncthreads();
-    if (rg == 0) {
-      float an = n, am = mean, a2 = m2;
+    const float inv_n = 1.f / (float)valid;
 #pragma unroll
-      for (int g = 1; g < RG; ++g) {
-        const int t = g * BN + c;
-        const float bn_ = sred[0][t];
-        if (bn_ == 0.f) continue;
-        const float tot = an + bn_, d = sred[1][t] - am, f = bn_ / tot;
-        am += d * f;
-        a2 += sred[2][t] + d * d * an * f;
-        an = tot;
+    for (int t = 0; t < NT; ++t) {
+      float sm = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        sm += row < valid ? (float)(bf16)acc[t][r] : 0.f;
       }
-      const int nmb = (M + TS_BM - 1) / TS_BM;
-      stats[(int64_t)mb * N + nt0 + c] = am;
-      stats[(int64_t)nmb * N + (int64_t)mb * N + nt0 + c] = a2;
-      if (c == 0 && nt0 == 0) stats[2 * (int64_t)nmb * N + mb] = (float)valid;
+      sm += __shfl_xor(sm, 32);
+      if (h == 0) sred[wid * BN + t * 32 + l32] = sm;
+    }
+    __syncthreads();
+    float mean_t[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = t * 32 + l32;
+      mean_t[t] = (sred[col] + sred[BN + col] + sred[2 * BN + col] + sred[3 * BN + col]) * inv_n;
+    }
+    const float mean_w = threadIdx.x < BN ? (sred[threadIdx.x] + sred[BN + threadIdx.x] + sred[2 * BN + threadIdx.x] +
+                                             sred[3 * BN + threadIdx.x]) * inv_n
+                                          : 0.f;
+    __syncthreads();   // every wave has read the sums before they are overwritten by the M2 partials
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float m2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float d = (float)(bf16)acc[t][r] - mean_t[t];
+        m2 += row < valid ? d * d : 0.f;
+      }
+      m2 += __shfl_xor(m2, 32);
+      if (h == 0) sred[wid * BN + t * 32 + l32] = m2;
+    }
+    __syncthreads();
+    if (threadIdx.x < BN) {
+      const int col = threadIdx.x, nmb = (M + TS_BM - 1) / TS_BM;
+      stats[(int64_t)mb * N + nt0 + col] = mean_w;
+      stats[(int64_t)nmb * N + (int64_t)mb * N + nt0 + col] =
+          sred[col] + sred[BN + col] + sred[2 * BN + col] + sred[3 * BN + col];
+      if (col == 0 && nt0 == 0) stats[2 * (int64_t)nmb * N + mb] = (float)valid;
     }
   }
 }
