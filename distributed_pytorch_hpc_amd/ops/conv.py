@@ -31,11 +31,8 @@ from . import _lib
 # DPH_DIRECT_MAIN_GRAD=0: return weight gradients to autograd (engine copies them) instead of writing the bucket
 _DIRECT = os.environ.get("DPH_DIRECT_MAIN_GRAD", "1") != "0"
 
-# Set by runtime/graphs.GraphedStep around its warm-up and capture: the convolutions take MIOpen inside
-# whole-step HIP graphs.  Known issue: a captured ResNet-50 step (B=64, 224^2) with the 14x14 1x1 convolutions
-# on these kernels diverges from the second replay on when other GPU work runs between replays, while the same
-# kernels replay correctly in isolation (single layers and blocks of every ResNet-50 shape, guard-region checks
-# clean) -- unresolved, so graphed steps do not use them.
+# Set by runtime/graphs.GraphedStep (DPH_GRAPH_SAFE_CONV=1 only, an investigation knob): convolutions take MIOpen
+# inside whole-step HIP graphs.
 _GRAPHED_STEP = False
 
 

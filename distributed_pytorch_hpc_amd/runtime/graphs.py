@@ -10,7 +10,7 @@ Python or autograd bookkeeping on the host.
     for x, y in loader:
         loss = step(x, y, lr=sched_lr)      # eager for the first `warmup` calls, then capture + replay
 
-Every call is one real step on its own batch: the first ``warmup`` calls run eagerly on a side stream (lazy
+Every call is one real step on its own batch: the first ``warmup`` calls run eagerly on the current stream (lazy
 library initialisation, MIOpen / hipBLASLt algorithm selection, allocator warm-up happen outside the capture),
 call ``warmup + 1`` captures and then replays, later calls only copy the batch into the graph's static input
 buffers and replay.  Requirements, as for any graph: fixed shapes, no host synchronisation inside the step
@@ -23,12 +23,16 @@ next replay): consume or clone it before the next call.
 Multi-rank steps would capture their RCCL collectives into the graph too; that path is off unless
 ``allow_collectives=True`` (not exercised on the 1-GPU test box).
 
-Inside graphed steps the channels-last 1x1 / 3x3 convolutions run on MIOpen (ops/conv.py ``_GRAPHED_STEP``: an
-unresolved divergence of replayed ResNet-50 steps with the 14x14 1x1 convolutions on the framework kernels).
+Warm-up runs on the CURRENT stream, not on a side stream: with side-stream warm-up a captured ResNet-50 step
+diverged from its second replay on whenever other GPU work ran between replays (reproduced with the 14x14 1x1
+convolution kernels in the step; same-stream warm-up replays correctly, tests/test_graphs.py).
+``DPH_GRAPH_WARMUP_SIDE=1`` restores side-stream warm-up and ``DPH_GRAPH_SAFE_CONV=1`` routes convolutions to
+MIOpen inside graphed steps, both for investigation.
 """
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -44,7 +48,7 @@ def _graph_safe_ops():
     from ..ops import conv
 
     old = conv._GRAPHED_STEP
-    conv._GRAPHED_STEP = True
+    conv._GRAPHED_STEP = os.environ.get("DPH_GRAPH_SAFE_CONV", "0") == "1"   # investigation knob
     try:
         yield
     finally:
@@ -109,10 +113,11 @@ class GraphedStep:
                 self.optimizer.param_groups[0]["lr"] = lr
         self._set_lr(lr)
         cur = torch.cuda.current_stream()
-        self._side.wait_stream(cur)
-        with torch.cuda.stream(self._side), _graph_safe_ops():
+        side = self._side if os.environ.get("DPH_GRAPH_WARMUP_SIDE", "0") == "1" else cur
+        side.wait_stream(cur)
+        with torch.cuda.stream(side), _graph_safe_ops():
             out = self.step_fn(*self.static_in)
-        cur.wait_stream(self._side)
+        cur.wait_stream(side)
         return out
 
     def _capture(self):
