@@ -130,6 +130,9 @@ def _run(model, opt_cfg, batches, graphed, warmup=2, fsdp=False, autocast=None):
         lr = opt_cfg.lr * (1.0 - 0.05 * i)   # a schedule: the graph must pick up the host's lr every replay
         if graphed:
             losses.append(runner(x, y, lr=lr).clone())
+            # unrelated GPU work between replays (a stale or aliased buffer inside the graph shows up as NaN)
+            junk = [torch.full((16 << 20,), float("nan"), device=DEV) for _ in range(4)]
+            del junk
         else:
             opt.param_groups[0]["lr"] = lr
             if fsdp:
@@ -157,6 +160,7 @@ def test_graphed_mlp_adamw_matches_eager(dph_native):
     for a, b in zip(pg, pe):
         assert rel_err(a, b) < 1e-5
     assert rel_err(lg, le) < 1e-5
+    assert torch.isfinite(lg).all()
 
 
 @pytest.mark.gpu
