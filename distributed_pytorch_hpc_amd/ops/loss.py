@@ -50,12 +50,21 @@ def fused_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index
     return F.cross_entropy(logits.float(), target, ignore_index=ignore_index, label_smoothing=label_smoothing)
 
 
+_LAT_W: dict = {}
+
+
 def latitude_weights(n_lat: int, device=None, dtype=torch.float32) -> torch.Tensor:
-    """cos(latitude) weights over a [90, -90] grid normalised to mean 1 (multinode_ddp_unet.py:221-229)."""
-    lat = torch.linspace(90.0, -90.0, n_lat, dtype=torch.float64)
-    w = torch.cos(lat * math.pi / 180.0)
-    w = w / w.mean()
-    return w.to(device=device, dtype=dtype)
+    """cos(latitude) weights over a [90, -90] grid normalised to mean 1 (multinode_ddp_unet.py:221-229).
+    Cached per (n_lat, device, dtype): built once on the host, so a HIP-graph capture of the loss finds them
+    resident (a host-to-device copy is not allowed while a stream is capturing)."""
+    key = (int(n_lat), str(torch.device(device) if device is not None else "cpu"), dtype)
+    w = _LAT_W.get(key)
+    if w is None:
+        lat = torch.linspace(90.0, -90.0, n_lat, dtype=torch.float64)
+        w = torch.cos(lat * math.pi / 180.0)
+        w = (w / w.mean()).to(device=device, dtype=dtype)
+        _LAT_W[key] = w
+    return w
 
 
 class _LatMseFn(torch.autograd.Function):
