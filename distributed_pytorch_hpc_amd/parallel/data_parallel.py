@@ -37,7 +37,7 @@ from torch import nn
 
 from ..ops import _lib
 from ..train import optim as optim_ref
-from ..utils.flat import ALIGN, align_up
+from ..utils.flat import ALIGN, align_up, param_view
 from .linear import convert_linears_, join_wgrad_stream, wgrad_stream
 
 
@@ -196,10 +196,10 @@ class DataParallelEngine:
                 o = b.offset
                 for p in b.params:
                     n = p.numel()
-                    v = self.flat_param[o:o + n].view(p.shape)
+                    v = param_view(self.flat_param[o:o + n], p)   # channels-last weights stay channels-last
                     v.copy_(p.data)
+                    p.main_grad = param_view(self.flat_grad[o:o + n], p)
                     p.data = v
-                    p.main_grad = self.flat_grad[o:o + n].view(p.shape)
                     p._dph_accum = False
                     p._dph_grad_ready = partial(self._on_grad_ready, p)
                     self._bucket_of[id(p)] = b

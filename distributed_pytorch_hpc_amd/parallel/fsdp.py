@@ -33,7 +33,7 @@ from torch import nn
 
 from ..ops import _lib
 from ..train import optim as optim_ref
-from ..utils.flat import ALIGN, align_up
+from ..utils.flat import ALIGN, align_up, flat_order, param_view
 from .data_parallel import DataParallelEngine, MixedPrecision, OptimConfig, _EngineOptimizer, _hyper_for
 from .linear import convert_linears_, join_wgrad_stream, wgrad_stream
 
@@ -153,7 +153,7 @@ class ZeRO3Engine:
                 o = 0
                 for p in u.params:
                     n = p.numel()
-                    full[o:o + n].copy_(p.data.reshape(-1))
+                    full[o:o + n].copy_(flat_order(p.data))
                     o += align_up(n)
                 if self.world > 1:   # every rank starts from rank 0's weights
                     src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
@@ -164,8 +164,8 @@ class ZeRO3Engine:
                 o = 0
                 for p in u.params:
                     n = p.numel()
-                    p.data = u.full[o:o + n].view(p.shape)
-                    p.main_grad = u.grad_full[o:o + n].view(p.shape)
+                    p.main_grad = param_view(u.grad_full[o:o + n], p)   # channels-last weights stay so
+                    p.data = param_view(u.full[o:o + n], p)
                     p._dph_accum = False
                     p._dph_grad_ready = partial(self._on_grad_ready, p)
                     self._unit_of[id(p)] = u

@@ -65,3 +65,24 @@ def flatten_params_(params: list[torch.nn.Parameter], pad_to: int = 1) -> FlatBu
             v.copy_(p.data)
             p.data = v
     return fb
+
+
+def _cl4(t: torch.Tensor) -> bool:
+    """4-D tensor stored channels-last (and not also plain-contiguous, e.g. a 1x1 kernel)."""
+    return t.dim() == 4 and not t.is_contiguous() and t.is_contiguous(memory_format=torch.channels_last)
+
+
+def flat_order(t: torch.Tensor) -> torch.Tensor:
+    """``t`` flattened in its storage order: NHWC for channels-last 4-D tensors, row-major otherwise."""
+    return t.permute(0, 2, 3, 1).reshape(-1) if _cl4(t) else t.reshape(-1)
+
+
+def param_view(flat_slice: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+    """View of a flat-buffer slice shaped like ``like``, channels-last when ``like`` is, so a channels-last
+    convolution weight living in an engine's flat bucket is read in place by MIOpen instead of being copied to NHWC
+    on every call.  Pairs with ``flat_order`` (same element order).  The flat layout (hence sharded optimizer state)
+    follows the model's memory format: resume with the format it was saved with."""
+    if _cl4(like):
+        n, c, h, w = like.shape
+        return flat_slice.view(n, h, w, c).permute(0, 3, 1, 2)
+    return flat_slice.view(like.shape)
