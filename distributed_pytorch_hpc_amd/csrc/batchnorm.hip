@@ -103,7 +103,8 @@ __global__ __launch_bounds__(BN_NT) void bn_finalize_k(const float* __restrict__
                                                        RT* __restrict__ rmean, RT* __restrict__ rvar, float momentum,
                                                        float eps, float* __restrict__ mean_out,
                                                        float* __restrict__ invstd_out, float* __restrict__ scale,
-                                                       float* __restrict__ shift) {
+                                                       float* __restrict__ shift, int64_t* __restrict__ nbt) {
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;   // num_batches_tracked, one launch fewer
   __shared__ float sh[3][BN_NT];
   const int c = blockIdx.x * 8 + (threadIdx.x & 7), grp = threadIdx.x >> 3;
   Stat acc = {0.f, 0.f, 0.f};
@@ -348,7 +349,7 @@ int bn_partial_blocks(int64_t M, int64_t C) {
 void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const void* b, void* rmean, void* rvar,
                   float* mean, float* invstd, float* scale, float* shift, float* workspace, int64_t M, int64_t C,
                   float momentum, float eps, bool relu, int dt, int pdt, int rdt, hipStream_t st,
-                  const float* pre_stats, int pre_groups) {
+                  const float* pre_stats, int pre_groups, int64_t* nbt) {
   int64_t rpb;
   int G = stats_grid(M, (int)C, &rpb);
   const float* pmean = workspace;
@@ -376,7 +377,7 @@ void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const 
   const dim3 fg((unsigned)(C / 8));
 #define DPH_BN_FIN(PT_, RT_)                                                                                    \
   hipLaunchKernelGGL((bn_finalize_k<PT_, RT_>), fg, dim3(BN_NT), 0, st, pmean, pm2, pn, G, (int)C, (const PT_*)w, \
-                     (const PT_*)b, (RT_*)rmean, (RT_*)rvar, momentum, eps, mean, invstd, scale, shift)
+                     (const PT_*)b, (RT_*)rmean, (RT_*)rvar, momentum, eps, mean, invstd, scale, shift, nbt)
   if (pdt == kBF16 && rdt == kBF16) DPH_BN_FIN(bf16, bf16);
   else if (pdt == kBF16) DPH_BN_FIN(bf16, float);
   else if (rdt == kBF16) DPH_BN_FIN(float, bf16);

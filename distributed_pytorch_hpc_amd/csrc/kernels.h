@@ -126,7 +126,8 @@ int bn_partial_blocks(int64_t M, int64_t C);
 void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const void* b, void* rmean, void* rvar,
                   float* mean, float* invstd, float* scale, float* shift, float* workspace, int64_t M, int64_t C,
                   float momentum, float eps, bool relu, int dtype, int param_dtype, int running_dtype,
-                  hipStream_t stream, const float* pre_stats = nullptr, int pre_groups = 0);
+                  hipStream_t stream, const float* pre_stats = nullptr, int pre_groups = 0,
+                  int64_t* num_batches_tracked = nullptr);
 void bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int64_t M, int64_t C,
               bool relu, int dtype, hipStream_t stream);
 // xmask_ss (optional, fp32 [scale | shift] of the forward): ReLU mask from x instead of reading y.

@@ -497,7 +497,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
                                               const c10::optional<Tensor>& w, const c10::optional<Tensor>& b,
                                               const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
                                               double momentum, double eps, bool relu,
-                                              const c10::optional<Tensor>& pre_stats) {
+                                              const c10::optional<Tensor>& pre_stats,
+                                              const c10::optional<Tensor>& num_batches_tracked) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
   const int64_t C = bn_channels(x), M = x.numel() / C;
@@ -513,6 +514,13 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
   auto ss = at::empty({2 * C}, fopt);   // [scale | shift]: the backward recomputes the ReLU mask from them
   const Tensor* pre = pre_stats.has_value() ? &*pre_stats : nullptr;
+  int64_t* nbt = nullptr;   // incremented by the finalize kernel (nn.BatchNorm2d's num_batches_tracked += 1)
+  if (num_batches_tracked.has_value()) {
+    TORCH_CHECK(num_batches_tracked->scalar_type() == at::kLong && num_batches_tracked->numel() == 1 &&
+                    num_batches_tracked->device() == x.device(),
+                "bn_act_fwd: num_batches_tracked must be an int64 scalar on x's device");
+    nbt = num_batches_tracked->data_ptr<int64_t>();
+  }
   int pre_groups = 0;
   if (pre) {
     TORCH_CHECK(pre->scalar_type() == at::kFloat && pre->is_contiguous() && pre->numel() % (2 * C + 1) == 0 &&
@@ -529,7 +537,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
                     rvar ? rvar->data_ptr() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                     ss.data_ptr<float>(), ss.data_ptr<float>() + C, ws.data_ptr<float>(), M, C, (float)momentum,
                     (float)eps, relu, dt_code(x), pdt, rdt, cur_stream(), pre ? pre->data_ptr<float>() : nullptr,
-                    pre_groups);
+                    pre_groups, nbt);
   return {y, mean, invstd, ss};
 }
 
@@ -696,7 +704,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-        "float momentum, float eps, bool relu, Tensor? pre_stats=None) -> (Tensor, Tensor, Tensor, Tensor)");
+        "float momentum, float eps, bool relu, Tensor? pre_stats=None, Tensor(c!)? num_batches_tracked=None) "
+        "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "
         "bool need_dwb, Tensor? xmask_ss=None, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) "

@@ -74,7 +74,7 @@ def _sumsq(x, out):
 
 
 @register_fake("dph::bn_act_fwd")
-def _bn_act_fwd(x, res, w, b, rm, rv, momentum, eps, relu, pre_stats=None):
+def _bn_act_fwd(x, res, w, b, rm, rv, momentum, eps, relu, pre_stats=None, num_batches_tracked=None):
     c = x.shape[1]
     return (torch.empty_like(x), x.new_empty((c,), dtype=torch.float32), x.new_empty((c,), dtype=torch.float32),
             x.new_empty((2 * c,), dtype=torch.float32))

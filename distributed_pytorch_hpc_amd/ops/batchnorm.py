@@ -40,9 +40,9 @@ def _native_ok(x: torch.Tensor, residual) -> bool:
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, slot=None,
-                pre_stats=None):
+                pre_stats=None, nbt=None):
         y, mean, invstd, ss = _lib.ops().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, momentum,
-                                                    eps, relu, pre_stats)
+                                                    eps, relu, pre_stats, nbt)
         # ReLU without residual: the backward recomputes the mask from x with the forward's scale / shift and
         # never reads y (one activation-sized read less in each backward pass)
         ctx.xmask = relu and residual is None
@@ -77,11 +77,12 @@ class _BNActFn(torch.autograd.Function):
             ctx.slot.t = dres
             dres = None
         return (dx, dw if need_wb else None, db if need_wb else None, None, None, dres if ctx.has_res else None,
-                None, None, None, None, None)
+                None, None, None, None, None, None)
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
-                   residual=None, relu: bool = True, residual_grad_slot=None, stats_slot=None):
+                   residual=None, relu: bool = True, residual_grad_slot=None, stats_slot=None,
+                   num_batches_tracked=None):
     """act(batch_norm(x) + residual) with the fused kernels when eligible.  ``residual_grad_slot``
     (ops.conv.GradSlot): hand the residual's gradient to the 1x1 convolution that consumes the same input."""
     if _native_ok(x, residual):
@@ -92,9 +93,9 @@ def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, m
             if slot is not None and residual is not None and slot.consumer and torch.is_grad_enabled():
                 slot.armed = True
                 return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual.detach(), momentum, eps,
-                                      relu, slot, pre)
+                                      relu, slot, pre, num_batches_tracked)
             return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, None,
-                                  pre)
+                                  pre, num_batches_tracked)
         with torch.no_grad():
             inv = torch.rsqrt(running_var.float() + eps)
             scale = inv * (weight.float() if weight is not None else 1.0)
@@ -118,16 +119,20 @@ class BatchNormAct2d(nn.BatchNorm2d):
     def forward(self, x, residual=None, residual_grad_slot=None, stats_slot=None):
         training = self.training or not self.track_running_stats
         momentum = self.momentum
+        nbt = None
         if self.training and self.track_running_stats:
-            self.num_batches_tracked.add_(1)
-            if momentum is None:   # cumulative moving average, as nn.BatchNorm2d
-                momentum = 1.0 / float(self.num_batches_tracked)
+            if momentum is None or not _native_ok(x, residual):
+                self.num_batches_tracked.add_(1)
+                if momentum is None:   # cumulative moving average, as nn.BatchNorm2d
+                    momentum = 1.0 / float(self.num_batches_tracked)
+            else:   # the fused kernel increments the counter (one launch per BN layer fewer)
+                nbt = self.num_batches_tracked
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
         rv = self.running_var if (not self.training or self.track_running_stats) else None
         if training and rm is not None and not self.training:
             rm = rv = None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual, self.act,
-                              residual_grad_slot, stats_slot)
+                              residual_grad_slot, stats_slot, nbt)
 
     def extra_repr(self):
         return super().extra_repr() + f", act={'relu' if self.act else 'none'}"

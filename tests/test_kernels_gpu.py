@@ -409,6 +409,20 @@ def test_conv1x1_bn_main_grad_direct(dph_native):
         assert rel_err(p.main_grad, r.grad) < 2e-2
 
 
+def test_bn_module_counts_batches_in_kernel(dph_native):
+    """num_batches_tracked is incremented by the fused finalize kernel (no separate add launch)."""
+    from distributed_pytorch_hpc_amd.ops.batchnorm import BatchNormAct2d
+
+    m = BatchNormAct2d(64).to(DEV)
+    x = torch.randn(4, 64, 8, 8, device=DEV).contiguous(memory_format=torch.channels_last)
+    for _ in range(3):
+        m(x)
+    assert int(m.num_batches_tracked) == 3
+    m.momentum = None   # cumulative average keeps the host-side increment
+    m(x)
+    assert int(m.num_batches_tracked) == 4
+
+
 def test_bn_act_module_native_matches_torch(dph_native):
     """BatchNormAct2d (fused kernels) == nn.BatchNorm2d + add + ReLU, train and eval, incl. running stats."""
     from distributed_pytorch_hpc_amd.ops import BatchNormAct2d
