@@ -49,3 +49,34 @@ def test_gradient_accumulation_two_microbatches():
     ref(xs[1]).sum().backward()
     for a, b in zip(m.parameters(), ref.parameters()):
         torch.testing.assert_close(a.main_grad, b.grad)
+
+
+def test_channels_last_weights_stay_channels_last_in_flat_buckets():
+    """utils.flat.param_view: channels-last conv weights become channels-last views of the engine's flat buffer
+    (no per-call NHWC copies for MIOpen); values and SGD updates match a plain-layout copy of the model."""
+    import torch.nn.functional as F
+
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig
+
+    torch.manual_seed(0)
+    ref = torch.nn.Sequential(torch.nn.Conv2d(4, 8, 3, padding=1, bias=False), torch.nn.ReLU(),
+                              torch.nn.Conv2d(8, 4, 3, padding=1))
+    cl = torch.nn.Sequential(torch.nn.Conv2d(4, 8, 3, padding=1, bias=False), torch.nn.ReLU(),
+                             torch.nn.Conv2d(8, 4, 3, padding=1))
+    cl.load_state_dict(ref.state_dict())
+    cl = cl.to(memory_format=torch.channels_last)
+    engines = [DataParallelEngine(m) for m in (ref, cl)]
+    for e in engines:
+        e.configure_optimizer(OptimConfig("sgd", lr=0.1, momentum=0.9))
+    w = cl[0].weight
+    assert w.is_contiguous(memory_format=torch.channels_last) and not w.is_contiguous()
+    assert w.main_grad.is_contiguous(memory_format=torch.channels_last)
+    assert w.untyped_storage().data_ptr() == engines[1].flat_param.untyped_storage().data_ptr()
+    x = torch.randn(2, 4, 6, 6)
+    for _ in range(2):
+        for m, e in zip((ref, cl), engines):
+            e.zero_grad()
+            F.mse_loss(m(x.contiguous(memory_format=torch.channels_last) if m is cl else x), x).backward()
+            e.step()
+    for a, b in zip(ref.parameters(), cl.parameters()):
+        assert torch.allclose(a, b, atol=1e-5)
