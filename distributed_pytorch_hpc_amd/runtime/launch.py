@@ -36,6 +36,12 @@ def _spawn(args, attempt: int, port: int):
             env["DPH_BACKEND"] = args.backend
         if args.omp_threads:
             env["OMP_NUM_THREADS"] = str(args.omp_threads)
+        elif "OMP_NUM_THREADS" not in env:   # ranks split the cores instead of oversubscribing them
+            try:
+                cores = len(os.sched_getaffinity(0))
+            except AttributeError:
+                cores = os.cpu_count() or 1
+            env["OMP_NUM_THREADS"] = str(max(1, cores // max(args.nproc, 1)))
         out = err = None
         if args.log_dir:
             os.makedirs(args.log_dir, exist_ok=True)
