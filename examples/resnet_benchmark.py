@@ -64,13 +64,8 @@ def main(argv=None):
     ap.add_argument("--resume", default=None, help="snapshot path (DDP): resume from / save to")
     ap.add_argument("--logfile", default=None, help="append a result line (reference: resnet_benchmark.log)")
     ap.add_argument("--eval-steps", type=int, default=0)
-    ap.add_argument("--no-conv-search", action="store_true",
-                    help="MIOpen immediate mode (heuristic solver) instead of timing its solvers per shape")
     args = ap.parse_args(argv)
-    rank, world, local, dev = start(args)
-    # MIOpen find mode: time the candidate solvers once per convolution shape (the first, excluded epoch) and keep
-    # the fastest -- the heuristic immediate-mode choice is slower on several ResNet-50 shapes
-    torch.backends.cudnn.benchmark = not args.no_conv_search
+    rank, world, local, dev = start(args)   # MIOpen find mode on GPU unless --no-conv-search (train/cli.py)
     backend = dist.get_backend() if dist.is_initialized() else ("nccl" if dev.type == "cuda" else "gloo")
 
     torch.manual_seed(args.seed)
