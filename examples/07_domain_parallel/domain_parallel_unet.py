@@ -45,6 +45,9 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--lr", type=float, default=1e-4)
     ap.add_argument("--check", action="store_true", help="compare step-0 loss with an unsharded replay")
+    # MIOpen find mode off by default here: the halo-padded slab shapes (and --check's unsharded replay) are new
+    # convolution shapes for every layer, and a few-step fp32 run spends minutes timing solvers it never reuses.
+    ap.set_defaults(conv_search=False)
     args = ap.parse_args(argv)
     rank, world, local, dev = start(args)
     assert world % args.dp == 0
