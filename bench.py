@@ -49,6 +49,9 @@ def parse(argv=None):
                     help="activation checkpointing: none | auto (fit 288 GB) | N (every N-th block)")
     ap.add_argument("--force-dist", action="store_true",
                     help="create the RCCL process group even for one rank (exercises the N>1 collective path)")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default=None,
+                    help="process-group backend (default: nccl = RCCL on GPU); gloo lets several ranks share one GPU "
+                         "to rehearse the N > 1 path (tests/test_bench_gpu.py)")
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: gloo + eager reference ops (tests of the N > 1 code path with tiny models only)")
@@ -62,7 +65,7 @@ def main(argv=None):
 
     cpu = args.device == "cpu"
     if world_env > 1 or args.force_dist:
-        rank, world, local = rt.init_distributed(backend="gloo" if cpu else None, verbose=not args.quiet)
+        rank, world, local = rt.init_distributed(backend="gloo" if cpu else args.backend, verbose=not args.quiet)
     else:
         rank, world, local = 0, 1, 0
         if not cpu:

@@ -1,0 +1,32 @@
+"""bench.py's N > 1 path on GPU tensors: two ranks share one MI355X over gloo (RCCL needs a GPU per rank), tiny
+Llama, HIP kernels.  Same contract checks as tests/test_bench.py; the round-end driver runs this code path with RCCL
+on 2, 4 and 8 GPUs."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_two_ranks_share_one_gpu(tmp_path):
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--backend", "gloo", "--model", "tiny", "--seq-len", "128", "--micro-batch", "2",
+           "--steps", "2", "--warmup", "1", "--quiet"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=100, cwd=str(tmp_path),
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    recs = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(recs) == 1, p.stdout
+    r = recs[0]
+    assert r["n_gpus"] == 2 and r["dtype"] == "bf16" and r["value"] > 0
+    assert r["config"]["parallelism"] == "fsdp2" and r["config"]["global_batch"] == 4
+    assert r["config"]["kernels"] == "dph"
