@@ -454,26 +454,57 @@ class DataParallelEngine:
         self._wait_ag(range(len(self.buckets)))
 
     # ------------------------------------------------------------------------------------------ state
+    # checkpoint protocol shared with fsdp.ZeRO3Engine (utils/checkpointing.py): ``groups`` are the buckets, each a
+    # padded flat vector of its parameters; this rank's optimizer-side slice of bucket b is ``opt_slice(b)``.
+    @property
+    def groups(self):
+        return self.buckets
+
+    @property
+    def sharded_state(self) -> bool:
+        return self.shard
+
+    def opt_slice(self, b: _Bucket) -> slice:
+        if self.shard:
+            return slice(b.shard_offset, b.shard_offset + b.shard_numel)
+        return slice(b.offset, b.offset + b.numel)
+
+    @torch.no_grad()
+    def refresh_params_from_master(self):
+        """After the fp32 master changed outside ``step`` (checkpoint load): parameters <- master (re-gathered
+        across the group when sharded)."""
+        self.synchronize()
+        for b in self.buckets:
+            self.param_shard_view(b).copy_(self.master_view(b))
+            if self.shard:
+                dist.all_gather_into_tensor(self.param_view(b), self.param_shard_view(b).clone(), group=self.group)
+
+    @torch.no_grad()
+    def load_full_state_dict(self, sd: dict):
+        """Full model state (parameters live in the flat buffer, so the module loads in place); the fp32 master is
+        re-derived from the loaded parameters (a following optimizer-state load overrides it)."""
+        self.synchronize()
+        self.module.load_state_dict(sd)
+        for b in self.buckets:
+            self.master_view(b).copy_(self.param_shard_view(b))
+
     def optimizer_state_dict(self) -> dict:
         """Rank-local optimizer state (the shard when sharded) + layout metadata."""
         self.synchronize()
         return {"step": self.step_count, "master": self.master.cpu(),
                 "state": [s.cpu() for s in self.opt_state], "world": self.world, "rank": self.rank,
-                "shard": self.shard, "total": self.total}
+                "shard": self.shard, "total": self.total, "kind": "dp"}
 
     def load_optimizer_state_dict(self, sd: dict):
-        assert sd["total"] == self.total and sd["shard"] == self.shard and sd["world"] == self.world, \
-            "optimizer state layout mismatch (resharding needs ckpt.reshard_optimizer)"
+        assert sd.get("kind", "dp") == "dp" and sd["total"] == self.total and sd["shard"] == self.shard and \
+            sd["world"] == self.world, \
+            "optimizer state layout mismatch (another world size or engine: use utils.checkpointing)"
         self.step_count = int(sd["step"])
-        self.master.copy_(sd["master"])
-        for s, t in zip(self.opt_state, sd["state"]):
-            s.copy_(t)
         with torch.no_grad():
-            for b in self.buckets:
-                self.param_shard_view(b).copy_(self.master_view(b))
-                if self.shard:
-                    dist.all_gather_into_tensor(self.param_view(b), self.param_shard_view(b).clone(),
-                                                group=self.group)
+            self.master.copy_(sd["master"])
+            for s, t in zip(self.opt_state, sd["state"]):
+                s.copy_(t)
+        self.refresh_params_from_master()
 
 
 class _EngineOptimizer:

@@ -33,7 +33,7 @@ from torch import nn
 
 from ..ops import _lib
 from ..train import optim as optim_ref
-from ..utils.flat import ALIGN, align_up, flat_order, param_view
+from ..utils.flat import ALIGN, align_up, flat_order, flat_order_like, param_view
 from .data_parallel import DataParallelEngine, MixedPrecision, OptimConfig, _EngineOptimizer, _hyper_for
 from .linear import convert_linears_, join_wgrad_stream, wgrad_stream
 
@@ -390,34 +390,89 @@ class ZeRO3Engine:
                 u.ag_work = None
 
     # ---------------------------------------------------------------------------------------- state
+    # checkpoint protocol shared with DataParallelEngine (utils/checkpointing.py): ``groups`` are the units, each a
+    # padded flat vector of its parameters; this rank's optimizer-side slice of unit u is ``opt_slice(u)``.
+    sharded_state = True
+
+    @property
+    def groups(self):
+        return self.units
+
+    def opt_slice(self, u) -> slice:
+        return slice(u.shard_offset, u.shard_offset + u.shard_numel)
+
     def full_state_dict(self, rank0_only: bool = True, offload_to_cpu: bool = True) -> dict:
-        """FULL_STATE_DICT consolidation (multinode_fsdp_unet.py:285-291): gather every unit, copy out, free."""
+        """FULL_STATE_DICT consolidation (multinode_fsdp_unet.py:285-291): gather every unit, copy out, free.
+        Collective over the shard group; with ``rank0_only`` only group rank 0 makes (and returns) the copies."""
+        keep = not rank0_only or self.rank == 0
         out = {}
         names = {id(p): n for n, p in self.module.named_parameters()}
         for u in self.units:
             was = u.gathered
             self._gather(u)
-            for p in u.params:
-                t = p.detach()
-                out[names[id(p)]] = t.cpu().clone() if offload_to_cpu else t.clone()
+            if keep:
+                for p in u.params:
+                    t = p.detach()
+                    out[names[id(p)]] = t.cpu().clone() if offload_to_cpu else t.clone()
             if not was:
                 self._release(u)
+        if not keep:
+            return {}
         for n, b in self.module.named_buffers():
             out[n] = b.detach().cpu().clone() if offload_to_cpu else b.detach().clone()
-        if rank0_only and self.rank != 0:
-            return {}
         return out
 
+    @torch.no_grad()
+    def load_full_state_dict(self, sd: dict):
+        """Inverse of ``full_state_dict``: every rank passes the same full (unsharded) state; each unit's padded
+        vector is rebuilt from it and this rank keeps its 1/N slice (parameter shard + fp32 master).  Buffers are
+        copied into the module.  Released units are never written through the module's (freed) parameters."""
+        names = {id(p): n for n, p in self.module.named_parameters()}
+        missing = [names[id(p)] for p in self.params if names[id(p)] not in sd]
+        if missing:
+            raise KeyError(f"load_full_state_dict: missing parameters {missing[:4]}")
+        for u in self.units:
+            full = torch.zeros(u.numel, dtype=self.param_dtype)
+            o = 0
+            for p in u.params:
+                n = p.numel()
+                full[o:o + n].copy_(flat_order_like(sd[names[id(p)]], p))
+                o += align_up(n)
+            mine = full[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel].to(self.device)
+            self.shard_view(u).copy_(mine)
+            self.master_view(u).copy_(mine.float())
+        for n, b in self.module.named_buffers():
+            if n in sd:
+                b.copy_(sd[n])
+        self.refresh_params_from_master(cast=False)
+
+    @torch.no_grad()
+    def refresh_params_from_master(self, cast: bool = True):
+        """After the fp32 master changed outside ``step`` (checkpoint load): parameter shard <- master, and the
+        resident (gathered) units are re-gathered so the module sees the new values."""
+        self.synchronize()
+        if cast:
+            self.param_shard.copy_(self.master)
+        for u in self.units:
+            if u.gathered:
+                u.gathered = False
+                self._gather(u)
+
     def optimizer_state_dict(self):
+        self.synchronize()
         return {"step": self.step_count, "master": self.master.cpu(), "state": [s.cpu() for s in self.opt_state],
-                "world": self.world, "rank": self.rank, "shard": True, "total": self.shard_total * self.world}
+                "world": self.world, "rank": self.rank, "shard": True, "total": self.shard_total * self.world,
+                "kind": "zero3"}
 
     def load_optimizer_state_dict(self, sd):
+        assert sd.get("kind") == "zero3" and sd["world"] == self.world and \
+            sd["total"] == self.shard_total * self.world, \
+            "optimizer state layout mismatch (another world size or engine: use utils.checkpointing)"
         self.step_count = int(sd["step"])
         self.master.copy_(sd["master"])
         for s, t in zip(self.opt_state, sd["state"]):
             s.copy_(t)
-        self.param_shard.copy_(self.master)
+        self.refresh_params_from_master()
 
 
 # ------------------------------------------------------------------------------------------------ module wrapper
@@ -456,6 +511,10 @@ class FullyShardedDataParallel(nn.Module):
     def state_dict(self, *args, **kwargs):
         """Unsharded parameters (gathered unit by unit: a FULL_SHARD model's released storage is never read)."""
         return self.full_state_dict(rank0_only=False, offload_to_cpu=True)
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """Full (unsharded) state as returned by ``state_dict``; every rank passes the same one."""
+        self.engine.load_full_state_dict(state_dict)
 
     def full_state_dict(self, rank0_only: bool = True, offload_to_cpu: bool = True) -> dict:
         if isinstance(self.engine, ZeRO3Engine):

@@ -94,7 +94,13 @@ def default_backend() -> str:
 def device_for(local_rank: int, backend: str | None = None) -> torch.device:
     backend = backend or default_backend()
     if backend == "nccl" and torch.cuda.is_available():
-        return torch.device("cuda", local_rank % torch.cuda.device_count())
+        n = torch.cuda.device_count()
+        if not 0 <= local_rank < n:
+            # RCCL cannot put two ranks on one device: a wrong --nproc-per-node / HIP_VISIBLE_DEVICES must fail here,
+            # not later inside a collective (gloo ranks may share a GPU: bench.py --backend gloo)
+            raise RuntimeError(f"local rank {local_rank} has no GPU of its own ({n} visible); launch at most {n} "
+                               f"ranks per node with the nccl (RCCL) backend")
+        return torch.device("cuda", local_rank)
     return torch.device("cpu")
 
 

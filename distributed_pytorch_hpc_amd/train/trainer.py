@@ -97,8 +97,8 @@ class Trainer:
         self.global_step = 0
         self.history: list[EpochStats] = []
         self.engine = getattr(optimizer, "engine", None)
-        self._sharded = bool(self.engine is not None and getattr(self.engine, "shard", False)) or \
-            type(self.engine).__name__ == "ZeRO3Engine"
+        # sharded optimizer state (ZeRO-2 / FULL_SHARD): per-rank snapshot files instead of one consolidated file
+        self._sharded = bool(self.engine is not None and getattr(self.engine, "sharded_state", False))
         if snapshot_path:
             self._load_snapshot()
 

@@ -7,13 +7,20 @@ Fixes the reference defects X15 (one module used everywhere; a single writer per
 
 Two formats:
   * ``save_checkpoint`` / ``load_checkpoint``: consolidated single file written by global rank 0 (small models,
-    interoperability).  Model state is unwrapped from ``.module``.
+    interoperability).  Every rank must call both.  With an engine-backed model (DDP / FSDP / ZeRO engines of
+    parallel/) the model state is the FULL state -- gathered unit by unit for FULL_SHARD, whose module parameters
+    point at released storage -- and the optimizer state is stored per parameter name in the logical tensor shape
+    (``format: "full"``), so a file loads into any strategy and any data-parallel world size.
   * ``ShardedCheckpointer``: one directory per step, ``rank{r}.pt`` per rank holding that rank's model shard
-    (TP/PP shards; data-parallel replicas are written by their dp-rank-0 only) and optimizer shard (the
-    DataParallelEngine's fp32 master / m / v slice) + ``meta.json``.  Loading at a DIFFERENT data-parallel world
-    size re-slices the engine's flat optimizer state (``reshard_engine_state``).
+    (TP/PP shards; data-parallel replicas are written by their dp-rank-0 only; FULL_SHARD writes the gathered full
+    state from dp-rank 0) and optimizer shard (the engine's fp32 master / m / v slice) + ``meta.json``.  Loading at
+    a DIFFERENT data-parallel world size re-slices the engine's flat optimizer state (``reshard_engine_state``).
 Both store the step/epoch, torch + HIP RNG state and arbitrary extra metadata; files are loaded with
 ``weights_only=True`` (tensors, numbers, strings, lists, dicts only).
+
+Engines implement a small protocol (parallel/data_parallel.py, parallel/fsdp.py): ``groups`` (buckets / units:
+padded flat vectors of ``.params``), ``opt_slice(g)`` (this rank's slice of g in master / optimizer state),
+``sharded_state``, ``refresh_params_from_master()``, ``load_full_state_dict(sd)``.
 """
 from __future__ import annotations
 
@@ -24,6 +31,8 @@ from typing import Optional
 
 import torch
 import torch.distributed as dist
+
+from .flat import ALIGN, align_up, flat_order_like, param_view
 
 
 def _rank():
@@ -37,6 +46,15 @@ def _barrier():
 
 def _unwrap(model):
     return model.module if hasattr(model, "module") else model
+
+
+def _engine_of(model, optimizer=None):
+    """The framework engine behind ``optimizer`` (``make_optimizer`` facade) or ``model`` (DDP / FSDP wrapper)."""
+    for o in (optimizer, model):
+        e = getattr(o, "engine", None)
+        if e is not None and hasattr(e, "groups"):
+            return e
+    return None
 
 
 def rng_state() -> dict:
@@ -53,14 +71,113 @@ def set_rng_state(st: dict):
         torch.cuda.set_rng_state(st["cuda"])
 
 
+# ------------------------------------------------------------------------------------------------ engine state
+def _rank_slice(engine, g) -> slice:
+    """This rank's part of group g's padded full vector."""
+    if engine.sharded_state:
+        return slice(engine.rank * g.shard_numel, (engine.rank + 1) * g.shard_numel)
+    return slice(0, g.numel)
+
+
+def _state_vectors(engine) -> list[torch.Tensor]:
+    """fp32 master + the optimizer-state vectors laid out like it (SGD without momentum keeps a dummy)."""
+    n = engine.master.numel()
+    return [engine.master] + [s for s in engine.opt_state if s.numel() == n]
+
+
+def _gather_group(engine, vec: torch.Tensor, g) -> torch.Tensor:
+    local = vec[engine.opt_slice(g)]
+    if not engine.sharded_state or engine.world == 1:
+        return local
+    full = torch.empty(g.numel, dtype=vec.dtype, device=vec.device)
+    dist.all_gather_into_tensor(full, local.clone() if engine.is_gloo else local, group=engine.group)
+    return full
+
+
+def full_model_state(model, engine=None) -> dict:
+    """Unsharded model state (CPU) on global rank 0, ``{}`` elsewhere.  Collective when the parameters are sharded
+    (FULL_SHARD gathers unit by unit) -- call it on every rank."""
+    engine = engine if engine is not None else _engine_of(model)
+    if engine is not None and hasattr(engine, "full_state_dict"):
+        return engine.full_state_dict(rank0_only=True, offload_to_cpu=True)   # kept on the group's rank 0
+    if engine is not None:
+        engine.synchronize()   # sharded (ZeRO-2) parameter all-gathers still in flight
+    if _rank() != 0:
+        return {}
+    return {k: v.detach().cpu().clone() for k, v in _unwrap(model).state_dict().items()}
+
+
+def full_optimizer_state(engine) -> dict:
+    """Layout-independent optimizer state: fp32 master and every state vector, per parameter NAME in the
+    parameter's logical shape.  Collective over the engine's group; the dict is returned on group rank 0 only."""
+    engine.synchronize()
+    names = {id(p): n for n, p in engine.module.named_parameters()}
+    vecs = _state_vectors(engine)
+    keep = engine.rank == 0
+    tensors: list[dict] = [{} for _ in vecs]
+    for g in engine.groups:
+        for k, vec in enumerate(vecs):
+            full = _gather_group(engine, vec, g)
+            if not keep:
+                continue
+            o = 0
+            for p in g.params:
+                n = p.numel()
+                tensors[k][names[id(p)]] = param_view(full[o:o + n], p).contiguous().cpu().clone()
+                o += align_up(n)
+    if not keep:
+        return {}
+    cfg = engine.opt_cfg
+    return {"format": "full", "step": int(engine.step_count), "optimizer": cfg.name if cfg else None,
+            "master": tensors[0], "state": tensors[1:]}
+
+
+@torch.no_grad()
+def load_full_optimizer_state(engine, sd: dict):
+    """Inverse of ``full_optimizer_state`` for any engine / world size (every rank passes the same dict)."""
+    names = {id(p): n for n, p in engine.module.named_parameters()}
+    vecs = _state_vectors(engine)
+    srcs = [sd["master"]] + list(sd["state"])
+    if len(srcs) != len(vecs):
+        raise ValueError(f"optimizer state has {len(srcs) - 1} state vectors, the engine {len(vecs) - 1} "
+                         f"(saved with optimizer {sd.get('optimizer')!r}?)")
+    engine.synchronize()
+    for g in engine.groups:
+        rs = _rank_slice(engine, g)
+        for src, vec in zip(srcs, vecs):
+            full = torch.zeros(g.numel, dtype=torch.float32)
+            o = 0
+            for p in g.params:
+                n = p.numel()
+                full[o:o + n].copy_(flat_order_like(src[names[id(p)]], p))
+                o += align_up(n)
+            vec[engine.opt_slice(g)].copy_(full[rs])
+    engine.step_count = int(sd["step"])
+    engine.refresh_params_from_master()
+
+
+def _load_model_state(model, engine, sd: dict):
+    if engine is not None:
+        engine.load_full_state_dict(sd)
+    else:
+        _unwrap(model).load_state_dict(sd)
+
+
+# ------------------------------------------------------------------------------------------------ consolidated
 def save_checkpoint(model, optimizer, epoch: int, path: str, extra: Optional[dict] = None, rank: Optional[int] = None):
-    """Consolidated checkpoint from global rank 0; every rank must call it (barrier)."""
+    """Consolidated checkpoint written by global rank 0.  Every rank must call it (collective gathers for sharded
+    engines, barrier at the end)."""
     rank = _rank() if rank is None else rank
+    engine = _engine_of(model, optimizer)
+    model_sd = full_model_state(model, engine)
+    opt_sd = None
+    if optimizer is not None:
+        opt_sd = full_optimizer_state(engine) if engine is not None else \
+            (optimizer.state_dict() if rank == 0 else None)
     if rank == 0:
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
-        state = {"model_state_dict": {k: v.detach().cpu() for k, v in _unwrap(model).state_dict().items()},
-                 "optimizer_state_dict": optimizer.state_dict() if optimizer is not None else None,
-                 "epoch": int(epoch), "rng": rng_state(), "extra": extra or {}}
+        state = {"model_state_dict": model_sd, "optimizer_state_dict": opt_sd, "epoch": int(epoch),
+                 "rng": rng_state(), "extra": extra or {}}
         tmp = path + ".tmp"
         torch.save(state, tmp)
         os.replace(tmp, path)   # atomic: a crash never leaves a truncated checkpoint
@@ -68,13 +185,22 @@ def save_checkpoint(model, optimizer, epoch: int, path: str, extra: Optional[dic
 
 
 def load_checkpoint(model, optimizer, path: str, device=None) -> int:
-    """Restores model (+optimizer) in place; returns the stored epoch, or 0 when ``path`` is missing."""
+    """Restores model (+optimizer) in place on every rank; returns the stored epoch, or 0 when ``path`` is
+    missing."""
     if not os.path.exists(path):
         return 0
     state = torch.load(path, map_location=device or "cpu", weights_only=True)
-    _unwrap(model).load_state_dict(state["model_state_dict"])
-    if optimizer is not None and state.get("optimizer_state_dict") is not None:
-        optimizer.load_state_dict(state["optimizer_state_dict"])
+    engine = _engine_of(model, optimizer)
+    _load_model_state(model, engine, state["model_state_dict"])
+    osd = state.get("optimizer_state_dict")
+    if optimizer is not None and osd is not None:
+        if osd.get("format") == "full":
+            if engine is None:
+                raise ValueError("checkpoint holds a framework-engine optimizer state; build the optimizer with "
+                                 "DDP/FSDP.make_optimizer to load it")
+            load_full_optimizer_state(engine, osd)
+        else:
+            optimizer.load_state_dict(osd)
     if "rng" in state:
         set_rng_state(state["rng"])
     return int(state.get("epoch", 0))
@@ -85,12 +211,15 @@ class ShardedCheckpointer:
     def __init__(self, root: str, model, engine=None, dp_group=None, keep_last: int = 2):
         self.root = root
         self.model = _unwrap(model)
-        self.engine = engine
-        self.dp_group = dp_group if dp_group is not None else (engine.group if engine is not None else None)
+        self.engine = engine if engine is not None else _engine_of(model)
+        self.dp_group = dp_group if dp_group is not None else (self.engine.group if self.engine is not None else None)
         self.keep_last = keep_last
 
     def _dir(self, step: int) -> str:
         return os.path.join(self.root, f"step{step:08d}")
+
+    def _full_shard(self) -> bool:
+        return self.engine is not None and hasattr(self.engine, "full_state_dict")
 
     def save(self, step: int, extra: Optional[dict] = None):
         rank = _rank()
@@ -102,7 +231,14 @@ class ShardedCheckpointer:
             (_rank() if self.engine is not None and self.engine.world > 1 else 0)
         state = {"step": int(step), "rng": rng_state(), "extra": extra or {}}
         # model shard: data-parallel replicas are identical -> only dp-rank 0 of each model-parallel slice writes
-        if dp_rank == 0 or self.engine is None:
+        if self._full_shard():
+            # FULL_SHARD: the module's parameters are released between uses; gather the full state (collective)
+            sd = self.engine.full_state_dict(rank0_only=True, offload_to_cpu=True)
+            if dp_rank == 0:
+                state["model"] = sd
+        elif dp_rank == 0 or self.engine is None:
+            if self.engine is not None:
+                self.engine.synchronize()
             state["model"] = {k: v.detach().cpu() for k, v in self.model.state_dict().items()}
         if self.engine is not None and self.engine.opt_cfg is not None:
             state["optim"] = self.engine.optimizer_state_dict()
@@ -142,7 +278,10 @@ class ShardedCheckpointer:
         model_sd = state.get("model")
         if model_sd is None:   # a dp replica that did not write the model: read rank 0 of the same slice (rank 0)
             model_sd = torch.load(os.path.join(path, "rank0.pt"), map_location="cpu", weights_only=True)["model"]
-        self.model.load_state_dict(model_sd)
+        if self.engine is not None:
+            self.engine.load_full_state_dict(model_sd)
+        else:
+            self.model.load_state_dict(model_sd)
         if self.engine is not None and self.engine.opt_cfg is not None:
             if same_world and "optim" in state:
                 self.engine.load_optimizer_state_dict(state["optim"])
@@ -156,73 +295,45 @@ class ShardedCheckpointer:
         return int(meta["step"])
 
 
+@torch.no_grad()
 def reshard_engine_state(engine, shards: list[dict]):
     """Rebuild the engine's optimizer state from the per-rank states of a run with another dp world size.
 
-    Every saved rank stored its slice of every bucket (bucket layout is a pure function of the model and the
-    world size); the full flat fp32 vectors are reassembled from the OLD layout, then re-sliced for this engine.
+    Every saved rank stored its slice of every group (bucket / unit); the group layout is a pure function of the
+    model, the bucketing / wrap policy and the world size (padding to ALIGN * world).  The full padded group vectors
+    are reassembled from the OLD layout, then this rank's slice of the NEW layout is copied out.
     """
-    from ..parallel.data_parallel import DataParallelEngine  # noqa: F401  (type reference)
+    old_world, old_sharded = shards[0]["world"], shards[0]["shard"]
+    if shards[0].get("kind", "dp") != ("zero3" if hasattr(engine, "full_state_dict") else "dp"):
+        raise ValueError("reshard_engine_state: checkpoint written by another engine kind; use the consolidated "
+                         "save_checkpoint/load_checkpoint format to change strategy")
+    sizes = [align_up(sum(align_up(p.numel()) for p in g.params), ALIGN * old_world) for g in engine.groups]
+    old_total = sum(sizes)
 
-    old_world = shards[0]["world"]
-    old_sharded = shards[0]["shard"]
-    if not old_sharded:
-        full = {"master": shards[0]["master"], "state": shards[0]["state"]}
-    else:
-        # old bucket sizes: recompute from this engine's parameter order with the old world's padding
-        from ..utils.flat import ALIGN, align_up
+    def assemble(get):
+        if not old_sharded:
+            return get(shards[0])
+        parts, offs = [], [0] * old_world
+        for sz in sizes:
+            sh = sz // old_world
+            for r in range(old_world):
+                parts.append(get(shards[r])[offs[r]:offs[r] + sh])
+                offs[r] += sh
+        return torch.cat(parts)
 
-        sizes = []
-        for b in engine.buckets:
-            n = sum(align_up(p.numel()) for p in b.params)
-            sizes.append(align_up(n, ALIGN * old_world))
-        def assemble(key, idx=None):
-            parts = []
-            offs = [0] * old_world
-            for sz in sizes:
-                sh = sz // old_world
-                for r in range(old_world):
-                    src = shards[r][key] if idx is None else shards[r][key][idx]
-                    parts.append(src[offs[r]:offs[r] + sh])
-                    offs[r] += sh
-            return torch.cat(parts)
-        full = {"master": assemble("master"), "state": [assemble("state", i) for i in range(len(shards[0]["state"]))]}
-    # full vectors are in the old padded layout; re-slice per bucket into the new layout
-    from ..utils.flat import ALIGN, align_up
-
-    def old_bucket_offsets(world):
-        offs, o = [], 0
-        for b in engine.buckets:
-            n = align_up(sum(align_up(p.numel()) for p in b.params), ALIGN * world)
-            offs.append((o, n))
-            o += n
-        return offs
-
-    old = old_bucket_offsets(old_world if old_sharded else engine.world)
-    if not old_sharded:
-        old = old_bucket_offsets(old_world)
-    with torch.no_grad():
-        for b, (o, n) in zip(engine.buckets, old):
-            real = sum(align_up(p.numel()) for p in b.params)
-            src_m = full["master"][o:o + real]
-            dst = torch.zeros(b.numel, dtype=torch.float32)
-            dst[:real] = src_m
-            engine_slice = slice(b.offset, b.offset + b.numel)
-            if engine.shard:
-                s = engine.rank * b.shard_numel
-                engine.master_view(b).copy_(dst[s:s + b.shard_numel])
-                for i, st in enumerate(engine.opt_state):
-                    t = torch.zeros(b.numel, dtype=torch.float32)
-                    t[:real] = full["state"][i][o:o + real]
-                    st[b.shard_offset:b.shard_offset + b.shard_numel].copy_(t[s:s + b.shard_numel])
-            else:
-                engine.master[engine_slice].copy_(dst)
-                for i, st in enumerate(engine.opt_state):
-                    t = torch.zeros(b.numel, dtype=torch.float32)
-                    t[:real] = full["state"][i][o:o + real]
-                    st[engine_slice].copy_(t)
-            engine.param_shard_view(b).copy_(engine.master_view(b))
+    n_state = len(shards[0]["state"])
+    fulls = [assemble(lambda s: s["master"])] + [assemble(lambda s, i=i: s["state"][i]) for i in range(n_state)]
+    dsts = [engine.master] + list(engine.opt_state)
+    o = 0
+    for g, sz in zip(engine.groups, sizes):
+        real = sum(align_up(p.numel()) for p in g.params)
+        rs = _rank_slice(engine, g)
+        for src, dst in zip(fulls, dsts):
+            if src.numel() != old_total or dst.numel() != engine.master.numel():
+                continue   # not laid out like the master (SGD without momentum: a dummy)
+            t = torch.zeros(g.numel, dtype=torch.float32)
+            t[:real] = src[o:o + real]
+            dst[engine.opt_slice(g)].copy_(t[rs])
+        o += sz
     engine.step_count = int(shards[0]["step"])
-    if engine.shard:
-        for b in engine.buckets:
-            dist.all_gather_into_tensor(engine.param_view(b), engine.param_shard_view(b).clone(), group=engine.group)
+    engine.refresh_params_from_master()

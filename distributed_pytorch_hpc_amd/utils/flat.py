@@ -77,6 +77,12 @@ def flat_order(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1).reshape(-1) if _cl4(t) else t.reshape(-1)
 
 
+def flat_order_like(value: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+    """A logically-shaped ``value`` (any strides, e.g. from a state dict) flattened in ``like``'s storage order, i.e.
+    the element order ``like`` has inside an engine's flat buffer (inverse of ``param_view(...).contiguous()``)."""
+    return value.permute(0, 2, 3, 1).reshape(-1) if _cl4(like) else value.reshape(-1)
+
+
 def param_view(flat_slice: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
     """View of a flat-buffer slice shaped like ``like``, channels-last when ``like`` is, so a channels-last
     convolution weight living in an engine's flat bucket is read in place by MIOpen instead of being copied to NHWC

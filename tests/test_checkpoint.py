@@ -98,3 +98,116 @@ def test_sharded_resume_reshard_to_one_rank(tmp_path):
     got = _resume_single(str(tmp_path))
     for k in ref:
         assert torch.allclose(ref[k], got[k], atol=1e-5), k
+
+
+# ------------------------------------------------------------------------------------------------ FSDP / ZeRO engines
+# FULL_SHARD releases the module's parameter storage between uses (parallel/fsdp.py ZeRO3Engine): checkpoints must
+# gather the full state and load it back into the shards, for the consolidated and the sharded format, at the same
+# and at another world size, and across strategies.
+def _fsdp_setup(strategy="FULL_SHARD"):
+    from distributed_pytorch_hpc_amd.parallel.fsdp import FSDP, size_based_auto_wrap_policy
+
+    torch.manual_seed(3)
+    m = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 32), torch.nn.ReLU(),
+                            torch.nn.Linear(32, 8))
+    f = FSDP(m, sharding_strategy=strategy, auto_wrap_policy=size_based_auto_wrap_policy(1))
+    return f, f.make_optimizer("adamw", lr=1e-2, weight_decay=0.1)
+
+
+def _fsdp_batches(n):
+    g = torch.Generator().manual_seed(11)
+    return [(torch.randn(8, 16, generator=g), torch.randn(8, 8, generator=g)) for _ in range(n)]
+
+
+def _fsdp_train(f, opt, batches, rank, world):
+    for x, y in batches:
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(f(x.chunk(world)[rank]), y.chunk(world)[rank]).backward()
+        opt.step()
+    f.engine.synchronize()
+
+
+def _fsdp_uninterrupted(rank, world, strategy):
+    f, opt = _fsdp_setup(strategy)
+    _fsdp_train(f, opt, _fsdp_batches(4), rank, world)
+    return f.full_state_dict(rank0_only=False)
+
+
+def _fsdp_consolidated_save(rank, world, path, strategy):
+    from distributed_pytorch_hpc_amd.utils.checkpointing import save_checkpoint
+
+    f, opt = _fsdp_setup(strategy)
+    _fsdp_train(f, opt, _fsdp_batches(4)[:2], rank, world)
+    save_checkpoint(f, opt, 2, path)
+    return {}
+
+
+def _fsdp_consolidated_resume(rank, world, path, strategy):
+    from distributed_pytorch_hpc_amd.utils.checkpointing import load_checkpoint
+
+    f, opt = _fsdp_setup(strategy)
+    assert load_checkpoint(f, opt, path) == 2
+    assert opt.engine.step_count == 2
+    _fsdp_train(f, opt, _fsdp_batches(4)[2:], rank, world)
+    return f.full_state_dict(rank0_only=False)
+
+
+def _fsdp_sharded_save(rank, world, root):
+    from distributed_pytorch_hpc_amd.utils.checkpointing import ShardedCheckpointer
+
+    f, opt = _fsdp_setup()
+    _fsdp_train(f, opt, _fsdp_batches(4)[:2], rank, world)
+    ShardedCheckpointer(root, f).save(2)
+    return {}
+
+
+def _fsdp_sharded_resume(rank, world, root):
+    from distributed_pytorch_hpc_amd.utils.checkpointing import ShardedCheckpointer
+
+    f, opt = _fsdp_setup()
+    assert ShardedCheckpointer(root, f).load() == 2
+    _fsdp_train(f, opt, _fsdp_batches(4)[2:], rank, world)
+    return f.full_state_dict(rank0_only=False)
+
+
+def _close(ref, got, atol=1e-5):
+    assert ref.keys() == got.keys()
+    for k in ref:
+        assert ref[k].numel() > 0 and torch.allclose(ref[k], got[k], atol=atol), k
+
+
+def test_fsdp_full_shard_consolidated_single_rank(tmp_path):
+    """World 1 in-process: the saved file holds real (non-empty) tensors and loads into a fresh FSDP model."""
+    import torch.distributed as d
+
+    p = str(tmp_path / "ck.pt")
+    d.init_process_group("gloo", init_method=f"file://{tmp_path}/pg", rank=0, world_size=1)
+    try:
+        ref = _fsdp_uninterrupted(0, 1, "FULL_SHARD")
+        _fsdp_consolidated_save(0, 1, p, "FULL_SHARD")
+        sd = torch.load(p, weights_only=True)
+        assert all(v.numel() > 0 for v in sd["model_state_dict"].values())
+        assert sd["optimizer_state_dict"]["format"] == "full"
+        got = _fsdp_consolidated_resume(0, 1, p, "FULL_SHARD")
+    finally:
+        d.destroy_process_group()
+    _close(ref, got)
+
+
+def test_fsdp_full_shard_consolidated_two_ranks_resume_on_one(tmp_path):
+    p = str(tmp_path / "ck.pt")
+    ref = run_distributed(_fsdp_uninterrupted, 2, "FULL_SHARD")[0]
+    run_distributed(_fsdp_consolidated_save, 2, p, "FULL_SHARD")
+    got2 = run_distributed(_fsdp_consolidated_resume, 2, p, "FULL_SHARD")[0]
+    _close(ref, got2)
+    # the same file into another strategy (DDP-style NO_SHARD) and world size
+    got1 = run_distributed(_fsdp_consolidated_resume, 1, p, "NO_SHARD")[0]
+    _close(ref, got1)
+
+
+def test_fsdp_full_shard_sharded_checkpointer_reshard(tmp_path):
+    root = str(tmp_path / "ck")
+    ref = run_distributed(_fsdp_uninterrupted, 2, "FULL_SHARD")[0]
+    run_distributed(_fsdp_sharded_save, 2, root)
+    _close(ref, run_distributed(_fsdp_sharded_resume, 2, root)[0])
+    _close(ref, run_distributed(_fsdp_sharded_resume, 1, root)[0])

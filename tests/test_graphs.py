@@ -19,6 +19,32 @@ def rel_err(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
+def update_rel_err(a, b, what=""):
+    """Relative error of two parameter UPDATES; a zero reference update is a failure in its own right (a frozen
+    parameter), reported as such instead of overflowing the ratio."""
+    a, b = a.float(), b.float()
+    nb = b.norm().item()
+    assert nb > 0, f"reference update of {what} is exactly zero"
+    return (a - b).norm().item() / nb
+
+
+def masters(eng):
+    """The engine's fp32 master weights per parameter (world 1: a group's slice is its whole padded vector).  The
+    bf16 parameters are the wrong thing to compare: a few SGD steps move most of them by 0 or 1 ULP, so their
+    updates are quantised and a BN gamma at 1.0 either crosses a rounding threshold or not (the intermittent
+    '3.9e9' failures were exactly 2^-8 / 1e-12)."""
+    from distributed_pytorch_hpc_amd.utils.flat import align_up
+
+    out = []
+    for g in eng.groups:
+        v = eng.master[eng.opt_slice(g)]
+        o = 0
+        for p in g.params:
+            out.append(v[o:o + p.numel()].detach().clone())
+            o += align_up(p.numel())
+    return out
+
+
 # ------------------------------------------------------------------------------------------------ CPU
 def test_step_hyper_eager_writes_lr_and_step():
     h = StepHyper("cpu")
@@ -114,6 +140,7 @@ def _run(model, opt_cfg, batches, graphed, warmup=2, fsdp=False, autocast=None):
                 eng.step(lr=self.param_groups[0]["lr"])
 
         opt = _O()
+    m0 = masters(eng)
 
     def step_fn(x, y):
         opt.zero_grad(set_to_none=True)
@@ -141,6 +168,7 @@ def _run(model, opt_cfg, batches, graphed, warmup=2, fsdp=False, autocast=None):
     torch.cuda.synchronize()
     if graphed:
         assert runner.captured
+    eng.m0 = m0
     return [p.detach().float().clone() for p in model.parameters()], torch.stack(losses), eng
 
 
@@ -195,17 +223,28 @@ def test_graphed_resnet_fsdp_bf16_matches_eager(dph_native, arch):
     batches = [(torch.randn(16, 3, 32, 32, device=DEV, dtype=torch.bfloat16).contiguous(
         memory_format=torch.channels_last), torch.randint(0, 10, (16,), device=DEV)) for _ in range(6)]
     cfg = lambda: OptimConfig("sgd", lr=0.002, momentum=0.9, weight_decay=1e-4)   # noqa: E731
-    p0 = [p.detach().float().clone() for p in make().parameters()]
-    # MIOpen's bf16 convolutions are not bit-reproducible run to run: two eager runs set the noise floor.  Compare
-    # the parameter UPDATES (a frozen or stale parameter shows up there, not in the parameters themselves)
-    pe, le, _ = _run(make(), cfg(), batches, graphed=False, fsdp=True)
-    pe2, le2, _ = _run(make(), cfg(), batches, graphed=False, fsdp=True)
-    pg, lg, _ = _run(make(), cfg(), batches, graphed=True, fsdp=True)
-    de, de2, dg = ([a - b for a, b in zip(ps, p0)] for ps in (pe, pe2, pg))
-    floor = max(rel_err(a, b) for a, b in zip(de2, de))
-    worst = max(rel_err(a, b) for a, b in zip(dg, de))
-    assert worst < max(3 * floor, 5e-2), (worst, floor)
-    assert rel_err(lg, le) < max(3 * rel_err(le2, le), 1e-2)
+    # MIOpen's default bf16 convolution algorithms are not run-to-run reproducible, and six small-batch steps amplify
+    # that noise chaotically (20-120 % apart in the updates; the stock-PyTorch path the same,
+    # scripts/diag_nondeterminism.py).  With MIOpen's deterministic algorithms the framework's own path -- fused BN,
+    # 1x1-convolution kernels, direct gradient-bucket writes, FSDP units -- is bitwise reproducible, so two eager runs
+    # must agree EXACTLY (a race or a lost gradient write breaks that), and the graph replays the same kernels.
+    det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        _, le, ee = _run(make(), cfg(), batches, graphed=False, fsdp=True)
+        _, le2, ee2 = _run(make(), cfg(), batches, graphed=False, fsdp=True)
+        _, lg, eg = _run(make(), cfg(), batches, graphed=True, fsdp=True)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
+    # compare the fp32 master-weight UPDATES (a frozen or stale parameter shows up there)
+    de, de2, dg = ([a - b for a, b in zip(masters(e), e.m0)] for e in (ee, ee2, eg))
+    for i, (a, b) in enumerate(zip(de2, de)):
+        assert torch.equal(a, b), f"two eager runs differ at parameter {i}: {update_rel_err(a, b, i):.3e}"
+    assert torch.equal(le2, le)
+    worst = max(update_rel_err(a, b, f"eager param {i}") for i, (a, b) in enumerate(zip(dg, de)))
+    print(f"[{arch}] graph-vs-eager worst update rel err {worst:.3e}")
+    assert worst < 1e-3, worst
+    assert rel_err(lg, le) < 1e-4
 
 
 @pytest.mark.gpu

@@ -3,6 +3,8 @@ import os
 import subprocess
 import sys
 
+import torch
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -54,3 +56,18 @@ def test_utils_facade_has_reference_names():
                  "get_logger", "rank_log", "verify_min_gpu_count", "training_profiler", "print_profiler_summary",
                  "save_checkpoint", "load_checkpoint", "TrainingConfig", "redirect"):
         assert callable(getattr(u, name)), name
+
+
+def test_device_for_refuses_shared_gpu_under_rccl(monkeypatch):
+    """nccl (RCCL) ranks need a GPU each: local rank >= visible GPUs fails at startup; gloo ranks stay on the CPU
+    device (several may then share one GPU explicitly, bench.py --backend gloo)."""
+    import pytest
+
+    from distributed_pytorch_hpc_amd.runtime import env as rt
+
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
+    assert rt.device_for(1, "nccl") == torch.device("cuda", 1)
+    with pytest.raises(RuntimeError, match="no GPU of its own"):
+        rt.device_for(2, "nccl")
+    assert rt.device_for(5, "gloo").type == "cpu"
