@@ -125,6 +125,39 @@ __device__ __forceinline__ bf16x8 zero8() {
   return z;
 }
 
+// Epilogue of a 32 x HD accumulator set whose lane holds row `row` (columns dt * 32 + 8 gg + 4 h + j, j < 4): scale,
+// optionally rotate every interleaved pair (2i, 2i + 1) back by -theta(row + rope_off, i) (the gradient of RoPE), cast
+// to bf16 and store 4 columns per 8-B store.
+template <int DT>
+__device__ __forceinline__ void store_rows_bf16(bf16* out, const f32x16 (&acc)[DT], float mul, int h, int row,
+                                                const float* rc, const float* rs, int rope_off) {
+  constexpr int HALF = DT * 16;
+  const float* cr = rc ? rc + (int64_t)(row + rope_off) * HALF : nullptr;
+  const float* sr = rs ? rs + (int64_t)(row + rope_off) * HALF : nullptr;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = acc[dt][4 * gg + j] * mul;
+      if (cr) {
+        const int i0 = dt * 16 + 4 * gg + 2 * h;   // pair index of columns (j = 0, 1); j = 2, 3 is i0 + 1
+        const float2 c = *reinterpret_cast<const float2*>(cr + i0);
+        const float2 s = *reinterpret_cast<const float2*>(sr + i0);
+        const float a0 = v[0], b0 = v[1], a1 = v[2], b1 = v[3];
+        v[0] = fmaf(a0, c.x, b0 * s.x);
+        v[1] = fmaf(b0, c.x, -a0 * s.x);
+        v[2] = fmaf(a1, c.y, b1 * s.y);
+        v[3] = fmaf(b1, c.y, -a1 * s.y);
+      }
+      bf16x4 w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = (bf16)v[j];
+      *reinterpret_cast<bf16x4*>(out + dt * 32 + 8 * gg + 4 * h) = w;
+    }
+}
+
 // Per-lane plan for one 64-key K/V tile: swizzled LDS offsets of the ds_read_b128 row reads and the
 // ds_read_b64_tr_b16 transposed reads, and the LDS-DMA source offsets of the staging loads.  Computed once
 // per kernel so the tile loop issues loads with immediate offsets instead of recomputing the XOR swizzle.
@@ -572,19 +605,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
   if (mykey < p.Sk) {
     bf16* dkp = (bf16*)P.dk + (int64_t)b * P.dk_sb + (int64_t)mykey * P.dk_ss + (int64_t)hk * P.dk_sh;
     bf16* dvp = (bf16*)P.dv + (int64_t)b * P.dv_sb + (int64_t)mykey * P.dv_ss + (int64_t)hk * P.dv_sh;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        bf16x4 wk, wv;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          wk[j] = (bf16)(dk[dt][4 * gg + j] * p.scale);
-          wv[j] = (bf16)dv[dt][4 * gg + j];
-        }
-        *reinterpret_cast<bf16x4*>(dkp + dt * 32 + 8 * gg + 4 * h) = wk;
-        *reinterpret_cast<bf16x4*>(dvp + dt * 32 + 8 * gg + 4 * h) = wv;
-      }
+    store_rows_bf16<DT>(dkp, dk, p.scale, h, mykey, P.rope_cos, P.rope_sin, P.rope_off);
+    store_rows_bf16<DT>(dvp, dv, 1.f, h, mykey, nullptr, nullptr, 0);
   }
 }
 
@@ -705,15 +727,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
 
   if (myq < p.Sq) {
     bf16* dqp = (bf16*)P.dq + (int64_t)b * P.dq_sb + (int64_t)myq * P.dq_ss + (int64_t)hq * P.dq_sh;
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        bf16x4 w;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = (bf16)(dq[dt][4 * gg + j] * p.scale);
-        *reinterpret_cast<bf16x4*>(dqp + dt * 32 + 8 * gg + 4 * h) = w;
-      }
+    store_rows_bf16<DT>(dqp, dq, p.scale, h, myq, P.rope_cos, P.rope_sin, P.rope_off);
   }
 }
 

@@ -85,6 +85,10 @@ struct AttnBwdParams {
   float* dq_accum;       // fp32 [B, Sq, Hq, D] workspace, zeroed by the launcher
   void* dq; void* dk; void* dv;   // bf16 [B,S,H,D] at the strides below; dk/dv per KV head (GQA summed)
   int64_t dq_sb, dq_ss, dq_sh, dk_sb, dk_ss, dk_sh, dv_sb, dv_ss, dv_sh;
+  // optional fused inverse RoPE of dq / dk (interleaved pairs, fp32 tables [max_pos, D / 2], position = row +
+  // rope_off): the gradient of attention(rope(q), rope(k), v) w.r.t. the UNrotated q / k, rotated in the epilogue
+  // from the fp32 accumulators (one rounding, no separate rope pass over dq / dk)
+  const float* rope_cos; const float* rope_sin; int rope_off;
 };
 void flash_attn_bwd(const AttnBwdParams& p, hipStream_t stream);
 

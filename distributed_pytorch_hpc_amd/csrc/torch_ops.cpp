@@ -291,7 +291,8 @@ std::tuple<Tensor, Tensor> flash_attn_fwd(const Tensor& q, const Tensor& k, cons
 
 void flash_attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                          const Tensor& lse, double scale, bool causal, Tensor& dq, Tensor& dk, Tensor& dv,
-                         double dropout_p, int64_t seed) {
+                         double dropout_p, int64_t seed, const c10::optional<Tensor>& rope_cos = c10::nullopt,
+                         const c10::optional<Tensor>& rope_sin = c10::nullopt, int64_t rope_offset = 0) {
   c10::DeviceGuard g(q.device());
   check_attn_operand(q, "q"); check_attn_operand(k, "k"); check_attn_operand(v, "v");
   check_attn_operand(o, "o"); check_attn_operand(dout, "dout");
@@ -312,6 +313,20 @@ void flash_attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, c
   P.dq_sb = dq.stride(0); P.dq_ss = dq.stride(1); P.dq_sh = dq.stride(2);
   P.dk_sb = dk.stride(0); P.dk_ss = dk.stride(1); P.dk_sh = dk.stride(2);
   P.dv_sb = dv.stride(0); P.dv_ss = dv.stride(1); P.dv_sh = dv.stride(2);
+  if (rope_cos.has_value() && rope_cos->defined()) {
+    TORCH_CHECK(rope_sin.has_value() && rope_sin->defined(), "flash_attn_bwd: rope_cos without rope_sin");
+    const auto& c = *rope_cos;
+    const auto& sn = *rope_sin;
+    TORCH_CHECK(c.scalar_type() == at::kFloat && sn.scalar_type() == at::kFloat && c.is_contiguous() &&
+                    sn.is_contiguous() && c.dim() == 2 && c.sizes() == sn.sizes() && c.size(1) == D / 2,
+                "flash_attn_bwd: rope tables must be contiguous fp32 [max_pos, head_dim / 2]");
+    TORCH_CHECK(c.device() == q.device(), "flash_attn_bwd: rope tables on another device");
+    TORCH_CHECK(k.size(1) == Sq && rope_offset >= 0 && rope_offset + Sq <= c.size(0),
+                "flash_attn_bwd: fused RoPE needs Sq == Sk and positions inside the table");
+    P.rope_cos = c.data_ptr<float>();
+    P.rope_sin = sn.data_ptr<float>();
+    P.rope_off = (int)rope_offset;
+  }
   dph::flash_attn_bwd(P, cur_stream());
 }
 
@@ -327,8 +342,10 @@ std::tuple<Tensor, Tensor, Tensor> flash_attn_bwd(const Tensor& dout, const Tens
 
 void flash_attn_bwd_into(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                          const Tensor& lse, double scale, bool causal, Tensor dq, Tensor dk, Tensor dv,
-                         double dropout_p, int64_t seed) {
-  flash_attn_bwd_impl(dout, q, k, v, o, lse, scale, causal, dq, dk, dv, dropout_p, seed);
+                         double dropout_p, int64_t seed, const c10::optional<Tensor>& rope_cos,
+                         const c10::optional<Tensor>& rope_sin, int64_t rope_offset) {
+  flash_attn_bwd_impl(dout, q, k, v, o, lse, scale, causal, dq, dk, dv, dropout_p, seed, rope_cos, rope_sin,
+                      rope_offset);
 }
 
 // ------------------------------------------------------------------------------------------------ embedding
@@ -694,7 +711,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, "
         "float dropout_p=0., int seed=0) -> (Tensor, Tensor, Tensor)");
   m.def("flash_attn_bwd_into(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, "
-        "bool causal, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float dropout_p=0., int seed=0) -> ()");
+        "bool causal, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float dropout_p=0., int seed=0, "
+        "Tensor? rope_cos=None, Tensor? rope_sin=None, int rope_offset=0) -> ()");
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");

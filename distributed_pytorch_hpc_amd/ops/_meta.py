@@ -138,7 +138,8 @@ def _fa_bwd(dout, q, k, v, o, lse, scale, causal, dropout_p=0.0, seed=0):
 
 
 @register_fake("dph::flash_attn_bwd_into")
-def _fa_bwd_into(dout, q, k, v, o, lse, scale, causal, dq, dk, dv, dropout_p=0.0, seed=0):
+def _fa_bwd_into(dout, q, k, v, o, lse, scale, causal, dq, dk, dv, dropout_p=0.0, seed=0, rope_cos=None,
+                 rope_sin=None, rope_offset=0):
     return None
 
 

@@ -17,6 +17,7 @@ it for tests.  The seed comes from torch's CPU generator (``torch.manual_seed`` 
 from __future__ import annotations
 
 import math
+import os
 import warnings
 
 import torch
@@ -26,6 +27,8 @@ from . import _lib
 from .rope import rope_, rope_reference
 
 _NATIVE_D = (32, 64, 128)
+# DPH_FUSED_ROPE_BWD=0: separate inverse-RoPE pass over dq / dk instead of the fused kernel epilogue (A/B runs)
+_FUSED_ROPE_BWD = os.environ.get("DPH_FUSED_ROPE_BWD", "1") != "0"
 _warned = set()
 
 
@@ -147,7 +150,7 @@ class _RopeFlashAttnFn(torch.autograd.Function):
     """o = attention(rope(q), rope(k), v) with q/k/v strided views of the fused QKV output.
 
     RoPE is applied IN PLACE to the q/k parts of ``qkv`` (marked dirty); backward runs the flash
-    backward, rotates dq/dk back by -theta and returns one packed d(qkv).
+    backward with the inverse rotation of dq/dk fused into its epilogues and returns one packed d(qkv).
     """
 
     @staticmethod
@@ -179,10 +182,14 @@ class _RopeFlashAttnFn(torch.autograd.Function):
         dq = dqkv[:, :, : nh * hd].view(b, s, nh, hd)
         dk = dqkv[:, :, nh * hd: (nh + nkv) * hd].view(b, s, nkv, hd)
         dv = dqkv[:, :, (nh + nkv) * hd:].view(b, s, nkv, hd)
-        _lib.ops().flash_attn_bwd_into(do.view(b, s, nh, hd).contiguous(), q, k, v, o, lse, scale, causal,
-                                       dq, dk, dv)
-        # inverse rotation of dq and dk in one strided launch ([B, S, Hq + Hkv, hd] view)
-        rope_(dqkv[:, :, : (nh + nkv) * hd].view(b, s, nh + nkv, hd), cos, sin, pos_offset, True)
+        if _FUSED_ROPE_BWD:
+            # dq / dk leave the kernels already rotated back by -theta (RoPE's gradient, from the fp32 accumulators)
+            _lib.ops().flash_attn_bwd_into(do.view(b, s, nh, hd).contiguous(), q, k, v, o, lse, scale, causal,
+                                           dq, dk, dv, 0.0, 0, cos, sin, pos_offset)
+        else:
+            _lib.ops().flash_attn_bwd_into(do.view(b, s, nh, hd).contiguous(), q, k, v, o, lse, scale, causal,
+                                           dq, dk, dv)
+            rope_(dqkv[:, :, : (nh + nkv) * hd].view(b, s, nh + nkv, hd), cos, sin, pos_offset, True)
         if _dqkv_passthrough is not None:
             dqkv = dqkv + _dqkv_passthrough
         return dqkv, None, None, None, None, None, None, None, None

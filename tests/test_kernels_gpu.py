@@ -225,17 +225,19 @@ def test_flash_attention_padded_head_dim(dph_native):
     assert q.grad.shape == q.shape
 
 
-def test_rope_attention_fused(dph_native):
+@pytest.mark.parametrize("D,S,pos", [(64, 128, 0), (128, 192, 37), (32, 96, 5)])
+def test_rope_attention_fused(dph_native, D, S, pos):
+    """RoPE in place + flash attention; backward with the inverse rotation fused into the dq / dk epilogues."""
     torch.manual_seed(11)
-    B, S, H, KV, D = 2, 128, 4, 2, 64
+    B, H, KV = 2, 4, 2
     cos, sin = rope_mod.precompute_rope_tables(D, 256, device=DEV)
     qkv = torch.randn(B, S, (H + 2 * KV) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    o = ops.rope_attention(qkv * 1.0, cos, sin, H, KV, D)
+    o = ops.rope_attention(qkv * 1.0, cos, sin, H, KV, D, pos_offset=pos)
     x = qkv.detach().float().requires_grad_()
     q = x[:, :, : H * D].view(B, S, H, D)
     k = x[:, :, H * D:(H + KV) * D].view(B, S, KV, D)
     v = x[:, :, (H + KV) * D:].view(B, S, KV, D)
-    q, k = rope_mod.rope_reference(q, cos, sin), rope_mod.rope_reference(k, cos, sin)
+    q, k = rope_mod.rope_reference(q, cos, sin, pos), rope_mod.rope_reference(k, cos, sin, pos)
     orf = attn_mod.attention_reference(q, k, v, True, 1 / math.sqrt(D)).reshape(B, S, -1)
     assert rel_err(o, orf) < 2e-2
     g = torch.randn_like(o)
