@@ -66,6 +66,33 @@ template <> struct Vec8<float> {
   }
 };
 
+// LDS-DMA of 16 B per lane: global (wave-uniform SGPR base `sbase` + per-lane 32-bit byte offset `voff`) -> LDS
+// (lane-linear destination at the wave-uniform LDS byte address `lds`).  Issued from inline asm on purpose: hipcc
+// cannot tell that ds_reads of OTHER LDS regions do not alias an in-flight DMA and would drain every DMA (vmcnt(0))
+// before each read; the asm form is invisible to its wait bookkeeping, so completion must be counted by hand
+// (wait_vmcnt<N> + s_barrier) before any wave reads the destination.  hipcc's own counted waits for ordinary loads
+// only ever over-wait around these (vmcnt retires in issue order).
+__device__ __forceinline__ void lds_dma16(const void* sbase, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds)
+               : "memory");
+}
+
+// s_waitcnt with only the vector-memory counter constrained (LDS-DMA completion), gfx9 encoding.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// Wave-uniform LDS byte address of a __shared__ pointer (for lds_dma16's M0 operand).
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)(p));
+}
+
 template <typename T> __device__ __forceinline__ float to_f32(T v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f32(float v) { return (T)v; }
 

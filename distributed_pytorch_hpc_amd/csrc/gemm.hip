@@ -39,26 +39,11 @@ __device__ __forceinline__ bf16x8 tr2(const char* base, int off_lo, int off_hi) 
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// LDS-DMA of 16 B per lane: global (uniform SGPR base `sbase` + per-lane 32-bit byte offset `voff`) -> LDS
-// (lane-linear destination at the wave-uniform LDS byte address `lds`).  Issued from inline asm on purpose:
-// hipcc cannot tell that the transposed ds_reads of OTHER regions do not alias an in-flight DMA and would drain
-// every DMA (vmcnt(0)) before each read; the asm form is invisible to its wait bookkeeping, and completion is
-// counted explicitly (wait_vm<N> + s_barrier) before any region is read.  The SGPR-base form keeps the per-slot
-// address arithmetic scalar.
-__device__ __forceinline__ void glds16(const char* sbase, unsigned voff, unsigned lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(voff), "s"(sbase), "s"(lds)
-               : "memory");
-}
-
-// s_waitcnt with only the vector-memory counter constrained (LDS-DMA completion), gfx9 encoding.
+// LDS-DMA / counted-wait helpers (dph_common.h): the DMA is issued from inline asm so hipcc does not drain it before
+// the transposed ds_reads of other regions; completion is counted explicitly (wait_vm<N> + s_barrier).
+__device__ __forceinline__ void glds16(const char* sbase, unsigned voff, unsigned lds) { lds_dma16(sbase, voff, lds); }
 template <int N>
-__device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
+__device__ __forceinline__ void wait_vm() { wait_vmcnt<N>(); }
 
 // Pipeline: one K-step (64 tokens) = 4 phases of 16 k-rows.  Phase P's operands live in LDS region
 // R = P & 7 (tile parity x 16-row region; A rows at +0, B rows at +8 KB of a 16-KB region) and are filled by DMA
