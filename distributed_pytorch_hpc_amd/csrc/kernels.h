@@ -152,6 +152,13 @@ void latmse_fwd(const void* pred, const void* target, float* partial, float* out
 void latmse_bwd(const void* pred, const void* target, const float* gloss, void* dpred, void* dtarget, int64_t n,
                 int64_t H, int64_t W, int64_t n_global, int64_t lat_offset, int dtype, hipStream_t stream);
 
+// Batch assembly from a device-resident uint8 image set [N, H, W, C] (csrc/imageaug.hip): gather idx[B], random crop
+// (per-sample dy, dx in [0, 2 pad], zero padding) + horizontal flip (params [B, 3] int32, or null = centre, no flip),
+// scale 1/255, normalise ((v - mean) * inv_std), write NCHW or NHWC in fp32 / bf16.
+void image_augment(const uint8_t* images, const int64_t* idx, const int* params, const float* mean,
+                   const float* inv_std, void* out, int64_t B, int64_t H, int64_t W, int64_t C, int64_t pad,
+                   bool nhwc, int out_dtype, hipStream_t stream);
+
 // Single-node all-reduce over IPC-mapped peer buffers (csrc/custom_allreduce.hip).  ctx is an opaque handle.
 int64_t car_create(int rank, int world, int64_t max_bytes, double timeout_s);
 void car_ipc_handle(int64_t ctx, void* out64);

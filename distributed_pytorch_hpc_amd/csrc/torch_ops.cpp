@@ -348,6 +348,36 @@ void flash_attn_bwd_into(const Tensor& dout, const Tensor& q, const Tensor& k, c
                       rope_offset);
 }
 
+// ------------------------------------------------------------------------------------------------ image batches
+Tensor image_augment(const Tensor& images, const Tensor& idx, const c10::optional<Tensor>& params,
+                     const Tensor& mean, const Tensor& inv_std, int64_t pad, bool channels_last, bool bf16_out) {
+  c10::DeviceGuard g(images.device());
+  TORCH_CHECK(images.scalar_type() == at::kByte && images.dim() == 4 && images.is_contiguous(),
+              "image_augment: images must be contiguous uint8 [N, H, W, C]");
+  const int64_t H = images.size(1), W = images.size(2), C = images.size(3);
+  TORCH_CHECK(C == 1 || C == 3, "image_augment: 1 or 3 channels");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 1 && idx.is_contiguous(), "image_augment: int64 [B] idx");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && inv_std.scalar_type() == at::kFloat && mean.numel() == C &&
+                  inv_std.numel() == C && mean.is_contiguous() && inv_std.is_contiguous(),
+              "image_augment: fp32 mean / inv_std of C elements");
+  TORCH_CHECK(pad >= 0 && pad <= H && pad <= W, "image_augment: bad padding");
+  const int64_t B = idx.size(0);
+  const int* prm = nullptr;
+  if (params.has_value() && params->defined()) {
+    TORCH_CHECK(params->scalar_type() == at::kInt && params->is_contiguous() && params->numel() == 3 * B,
+                "image_augment: int32 [B, 3] (dy, dx, flip) params");
+    prm = params->data_ptr<int>();
+  }
+  for (const Tensor* t : {&idx, &mean, &inv_std}) TORCH_CHECK(t->device() == images.device(), "image_augment: device");
+  auto opts = images.options().dtype(bf16_out ? at::kBFloat16 : at::kFloat);
+  Tensor out = channels_last ? at::empty({B, C, H, W}, opts.memory_format(at::MemoryFormat::ChannelsLast))
+                             : at::empty({B, C, H, W}, opts);
+  dph::image_augment(images.data_ptr<uint8_t>(), idx.data_ptr<int64_t>(), prm, mean.data_ptr<float>(),
+                     inv_std.data_ptr<float>(), out.data_ptr(), B, H, W, C, pad, channels_last,
+                     bf16_out ? dph::kBF16 : dph::kF32, cur_stream());
+  return out;
+}
+
 // ------------------------------------------------------------------------------------------------ embedding
 Tensor embedding_fwd(const Tensor& ids, const Tensor& table, int64_t vocab_start) {
   c10::DeviceGuard g(table.device());
@@ -713,6 +743,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("flash_attn_bwd_into(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, "
         "bool causal, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, float dropout_p=0., int seed=0, "
         "Tensor? rope_cos=None, Tensor? rope_sin=None, int rope_offset=0) -> ()");
+  m.def("image_augment(Tensor images, Tensor idx, Tensor? params, Tensor mean, Tensor inv_std, int pad, "
+        "bool channels_last, bool bf16_out) -> Tensor");
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
@@ -754,6 +786,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("sgd_step_", &sgd_step_);
   m.impl("sumsq_", &sumsq_);
   m.impl("cross_entropy_fwd", &cross_entropy_fwd);
+  m.impl("image_augment", &image_augment);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("flash_attn_bwd_into", &flash_attn_bwd_into);

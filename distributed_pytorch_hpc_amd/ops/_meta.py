@@ -143,6 +143,13 @@ def _fa_bwd_into(dout, q, k, v, o, lse, scale, causal, dq, dk, dv, dropout_p=0.0
     return None
 
 
+@register_fake("dph::image_augment")
+def _img_aug(images, idx, params, mean, inv_std, pad, channels_last, bf16_out):
+    n, h, w, c = images.shape
+    out = images.new_empty((idx.shape[0], c, h, w), dtype=torch.bfloat16 if bf16_out else torch.float32)
+    return out.contiguous(memory_format=torch.channels_last) if channels_last else out
+
+
 @register_fake("dph::embedding_fwd")
 def _emb_fwd(ids, table, vocab_start):
     return table.new_empty((*ids.shape, table.shape[1]))

@@ -6,8 +6,10 @@ Identity, 10 classes; ``size_based_auto_wrap_policy(min_num_params=1e5)``; ``Sha
 ``--use-amp`` -> ``MixedPrecision(param=bf16, reduce=bf16, buffer=bf16)``; SGD lr 0.01 m 0.9 wd 5e-4; CE;
 Trainer.train_epoch / test L90-155).
 
-CIFAR-10 needs torchvision + a download, neither available: batches are synthetic CIFAR-shaped tensors
-(3x32x32, 10 classes) generated on device.  Evaluation is collective (every rank scores its shard) so it
+With ``--data-dir`` pointing at the CIFAR-10 binary distribution (cifar-10-batches-bin) the real dataset is used:
+held in HBM, batches gathered + augmented (RandomCrop(32, padding=4) + flip + Normalize, as the reference) on the
+GPU by data/cifar.py.  Without it (no download here) batches are synthetic CIFAR-shaped tensors (3x32x32, 10
+classes) generated on device.  Evaluation is collective (every rank scores its shard) so it
 works under FSDP (reference defect X9).  ``--sharding`` selects FULL_SHARD / SHARD_GRAD_OP / NO_SHARD /
 HYBRID_SHARD; ``--wrap`` size (default) or block (one unit per BasicBlock).
 
@@ -21,7 +23,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
-from distributed_pytorch_hpc_amd.data import DeviceBatches  # noqa: E402
+from distributed_pytorch_hpc_amd.data import CIFAR10, CIFARDeviceLoader, DeviceBatches  # noqa: E402
 from distributed_pytorch_hpc_amd.models import resnet  # noqa: E402
 from distributed_pytorch_hpc_amd.models.resnet import BasicBlock, Bottleneck  # noqa: E402
 from distributed_pytorch_hpc_amd.parallel.data_parallel import MixedPrecision  # noqa: E402
@@ -48,6 +50,7 @@ def main(argv=None):
     ap.add_argument("--wrap", choices=["size", "block"], default="size")
     ap.add_argument("--min-num-params", type=int, default=int(1e5))
     ap.add_argument("--save-full-state", default=None, help="write the consolidated FULL_STATE_DICT here")
+    ap.add_argument("--data-dir", default=None, help="CIFAR-10 binary distribution (cifar-10-batches-bin)")
     args = ap.parse_args(argv)
     rank, world, local, dev = start(args)
 
@@ -58,15 +61,22 @@ def main(argv=None):
     fsdp = FSDP(model, sharding_strategy=args.sharding, mixed_precision=mp, auto_wrap_policy=policy)
     opt = fsdp.make_optimizer("sgd", lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay)
     dtype = torch.bfloat16 if args.use_amp else torch.float32
-    train = DeviceBatches("images", args.batch_size, dev, seed=args.seed, rank=rank, image_size=args.image_size,
-                          num_classes=args.num_classes, dtype=dtype)
-    test = DeviceBatches("images", args.batch_size, dev, seed=args.seed + 1, rank=rank, image_size=args.image_size,
-                         num_classes=args.num_classes, dtype=dtype)
+    if args.data_dir:
+        train = CIFARDeviceLoader(CIFAR10(args.data_dir, train=True), args.batch_size, dev, dp_rank=rank,
+                                  dp_size=world, augment=True, seed=args.seed, dtype=dtype)
+        test = CIFARDeviceLoader(CIFAR10(args.data_dir, train=False), args.batch_size, dev, dp_rank=rank,
+                                 dp_size=world, augment=False, shuffle=False, drop_last=False, dtype=dtype)
+    else:
+        train = DeviceBatches("images", args.batch_size, dev, seed=args.seed, rank=rank, image_size=args.image_size,
+                              num_classes=args.num_classes, dtype=dtype)
+        test = DeviceBatches("images", args.batch_size, dev, seed=args.seed + 1, rank=rank,
+                             image_size=args.image_size, num_classes=args.num_classes, dtype=dtype)
 
     def loss_fn(out, y):
         return F.cross_entropy(out.float(), y)
 
     trainer = Trainer(fsdp, opt, train, loss_fn, dev, max_steps_per_epoch=args.steps_per_epoch,
+                      sampler=train if args.data_dir else None,
                       log_every=max(args.steps_per_epoch // 2, 1), metrics_file=args.metrics_file,
                       cuda_graph=args.cuda_graph)
     for epoch in range(args.epochs):

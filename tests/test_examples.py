@@ -80,3 +80,21 @@ def test_ddp_basic_resumes_from_snapshot(tmp_path):
     assert first["epochs"] == 2 and os.path.exists(tmp_path / "snap.pt")
     second = _run("01_data_parallel_ddp/ddp_basic.py", 2, ["4", "2", "--snapshot-path", "{tmp}/snap.pt"], tmp_path)
     assert second["epochs"] == 2   # resumed at epoch 2, ran epochs 2 and 3 only
+
+
+def test_fsdp_resnet_on_cifar_binary_files(tmp_path):
+    """--data-dir: the CIFAR-10 binary distribution (fake records here; no download) through the device loader."""
+    import numpy as np
+
+    from distributed_pytorch_hpc_amd.data.cifar import write_cifar_bin
+
+    rng = np.random.default_rng(0)
+    d = tmp_path / "cifar-10-batches-bin"
+    d.mkdir()
+    for name in [f"data_batch_{i}.bin" for i in range(1, 6)] + ["test_batch.bin"]:
+        write_cifar_bin(str(d / name), rng.integers(0, 256, (8, 32, 32, 3), dtype=np.uint8),
+                        rng.integers(0, 10, 8).astype(np.uint8))
+    out = _run("02_fully_sharded_fsdp/fsdp_resnet.py", 2, ["--arch", "resnet18", "--batch-size", "4",
+                                                           "--steps-per-epoch", "3", "--test-steps", "2",
+                                                           "--data-dir", str(d)], tmp_path)
+    assert out["example"] == "fsdp_resnet" and out["test"]["samples"] == 8   # the 8 test images, 4 per rank
