@@ -10,7 +10,8 @@ source of two BASELINE.json configs: ResNet-50 DDP on CPU/gloo (world 2) and Res
 MI355X version: ResNets defined natively (torchvision is not installed), channels-last bf16 convolutions
 through MIOpen under ``--amp``, gradient buckets on the RCCL engine (``--ddp``) or sharded FSDP units
 (``--use-fsdp``, bf16 MixedPrecision with ``--amp``), evaluation collective on every rank (reference X9: rank-0
-eval hangs under FSDP).  CIFAR-10 needs a download and is unavailable: ``--use-syn`` is the default.
+eval hangs under FSDP).  ``--data-dir`` trains on CIFAR-10 from its binary distribution (no download here): the
+dataset sits in HBM and batches are gathered + augmented on the GPU (data/cifar.py); otherwise ``--use-syn``.
 
     python examples/resnet_benchmark.py --device cpu --arch resnet50 --batch-size 8 --epochs 2 --steps-syn 2
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/resnet_benchmark.py --use-fsdp --amp --channels-last
@@ -25,7 +26,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
-from distributed_pytorch_hpc_amd.data import DeviceBatches  # noqa: E402
+from distributed_pytorch_hpc_amd.data import CIFAR10, CIFARDeviceLoader, DeviceBatches  # noqa: E402
 from distributed_pytorch_hpc_amd.models import resnet  # noqa: E402
 from distributed_pytorch_hpc_amd.models.resnet import BasicBlock, Bottleneck  # noqa: E402
 from distributed_pytorch_hpc_amd.parallel.data_parallel import DDP, MixedPrecision  # noqa: E402
@@ -64,7 +65,11 @@ def main(argv=None):
     ap.add_argument("--resume", default=None, help="snapshot path (DDP): resume from / save to")
     ap.add_argument("--logfile", default=None, help="append a result line (reference: resnet_benchmark.log)")
     ap.add_argument("--eval-steps", type=int, default=0)
+    ap.add_argument("--data-dir", default=None, help="CIFAR-10 binary distribution (cifar-10-batches-bin): real data, "
+                                                     "full epochs, 10 classes")
     args = ap.parse_args(argv)
+    if args.data_dir:
+        args.use_syn, args.num_classes = False, 10
     rank, world, local, dev = start(args)   # MIOpen find mode on GPU unless --no-conv-search (train/cli.py)
     backend = dist.get_backend() if dist.is_initialized() else ("nccl" if dev.type == "cuda" else "gloo")
 
@@ -85,6 +90,13 @@ def main(argv=None):
     opt = wrapped.make_optimizer("sgd", lr=args.lr, momentum=args.momentum, weight_decay=args.weight_decay)
     data = DeviceBatches("images", args.batch_size, dev, seed=args.seed, rank=rank, image_size=args.image_size,
                          num_classes=args.num_classes, dtype=in_dtype, fixed=True)
+    cifar = test = None
+    if args.data_dir:
+        cifar = CIFARDeviceLoader(CIFAR10(args.data_dir, train=True), args.batch_size, dev, dp_rank=rank,
+                                  dp_size=world, seed=args.seed, dtype=in_dtype, channels_last=args.channels_last)
+        test = CIFARDeviceLoader(CIFAR10(args.data_dir, train=False), args.batch_size, dev, dp_rank=rank,
+                                 dp_size=world, augment=False, shuffle=False, drop_last=False, dtype=in_dtype,
+                                 channels_last=args.channels_last)
 
     class _CL:
         """channels-last view of the synthetic stream"""
@@ -99,7 +111,8 @@ def main(argv=None):
     def loss_fn(out, y):
         return F.cross_entropy(out.float(), y)
 
-    trainer = Trainer(wrapped, opt, _CL(), loss_fn, dev, max_steps_per_epoch=args.steps_syn,
+    trainer = Trainer(wrapped, opt, cifar if cifar is not None else _CL(), loss_fn, dev,
+                      max_steps_per_epoch=None if cifar is not None else args.steps_syn, sampler=cifar,
                       log_every=max(args.steps_syn // 2, 1), autocast_dtype=autocast,
                       snapshot_path=args.resume if not args.use_fsdp else None,
                       save_every=1 if args.resume and not args.use_fsdp else 0, metrics_file=args.metrics_file,
@@ -110,7 +123,7 @@ def main(argv=None):
               flush=True)
     summary = trainer.train(args.epochs)
     if args.eval_steps:
-        summary["eval"] = trainer.evaluate(_CL(), max_steps=args.eval_steps)
+        summary["eval"] = trainer.evaluate(test if test is not None else _CL(), max_steps=args.eval_steps)
     summary.update(example="resnet_benchmark", arch=args.arch, params=n_params, world=world,
                    mode="fsdp" if args.use_fsdp else "ddp", amp=args.amp,
                    images_per_sec=summary["samples_per_sec_excl_first"] or summary["samples_per_sec"])

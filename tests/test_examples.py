@@ -98,3 +98,7 @@ def test_fsdp_resnet_on_cifar_binary_files(tmp_path):
                                                            "--steps-per-epoch", "3", "--test-steps", "2",
                                                            "--data-dir", str(d)], tmp_path)
     assert out["example"] == "fsdp_resnet" and out["test"]["samples"] == 8   # the 8 test images, 4 per rank
+    # the ResNet benchmark driver (scripts/main.py parity) on the same files: full epochs of 40 / 2 / 4 = 5 steps
+    out = _run("resnet_benchmark.py", 2, ["--arch", "resnet18", "--batch-size", "4", "--epochs", "1", "--eval-steps",
+                                          "1", "--data-dir", str(d)], tmp_path)
+    assert out["example"] == "resnet_benchmark" and out["eval"]["samples"] == 8
