@@ -1,4 +1,5 @@
 """Single-process checks of the data-parallel engine's fast paths against stock PyTorch."""
+import pytest
 import torch
 from torch import nn
 
@@ -80,3 +81,42 @@ def test_channels_last_weights_stay_channels_last_in_flat_buckets():
             e.step()
     for a, b in zip(ref.parameters(), cl.parameters()):
         assert torch.allclose(a, b, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["adamw", "sgd"])
+def test_overlapped_optimizer_step_matches_inline(dph_native, name):
+    """The optimizer update on a side stream (waited for per module by the next forward) gives bit-identical
+    parameters to the update on the compute stream, step after step, including a parameter the forward never uses
+    (its bucket is only covered by the root-forward join) and with gradient clipping."""
+    from distributed_pytorch_hpc_amd.models.llama2 import build_llama
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig
+
+    def run(overlap):
+        m = build_llama("tiny", device="cuda", seed=3)
+        m.unused = torch.nn.Parameter(torch.randn(64, device="cuda", dtype=torch.bfloat16))
+        eng = DataParallelEngine(m, bucket_cap_mb=0.05, overlap_step=overlap)   # explicit: the default is off
+        eng.configure_optimizer(OptimConfig(name, lr=1e-3, momentum=0.9, weight_decay=0.1,
+                                            max_grad_norm=1.0 if name == "adamw" else None))
+        g = torch.Generator(device="cuda").manual_seed(0)
+        losses = []
+        for _ in range(5):
+            t = torch.randint(0, 512, (2, 129), device="cuda", generator=g)
+            loss = m(t[:, :-1], t[:, 1:])
+            loss.backward()
+            eng.step()
+            eng.zero_grad()
+            # unrelated work on the compute stream between steps must not see stale parameters
+            junk = torch.full((1 << 22,), float("nan"), device="cuda")
+            del junk
+            losses.append(loss.detach())
+        eng.synchronize()
+        torch.cuda.synchronize()
+        assert (eng._opt_stream is not None) == overlap
+        return [p.detach().clone() for p in m.parameters()], torch.stack(losses)
+
+    pa, la = run(True)
+    pb, lb = run(False)
+    assert torch.equal(la, lb)
+    for a, b in zip(pa, pb):
+        assert torch.equal(a, b)
