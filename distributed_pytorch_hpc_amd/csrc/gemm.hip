@@ -61,7 +61,11 @@ __device__ __forceinline__ void wait_vm() { wait_vmcnt<N>(); }
 template <typename OutT, bool ACCUM>
 __global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                      OutT* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                     int64_t ldb, int64_t ldc) {
+                                                     int64_t ldb, int64_t ldc, int64_t cstride) {
+  // split-K (gridDim.y > 1): slice blockIdx.y reduces rows [y*K, (y+1)*K) of A / B into its own C slab
+  A += (int64_t)blockIdx.y * K * lda;
+  B += (int64_t)blockIdx.y * K * ldb;
+  C += (int64_t)blockIdx.y * cstride;
   __shared__ __attribute__((aligned(1024))) char lds[8 * 16384];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid >> 2, wn = wid & 3;                          // 2 x 4 waves
@@ -255,7 +259,11 @@ __device__ __forceinline__ bf16x4 tr1(const char* p) {
 template <typename OutT, bool ACCUM>
 __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                       OutT* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                      int64_t ldb, int64_t ldc) {
+                                                      int64_t ldb, int64_t ldc, int64_t cstride) {
+  // split-K (gridDim.y > 1): slice blockIdx.y reduces rows [y*K, (y+1)*K) of A / B into its own C slab
+  A += (int64_t)blockIdx.y * K * lda;
+  B += (int64_t)blockIdx.y * K * ldb;
+  C += (int64_t)blockIdx.y * cstride;
   __shared__ __attribute__((aligned(1024))) char lds[8 * 16384];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid >> 2, wn = wid & 3;                          // 2 x 4 waves
@@ -441,7 +449,40 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
     }
 }
 
+// fp32 split-K slabs W[S][Mb][Nb] -> C band (+ C when accumulating), in C's dtype.  Fixed summation order.
+template <typename OutT, bool ACCUM>
+__global__ __launch_bounds__(256) void gemm_split_reduce_k(const float* __restrict__ W, OutT* __restrict__ C, int Mb,
+                                                           int Nb, int64_t ldc, int S) {
+  const int64_t n4 = (int64_t)Mb * Nb / 4, slab = (int64_t)Mb * Nb;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < n4; v += (int64_t)gridDim.x * 256) {
+    const int64_t e = v * 4;
+    f32x4 acc = *reinterpret_cast<const f32x4*>(W + e);
+    for (int s = 1; s < S; ++s) acc += *reinterpret_cast<const f32x4*>(W + s * slab + e);
+    const int64_t r = e / Nb, c = e % Nb;
+    OutT* o = C + r * ldc + c;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float x = acc[j];
+      if (ACCUM) x += (float)o[j];
+      o[j] = (OutT)x;
+    }
+  }
+}
+
 int g_gemm_tn_mfma = 0;   // 0: not yet resolved from DPH_WGRAD_MFMA
+int g_gemm_tn_tail = 0;   // tail split: 0 = device CU count, > 0 = that many CUs (tests), < 0 = off
+
+int gemm_tn_cus() {
+  if (g_gemm_tn_tail > 0) return g_gemm_tn_tail;
+  static int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
 
 }  // namespace
 
@@ -455,33 +496,122 @@ int gemm_tn_mfma() {
 
 void gemm_tn_set_mfma(int shape) { g_gemm_tn_mfma = (shape == 16 || shape == 32) ? shape : 0; }
 
+void gemm_tn_set_tail(int cus) { g_gemm_tn_tail = cus; }
+
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K) {
   return M > 0 && N > 0 && K > 0 && M % GBM == 0 && N % GBN == 0 && K % GBK == 0;
 }
 
+// Tail plan.  One 256 x 256 tile per workgroup and one workgroup per CU: T tiles run in ceil(T / CU) waves, and a
+// partial last wave (w13's 1376 tiles = 5.375 waves, w2's 688 = 2.69 on the Llama-2-7B wgrad shapes) idles part of
+// the chip for a whole wave.  The plan keeps a band of whole waves on the plain kernel and computes the remaining
+// row or column band with K split S ways into fp32 slabs (one launch, gridDim.y = S), reduced into C afterwards:
+// the band then costs ceil(band * S / CU) / S waves instead of ceil(band / CU).
+GemmTnPlan gemm_tn_plan(int64_t M, int64_t N, int64_t K) {
+  GemmTnPlan pl{};
+  static const bool env_off = [] {   // DPH_WGRAD_TAIL=0: no tail split (A/B runs)
+    const char* e = getenv("DPH_WGRAD_TAIL");
+    return e && atoi(e) == 0;
+  }();
+  if (g_gemm_tn_tail < 0 || (env_off && g_gemm_tn_tail == 0) || gemm_tn_mfma() != 32) return pl;
+  const int cus = gemm_tn_cus();
+  const int64_t tm = M / GBM, tn = N / GBN, T = tm * tn;
+  if (T % cus == 0) return pl;
+  const bool forced = g_gemm_tn_tail > 0;
+  const int64_t min_k = forced ? GBK : 16 * GBK;   // >= 16 K-steps per slice on real shapes
+  // cost in seconds: a wave of 256 x 256 x K tiles at ~1.3 PFLOP/s over 256 CUs (measured kernel rate), plus the
+  // fp32 slabs written and read back at ~5 TB/s; the tail wave as it is costs one wave
+  const double t_wave = (double)K * GBM * GBN * 2.0 / (1.3e15 / 256.0);
+  double best = t_wave;
+  for (int dim = 0; dim < 2; ++dim) {
+    const int64_t along = dim == 0 ? tm : tn, other = dim == 0 ? tn : tm;
+    // largest prefix of whole bands whose tiles fill whole waves
+    int64_t keep = along;
+    while (keep > 0 && (keep * other) % cus) --keep;
+    const int64_t band = (along - keep) * other;
+    if (band == 0) continue;
+    for (int S : {2, 3, 4, 6, 8}) {
+      if (K % (S * GBK) || K / S < min_k) continue;
+      const double slab_bytes = 2.0 * S * (double)band * GBM * GBN * 4.0;
+      const double cost = (double)((band * S + cus - 1) / cus) / S * t_wave + (forced ? 0.0 : slab_bytes / 5e12);
+      if (cost < best * (forced ? 0.999 : 0.95)) {
+        best = cost;
+        pl.split = S;
+        pl.dim = dim;
+        pl.keep = keep * (dim == 0 ? GBM : GBN);
+      }
+    }
+  }
+  if (pl.split) {
+    const int64_t bm = pl.dim == 0 ? M - pl.keep : M, bn = pl.dim == 0 ? N : N - pl.keep;
+    pl.workspace_floats = (int64_t)pl.split * bm * bn;
+  }
+  return pl;
+}
+
 void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-             int64_t ldc, int out_dtype, bool accumulate, hipStream_t st) {
-  const int nwg = (int)((M / GBM) * (N / GBN));
-  const size_t lds = 0;   // static: 8 x 16 KB regions
-  const dim3 grid(nwg), block(GNT);
+             int64_t ldc, int out_dtype, bool accumulate, hipStream_t st, const GemmTnPlan* plan,
+             float* workspace) {
   const bool m16 = gemm_tn_mfma() == 16;
+  const size_t lds = 0;   // static: 8 x 16 KB regions
+  const dim3 block(GNT);
+  auto launch = [&](const bf16* a, const bf16* b, void* c, int64_t m, int64_t n, int64_t k, int64_t ldc_, int S,
+                    bool f32_out, bool acc, int64_t cstride) {
+    const dim3 grid((unsigned)((m / GBM) * (n / GBN)), (unsigned)S);
 #define DPH_GEMM_LAUNCH(T, ACC)                                                                                \
   do {                                                                                                         \
     if (m16)                                                                                                   \
-      hipLaunchKernelGGL((gemm_tn16_k<T, ACC>), grid, block, lds, st, (const bf16*)A, (const bf16*)B, (T*)C,   \
-                         (int)M, (int)N, (int)K, lda, ldb, ldc);                                               \
+      hipLaunchKernelGGL((gemm_tn16_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,     \
+                         lda, ldb, ldc_, cstride);                                                             \
     else                                                                                                       \
-      hipLaunchKernelGGL((gemm_tn_k<T, ACC>), grid, block, lds, st, (const bf16*)A, (const bf16*)B, (T*)C,     \
-                         (int)M, (int)N, (int)K, lda, ldb, ldc);                                               \
+      hipLaunchKernelGGL((gemm_tn_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k, lda,  \
+                         ldb, ldc_, cstride);                                                                  \
   } while (0)
-  if (out_dtype == kBF16) {
-    if (accumulate) DPH_GEMM_LAUNCH(bf16, true);
-    else DPH_GEMM_LAUNCH(bf16, false);
-  } else {
-    if (accumulate) DPH_GEMM_LAUNCH(float, true);
-    else DPH_GEMM_LAUNCH(float, false);
-  }
+    if (!f32_out && out_dtype == kBF16) {
+      if (acc) DPH_GEMM_LAUNCH(bf16, true);
+      else DPH_GEMM_LAUNCH(bf16, false);
+    } else {
+      if (acc) DPH_GEMM_LAUNCH(float, true);
+      else DPH_GEMM_LAUNCH(float, false);
+    }
 #undef DPH_GEMM_LAUNCH
+  };
+  const bf16* a = (const bf16*)A;
+  const bf16* b = (const bf16*)B;
+  if (!plan || !plan->split || !workspace) {
+    launch(a, b, C, M, N, K, ldc, 1, false, accumulate, 0);
+    return;
+  }
+  const int64_t esz = out_dtype == kBF16 ? 2 : 4;
+  char* c = (char*)C;
+  int64_t bm = M, bn = N;
+  const bf16 *ba = a, *bb = b;
+  char* bc = c;
+  if (plan->dim == 0) {   // band = rows [keep, M) of C = columns [keep, M) of A
+    if (plan->keep) launch(a, b, C, plan->keep, N, K, ldc, 1, false, accumulate, 0);
+    bm = M - plan->keep;
+    ba = a + plan->keep;
+    bc = c + plan->keep * ldc * esz;
+  } else {                // band = columns [keep, N) of C = columns [keep, N) of B
+    if (plan->keep) launch(a, b, C, M, plan->keep, K, ldc, 1, false, accumulate, 0);
+    bn = N - plan->keep;
+    bb = b + plan->keep;
+    bc = c + plan->keep * esz;
+  }
+  const int S = plan->split;
+  launch(ba, bb, workspace, bm, bn, K / S, bn, S, true, false, bm * bn);
+  const dim3 rgrid(stream_grid(bm * bn / 4, 256));
+  if (out_dtype == kBF16) {
+    if (accumulate) hipLaunchKernelGGL((gemm_split_reduce_k<bf16, true>), rgrid, dim3(256), 0, st, workspace,
+                                       (bf16*)bc, (int)bm, (int)bn, ldc, S);
+    else hipLaunchKernelGGL((gemm_split_reduce_k<bf16, false>), rgrid, dim3(256), 0, st, workspace, (bf16*)bc,
+                            (int)bm, (int)bn, ldc, S);
+  } else {
+    if (accumulate) hipLaunchKernelGGL((gemm_split_reduce_k<float, true>), rgrid, dim3(256), 0, st, workspace,
+                                       (float*)bc, (int)bm, (int)bn, ldc, S);
+    else hipLaunchKernelGGL((gemm_split_reduce_k<float, false>), rgrid, dim3(256), 0, st, workspace, (float*)bc,
+                            (int)bm, (int)bn, ldc, S);
+  }
 }
 
 }  // namespace dph

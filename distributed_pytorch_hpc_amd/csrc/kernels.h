@@ -105,8 +105,18 @@ bool gemm_tn_supported(int64_t M, int64_t N, int64_t K);
 constexpr int kGemmTnDefaultMfma = 32;
 int gemm_tn_mfma();
 void gemm_tn_set_mfma(int shape);
+// Partial-last-wave plan (csrc/gemm.hip gemm_tn_plan): compute the tile band that would run as a partial wave with K
+// split `split` ways into fp32 slabs (workspace_floats floats), keeping rows (dim 0) / columns (dim 1) [0, keep) on
+// the plain kernel.  split == 0: one launch.  gemm_tn_set_tail(n): plan for n CUs (tests), 0 = device, < 0 = off.
+struct GemmTnPlan {
+  int split, dim;
+  int64_t keep, workspace_floats;
+};
+GemmTnPlan gemm_tn_plan(int64_t M, int64_t N, int64_t K);
+void gemm_tn_set_tail(int cus);
 void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-             int64_t ldc, int out_dtype, bool accumulate, hipStream_t stream);
+             int64_t ldc, int out_dtype, bool accumulate, hipStream_t stream, const GemmTnPlan* plan = nullptr,
+             float* workspace = nullptr);
 
 // 1x1 convolution on channels-last activations as tall-skinny GEMMs (csrc/conv1x1.hip).  bf16 operands.
 // ts_gemm_nt: C[M, N] = A[M, K] B[N, K]^T (N, K % 64 == 0).  ts_gemm_tn: C[N, K] (+)= A[M, N]^T B[M, K] through

@@ -420,8 +420,19 @@ void gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate) {
               ", ", K, ")");
   check_align16(A, "A");
   check_align16(B, "B");
+  const dph::GemmTnPlan plan = dph::gemm_tn_plan(M, N, K);
+  Tensor ws;
+  if (plan.split) ws = at::empty({plan.workspace_floats}, A.options().dtype(at::kFloat));
   dph::gemm_tn(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0), dt_code(C),
-               accumulate, cur_stream());
+               accumulate, cur_stream(), &plan, plan.split ? ws.data_ptr<float>() : nullptr);
+}
+
+// tail split of the wgrad GEMM: n > 0 plans for n CUs (tests), 0 = the device's CU count (default), < 0 = off
+void gemm_tn_tail_(int64_t cus) { dph::gemm_tn_set_tail((int)cus); }
+
+std::vector<int64_t> gemm_tn_plan_info(int64_t M, int64_t N, int64_t K) {
+  const auto pl = dph::gemm_tn_plan(M, N, K);
+  return {pl.split, pl.dim, pl.keep, pl.workspace_floats};
 }
 
 // ------------------------------------------------------------------------------------------------ 1x1 conv GEMMs
@@ -748,6 +759,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
+  m.def("gemm_tn_tail_(int cus) -> ()", &gemm_tn_tail_);                          // catch-all kernels
+  m.def("gemm_tn_plan_info(int M, int N, int K) -> int[]", &gemm_tn_plan_info);
   m.def("gemm_tn_mfma_(int shape) -> int", &gemm_tn_mfma_);   // no tensor argument: catch-all kernel
   m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0, Tensor? add=None) -> Tensor");
   m.def("ts_gemm_nt_stats(Tensor A, Tensor B) -> (Tensor, Tensor)");

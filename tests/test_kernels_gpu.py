@@ -269,20 +269,46 @@ def test_embedding(dph_native):
                          [(512, 256, 256, torch.float32, False), (1024, 512, 768, torch.bfloat16, False),
                           (2048, 768, 512, torch.bfloat16, True), (64, 256, 512, torch.float32, True),
                           (192, 256, 256, torch.float32, False), (128, 512, 256, torch.float32, True)])
-@pytest.mark.parametrize("mfma", [16, 32])
-def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate, mfma):
+@pytest.mark.parametrize("mfma,tail", [(16, 0), (32, 0), (32, 3), (32, 8)])
+def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate, mfma, tail):
     """C (+)= A^T B with token-major A [K, M], B [K, N] (weight gradient dW = dY^T X), both MFMA-shape kernels
-    (K = 64 / 128 / 192 exercise the one- and two-K-step tails of the pipeline)."""
+    (K = 64 / 128 / 192 exercise the one- and two-K-step tails of the pipeline).  tail > 0 plans the partial-last-
+    wave split for that many CUs, so the small shapes take the split-K band + fp32 slab reduction path."""
     torch.ops.dph.gemm_tn_mfma_(mfma)
+    torch.ops.dph.gemm_tn_tail_(tail)
     torch.manual_seed(0)
     a = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
     b = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
     c0 = torch.randn(M, N, device=DEV, dtype=out_dtype)
     c = c0.clone()
     try:
+        if tail == 8:
+            assert torch.ops.dph.gemm_tn_plan_info(M, N, K)[0] > 0 or K < 128
         torch.ops.dph.gemm_tn_(c, a, b, accumulate)
     finally:
         torch.ops.dph.gemm_tn_mfma_(0)   # back to the default / DPH_WGRAD_MFMA
+        torch.ops.dph.gemm_tn_tail_(0)
+    ref = a.float().t() @ b.float() + (c0.float() if accumulate else 0)
+    assert rel_err(c, ref) < (1e-5 if out_dtype == torch.float32 else 8e-3)
+
+
+@pytest.mark.parametrize("M,N,dim", [(1024, 512, 0), (512, 1024, 1)])
+@pytest.mark.parametrize("out_dtype,accumulate", [(torch.float32, False), (torch.bfloat16, True)])
+def test_gemm_tn_tail_band(dph_native, M, N, dim, out_dtype, accumulate):
+    """Whole waves on the plain kernel + the last row (dim 0) / column (dim 1) band split along K into fp32 slabs:
+    planned for 3 CUs, 8 tiles = 2 whole waves of 3 + a 2-tile band split 4 ways."""
+    torch.ops.dph.gemm_tn_tail_(3)
+    try:
+        split, d, keep, _ = torch.ops.dph.gemm_tn_plan_info(M, N, 1024)
+        assert (split, d, keep) == (4, dim, 768)
+        torch.manual_seed(4)
+        a = torch.randn(1024, M, device=DEV, dtype=torch.bfloat16)
+        b = torch.randn(1024, N, device=DEV, dtype=torch.bfloat16)
+        c0 = torch.randn(M, N, device=DEV, dtype=out_dtype)
+        c = c0.clone()
+        torch.ops.dph.gemm_tn_(c, a, b, accumulate)
+    finally:
+        torch.ops.dph.gemm_tn_tail_(0)
     ref = a.float().t() @ b.float() + (c0.float() if accumulate else 0)
     assert rel_err(c, ref) < (1e-5 if out_dtype == torch.float32 else 8e-3)
 
