@@ -224,6 +224,33 @@ struct KVTilePlan {
       glds_stage<NC, BN, NT>(img + TILE, vp, v_ss, k0, Sk);
     }
   }
+
+  // The same copy issued as inline-asm LDS-DMA (lds_dma16): invisible to hipcc's wait bookkeeping, which otherwise
+  // drains the in-flight prefetch (vmcnt(0)) before the first ds_read of the CURRENT tile's V image (it cannot prove
+  // the two images disjoint).  The caller retires it with wait_vmcnt<0>() + s_barrier before reading `img`.
+  // `lds_w` is this wave's byte address of the image pair (lds_addr(img + wave * 1 KiB)).
+  int prow[NS], pch[NS];
+  __device__ __forceinline__ void init_async() {
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+      const int L = threadIdx.x + NT * i, line = L >> 4, slot = L & 15;
+      const int F = (line << 4) + (slot ^ (((line & 3) << 2) | ((line >> 2) & 3)));
+      prow[i] = F / NC;
+      pch[i] = (F % NC) * 8;
+    }
+  }
+  __device__ __forceinline__ void stage_async(unsigned lds_w, const bf16* kp, const bf16* vp, int64_t k_ss,
+                                              int64_t v_ss, int k0, int Sk) const {
+    const int rmax = Sk - 1 - k0;   // ragged last tile: rows past the end re-read the last valid row
+    const bf16* kt = kp + (int64_t)k0 * k_ss;
+    const bf16* vt = vp + (int64_t)k0 * v_ss;
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+      lds_dma16(kt, (unsigned)(((int64_t)min(prow[i], rmax) * k_ss + pch[i]) * 2), lds_w + NT * i * 16);
+#pragma unroll
+    for (int i = 0; i < NS; ++i)
+      lds_dma16(vt, (unsigned)(((int64_t)min(prow[i], rmax) * v_ss + pch[i]) * 2), lds_w + TILE + NT * i * 16);
+  }
 };
 
 // Logical (x, y, z) of a workgroup launched on a 1-D grid of nx*ny*nz blocks.  The hardware deals block ids
@@ -290,6 +317,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
 
   Plan plan;
   plan.init(lane, p.k_ss);
+  plan.init_async();
+  const unsigned lds_w = lds_addr(smem + (threadIdx.x >> 6) * 64 * 16);
 
   f32x16 o[DT];
 #pragma unroll
@@ -302,18 +331,28 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
   const unsigned drk = DROP ? attn_row_key(p.drop_seed, (unsigned)(b * p.Hq + hq), (unsigned)myq) : 0u;
   const unsigned dthr = DROP ? attn_drop_thr(p.drop_p) : 0u;
 
-  if (ntiles > 0) plan.stage(smem, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
-  __syncthreads();
+  if (ntiles > 0) plan.stage_async(lds_w, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
 
   auto tile = [&](const char* Kl, const char* Vl, int k0, bool need_mask) {
     // ---- S^T = K Q^T for two 32-key sub-tiles ----
+    // all 2 x KS K fragments are read before the MFMA chains (counted lgkmcnt waits): read one, wait, multiply
+    // exposed a full LDS round trip per MFMA
+    bf16x8 kf[2][KS];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) kf[sub][kk] = lds_b128(Kl, plan.row(sub, kk));
     f32x16 s[2];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      s[sub] = mfma32(lds_b128(Kl, plan.row(sub, 0)), qf[0], zacc);
+      s[sub] = mfma32(kf[sub][0], qf[0], zacc);
 #pragma unroll
-      for (int kk = 1; kk < KS; ++kk) s[sub] = mfma32(lds_b128(Kl, plan.row(sub, kk)), qf[kk], s[sub]);
+      for (int kk = 1; kk < KS; ++kk) s[sub] = mfma32(kf[sub][kk], qf[kk], s[sub]);
     }
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * KS, 0);   // the DS reads first ...
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);   // ... then the MFMAs
     // phase fences keep the scheduler from hoisting the next phase's LDS reads into this one's live range
     __builtin_amdgcn_sched_barrier(0);
     if (need_mask) {  // wave-uniform: only diagonal / ragged tiles pay for the selects
@@ -376,13 +415,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
 
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
-    if (t + 1 < ntiles) plan.stage(smem + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
+    if (t + 1 < ntiles)
+      plan.stage_async(lds_w + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
     const char* Kl = smem + buf * 2 * TILE;
     if (t < wtiles) {
       const int k0 = t * BN;
       tile(Kl, Kl + TILE, k0, (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0w + off)));
     }
-    __syncthreads();
+    wait_vmcnt<0>();   // this wave's share of tile t+1 has landed ...
+    __builtin_amdgcn_s_barrier();   // ... and every wave's, and nobody reads tile t's images any more
   }
 
   // ---- epilogue: O = O^T / l, lse ----
@@ -662,6 +703,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
 
   Plan plan;
   plan.init(lane, p.k_ss);
+  plan.init_async();
+  const unsigned lds_w = lds_addr(smem + (threadIdx.x >> 6) * 64 * 16);
 
   f32x16 dq[DT];
 #pragma unroll
@@ -670,19 +713,33 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
     for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
   const f32x16 zacc = {};
 
-  if (ntiles > 0) plan.stage(smem, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
-  __syncthreads();
+  if (ntiles > 0) plan.stage_async(lds_w, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
 
   auto tile = [&](const char* Kl, const char* Vl, int k0, bool need_mask) {
     bf16x8 sf[4];
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
-      f32x16 s = mfma32(lds_b128(Kl, plan.row(sub, 0)), qf[0], zacc);
-      f32x16 dp = mfma32(lds_b128(Vl, plan.row(sub, 0)), df[0], zacc);
+      // K and V fragments are read a half sub-tile (KH k-steps) ahead of their MFMAs with counted lgkmcnt waits
+      // (one read + wait + multiply at a time exposed an LDS round trip per MFMA; all KS at once spills)
+      constexpr int KH = KS / 2;
+      f32x16 s = zacc, dp = zacc;
 #pragma unroll
-      for (int kk = 1; kk < KS; ++kk) {
-        s = mfma32(lds_b128(Kl, plan.row(sub, kk)), qf[kk], s);
-        dp = mfma32(lds_b128(Vl, plan.row(sub, kk)), df[kk], dp);
+      for (int half = 0; half < 2; ++half) {
+        bf16x8 kf[KH], vf[KH];
+#pragma unroll
+        for (int j = 0; j < KH; ++j) {
+          kf[j] = lds_b128(Kl, plan.row(sub, half * KH + j));
+          vf[j] = lds_b128(Vl, plan.row(sub, half * KH + j));
+        }
+#pragma unroll
+        for (int j = 0; j < KH; ++j) {
+          s = mfma32(kf[j], qf[half * KH + j], s);
+          dp = mfma32(vf[j], df[half * KH + j], dp);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * KH, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * KH, 0);
       }
       if (need_mask) {  // wave-uniform; masked scores -> -inf -> p = 0
 #pragma unroll
@@ -717,13 +774,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
 
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
-    if (t + 1 < ntiles) plan.stage(smem + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
+    if (t + 1 < ntiles)
+      plan.stage_async(lds_w + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
     const char* Kl = smem + buf * 2 * TILE;
     if (t < wtiles) {
       const int k0 = t * BN;
       tile(Kl, Kl + TILE, k0, (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0w + off)));
     }
-    __syncthreads();
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
   }
 
   if (myq < p.Sq) {
