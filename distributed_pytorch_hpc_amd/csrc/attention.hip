@@ -253,6 +253,33 @@ struct KVTilePlan {
   }
 };
 
+// glds_stage issued through lds_dma16 (see KVTilePlan::stage_async) with the per-lane swizzled source row/chunk
+// hoisted out of the tile loop: ROWS x NC chunks of rows [row0, row0 + ROWS) of a strided tile, rows past `nvalid`
+// re-reading the last valid one.  `lds_w` = lds_addr(img + wave * 1 KiB).
+template <int NC, int ROWS, int NT>
+struct RowStagePlan {
+  static constexpr int CHUNKS = ROWS * NC, NI = (CHUNKS + NT - 1) / NT;
+  int prow[NI], pch[NI];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int L = threadIdx.x + NT * i, line = L >> 4, slot = L & 15;
+      const int F = (line << 4) + (slot ^ (((line & 3) << 2) | ((line >> 2) & 3)));
+      prow[i] = F / NC;
+      pch[i] = (F % NC) * 8;
+    }
+  }
+  __device__ __forceinline__ void stage(unsigned lds_w, const bf16* base, int64_t rstride, int row0,
+                                        int nvalid) const {
+    const int rmax = nvalid - 1 - row0;
+    const bf16* t = base + (int64_t)row0 * rstride;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      if (CHUNKS % NT == 0 || (int)threadIdx.x + NT * i < CHUNKS)
+        lds_dma16(t, (unsigned)(((int64_t)min(prow[i], rmax) * rstride + pch[i]) * 2), lds_w + NT * i * 16);
+  }
+};
+
 // Logical (x, y, z) of a workgroup launched on a 1-D grid of nx*ny*nz blocks.  The hardware deals block ids
 // round-robin over the 8 XCDs (ids congruent mod 8 share one L2), so XCD k is given the contiguous logical range
 // [k*n/8, (k+1)*n/8) with x fastest: the workgroups of one (batch, head) -- which all stream the same K/V (or
@@ -550,6 +577,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
   const int nqt_head = qstart < p.Sq ? (p.Sq - qstart + BMQ - 1) / BMQ : 0;
   const int total = nqt_head * grp;
 
+  // Q / dO tiles are prefetched by inline-asm LDS-DMA (RowStagePlan), retired by the explicit wait_vmcnt<0>() ahead
+  // of the end-of-tile barrier: with the compiler-visible builtin, hipcc drained the whole prefetch (vmcnt(0))
+  // before the transposed reads of the CURRENT tile.  The lse / delta row scalars are loaded raw and only scaled
+  // when written to LDS at the end of the tile, so their loads are not waited for (and, vmcnt retiring in order,
+  // the DMA behind them with it) at the top of the tile either.
+  RowStagePlan<NC, BMQ, NT> qplan;
+  qplan.init();
+  const unsigned lds_q = lds_addr(Qbuf + wid * 64 * 16);
   float st_lse = 0.f, st_del = 0.f;
   unsigned st_rk = 0u;
   const unsigned dthr = DROP ? attn_drop_thr(p.drop_p) : 0u;
@@ -559,20 +594,20 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
     const int qt0 = qstart + (it % nqt_head) * BMQ;
     const bf16* qp = (const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
     const bf16* dop = (const bf16*)P.dout + (int64_t)b * P.do_sb + (int64_t)hq * P.do_sh;
-    char* Ql = Qbuf + buf * 2 * QIMG;
-    glds_stage<NC, BMQ, NT>(Ql, qp, p.q_ss, qt0, p.Sq);
-    glds_stage<NC, BMQ, NT>(Ql + QIMG, dop, P.do_ss, qt0, p.Sq);
+    const unsigned ql = lds_q + buf * 2 * QIMG;
+    qplan.stage(ql, qp, p.q_ss, qt0, p.Sq);
+    qplan.stage(ql + QIMG, dop, P.do_ss, qt0, p.Sq);
     if (threadIdx.x < BMQ) {
-      const int q = qt0 + threadIdx.x;
+      const int q = min(qt0 + (int)threadIdx.x, p.Sq - 1);   // rows past Sq: finite, masked by the caller
       const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + q;
-      st_lse = q < p.Sq ? -p.lse[idx] * 1.4426950408889634f : 0.f;  // -lse in log2 units
-      st_del = q < p.Sq ? P.delta[idx] : 0.f;
-      if constexpr (DROP) st_rk = attn_row_key(p.drop_seed, (unsigned)(b * p.Hq + hq), (unsigned)q);
+      st_lse = p.lse[idx];
+      st_del = P.delta[idx];
+      if constexpr (DROP) st_rk = attn_row_key(p.drop_seed, (unsigned)(b * p.Hq + hq), (unsigned)(qt0 + threadIdx.x));
     }
   };
   auto stage_scalars = [&](int buf) {
     if (threadIdx.x < BMQ) {
-      lse_s[buf * BMQ + threadIdx.x] = st_lse;
+      lse_s[buf * BMQ + threadIdx.x] = -st_lse * 1.4426950408889634f;  // -lse in log2 units
       del_s[buf * BMQ + threadIdx.x] = st_del;
       if constexpr (DROP) rk_s[buf * BMQ + threadIdx.x] = st_rk;
     }
@@ -582,6 +617,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
     stage(0, 0);
     stage_scalars(0);
   }
+  wait_vmcnt<0>();
   __syncthreads();
 
   for (int it = 0; it < total; ++it) {
@@ -641,6 +677,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
         }
     }
     if (it + 1 < total) stage_scalars(buf ^ 1);
+    wait_vmcnt<0>();
     __syncthreads();
   }
 
