@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""A/B of the wgrad GEMM's MFMA shape (csrc/gemm.hip: gemm_tn_k on 32x32x16 vs gemm_tn16_k on 16x16x32) on the
-Llama-2-7B weight-gradient shapes, random operands, one process, interleaved arms (cdna_hip_programming.md rule 24).
-Also checks both against an fp32 reference.
+"""A/B of the wgrad GEMM variants (csrc/gemm.hip: 32 = gemm_tn_k, 8 waves of 128 x 64 on 32x32x16; 16 = gemm_tn16_k on
+16x16x32) on the Llama-2-7B weight-gradient shapes, random operands, one
+process, interleaved arms (cdna_hip_programming.md rule 24), plus hipBLASLt on the same product with K-contiguous
+operands (the layout the library runs fastest; its transposes are not counted) as the target.  Also checks every
+variant against an fp32 reference.
 
-    python benchmarks/gemm_mfma_ab.py [--tokens 32768] [--rounds 3] [--json out.json]
+    python benchmarks/gemm_mfma_ab.py [--variants 32,128] [--tokens 32768] [--rounds 3] [--json out.json]
 """
 import argparse
 import json
@@ -26,13 +28,16 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--variants", default="32,16")
+    ap.add_argument("--shapes", default=",".join(SHAPES))
     a = ap.parse_args()
+    variants = [int(v) for v in a.variants.split(",")]
     _lib.require()
     ops = torch.ops.dph
     K = a.tokens
     res = {}
     # numerics first (small K)
-    for shape in (16, 32):
+    for shape in variants:
         ops.gemm_tn_mfma_(shape)
         for acc in (False, True):
             ga = torch.randn(1024, 512, device="cuda", dtype=torch.bfloat16)
@@ -44,14 +49,25 @@ def main():
             err = ((c - ref).norm() / ref.norm()).item()
             res[f"relerr_mfma{shape}_acc{int(acc)}"] = err
             assert err < 1e-5, (shape, acc, err)
-    for name, (M, N) in SHAPES.items():
+    for name in a.shapes.split(","):
+        M, N = SHAPES[name]
         g = torch.randn(K, M, device="cuda", dtype=torch.bfloat16)
         x = torch.randn(K, N, device="cuda", dtype=torch.bfloat16)
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         flop = 2.0 * K * M * N
-        times = {16: [], 32: []}
+        times = {v: [] for v in variants}
+        gt, xt = g.t().contiguous(), x.t().contiguous()
+        times["blaslt_kcontig"] = []
         for _ in range(a.rounds):
-            for shape in (32, 16):
+            torch.mm(gt, xt.t(), out=c)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.iters):
+                torch.mm(gt, xt.t(), out=c)
+            e.record()
+            e.synchronize()
+            times["blaslt_kcontig"].append(s.elapsed_time(e) / a.iters)
+            for shape in variants:
                 ops.gemm_tn_mfma_(shape)
                 ops.gemm_tn_(c, g, x, False)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -62,17 +78,19 @@ def main():
                 e.synchronize()
                 times[shape].append(s.elapsed_time(e) / a.iters)
         ref = None
-        for shape in (32, 16):
+        for shape in variants:
             ops.gemm_tn_mfma_(shape)
             ops.gemm_tn_(c, g, x, False)
             if ref is None:
                 ref = c.float().clone()
             else:
-                res[f"{name}_max_diff_16_vs_32"] = (c.float() - ref).abs().max().item()
+                res[f"{name}_max_diff_{shape}_vs_{variants[0]}"] = (c.float() - ref).abs().max().item()
+        del gt, xt
         row = {f"tflops_mfma{s}": flop / (min(t) * 1e-3) / 1e12 for s, t in times.items()}
         row.update({f"ms_mfma{s}": min(t) for s, t in times.items()})
         res[name] = row
         print(name, json.dumps(row), flush=True)
+    ops.gemm_tn_mfma_(0)
     print(json.dumps(res))
     if a.json:
         with open(a.json, "w") as fh:
