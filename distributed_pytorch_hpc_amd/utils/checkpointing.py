@@ -229,7 +229,12 @@ class ShardedCheckpointer:
         _barrier()
         dp_rank = dist.get_rank(self.dp_group) if (dist.is_initialized() and self.dp_group is not None) else \
             (_rank() if self.engine is not None and self.engine.world > 1 else 0)
-        state = {"step": int(step), "rng": rng_state(), "extra": extra or {}}
+        # the global rank whose file holds this rank's model-parallel slice: dp-rank 0 of this rank's dp group
+        if dist.is_initialized() and self.dp_group is not None:
+            model_src = dist.get_global_rank(self.dp_group, 0)
+        else:
+            model_src = 0 if (self.engine is not None and self.engine.world > 1) else rank
+        state = {"step": int(step), "rng": rng_state(), "extra": extra or {}, "model_src": int(model_src)}
         # model shard: data-parallel replicas are identical -> only dp-rank 0 of each model-parallel slice writes
         if self._full_shard():
             # FULL_SHARD: the module's parameters are released between uses; gather the full state (collective)
@@ -248,6 +253,8 @@ class ShardedCheckpointer:
         if rank == 0:
             meta = {"step": step, "world_size": dist.get_world_size() if dist.is_initialized() else 1,
                     "dp_world": self.engine.world if self.engine is not None else 1}
+            if self.engine is None:   # without an engine or a dp group every rank holds its own (model-parallel) part
+                meta["dp_world"] = dist.get_world_size(self.dp_group) if self.dp_group is not None else 1
             with open(os.path.join(d, "meta.json"), "w") as fh:
                 json.dump(meta, fh)
             self._gc()
@@ -273,11 +280,18 @@ class ShardedCheckpointer:
         rank = _rank()
         world = dist.get_world_size() if dist.is_initialized() else 1
         same_world = meta["world_size"] == world
+        if not same_world and meta["world_size"] != meta.get("dp_world", meta["world_size"]):
+            raise ValueError(f"{path}: saved with model parallelism ({meta['world_size']} ranks, data-parallel "
+                             f"{meta['dp_world']}); resuming at another world size ({world}) is only supported for "
+                             f"pure data parallelism -- use save_checkpoint / load_checkpoint to change the layout")
         mine = os.path.join(path, f"rank{rank}.pt")
         state = torch.load(mine, map_location="cpu", weights_only=True) if (same_world and os.path.exists(mine)) else {}
         model_sd = state.get("model")
-        if model_sd is None:   # a dp replica that did not write the model: read rank 0 of the same slice (rank 0)
-            model_sd = torch.load(os.path.join(path, "rank0.pt"), map_location="cpu", weights_only=True)["model"]
+        if model_sd is None:
+            # a data-parallel replica that did not write the model: its slice's file (dp-rank 0 of its dp group);
+            # pure data parallelism at another world size: rank 0 holds the whole model
+            src = int(state.get("model_src", 0))
+            model_sd = torch.load(os.path.join(path, f"rank{src}.pt"), map_location="cpu", weights_only=True)["model"]
         if self.engine is not None:
             self.engine.load_full_state_dict(model_sd)
         else:

@@ -91,6 +91,47 @@ def test_sharded_resume_same_world(tmp_path):
         assert torch.allclose(ref[k], got[k], atol=1e-6), k
 
 
+def _slices_save_load(rank, world, root):
+    """World 4 = 2 model-parallel slices (ranks {0,1} and {2,3}, a different model each, as TP shards would be) x
+    dp 2.  Only dp-rank 0 of a slice writes its model; every rank must get ITS slice back."""
+    from distributed_pytorch_hpc_amd.models.llama2 import ModelArgs, build_llama
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig
+    from distributed_pytorch_hpc_amd.utils.checkpointing import ShardedCheckpointer
+
+    groups = [dist.new_group([0, 1]), dist.new_group([2, 3])]
+    sl = rank // 2
+    dpg = groups[sl]
+
+    def setup(seed):
+        m = build_llama(ModelArgs(**PRESET), device="cpu", dtype=torch.float32, seed=seed)
+        # parameters come back through the restored fp32 masters either way; a buffer only through the model file
+        m.register_buffer("slice_tag", torch.full((4,), float(seed)))
+        eng = DataParallelEngine(m, process_group=dpg, shard=True, bucket_cap_mb=0.02)
+        eng.configure_optimizer(OptimConfig(lr=1e-2))
+        return m, eng
+
+    m, eng = setup(100 + sl)
+    g = torch.Generator().manual_seed(20 + sl)
+    for _ in range(2):
+        t = torch.randint(0, 128, (4, 17), generator=g).chunk(2, 0)[dist.get_rank(dpg)]
+        m(t[:, :-1], t[:, 1:]).backward()
+        eng.step()
+        eng.zero_grad()
+    eng.synchronize()
+    saved = {k: v.clone() for k, v in m.state_dict().items()}
+    ShardedCheckpointer(root, m, eng).save(2)
+    m2, eng2 = setup(999)
+    assert ShardedCheckpointer(root, m2, eng2).load() == 2
+    for k, v in m2.state_dict().items():
+        assert torch.equal(v, saved[k]), (rank, k)
+    assert torch.equal(eng2.master, eng.master) and eng2.step_count == 2
+    return sl
+
+
+def test_sharded_model_parallel_slices_resume(tmp_path):
+    assert run_distributed(_slices_save_load, 4, str(tmp_path)) == [0, 0, 1, 1]
+
+
 def test_sharded_resume_reshard_to_one_rank(tmp_path):
     # save at dp=2 (sharded optimizer), resume on a single rank
     run_distributed(_save_then_resume, 2, str(tmp_path), True)
