@@ -239,9 +239,8 @@ class ZeRO3Engine:
             self._start_gather(self.units[u.idx + 1])
 
     def _post_forward(self, u, module, args, out):
-        if self.reshard and u is not self.units[-1] and torch.is_grad_enabled():
-            self._release(u)
-        elif self.reshard and u is not self.units[-1]:
+        # reshard after forward (the backward pre-hook gathers again); the root unit stays resident
+        if self.reshard and u is not self.units[-1]:
             self._release(u)
 
     def _pre_backward(self, u, module, grad_out):
@@ -513,7 +512,14 @@ class FullyShardedDataParallel(nn.Module):
         return self.full_state_dict(rank0_only=False, offload_to_cpu=True)
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
-        """Full (unsharded) state as returned by ``state_dict``; every rank passes the same one."""
+        """Full (unsharded) state as returned by ``state_dict``; every rank passes the same one.  Missing parameters
+        always raise; with ``strict`` keys the module does not have raise too."""
+        if strict:
+            known = set(self.module.state_dict().keys()) if not isinstance(self.engine, ZeRO3Engine) else \
+                {n for n, _ in self.module.named_parameters()} | {n for n, _ in self.module.named_buffers()}
+            extra = sorted(set(state_dict) - known)
+            if extra:
+                raise KeyError(f"load_state_dict: unexpected keys {extra[:4]}")
         self.engine.load_full_state_dict(state_dict)
 
     def full_state_dict(self, rank0_only: bool = True, offload_to_cpu: bool = True) -> dict:
