@@ -215,6 +215,19 @@ def test_flash_attention(dph_native, B, Sq, Sk, Hq, Hkv, D, causal):
     assert rel_err(v.grad, vr.grad) < 3e-2
 
 
+def test_flash_attention_eight_wave_variant(dph_native):
+    """The opt-in 8-wave workgroups (DPH_ATTN_WAVES=8, read once per process) in a child process."""
+    import os
+    import subprocess
+    import sys
+
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "attn_check.py")
+    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_ATTN_WAVES="8"), capture_output=True,
+                       text=True, timeout=100)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    assert '"ok": true' in p.stdout
+
+
 def test_flash_attention_padded_head_dim(dph_native):
     torch.manual_seed(10)
     q, k, v = (torch.randn(2, 64, 4, 16, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
