@@ -54,3 +54,14 @@ def test_send_recv_smoke_gloo(tmp_path):
                                                   "--json", str(tmp_path / "s.json")], str(tmp_path))
     res = json.loads((tmp_path / "s.json").read_text())
     assert res["smoke"] == "ok" and res["world"] == 3 and res["fanout_s"] > 0
+
+
+def test_torch_baseline_comparator_gloo(tmp_path):
+    """The stock-PyTorch comparator (torch DDP over gloo, ATen ops, torch AdamW) on a tiny Llama."""
+    out = _torchrun("benchmarks/torch_baseline.py", 2, ["--device", "cpu", "--model", "tiny", "--seq-len", "32",
+                                                        "--micro-batch", "2", "--steps", "2", "--warmup", "1",
+                                                        "--gpus", "2", "--json-out", str(tmp_path / "t.json")],
+                    str(tmp_path))
+    rec = json.loads((tmp_path / "t.json").read_text())
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "torch-ddp2" and rec["value"] > 0
+    assert sum(ln.startswith("{") for ln in out.splitlines()) == 1   # rank 0 only
