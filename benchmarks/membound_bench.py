@@ -28,6 +28,11 @@ def main():
     o = _lib.ops()
     T, D, F = 32768, 4096, 11008
     res = {}
+    big = torch.randn(T, 2 * F, device="cuda", dtype=torch.bfloat16)   # 1.44 GB: far beyond the Infinity Cache
+    res["copy_clone"] = 2 * big.numel() * 2 / timeit(lambda: big.clone()) / 1e6
+    dst = torch.empty_like(big)
+    res["copy_"] = 2 * big.numel() * 2 / timeit(lambda: dst.copy_(big)) / 1e6
+    del big, dst
     x = torch.randn(T, D, device="cuda", dtype=torch.bfloat16)
     r = torch.randn_like(x)
     w = torch.ones(D, device="cuda", dtype=torch.bfloat16)
