@@ -215,6 +215,23 @@ def test_flash_attention(dph_native, B, Sq, Sk, Hq, Hkv, D, causal):
     assert rel_err(v.grad, vr.grad) < 3e-2
 
 
+def test_flash_attention_long_sequence(dph_native):
+    """S = 16384 (the reference model allows max_seq_len 32768): tile / offset arithmetic at long lengths, causal GQA."""
+    torch.manual_seed(12)
+    B, S, Hq, Hkv, D = 1, 16384, 2, 1, 128
+    q = torch.randn(B, S, Hq, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = ops.flash_attention(q, k, v, causal=True)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = attn_mod.attention_reference(qr, kr, vr, True, 1.0 / math.sqrt(D))   # 2 GB of fp32 scores: fine here
+    orf.backward(do.float())
+    assert rel_err(o, orf) < 2e-2
+    assert rel_err(q.grad, qr.grad) < 3e-2 and rel_err(k.grad, kr.grad) < 3e-2 and rel_err(v.grad, vr.grad) < 3e-2
+
+
 def test_flash_attention_eight_wave_variant(dph_native):
     """The opt-in 8-wave workgroups (DPH_ATTN_WAVES=8, read once per process) in a child process."""
     import os
