@@ -19,6 +19,7 @@ import sqlite3
 from collections import defaultdict
 
 CATEGORIES = [
+    ("conv(miopen/ck)", re.compile(r"igemm_|grouped_conv|naive_conv|MIOpen|miopen|SubTensorOp", re.I)),
     ("gemm", re.compile(r"Cijk_|gemm|Gemm|hipblaslt|_MT\d+x\d+", re.I)),
     ("attn_fwd", re.compile(r"attn_fwd_k")),
     ("attn_bwd_dkdv", re.compile(r"attn_bwd_dkdv_k")),
@@ -31,13 +32,16 @@ CATEGORIES = [
     ("embedding", re.compile(r"embed")),
     ("optimizer", re.compile(r"adamw|sgd_k|sumsq")),
     ("rccl", re.compile(r"ncclDevKernel|rccl|nccl", re.I)),
+    ("batchnorm(dph)", re.compile(r"bn_(stats|apply|finalize|merge|bwd)")),
+    ("conv1x1(dph)", re.compile(r"ts_nt_k|ts_tn_k|ts_reduce|conv1x1")),
     ("copy/fill", re.compile(r"copy|fill|FillFunctor|direct_copy", re.I)),
     ("elementwise(aten)", re.compile(r"elementwise|vectorized|reduce_kernel", re.I)),
 ]
 
 
 def short_name(name: str) -> str:
-    n = name.split("(")[0]
+    # demangled names carry "(anonymous namespace)" before the argument list: drop it, then cut the arguments
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     if n.startswith("void "):
         n = n[5:]
     return n[:120]
