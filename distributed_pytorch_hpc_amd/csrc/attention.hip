@@ -280,14 +280,11 @@ struct RowStagePlan {
   }
 };
 
-// Logical (x, y, z) of a workgroup launched on a 1-D grid of nx*ny*nz blocks.  The hardware deals block ids
-// round-robin over the 8 XCDs (ids congruent mod 8 share one L2), so XCD k is given the contiguous logical range
-// [k*n/8, (k+1)*n/8) with x fastest: the workgroups of one (batch, head) -- which all stream the same K/V (or
-// Q/dO) -- run on one XCD and share its L2 instead of every XCD fetching every head (bijective for any n).
+// Logical (x, y, z) of a workgroup launched on a 1-D grid of nx*ny*nz blocks, XCD-aware (xcd_remap) with x fastest:
+// the workgroups of one (batch, head) -- which all stream the same K/V (or Q/dO) -- run on one XCD and share its L2
+// instead of every XCD fetching every head.
 __device__ __forceinline__ void xcd_block(int nx, int ny, int& x, int& y, int& z, int n) {
-  const int id = blockIdx.x, xcd = id & 7, slot = id >> 3;
-  const int base = n >> 3, rem = n & 7;
-  const int logical = xcd * base + min(xcd, rem) + slot;
+  const int logical = xcd_remap(blockIdx.x, n);
   x = logical % nx;
   y = (logical / nx) % ny;
   z = logical / (nx * ny);

@@ -35,12 +35,6 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-// bijective XCD-aware remap of a 1-D grid: blocks congruent mod 8 (one XCD) get a contiguous logical range
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
-
 constexpr int TS_BM = 128, TS_BK = 64, TS_NT = 256;
 constexpr int TS_BROW = 72;   // B slab row: 64 bf16 + 8 pad (144 B: 16 consecutive rows hit 16 distinct 16-B slots)
 constexpr int TS_KF = TS_BK / 16;   // MFMA k-steps (A fragments) per K-step

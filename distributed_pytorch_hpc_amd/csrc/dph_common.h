@@ -87,6 +87,14 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
+// Bijective XCD-aware remap of a 1-D grid of n workgroups.  The hardware deals block ids round-robin over the 8 XCDs
+// (ids congruent mod 8 share one L2), so XCD k is given the contiguous logical range [k*n/8, (k+1)*n/8): neighbouring
+// logical tiles -- which share operand panels / heads -- run on one XCD and share its L2.
+__device__ __forceinline__ int xcd_remap(int bid, int n) {
+  const int xcd = bid & 7;
+  return xcd * (n >> 3) + min(xcd, n & 7) + (bid >> 3);
+}
+
 // Wave-uniform LDS byte address of a __shared__ pointer (for lds_dma16's M0 operand).
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return __builtin_amdgcn_readfirstlane(

@@ -32,6 +32,16 @@ constexpr int ROWB = GBM * 2;              // bytes per LDS image row (256 bf16)
 constexpr int TILEB = GBK * ROWB;          // 32 KB per operand tile
 constexpr int GROUP_M = 8;
 
+// Tile (tm, tn) of logical workgroup lin: columns of GROUP_M-tall tile groups, m fastest, so the workgroups an XCD
+// runs together share GROUP_M A panels and a few B panels in its L2.
+__device__ __forceinline__ void grouped_tile(int lin, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int first_m = lin / (GROUP_M * tiles_n) * GROUP_M;
+  const int gsz = min(tiles_m - first_m, GROUP_M);
+  const int in_group = lin % (GROUP_M * tiles_n);
+  tm = first_m + in_group % gsz;
+  tn = in_group / gsz;
+}
+
 __device__ __forceinline__ bf16x8 tr2(const char* base, int off_lo, int off_hi) {
   i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_g*)(base + off_lo));
   i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_g*)(base + off_hi));
@@ -74,14 +84,8 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, 
 
   // ---- XCD-aware, grouped tile order ----
   const int tiles_m = M / GBM, tiles_n = N / GBN, nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int group = lin / (GROUP_M * tiles_n);
-  const int first_m = group * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (lin % (GROUP_M * tiles_n)) % gsz;
-  const int tn = (lin % (GROUP_M * tiles_n)) / gsz;
+  int tm, tn;
+  grouped_tile(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
 
   // ---- per-lane transposed-read offsets within a region (hi half = +8 rows = +4096 bytes) ----
@@ -271,14 +275,8 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
 
   // ---- XCD-aware, grouped tile order (as gemm_tn_k) ----
   const int tiles_m = M / GBM, tiles_n = N / GBN, nwg = tiles_m * tiles_n;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  const int group = lin / (GROUP_M * tiles_n);
-  const int first_m = group * GROUP_M;
-  const int gsz = min(tiles_m - first_m, GROUP_M);
-  const int tm = first_m + (lin % (GROUP_M * tiles_n)) % gsz;
-  const int tn = (lin % (GROUP_M * tiles_n)) / gsz;
+  int tm, tn;
+  grouped_tile(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
 
   // ---- per-lane transposed-read offsets within a region: row 4g + tq, chunk (logical) c -> slot c ^ f(row) ----
