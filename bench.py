@@ -53,6 +53,9 @@ def parse(argv=None):
                     help="process-group backend (default: nccl = RCCL on GPU); gloo lets several ranks share one GPU "
                          "to rehearse the N > 1 path (tests/test_bench_gpu.py)")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--fp8", action="store_true",
+                    help="opt-in FP8 GEMMs for the projections (ops/fp8.py; e4m3 activations/weights, e5m2 gradients, "
+                         "LM head bf16). Reported with dtype 'bf16+fp8-gemm' -- not the bf16 headline number")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: gloo + eager reference ops (tests of the N > 1 code path with tiny models only)")
     return ap.parse_args(argv)
@@ -100,6 +103,10 @@ def main(argv=None):
     mode = args.parallel
     if mode == "auto":
         mode = "fsdp" if world > 1 or args.force_dist else "ddp"
+    if args.fp8 and not cpu:
+        from distributed_pytorch_hpc_amd.ops import fp8 as fp8_mod
+
+        fp8_mod.enable_for_llama(model)
     engine = DataParallelEngine(
         model, shard=(mode == "fsdp"),
         mixed_precision=MixedPrecision(param_dtype=dtype,
@@ -162,7 +169,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32" if cpu else "bf16",
+            "dtype": "fp32" if cpu else ("bf16+fp8-gemm" if args.fp8 else "bf16"),
             "data": "synthetic (random tokens, random-init weights)",
             "config": {
                 "model": "Llama-2-7B" if args.model == "llama2-7b" else args.model,

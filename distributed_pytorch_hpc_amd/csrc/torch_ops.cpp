@@ -378,6 +378,30 @@ Tensor image_augment(const Tensor& images, const Tensor& idx, const c10::optiona
   return out;
 }
 
+// ------------------------------------------------------------------------------------------------ fp8
+// (y [R, C] or empty, yt [C, R] or empty, dequant fp32 scalar): per-tensor current scaling from max|x|.
+std::tuple<Tensor, Tensor, Tensor> fp8_quantize(const Tensor& x, int64_t fmt, bool rowmajor, bool transposed) {
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous(),
+              "fp8_quantize: contiguous bf16 [R, C]");
+  TORCH_CHECK(fmt == dph::kFP8E4M3 || fmt == dph::kFP8E5M2, "fp8_quantize: fmt 0 (e4m3) or 1 (e5m2)");
+  TORCH_CHECK(rowmajor || transposed, "fp8_quantize: nothing to write");
+  const int64_t R = x.size(0), C = x.size(1);
+  TORCH_CHECK(R % 64 == 0 && C % 64 == 0, "fp8_quantize: R and C must be multiples of 64");
+  TORCH_CHECK(x.data_ptr() == nullptr || reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "fp8_quantize: 16-B aligned input");
+  const auto f8 = fmt == dph::kFP8E4M3 ? at::kFloat8_e4m3fn : at::kFloat8_e5m2;
+  Tensor y = rowmajor ? at::empty({R, C}, x.options().dtype(f8)) : at::empty({0}, x.options().dtype(f8));
+  Tensor yt = transposed ? at::empty({C, R}, x.options().dtype(f8)) : at::empty({0}, x.options().dtype(f8));
+  Tensor amax = at::zeros({1}, x.options().dtype(at::kInt));
+  Tensor dq = at::empty({}, x.options().dtype(at::kFloat));
+  auto st = cur_stream();
+  dph::fp8_amax(x.data_ptr(), R * C, reinterpret_cast<unsigned*>(amax.data_ptr<int>()), st);
+  dph::fp8_quant(x.data_ptr(), R, C, reinterpret_cast<const unsigned*>(amax.data_ptr<int>()), (int)fmt,
+                 rowmajor ? y.data_ptr() : nullptr, transposed ? yt.data_ptr() : nullptr, dq.data_ptr<float>(), st);
+  return {y, yt, dq};
+}
+
 // ------------------------------------------------------------------------------------------------ embedding
 Tensor embedding_fwd(const Tensor& ids, const Tensor& table, int64_t vocab_start) {
   c10::DeviceGuard g(table.device());
@@ -756,6 +780,7 @@ TORCH_LIBRARY(dph, m) {
         "Tensor? rope_cos=None, Tensor? rope_sin=None, int rope_offset=0) -> ()");
   m.def("image_augment(Tensor images, Tensor idx, Tensor? params, Tensor mean, Tensor inv_std, int pad, "
         "bool channels_last, bool bf16_out) -> Tensor");
+  m.def("fp8_quantize(Tensor x, int fmt, bool rowmajor, bool transposed) -> (Tensor, Tensor, Tensor)");
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
@@ -803,6 +828,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("flash_attn_fwd", &flash_attn_fwd);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("flash_attn_bwd_into", &flash_attn_bwd_into);
+  m.impl("fp8_quantize", &fp8_quantize);
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("gemm_tn_", &gemm_tn_);

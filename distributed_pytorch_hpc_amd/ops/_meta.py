@@ -150,6 +150,15 @@ def _img_aug(images, idx, params, mean, inv_std, pad, channels_last, bf16_out):
     return out.contiguous(memory_format=torch.channels_last) if channels_last else out
 
 
+@register_fake("dph::fp8_quantize")
+def _fp8_quant(x, fmt, rowmajor, transposed):
+    f8 = torch.float8_e4m3fn if fmt == 0 else torch.float8_e5m2
+    r, c = x.shape
+    y = x.new_empty((r, c) if rowmajor else (0,), dtype=f8)
+    yt = x.new_empty((c, r) if transposed else (0,), dtype=f8)
+    return y, yt, x.new_empty((), dtype=torch.float32)
+
+
 @register_fake("dph::embedding_fwd")
 def _emb_fwd(ids, table, vocab_start):
     return table.new_empty((*ids.shape, table.shape[1]))

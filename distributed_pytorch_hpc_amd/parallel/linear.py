@@ -16,6 +16,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from ..ops import fp8 as _fp8
+
 # Opt-in (DPH_WGRAD_STREAM=1): weight-gradient GEMMs on a side stream (per device).  dW is off the backward's
 # critical path, so the CDNA4 wgrad kernel could overlap the next dgrad / attention-backward / norm kernels and
 # fill their tail waves.  The data-parallel engine orders its collectives after this stream and joins it at the
@@ -133,6 +135,24 @@ def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
     return gw
 
 
+def weight_grad_from(w: torch.Tensor, mm):
+    """dW for a GEMM given as ``mm(out)`` (writes into ``out`` when given, else returns a new bf16 tensor), routed like
+    ``weight_grad``: written straight into the engine's bucket view (first micro-batch, matching dtype) or added to
+    it, the engine notified and None returned; without an engine the gradient itself is returned (ops/fp8.py)."""
+    mg = getattr(w, "main_grad", None)
+    if mg is None:
+        return mm(None)
+    if not getattr(w, "_dph_accum", False) and mg.dtype == torch.bfloat16 and mg.is_contiguous():
+        mm(mg)
+    elif getattr(w, "_dph_accum", False):
+        mg.add_(mm(None))
+    else:
+        mg.copy_(mm(None))
+    w._dph_accum = True
+    w._dph_grad_ready()
+    return None
+
+
 def _autocast_dtype(t: torch.Tensor):
     dev = t.device.type
     return torch.get_autocast_dtype(dev) if torch.is_autocast_enabled(dev) else None
@@ -169,6 +189,8 @@ class _LinearFn(torch.autograd.Function):
 
 
 def linear(x, w, b=None):
+    if b is None and _fp8.fp8_enabled() and x.dim() >= 2 and _fp8.applicable(x.reshape(-1, x.shape[-1]), w):
+        return _fp8.fp8_linear(x, w)   # opt-in FP8 GEMMs (ops/fp8.py)
     if getattr(w, "main_grad", None) is not None and torch.is_grad_enabled() and w.requires_grad:
         return _LinearFn.apply(x, w, b)
     return F.linear(x, w, b)

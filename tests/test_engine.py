@@ -120,3 +120,32 @@ def test_overlapped_optimizer_step_matches_inline(dph_native, name):
     assert torch.equal(la, lb)
     for a, b in zip(pa, pb):
         assert torch.equal(a, b)
+
+
+def test_fp8_mode_falls_back_off_gpu():
+    """FP8 GEMM mode (ops/fp8.py) only engages on bf16 CUDA tensors: on CPU the step is the plain one, bit for bit."""
+    import torch
+
+    from distributed_pytorch_hpc_amd.models.llama2 import ModelArgs, build_llama
+    from distributed_pytorch_hpc_amd.ops import fp8
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig
+
+    args = ModelArgs(dim=64, n_layers=1, n_heads=4, vocab_size=128, max_seq_len=64, multiple_of=32)
+    t = torch.randint(0, 128, (2, 33), generator=torch.Generator().manual_seed(0))
+
+    def run(on):
+        m = build_llama(args, device="cpu", dtype=torch.float32, seed=2)
+        if on:
+            fp8.enable_for_llama(m)
+        eng = DataParallelEngine(m)
+        eng.configure_optimizer(OptimConfig(lr=1e-2))
+        try:
+            loss = m(t[:, :-1], t[:, 1:])
+            loss.backward()
+            eng.step()
+        finally:
+            fp8.set_fp8(False)
+        return loss.item(), [p.detach().clone() for p in m.parameters()]
+
+    (l0, p0), (l1, p1) = run(False), run(True)
+    assert l0 == l1 and all(torch.equal(a, b) for a, b in zip(p0, p1))
