@@ -169,14 +169,13 @@ void image_augment(const uint8_t* images, const int64_t* idx, const int* params,
                    const float* inv_std, void* out, int64_t B, int64_t H, int64_t W, int64_t C, int64_t pad,
                    bool nhwc, int out_dtype, hipStream_t stream);
 
-// Per-tensor FP8 quantisation (csrc/fp8.hip): OCP e4m3 / e5m2.  fp8_amax: atomicMax of max|x| (float bits) into
-// *amax_bits (zeroed by the caller) over n contiguous bf16 (n % 8 == 0).  fp8_quant: x [R, C] contiguous bf16,
-// R % 64 == C % 64 == 0 -> y [R, C] and / or yt [C, R] fp8 (null = not written) with scale FMAX / amax, and
-// *dequant = amax / FMAX.
+// Per-tensor FP8 quantisation (csrc/fp8.hip): OCP e4m3 / e5m2.  fp8_amax: max|x| over n contiguous bf16 (n % 8 == 0)
+// via fp8_amax_blocks(n) per-block partials -> scal[3] = [amax, FMAX / amax, amax / FMAX].  fp8_quant: x [R, C]
+// contiguous bf16, R % 64 == C % 64 == 0 -> y [R, C] and / or yt [C, R] fp8 (null = not written), scaled by scal[1].
 constexpr int kFP8E4M3 = 0, kFP8E5M2 = 1;
-void fp8_amax(const void* x, int64_t n, unsigned* amax_bits, hipStream_t stream);
-void fp8_quant(const void* x, int64_t R, int64_t C, const unsigned* amax_bits, int fmt, void* y, void* yt,
-               float* dequant, hipStream_t stream);
+int fp8_amax_blocks(int64_t n);
+void fp8_amax(const void* x, int64_t n, int fmt, float* partial, float* scal, hipStream_t stream);
+void fp8_quant(const void* x, int64_t R, int64_t C, const float* scal, int fmt, void* y, void* yt, hipStream_t stream);
 
 // Single-node all-reduce over IPC-mapped peer buffers (csrc/custom_allreduce.hip).  ctx is an opaque handle.
 int64_t car_create(int rank, int world, int64_t max_bytes, double timeout_s);

@@ -393,13 +393,14 @@ std::tuple<Tensor, Tensor, Tensor> fp8_quantize(const Tensor& x, int64_t fmt, bo
   const auto f8 = fmt == dph::kFP8E4M3 ? at::kFloat8_e4m3fn : at::kFloat8_e5m2;
   Tensor y = rowmajor ? at::empty({R, C}, x.options().dtype(f8)) : at::empty({0}, x.options().dtype(f8));
   Tensor yt = transposed ? at::empty({C, R}, x.options().dtype(f8)) : at::empty({0}, x.options().dtype(f8));
-  Tensor amax = at::zeros({1}, x.options().dtype(at::kInt));
-  Tensor dq = at::empty({}, x.options().dtype(at::kFloat));
+  // one small fp32 buffer: [amax, scale, dequant | per-block partials]; the dequant scale is returned as a view
+  Tensor buf = at::empty({3 + dph::fp8_amax_blocks(R * C)}, x.options().dtype(at::kFloat));
+  float* scal = buf.data_ptr<float>();
   auto st = cur_stream();
-  dph::fp8_amax(x.data_ptr(), R * C, reinterpret_cast<unsigned*>(amax.data_ptr<int>()), st);
-  dph::fp8_quant(x.data_ptr(), R, C, reinterpret_cast<const unsigned*>(amax.data_ptr<int>()), (int)fmt,
-                 rowmajor ? y.data_ptr() : nullptr, transposed ? yt.data_ptr() : nullptr, dq.data_ptr<float>(), st);
-  return {y, yt, dq};
+  dph::fp8_amax(x.data_ptr(), R * C, (int)fmt, scal + 3, scal, st);
+  dph::fp8_quant(x.data_ptr(), R, C, scal, (int)fmt, rowmajor ? y.data_ptr() : nullptr,
+                 transposed ? yt.data_ptr() : nullptr, st);
+  return {y, yt, buf.select(0, 2)};
 }
 
 // ------------------------------------------------------------------------------------------------ embedding

@@ -9,7 +9,7 @@ scaling; everything else (attention, norms, activations, optimizer, master weigh
 
 ``csrc/fp8.hip`` makes the quantised copies in two passes over the bf16 tensor (amax, then scale + convert, the
 row-major and the transposed copy from one read); the forward saves X^T in fp8 (1 byte per element) for the weight
-gradient instead of the bf16 X.  Scales follow the usual recipe: scale = FMAX / amax, dequantisation amax / FMAX.
+gradient instead of the bf16 X, and W^T in fp8 for the input gradient (the weight is quantised once per step).  Scales follow the usual recipe: scale = FMAX / amax, dequantisation amax / FMAX.
 
 Enable with ``DPH_FP8=1`` or ``set_fp8(True)``; exempt a layer with ``exempt(module)`` (``enable_for_llama`` exempts
 the LM head).  Shapes the quantiser does not tile (any dim not a multiple of 64) fall back to the bf16 path.
@@ -70,11 +70,13 @@ class _FP8LinearFn(torch.autograd.Function):
         k = x.shape[-1]
         x2 = x.reshape(-1, k).contiguous()
         xq, xqt, sx = quantize(x2, E4M3, rowmajor=True, transposed=w.requires_grad)
-        wq, _, sw = quantize(w, E4M3, rowmajor=True)
+        # both weight copies from one pass: W for this GEMM, W^T (kept for the input gradient) if x needs one
+        wq, wtq, sw = quantize(w, E4M3, rowmajor=True, transposed=x.requires_grad)
         # the output is allocated in its final shape (not returned as a view: callers rotate q / k in place)
         y = x2.new_empty(*x.shape[:-1], w.shape[0])
         torch._scaled_mm(xq, wq.t(), scale_a=sx, scale_b=sw, out_dtype=torch.bfloat16, out=y.view(-1, w.shape[0]))
-        ctx.save_for_backward(xqt if xqt is not None else x2.new_empty(0), sx, w)
+        empty = x2.new_empty(0)
+        ctx.save_for_backward(xqt if xqt is not None else empty, sx, w, wtq if wtq is not None else empty, sw)
         ctx.x_shape = x.shape
         return y
 
@@ -82,15 +84,14 @@ class _FP8LinearFn(torch.autograd.Function):
     def backward(ctx, gy):
         from ..parallel.linear import weight_grad_from
 
-        xqt, sx, w = ctx.saved_tensors
+        xqt, sx, w, wtq, sw = ctx.saved_tensors
         n = w.shape[0]
         g2 = gy.reshape(-1, n).contiguous()
         need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         gq, gqt, sg = quantize(g2, E5M2, rowmajor=need_x, transposed=need_w)
         gx = gw = None
         if need_x:
-            _, wtq, sw = quantize(w, E4M3, rowmajor=False, transposed=True)   # W^T [K, N]
-            gx = gq.new_empty(ctx.x_shape, dtype=torch.bfloat16)
+            gx = gq.new_empty(ctx.x_shape, dtype=torch.bfloat16)   # dX = dY (W^T)^T with W^T [K, N] from the forward
             torch._scaled_mm(gq, wtq.t(), scale_a=sg, scale_b=sw, out_dtype=torch.bfloat16,
                              out=gx.view(-1, ctx.x_shape[-1]))
         if need_w:
