@@ -13,20 +13,23 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_bench_two_ranks_share_one_gpu(tmp_path):
+@pytest.mark.parametrize("fp8", [False, True])
+def test_bench_two_ranks_share_one_gpu(tmp_path, fp8):
+    """fp8: the opt-in FP8-GEMM mode under the sharded engine (weight gradients written into ZeRO-2 buckets)."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--backend", "gloo", "--model", "tiny", "--seq-len", "128", "--micro-batch", "2",
-           "--steps", "2", "--warmup", "1", "--quiet"]
+           "--steps", "2", "--warmup", "1", "--quiet"] + (["--fp8"] if fp8 else [])
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=100, cwd=str(tmp_path),
                        env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
     assert p.returncode == 0, p.stderr[-3000:]
     recs = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(recs) == 1, p.stdout
     r = recs[0]
-    assert r["n_gpus"] == 2 and r["dtype"] == "bf16" and r["value"] > 0
+    assert r["n_gpus"] == 2 and r["dtype"] == ("bf16+fp8-gemm" if fp8 else "bf16") and r["value"] > 0
+    assert abs(r["loss_last"] - r["loss_first_warmup"]) < 2.0
     assert r["config"]["parallelism"] == "fsdp2" and r["config"]["global_batch"] == 4
     assert r["config"]["kernels"] == "dph"
