@@ -55,13 +55,15 @@ def quantize(x: torch.Tensor, fmt: int, rowmajor: bool = True, transposed: bool 
     return (y if rowmajor else None), (yt if transposed else None), s
 
 
-def applicable(x2: torch.Tensor, w: torch.Tensor) -> bool:
-    if not _enabled or getattr(w, "_dph_fp8_exempt", False) or not x2.is_cuda or _lib.reference_mode():
+def applicable(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """x [..., K] and w [N, K] take the FP8 path: enabled, not exempt, bf16 on the GPU, all GEMM dims multiples of 64."""
+    if not _enabled or getattr(w, "_dph_fp8_exempt", False) or not x.is_cuda or _lib.reference_mode():
         return False
-    if x2.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.dim() != 2 or not w.is_contiguous():
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or w.dim() != 2 or not w.is_contiguous():
         return False
-    t, k = x2.shape
-    return t % 64 == 0 and k % 64 == 0 and w.shape[0] % 64 == 0 and w.shape[1] == k
+    k = x.shape[-1]
+    t = x.numel() // max(k, 1)
+    return x.dim() >= 2 and t % 64 == 0 and k % 64 == 0 and w.shape[0] % 64 == 0 and w.shape[1] == k
 
 
 class _FP8LinearFn(torch.autograd.Function):

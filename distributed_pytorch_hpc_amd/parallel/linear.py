@@ -189,7 +189,7 @@ class _LinearFn(torch.autograd.Function):
 
 
 def linear(x, w, b=None):
-    if b is None and _fp8.fp8_enabled() and x.dim() >= 2 and _fp8.applicable(x.reshape(-1, x.shape[-1]), w):
+    if b is None and _fp8.fp8_enabled() and _fp8.applicable(x, w):
         return _fp8.fp8_linear(x, w)   # opt-in FP8 GEMMs (ops/fp8.py)
     if getattr(w, "main_grad", None) is not None and torch.is_grad_enabled() and w.requires_grad:
         return _LinearFn.apply(x, w, b)
