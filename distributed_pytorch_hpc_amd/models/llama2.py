@@ -194,6 +194,8 @@ class Transformer(nn.Module):
         self.layers = nn.ModuleList([TransformerBlock(i, args) for i in range(args.n_layers)])
         self.norm = ops.RMSNorm(args.dim, eps=args.norm_eps)
         self.output = nn.Linear(args.dim, args.vocab_size, bias=False)
+        # the LM head stays bf16 in FP8-GEMM mode (ops/fp8.py): its logits feed the loss directly
+        self.output.weight._dph_fp8_exempt = True
         self.init_weights()
 
     @classmethod

@@ -11,8 +11,8 @@ scaling; everything else (attention, norms, activations, optimizer, master weigh
 row-major and the transposed copy from one read); the forward saves X^T in fp8 (1 byte per element) for the weight
 gradient instead of the bf16 X, and W^T in fp8 for the input gradient (the weight is quantised once per step).  Scales follow the usual recipe: scale = FMAX / amax, dequantisation amax / FMAX.
 
-Enable with ``DPH_FP8=1`` or ``set_fp8(True)``; exempt a layer with ``exempt(module)`` (``enable_for_llama`` exempts
-the LM head).  Shapes the quantiser does not tile (any dim not a multiple of 64) fall back to the bf16 path.
+Enable with ``DPH_FP8=1``, ``set_fp8(True)`` or any example driver's ``--fp8`` (train/cli.py); exempt a layer with
+``exempt(module)`` (the Llama LM head is exempt by construction, and the marker survives tensor-parallel sharding).  Shapes the quantiser does not tile (any dim not a multiple of 64) fall back to the bf16 path.
 This mode is NOT the headline precision: ``bench.py`` reports it only with ``--fp8`` and labels the dtype.
 """
 from __future__ import annotations

@@ -69,6 +69,12 @@ def shard_rows_grouped(w: torch.Tensor, sizes: list[int], group) -> torch.Tensor
     return torch.cat([shard_rows(p, group) for p in parts], 0).contiguous()
 
 
+def _carry_flags(src: torch.Tensor, dst: torch.Tensor) -> None:
+    """Per-parameter markers survive sharding (e.g. ops/fp8.py's exemption of the LM head)."""
+    if getattr(src, "_dph_fp8_exempt", False):
+        dst._dph_fp8_exempt = True
+
+
 class ColwiseParallelLinear(nn.Module):
     def __init__(self, lin: nn.Linear, group, sequence_parallel: bool = False, gather_output: bool = False,
                  shard_fn: Optional[Callable] = None, seq_dim: int = 1):
@@ -77,6 +83,7 @@ class ColwiseParallelLinear(nn.Module):
         w = lin.weight.detach()
         self.weight = nn.Parameter(shard_fn(w, group) if shard_fn else shard_rows(w, group),
                                    requires_grad=lin.weight.requires_grad)
+        _carry_flags(lin.weight, self.weight)
         self.bias = None
         if lin.bias is not None:
             self.bias = nn.Parameter(shard_rows(lin.bias.detach()[:, None], group)[:, 0].contiguous())
@@ -102,6 +109,7 @@ class RowwiseParallelLinear(nn.Module):
         w = lin.weight.detach()
         self.weight = nn.Parameter(shard_fn(w, group) if shard_fn else shard_cols(w, group),
                                    requires_grad=lin.weight.requires_grad)
+        _carry_flags(lin.weight, self.weight)
         self.bias = nn.Parameter(lin.bias.detach().clone()) if lin.bias is not None else None
         self.in_features, self.out_features = self.weight.shape[1], lin.out_features
         self.async_chunks = 0   # > 0: GEMM pipelined against the sequence reduce-scatter (parallel/async_tp.py)

@@ -31,6 +31,9 @@ def common_parser(description: str) -> argparse.ArgumentParser:
     ap.add_argument("--cuda-graph", action="store_true",
                     help="replay each training step as one captured HIP graph after 3 eager warm-up steps "
                          "(runtime/graphs.py; single GPU, fixed shapes)")
+    ap.add_argument("--fp8", action="store_true",
+                    help="opt-in FP8 GEMMs for the linear projections (ops/fp8.py; e4m3 / e5m2, per-tensor scaling; "
+                         "GPU only, bf16 elsewhere); same as DPH_FP8=1")
     return ap
 
 
@@ -53,6 +56,10 @@ def start(args, verbose: bool = True):
     search = getattr(args, "conv_search", None)
     torch.backends.cudnn.benchmark = bool(search) if search is not None else dev == "cuda"
     backend = args.backend or ("nccl" if dev == "cuda" else "gloo")
+    if getattr(args, "fp8", False):
+        from ..ops import fp8
+
+        fp8.set_fp8(True)
     return setup_run(backend=backend, device=dev, seed=args.seed, verbose=verbose)
 
 

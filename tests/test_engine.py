@@ -149,3 +149,16 @@ def test_fp8_mode_falls_back_off_gpu():
 
     (l0, p0), (l1, p1) = run(False), run(True)
     assert l0 == l1 and all(torch.equal(a, b) for a, b in zip(p0, p1))
+
+
+def test_fp8_exemption_survives_tp_sharding():
+    """The LM head is FP8-exempt by construction, and the marker is carried onto its tensor-parallel shard."""
+    from distributed_pytorch_hpc_amd.models.llama2 import ModelArgs, Transformer
+    from distributed_pytorch_hpc_amd.parallel.tensor_parallel import ColwiseParallelLinear, RowwiseParallelLinear
+
+    m = Transformer(ModelArgs(dim=64, n_layers=1, n_heads=4, vocab_size=128, multiple_of=32, max_seq_len=16))
+    assert getattr(m.output.weight, "_dph_fp8_exempt", False)
+    assert not getattr(m.layers[0].attention.wqkv.weight, "_dph_fp8_exempt", False)
+    col = ColwiseParallelLinear(m.output, None)
+    row = RowwiseParallelLinear(m.output, None)
+    assert col.weight._dph_fp8_exempt and row.weight._dph_fp8_exempt
