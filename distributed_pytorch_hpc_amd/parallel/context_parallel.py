@@ -13,7 +13,8 @@ Ring (``RingAttention``): each rank keeps its query chunk; K/V chunks rotate aro
 batch_isend_irecv posted BEFORE the local block so the xGMI transfer overlaps the flash kernel).  Blocks are
 merged with the online-softmax rule on (o, lse) -- the flash forward kernel emits the log-sum-exp.  Backward
 re-runs the ring: per block the flash backward kernel, fed the FINAL (o, lse), yields exact dq/dk/dv
-contributions; dK/dV accumulators travel with their K/V chunk and arrive home after P hops.  With causal
+contributions; the next K/V hop is posted before the block's kernel (overlapped like the forward), and the dK/dV
+accumulators travel one hop behind their K/V chunk, arriving home after P hops.  With causal
 attention and contiguous chunks, block (q_r, kv_j) is full for j < r, causal for j == r, skipped for j > r --
 rank P-1 does P blocks of work while rank 0 does one.
 
@@ -200,6 +201,10 @@ class _RingAttnFn(torch.autograd.Function):
         dvc = torch.zeros_like(v, dtype=torch.float32)
         for i in range(p):
             j = (r - i) % p
+            # K/V for the next step need nothing from this one: post them before the block's backward kernel
+            kv_works = kv_next = None
+            if i < p - 1:
+                kv_works, kv_next = ring.start([kc, vc])
             if not causal or (not zigzag and j <= r) or (zigzag and j == r):
                 dq_i, dk_i, dv_i = _attn_bwd(do, q, kc, vc, o, lse, causal and j == r, scale)
                 dq += dq_i.float()
@@ -216,14 +221,13 @@ class _RingAttnFn(torch.autograd.Function):
                 dq[:, c:] += dq_i.float()
                 dkc += dk_i.float()
                 dvc += dv_i.float()
-            # move (K, V, dK-acc, dV-acc) one hop; after p hops every accumulator is home
-            if i < p - 1:
-                works, (kc, vc, dkc_n, dvc_n) = ring.start([kc, vc, dkc, dvc])
-            else:
-                works, (dkc_n, dvc_n) = ring.start([dkc, dvc])
-            for w in works:
+            # the dK / dV accumulators follow their chunk one hop; after p hops every accumulator is home
+            works, (dkc_n, dvc_n) = ring.start([dkc, dvc])
+            for w in (kv_works or []) + works:
                 w.wait()
             dkc, dvc = dkc_n, dvc_n
+            if kv_next is not None:
+                kc, vc = kv_next
         return dq.to(q.dtype), dkc.to(k.dtype), dvc.to(v.dtype), None, None, None, None
 
 
