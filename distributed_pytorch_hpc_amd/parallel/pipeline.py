@@ -148,9 +148,15 @@ class PipelineSchedule:
             x.requires_grad_(True)
         return x
 
+    def _split(self, t: torch.Tensor, what: str) -> list:
+        # every micro-batch must have micro-batch 0's shape: only that one carries a shape header (P2P.recv_forward)
+        if t.shape[0] % self.m:
+            raise ValueError(f"pipeline {what}: batch {t.shape[0]} is not divisible by n_microbatches={self.m}")
+        return list(t.chunk(self.m, 0))
+
     def step(self, inputs: Optional[torch.Tensor] = None, target: Optional[torch.Tensor] = None) -> list:
-        mbs = list(inputs.chunk(self.m, 0)) if self.is_first else [None] * self.m
-        tgts = list(target.chunk(self.m, 0)) if (self.is_last and target is not None) else [None] * self.m
+        mbs = self._split(inputs, "inputs") if self.is_first else [None] * self.m
+        tgts = self._split(target, "target") if (self.is_last and target is not None) else [None] * self.m
         if self.schedule == "gpipe":
             return self._gpipe(mbs, tgts)
         return self._1f1b(mbs, tgts)
@@ -159,7 +165,7 @@ class PipelineSchedule:
     def forward(self, inputs: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
         """Forward-only pipelined pass (evaluation / inference); the last stage returns the concatenated
         outputs of all micro-batches, other stages None."""
-        mbs = list(inputs.chunk(self.m, 0)) if self.is_first else [None] * self.m
+        mbs = self._split(inputs, "inputs") if self.is_first else [None] * self.m
         outs = []
         for i in range(self.m):
             x = mbs[i] if self.is_first else self.p2p.recv_forward(i == 0)

@@ -91,3 +91,17 @@ def test_bubble_math():
 
     assert abs(bubble_fraction(4, 4) - 3 / 7) < 1e-12
     assert bubble_fraction(1, 8) == 0.0
+
+
+def test_uneven_microbatches_rejected_before_any_transfer():
+    """Only micro-batch 0 carries a shape header: a batch not divisible by n_microbatches must fail on the
+    stage that holds it, before any send (single stage, no process group)."""
+    from distributed_pytorch_hpc_amd.parallel.pipeline import PipelineSchedule
+
+    sched = PipelineSchedule(torch.nn.Linear(4, 4), 0, 1, 4, loss_fn=lambda y, t: (y - t).pow(2).mean(),
+                             device=torch.device("cpu"))
+    with pytest.raises(ValueError, match="not divisible"):
+        sched.step(inputs=torch.randn(6, 4), target=torch.randn(6, 4))
+    with pytest.raises(ValueError, match="not divisible"):
+        sched.forward(torch.randn(2, 4))
+    assert len(sched.step(inputs=torch.randn(8, 4), target=torch.randn(8, 4))) == 4
