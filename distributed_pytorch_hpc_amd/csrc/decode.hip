@@ -1,0 +1,249 @@
+// Serving path of the Llama decoder (models/llama2.py KVCache, inference/generator.py): the KV-cache append and the
+// single-token decode attention.  Decode attention is a memory-bound stream over the cache (512 B of K+V per key and
+// KV head at head_dim 128), so it is built for bytes in flight, not for MFMA:
+//
+//   kv_append_k      : RoPE of q (in place in the fused QKV GEMM output) and of k, k and v written into the cache at
+//                      position pos[b] + s.  Positions are read from device memory, so a captured HIP-graph decode
+//                      step replays correctly with the cache advancing between replays.
+//   decode_attn_k    : split-KV ("flash-decoding") -- one wave per 64-key chunk of one (batch, KV head), all G query
+//                      heads of that KV head's group at once (GQA: the K/V rows are read once per chunk).  16 lanes
+//                      per 256-B key row (head_dim 128), 4 keys per wave instruction; every K and V row of the
+//                      chunk is loaded up front (16 + 16 KiB per wave in flight) and scores, softmax and P.V stay in
+//                      registers -- no LDS, no barriers.  Writes the chunk's unnormalised o and its (max, sum).
+//   decode_combine_k : one wave per (batch, query head) merges the chunks of the sequence (log-sum-exp rescaling)
+//                      and writes bf16 o straight into the [B, Hq * D] input of the output projection.
+// Keys past a sequence's length re-read its last valid row (finite data) and get probability 0, so the cache never
+// needs clearing and every load stays inside the written region.
+#include "dph_common.h"
+#include "kernels.h"
+
+namespace dph {
+
+namespace {
+
+__global__ __launch_bounds__(256) void kv_append_k(KVAppendParams p) {
+  const int CH = p.D / 8, NH = p.Hq + 2 * p.Hkv;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)p.B * p.S * NH * CH;
+  if (i >= total) return;
+  const int c = (int)(i % CH);
+  int64_t r = i / CH;
+  const int h = (int)(r % NH);
+  r /= NH;
+  const int s = (int)(r % p.S);
+  const int b = (int)(r / p.S);
+  const int t = p.pos[b] + s;
+  if (t >= p.Smax) return;   // the host checks capacity; never write past the cache
+  bf16* src = (bf16*)p.qkv + (int64_t)b * p.qkv_sb + (int64_t)s * p.qkv_ss + (int64_t)h * p.D + c * 8;
+  float v[8];
+  Vec8<bf16>::load(src, v);
+  if (h < p.Hq + p.Hkv) {   // interleaved-pair rotation, pair index 4c + j, angle table row t
+    const float* cs = p.cos + (int64_t)t * (p.D / 2) + c * 4;
+    const float* sn = p.sin + (int64_t)t * (p.D / 2) + c * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = v[2 * j], bb = v[2 * j + 1], co = cs[j], si = sn[j];
+      v[2 * j] = a * co - bb * si;
+      v[2 * j + 1] = a * si + bb * co;
+    }
+  }
+  if (h < p.Hq) {
+    Vec8<bf16>::store(src, v);
+  } else {
+    const bool is_k = h < p.Hq + p.Hkv;
+    const int hk = is_k ? h - p.Hq : h - p.Hq - p.Hkv;
+    bf16* dst = (bf16*)(is_k ? p.kc : p.vc) + (int64_t)b * p.c_sb + (int64_t)t * p.c_ss + (int64_t)hk * p.c_sh + c * 8;
+    Vec8<bf16>::store(dst, v);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ float group_sum(float v) {   // sum over aligned groups of N lanes
+#pragma unroll
+  for (int o = N / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int FROM>
+__device__ __forceinline__ float across_groups_max(float v) {   // max over lanes congruent mod FROM
+#pragma unroll
+  for (int o = FROM; o < 64; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+template <int FROM>
+__device__ __forceinline__ float across_groups_sum(float v) {
+#pragma unroll
+  for (int o = FROM; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int HD, int G>
+__global__ __launch_bounds__(256) void decode_attn_k(DecodeParams p) {
+  constexpr int TPK = HD / 8;     // lanes per key row (8 bf16 = 16 B each)
+  constexpr int KPI = 64 / TPK;   // keys per wave instruction
+  constexpr int NIT = 64 / KPI;   // instructions per 64-key chunk
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t = lane % TPK, j = lane / TPK;
+  const int b = blockIdx.z, hg = blockIdx.y;
+  const int chunk = blockIdx.x * 4 + wave;
+  const int len = min(p.pos[b] + p.len_add, p.Smax);
+  const int k0 = chunk * 64;
+  if (chunk >= p.nch || k0 >= len) return;   // no barriers below: a finished wave may leave
+  const int hq0 = hg * G;
+  const int hkv = hq0 / (p.Hq / p.Hkv);
+
+  const float sl2 = p.scale * 1.4426950408889634f;
+  float qf[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    Vec8<bf16>::load((const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)(hq0 + g) * p.q_sh + t * 8, qf[g]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qf[g][e] *= sl2;
+  }
+
+  const bf16* kb = (const bf16*)p.kc + (int64_t)b * p.c_sb + (int64_t)hkv * p.c_sh + t * 8;
+  const bf16* vb = (const bf16*)p.vc + (int64_t)b * p.c_sb + (int64_t)hkv * p.c_sh + t * 8;
+  bf16x8 kr[NIT], vr[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int row = min(k0 + it * KPI + j, len - 1);
+    kr[it] = *reinterpret_cast<const bf16x8*>(kb + (int64_t)row * p.c_ss);
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int row = min(k0 + it * KPI + j, len - 1);
+    vr[it] = *reinterpret_cast<const bf16x8*>(vb + (int64_t)row * p.c_ss);
+  }
+
+  // scores (log2 units): s[g][it] is key k0 + it * KPI + j, identical in the TPK lanes of group j
+  float s[G][NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const bool valid = k0 + it * KPI + j < len;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d = fmaf(qf[g][e], (float)kr[it][e], d);
+      d = group_sum<TPK>(d);
+      s[g][it] = valid ? d : -INFINITY;
+    }
+  }
+  float m[G], l[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float mx = s[g][0];
+#pragma unroll
+    for (int it = 1; it < NIT; ++it) mx = fmaxf(mx, s[g][it]);
+    m[g] = across_groups_max<TPK>(mx);   // finite: key k0 < len is valid
+    float sum = 0.f;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      s[g][it] = exp2f(s[g][it] - m[g]);
+      sum += s[g][it];
+    }
+    l[g] = across_groups_sum<TPK>(sum);
+  }
+
+  float acc[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[g][e] = 0.f;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(s[g][it], (float)vr[it][e], acc[g][e]);
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[g][e] = across_groups_sum<TPK>(acc[g][e]);
+
+  if (j == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int64_t slot = ((int64_t)b * p.Hq + hq0 + g) * p.nch + chunk;
+      Vec8<float>::store(p.opart + slot * HD + t * 8, acc[g]);
+      if (t == 0) {
+        p.mlpart[2 * slot] = m[g];
+        p.mlpart[2 * slot + 1] = l[g];
+      }
+    }
+  }
+}
+
+// one wave per (b, hq); lane d-slice of EPL = max(HD / 64, 1) elements (HD 32: lanes >= 32 idle)
+template <int HD>
+__global__ __launch_bounds__(256) void decode_combine_k(DecodeParams p) {
+  constexpr int EPL = HD >= 64 ? HD / 64 : 1;
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= p.B * p.Hq) return;
+  const int b = w / p.Hq, hq = w % p.Hq;
+  const int len = min(p.pos[b] + p.len_add, p.Smax);
+  const int n = min((len + 63) / 64, p.nch);
+  const float* ml = p.mlpart + (int64_t)w * p.nch * 2;
+  const float* op = p.opart + (int64_t)w * p.nch * HD;
+  float M = -INFINITY;
+  for (int c = lane; c < n; c += 64) M = fmaxf(M, ml[2 * c]);
+  M = wave_max(M);
+  float L = 0.f, acc[EPL];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
+  const bool active = lane * EPL < HD;
+#pragma unroll 4
+  for (int c = 0; c < n; ++c) {
+    const float wgt = exp2f(ml[2 * c] - M);
+    L = fmaf(wgt, ml[2 * c + 1], L);
+    if (active) {
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) acc[e] = fmaf(wgt, op[(int64_t)c * HD + lane * EPL + e], acc[e]);
+    }
+  }
+  if (active && n > 0) {
+    const float inv = 1.f / L;
+    bf16* out = (bf16*)p.out + (int64_t)b * p.out_sb + (int64_t)hq * HD + lane * EPL;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) out[e] = (bf16)(acc[e] * inv);
+  }
+}
+
+}  // namespace
+
+void kv_append(const KVAppendParams& p, hipStream_t st) {
+  const int64_t total = (int64_t)p.B * p.S * (p.Hq + 2 * p.Hkv) * (p.D / 8);
+  if (total == 0) return;
+  hipLaunchKernelGGL(kv_append_k, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, p);
+}
+
+// Query heads per wave: the largest of 4 / 2 / 1 dividing the GQA group (K/V rows are read once per head group).
+int decode_heads_per_wave(int Hq, int Hkv) {
+  const int rep = Hq / Hkv;
+  return rep % 4 == 0 ? 4 : (rep % 2 == 0 ? 2 : 1);
+}
+
+void decode_attention(const DecodeParams& p, hipStream_t st) {
+  const int G = decode_heads_per_wave(p.Hq, p.Hkv);
+  const dim3 grid((unsigned)cdiv(p.nch, 4), (unsigned)(p.Hq / G), (unsigned)p.B);
+#define DPH_DEC(HD_, G_) hipLaunchKernelGGL((decode_attn_k<HD_, G_>), grid, dim3(256), 0, st, p)
+#define DPH_DEC_G(HD_)          \
+  do {                          \
+    if (G == 4) DPH_DEC(HD_, 4); \
+    else if (G == 2) DPH_DEC(HD_, 2); \
+    else DPH_DEC(HD_, 1);       \
+  } while (0)
+  if (p.D == 128) DPH_DEC_G(128);
+  else if (p.D == 64) DPH_DEC_G(64);
+  else DPH_DEC_G(32);
+#undef DPH_DEC_G
+#undef DPH_DEC
+  const dim3 cgrid((unsigned)cdiv((int64_t)p.B * p.Hq, 4));
+  if (p.D == 128) hipLaunchKernelGGL(decode_combine_k<128>, cgrid, dim3(256), 0, st, p);
+  else if (p.D == 64) hipLaunchKernelGGL(decode_combine_k<64>, cgrid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL(decode_combine_k<32>, cgrid, dim3(256), 0, st, p);
+}
+
+}  // namespace dph

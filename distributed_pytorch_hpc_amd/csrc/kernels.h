@@ -177,6 +177,28 @@ int fp8_amax_blocks(int64_t n);
 void fp8_amax(const void* x, int64_t n, int fmt, float* partial, float* scal, hipStream_t stream);
 void fp8_quant(const void* x, int64_t R, int64_t C, const float* scal, int fmt, void* y, void* yt, hipStream_t stream);
 
+// Serving path (csrc/decode.hip).  Caches are [B, Smax, Hkv, D] bf16 (K and V at the same strides, elements);
+// pos[b] (int32, device) = tokens already cached for sequence b.
+struct KVAppendParams {
+  void* qkv; int64_t qkv_sb, qkv_ss;     // [B, S, (Hq + 2 Hkv) * D] bf16; q rotated in place
+  void* kc; void* vc; int64_t c_sb, c_ss, c_sh;
+  const int* pos; const float* cos; const float* sin;   // RoPE tables fp32 [max_pos, D / 2]
+  int B, S, Hq, Hkv, D, Smax;
+};
+void kv_append(const KVAppendParams& p, hipStream_t stream);
+struct DecodeParams {
+  const void* q; int64_t q_sb, q_sh;     // q[b, hq, :] bf16
+  const void* kc; const void* vc; int64_t c_sb, c_ss, c_sh;
+  const int* pos; int len_add;           // keys visible to sequence b: pos[b] + len_add
+  float* opart; float* mlpart;           // workspace [B, Hq, nch, D] / [B, Hq, nch, 2] fp32
+  void* out; int64_t out_sb;             // bf16 out[b, hq * D + d]
+  int B, Hq, Hkv, D, nch;                // nch = 64-key chunks covered (>= ceil(max length / 64))
+  int Smax;                              // cache capacity: lengths are clamped to it (no read past the cache)
+  float scale;
+};
+int decode_heads_per_wave(int Hq, int Hkv);
+void decode_attention(const DecodeParams& p, hipStream_t stream);
+
 // Single-node all-reduce over IPC-mapped peer buffers (csrc/custom_allreduce.hip).  ctx is an opaque handle.
 int64_t car_create(int rank, int world, int64_t max_bytes, double timeout_s);
 void car_ipc_handle(int64_t ctx, void* out64);

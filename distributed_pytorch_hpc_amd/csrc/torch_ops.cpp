@@ -403,6 +403,76 @@ std::tuple<Tensor, Tensor, Tensor> fp8_quantize(const Tensor& x, int64_t fmt, bo
   return {y, yt, buf.select(0, 2)};
 }
 
+// ------------------------------------------------------------------------------------------------ serving
+void check_kv_cache(const Tensor& kc, const Tensor& vc) {
+  TORCH_CHECK(kc.dim() == 4 && kc.scalar_type() == at::kBFloat16 && kc.sizes() == vc.sizes() &&
+                  kc.strides() == vc.strides() && vc.scalar_type() == at::kBFloat16,
+              "kv cache: k and v must be bf16 [B, Smax, Hkv, D] with equal strides");
+  TORCH_CHECK(kc.stride(3) == 1 && kc.stride(0) % 8 == 0 && kc.stride(1) % 8 == 0 && kc.stride(2) % 8 == 0,
+              "kv cache: head dim contiguous, strides multiples of 8 elements");
+  check_align16(kc, "k_cache"); check_align16(vc, "v_cache");
+}
+
+void check_positions(const Tensor& pos, const Tensor& like, int64_t B) {
+  TORCH_CHECK(pos.scalar_type() == at::kInt && pos.dim() == 1 && pos.size(0) == B && pos.is_contiguous() &&
+                  pos.device() == like.device(),
+              "kv cache: pos must be a contiguous int32 [B] tensor on the cache's device");
+}
+
+void kv_append_(Tensor& qkv, Tensor& kc, Tensor& vc, const Tensor& pos, const Tensor& cos, const Tensor& sin,
+                int64_t n_heads, int64_t n_kv_heads) {
+  c10::DeviceGuard g(qkv.device());
+  check_kv_cache(kc, vc);
+  const int64_t B = qkv.size(0), S = qkv.size(1), D = kc.size(3);
+  TORCH_CHECK(qkv.dim() == 3 && qkv.scalar_type() == at::kBFloat16 && qkv.stride(2) == 1 &&
+                  qkv.size(2) == (n_heads + 2 * n_kv_heads) * D && qkv.stride(0) % 8 == 0 && qkv.stride(1) % 8 == 0,
+              "kv_append: qkv must be bf16 [B, S, (Hq + 2 Hkv) * D] with a contiguous last dim");
+  check_align16(qkv, "qkv");
+  TORCH_CHECK(kc.size(0) == B && kc.size(2) == n_kv_heads && n_heads % n_kv_heads == 0 && D % 8 == 0,
+              "kv_append: cache batch / heads do not match qkv");
+  check_positions(pos, qkv, B);
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat && cos.is_contiguous() &&
+                  sin.is_contiguous() && cos.dim() == 2 && cos.sizes() == sin.sizes() && cos.size(1) == D / 2 &&
+                  cos.size(0) >= kc.size(1) && cos.device() == qkv.device(),
+              "kv_append: rope tables must be contiguous fp32 [>= Smax, D / 2] on the same device");
+  dph::KVAppendParams p{};
+  p.qkv = qkv.data_ptr(); p.qkv_sb = qkv.stride(0); p.qkv_ss = qkv.stride(1);
+  p.kc = kc.data_ptr(); p.vc = vc.data_ptr(); p.c_sb = kc.stride(0); p.c_ss = kc.stride(1); p.c_sh = kc.stride(2);
+  p.pos = pos.data_ptr<int>(); p.cos = cos.data_ptr<float>(); p.sin = sin.data_ptr<float>();
+  p.B = (int)B; p.S = (int)S; p.Hq = (int)n_heads; p.Hkv = (int)n_kv_heads; p.D = (int)D; p.Smax = (int)kc.size(1);
+  dph::kv_append(p, cur_stream());
+}
+
+Tensor decode_attention(const Tensor& qkv, const Tensor& kc, const Tensor& vc, const Tensor& pos, int64_t n_heads,
+                        int64_t n_kv_heads, double scale, int64_t max_len) {
+  c10::DeviceGuard g(qkv.device());
+  check_kv_cache(kc, vc);
+  const int64_t B = qkv.size(0), D = kc.size(3), Smax = kc.size(1);
+  TORCH_CHECK(D == 32 || D == 64 || D == 128, "decode_attention: head_dim must be 32, 64 or 128");
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(1) == 1 && qkv.scalar_type() == at::kBFloat16 && qkv.stride(2) == 1 &&
+                  qkv.size(2) == (n_heads + 2 * n_kv_heads) * D && qkv.stride(0) % 8 == 0,
+              "decode_attention: qkv must be bf16 [B, 1, (Hq + 2 Hkv) * D]");
+  check_align16(qkv, "qkv");
+  TORCH_CHECK(kc.size(0) == B && kc.size(2) == n_kv_heads && n_heads % n_kv_heads == 0,
+              "decode_attention: cache batch / heads do not match qkv");
+  check_positions(pos, qkv, B);
+  TORCH_CHECK(max_len >= 1 && max_len <= Smax, "decode_attention: max_len must be in [1, Smax]");
+  const int64_t nch = (max_len + 63) / 64;
+  auto out = at::empty({B, n_heads * D}, qkv.options());
+  auto opart = at::empty({B, n_heads, nch, D}, qkv.options().dtype(at::kFloat));
+  auto ml = at::empty({B, n_heads, nch, 2}, qkv.options().dtype(at::kFloat));
+  dph::DecodeParams p{};
+  p.q = qkv.data_ptr(); p.q_sb = qkv.stride(0); p.q_sh = D;
+  p.kc = kc.data_ptr(); p.vc = vc.data_ptr(); p.c_sb = kc.stride(0); p.c_ss = kc.stride(1); p.c_sh = kc.stride(2);
+  p.pos = pos.data_ptr<int>(); p.len_add = 1;
+  p.opart = opart.data_ptr<float>(); p.mlpart = ml.data_ptr<float>();
+  p.out = out.data_ptr(); p.out_sb = out.stride(0);
+  p.B = (int)B; p.Hq = (int)n_heads; p.Hkv = (int)n_kv_heads; p.D = (int)D; p.nch = (int)nch; p.Smax = (int)Smax;
+  p.scale = (float)scale;
+  dph::decode_attention(p, cur_stream());
+  return out;
+}
+
 // ------------------------------------------------------------------------------------------------ embedding
 Tensor embedding_fwd(const Tensor& ids, const Tensor& table, int64_t vocab_start) {
   c10::DeviceGuard g(table.device());
@@ -782,6 +852,10 @@ TORCH_LIBRARY(dph, m) {
   m.def("image_augment(Tensor images, Tensor idx, Tensor? params, Tensor mean, Tensor inv_std, int pad, "
         "bool channels_last, bool bf16_out) -> Tensor");
   m.def("fp8_quantize(Tensor x, int fmt, bool rowmajor, bool transposed) -> (Tensor, Tensor, Tensor)");
+  m.def("kv_append_(Tensor(a!) qkv, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor pos, Tensor cos, Tensor sin, "
+        "int n_heads, int n_kv_heads) -> ()");
+  m.def("decode_attention(Tensor qkv, Tensor k_cache, Tensor v_cache, Tensor pos, int n_heads, int n_kv_heads, "
+        "float scale, int max_len) -> Tensor");
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
@@ -830,6 +904,8 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("flash_attn_bwd_into", &flash_attn_bwd_into);
   m.impl("fp8_quantize", &fp8_quantize);
+  m.impl("kv_append_", &kv_append_);
+  m.impl("decode_attention", &decode_attention);
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("gemm_tn_", &gemm_tn_);

@@ -14,6 +14,8 @@ MI355X-first changes (numerically equivalent):
   * With targets, ``forward`` returns the mean cross-entropy through the fused CE kernel, which never
     materialises fp32 logits.
 ``convert_reference_state_dict`` maps a reference checkpoint (wq/wk/wv, w1/w3) onto this layout.
+Serving (beyond the reference): ``KVCache`` + ``Transformer.forward_inference`` (prefill and single-token decode
+through csrc/decode.hip), driven by ``inference.Generator``.
 """
 from __future__ import annotations
 
@@ -119,15 +121,38 @@ class Attention(nn.Module):
         nn.init.trunc_normal_(self.wqkv.weight, mean=0.0, std=0.02)
         nn.init.trunc_normal_(self.wo.weight, mean=0.0, std=init_std)
 
-    def forward(self, x: torch.Tensor, pos_offset: int = 0) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, pos_offset: int = 0, cache: Optional["KVCache"] = None,
+                layer: int = 0) -> torch.Tensor:
         qkv = self.wqkv(x)
         cos, sin = rope_tables(self.head_dim, self.max_pos, self.theta, qkv.device)
+        if cache is not None:
+            return self.wo(self._cached_attention(qkv.contiguous(), cos, sin, cache, layer))
         if self.cp_attention is not None:
             o = self.cp_attention(qkv, cos, sin, self.n_local_heads, self.n_local_kv_heads, self.head_dim)
         else:
             o = ops.rope_attention(qkv, cos, sin, self.n_local_heads, self.n_local_kv_heads, self.head_dim,
                                    causal=True, pos_offset=pos_offset)
         return self.wo(o)
+
+    def _cached_attention(self, qkv, cos, sin, cache: "KVCache", layer: int) -> torch.Tensor:
+        """Serving path: append this step's k / v (RoPE at each sequence's cache position) and attend over the cache.
+        One new token per sequence runs the split-KV decode kernel; several (prefill, chunked append) run the flash
+        kernel over the cached prefix with the bottom-right causal mask."""
+        if self.cp_attention is not None:
+            raise NotImplementedError("KV-cache inference with context-parallel attention")
+        b, s, _ = qkv.shape
+        nh, nkv, hd = self.n_local_heads, self.n_local_kv_heads, self.head_dim
+        kc, vc = cache.k[layer], cache.v[layer]
+        ops.kv_append_(qkv, kc, vc, cache.pos, cos, sin, nh, nkv)
+        if s == 1:
+            return ops.decode_attention(qkv, kc, vc, cache.pos, nh, nkv, max_len=cache.attn_bound()).view(b, 1, -1)
+        n = cache.length
+        if n is None:
+            raise RuntimeError("a multi-token append needs every sequence of the cache at the same, host-known length "
+                               "(prefill ragged prompts one sequence at a time through KVCache.slot)")
+        q = qkv[:, :, : nh * hd].view(b, s, nh, hd)
+        o = ops.flash_attention(q, kc[:, : n + s], vc[:, : n + s], causal=True)
+        return o.reshape(b, s, nh * hd)
 
 
 class FeedForward(nn.Module):
@@ -167,15 +192,16 @@ class TransformerBlock(nn.Module):
         self.attention.init_weights(self.weight_init_std)
         self.feed_forward.init_weights(self.weight_init_std)
 
-    def forward(self, x: torch.Tensor, delta: Optional[torch.Tensor] = None):
+    def forward(self, x: torch.Tensor, delta: Optional[torch.Tensor] = None, cache: Optional["KVCache"] = None):
         """Takes the residual stream as (x, delta) with x + delta = reference block input and returns
         (h, ffn_out) with h + ffn_out = reference block output (the final add is deferred into the next
-        norm).  ``forward(x)`` with delta None is the plain reference input."""
+        norm).  ``forward(x)`` with delta None is the plain reference input; ``cache`` selects the serving path."""
         if delta is None:
             r, a = x, self.attention_norm(x)
         else:
             r, a = self.attention_norm(x, delta)
-        h, f = self.ffn_norm(r, self.attention(a))
+        attn = self.attention(a) if cache is None else self.attention(a, cache=cache, layer=self.layer_id)
+        h, f = self.ffn_norm(r, attn)
         return h, self.feed_forward(f)
 
 
@@ -240,6 +266,81 @@ class Transformer(nn.Module):
         for layer in self.layers:
             h, delta = layer(h, delta)
         return self.head(h, delta, targets)
+
+    @torch.no_grad()
+    def forward_inference(self, tokens: torch.Tensor, cache: "KVCache", last_only: bool = True) -> torch.Tensor:
+        """Incremental forward for serving: tokens [B, S] continue each sequence of ``cache`` (prefill: S = prompt
+        length on an empty cache; decode: S = 1).  Returns fp32 logits of the last position [B, V] (or of every new
+        position [B, S, V]) and advances the cache by S."""
+        s = tokens.shape[1]
+        if cache.lengths is not None and max(cache.lengths) + s > cache.max_len:
+            raise ValueError(f"KV cache full: {max(cache.lengths)} + {s} tokens > capacity {cache.max_len}")
+        h, delta = self.embed(tokens), None
+        for layer in self.layers:
+            h, delta = layer(h, delta, cache=cache)
+        if last_only and s > 1:
+            h = h[:, -1:].contiguous()
+            delta = delta[:, -1:].contiguous() if delta is not None else None
+        logits = self.head(h, delta)
+        cache.advance(s)
+        return logits[:, -1] if last_only else logits
+
+
+class KVCache:
+    """Per-layer key / value cache of a Transformer for incremental decoding (serving; the reference model is
+    training-only).  ``k`` / ``v``: [n_layers, B, max_len, Hkv_local, head_dim]; ``pos``: int32 [B] device tensor =
+    tokens cached per sequence, read by the kernels (a captured decode graph advances it on the device alone).
+    ``lengths`` mirrors pos on the host while it is known (None inside / after graph replays that the owner
+    tracks itself).  ``slot(i)`` is a view of sequence i (prefill of prompts of different lengths).
+    Sized for HBM: 7B at 4 096 tokens is 2 GiB per sequence in bf16."""
+
+    def __init__(self, model: "Transformer", batch: int, max_len: int, device=None, dtype: torch.dtype | None = None):
+        args = model.model_args
+        attn = model.layers[0].attention if len(model.layers) else None
+        hkv = attn.n_local_kv_heads if attn is not None else args.kv_heads
+        ref = next(model.parameters())
+        device = ref.device if device is None else torch.device(device)
+        dtype = ref.dtype if dtype is None else dtype
+        if max_len > 2 * args.max_seq_len:
+            raise ValueError(f"max_len {max_len} exceeds the RoPE table ({2 * args.max_seq_len} positions)")
+        n_layers = max((layer.layer_id for layer in model.layers), default=-1) + 1   # pipeline stages keep ids
+        shape = (n_layers, batch, max_len, hkv, args.head_dim)
+        self.k = torch.zeros(shape, dtype=dtype, device=device)
+        self.v = torch.zeros(shape, dtype=dtype, device=device)
+        self.pos = torch.zeros(batch, dtype=torch.int32, device=device)
+        self.batch, self.max_len = batch, max_len
+        self.lengths: Optional[list] = [0] * batch
+        self._parent, self._index = None, None
+
+    @property
+    def length(self) -> Optional[int]:
+        """The common length of every sequence when known on the host, else None."""
+        if self.lengths is None or len(set(self.lengths)) != 1:
+            return None
+        return self.lengths[0]
+
+    def attn_bound(self) -> int:
+        """Upper bound of pos + 1 over the batch for the decode kernel's launch (the capacity when unknown)."""
+        return self.max_len if self.lengths is None else min(max(self.lengths) + 1, self.max_len)
+
+    def advance(self, n: int) -> None:
+        self.pos.add_(n)
+        if self.lengths is not None:
+            self.lengths = [x + n for x in self.lengths]
+        if self._parent is not None and self._parent.lengths is not None:
+            self._parent.lengths[self._index] += n
+
+    def reset(self) -> None:
+        self.pos.zero_()
+        self.lengths = [0] * self.batch
+
+    def slot(self, i: int) -> "KVCache":
+        view = object.__new__(KVCache)
+        view.k, view.v, view.pos = self.k[:, i:i + 1], self.v[:, i:i + 1], self.pos[i:i + 1]
+        view.batch, view.max_len = 1, self.max_len
+        view.lengths = None if self.lengths is None else [self.lengths[i]]
+        view._parent, view._index = self, i
+        return view
 
 
 def build_llama(args: ModelArgs | str, device=None, dtype: torch.dtype = torch.bfloat16, seed: int = 0,

@@ -177,3 +177,13 @@ def _latmse_fwd(pred, target, n_global, lat_offset):
 @register_fake("dph::latmse_bwd")
 def _latmse_bwd(gloss, pred, target, n_global, lat_offset, need_dtarget):
     return torch.empty_like(pred), (torch.empty_like(target) if need_dtarget else pred.new_empty((0,)))
+
+
+@register_fake("dph::kv_append_")
+def _kv_append(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads):
+    return None
+
+
+@register_fake("dph::decode_attention")
+def _decode_attn(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale, max_len):
+    return qkv.new_empty((qkv.shape[0], n_heads * k_cache.shape[-1]))

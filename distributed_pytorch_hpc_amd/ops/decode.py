@@ -1,0 +1,73 @@
+"""Serving-path ops: KV-cache append (RoPE fused) and single-token decode attention (csrc/decode.hip).
+
+The reference is training-only (fsdp_tp/llama2_model.py has no cache); these ops back ``models.llama2.KVCache`` and
+``inference.Generator``.  Layout: the fused QKV projection output [B, S, (Hq + 2 Hkv) * D] (the same buffer the
+training path rotates in place) and per-layer caches [B, Smax, Hkv, D]; ``pos`` is an int32 [B] device tensor with
+the number of tokens already cached per sequence, so a decode step never needs the lengths on the host (HIP graphs).
+
+GPU tensors run the HIP kernels (the extension must be present); CPU tensors run the PyTorch references below, which
+are also the oracles of tests/test_decode_gpu.py.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+from .attention import attention_reference
+from .rope import rope_reference
+
+
+def _split(qkv: torch.Tensor, n_heads: int, n_kv_heads: int, head_dim: int):
+    b, s, _ = qkv.shape
+    q = qkv[:, :, : n_heads * head_dim].view(b, s, n_heads, head_dim)
+    k = qkv[:, :, n_heads * head_dim: (n_heads + n_kv_heads) * head_dim].view(b, s, n_kv_heads, head_dim)
+    v = qkv[:, :, (n_heads + n_kv_heads) * head_dim:].view(b, s, n_kv_heads, head_dim)
+    return q, k, v
+
+
+def kv_append_reference(qkv, k_cache, v_cache, pos, cos, sin, n_heads: int, n_kv_heads: int) -> None:
+    hd = k_cache.shape[-1]
+    q, k, v = _split(qkv, n_heads, n_kv_heads, hd)
+    s = qkv.shape[1]
+    for b, p in enumerate(pos.tolist()):
+        if p + s > k_cache.shape[1]:
+            raise ValueError(f"kv cache overflow: sequence {b} at {p} + {s} > capacity {k_cache.shape[1]}")
+        q[b:b + 1].copy_(rope_reference(q[b:b + 1], cos, sin, p))
+        k_cache[b, p:p + s].copy_(rope_reference(k[b:b + 1], cos, sin, p)[0])
+        v_cache[b, p:p + s].copy_(v[b])
+
+
+def kv_append_(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor,
+               sin: torch.Tensor, n_heads: int, n_kv_heads: int) -> None:
+    """Rotate q in place in ``qkv`` [B, S, (Hq + 2 Hkv) * D], write rotated k and v into the caches at positions
+    pos[b] .. pos[b] + S - 1.  ``pos`` is not advanced (the caller does that once per model step)."""
+    if _lib.use_native(qkv):
+        _lib.ops().kv_append_(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads)
+        return
+    kv_append_reference(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads)
+
+
+def decode_attention_reference(qkv, k_cache, v_cache, pos, n_heads: int, n_kv_heads: int, scale: float):
+    hd = k_cache.shape[-1]
+    q, _, _ = _split(qkv, n_heads, n_kv_heads, hd)
+    outs = []
+    for b, p in enumerate(pos.tolist()):
+        n = p + 1
+        outs.append(attention_reference(q[b:b + 1].float(), k_cache[b:b + 1, :n].float(),
+                                        v_cache[b:b + 1, :n].float(), causal=False, scale=scale))
+    return torch.cat(outs, 0).reshape(qkv.shape[0], n_heads * hd).to(qkv.dtype)
+
+
+def decode_attention(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, pos: torch.Tensor, n_heads: int,
+                     n_kv_heads: int, scale: float | None = None, max_len: int | None = None) -> torch.Tensor:
+    """Attention of the single new token per sequence (qkv [B, 1, ...], already appended) over keys 0 .. pos[b];
+    returns [B, Hq * D].  ``max_len`` bounds pos + 1 over the batch (default: the cache capacity, as in a captured
+    graph); a tighter bound only launches fewer workgroups."""
+    hd = k_cache.shape[-1]
+    scale = 1.0 / math.sqrt(hd) if scale is None else scale
+    if _lib.use_native(qkv):
+        return _lib.ops().decode_attention(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale,
+                                           int(max_len or k_cache.shape[1]))
+    return decode_attention_reference(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale)
