@@ -246,4 +246,125 @@ void decode_attention(const DecodeParams& p, hipStream_t st) {
   else hipLaunchKernelGGL(decode_combine_k<32>, cgrid, dim3(256), 0, st, p);
 }
 
+// ==================================================================================================
+// Skinny GEMM for decode: y[M, N] = x[M, K] W[N, K]^T with M <= 64 (one token per sequence), bf16, fp32 accumulate.
+// Pure weight streaming (2 N K bytes read once, x re-read from L2): hipBLASLt's small-M tiles ran the Llama-2-7B
+// decode projections at 2.6-3.7 TB/s (profiles/serving/).  One workgroup = 16 output rows (n) x all M, 8 waves
+// splitting K; each 16-row W tile goes straight from HBM into the A operand of v_mfma_f32_16x16x32_bf16 (lane l: row
+// l & 15, k 8 (l >> 4) .. +7 -- 64 contiguous bytes per row per instruction), x^T is the B operand, so the matrix
+// core does the k reduction and no shuffles are needed.  U unrolled k-steps keep U x 1 KiB of W in flight per wave;
+// the 8 partial tiles are summed through LDS.
+// ==================================================================================================
+namespace {
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+constexpr int SG_WAVES = 8;
+
+template <int MT, int U>
+__global__ __launch_bounds__(64 * SG_WAVES) void skinny_gemm_k(const bf16* __restrict__ x, int64_t ldx,
+                                                              const bf16* __restrict__ w, int64_t ldw,
+                                                              bf16* __restrict__ y, int64_t ldy, int M, int K) {
+  __shared__ f32x4 red[SG_WAVES][MT][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int kq = K / SG_WAVES;
+  const int kbeg = wave * kq;
+  const bf16* wp = w + (int64_t)(n0 + r) * ldw + kbeg + 8 * g;
+  const bf16* xp[MT];
+  bool xv[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = mt * 16 + r;
+    xv[mt] = m < M;
+    xp[mt] = x + (int64_t)(xv[mt] ? m : 0) * ldx + kbeg + 8 * g;
+  }
+  const bf16x8 z = {};
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // software pipeline over groups of U k-steps: the W tiles and x slices (B operands, L2) of group g+1 are requested
+  // before group g's MFMAs, which only read registers loaded one group earlier -- whatever order hipcc issues the
+  // loads in, the counted vmcnt in front of the MFMAs leaves the prefetch in flight.  The last group re-reads its
+  // own slices (no branch: a conditional prefetch makes hipcc pick one conservative count for both paths).  Lanes
+  // past M load row 0 and select zero.
+  const int ng = kq / (32 * U);
+  bf16x8 a[U], b[MT][U];
+  if (ng > 0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      a[u] = *reinterpret_cast<const bf16x8*>(wp + 32 * u);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) b[mt][u] = *reinterpret_cast<const bf16x8*>(xp[mt] + 32 * u);
+    }
+  }
+  for (int gi = 0; gi < ng; ++gi) {
+    const int kn = (gi + 1 < ng ? gi + 1 : gi) * 32 * U;
+    bf16x8 an[U], bn[MT][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      an[u] = *reinterpret_cast<const bf16x8*>(wp + kn + 32 * u);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) bn[mt][u] = *reinterpret_cast<const bf16x8*>(xp[mt] + kn + 32 * u);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the whole prefetch ahead of this group's MFMAs
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16(a[u], xv[mt] ? b[mt][u] : z, acc[mt]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      a[u] = an[u];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) b[mt][u] = bn[mt][u];
+    }
+  }
+  for (int k = ng * 32 * U; k < kq; k += 32) {
+    const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(wp + k);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(xp[mt] + k);
+      acc[mt] = mfma16(a1, xv[mt] ? b1 : z, acc[mt]);
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) red[wave][mt][lane] = acc[mt];
+  __syncthreads();
+  if (wave < MT) {   // wave mt sums m-tile mt: C[n = 4 g + i][m = mt * 16 + r]
+    f32x4 s = red[0][wave][lane];
+#pragma unroll
+    for (int v = 1; v < SG_WAVES; ++v) s += red[v][wave][lane];
+    const int m = wave * 16 + r;
+    if (m < M) {
+      bf16x4 o;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = (bf16)s[i];
+      *reinterpret_cast<bf16x4*>(y + (int64_t)m * ldy + n0 + 4 * g) = o;
+    }
+  }
+}
+
+}  // namespace
+
+bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K) {
+  return M >= 1 && M <= 64 && N % 16 == 0 && N > 0 && K % (32 * SG_WAVES) == 0 && K > 0;
+}
+
+void skinny_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, int64_t ldy, int M, int N, int K,
+                 hipStream_t st) {
+  const dim3 grid((unsigned)(N / 16)), block(64 * SG_WAVES);
+  const bf16* xb = (const bf16*)x;
+  const bf16* wb = (const bf16*)w;
+  bf16* yb = (bf16*)y;
+  switch ((M + 15) / 16) {
+    case 1: hipLaunchKernelGGL((skinny_gemm_k<1, 8>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
+    case 2: hipLaunchKernelGGL((skinny_gemm_k<2, 8>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
+    case 3: hipLaunchKernelGGL((skinny_gemm_k<3, 4>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
+    default: hipLaunchKernelGGL((skinny_gemm_k<4, 4>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
+  }
+}
+
 }  // namespace dph

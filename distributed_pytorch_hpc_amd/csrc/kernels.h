@@ -198,6 +198,10 @@ struct DecodeParams {
 };
 int decode_heads_per_wave(int Hq, int Hkv);
 void decode_attention(const DecodeParams& p, hipStream_t stream);
+// y[M, N] = x[M, K] W[N, K]^T for decode-sized M (<= 64): bf16, rows of x / W / y at strides ldx / ldw / ldy.
+bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K);
+void skinny_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, int64_t ldy, int M, int N, int K,
+                 hipStream_t stream);
 
 // Single-node all-reduce over IPC-mapped peer buffers (csrc/custom_allreduce.hip).  ctx is an opaque handle.
 int64_t car_create(int rank, int world, int64_t max_bytes, double timeout_s);

@@ -473,6 +473,23 @@ Tensor decode_attention(const Tensor& qkv, const Tensor& kc, const Tensor& vc, c
   return out;
 }
 
+Tensor skinny_linear(const Tensor& x, const Tensor& w) {
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "skinny_linear: bf16 only");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && x.size(-1) == w.size(1), "skinny_linear: w [N, K] contiguous");
+  const int64_t K = w.size(1), N = w.size(0), M = x.numel() / std::max<int64_t>(K, 1);
+  TORCH_CHECK(dph::skinny_gemm_supported(M, N, K), "skinny_linear: needs rows <= 64, N % 16 == 0, K % 256 == 0");
+  auto x2 = x.reshape({M, K});
+  TORCH_CHECK(x2.stride(1) == 1 && x2.stride(0) % 8 == 0, "skinny_linear: x rows must be contiguous, 16-B aligned");
+  check_align16(x2, "x"); check_align16(w, "w");
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  auto y = at::empty(sizes, x.options());
+  dph::skinny_gemm(x2.data_ptr(), x2.stride(0), w.data_ptr(), K, y.data_ptr(), N, (int)M, (int)N, (int)K,
+                   cur_stream());
+  return y;
+}
+
 // ------------------------------------------------------------------------------------------------ embedding
 Tensor embedding_fwd(const Tensor& ids, const Tensor& table, int64_t vocab_start) {
   c10::DeviceGuard g(table.device());
@@ -856,6 +873,7 @@ TORCH_LIBRARY(dph, m) {
         "int n_heads, int n_kv_heads) -> ()");
   m.def("decode_attention(Tensor qkv, Tensor k_cache, Tensor v_cache, Tensor pos, int n_heads, int n_kv_heads, "
         "float scale, int max_len) -> Tensor");
+  m.def("skinny_linear(Tensor x, Tensor w) -> Tensor");
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
@@ -906,6 +924,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("fp8_quantize", &fp8_quantize);
   m.impl("kv_append_", &kv_append_);
   m.impl("decode_attention", &decode_attention);
+  m.impl("skinny_linear", &skinny_linear);
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("gemm_tn_", &gemm_tn_);

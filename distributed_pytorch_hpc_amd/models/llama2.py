@@ -28,6 +28,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from .. import ops
+from ..ops import decode as decode_ops
 from ..ops.rope import precompute_rope_tables
 
 
@@ -100,6 +101,14 @@ def rope_tables(head_dim: int, max_pos: int, theta: float, device) -> tuple[torc
     return t
 
 
+def _proj(mod: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """Linear projection; a decode-sized row count without autograd (serving) takes the weight-streaming skinny
+    GEMM of csrc/decode.hip, everything else the module itself."""
+    if not torch.is_grad_enabled() and type(mod) is nn.Linear and decode_ops.skinny_ok(x, mod):
+        return decode_ops.skinny_linear(x, mod.weight)
+    return mod(x)
+
+
 # ---------------------------------------------------------------------------------------------- modules
 class Attention(nn.Module):
     def __init__(self, args: ModelArgs):
@@ -123,16 +132,16 @@ class Attention(nn.Module):
 
     def forward(self, x: torch.Tensor, pos_offset: int = 0, cache: Optional["KVCache"] = None,
                 layer: int = 0) -> torch.Tensor:
-        qkv = self.wqkv(x)
+        qkv = _proj(self.wqkv, x)
         cos, sin = rope_tables(self.head_dim, self.max_pos, self.theta, qkv.device)
         if cache is not None:
-            return self.wo(self._cached_attention(qkv.contiguous(), cos, sin, cache, layer))
+            return _proj(self.wo, self._cached_attention(qkv.contiguous(), cos, sin, cache, layer))
         if self.cp_attention is not None:
             o = self.cp_attention(qkv, cos, sin, self.n_local_heads, self.n_local_kv_heads, self.head_dim)
         else:
             o = ops.rope_attention(qkv, cos, sin, self.n_local_heads, self.n_local_kv_heads, self.head_dim,
                                    causal=True, pos_offset=pos_offset)
-        return self.wo(o)
+        return _proj(self.wo, o)
 
     def _cached_attention(self, qkv, cos, sin, cache: "KVCache", layer: int) -> torch.Tensor:
         """Serving path: append this step's k / v (RoPE at each sequence's cache position) and attend over the cache.
@@ -170,7 +179,7 @@ class FeedForward(nn.Module):
         nn.init.trunc_normal_(self.w2.weight, mean=0.0, std=init_std)
 
     def forward(self, x):
-        return self.w2(ops.swiglu(self.w13(x)))
+        return _proj(self.w2, ops.swiglu(_proj(self.w13, x)))
 
 
 class TransformerBlock(nn.Module):
@@ -245,7 +254,7 @@ class Transformer(nn.Module):
             x = self.norm(h)
         else:
             _, x = self.norm(h, delta)
-        logits = self.output(x)
+        logits = _proj(self.output, x)
         if self.loss_parallel and self.tp_group is not None:
             # vocab-sharded logits [B, S, V/tp] ("loss parallel", no [B, S, V] all-gather)
             vloc = logits.shape[-1]

@@ -187,3 +187,8 @@ def _kv_append(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads):
 @register_fake("dph::decode_attention")
 def _decode_attn(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale, max_len):
     return qkv.new_empty((qkv.shape[0], n_heads * k_cache.shape[-1]))
+
+
+@register_fake("dph::skinny_linear")
+def _skinny_linear(x, w):
+    return x.new_empty((*x.shape[:-1], w.shape[0]))

@@ -71,3 +71,26 @@ def decode_attention(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Te
         return _lib.ops().decode_attention(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale,
                                            int(max_len or k_cache.shape[1]))
     return decode_attention_reference(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale)
+
+
+def skinny_ok(x: torch.Tensor, mod: torch.nn.Module) -> bool:
+    """A bias-free nn.Linear call with decode-sized row count (<= 64) that the weight-streaming kernel covers.
+    Modules with hooks (FSDP units gather their weights in them) keep the module call."""
+    w = getattr(mod, "weight", None)
+    if w is None or getattr(mod, "bias", None) is not None or mod._forward_hooks or mod._forward_pre_hooks:
+        return False
+    if not (x.is_cuda and w.is_cuda) or _lib.reference_mode() or x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        return False
+    if w.dim() != 2 or not w.is_contiguous() or x.shape[-1] != w.shape[1] or x.stride(-1) != 1:
+        return False
+    k, n = w.shape[1], w.shape[0]
+    m = x.numel() // max(k, 1)
+    # where it measured faster than hipBLASLt (benchmarks/skinny_gemm_bench.py, profiles/serving/): at most 16 rows
+    # and N <= 8192 (wo / w2 of 7B: 1.4-1.9x); hipBLASLt's small-M tiles already stream the wide projections at
+    # 3.7-4.5 TB/s, and from 32 rows on its tiled reuse of x wins
+    return 1 <= m <= 16 and n <= 8192 and n % 16 == 0 and k % 256 == 0
+
+
+def skinny_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """x [..., K] @ w[N, K]^T for at most 64 rows (decode): streams W once at HBM rate (csrc/decode.hip)."""
+    return _lib.ops().skinny_linear(x, w)

@@ -87,3 +87,19 @@ def test_generator_graph_replay_matches_eager(dph_native):
     assert g._graph is not None
     assert graphed == eager
     assert g.generate(prompts, 24) == eager          # the captured graph is reused after reset
+
+
+@pytest.mark.parametrize("m", [1, 5, 16, 17, 40, 64])
+@pytest.mark.parametrize("n,k", [(4096, 4096), (272, 11008), (96, 256)])
+def test_skinny_linear_matches_fp32(dph_native, m, n, k):
+    from distributed_pytorch_hpc_amd.ops.decode import skinny_linear
+
+    g = torch.Generator(device="cuda").manual_seed(m + n)
+    x = torch.randn(m, k, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(n, k, device="cuda", generator=g) / k ** 0.5).to(torch.bfloat16)
+    y = skinny_linear(x, w)
+    ref = x.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+    # strided rows (a view into a wider buffer) and a leading batch shape
+    xb = torch.randn(m, 1, k + 256, device="cuda", generator=g).to(torch.bfloat16)[..., :k]
+    torch.testing.assert_close(skinny_linear(xb, w).float(), (xb.float() @ w.float().t()), atol=2e-2, rtol=2e-2)
