@@ -32,7 +32,7 @@ def bench(fn, iters=50):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ms", type=int, nargs="+", default=[1, 8, 32, 64])
+    ap.add_argument("--ms", type=int, nargs="+", default=[1, 2, 8, 16, 32])
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
     from distributed_pytorch_hpc_amd.ops import _lib

@@ -347,10 +347,78 @@ __global__ __launch_bounds__(64 * SG_WAVES) void skinny_gemm_k(const bf16* __res
   }
 }
 
+// GEMV form for M <= 2 (batch-1/2 decode): the MFMA form above spends 15/16 of its x operand on padding there.
+// A workgroup owns 8 rows of W; its waves split K in slices of C = 2 chunks of 512 (lane: 8 consecutive k per
+// chunk, so one wave instruction reads 1 KiB of one row); every lane issues all R x C = 16 W loads up front (16 KiB
+// per wave in flight, counted waits as the FMAs consume them; <= 128 VGPRs so 4 waves / SIMD stay resident), keeps
+// its 8 x values per chunk and m packed in registers, then each row's partial is reduced over the lanes and over
+// the waves through LDS.  K <= 16 waves x 1024.
+template <int M>
+__global__ __launch_bounds__(1024) void gemv_k(const bf16* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
+                                               int64_t ldw, bf16* __restrict__ y, int64_t ldy, int K) {
+  constexpr int R = 8, C = 2;
+  __shared__ float red[16][R * M];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int n0 = blockIdx.x * R;
+  int kc[C];
+  bool cv[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int k = (wave * C + c) * 512 + lane * 8;
+    cv[c] = k < K;
+    kc[c] = cv[c] ? k : 0;   // out-of-range lanes read column 0 and contribute zero
+  }
+  bf16x8 wr[R][C];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < C; ++c) wr[r][c] = *reinterpret_cast<const bf16x8*>(w + (int64_t)(n0 + r) * ldw + kc[c]);
+  bf16x8 xs[C][M];
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      xs[c][m] = *reinterpret_cast<const bf16x8*>(x + (int64_t)m * ldx + kc[c]);
+      if (!cv[c]) xs[c][m] = bf16x8{};
+    }
+  float acc[R][M];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[r][m] = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float wv = (float)wr[r][c][e];
+#pragma unroll
+        for (int m = 0; m < M; ++m) acc[r][m] = fmaf(wv, (float)xs[c][m][e], acc[r][m]);
+      }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float v = wave_sum(acc[r][m]);
+      if (lane == 0) red[wave][r * M + m] = v;
+    }
+  __syncthreads();
+  if ((int)threadIdx.x < R * M) {
+    float sum = 0.f;
+    for (int v = 0; v < nw; ++v) sum += red[v][threadIdx.x];
+    const int r = threadIdx.x / M, m = threadIdx.x % M;
+    y[(int64_t)m * ldy + n0 + r] = (bf16)sum;
+  }
+}
+
 }  // namespace
 
+constexpr int GEMV_MAX_M = 2, GEMV_MAX_K = 16 * 1024, GEMV_ROWS = 8;
+
 bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K) {
-  return M >= 1 && M <= 64 && N % 16 == 0 && N > 0 && K % (32 * SG_WAVES) == 0 && K > 0;
+  if (M < 1 || M > 64 || N <= 0 || K <= 0) return false;
+  if (M <= GEMV_MAX_M && K <= GEMV_MAX_K && K % 8 == 0) return N % GEMV_ROWS == 0;
+  return N % 16 == 0 && K % (32 * SG_WAVES) == 0;
 }
 
 void skinny_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, int64_t ldy, int M, int N, int K,
@@ -359,6 +427,12 @@ void skinny_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
   const bf16* xb = (const bf16*)x;
   const bf16* wb = (const bf16*)w;
   bf16* yb = (bf16*)y;
+  if (M <= GEMV_MAX_M && K <= GEMV_MAX_K && K % 8 == 0) {
+    const dim3 ggrid((unsigned)(N / GEMV_ROWS)), gblock((unsigned)(64 * cdiv(K, 1024)));   // a wave per 1024 of K
+    if (M == 1) hipLaunchKernelGGL(gemv_k<1>, ggrid, gblock, 0, st, xb, ldx, wb, ldw, yb, ldy, K);
+    else hipLaunchKernelGGL(gemv_k<2>, ggrid, gblock, 0, st, xb, ldx, wb, ldw, yb, ldy, K);
+    return;
+  }
   switch ((M + 15) / 16) {
     case 1: hipLaunchKernelGGL((skinny_gemm_k<1, 8>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
     case 2: hipLaunchKernelGGL((skinny_gemm_k<2, 8>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;

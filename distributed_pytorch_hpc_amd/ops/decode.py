@@ -85,10 +85,13 @@ def skinny_ok(x: torch.Tensor, mod: torch.nn.Module) -> bool:
         return False
     k, n = w.shape[1], w.shape[0]
     m = x.numel() // max(k, 1)
-    # where it measured faster than hipBLASLt (benchmarks/skinny_gemm_bench.py, profiles/serving/): at most 16 rows
-    # and N <= 8192 (wo / w2 of 7B: 1.4-1.9x); hipBLASLt's small-M tiles already stream the wide projections at
-    # 3.7-4.5 TB/s, and from 32 rows on its tiled reuse of x wins
-    return 1 <= m <= 16 and n <= 8192 and n % 16 == 0 and k % 256 == 0
+    # 1-2 rows: the GEMV form (any N % 8, K % 8, K <= 16384).  3-16 rows: the MFMA form where it measured faster than
+    # hipBLASLt (benchmarks/skinny_gemm_bench.py, profiles/serving/): N <= 8192 (wo / w2 of 7B: 1.4-1.9x);
+    # hipBLASLt's small-M tiles already stream the wide projections at 3.7-4.5 TB/s, and from 32 rows on its tiled
+    # reuse of x wins
+    if m <= 2:
+        return m >= 1 and n % 8 == 0 and k % 8 == 0 and k <= 16384
+    return m <= 16 and n <= 8192 and n % 16 == 0 and k % 256 == 0
 
 
 def skinny_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:

@@ -89,11 +89,13 @@ def test_generator_graph_replay_matches_eager(dph_native):
     assert g.generate(prompts, 24) == eager          # the captured graph is reused after reset
 
 
-@pytest.mark.parametrize("m", [1, 5, 16, 17, 40, 64])
-@pytest.mark.parametrize("n,k", [(4096, 4096), (272, 11008), (96, 256)])
+@pytest.mark.parametrize("m", [1, 2, 5, 16, 17, 40, 64])
+@pytest.mark.parametrize("n,k", [(4096, 4096), (272, 11008), (96, 256), (40, 1000)])
 def test_skinny_linear_matches_fp32(dph_native, m, n, k):
     from distributed_pytorch_hpc_amd.ops.decode import skinny_linear
 
+    if (n % 16 or k % 256) and m > 2:
+        pytest.skip("shape covered by the GEMV form only (1-2 rows)")
     g = torch.Generator(device="cuda").manual_seed(m + n)
     x = torch.randn(m, k, device="cuda", generator=g).to(torch.bfloat16)
     w = (torch.randn(n, k, device="cuda", generator=g) / k ** 0.5).to(torch.bfloat16)
