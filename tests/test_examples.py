@@ -44,6 +44,9 @@ CASES = [
                                                       "--seq-len", "32", "--model", "tiny"]),
     ("07_domain_parallel/domain_parallel_unet.py", 2, ["--lat", "32", "--lon", "32", "--channels", "3",
                                                        "--base-dim", "8", "--steps", "2", "--check"]),
+    ("08_serving/generate_llama.py", 2, ["--batch", "2", "--prompt-len", "8", "--max-new", "6"]),
+    ("08_serving/generate_llama.py", 1, ["--batch", "3", "--prompt-len", "5", "--max-new", "4", "--temperature",
+                                         "0.8", "--top-k", "20"]),
     ("resnet_benchmark.py", 2, ["--arch", "resnet18", "--batch-size", "4", "--image-size", "32", "--epochs", "2",
                                 "--steps-syn", "1"]),
 ]
