@@ -101,6 +101,52 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_big_k(const T* __restrict__ x
   }
 }
 
+// Few rows (decode: one per sequence): one 256-thread workgroup per row instead of one wave, and the weight loads
+// issued together with x / residual -- one memory round trip instead of two, 4 waves per row instead of 1.
+// CPT = 16-B chunks per thread (D <= CPT * 2048).
+template <typename T, typename W, int CPT, bool RES>
+__global__ __launch_bounds__(256) void rmsnorm_fwd_row_k(const T* __restrict__ x, const W* __restrict__ w,
+                                                         const T* __restrict__ res, T* __restrict__ h_out,
+                                                         T* __restrict__ y, float* __restrict__ rstd, int D,
+                                                         float eps) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  float v[CPT][8], wv[CPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int idx = (c * 256 + threadIdx.x) * 8;
+    if (idx < D) {
+      Vec8<T>::load(x + r * D + idx, v[c]);
+      Vec8<W>::load(w + idx, wv[c]);
+      if (RES) {
+        float rr[8];
+        Vec8<T>::load(res + r * D + idx, rr);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[c][i] = (float)(T)(v[c][i] + rr[i]);   // h rounded as stored
+        Vec8<T>::store(h_out + r * D + idx, v[c]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+    }
+  }
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float rs = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)D + eps);
+  if (threadIdx.x == 0 && rstd) rstd[r] = rs;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int idx = (c * 256 + threadIdx.x) * 8;
+    if (idx < D) {
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = v[c][i] * rs * wv[c][i];
+      Vec8<T>::store(y + r * D + idx, o);
+    }
+  }
+}
+
 // Backward. CPT = 16-B chunks per thread (D <= CPT * 2048).
 template <typename T, typename W, int CPT>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_k(const T* __restrict__ dy, const T* __restrict__ x,
@@ -218,6 +264,18 @@ static void fwd_dispatch(const void* x, const void* w, const void* res, void* h_
   const int grid = stream_grid(rows, 4);
   const T* xp = (const T*)x; const W* wp = (const W*)w; const T* rp = (const T*)res;
   T* hp = (T*)h_out; T* yp = (T*)y;
+  if (rows <= 1024 && D <= 8192) {   // decode-sized: a workgroup per row
+#define ROWL(C)                                                                                                \
+  if (res) hipLaunchKernelGGL((rmsnorm_fwd_row_k<T, W, C, true>), dim3((unsigned)rows), dim3(256), 0, st, xp, wp, \
+                              rp, hp, yp, rstd, D, eps);                                                       \
+  else hipLaunchKernelGGL((rmsnorm_fwd_row_k<T, W, C, false>), dim3((unsigned)rows), dim3(256), 0, st, xp, wp, rp, \
+                          hp, yp, rstd, D, eps);
+    if (D <= 2048) { ROWL(1) }
+    else if (D <= 4096) { ROWL(2) }
+    else { ROWL(4) }
+#undef ROWL
+    return;
+  }
 #define LAUNCH(N)                                                                                       \
   if (res) hipLaunchKernelGGL((rmsnorm_fwd_k<T, W, N, true>), dim3(grid), dim3(256), 0, st, xp, wp, rp, hp, yp, \
                               rstd, rows, D, eps);                                                      \

@@ -19,7 +19,8 @@ def rel_err(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize("rows,dim", [(1000, 4096), (257, 256), (64, 12288), (33, 1376)])
+@pytest.mark.parametrize("rows,dim", [(1000, 4096), (257, 256), (64, 12288), (33, 1376), (1, 4096), (8, 8192),
+                                      (3000, 4096), (5, 1000)])
 def test_rmsnorm(dph_native, rows, dim):
     torch.manual_seed(0)
     x = torch.randn(rows, dim, device=DEV, dtype=torch.bfloat16, requires_grad=True)
@@ -36,11 +37,12 @@ def test_rmsnorm(dph_native, rows, dim):
     assert rel_err(w.grad, wr.grad) < 2e-2
 
 
-def test_add_rmsnorm(dph_native):
+@pytest.mark.parametrize("rows,dim", [(300, 1024), (1, 4096), (3000, 1024)])   # row-per-workgroup / wave-per-row
+def test_add_rmsnorm(dph_native, rows, dim):
     torch.manual_seed(1)
-    x = torch.randn(300, 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    r = torch.randn(300, 1024, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    w = torch.rand(1024, device=DEV, dtype=torch.bfloat16).requires_grad_()
+    x = torch.randn(rows, dim, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(rows, dim, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    w = torch.rand(dim, device=DEV, dtype=torch.bfloat16).requires_grad_()
     h, y = ops.add_rms_norm(x, r, w, 1e-5)
     xr, rr, wr = (t.detach().float().requires_grad_() for t in (x, r, w))
     hr = xr + rr
