@@ -353,13 +353,23 @@ __global__ __launch_bounds__(64 * SG_WAVES) void skinny_gemm_k(const bf16* __res
 // per wave in flight, counted waits as the FMAs consume them; <= 128 VGPRs so 4 waves / SIMD stay resident), keeps
 // its 8 x values per chunk and m packed in registers, then each row's partial is reduced over the lanes and over
 // the waves through LDS.  K <= 16 waves x 1024.
-template <int M>
-__global__ __launch_bounds__(1024) void gemv_k(const bf16* __restrict__ x, int64_t ldx, const bf16* __restrict__ w,
-                                               int64_t ldw, bf16* __restrict__ y, int64_t ldy, int K) {
+//
+// The x operand can be PRODUCED in the kernel while the W loads are in flight (decode is launch-latency bound at
+// batch 1, ~4 us per small kernel): XM = GX_SWIGLU reads the fused [gate | up] w13 output and forms silu(g) * u
+// (the w2 input), XM = GX_NORM forms RMSNorm(x + res) * g (the wqkv / w13 / LM-head input; the sum of squares is
+// reduced over the workgroup's waves, every workgroup recomputes it from L2) and workgroup 0 writes h = x + res
+// for the residual stream.  Both round to bf16 where the separate kernels store, so the fused and unfused paths
+// agree to the rounding of the sum-of-squares order.
+enum { GX_PLAIN = 0, GX_SWIGLU = 1, GX_NORM = 2 };
+
+template <int M, int XM>
+__global__ __launch_bounds__(1024) void gemv_k(GemvArgs a) {
   constexpr int R = 8, C = 2;
   __shared__ float red[16][R * M];
+  __shared__ float nred[16][M];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int n0 = blockIdx.x * R;
+  const int K = a.K;
   int kc[C];
   bool cv[C];
 #pragma unroll
@@ -368,19 +378,81 @@ __global__ __launch_bounds__(1024) void gemv_k(const bf16* __restrict__ x, int64
     cv[c] = k < K;
     kc[c] = cv[c] ? k : 0;   // out-of-range lanes read column 0 and contribute zero
   }
+  const bf16* w = (const bf16*)a.w;
   bf16x8 wr[R][C];
 #pragma unroll
   for (int r = 0; r < R; ++r)
 #pragma unroll
-    for (int c = 0; c < C; ++c) wr[r][c] = *reinterpret_cast<const bf16x8*>(w + (int64_t)(n0 + r) * ldw + kc[c]);
+    for (int c = 0; c < C; ++c) wr[r][c] = *reinterpret_cast<const bf16x8*>(w + (int64_t)(n0 + r) * a.ldw + kc[c]);
+
+  const bf16* x = (const bf16*)a.x;
   bf16x8 xs[C][M];
+  if constexpr (XM == GX_PLAIN) {
 #pragma unroll
-  for (int c = 0; c < C; ++c)
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int m = 0; m < M; ++m) xs[c][m] = *reinterpret_cast<const bf16x8*>(x + (int64_t)m * a.ldx + kc[c]);
+  } else if constexpr (XM == GX_SWIGLU) {
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float g[8], u[8];
+        Vec8<bf16>::load(x + (int64_t)m * a.ldx + kc[c], g);
+        Vec8<bf16>::load(x + (int64_t)m * a.ldx + K + kc[c], u);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xs[c][m][e] = (bf16)(g[e] * (1.f / (1.f + __expf(-g[e]))) * u[e]);
+      }
+  } else {
+    const bf16* res = (const bf16*)a.res;
+    float hv[C][M][8], ss[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) ss[m] = 0.f;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        Vec8<bf16>::load(x + (int64_t)m * a.ldx + kc[c], hv[c][m]);
+        if (res) {
+          float rr[8];
+          Vec8<bf16>::load(res + (int64_t)m * a.ldres + kc[c], rr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hv[c][m][e] = (float)(bf16)(hv[c][m][e] + rr[e]);   // h rounded as stored
+          if (a.h_out && blockIdx.x == 0 && cv[c]) Vec8<bf16>::store((bf16*)a.h_out + (int64_t)m * a.ldh + kc[c], hv[c][m]);
+        }
+        if (cv[c]) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ss[m] += hv[c][m][e] * hv[c][m][e];
+        }
+      }
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      xs[c][m] = *reinterpret_cast<const bf16x8*>(x + (int64_t)m * ldx + kc[c]);
-      if (!cv[c]) xs[c][m] = bf16x8{};
+      const float v = wave_sum(ss[m]);
+      if (lane == 0) nred[wave][m] = v;
     }
+    __syncthreads();
+    const bf16* gw = (const bf16*)a.g;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      float gv[8];
+      Vec8<bf16>::load(gw + kc[c], gv);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        float tot = 0.f;
+        for (int v = 0; v < nw; ++v) tot += nred[v][m];
+        const float rs = rsqrtf(tot / (float)K + a.eps);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xs[c][m][e] = (bf16)(hv[c][m][e] * rs * gv[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c)
+    if (!cv[c]) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) xs[c][m] = bf16x8{};
+    }
+
   float acc[R][M];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -407,13 +479,32 @@ __global__ __launch_bounds__(1024) void gemv_k(const bf16* __restrict__ x, int64
     float sum = 0.f;
     for (int v = 0; v < nw; ++v) sum += red[v][threadIdx.x];
     const int r = threadIdx.x / M, m = threadIdx.x % M;
-    y[(int64_t)m * ldy + n0 + r] = (bf16)sum;
+    ((bf16*)a.y)[(int64_t)m * a.ldy + n0 + r] = (bf16)sum;
   }
 }
 
 }  // namespace
 
 constexpr int GEMV_MAX_M = 2, GEMV_MAX_K = 16 * 1024, GEMV_ROWS = 8;
+
+bool gemv_supported(int64_t M, int64_t N, int64_t K) {
+  return M >= 1 && M <= GEMV_MAX_M && N > 0 && N % GEMV_ROWS == 0 && K > 0 && K <= GEMV_MAX_K && K % 8 == 0;
+}
+
+void gemv(const GemvArgs& a, int xmode, hipStream_t st) {
+  const dim3 grid((unsigned)(a.N / GEMV_ROWS)), block((unsigned)(64 * cdiv(a.K, 1024)));   // a wave per 1024 of K
+#define DPH_GEMV(M_, XM_) hipLaunchKernelGGL((gemv_k<M_, XM_>), grid, block, 0, st, a)
+#define DPH_GEMV_M(XM_)          \
+  do {                           \
+    if (a.M == 1) DPH_GEMV(1, XM_); \
+    else DPH_GEMV(2, XM_);       \
+  } while (0)
+  if (xmode == GX_SWIGLU) DPH_GEMV_M(GX_SWIGLU);
+  else if (xmode == GX_NORM) DPH_GEMV(1, GX_NORM);   // one row only (two rows spill; callers check)
+  else DPH_GEMV_M(GX_PLAIN);
+#undef DPH_GEMV_M
+#undef DPH_GEMV
+}
 
 bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K) {
   if (M < 1 || M > 64 || N <= 0 || K <= 0) return false;
@@ -428,9 +519,9 @@ void skinny_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
   const bf16* wb = (const bf16*)w;
   bf16* yb = (bf16*)y;
   if (M <= GEMV_MAX_M && K <= GEMV_MAX_K && K % 8 == 0) {
-    const dim3 ggrid((unsigned)(N / GEMV_ROWS)), gblock((unsigned)(64 * cdiv(K, 1024)));   // a wave per 1024 of K
-    if (M == 1) hipLaunchKernelGGL(gemv_k<1>, ggrid, gblock, 0, st, xb, ldx, wb, ldw, yb, ldy, K);
-    else hipLaunchKernelGGL(gemv_k<2>, ggrid, gblock, 0, st, xb, ldx, wb, ldw, yb, ldy, K);
+    GemvArgs a{};
+    a.x = x; a.ldx = ldx; a.w = w; a.ldw = ldw; a.y = y; a.ldy = ldy; a.M = M; a.N = N; a.K = K;
+    gemv(a, GX_PLAIN, st);
     return;
   }
   switch ((M + 15) / 16) {

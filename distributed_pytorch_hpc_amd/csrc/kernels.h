@@ -200,6 +200,19 @@ int decode_heads_per_wave(int Hq, int Hkv);
 void decode_attention(const DecodeParams& p, hipStream_t stream);
 // y[M, N] = x[M, K] W[N, K]^T for decode-sized M (<= 64): bf16, rows of x / W / y at strides ldx / ldw / ldy.
 bool skinny_gemm_supported(int64_t M, int64_t N, int64_t K);
+// GEMV (M <= 2 rows) with the x operand optionally produced in the kernel: xmode 0 = x [M, K]; 1 = silu(gate) * up
+// from x = [M, 2K] (gate | up); 2 = RMSNorm(x + res) * g (res, h_out optional; h_out = x + res written once).
+struct GemvArgs {
+  const void* x; int64_t ldx;
+  const void* res; int64_t ldres;
+  const void* g; float eps;
+  void* h_out; int64_t ldh;
+  const void* w; int64_t ldw;
+  void* y; int64_t ldy;
+  int M, N, K;
+};
+bool gemv_supported(int64_t M, int64_t N, int64_t K);
+void gemv(const GemvArgs& a, int xmode, hipStream_t stream);
 void skinny_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y, int64_t ldy, int M, int N, int K,
                  hipStream_t stream);
 

@@ -490,6 +490,59 @@ Tensor skinny_linear(const Tensor& x, const Tensor& w) {
   return y;
 }
 
+Tensor gemv_swiglu(const Tensor& x2, const Tensor& w) {
+  c10::DeviceGuard g(x2.device());
+  TORCH_CHECK(x2.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 && w.dim() == 2 &&
+                  w.is_contiguous(), "gemv_swiglu: bf16, w [N, K] contiguous");
+  const int64_t K = w.size(1), N = w.size(0);
+  TORCH_CHECK(x2.size(-1) == 2 * K, "gemv_swiglu: x2 must be [..., 2K] (gate | up)");
+  const int64_t M = x2.numel() / (2 * K);
+  TORCH_CHECK(dph::gemv_supported(M, N, K), "gemv_swiglu: needs 1-2 rows, N % 8, K % 8, K <= 16384");
+  auto xr = x2.reshape({M, 2 * K});
+  TORCH_CHECK(xr.stride(1) == 1 && xr.stride(0) % 8 == 0, "gemv_swiglu: rows must be contiguous");
+  check_align16(xr, "x2"); check_align16(w, "w");
+  auto sizes = x2.sizes().vec();
+  sizes.back() = N;
+  auto y = at::empty(sizes, x2.options());
+  dph::GemvArgs a{};
+  a.x = xr.data_ptr(); a.ldx = xr.stride(0); a.w = w.data_ptr(); a.ldw = K; a.y = y.data_ptr(); a.ldy = N;
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  dph::gemv(a, 1, cur_stream());
+  return y;
+}
+
+std::tuple<Tensor, Tensor> gemv_rmsnorm(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& gw, double eps,
+                                        const Tensor& w) {
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 && gw.scalar_type() == at::kBFloat16,
+              "gemv_rmsnorm: bf16 x, norm weight and w");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && gw.is_contiguous() && gw.numel() == w.size(1),
+              "gemv_rmsnorm: w [N, K] contiguous, norm weight [K]");
+  const int64_t K = w.size(1), N = w.size(0);
+  TORCH_CHECK(x.size(-1) == K && x.numel() == K, "gemv_rmsnorm: exactly one row of K");
+  TORCH_CHECK(dph::gemv_supported(1, N, K), "gemv_rmsnorm: needs N % 8, K % 8, K <= 16384");
+  auto xr = x.reshape({1, K}).contiguous();
+  check_align16(xr, "x"); check_align16(w, "w"); check_align16(gw, "norm weight");
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  auto y = at::empty(sizes, x.options());
+  dph::GemvArgs a{};
+  a.x = xr.data_ptr(); a.ldx = K; a.g = gw.data_ptr(); a.eps = (float)eps;
+  Tensor h;
+  if (res.has_value() && res->defined()) {
+    TORCH_CHECK(res->sizes() == x.sizes() && res->scalar_type() == at::kBFloat16, "gemv_rmsnorm: residual shape");
+    auto rr = res->reshape({1, K}).contiguous();
+    check_align16(rr, "res");
+    h = at::empty_like(x);
+    a.res = rr.data_ptr(); a.ldres = K; a.h_out = h.data_ptr(); a.ldh = K;
+  } else {
+    h = at::empty({0}, x.options());   // no residual: h is x itself (not returned as an alias)
+  }
+  a.w = w.data_ptr(); a.ldw = K; a.y = y.data_ptr(); a.ldy = N; a.M = 1; a.N = (int)N; a.K = (int)K;
+  dph::gemv(a, 2, cur_stream());
+  return {y, h};
+}
+
 // ------------------------------------------------------------------------------------------------ embedding
 Tensor embedding_fwd(const Tensor& ids, const Tensor& table, int64_t vocab_start) {
   c10::DeviceGuard g(table.device());
@@ -874,6 +927,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("decode_attention(Tensor qkv, Tensor k_cache, Tensor v_cache, Tensor pos, int n_heads, int n_kv_heads, "
         "float scale, int max_len) -> Tensor");
   m.def("skinny_linear(Tensor x, Tensor w) -> Tensor");
+  m.def("gemv_swiglu(Tensor x2, Tensor w) -> Tensor");
+  m.def("gemv_rmsnorm(Tensor x, Tensor? res, Tensor norm_weight, float eps, Tensor w) -> (Tensor, Tensor)");
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
@@ -925,6 +980,8 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("kv_append_", &kv_append_);
   m.impl("decode_attention", &decode_attention);
   m.impl("skinny_linear", &skinny_linear);
+  m.impl("gemv_swiglu", &gemv_swiglu);
+  m.impl("gemv_rmsnorm", &gemv_rmsnorm);
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("gemm_tn_", &gemm_tn_);

@@ -135,13 +135,18 @@ class Attention(nn.Module):
         qkv = _proj(self.wqkv, x)
         cos, sin = rope_tables(self.head_dim, self.max_pos, self.theta, qkv.device)
         if cache is not None:
-            return _proj(self.wo, self._cached_attention(qkv.contiguous(), cos, sin, cache, layer))
+            return self.decode_from_qkv(qkv, cache, layer)
         if self.cp_attention is not None:
             o = self.cp_attention(qkv, cos, sin, self.n_local_heads, self.n_local_kv_heads, self.head_dim)
         else:
             o = ops.rope_attention(qkv, cos, sin, self.n_local_heads, self.n_local_kv_heads, self.head_dim,
                                    causal=True, pos_offset=pos_offset)
         return _proj(self.wo, o)
+
+    def decode_from_qkv(self, qkv: torch.Tensor, cache: "KVCache", layer: int) -> torch.Tensor:
+        """Serving: cached attention of an already projected qkv, then the output projection."""
+        cos, sin = rope_tables(self.head_dim, self.max_pos, self.theta, qkv.device)
+        return _proj(self.wo, self._cached_attention(qkv.contiguous(), cos, sin, cache, layer))
 
     def _cached_attention(self, qkv, cos, sin, cache: "KVCache", layer: int) -> torch.Tensor:
         """Serving path: append this step's k / v (RoPE at each sequence's cache position) and attend over the cache.
@@ -205,6 +210,16 @@ class TransformerBlock(nn.Module):
         """Takes the residual stream as (x, delta) with x + delta = reference block input and returns
         (h, ffn_out) with h + ffn_out = reference block output (the final add is deferred into the next
         norm).  ``forward(x)`` with delta None is the plain reference input; ``cache`` selects the serving path."""
+        att, ff = self.attention, self.feed_forward
+        if cache is not None and decode_ops.fused_decode_ok(x, self.attention_norm, self.ffn_norm, att.wqkv, ff.w13,
+                                                            ff.w2):
+            # batch-1 decode: the norms and SwiGLU are computed inside the projection kernels (one launch each
+            # instead of two; decode_ops.gemv_rmsnorm / gemv_swiglu)
+            qkv, r = decode_ops.gemv_rmsnorm(x, delta, self.attention_norm.weight, self.attention_norm.eps,
+                                             att.wqkv.weight)
+            attn = att.decode_from_qkv(qkv, cache, self.layer_id)
+            f13, h = decode_ops.gemv_rmsnorm(r, attn, self.ffn_norm.weight, self.ffn_norm.eps, ff.w13.weight)
+            return h, decode_ops.gemv_swiglu(f13, ff.w2.weight)
         if delta is None:
             r, a = x, self.attention_norm(x)
         else:
@@ -290,7 +305,11 @@ class Transformer(nn.Module):
         if last_only and s > 1:
             h = h[:, -1:].contiguous()
             delta = delta[:, -1:].contiguous() if delta is not None else None
-        logits = self.head(h, delta)
+        if not (self.loss_parallel and self.tp_group is not None) and decode_ops.fused_decode_ok(h, self.norm,
+                                                                                                  self.output):
+            logits = decode_ops.gemv_rmsnorm(h, delta, self.norm.weight, self.norm.eps, self.output.weight)[0].float()
+        else:
+            logits = self.head(h, delta)
         cache.advance(s)
         return logits[:, -1] if last_only else logits
 

@@ -192,3 +192,13 @@ def _decode_attn(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale, max_len
 @register_fake("dph::skinny_linear")
 def _skinny_linear(x, w):
     return x.new_empty((*x.shape[:-1], w.shape[0]))
+
+
+@register_fake("dph::gemv_swiglu")
+def _gemv_swiglu(x2, w):
+    return x2.new_empty((*x2.shape[:-1], w.shape[0]))
+
+
+@register_fake("dph::gemv_rmsnorm")
+def _gemv_rmsnorm(x, res, norm_weight, eps, w):
+    return x.new_empty((*x.shape[:-1], w.shape[0])), (torch.empty_like(x) if res is not None else x.new_empty((0,)))

@@ -97,3 +97,34 @@ def skinny_ok(x: torch.Tensor, mod: torch.nn.Module) -> bool:
 def skinny_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """x [..., K] @ w[N, K]^T for at most 64 rows (decode): streams W once at HBM rate (csrc/decode.hip)."""
     return _lib.ops().skinny_linear(x, w)
+
+
+def _plain(mod) -> bool:
+    return not mod._forward_hooks and not mod._forward_pre_hooks
+
+
+def fused_decode_ok(x: torch.Tensor, *mods) -> bool:
+    """One decode row (batch 1) on the GPU with plain bias-free bf16 nn.Linear / norm modules: the producer-fused
+    GEMV path (RMSNorm or SwiGLU computed inside the projection kernel) applies."""
+    if not x.is_cuda or _lib.reference_mode() or x.dtype != torch.bfloat16 or x.numel() != x.shape[-1]:
+        return False
+    for m in mods:
+        w = getattr(m, "weight", None)
+        if w is None or not _plain(m) or getattr(m, "bias", None) is not None or w.dtype != torch.bfloat16:
+            return False
+        if w.dim() == 2 and type(m) is not torch.nn.Linear:   # tensor-parallel wrappers do collectives in forward
+            return False
+        if not w.is_contiguous() or (w.dim() == 2 and (w.shape[0] % 8 or w.shape[1] % 8 or w.shape[1] > 16384)):
+            return False
+    return True
+
+
+def gemv_rmsnorm(x: torch.Tensor, res: torch.Tensor | None, norm_weight: torch.Tensor, eps: float, w: torch.Tensor):
+    """(RMSNorm(x + res) * g) @ w^T for one row, the norm computed inside the GEMV kernel; returns (y, h = x + res)."""
+    y, h = _lib.ops().gemv_rmsnorm(x, res, norm_weight, eps, w)
+    return y, (x if res is None else h)
+
+
+def gemv_swiglu(x2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """(silu(gate) * up) @ w^T for 1-2 rows of the fused [gate | up] projection output."""
+    return _lib.ops().gemv_swiglu(x2, w)

@@ -105,3 +105,49 @@ def test_skinny_linear_matches_fp32(dph_native, m, n, k):
     # strided rows (a view into a wider buffer) and a leading batch shape
     xb = torch.randn(m, 1, k + 256, device="cuda", generator=g).to(torch.bfloat16)[..., :k]
     torch.testing.assert_close(skinny_linear(xb, w).float(), (xb.float() @ w.float().t()), atol=2e-2, rtol=2e-2)
+
+
+def test_producer_fused_gemv_matches_composition(dph_native):
+    """RMSNorm(x + res) and SwiGLU computed inside the GEMV equal the separate kernels followed by the projection."""
+    from distributed_pytorch_hpc_amd import ops
+    from distributed_pytorch_hpc_amd.ops.decode import gemv_rmsnorm, gemv_swiglu, skinny_linear
+
+    g = torch.Generator(device="cuda").manual_seed(7)
+    k, n = 4096, 1024
+    x = torch.randn(1, 1, k, device="cuda", generator=g).to(torch.bfloat16)
+    res = torch.randn(1, 1, k, device="cuda", generator=g).to(torch.bfloat16)
+    nw = (1 + 0.1 * torch.randn(k, device="cuda", generator=g)).to(torch.bfloat16)
+    w = (torch.randn(n, k, device="cuda", generator=g) / k ** 0.5).to(torch.bfloat16)
+    y, h = gemv_rmsnorm(x, res, nw, 1e-5, w)
+    h_ref, a_ref = ops.add_rms_norm(x, res, nw, 1e-5)
+    assert torch.equal(h, h_ref)
+    torch.testing.assert_close(y.float(), skinny_linear(a_ref, w).float(), atol=2e-2, rtol=2e-2)
+    y0, h0 = gemv_rmsnorm(x, None, nw, 1e-5, w)
+    assert h0 is x
+    torch.testing.assert_close(y0.float(), skinny_linear(ops.rms_norm(x, nw, 1e-5), w).float(), atol=2e-2, rtol=2e-2)
+    for m in (1, 2):
+        x2 = torch.randn(m, 1, 2 * 11008, device="cuda", generator=g).to(torch.bfloat16)
+        w2 = (torch.randn(4096, 11008, device="cuda", generator=g) / 11008 ** 0.5).to(torch.bfloat16)
+        torch.testing.assert_close(gemv_swiglu(x2, w2).float(), skinny_linear(ops.swiglu(x2), w2).float(), atol=2e-2,
+                                   rtol=2e-2)
+
+
+def test_batch1_fused_decode_matches_unfused(dph_native, monkeypatch):
+    from distributed_pytorch_hpc_amd.models.llama2 import KVCache
+    from distributed_pytorch_hpc_amd.ops import decode as decode_ops
+
+    m = _tiny_llama(seed=5)
+    t = torch.randint(0, 512, (1, 40), device="cuda", generator=torch.Generator(device="cuda").manual_seed(2))
+
+    def run():
+        c = KVCache(m, 1, 64)
+        out = [m.forward_inference(t[:, :32], c)]
+        for i in range(32, 40):
+            out.append(m.forward_inference(t[:, i:i + 1], c))
+        return torch.stack(out, 1)
+
+    fused = run()
+    monkeypatch.setattr(decode_ops, "fused_decode_ok", lambda *a, **k: False)
+    plain = run()
+    assert (fused - plain).norm() / plain.norm() < 1e-2
+    assert torch.equal(fused.argmax(-1), plain.argmax(-1))
