@@ -1,4 +1,4 @@
 """Serving: KV-cache generation for the Llama decoder (beyond the training-only reference)."""
-from .generator import Generator
+from .generator import ContinuousBatcher, Generator, Request
 
-__all__ = ["Generator"]
+__all__ = ["ContinuousBatcher", "Generator", "Request"]

@@ -15,6 +15,7 @@ The reference trains only (its llama2_model.py has no KV cache); this is the ser
 """
 from __future__ import annotations
 
+from dataclasses import dataclass, field
 from typing import Optional, Sequence
 
 import torch
@@ -29,7 +30,12 @@ class Generator:
         self.cache = KVCache(model, batch, max_len, dtype=dtype)
         dev = self.cache.pos.device
         self.device = dev
-        self.graphs = (dev.type == "cuda") if graphs is None else bool(graphs)
+        if graphs is None:
+            # multi-rank (tensor-parallel) steps would capture their RCCL all-reduces: eager unless asked for
+            multi = torch.distributed.is_available() and torch.distributed.is_initialized() and \
+                torch.distributed.get_world_size() > 1
+            graphs = dev.type == "cuda" and not multi
+        self.graphs = bool(graphs)
         if self.graphs and dev.type != "cuda":
             raise ValueError("Generator: HIP graphs need the model on a GPU")
         self._graph: Optional[torch.cuda.CUDAGraph] = None
@@ -130,3 +136,96 @@ class Generator:
                 break
             logits = self.decode(tok)
         return rows
+
+
+@dataclass
+class Request:
+    prompt: list
+    max_new_tokens: int
+    eos_id: Optional[int] = None
+    output: list = field(default_factory=list)   # generated ids
+    done: bool = False
+
+    def _push(self, tok: int) -> None:
+        self.output.append(tok)
+        self.done = len(self.output) >= self.max_new_tokens or (self.eos_id is not None and tok == self.eos_id)
+
+
+class ContinuousBatcher:
+    """A stream of requests served on the Generator's fixed cache slots.
+
+    Every ``step()`` admits waiting requests into free slots (per-slot prefill into ``KVCache.slot(i)`` while the
+    other sequences keep their caches), then runs ONE decode step for the whole batch -- the same captured HIP graph
+    every time, since positions live on the device -- and samples the next token of every active sequence.  A
+    sequence that reaches its eos or token budget frees its slot for the next request on the following step.  Idle
+    slots decode garbage that is never read; their position is reset each step so they never fill up.
+
+        cb = ContinuousBatcher(Generator(model, batch=8, max_len=4096))
+        for p in prompts: cb.submit(p, max_new_tokens=128)
+        finished = cb.run()
+    """
+
+    def __init__(self, generator: Generator, temperature: float = 0.0, top_k: Optional[int] = None,
+                 rng: Optional[torch.Generator] = None):
+        self.gen = generator
+        self.temperature, self.top_k, self.rng = temperature, top_k, rng
+        self.slots: list = [None] * generator.batch
+        self.queue: list = []
+        self._next = torch.zeros(generator.batch, dtype=torch.long, device=generator.device)
+        generator.reset()
+
+    def submit(self, prompt: Sequence[int], max_new_tokens: int, eos_id: Optional[int] = None) -> Request:
+        if not prompt or max_new_tokens < 1:
+            raise ValueError("ContinuousBatcher: empty prompt or no tokens requested")
+        if len(prompt) + max_new_tokens > self.gen.cache.max_len + 1:
+            raise ValueError(f"request of {len(prompt)} + {max_new_tokens} tokens exceeds the cache "
+                             f"({self.gen.cache.max_len})")
+        r = Request(list(prompt), max_new_tokens, eos_id)
+        self.queue.append(r)
+        return r
+
+    @property
+    def active(self) -> int:
+        return sum(r is not None for r in self.slots)
+
+    @torch.no_grad()
+    def step(self) -> list:
+        """Admit, decode one token for every active sequence; returns the requests finished in this step."""
+        cache, finished = self.gen.cache, []
+        for i in range(len(self.slots)):
+            if self.slots[i] is None and self.queue:
+                r = self.queue.pop(0)
+                cache.reset_slot(i)
+                ids = torch.tensor([r.prompt], dtype=torch.long, device=self.gen.device)
+                logits = self.gen.model.forward_inference(ids, cache.slot(i))
+                tok = int(Generator.sample(logits, self.temperature, self.top_k, self.rng)[0])
+                r._push(tok)
+                if r.done:
+                    finished.append(r)
+                else:
+                    self.slots[i] = r
+                    self._next[i] = tok
+        if self.active == 0:
+            return finished
+        for i, r in enumerate(self.slots):
+            if r is None:
+                cache.reset_slot(i)
+        logits = self.gen.decode(self._next)
+        toks = Generator.sample(logits, self.temperature, self.top_k, self.rng)
+        self._next.copy_(toks)
+        for i, t in enumerate(toks.tolist()):
+            r = self.slots[i]
+            if r is None:
+                continue
+            r._push(t)
+            if r.done:
+                finished.append(r)
+                self.slots[i] = None
+        return finished
+
+    def run(self) -> list:
+        """Serve until the queue is empty and every slot is idle; returns the requests in completion order."""
+        out = []
+        while self.queue or self.active:
+            out.extend(self.step())
+        return out

@@ -362,6 +362,12 @@ class KVCache:
         self.pos.zero_()
         self.lengths = [0] * self.batch
 
+    def reset_slot(self, i: int) -> None:
+        """Empty sequence slot i (continuous batching: a finished sequence's slot takes the next request)."""
+        self.pos[i] = 0
+        if self.lengths is not None:
+            self.lengths[i] = 0
+
     def slot(self, i: int) -> "KVCache":
         view = object.__new__(KVCache)
         view.k, view.v, view.pos = self.k[:, i:i + 1], self.v[:, i:i + 1], self.pos[i:i + 1]

@@ -151,3 +151,21 @@ def test_batch1_fused_decode_matches_unfused(dph_native, monkeypatch):
     plain = run()
     assert (fused - plain).norm() / plain.norm() < 1e-2
     assert torch.equal(fused.argmax(-1), plain.argmax(-1))
+
+
+def test_continuous_batching_graphs_match_eager(dph_native):
+    from distributed_pytorch_hpc_amd.inference import ContinuousBatcher, Generator
+
+    m = _tiny_llama(seed=9)
+    reqs = [([5, 6, 7], 9), ([8, 9, 10, 11, 12, 13, 14], 4), ([15], 12), ([16, 17], 2), ([18, 19, 20, 21], 7)]
+
+    def serve(graphs):
+        cb = ContinuousBatcher(Generator(m, 2, 32, graphs=graphs))
+        hs = [cb.submit(p, n) for p, n in reqs]
+        cb.run()
+        return [h.output for h in hs], cb.gen._graph is not None
+
+    eager, _ = serve(False)
+    graphed, captured = serve(True)
+    assert captured and graphed == eager
+    assert [len(o) for o in eager] == [n for _, n in reqs]

@@ -106,3 +106,18 @@ def test_tensor_parallel_generation_matches_single_process():
     ref = Generator(_model(vocab=96), 2, 32).generate([[1, 2, 3, 4, 5], [7, 8, 9, 10, 11]], 6)
     for out in run_distributed(_tp_generate_worker, 2):
         assert out == ref
+
+
+def test_continuous_batching_matches_one_request_at_a_time():
+    """5 requests of different lengths on 2 cache slots: every output equals that request generated alone."""
+    from distributed_pytorch_hpc_amd.inference import ContinuousBatcher, Generator
+
+    m = _model()
+    reqs = [([1, 2, 3], 5), ([4, 5, 6, 7, 8, 9], 3), ([10], 6), ([11, 12], 1), ([13, 14, 15, 16], 4)]
+    cb = ContinuousBatcher(Generator(m, 2, 16))
+    handles = [cb.submit(p, n) for p, n in reqs]
+    done = cb.run()
+    assert len(done) == len(reqs) and all(h.done for h in handles) and cb.active == 0
+    solo = Generator(m, 1, 16)
+    for h, (p, n) in zip(handles, reqs):
+        assert h.prompt + h.output == solo.generate([p], n)[0]
