@@ -14,6 +14,9 @@
 //                      and writes bf16 o straight into the [B, Hq * D] input of the output projection.
 // Keys past a sequence's length re-read its last valid row (finite data) and get probability 0, so the cache never
 // needs clearing and every load stays inside the written region.
+#include <cstdio>
+#include <cstdlib>
+
 #include "dph_common.h"
 #include "kernels.h"
 
@@ -249,11 +252,11 @@ void decode_attention(const DecodeParams& p, hipStream_t st) {
 // ==================================================================================================
 // Skinny GEMM for decode: y[M, N] = x[M, K] W[N, K]^T with M <= 64 (one token per sequence), bf16, fp32 accumulate.
 // Pure weight streaming (2 N K bytes read once, x re-read from L2): hipBLASLt's small-M tiles ran the Llama-2-7B
-// decode projections at 2.6-3.7 TB/s (profiles/serving/).  One workgroup = 16 output rows (n) x all M, 8 waves
+// decode projections at 2.6-3.7 TB/s (profiles/serving/).  One workgroup = 16 output rows (n) x all M, SG_WAVES waves
 // splitting K; each 16-row W tile goes straight from HBM into the A operand of v_mfma_f32_16x16x32_bf16 (lane l: row
 // l & 15, k 8 (l >> 4) .. +7 -- 64 contiguous bytes per row per instruction), x^T is the B operand, so the matrix
 // core does the k reduction and no shuffles are needed.  U unrolled k-steps keep U x 1 KiB of W in flight per wave;
-// the 8 partial tiles are summed through LDS.
+// the per-wave partial tiles are summed through LDS.
 // ==================================================================================================
 namespace {
 
@@ -261,17 +264,19 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-constexpr int SG_WAVES = 8;
+// default K split (workgroup = SG_WAVES waves) and unroll: the best of the (waves x unroll) sweep on every 7B
+// decode projection (profiles/serving/skinny_sweep/); DPH_SKINNY_CFG="waves,unroll" overrides
+constexpr int SG_WAVES = 4, SG_UNROLL = 4;
 
-template <int MT, int U>
-__global__ __launch_bounds__(64 * SG_WAVES) void skinny_gemm_k(const bf16* __restrict__ x, int64_t ldx,
-                                                              const bf16* __restrict__ w, int64_t ldw,
-                                                              bf16* __restrict__ y, int64_t ldy, int M, int K) {
-  __shared__ f32x4 red[SG_WAVES][MT][64];
+template <int MT, int U, int NWV = SG_WAVES>
+__global__ __launch_bounds__(64 * NWV) void skinny_gemm_k(const bf16* __restrict__ x, int64_t ldx,
+                                                         const bf16* __restrict__ w, int64_t ldw,
+                                                         bf16* __restrict__ y, int64_t ldy, int M, int K) {
+  __shared__ f32x4 red[NWV][MT][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16;
-  const int kq = K / SG_WAVES;
+  const int kq = K / NWV;
   const int kbeg = wave * kq;
   const bf16* wp = w + (int64_t)(n0 + r) * ldw + kbeg + 8 * g;
   const bf16* xp[MT];
@@ -336,7 +341,7 @@ __global__ __launch_bounds__(64 * SG_WAVES) void skinny_gemm_k(const bf16* __res
   if (wave < MT) {   // wave mt sums m-tile mt: C[n = 4 g + i][m = mt * 16 + r]
     f32x4 s = red[0][wave][lane];
 #pragma unroll
-    for (int v = 1; v < SG_WAVES; ++v) s += red[v][wave][lane];
+    for (int v = 1; v < NWV; ++v) s += red[v][wave][lane];
     const int m = wave * 16 + r;
     if (m < M) {
       bf16x4 o;
@@ -524,9 +529,36 @@ void skinny_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
     gemv(a, GX_PLAIN, st);
     return;
   }
-  switch ((M + 15) / 16) {
-    case 1: hipLaunchKernelGGL((skinny_gemm_k<1, 8>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
-    case 2: hipLaunchKernelGGL((skinny_gemm_k<2, 8>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
+  // DPH_SKINNY_CFG="waves,unroll" (A/B runs of benchmarks/skinny_gemm_bench.py): waves in {2, 4, 8}, unroll in {4, 8}
+  static int cfg_w = -1, cfg_u = -1;
+  if (cfg_w < 0) {
+    cfg_w = SG_WAVES; cfg_u = 0;
+    if (const char* e = getenv("DPH_SKINNY_CFG")) {
+      int a = 0, b = 0;
+      if (sscanf(e, "%d,%d", &a, &b) == 2 && (a == 2 || a == 4 || a == 8) && (b == 4 || b == 8)) { cfg_w = a; cfg_u = b; }
+    }
+  }
+  const int mt = (M + 15) / 16;
+  if (cfg_u != 0 && K % (32 * cfg_w) == 0) {
+    const dim3 blk(64 * cfg_w);
+#define DPH_SK(MT_, U_, W_) hipLaunchKernelGGL((skinny_gemm_k<MT_, U_, W_>), grid, blk, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K)
+#define DPH_SK_MT(U_, W_)                          \
+  do {                                             \
+    if (mt == 1) DPH_SK(1, U_, W_);                \
+    else if (mt == 2) DPH_SK(2, U_, W_);           \
+    else if (mt == 3) DPH_SK(3, 4, W_);            \
+    else DPH_SK(4, 4, W_);                         \
+  } while (0)
+    if (cfg_w == 2) { if (cfg_u == 4) DPH_SK_MT(4, 2); else DPH_SK_MT(8, 2); }
+    else if (cfg_w == 4) { if (cfg_u == 4) DPH_SK_MT(4, 4); else DPH_SK_MT(8, 4); }
+    else { if (cfg_u == 4) DPH_SK_MT(4, 8); else DPH_SK_MT(8, 8); }
+#undef DPH_SK_MT
+#undef DPH_SK
+    return;
+  }
+  switch (mt) {
+    case 1: hipLaunchKernelGGL((skinny_gemm_k<1, SG_UNROLL>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
+    case 2: hipLaunchKernelGGL((skinny_gemm_k<2, SG_UNROLL>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
     case 3: hipLaunchKernelGGL((skinny_gemm_k<3, 4>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
     default: hipLaunchKernelGGL((skinny_gemm_k<4, 4>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
   }

@@ -478,7 +478,7 @@ Tensor skinny_linear(const Tensor& x, const Tensor& w) {
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "skinny_linear: bf16 only");
   TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && x.size(-1) == w.size(1), "skinny_linear: w [N, K] contiguous");
   const int64_t K = w.size(1), N = w.size(0), M = x.numel() / std::max<int64_t>(K, 1);
-  TORCH_CHECK(dph::skinny_gemm_supported(M, N, K), "skinny_linear: needs rows <= 64 and (1-2 rows: N % 8, K % 8, K <= 16384; else N % 16, K % 256)");
+  TORCH_CHECK(dph::skinny_gemm_supported(M, N, K), "skinny_linear: needs rows <= 64 and (1-2 rows: N % 8, K % 8, K <= 16384; else N % 16, K % 128)");
   auto x2 = x.reshape({M, K});
   TORCH_CHECK(x2.stride(1) == 1 && x2.stride(0) % 8 == 0, "skinny_linear: x rows must be contiguous, 16-B aligned");
   check_align16(x2, "x"); check_align16(w, "w");

@@ -85,13 +85,15 @@ def skinny_ok(x: torch.Tensor, mod: torch.nn.Module) -> bool:
         return False
     k, n = w.shape[1], w.shape[0]
     m = x.numel() // max(k, 1)
-    # 1-2 rows: the GEMV form (any N % 8, K % 8, K <= 16384).  3-16 rows: the MFMA form where it measured faster than
-    # hipBLASLt (benchmarks/skinny_gemm_bench.py, profiles/serving/): N <= 8192 (wo / w2 of 7B: 1.4-1.9x);
-    # hipBLASLt's small-M tiles already stream the wide projections at 3.7-4.5 TB/s, and from 32 rows on its tiled
-    # reuse of x wins
+    # 1-2 rows: the GEMV form (any N % 8, K % 8, K <= 16384).  3-16 rows: the MFMA form (4 waves x unroll 4) where it
+    # measured faster than hipBLASLt (benchmarks/skinny_gemm_bench.py, profiles/serving/skinny_sweep/): every 7B
+    # projection up to 4 rows, up to 8 rows below N = 24 576 (wqkv, w13), up to 16 rows at N <= 8192 (wo, w2: 1.5-2x);
+    # the LM head from 8 rows and the wide projections from 16 rows stay on hipBLASLt's tiled reuse of x
     if m <= 2:
         return m >= 1 and n % 8 == 0 and k % 8 == 0 and k <= 16384
-    return m <= 16 and n <= 8192 and n % 16 == 0 and k % 256 == 0
+    if n % 16 or k % 128:
+        return False
+    return m <= 4 or (m <= 8 and n <= 24576) or (m <= 16 and n <= 8192)
 
 
 def skinny_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
