@@ -81,6 +81,9 @@ PRESETS = {
     "llama2-1b": ModelArgs(dim=2048, n_layers=16, n_heads=16, vocab_size=32000, max_seq_len=4096),
     "llama2-7b": ModelArgs(dim=4096, n_layers=32, n_heads=32, vocab_size=32000, max_seq_len=4096),
     "llama2-13b": ModelArgs(dim=5120, n_layers=40, n_heads=40, vocab_size=32000, max_seq_len=4096),
+    # GQA (8 KV heads), FFN 28 672: 69 B parameters, 138 GB in bf16 -- serving fits on ONE 288 GB MI355X
+    "llama2-70b": ModelArgs(dim=8192, n_layers=80, n_heads=64, n_kv_heads=8, vocab_size=32000, multiple_of=4096,
+                            ffn_dim_multiplier=1.3, max_seq_len=4096),
 }
 
 
@@ -211,15 +214,16 @@ class TransformerBlock(nn.Module):
         (h, ffn_out) with h + ffn_out = reference block output (the final add is deferred into the next
         norm).  ``forward(x)`` with delta None is the plain reference input; ``cache`` selects the serving path."""
         att, ff = self.attention, self.feed_forward
-        if cache is not None and decode_ops.fused_decode_ok(x, self.attention_norm, self.ffn_norm, att.wqkv, ff.w13,
-                                                            ff.w2):
-            # batch-1 decode: the norms and SwiGLU are computed inside the projection kernels (one launch each
-            # instead of two; decode_ops.gemv_rmsnorm / gemv_swiglu)
+        if cache is not None and decode_ops.fused_decode_ok(x, self.attention_norm, self.ffn_norm, att.wqkv, ff.w13):
+            # batch-1 decode: the norms (and SwiGLU where the GEMV covers w2's width) are computed inside the
+            # projection kernels (one launch each instead of two; decode_ops.gemv_rmsnorm / gemv_swiglu)
             qkv, r = decode_ops.gemv_rmsnorm(x, delta, self.attention_norm.weight, self.attention_norm.eps,
                                              att.wqkv.weight)
             attn = att.decode_from_qkv(qkv, cache, self.layer_id)
             f13, h = decode_ops.gemv_rmsnorm(r, attn, self.ffn_norm.weight, self.ffn_norm.eps, ff.w13.weight)
-            return h, decode_ops.gemv_swiglu(f13, ff.w2.weight)
+            if decode_ops.fused_decode_ok(f13[..., : ff.w2.weight.shape[1]], ff.w2):
+                return h, decode_ops.gemv_swiglu(f13, ff.w2.weight)
+            return h, _proj(ff.w2, ops.swiglu(f13))
         if delta is None:
             r, a = x, self.attention_norm(x)
         else:
@@ -379,14 +383,24 @@ class KVCache:
 
 def build_llama(args: ModelArgs | str, device=None, dtype: torch.dtype = torch.bfloat16, seed: int = 0,
                 **overrides) -> Transformer:
-    """Construct and initialise directly on ``device`` (fast for 7B on a GPU), then cast to ``dtype``."""
+    """Construct and initialise directly on ``device`` (fast for 7B on a GPU), then cast to ``dtype``.
+
+    Models whose fp32 copy would not fit beside the cast (more than 16 B parameters, e.g. 70B: 276 GB fp32) are
+    built and initialised in ``dtype`` directly instead -- the same distributions, drawn in the lower precision."""
     if isinstance(args, str):
         args = get_preset(args, **overrides)
     elif overrides:
         args = replace(args, **overrides)
     torch.manual_seed(seed)
-    with torch.device(device if device is not None else "cpu"):
-        model = Transformer(args)
+    direct = args.num_params() > 16e9 and dtype != torch.float32
+    old = torch.get_default_dtype()
+    if direct:
+        torch.set_default_dtype(dtype)
+    try:
+        with torch.device(device if device is not None else "cpu"):
+            model = Transformer(args)
+    finally:
+        torch.set_default_dtype(old)
     return model.to(dtype)
 
 
