@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--prompt", type=int, default=1024)
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--modes", nargs="+", choices=["eager", "graph"], default=["eager", "graph"])
+    ap.add_argument("--kv-dtype", choices=["bf16", "fp8"], default="bf16",
+                    help="KV-cache entries: bf16, or OCP e4m3 (half the cache bytes; opt-in, lossy)")
     ap.add_argument("--json", default=None)
     args = ap.parse_args()
 
@@ -45,16 +47,18 @@ def main():
 
     _lib.require()
     margs = get_preset(args.model)
+    margs = get_preset(args.model, max_seq_len=max(margs.max_seq_len, args.prompt + args.steps + 16))
     model = build_llama(margs, device="cuda", dtype=torch.bfloat16, seed=0)
     wbytes = sum(p.numel() * p.element_size() for p in model.parameters()) - margs.vocab_size * margs.dim * 2
-    kv_per_tok = margs.n_layers * 2 * margs.kv_heads * margs.head_dim * 2
+    kv_dtype = torch.float8_e4m3fn if args.kv_dtype == "fp8" else None
+    kv_per_tok = margs.n_layers * 2 * margs.kv_heads * margs.head_dim * (1 if kv_dtype is not None else 2)
     rows = []
     for B in args.batches:
         max_len = args.prompt + args.steps + 8
         prompts = torch.randint(0, margs.vocab_size, (B, args.prompt), device="cuda")
         rec = {"batch": B, "prompt": args.prompt, "decode_steps": args.steps}
         for graphs in [m == "graph" for m in args.modes]:
-            gen = Generator(model, B, max_len, graphs=graphs)
+            gen = Generator(model, B, max_len, graphs=graphs, dtype=kv_dtype)
             gen.prefill(prompts)   # warm-up (library heuristics, allocator)
             gen.reset()
             torch.cuda.synchronize()
@@ -84,7 +88,7 @@ def main():
             torch.cuda.empty_cache()
         rows.append(rec)
         print(json.dumps(rec), flush=True)
-    res = {"model": args.model, "dtype": "bf16", "data": "synthetic prompts, random-init weights",
+    res = {"model": args.model, "dtype": "bf16", "kv_cache": args.kv_dtype, "data": "synthetic prompts, random-init weights",
            "weight_bytes": wbytes, "kv_bytes_per_token": kv_per_tok, "rows": rows}
     if args.json:
         with open(args.json, "w") as fh:

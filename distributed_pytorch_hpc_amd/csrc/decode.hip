@@ -10,6 +10,8 @@
 //                      per 256-B key row (head_dim 128), 4 keys per wave instruction; every K and V row of the
 //                      chunk is loaded up front (16 + 16 KiB per wave in flight) and scores, softmax and P.V stay in
 //                      registers -- no LDS, no barriers.  Writes the chunk's unnormalised o and its (max, sum).
+//                      Opt-in FP8 caches (OCP e4m3 x a per-cache scale) halve the bytes: 8-B rows per lane,
+//                      widened by v_cvt_pk_f32_fp8.
 //   decode_combine_k : one wave per (batch, query head) merges the chunks of the sequence (log-sum-exp rescaling)
 //                      and writes bf16 o straight into the [B, Hq * D] input of the output projection.
 // Keys past a sequence's length re-read its last valid row (finite data) and get probability 0, so the cache never
@@ -55,10 +57,51 @@ __global__ __launch_bounds__(256) void kv_append_k(KVAppendParams p) {
   } else {
     const bool is_k = h < p.Hq + p.Hkv;
     const int hk = is_k ? h - p.Hq : h - p.Hq - p.Hkv;
-    bf16* dst = (bf16*)(is_k ? p.kc : p.vc) + (int64_t)b * p.c_sb + (int64_t)t * p.c_ss + (int64_t)hk * p.c_sh + c * 8;
-    Vec8<bf16>::store(dst, v);
+    const int64_t off = (int64_t)b * p.c_sb + (int64_t)t * p.c_ss + (int64_t)hk * p.c_sh + c * 8;
+    if (p.kv_fp8) {   // key / value rounded to bf16 first (what the bf16 cache would hold), then to e4m3
+      const float inv = 1.f / p.kv_scale;
+      float q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] = __builtin_amdgcn_fmed3f((float)(bf16)v[j] * inv, 448.f, -448.f);
+      uint2 o;
+      o.x = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false),
+                                                      true);
+      o.y = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false),
+                                                      true);
+      *reinterpret_cast<uint2*>((uint8_t*)(is_k ? p.kc : p.vc) + off) = o;
+    } else {
+      Vec8<bf16>::store((bf16*)(is_k ? p.kc : p.vc) + off, v);
+    }
   }
 }
+
+// 8 cache elements of one key / value row -> fp32 (bf16 or OCP e4m3 x scale)
+template <bool FP8>
+struct KVRow;
+template <>
+struct KVRow<false> {
+  typedef bf16x8 raw;
+  static __device__ __forceinline__ raw load(const void* base, int64_t off) {
+    return *reinterpret_cast<const bf16x8*>((const bf16*)base + off);
+  }
+  static __device__ __forceinline__ void unpack(const raw& r, float (&o)[8], float) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (float)r[e];
+  }
+};
+template <>
+struct KVRow<true> {
+  typedef uint2 raw;
+  static __device__ __forceinline__ raw load(const void* base, int64_t off) {
+    return *reinterpret_cast<const uint2*>((const uint8_t*)base + off);
+  }
+  static __device__ __forceinline__ void unpack(const raw& r, float (&o)[8], float sc) {
+    const auto a = __builtin_amdgcn_cvt_pk_f32_fp8((int)r.x, false), b = __builtin_amdgcn_cvt_pk_f32_fp8((int)r.x, true);
+    const auto c = __builtin_amdgcn_cvt_pk_f32_fp8((int)r.y, false), d = __builtin_amdgcn_cvt_pk_f32_fp8((int)r.y, true);
+    o[0] = a[0] * sc; o[1] = a[1] * sc; o[2] = b[0] * sc; o[3] = b[1] * sc;
+    o[4] = c[0] * sc; o[5] = c[1] * sc; o[6] = d[0] * sc; o[7] = d[1] * sc;
+  }
+};
 
 template <int N>
 __device__ __forceinline__ float group_sum(float v) {   // sum over aligned groups of N lanes
@@ -81,8 +124,9 @@ __device__ __forceinline__ float across_groups_sum(float v) {
   return v;
 }
 
-template <int HD, int G>
+template <int HD, int G, bool FP8>
 __global__ __launch_bounds__(256) void decode_attn_k(DecodeParams p) {
+  using KV = KVRow<FP8>;
   constexpr int TPK = HD / 8;     // lanes per key row (8 bf16 = 16 B each)
   constexpr int KPI = 64 / TPK;   // keys per wave instruction
   constexpr int NIT = 64 / KPI;   // instructions per 64-key chunk
@@ -105,18 +149,18 @@ __global__ __launch_bounds__(256) void decode_attn_k(DecodeParams p) {
     for (int e = 0; e < 8; ++e) qf[g][e] *= sl2;
   }
 
-  const bf16* kb = (const bf16*)p.kc + (int64_t)b * p.c_sb + (int64_t)hkv * p.c_sh + t * 8;
-  const bf16* vb = (const bf16*)p.vc + (int64_t)b * p.c_sb + (int64_t)hkv * p.c_sh + t * 8;
-  bf16x8 kr[NIT], vr[NIT];
+  const int64_t hoff = (int64_t)b * p.c_sb + (int64_t)hkv * p.c_sh + t * 8;
+  const float ksc = p.kv_scale;
+  typename KV::raw kr[NIT], vr[NIT];
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int row = min(k0 + it * KPI + j, len - 1);
-    kr[it] = *reinterpret_cast<const bf16x8*>(kb + (int64_t)row * p.c_ss);
+    kr[it] = KV::load(p.kc, hoff + (int64_t)row * p.c_ss);
   }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int row = min(k0 + it * KPI + j, len - 1);
-    vr[it] = *reinterpret_cast<const bf16x8*>(vb + (int64_t)row * p.c_ss);
+    vr[it] = KV::load(p.vc, hoff + (int64_t)row * p.c_ss);
   }
 
   // scores (log2 units): s[g][it] is key k0 + it * KPI + j, identical in the TPK lanes of group j
@@ -124,11 +168,13 @@ __global__ __launch_bounds__(256) void decode_attn_k(DecodeParams p) {
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const bool valid = k0 + it * KPI + j < len;
+    float kf[8];
+    KV::unpack(kr[it], kf, ksc);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       float d = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d = fmaf(qf[g][e], (float)kr[it][e], d);
+      for (int e = 0; e < 8; ++e) d = fmaf(qf[g][e], kf[e], d);
       d = group_sum<TPK>(d);
       s[g][it] = valid ? d : -INFINITY;
     }
@@ -155,11 +201,14 @@ __global__ __launch_bounds__(256) void decode_attn_k(DecodeParams p) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[g][e] = 0.f;
 #pragma unroll
-  for (int it = 0; it < NIT; ++it)
+  for (int it = 0; it < NIT; ++it) {
+    float vf[8];
+    KV::unpack(vr[it], vf, ksc);
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(s[g][it], (float)vr[it][e], acc[g][e]);
+      for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(s[g][it], vf[e], acc[g][e]);
+  }
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -231,7 +280,11 @@ int decode_heads_per_wave(int Hq, int Hkv) {
 void decode_attention(const DecodeParams& p, hipStream_t st) {
   const int G = decode_heads_per_wave(p.Hq, p.Hkv);
   const dim3 grid((unsigned)cdiv(p.nch, 4), (unsigned)(p.Hq / G), (unsigned)p.B);
-#define DPH_DEC(HD_, G_) hipLaunchKernelGGL((decode_attn_k<HD_, G_>), grid, dim3(256), 0, st, p)
+#define DPH_DEC(HD_, G_)                                                                     \
+  do {                                                                                       \
+    if (p.kv_fp8) hipLaunchKernelGGL((decode_attn_k<HD_, G_, true>), grid, dim3(256), 0, st, p); \
+    else hipLaunchKernelGGL((decode_attn_k<HD_, G_, false>), grid, dim3(256), 0, st, p);       \
+  } while (0)
 #define DPH_DEC_G(HD_)          \
   do {                          \
     if (G == 4) DPH_DEC(HD_, 4); \

@@ -184,6 +184,8 @@ struct KVAppendParams {
   void* kc; void* vc; int64_t c_sb, c_ss, c_sh;
   const int* pos; const float* cos; const float* sin;   // RoPE tables fp32 [max_pos, D / 2]
   int B, S, Hq, Hkv, D, Smax;
+  int kv_fp8;                            // caches hold OCP e4m3 bytes (value / kv_scale), else bf16
+  float kv_scale;
 };
 void kv_append(const KVAppendParams& p, hipStream_t stream);
 struct DecodeParams {
@@ -195,6 +197,8 @@ struct DecodeParams {
   int B, Hq, Hkv, D, nch;                // nch = 64-key chunks covered (>= ceil(max length / 64))
   int Smax;                              // cache capacity: lengths are clamped to it (no read past the cache)
   float scale;
+  int kv_fp8;                            // e4m3 caches: stored value x kv_scale = key / value
+  float kv_scale;
 };
 int decode_heads_per_wave(int Hq, int Hkv);
 void decode_attention(const DecodeParams& p, hipStream_t stream);

@@ -404,13 +404,16 @@ std::tuple<Tensor, Tensor, Tensor> fp8_quantize(const Tensor& x, int64_t fmt, bo
 }
 
 // ------------------------------------------------------------------------------------------------ serving
-void check_kv_cache(const Tensor& kc, const Tensor& vc) {
-  TORCH_CHECK(kc.dim() == 4 && kc.scalar_type() == at::kBFloat16 && kc.sizes() == vc.sizes() &&
-                  kc.strides() == vc.strides() && vc.scalar_type() == at::kBFloat16,
-              "kv cache: k and v must be bf16 [B, Smax, Hkv, D] with equal strides");
+// returns 1 for OCP e4m3 caches, 0 for bf16
+int check_kv_cache(const Tensor& kc, const Tensor& vc) {
+  const bool fp8 = kc.scalar_type() == at::kFloat8_e4m3fn;
+  TORCH_CHECK(kc.dim() == 4 && (fp8 || kc.scalar_type() == at::kBFloat16) && kc.sizes() == vc.sizes() &&
+                  kc.strides() == vc.strides() && vc.scalar_type() == kc.scalar_type(),
+              "kv cache: k and v must be bf16 or float8_e4m3fn [B, Smax, Hkv, D] with equal strides");
   TORCH_CHECK(kc.stride(3) == 1 && kc.stride(0) % 8 == 0 && kc.stride(1) % 8 == 0 && kc.stride(2) % 8 == 0,
               "kv cache: head dim contiguous, strides multiples of 8 elements");
   check_align16(kc, "k_cache"); check_align16(vc, "v_cache");
+  return fp8 ? 1 : 0;
 }
 
 void check_positions(const Tensor& pos, const Tensor& like, int64_t B) {
@@ -420,9 +423,10 @@ void check_positions(const Tensor& pos, const Tensor& like, int64_t B) {
 }
 
 void kv_append_(Tensor& qkv, Tensor& kc, Tensor& vc, const Tensor& pos, const Tensor& cos, const Tensor& sin,
-                int64_t n_heads, int64_t n_kv_heads) {
+                int64_t n_heads, int64_t n_kv_heads, double kv_scale) {
   c10::DeviceGuard g(qkv.device());
-  check_kv_cache(kc, vc);
+  const int fp8 = check_kv_cache(kc, vc);
+  TORCH_CHECK(kv_scale > 0.0, "kv_append: kv_scale must be positive");
   const int64_t B = qkv.size(0), S = qkv.size(1), D = kc.size(3);
   TORCH_CHECK(qkv.dim() == 3 && qkv.scalar_type() == at::kBFloat16 && qkv.stride(2) == 1 &&
                   qkv.size(2) == (n_heads + 2 * n_kv_heads) * D && qkv.stride(0) % 8 == 0 && qkv.stride(1) % 8 == 0,
@@ -440,13 +444,14 @@ void kv_append_(Tensor& qkv, Tensor& kc, Tensor& vc, const Tensor& pos, const Te
   p.kc = kc.data_ptr(); p.vc = vc.data_ptr(); p.c_sb = kc.stride(0); p.c_ss = kc.stride(1); p.c_sh = kc.stride(2);
   p.pos = pos.data_ptr<int>(); p.cos = cos.data_ptr<float>(); p.sin = sin.data_ptr<float>();
   p.B = (int)B; p.S = (int)S; p.Hq = (int)n_heads; p.Hkv = (int)n_kv_heads; p.D = (int)D; p.Smax = (int)kc.size(1);
+  p.kv_fp8 = fp8; p.kv_scale = (float)kv_scale;
   dph::kv_append(p, cur_stream());
 }
 
 Tensor decode_attention(const Tensor& qkv, const Tensor& kc, const Tensor& vc, const Tensor& pos, int64_t n_heads,
-                        int64_t n_kv_heads, double scale, int64_t max_len) {
+                        int64_t n_kv_heads, double scale, int64_t max_len, double kv_scale) {
   c10::DeviceGuard g(qkv.device());
-  check_kv_cache(kc, vc);
+  const int fp8 = check_kv_cache(kc, vc);
   const int64_t B = qkv.size(0), D = kc.size(3), Smax = kc.size(1);
   TORCH_CHECK(D == 32 || D == 64 || D == 128, "decode_attention: head_dim must be 32, 64 or 128");
   TORCH_CHECK(qkv.dim() == 3 && qkv.size(1) == 1 && qkv.scalar_type() == at::kBFloat16 && qkv.stride(2) == 1 &&
@@ -469,6 +474,7 @@ Tensor decode_attention(const Tensor& qkv, const Tensor& kc, const Tensor& vc, c
   p.out = out.data_ptr(); p.out_sb = out.stride(0);
   p.B = (int)B; p.Hq = (int)n_heads; p.Hkv = (int)n_kv_heads; p.D = (int)D; p.nch = (int)nch; p.Smax = (int)Smax;
   p.scale = (float)scale;
+  p.kv_fp8 = fp8; p.kv_scale = (float)kv_scale;
   dph::decode_attention(p, cur_stream());
   return out;
 }
@@ -923,9 +929,9 @@ TORCH_LIBRARY(dph, m) {
         "bool channels_last, bool bf16_out) -> Tensor");
   m.def("fp8_quantize(Tensor x, int fmt, bool rowmajor, bool transposed) -> (Tensor, Tensor, Tensor)");
   m.def("kv_append_(Tensor(a!) qkv, Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor pos, Tensor cos, Tensor sin, "
-        "int n_heads, int n_kv_heads) -> ()");
+        "int n_heads, int n_kv_heads, float kv_scale=1.) -> ()");
   m.def("decode_attention(Tensor qkv, Tensor k_cache, Tensor v_cache, Tensor pos, int n_heads, int n_kv_heads, "
-        "float scale, int max_len) -> Tensor");
+        "float scale, int max_len, float kv_scale=1.) -> Tensor");
   m.def("skinny_linear(Tensor x, Tensor w) -> Tensor");
   m.def("gemv_swiglu(Tensor x2, Tensor w) -> Tensor");
   m.def("gemv_rmsnorm(Tensor x, Tensor? res, Tensor norm_weight, float eps, Tensor w) -> (Tensor, Tensor)");

@@ -25,9 +25,10 @@ from ..models.llama2 import KVCache, Transformer
 
 class Generator:
     def __init__(self, model: Transformer, batch: int, max_len: int, graphs: Optional[bool] = None,
-                 dtype: torch.dtype | None = None):
+                 dtype: torch.dtype | None = None, kv_scale: float = 1.0):
+        """``dtype``: KV-cache element type (default the model's; ``torch.float8_e4m3fn`` halves the cache bytes)."""
         self.model = model
-        self.cache = KVCache(model, batch, max_len, dtype=dtype)
+        self.cache = KVCache(model, batch, max_len, dtype=dtype, kv_scale=kv_scale)
         dev = self.cache.pos.device
         self.device = dev
         if graphs is None:

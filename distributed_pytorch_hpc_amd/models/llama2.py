@@ -160,15 +160,27 @@ class Attention(nn.Module):
         b, s, _ = qkv.shape
         nh, nkv, hd = self.n_local_heads, self.n_local_kv_heads, self.head_dim
         kc, vc = cache.k[layer], cache.v[layer]
-        ops.kv_append_(qkv, kc, vc, cache.pos, cos, sin, nh, nkv)
+        ops.kv_append_(qkv, kc, vc, cache.pos, cos, sin, nh, nkv, cache.kv_scale)
         if s == 1:
-            return ops.decode_attention(qkv, kc, vc, cache.pos, nh, nkv, max_len=cache.attn_bound()).view(b, 1, -1)
+            return ops.decode_attention(qkv, kc, vc, cache.pos, nh, nkv, max_len=cache.attn_bound(),
+                                        kv_scale=cache.kv_scale).view(b, 1, -1)
         n = cache.length
         if n is None:
             raise RuntimeError("a multi-token append needs every sequence of the cache at the same, host-known length "
                                "(prefill ragged prompts one sequence at a time through KVCache.slot)")
         q = qkv[:, :, : nh * hd].view(b, s, nh, hd)
-        o = ops.flash_attention(q, kc[:, : n + s], vc[:, : n + s], causal=True)
+        if not cache.fp8:
+            o = ops.flash_attention(q, kc[:, : n + s], vc[:, : n + s], causal=True)
+        else:
+            # FP8 cache: the new tokens attend over bf16 keys / values -- their own (rotated here, in place in qkv;
+            # the cache got the quantised copy) after the dequantised prefix
+            k = qkv[:, :, nh * hd: (nh + nkv) * hd].view(b, s, nkv, hd)
+            v = qkv[:, :, (nh + nkv) * hd:].view(b, s, nkv, hd)
+            ops.rope_(k, cos, sin, n)
+            if n:
+                k = torch.cat([decode_ops.dequantize_kv(kc[:, :n], cache.kv_scale, k.dtype), k], 1)
+                v = torch.cat([decode_ops.dequantize_kv(vc[:, :n], cache.kv_scale, v.dtype), v], 1)
+            o = ops.flash_attention(q, k, v, causal=True)
         return o.reshape(b, s, nh * hd)
 
 
@@ -324,9 +336,11 @@ class KVCache:
     tokens cached per sequence, read by the kernels (a captured decode graph advances it on the device alone).
     ``lengths`` mirrors pos on the host while it is known (None inside / after graph replays that the owner
     tracks itself).  ``slot(i)`` is a view of sequence i (prefill of prompts of different lengths).
+    ``dtype=torch.float8_e4m3fn`` stores OCP e4m3 keys / values (value / ``kv_scale``): half the cache bytes.
     Sized for HBM: 7B at 4 096 tokens is 2 GiB per sequence in bf16."""
 
-    def __init__(self, model: "Transformer", batch: int, max_len: int, device=None, dtype: torch.dtype | None = None):
+    def __init__(self, model: "Transformer", batch: int, max_len: int, device=None, dtype: torch.dtype | None = None,
+                 kv_scale: float = 1.0):
         args = model.model_args
         attn = model.layers[0].attention if len(model.layers) else None
         hkv = attn.n_local_kv_heads if attn is not None else args.kv_heads
@@ -341,6 +355,10 @@ class KVCache:
         self.v = torch.zeros(shape, dtype=dtype, device=device)
         self.pos = torch.zeros(batch, dtype=torch.int32, device=device)
         self.batch, self.max_len = batch, max_len
+        # dtype torch.float8_e4m3fn: OCP e4m3 entries holding key / kv_scale (half the bytes of bf16; decode is
+        # bound by the cache read at large batch / long context)
+        self.fp8 = dtype == decode_ops.FP8_KV
+        self.kv_scale = float(kv_scale)
         self.lengths: Optional[list] = [0] * batch
         self._parent, self._index = None, None
 
@@ -376,6 +394,7 @@ class KVCache:
         view = object.__new__(KVCache)
         view.k, view.v, view.pos = self.k[:, i:i + 1], self.v[:, i:i + 1], self.pos[i:i + 1]
         view.batch, view.max_len = 1, self.max_len
+        view.fp8, view.kv_scale = self.fp8, self.kv_scale
         view.lengths = None if self.lengths is None else [self.lengths[i]]
         view._parent, view._index = self, i
         return view

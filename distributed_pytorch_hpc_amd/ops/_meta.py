@@ -180,12 +180,12 @@ def _latmse_bwd(gloss, pred, target, n_global, lat_offset, need_dtarget):
 
 
 @register_fake("dph::kv_append_")
-def _kv_append(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads):
+def _kv_append(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads, kv_scale=1.0):
     return None
 
 
 @register_fake("dph::decode_attention")
-def _decode_attn(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale, max_len):
+def _decode_attn(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale, max_len, kv_scale=1.0):
     return qkv.new_empty((qkv.shape[0], n_heads * k_cache.shape[-1]))
 
 

@@ -27,41 +27,61 @@ def _split(qkv: torch.Tensor, n_heads: int, n_kv_heads: int, head_dim: int):
     return q, k, v
 
 
-def kv_append_reference(qkv, k_cache, v_cache, pos, cos, sin, n_heads: int, n_kv_heads: int) -> None:
+FP8_KV = torch.float8_e4m3fn
+FP8_MAX = 448.0
+
+
+def quantize_kv(x: torch.Tensor, scale: float) -> torch.Tensor:
+    """bf16 keys / values -> OCP e4m3 cache entries (x / scale, saturated; torch's cast itself does not saturate)."""
+    return (x.to(torch.bfloat16).float() / scale).clamp(-FP8_MAX, FP8_MAX).to(FP8_KV)
+
+
+def dequantize_kv(c: torch.Tensor, scale: float, dtype: torch.dtype) -> torch.Tensor:
+    return c if c.dtype != FP8_KV else (c.float() * scale).to(dtype)
+
+
+def kv_append_reference(qkv, k_cache, v_cache, pos, cos, sin, n_heads: int, n_kv_heads: int,
+                        kv_scale: float = 1.0) -> None:
     hd = k_cache.shape[-1]
     q, k, v = _split(qkv, n_heads, n_kv_heads, hd)
     s = qkv.shape[1]
+    fp8 = k_cache.dtype == FP8_KV
     for b, p in enumerate(pos.tolist()):
         if p + s > k_cache.shape[1]:
             raise ValueError(f"kv cache overflow: sequence {b} at {p} + {s} > capacity {k_cache.shape[1]}")
         q[b:b + 1].copy_(rope_reference(q[b:b + 1], cos, sin, p))
-        k_cache[b, p:p + s].copy_(rope_reference(k[b:b + 1], cos, sin, p)[0])
-        v_cache[b, p:p + s].copy_(v[b])
+        kr = rope_reference(k[b:b + 1], cos, sin, p)[0]
+        k_cache[b, p:p + s].copy_(quantize_kv(kr, kv_scale) if fp8 else kr)
+        v_cache[b, p:p + s].copy_(quantize_kv(v[b], kv_scale) if fp8 else v[b])
 
 
 def kv_append_(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, pos: torch.Tensor, cos: torch.Tensor,
-               sin: torch.Tensor, n_heads: int, n_kv_heads: int) -> None:
+               sin: torch.Tensor, n_heads: int, n_kv_heads: int, kv_scale: float = 1.0) -> None:
     """Rotate q in place in ``qkv`` [B, S, (Hq + 2 Hkv) * D], write rotated k and v into the caches at positions
-    pos[b] .. pos[b] + S - 1.  ``pos`` is not advanced (the caller does that once per model step)."""
+    pos[b] .. pos[b] + S - 1 (bf16, or OCP e4m3 holding value / kv_scale).  ``pos`` is not advanced (the caller
+    does that once per model step)."""
     if _lib.use_native(qkv):
-        _lib.ops().kv_append_(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads)
+        _lib.ops().kv_append_(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads, float(kv_scale))
         return
-    kv_append_reference(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads)
+    kv_append_reference(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads, kv_scale)
 
 
-def decode_attention_reference(qkv, k_cache, v_cache, pos, n_heads: int, n_kv_heads: int, scale: float):
+def decode_attention_reference(qkv, k_cache, v_cache, pos, n_heads: int, n_kv_heads: int, scale: float,
+                               kv_scale: float = 1.0):
     hd = k_cache.shape[-1]
     q, _, _ = _split(qkv, n_heads, n_kv_heads, hd)
     outs = []
     for b, p in enumerate(pos.tolist()):
         n = p + 1
-        outs.append(attention_reference(q[b:b + 1].float(), k_cache[b:b + 1, :n].float(),
-                                        v_cache[b:b + 1, :n].float(), causal=False, scale=scale))
+        kk = dequantize_kv(k_cache[b:b + 1, :n], kv_scale, torch.float32).float()
+        vv = dequantize_kv(v_cache[b:b + 1, :n], kv_scale, torch.float32).float()
+        outs.append(attention_reference(q[b:b + 1].float(), kk, vv, causal=False, scale=scale))
     return torch.cat(outs, 0).reshape(qkv.shape[0], n_heads * hd).to(qkv.dtype)
 
 
 def decode_attention(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, pos: torch.Tensor, n_heads: int,
-                     n_kv_heads: int, scale: float | None = None, max_len: int | None = None) -> torch.Tensor:
+                     n_kv_heads: int, scale: float | None = None, max_len: int | None = None,
+                     kv_scale: float = 1.0) -> torch.Tensor:
     """Attention of the single new token per sequence (qkv [B, 1, ...], already appended) over keys 0 .. pos[b];
     returns [B, Hq * D].  ``max_len`` bounds pos + 1 over the batch (default: the cache capacity, as in a captured
     graph); a tighter bound only launches fewer workgroups."""
@@ -69,8 +89,8 @@ def decode_attention(qkv: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Te
     scale = 1.0 / math.sqrt(hd) if scale is None else scale
     if _lib.use_native(qkv):
         return _lib.ops().decode_attention(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale,
-                                           int(max_len or k_cache.shape[1]))
-    return decode_attention_reference(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale)
+                                           int(max_len or k_cache.shape[1]), float(kv_scale))
+    return decode_attention_reference(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale, kv_scale)
 
 
 def skinny_ok(x: torch.Tensor, mod: torch.nn.Module) -> bool:

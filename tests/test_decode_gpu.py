@@ -13,6 +13,27 @@ def _qkv(b, s, hq, hkv, d, seed=0):
 
 
 @pytest.mark.parametrize("s", [1, 5])
+def test_kv_append_fp8_cache_bitwise(dph_native, s):
+    """The kernel's e4m3 entries equal torch's cast of the bf16 rotated key / value divided by the scale."""
+    from distributed_pytorch_hpc_amd.ops.decode import kv_append_, kv_append_reference
+    from distributed_pytorch_hpc_amd.ops.rope import precompute_rope_tables
+
+    b, hq, hkv, d, smax = 3, 8, 2, 128, 64
+    cos, sin = precompute_rope_tables(d, 128, device="cuda")
+    pos = torch.tensor([0, 7, 20], dtype=torch.int32, device="cuda")
+    qkv = _qkv(b, s, hq, hkv, d) * 40   # values past the e4m3 range saturate
+    kc = torch.zeros(b, smax, hkv, d, dtype=torch.float8_e4m3fn, device="cuda")
+    vc = torch.zeros_like(kc)
+    q2, k2, v2 = qkv.clone(), kc.clone(), vc.clone()
+    kv_append_(qkv, kc, vc, pos, cos, sin, hq, hkv, 0.5)
+    # the reference rounds the rotated key through bf16 exactly as the kernel does
+    kv_append_reference(q2, k2, v2, pos, cos, sin, hq, hkv, 0.5)
+    assert torch.equal(vc.view(torch.uint8), v2.view(torch.uint8))
+    diff = (kc.float() - k2.float()).abs()
+    assert (diff > 0).float().mean() < 0.01   # rotation rounding (fma vs mul+add) may move a few values one step
+
+
+@pytest.mark.parametrize("s", [1, 5])
 def test_kv_append_matches_reference(dph_native, s):
     from distributed_pytorch_hpc_amd.ops.decode import kv_append_, kv_append_reference
     from distributed_pytorch_hpc_amd.ops.rope import precompute_rope_tables
@@ -31,11 +52,12 @@ def test_kv_append_matches_reference(dph_native, s):
     assert torch.equal(vc, v2)
 
 
+@pytest.mark.parametrize("fp8", [False, True])
 @pytest.mark.parametrize("hq,hkv,d", [(32, 32, 128), (8, 2, 128), (12, 4, 64), (16, 4, 32), (8, 1, 128)])
-def test_decode_attention_matches_fp32_reference(dph_native, hq, hkv, d):
-    from distributed_pytorch_hpc_amd.ops.decode import decode_attention, decode_attention_reference
+def test_decode_attention_matches_fp32_reference(dph_native, hq, hkv, d, fp8):
+    from distributed_pytorch_hpc_amd.ops.decode import decode_attention, decode_attention_reference, quantize_kv
 
-    b, smax = 3, 300
+    b, smax, ks = 3, 300, 0.25
     pos = torch.tensor([0, 130, 299], dtype=torch.int32, device="cuda")
     g = torch.Generator(device="cuda").manual_seed(1)
     kc = torch.randn(b, smax, hkv, d, device="cuda", generator=g).to(torch.bfloat16)
@@ -43,10 +65,13 @@ def test_decode_attention_matches_fp32_reference(dph_native, hq, hkv, d):
     for i, p in enumerate(pos.tolist()):   # past each sequence's end: NaN, which must never be read into o
         kc[i, p + 1:] = float("nan")
         vc[i, p + 1:] = float("nan")
+    if fp8:   # e4m3 entries (NaN stays NaN through the cast)
+        kc, vc = quantize_kv(kc, ks), quantize_kv(vc, ks)
+    sc = ks if fp8 else 1.0
     qkv = _qkv(b, 1, hq, hkv, d, seed=2)
-    ref = decode_attention_reference(qkv, kc, vc, pos, hq, hkv, 1.0 / math.sqrt(d)).float()
+    ref = decode_attention_reference(qkv, kc, vc, pos, hq, hkv, 1.0 / math.sqrt(d), kv_scale=sc).float()
     for bound in (None, 300):   # launch over the capacity (graph mode) or a tight bound: same result
-        out = decode_attention(qkv, kc, vc, pos, hq, hkv, max_len=bound)
+        out = decode_attention(qkv, kc, vc, pos, hq, hkv, max_len=bound, kv_scale=sc)
         assert out.shape == (b, hq * d) and torch.isfinite(out).all()
         torch.testing.assert_close(out.float(), ref, atol=1e-2, rtol=1e-2)
 
@@ -169,3 +194,23 @@ def test_continuous_batching_graphs_match_eager(dph_native):
     graphed, captured = serve(True)
     assert captured and graphed == eager
     assert [len(o) for o in eager] == [n for _, n in reqs]
+
+
+def test_llama_serving_fp8_kv_cache(dph_native):
+    from distributed_pytorch_hpc_amd.inference import Generator
+    from distributed_pytorch_hpc_amd.models.llama2 import KVCache
+
+    m = _tiny_llama(seed=11)
+    t = torch.randint(0, 512, (2, 72), device="cuda", generator=torch.Generator(device="cuda").manual_seed(4))
+
+    def run(dtype):
+        c = KVCache(m, 2, 128, dtype=dtype)
+        out = [m.forward_inference(t[:, :64], c)]
+        out += [m.forward_inference(t[:, i:i + 1], c) for i in range(64, 72)]
+        return torch.stack(out, 1)
+
+    bf, f8 = run(None), run(torch.float8_e4m3fn)
+    assert (f8 - bf).norm() / bf.norm() < 0.05
+    eager = Generator(m, 2, 64, graphs=False, dtype=torch.float8_e4m3fn).generate([[1, 2, 3], [4, 5, 6, 7]], 12)
+    graphed = Generator(m, 2, 64, graphs=True, dtype=torch.float8_e4m3fn).generate([[1, 2, 3], [4, 5, 6, 7]], 12)
+    assert graphed == eager

@@ -121,3 +121,20 @@ def test_continuous_batching_matches_one_request_at_a_time():
     solo = Generator(m, 1, 16)
     for h, (p, n) in zip(handles, reqs):
         assert h.prompt + h.output == solo.generate([p], n)[0]
+
+
+def test_fp8_kv_cache_tracks_the_full_forward():
+    """OCP e4m3 cache entries (x / kv_scale): prefill + decode logits stay close to the exact full forward."""
+    from distributed_pytorch_hpc_amd.models.llama2 import KVCache
+
+    m = _model()
+    t = torch.randint(0, 97, (2, 16))
+    full = m(t)
+    c = KVCache(m, 2, 32, dtype=torch.float8_e4m3fn, kv_scale=0.5)
+    assert c.fp8 and c.k.dtype == torch.float8_e4m3fn
+    got = [m.forward_inference(t[:, :10], c)]
+    got += [m.forward_inference(t[:, i:i + 1], c) for i in range(10, 13)]
+    got.append(m.forward_inference(t[:, 13:16], c, last_only=False)[:, -1])   # chunked append over an fp8 prefix
+    got = torch.stack(got, 1)
+    ref = torch.stack([full[:, 9], full[:, 10], full[:, 11], full[:, 12], full[:, 15]], 1)
+    assert (got - ref).norm() / ref.norm() < 0.05
