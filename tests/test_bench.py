@@ -26,7 +26,7 @@ def _lines(out):
     return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
 
 
-@pytest.mark.parametrize("n", [1, 2])
+@pytest.mark.parametrize("n", [1, 2, 4])
 def test_bench_contract(n, tmp_path):
     env = dict(os.environ, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1")
     if n == 1:
@@ -45,3 +45,19 @@ def test_bench_contract(n, tmp_path):
     assert r["config"]["parallelism"] == ("ddp1" if n == 1 else f"fsdp{n}")
     assert r["config"]["global_batch"] == 2 * n and r["config"]["seq_len"] == 64
     assert abs(r["value"] - n * 2 * 64 * 2 / (r["ms_per_step"] * 2 / 1000)) / r["value"] < 1e-3
+
+
+def test_scaling_sweep_harness(tmp_path):
+    """benchmarks/scaling_sweep.py runs bench.py at N = 1 and 2 (gloo, tiny model) and derives E(N) itself."""
+    sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+    import scaling_sweep
+
+    out = tmp_path / "scaling"
+    rows = scaling_sweep.main(["--ns", "1", "2", "--steps", "2", "--warmup", "1", "--out", str(out), "--"] + ARGS[:-5]
+                              + ["--quiet"])
+    assert [r["n_gpus"] for r in rows] == [1, 2]
+    assert rows[0]["scaling_efficiency"] == 1.0
+    assert rows[1]["parallelism"] == "fsdp2" and rows[1]["global_batch"] == 4
+    assert abs(rows[1]["scaling_efficiency"] - rows[1]["tokens_per_s"] / (2 * rows[0]["tokens_per_s"])) < 1e-3
+    assert (out / "scaling.json").exists() and (out / "n2.log").exists()
+    assert "| 2 | fsdp2 |" in (out / "scaling.md").read_text()
