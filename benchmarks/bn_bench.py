@@ -75,7 +75,20 @@ def main():
         rows.append(row)
         print(json.dumps(row), flush=True)
         del x, r, dy, y
+    # the stem's max pooling (ops/pool.py) vs ATen, forward + backward
+    from distributed_pytorch_hpc_amd.ops.pool import max_pool3s2
+
+    xs = torch.randn(args.batch, 64, 112, 112, device="cuda", dtype=torch.bfloat16)
+    xs = xs.contiguous(memory_format=torch.channels_last).requires_grad_()
+    gy = torch.randn(args.batch, 64, 56, 56, device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    pool = {}
+    for name, fn in (("dph", max_pool3s2), ("aten", lambda t: torch.nn.functional.max_pool2d(t, 3, 2, 1))):
+        pool[name + "_fwd_us"] = round(timeit(lambda: fn(xs.detach())) * 1e3, 1)
+        pool[name + "_fwd_bwd_us"] = round(timeit(lambda: fn(xs).backward(gy)) * 1e3, 1)
+    print(json.dumps({"stem_maxpool": pool}), flush=True)
     summ = {k + "_ms_per_step_if_all_layers": round(v, 3) for k, v in tot.items()}
+    summ["stem_maxpool"] = pool
     print(json.dumps(summ), flush=True)
     if args.json:
         with open(args.json, "w") as fh:

@@ -149,6 +149,13 @@ void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, con
             void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dtype,
             int param_dtype, hipStream_t stream, const float* xmask_ss = nullptr);
 
+// 3x3 / stride 2 / padding 1 max pooling, channels-last [N, H, W, C] (C % 8 == 0), csrc/pool.hip.  tap: one byte
+// per output element, the window position (0..8) of the max; the backward gathers through it.
+void maxpool3s2_fwd(const void* x, void* y, uint8_t* tap, int64_t N, int64_t H, int64_t W, int64_t C, int dtype,
+                    hipStream_t stream);
+void maxpool3s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C,
+                    int dtype, hipStream_t stream);
+
 // dst[C, R] = src[R, C]^T (bf16, row-major, leading dims in elements; vector path needs 16-B aligned rows).
 void transpose2d(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_src, int64_t ld_dst,
                  hipStream_t stream);

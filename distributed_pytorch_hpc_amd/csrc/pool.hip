@@ -1,0 +1,134 @@
+// 3x3 / stride 2 / padding 1 max pooling on channels-last (NHWC) activations: the ResNet stem's MaxPool2d
+// (torchvision layout of scripts/main.py's resnet50: conv1 7x7/2 -> bn1 -> relu -> maxpool 3x3/2/1).
+//
+// ATen's NHWC max_pool backward scatters through 64-bit indices and took 0.67 ms of a ResNet-50 B=256 step
+// (profiles/rocprof_resnet50_fsdp_bf16_r2_summary.txt) for a 411 MB input gradient.  Here:
+//   forward : one thread = one output pixel x 8 channels; the 9 taps are 16-B loads; the window position of the max
+//             (0..8) is kept as one byte per element (8 B per thread, one store) instead of an int64 flat index;
+//             ties and NaNs resolve exactly like ATen (scan kh-major, take v > max or NaN).
+//   backward: a GATHER per input pixel (no atomics, deterministic): an input row iy is covered by output rows
+//             oy = iy/2 (iy even) or (iy-1)/2 and (iy+1)/2 (iy odd) -- at most 2 x 2 windows -- and receives dy of
+//             each window whose stored tap is its own (fp32 sum, one rounding).  dx is written exactly once, so no
+//             zero-fill pass.
+// Traffic: forward reads x (the 9-fold reuse stays in L2) and writes y + 1 byte/elem; backward reads dy + taps
+// (each about 2.25x, L2) and writes dx: both run near a device copy of x.
+#include "dph_common.h"
+#include "kernels.h"
+
+namespace dph {
+
+namespace {
+
+constexpr int PNT = 256;
+
+template <typename T>
+__global__ __launch_bounds__(PNT) void maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y,
+                                                     uint8_t* __restrict__ tap, int H, int W, int Ho, int Wo, int C,
+                                                     int64_t total) {
+  const int cv = C >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * PNT + threadIdx.x; i < total; i += (int64_t)gridDim.x * PNT) {
+    const int c8 = (int)(i % cv);
+    const int64_t p = i / cv;                       // output pixel n * Ho * Wo + oy * Wo + ox
+    const int ox = (int)(p % Wo);
+    const int64_t q = p / Wo;
+    const int oy = (int)(q % Ho);
+    const int64_t n = q / Ho;
+    float mx[8];
+    int arg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { mx[k] = -__builtin_inff(); arg[k] = 0; }
+    // ATen initialises the index to the window's first in-image tap; a window of all -inf keeps that tap
+    const int ih0 = 2 * oy - 1, iw0 = 2 * ox - 1;
+    const int kh0 = ih0 < 0 ? 1 : 0, kw0 = iw0 < 0 ? 1 : 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) arg[k] = kh0 * 3 + kw0;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = ih0 + kh;
+      if (ih < 0 || ih >= H) continue;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = iw0 + kw;
+        if (iw < 0 || iw >= W) continue;
+        float v[8];
+        Vec8<T>::load(x + ((n * H + ih) * W + iw) * C + c8 * 8, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          if (v[k] > mx[k] || __builtin_isnan(v[k])) {
+            mx[k] = v[k];
+            arg[k] = kh * 3 + kw;
+          }
+        }
+      }
+    }
+    Vec8<T>::store(y + p * C + c8 * 8, mx);
+    uint64_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) packed |= (uint64_t)arg[k] << (8 * k);
+    *reinterpret_cast<uint64_t*>(tap + p * C + c8 * 8) = packed;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(PNT) void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ tap,
+                                                     T* __restrict__ dx, int H, int W, int Ho, int Wo, int C,
+                                                     int64_t total) {
+  const int cv = C >> 3;
+  for (int64_t i = (int64_t)blockIdx.x * PNT + threadIdx.x; i < total; i += (int64_t)gridDim.x * PNT) {
+    const int c8 = (int)(i % cv);
+    const int64_t p = i / cv;                       // input pixel n * H * W + iy * W + ix
+    const int ix = (int)(p % W);
+    const int64_t q = p / W;
+    const int iy = (int)(q % H);
+    const int64_t n = q / H;
+    // output windows covering iy: oy with 2 oy - 1 <= iy <= 2 oy + 1
+    const int oy_lo = iy >> 1, oy_hi = min((iy + 1) >> 1, Ho - 1);
+    const int ox_lo = ix >> 1, ox_hi = min((ix + 1) >> 1, Wo - 1);
+    float acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+    for (int oy = oy_lo; oy <= oy_hi; ++oy) {
+      const int kh = iy - 2 * oy + 1;
+      for (int ox = ox_lo; ox <= ox_hi; ++ox) {
+        const int kw = ix - 2 * ox + 1;
+        const int me = kh * 3 + kw;
+        const int64_t o = ((n * Ho + oy) * Wo + ox) * C + c8 * 8;
+        const uint64_t packed = *reinterpret_cast<const uint64_t*>(tap + o);
+        float g[8];
+        Vec8<T>::load(dy + o, g);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if ((int)((packed >> (8 * k)) & 0xff) == me) acc[k] += g[k];
+      }
+    }
+    Vec8<T>::store(dx + p * C + c8 * 8, acc);
+  }
+}
+
+}  // namespace
+
+void maxpool3s2_fwd(const void* x, void* y, uint8_t* tap, int64_t N, int64_t H, int64_t W, int64_t C, int dtype,
+                    hipStream_t st) {
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int64_t total = N * Ho * Wo * (C / 8);
+  if (total == 0) return;
+  const dim3 grid(stream_grid(total, PNT));
+  DPH_DISPATCH_FLOAT(dtype, T, {
+    hipLaunchKernelGGL(maxpool_fwd_k<T>, grid, dim3(PNT), 0, st, (const T*)x, (T*)y, tap, (int)H, (int)W, (int)Ho,
+                       (int)Wo, (int)C, total);
+  });
+}
+
+void maxpool3s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C,
+                    int dtype, hipStream_t st) {
+  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int64_t total = N * H * W * (C / 8);
+  if (total == 0) return;
+  const dim3 grid(stream_grid(total, PNT));
+  DPH_DISPATCH_FLOAT(dtype, T, {
+    hipLaunchKernelGGL(maxpool_bwd_k<T>, grid, dim3(PNT), 0, st, (const T*)dy, tap, (T*)dx, (int)H, (int)W, (int)Ho,
+                       (int)Wo, (int)C, total);
+  });
+}
+
+}  // namespace dph

@@ -20,6 +20,7 @@ from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot
+from ..ops.pool import MaxPool2d
 
 
 def conv3x3(cin, cout, stride=1):
@@ -86,7 +87,7 @@ class ResNet(nn.Module):
             self.maxpool = nn.Identity()
         else:
             self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
-            self.maxpool = nn.MaxPool2d(3, 2, 1)
+            self.maxpool = MaxPool2d(3, 2, 1)   # channels-last HIP kernels (ops/pool.py)
         self.bn1 = BatchNormAct2d(64)
         self.layer1 = self._make(block, 64, layers[0])
         self.layer2 = self._make(block, 128, layers[1], 2)

@@ -98,6 +98,20 @@ def _transpose2d(x):
     return x.new_empty((x.shape[1], x.shape[0]))
 
 
+@register_fake("dph::maxpool3s2_fwd")
+def _maxpool3s2_fwd(x):
+    n, c, h, w = x.shape
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    y = x.new_empty((n, c, ho, wo)).contiguous(memory_format=torch.channels_last)
+    return y, x.new_empty((n, ho, wo, c), dtype=torch.uint8)
+
+
+@register_fake("dph::maxpool3s2_bwd")
+def _maxpool3s2_bwd(dy, tap, H, W):
+    n, c = dy.shape[:2]
+    return dy.new_empty((n, c, H, W)).contiguous(memory_format=torch.channels_last)
+
+
 @register_fake("dph::gemm_tn_")
 def _gemm_tn(C, A, B, accumulate):
     return None

@@ -779,3 +779,44 @@ def test_conv3x3_module_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W, 
     assert rel_err(y, yr) < 8e-3
     assert rel_err(x.grad, xr.grad) < 1e-2
     assert rel_err(conv.weight.grad, wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 16, 7, 9), (2, 8, 1, 5), (2, 24, 6, 6)])
+def test_maxpool3s2_matches_torch(dph_native, dtype, shape):
+    """csrc/pool.hip vs F.max_pool2d(3, 2, 1) in fp32: forward values bitwise, input gradient (gather over the stored
+    window taps) equal to autograd's scatter -- random data has no ties within a window in fp32."""
+    from distributed_pytorch_hpc_amd.ops.pool import MaxPool2d, maxpool3s2_native_ok
+
+    torch.manual_seed(0)
+    x = torch.randn(*shape, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    assert maxpool3s2_native_ok(x)
+    y = MaxPool2d(3, 2, 1)(x)
+    xr = x.detach().float().requires_grad_()
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(y.float(), yr)
+    g = torch.randn_like(yr)
+    y.backward(g.to(dtype))
+    yr.backward(g.to(dtype).float())
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
+    if dtype == torch.float32:
+        torch.testing.assert_close(x.grad, xr.grad, rtol=1e-6, atol=1e-6)
+    else:   # bf16 inputs tie more often; the sums of up to 4 windows round once
+        assert rel_err(x.grad, xr.grad) < 1e-2
+
+
+def test_maxpool3s2_ties_follow_aten(dph_native):
+    """Constant and post-ReLU (many zeros) inputs: the first maximum in kh-major scan order wins, as in ATen."""
+    from distributed_pytorch_hpc_amd.ops.pool import max_pool3s2
+
+    for x in (torch.ones(2, 8, 9, 9, device=DEV, dtype=torch.bfloat16),
+              torch.relu(torch.randn(2, 64, 20, 20, device=DEV)).to(torch.bfloat16)):
+        x = x.contiguous(memory_format=torch.channels_last).requires_grad_()
+        xr = x.detach().clone().requires_grad_()
+        y, yr = max_pool3s2(x), F.max_pool2d(xr, 3, 2, 1)
+        assert torch.equal(y, yr)
+        g = torch.randn_like(y)
+        y.backward(g)
+        yr.backward(g)
+        assert torch.equal(x.grad, xr.grad)
