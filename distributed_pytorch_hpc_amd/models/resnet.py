@@ -19,7 +19,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot
+from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot, grad_tap
 from ..ops.pool import MaxPool2d
 
 
@@ -64,17 +64,24 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        # identity blocks: conv1's input-gradient kernel also adds bn3's residual gradient (ops.conv.GradSlot)
+        # conv1's input-gradient kernel also adds x's other gradient (ops.conv.GradSlot): bn3's residual gradient in
+        # identity blocks, the downsample convolution's input gradient in downsample blocks
         slot = None
-        if self.downsample is None and isinstance(self.conv1, Conv1x1) and x.requires_grad and torch.is_grad_enabled():
+        if isinstance(self.conv1, Conv1x1) and x.requires_grad and torch.is_grad_enabled():
             slot = GradSlot()
         # training-mode BN after a 1x1 convolution takes its statistics from the convolution's epilogue
         s1 = StatsSlot() if self.bn1.training and isinstance(self.conv1, Conv1x1) else None
         s3 = StatsSlot() if self.bn3.training and isinstance(self.conv3, Conv1x1) else None
-        idt = x if self.downsample is None else self.downsample(x)
         out = self.bn1(self.conv1(x, grad_slot=slot, stats_slot=s1), stats_slot=s1)
+        if self.downsample is None:
+            idt, res_slot = x, slot
+        else:
+            # built after conv1 / bn1, so autograd runs the downsample branch's backward (ending in the tap) before
+            # conv1's: the tap parks the branch's gradient of x for conv1's dgrad epilogue (no separate add over x)
+            tapped = grad_tap(x, slot) if slot is not None and slot.consumer else x
+            idt, res_slot = self.downsample(tapped), None
         out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out, stats_slot=s3), idt, residual_grad_slot=slot, stats_slot=s3)
+        return self.bn3(self.conv3(out, stats_slot=s3), idt, residual_grad_slot=res_slot, stats_slot=s3)
 
 
 class ResNet(nn.Module):

@@ -83,6 +83,30 @@ class GradSlot:
         self.t = None
 
 
+class _GradTapFn(torch.autograd.Function):
+    """Identity whose backward parks the incoming gradient in ``slot.t`` (instead of returning it to autograd), for
+    the 1x1 convolution that consumes the same tensor to add in its input-gradient epilogue."""
+
+    @staticmethod
+    def forward(ctx, x, slot):
+        ctx.slot = slot
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.slot.t = g
+        return None, None
+
+
+def grad_tap(x: torch.Tensor, slot: GradSlot) -> torch.Tensor:
+    """Route the gradient that flows back into ``x`` through this branch into ``slot`` (armed here); the slot's
+    consumer -- a Conv1x1 whose forward ran on ``x`` BEFORE this call, so that autograd runs this branch's backward
+    first -- adds it in its dgrad epilogue.  Used for a ResNet downsample branch: x's two gradients (main branch and
+    downsample convolution) are then summed inside conv1's kernel instead of by a separate add over x."""
+    slot.armed = True
+    return _GradTapFn.apply(x, slot)
+
+
 class StatsSlot:
     """BatchNorm statistics of a 1x1 convolution's output, computed in the convolution's epilogue
     (``ts_gemm_nt_stats``: per-128-row-block [mean | M2 | rows] partials) and consumed by the BatchNorm that

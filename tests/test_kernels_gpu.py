@@ -820,3 +820,50 @@ def test_maxpool3s2_ties_follow_aten(dph_native):
         y.backward(g)
         yr.backward(g)
         assert torch.equal(x.grad, xr.grad)
+
+
+@pytest.mark.parametrize("inplanes,planes,stride", [(64, 64, 1), (256, 128, 2)])
+def test_bottleneck_downsample_grad_tap(dph_native, monkeypatch, inplanes, planes, stride):
+    """Downsample bottleneck: the downsample convolution's input gradient is parked by ops.conv.grad_tap and added
+    inside conv1's input-gradient kernel (autograd runs the downsample branch first); gradients match the MIOpen path
+    where autograd adds the two gradients of x."""
+    import importlib
+
+    from torch import nn
+
+    from distributed_pytorch_hpc_amd.ops.batchnorm import BatchNormAct2d
+    from distributed_pytorch_hpc_amd.ops.conv import GradSlot
+
+    resnet_mod = importlib.import_module("distributed_pytorch_hpc_amd.models.resnet")
+    made = []
+
+    class _Spy(GradSlot):
+        __slots__ = ()
+
+        def __init__(self):
+            super().__init__()
+            made.append(self)
+
+    monkeypatch.setattr(resnet_mod, "GradSlot", _Spy)
+    torch.manual_seed(0)
+    down = nn.Sequential(resnet_mod.conv1x1(inplanes, planes * 4, stride), BatchNormAct2d(planes * 4, act=False))
+    block = resnet_mod.Bottleneck(inplanes, planes, stride, down).to(DEV).to(torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    x = torch.randn(8, inplanes, 16, 16, device=DEV, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+
+    def run(flag):
+        monkeypatch.setenv("DPH_CONV1X1", flag)
+        block.zero_grad(set_to_none=True)
+        x.grad = None
+        made.clear()
+        block(x).float().pow(2).mean().backward()
+        return x.grad.float().clone(), {n: p.grad.float().clone() for n, p in block.named_parameters()}
+
+    gx1, g1 = run("1")
+    assert made and made[0].armed and made[0].t is None     # parked by the tap, consumed by conv1's epilogue
+    gx0, g0 = run("0")
+    assert not made[0].armed
+    assert rel_err(gx1, gx0) < 2e-2
+    for n in g0:
+        assert rel_err(g1[n], g0[n]) < 5e-2, n
