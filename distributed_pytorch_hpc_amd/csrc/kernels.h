@@ -156,6 +156,11 @@ void maxpool3s2_fwd(const void* x, void* y, uint8_t* tap, int64_t N, int64_t H, 
 void maxpool3s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C,
                     int dtype, hipStream_t stream);
 
+// out[c] = sum_m x[m, c] over a row-major [M, C] (channels-last) tensor, csrc/chsum.hip: fp32 partials
+// part[chsum_partial_blocks(M, C) * C], out in out_dtype (fp32 / bf16).  Deterministic.
+int chsum_partial_blocks(int64_t M, int64_t C);
+void chsum(const void* x, float* part, void* out, int64_t M, int64_t C, int dtype, int out_dtype, hipStream_t stream);
+
 // dst[C, R] = src[R, C]^T (bf16, row-major, leading dims in elements; vector path needs 16-B aligned rows).
 void transpose2d(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_src, int64_t ld_dst,
                  hipStream_t stream);

@@ -689,6 +689,23 @@ int64_t gemm_tn_mfma_(int64_t shape) {
   return dph::gemm_tn_mfma();
 }
 
+// ------------------------------------------------------------------------------------------------ channel sum
+// x channels-last [N, C, H, W] or contiguous [M, C] -> [C] in out_dtype (the convolution bias gradient).
+Tensor channel_sum(const Tensor& x, at::ScalarType out_dtype) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK((x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast)) || (x.dim() == 2 && x.is_contiguous()),
+              "channel_sum: channels-last [N, C, H, W] or contiguous [M, C]");
+  TORCH_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16, "channel_sum: fp32 / bf16 output");
+  const int64_t C = x.size(1), M = C ? x.numel() / C : 0;
+  auto out = at::empty({C}, x.options().dtype(out_dtype));
+  if (C == 0) return out;
+  auto part = at::empty({(int64_t)dph::chsum_partial_blocks(M, C) * C}, x.options().dtype(at::kFloat));
+  dph::chsum(x.data_ptr(), part.data_ptr<float>(), out.data_ptr(), M, C, dt_code(x),
+             out_dtype == at::kBFloat16 ? dph::kBF16 : dph::kF32, cur_stream());
+  return out;
+}
+
 // ------------------------------------------------------------------------------------------------ max pooling
 // x: channels-last [N, C, H, W], C % 8 == 0.  Returns (y channels-last [N, C, Ho, Wo], tap uint8 [N, Ho, Wo, C]).
 std::tuple<Tensor, Tensor> maxpool3s2_fwd(const Tensor& x) {
@@ -980,6 +997,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("maxpool3s2_fwd(Tensor x) -> (Tensor, Tensor)");
+  m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
   m.def("maxpool3s2_bwd(Tensor dy, Tensor tap, int H, int W) -> Tensor");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
         "float momentum, float eps, bool relu, Tensor? pre_stats=None, Tensor(c!)? num_batches_tracked=None) "
@@ -1032,6 +1050,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("ts_gemm_tn_", &ts_gemm_tn_);
   m.impl("transpose2d", &transpose2d);
   m.impl("maxpool3s2_fwd", &maxpool3s2_fwd);
+  m.impl("channel_sum", &channel_sum);
   m.impl("maxpool3s2_bwd", &maxpool3s2_bwd);
   m.impl("bn_act_fwd", &bn_act_fwd);
   m.impl("bn_act_apply", &bn_act_apply);

@@ -13,11 +13,16 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from ..ops.batchnorm import BatchNormAct2d
+from ..ops.conv import BiasConv2d, BiasConvTranspose2d
+
 
 def conv_block(in_ch: int, out_ch: int) -> nn.Sequential:
+    # conv -> BN -> ReLU twice, as the reference; BN + ReLU run as one fused channels-last op (BatchNormAct2d, a
+    # BatchNorm2d subclass: same state-dict keys; the ReLU slots stay as Identity so the indices are unchanged)
     return nn.Sequential(
-        nn.Conv2d(in_ch, out_ch, 3, padding=1), nn.BatchNorm2d(out_ch), nn.ReLU(inplace=True),
-        nn.Conv2d(out_ch, out_ch, 3, padding=1), nn.BatchNorm2d(out_ch), nn.ReLU(inplace=True),
+        BiasConv2d(in_ch, out_ch, 3, padding=1), BatchNormAct2d(out_ch), nn.Identity(),
+        BiasConv2d(out_ch, out_ch, 3, padding=1), BatchNormAct2d(out_ch), nn.Identity(),
     )
 
 
@@ -29,13 +34,13 @@ class SimpleUNet(nn.Module):
         self.enc2 = conv_block(b, 2 * b)
         self.enc3 = conv_block(2 * b, 4 * b)
         self.bottleneck = conv_block(4 * b, 8 * b)
-        self.up3 = nn.ConvTranspose2d(8 * b, 4 * b, 2, 2)
+        self.up3 = BiasConvTranspose2d(8 * b, 4 * b, 2, 2)
         self.dec3 = conv_block(8 * b, 4 * b)
-        self.up2 = nn.ConvTranspose2d(4 * b, 2 * b, 2, 2)
+        self.up2 = BiasConvTranspose2d(4 * b, 2 * b, 2, 2)
         self.dec2 = conv_block(4 * b, 2 * b)
-        self.up1 = nn.ConvTranspose2d(2 * b, b, 2, 2)
+        self.up1 = BiasConvTranspose2d(2 * b, b, 2, 2)
         self.dec1 = conv_block(2 * b, b)
-        self.out = nn.Conv2d(b, out_channels, kernel_size=1)
+        self.out = BiasConv2d(b, out_channels, kernel_size=1)
         self.pool = nn.MaxPool2d(2)
 
     @staticmethod

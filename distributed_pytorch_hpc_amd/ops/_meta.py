@@ -216,3 +216,8 @@ def _gemv_swiglu(x2, w):
 @register_fake("dph::gemv_rmsnorm")
 def _gemv_rmsnorm(x, res, norm_weight, eps, w):
     return x.new_empty((*x.shape[:-1], w.shape[0])), (torch.empty_like(x) if res is not None else x.new_empty((0,)))
+
+
+@register_fake("dph::channel_sum")
+def _channel_sum(x, out_dtype):
+    return x.new_empty((x.shape[1],), dtype=out_dtype)

@@ -247,3 +247,67 @@ class Conv1x1(nn.Conv2d):
                 grad_slot.consumer = True
             return _Conv1x1Fn.apply(x, self.weight, grad_slot, stats_slot)
         return F.conv2d(x, self.weight)
+
+
+# ------------------------------------------------------------------------------------------------ bias convolutions
+class _ConvBiasFn(torch.autograd.Function):
+    """MIOpen convolution (forward, input and weight gradients through aten.convolution[_backward]) whose bias
+    gradient is the deterministic channels-last per-channel sum of csrc/chsum.hip instead of ATen's outer-dimension
+    reduction (1.9 ms for the 65-channel output convolution of SimpleUNet at B=4, 181x360)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, stride, padding, dilation, transposed, output_padding, groups):
+        y = torch.ops.aten.convolution(x, w, b, stride, padding, dilation, transposed, output_padding, groups)
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, padding, dilation, transposed, output_padding, groups)
+        ctx.bdtype = b.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, padding, dilation, transposed, output_padding, groups = ctx.cfg
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        nx, nw, nb = ctx.needs_input_grad[:3]
+        dx = dw = db = None
+        if nx or nw:
+            dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, stride, padding, dilation, transposed,
+                                                            output_padding, groups, [nx, nw, False])
+        if nb:
+            db = _lib.ops().channel_sum(dy, ctx.bdtype)
+        return dx, dw, db, None, None, None, None, None, None
+
+
+def _bias_conv_ok(m: nn.Module, x: torch.Tensor) -> bool:
+    return (m.bias is not None and x.is_cuda and x.dim() == 4 and m.padding_mode == "zeros"
+            and not isinstance(m.padding, str) and x.dtype in (torch.bfloat16, torch.float32)
+            and x.is_contiguous(memory_format=torch.channels_last) and _lib.use_native(x))
+
+
+def _bias_conv(m: nn.Module, x: torch.Tensor, transposed: bool, output_padding) -> torch.Tensor:
+    w, b = m.weight, m.bias
+    args = (list(m.stride), list(m.padding), list(m.dilation), transposed, list(output_padding), m.groups)
+    if torch.is_autocast_enabled("cuda"):   # same casts as autocast's conv2d: inputs, weight and bias to its dtype
+        dt = torch.get_autocast_dtype("cuda")
+        with torch.autocast("cuda", enabled=False):
+            return _ConvBiasFn.apply(x.to(dt), w.to(dt), b.to(dt), *args)
+    return _ConvBiasFn.apply(x, w, b, *args)
+
+
+class BiasConv2d(nn.Conv2d):
+    """``nn.Conv2d`` (same parameters and state dict) whose channels-last GPU path computes the bias gradient with
+    the per-channel sum kernel; everything else is the stock MIOpen convolution."""
+
+    def forward(self, x):
+        if _bias_conv_ok(self, x):
+            return _bias_conv(self, x, False, (0, 0))
+        return super().forward(x)
+
+
+class BiasConvTranspose2d(nn.ConvTranspose2d):
+    """``nn.ConvTranspose2d`` counterpart of ``BiasConv2d`` (no ``output_size`` argument on the fast path)."""
+
+    def forward(self, x, output_size=None):
+        if output_size is None and _bias_conv_ok(self, x):
+            return _bias_conv(self, x, True, self.output_padding)
+        return super().forward(x, output_size)
