@@ -149,11 +149,13 @@ void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, con
             void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dtype,
             int param_dtype, hipStream_t stream, const float* xmask_ss = nullptr);
 
-// 3x3 / stride 2 / padding 1 max pooling, channels-last [N, H, W, C] (C % 8 == 0), csrc/pool.hip.  tap: one byte
-// per output element, the window position (0..8) of the max; the backward gathers through it.
-void maxpool3s2_fwd(const void* x, void* y, uint8_t* tap, int64_t N, int64_t H, int64_t W, int64_t C, int dtype,
-                    hipStream_t stream);
-void maxpool3s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C,
+// Stride-2 max pooling, channels-last [N, H, W, C] (C % 8 == 0), csrc/pool.hip: k = 3 (padding 1) or 2 (padding 0),
+// floor mode.  tap: one byte per output element, the window position (0..k*k-1) of the max; the backward gathers
+// through it.
+inline int64_t maxpool_s2_out(int64_t n, int k) { return k == 3 ? (n - 1) / 2 + 1 : n / 2; }
+void maxpool_s2_fwd(const void* x, void* y, uint8_t* tap, int64_t N, int64_t H, int64_t W, int64_t C, int k,
+                    int dtype, hipStream_t stream);
+void maxpool_s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C, int k,
                     int dtype, hipStream_t stream);
 
 // out[c] = sum_m x[m, c] over a row-major [M, C] (channels-last) tensor, csrc/chsum.hip: fp32 partials

@@ -1,15 +1,17 @@
-// 3x3 / stride 2 / padding 1 max pooling on channels-last (NHWC) activations: the ResNet stem's MaxPool2d
-// (torchvision layout of scripts/main.py's resnet50: conv1 7x7/2 -> bn1 -> relu -> maxpool 3x3/2/1).
+// Stride-2 max pooling on channels-last (NHWC) activations: 3x3 / padding 1 (the ResNet stem's MaxPool2d, torchvision
+// layout of scripts/main.py's resnet50: conv1 7x7/2 -> bn1 -> relu -> maxpool 3x3/2/1) and 2x2 / padding 0 (the
+// SimpleUNet encoder's MaxPool2d(2), multinode_ddp_unet.py:171-214; floor mode, so an odd last row / column is
+// dropped as in ATen).
 //
 // ATen's NHWC max_pool backward scatters through 64-bit indices and took 0.67 ms of a ResNet-50 B=256 step
 // (profiles/rocprof_resnet50_fsdp_bf16_r2_summary.txt) for a 411 MB input gradient.  Here:
-//   forward : one thread = one output pixel x 8 channels; the 9 taps are 16-B loads; the window position of the max
-//             (0..8) is kept as one byte per element (8 B per thread, one store) instead of an int64 flat index;
-//             ties and NaNs resolve exactly like ATen (scan kh-major, take v > max or NaN).
-//   backward: a GATHER per input pixel (no atomics, deterministic): an input row iy is covered by output rows
-//             oy = iy/2 (iy even) or (iy-1)/2 and (iy+1)/2 (iy odd) -- at most 2 x 2 windows -- and receives dy of
-//             each window whose stored tap is its own (fp32 sum, one rounding).  dx is written exactly once, so no
-//             zero-fill pass.
+//   forward : one thread = one output pixel x 8 channels; the K*K taps are 16-B loads; the window position of the
+//             max (0..K*K-1) is kept as one byte per element (8 B per thread, one store) instead of an int64 flat
+//             index; ties and NaNs resolve exactly like ATen (scan kh-major, take v > max or NaN).
+//   backward: a GATHER per input pixel (no atomics, deterministic): input row iy is covered by the output rows oy
+//             with 2 oy - P <= iy <= 2 oy - P + K - 1 (3x3/1: at most 2, 2x2/0: one) and receives dy of each window
+//             whose stored tap is its own (fp32 sum, one rounding).  dx is written exactly once, so no zero-fill
+//             pass (rows / columns outside every window get 0).
 // Traffic: forward reads x (the 9-fold reuse stays in L2) and writes y + 1 byte/elem; backward reads dy + taps
 // (each about 2.25x, L2) and writes dx: both run near a device copy of x.
 #include "dph_common.h"
@@ -21,7 +23,7 @@ namespace {
 
 constexpr int PNT = 256;
 
-template <typename T>
+template <typename T, int K, int P>
 __global__ __launch_bounds__(PNT) void maxpool_fwd_k(const T* __restrict__ x, T* __restrict__ y,
                                                      uint8_t* __restrict__ tap, int H, int W, int Ho, int Wo, int C,
                                                      int64_t total) {
@@ -37,17 +39,17 @@ __global__ __launch_bounds__(PNT) void maxpool_fwd_k(const T* __restrict__ x, T*
     int arg[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) { mx[k] = -__builtin_inff(); arg[k] = 0; }
-    // ATen initialises the index to the window's first in-image tap; a window of all -inf keeps that tap
-    const int ih0 = 2 * oy - 1, iw0 = 2 * ox - 1;
-    const int kh0 = ih0 < 0 ? 1 : 0, kw0 = iw0 < 0 ? 1 : 0;
+    // a window of all -inf keeps its first in-image tap
+    const int ih0 = 2 * oy - P, iw0 = 2 * ox - P;
+    const int kh0 = ih0 < 0 ? -ih0 : 0, kw0 = iw0 < 0 ? -iw0 : 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) arg[k] = kh0 * 3 + kw0;
+    for (int k = 0; k < 8; ++k) arg[k] = kh0 * K + kw0;
 #pragma unroll
-    for (int kh = 0; kh < 3; ++kh) {
+    for (int kh = 0; kh < K; ++kh) {
       const int ih = ih0 + kh;
       if (ih < 0 || ih >= H) continue;
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
+      for (int kw = 0; kw < K; ++kw) {
         const int iw = iw0 + kw;
         if (iw < 0 || iw >= W) continue;
         float v[8];
@@ -56,7 +58,7 @@ __global__ __launch_bounds__(PNT) void maxpool_fwd_k(const T* __restrict__ x, T*
         for (int k = 0; k < 8; ++k) {
           if (v[k] > mx[k] || __builtin_isnan(v[k])) {
             mx[k] = v[k];
-            arg[k] = kh * 3 + kw;
+            arg[k] = kh * K + kw;
           }
         }
       }
@@ -69,7 +71,7 @@ __global__ __launch_bounds__(PNT) void maxpool_fwd_k(const T* __restrict__ x, T*
   }
 }
 
-template <typename T>
+template <typename T, int K, int P>
 __global__ __launch_bounds__(PNT) void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ tap,
                                                      T* __restrict__ dx, int H, int W, int Ho, int Wo, int C,
                                                      int64_t total) {
@@ -81,17 +83,17 @@ __global__ __launch_bounds__(PNT) void maxpool_bwd_k(const T* __restrict__ dy, c
     const int64_t q = p / W;
     const int iy = (int)(q % H);
     const int64_t n = q / H;
-    // output windows covering iy: oy with 2 oy - 1 <= iy <= 2 oy + 1
-    const int oy_lo = iy >> 1, oy_hi = min((iy + 1) >> 1, Ho - 1);
-    const int ox_lo = ix >> 1, ox_hi = min((ix + 1) >> 1, Wo - 1);
+    // output windows covering iy: oy with 2 oy - P <= iy <= 2 oy - P + K - 1
+    const int oy_lo = max(0, (iy + P - K + 2) >> 1), oy_hi = min((iy + P) >> 1, Ho - 1);
+    const int ox_lo = max(0, (ix + P - K + 2) >> 1), ox_hi = min((ix + P) >> 1, Wo - 1);
     float acc[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] = 0.f;
     for (int oy = oy_lo; oy <= oy_hi; ++oy) {
-      const int kh = iy - 2 * oy + 1;
+      const int kh = iy - 2 * oy + P;
       for (int ox = ox_lo; ox <= ox_hi; ++ox) {
-        const int kw = ix - 2 * ox + 1;
-        const int me = kh * 3 + kw;
+        const int kw = ix - 2 * ox + P;
+        const int me = kh * K + kw;
         const int64_t o = ((n * Ho + oy) * Wo + ox) * C + c8 * 8;
         const uint64_t packed = *reinterpret_cast<const uint64_t*>(tap + o);
         float g[8];
@@ -107,28 +109,35 @@ __global__ __launch_bounds__(PNT) void maxpool_bwd_k(const T* __restrict__ dy, c
 
 }  // namespace
 
-void maxpool3s2_fwd(const void* x, void* y, uint8_t* tap, int64_t N, int64_t H, int64_t W, int64_t C, int dtype,
-                    hipStream_t st) {
-  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+#define DPH_POOL_KP(k, ...)                                                      \
+  do {                                                                           \
+    if (k == 3) { constexpr int K = 3, P = 1; __VA_ARGS__; }                     \
+    else { constexpr int K = 2, P = 0; __VA_ARGS__; }                            \
+  } while (0)
+
+void maxpool_s2_fwd(const void* x, void* y, uint8_t* tap, int64_t N, int64_t H, int64_t W, int64_t C, int k,
+                    int dtype, hipStream_t st) {
+  const int64_t Ho = maxpool_s2_out(H, k), Wo = maxpool_s2_out(W, k);
   const int64_t total = N * Ho * Wo * (C / 8);
-  if (total == 0) return;
+  if (total <= 0) return;
   const dim3 grid(stream_grid(total, PNT));
   DPH_DISPATCH_FLOAT(dtype, T, {
-    hipLaunchKernelGGL(maxpool_fwd_k<T>, grid, dim3(PNT), 0, st, (const T*)x, (T*)y, tap, (int)H, (int)W, (int)Ho,
-                       (int)Wo, (int)C, total);
+    DPH_POOL_KP(k, hipLaunchKernelGGL((maxpool_fwd_k<T, K, P>), grid, dim3(PNT), 0, st, (const T*)x, (T*)y, tap,
+                                      (int)H, (int)W, (int)Ho, (int)Wo, (int)C, total));
   });
 }
 
-void maxpool3s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C,
+void maxpool_s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C, int k,
                     int dtype, hipStream_t st) {
-  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int64_t Ho = maxpool_s2_out(H, k), Wo = maxpool_s2_out(W, k);
   const int64_t total = N * H * W * (C / 8);
-  if (total == 0) return;
+  if (total <= 0) return;
   const dim3 grid(stream_grid(total, PNT));
   DPH_DISPATCH_FLOAT(dtype, T, {
-    hipLaunchKernelGGL(maxpool_bwd_k<T>, grid, dim3(PNT), 0, st, (const T*)dy, tap, (T*)dx, (int)H, (int)W, (int)Ho,
-                       (int)Wo, (int)C, total);
+    DPH_POOL_KP(k, hipLaunchKernelGGL((maxpool_bwd_k<T, K, P>), grid, dim3(PNT), 0, st, (const T*)dy, tap, (T*)dx,
+                                      (int)H, (int)W, (int)Ho, (int)Wo, (int)C, total));
   });
 }
+#undef DPH_POOL_KP
 
 }  // namespace dph

@@ -707,36 +707,42 @@ Tensor channel_sum(const Tensor& x, at::ScalarType out_dtype) {
 }
 
 // ------------------------------------------------------------------------------------------------ max pooling
-// x: channels-last [N, C, H, W], C % 8 == 0.  Returns (y channels-last [N, C, Ho, Wo], tap uint8 [N, Ho, Wo, C]).
-std::tuple<Tensor, Tensor> maxpool3s2_fwd(const Tensor& x) {
+// x: channels-last [N, C, H, W], C % 8 == 0; k = 3 (3x3 / 2 / 1) or 2 (2x2 / 2 / 0).
+// Returns (y channels-last [N, C, Ho, Wo], tap uint8 [N, Ho, Wo, C]).
+std::tuple<Tensor, Tensor> maxpool_s2_fwd(const Tensor& x, int64_t k) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
+  TORCH_CHECK(k == 2 || k == 3, "maxpool_s2: kernel 2 or 3");
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "maxpool3s2: channels-last [N, C, H, W] input");
+              "maxpool_s2: channels-last [N, C, H, W] input");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-  TORCH_CHECK(C % 8 == 0 && H >= 1 && W >= 1, "maxpool3s2: channels must be a multiple of 8");
+  TORCH_CHECK(C % 8 == 0 && H >= k - 1 && W >= k - 1, "maxpool_s2: channels must be a multiple of 8");
   check_align16(x, "x");
-  const int64_t Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int64_t Ho = dph::maxpool_s2_out(H, (int)k), Wo = dph::maxpool_s2_out(W, (int)k);
+  TORCH_CHECK(Ho >= 1 && Wo >= 1, "maxpool_s2: empty output");
   auto y = at::empty({N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   auto tap = at::empty({N, Ho, Wo, C}, x.options().dtype(at::kByte));
-  dph::maxpool3s2_fwd(x.data_ptr(), y.data_ptr(), tap.data_ptr<uint8_t>(), N, H, W, C, dt_code(x), cur_stream());
+  dph::maxpool_s2_fwd(x.data_ptr(), y.data_ptr(), tap.data_ptr<uint8_t>(), N, H, W, C, (int)k, dt_code(x),
+                      cur_stream());
   return {y, tap};
 }
 
-Tensor maxpool3s2_bwd(const Tensor& dy, const Tensor& tap, int64_t H, int64_t W) {
+Tensor maxpool_s2_bwd(const Tensor& dy, const Tensor& tap, int64_t H, int64_t W, int64_t k) {
   check_cuda(dy, "dy");
   c10::DeviceGuard g(dy.device());
+  TORCH_CHECK(k == 2 || k == 3, "maxpool_s2_bwd: kernel 2 or 3");
   TORCH_CHECK(dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "maxpool3s2_bwd: channels-last [N, C, Ho, Wo] gradient");
+              "maxpool_s2_bwd: channels-last [N, C, Ho, Wo] gradient");
   const int64_t N = dy.size(0), C = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
-  TORCH_CHECK(C % 8 == 0 && Ho == (H - 1) / 2 + 1 && Wo == (W - 1) / 2 + 1,
-              "maxpool3s2_bwd: gradient shape does not match a 3x3/2/1 pooling of ", H, "x", W);
+  TORCH_CHECK(C % 8 == 0 && Ho == dph::maxpool_s2_out(H, (int)k) && Wo == dph::maxpool_s2_out(W, (int)k),
+              "maxpool_s2_bwd: gradient shape does not match a stride-2 pooling of ", H, "x", W);
   TORCH_CHECK(tap.scalar_type() == at::kByte && tap.is_contiguous() && tap.dim() == 4 && tap.size(0) == N &&
                   tap.size(1) == Ho && tap.size(2) == Wo && tap.size(3) == C && tap.device() == dy.device(),
-              "maxpool3s2_bwd: tap must be the forward's uint8 [N, Ho, Wo, C]");
+              "maxpool_s2_bwd: tap must be the forward's uint8 [N, Ho, Wo, C]");
   check_align16(dy, "dy");
   auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
-  dph::maxpool3s2_bwd(dy.data_ptr(), tap.data_ptr<uint8_t>(), dx.data_ptr(), N, H, W, C, dt_code(dy), cur_stream());
+  dph::maxpool_s2_bwd(dy.data_ptr(), tap.data_ptr<uint8_t>(), dx.data_ptr(), N, H, W, C, (int)k, dt_code(dy),
+                      cur_stream());
   return dx;
 }
 
@@ -996,9 +1002,9 @@ TORCH_LIBRARY(dph, m) {
   m.def("ts_gemm_nt_stats(Tensor A, Tensor B) -> (Tensor, Tensor)");
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
-  m.def("maxpool3s2_fwd(Tensor x) -> (Tensor, Tensor)");
+  m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
-  m.def("maxpool3s2_bwd(Tensor dy, Tensor tap, int H, int W) -> Tensor");
+  m.def("maxpool_s2_bwd(Tensor dy, Tensor tap, int H, int W, int k) -> Tensor");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
         "float momentum, float eps, bool relu, Tensor? pre_stats=None, Tensor(c!)? num_batches_tracked=None) "
         "-> (Tensor, Tensor, Tensor, Tensor)");
@@ -1049,9 +1055,9 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("ts_gemm_nt_stats", &ts_gemm_nt_stats);
   m.impl("ts_gemm_tn_", &ts_gemm_tn_);
   m.impl("transpose2d", &transpose2d);
-  m.impl("maxpool3s2_fwd", &maxpool3s2_fwd);
+  m.impl("maxpool_s2_fwd", &maxpool_s2_fwd);
   m.impl("channel_sum", &channel_sum);
-  m.impl("maxpool3s2_bwd", &maxpool3s2_bwd);
+  m.impl("maxpool_s2_bwd", &maxpool_s2_bwd);
   m.impl("bn_act_fwd", &bn_act_fwd);
   m.impl("bn_act_apply", &bn_act_apply);
   m.impl("bn_act_bwd", &bn_act_bwd);

@@ -15,6 +15,7 @@ from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv import BiasConv2d, BiasConvTranspose2d
+from ..ops.pool import MaxPool2d
 
 
 def conv_block(in_ch: int, out_ch: int) -> nn.Sequential:
@@ -41,7 +42,7 @@ class SimpleUNet(nn.Module):
         self.up1 = BiasConvTranspose2d(2 * b, b, 2, 2)
         self.dec1 = conv_block(2 * b, b)
         self.out = BiasConv2d(b, out_channels, kernel_size=1)
-        self.pool = nn.MaxPool2d(2)
+        self.pool = MaxPool2d(2)   # channels-last HIP kernels (ops/pool.py)
 
     @staticmethod
     def _up(x, size):

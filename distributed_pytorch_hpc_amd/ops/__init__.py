@@ -11,7 +11,7 @@ from .decode import decode_attention, kv_append_
 from .attention import attention_reference, flash_attention, flash_bwd, flash_fwd, rope_attention
 from .embedding import Embedding, embedding
 from .loss import fused_cross_entropy, latitude_weighted_mse, latitude_weights, vocab_parallel_cross_entropy
-from .pool import MaxPool2d, max_pool3s2
+from .pool import MaxPool2d, max_pool2s2, max_pool3s2
 from .norms import LayerNorm, RMSNorm, add_rms_norm, layer_norm, rms_norm, rmsnorm_reference
 from .rope import apply_rope, precompute_rope_tables, rope_, rope_reference
 
@@ -22,5 +22,5 @@ __all__ = [
     "flash_bwd", "rope_attention", "BatchNormAct2d", "Conv1x1", "Conv3x3", "batch_norm_act", "Embedding", "embedding", "fused_cross_entropy", "latitude_weighted_mse",
     "latitude_weights", "vocab_parallel_cross_entropy", "LayerNorm", "RMSNorm", "add_rms_norm", "layer_norm",
     "rms_norm", "rmsnorm_reference", "apply_rope", "precompute_rope_tables", "rope_", "rope_reference",
-    "native_available", "decode_attention", "kv_append_", "MaxPool2d", "max_pool3s2",
+    "native_available", "decode_attention", "kv_append_", "MaxPool2d", "max_pool2s2", "max_pool3s2",
 ]

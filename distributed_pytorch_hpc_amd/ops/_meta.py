@@ -98,124 +98,22 @@ def _transpose2d(x):
     return x.new_empty((x.shape[1], x.shape[0]))
 
 
-@register_fake("dph::maxpool3s2_fwd")
-def _maxpool3s2_fwd(x):
+def _pool_out(n, k):
+    return (n - 1) // 2 + 1 if k == 3 else n // 2
+
+
+@register_fake("dph::maxpool_s2_fwd")
+def _maxpool_s2_fwd(x, k):
     n, c, h, w = x.shape
-    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    ho, wo = _pool_out(h, k), _pool_out(w, k)
     y = x.new_empty((n, c, ho, wo)).contiguous(memory_format=torch.channels_last)
     return y, x.new_empty((n, ho, wo, c), dtype=torch.uint8)
 
 
-@register_fake("dph::maxpool3s2_bwd")
-def _maxpool3s2_bwd(dy, tap, H, W):
+@register_fake("dph::maxpool_s2_bwd")
+def _maxpool_s2_bwd(dy, tap, H, W, k):
     n, c = dy.shape[:2]
     return dy.new_empty((n, c, H, W)).contiguous(memory_format=torch.channels_last)
-
-
-@register_fake("dph::gemm_tn_")
-def _gemm_tn(C, A, B, accumulate):
-    return None
-
-
-@register_fake("dph::ts_gemm_nt_stats")
-def _ts_gemm_nt_stats(A, B):
-    m, n = A.shape[0], B.shape[0]
-    nmb = (m + 127) // 128
-    return A.new_empty((m, n)), A.new_empty((2 * nmb * n + nmb,), dtype=torch.float32)
-
-
-@register_fake("dph::ts_gemm_nt")
-def _ts_gemm_nt(A, B, H=0, W=0, add=None):
-    return A.new_empty((A.shape[0], B.shape[0]))
-
-
-@register_fake("dph::ts_gemm_tn_")
-def _ts_gemm_tn(C, A, B, accumulate, H=0, W=0):
-    return None
-
-
-@register_fake("dph::cross_entropy_fwd")
-def _xent(logits, target, inv_count, ignore_index, grad_inplace, smoothing):
-    n = logits.shape[0]
-    return logits.new_empty((n,), dtype=torch.float32), logits.new_empty((n,), dtype=torch.float32)
-
-
-@register_fake("dph::flash_attn_fwd")
-def _fa_fwd(q, k, v, scale, causal, dropout_p=0.0, seed=0):
-    b, s, h, d = q.shape
-    return q.new_empty((b, s, h, d)), q.new_empty((b, h, s), dtype=torch.float32)
-
-
-@register_fake("dph::flash_attn_bwd")
-def _fa_bwd(dout, q, k, v, o, lse, scale, causal, dropout_p=0.0, seed=0):
-    return torch.empty_like(q), k.new_empty(k.shape), v.new_empty(v.shape)
-
-
-@register_fake("dph::flash_attn_bwd_into")
-def _fa_bwd_into(dout, q, k, v, o, lse, scale, causal, dq, dk, dv, dropout_p=0.0, seed=0, rope_cos=None,
-                 rope_sin=None, rope_offset=0):
-    return None
-
-
-@register_fake("dph::image_augment")
-def _img_aug(images, idx, params, mean, inv_std, pad, channels_last, bf16_out):
-    n, h, w, c = images.shape
-    out = images.new_empty((idx.shape[0], c, h, w), dtype=torch.bfloat16 if bf16_out else torch.float32)
-    return out.contiguous(memory_format=torch.channels_last) if channels_last else out
-
-
-@register_fake("dph::fp8_quantize")
-def _fp8_quant(x, fmt, rowmajor, transposed):
-    f8 = torch.float8_e4m3fn if fmt == 0 else torch.float8_e5m2
-    r, c = x.shape
-    y = x.new_empty((r, c) if rowmajor else (0,), dtype=f8)
-    yt = x.new_empty((c, r) if transposed else (0,), dtype=f8)
-    return y, yt, x.new_empty((), dtype=torch.float32)
-
-
-@register_fake("dph::embedding_fwd")
-def _emb_fwd(ids, table, vocab_start):
-    return table.new_empty((*ids.shape, table.shape[1]))
-
-
-@register_fake("dph::embedding_bwd")
-def _emb_bwd(ids, dout, vocab_local, vocab_start):
-    return dout.new_empty((vocab_local, dout.shape[-1]), dtype=torch.float32)
-
-
-@register_fake("dph::latmse_fwd")
-def _latmse_fwd(pred, target, n_global, lat_offset):
-    return pred.new_empty((), dtype=torch.float32)
-
-
-@register_fake("dph::latmse_bwd")
-def _latmse_bwd(gloss, pred, target, n_global, lat_offset, need_dtarget):
-    return torch.empty_like(pred), (torch.empty_like(target) if need_dtarget else pred.new_empty((0,)))
-
-
-@register_fake("dph::kv_append_")
-def _kv_append(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads, kv_scale=1.0):
-    return None
-
-
-@register_fake("dph::decode_attention")
-def _decode_attn(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale, max_len, kv_scale=1.0):
-    return qkv.new_empty((qkv.shape[0], n_heads * k_cache.shape[-1]))
-
-
-@register_fake("dph::skinny_linear")
-def _skinny_linear(x, w):
-    return x.new_empty((*x.shape[:-1], w.shape[0]))
-
-
-@register_fake("dph::gemv_swiglu")
-def _gemv_swiglu(x2, w):
-    return x2.new_empty((*x2.shape[:-1], w.shape[0]))
-
-
-@register_fake("dph::gemv_rmsnorm")
-def _gemv_rmsnorm(x, res, norm_weight, eps, w):
-    return x.new_empty((*x.shape[:-1], w.shape[0])), (torch.empty_like(x) if res is not None else x.new_empty((0,)))
 
 
 @register_fake("dph::channel_sum")

@@ -1,10 +1,11 @@
-"""3x3 / stride 2 / padding 1 max pooling for channels-last activations (csrc/pool.hip).
+"""Stride-2 max pooling for channels-last activations (csrc/pool.hip): 3x3 / padding 1 and 2x2 / padding 0.
 
 ``MaxPool2d`` is a drop-in ``nn.MaxPool2d`` (no parameters, same module tree): for the ResNet stem's
 ``MaxPool2d(3, 2, 1)`` (reference scripts/main.py:249 builds torchvision resnet50, whose stem is conv 7x7/2 -> BN ->
-ReLU -> max-pool 3x3/2/1) on a channels-last GPU tensor with C % 8 == 0 it runs the HIP kernels: the forward keeps
-the window position of each max as one byte, the backward gathers the gradient per input pixel (deterministic, no
-atomics, no zero-fill).  Any other configuration, or CPU tensors, take ``F.max_pool2d``.
+ReLU -> max-pool 3x3/2/1) and SimpleUNet's ``MaxPool2d(2)`` (multinode_ddp_unet.py:171-214) on a channels-last GPU
+tensor with C % 8 == 0 it runs the HIP kernels: the forward keeps the window position of each max as one byte, the
+backward gathers the gradient per input pixel (deterministic, no atomics, no zero-fill).  Any other configuration,
+or CPU tensors, take ``F.max_pool2d``.
 """
 from __future__ import annotations
 
@@ -21,34 +22,50 @@ def maxpool3s2_native_ok(x: torch.Tensor) -> bool:
             and x.data_ptr() % 16 == 0)
 
 
-class _MaxPool3s2Fn(torch.autograd.Function):
+class _MaxPoolS2Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x):
-        y, tap = _lib.ops().maxpool3s2_fwd(x)
+    def forward(ctx, x, k):
+        y, tap = _lib.ops().maxpool_s2_fwd(x, k)
         ctx.save_for_backward(tap)
-        ctx.hw = (x.shape[2], x.shape[3])
+        ctx.hw, ctx.k = (x.shape[2], x.shape[3]), k
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (tap,) = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
-        return _lib.ops().maxpool3s2_bwd(dy, tap, ctx.hw[0], ctx.hw[1])
+        return _lib.ops().maxpool_s2_bwd(dy, tap, ctx.hw[0], ctx.hw[1], ctx.k), None
 
 
 def max_pool3s2(x: torch.Tensor) -> torch.Tensor:
     """``F.max_pool2d(x, 3, 2, 1)`` with the HIP kernels when eligible."""
     if maxpool3s2_native_ok(x):
-        return _MaxPool3s2Fn.apply(x)
+        return _MaxPoolS2Fn.apply(x, 3)
     return F.max_pool2d(x, 3, 2, 1)
 
 
+def max_pool2s2(x: torch.Tensor) -> torch.Tensor:
+    """``F.max_pool2d(x, 2)`` with the HIP kernels when eligible."""
+    if maxpool3s2_native_ok(x) and x.shape[2] >= 2 and x.shape[3] >= 2:
+        return _MaxPoolS2Fn.apply(x, 2)
+    return F.max_pool2d(x, 2)
+
+
 class MaxPool2d(nn.MaxPool2d):
-    """``nn.MaxPool2d`` whose 3x3 / stride 2 / padding 1 case runs the channels-last HIP kernels."""
+    """``nn.MaxPool2d`` whose 3x3 / stride 2 / padding 1 and 2x2 / stride 2 cases run the channels-last HIP
+    kernels."""
 
     def forward(self, x):
-        fast = (self.kernel_size in (3, (3, 3)) and self.stride in (2, (2, 2)) and self.padding in (1, (1, 1))
-                and self.dilation in (1, (1, 1)) and not self.ceil_mode and not self.return_indices)
-        if fast and maxpool3s2_native_ok(x):
-            return _MaxPool3s2Fn.apply(x)
+        k = {(3, 1): 3, (2, 0): 2}.get((_one(self.kernel_size), _one(self.padding)))
+        fast = (k is not None and _one(self.stride) == 2 and _one(self.dilation) == 1 and not self.ceil_mode
+                and not self.return_indices)
+        if fast and maxpool3s2_native_ok(x) and x.shape[2] >= k - 1 and x.shape[3] >= k - 1:
+            return _MaxPoolS2Fn.apply(x, k)
         return super().forward(x)
+
+
+def _one(v):
+    """A square pooling parameter as an int (None when the two dimensions differ)."""
+    if isinstance(v, (tuple, list)):
+        return v[0] if len(set(v)) == 1 else None
+    return v

@@ -782,18 +782,22 @@ def test_conv3x3_module_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W, 
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 16, 7, 9), (2, 8, 1, 5), (2, 24, 6, 6)])
-def test_maxpool3s2_matches_torch(dph_native, dtype, shape):
-    """csrc/pool.hip vs F.max_pool2d(3, 2, 1) in fp32: forward values bitwise, input gradient (gather over the stored
-    window taps) equal to autograd's scatter -- random data has no ties within a window in fp32."""
+@pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 16, 7, 9), (2, 8, 1, 5), (2, 24, 6, 6), (2, 64, 181, 360)])
+@pytest.mark.parametrize("k", [3, 2])
+def test_maxpool3s2_matches_torch(dph_native, dtype, shape, k):
+    """csrc/pool.hip vs F.max_pool2d (3x3/2/1 and 2x2/2/0) in fp32: forward values bitwise, input gradient (gather
+    over the stored window taps) equal to autograd's scatter -- random data has no ties within a window in fp32."""
     from distributed_pytorch_hpc_amd.ops.pool import MaxPool2d, maxpool3s2_native_ok
 
+    if k == 2 and min(shape[2:]) < 2:
+        pytest.skip("2x2 pooling of a 1-row input is empty")
     torch.manual_seed(0)
     x = torch.randn(*shape, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
     assert maxpool3s2_native_ok(x)
-    y = MaxPool2d(3, 2, 1)(x)
+    pool = MaxPool2d(3, 2, 1) if k == 3 else MaxPool2d(2)
+    y = pool(x)
     xr = x.detach().float().requires_grad_()
-    yr = F.max_pool2d(xr, 3, 2, 1)
+    yr = F.max_pool2d(xr, 3, 2, 1) if k == 3 else F.max_pool2d(xr, 2)
     assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
     assert torch.equal(y.float(), yr)
     g = torch.randn_like(yr)
@@ -808,13 +812,15 @@ def test_maxpool3s2_matches_torch(dph_native, dtype, shape):
 
 def test_maxpool3s2_ties_follow_aten(dph_native):
     """Constant and post-ReLU (many zeros) inputs: the first maximum in kh-major scan order wins, as in ATen."""
-    from distributed_pytorch_hpc_amd.ops.pool import max_pool3s2
+    from distributed_pytorch_hpc_amd.ops.pool import max_pool2s2, max_pool3s2
 
-    for x in (torch.ones(2, 8, 9, 9, device=DEV, dtype=torch.bfloat16),
-              torch.relu(torch.randn(2, 64, 20, 20, device=DEV)).to(torch.bfloat16)):
+    for (x, ours, ref) in ((t, o, r) for t in (torch.ones(2, 8, 9, 9, device=DEV, dtype=torch.bfloat16),
+                                               torch.relu(torch.randn(2, 64, 21, 20, device=DEV)).to(torch.bfloat16))
+                           for o, r in ((max_pool3s2, lambda a: F.max_pool2d(a, 3, 2, 1)),
+                                        (max_pool2s2, lambda a: F.max_pool2d(a, 2)))):
         x = x.contiguous(memory_format=torch.channels_last).requires_grad_()
         xr = x.detach().clone().requires_grad_()
-        y, yr = max_pool3s2(x), F.max_pool2d(xr, 3, 2, 1)
+        y, yr = ours(x), ref(xr)
         assert torch.equal(y, yr)
         g = torch.randn_like(y)
         y.backward(g)
