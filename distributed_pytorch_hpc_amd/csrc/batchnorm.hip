@@ -181,19 +181,25 @@ __global__ __launch_bounds__(BN_NT) void bn_merge_k(const float* __restrict__ pm
   if (c == 0) on[sgm] = acc.n;
 }
 
-// y = act(x * scale + shift [+ res])
+// y = act(x * scale + shift [+ res]).  The grid stride (gridDim.x * 256 vectors) is a multiple of ch8 = C / 8 (a
+// power of two <= 256), so a thread's channel chunk never changes: its 8 scales / shifts are loaded once, into
+// registers, instead of per element from L1.
 template <typename T, bool RES, bool RELU>
 __global__ __launch_bounds__(BN_NT) void bn_apply_k(const T* __restrict__ x, const T* __restrict__ res,
                                                     const float* __restrict__ scale, const float* __restrict__ shift,
                                                     T* __restrict__ y, int64_t nvec, int ch8) {
-  for (int64_t v = (int64_t)blockIdx.x * BN_NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * BN_NT) {
-    const int c0 = (int)(v % ch8) * 8;
+  const int64_t v0 = (int64_t)blockIdx.x * BN_NT + threadIdx.x;
+  const int c0 = (int)(v0 % ch8) * 8;
+  float sc[8], sf[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { sc[i] = scale[c0 + i]; sf[i] = shift[c0 + i]; }
+  for (int64_t v = v0; v < nvec; v += (int64_t)gridDim.x * BN_NT) {
     float a[8], rr[8];
     Vec8<T>::load(x + v * 8, a);
     if (RES) Vec8<T>::load(res + v * 8, rr);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      float t = fmaf(a[i], scale[c0 + i], shift[c0 + i]);
+      float t = fmaf(a[i], sc[i], sf[i]);
       if (RES) t += rr[i];
       a[i] = RELU ? fmaxf(t, 0.f) : t;
     }
@@ -308,19 +314,32 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_dx_k(const T* __restrict__ dy, c
                                                      const float* __restrict__ ss, T* __restrict__ dx,
                                                      T* __restrict__ dres, int64_t nvec, int ch8) {
   const int C = ch8 * 8;
-  for (int64_t v = (int64_t)blockIdx.x * BN_NT + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * BN_NT) {
-    const int c0 = (int)(v % ch8) * 8;
+  // the thread's channel chunk is fixed (grid stride % ch8 == 0, see bn_apply_k): per-channel values in registers
+  const int64_t v0 = (int64_t)blockIdx.x * BN_NT + threadIdx.x;
+  const int c0 = (int)(v0 % ch8) * 8;
+  float mu[8], is[8], k0[8], k1[8], k2[8], ms[8], mb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = c0 + i;
+    mu[i] = mean[c];
+    is[i] = invstd[c];
+    k0[i] = coef[c];
+    k1[i] = coef[C + c];
+    k2[i] = coef[2 * C + c];
+    ms[i] = XMASK ? ss[c] : 0.f;
+    mb[i] = XMASK ? ss[C + c] : 0.f;
+  }
+  for (int64_t v = v0; v < nvec; v += (int64_t)gridDim.x * BN_NT) {
     float g[8], xv[8], yv[8], o[8];
     Vec8<T>::load(dy + v * 8, g);
     Vec8<T>::load(x + v * 8, xv);
     if (RELU && !XMASK) Vec8<T>::load(y + v * 8, yv);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int c = c0 + i;
-      const bool on = XMASK ? fmaf(xv[i], ss[c], ss[C + c]) > 0.f : (!RELU || yv[i] > 0.f);
+      const bool on = XMASK ? fmaf(xv[i], ms[i], mb[i]) > 0.f : (!RELU || yv[i] > 0.f);
       const float dz = on ? g[i] : 0.f;
-      const float xh = (xv[i] - mean[c]) * invstd[c];
-      o[i] = coef[c] * (dz - coef[C + c] - xh * coef[2 * C + c]);
+      const float xh = (xv[i] - mu[i]) * is[i];
+      o[i] = k0[i] * (dz - k1[i] - xh * k2[i]);
       g[i] = dz;
     }
     Vec8<T>::store(dx + v * 8, o);
