@@ -2,9 +2,9 @@
 """Bandwidth of the fused BatchNorm(+residual)+ReLU kernels (csrc/batchnorm.hip) at every ResNet-50 BN shape of a
 B = 256, 224 x 224 channels-last bf16 step, against a device copy of the same activation.
 
-Traffic counted per call (A = activation bytes): forward stats + apply 3A (4A with a residual); backward with the
-ReLU mask recomputed from x 5A (reduce: dy, x; dx: dy, x -> dx); backward with a residual 8A (reduce: dy, y, x;
-dx: dy, y, x -> dx, dres).  One JSON object per shape on stdout plus a summary line.
+Traffic counted per call (A = activation bytes): forward stats + apply 3A (4A + A/16 with a residual: the ReLU bit
+mask); backward with the ReLU mask recomputed from x 5A (reduce: dy, x; dx: dy, x -> dx); backward with a residual
+6A + A/8 (reduce: dy, x, bits; dx: dy, x, bits -> dx, dres).  One JSON object per shape on stdout plus a summary line.
 
     python benchmarks/bn_bench.py [--batch 256] [--json out.json]
 """
@@ -57,16 +57,18 @@ def main():
         b = torch.randn(c, device="cuda", dtype=torch.bfloat16) * 0.1
         rm = torch.zeros(c, device="cuda")
         rv = torch.ones(c, device="cuda")
+        bits = torch.empty(m * c // 8, device="cuda", dtype=torch.uint8)   # ReLU-after-residual mask (1 bit/elem)
         a = x.numel() * 2
         t = {
             "copy": timeit(lambda: x.clone()),
             "fwd": timeit(lambda: o.bn_act_fwd(x, None, w, b, rm, rv, 0.1, 1e-5, True, None, None)),
-            "fwd_res": timeit(lambda: o.bn_act_fwd(x, r, w, b, rm, rv, 0.1, 1e-5, True, None, None)),
+            "fwd_res": timeit(lambda: o.bn_act_fwd(x, r, w, b, rm, rv, 0.1, 1e-5, True, None, None, bits)),
         }
         y, mean, invstd, ss = o.bn_act_fwd(x, None, w, b, rm, rv, 0.1, 1e-5, True, None, None)
         t["bwd_xmask"] = timeit(lambda: o.bn_act_bwd(dy, x, x, mean, invstd, w, True, False, True, ss, None, None))
-        t["bwd_res"] = timeit(lambda: o.bn_act_bwd(dy, y, x, mean, invstd, w, True, True, True, None, None, None))
-        traffic = {"copy": 2, "fwd": 3, "fwd_res": 4, "bwd_xmask": 5, "bwd_res": 8}
+        t["bwd_res"] = timeit(lambda: o.bn_act_bwd(dy, y, x, mean, invstd, w, True, True, True, None, None, None,
+                                                   bits))
+        traffic = {"copy": 2, "fwd": 3, "fwd_res": 4 + 1 / 16, "bwd_xmask": 5, "bwd_res": 6 + 1 / 8}
         row = {"M": m, "C": c, "calls": calls, "MB": round(a / 1e6, 1)}
         for k, ms in t.items():
             row[k + "_us"] = round(ms * 1e3, 1)

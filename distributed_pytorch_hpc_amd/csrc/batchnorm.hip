@@ -9,6 +9,8 @@
 //   backward: reduce (read dy, y, x) + dx (read dy, y, x, write dx [+ dres])      = 7A (+A)
 //             ReLU without residual: the mask [x * scale + shift > 0] is recomputed from x with the forward's
 //             own fp32 scale / shift (bit-identical to y > 0), so y is not read:  5A
+//             ReLU with residual: the forward's apply pass also writes the mask [y > 0] as one BIT per element
+//             (A / 16 bytes) and both backward passes read it instead of y:  5A + A / 8
 // Statistics are accumulated with a per-thread shift (the thread's first value) and merged across threads and
 // blocks with Chan's parallel-variance formula, so large-mean channels do not lose the variance to fp32
 // cancellation; all reductions go through fixed-order partial buffers (deterministic).
@@ -183,11 +185,12 @@ __global__ __launch_bounds__(BN_NT) void bn_merge_k(const float* __restrict__ pm
 
 // y = act(x * scale + shift [+ res]).  The grid stride (gridDim.x * 256 vectors) is a multiple of ch8 = C / 8 (a
 // power of two <= 256), so a thread's channel chunk never changes: its 8 scales / shifts are loaded once, into
-// registers, instead of per element from L1.
-template <typename T, bool RES, bool RELU>
+// registers, instead of per element from L1.  MASK: also store [y > 0] of the vector's 8 elements as one byte.
+template <typename T, bool RES, bool RELU, bool MASK = false>
 __global__ __launch_bounds__(BN_NT) void bn_apply_k(const T* __restrict__ x, const T* __restrict__ res,
                                                     const float* __restrict__ scale, const float* __restrict__ shift,
-                                                    T* __restrict__ y, int64_t nvec, int ch8) {
+                                                    T* __restrict__ y, int64_t nvec, int ch8,
+                                                    uint8_t* __restrict__ mask = nullptr) {
   const int64_t v0 = (int64_t)blockIdx.x * BN_NT + threadIdx.x;
   const int c0 = (int)(v0 % ch8) * 8;
   float sc[8], sf[8];
@@ -204,17 +207,25 @@ __global__ __launch_bounds__(BN_NT) void bn_apply_k(const T* __restrict__ x, con
       a[i] = RELU ? fmaxf(t, 0.f) : t;
     }
     Vec8<T>::store(y + v * 8, a);
+    if constexpr (MASK) {   // from the stored (rounded) values: the same test the backward applied to y
+      unsigned m = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) m |= ((float)from_f32<T>(a[i]) > 0.f ? 1u : 0u) << i;
+      mask[v] = (uint8_t)m;
+    }
   }
 }
 
 // Backward reduction: per channel sum(dz) and sum(dz * xhat), dz = dy * [y > 0 when RELU].
 // XMASK: the ReLU mask comes from x * scale + shift (ss = [scale | shift], the forward's values) instead of y.
-template <typename T, bool RELU, bool XMASK>
+// BMASK: the ReLU mask comes from the forward's bit mask (one byte per 8-channel vector) instead of y.
+template <typename T, bool RELU, bool XMASK, bool BMASK = false>
 __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_k(const T* __restrict__ dy, const T* __restrict__ y,
                                                          const T* __restrict__ x, const float* __restrict__ mean,
                                                          const float* __restrict__ invstd,
                                                          const float* __restrict__ ss, float* __restrict__ part,
-                                                         int64_t M, int C, int64_t rows_per_block) {
+                                                         int64_t M, int C, int64_t rows_per_block,
+                                                         const uint8_t* __restrict__ bmask = nullptr) {
   extern __shared__ float sh[];   // [2][BN_NT][8]
   const int ch8 = C / 8, rpi = BN_NT / ch8;
   const int cc = threadIdx.x % ch8, r0 = threadIdx.x / ch8;
@@ -233,10 +244,12 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_k(const T* __restrict__ d
     float g[8], xv[8], yv[8];
     Vec8<T>::load(dy + r * C + cc * 8, g);
     Vec8<T>::load(x + r * C + cc * 8, xv);
-    if (RELU && !XMASK) Vec8<T>::load(y + r * C + cc * 8, yv);
+    if (RELU && !XMASK && !BMASK) Vec8<T>::load(y + r * C + cc * 8, yv);
+    const unsigned mb = BMASK ? bmask[r * ch8 + cc] : 0u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const bool on = XMASK ? fmaf(xv[i], xs[i], xb[i]) > 0.f : (!RELU || yv[i] > 0.f);
+      const bool on = BMASK ? ((mb >> i) & 1u) != 0u
+                            : (XMASK ? fmaf(xv[i], xs[i], xb[i]) > 0.f : (!RELU || yv[i] > 0.f));
       const float dz = on ? g[i] : 0.f;
       sd[i] += dz;
       sdx[i] = fmaf(dz, (xv[i] - mu[i]) * is[i], sdx[i]);
@@ -307,12 +320,13 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_finalize_k(const float* __restri
   coef[2 * C + c] = b / count;
 }
 
-template <typename T, bool RELU, bool DRES, bool XMASK>
+template <typename T, bool RELU, bool DRES, bool XMASK, bool BMASK = false>
 __global__ __launch_bounds__(BN_NT) void bn_bwd_dx_k(const T* __restrict__ dy, const T* __restrict__ y,
                                                      const T* __restrict__ x, const float* __restrict__ mean,
                                                      const float* __restrict__ invstd, const float* __restrict__ coef,
                                                      const float* __restrict__ ss, T* __restrict__ dx,
-                                                     T* __restrict__ dres, int64_t nvec, int ch8) {
+                                                     T* __restrict__ dres, int64_t nvec, int ch8,
+                                                     const uint8_t* __restrict__ bmask = nullptr) {
   const int C = ch8 * 8;
   // the thread's channel chunk is fixed (grid stride % ch8 == 0, see bn_apply_k): per-channel values in registers
   const int64_t v0 = (int64_t)blockIdx.x * BN_NT + threadIdx.x;
@@ -333,10 +347,12 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_dx_k(const T* __restrict__ dy, c
     float g[8], xv[8], yv[8], o[8];
     Vec8<T>::load(dy + v * 8, g);
     Vec8<T>::load(x + v * 8, xv);
-    if (RELU && !XMASK) Vec8<T>::load(y + v * 8, yv);
+    if (RELU && !XMASK && !BMASK) Vec8<T>::load(y + v * 8, yv);
+    const unsigned bits = BMASK ? bmask[v] : 0u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const bool on = XMASK ? fmaf(xv[i], ms[i], mb[i]) > 0.f : (!RELU || yv[i] > 0.f);
+      const bool on = BMASK ? ((bits >> i) & 1u) != 0u
+                            : (XMASK ? fmaf(xv[i], ms[i], mb[i]) > 0.f : (!RELU || yv[i] > 0.f));
       const float dz = on ? g[i] : 0.f;
       const float xh = (xv[i] - mu[i]) * is[i];
       o[i] = k0[i] * (dz - k1[i] - xh * k2[i]);
@@ -368,7 +384,7 @@ int bn_partial_blocks(int64_t M, int64_t C) {
 void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const void* b, void* rmean, void* rvar,
                   float* mean, float* invstd, float* scale, float* shift, float* workspace, int64_t M, int64_t C,
                   float momentum, float eps, bool relu, int dt, int pdt, int rdt, hipStream_t st,
-                  const float* pre_stats, int pre_groups, int64_t* nbt) {
+                  const float* pre_stats, int pre_groups, int64_t* nbt, uint8_t* relu_mask) {
   int64_t rpb;
   int G = stats_grid(M, (int)C, &rpb);
   const float* pmean = workspace;
@@ -402,42 +418,48 @@ void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const 
   else if (rdt == kBF16) DPH_BN_FIN(float, bf16);
   else DPH_BN_FIN(float, float);
 #undef DPH_BN_FIN
-  bn_apply(x, res, scale, shift, y, M, C, relu, dt, st);
+  bn_apply(x, res, scale, shift, y, M, C, relu, dt, st, relu_mask);
 }
 
 void bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int64_t M, int64_t C,
-              bool relu, int dt, hipStream_t st) {
+              bool relu, int dt, hipStream_t st, uint8_t* relu_mask) {
   const int64_t nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, BN_NT));
   DPH_DISPATCH_FLOAT(dt, T, {
-    if (res && relu) hipLaunchKernelGGL((bn_apply_k<T, true, true>), grid, dim3(BN_NT), 0, st, (const T*)x,
-                                        (const T*)res, scale, shift, (T*)y, nvec, (int)(C / 8));
+    if (res && relu && relu_mask)
+      hipLaunchKernelGGL((bn_apply_k<T, true, true, true>), grid, dim3(BN_NT), 0, st, (const T*)x, (const T*)res,
+                         scale, shift, (T*)y, nvec, (int)(C / 8), relu_mask);
+    else if (res && relu) hipLaunchKernelGGL((bn_apply_k<T, true, true>), grid, dim3(BN_NT), 0, st, (const T*)x,
+                                             (const T*)res, scale, shift, (T*)y, nvec, (int)(C / 8), nullptr);
     else if (res) hipLaunchKernelGGL((bn_apply_k<T, true, false>), grid, dim3(BN_NT), 0, st, (const T*)x,
-                                     (const T*)res, scale, shift, (T*)y, nvec, (int)(C / 8));
+                                     (const T*)res, scale, shift, (T*)y, nvec, (int)(C / 8), nullptr);
     else if (relu) hipLaunchKernelGGL((bn_apply_k<T, false, true>), grid, dim3(BN_NT), 0, st, (const T*)x,
-                                      (const T*)nullptr, scale, shift, (T*)y, nvec, (int)(C / 8));
+                                      (const T*)nullptr, scale, shift, (T*)y, nvec, (int)(C / 8), nullptr);
     else hipLaunchKernelGGL((bn_apply_k<T, false, false>), grid, dim3(BN_NT), 0, st, (const T*)x, (const T*)nullptr,
-                            scale, shift, (T*)y, nvec, (int)(C / 8));
+                            scale, shift, (T*)y, nvec, (int)(C / 8), nullptr);
   });
 }
 
 void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
             void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dt,
-            int pdt, hipStream_t st, const float* xmask_ss) {
-  const bool xm = relu && xmask_ss != nullptr;
+            int pdt, hipStream_t st, const float* xmask_ss, const uint8_t* relu_mask) {
+  const bool bm = relu && relu_mask != nullptr;
+  const bool xm = relu && !bm && xmask_ss != nullptr;
   int64_t rpb;
   const int G = stats_grid(M, (int)C, &rpb);
   float* part = workspace;                       // [G][2C]
   float* coef = workspace + 2 * (int64_t)G * C;  // [3C]
   const size_t shs = 2 * BN_NT * 8 * sizeof(float);
+#define DPH_BN_RED(R_, X_, B_)                                                                                     \
+  hipLaunchKernelGGL((bn_bwd_reduce_k<T, R_, X_, B_>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy, (const T*)y,  \
+                     (const T*)x, mean, invstd, xmask_ss, part, M, (int)C, rpb, relu_mask)
   DPH_DISPATCH_FLOAT(dt, T, {
-    if (xm) hipLaunchKernelGGL((bn_bwd_reduce_k<T, true, true>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy,
-                               (const T*)y, (const T*)x, mean, invstd, xmask_ss, part, M, (int)C, rpb);
-    else if (relu) hipLaunchKernelGGL((bn_bwd_reduce_k<T, true, false>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy,
-                                      (const T*)y, (const T*)x, mean, invstd, nullptr, part, M, (int)C, rpb);
-    else hipLaunchKernelGGL((bn_bwd_reduce_k<T, false, false>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy,
-                            (const T*)y, (const T*)x, mean, invstd, nullptr, part, M, (int)C, rpb);
+    if (bm) DPH_BN_RED(true, false, true);
+    else if (xm) DPH_BN_RED(true, true, false);
+    else if (relu) DPH_BN_RED(true, false, false);
+    else DPH_BN_RED(false, false, false);
   });
+#undef DPH_BN_RED
   const dim3 fg((unsigned)(C / 8));
   if (pdt == kBF16)
     hipLaunchKernelGGL((bn_bwd_finalize_k<bf16>), fg, dim3(BN_NT), 0, st, part, G, (int)C, (float)M, (const bf16*)w,
@@ -447,16 +469,18 @@ void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, con
                        (const float*)w, invstd, (float*)dw, (float*)db, coef);
   const int64_t nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, BN_NT));
-#define DPH_BN_DX(R_, D_, X_)                                                                                     \
-  hipLaunchKernelGGL((bn_bwd_dx_k<T, R_, D_, X_>), grid, dim3(BN_NT), 0, st, (const T*)dy, (const T*)y,           \
-                     (const T*)x, mean, invstd, coef, xmask_ss, (T*)dx, (T*)dres, nvec, (int)(C / 8))
+#define DPH_BN_DX(R_, D_, X_, B_)                                                                                 \
+  hipLaunchKernelGGL((bn_bwd_dx_k<T, R_, D_, X_, B_>), grid, dim3(BN_NT), 0, st, (const T*)dy, (const T*)y,       \
+                     (const T*)x, mean, invstd, coef, xmask_ss, (T*)dx, (T*)dres, nvec, (int)(C / 8), relu_mask)
   DPH_DISPATCH_FLOAT(dt, T, {
-    if (xm && dres) DPH_BN_DX(true, true, true);
-    else if (xm) DPH_BN_DX(true, false, true);
-    else if (relu && dres) DPH_BN_DX(true, true, false);
-    else if (relu) DPH_BN_DX(true, false, false);
-    else if (dres) DPH_BN_DX(false, true, false);
-    else DPH_BN_DX(false, false, false);
+    if (bm && dres) DPH_BN_DX(true, true, false, true);
+    else if (bm) DPH_BN_DX(true, false, false, true);
+    else if (xm && dres) DPH_BN_DX(true, true, true, false);
+    else if (xm) DPH_BN_DX(true, false, true, false);
+    else if (relu && dres) DPH_BN_DX(true, true, false, false);
+    else if (relu) DPH_BN_DX(true, false, false, false);
+    else if (dres) DPH_BN_DX(false, true, false, false);
+    else DPH_BN_DX(false, false, false, false);
   });
 #undef DPH_BN_DX
 }

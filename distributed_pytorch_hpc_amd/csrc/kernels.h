@@ -141,13 +141,16 @@ void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const 
                   float* mean, float* invstd, float* scale, float* shift, float* workspace, int64_t M, int64_t C,
                   float momentum, float eps, bool relu, int dtype, int param_dtype, int running_dtype,
                   hipStream_t stream, const float* pre_stats = nullptr, int pre_groups = 0,
-                  int64_t* num_batches_tracked = nullptr);
+                  int64_t* num_batches_tracked = nullptr, uint8_t* relu_mask = nullptr);
+// relu_mask (optional, ReLU only): also write [y > 0] as bits, one byte per 8-channel vector ([M * C / 8] bytes).
 void bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int64_t M, int64_t C,
-              bool relu, int dtype, hipStream_t stream);
+              bool relu, int dtype, hipStream_t stream, uint8_t* relu_mask = nullptr);
 // xmask_ss (optional, fp32 [scale | shift] of the forward): ReLU mask from x instead of reading y.
+// relu_mask (optional): the forward's bit mask instead of y (takes precedence over xmask_ss).
 void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
             void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dtype,
-            int param_dtype, hipStream_t stream, const float* xmask_ss = nullptr);
+            int param_dtype, hipStream_t stream, const float* xmask_ss = nullptr,
+            const uint8_t* relu_mask = nullptr);
 
 // Stride-2 max pooling, channels-last [N, H, W, C] (C % 8 == 0), csrc/pool.hip: k = 3 (padding 1) or 2 (padding 0),
 // floor mode.  tap: one byte per output element, the window position (0..k*k-1) of the max; the backward gathers

@@ -784,7 +784,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
                                               const c10::optional<Tensor>& rmean, const c10::optional<Tensor>& rvar,
                                               double momentum, double eps, bool relu,
                                               const c10::optional<Tensor>& pre_stats,
-                                              const c10::optional<Tensor>& num_batches_tracked) {
+                                              const c10::optional<Tensor>& num_batches_tracked,
+                                              const c10::optional<Tensor>& relu_mask_out) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
   const int64_t C = bn_channels(x), M = x.numel() / C;
@@ -814,6 +815,13 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
                 "bn_act_fwd: pre_stats must be fp32 [mean G*C | M2 G*C | rows G]");
     pre_groups = (int)(pre->numel() / (2 * C + 1));
   }
+  uint8_t* rmask = nullptr;   // [y > 0] bits for the backward (ReLU after a residual add: y is not re-read)
+  if (relu_mask_out.has_value()) {
+    TORCH_CHECK(relu && relu_mask_out->scalar_type() == at::kByte && relu_mask_out->is_contiguous() &&
+                    relu_mask_out->numel() == M * C / 8 && relu_mask_out->device() == x.device(),
+                "bn_act_fwd: relu_mask_out must be a contiguous uint8 [M * C / 8] and relu set");
+    rmask = relu_mask_out->data_ptr<uint8_t>();
+  }
   const int G = dph::bn_partial_blocks(M, C);
   auto ws = at::empty({2 * (int64_t)G * C + G}, fopt);
   const int pdt = w ? dt_code(*w) : (b ? dt_code(*b) : dph::kF32);
@@ -823,7 +831,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
                     rvar ? rvar->data_ptr() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                     ss.data_ptr<float>(), ss.data_ptr<float>() + C, ws.data_ptr<float>(), M, C, (float)momentum,
                     (float)eps, relu, dt_code(x), pdt, rdt, cur_stream(), pre ? pre->data_ptr<float>() : nullptr,
-                    pre_groups, nbt);
+                    pre_groups, nbt, rmask);
   return {y, mean, invstd, ss};
 }
 
@@ -847,13 +855,21 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Te
                                                       const c10::optional<Tensor>& w, bool relu, bool need_dres,
                                                       bool need_dwb, const c10::optional<Tensor>& xmask_ss,
                                                       const c10::optional<Tensor>& dw_out,
-                                                      const c10::optional<Tensor>& db_out) {
+                                                      const c10::optional<Tensor>& db_out,
+                                                      const c10::optional<Tensor>& relu_mask) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
   const int64_t C = bn_channels(x), M = x.numel() / C;
   check_like(dy, x, "dy");
-  const bool xm = relu && xmask_ss.has_value();
-  if (xm) {
+  const bool bm = relu && relu_mask.has_value();
+  if (bm) {
+    TORCH_CHECK(relu_mask->scalar_type() == at::kByte && relu_mask->is_contiguous() &&
+                    relu_mask->numel() == M * C / 8 && relu_mask->device() == x.device(),
+                "bn_act_bwd: relu_mask must be the forward's uint8 [M * C / 8] bits");
+  }
+  const bool xm = relu && !bm && xmask_ss.has_value();
+  if (bm) {
+  } else if (xm) {
     TORCH_CHECK(xmask_ss->scalar_type() == at::kFloat && xmask_ss->numel() == 2 * C && xmask_ss->is_contiguous(),
                 "bn_act_bwd: xmask_ss must be the forward's fp32 [scale | shift]");
   } else {
@@ -880,7 +896,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Te
   dph::bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
               w ? w->data_ptr() : nullptr, dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr,
               need_dwb ? dw.data_ptr() : nullptr, need_dwb ? db.data_ptr() : nullptr, ws.data_ptr<float>(), M, C, relu,
-              dt_code(x), w ? dt_code(*w) : dph::kF32, cur_stream(), xm ? xmask_ss->data_ptr<float>() : nullptr);
+              dt_code(x), w ? dt_code(*w) : dph::kF32, cur_stream(), xm ? xmask_ss->data_ptr<float>() : nullptr,
+              bm ? relu_mask->data_ptr<uint8_t>() : nullptr);
   return {dx, dres, dw, db};
 }
 
@@ -1006,11 +1023,13 @@ TORCH_LIBRARY(dph, m) {
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
   m.def("maxpool_s2_bwd(Tensor dy, Tensor tap, int H, int W, int k) -> Tensor");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
-        "float momentum, float eps, bool relu, Tensor? pre_stats=None, Tensor(c!)? num_batches_tracked=None) "
+        "float momentum, float eps, bool relu, Tensor? pre_stats=None, Tensor(c!)? num_batches_tracked=None, "
+        "Tensor(d!)? relu_mask_out=None) "
         "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "
-        "bool need_dwb, Tensor? xmask_ss=None, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) "
+        "bool need_dwb, Tensor? xmask_ss=None, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, "
+        "Tensor? relu_mask=None) "
         "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("latmse_fwd(Tensor pred, Tensor target, int n_global, int lat_offset) -> Tensor");
   m.def("latmse_bwd(Tensor gloss, Tensor pred, Tensor target, int n_global, int lat_offset, bool need_dtarget) -> "

@@ -74,7 +74,8 @@ def _sumsq(x, out):
 
 
 @register_fake("dph::bn_act_fwd")
-def _bn_act_fwd(x, res, w, b, rm, rv, momentum, eps, relu, pre_stats=None, num_batches_tracked=None):
+def _bn_act_fwd(x, res, w, b, rm, rv, momentum, eps, relu, pre_stats=None, num_batches_tracked=None,
+                relu_mask_out=None):
     c = x.shape[1]
     return (torch.empty_like(x), x.new_empty((c,), dtype=torch.float32), x.new_empty((c,), dtype=torch.float32),
             x.new_empty((2 * c,), dtype=torch.float32))
@@ -86,7 +87,8 @@ def _bn_act_apply(x, res, scale, shift, relu):
 
 
 @register_fake("dph::bn_act_bwd")
-def _bn_act_bwd(dy, y, x, mean, invstd, w, relu, need_dres, need_dwb, xmask_ss=None, dw_out=None, db_out=None):
+def _bn_act_bwd(dy, y, x, mean, invstd, w, relu, need_dres, need_dwb, xmask_ss=None, dw_out=None, db_out=None,
+                relu_mask=None):
     c = x.shape[1]
     pdt = w.dtype if w is not None else torch.float32
     return (torch.empty_like(x), torch.empty_like(x) if need_dres else x.new_empty((0,)),

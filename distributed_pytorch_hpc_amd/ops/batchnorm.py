@@ -41,12 +41,15 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, slot=None,
                 pre_stats=None, nbt=None):
-        y, mean, invstd, ss = _lib.ops().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, momentum,
-                                                    eps, relu, pre_stats, nbt)
         # ReLU without residual: the backward recomputes the mask from x with the forward's scale / shift and
-        # never reads y (one activation-sized read less in each backward pass)
+        # never reads y (one activation-sized read less in each backward pass).  ReLU after a residual add: the
+        # forward writes [y > 0] as bits (1/16 of y's bytes) and the backward reads those instead of y.
         ctx.xmask = relu and residual is None
-        ctx.save_for_backward(x, ss if ctx.xmask else y, mean, invstd, weight)
+        ctx.bmask = relu and residual is not None
+        bits = x.new_empty((x.numel() // 8,), dtype=torch.uint8) if ctx.bmask else None
+        y, mean, invstd, ss = _lib.ops().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, momentum,
+                                                    eps, relu, pre_stats, nbt, bits)
+        ctx.save_for_backward(x, ss if ctx.xmask else (bits if ctx.bmask else y), mean, invstd, weight)
         ctx.relu, ctx.has_res = relu, residual is not None
         ctx.has_wb = weight is not None
         ctx.params = (weight, bias)
@@ -55,10 +58,13 @@ class _BNActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, y_or_ss, mean, invstd, weight = ctx.saved_tensors
+        x, saved, mean, invstd, weight = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         need_wb = ctx.has_wb and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
-        y, ss = (x, y_or_ss) if ctx.xmask else (y_or_ss, None)
+        # y is only read by the kernels when neither mask form applies (no ReLU: it is not read at all)
+        y = saved if not (ctx.xmask or ctx.bmask) else x
+        ss = saved if ctx.xmask else None
+        bits = saved if ctx.bmask else None
         # engine-owned parameters (parallel/data_parallel.py main_grad views) on their first gradient of the step:
         # the kernel writes dgamma / dbeta straight into the gradient bucket, autograd gets None
         wp, bp = ctx.params
@@ -67,7 +73,7 @@ class _BNActFn(torch.autograd.Function):
             and p.main_grad.is_contiguous() and p.main_grad.dtype == p.dtype for p in (wp, bp)))
         dx, dres, dw, db = _lib.ops().bn_act_bwd(dy, y, x, mean, invstd, weight if ctx.has_wb else None, ctx.relu,
                                                  ctx.has_res, need_wb, ss, wp.main_grad if direct else None,
-                                                 bp.main_grad if direct else None)
+                                                 bp.main_grad if direct else None, bits)
         if direct:
             for p in (wp, bp):
                 p._dph_accum = True

@@ -946,3 +946,28 @@ def test_unet_fused_path_matches_reference(dph_native):
     # fp32 both ways; the BN reductions sum in a different order (measured 2e-3 over 18 BN layers; the biases of
     # the convolutions that feed a BN have an exactly-zero gradient in exact arithmetic, so theirs is rounding noise)
     assert rel_err(grads[0], grads[1]) < 1e-2
+
+
+@pytest.mark.parametrize("C", [64, 256, 2048])
+def test_bn_residual_relu_bitmask_matches_y_path(dph_native, C):
+    """ReLU after a residual add: the backward reading the forward's bit mask equals the backward reading y, bitwise."""
+    from distributed_pytorch_hpc_amd.ops import _lib
+
+    o = _lib.ops()
+    torch.manual_seed(0)
+    x = torch.randn(4, C, 9, 7, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    r = torch.randn_like(x)
+    dy = torch.randn_like(x)
+    w = (torch.rand(C, device=DEV) + 0.5).to(torch.bfloat16)
+    b = (0.1 * torch.randn(C, device=DEV)).to(torch.bfloat16)
+    bits = torch.zeros(x.numel() // 8, device=DEV, dtype=torch.uint8)
+    y, mean, invstd, _ = o.bn_act_fwd(x, r, w, b, None, None, 0.1, 1e-5, True, None, None, bits)
+    y2, *_ = o.bn_act_fwd(x, r, w, b, None, None, 0.1, 1e-5, True, None, None)
+    assert torch.equal(y, y2)
+    ref_bits = (y.permute(0, 2, 3, 1).reshape(-1, 8) > 0).to(torch.int32)
+    ref_bits = (ref_bits << torch.arange(8, device=DEV, dtype=torch.int32)).sum(1).to(torch.uint8)
+    assert torch.equal(bits, ref_bits)
+    got = o.bn_act_bwd(dy, x, x, mean, invstd, w, True, True, True, None, None, None, bits)
+    ref = o.bn_act_bwd(dy, y, x, mean, invstd, w, True, True, True, None, None, None)
+    for g, e in zip(got, ref):
+        assert torch.equal(g, e)
