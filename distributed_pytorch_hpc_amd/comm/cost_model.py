@@ -148,3 +148,46 @@ def measure(op: str, sizes_bytes: list[int], group=None, device=None, dtype=torc
         # message size in the rccl-tests convention: all-gather counts the gathered (output) bytes
         out.append((float(numel * esz * (world if op == "all_gather" else 1)), tt.item()))
     return out
+
+
+@dataclass
+class StepPrediction:
+    world: int
+    ms_per_step: float
+    exposed_comm_ms: float
+    rs_ms: float
+    ag_ms: float
+    optimizer_ms: float
+    efficiency: float        # value(N) / (N * value(1)) for a weak-scaling run
+
+
+def predict_sharded_step(compute_ms: float, optimizer_ms: float, grad_bytes: float, param_bytes: float, world: int,
+                         bucket_bytes: float, fits: dict[str, AlphaBeta] | None = None,
+                         backward_fraction: float = 2.0 / 3.0, comm_slowdown: float = 0.0) -> StepPrediction:
+    """Weak-scaling step time of the sharded data-parallel engine (parallel/data_parallel.py, shard=True: bucketed
+    reduce-scatter of the gradients overlapped with backward, 1/N optimizer sweep, bucketed parameter all-gather
+    overlapped with the next forward) from the 1-GPU step and the alpha-beta fits.
+
+    ``compute_ms``: forward + backward of the 1-GPU step (its optimizer excluded: ``optimizer_ms``).  Exposed
+    communication = the last reduce-scatter bucket (issued when backward ends) + the first all-gather bucket (the
+    next forward waits for it) + whatever part of the reduce-scatter (all-gather) stream does not fit under the
+    backward (forward) window.  ``comm_slowdown``: fractional compute slowdown while collectives run beside it
+    (RCCL kernels occupy CUs); 0 unless measured.  A MODEL for planning and for checking the driver's measured
+    curve against -- not a measurement."""
+    if world <= 1:
+        t = compute_ms + optimizer_ms
+        return StepPrediction(1, t, 0.0, 0.0, 0.0, optimizer_ms, 1.0)
+    fits = fits or load_fits()
+    rs = AlphaBeta("reduce_scatter", world, fits["reduce_scatter"].alpha_s, fits["reduce_scatter"].beta_bus_Bps)
+    ag = AlphaBeta("all_gather", world, fits["all_gather"].alpha_s, fits["all_gather"].beta_bus_Bps)
+    nb_g = max(1, math.ceil(grad_bytes / bucket_bytes))
+    nb_p = max(1, math.ceil(param_bytes / bucket_bytes))
+    rs_ms = 1e3 * nb_g * rs.time(grad_bytes / nb_g)
+    ag_ms = 1e3 * nb_p * ag.time(param_bytes / nb_p)
+    bwd_ms, fwd_ms = compute_ms * backward_fraction, compute_ms * (1.0 - backward_fraction)
+    exposed = 1e3 * rs.time(grad_bytes / nb_g) + 1e3 * ag.time(param_bytes / nb_p)
+    exposed += max(0.0, rs_ms - bwd_ms) + max(0.0, ag_ms - fwd_ms)
+    busy = compute_ms * (1.0 + comm_slowdown * min(1.0, (rs_ms + ag_ms) / compute_ms))
+    t = busy + optimizer_ms / world + exposed
+    t1 = compute_ms + optimizer_ms
+    return StepPrediction(world, t, exposed, rs_ms, ag_ms, optimizer_ms / world, t1 / t)

@@ -82,3 +82,21 @@ def test_engine_auto_buckets(tmp_path):
     res = run_distributed(_engine_auto, 2, path)[0]
     # 8 x (256*256 + 256) fp32 params = 2.1 MB: the overlap bound (>= 4 buckets) wins -> 1 MiB granule buckets
     assert res["mb"] == 1.0 and res["n"] >= 2
+
+
+def test_sharded_step_prediction_weak_scaling():
+    """predict_sharded_step: N=1 is the 1-GPU step; the optimizer sweep shrinks 1/N; with collectives that fit under
+    the compute windows only the first / last bucket is exposed; starving the bus makes communication exposed."""
+    from distributed_pytorch_hpc_amd.comm.cost_model import AlphaBeta, predict_sharded_step
+
+    fits = {op: AlphaBeta(op, 8, 30e-6, 300e9) for op in ("reduce_scatter", "all_gather")}
+    g = p = 13.5e9
+    one = predict_sharded_step(1110.0, 35.0, g, p, 1, 256 * 2 ** 20, fits)
+    assert one.ms_per_step == 1145.0 and one.efficiency == 1.0
+    eight = predict_sharded_step(1110.0, 35.0, g, p, 8, 256 * 2 ** 20, fits)
+    assert eight.optimizer_ms == 35.0 / 8
+    assert 0.0 < eight.exposed_comm_ms < 5.0                   # one 256 MiB bucket each way
+    assert eight.efficiency > 1.0                              # sharded optimizer: N > 1 can beat N = 1 per GPU
+    slow = {op: AlphaBeta(op, 8, 30e-6, 10e9) for op in ("reduce_scatter", "all_gather")}
+    starved = predict_sharded_step(1110.0, 35.0, g, p, 8, 256 * 2 ** 20, slow)
+    assert starved.exposed_comm_ms > 500.0 and starved.efficiency < 0.7
