@@ -123,8 +123,11 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_k(const T* __restrict__ x, flo
 
 // Merge G partials per channel; produce mean / invstd, the apply coefficients and the running-stat update.
 // One block per 8-channel chunk: 32 row-groups of 8 lanes each merge a strided slice of the partials (loads
-// issued 4 at a time so the chain is not one memory latency per partial), then a fixed-order LDS tree.
+// issued FIN_UNROLL at a time so the chain is not one memory latency per partial), then a fixed-order LDS tree.
 constexpr int FIN_GROUPS = BN_NT / 8;
+// Partials loaded per group before they are merged: the chain over G <= 1024 partials is latency-bound (a finalize
+// ran ~10 us, most of it load rounds); 8 per round halves the rounds.  Merge order per thread is unchanged.
+constexpr int FIN_UNROLL = 8;
 
 template <typename PT, typename RT>
 __global__ __launch_bounds__(BN_NT) void bn_finalize_k(const float* __restrict__ pmean, const float* __restrict__ pm2,
@@ -138,15 +141,15 @@ __global__ __launch_bounds__(BN_NT) void bn_finalize_k(const float* __restrict__
   __shared__ float sh[3][BN_NT];
   const int c = blockIdx.x * 8 + (threadIdx.x & 7), grp = threadIdx.x >> 3;
   Stat acc = {0.f, 0.f, 0.f};
-  for (int g0 = grp; g0 < G; g0 += 4 * FIN_GROUPS) {
-    Stat st[4];
+  for (int g0 = grp; g0 < G; g0 += FIN_UNROLL * FIN_GROUPS) {
+    Stat st[FIN_UNROLL];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < FIN_UNROLL; ++u) {
       const int g = g0 + u * FIN_GROUPS;
       st[u] = g < G ? Stat{pn[g], pmean[(int64_t)g * C + c], pm2[(int64_t)g * C + c]} : Stat{0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) acc = chan_merge(acc, st[u]);
+    for (int u = 0; u < FIN_UNROLL; ++u) acc = chan_merge(acc, st[u]);
   }
   sh[0][threadIdx.x] = acc.n;
   sh[1][threadIdx.x] = acc.mean;
@@ -313,16 +316,16 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_finalize_k(const float* __restri
   __shared__ float sh[2][BN_NT];
   const int c = blockIdx.x * 8 + (threadIdx.x & 7), grp = threadIdx.x >> 3;
   float a = 0.f, b = 0.f;
-  for (int g0 = grp; g0 < G; g0 += 4 * FIN_GROUPS) {
-    float pa[4], pb[4];
+  for (int g0 = grp; g0 < G; g0 += FIN_UNROLL * FIN_GROUPS) {
+    float pa[FIN_UNROLL], pb[FIN_UNROLL];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < FIN_UNROLL; ++u) {
       const int g = g0 + u * FIN_GROUPS;
       pa[u] = g < G ? part[(int64_t)g * 2 * C + c] : 0.f;
       pb[u] = g < G ? part[(int64_t)g * 2 * C + C + c] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < FIN_UNROLL; ++u) {
       a += pa[u];
       b += pb[u];
     }

@@ -13,7 +13,7 @@ for t in 0 1; do
     > "$out/bn_bench_tree$t.log" 2>&1
   db=$(find "$raw" -name "*results.db" -print -quit)
   python benchmarks/prof_summary.py "$db" --json "$out/summary_tree$t.json" > "$out/summary_tree$t.txt"
-  grep -E "bn_stats|bn_bwd_reduce" "$out/summary_tree$t.txt" | head -8
+  grep -E "bn_stats|finalize" "$out/summary_tree$t.txt" | head -8
   rm -rf "$raw"
 done
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_graphs.py -x -q -k "bn or resnet or bottleneck or unet or conv" \
