@@ -19,7 +19,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot, grad_tap
+from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot, StemConv2d, grad_tap
 from ..ops.pool import MaxPool2d
 
 
@@ -93,7 +93,7 @@ class ResNet(nn.Module):
             self.conv1 = nn.Conv2d(3, 64, 3, 1, 1, bias=False)
             self.maxpool = nn.Identity()
         else:
-            self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+            self.conv1 = StemConv2d(3, 64, 7, 2, 3, bias=False)   # 4-channel NHWC padding on the GPU (ops/conv.py)
             self.maxpool = MaxPool2d(3, 2, 1)   # channels-last HIP kernels (ops/pool.py)
         self.bn1 = BatchNormAct2d(64)
         self.layer1 = self._make(block, 64, layers[0])

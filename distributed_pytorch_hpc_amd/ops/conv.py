@@ -311,3 +311,29 @@ class BiasConvTranspose2d(nn.ConvTranspose2d):
         if output_size is None and _bias_conv_ok(self, x):
             return _bias_conv(self, x, True, self.output_padding)
         return super().forward(x, output_size)
+
+
+# ------------------------------------------------------------------------------------------------ RGB stem
+class StemConv2d(nn.Conv2d):
+    """``nn.Conv2d`` for a 3-channel (RGB) image stem whose channels-last GPU path zero-pads the input channels to 4.
+
+    With 3 channels an NHWC pixel is 6 bytes and MIOpen's implicit-GEMM kernels run the ResNet stem (7x7 / 2, 64
+    filters, B=256 x 224 x 224, bf16) in 0.876 ms forward + weight gradient; at 4 channels (8-byte pixels) 0.603 ms,
+    at 8 channels 0.777 (`benchmarks/stem_conv_bench.py`, profiles/r2s3/stem_conv_bench.log).  The padded copy of the
+    image (written once per step, in the compute dtype) and a zero weight slice make the 4-channel convolution
+    exactly the 3-channel one; the parameter keeps its [Cout, 3, k, k] shape (state dicts unchanged) and receives
+    the gradient of its own 3 channels."""
+
+    def forward(self, x):
+        if not (self.in_channels == 3 and self.groups == 1 and x.is_cuda and x.dim() == 4
+                and self.padding_mode == "zeros" and not isinstance(self.padding, str)
+                and x.is_contiguous(memory_format=torch.channels_last) and _lib.use_native(x)):
+            return super().forward(x)
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else x.dtype
+        b, _, h, w = x.shape
+        x4 = torch.empty((b, 4, h, w), device=x.device, dtype=dt, memory_format=torch.channels_last)
+        x4[:, 3].zero_()
+        x4[:, :3].copy_(x)
+        wt = self.weight
+        w4 = torch.cat([wt, wt.new_zeros((wt.shape[0], 1) + tuple(wt.shape[2:]))], 1)
+        return F.conv2d(x4, w4, self.bias, self.stride, self.padding, self.dilation, 1)

@@ -971,3 +971,26 @@ def test_bn_residual_relu_bitmask_matches_y_path(dph_native, C):
     ref = o.bn_act_bwd(dy, y, x, mean, invstd, w, True, True, True, None, None, None)
     for g, e in zip(got, ref):
         assert torch.equal(g, e)
+
+
+@pytest.mark.parametrize("autocast", [False, True])
+def test_stem_conv_channel_padding_matches_conv2d(dph_native, autocast):
+    """ops.conv.StemConv2d (RGB input zero-padded to 4 NHWC channels, zero weight slice) == nn.Conv2d: output and
+    weight gradient (its 3 channels only)."""
+    from distributed_pytorch_hpc_amd.ops.conv import StemConv2d
+
+    torch.manual_seed(0)
+    ref = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False).to(DEV).to(memory_format=torch.channels_last)
+    new = StemConv2d(3, 64, 7, 2, 3, bias=False).to(DEV).to(memory_format=torch.channels_last)
+    new.load_state_dict(ref.state_dict())
+    x = torch.randn(4, 3, 64, 48, device=DEV).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        ya, yb = ref(x), new(x)
+    assert ya.dtype == yb.dtype and ya.shape == yb.shape
+    tol = 1e-2 if autocast else 1e-5
+    assert rel_err(yb, ya) < tol
+    g = torch.randn_like(ya.float())
+    ya.float().backward(g)
+    yb.float().backward(g)
+    assert new.weight.grad.shape == (64, 3, 7, 7)
+    assert rel_err(new.weight.grad, ref.weight.grad) < tol
