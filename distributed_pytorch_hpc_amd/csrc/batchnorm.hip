@@ -124,13 +124,16 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_k(const T* __restrict__ x, flo
 // Merge G partials per channel; produce mean / invstd, the apply coefficients and the running-stat update.
 // One block per 8-channel chunk: 32 row-groups of 8 lanes each merge a strided slice of the partials (loads
 // issued FIN_UNROLL at a time so the chain is not one memory latency per partial), then a fixed-order LDS tree.
-constexpr int FIN_GROUPS = BN_NT / 8;
+// 1024 threads = 128 row groups of 8 channel lanes per 8-channel chunk: at C = 64 only 8 workgroups exist, so the
+// merge of up to 1024 partials is latency-bound; more groups per workgroup = fewer load rounds per thread.
+constexpr int FIN_NT = 1024;
+constexpr int FIN_GROUPS = FIN_NT / 8;
 // Partials loaded per group before they are merged: the chain over G <= 1024 partials is latency-bound (a finalize
 // ran ~10 us, most of it load rounds); 8 per round halves the rounds.  Merge order per thread is unchanged.
 constexpr int FIN_UNROLL = 8;
 
 template <typename PT, typename RT>
-__global__ __launch_bounds__(BN_NT) void bn_finalize_k(const float* __restrict__ pmean, const float* __restrict__ pm2,
+__global__ __launch_bounds__(FIN_NT) void bn_finalize_k(const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                        const float* __restrict__ pn, int G, int C,
                                                        const PT* __restrict__ w, const PT* __restrict__ b,
                                                        RT* __restrict__ rmean, RT* __restrict__ rvar, float momentum,
@@ -138,7 +141,7 @@ __global__ __launch_bounds__(BN_NT) void bn_finalize_k(const float* __restrict__
                                                        float* __restrict__ invstd_out, float* __restrict__ scale,
                                                        float* __restrict__ shift, int64_t* __restrict__ nbt) {
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;   // num_batches_tracked, one launch fewer
-  __shared__ float sh[3][BN_NT];
+  __shared__ float sh[3][FIN_NT];
   const int c = blockIdx.x * 8 + (threadIdx.x & 7), grp = threadIdx.x >> 3;
   Stat acc = {0.f, 0.f, 0.f};
   for (int g0 = grp; g0 < G; g0 += FIN_UNROLL * FIN_GROUPS) {
@@ -183,11 +186,11 @@ __global__ __launch_bounds__(BN_NT) void bn_finalize_k(const float* __restrict__
 // Merge G (large) statistics partials into gridDim.y segment partials: block (channel chunk, segment s) Chan-merges
 // partials [s*G/S, (s+1)*G/S) of its 8 channels (32 thread groups, then an LDS tree), so bn_finalize_k sees few
 // partials.  Used when the partials come per 128-row block from the 1x1 convolution epilogue (thousands of them).
-__global__ __launch_bounds__(BN_NT) void bn_merge_k(const float* __restrict__ pmean, const float* __restrict__ pm2,
+__global__ __launch_bounds__(FIN_NT) void bn_merge_k(const float* __restrict__ pmean, const float* __restrict__ pm2,
                                                     const float* __restrict__ pn, int G, int C,
                                                     float* __restrict__ omean, float* __restrict__ om2,
                                                     float* __restrict__ on) {
-  __shared__ float sh[3][BN_NT];
+  __shared__ float sh[3][FIN_NT];
   const int c = blockIdx.x * 8 + (threadIdx.x & 7), grp = threadIdx.x >> 3;
   const int S = gridDim.y, sgm = blockIdx.y;
   const int g_beg = (int)((int64_t)G * sgm / S), g_end = (int)((int64_t)G * (sgm + 1) / S);
@@ -309,11 +312,11 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_reduce_k(const T* __restrict__ d
 
 // Sum the G partials (same block shape as bn_finalize_k); dgamma = sum(dz xhat), dbeta = sum(dz); dx coefficients.
 template <typename PT>
-__global__ __launch_bounds__(BN_NT) void bn_bwd_finalize_k(const float* __restrict__ part, int G, int C, float count,
+__global__ __launch_bounds__(FIN_NT) void bn_bwd_finalize_k(const float* __restrict__ part, int G, int C, float count,
                                                            const PT* __restrict__ w, const float* __restrict__ invstd,
                                                            PT* __restrict__ dw, PT* __restrict__ db,
                                                            float* __restrict__ coef) {
-  __shared__ float sh[2][BN_NT];
+  __shared__ float sh[2][FIN_NT];
   const int c = blockIdx.x * 8 + (threadIdx.x & 7), grp = threadIdx.x >> 3;
   float a = 0.f, b = 0.f;
   for (int g0 = grp; g0 < G; g0 += FIN_UNROLL * FIN_GROUPS) {
@@ -438,7 +441,7 @@ void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const 
     float* om = workspace;
     float* o2 = workspace + (int64_t)S * C;
     float* on = workspace + 2 * (int64_t)S * C;
-    hipLaunchKernelGGL(bn_merge_k, dim3((unsigned)(C / 8), (unsigned)S), dim3(BN_NT), 0, st, pre_stats,
+    hipLaunchKernelGGL(bn_merge_k, dim3((unsigned)(C / 8), (unsigned)S), dim3(FIN_NT), 0, st, pre_stats,
                        pre_stats + (int64_t)pre_groups * C, pre_stats + 2 * (int64_t)pre_groups * C, pre_groups,
                        (int)C, om, o2, on);
     G = S;
@@ -458,7 +461,7 @@ void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const 
   }
   const dim3 fg((unsigned)(C / 8));
 #define DPH_BN_FIN(PT_, RT_)                                                                                    \
-  hipLaunchKernelGGL((bn_finalize_k<PT_, RT_>), fg, dim3(BN_NT), 0, st, pmean, pm2, pn, G, (int)C, (const PT_*)w, \
+  hipLaunchKernelGGL((bn_finalize_k<PT_, RT_>), fg, dim3(FIN_NT), 0, st, pmean, pm2, pn, G, (int)C, (const PT_*)w, \
                      (const PT_*)b, (RT_*)rmean, (RT_*)rvar, momentum, eps, mean, invstd, scale, shift, nbt)
   if (pdt == kBF16 && rdt == kBF16) DPH_BN_FIN(bf16, bf16);
   else if (pdt == kBF16) DPH_BN_FIN(bf16, float);
@@ -509,10 +512,10 @@ void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, con
 #undef DPH_BN_RED
   const dim3 fg((unsigned)(C / 8));
   if (pdt == kBF16)
-    hipLaunchKernelGGL((bn_bwd_finalize_k<bf16>), fg, dim3(BN_NT), 0, st, part, G, (int)C, (float)M, (const bf16*)w,
+    hipLaunchKernelGGL((bn_bwd_finalize_k<bf16>), fg, dim3(FIN_NT), 0, st, part, G, (int)C, (float)M, (const bf16*)w,
                        invstd, (bf16*)dw, (bf16*)db, coef);
   else
-    hipLaunchKernelGGL((bn_bwd_finalize_k<float>), fg, dim3(BN_NT), 0, st, part, G, (int)C, (float)M,
+    hipLaunchKernelGGL((bn_bwd_finalize_k<float>), fg, dim3(FIN_NT), 0, st, part, G, (int)C, (float)M,
                        (const float*)w, invstd, (float*)dw, (float*)db, coef);
   const int64_t nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, BN_NT));
