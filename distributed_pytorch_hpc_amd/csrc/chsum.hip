@@ -44,6 +44,37 @@ __global__ __launch_bounds__(CS_NT) void chsum_partial_k(const T* __restrict__ x
   }
 }
 
+// C % 8 == 0 and C <= 2048 (every UNet convolution but the 65-channel output): a lane owns an 8-channel chunk and
+// reads it with one 16-B load per row; 256 / (C / 8) row lanes, then the same fixed-order sum over the row lanes.
+template <typename T>
+__global__ __launch_bounds__(CS_NT) void chsum_partial_vec_k(const T* __restrict__ x, float* __restrict__ part,
+                                                             int64_t M, int C, int64_t rows_per_block) {
+  __shared__ float sh[CS_NT * 8];
+  const int ch8 = C / 8, R = CS_NT / ch8;
+  const int lane_r = threadIdx.x / ch8, lane_c = threadIdx.x % ch8;
+  const int64_t beg = (int64_t)blockIdx.x * rows_per_block, end = min(M, beg + rows_per_block);
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+  for (int64_t r = beg + lane_r; r < end; r += R) {
+    float v[8];
+    Vec8<T>::load(x + r * C + lane_c * 8, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += v[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sh[threadIdx.x * 8 + i] = acc[i];
+  __syncthreads();
+  if (lane_r == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float t = sh[threadIdx.x * 8 + i];
+      for (int k = 1; k < R; ++k) t += sh[(k * ch8 + lane_c) * 8 + i];
+      part[(int64_t)blockIdx.x * C + lane_c * 8 + i] = t;
+    }
+  }
+}
+
 // one workgroup per channel: threads stride over the slabs, then a fixed-order LDS tree
 template <typename OT>
 __global__ __launch_bounds__(CS_NT) void chsum_final_k(const float* __restrict__ part, OT* __restrict__ out, int G,
@@ -73,8 +104,12 @@ int chsum_partial_blocks(int64_t M, int64_t C) {
 void chsum(const void* x, float* part, void* out, int64_t M, int64_t C, int dtype, int out_dtype, hipStream_t st) {
   const int G = chsum_partial_blocks(M, C);
   const int64_t rpb = (M + G - 1) / G;
+  const bool vec = C % 8 == 0 && C <= 8 * CS_NT && (CS_NT % (C / 8)) == 0 && (reinterpret_cast<uintptr_t>(x) % 16) == 0;
   DPH_DISPATCH_FLOAT(dtype, T, {
-    hipLaunchKernelGGL(chsum_partial_k<T>, dim3(G), dim3(CS_NT), 0, st, (const T*)x, part, M, (int)C, rpb);
+    if (vec)
+      hipLaunchKernelGGL(chsum_partial_vec_k<T>, dim3(G), dim3(CS_NT), 0, st, (const T*)x, part, M, (int)C, rpb);
+    else
+      hipLaunchKernelGGL(chsum_partial_k<T>, dim3(G), dim3(CS_NT), 0, st, (const T*)x, part, M, (int)C, rpb);
   });
   const dim3 fg((unsigned)C);
   if (out_dtype == kBF16)
