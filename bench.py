@@ -3,13 +3,25 @@
 
 Metric and config come from BASELINE.json ("tokens/sec + DDP/FSDP scaling efficiency, Llama-2-7B at
 1/2/4/8 MI355X").  Every rank trains the full Llama-2-7B architecture (random init, synthetic tokens)
-with a fixed per-GPU batch; N > 1 runs the FSDP engine (reduce-scatter gradients overlapped with
-backward, sharded fp32 AdamW state, parameter all-gather overlapped with the next forward) over RCCL.
+with a fixed per-GPU batch on the sharded data-parallel engine (reduce-scatter of bf16 gradient buckets
+overlapped with backward, sharded fp32 AdamW state, parameter all-gather overlapped with the next forward) over
+RCCL.  N = 1 runs the same engine in a world of one (RCCL process group created; its collectives are no-ops), so
+T_1 and T_N come from the same code.
 The timed region holds EXACTLY --steps full optimizer steps (forward + backward + gradient collectives +
 AdamW + parameter all-gather), bracketed by a barrier and a device synchronize on both sides; the
 reported time is the MAX over ranks; rank 0 prints one JSON line.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Before anything is timed, a run with N > 1 (runtime/preflight.py):
+  * self-tests every collective the engines use (all-reduce / reduce-scatter / all-gather in fp32 and bf16, a P2P
+    ring) with exact known values on the real group -- a mismatch or timeout aborts with exit code 3;
+  * sizes the gradient buckets from a ~1-2 s alpha-beta probe of reduce-scatter / all-gather (--bucket-mb
+    calibrate, the default); the fit and the chosen size go into the JSON;
+  * after the warm-up, checks that the flat parameters of every replica agree bitwise (exit code 4 if not).
+
+Other BASELINE.json configs run under the same contract with --layout (train/bench_layouts.py):
+tp (Llama-2 7B TP=N + SP), hybrid (FSDP(N/4) x TP(4)), pp (PP 4 x DDP N/4, 1F1B), resnet-fsdp (ResNet-50 FSDP bf16).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--layout dp|tp|hybrid|pp|resnet-fsdp]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 """
@@ -24,7 +36,7 @@ import time
 import torch
 import torch.distributed as dist
 
-BASELINE_METRIC = "tokens/sec + DDP/FSDP scaling efficiency, Llama-2-7B at 1/2/4/8 MI355X"
+from distributed_pytorch_hpc_amd.train.bench_layouts import BASELINE_METRIC, BUILDERS, LAYOUTS  # noqa: F401
 
 
 def parse(argv=None):
@@ -32,14 +44,25 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--model", default="llama2-7b")
+    ap.add_argument("--layout", choices=LAYOUTS, default="dp",
+                    help="dp: headline weak-scaling FSDP; tp / hybrid / pp / resnet-fsdp: BASELINE configs 3 / 4 / 5 / 2")
+    ap.add_argument("--model", default=None, help="llama preset (default llama2-7b)")
+    ap.add_argument("--arch", default="resnet50", help="resnet-fsdp layout: ResNet depth")
     ap.add_argument("--seq-len", type=int, default=4096)
-    ap.add_argument("--micro-batch", type=int, default=8,
-                    help="sequences per GPU per step (8 x 4096 tokens: ~249 GB peak on one 288 GB MI355X)")
+    ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--micro-batch", type=int, default=None,
+                    help="sequences (images) per GPU / per dp replica per step; default 8 (dp, tp, hybrid), 16 (pp), "
+                         "256 (resnet-fsdp).  8 x 4096 tokens: ~249 GB peak on one 288 GB MI355X")
+    ap.add_argument("--tp", type=int, default=None, help="tp / hybrid layouts: tensor-parallel degree")
+    ap.add_argument("--async-tp", type=int, default=2, help="tp / hybrid: micro-collectives per SP collective")
+    ap.add_argument("--pp", type=int, default=None, help="pp layout: pipeline stages (default 4)")
+    ap.add_argument("--microbatches", type=int, default=8, help="pp layout: micro-batches per step")
+    ap.add_argument("--schedule", choices=["1f1b", "gpipe"], default="1f1b")
     ap.add_argument("--parallel", choices=["auto", "fsdp", "ddp"], default="auto",
-                    help="auto: single-GPU engine for N=1, FSDP (sharded optimizer) for N>1")
-    ap.add_argument("--bucket-mb", default="256",
-                    help="gradient bucket size in MiB, or 'auto' (alpha-beta fit of comm/cost_model.py, $DPH_COMM_FIT)")
+                    help="dp layout: auto = the sharded (FSDP / ZeRO-2) engine; ddp = replicated optimizer state")
+    ap.add_argument("--bucket-mb", default="calibrate",
+                    help="gradient bucket size in MiB; 'calibrate' (in-run alpha-beta probe, default); 'auto' "
+                         "(comm/cost_model.py fit from $DPH_COMM_FIT or the nominal prior)")
     ap.add_argument("--grad-dtype", choices=["bf16", "fp32"], default="bf16")
     ap.add_argument("--lr", type=float, default=3e-4)
     ap.add_argument("--kernels", choices=["dph", "aten"], default="dph",
@@ -47,8 +70,10 @@ def parse(argv=None):
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--ac", default="none",
                     help="activation checkpointing: none | auto (fit 288 GB) | N (every N-th block)")
-    ap.add_argument("--force-dist", action="store_true",
-                    help="create the RCCL process group even for one rank (exercises the N>1 collective path)")
+    ap.add_argument("--no-dist", action="store_true",
+                    help="N = 1 without a process group (the engine is the same; no RCCL communicator)")
+    ap.add_argument("--force-dist", action="store_true", help=argparse.SUPPRESS)   # the default now; kept for scripts
+    ap.add_argument("--no-preflight", action="store_true", help="skip the collective self-test and replica check")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default=None,
                     help="process-group backend (default: nccl = RCCL on GPU); gloo lets several ranks share one GPU "
                          "to rehearse the N > 1 path (tests/test_bench_gpu.py)")
@@ -58,16 +83,30 @@ def parse(argv=None):
                          "LM head bf16). Reported with dtype 'bf16+fp8-gemm' -- not the bf16 headline number")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: gloo + eager reference ops (tests of the N > 1 code path with tiny models only)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.model is None:
+        args.model = "llama2-7b"
+    if args.micro_batch is None:
+        args.micro_batch = {"pp": 16, "resnet-fsdp": 256}.get(args.layout, 8)
+    return args
+
+
+def _fail(code: int, msg: str):
+    print(f"[bench] FATAL: {msg}", file=sys.stderr, flush=True)
+    sys.stderr.flush()
+    os._exit(code)   # a rank that failed a check must not wait in a collective the others never reach
 
 
 def main(argv=None):
     args = parse(argv)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     from distributed_pytorch_hpc_amd.runtime import env as rt
+    from distributed_pytorch_hpc_amd.runtime import preflight
 
     cpu = args.device == "cpu"
-    if world_env > 1 or args.force_dist:
+    if world_env > 1 or not args.no_dist:
+        if world_env == 1 and "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(rt.free_port())   # a world of one needs no fixed rendezvous port
         rank, world, local = rt.init_distributed(backend="gloo" if cpu else args.backend, verbose=not args.quiet)
     else:
         rank, world, local = 0, 1, 0
@@ -78,55 +117,28 @@ def main(argv=None):
     dev = torch.device("cpu") if cpu else torch.device("cuda", torch.cuda.current_device())
     sync = (lambda: None) if cpu else torch.cuda.synchronize
 
-    from distributed_pytorch_hpc_amd.models.llama2 import build_llama, get_preset
+    def log(msg):
+        if rank == 0 and not args.quiet:
+            print(msg, file=sys.stderr, flush=True)
+
     from distributed_pytorch_hpc_amd.ops import _lib
-    from distributed_pytorch_hpc_amd.parallel.data_parallel import (DataParallelEngine, MixedPrecision,
-                                                                    OptimConfig)
 
     if not cpu:
         _lib.require()
     if args.kernels == "aten":
         _lib.set_reference_mode(True)
-    margs = get_preset(args.model, max_seq_len=max(args.seq_len, 4096))
-    dtype = torch.float32 if cpu else torch.bfloat16
-    model = build_llama(margs, device=dev, dtype=dtype, seed=1234)
-    ac_every = 0
-    if args.ac != "none":
-        from distributed_pytorch_hpc_amd.parallel.activation_checkpoint import (apply_llama_checkpointing,
-                                                                                plan_llama_checkpointing)
 
-        n_par = margs.num_params()
-        static_gb = n_par * (4 + (12 / world if world > 1 else 12)) / 1e9
-        ac_every = (plan_llama_checkpointing(margs, args.micro_batch, args.seq_len, static_gb=static_gb)
-                    if args.ac == "auto" else int(args.ac))
-        apply_llama_checkpointing(model, ac_every)
-    mode = args.parallel
-    if mode == "auto":
-        mode = "fsdp" if world > 1 or args.force_dist else "ddp"
-    if args.fp8 and not cpu:
-        from distributed_pytorch_hpc_amd.ops import fp8 as fp8_mod
+    # ---- pre-flight collective self-test on the real group (outside the timed region) ----
+    pre = {"preflight_ok": None}
+    if world > 1 and not args.no_preflight:
+        try:
+            rep = preflight.collective_selftest(None, dev)
+            pre = {"preflight_ok": True, "preflight_checked": rep["checked"]}
+            log(f"[bench] pre-flight OK on {world} ranks: {', '.join(rep['checked'])}")
+        except preflight.PreflightError as e:
+            _fail(3, f"rank {rank}: collective self-test failed: {e}")
 
-        fp8_mod.enable_for_llama(model)
-    engine = DataParallelEngine(
-        model, shard=(mode == "fsdp"),
-        mixed_precision=MixedPrecision(param_dtype=dtype,
-                                       reduce_dtype=torch.bfloat16 if args.grad_dtype == "bf16" and not cpu
-                                       else torch.float32),
-        bucket_cap_mb=args.bucket_mb if args.bucket_mb == "auto" else float(args.bucket_mb))
-    engine.configure_optimizer(OptimConfig(name="adamw", lr=args.lr, betas=(0.9, 0.95), weight_decay=0.1))
-
-    B, S = args.micro_batch, args.seq_len
-    g = torch.Generator(device=dev)
-    g.manual_seed(1000 + rank)
-    batches = [torch.randint(0, margs.vocab_size, (B, S + 1), device=dev, generator=g) for _ in range(4)]
-
-    def train_step(i):
-        t = batches[i % len(batches)]
-        loss = model(t[:, :-1], t[:, 1:])
-        loss.backward()
-        engine.step()
-        engine.zero_grad()
-        return loss
+    wl = BUILDERS[args.layout](args, rank, world, dev, log)
 
     def sync_all():
         sync()
@@ -134,60 +146,65 @@ def main(argv=None):
             rt.barrier()
         sync()
 
+    loss = None
     for i in range(args.warmup):
-        loss = train_step(i)
-    if args.warmup:
-        first_loss = float(loss.detach())
+        loss = wl.step(i)
+    first_loss = float(loss.detach()) if loss is not None else None
+    wl.engine.synchronize()
     sync_all()
+    # ---- replicas must hold bitwise-identical parameters after the warm-up updates ----
+    replica = {"param_checksum_ok": None}
+    if world > 1 and wl.replica_flat is not None and not args.no_preflight and args.warmup:
+        try:
+            rep = preflight.replicas_agree(wl.replica_flat, wl.replica_group)
+            replica = {"param_checksum_ok": True}
+            log(f"[bench] replicas agree after warm-up (checksum {rep['checksum'][0]:.6e})")
+        except preflight.PreflightError as e:
+            _fail(4, f"rank {rank}: {e}")
+        sync_all()
+
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss = train_step(args.warmup + i)
-    engine.synchronize()
+        loss = wl.step(args.warmup + i)
+    wl.engine.synchronize()
     sync_all()
     elapsed = time.perf_counter() - t0
-    last_loss = float(loss.detach())
+    last_loss = float(loss.detach()) if loss is not None else None
     if dist.is_initialized():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    tokens = world * B * S * args.steps
-    tps = tokens / elapsed
+    items = wl.items_per_step * args.steps
+    rate = items / elapsed
     ms = 1000.0 * elapsed / args.steps
-    flops_tok = margs.flops_per_token(S)
-    mfu = tps / world * flops_tok / 2.5e15
     peak_gb = 0.0 if cpu else torch.cuda.max_memory_allocated() / 1e9
     if rank == 0:
         rec = {
-            "metric": BASELINE_METRIC,
-            "value": round(tps, 2),
-            "unit": "tokens/s",
+            "metric": wl.metric,
+            "value": round(rate, 2),
+            "unit": wl.unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": wl.scaling,
             "vs_baseline": None,
             "dtype": "fp32" if cpu else ("bf16+fp8-gemm" if args.fp8 else "bf16"),
-            "data": "synthetic (random tokens, random-init weights)",
-            "config": {
-                "model": "Llama-2-7B" if args.model == "llama2-7b" else args.model,
-                "global_batch": world * B,
-                "seq_len": S,
-                "parallelism": f"{mode}{world}",
-                "micro_batch_per_gpu": B,
-                "tokens_per_step": world * B * S,
-                "kernels": args.kernels,
-                "bucket_mb": round(engine.bucket_cap_mb, 1),
-                "activation_checkpoint_every": ac_every,
-            },
-            "tokens_per_sec_per_gpu": round(tps / world, 2),
-            "mfu_vs_2.5PF_bf16_dense": round(mfu, 4),
+            "data": "synthetic (random tokens / images, random-init weights)",
+            "config": {**wl.config, "layout": args.layout},
+            f"{wl.unit.split('/')[0]}_per_sec_per_gpu": round(rate / world, 2),
             "peak_hbm_gb": round(peak_gb, 2),
-            "loss_first_warmup": round(first_loss, 4) if args.warmup else None,
-            "loss_last": round(last_loss, 4),
+            "loss_first_warmup": round(first_loss, 4) if first_loss is not None else None,
+            "loss_last": round(last_loss, 4) if last_loss is not None else None,
+            "world": world,
+            "process_group": dist.get_backend() if dist.is_initialized() else None,
+            "rccl_version": preflight.rccl_version() if not cpu else None,
+            **pre, **replica, **wl.extra,
         }
+        if wl.flops_per_item:
+            rec["mfu_vs_2.5PF_bf16_dense"] = round(rate / world * wl.flops_per_item / 2.5e15, 4)
         line = json.dumps(rec)
         print(line, flush=True)
         if args.json_out:

@@ -12,6 +12,10 @@ reference's guides discuss but never publish (BASELINE.md "Not pu
 
     python benchmarks/scaling_sweep.py --ns 1 2 4 8 --steps 10 --warmup 3 --out results/scaling
     python benchmarks/scaling_sweep.py --ns 1 2 -- --device cpu --model tiny --seq-len 64 --micro-batch 2
+    python benchmarks/scaling_sweep.py --layouts dp tp hybrid pp resnet-fsdp --ns 1 2 4 8 --out results/all
+
+``--layouts`` sweeps every BASELINE.json config bench.py knows (train/bench_layouts.py) under the same contract; a
+layout's efficiency uses the same formula (for the strong-scaling tp layout it is speedup / N).
 """
 from __future__ import annotations
 
@@ -64,11 +68,13 @@ def efficiency_table(recs: dict[int, dict]) -> tuple[list[dict], str]:
     for n in sorted(recs):
         r = recs[n]
         eff = r["value"] / (n * base["value"]) if base else None
-        rows.append({"n_gpus": n, "tokens_per_s": r["value"], "tokens_per_s_per_gpu": round(r["value"] / n, 1),
+        rows.append({"n_gpus": n, "value": r["value"], "unit": r["unit"], "tokens_per_s": r["value"],
+                     "tokens_per_s_per_gpu": round(r["value"] / n, 1),
                      "ms_per_step": r["ms_per_step"], "parallelism": r["config"]["parallelism"],
                      "global_batch": r["config"]["global_batch"], "peak_hbm_gb": r.get("peak_hbm_gb"),
                      "scaling_efficiency": None if eff is None else round(eff, 4)})
-    lines = ["| N | parallelism | global batch | tokens/s | per GPU | ms/step | efficiency |",
+    unit = next(iter(recs.values()))["unit"] if recs else "tokens/s"
+    lines = [f"| N | parallelism | global batch | {unit} | per GPU | ms/step | efficiency |",
              "|---|---|---|---|---|---|---|"]
     for row in rows:
         e = "—" if row["scaling_efficiency"] is None else f"{100 * row['scaling_efficiency']:.1f} %"
@@ -89,7 +95,19 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--timeout", type=float, default=900.0, help="seconds per N")
     ap.add_argument("--out", default=None, help="directory for n<N>.log, scaling.json and scaling.md")
+    ap.add_argument("--layouts", nargs="+", default=None,
+                    help="sweep these bench.py layouts (dp tp hybrid pp resnet-fsdp), one sub-directory of --out each")
     args = ap.parse_args(argv)
+    if args.layouts:
+        out = {}
+        for lay in args.layouts:
+            sub = ["--ns", *map(str, args.ns), "--steps", str(args.steps), "--warmup", str(args.warmup),
+                   "--timeout", str(args.timeout)]
+            if args.out:
+                sub += ["--out", os.path.join(args.out, lay)]
+            print(f"[scaling] layout {lay}", flush=True)
+            out[lay] = main(sub + ["--"] + extra + ["--layout", lay])
+        return out
     if args.out:
         os.makedirs(args.out, exist_ok=True)
     recs: dict[int, dict] = {}

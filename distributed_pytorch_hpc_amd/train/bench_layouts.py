@@ -1,0 +1,286 @@
+"""Workloads of ``bench.py``: one builder per BASELINE.json config, all measured under the same contract (W untimed
+warm-up steps, EXACTLY K timed full optimizer steps bracketed by barrier + device synchronize, MAX over ranks, one
+JSON line from rank 0).
+
+| layout        | BASELINE.json config                                                  | reference path                       |
+|---------------|-----------------------------------------------------------------------|--------------------------------------|
+| ``dp``        | headline: tokens/s + DDP/FSDP scaling, Llama-2-7B at 1/2/4/8 MI355X   | fsdp_tp/fsdp_tp_example.py (dp part) |
+| ``tp``        | Llama-2 7B TP=8 over xGMI                                             | fsdp_tp/tensor_parallel_example.py   |
+| ``hybrid``    | Llama-2 7B hybrid FSDP(2) x TP(4) via DeviceMesh                      | fsdp_tp/fsdp_tp_example.py:103-187   |
+| ``pp``        | Llama-2 7B PP 4 stages x DDP 2 (send/recv micro-batch pipeline)       | scripts/04_pipeline_parallel_pp/03   |
+| ``resnet-fsdp`` | ResNet-50 FSDP bf16 on 8 x MI355X                                   | scripts/main.py + resnet_fsdp_training.py |
+
+Each builder returns a ``Workload``: the step function, the engine to synchronise, the group whose ranks hold
+replicas of the same flat parameters (checked bitwise after warm-up), the work per step and the JSON ``config``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+BASELINE_METRIC = "tokens/sec + DDP/FSDP scaling efficiency, Llama-2-7B at 1/2/4/8 MI355X"
+LAYOUTS = ("dp", "tp", "hybrid", "pp", "resnet-fsdp")
+
+
+@dataclass
+class Workload:
+    step: Callable[[int], Optional[torch.Tensor]]
+    engine: object
+    metric: str
+    unit: str
+    items_per_step: int                  # tokens (or images) processed per step by the whole job
+    scaling: str                         # "weak" | "strong"
+    config: dict
+    replica_group: object = None         # ranks holding identical flat parameters (None: every rank / n.a.)
+    replica_flat: Optional[torch.Tensor] = None
+    flops_per_item: float = 0.0
+    extra: dict = field(default_factory=dict)
+
+
+def _bucket(args, world_dp: int, grad_bytes: float, sharded: bool, group, dev, log) -> tuple[float, dict]:
+    """Bucket size for the data-parallel engine: a number (MiB), 'auto' ($DPH_COMM_FIT / nominal prior) or
+    'calibrate' (in-run alpha-beta probe of reduce-scatter / all-gather on ``group``; default for dp > 1)."""
+    from ..comm import cost_model
+    from ..runtime import preflight
+
+    spec = str(args.bucket_mb)
+    if spec == "calibrate" and world_dp <= 1:
+        return 256.0, {"bucket_source": "default (no data-parallel collectives at dp = 1)"}
+    if spec == "calibrate":
+        sizes = (4, 16, 64, 256) if dev.type == "cuda" else (0.0625, 0.25, 1.0)
+        fits = preflight.probe_alpha_beta(group, dev, sizes_mib=sizes,
+                                          dtype=torch.bfloat16 if dev.type == "cuda" else torch.float32)
+        mib = preflight.calibrated_bucket_mb(fits, grad_bytes, sharded,
+                                             lo_mib=32.0 if dev.type == "cuda" else 0.01)
+        log(f"[bench] alpha-beta probe: " + ", ".join(
+            f"{k} alpha {1e6 * v.alpha_s:.1f} us, busbw {v.beta_bus_Bps / 1e9:.1f} GB/s" for k, v in fits.items())
+            + f" -> bucket {mib:.1f} MiB")
+        return mib, {"bucket_source": "in-run alpha-beta probe", "comm_fit": preflight.fits_json(fits)}
+    if spec == "auto":
+        mib = cost_model.auto_bucket_mb(grad_bytes, world_dp, sharded)
+        return mib, {"bucket_source": "cost model ($DPH_COMM_FIT or nominal prior)"}
+    return float(spec), {"bucket_source": "fixed"}
+
+
+def _llama(args, dev, dtype, n_layers=None):
+    from ..models.llama2 import build_llama, get_preset
+
+    over = {"max_seq_len": max(args.seq_len, 4096 if dev.type == "cuda" else args.seq_len)}
+    if n_layers:
+        over["n_layers"] = n_layers
+    margs = get_preset(args.model, **over)
+    return margs, build_llama(margs, device=dev, dtype=dtype, seed=1234)
+
+
+def _tokens(margs, B, S, dev, seed):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    return [torch.randint(0, margs.vocab_size, (B, S + 1), device=dev, generator=g) for _ in range(4)]
+
+
+def _model_name(args):
+    return {"llama2-7b": "Llama-2-7B", "llama2-13b": "Llama-2-13B", "llama2-1b": "Llama-2-1B"}.get(args.model,
+                                                                                                 args.model)
+
+
+def build_dp(args, rank, world, dev, log) -> Workload:
+    """Headline: every rank trains the full model on its own batch; N > 1 = sharded engine (reduce-scatter of bf16
+    gradient buckets overlapped with backward, 1/N fp32 AdamW, parameter all-gather overlapped with the next
+    forward).  N = 1 takes the same engine class (its collectives are no-ops in a world of one)."""
+    from ..parallel.data_parallel import DataParallelEngine, MixedPrecision, OptimConfig
+
+    cpu = dev.type == "cpu"
+    dtype = torch.float32 if cpu else torch.bfloat16
+    margs, model = _llama(args, dev, dtype)
+    ac_every = 0
+    if args.ac != "none":
+        from ..parallel.activation_checkpoint import apply_llama_checkpointing, plan_llama_checkpointing
+
+        static_gb = margs.num_params() * (4 + (12 / world if world > 1 else 12)) / 1e9
+        ac_every = (plan_llama_checkpointing(margs, args.micro_batch, args.seq_len, static_gb=static_gb)
+                    if args.ac == "auto" else int(args.ac))
+        apply_llama_checkpointing(model, ac_every)
+    mode = args.parallel
+    if mode == "auto":
+        mode = "fsdp" if dist.is_initialized() else "ddp"
+    if args.fp8 and not cpu:
+        from ..ops import fp8 as fp8_mod
+
+        fp8_mod.enable_for_llama(model)
+    reduce_dtype = torch.bfloat16 if args.grad_dtype == "bf16" and not cpu else torch.float32
+    grad_bytes = sum(p.numel() for p in model.parameters()) * torch.empty((), dtype=reduce_dtype).element_size()
+    bucket_mb, binfo = _bucket(args, world, grad_bytes, mode == "fsdp", None, dev, log)
+    engine = DataParallelEngine(model, shard=(mode == "fsdp"),
+                                mixed_precision=MixedPrecision(param_dtype=dtype, reduce_dtype=reduce_dtype),
+                                bucket_cap_mb=bucket_mb)
+    engine.configure_optimizer(OptimConfig(name="adamw", lr=args.lr, betas=(0.9, 0.95), weight_decay=0.1))
+    B, S = args.micro_batch, args.seq_len
+    batches = _tokens(margs, B, S, dev, 1000 + rank)
+
+    def step(i):
+        t = batches[i % len(batches)]
+        loss = model(t[:, :-1], t[:, 1:])
+        loss.backward()
+        engine.step()
+        engine.zero_grad()
+        return loss
+
+    cfg = {"model": _model_name(args), "global_batch": world * B, "seq_len": S, "parallelism": f"{mode}{world}",
+           "micro_batch_per_gpu": B, "tokens_per_step": world * B * S, "kernels": args.kernels,
+           "bucket_mb": round(engine.bucket_cap_mb, 1), "activation_checkpoint_every": ac_every, **binfo}
+    return Workload(step, engine, BASELINE_METRIC, "tokens/s", world * B * S, "weak", cfg,
+                    replica_group=None, replica_flat=engine.flat_param,
+                    flops_per_item=margs.flops_per_token(S))
+
+
+def _tp_hybrid(args, rank, world, dev, log, tp: int, layout: str) -> Workload:
+    from ..comm.mesh import DeviceMesh2D
+    from ..parallel.data_parallel import DataParallelEngine, MixedPrecision, OptimConfig
+    from ..parallel.tensor_parallel import parallelize_llama
+
+    assert world % tp == 0, f"world {world} is not divisible by tp {tp}"
+    dp = world // tp
+    cpu = dev.type == "cpu"
+    dtype = torch.float32 if cpu else torch.bfloat16
+    mesh = DeviceMesh2D(dp, tp) if world > 1 else None
+    margs, model = _llama(args, dev, dtype)
+    if tp > 1:
+        parallelize_llama(model, mesh.tp_group, sequence_parallel=True, loss_parallel=True, async_tp=args.async_tp)
+    dp_group = mesh.dp_group if mesh is not None else None
+    reduce_dtype = torch.bfloat16 if not cpu else torch.float32
+    grad_bytes = sum(p.numel() for p in model.parameters()) * torch.empty((), dtype=reduce_dtype).element_size()
+    bucket_mb, binfo = _bucket(args, dp, grad_bytes, dp > 1, dp_group, dev, log)
+    engine = DataParallelEngine(model, dp_group, shard=dp > 1,
+                                mixed_precision=MixedPrecision(param_dtype=dtype, reduce_dtype=reduce_dtype),
+                                bucket_cap_mb=bucket_mb)
+    engine.configure_optimizer(OptimConfig(name="adamw", lr=args.lr, betas=(0.9, 0.95), weight_decay=0.1))
+    B, S = args.micro_batch, args.seq_len
+    dp_rank = mesh.dp_rank if mesh is not None else 0
+    batches = _tokens(margs, B, S, dev, 1000 + dp_rank)   # TP peers see the same batch
+
+    def step(i):
+        t = batches[i % len(batches)]
+        loss = model(t[:, :-1], t[:, 1:])
+        loss.backward()
+        engine.step()
+        engine.zero_grad()
+        return loss
+
+    par = f"tp{tp}" if dp == 1 else f"fsdp{dp}xtp{tp}"
+    cfg = {"model": _model_name(args), "global_batch": dp * B, "seq_len": S, "parallelism": par, "tp": tp, "dp": dp,
+           "sequence_parallel": tp > 1, "loss_parallel": tp > 1, "async_tp": args.async_tp if tp > 1 else 0,
+           "micro_batch_per_dp_replica": B, "tokens_per_step": dp * B * S, "bucket_mb": round(engine.bucket_cap_mb, 1),
+           **binfo}
+    metric = ("tokens/sec, Llama-2 7B TP=8 over xGMI" if layout == "tp"
+              else "tokens/sec, Llama-2 7B hybrid FSDP(2) x TP(4) via DeviceMesh")
+    # strong scaling for pure TP (the batch is fixed as N grows), weak over the dp dimension for the hybrid
+    return Workload(step, engine, metric, "tokens/s", dp * B * S, "strong" if layout == "tp" else "weak", cfg,
+                    replica_group=dp_group, replica_flat=engine.flat_param if dp > 1 else None,
+                    flops_per_item=margs.flops_per_token(S))
+
+
+def build_tp(args, rank, world, dev, log) -> Workload:
+    return _tp_hybrid(args, rank, world, dev, log, args.tp or world, "tp")
+
+
+def build_hybrid(args, rank, world, dev, log) -> Workload:
+    return _tp_hybrid(args, rank, world, dev, log, args.tp or (4 if world % 4 == 0 else world), "hybrid")
+
+
+def build_pp(args, rank, world, dev, log) -> Workload:
+    from ..comm.mesh import Mesh
+    from ..parallel.data_parallel import DataParallelEngine, MixedPrecision, OptimConfig
+    from ..parallel.pipeline import PipelineSchedule, make_lm_loss, split_llama
+
+    pp = args.pp or (4 if world % 4 == 0 else world)
+    assert world % pp == 0, f"world {world} is not divisible by pp {pp}"
+    dp = world // pp
+    cpu = dev.type == "cpu"
+    dtype = torch.float32 if cpu else torch.bfloat16
+    if world > 1:
+        mesh = Mesh((pp, dp), ("pp", "dp"))
+        stage, dp_rank = mesh.local_rank("pp"), mesh.local_rank("dp")
+        pp_group, dp_group = mesh.group("pp"), mesh.group("dp")
+    else:
+        stage = dp_rank = 0
+        pp_group = dp_group = None
+    margs, model = _llama(args, dev, dtype)
+    assert margs.n_layers >= pp
+    stage_mod = split_llama(model, pp, stage)
+    del model
+    reduce_dtype = torch.bfloat16 if not cpu else torch.float32
+    grad_bytes = sum(p.numel() for p in stage_mod.parameters()) * torch.empty((), dtype=reduce_dtype).element_size()
+    bucket_mb, binfo = _bucket(args, dp, grad_bytes, dp > 1, dp_group, dev, log)
+    engine = DataParallelEngine(stage_mod, dp_group, shard=dp > 1,
+                                mixed_precision=MixedPrecision(param_dtype=dtype, reduce_dtype=reduce_dtype),
+                                bucket_cap_mb=bucket_mb)
+    engine.configure_optimizer(OptimConfig(name="adamw", lr=args.lr, betas=(0.9, 0.95), weight_decay=0.1))
+    M = args.microbatches
+    B, S = args.micro_batch, args.seq_len
+    assert B % M == 0, f"--micro-batch {B} (sequences per dp replica) must be divisible by --microbatches {M}"
+    sched = PipelineSchedule(stage_mod, stage, pp, M, loss_fn=make_lm_loss(None), group=pp_group,
+                             schedule=args.schedule, device=dev, dp_engine=engine)
+    batches = _tokens(margs, B, S, dev, 1000 + dp_rank)
+    first, last = stage == 0, stage == pp - 1
+
+    def step(i):
+        t = batches[i % len(batches)]
+        losses = sched.step(inputs=t[:, :-1] if first else None, target=t[:, 1:] if last else None)
+        engine.step()
+        engine.zero_grad()
+        return torch.stack(losses).mean() if losses else None
+
+    cfg = {"model": _model_name(args), "global_batch": dp * B, "seq_len": S, "parallelism": f"pp{pp}xddp{dp}",
+           "pp": pp, "dp": dp, "microbatches": M, "schedule": args.schedule,
+           "bubble_fraction": round(sched.bubble, 4), "tokens_per_step": dp * B * S,
+           "bucket_mb": round(engine.bucket_cap_mb, 1), **binfo}
+    return Workload(step, engine, "tokens/sec, Llama-2 7B PP 4 stages x DDP 2 (1F1B send/recv pipeline)",
+                    "tokens/s", dp * B * S, "weak", cfg, replica_group=dp_group,
+                    replica_flat=engine.flat_param if dp > 1 else None, flops_per_item=margs.flops_per_token(S),
+                    extra={"loss_on_rank0": last})
+
+
+def build_resnet_fsdp(args, rank, world, dev, log) -> Workload:
+    import torch.nn.functional as F
+
+    from ..models import resnet
+    from ..models.resnet import BasicBlock, Bottleneck
+    from ..parallel.data_parallel import MixedPrecision
+    from ..parallel.fsdp import FSDP, ModuleWrapPolicy
+
+    cpu = dev.type == "cpu"
+    arch = args.arch
+    torch.backends.cudnn.benchmark = not cpu   # MIOpen find mode: solvers timed once per shape during warm-up
+    torch.manual_seed(1234)
+    model = resnet(arch, num_classes=1000).to(dev).to(memory_format=torch.channels_last)
+    mp = MixedPrecision(torch.bfloat16, torch.bfloat16, torch.bfloat16) if not cpu else None
+    wrapped = FSDP(model, mixed_precision=mp, auto_wrap_policy=ModuleWrapPolicy({BasicBlock, Bottleneck}))
+    opt = wrapped.make_optimizer("sgd", lr=0.1, momentum=0.9, weight_decay=1e-5)
+    B, R = args.micro_batch, args.image_size
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    x = torch.rand(B, 3, R, R, device=dev, generator=g, dtype=torch.float32 if cpu else torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (B,), device=dev, generator=g)
+
+    def step(i):
+        out = wrapped(x)
+        loss = F.cross_entropy(out.float(), y)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        return loss
+
+    cfg = {"model": {"resnet50": "ResNet-50"}.get(arch, arch), "global_batch": world * B, "image_size": R,
+           "parallelism": f"fsdp{world}", "micro_batch_per_gpu": B, "sharding": "FULL_SHARD per bottleneck",
+           "mixed_precision": "bf16 params / reduce / buffers" if not cpu else "fp32", "channels_last": True,
+           "optimizer": "SGD m=0.9 wd=1e-5 (scripts/main.py)"}
+    return Workload(step, wrapped.engine, "images/sec, ResNet-50 FSDP bf16 on 8 x MI355X", "images/s", world * B,
+                    "weak", cfg, replica_group=None, replica_flat=None,
+                    extra={"replica_check": "n/a (FULL_SHARD: no replicated parameters)"})
+
+
+BUILDERS = {"dp": build_dp, "tp": build_tp, "hybrid": build_hybrid, "pp": build_pp, "resnet-fsdp": build_resnet_fsdp}

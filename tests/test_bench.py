@@ -26,7 +26,7 @@ def _lines(out):
     return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
 
 
-@pytest.mark.parametrize("n", [1, 2, 4])
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
 def test_bench_contract(n, tmp_path):
     env = dict(os.environ, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1")
     if n == 1:
@@ -42,7 +42,14 @@ def test_bench_contract(n, tmp_path):
     r = recs[0]
     assert KEYS <= set(r)
     assert r["n_gpus"] == n and r["steps"] == 2 and r["warmup"] == 1 and r["value"] > 0
-    assert r["config"]["parallelism"] == ("ddp1" if n == 1 else f"fsdp{n}")
+    assert r["config"]["parallelism"] == f"fsdp{n}"     # N = 1 runs the same engine in a world of one
+    assert r["world"] == n and r["process_group"] == "gloo"
+    if n > 1:
+        assert r["preflight_ok"] is True and "p2p_ring" in r["preflight_checked"]
+        assert r["param_checksum_ok"] is True
+        assert r["config"]["bucket_source"] == "in-run alpha-beta probe"
+        assert set(r["config"]["comm_fit"]) == {"reduce_scatter", "all_gather"}
+        assert r["config"]["comm_fit"]["reduce_scatter"]["alpha_s"] >= 0
     assert r["config"]["global_batch"] == 2 * n and r["config"]["seq_len"] == 64
     assert abs(r["value"] - n * 2 * 64 * 2 / (r["ms_per_step"] * 2 / 1000)) / r["value"] < 1e-3
 
@@ -61,3 +68,122 @@ def test_scaling_sweep_harness(tmp_path):
     assert abs(rows[1]["scaling_efficiency"] - rows[1]["tokens_per_s"] / (2 * rows[0]["tokens_per_s"])) < 1e-3
     assert (out / "scaling.json").exists() and (out / "n2.log").exists()
     assert "| 2 | fsdp2 |" in (out / "scaling.md").read_text()
+
+
+ARGS8 = ["--device", "cpu", "--model", "tiny8", "--seq-len", "64", "--steps", "2", "--warmup", "1", "--quiet"]
+
+
+@pytest.mark.parametrize("layout,extra,par,scaling,batch", [
+    ("tp", ["--micro-batch", "4"], "tp8", "strong", 4),
+    ("hybrid", ["--micro-batch", "4"], "fsdp2xtp4", "weak", 8),
+    ("pp", ["--micro-batch", "8", "--microbatches", "4"], "pp4xddp2", "weak", 16),
+])
+def test_bench_baseline_layouts_world8(layout, extra, par, scaling, batch, tmp_path):
+    """BASELINE configs 3-5 (TP=8, FSDP(2) x TP(4), PP4 x DDP2) under bench.py's JSON contract at world 8 (gloo)."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "8",
+           "--layout", layout] + ARGS8 + extra
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    recs = _lines(p.stdout)
+    assert len(recs) == 1, p.stdout
+    r = recs[0]
+    assert KEYS <= set(r) and r["n_gpus"] == 8 and r["unit"] == "tokens/s"
+    assert r["config"]["parallelism"] == par and r["scaling"] == scaling and r["config"]["layout"] == layout
+    assert r["config"]["global_batch"] == batch
+    assert r["preflight_ok"] is True
+    if layout != "tp":   # replicas exist only over a dp dimension
+        assert r["param_checksum_ok"] is True
+    assert abs(r["value"] - batch * 64 * 2 / (r["ms_per_step"] * 2 / 1000)) / r["value"] < 1e-3
+
+
+def test_bench_resnet_fsdp_layout(tmp_path):
+    """BASELINE config 2 (ResNet-50 FSDP bf16) under the contract; a ResNet-18 at 32 px keeps it CPU-sized."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--layout", "resnet-fsdp", "--device", "cpu", "--arch", "resnet18", "--image-size", "32",
+           "--micro-batch", "2", "--steps", "2", "--warmup", "1", "--quiet"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = _lines(p.stdout)[0]
+    assert r["unit"] == "images/s" and r["config"]["parallelism"] == "fsdp2" and r["config"]["global_batch"] == 4
+    assert r["preflight_ok"] is True and r["images_per_sec_per_gpu"] > 0
+
+
+# ---- pre-flight failure injection: a corrupted collective / diverged replica must abort, not publish ----
+def _selftest_corrupt_worker(rank, world, which):
+    import torch.distributed as dist
+
+    from distributed_pytorch_hpc_amd.runtime import preflight
+
+    real = getattr(dist, which)
+
+    def bad(*a, **kw):
+        w = real(*a, **kw)
+        if w is not None:
+            w.wait()
+        if rank == 1:
+            a[0].add_(1)     # rank 1's result (after the collective completed) is off by one everywhere
+        return None
+
+    setattr(dist, which, bad)
+    try:
+        preflight.collective_selftest(None, None)
+    except preflight.PreflightError as e:
+        return str(e)
+    finally:
+        setattr(dist, which, real)
+    return "no error"
+
+
+@pytest.mark.parametrize("which", ["all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor"])
+def test_preflight_detects_corrupted_collective(which):
+    from dist_utils import run_distributed
+
+    outs = run_distributed(_selftest_corrupt_worker, 2, which)
+    # rank 1 names its mismatch; rank 0 either finishes or fails on the next collective its peer never joins
+    assert "mismatch on rank 1" in outs[1], outs
+    assert outs[0] == "no error" or "mismatch" not in outs[0], outs
+
+
+def _replica_worker(rank, world, diverge):
+    import torch
+
+    from distributed_pytorch_hpc_amd.runtime import preflight
+
+    flat = torch.linspace(-1, 1, 1000)
+    if diverge and rank == world - 1:
+        flat[[10, 20]] = flat[[20, 10]]    # a swapped pair: same plain sum, different position-weighted sum
+    try:
+        return preflight.replicas_agree(flat)["ok"]
+    except preflight.PreflightError as e:
+        return str(e)
+
+
+def test_replica_checksum_detects_divergence():
+    from dist_utils import run_distributed
+
+    assert run_distributed(_replica_worker, 4, False) == [True] * 4
+    outs = run_distributed(_replica_worker, 4, True)
+    assert all(isinstance(o, str) and "diverged" in o for o in outs), outs
+
+
+def _probe_worker(rank, world):
+    from distributed_pytorch_hpc_amd.runtime import preflight
+
+    fits = preflight.probe_alpha_beta(None, None, sizes_mib=(0.0625, 0.25), budget_s=5.0)
+    mib = preflight.calibrated_bucket_mb(fits, 64 * 2 ** 20, True, lo_mib=1.0, hi_mib=64.0)
+    return {k: (v.alpha_s, v.beta_bus_Bps) for k, v in fits.items()}, mib
+
+
+def test_alpha_beta_probe_and_bucket_choice():
+    from dist_utils import run_distributed
+
+    outs = run_distributed(_probe_worker, 2)
+    fits, mib = outs[0]
+    assert set(fits) == {"reduce_scatter", "all_gather"}
+    for a, b in fits.values():
+        assert a >= 0 and b > 0
+    assert 1.0 <= mib <= 64.0

@@ -33,3 +33,21 @@ def test_bench_two_ranks_share_one_gpu(tmp_path, fp8):
     assert abs(r["loss_last"] - r["loss_first_warmup"]) < 2.0
     assert r["config"]["parallelism"] == "fsdp2" and r["config"]["global_batch"] == 4
     assert r["config"]["kernels"] == "dph"
+    assert r["preflight_ok"] is True and r["param_checksum_ok"] is True
+
+
+def test_bench_tp_layout_two_ranks_share_one_gpu(tmp_path):
+    """--layout tp (BASELINE config 3's TP + SP + loss-parallel plan) on GPU tensors: two gloo ranks, one MI355X."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--backend", "gloo", "--layout", "tp", "--model", "tiny8", "--seq-len", "128",
+           "--micro-batch", "2", "--steps", "2", "--warmup", "1", "--quiet"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=100, cwd=str(tmp_path),
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")][0]
+    assert r["config"]["parallelism"] == "tp2" and r["dtype"] == "bf16" and r["value"] > 0
+    assert abs(r["loss_last"] - r["loss_first_warmup"]) < 2.0
