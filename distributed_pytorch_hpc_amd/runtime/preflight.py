@@ -110,12 +110,17 @@ def collective_selftest(group=None, device=None, timeout_s: float = 120.0, numel
     return report
 
 
-def checksum(flat: torch.Tensor) -> torch.Tensor:
+def checksum(flat: torch.Tensor, chunk: int = 1 << 26) -> torch.Tensor:
     """Two order-sensitive float64 checksums of a flat tensor: plain sum and a position-weighted sum (a swapped pair
-    of elements changes the second)."""
-    x = flat.detach().reshape(-1).double()
-    w = (torch.arange(x.numel(), device=x.device, dtype=torch.float64) % 1021) + 1.0
-    return torch.stack([x.sum(), (x * w).sum()])
+    of elements changes the second).  Chunked: a 7B-parameter buffer as one float64 copy would need 54 GB."""
+    x = flat.detach().reshape(-1)
+    acc = torch.zeros(2, dtype=torch.float64, device=x.device)
+    for o in range(0, x.numel(), chunk):
+        c = x[o:o + chunk].double()
+        w = (torch.arange(o, o + c.numel(), device=x.device, dtype=torch.int64) % 1021 + 1).double()
+        acc[0] += c.sum()
+        acc[1] += (c * w).sum()
+    return acc
 
 
 def replicas_agree(flat: torch.Tensor, group=None, timeout_s: float = 120.0) -> dict:
