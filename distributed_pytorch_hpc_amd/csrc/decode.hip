@@ -391,11 +391,12 @@ __global__ __launch_bounds__(64 * NWV) void skinny_gemm_k(const bf16* __restrict
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) red[wave][mt][lane] = acc[mt];
   __syncthreads();
-  if (wave < MT) {   // wave mt sums m-tile mt: C[n = 4 g + i][m = mt * 16 + r]
-    f32x4 s = red[0][wave][lane];
+  // wave w sums m-tiles w, w + NWV, ...: C[n = 4 g + i][m = mt * 16 + r] (fewer waves than m-tiles is legal)
+  for (int mt = wave; mt < MT; mt += NWV) {
+    f32x4 s = red[0][mt][lane];
 #pragma unroll
-    for (int v = 1; v < NWV; ++v) s += red[v][wave][lane];
-    const int m = wave * 16 + r;
+    for (int v = 1; v < NWV; ++v) s += red[v][mt][lane];
+    const int m = mt * 16 + r;
     if (m < M) {
       bf16x4 o;
 #pragma unroll

@@ -817,9 +817,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
   }
   uint8_t* rmask = nullptr;   // [y > 0] bits for the backward (ReLU after a residual add: y is not re-read)
   if (relu_mask_out.has_value()) {
-    TORCH_CHECK(relu && relu_mask_out->scalar_type() == at::kByte && relu_mask_out->is_contiguous() &&
-                    relu_mask_out->numel() == M * C / 8 && relu_mask_out->device() == x.device(),
-                "bn_act_fwd: relu_mask_out must be a contiguous uint8 [M * C / 8] and relu set");
+    // the kernel writes the mask on the residual + ReLU path only (bn_apply): without a residual the bits would
+    // stay uninitialised and bn_act_bwd would read them as the ReLU mask
+    TORCH_CHECK(relu && res.has_value() && relu_mask_out->scalar_type() == at::kByte &&
+                    relu_mask_out->is_contiguous() && relu_mask_out->numel() == M * C / 8 &&
+                    relu_mask_out->device() == x.device(),
+                "bn_act_fwd: relu_mask_out must be a contiguous uint8 [M * C / 8], with relu set and a residual");
     rmask = relu_mask_out->data_ptr<uint8_t>();
   }
   const int G = dph::bn_partial_blocks(M, C);

@@ -121,3 +121,117 @@ def _maxpool_s2_bwd(dy, tap, H, W, k):
 @register_fake("dph::channel_sum")
 def _channel_sum(x, out_dtype):
     return x.new_empty((x.shape[1],), dtype=out_dtype)
+
+
+# ---- attention / GEMM / embedding / loss (restored) and serving / FP8 ops ----
+@register_fake("dph::flash_attn_fwd")
+def _flash_attn_fwd(q, k, v, scale, causal, dropout_p=0.0, seed=0):
+    # q [B, S, H, D] -> o [B, S, H, Dv], lse [B, H, S] fp32
+    o = q.new_empty(q.shape)
+    return o, q.new_empty((q.shape[0], q.shape[2], q.shape[1]), dtype=torch.float32)
+
+
+@register_fake("dph::flash_attn_bwd")
+def _flash_attn_bwd(dout, q, k, v, o, lse, scale, causal, dropout_p=0.0, seed=0):
+    return torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+
+
+@register_fake("dph::flash_attn_bwd_into")
+def _flash_attn_bwd_into(dout, q, k, v, o, lse, scale, causal, dq, dk, dv, dropout_p=0.0, seed=0, rope_cos=None,
+                         rope_sin=None, rope_offset=0):
+    return None
+
+
+@register_fake("dph::cross_entropy_fwd")
+def _cross_entropy_fwd(logits, target, inv_count, ignore_index, grad_inplace, smoothing):
+    n = logits.shape[0]
+    return logits.new_empty((n,), dtype=torch.float32), logits.new_empty((n,), dtype=torch.float32)
+
+
+@register_fake("dph::embedding_fwd")
+def _embedding_fwd(ids, table, vocab_start):
+    return table.new_empty((*ids.shape, table.shape[1]))
+
+
+@register_fake("dph::embedding_bwd")
+def _embedding_bwd(ids, dout, vocab_local, vocab_start):
+    return dout.new_empty((vocab_local, dout.shape[-1]), dtype=torch.float32)
+
+
+@register_fake("dph::gemm_tn_")
+def _gemm_tn(C, A, B, accumulate):
+    return None
+
+
+@register_fake("dph::ts_gemm_nt")
+def _ts_gemm_nt(A, B, H=0, W=0, add=None):
+    return A.new_empty((A.shape[0], B.shape[0]))
+
+
+@register_fake("dph::ts_gemm_nt_stats")
+def _ts_gemm_nt_stats(A, B):
+    M, N = A.shape[0], B.shape[0]
+    nmb = (M + 127) // 128
+    return A.new_empty((M, N)), A.new_empty((2 * nmb * N + nmb,), dtype=torch.float32)
+
+
+@register_fake("dph::ts_gemm_tn_")
+def _ts_gemm_tn(C, A, B, accumulate, H=0, W=0):
+    return None
+
+
+@register_fake("dph::latmse_fwd")
+def _latmse_fwd(pred, target, n_global, lat_offset):
+    return pred.new_empty((), dtype=torch.float32)
+
+
+@register_fake("dph::latmse_bwd")
+def _latmse_bwd(gloss, pred, target, n_global, lat_offset, need_dtarget):
+    return torch.empty_like(pred), (torch.empty_like(target) if need_dtarget else pred.new_empty((0,)))
+
+
+@register_fake("dph::image_augment")
+def _image_augment(images, idx, params, mean, inv_std, pad, channels_last, bf16_out):
+    _, H, W, C = images.shape
+    y = images.new_empty((idx.shape[0], C, H, W), dtype=torch.bfloat16 if bf16_out else torch.float32)
+    return y.contiguous(memory_format=torch.channels_last) if channels_last else y
+
+
+@register_fake("dph::fp8_quantize")
+def _fp8_quantize(x, fmt, rowmajor, transposed):
+    f8 = torch.float8_e4m3fn if fmt == 0 else torch.float8_e5m2
+    R, C = x.shape
+    y = x.new_empty((R, C) if rowmajor else (0,), dtype=f8)
+    yt = x.new_empty((C, R) if transposed else (0,), dtype=f8)
+    return y, yt, x.new_empty((), dtype=torch.float32)
+
+
+@register_fake("dph::kv_append_")
+def _kv_append(qkv, k_cache, v_cache, pos, cos, sin, n_heads, n_kv_heads, kv_scale=1.0):
+    return None
+
+
+@register_fake("dph::decode_attention")
+def _decode_attention(qkv, k_cache, v_cache, pos, n_heads, n_kv_heads, scale, max_len, kv_scale=1.0):
+    D = k_cache.shape[-1]
+    return qkv.new_empty((qkv.shape[0], n_heads * D))
+
+
+@register_fake("dph::skinny_linear")
+def _skinny_linear(x, w):
+    return x.new_empty((*x.shape[:-1], w.shape[0]))
+
+
+@register_fake("dph::gemv_swiglu")
+def _gemv_swiglu(x2, w):
+    return x2.new_empty((*x2.shape[:-1], w.shape[0]))
+
+
+@register_fake("dph::gemv_rmsnorm")
+def _gemv_rmsnorm(x, res, norm_weight, eps, w):
+    return x.new_empty((*x.shape[:-1], w.shape[0])), (torch.empty_like(x) if res is not None else x.new_empty((0,)))
+
+
+@register_fake("dph::car_allreduce")
+def _car_allreduce(ctx, inp, out, algo, scale, max_blocks):
+    return None

@@ -535,7 +535,9 @@ class DataParallelEngine:
         self.synchronize()
         return {"step": self.step_count, "master": self.master.cpu(),
                 "state": [s.cpu() for s in self.opt_state], "world": self.world, "rank": self.rank,
-                "shard": self.shard, "total": self.total, "kind": "dp"}
+                "shard": self.shard, "total": self.total, "kind": "dp",
+                # unpadded length of every bucket: lets a resume with another bucket partition re-cut the state
+                "group_real": [sum(align_up(p.numel()) for p in b.params) for b in self.buckets]}
 
     def load_optimizer_state_dict(self, sd: dict):
         assert sd.get("kind", "dp") == "dp" and sd["total"] == self.total and sd["shard"] == self.shard and \

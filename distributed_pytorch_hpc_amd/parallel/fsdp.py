@@ -435,7 +435,7 @@ class ZeRO3Engine:
             o = 0
             for p in u.params:
                 n = p.numel()
-                full[o:o + n].copy_(flat_order_like(sd[names[id(p)]], p))
+                full[o:o + n].copy_(flat_order_like(sd[names[id(p)]], p, names[id(p)]))
                 o += align_up(n)
             mine = full[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel].to(self.device)
             self.shard_view(u).copy_(mine)
@@ -461,7 +461,7 @@ class ZeRO3Engine:
         self.synchronize()
         return {"step": self.step_count, "master": self.master.cpu(), "state": [s.cpu() for s in self.opt_state],
                 "world": self.world, "rank": self.rank, "shard": True, "total": self.shard_total * self.world,
-                "kind": "zero3"}
+                "kind": "zero3", "group_real": [sum(align_up(p.numel()) for p in u.params) for u in self.units]}
 
     def load_optimizer_state_dict(self, sd):
         assert sd.get("kind") == "zero3" and sd["world"] == self.world and \

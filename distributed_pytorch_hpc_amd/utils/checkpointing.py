@@ -149,7 +149,7 @@ def load_full_optimizer_state(engine, sd: dict):
             o = 0
             for p in g.params:
                 n = p.numel()
-                full[o:o + n].copy_(flat_order_like(src[names[id(p)]], p))
+                full[o:o + n].copy_(flat_order_like(src[names[id(p)]], p, names[id(p)]))
                 o += align_up(n)
             vec[engine.opt_slice(g)].copy_(full[rs])
     engine.step_count = int(sd["step"])
@@ -311,43 +311,81 @@ class ShardedCheckpointer:
 
 @torch.no_grad()
 def reshard_engine_state(engine, shards: list[dict]):
-    """Rebuild the engine's optimizer state from the per-rank states of a run with another dp world size.
+    """Rebuild the engine's optimizer state from the per-rank states of a run with another dp world size (and
+    possibly another bucket partition, e.g. a different ``bucket_cap_mb`` or the world-dependent 'calibrate' /
+    'auto' sizes).
 
-    Every saved rank stored its slice of every group (bucket / unit); the group layout is a pure function of the
-    model, the bucketing / wrap policy and the world size (padding to ALIGN * world).  The full padded group vectors
-    are reassembled from the OLD layout, then this rank's slice of the NEW layout is copied out.
+    Every saved rank stored its slice of every group (bucket / unit), each group padded to ALIGN * world.  The
+    saved ``group_real`` (unpadded group lengths) gives the OLD partition; stripping each old group's padding yields
+    the dense sequence of aligned parameter segments, which is the same for any partition of the same model (the
+    parameter order does not depend on where the buckets are cut) and is re-cut into this engine's groups.  A
+    checkpoint without ``group_real`` (older format) must match this engine's partition exactly; a mismatch raises
+    instead of silently leaving the fp32 master / AdamW moments unrestored.
     """
     old_world, old_sharded = shards[0]["world"], shards[0]["shard"]
     if shards[0].get("kind", "dp") != ("zero3" if hasattr(engine, "full_state_dict") else "dp"):
         raise ValueError("reshard_engine_state: checkpoint written by another engine kind; use the consolidated "
                          "save_checkpoint/load_checkpoint format to change strategy")
-    sizes = [align_up(sum(align_up(p.numel()) for p in g.params), ALIGN * old_world) for g in engine.groups]
+    new_real = [sum(align_up(p.numel()) for p in g.params) for g in engine.groups]
+    old_real = shards[0].get("group_real")
+    if old_real is None:
+        old_real = new_real
+        old_total = sum(align_up(r, ALIGN * old_world) for r in old_real)
+        if "total" in shards[0] and int(shards[0]["total"]) != old_total:
+            raise ValueError(f"reshard_engine_state: the checkpoint's bucket partition (total {shards[0]['total']}) "
+                             f"differs from this engine's ({old_total}) and the checkpoint records no group sizes; "
+                             f"resume with the original bucket partition")
+    if sum(old_real) != sum(new_real):
+        raise ValueError(f"reshard_engine_state: checkpoint holds {sum(old_real)} parameter elements, this engine "
+                         f"{sum(new_real)} (another model?)")
+    sizes = [align_up(r, ALIGN * old_world) for r in old_real]
     old_total = sum(sizes)
 
     def assemble(get):
+        """Dense (padding-free) concatenation of the old groups' real parts."""
         if not old_sharded:
-            return get(shards[0])
-        parts, offs = [], [0] * old_world
-        for sz in sizes:
-            sh = sz // old_world
-            for r in range(old_world):
-                parts.append(get(shards[r])[offs[r]:offs[r] + sh])
-                offs[r] += sh
-        return torch.cat(parts)
+            full = get(shards[0])
+        else:
+            parts, offs = [], [0] * old_world
+            for sz in sizes:
+                sh = sz // old_world
+                for r in range(old_world):
+                    parts.append(get(shards[r])[offs[r]:offs[r] + sh])
+                    offs[r] += sh
+            full = torch.cat(parts)
+        if full.numel() != old_total:
+            raise ValueError(f"reshard_engine_state: saved vector of {full.numel()} elements, layout needs {old_total}")
+        dense, o = [], 0
+        for sz, real in zip(sizes, old_real):
+            dense.append(full[o:o + real])
+            o += sz
+        return torch.cat(dense)
 
     n_state = len(shards[0]["state"])
-    fulls = [assemble(lambda s: s["master"])] + [assemble(lambda s, i=i: s["state"][i]) for i in range(n_state)]
     dsts = [engine.master] + list(engine.opt_state)
-    o = 0
-    for g, sz in zip(engine.groups, sizes):
-        real = sum(align_up(p.numel()) for p in g.params)
-        rs = _rank_slice(engine, g)
-        for src, dst in zip(fulls, dsts):
-            if src.numel() != old_total or dst.numel() != engine.master.numel():
-                continue   # not laid out like the master (SGD without momentum: a dummy)
+    if n_state != len(engine.opt_state):
+        raise ValueError(f"reshard_engine_state: {n_state} optimizer-state vectors saved, engine has "
+                         f"{len(engine.opt_state)} (another optimizer?)")
+    getters = [lambda s: s["master"]] + [lambda s, i=i: s["state"][i] for i in range(n_state)]
+    # The caller loaded the checkpoint's model first, so the engine's master currently holds those weights (rounded
+    # to the parameter dtype).  The re-cut fp32 master must round to exactly them: a wrong partition guess (older
+    # checkpoints without group sizes) shows up here instead of training on scrambled optimizer state.
+    current = engine.master.detach().cpu().clone()
+    pdt = getattr(engine, "param_dtype", torch.float32)
+    for k, (get, dst) in enumerate(zip(getters, dsts)):
+        if dst.numel() == 1 and get(shards[0]).numel() == 1:
+            continue   # SGD without momentum: a one-element dummy, not laid out like the master
+        dense = assemble(get)
+        o = 0
+        for g, real in zip(engine.groups, new_real):
             t = torch.zeros(g.numel, dtype=torch.float32)
-            t[:real] = src[o:o + real]
-            dst[engine.opt_slice(g)].copy_(t[rs])
-        o += sz
+            t[:real] = dense[o:o + real]
+            mine = t[_rank_slice(engine, g)]
+            if k == 0 and not torch.equal(mine.to(pdt).float(), current[engine.opt_slice(g)]):
+                raise ValueError("reshard_engine_state: the checkpoint's fp32 master does not match its model weights "
+                                 "under this engine's bucket partition (saved with another bucket_cap_mb and no "
+                                 "recorded group sizes?); resume with the original bucket partition")
+            dst[engine.opt_slice(g)].copy_(mine)
+            o += real
     engine.step_count = int(shards[0]["step"])
     engine.refresh_params_from_master()

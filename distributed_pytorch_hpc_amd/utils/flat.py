@@ -77,9 +77,14 @@ def flat_order(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1).reshape(-1) if _cl4(t) else t.reshape(-1)
 
 
-def flat_order_like(value: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+def flat_order_like(value: torch.Tensor, like: torch.Tensor, name: str | None = None) -> torch.Tensor:
     """A logically-shaped ``value`` (any strides, e.g. from a state dict) flattened in ``like``'s storage order, i.e.
-    the element order ``like`` has inside an engine's flat buffer (inverse of ``param_view(...).contiguous()``)."""
+    the element order ``like`` has inside an engine's flat buffer (inverse of ``param_view(...).contiguous()``).
+    The shapes must match exactly: a same-numel tensor of another shape (e.g. a transposed weight) would otherwise
+    load silently in scrambled order."""
+    if tuple(value.shape) != tuple(like.shape):
+        raise ValueError(f"size mismatch for {name or 'parameter'}: copying a param with shape {tuple(value.shape)}, "
+                         f"the shape in the current model is {tuple(like.shape)}")
     return value.permute(0, 2, 3, 1).reshape(-1) if _cl4(like) else value.reshape(-1)
 
 

@@ -9,12 +9,12 @@ from dist_utils import run_distributed
 PRESET = dict(dim=64, n_layers=2, n_heads=4, vocab_size=128, max_seq_len=64, multiple_of=32)
 
 
-def _setup(shard):
+def _setup(shard, bucket_mb=0.02):
     from distributed_pytorch_hpc_amd.models.llama2 import ModelArgs, build_llama
     from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig
 
     m = build_llama(ModelArgs(**PRESET), device="cpu", dtype=torch.float32, seed=5)
-    eng = DataParallelEngine(m, shard=shard, bucket_cap_mb=0.02)
+    eng = DataParallelEngine(m, shard=shard, bucket_cap_mb=bucket_mb)
     eng.configure_optimizer(OptimConfig(lr=1e-2, weight_decay=0.1))
     return m, eng
 
@@ -56,10 +56,10 @@ def _save_then_resume(rank, world, root, resume_world_same):
     return {k: v.clone() for k, v in m2.state_dict().items()}
 
 
-def _resume_single(root):
+def _resume_single(root, bucket_mb=0.02):
     from distributed_pytorch_hpc_amd.utils.checkpointing import ShardedCheckpointer
 
-    m, eng = _setup(False)
+    m, eng = _setup(False, bucket_mb)
     step = ShardedCheckpointer(root, m, eng).load()
     assert step == 2
     _train(m, eng, _batches(4)[2:], 0, 1)
@@ -139,6 +139,34 @@ def test_sharded_resume_reshard_to_one_rank(tmp_path):
     got = _resume_single(str(tmp_path))
     for k in ref:
         assert torch.allclose(ref[k], got[k], atol=1e-5), k
+
+
+def test_sharded_resume_reshard_other_bucket_partition(tmp_path):
+    """Resume at dp=1 with another bucket size (the 'calibrate' / 'auto' sizes depend on the world): the state is
+    re-cut from the saved group sizes, and the fp32 master AND the AdamW moments come back."""
+    run_distributed(_save_then_resume, 2, str(tmp_path), True)
+    ref = run_distributed(_uninterrupted, 2)[0]
+    got = _resume_single(str(tmp_path), bucket_mb=0.05)
+    for k in ref:
+        assert torch.allclose(ref[k], got[k], atol=1e-5), k
+
+
+def test_reshard_without_group_sizes_refuses_other_partition(tmp_path):
+    """An older checkpoint (no recorded group sizes) whose partition differs must raise, not silently skip."""
+    import glob
+
+    import pytest
+
+    from distributed_pytorch_hpc_amd.utils.checkpointing import ShardedCheckpointer
+
+    run_distributed(_save_then_resume, 2, str(tmp_path), True)
+    for f in glob.glob(os.path.join(str(tmp_path), "**", "rank*.pt"), recursive=True):
+        st = torch.load(f, map_location="cpu", weights_only=True)
+        st["optim"].pop("group_real", None)
+        torch.save(st, f)
+    m, eng = _setup(False, bucket_mb=0.05)
+    with pytest.raises(ValueError, match="bucket partition"):   # caught by the master-vs-weights check
+        ShardedCheckpointer(str(tmp_path), m, eng).load()
 
 
 # ------------------------------------------------------------------------------------------------ FSDP / ZeRO engines
@@ -252,3 +280,15 @@ def test_fsdp_full_shard_sharded_checkpointer_reshard(tmp_path):
     run_distributed(_fsdp_sharded_save, 2, root)
     _close(ref, run_distributed(_fsdp_sharded_resume, 2, root)[0])
     _close(ref, run_distributed(_fsdp_sharded_resume, 1, root)[0])
+
+
+def test_fsdp_full_shard_load_rejects_wrong_shape():
+    """A same-numel tensor of another shape (a transposed weight) must not load silently in scrambled order."""
+    import pytest
+
+    f, _ = _fsdp_setup()
+    sd = f.full_state_dict(rank0_only=False)
+    sd["2.weight"] = sd["2.weight"].t().contiguous()        # 32 x 32: same numel, transposed
+    sd["0.weight"] = sd["0.weight"].reshape(16, 32)          # 32 x 16 -> 16 x 32
+    with pytest.raises(ValueError, match=r"size mismatch for 0\.weight"):
+        f.load_state_dict(sd)
