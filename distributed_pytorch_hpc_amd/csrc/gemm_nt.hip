@@ -1,0 +1,340 @@
+// Forward / input-gradient GEMM for CDNA4 (gfx950):  C[M, N] = A[M, K] B[N, K]^T, both operands K-contiguous
+// (token-major activations x [out, in] weights: y = x W^T; the input gradient dX = dY W runs on the same kernel
+// with a transposed weight copy), with fusable epilogues:
+//   * STORE   -- plain bf16 C;
+//   * SWIGLU  -- the fused w13 projection of the Llama FFN: B = [W1; W3] ([2H, K]); one 256-column tile holds the
+//                gate AND up columns of 128 hidden units, so h = silu(gate) * up is formed in registers and the
+//                kernel writes x13 = [gate | up] (saved for backward) and h (the next GEMM's input) -- the separate
+//                swiglu_fwd pass (read 2H, write H per token) disappears;
+//   * DSWIGLU -- the input gradient of w2 (dh = dY W2) followed by the SwiGLU backward: the epilogue reads the
+//                saved gate / up values and writes d13 = [dgate | dup] straight away (no dh round trip);
+//   * ROPE    -- the fused wqkv projection with the rotary embedding of the q / k columns applied to the fp32
+//                accumulators (one rounding instead of GEMM-round + rope-round, no separate rope pass).
+//
+// Structure (cdna_hip_programming.md §5 "256^2 8-phase template", designed for this layout):
+//   * 256 x 256 output tile per workgroup, 8 waves as 2 (M) x 4 (N), wave tile 128 tokens x 64 features,
+//     v_mfma_f32_16x16x32_bf16 with the weight rows as the MFMA A operand and the token rows as B, so a lane ends
+//     with 4 CONSECUTIVE features of one token (8-byte stores; RoPE pairs and gate/up pairs are lane-local);
+//   * K-tiles of 64, staged global -> LDS by LDS-DMA (global_load_lds_dwordx4, 16 B / lane, full 128-B rows,
+//     XOR-swizzled 16-B chunks: slot = chunk ^ ((row >> 1) & 7), conflict-free ds_read_b128 fragment reads);
+//   * each K-tile is four "quarter" images (16 KB each): Q_A0 / Q_A1 = the first / second 64 token rows of every
+//     wave row-group, Q_B0 / Q_B1 = the first / second 32 feature rows of every wave column-group.  A K-tile
+//     runs as 4 phases, one quadrant of the wave tile each: (A0,B0) (A0,B1) (A1,B1) (A1,B0), so phase 1 reads
+//     A0+B0 fragments, phase 2 B1, phase 3 A1, phase 4 nothing;
+//   * every phase issues ONE quarter of a future K-tile (Q_B1 / Q_A1 of t+1, Q_A0 / Q_B0 of t+2, each region
+//     >= 2 phases after its last read) and waits vmcnt(8): four quarters (64 KB per CU) stay in flight across
+//     the barriers and the wait retires exactly what the next phase reads;
+//   * the second half of the waves (4..7) runs one barrier behind the first (stagger): on every SIMD one wave
+//     issues its MFMAs while its partner reads fragments / issues DMA -- the matrix pipe ping-pongs;
+//   * workgroups are remapped XCD-aware and grouped GROUP_M tiles tall (as gemm.hip) for L2 reuse.
+// Requirements (host-checked): M % 256, N % 256 (SWIGLU: H % 128), K % 64, leading dims % 8, 16-B aligned bases.
+#include <type_traits>
+
+#include "dph_common.h"
+#include "kernels.h"
+
+namespace dph {
+
+namespace {
+
+constexpr int NBM = 256, NBN = 256, NBK = 64, NNT = 512;
+constexpr int QB = 16384;       // one quarter image: 128 rows x 128 B
+constexpr int BUFB = 4 * QB;    // one K-tile: Q_A0 | Q_A1 | Q_B0 | Q_B1
+constexpr int NGROUP_M = 8;
+
+enum : int { Q_A0 = 0, Q_A1 = 1, Q_B0 = 2, Q_B1 = 3 };
+
+__device__ __forceinline__ void nt_grouped_tile(int lin, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int first_m = lin / (NGROUP_M * tiles_n) * NGROUP_M;
+  const int gsz = min(tiles_m - first_m, NGROUP_M);
+  const int in_group = lin % (NGROUP_M * tiles_n);
+  tm = first_m + in_group % gsz;
+  tn = in_group / gsz;
+}
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float nt_sigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
+
+template <int MODE>
+__global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
+  __shared__ __attribute__((aligned(1024))) char lds[2 * BUFB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int r16 = lane & 15, kq = lane >> 4;
+
+  // ---- tile of this workgroup (XCD-aware, grouped) ----
+  const int tiles_m = p.M / NBM, tiles_n = p.tiles_n;
+  int tm, tn;
+  nt_grouped_tile(xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * NBM;
+  // first global weight row of Q_B0's / Q_B1's image row 0, and the image-row -> weight-row map:
+  //   STORE / DSWIGLU / ROPE: rho -> n0 + 64 (rho >> 5) + (rho & 31) (+ 32 for Q_B1)   (wave wn: 64 rows)
+  //   SWIGLU:                 rho -> 128 tn + rho (gate) / H + 128 tn + rho (up)      (wave wn: 32 units)
+  int64_t nbase0, nbase1;
+  if constexpr (MODE == kNtSwiglu) {
+    nbase0 = (int64_t)tn * 128;
+    nbase1 = (int64_t)p.H + (int64_t)tn * 128;
+  } else {
+    nbase0 = (int64_t)tn * NBN;
+    nbase1 = nbase0 + 32;
+  }
+
+  // ---- per-lane LDS-DMA source offsets (bytes, relative to the quarter's row-0 pointer at k-tile 0) ----
+  unsigned voff[4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = i * NNT + tid, rho = c >> 3, kc = (c & 7) ^ ((rho >> 1) & 7);
+      int row;
+      if (q < 2) row = 128 * (rho >> 6) + (rho & 63);            // Q_A1's base pointer carries the +64
+      else if (MODE == kNtSwiglu) row = rho;
+      else row = 64 * (rho >> 5) + (rho & 31);                    // Q_B1's base pointer carries the +32
+      const int64_t ld = q < 2 ? p.lda : p.ldb;
+      voff[q][i] = (unsigned)(row * ld * 2 + kc * 16);
+    }
+  const char* qptr[4];
+  const bf16* Ap = reinterpret_cast<const bf16*>(p.A);
+  const bf16* Bp = reinterpret_cast<const bf16*>(p.B);
+  qptr[Q_A0] = reinterpret_cast<const char*>(Ap + (int64_t)m0 * p.lda);
+  qptr[Q_A1] = reinterpret_cast<const char*>(Ap + (int64_t)(m0 + 64) * p.lda);
+  qptr[Q_B0] = reinterpret_cast<const char*>(Bp + nbase0 * p.ldb);
+  qptr[Q_B1] = reinterpret_cast<const char*>(Bp + nbase1 * p.ldb);
+  const unsigned lds_w = lds_addr(lds + wid * 1024);
+  const int nk = p.K / NBK;
+
+  auto dma = [&](auto QI, int kt, auto BI) {
+    constexpr int Q = decltype(QI)::value, BUF = decltype(BI)::value;
+    const int ktc = min(kt, nk - 1);   // past the end: re-load the last tile into a slot nobody reads again
+    const char* src = qptr[Q] + (int64_t)ktc * (NBK * 2);
+    const unsigned d = lds_w + BUF * BUFB + Q * QB;
+    lds_dma16(src, voff[Q][0], d);
+    lds_dma16(src, voff[Q][1], d + NNT * 16);
+  };
+
+  // ---- per-lane fragment read offsets: row r16 of a 16-row block, logical chunk 4 s + kq ----
+  const int xsw = (r16 >> 1) & 7;
+  const int off_s0 = r16 * 128 + ((kq ^ xsw) << 4);
+  const int off_s1 = r16 * 128 + (((4 + kq) ^ xsw) << 4);
+  const char* a_img = lds + wm * 8192;    // + Q * QB + buf * BUFB, + mb * 2048
+  const char* b_img = lds + wn * 4096;    // + Q * QB + buf * BUFB, + nb * 2048
+
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto read_a = [&](auto QI, auto BI) {
+    constexpr int Q = decltype(QI)::value, BUF = decltype(BI)::value;
+    const char* base = a_img + BUF * BUFB + Q * QB;
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      fa[mb][0] = *reinterpret_cast<const bf16x8*>(base + mb * 2048 + off_s0);
+      fa[mb][1] = *reinterpret_cast<const bf16x8*>(base + mb * 2048 + off_s1);
+    }
+  };
+  auto read_b = [&](auto QI, auto BI, bf16x8 (&fb)[2][2]) {
+    constexpr int Q = decltype(QI)::value, BUF = decltype(BI)::value;
+    const char* base = b_img + BUF * BUFB + Q * QB;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      fb[nb][0] = *reinterpret_cast<const bf16x8*>(base + nb * 2048 + off_s0);
+      fb[nb][1] = *reinterpret_cast<const bf16x8*>(base + nb * 2048 + off_s1);
+    }
+  };
+  // quadrant (a-half AH, b-half BH): 4 token blocks x 2 feature blocks x 2 k-steps of 32
+  auto mma = [&](auto AHI, auto BHI, const bf16x8 (&fb)[2][2]) {
+    constexpr int AH = decltype(AHI)::value, BH = decltype(BHI)::value;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+          acc[4 * AH + mb][2 * BH + nb] = mfma16(fb[nb][s], fa[mb][s], acc[4 * AH + mb][2 * BH + nb]);
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using IA0 = std::integral_constant<int, Q_A0>;
+  using IA1 = std::integral_constant<int, Q_A1>;
+  using IB0 = std::integral_constant<int, Q_B0>;
+  using IB1 = std::integral_constant<int, Q_B1>;
+
+  // One phase P (0..3) of K-tile kt held in buffer CUR:
+  //   reads (covered by the previous phase's wait + barrier) -> one quarter of DMA -> vmcnt(8) -> barrier ->
+  //   16 MFMAs -> barrier.
+  auto phase = [&](auto PI, auto CI, int kt) {
+    constexpr int P = decltype(PI)::value, CUR = decltype(CI)::value;
+    using ICUR = std::integral_constant<int, CUR>;
+    using INXT = std::integral_constant<int, CUR ^ 1>;
+    if constexpr (P == 0) { read_b(IB0{}, ICUR{}, fb0); read_a(IA0{}, ICUR{}); }
+    if constexpr (P == 1) read_b(IB1{}, ICUR{}, fb1);
+    if constexpr (P == 2) read_a(IA1{}, ICUR{});
+    if constexpr (P == 0) dma(IB1{}, kt + 1, INXT{});
+    if constexpr (P == 1) dma(IA1{}, kt + 1, INXT{});
+    if constexpr (P == 2) dma(IA0{}, kt + 2, ICUR{});
+    if constexpr (P == 3) dma(IB0{}, kt + 2, ICUR{});
+    wait_vmcnt<8>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    if constexpr (P == 0) mma(I0{}, I0{}, fb0);
+    if constexpr (P == 1) mma(I0{}, I1{}, fb1);
+    if constexpr (P == 2) mma(I1{}, I1{}, fb1);
+    if constexpr (P == 3) mma(I1{}, I0{}, fb0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // ---- prologue: Q_A0(0) Q_B0(0) Q_B1(0) Q_A1(0) Q_A0(1) Q_B0(1), as if phases of tiles -2 / -1 had run ----
+  dma(IA0{}, 0, I0{});
+  dma(IB0{}, 0, I0{});
+  dma(IB1{}, 0, I0{});
+  dma(IA1{}, 0, I0{});
+  dma(IA0{}, 1, I1{});
+  dma(IB0{}, 1, I1{});
+  wait_vmcnt<8>();
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  // stagger: waves 4..7 run one barrier behind waves 0..3 (uniform per wave: wid is wave-uniform)
+  const bool late = __builtin_amdgcn_readfirstlane(wid) >= 4;
+  if (late) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  int kt = 0;
+  for (; kt + 2 <= nk; kt += 2) {
+    phase(I0{}, I0{}, kt);
+    phase(I1{}, I0{}, kt);
+    phase(std::integral_constant<int, 2>{}, I0{}, kt);
+    phase(std::integral_constant<int, 3>{}, I0{}, kt);
+    phase(I0{}, I1{}, kt + 1);
+    phase(I1{}, I1{}, kt + 1);
+    phase(std::integral_constant<int, 2>{}, I1{}, kt + 1);
+    phase(std::integral_constant<int, 3>{}, I1{}, kt + 1);
+  }
+  if (kt < nk) {   // odd number of K-tiles: the last one sits in buffer 0
+    phase(I0{}, I0{}, kt);
+    phase(I1{}, I0{}, kt);
+    phase(std::integral_constant<int, 2>{}, I0{}, kt);
+    phase(std::integral_constant<int, 3>{}, I0{}, kt);
+  }
+  if (!late) __builtin_amdgcn_s_barrier();   // balance the stagger
+  wait_vmcnt<0>();                            // the clamped tail DMAs must land before the workgroup exits
+
+  // ---- epilogue: acc[mb][nb][j] = C[token m0 + 128 wm + 16 mb + r16][feature col(nb) + 4 kq + j] ----
+  const int64_t tok0 = (int64_t)m0 + 128 * wm + r16;
+  if constexpr (MODE == kNtSwiglu) {
+    // gate units u = 128 tn + 32 wn + 16 nb + 4 kq + j (nb < 2); acc[.][nb + 2] holds the matching up values
+    bf16* x13 = (bf16*)p.C;
+    bf16* hout = (bf16*)p.C2;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) {
+      const int64_t t = tok0 + 16 * mb;
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int64_t u = (int64_t)tn * 128 + 32 * wn + 16 * nb + 4 * kq;
+        bf16x4 g, up, hv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          g[j] = (bf16)acc[mb][nb][j];
+          up[j] = (bf16)acc[mb][nb + 2][j];
+          const float gf = (float)g[j];   // exactly swiglu_fwd_k's math on the rounded gate / up
+          hv[j] = (bf16)(gf * nt_sigmoid(gf) * (float)up[j]);
+        }
+        *reinterpret_cast<bf16x4*>(x13 + t * p.ldc + u) = g;
+        *reinterpret_cast<bf16x4*>(x13 + t * p.ldc + p.H + u) = up;
+        *reinterpret_cast<bf16x4*>(hout + t * p.ldc2 + u) = hv;
+      }
+    }
+  } else if constexpr (MODE == kNtDswiglu) {
+    // dh for hidden units u = n0 + 64 wn + 16 nb + 4 kq + j; x13 = saved [gate | up], d13 = [dgate | dup]
+    const bf16* x13 = (const bf16*)p.X;
+    bf16* d13 = (bf16*)p.C;
+    const int64_t ubase = (int64_t)tn * NBN + 64 * wn + 4 * kq;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) {
+      const int64_t t = tok0 + 16 * mb;
+      bf16x4 gv[4], uv[4];
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {   // issue all 8 loads of the row before any math
+        gv[nb] = *reinterpret_cast<const bf16x4*>(x13 + t * p.ldx + ubase + 16 * nb);
+        uv[nb] = *reinterpret_cast<const bf16x4*>(x13 + t * p.ldx + p.H + ubase + 16 * nb);
+      }
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        bf16x4 dg, du;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = (float)(bf16)acc[mb][nb][j];   // dh rounded like the unfused GEMM output
+          const float g = (float)gv[nb][j], u = (float)uv[nb][j];
+          const float s = nt_sigmoid(g);
+          du[j] = (bf16)(d * (g * s));
+          dg[j] = (bf16)(d * u * s * (1.f + g * (1.f - s)));
+        }
+        *reinterpret_cast<bf16x4*>(d13 + t * p.ldc + ubase + 16 * nb) = dg;
+        *reinterpret_cast<bf16x4*>(d13 + t * p.ldc + p.H + ubase + 16 * nb) = du;
+      }
+    }
+  } else {
+    bf16* C = (bf16*)p.C;
+    const int n_base = tn * NBN + 64 * wn + 4 * kq;
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb) {
+      const int64_t t = tok0 + 16 * mb;
+      int pos = 0;
+      if constexpr (MODE == kNtRope) pos = (int)(t % p.S) + p.pos_off;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int n = n_base + 16 * nb;
+        f32x4 v = acc[mb][nb];
+        if constexpr (MODE == kNtRope) {
+          if (n < p.n_rot) {   // interleaved pairs (n, n+1), (n+2, n+3) of head column d = n % hd
+            const int i0 = (n % p.hd) >> 1;
+            const float* ct = p.rope_cos + (int64_t)pos * (p.hd >> 1) + i0;
+            const float* st = p.rope_sin + (int64_t)pos * (p.hd >> 1) + i0;
+            const float c0 = ct[0], c1 = ct[1], s0 = st[0], s1 = st[1];
+            const float a0 = v[0], b0 = v[1], a1 = v[2], b1 = v[3];
+            v[0] = a0 * c0 - b0 * s0;
+            v[1] = a0 * s0 + b0 * c0;
+            v[2] = a1 * c1 - b1 * s1;
+            v[3] = a1 * s1 + b1 * c1;
+          }
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+        *reinterpret_cast<bf16x4*>(C + t * p.ldc + n) = o;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool gemm_nt_supported(int mode, int64_t M, int64_t N, int64_t K) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % NBM || K % NBK) return false;
+  return mode == kNtSwiglu ? N % 128 == 0 : N % NBN == 0;
+}
+
+void gemm_nt(int mode, const GemmNtParams& prm, hipStream_t st) {
+  GemmNtParams p = prm;
+  p.tiles_n = mode == kNtSwiglu ? p.N / 128 : p.N / NBN;
+  const dim3 grid((unsigned)((p.M / NBM) * p.tiles_n)), block(NNT);
+  switch (mode) {
+    case kNtSwiglu: hipLaunchKernelGGL(gemm_nt_k<kNtSwiglu>, grid, block, 0, st, p); break;
+    case kNtDswiglu: hipLaunchKernelGGL(gemm_nt_k<kNtDswiglu>, grid, block, 0, st, p); break;
+    case kNtRope: hipLaunchKernelGGL(gemm_nt_k<kNtRope>, grid, block, 0, st, p); break;
+    default: hipLaunchKernelGGL(gemm_nt_k<kNtStore>, grid, block, 0, st, p); break;
+  }
+}
+
+}  // namespace dph

@@ -118,6 +118,26 @@ void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_
              int64_t ldc, int out_dtype, bool accumulate, hipStream_t stream, const GemmTnPlan* plan = nullptr,
              float* workspace = nullptr);
 
+// Forward / input-gradient GEMM C[M, N] = A[M, K] B[N, K]^T with fusable epilogues (csrc/gemm_nt.hip).  bf16.
+enum : int { kNtStore = 0, kNtSwiglu = 1, kNtDswiglu = 2, kNtRope = 3 };
+struct GemmNtParams {
+  const void* A;        // bf16 [M, K], row stride lda
+  const void* B;        // bf16 [N, K] (SWIGLU: [2H, K] = [W1; W3]), row stride ldb
+  void* C;              // STORE / ROPE: [M, N]; SWIGLU: x13 [M, 2H]; DSWIGLU: d13 [M, 2H]   (row stride ldc)
+  void* C2;             // SWIGLU: h [M, H] (row stride ldc2)
+  const void* X;        // DSWIGLU: saved x13 = [gate | up] [M, 2H] (row stride ldx)
+  int M, N, K;          // SWIGLU / DSWIGLU: N = H
+  int H;                // SWIGLU / DSWIGLU: hidden size (column offset of the up half)
+  int64_t lda, ldb, ldc, ldc2, ldx;
+  // ROPE: columns < n_rot are rotated in interleaved pairs within heads of hd, position = row % S + pos_off
+  const float* rope_cos;
+  const float* rope_sin;
+  int S, hd, n_rot, pos_off;
+  int tiles_n;          // set by gemm_nt
+};
+bool gemm_nt_supported(int mode, int64_t M, int64_t N, int64_t K);
+void gemm_nt(int mode, const GemmNtParams& p, hipStream_t stream);
+
 // 1x1 convolution on channels-last activations as tall-skinny GEMMs (csrc/conv1x1.hip).  bf16 operands.
 // ts_gemm_nt: C[M, N] = A[M, K] B[N, K]^T (N, K % 64 == 0).  ts_gemm_tn: C[N, K] (+)= A[M, N]^T B[M, K] through
 // fp32 partials over nsplit pixel chunks (partial: nsplit * N * K floats; ts_gemm_tn_splits picks nsplit).

@@ -976,6 +976,124 @@ void car_destroy_op(int64_t ctx) { dph::car_destroy(ctx); }
 
 }  // namespace
 
+
+// ---- forward / input-gradient GEMM with fused epilogues (csrc/gemm_nt.hip) ----
+namespace {
+Tensor rows2d(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, ": bf16 required");
+  Tensor r = t.reshape({-1, t.size(-1)});
+  TORCH_CHECK(r.stride(1) == 1 && r.stride(0) % 8 == 0, name, ": rows must be contiguous with 16-B aligned starts");
+  check_align16(r, name);
+  return r;
+}
+dph::GemmNtParams nt_params(const Tensor& A, const Tensor& B) {
+  dph::GemmNtParams p{};
+  p.A = A.data_ptr();
+  p.B = B.data_ptr();
+  p.M = (int)A.size(0);
+  p.K = (int)A.size(1);
+  p.lda = A.stride(0);
+  p.ldb = B.stride(0);
+  return p;
+}
+std::vector<int64_t> out_sizes(const Tensor& x, int64_t n) {
+  auto s = x.sizes().vec();
+  s.back() = n;
+  return s;
+}
+}  // namespace
+
+// C = A B^T (A [..., K], B [N, K]) -> [..., N]
+Tensor gemm_nt(const Tensor& A, const Tensor& B) {
+  check_cuda(A, "A");
+  c10::DeviceGuard g(A.device());
+  const Tensor a = rows2d(A, "gemm_nt A"), b = rows2d(B, "gemm_nt B");
+  TORCH_CHECK(B.dim() == 2 && b.size(1) == a.size(1), "gemm_nt: B must be [N, K] with A's K");
+  TORCH_CHECK(dph::gemm_nt_supported(dph::kNtStore, a.size(0), b.size(0), a.size(1)),
+              "gemm_nt: need rows % 256, N % 256, K % 64 (got ", a.size(0), ", ", b.size(0), ", ", a.size(1), ")");
+  Tensor C = at::empty(out_sizes(A, b.size(0)), A.options());
+  auto p = nt_params(a, b);
+  p.N = (int)b.size(0);
+  p.C = C.data_ptr();
+  p.ldc = b.size(0);
+  dph::gemm_nt(dph::kNtStore, p, cur_stream());
+  return C;
+}
+
+// x13 = x [W1; W3]^T ([..., 2H]) and h = silu(x13[:, :H]) * x13[:, H:] ([..., H]) in one pass
+std::tuple<Tensor, Tensor> gemm_nt_swiglu(const Tensor& x, const Tensor& w13) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  const Tensor a = rows2d(x, "gemm_nt_swiglu x"), b = rows2d(w13, "gemm_nt_swiglu w13");
+  TORCH_CHECK(w13.dim() == 2 && b.size(1) == a.size(1) && b.size(0) % 2 == 0, "gemm_nt_swiglu: w13 [2H, K]");
+  const int64_t H = b.size(0) / 2;
+  TORCH_CHECK(dph::gemm_nt_supported(dph::kNtSwiglu, a.size(0), H, a.size(1)),
+              "gemm_nt_swiglu: need rows % 256, H % 128, K % 64 (got ", a.size(0), ", ", H, ", ", a.size(1), ")");
+  Tensor x13 = at::empty(out_sizes(x, 2 * H), x.options());
+  Tensor h = at::empty(out_sizes(x, H), x.options());
+  auto p = nt_params(a, b);
+  p.N = (int)H;
+  p.H = (int)H;
+  p.C = x13.data_ptr();
+  p.ldc = 2 * H;
+  p.C2 = h.data_ptr();
+  p.ldc2 = H;
+  dph::gemm_nt(dph::kNtSwiglu, p, cur_stream());
+  return {x13, h};
+}
+
+// d13 = SwiGLU-backward(dh = dy W2, x13): dy [..., K], w2t = W2^T [H, K], x13 [..., 2H] -> [..., 2H]
+Tensor gemm_nt_dswiglu(const Tensor& dy, const Tensor& w2t, const Tensor& x13) {
+  check_cuda(dy, "dy");
+  c10::DeviceGuard g(dy.device());
+  const Tensor a = rows2d(dy, "gemm_nt_dswiglu dy"), b = rows2d(w2t, "gemm_nt_dswiglu w2t");
+  const Tensor xr = rows2d(x13, "gemm_nt_dswiglu x13");
+  const int64_t H = b.size(0);
+  TORCH_CHECK(w2t.dim() == 2 && b.size(1) == a.size(1) && xr.size(0) == a.size(0) && xr.size(1) == 2 * H,
+              "gemm_nt_dswiglu: w2t [H, K], x13 [rows, 2H]");
+  TORCH_CHECK(dph::gemm_nt_supported(dph::kNtDswiglu, a.size(0), H, a.size(1)),
+              "gemm_nt_dswiglu: need rows % 256, H % 256, K % 64 (got ", a.size(0), ", ", H, ", ", a.size(1), ")");
+  Tensor d13 = at::empty(out_sizes(dy, 2 * H), dy.options());
+  auto p = nt_params(a, b);
+  p.N = (int)H;
+  p.H = (int)H;
+  p.C = d13.data_ptr();
+  p.ldc = 2 * H;
+  p.X = xr.data_ptr();
+  p.ldx = xr.stride(0);
+  dph::gemm_nt(dph::kNtDswiglu, p, cur_stream());
+  return d13;
+}
+
+// C = x W^T with interleaved RoPE on columns [0, n_rot) (heads of hd), position = row % S + pos_off
+Tensor gemm_nt_rope(const Tensor& x, const Tensor& w, const Tensor& cos_t, const Tensor& sin_t, int64_t S,
+                    int64_t hd, int64_t n_rot, int64_t pos_off) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  const Tensor a = rows2d(x, "gemm_nt_rope x"), b = rows2d(w, "gemm_nt_rope w");
+  TORCH_CHECK(w.dim() == 2 && b.size(1) == a.size(1), "gemm_nt_rope: w [N, K]");
+  TORCH_CHECK(cos_t.scalar_type() == at::kFloat && sin_t.scalar_type() == at::kFloat && cos_t.is_contiguous() &&
+                  sin_t.is_contiguous() && cos_t.size(-1) * 2 == hd && hd % 4 == 0,
+              "gemm_nt_rope: fp32 contiguous cos / sin tables [positions, hd / 2]");
+  TORCH_CHECK(n_rot % hd == 0 && n_rot <= b.size(0) && S > 0 && a.size(0) % S == 0 &&
+                  cos_t.size(0) >= S + pos_off, "gemm_nt_rope: bad rotary layout");
+  TORCH_CHECK(dph::gemm_nt_supported(dph::kNtRope, a.size(0), b.size(0), a.size(1)),
+              "gemm_nt_rope: need rows % 256, N % 256, K % 64");
+  Tensor C = at::empty(out_sizes(x, b.size(0)), x.options());
+  auto p = nt_params(a, b);
+  p.N = (int)b.size(0);
+  p.C = C.data_ptr();
+  p.ldc = b.size(0);
+  p.rope_cos = cos_t.data_ptr<float>();
+  p.rope_sin = sin_t.data_ptr<float>();
+  p.S = (int)S;
+  p.hd = (int)hd;
+  p.n_rot = (int)n_rot;
+  p.pos_off = (int)pos_off;
+  dph::gemm_nt(dph::kNtRope, p, cur_stream());
+  return C;
+}
+
 TORCH_LIBRARY(dph, m) {
   m.def("rmsnorm_fwd(Tensor x, Tensor w, float eps, Tensor? residual=None) -> (Tensor, Tensor, Tensor)");
   m.def("rmsnorm_bwd(Tensor dy, Tensor x, Tensor w, Tensor rstd, Tensor? dres=None) -> (Tensor, Tensor)");
@@ -1015,6 +1133,10 @@ TORCH_LIBRARY(dph, m) {
   m.def("embedding_fwd(Tensor ids, Tensor table, int vocab_start) -> Tensor");
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
+  m.def("gemm_nt(Tensor A, Tensor B) -> Tensor");
+  m.def("gemm_nt_swiglu(Tensor x, Tensor w13) -> (Tensor, Tensor)");
+  m.def("gemm_nt_dswiglu(Tensor dy, Tensor w2t, Tensor x13) -> Tensor");
+  m.def("gemm_nt_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int S, int hd, int n_rot, int pos_off) -> Tensor");
   m.def("gemm_tn_tail_(int cus) -> ()", &gemm_tn_tail_);                          // catch-all kernels
   m.def("gemm_tn_plan_info(int M, int N, int K) -> int[]", &gemm_tn_plan_info);
   m.def("gemm_tn_mfma_(int shape) -> int", &gemm_tn_mfma_);   // no tensor argument: catch-all kernel
@@ -1073,6 +1195,10 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("embedding_fwd", &embedding_fwd);
   m.impl("embedding_bwd", &embedding_bwd);
   m.impl("gemm_tn_", &gemm_tn_);
+  m.impl("gemm_nt", &gemm_nt);
+  m.impl("gemm_nt_swiglu", &gemm_nt_swiglu);
+  m.impl("gemm_nt_dswiglu", &gemm_nt_dswiglu);
+  m.impl("gemm_nt_rope", &gemm_nt_rope);
   m.impl("ts_gemm_nt", &ts_gemm_nt);
   m.impl("ts_gemm_nt_stats", &ts_gemm_nt_stats);
   m.impl("ts_gemm_tn_", &ts_gemm_tn_);

@@ -235,3 +235,24 @@ def _gemv_rmsnorm(x, res, norm_weight, eps, w):
 @register_fake("dph::car_allreduce")
 def _car_allreduce(ctx, inp, out, algo, scale, max_blocks):
     return None
+
+
+@register_fake("dph::gemm_nt")
+def _gemm_nt(A, B):
+    return A.new_empty((*A.shape[:-1], B.shape[0]))
+
+
+@register_fake("dph::gemm_nt_swiglu")
+def _gemm_nt_swiglu(x, w13):
+    H = w13.shape[0] // 2
+    return x.new_empty((*x.shape[:-1], 2 * H)), x.new_empty((*x.shape[:-1], H))
+
+
+@register_fake("dph::gemm_nt_dswiglu")
+def _gemm_nt_dswiglu(dy, w2t, x13):
+    return dy.new_empty((*dy.shape[:-1], 2 * w2t.shape[0]))
+
+
+@register_fake("dph::gemm_nt_rope")
+def _gemm_nt_rope(x, w, cos, sin, S, hd, n_rot, pos_off):
+    return x.new_empty((*x.shape[:-1], w.shape[0]))
