@@ -30,6 +30,7 @@ from torch import nn
 from .. import ops
 from ..ops import decode as decode_ops
 from ..ops.rope import precompute_rope_tables
+from ..parallel import fused_layers
 
 
 @dataclass
@@ -137,6 +138,13 @@ class Attention(nn.Module):
 
     def forward(self, x: torch.Tensor, pos_offset: int = 0, cache: Optional["KVCache"] = None,
                 layer: int = 0) -> torch.Tensor:
+        if cache is None and self.cp_attention is None and \
+                fused_layers.qkv_rope_attention_ok(x, self.wqkv, self.head_dim):
+            # projection + RoPE (in the GEMM epilogue) + flash attention as one autograd node (parallel/fused_layers)
+            cos, sin = rope_tables(self.head_dim, self.max_pos, self.theta, x.device)
+            o = fused_layers.qkv_rope_attention(x, self.wqkv, cos, sin, self.n_local_heads, self.n_local_kv_heads,
+                                                self.head_dim, pos_offset)
+            return _proj(self.wo, o)
         qkv = _proj(self.wqkv, x)
         cos, sin = rope_tables(self.head_dim, self.max_pos, self.theta, qkv.device)
         if cache is not None:
@@ -201,6 +209,9 @@ class FeedForward(nn.Module):
         nn.init.trunc_normal_(self.w2.weight, mean=0.0, std=init_std)
 
     def forward(self, x):
+        if fused_layers.swiglu_mlp_ok(x, self.w13, self.w2):
+            # SwiGLU in the w13 GEMM's epilogue, its backward in w2's input-gradient epilogue (parallel/fused_layers)
+            return fused_layers.swiglu_mlp(x, self.w13, self.w2)
         return _proj(self.w2, ops.swiglu(_proj(self.w13, x)))
 
 

@@ -1,0 +1,179 @@
+"""Fused Llama sub-blocks: the projection GEMMs carry the neighbouring element-wise work in their epilogues
+(csrc/gemm_nt.hip), forward and backward.
+
+* ``swiglu_mlp(x, w13, w2)`` -- the FeedForward ``w2(silu(w1 x) * w3 x)`` of fsdp_tp/llama2_model.py:262-267.
+  Forward: ONE kernel writes the saved gate / up projection AND h = silu(gate) * up (no swiglu_fwd pass), then
+  y = h W2^T.  Backward: the input gradient of w2 runs with the SwiGLU backward in its epilogue (dh never touches
+  HBM; no swiglu_bwd pass), then the w13 input / weight gradients.
+* ``qkv_rope_attention(x, wqkv, ...)`` -- the attention core of fsdp_tp/llama2_model.py:176-228 from the block input:
+  the wqkv projection applies RoPE to q / k on its fp32 accumulators (no rope pass, one rounding), flash attention
+  forward; backward = flash backward with the inverse rotation in its epilogues + the projection's gradients.
+
+Weight gradients take the same route as every other linear layer of the framework (parallel/linear.py:
+``weight_grad`` writes them straight into the data-parallel engine's bucket and notifies it), so the engines'
+overlapped reduce-scatter / all-reduce see no difference.  The fused paths are taken for plain (not tensor-parallel,
+not FP8) bf16 projections whose shapes the kernel tiles (rows % 256, features % 256, K % 64); everything else runs
+the unfused modules.  ``DPH_FUSED_MLP=0`` / ``DPH_FUSED_QKV=0`` turn them off (A/B runs).
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import torch
+
+from ..ops import _lib
+from ..ops import fp8 as _fp8
+from .linear import _dgrad, weight_grad
+
+_FUSED_MLP = os.environ.get("DPH_FUSED_MLP", "1") != "0"
+_FUSED_QKV = os.environ.get("DPH_FUSED_QKV", "1") != "0"
+# DPH_GEMM_NT: which forward / input-gradient GEMMs run on the CDNA4 kernel instead of hipBLASLt:
+# "fused" (default: only those with a fused epilogue), "all", or "0" (none -- also disables the fused paths)
+_GEMM_NT = os.environ.get("DPH_GEMM_NT", "fused")
+
+
+def set_enabled(mlp: bool | None = None, qkv: bool | None = None, gemm_nt: str | None = None):
+    """Toggle the fused paths at run time (tests / A/B runs); returns the previous (mlp, qkv, gemm_nt)."""
+    global _FUSED_MLP, _FUSED_QKV, _GEMM_NT
+    old = (_FUSED_MLP, _FUSED_QKV, _GEMM_NT)
+    if mlp is not None:
+        _FUSED_MLP = bool(mlp)
+    if qkv is not None:
+        _FUSED_QKV = bool(qkv)
+    if gemm_nt is not None:
+        _GEMM_NT = gemm_nt
+    return old
+
+
+def _plain_weight(mod) -> bool:
+    from torch import nn
+
+    return isinstance(mod, nn.Linear) and mod.bias is None and not getattr(mod.weight, "_dph_tp", False)
+
+
+def _native_bf16(*ts) -> bool:
+    return all(t.is_cuda and t.dtype == torch.bfloat16 for t in ts) and not _lib.reference_mode() and \
+        _lib.use_native(ts[0])
+
+
+def _rows_ok(t: torch.Tensor) -> bool:
+    return t.stride(-1) == 1 and t.is_contiguous() and t.data_ptr() % 16 == 0
+
+
+def nt_matmul(a2: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a2 [M, K] @ b[N, K]^T on the CDNA4 kernel when enabled for all GEMMs and tileable, else hipBLASLt."""
+    if _GEMM_NT == "all" and _native_bf16(a2, b) and a2.shape[0] % 256 == 0 and b.shape[0] % 256 == 0 and \
+            a2.shape[1] % 64 == 0 and _rows_ok(a2) and b.is_contiguous():
+        return _lib.ops().gemm_nt(a2, b)
+    return torch.matmul(a2, b.t())
+
+
+def _dgrad_nt(g2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dX = dY W for a [N, K] weight: the library path of parallel/linear.py, or the CDNA4 kernel on W^T."""
+    if _GEMM_NT == "all" and g2.shape[0] % 256 == 0 and w.shape[1] % 256 == 0 and w.shape[0] % 64 == 0:
+        return _lib.ops().gemm_nt(g2, _lib.ops().transpose2d(w))
+    return _dgrad(g2, w)
+
+
+# ---------------------------------------------------------------------------------------------- SwiGLU MLP
+class _SwiGLUMLPFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w13, w2):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        x13, h = _lib.ops().gemm_nt_swiglu(x2, w13)
+        y = nt_matmul(h, w2)
+        ctx.save_for_backward(x2, w13, x13, h, w2)
+        ctx.shape = shape
+        return y.view(*shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w13, x13, h, w2 = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        gx = gw13 = gw2 = None
+        # w2's input gradient with the SwiGLU backward fused: d13 = [dgate | dup] straight from dh's accumulators
+        w2t = _lib.ops().transpose2d(w2)
+        d13 = _lib.ops().gemm_nt_dswiglu(dy2, w2t, x13)
+        del w2t
+        if ctx.needs_input_grad[2]:
+            gw2 = weight_grad(w2, dy2, h)
+        if ctx.needs_input_grad[0]:
+            gx = _dgrad_nt(d13, w13).view(ctx.shape)
+        if ctx.needs_input_grad[1]:
+            gw13 = weight_grad(w13, d13, x2)
+        return gx, gw13, gw2
+
+
+def swiglu_mlp_ok(x: torch.Tensor, w13_mod, w2_mod) -> bool:
+    if not (_FUSED_MLP and _GEMM_NT != "0" and _plain_weight(w13_mod) and _plain_weight(w2_mod)):
+        return False
+    if _fp8.fp8_enabled() or not _native_bf16(x, w13_mod.weight, w2_mod.weight) or not _rows_ok(x):
+        return False
+    rows, k = x.numel() // x.shape[-1], x.shape[-1]
+    h2 = w13_mod.weight.shape[0]
+    return (rows % 256 == 0 and k % 64 == 0 and h2 % 512 == 0 and w2_mod.weight.shape[1] == h2 // 2
+            and w2_mod.weight.shape[0] % 256 == 0 and w13_mod.weight.is_contiguous() and w2_mod.weight.is_contiguous())
+
+
+def swiglu_mlp(x: torch.Tensor, w13_mod, w2_mod) -> torch.Tensor:
+    return _SwiGLUMLPFn.apply(x, w13_mod.weight, w2_mod.weight)
+
+
+# ---------------------------------------------------------------------------------------------- QKV + RoPE + attention
+class _QKVRopeAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wqkv, cos, sin, nh, nkv, hd, pos_offset):
+        b, s, k = x.shape
+        x2 = x.reshape(-1, k)
+        n_rot = (nh + nkv) * hd
+        qkv = _lib.ops().gemm_nt_rope(x2, wqkv, cos, sin, s, hd, n_rot, pos_offset).view(b, s, -1)
+        q = qkv[:, :, : nh * hd].view(b, s, nh, hd)
+        kk = qkv[:, :, nh * hd: n_rot].view(b, s, nkv, hd)
+        v = qkv[:, :, n_rot:].view(b, s, nkv, hd)
+        scale = 1.0 / math.sqrt(hd)
+        o, lse = _lib.ops().flash_attn_fwd(q, kk, v, scale, True, 0.0, 0)
+        ctx.save_for_backward(x2, wqkv, qkv, o, lse, cos, sin)
+        ctx.cfg = (nh, nkv, hd, scale, pos_offset, x.shape)
+        return o.view(b, s, nh * hd)
+
+    @staticmethod
+    def backward(ctx, do):
+        x2, wqkv, qkv, o, lse, cos, sin = ctx.saved_tensors
+        nh, nkv, hd, scale, pos_offset, xshape = ctx.cfg
+        b, s, _ = qkv.shape
+        n_rot = (nh + nkv) * hd
+        q = qkv[:, :, : nh * hd].view(b, s, nh, hd)
+        k = qkv[:, :, nh * hd: n_rot].view(b, s, nkv, hd)
+        v = qkv[:, :, n_rot:].view(b, s, nkv, hd)
+        dqkv = torch.empty_like(qkv)
+        dq = dqkv[:, :, : nh * hd].view(b, s, nh, hd)
+        dk = dqkv[:, :, nh * hd: n_rot].view(b, s, nkv, hd)
+        dv = dqkv[:, :, n_rot:].view(b, s, nkv, hd)
+        # dq / dk come out rotated back by -theta: the gradient w.r.t. the projection's (pre-RoPE) output
+        _lib.ops().flash_attn_bwd_into(do.reshape(b, s, nh, hd).contiguous(), q, k, v, o, lse, scale, True,
+                                       dq, dk, dv, 0.0, 0, cos, sin, pos_offset)
+        g2 = dqkv.view(b * s, -1)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = _dgrad_nt(g2, wqkv).view(xshape)
+        if ctx.needs_input_grad[1]:
+            gw = weight_grad(wqkv, g2, x2)
+        return gx, gw, None, None, None, None, None, None
+
+
+def qkv_rope_attention_ok(x: torch.Tensor, wqkv_mod, hd: int) -> bool:
+    if not (_FUSED_QKV and _GEMM_NT != "0" and _plain_weight(wqkv_mod)) or x.dim() != 3:
+        return False
+    if _fp8.fp8_enabled() or not _native_bf16(x, wqkv_mod.weight) or not _rows_ok(x):
+        return False
+    b, s, k = x.shape
+    n = wqkv_mod.weight.shape[0]
+    return ((b * s) % 256 == 0 and k % 64 == 0 and n % 256 == 0 and hd in (64, 128) and
+            wqkv_mod.weight.is_contiguous())
+
+
+def qkv_rope_attention(x, wqkv_mod, cos, sin, n_heads: int, n_kv_heads: int, head_dim: int,
+                       pos_offset: int = 0) -> torch.Tensor:
+    return _QKVRopeAttnFn.apply(x, wqkv_mod.weight, cos, sin, n_heads, n_kv_heads, head_dim, pos_offset)

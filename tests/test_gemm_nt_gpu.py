@@ -93,3 +93,42 @@ def test_gemm_nt_rope(dph_native, S, hd, heads):
         rot = torch.stack([a * c - b * s, a * s + b * c], -1).reshape(B * S, -1)
         ref = torch.cat([rot, ref[:, 2 * heads * hd:]], 1)
         assert rel_err(y, ref) < 5e-3, pos_off
+
+
+def _tiny_llama(seed):
+    from distributed_pytorch_hpc_amd.models.llama2 import ModelArgs, build_llama
+
+    # dim 256, FFN 768, 2 heads of 128: every projection tiles the NT kernel (rows 2 x 256, N % 256, K % 64)
+    args = ModelArgs(dim=256, n_layers=2, n_heads=2, vocab_size=512, multiple_of=256, max_seq_len=512)
+    return build_llama(args, device=DEV, dtype=torch.bfloat16, seed=seed)
+
+
+@pytest.mark.parametrize("which", ["mlp", "qkv", "both"])
+def test_llama_fused_blocks_match_unfused(dph_native, which):
+    """Loss and every parameter gradient of a Llama with the fused SwiGLU-MLP / QKV+RoPE+attention paths against
+    the same model through the unfused modules (library GEMMs + separate SwiGLU / RoPE kernels)."""
+    from distributed_pytorch_hpc_amd.parallel import fused_layers
+
+    g = torch.Generator(device=DEV).manual_seed(0)
+    t = torch.randint(0, 512, (2, 257), device=DEV, generator=g)
+    out = {}
+    for fused in (False, True):
+        old = fused_layers.set_enabled(mlp=fused and which != "qkv", qkv=fused and which != "mlp")
+        try:
+            m = _tiny_llama(3)
+            ff = m.layers[0].feed_forward
+            at = m.layers[0].attention
+            x = torch.randn(2, 256, 256, device=DEV, dtype=torch.bfloat16)
+            if fused and which != "qkv":
+                assert fused_layers.swiglu_mlp_ok(x, ff.w13, ff.w2)
+            if fused and which != "mlp":
+                assert fused_layers.qkv_rope_attention_ok(x, at.wqkv, at.head_dim)
+            loss = m(t[:, :-1], t[:, 1:])
+            loss.backward()
+            out[fused] = (loss.item(), {n: p.grad.float().clone() for n, p in m.named_parameters()})
+        finally:
+            fused_layers.set_enabled(*old)
+    (l0, g0), (l1, g1) = out[False], out[True]
+    assert abs(l0 - l1) < 1e-2 * abs(l0)
+    for n in g0:
+        assert rel_err(g1[n], g0[n]) < 3e-2, n
