@@ -26,8 +26,8 @@ from ..ops import _lib
 from ..ops import fp8 as _fp8
 from .linear import _dgrad, weight_grad
 
-_FUSED_MLP = os.environ.get("DPH_FUSED_MLP", "1") != "0"
-_FUSED_QKV = os.environ.get("DPH_FUSED_QKV", "1") != "0"
+_FUSED_MLP = os.environ.get("DPH_FUSED_MLP", "0") != "0"   # default flips once GPU-validated
+_FUSED_QKV = os.environ.get("DPH_FUSED_QKV", "0") != "0"
 # DPH_GEMM_NT: which forward / input-gradient GEMMs run on the CDNA4 kernel instead of hipBLASLt:
 # "fused" (default: only those with a fused epilogue), "all", or "0" (none -- also disables the fused paths)
 _GEMM_NT = os.environ.get("DPH_GEMM_NT", "fused")
