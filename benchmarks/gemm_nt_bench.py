@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--json", default=None)
     ap.add_argument("--shapes", default=",".join(list(FWD) + list(DGRAD)))
+    ap.add_argument("--variants", default="0,1", help="gemm_nt pipeline variants to A/B (csrc/gemm_nt.hip LOOK)")
+    ap.add_argument("--no-fused", action="store_true")
     a = ap.parse_args()
     _lib.require()
     ops = torch.ops.dph
@@ -50,20 +52,34 @@ def main():
         x = torch.randn(T, K, device="cuda").to(torch.bfloat16)
         w = (0.02 * torch.randn(N, K, device="cuda")).to(torch.bfloat16)
         flop = 2.0 * T * N * K
-        t = {"blaslt": [], "dph": []}
+        variants = [int(v) for v in a.variants.split(",")]
+        t = {"blaslt": [], **{f"dph_v{v}": [] for v in variants}}
+        ref = x.float() @ w.float().t()
+        errs = {}
+        for v in variants:
+            ops.gemm_nt_variant_(v)
+            errs[v] = ((ops.gemm_nt(x, w).float() - ref).norm() / ref.norm()).item()
+        del ref
         for _ in range(a.rounds):
             t["blaslt"].append(timeit(lambda: torch.matmul(x, w.t()), a.iters))
-            t["dph"].append(timeit(lambda: ops.gemm_nt(x, w), a.iters))
-        err = ((ops.gemm_nt(x, w).float() - (x.float() @ w.float().t())).norm()
-               / (x.float() @ w.float().t()).norm()).item()
+            for v in variants:
+                ops.gemm_nt_variant_(v)
+                t[f"dph_v{v}"].append(timeit(lambda: ops.gemm_nt(x, w), a.iters))
+        ops.gemm_nt_variant_(-1)
         row = {k: {"ms_min": min(v), "ms_med": sorted(v)[len(v) // 2], "tflops_max": flop / min(v) / 1e9}
                for k, v in t.items()}
-        row["relerr"] = err
+        row["relerr"] = errs
         res[name] = row
-        print(f"{name:14s} T={T} N={N:6d} K={K:6d}  blaslt {row['blaslt']['tflops_max']:7.1f} TF  "
-              f"dph {row['dph']['tflops_max']:7.1f} TF  ratio {row['dph']['tflops_max'] / row['blaslt']['tflops_max']:.3f}"
-              f"  relerr {err:.2e}", flush=True)
+        bl = row["blaslt"]["tflops_max"]
+        print(f"{name:14s} N={N:6d} K={K:6d}  blaslt {bl:7.1f} TF  " + "  ".join(
+            f"v{v} {row[f'dph_v{v}']['tflops_max']:7.1f} ({row[f'dph_v{v}']['tflops_max'] / bl:.3f})" for v in variants)
+            + f"  relerr {max(errs.values()):.2e}", flush=True)
         del x, w
+    if a.no_fused:
+        if a.json:
+            with open(a.json, "w") as fh:
+                json.dump(res, fh, indent=1)
+        return
     # fused epilogues vs library GEMM + separate kernel
     H, D = 11008, 4096
     x = torch.randn(T, D, device="cuda").to(torch.bfloat16)

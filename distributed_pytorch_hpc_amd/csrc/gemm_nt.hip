@@ -58,8 +58,13 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
 
 __device__ __forceinline__ float nt_sigmoid(float x) { return 1.f / (1.f + __expf(-x)); }
 
-template <int MODE>
+// LOOK = 1: phase 1 reads only the A0 fragments; the next K-tile's B0 fragments are read inside phase 4's MFMA
+// segment (interleaved with its MFMAs) into the B register set phase 4 does not use, so the four read segments
+// carry 8 / 4 / 8 / 0 ds_read_b128 instead of 12 / 4 / 8 / 0.  Reading in an MFMA segment needs the data retired one
+// phase earlier under the stagger, so three quarters stay in flight (vmcnt(6)) instead of four.
+template <int MODE, int LOOK>
 __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
+  constexpr int VMC = LOOK ? 6 : 8;
   __shared__ __attribute__((aligned(1024))) char lds[2 * BUFB];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 2, wn = wid & 3;
@@ -167,28 +172,47 @@ __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
   using IB1 = std::integral_constant<int, Q_B1>;
 
   // One phase P (0..3) of K-tile kt held in buffer CUR:
-  //   reads (covered by the previous phase's wait + barrier) -> one quarter of DMA -> vmcnt(8) -> barrier ->
-  //   16 MFMAs -> barrier.
+  //   reads (covered by the previous phase's wait + barrier) -> one quarter of DMA -> vmcnt -> barrier ->
+  //   16 MFMAs (LOOK: + the next tile's B0 reads in phase 4) -> barrier.
+  // B register sets: without LOOK fb0 = B0, fb1 = B1 always; with LOOK they swap roles every K-tile (B0 of tile t
+  // lives in fb0 for even t, fb1 for odd t), so the lookahead read of phase 4 lands in the set phase 4 leaves idle.
   auto phase = [&](auto PI, auto CI, int kt) {
     constexpr int P = decltype(PI)::value, CUR = decltype(CI)::value;
     using ICUR = std::integral_constant<int, CUR>;
     using INXT = std::integral_constant<int, CUR ^ 1>;
-    if constexpr (P == 0) { read_b(IB0{}, ICUR{}, fb0); read_a(IA0{}, ICUR{}); }
-    if constexpr (P == 1) read_b(IB1{}, ICUR{}, fb1);
+    constexpr bool SW = LOOK && CUR == 1;          // swapped B roles in odd tiles
+    auto& fB0 = SW ? fb1 : fb0;
+    auto& fB1 = SW ? fb0 : fb1;
+    if constexpr (P == 0) {
+      if constexpr (!LOOK) read_b(IB0{}, ICUR{}, fB0);
+      read_a(IA0{}, ICUR{});
+    }
+    if constexpr (P == 1) read_b(IB1{}, ICUR{}, fB1);
     if constexpr (P == 2) read_a(IA1{}, ICUR{});
     if constexpr (P == 0) dma(IB1{}, kt + 1, INXT{});
     if constexpr (P == 1) dma(IA1{}, kt + 1, INXT{});
     if constexpr (P == 2) dma(IA0{}, kt + 2, ICUR{});
     if constexpr (P == 3) dma(IB0{}, kt + 2, ICUR{});
-    wait_vmcnt<8>();
+    wait_vmcnt<VMC>();
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (P == 0) mma(I0{}, I0{}, fb0);
-    if constexpr (P == 1) mma(I0{}, I1{}, fb1);
-    if constexpr (P == 2) mma(I1{}, I1{}, fb1);
-    if constexpr (P == 3) mma(I1{}, I0{}, fb0);
+    if constexpr (P == 0) mma(I0{}, I0{}, fB0);
+    if constexpr (P == 1) mma(I0{}, I1{}, fB1);
+    if constexpr (P == 2) mma(I1{}, I1{}, fB1);
+    if constexpr (P == 3) {
+      mma(I1{}, I0{}, fB0);
+      if constexpr (LOOK) {   // next tile's B0 (retired by phase 3's wait) into the idle set, between the MFMAs
+        read_b(IB0{}, INXT{}, fB1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);   // 3 MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
@@ -202,9 +226,10 @@ __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
   dma(IA1{}, 0, I0{});
   dma(IA0{}, 1, I1{});
   dma(IB0{}, 1, I1{});
-  wait_vmcnt<8>();
+  wait_vmcnt<8>();   // Q_A0(0), Q_B0(0) landed
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
+  if constexpr (LOOK) read_b(IB0{}, I0{}, fb0);   // tile 0's B0 (phase 4 of tile -1 would have read it)
   // stagger: waves 4..7 run one barrier behind waves 0..3 (uniform per wave: wid is wave-uniform)
   const bool late = __builtin_amdgcn_readfirstlane(wid) >= 4;
   if (late) __builtin_amdgcn_s_barrier();
@@ -325,16 +350,37 @@ bool gemm_nt_supported(int mode, int64_t M, int64_t N, int64_t K) {
   return mode == kNtSwiglu ? N % 128 == 0 : N % NBN == 0;
 }
 
+namespace {
+int g_nt_variant = -1;   // -1: unresolved (env DPH_GEMM_NT_VARIANT, default kGemmNtDefaultVariant)
+}
+
+int gemm_nt_variant() {
+  if (g_nt_variant < 0) {
+    const char* e = getenv("DPH_GEMM_NT_VARIANT");
+    g_nt_variant = e ? (atoi(e) ? 1 : 0) : kGemmNtDefaultVariant;
+  }
+  return g_nt_variant;
+}
+
+void gemm_nt_set_variant(int v) { g_nt_variant = v < 0 ? -1 : (v ? 1 : 0); }
+
 void gemm_nt(int mode, const GemmNtParams& prm, hipStream_t st) {
   GemmNtParams p = prm;
   p.tiles_n = mode == kNtSwiglu ? p.N / 128 : p.N / NBN;
   const dim3 grid((unsigned)((p.M / NBM) * p.tiles_n)), block(NNT);
+  const bool look = gemm_nt_variant() == 1;
+#define DPH_NT_LAUNCH(MD)                                                                     \
+  do {                                                                                        \
+    if (look) hipLaunchKernelGGL((gemm_nt_k<MD, 1>), grid, block, 0, st, p);                 \
+    else hipLaunchKernelGGL((gemm_nt_k<MD, 0>), grid, block, 0, st, p);                      \
+  } while (0)
   switch (mode) {
-    case kNtSwiglu: hipLaunchKernelGGL(gemm_nt_k<kNtSwiglu>, grid, block, 0, st, p); break;
-    case kNtDswiglu: hipLaunchKernelGGL(gemm_nt_k<kNtDswiglu>, grid, block, 0, st, p); break;
-    case kNtRope: hipLaunchKernelGGL(gemm_nt_k<kNtRope>, grid, block, 0, st, p); break;
-    default: hipLaunchKernelGGL(gemm_nt_k<kNtStore>, grid, block, 0, st, p); break;
+    case kNtSwiglu: DPH_NT_LAUNCH(kNtSwiglu); break;
+    case kNtDswiglu: DPH_NT_LAUNCH(kNtDswiglu); break;
+    case kNtRope: DPH_NT_LAUNCH(kNtRope); break;
+    default: DPH_NT_LAUNCH(kNtStore); break;
   }
+#undef DPH_NT_LAUNCH
 }
 
 }  // namespace dph

@@ -137,6 +137,10 @@ struct GemmNtParams {
 };
 bool gemm_nt_supported(int mode, int64_t M, int64_t N, int64_t K);
 void gemm_nt(int mode, const GemmNtParams& p, hipStream_t stream);
+// pipeline variant of gemm_nt_k (0: 12/4/8/0 fragment reads per phase, 1: lookahead B0 reads, 8/4/8/0)
+constexpr int kGemmNtDefaultVariant = 0;
+int gemm_nt_variant();
+void gemm_nt_set_variant(int v);
 
 // 1x1 convolution on channels-last activations as tall-skinny GEMMs (csrc/conv1x1.hip).  bf16 operands.
 // ts_gemm_nt: C[M, N] = A[M, K] B[N, K]^T (N, K % 64 == 0).  ts_gemm_tn: C[N, K] (+)= A[M, N]^T B[M, K] through

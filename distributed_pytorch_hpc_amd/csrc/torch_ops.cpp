@@ -1003,6 +1003,12 @@ std::vector<int64_t> out_sizes(const Tensor& x, int64_t n) {
 }
 }  // namespace
 
+// select the gemm_nt pipeline variant (v < 0: back to the env / default); returns the active one
+int64_t gemm_nt_variant_(int64_t v) {
+  dph::gemm_nt_set_variant((int)v);
+  return dph::gemm_nt_variant();
+}
+
 // C = A B^T (A [..., K], B [N, K]) -> [..., N]
 Tensor gemm_nt(const Tensor& A, const Tensor& B) {
   check_cuda(A, "A");
@@ -1134,6 +1140,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
   m.def("gemm_nt(Tensor A, Tensor B) -> Tensor");
+  m.def("gemm_nt_variant_(int v) -> int", &gemm_nt_variant_);   // no tensor argument: catch-all kernel
   m.def("gemm_nt_swiglu(Tensor x, Tensor w13) -> (Tensor, Tensor)");
   m.def("gemm_nt_dswiglu(Tensor dy, Tensor w2t, Tensor x13) -> Tensor");
   m.def("gemm_nt_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int S, int hd, int n_rot, int pos_off) -> Tensor");
