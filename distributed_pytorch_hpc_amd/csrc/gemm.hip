@@ -14,8 +14,11 @@
 //     a half-wave's transposed read cover all 64 banks exactly once;
 //   * workgroups are remapped so each XCD (blockIdx % 8 under round-robin dispatch) owns a contiguous range of
 //     output tiles, grouped GROUP_M tiles tall, for L2 reuse of the shared A / B column panels.
-// Requirements (checked by the host op): M % 256 == 0, N % 256 == 0, K % 64 == 0, lda / ldb % 8 == 0,
-// 16-B aligned bases.  Other shapes use hipBLASLt.
+// Requirements (checked by the host op): M % 8 == 0, N % 8 == 0, K % 64 == 0, lda / ldb % 8 == 0, 16-B aligned
+// bases.  Ragged M / N (the tensor-parallel shards of Llama-2-7B: w13 2752 rows at tp=8, w2 1376 columns, the
+// vocab-sharded head 4000 rows) run as partial edge tiles: the LDS-DMA source column of a lane whose 16-B chunk lies
+// past the edge is clamped to the last valid chunk (finite data, never stored) and the epilogue masks rows / columns
+// beyond M / N.  Other shapes use hipBLASLt.
 #include <type_traits>
 
 #include "dph_common.h"
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, 
   const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
 
   // ---- XCD-aware, grouped tile order ----
-  const int tiles_m = M / GBM, tiles_n = N / GBN, nwg = tiles_m * tiles_n;
+  const int tiles_m = (M + GBM - 1) / GBM, tiles_n = (N + GBN - 1) / GBN, nwg = tiles_m * tiles_n;
   int tm, tn;
   grouped_tile(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
@@ -102,7 +105,9 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, 
   // ---- per-lane DMA source offsets: chunk tid of a 16-row region (row tid/32, swizzled slot) ----
   const int srow = threadIdx.x >> 5, lr = (threadIdx.x >> 4) & 1, sslot = threadIdx.x & 15;
   const int sch = (lr << 4) | (sslot ^ ((srow & 3) << 2));
-  const unsigned voffA = (unsigned)((srow * lda + sch * 8) * 2), voffB = (unsigned)((srow * ldb + sch * 8) * 2);
+  // edge tiles: a chunk past M / N re-reads the last valid chunk (its columns are never stored)
+  const int colA = min(sch * 8, M - 8 - m0), colB = min(sch * 8, N - 8 - n0);
+  const unsigned voffA = (unsigned)((srow * lda + colA) * 2), voffB = (unsigned)((srow * ldb + colB) * 2);
   const char* Ag = reinterpret_cast<const char*>(A + m0);        // uniform
   const char* Bg = reinterpret_cast<const char*>(B + n0);
   const int64_t stepA = 16 * lda * 2, stepB = 16 * ldb * 2;       // bytes per 16-row region
@@ -226,6 +231,7 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, 
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int row = m0 + wm * 128 + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (row >= M || col >= N) continue;
         OutT* p = C + (int64_t)row * ldc + col;
         float v = acc[mt][nt][i];
         if (ACCUM) v += (float)*p;
@@ -274,7 +280,7 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
   const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
 
   // ---- XCD-aware, grouped tile order (as gemm_tn_k) ----
-  const int tiles_m = M / GBM, tiles_n = N / GBN, nwg = tiles_m * tiles_n;
+  const int tiles_m = (M + GBM - 1) / GBM, tiles_n = (N + GBN - 1) / GBN, nwg = tiles_m * tiles_n;
   int tm, tn;
   grouped_tile(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
@@ -292,7 +298,9 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
   // ---- per-lane DMA source offsets: row tid/32 of the region, physical slot tid & 31 ----
   const int srow = threadIdx.x >> 5, lr = (threadIdx.x >> 4) & 1, sslot = threadIdx.x & 15;
   const int sch = (lr << 4) | (sslot ^ ((srow & 7) << 1));
-  const unsigned voffA = (unsigned)((srow * lda + sch * 8) * 2), voffB = (unsigned)((srow * ldb + sch * 8) * 2);
+  // edge tiles: a chunk past M / N re-reads the last valid chunk (its columns are never stored)
+  const int colA = min(sch * 8, M - 8 - m0), colB = min(sch * 8, N - 8 - n0);
+  const unsigned voffA = (unsigned)((srow * lda + colA) * 2), voffB = (unsigned)((srow * ldb + colB) * 2);
   const char* Ag = reinterpret_cast<const char*>(A + m0);        // uniform
   const char* Bg = reinterpret_cast<const char*>(B + n0);
   const int64_t stepA = 16 * lda * 2, stepB = 16 * ldb * 2;       // bytes per 16-row region
@@ -439,6 +447,7 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = m0 + wm * 128 + mb * 16 + 4 * g + i;
+        if (row >= M || col >= N) continue;
         OutT* p = C + (int64_t)row * ldc + col;
         float v = acc[mb][nb][i];
         if (ACCUM) v += (float)*p;
@@ -497,7 +506,7 @@ void gemm_tn_set_mfma(int shape) { g_gemm_tn_mfma = (shape == 16 || shape == 32)
 void gemm_tn_set_tail(int cus) { g_gemm_tn_tail = cus; }
 
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K) {
-  return M > 0 && N > 0 && K > 0 && M % GBM == 0 && N % GBN == 0 && K % GBK == 0;
+  return M >= 8 && N >= 8 && K > 0 && M % 8 == 0 && N % 8 == 0 && K % GBK == 0;
 }
 
 // Tail plan.  One 256 x 256 tile per workgroup and one workgroup per CU: T tiles run in ceil(T / CU) waves, and a
@@ -512,6 +521,7 @@ GemmTnPlan gemm_tn_plan(int64_t M, int64_t N, int64_t K) {
     return e && atoi(e) == 0;
   }();
   if (g_gemm_tn_tail < 0 || (env_off && g_gemm_tn_tail == 0) || gemm_tn_mfma() != 32) return pl;
+  if (M % GBM || N % GBN) return pl;   // ragged edge tiles: one launch
   const int cus = gemm_tn_cus();
   const int64_t tm = M / GBM, tn = N / GBN, T = tm * tn;
   if (T % cus == 0) return pl;
@@ -555,7 +565,7 @@ void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_
   const dim3 block(GNT);
   auto launch = [&](const bf16* a, const bf16* b, void* c, int64_t m, int64_t n, int64_t k, int64_t ldc_, int S,
                     bool f32_out, bool acc, int64_t cstride) {
-    const dim3 grid((unsigned)((m / GBM) * (n / GBN)), (unsigned)S);
+    const dim3 grid((unsigned)(((m + GBM - 1) / GBM) * ((n + GBN - 1) / GBN)), (unsigned)S);
 #define DPH_GEMM_LAUNCH(T, ACC)                                                                                \
   do {                                                                                                         \
     if (m16)                                                                                                   \

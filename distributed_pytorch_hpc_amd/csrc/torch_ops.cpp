@@ -587,7 +587,7 @@ void gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate) {
   TORCH_CHECK(B.size(0) == K && C.size(0) == M && C.size(1) == N, "gemm_tn: shape mismatch");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "gemm_tn: row-major operands required");
   TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0, "gemm_tn: leading dims must be multiples of 8");
-  TORCH_CHECK(dph::gemm_tn_supported(M, N, K), "gemm_tn: need M, N % 256 == 0 and K % 64 == 0 (got ", M, ", ", N,
+  TORCH_CHECK(dph::gemm_tn_supported(M, N, K), "gemm_tn: need M, N % 8 == 0 and K % 64 == 0 (got ", M, ", ", N,
               ", ", K, ")");
   check_align16(A, "A");
   check_align16(B, "B");

@@ -26,7 +26,10 @@ from ..ops import _lib
 from ..ops import fp8 as _fp8
 from .linear import _dgrad, weight_grad
 
-_FUSED_MLP = os.environ.get("DPH_FUSED_MLP", "0") != "0"   # default flips once GPU-validated
+# DPH_FUSED_MLP: "1" = SwiGLU in the w13 GEMM epilogue AND dSwiGLU in w2's input-gradient epilogue; "bwd" = only the
+# backward fusion (forward: library GEMM + swiglu_fwd); "0" = unfused modules
+_FUSED_MLP = os.environ.get("DPH_FUSED_MLP", "0")
+_FUSED_MLP = False if _FUSED_MLP == "0" else ("bwd" if _FUSED_MLP == "bwd" else True)
 _FUSED_QKV = os.environ.get("DPH_FUSED_QKV", "0") != "0"
 # DPH_GEMM_NT: which forward / input-gradient GEMMs run on the CDNA4 kernel instead of hipBLASLt:
 # "fused" (default: only those with a fused epilogue), "all", or "0" (none -- also disables the fused paths)
@@ -38,7 +41,7 @@ def set_enabled(mlp: bool | None = None, qkv: bool | None = None, gemm_nt: str |
     global _FUSED_MLP, _FUSED_QKV, _GEMM_NT
     old = (_FUSED_MLP, _FUSED_QKV, _GEMM_NT)
     if mlp is not None:
-        _FUSED_MLP = bool(mlp)
+        _FUSED_MLP = mlp if mlp == "bwd" else bool(mlp)
     if qkv is not None:
         _FUSED_QKV = bool(qkv)
     if gemm_nt is not None:
@@ -79,10 +82,14 @@ def _dgrad_nt(g2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 # ---------------------------------------------------------------------------------------------- SwiGLU MLP
 class _SwiGLUMLPFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w13, w2):
+    def forward(ctx, x, w13, w2, fused_fwd=True):
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
-        x13, h = _lib.ops().gemm_nt_swiglu(x2, w13)
+        if fused_fwd:
+            x13, h = _lib.ops().gemm_nt_swiglu(x2, w13)
+        else:
+            x13 = torch.matmul(x2, w13.t())
+            h = _lib.ops().swiglu_fwd(x13)
         y = nt_matmul(h, w2)
         ctx.save_for_backward(x2, w13, x13, h, w2)
         ctx.shape = shape
@@ -103,7 +110,7 @@ class _SwiGLUMLPFn(torch.autograd.Function):
             gx = _dgrad_nt(d13, w13).view(ctx.shape)
         if ctx.needs_input_grad[1]:
             gw13 = weight_grad(w13, d13, x2)
-        return gx, gw13, gw2
+        return gx, gw13, gw2, None
 
 
 def swiglu_mlp_ok(x: torch.Tensor, w13_mod, w2_mod) -> bool:
@@ -118,7 +125,7 @@ def swiglu_mlp_ok(x: torch.Tensor, w13_mod, w2_mod) -> bool:
 
 
 def swiglu_mlp(x: torch.Tensor, w13_mod, w2_mod) -> torch.Tensor:
-    return _SwiGLUMLPFn.apply(x, w13_mod.weight, w2_mod.weight)
+    return _SwiGLUMLPFn.apply(x, w13_mod.weight, w2_mod.weight, _FUSED_MLP is True)
 
 
 # ---------------------------------------------------------------------------------------------- QKV + RoPE + attention

@@ -53,7 +53,8 @@ def wgrad_stream(device: torch.device):
 
 def _native_wgrad(out: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor, accumulate: bool) -> bool:
     """out[N_out, N_in] (+)= g2^T x2 on the CDNA4 weight-gradient kernel (csrc/gemm.hip) when the shapes fit
-    its 256 x 256 x 64 tiling; False -> caller uses hipBLASLt."""
+    its tiling (M, N % 8 -- ragged tensor-parallel shards run as edge tiles -- and tokens % 64); False -> caller uses
+    hipBLASLt."""
     if not (g2.is_cuda and g2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16):
         return False
     from ..ops import _lib
@@ -62,7 +63,7 @@ def _native_wgrad(out: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor, accumul
         return False
     T, M = g2.shape
     N = x2.shape[1]
-    if M % 256 or N % 256 or T % 64 or T == 0:
+    if M % 8 or N % 8 or M < 8 or N < 8 or T % 64 or T == 0:
         return False
     if g2.stride(1) != 1 or x2.stride(1) != 1 or g2.stride(0) % 8 or x2.stride(0) % 8:
         return False

@@ -103,7 +103,7 @@ def _tiny_llama(seed):
     return build_llama(args, device=DEV, dtype=torch.bfloat16, seed=seed)
 
 
-@pytest.mark.parametrize("which", ["mlp", "qkv", "both"])
+@pytest.mark.parametrize("which", ["mlp", "mlp_bwd", "qkv", "both"])
 def test_llama_fused_blocks_match_unfused(dph_native, which):
     """Loss and every parameter gradient of a Llama with the fused SwiGLU-MLP / QKV+RoPE+attention paths against
     the same model through the unfused modules (library GEMMs + separate SwiGLU / RoPE kernels)."""
@@ -113,7 +113,8 @@ def test_llama_fused_blocks_match_unfused(dph_native, which):
     t = torch.randint(0, 512, (2, 257), device=DEV, generator=g)
     out = {}
     for fused in (False, True):
-        old = fused_layers.set_enabled(mlp=fused and which != "qkv", qkv=fused and which != "mlp")
+        mlp = ("bwd" if which == "mlp_bwd" else True) if fused and which != "qkv" else False
+        old = fused_layers.set_enabled(mlp=mlp, qkv=fused and which in ("qkv", "both"))
         try:
             m = _tiny_llama(3)
             ff = m.layers[0].feed_forward
@@ -121,7 +122,7 @@ def test_llama_fused_blocks_match_unfused(dph_native, which):
             x = torch.randn(2, 256, 256, device=DEV, dtype=torch.bfloat16)
             if fused and which != "qkv":
                 assert fused_layers.swiglu_mlp_ok(x, ff.w13, ff.w2)
-            if fused and which != "mlp":
+            if fused and which in ("qkv", "both"):
                 assert fused_layers.qkv_rope_attention_ok(x, at.wqkv, at.head_dim)
             loss = m(t[:, :-1], t[:, 1:])
             loss.backward()

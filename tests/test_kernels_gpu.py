@@ -345,6 +345,27 @@ def test_gemm_tn_tail_band(dph_native, M, N, dim, out_dtype, accumulate):
     assert rel_err(c, ref) < (1e-5 if out_dtype == torch.float32 else 8e-3)
 
 
+@pytest.mark.parametrize("K,M,N", [(256, 2752 // 4, 4096 // 8), (128, 264, 520), (192, 4000 // 10, 1376 // 4),
+                                   (64, 8, 256), (512, 1000, 24)])
+@pytest.mark.parametrize("mfma", [16, 32])
+def test_gemm_tn_wgrad_ragged_edge_tiles(dph_native, K, M, N, mfma):
+    """Tensor-parallel shard shapes (M, N % 8 but not % 256: w13 / w2 / vocab-head shards at tp=8) as partial edge
+    tiles: every in-bounds element matches the fp32 reference and nothing past the matrix edge is written."""
+    torch.ops.dph.gemm_tn_mfma_(mfma)
+    try:
+        torch.manual_seed(5)
+        a = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
+        b = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
+        big = torch.full((M + 8, N + 16), 7.0, device=DEV, dtype=torch.float32)   # guard rows / columns
+        c = big[:M, :N]
+        torch.ops.dph.gemm_tn_(c, a, b, False)
+    finally:
+        torch.ops.dph.gemm_tn_mfma_(0)
+    ref = a.float().t() @ b.float()
+    assert rel_err(c, ref) < 1e-5
+    assert (big[M:] == 7.0).all() and (big[:, N:] == 7.0).all()
+
+
 def test_gemm_tn_strided_operands(dph_native):
     """Operands that are column slices of wider activations (packed projections)."""
     torch.manual_seed(1)
