@@ -27,11 +27,14 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 
+CIFAR_STEM = True
+
+
 def make(arch, dev):
     from distributed_pytorch_hpc_amd.models import resnet
 
     torch.manual_seed(0)
-    return resnet(arch, num_classes=10, cifar_stem=True).to(dev).to(memory_format=torch.channels_last)
+    return resnet(arch, num_classes=10, cifar_stem=CIFAR_STEM).to(dev).to(memory_format=torch.channels_last)
 
 
 def run(arch, batches, graphed, interference, side, extra_env=None):
@@ -84,15 +87,19 @@ def main():
     ap.add_argument("--arch", default="resnet50")
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--image-size", type=int, default=32)
+    ap.add_argument("--imagenet-stem", action="store_true", help="7x7/2 stem + 3x3/2 max pool (224 px -> 56/28/14/7)")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
+    global CIFAR_STEM
+    CIFAR_STEM = not a.imagenet_stem
     from distributed_pytorch_hpc_amd.ops import _lib
 
     _lib.require()
     torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
     dev = torch.device("cuda")
     torch.manual_seed(3)
-    batches = [(torch.randn(a.batch, 3, 32, 32, device=dev, dtype=torch.bfloat16).contiguous(
+    batches = [(torch.randn(a.batch, 3, a.image_size, a.image_size, device=dev, dtype=torch.bfloat16).contiguous(
         memory_format=torch.channels_last), torch.randint(0, 10, (a.batch,), device=dev)) for _ in range(a.steps)]
     ref, ref_t = run(a.arch, batches, False, "none", False)
     ref2, ref2_t = run(a.arch, batches, False, "alloc", False)
