@@ -272,3 +272,37 @@ def test_trainer_cuda_graph(dph_native):
     assert tr._graphed is not None and tr._graphed.captured
     assert ddp.engine.step_count == 20
     assert tr.history[-1].loss < tr.history[0].loss
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("side,interference", [("side", "alloc"), ("side", "noalloc"), ("current", "alloc")])
+def test_graph_warmup_stream_and_interference_bitwise(dph_native, side, interference):
+    """Regression for the round-2 report (side-stream warm-up, unrelated GPU work between replays): under MIOpen's
+    deterministic algorithms every replayed ResNet-50 step (FSDP bf16, 14 x 14 layers: ImageNet stem at 224 px) must
+    produce the eager run's loss BITWISE, whichever stream warmed up and whatever ran between replays
+    (scripts/diag_graph_side_stream.py holds the full matrix)."""
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "diag_graph", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
+                                   "diag_graph_side_stream.py"))
+    d = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(d)
+    d.CIFAR_STEM = False
+    det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    old = os.environ.get("DPH_GRAPH_WARMUP_SIDE")
+    try:
+        torch.manual_seed(3)
+        batches = [(torch.randn(8, 3, 224, 224, device=DEV, dtype=torch.bfloat16).contiguous(
+            memory_format=torch.channels_last), torch.randint(0, 10, (8,), device=DEV)) for _ in range(6)]
+        ref, _ = d.run("resnet50", batches, False, "none", False)
+        got, _ = d.run("resnet50", batches, True, interference, side == "side")
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
+        if old is None:
+            os.environ.pop("DPH_GRAPH_WARMUP_SIDE", None)
+        else:
+            os.environ["DPH_GRAPH_WARMUP_SIDE"] = old
+    assert got == ref, (got, ref)
