@@ -23,11 +23,18 @@ next replay): consume or clone it before the next call.
 Multi-rank steps would capture their RCCL collectives into the graph too; that path is off unless
 ``allow_collectives=True`` (not exercised on the 1-GPU test box).
 
-Warm-up runs on the CURRENT stream, not on a side stream: with side-stream warm-up a captured ResNet-50 step
-diverged from its second replay on whenever other GPU work ran between replays (reproduced with the 14x14 1x1
-convolution kernels in the step; same-stream warm-up replays correctly, tests/test_graphs.py).
-``DPH_GRAPH_WARMUP_SIDE=1`` restores side-stream warm-up and ``DPH_GRAPH_SAFE_CONV=1`` routes convolutions to
-MIOpen inside graphed steps, both for investigation.
+Warm-up runs on the current stream by default; ``DPH_GRAPH_WARMUP_SIDE=1`` warms up on a side stream (the usual
+capture recipe).  Round 2 reported replayed ResNet-50 steps diverging with side-stream warm-up; round 3 re-examined
+it with ``scripts/diag_graph_side_stream.py`` under MIOpen's deterministic algorithms (two eager runs bitwise equal):
+side- and current-stream warm-up, with fresh allocations + writes, in-place writes, or host-synchronised work between
+replays, with and without the 1x1 convolution kernels, at 32 px and at 224 px (the 14 x 14 layers) -- every replayed
+loss equals the eager one bitwise (``profiles/r3/graph_side_stream_diag_*.json``).  The round-2 comparison ran under
+MIOpen's non-deterministic bf16 solvers, where two EAGER runs already differed by a relative update error of 2.1
+(``profiles/diag_nondeterminism_resnet*.log``), so its "divergence" had no bitwise baseline; the one blow-up recorded
+then (``gpu_tests_intermittent_resnet50_graph_fail.log``) happened with current-stream warm-up, i.e. it was not
+tied to the warm-up stream.  ``tests/test_graphs.py::test_graph_warmup_stream_and_interference_bitwise`` keeps both
+warm-up modes bitwise-checked against eager with unrelated GPU work between replays.  ``DPH_GRAPH_SAFE_CONV=1``
+routes convolutions to MIOpen inside graphed steps (investigation knob).
 """
 from __future__ import annotations
 
