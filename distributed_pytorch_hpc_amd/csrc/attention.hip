@@ -452,7 +452,34 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
 
   // ---- epilogue: O = O^T / l, lse ----
   lsum = half_sum(lsum);
-  if (myq < p.Sq) {
+  if (myq < p.Sq && p.acc_o) {
+    // ring merge into the fp32 accumulators (both half-waves read the old lse before half 0 writes the new one:
+    // one instruction stream, loads issued first)
+    const float inv = lsum > 0.f ? (DROP ? 1.f / (1.f - p.drop_p) : 1.f) / lsum : 0.f;
+    const float lse_b = lsum > 0.f ? (m + __log2f(lsum)) * 0.6931471805599453f : -INFINITY;
+    float* al = p.acc_lse + (int64_t)b * p.al_sb + (int64_t)hq * p.al_sh + myq;
+    const float old = *al;
+    const float mx = fmaxf(old, lse_b);
+    float w1 = 0.f, w2 = 0.f, nl = -INFINITY;
+    if (mx != -INFINITY) {
+      const float e1 = __expf(old - mx), e2 = __expf(lse_b - mx), sum = e1 + e2;
+      nl = mx + __logf(sum);
+      w1 = e1 / sum;
+      w2 = e2 / sum * inv;
+    }
+    float* ao = p.acc_o + (int64_t)b * p.ao_sb + (int64_t)myq * p.ao_ss + (int64_t)hq * p.ao_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        f32x4* ptr = reinterpret_cast<f32x4*>(ao + dt * 32 + 8 * gg + 4 * h);
+        f32x4 cur = *ptr;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cur[j] = cur[j] * w1 + o[dt][4 * gg + j] * w2;
+        *ptr = cur;
+      }
+    if (h == 0) *al = nl;
+  } else if (myq < p.Sq) {
     const float inv = lsum > 0.f ? (DROP ? 1.f / (1.f - p.drop_p) : 1.f) / lsum : 0.f;
     bf16* op = (bf16*)p.o + (int64_t)b * p.o_sb + (int64_t)myq * p.o_ss + (int64_t)hq * p.o_sh;
 #pragma unroll

@@ -75,6 +75,12 @@ struct AttnParams {
   // both backward kernels from a counter hash of (drop_seed, b * Hq + hq, query, key) -- see attn_keep().
   float drop_p;
   unsigned drop_seed;
+  // Optional ring-attention merge (context parallelism): fp32 running output acc_o [B, Sq, Hq, D] (strides ao_*) and
+  // natural-log log-sum-exp acc_lse [B, Hq, Sq] (strides al_*, unit stride along the sequence).  When acc_o is set
+  // the kernel folds its normalised block result into them with the online-softmax merge in its epilogue
+  // (lse' = logaddexp(lse, lse_b), acc' = acc e^(lse - lse') + o_b e^(lse_b - lse')) instead of writing o / lse.
+  float* acc_o; int64_t ao_sb, ao_ss, ao_sh;
+  float* acc_lse; int64_t al_sb, al_sh;
 };
 void flash_attn_fwd(const AttnParams& p, hipStream_t stream);
 

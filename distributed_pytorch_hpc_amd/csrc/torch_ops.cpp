@@ -330,6 +330,33 @@ void flash_attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, c
   dph::flash_attn_bwd(P, cur_stream());
 }
 
+// Ring-attention step: attention of q against this K/V block, merged in the kernel's epilogue into the fp32 running
+// output acc_o [B, Sq, Hq, D] and log-sum-exp acc_lse [B, Hq, Sq] (views allowed: unit stride along D / the sequence).
+void flash_attn_fwd_merge_(const Tensor& q, const Tensor& k, const Tensor& v, double scale, bool causal, Tensor acc_o,
+                           Tensor acc_lse) {
+  c10::DeviceGuard g(q.device());
+  check_attn_operand(q, "q"); check_attn_operand(k, "k"); check_attn_operand(v, "v");
+  const int64_t D = q.size(3);
+  TORCH_CHECK(D == 32 || D == 64 || D == 128, "flash_attn_fwd_merge_: head_dim must be 32, 64 or 128");
+  TORCH_CHECK(k.size(3) == D && v.size(3) == D && k.sizes() == v.sizes(), "flash_attn_fwd_merge_: k/v mismatch");
+  TORCH_CHECK(acc_o.scalar_type() == at::kFloat && acc_o.dim() == 4 && acc_o.sizes() == q.sizes() &&
+                  acc_o.stride(3) == 1 && acc_o.device() == q.device(),
+              "flash_attn_fwd_merge_: acc_o must be fp32 [B, Sq, Hq, D] with unit stride along D");
+  TORCH_CHECK(acc_o.stride(0) % 4 == 0 && acc_o.stride(1) % 4 == 0 && acc_o.stride(2) % 4 == 0 &&
+                  reinterpret_cast<uintptr_t>(acc_o.data_ptr()) % 16 == 0,
+              "flash_attn_fwd_merge_: acc_o rows must be 16-B aligned");
+  TORCH_CHECK(acc_lse.scalar_type() == at::kFloat && acc_lse.dim() == 3 && acc_lse.size(0) == q.size(0) &&
+                  acc_lse.size(1) == q.size(2) && acc_lse.size(2) == q.size(1) && acc_lse.stride(2) == 1,
+              "flash_attn_fwd_merge_: acc_lse must be fp32 [B, Hq, Sq] with unit stride along the sequence");
+  auto p = make_params(q, k, v, acc_o, Tensor(), scale, causal);
+  p.o = nullptr;
+  p.acc_o = acc_o.data_ptr<float>();
+  p.ao_sb = acc_o.stride(0); p.ao_ss = acc_o.stride(1); p.ao_sh = acc_o.stride(2);
+  p.acc_lse = acc_lse.data_ptr<float>();
+  p.al_sb = acc_lse.stride(0); p.al_sh = acc_lse.stride(1);
+  dph::flash_attn_fwd(p, cur_stream());
+}
+
 std::tuple<Tensor, Tensor, Tensor> flash_attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k,
                                                   const Tensor& v, const Tensor& o, const Tensor& lse, double scale,
                                                   bool causal, double dropout_p, int64_t seed) {
@@ -1121,6 +1148,8 @@ TORCH_LIBRARY(dph, m) {
         "float smoothing) -> (Tensor, Tensor)");
   m.def("flash_attn_fwd(Tensor q, Tensor k, Tensor v, float scale, bool causal, float dropout_p=0., int seed=0) "
         "-> (Tensor, Tensor)");
+  m.def("flash_attn_fwd_merge_(Tensor q, Tensor k, Tensor v, float scale, bool causal, Tensor(a!) acc_o, "
+        "Tensor(b!) acc_lse) -> ()");
   m.def("flash_attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, bool causal, "
         "float dropout_p=0., int seed=0) -> (Tensor, Tensor, Tensor)");
   m.def("flash_attn_bwd_into(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, float scale, "
@@ -1191,6 +1220,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("cross_entropy_fwd", &cross_entropy_fwd);
   m.impl("image_augment", &image_augment);
   m.impl("flash_attn_fwd", &flash_attn_fwd);
+  m.impl("flash_attn_fwd_merge_", &flash_attn_fwd_merge_);
   m.impl("flash_attn_bwd", &flash_attn_bwd);
   m.impl("flash_attn_bwd_into", &flash_attn_bwd_into);
   m.impl("fp8_quantize", &fp8_quantize);

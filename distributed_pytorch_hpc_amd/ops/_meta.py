@@ -256,3 +256,8 @@ def _gemm_nt_dswiglu(dy, w2t, x13):
 @register_fake("dph::gemm_nt_rope")
 def _gemm_nt_rope(x, w, cos, sin, S, hd, n_rot, pos_off):
     return x.new_empty((*x.shape[:-1], w.shape[0]))
+
+
+@register_fake("dph::flash_attn_fwd_merge_")
+def _flash_attn_fwd_merge(q, k, v, scale, causal, acc_o, acc_lse):
+    return None

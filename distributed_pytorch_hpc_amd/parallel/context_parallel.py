@@ -27,6 +27,7 @@ each chunk's global positions.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.distributed as dist
@@ -120,6 +121,12 @@ def _attn_bwd(do, q, k, v, o, lse, causal, scale):
     return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype)
 
 
+def _fused_merge_ok(q) -> bool:
+    """The flash forward can merge into the ring accumulators in its epilogue (bf16 CUDA operands, native head dim)."""
+    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (32, 64, 128) and _lib.use_native(q)
+            and os.environ.get("DPH_RING_FUSED_MERGE", "1") != "0")
+
+
 def _merge(o, lse, o2, lse2):
     """Online-softmax merge of two partial attentions (fp32 accumulators)."""
     new = torch.logaddexp(lse, lse2)
@@ -156,7 +163,16 @@ class _RingAttnFn(torch.autograd.Function):
         o = torch.zeros(q.shape, dtype=torch.float32, device=q.device)
         lse = torch.full((q.shape[0], q.shape[2], q.shape[1]), float("-inf"), dtype=torch.float32, device=q.device)
 
-        def accumulate(rows, ob, lb):
+        fused = _fused_merge_ok(q)
+
+        def accumulate(rows, qb, kb, vb, blk_causal):
+            """Fold attention(q[rows], kb, vb) into (o, lse)[rows]: in the flash kernel's epilogue on the GPU (the
+            running fp32 output and lse are read-modify-written once per step, no separate merge pass), else the
+            eager online-softmax merge."""
+            if fused:
+                _lib.ops().flash_attn_fwd_merge_(qb, kb, vb, scale, blk_causal, o[:, rows], lse[:, :, rows])
+                return
+            ob, lb = _attn_fwd_lse(qb, kb, vb, blk_causal, scale)
             o_r, l_r = o[:, rows], lse[:, :, rows]
             new_o, new_l = _merge(o_r, l_r, ob, lb)
             o[:, rows], lse[:, :, rows] = new_o, new_l
@@ -169,16 +185,16 @@ class _RingAttnFn(torch.autograd.Function):
                 works, bufs = ring.start([kc, vc])
             allq = slice(0, q.shape[1])
             if not causal:
-                accumulate(allq, *_attn_fwd_lse(q, kc, vc, False, scale))
+                accumulate(allq, q, kc, vc, False)
             elif not zigzag:
                 if j <= r:
-                    accumulate(allq, *_attn_fwd_lse(q, kc, vc, j == r, scale))
+                    accumulate(allq, q, kc, vc, j == r)
             elif j == r:
-                accumulate(allq, *_attn_fwd_lse(q, kc, vc, True, scale))
+                accumulate(allq, q, kc, vc, True)
             elif j < r:
-                accumulate(allq, *_attn_fwd_lse(q, kc[:, :c], vc[:, :c], False, scale))
+                accumulate(allq, q, kc[:, :c], vc[:, :c], False)
             else:
-                accumulate(slice(c, 2 * c), *_attn_fwd_lse(q[:, c:], kc, vc, False, scale))
+                accumulate(slice(c, 2 * c), q[:, c:], kc, vc, False)
             if works is not None:
                 for w in works:
                     w.wait()
