@@ -180,15 +180,67 @@ def split_along_dim(x, dim, group):
 
 # ------------------------------------------------------------------------------------------- all-to-all
 def _a2a(x: torch.Tensor, scatter_dim: int, gather_dim: int, group) -> torch.Tensor:
-    """Split ``x`` into world chunks along scatter_dim, exchange, concatenate along gather_dim."""
+    """Split ``x`` into world chunks along scatter_dim, exchange, concatenate along gather_dim.
+
+    Two copies in all: the input is laid out once with the rank as the leading dimension (the exchange buffer of
+    all_to_all_single) and the output once into the gathered layout -- no per-chunk copies, stack or cat."""
     ws = _ws(group)
     if ws == 1:
         return x
-    chunks = [c.contiguous() for c in x.chunk(ws, dim=scatter_dim)]
-    inp = torch.stack(chunks, 0).contiguous()
+    n = x.shape[scatter_dim]
+    assert n % ws == 0, f"all_to_all: dim {scatter_dim} ({n}) not divisible by the group size {ws}"
+    inp = x.unflatten(scatter_dim, (ws, n // ws)).movedim(scatter_dim, 0).contiguous()
     out = torch.empty_like(inp)
     dist.all_to_all_single(out, inp, group=group)
-    return torch.cat(out.unbind(0), dim=gather_dim)
+    return out.movedim(0, gather_dim).flatten(gather_dim, gather_dim + 1)
+
+
+def _pack_heads(qkv: torch.Tensor, nh: int, nkv: int, hd: int, ws: int) -> torch.Tensor:
+    """[B, s, (nh + 2 nkv) hd] -> exchange buffer [P, B, s, (nh + 2 nkv) / P * hd]: rank j's slot holds ITS q / k / v
+    head groups, packed [q_j | k_j | v_j] (one copy)."""
+    b, s, _ = qkv.shape
+    q = qkv[..., : nh * hd].view(b, s, ws, nh // ws * hd)
+    k = qkv[..., nh * hd: (nh + nkv) * hd].view(b, s, ws, nkv // ws * hd)
+    v = qkv[..., (nh + nkv) * hd:].view(b, s, ws, nkv // ws * hd)
+    return torch.cat([q, k, v], -1).movedim(2, 0).contiguous()
+
+
+def _unpack_heads(buf: torch.Tensor, nh: int, nkv: int, hd: int, ws: int) -> torch.Tensor:
+    """Inverse of ``_pack_heads``: [P, B, s, packed_j] -> [B, s, (nh + 2 nkv) hd]."""
+    t = buf.movedim(0, 2)                                        # [B, s, P, packed]
+    q, k, v = t.split([nh // ws * hd, nkv // ws * hd, nkv // ws * hd], -1)
+    return torch.cat([q.flatten(2), k.flatten(2), v.flatten(2)], -1)
+
+
+class _UlyssesQKV(torch.autograd.Function):
+    """Sequence-sharded packed qkv [B, S/P, (nh + 2 nkv) hd] -> head-sharded, full-sequence packed qkv
+    [B, S, (nh + 2 nkv) / P * hd] in ONE all-to-all (instead of one per q / k / v plus a concatenation)."""
+
+    @staticmethod
+    def forward(ctx, qkv, nh, nkv, hd, group):
+        ws = _ws(group)
+        ctx.cfg = (nh, nkv, hd, group)
+        inp = _pack_heads(qkv, nh, nkv, hd, ws)
+        out = torch.empty_like(inp)
+        dist.all_to_all_single(out, inp, group=group)
+        return out.movedim(0, 1).flatten(1, 2)                   # [B, P * s, packed]
+
+    @staticmethod
+    def backward(ctx, g):
+        nh, nkv, hd, group = ctx.cfg
+        ws = _ws(group)
+        b, S, packed = g.shape
+        inp = g.reshape(b, ws, S // ws, packed).movedim(1, 0).contiguous()
+        out = torch.empty_like(inp)
+        dist.all_to_all_single(out, inp, group=group)
+        return _unpack_heads(out, nh, nkv, hd, ws), None, None, None, None
+
+
+def ulysses_qkv(qkv: torch.Tensor, nh: int, nkv: int, hd: int, group) -> torch.Tensor:
+    if _ws(group) == 1:
+        return qkv
+    assert nh % _ws(group) == 0 and nkv % _ws(group) == 0, "Ulysses needs head counts divisible by the group size"
+    return _UlyssesQKV.apply(qkv, nh, nkv, hd, group)
 
 
 class _AllToAll(torch.autograd.Function):

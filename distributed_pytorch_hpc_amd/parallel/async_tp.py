@@ -38,17 +38,21 @@ def _chunks_for(seq_local: int, chunks: int) -> int:
     return k
 
 
-def _ag_async(x: torch.Tensor, group):
-    """all-gather of a contiguous [B, m, D] micro-chunk -> ([P, B, m, D] buffer, work)."""
+def _ag_async(x: torch.Tensor, group, out: torch.Tensor | None = None):
+    """all-gather of a contiguous [B, m, D] micro-chunk -> ([P, B, m, D] buffer, work); ``out`` (contiguous
+    [P * B, m, D]) lets the caller gather straight into a slot of a larger buffer."""
     P = _ws(group)
-    out = torch.empty((P * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)   # dim-0 concatenation
+    if out is None:
+        out = torch.empty((P * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)   # dim-0 concatenation
     work = dist.all_gather_into_tensor(out, x, group=group, async_op=True)
     return out.view(P, *x.shape), work
 
 
-def _rs_async(x: torch.Tensor, group):
-    """reduce-scatter of a contiguous [P, B, m, D] partial -> ([B, m, D] buffer, work)."""
-    out = torch.empty(x.shape[1:], dtype=x.dtype, device=x.device)
+def _rs_async(x: torch.Tensor, group, out: torch.Tensor | None = None):
+    """reduce-scatter of a contiguous [P, B, m, D] partial -> ([B, m, D] buffer, work); ``out`` may be a contiguous
+    slot of the caller's output (no concatenation afterwards)."""
+    if out is None:
+        out = torch.empty(x.shape[1:], dtype=x.dtype, device=x.device)
     inp = x.reshape(x.shape[0] * x.shape[1], *x.shape[2:])                              # dim-0 concatenation
     return out, dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group, async_op=True)
 
@@ -66,30 +70,42 @@ def _seq_major(t: torch.Tensor) -> torch.Tensor:
 
 
 def _ag_matmul(x: torch.Tensor, w: torch.Tensor, group, k: int, transpose_w: bool):
-    """AG(x) @ op(w) with k pipelined micro all-gathers; x [B, Sl, D].  Returns (y [B, S, N], gathered [k,P,B,m,D])."""
+    """AG(x) @ op(w) with k pipelined micro all-gathers; x [B, Sl, D].  Returns (y [B, S, N], gathered [k,P,B,m,D]).
+
+    The micro all-gathers land in slots of ONE chunk-major buffer (kept for the weight gradient: no stack), and each
+    micro-GEMM's [P, B, m, N] result is copied once into its rank-major sequence positions of y (one copy, overlapping
+    the next micro all-gather; no stack + permute)."""
     B, Sl, D = x.shape
+    P = _ws(group)
     m = Sl // k
-    pend = [_ag_async(x[:, i * m:(i + 1) * m].contiguous(), group) for i in range(k)]
-    ys = []
-    for g, work in pend:
+    xg = torch.empty((k, P * B, m, D), dtype=x.dtype, device=x.device)
+    pend = [_ag_async(x[:, i * m:(i + 1) * m].contiguous(), group, xg[i]) for i in range(k)]
+    N = w.shape[0] if transpose_w else w.shape[1]
+    y = torch.empty((B, P * Sl, N), dtype=x.dtype, device=x.device)
+    yv = y.view(B, P, k, m, N)
+    for i, (g, work) in enumerate(pend):
         work.wait()
-        ys.append(torch.matmul(g, w.t()) if transpose_w else _dgrad(g, w))
-    y = _seq_major(torch.stack(ys, 0))
-    return y, torch.stack([g for g, _ in pend], 0)
+        yi = torch.matmul(g, w.t()) if transpose_w else _dgrad(g, w)         # [P, B, m, N]
+        yv[:, :, i].copy_(yi.permute(1, 0, 2, 3))
+    return y, xg.view(k, P, B, m, D)
 
 
 def _matmul_rs(x_cm: torch.Tensor, w: torch.Tensor, group, transpose_w: bool) -> torch.Tensor:
     """RS(x @ op(w)) with the GEMM of micro-chunk i+1 overlapping the reduce-scatter of i; x_cm [k, P, B, m, F]
-    chunk-major.  Returns [B, Sl, N] (this rank's sequence shard)."""
+    chunk-major.  Returns [B, Sl, N] (this rank's sequence shard); with one sequence per rank (B = 1) the micro
+    reduce-scatters write straight into their slice of it."""
+    k, _, B, m, _ = x_cm.shape
+    N = w.shape[0] if transpose_w else w.shape[1]
+    y = torch.empty((B, k * m, N), dtype=x_cm.dtype, device=x_cm.device) if B == 1 else None
     pend = []
-    for i in range(x_cm.shape[0]):
+    for i in range(k):
         part = torch.matmul(x_cm[i], w.t()) if transpose_w else _dgrad(x_cm[i], w)
-        pend.append(_rs_async(part, group))
+        pend.append(_rs_async(part, group, y[:, i * m:(i + 1) * m] if y is not None else None))
     outs = []
     for o, work in pend:
         work.wait()
         outs.append(o)
-    return torch.cat(outs, 1)
+    return y if y is not None else torch.cat(outs, 1)
 
 
 class _AGMatmulFn(torch.autograd.Function):

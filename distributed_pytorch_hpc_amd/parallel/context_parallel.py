@@ -63,13 +63,10 @@ class UlyssesAttention:
         p = _ws(self.group)
         assert nh % p == 0 and nkv % p == 0, f"Ulysses needs heads ({nh}, kv {nkv}) divisible by cp={p}"
         b, s_loc, _ = qkv.shape
-        q, k, v = _split_qkv(qkv, nh, nkv, hd)
-        # [B, S/P, H, D] -> [B, S, H/P, D]
-        q = cf.all_to_all(q, 2, 1, self.group)
-        k = cf.all_to_all(k, 2, 1, self.group)
-        v = cf.all_to_all(v, 2, 1, self.group)
-        s = q.shape[1]
-        packed = torch.cat([q.reshape(b, s, -1), k.reshape(b, s, -1), v.reshape(b, s, -1)], dim=-1)
+        # [B, S/P, (H + 2 Hkv) hd] -> [B, S, (H + 2 Hkv) / P * hd]: one all-to-all for q, k and v together, landing
+        # directly in the packed layout the fused RoPE + attention kernel reads (comm/functional.py ulysses_qkv)
+        packed = cf.ulysses_qkv(qkv.contiguous(), nh, nkv, hd, self.group)
+        s = packed.shape[1]
         o = ops.rope_attention(packed, cos, sin, nh // p, nkv // p, hd, causal=self.causal)
         o = o.view(b, s, nh // p, hd)
         o = cf.all_to_all(o, 1, 2, self.group)    # back to [B, S/P, H, D]

@@ -23,14 +23,14 @@ def _batches(global_b=4, s=16):
     return [torch.randint(0, PRESET["vocab_size"], (global_b, s + 1), generator=g) for _ in range(STEPS)]
 
 
-def _reference():
+def _reference(global_b=4):
     from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig
 
     m = _model()
     eng = DataParallelEngine(m, shard=False)
     eng.configure_optimizer(OptimConfig(lr=1e-2, weight_decay=0.1))
     losses = []
-    for t in _batches():
+    for t in _batches(global_b):
         loss = m(t[:, :-1], t[:, 1:])
         loss.backward()
         eng.step()
@@ -82,7 +82,7 @@ def test_fsdp_sharded_optimizer_matches_single_process():
         _check(ref, o)
 
 
-def _tp_worker(rank, world, dp, sp, loss_parallel, async_tp=0):
+def _tp_worker(rank, world, dp, sp, loss_parallel, async_tp=0, global_b=4):
     from distributed_pytorch_hpc_amd.comm.mesh import DeviceMesh2D
     from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig
     from distributed_pytorch_hpc_amd.parallel.tensor_parallel import parallelize_llama
@@ -93,7 +93,7 @@ def _tp_worker(rank, world, dp, sp, loss_parallel, async_tp=0):
     eng = DataParallelEngine(m, process_group=mesh.dp_group, shard=dp > 1, bucket_cap_mb=0.02)
     eng.configure_optimizer(OptimConfig(lr=1e-2, weight_decay=0.1))
     losses = []
-    for t in _batches():
+    for t in _batches(global_b):
         local = t.chunk(dp, 0)[mesh.dp_rank]
         loss = m(local[:, :-1], local[:, 1:])
         loss.backward()
@@ -158,3 +158,10 @@ def test_async_tp_tp4_uneven_chunks_matches_single_process():
     ref = _reference()
     outs = run_distributed(_tp_worker, 4, 1, True, True, 3)
     _check_tp(ref, outs, 4)
+
+
+def test_async_tp_single_sequence_matches_single_process():
+    """One sequence per rank: the micro reduce-scatters land directly in their output slices (parallel/async_tp.py)."""
+    ref = _reference(global_b=1)
+    outs = run_distributed(_tp_worker, 2, 1, True, True, 2, 1)
+    _check_tp(ref, outs, 2)
