@@ -19,9 +19,11 @@ Before anything is timed, a run with N > 1 (runtime/preflight.py):
   * after the warm-up, checks that the flat parameters of every replica agree bitwise (exit code 4 if not).
 
 Other BASELINE.json configs run under the same contract with --layout (train/bench_layouts.py):
-tp (Llama-2 7B TP=N + SP), hybrid (FSDP(N/4) x TP(4)), pp (PP 4 x DDP N/4, 1F1B), resnet-fsdp (ResNet-50 FSDP bf16).
+tp (Llama-2 7B TP=N + SP), hybrid (FSDP(N/4) x TP(4)), pp (PP 4 x DDP N/4, 1F1B), resnet-fsdp (ResNet-50 FSDP bf16),
+unet-ddp (SimpleUNet DDP on ERA5-shaped 65 x 181 x 360 fields, B = 4 per GPU).  Every line also carries the median
+and spread of rank 0's per-step device times ("step_ms", CUDA events between consecutive timed steps).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--layout dp|tp|hybrid|pp|resnet-fsdp]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--layout dp|tp|hybrid|pp|resnet-fsdp|unet-ddp]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 """
@@ -50,6 +52,8 @@ def parse(argv=None):
     ap.add_argument("--arch", default="resnet50", help="resnet-fsdp layout: ResNet depth")
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--image-size", type=int, default=224)
+    ap.add_argument("--unet-precision", choices=["bf16", "fp32"], default="bf16",
+                    help="unet-ddp layout: bf16 autocast over fp32 weights, or the reference's fp32")
     ap.add_argument("--micro-batch", type=int, default=None,
                     help="sequences (images) per GPU / per dp replica per step; default 8 (dp, tp, hybrid), 16 (pp), "
                          "256 (resnet-fsdp).  8 x 4096 tokens: ~249 GB peak on one 288 GB MI355X")
@@ -87,8 +91,23 @@ def parse(argv=None):
     if args.model is None:
         args.model = "llama2-7b"
     if args.micro_batch is None:
-        args.micro_batch = {"pp": 16, "resnet-fsdp": 256}.get(args.layout, 8)
+        args.micro_batch = {"pp": 16, "resnet-fsdp": 256, "unet-ddp": 4}.get(args.layout, 8)
     return args
+
+
+def _spread(v):
+    """Median and spread of rank 0's per-step times (device events between consecutive steps)."""
+    if not v:
+        return None
+    s = sorted(v)
+
+    def q(f):
+        return s[min(len(s) - 1, max(0, round(f * (len(s) - 1))))]
+
+    mean = sum(s) / len(s)
+    sd = (sum((x - mean) ** 2 for x in s) / max(len(s) - 1, 1)) ** 0.5
+    return {"median": round(q(0.5), 3), "p10": round(q(0.1), 3), "p90": round(q(0.9), 3), "min": round(s[0], 3),
+            "max": round(s[-1], 3), "mean": round(mean, 3), "stdev": round(sd, 3), "n": len(s)}
 
 
 def _fail(code: int, msg: str):
@@ -163,12 +182,24 @@ def main(argv=None):
             _fail(4, f"rank {rank}: {e}")
         sync_all()
 
+    # per-step device-time marks: events recorded between steps (no host synchronisation inside the timed region)
+    marks = [] if cpu else [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    host_marks = []
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if marks:
+            marks[i].record()
+        else:
+            host_marks.append(time.perf_counter())
         loss = wl.step(args.warmup + i)
+    if marks:
+        marks[-1].record()
     wl.engine.synchronize()
+    host_marks.append(time.perf_counter())
     sync_all()
     elapsed = time.perf_counter() - t0
+    step_ms = ([marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)] if marks else
+               [1000.0 * (host_marks[i + 1] - host_marks[i]) for i in range(args.steps)])
     last_loss = float(loss.detach()) if loss is not None else None
     if dist.is_initialized():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -195,6 +226,7 @@ def main(argv=None):
             "data": "synthetic (random tokens / images, random-init weights)",
             "config": {**wl.config, "layout": args.layout},
             f"{wl.unit.split('/')[0]}_per_sec_per_gpu": round(rate / world, 2),
+            "step_ms": _spread(step_ms),
             "peak_hbm_gb": round(peak_gb, 2),
             "loss_first_warmup": round(first_loss, 4) if first_loss is not None else None,
             "loss_last": round(last_loss, 4) if last_loss is not None else None,

@@ -191,6 +191,14 @@ void maxpool_s2_fwd(const void* x, void* y, uint8_t* tap, int64_t N, int64_t H, 
 void maxpool_s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C, int k,
                     int dtype, hipStream_t stream);
 
+// SimpleUNet up-path, csrc/upsample.hip.  y: the ConvTranspose2d(2, 2) GEMM output [N*H*W, 4*Co] (columns (i, j, co));
+// skip / out / dcat / dskip channels-last.  out[n, oh, ow, :] = [bilinear(pixel_shuffle(y) + bias)(oh, ow), skip].
+// Co, Cs % 8 == 0; bias fp32 or null.
+void upcat_fwd(const void* y, const float* bias, const void* skip, void* out, int64_t N, int64_t H, int64_t W,
+               int64_t Co, int64_t Ho, int64_t Wo, int64_t Cs, int dtype, hipStream_t stream);
+void upcat_bwd(const void* dcat, void* dy, void* dskip, int64_t N, int64_t H, int64_t W, int64_t Co, int64_t Ho,
+               int64_t Wo, int64_t Cs, int dtype, hipStream_t stream);
+
 // out[c] = sum_m x[m, c] over a row-major [M, C] (channels-last) tensor, csrc/chsum.hip: fp32 partials
 // part[chsum_partial_blocks(M, C) * C], out in out_dtype (fp32 / bf16).  Deterministic.
 int chsum_partial_blocks(int64_t M, int64_t C);

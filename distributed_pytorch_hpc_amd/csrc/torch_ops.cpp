@@ -773,6 +773,53 @@ Tensor maxpool_s2_bwd(const Tensor& dy, const Tensor& tap, int64_t H, int64_t W,
   return dx;
 }
 
+// ------------------------------------------------------------------------------------------------ UNet up-path
+// y2: [N*H*W, 4*Co] ConvTranspose2d(2, 2) GEMM output; skip: channels-last [N, Cs, Ho, Wo].
+// Returns channels-last [N, Co + Cs, Ho, Wo] = cat([bilinear(pixel_shuffle(y2) + bias, (Ho, Wo)), skip]).
+Tensor upcat_fwd(const Tensor& y2, const c10::optional<Tensor>& bias, const Tensor& skip, int64_t H, int64_t W) {
+  check_cuda(y2, "y2");
+  check_cuda(skip, "skip");
+  c10::DeviceGuard g(y2.device());
+  TORCH_CHECK(skip.dim() == 4 && skip.is_contiguous(at::MemoryFormat::ChannelsLast), "upcat: channels-last skip");
+  TORCH_CHECK(y2.dim() == 2 && y2.is_contiguous() && y2.scalar_type() == skip.scalar_type(),
+              "upcat: contiguous [N*H*W, 4*Co] GEMM output of the skip's dtype");
+  const int64_t N = skip.size(0), Cs = skip.size(1), Ho = skip.size(2), Wo = skip.size(3);
+  TORCH_CHECK(H > 0 && W > 0 && y2.size(0) == N * H * W && y2.size(1) % 32 == 0, "upcat: y2 must be [N*H*W, 4*Co]");
+  const int64_t Co = y2.size(1) / 4;
+  TORCH_CHECK(Co % 8 == 0 && Cs % 8 == 0, "upcat: channel counts must be multiples of 8");
+  TORCH_CHECK(Ho > 0 && Wo > 0 && Ho <= 4 * H && Wo <= 4 * W && 4 * Ho >= 2 * H && 4 * Wo >= 2 * W,
+              "upcat: resize ratio outside [0.5, 2]");
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == Co &&
+                    bias->device() == y2.device(),
+                "upcat: fp32 bias [Co]");
+    bp = bias->data_ptr<float>();
+  }
+  check_align16(y2, "y2");
+  check_align16(skip, "skip");
+  auto out = at::empty({N, Co + Cs, Ho, Wo}, skip.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dph::upcat_fwd(y2.data_ptr(), bp, skip.data_ptr(), out.data_ptr(), N, H, W, Co, Ho, Wo, Cs, dt_code(skip),
+                 cur_stream());
+  return out;
+}
+
+// dcat: channels-last [N, Co + Cs, Ho, Wo]; returns (dy2 [N*H*W, 4*Co], dskip channels-last [N, Cs, Ho, Wo])
+std::tuple<Tensor, Tensor> upcat_bwd(const Tensor& dcat, int64_t H, int64_t W, int64_t Co) {
+  check_cuda(dcat, "dcat");
+  c10::DeviceGuard g(dcat.device());
+  TORCH_CHECK(dcat.dim() == 4 && dcat.is_contiguous(at::MemoryFormat::ChannelsLast), "upcat_bwd: channels-last dcat");
+  const int64_t N = dcat.size(0), Ct = dcat.size(1), Ho = dcat.size(2), Wo = dcat.size(3), Cs = Ct - Co;
+  TORCH_CHECK(Co > 0 && Co % 8 == 0 && Cs >= 0 && Cs % 8 == 0 && H > 0 && W > 0, "upcat_bwd: bad channel split");
+  TORCH_CHECK(Ho <= 4 * H && Wo <= 4 * W && 4 * Ho >= 2 * H && 4 * Wo >= 2 * W, "upcat_bwd: resize ratio outside [0.5, 2]");
+  check_align16(dcat, "dcat");
+  auto dy = at::empty({N * H * W, 4 * Co}, dcat.options());
+  auto dskip = at::empty({N, Cs, Ho, Wo}, dcat.options().memory_format(at::MemoryFormat::ChannelsLast));
+  dph::upcat_bwd(dcat.data_ptr(), dy.data_ptr(), dskip.data_ptr(), N, H, W, Co, Ho, Wo, Cs, dt_code(dcat),
+                 cur_stream());
+  return {dy, dskip};
+}
+
 // ------------------------------------------------------------------------------------------------ transpose
 Tensor transpose2d(const Tensor& x) {
   check_cuda(x, "x");
@@ -1183,6 +1230,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
   m.def("maxpool_s2_bwd(Tensor dy, Tensor tap, int H, int W, int k) -> Tensor");
+  m.def("upcat_fwd(Tensor y2, Tensor? bias, Tensor skip, int H, int W) -> Tensor");
+  m.def("upcat_bwd(Tensor dcat, int H, int W, int Co) -> (Tensor, Tensor)");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
         "float momentum, float eps, bool relu, Tensor? pre_stats=None, Tensor(c!)? num_batches_tracked=None, "
         "Tensor(d!)? relu_mask_out=None) "
@@ -1243,6 +1292,8 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("maxpool_s2_fwd", &maxpool_s2_fwd);
   m.impl("channel_sum", &channel_sum);
   m.impl("maxpool_s2_bwd", &maxpool_s2_bwd);
+  m.impl("upcat_fwd", &upcat_fwd);
+  m.impl("upcat_bwd", &upcat_bwd);
   m.impl("bn_act_fwd", &bn_act_fwd);
   m.impl("bn_act_apply", &bn_act_apply);
   m.impl("bn_act_bwd", &bn_act_bwd);

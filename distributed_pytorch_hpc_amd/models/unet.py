@@ -4,18 +4,19 @@ scripts/01_data_parallel_ddp/multinode_ddp_unet.py:171-214; 7,742,849 parameters
 Same modules and names (enc1..3, bottleneck, up1..3, dec1..3, out, pool).  Convolutions run through MIOpen in
 channels-last (NHWC) layout when the model is moved to the GPU with ``to_channels_last`` -- the MI355X-native
 layout for implicit-GEMM convolutions; the odd 181-latitude grid is handled like the reference (bilinear
-resize of each up-sampled map to its skip connection size).  ``halo`` (domain parallelism, parallel/domain.py)
+resize of each up-sampled map to its skip connection size), with transposed convolution + resize + concat run as one
+GEMM and one copy kernel per decoder level (ops/upsample.py, csrc/upsample.hip).  ``halo`` (domain parallelism, parallel/domain.py)
 swaps the 3x3 convolutions for halo-exchanging ones when the latitude axis is sharded across ranks.
 """
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv import BiasConv2d, BiasConvTranspose2d
 from ..ops.pool import MaxPool2d
+from ..ops.upsample import up_concat
 
 
 def conv_block(in_ch: int, out_ch: int) -> nn.Sequential:
@@ -44,19 +45,15 @@ class SimpleUNet(nn.Module):
         self.out = BiasConv2d(b, out_channels, kernel_size=1)
         self.pool = MaxPool2d(2)   # channels-last HIP kernels (ops/pool.py)
 
-    @staticmethod
-    def _up(x, size):
-        return x if tuple(x.shape[2:]) == tuple(size) else F.interpolate(x, size=size, mode="bilinear",
-                                                                          align_corners=False)
-
     def forward(self, x):
         e1 = self.enc1(x)
         e2 = self.enc2(self.pool(e1))
         e3 = self.enc3(self.pool(e2))
         bt = self.bottleneck(self.pool(e3))
-        d3 = self.dec3(torch.cat([self._up(self.up3(bt), e3.shape[2:]), e3], dim=1))
-        d2 = self.dec2(torch.cat([self._up(self.up2(d3), e2.shape[2:]), e2], dim=1))
-        d1 = self.dec1(torch.cat([self._up(self.up1(d2), e1.shape[2:]), e1], dim=1))
+        # up-sample + resize + concat: one GEMM and one copy kernel per level on the GPU (ops/upsample.py)
+        d3 = self.dec3(up_concat(self.up3, bt, e3))
+        d2 = self.dec2(up_concat(self.up2, d3, e2))
+        d1 = self.dec1(up_concat(self.up1, d2, e1))
         return self.out(d1)
 
 

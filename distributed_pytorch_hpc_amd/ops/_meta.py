@@ -118,6 +118,19 @@ def _maxpool_s2_bwd(dy, tap, H, W, k):
     return dy.new_empty((n, c, H, W)).contiguous(memory_format=torch.channels_last)
 
 
+@register_fake("dph::upcat_fwd")
+def _upcat_fwd(y2, bias, skip, H, W):
+    n, cs, ho, wo = skip.shape
+    return skip.new_empty((n, y2.shape[1] // 4 + cs, ho, wo)).contiguous(memory_format=torch.channels_last)
+
+
+@register_fake("dph::upcat_bwd")
+def _upcat_bwd(dcat, H, W, Co):
+    n, ct, ho, wo = dcat.shape
+    return (dcat.new_empty((n * H * W, 4 * Co)),
+            dcat.new_empty((n, ct - Co, ho, wo)).contiguous(memory_format=torch.channels_last))
+
+
 @register_fake("dph::channel_sum")
 def _channel_sum(x, out_dtype):
     return x.new_empty((x.shape[1],), dtype=out_dtype)

@@ -9,6 +9,7 @@ JSON line from rank 0).
 | ``hybrid``    | Llama-2 7B hybrid FSDP(2) x TP(4) via DeviceMesh                      | fsdp_tp/fsdp_tp_example.py:103-187   |
 | ``pp``        | Llama-2 7B PP 4 stages x DDP 2 (send/recv micro-batch pipeline)       | scripts/04_pipeline_parallel_pp/03   |
 | ``resnet-fsdp`` | ResNet-50 FSDP bf16 on 8 x MI355X                                   | scripts/main.py + resnet_fsdp_training.py |
+| ``unet-ddp``  | SimpleUNet DDP, ERA5 65 x 181 x 360, B = 4 per GPU (samples/s)        | scripts/01_data_parallel_ddp/multinode_ddp_unet.py |
 
 Each builder returns a ``Workload``: the step function, the engine to synchronise, the group whose ranks hold
 replicas of the same flat parameters (checked bitwise after warm-up), the work per step and the JSON ``config``.
@@ -22,7 +23,7 @@ import torch
 import torch.distributed as dist
 
 BASELINE_METRIC = "tokens/sec + DDP/FSDP scaling efficiency, Llama-2-7B at 1/2/4/8 MI355X"
-LAYOUTS = ("dp", "tp", "hybrid", "pp", "resnet-fsdp")
+LAYOUTS = ("dp", "tp", "hybrid", "pp", "resnet-fsdp", "unet-ddp")
 
 
 @dataclass
@@ -283,4 +284,51 @@ def build_resnet_fsdp(args, rank, world, dev, log) -> Workload:
                     extra={"replica_check": "n/a (FULL_SHARD: no replicated parameters)"})
 
 
-BUILDERS = {"dp": build_dp, "tp": build_tp, "hybrid": build_hybrid, "pp": build_pp, "resnet-fsdp": build_resnet_fsdp}
+def build_unet_ddp(args, rank, world, dev, log) -> Workload:
+    """SimpleUNet data-parallel training on ERA5-shaped fields (scripts/01_data_parallel_ddp/multinode_ddp_unet.py:
+    B = 4 per GPU, AdamW lr 1e-4 wd 1e-5, latitude-weighted MSE, 65 channels on the 181 x 360 grid).  MI355X path:
+    channels-last activations, bf16 autocast over fp32 master weights (``--unet-precision fp32`` = the reference's
+    fp32), DDP engine with one gradient bucket all-reduced during backward."""
+    from ..models.unet import SimpleUNet, to_channels_last
+    from ..ops.loss import latitude_weighted_mse
+    from ..parallel.data_parallel import DDP
+
+    cpu = dev.type == "cpu"
+    C = 65 if not cpu else 5
+    lat, lon = (181, 360) if not cpu else (19, 36)
+    base = 64 if not cpu else 8
+    torch.backends.cudnn.benchmark = not cpu
+    torch.manual_seed(1234)
+    model = to_channels_last(SimpleUNet(C, C, base).to(dev))
+    n_params = sum(p.numel() for p in model.parameters())
+    grad_bytes = n_params * 4
+    bucket_mb, binfo = _bucket(args, world, grad_bytes, False, None, dev, log)
+    ddp = DDP(model, bucket_cap_mb=bucket_mb)
+    opt = ddp.make_optimizer("adamw", lr=1e-4, weight_decay=1e-5)
+    B = args.micro_batch
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    x = torch.randn(B, C, lat, lon, device=dev, generator=g).contiguous(memory_format=torch.channels_last)
+    y = (x + 0.1 * torch.randn(B, C, lat, lon, device=dev, generator=g)).contiguous(memory_format=torch.channels_last)
+    amp = (not cpu) and args.unet_precision == "bf16"
+
+    def step(i):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            out = ddp(x)
+        loss = latitude_weighted_mse(out.float() if out.dtype != torch.float32 else out, y)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        return loss
+
+    cfg = {"model": "SimpleUNet (7,742,849 params)" if not cpu else f"SimpleUNet-mini ({n_params} params)",
+           "global_batch": world * B, "grid": f"{C} x {lat} x {lon}", "parallelism": f"ddp{world}",
+           "micro_batch_per_gpu": B, "precision": "bf16 autocast, fp32 master weights" if amp else "fp32",
+           "channels_last": True, "optimizer": "AdamW lr 1e-4 wd 1e-5 (multinode_ddp_unet.py:316)",
+           "loss": "latitude-weighted MSE", "bucket_mb": round(bucket_mb, 1)}
+    return Workload(step, ddp.engine, "samples/sec, SimpleUNet DDP ERA5 65x181x360", "samples/s", world * B,
+                    "weak", cfg, replica_group=None, replica_flat=ddp.engine.flat_param, extra=binfo)
+
+
+BUILDERS = {"dp": build_dp, "tp": build_tp, "hybrid": build_hybrid, "pp": build_pp, "resnet-fsdp": build_resnet_fsdp,
+            "unet-ddp": build_unet_ddp}

@@ -112,6 +112,21 @@ def test_bench_resnet_fsdp_layout(tmp_path):
     assert r["preflight_ok"] is True and r["images_per_sec_per_gpu"] > 0
 
 
+def test_bench_unet_ddp_layout(tmp_path):
+    """SimpleUNet DDP under the contract (CPU: a narrow UNet on a 19 x 36 grid); per-step spread reported."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2",
+           "--layout", "unet-ddp", "--device", "cpu", "--steps", "4", "--warmup", "1", "--quiet"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = _lines(p.stdout)[0]
+    assert r["unit"] == "samples/s" and r["config"]["parallelism"] == "ddp2" and r["config"]["global_batch"] == 8
+    assert r["preflight_ok"] is True and r["param_checksum_ok"] is True
+    st = r["step_ms"]
+    assert st["n"] == 4 and st["min"] <= st["median"] <= st["max"] and st["p10"] <= st["p90"]
+
+
 # ---- pre-flight failure injection: a corrupted collective / diverged replica must abort, not publish ----
 def _selftest_corrupt_worker(rank, world, which):
     import torch.distributed as dist
