@@ -18,11 +18,15 @@ runs the three-op reference sequence.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
+
+_ENABLED = os.environ.get("DPH_FUSED_UPCAT", "1") != "0"    # A/B knob: 0 = the reference three-op sequence
 
 
 def _pair(v):
@@ -36,6 +40,8 @@ def _compute_dtype(x: torch.Tensor) -> torch.dtype:
 
 
 def up_concat_native_ok(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> bool:
+    if not _ENABLED:
+        return False
     if not (isinstance(up, nn.ConvTranspose2d) and _pair(up.kernel_size) == (2, 2) and _pair(up.stride) == (2, 2)
             and _pair(up.padding) == (0, 0) and _pair(up.output_padding) == (0, 0) and _pair(up.dilation) == (1, 1)
             and up.groups == 1):
