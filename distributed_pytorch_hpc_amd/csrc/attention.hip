@@ -531,9 +531,13 @@ __global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ o, 
 // of the GQA group x 32-row query tiles (double-buffered Q / dO LDS images, one barrier per tile).
 // S and dP are computed with the key on the lane, so P and dS are directly the B operands of
 // dV^T += dO^T P and dK^T += Q^T dS: no LDS round trip, no atomics.
-template <int HD, bool CAUSAL, int NW, bool DROP = false>
+// VAR (A/B knob, DPH_ATTN_BWD_VAR): bit 0 = row constants as the initial S / dP accumulators (no dropout), bit 1 =
+// the dV / dK transposed reads software-pipelined one step ahead, the first step issued before the softmax.
+template <int HD, bool CAUSAL, int NW, bool DROP = false, int VAR = 0>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams P) {
   constexpr int NT = 64 * NW, BNK = 32 * NW, BMQ = 32, NC = HD / 8, KS = HD / 16, DT = HD / 32;
+  constexpr bool RINIT = !DROP && (VAR & 1);
+  constexpr bool TRPIPE = (VAR & 2) != 0;
   constexpr int QIMG = BMQ * HD * 2;        // Q / dO tile image [32 q][HD]
   constexpr int KIMG = BNK * HD * 2;        // K image [128 keys][HD] (B operand of S = Q K^T)
   // img_off's line permutation repeats every 16 lines.  For NC >= 8, rows r and r + 32 are a multiple of 16
@@ -629,12 +633,32 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
       if constexpr (DROP) st_rk = attn_row_key(p.drop_seed, (unsigned)(b * p.Hq + hq), (unsigned)(qt0 + threadIdx.x));
     }
   };
+  // Row constants: without dropout they become the INITIAL accumulators of the S and dP chains (S' = Q K^T - lse/scale,
+  // dP' = dO V^T - delta), so p = exp2(S' scale log2e) and dS = p dP' need no per-element row reads after the chains
+  // (cdna_hip_programming.md 'Row constants as the initial accumulator'); dropout keeps the explicit form.
+  const float inv_scale = 1.f / p.scale;
   auto stage_scalars = [&](int buf) {
     if (threadIdx.x < BMQ) {
-      lse_s[buf * BMQ + threadIdx.x] = -st_lse * 1.4426950408889634f;  // -lse in log2 units
-      del_s[buf * BMQ + threadIdx.x] = st_del;
-      if constexpr (DROP) rk_s[buf * BMQ + threadIdx.x] = st_rk;
+      if constexpr (!RINIT) {
+        lse_s[buf * BMQ + threadIdx.x] = -st_lse * 1.4426950408889634f;  // -lse in log2 units
+        del_s[buf * BMQ + threadIdx.x] = st_del;
+        if constexpr (DROP) rk_s[buf * BMQ + threadIdx.x] = st_rk;
+      } else {
+        lse_s[buf * BMQ + threadIdx.x] = -st_lse * inv_scale;
+        del_s[buf * BMQ + threadIdx.x] = -st_del;
+      }
     }
+  };
+  // accumulator register r holds query row acc_row(r, h) = (r & 3) + 8 (r >> 2) + 4 h: four 16-B row reads
+  auto row_init = [&](const float* rows) {
+    f32x16 a;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(rows + 8 * j + 4 * h);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[4 * j + i] = v[i];
+    }
+    return a;
   };
 
   if (total > 0) {
@@ -652,8 +676,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
     const char* Ol = Ql + QIMG;
     // a wave whose 32 keys are all hidden from this query tile by the causal mask skips the tile
     if (!(CAUSAL && key0 > qt0 + BMQ - 1 + off)) {
-      f32x16 s = mfma32(lds_b128(Ql, qro[0]), lds_b128(Kimg, kofs(0)), zacc);
-      f32x16 dp = mfma32(lds_b128(Ol, qro[0]), vf[0], zacc);
+      const float* ls = lse_s + buf * BMQ;
+      const float* ds = del_s + buf * BMQ;
+      f32x16 s = mfma32(lds_b128(Ql, qro[0]), lds_b128(Kimg, kofs(0)), RINIT ? row_init(ls) : zacc);
+      f32x16 dp = mfma32(lds_b128(Ol, qro[0]), vf[0], RINIT ? row_init(ds) : zacc);
 #pragma unroll
       for (int kk = 1; kk < KS; ++kk) {
         s = mfma32(lds_b128(Ql, qro[kk]), lds_b128(Kimg, kofs(kk)), s);
@@ -667,17 +693,28 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
           s[r] = (q >= p.Sq || mykey >= p.Sk || (CAUSAL && mykey > q + off)) ? -INFINITY : s[r];
         }
       }
-      const float* ls = lse_s + buf * BMQ;
-      const float* ds = del_s + buf * BMQ;
+      // TRPIPE: the first dV / dK step's transposed operands are read now, their latency covered by the softmax
+      bf16x8 tro_o[2], tro_q[2];
+      if constexpr (TRPIPE) {
+        tro_o[0] = lds_tr2(Ol, trofs(0, 0, 0), trofs(0, 0, 1));
+        tro_q[0] = lds_tr2(Ql, trofs(0, 0, 0), trofs(0, 0, 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int qr = acc_row(r, h);
-        const float pv = exp2_(fmaf(s[r], sl2, ls[qr]));
-        if constexpr (DROP) {   // dV from the dropped, rescaled P; dS = P (Z dP / (1-p) - delta)
+        if constexpr (RINIT) {
+          const float pv = exp2_(s[r] * sl2);
+          s[r] = pv;
+          dp[r] = pv * dp[r];
+        } else if constexpr (DROP) {   // dV from the dropped, rescaled P; dS = P (Z dP / (1-p) - delta)
+          const int qr = acc_row(r, h);
+          const float pv = exp2_(fmaf(s[r], sl2, ls[qr]));
           const bool keep = attn_keep(rk_s[buf * BMQ + qr], (unsigned)mykey, dthr);
           s[r] = keep ? pv * drs : 0.f;
           dp[r] = pv * ((keep ? dp[r] * drs : 0.f) - ds[qr]);
         } else {
+          const int qr = acc_row(r, h);
+          const float pv = exp2_(fmaf(s[r], sl2, ls[qr]));
           s[r] = pv;
           dp[r] = pv * (dp[r] - ds[qr]);
         }
@@ -691,14 +728,32 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
           sb[ks][j] = (bf16)dp[8 * ks + j];
         }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (TRPIPE) {
+        // step i = (ks, dt): its operands were read one step earlier; each step issues the next step's 4 reads
+        // ahead of its own 2 MFMAs
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          const int o0 = trofs(ks, dt, 0), o1 = trofs(ks, dt, 1);
-          dv[dt] = mfma32(lds_tr2(Ol, o0, o1), pb[ks], dv[dt]);
-          dk[dt] = mfma32(lds_tr2(Ql, o0, o1), sb[ks], dk[dt]);
+        for (int i = 0; i < 2 * DT; ++i) {
+          const int ks = i / DT, dt = i % DT;
+          if (i + 1 < 2 * DT) {
+            const int k2 = (i + 1) / DT, d2 = (i + 1) % DT;
+            tro_o[(i + 1) & 1] = lds_tr2(Ol, trofs(k2, d2, 0), trofs(k2, d2, 1));
+            tro_q[(i + 1) & 1] = lds_tr2(Ql, trofs(k2, d2, 0), trofs(k2, d2, 1));
+          }
+          dv[dt] = mfma32(tro_o[i & 1], pb[ks], dv[dt]);
+          dk[dt] = mfma32(tro_q[i & 1], sb[ks], dk[dt]);
+          if (i + 1 < 2 * DT) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
         }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const int o0 = trofs(ks, dt, 0), o1 = trofs(ks, dt, 1);
+            dv[dt] = mfma32(lds_tr2(Ol, o0, o1), pb[ks], dv[dt]);
+            dk[dt] = mfma32(lds_tr2(Ql, o0, o1), sb[ks], dk[dt]);
+          }
+      }
     }
     if (it + 1 < total) stage_scalars(buf ^ 1);
     wait_vmcnt<0>();
@@ -855,6 +910,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
 // ==================================================================================================
 // Waves per workgroup (4 or 8; DPH_ATTN_WAVES overrides, for A/B runs).  8 waves = 256 query rows (or keys) share
 // every staged K/V (or Q/dO) tile: half the LDS fill traffic per MFMA of 4 waves, one workgroup per CU.
+constexpr int kAttnBwdDefaultVar = 0;
+
 static int attn_waves(int fallback) {
   static const int w = [] {
     const char* e = getenv("DPH_ATTN_WAVES");
@@ -896,14 +953,35 @@ void flash_attn_fwd(const AttnParams& p, hipStream_t st) {
   }
 }
 
-template <int HD, int NW>
-static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
+// dK/dV kernel variant (template VAR of attn_bwd_dkdv_k); DPH_ATTN_BWD_VAR overrides, for A/B runs
+static int attn_bwd_var() {
+  static const int v = [] {
+    const char* e = getenv("DPH_ATTN_BWD_VAR");
+    const int x = e ? atoi(e) : kAttnBwdDefaultVar;
+    return (x >= 0 && x <= 3) ? x : kAttnBwdDefaultVar;
+  }();
+  return v;
+}
+
+template <int HD, int NW, int VAR>
+static void dkdv_launch(const AttnBwdParams& P, hipStream_t st) {
   const AttnParams& p = P.f;
   constexpr int BNK = 32 * NW;
   const size_t lds_kv = BNK * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
   const dim3 grid_kv((unsigned)((p.Sk + BNK - 1) / BNK * p.Hkv * p.B));
-  if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, NW>), grid_kv, dim3(64 * NW), lds_kv, st, P);
-  else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, NW>), grid_kv, dim3(64 * NW), lds_kv, st, P);
+  if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, NW, false, VAR>), grid_kv, dim3(64 * NW), lds_kv, st, P);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, NW, false, VAR>), grid_kv, dim3(64 * NW), lds_kv, st, P);
+}
+
+template <int HD, int NW>
+static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
+  const AttnParams& p = P.f;
+  switch (attn_bwd_var()) {
+    case 1: dkdv_launch<HD, NW, 1>(P, st); break;
+    case 2: dkdv_launch<HD, NW, 2>(P, st); break;
+    case 3: dkdv_launch<HD, NW, 3>(P, st); break;
+    default: dkdv_launch<HD, NW, 0>(P, st); break;
+  }
   const size_t lds_q = 2 * 2 * 64 * HD * 2;
   const dim3 grid_q((unsigned)((p.Sq + 32 * NW - 1) / (32 * NW) * p.Hq * p.B));
   if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW>), grid_q, dim3(64 * NW), lds_q, st, P);
