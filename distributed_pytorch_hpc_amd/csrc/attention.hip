@@ -772,7 +772,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
 // query (lane & 31).  Per 64-key tile: S^T = K Q^T and dP^T = V dO^T (A = K / V rows from LDS, B = Q^T / dO^T
 // fragments in registers), P^T = exp2(S^T c - lse) and dS^T = P^T (dP^T - delta) lane-locally (lse and delta
 // are one scalar per lane), then dQ^T += K^T dS^T with dS^T consumed straight from the accumulator.
-template <int HD, bool CAUSAL, int NW, bool DROP = false>
+// PF (A/B knob, DPH_ATTN_DQ_VAR=1): the dQ product's transposed K reads software-pipelined one MFMA ahead, the first
+// issued before the last sub-tile's softmax.
+template <int HD, bool CAUSAL, int NW, bool DROP = false, bool PF = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P) {
   using Plan = KVTilePlan<HD, 64 * NW>;
   constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
@@ -835,6 +837,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
 
   auto tile = [&](const char* Kl, const char* Vl, int k0, bool need_mask) {
     bf16x8 sf[4];
+    bf16x8 tk[2];   // PF: ring of transposed K operands, step i = (ks, dt) = (i / DT, i % DT)
+    auto tk_read = [&](int i) { return lds_tr2(Kl, plan.tr(i / DT, i % DT, 0), plan.tr(i / DT, i % DT, 1)); };
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       // K and V fragments are read a half sub-tile (KH k-steps) ahead of their MFMAs with counted lgkmcnt waits
@@ -856,6 +860,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
         }
         __builtin_amdgcn_sched_group_barrier(0x100, 2 * KH, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 2 * KH, 0);
+      }
+      if constexpr (PF) {
+        if (sub == 1) {
+          tk[0] = tk_read(0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
       if (need_mask) {  // wave-uniform; masked scores -> -inf -> p = 0
 #pragma unroll
@@ -881,11 +891,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
       __builtin_amdgcn_sched_barrier(0);
     }
     // dQ^T += K^T dS^T
+    if constexpr (PF) {
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
+      for (int i = 0; i < 4 * DT; ++i) {
+        if (i + 1 < 4 * DT) tk[(i + 1) & 1] = tk_read(i + 1);
+        dq[i % DT] = mfma32(tk[i & 1], sf[i / DT], dq[i % DT]);
+        if (i + 1 < 4 * DT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    } else {
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-        dq[dt] = mfma32(lds_tr2(Kl, plan.tr(ks, dt, 0), plan.tr(ks, dt, 1)), sf[ks], dq[dt]);
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+          dq[dt] = mfma32(lds_tr2(Kl, plan.tr(ks, dt, 0), plan.tr(ks, dt, 1)), sf[ks], dq[dt]);
+    }
   };
 
   for (int t = 0; t < ntiles; ++t) {
@@ -910,7 +930,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
 // ==================================================================================================
 // Waves per workgroup (4 or 8; DPH_ATTN_WAVES overrides, for A/B runs).  8 waves = 256 query rows (or keys) share
 // every staged K/V (or Q/dO) tile: half the LDS fill traffic per MFMA of 4 waves, one workgroup per CU.
-constexpr int kAttnBwdDefaultVar = 0;
+constexpr bool kAttnDqDefaultPf = false;
+constexpr int kAttnBwdDefaultVar = 2;   // A/B on one MI355X: 0 -> 659/663, 1 -> 645/650, 2 -> 673/672, 3 -> 664/660 TF
 
 static int attn_waves(int fallback) {
   static const int w = [] {
@@ -984,8 +1005,17 @@ static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
   }
   const size_t lds_q = 2 * 2 * 64 * HD * 2;
   const dim3 grid_q((unsigned)((p.Sq + 32 * NW - 1) / (32 * NW) * p.Hq * p.B));
-  if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW>), grid_q, dim3(64 * NW), lds_q, st, P);
-  else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW>), grid_q, dim3(64 * NW), lds_q, st, P);
+  static const bool dq_pf = [] {
+    const char* e = getenv("DPH_ATTN_DQ_VAR");
+    return e ? atoi(e) == 1 : kAttnDqDefaultPf;
+  }();
+  if (dq_pf) {
+    if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW, false, true>), grid_q, dim3(64 * NW), lds_q, st, P);
+    else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW, false, true>), grid_q, dim3(64 * NW), lds_q, st, P);
+  } else {
+    if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW>), grid_q, dim3(64 * NW), lds_q, st, P);
+    else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW>), grid_q, dim3(64 * NW), lds_q, st, P);
+  }
 }
 
 template <int HD>

@@ -101,12 +101,12 @@ def test_unet_fused_up_path_step_matches_reference():
     x = _cl(torch.randn(2, 16, 45, 90, device=dev))
     y = _cl(torch.randn(2, 16, 45, 90, device=dev))
 
-    def run(fused):
+    def run(fused, amp=True):
         m.zero_grad(set_to_none=True)
         old = upsample._ENABLED
         upsample._ENABLED = fused
         try:
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
                 out = m(x)
             loss = latitude_weighted_mse(out.float(), y)
             loss.backward()
@@ -114,9 +114,16 @@ def test_unet_fused_up_path_step_matches_reference():
             upsample._ENABLED = old
         return loss.item(), {k: p.grad.float().clone() for k, p in m.named_parameters()}
 
+    l32, g32 = run(False, amp=False)           # fp32 everywhere: the yardstick for both bf16 paths
     l_ref, g_ref = run(False)
     l_dph, g_dph = run(True)
-    assert abs(l_ref - l_dph) < 1e-2 * abs(l_ref)
-    for k in ("up3.weight", "up3.bias", "up2.weight", "up1.weight", "up1.bias", "enc1.0.weight"):
-        r = ((g_dph[k] - g_ref[k]).norm() / g_ref[k].norm()).item()
-        assert r < 6e-2, (k, r)
+    assert abs(l_ref - l_dph) < 1e-2 * abs(l_ref) and abs(l32 - l_dph) < 2e-2 * abs(l32)
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm()).item()
+
+    for k in ("up3.weight", "up3.bias", "up2.weight", "up2.bias", "up1.weight", "up1.bias", "dec1.0.weight",
+              "enc1.0.weight"):
+        e_dph, e_ref = rel(g_dph[k], g32[k]), rel(g_ref[k], g32[k])
+        # the fused bf16 path is no further from fp32 than the unfused bf16 path (plus a small margin)
+        assert e_dph < 1.5 * e_ref + 2e-2, (k, e_dph, e_ref)
