@@ -381,6 +381,15 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     return e ? atoi(e) : 0;
   }();
   const bool wide = N % 128 == 0 && force_bn != 64;
+  // 3x3: the LDS-DMA implicit GEMM of conv3x3.hip (DPH_CONV3_KERNEL=ts keeps this file's register-staged C3 path)
+  static const bool c3_ts = [] {
+    const char* e = getenv("DPH_CONV3_KERNEL");
+    return e && e[0] == 't';
+  }();
+  if (c3 && D == nullptr && stats == nullptr && !c3_ts && conv3_supported(M, N, K, lda, ldb)) {
+    conv3_gemm(A, B, C, M, N, K, lda, ldb, ldc, H, W, st);
+    return;
+  }
   if (stats != nullptr && !c3) {   // BatchNorm statistics of the output (1x1 forward only)
     if (wide)
       hipLaunchKernelGGL((ts_nt_k<128, false, false, true>), dim3(nmb * (int)(N / 128)), dim3(TS_NT), 0, st,

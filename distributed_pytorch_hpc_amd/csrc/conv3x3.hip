@@ -1,0 +1,213 @@
+// 3x3 / stride 1 / padding 1 convolution on channels-last activations as an implicit GEMM with an LDS-DMA pipeline,
+// for CDNA4 (gfx950): the ResNet-50 bottleneck conv2 (scripts/main.py:249 builds torchvision resnet50) and, through
+// ops/conv.py, any stride-1 3x3 convolution whose channel counts are multiples of 64.
+//
+//   C[M, N] = sum_k A_g[M, K] B[N, K]^T,   M = N_img*H*W pixels, K = 9 * Cin tap-major (k = tap * Cin + c),
+//   A_g[m, tap * Cin + c] = X[m + dy * W + dx, c]  (dy, dx) = (tap / 3 - 1, tap % 3 - 1), zero outside the image.
+//
+// Forward: X = input, B = weight [Cout, (kh, kw, Cin)].  Input gradient: X = dY, B = the flipped, channel-transposed
+// weight [Cin, (kh, kw, Cout)] (ops/conv.py) -- the same kernel.
+//
+// Structure (replaces the register-staged ts_nt_k<.., C3> path of conv1x1.hip, which tops out near 0.5 PFLOP/s with
+// one K-step in flight and A straight from L2 into registers):
+//   * 128 x BN output tile per workgroup (BN = 64 | 128), 4 waves as 2 (M) x 2 (N), wave tile 64 x BN/2,
+//     v_mfma_f32_32x32x16_bf16 with the pixel rows as the A operand;
+//   * K-steps of 64 channels of one tap; both operands staged global -> LDS by LDS-DMA (global_load_lds_dwordx4,
+//     16 B per lane, one 1-KiB piece = 8 rows of 128 B per wave-instruction) into a STAGES-deep ring of XOR-swizzled
+//     images (slot = chunk ^ ((row >> 1) & 7): conflict-free ds_read_b128 fragment reads); the A gather is just the
+//     per-lane DMA source address (the row shifted by the tap); rows whose tap falls outside the image are fetched
+//     from the row itself and their fragments zeroed in registers (v_cndmask), so no padded copy of the input exists;
+//   * one raw s_barrier per K-step, counted vmcnt: STAGES - 1 K-steps stay in flight behind the MFMAs;
+//   * C tile through LDS, written as whole 16-B row segments; workgroups remapped XCD-aware with the N-tiles of one
+//     row block adjacent (they read the same shifted input rows from one L2).
+#include "dph_common.h"
+#include "kernels.h"
+
+namespace dph {
+
+namespace {
+
+constexpr int C3_BM = 128, C3_BK = 64, C3_NT = 256;
+constexpr int C3_ROWB = 128;   // LDS image row: 64 bf16
+
+__device__ __forceinline__ f32x16 c3_mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// byte offset of 16-B chunk c of image row r
+__device__ __forceinline__ int c3_off(int r, int c) { return r * C3_ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
+
+template <int BN, int STAGES>
+__global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, const bf16* __restrict__ B,
+                                                   bf16* __restrict__ C, int M, int N, int K, int64_t ldx,
+                                                   int64_t ldb, int64_t ldc, int H, int W, int Cin) {
+  constexpr int AIMG = C3_BM * C3_ROWB, BIMG = BN * C3_ROWB, STG = AIMG + BIMG;
+  constexpr int AI = C3_BM / 8 / 4;        // A DMA pieces (8 rows) per wave per K-step
+  constexpr int BI = BN / 8 / 4;           // B DMA pieces per wave per K-step
+  static_assert(AI % 2 == 0 && BI % 2 == 0, "piece parity = j parity");
+  constexpr int PER = AI + BI;             // DMA instructions per thread per K-step
+  constexpr int WN = BN / 2, NTW = WN / 32;   // wave tile columns, 32-column MFMA tiles per wave
+  constexpr int CROW = BN + 8;             // epilogue LDS row (bf16)
+  constexpr int LDS = STAGES * STG > C3_BM * CROW * 2 ? STAGES * STG : C3_BM * CROW * 2;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS];
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l32 = lane & 31, h = lane >> 5;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntn = N / BN, nmb = (M + C3_BM - 1) / C3_BM;
+  const int lin = xcd_remap(blockIdx.x, nmb * ntn);
+  const int mb = lin / ntn, n0 = (lin % ntn) * BN;
+  const int m0 = mb * C3_BM;
+  const int HW = H * W;
+
+  // ---- DMA lanes: piece j of this wave covers image rows (wid * AI + j) * 8 + lane / 8, slot lane % 8 ----
+  const int prow = lane >> 3, pslot = lane & 7;
+  int ay[AI], ax[AI], am[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int r = (wid * AI + j) * 8 + prow;
+    const int m = min(m0 + r, M - 1);
+    am[j] = m;
+    ax[j] = m % W;
+    ay[j] = (m / W) % H;
+  }
+  // source chunk of a piece's lane: image row r = 8 q + prow has (r >> 1) & 7 = (4 q + (prow >> 1)) & 7, so the chunk
+  // depends on the parity of the piece index q (AI and BI are even: q's parity is j's)
+  const int chunk0 = pslot ^ ((prow >> 1) & 7), chunk1 = pslot ^ (((prow >> 1) + 4) & 7);
+  unsigned boff[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int r = (wid * BI + j) * 8 + prow;
+    boff[j] = (unsigned)(((int64_t)(n0 + r) * ldb + ((j & 1) ? chunk1 : chunk0) * 8) * 2);
+  }
+  const unsigned lds0 = lds_addr(smem);
+
+  auto issue = [&](int ks, int stage) {
+    const int k0 = ks * C3_BK;
+    const int tap = k0 / Cin, cb = k0 - tap * Cin;
+    const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+    const unsigned sa = lds0 + stage * STG + wid * AI * 1024;
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+      const bool ok = (unsigned)(ay[j] + dy) < (unsigned)H && (unsigned)(ax[j] + dx) < (unsigned)W;
+      const int src = ok ? am[j] + dy * W + dx : am[j];
+      lds_dma16(X, (unsigned)(((int64_t)src * ldx + cb + ((j & 1) ? chunk1 : chunk0) * 8) * 2), sa + j * 1024);
+    }
+    const unsigned sb = lds0 + stage * STG + AIMG + wid * BI * 1024;
+#pragma unroll
+    for (int j = 0; j < BI; ++j) lds_dma16(B, boff[j] + (unsigned)(k0 * 2), sb + j * 1024);
+  };
+
+  // ---- fragment readers: A rows wm*64 + i*32 + l32 (i < 2), B rows wn*WN + j*32 + l32 ----
+  int fy[2], fx[2];
+  bool fin[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + wm * 64 + i * 32 + l32;
+    fin[i] = m < M;
+    const int mm = min(m, M - 1);
+    fx[i] = mm % W;
+    fy[i] = (mm / W) % H;
+  }
+  int aoff[2][4], bofs[NTW][4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) aoff[i][f] = c3_off(wm * 64 + i * 32 + l32, 2 * f + h);
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) bofs[j][f] = AIMG + c3_off(wn * WN + j * 32 + l32, 2 * f + h);
+  }
+
+  f32x16 acc[2][NTW];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nks = K / C3_BK;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nks) issue(s, s);
+
+  for (int ks = 0; ks < nks; ++ks) {
+    // K-step ks landed (the later STAGES-2 steps may stay in flight), then every wave's pieces of it
+    if (ks + STAGES - 2 < nks) wait_vmcnt<(STAGES - 2) * PER>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    // the stage refilled now was read in step ks - 1, which every wave finished before the barrier
+    if (ks + STAGES - 1 < nks) issue(ks + STAGES - 1, (ks + STAGES - 1) % STAGES);
+    const char* st = smem + (ks % STAGES) * STG;
+    const int tap = ks * C3_BK / Cin;
+    const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+    bool ok[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      ok[i] = fin[i] && (unsigned)(fy[i] + dy) < (unsigned)H && (unsigned)(fx[i] + dx) < (unsigned)W;
+    // all fragments of the K-step are read first (one LDS round trip per K-step, consumed in issue order by
+    // counted lgkmcnt waits), then the 8 * NTW MFMAs
+    bf16x8 a[4][2], b[4][NTW];
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[f][i] = *reinterpret_cast<const bf16x8*>(st + aoff[i][f]);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) b[f][j] = *reinterpret_cast<const bf16x8*>(st + bofs[j][f]);
+    }
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bf16x8 av = ok[i] ? a[f][i] : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) acc[i][j] = c3_mfma(av, b[f][j], acc[i][j]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue through LDS: register r of tile (i, j) = C[wm*64 + i*32 + (r&3) + 8(r>>2) + 4h][wn*WN + j*32 + l32]
+  bf16* Cs = reinterpret_cast<bf16*>(smem);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        Cs[(wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CROW + wn * WN + j * 32 + l32] = (bf16)acc[i][j][r];
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int i = threadIdx.x; i < C3_BM * CPR; i += C3_NT) {
+    const int row = i / CPR, ch = i % CPR;
+    if (m0 + row < M)
+      *reinterpret_cast<bf16x8*>(C + (int64_t)(m0 + row) * ldc + n0 + ch * 8) =
+          *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
+  }
+  (void)HW;
+}
+
+}  // namespace
+
+bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
+  // 32-bit DMA source offsets: the whole input and weight must lie within 4 GiB of their bases
+  return M > 0 && N % 64 == 0 && K % (9 * 64) == 0 && M * lda * 2 < (int64_t(1) << 32) &&
+         N * ldb * 2 < (int64_t(1) << 32);
+}
+
+void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                int64_t ldc, int H, int W, hipStream_t st) {
+  const int nmb = (int)cdiv(M, C3_BM), cin = (int)(K / 9);
+  static const int force_bn = [] {
+    const char* e = getenv("DPH_CONV3_BN");
+    return e ? atoi(e) : 0;
+  }();
+  const bool wide = N % 128 == 0 && force_bn != 64;
+  if (wide)
+    hipLaunchKernelGGL((conv3_k<128, 2>), dim3(nmb * (int)(N / 128)), dim3(C3_NT), 0, st, (const bf16*)A,
+                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin);
+  else
+    hipLaunchKernelGGL((conv3_k<64, 3>), dim3(nmb * (int)(N / 64)), dim3(C3_NT), 0, st, (const bf16*)A,
+                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin);
+}
+
+}  // namespace dph
