@@ -80,19 +80,20 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
     boff[j] = (unsigned)(((int64_t)(n0 + r) * ldb + ((j & 1) ? chunk1 : chunk0) * 8) * 2);
   }
   const unsigned lds0 = lds_addr(smem);
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);   // the DMA destination (M0) must be provably wave-uniform
 
   auto issue = [&](int ks, int stage) {
     const int k0 = ks * C3_BK;
     const int tap = k0 / Cin, cb = k0 - tap * Cin;
     const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-    const unsigned sa = lds0 + stage * STG + wid * AI * 1024;
+    const unsigned sa = lds0 + stage * STG + wid_u * AI * 1024;
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
       const bool ok = (unsigned)(ay[j] + dy) < (unsigned)H && (unsigned)(ax[j] + dx) < (unsigned)W;
       const int src = ok ? am[j] + dy * W + dx : am[j];
       lds_dma16(X, (unsigned)(((int64_t)src * ldx + cb + ((j & 1) ? chunk1 : chunk0) * 8) * 2), sa + j * 1024);
     }
-    const unsigned sb = lds0 + stage * STG + AIMG + wid * BI * 1024;
+    const unsigned sb = lds0 + stage * STG + AIMG + wid_u * BI * 1024;
 #pragma unroll
     for (int j = 0; j < BI; ++j) lds_dma16(B, boff[j] + (unsigned)(k0 * 2), sb + j * 1024);
   };
