@@ -386,8 +386,8 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     const char* e = getenv("DPH_CONV3_KERNEL");
     return e && e[0] == 't';
   }();
-  if (c3 && D == nullptr && stats == nullptr && !c3_ts && conv3_supported(M, N, K, lda, ldb)) {
-    conv3_gemm(A, B, C, M, N, K, lda, ldb, ldc, H, W, st);
+  if (c3 && D == nullptr && !c3_ts && conv3_supported(M, N, K, lda, ldb)) {
+    conv3_gemm(A, B, C, M, N, K, lda, ldb, ldc, H, W, st, stats);   // (+ BatchNorm partials of the output)
     return;
   }
   if (stats != nullptr && !c3) {   // BatchNorm statistics of the output (1x1 forward only)

@@ -37,10 +37,14 @@ __device__ __forceinline__ f32x16 c3_mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 // byte offset of 16-B chunk c of image row r
 __device__ __forceinline__ int c3_off(int r, int c) { return r * C3_ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
 
-template <int BN, int STAGES>
+// STATS: also the per-128-row-block BatchNorm partials of the bf16 output (the layout of conv1x1.hip's ts_nt_k
+// STATS epilogue: stats[mb * N + n] = mean, stats[nmb * N + mb * N + n] = M2, stats[2 * nmb * N + mb] = rows), so
+// the BatchNorm after the 3x3 convolution skips its statistics pass.
+template <int BN, int STAGES, bool STATS = false>
 __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, const bf16* __restrict__ B,
                                                    bf16* __restrict__ C, int M, int N, int K, int64_t ldx,
-                                                   int64_t ldb, int64_t ldc, int H, int W, int Cin) {
+                                                   int64_t ldb, int64_t ldc, int H, int W, int Cin,
+                                                   float* __restrict__ stats = nullptr) {
   constexpr int AIMG = C3_BM * C3_ROWB, BIMG = BN * C3_ROWB, STG = AIMG + BIMG;
   constexpr int AI = C3_BM / 8 / 4;        // A DMA pieces (8 rows) per wave per K-step
   constexpr int BI = BN / 8 / 4;           // B DMA pieces per wave per K-step
@@ -48,7 +52,8 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
   constexpr int PER = AI + BI;             // DMA instructions per thread per K-step
   constexpr int WN = BN / 2, NTW = WN / 32;   // wave tile columns, 32-column MFMA tiles per wave
   constexpr int CROW = BN + 8;             // epilogue LDS row (bf16)
-  constexpr int LDS = STAGES * STG > C3_BM * CROW * 2 ? STAGES * STG : C3_BM * CROW * 2;
+  constexpr int LDS_C = C3_BM * CROW * 2 + (STATS ? 2 * BN * 4 : 0);
+  constexpr int LDS = STAGES * STG > LDS_C ? STAGES * STG : LDS_C;
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l32 = lane & 31, h = lane >> 5;
@@ -184,6 +189,56 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
       *reinterpret_cast<bf16x8*>(C + (int64_t)(m0 + row) * ldc + n0 + ch * 8) =
           *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
   }
+  if constexpr (STATS) {
+    // pass 1 column sums, pass 2 squared deviations from the block mean, of the bf16-rounded outputs; lane halves meet
+    // by a cross-half shuffle, the two M-waves of a column in a [2][BN] LDS block behind the C tile
+    float* sred = reinterpret_cast<float*>(smem + C3_BM * CROW * 2);
+    const int valid = min(C3_BM, M - m0);
+    const float inv_n = 1.f / (float)valid;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          sm += row < valid ? (float)(bf16)acc[i][j][r] : 0.f;
+        }
+      sm += __shfl_xor(sm, 32);
+      if (h == 0) sred[wm * BN + wn * WN + j * 32 + l32] = sm;
+    }
+    __syncthreads();
+    float mean_t[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int col = wn * WN + j * 32 + l32;
+      mean_t[j] = (sred[col] + sred[BN + col]) * inv_n;
+    }
+    const float mean_w = threadIdx.x < BN ? (sred[threadIdx.x] + sred[BN + threadIdx.x]) * inv_n : 0.f;
+    __syncthreads();   // every wave has read the sums before the M2 partials overwrite them
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      float m2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float d = (float)(bf16)acc[i][j][r] - mean_t[j];
+          m2 += row < valid ? d * d : 0.f;
+        }
+      m2 += __shfl_xor(m2, 32);
+      if (h == 0) sred[wm * BN + wn * WN + j * 32 + l32] = m2;
+    }
+    __syncthreads();
+    if (threadIdx.x < BN) {
+      const int col = threadIdx.x;
+      stats[(int64_t)mb * N + n0 + col] = mean_w;
+      stats[(int64_t)nmb * N + (int64_t)mb * N + n0 + col] = sred[col] + sred[BN + col];
+      if (col == 0 && n0 == 0) stats[2 * (int64_t)nmb * N + mb] = (float)valid;
+    }
+  }
   (void)HW;
 }
 
@@ -196,19 +251,24 @@ bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) 
 }
 
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, int H, int W, hipStream_t st) {
+                int64_t ldc, int H, int W, hipStream_t st, float* stats) {
   const int nmb = (int)cdiv(M, C3_BM), cin = (int)(K / 9);
   static const int force_bn = [] {
     const char* e = getenv("DPH_CONV3_BN");
     return e ? atoi(e) : 0;
   }();
   const bool wide = N % 128 == 0 && force_bn != 64;
-  if (wide)
-    hipLaunchKernelGGL((conv3_k<128, 2>), dim3(nmb * (int)(N / 128)), dim3(C3_NT), 0, st, (const bf16*)A,
-                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin);
-  else
-    hipLaunchKernelGGL((conv3_k<64, 3>), dim3(nmb * (int)(N / 64)), dim3(C3_NT), 0, st, (const bf16*)A,
-                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin);
+#define DPH_C3(BN_, ST_, STATS_)                                                                                 \
+  hipLaunchKernelGGL((conv3_k<BN_, ST_, STATS_>), dim3(nmb * (int)(N / BN_)), dim3(C3_NT), 0, st, (const bf16*)A, \
+                     (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, stats)
+  if (stats) {
+    if (wide) DPH_C3(128, 2, true);
+    else DPH_C3(64, 3, true);
+  } else {
+    if (wide) DPH_C3(128, 2, false);
+    else DPH_C3(64, 3, false);
+  }
+#undef DPH_C3
 }
 
 }  // namespace dph

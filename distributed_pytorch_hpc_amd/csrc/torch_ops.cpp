@@ -668,13 +668,16 @@ Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W, const 
 }
 
 // C = A B^T plus the BatchNorm statistics partials of C per 128-row block ([mean | M2 | rows], see conv1x1.hip).
-std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B) {
+std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B, int64_t H, int64_t W) {
   check_cuda(A, "A");
   c10::DeviceGuard g(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
               "ts_gemm_nt_stats: bf16 2-D operands");
-  const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
-  TORCH_CHECK(B.size(1) == K, "ts_gemm_nt_stats: K mismatch");
+  const int64_t M = A.size(0), N = B.size(0), K = B.size(1);
+  TORCH_CHECK(H > 0 ? (W > 0 && K == 9 * A.size(1) && M % (H * W) == 0) : A.size(1) == K,
+              "ts_gemm_nt_stats: K mismatch (3x3: B is [N, 9 * Cin], rows a multiple of H * W)");
+  TORCH_CHECK(H == 0 || dph::conv3_supported(M, N, K, A.stride(0), B.stride(0)),
+              "ts_gemm_nt_stats: 3x3 statistics need the LDS-DMA kernel's shapes");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
               "ts_gemm_nt_stats: row-major operands with 16-B aligned rows required");
   TORCH_CHECK(dph::conv1x1_supported(M, N, K), "ts_gemm_nt_stats: need N, K % 64 == 0");
@@ -684,7 +687,7 @@ std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B) {
   Tensor C = at::empty({M, N}, A.options());
   Tensor st = at::empty({2 * nmb * N + nmb}, A.options().dtype(at::kFloat));
   dph::ts_gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
-                  cur_stream(), 0, 0, nullptr, st.data_ptr<float>());
+                  cur_stream(), (int)H, (int)W, nullptr, st.data_ptr<float>());
   return {C, st};
 }
 
@@ -1224,7 +1227,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("gemm_tn_plan_info(int M, int N, int K) -> int[]", &gemm_tn_plan_info);
   m.def("gemm_tn_mfma_(int shape) -> int", &gemm_tn_mfma_);   // no tensor argument: catch-all kernel
   m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0, Tensor? add=None) -> Tensor");
-  m.def("ts_gemm_nt_stats(Tensor A, Tensor B) -> (Tensor, Tensor)");
+  m.def("ts_gemm_nt_stats(Tensor A, Tensor B, int H=0, int W=0) -> (Tensor, Tensor)");
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");

@@ -80,7 +80,11 @@ class Bottleneck(nn.Module):
             # conv1's: the tap parks the branch's gradient of x for conv1's dgrad epilogue (no separate add over x)
             tapped = grad_tap(x, slot) if slot is not None and slot.consumer else x
             idt, res_slot = self.downsample(tapped), None
-        out = self.bn2(self.conv2(out))
+        if isinstance(self.conv2, Conv3x3):
+            s2 = StatsSlot() if self.bn2.training else None
+            out = self.bn2(self.conv2(out, stats_slot=s2), stats_slot=s2)
+        else:
+            out = self.bn2(self.conv2(out))
         return self.bn3(self.conv3(out, stats_slot=s3), idt, residual_grad_slot=res_slot, stats_slot=s3)
 
 

@@ -182,7 +182,7 @@ def _ts_gemm_nt(A, B, H=0, W=0, add=None):
 
 
 @register_fake("dph::ts_gemm_nt_stats")
-def _ts_gemm_nt_stats(A, B):
+def _ts_gemm_nt_stats(A, B, H=0, W=0):
     M, N = A.shape[0], B.shape[0]
     nmb = (M + 127) // 128
     return A.new_empty((M, N)), A.new_empty((2 * nmb * N + nmb,), dtype=torch.float32)

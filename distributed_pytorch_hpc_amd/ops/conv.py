@@ -167,9 +167,24 @@ class _Conv1x1Fn(torch.autograd.Function):
         return dx, gw, None, None
 
 
+def _conv3_stats_ok() -> bool:
+    # the BatchNorm-statistics epilogue exists on the LDS-DMA kernel only (csrc/conv3x3.hip)
+    return os.environ.get("DPH_CONV3_KERNEL", "dma")[:1] != "t"
+
+
+def _main_grad_cl(w: torch.Tensor, cout: int, k: int):
+    """The engine-owned gradient of a channels-last 4-D weight viewed as [Cout, (kh, kw, Cin)] (its memory order),
+    or None."""
+    mg = getattr(w, "main_grad", None)
+    if (mg is None or not _DIRECT or mg.dim() != 4 or not mg.is_contiguous(memory_format=torch.channels_last)
+            or mg.data_ptr() % 16):
+        return None
+    return mg.permute(0, 2, 3, 1).view(cout, k)
+
+
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w):
+    def forward(ctx, x, w, stats_slot=None):
         wdtype = w.dtype
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -178,9 +193,13 @@ class _Conv3x3Fn(torch.autograd.Function):
         cout = wb.shape[0]
         x2 = _nhwc2d(x)
         wk = wb.permute(0, 2, 3, 1).reshape(cout, 9 * C)             # [Cout, (kh, kw, Cin)]
-        y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W)
+        if stats_slot is not None:
+            y2, stats_slot.stats = _lib.ops().ts_gemm_nt_stats(x2, wk, H, W)   # + BN partials of the output
+            stats_slot.rows, stats_slot.cols = y2.shape
+        else:
+            y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W)
         ctx.save_for_backward(x2, wb)
-        ctx.shape, ctx.wdtype = (B, C, H, W), wdtype
+        ctx.shape, ctx.wdtype, ctx.param = (B, C, H, W), wdtype, w
         return y2.view(B, H, W, cout).permute(0, 3, 1, 2)
 
     @staticmethod
@@ -195,10 +214,17 @@ class _Conv3x3Fn(torch.autograd.Function):
             wf = wb.flip(2, 3).permute(1, 2, 3, 0).reshape(C, 9 * cout)
             dx = _lib.ops().ts_gemm_nt(dy2, wf, H, W).view(B, H, W, C).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
-            gk = torch.empty((cout, 9 * C), dtype=ctx.wdtype, device=dy.device)
-            _lib.ops().ts_gemm_tn_(gk, dy2, x2, False, H, W)
-            gw = gk.view(cout, 3, 3, C).permute(0, 3, 1, 2).contiguous()
-        return dx, gw
+            w = ctx.param
+            mg = _main_grad_cl(w, cout, 9 * C)
+            if mg is not None:   # straight into the engine's bucket (channels-last weight = [Cout, (kh, kw, Cin)])
+                _lib.ops().ts_gemm_tn_(mg, dy2, x2, bool(getattr(w, "_dph_accum", False)), H, W)
+                w._dph_accum = True
+                w._dph_grad_ready()
+            else:
+                gk = torch.empty((cout, 9 * C), dtype=ctx.wdtype, device=dy.device)
+                _lib.ops().ts_gemm_tn_(gk, dy2, x2, False, H, W)
+                gw = gk.view(cout, 3, 3, C).permute(0, 3, 1, 2).contiguous()
+        return dx, gw, None
 
 
 def conv3x3_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -217,10 +243,10 @@ class Conv3x3(nn.Conv2d):
     def __init__(self, in_channels: int, out_channels: int):
         super().__init__(in_channels, out_channels, kernel_size=3, stride=1, padding=1, bias=False)
 
-    def forward(self, x):
+    def forward(self, x, stats_slot: StatsSlot | None = None):
         if conv3x3_native_ok(x, self.weight):
             _lib.require()
-            return _Conv3x3Fn.apply(x, self.weight)
+            return _Conv3x3Fn.apply(x, self.weight, stats_slot if _conv3_stats_ok() else None)
         return F.conv2d(x, self.weight, padding=1)
 
 
