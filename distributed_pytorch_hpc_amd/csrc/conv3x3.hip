@@ -44,7 +44,7 @@ template <int BN, int STAGES, bool STATS = false>
 __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, const bf16* __restrict__ B,
                                                    bf16* __restrict__ C, int M, int N, int K, int64_t ldx,
                                                    int64_t ldb, int64_t ldc, int H, int W, int Cin,
-                                                   float* __restrict__ stats = nullptr) {
+                                                   float* __restrict__ stats, const float* __restrict__ bias) {
   constexpr int AIMG = C3_BM * C3_ROWB, BIMG = BN * C3_ROWB, STG = AIMG + BIMG;
   constexpr int AI = C3_BM / 8 / 4;        // A DMA pieces (8 rows) per wave per K-step
   constexpr int BI = BN / 8 / 4;           // B DMA pieces per wave per K-step
@@ -171,6 +171,16 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
     }
   }
   __syncthreads();
+  if (bias != nullptr) {   // per-output-channel bias (fp32) on the accumulators: C and its statistics include it
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const float bj = bias[n0 + wn * WN + j * 32 + l32];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] += bj;
+    }
+  }
 
   // ---- epilogue through LDS: register r of tile (i, j) = C[wm*64 + i*32 + (r&3) + 8(r>>2) + 4h][wn*WN + j*32 + l32]
   bf16* Cs = reinterpret_cast<bf16*>(smem);
@@ -251,7 +261,7 @@ bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) 
 }
 
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, int H, int W, hipStream_t st, float* stats) {
+                int64_t ldc, int H, int W, hipStream_t st, float* stats, const float* bias) {
   const int nmb = (int)cdiv(M, C3_BM), cin = (int)(K / 9);
   static const int force_bn = [] {
     const char* e = getenv("DPH_CONV3_BN");
@@ -260,7 +270,7 @@ void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
   const bool wide = N % 128 == 0 && force_bn != 64;
 #define DPH_C3(BN_, ST_, STATS_)                                                                                 \
   hipLaunchKernelGGL((conv3_k<BN_, ST_, STATS_>), dim3(nmb * (int)(N / BN_)), dim3(C3_NT), 0, st, (const bf16*)A, \
-                     (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, stats)
+                     (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, stats, bias)
   if (stats) {
     if (wide) DPH_C3(128, 2, true);
     else DPH_C3(64, 3, true);

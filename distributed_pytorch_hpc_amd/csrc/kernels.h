@@ -159,7 +159,7 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 // 3x3 implicit GEMM with an LDS-DMA pipeline (csrc/conv3x3.hip); ts_gemm_nt's H, W > 0 path when supported.
 bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, int H, int W, hipStream_t stream, float* stats = nullptr);
+                int64_t ldc, int H, int W, hipStream_t stream, float* stats = nullptr, const float* bias = nullptr);
 int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K);
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
                 int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t stream, int H = 0,

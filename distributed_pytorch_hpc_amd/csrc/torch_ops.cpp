@@ -638,7 +638,8 @@ std::vector<int64_t> gemm_tn_plan_info(int64_t M, int64_t N, int64_t K) {
 // H, W > 0: 3x3 / stride-1 / pad-1 convolution as implicit GEMM, A = channels-last input [n*H*W, Cin],
 // B = weights [Cout, 9 * Cin] (tap-major).
 // add (optional): C = A B^T + add, add [M, N] bf16 row-major (a residual branch's gradient merged in the epilogue)
-Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W, const c10::optional<Tensor>& add) {
+Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W, const c10::optional<Tensor>& add,
+                  const c10::optional<Tensor>& bias) {
   check_cuda(A, "A");
   c10::DeviceGuard g(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "ts_gemm_nt: 2-D operands required");
@@ -661,6 +662,16 @@ Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W, const 
                 "ts_gemm_nt: add must be a contiguous bf16 [M, N] tensor");
     check_align16(*add, "add");
     D = add->data_ptr();
+  }
+  if (bias.has_value()) {   // 3x3 with a per-output-channel fp32 bias in the LDS-DMA kernel's epilogue
+    TORCH_CHECK(H > 0 && !add.has_value() && dph::conv3_supported(M, N, K, A.stride(0), B.stride(0)),
+                "ts_gemm_nt: bias is supported on the 3x3 LDS-DMA path only");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous() &&
+                    bias->device() == A.device(),
+                "ts_gemm_nt: bias must be a contiguous fp32 [N] tensor");
+    dph::conv3_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
+                    (int)H, (int)W, cur_stream(), nullptr, bias->data_ptr<float>());
+    return C;
   }
   dph::ts_gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
                   cur_stream(), (int)H, (int)W, D);
@@ -1226,7 +1237,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("gemm_tn_tail_(int cus) -> ()", &gemm_tn_tail_);                          // catch-all kernels
   m.def("gemm_tn_plan_info(int M, int N, int K) -> int[]", &gemm_tn_plan_info);
   m.def("gemm_tn_mfma_(int shape) -> int", &gemm_tn_mfma_);   // no tensor argument: catch-all kernel
-  m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0, Tensor? add=None) -> Tensor");
+  m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0, Tensor? add=None, Tensor? bias=None) -> Tensor");
   m.def("ts_gemm_nt_stats(Tensor A, Tensor B, int H=0, int W=0) -> (Tensor, Tensor)");
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");

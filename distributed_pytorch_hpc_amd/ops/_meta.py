@@ -177,7 +177,7 @@ def _gemm_tn(C, A, B, accumulate):
 
 
 @register_fake("dph::ts_gemm_nt")
-def _ts_gemm_nt(A, B, H=0, W=0, add=None):
+def _ts_gemm_nt(A, B, H=0, W=0, add=None, bias=None):
     return A.new_empty((A.shape[0], B.shape[0]))
 
 

@@ -184,7 +184,7 @@ def _main_grad_cl(w: torch.Tensor, cout: int, k: int):
 
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stats_slot=None):
+    def forward(ctx, x, w, stats_slot=None, bias=None):
         wdtype = w.dtype
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -193,11 +193,14 @@ class _Conv3x3Fn(torch.autograd.Function):
         cout = wb.shape[0]
         x2 = _nhwc2d(x)
         wk = wb.permute(0, 2, 3, 1).reshape(cout, 9 * C)             # [Cout, (kh, kw, Cin)]
-        if stats_slot is not None:
+        if bias is not None:   # fp32 bias in the epilogue (SimpleUNet's biased 3x3 convolutions)
+            y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W, None, bias)
+        elif stats_slot is not None:
             y2, stats_slot.stats = _lib.ops().ts_gemm_nt_stats(x2, wk, H, W)   # + BN partials of the output
             stats_slot.rows, stats_slot.cols = y2.shape
         else:
             y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W)
+        ctx.has_bias = bias is not None
         ctx.save_for_backward(x2, wb)
         ctx.shape, ctx.wdtype, ctx.param = (B, C, H, W), wdtype, w
         return y2.view(B, H, W, cout).permute(0, 3, 1, 2)
@@ -224,7 +227,10 @@ class _Conv3x3Fn(torch.autograd.Function):
                 gk = torch.empty((cout, 9 * C), dtype=ctx.wdtype, device=dy.device)
                 _lib.ops().ts_gemm_tn_(gk, dy2, x2, False, H, W)
                 gw = gk.view(cout, 3, 3, C).permute(0, 3, 1, 2).contiguous()
-        return dx, gw, None
+        db = None
+        if ctx.has_bias and ctx.needs_input_grad[3]:
+            db = _lib.ops().channel_sum(dy2, torch.float32)
+        return dx, gw, None, db
 
 
 def conv3x3_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -320,11 +326,23 @@ def _bias_conv(m: nn.Module, x: torch.Tensor, transposed: bool, output_padding) 
     return _ConvBiasFn.apply(x, w, b, *args)
 
 
+def _bias_conv3x3_ok(m: nn.Module, x: torch.Tensor) -> bool:
+    return (tuple(m.kernel_size) == (3, 3) and tuple(m.stride) == (1, 1) and tuple(m.padding) == (1, 1)
+            and tuple(m.dilation) == (1, 1) and m.groups == 1 and m.padding_mode == "zeros" and m.bias is not None
+            and _conv3_stats_ok() and conv3x3_native_ok(x, m.weight))
+
+
 class BiasConv2d(nn.Conv2d):
     """``nn.Conv2d`` (same parameters and state dict) whose channels-last GPU path computes the bias gradient with
-    the per-channel sum kernel; everything else is the stock MIOpen convolution."""
+    the per-channel sum kernel; stride-1 3x3 convolutions with 64-multiple channel counts take the implicit-GEMM
+    kernel of csrc/conv3x3.hip with the bias in its epilogue (when the 3x3 path is on), everything else the stock
+    MIOpen convolution."""
 
     def forward(self, x):
+        if _bias_conv3x3_ok(self, x):
+            _lib.require()
+            b = self.bias if self.bias.dtype == torch.float32 else self.bias.float()
+            return _Conv3x3Fn.apply(x, self.weight, None, b)
         if _bias_conv_ok(self, x):
             return _bias_conv(self, x, False, (0, 0))
         return super().forward(x)

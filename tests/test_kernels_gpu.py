@@ -802,6 +802,78 @@ def test_conv3x3_module_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W, 
     assert rel_err(conv.weight.grad, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("B,C,Co,H,W", [(2, 64, 128, 13, 17), (1, 128, 64, 45, 90)])
+def test_bias_conv3x3_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W):
+    """BiasConv2d 3x3 on the LDS-DMA kernel (bias in the epilogue, bias gradient = channel sum) under bf16 autocast
+    vs F.conv2d in fp32 on the same bf16-rounded operands."""
+    from distributed_pytorch_hpc_amd.ops.conv import BiasConv2d, _bias_conv3x3_ok
+
+    monkeypatch.setenv("DPH_CONV3X3", "1")
+    torch.manual_seed(3)
+    conv = BiasConv2d(C, Co, 3, padding=1).to(DEV).to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        conv.bias.uniform_(-1, 1)
+    x = torch.randn(B, C, H, W, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        assert _bias_conv3x3_ok(conv, x)
+        y = conv(x)
+    g = torch.randn_like(y.float())
+    y.float().backward(g)
+    xr = x.detach().to(torch.bfloat16).float().requires_grad_()
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_()
+    br = conv.bias.detach().clone().requires_grad_()
+    yr = torch.nn.functional.conv2d(xr, wr, br, padding=1)
+    yr.backward(g.to(torch.bfloat16).float())
+    assert rel_err(y, yr) < 8e-3
+    assert rel_err(x.grad, xr.grad) < 1e-2
+    assert rel_err(conv.weight.grad, wr.grad) < 1e-2
+    assert rel_err(conv.bias.grad, br.grad) < 1e-3
+
+
+@pytest.mark.parametrize("M_img,C,Co,H,W", [(3, 64, 128, 10, 11), (2, 128, 64, 28, 28)])
+def test_conv3x3_stats_epilogue(dph_native, M_img, C, Co, H, W):
+    """ts_gemm_nt_stats on the 3x3 path: the per-128-row-block [mean | M2 | rows] partials of the bf16 output."""
+    from distributed_pytorch_hpc_amd.ops import _lib
+
+    torch.manual_seed(4)
+    x2 = torch.randn(M_img * H * W, C, device=DEV, dtype=torch.bfloat16)
+    wk = (torch.randn(Co, 9 * C, device=DEV) * 0.05).to(torch.bfloat16)
+    y, st = _lib.ops().ts_gemm_nt_stats(x2, wk, H, W)
+    assert torch.equal(y, _lib.ops().ts_gemm_nt(x2, wk, H, W))
+    M = y.shape[0]
+    nmb = (M + 127) // 128
+    yf = y.float()
+    for mb in range(nmb):
+        blk = yf[mb * 128:(mb + 1) * 128]
+        mean = blk.mean(0)
+        torch.testing.assert_close(st[mb * Co:(mb + 1) * Co], mean, rtol=1e-4, atol=1e-4)
+        m2 = ((blk - mean) ** 2).sum(0)
+        torch.testing.assert_close(st[nmb * Co + mb * Co: nmb * Co + (mb + 1) * Co], m2, rtol=1e-3, atol=1e-3)
+        assert st[2 * nmb * Co + mb].item() == blk.shape[0]
+
+
+def test_resnet_bottleneck_conv3x3_path_matches_miopen(dph_native, monkeypatch):
+    """A stride-1 bottleneck with conv2 on the LDS-DMA 3x3 kernel (+ bn2 statistics from its epilogue) vs MIOpen."""
+    from distributed_pytorch_hpc_amd.models.resnet import Bottleneck
+
+    torch.manual_seed(6)
+    block = Bottleneck(256, 64).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x0 = torch.randn(4, 256, 14, 14, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    def run(flag):
+        monkeypatch.setenv("DPH_CONV3X3", flag)
+        block.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        block(x).float().pow(2).mean().backward()
+        return x.grad.float().clone(), {n: p.grad.float().clone() for n, p in block.named_parameters()}
+
+    gx0, g0 = run("0")
+    gx1, g1 = run("1")
+    assert rel_err(gx1, gx0) < 3e-2
+    for n in g0:
+        assert rel_err(g1[n], g0[n]) < 6e-2, n
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(4, 64, 112, 112), (3, 16, 7, 9), (2, 8, 1, 5), (2, 24, 6, 6), (2, 64, 181, 360)])
 @pytest.mark.parametrize("k", [3, 2])
