@@ -40,7 +40,9 @@ __device__ __forceinline__ int c3_off(int r, int c) { return r * C3_ROWB + ((c ^
 // STATS: also the per-128-row-block BatchNorm partials of the bf16 output (the layout of conv1x1.hip's ts_nt_k
 // STATS epilogue: stats[mb * N + n] = mean, stats[nmb * N + mb * N + n] = M2, stats[2 * nmb * N + mb] = rows), so
 // the BatchNorm after the 3x3 convolution skips its statistics pass.
-template <int BN, int STAGES, bool STATS = false>
+// ZB: padding taps / rows past M zero-filled by the DMA itself (buffer_load ... lds with an out-of-range offset),
+// instead of fetching the row and zeroing the fragment registers (A/B knob DPH_CONV3_ZERO=oob).
+template <int BN, int STAGES, bool STATS = false, bool ZB = false>
 __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, const bf16* __restrict__ B,
                                                    bf16* __restrict__ C, int M, int N, int K, int64_t ldx,
                                                    int64_t ldb, int64_t ldc, int H, int W, int Cin,
@@ -67,10 +69,12 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
   // ---- DMA lanes: piece j of this wave covers image rows (wid * AI + j) * 8 + lane / 8, slot lane % 8 ----
   const int prow = lane >> 3, pslot = lane & 7;
   int ay[AI], ax[AI], am[AI];
+  bool arow_in[AI];
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
     const int r = (wid * AI + j) * 8 + prow;
     const int m = min(m0 + r, M - 1);
+    arow_in[j] = m0 + r < M;
     am[j] = m;
     ax[j] = m % W;
     ay[j] = (m / W) % H;
@@ -85,6 +89,7 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
     boff[j] = (unsigned)(((int64_t)(n0 + r) * ldb + ((j & 1) ? chunk1 : chunk0) * 8) * 2);
   }
   const unsigned lds0 = lds_addr(smem);
+  const dph_rsrc xres = make_rsrc(X, (unsigned)((int64_t)M * ldx * 2));
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);   // the DMA destination (M0) must be provably wave-uniform
 
   auto issue = [&](int ks, int stage) {
@@ -95,8 +100,13 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
       const bool ok = (unsigned)(ay[j] + dy) < (unsigned)H && (unsigned)(ax[j] + dx) < (unsigned)W;
-      const int src = ok ? am[j] + dy * W + dx : am[j];
-      lds_dma16(X, (unsigned)(((int64_t)src * ldx + cb + ((j & 1) ? chunk1 : chunk0) * 8) * 2), sa + j * 1024);
+      if constexpr (ZB) {
+        const unsigned off = (unsigned)(((int64_t)(am[j] + dy * W + dx) * ldx + cb + ((j & 1) ? chunk1 : chunk0) * 8) * 2);
+        lds_dma16_buf(xres, (ok && arow_in[j]) ? off : 0x80000000u, sa + j * 1024);
+      } else {
+        const int src = ok ? am[j] + dy * W + dx : am[j];
+        lds_dma16(X, (unsigned)(((int64_t)src * ldx + cb + ((j & 1) ? chunk1 : chunk0) * 8) * 2), sa + j * 1024);
+      }
     }
     const unsigned sb = lds0 + stage * STG + AIMG + wid_u * BI * 1024;
 #pragma unroll
@@ -164,7 +174,7 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
     for (int f = 0; f < 4; ++f) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const bf16x8 av = ok[i] ? a[f][i] : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        const bf16x8 av = (ZB || ok[i]) ? a[f][i] : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < NTW; ++j) acc[i][j] = c3_mfma(av, b[f][j], acc[i][j]);
       }
@@ -268,15 +278,27 @@ void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     return e ? atoi(e) : 0;
   }();
   const bool wide = N % 128 == 0 && force_bn != 64;
-#define DPH_C3(BN_, ST_, STATS_)                                                                                 \
-  hipLaunchKernelGGL((conv3_k<BN_, ST_, STATS_>), dim3(nmb * (int)(N / BN_)), dim3(C3_NT), 0, st, (const bf16*)A, \
+  static const bool zb = [] {
+    const char* e = getenv("DPH_CONV3_ZERO");
+    return e && e[0] == 'o';
+  }();
+#define DPH_C3(BN_, ST_, STATS_, ZB_)                                                                                 \
+  hipLaunchKernelGGL((conv3_k<BN_, ST_, STATS_, ZB_>), dim3(nmb * (int)(N / BN_)), dim3(C3_NT), 0, st, (const bf16*)A, \
                      (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, stats, bias)
-  if (stats) {
-    if (wide) DPH_C3(128, 2, true);
-    else DPH_C3(64, 3, true);
+  if (zb) {
+    if (stats) {
+      if (wide) DPH_C3(128, 2, true, true);
+      else DPH_C3(64, 3, true, true);
+    } else {
+      if (wide) DPH_C3(128, 2, false, true);
+      else DPH_C3(64, 3, false, true);
+    }
+  } else if (stats) {
+    if (wide) DPH_C3(128, 2, true, false);
+    else DPH_C3(64, 3, true, false);
   } else {
-    if (wide) DPH_C3(128, 2, false);
-    else DPH_C3(64, 3, false);
+    if (wide) DPH_C3(128, 2, false, false);
+    else DPH_C3(64, 3, false, false);
   }
 #undef DPH_C3
 }

@@ -80,6 +80,29 @@ __device__ __forceinline__ void lds_dma16(const void* sbase, unsigned voff, unsi
                : "memory");
 }
 
+// Buffer resource (V#) of a raw byte buffer [base, base + bytes): stride 0, the range-checked form -- a load whose
+// offset lies past `bytes` returns zeros (gfx9 word 3 = 0x00020000).  Built from wave-uniform values.
+typedef int dph_rsrc __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ dph_rsrc make_rsrc(const void* base, unsigned bytes) {
+  const unsigned long long b = (unsigned long long)base;
+  dph_rsrc r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)b);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((b >> 32) & 0xffffu));
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+
+// LDS-DMA of 16 B per lane through a buffer resource: lds_dma16 with the per-lane byte offset `voff` range-checked
+// against the resource (an out-of-range lane writes 16 zero bytes to its LDS slot -- zero padding without a copy).
+__device__ __forceinline__ void lds_dma16_buf(dph_rsrc rsrc, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(lds)
+               : "memory");
+}
+
 // s_waitcnt with only the vector-memory counter constrained (LDS-DMA completion), gfx9 encoding.
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {

@@ -6,6 +6,8 @@ O=gpurun_out
 run() { local name=$1; shift; timeout -k 10 300 "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; return $rc; }
 run r3_s10_conv3_tests python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "conv3x3 or bottleneck" || exit 1
 run r3_s10_conv3_bench python -u benchmarks/conv3x3_bench.py --json $O/r3_conv3_bench.json || exit 1
+DPH_CONV3_ZERO=oob run r3_s10_conv3_tests_oob python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "conv3x3 or bottleneck" || exit 1
+DPH_CONV3_ZERO=oob run r3_s10_conv3_bench_oob python -u benchmarks/conv3x3_bench.py --json $O/r3_conv3_bench_oob.json || exit 1
 DPH_CONV3_KERNEL=ts run r3_s10_conv3_bench_old python -u benchmarks/conv3x3_bench.py --json $O/r3_conv3_bench_old.json || exit 1
 DPH_ATTN_DQ_VAR=1 run r3_s10_attn_dqpf_tests python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py tests/test_attention_dropout.py -k "flash or attention or attn" || exit 1
 for rep in 1 2; do for v in 0 1; do
