@@ -41,7 +41,7 @@ __device__ __forceinline__ int c3_off(int r, int c) { return r * C3_ROWB + ((c ^
 // STATS epilogue: stats[mb * N + n] = mean, stats[nmb * N + mb * N + n] = M2, stats[2 * nmb * N + mb] = rows), so
 // the BatchNorm after the 3x3 convolution skips its statistics pass.
 // ZB: padding taps / rows past M zero-filled by the DMA itself (buffer_load ... lds with an out-of-range offset),
-// instead of fetching the row and zeroing the fragment registers (A/B knob DPH_CONV3_ZERO=oob).
+// instead of fetching the row and zeroing the fragment registers (the default; DPH_CONV3_ZERO=mask for the latter).
 template <int BN, int STAGES, bool STATS = false, bool ZB = false>
 __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, const bf16* __restrict__ B,
                                                    bf16* __restrict__ C, int M, int N, int K, int64_t ldx,
@@ -278,9 +278,11 @@ void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     return e ? atoi(e) : 0;
   }();
   const bool wide = N % 128 == 0 && force_bn != 64;
+  // padding by range-checked buffer DMA (default: 1.0-1.2x the register-zeroing form on every ResNet-50 / UNet shape,
+  // profiles/r3/conv3_bench_*.json); DPH_CONV3_ZERO=mask selects the register form
   static const bool zb = [] {
     const char* e = getenv("DPH_CONV3_ZERO");
-    return e && e[0] == 'o';
+    return !(e && e[0] == 'm');
   }();
 #define DPH_C3(BN_, ST_, STATS_, ZB_)                                                                                 \
   hipLaunchKernelGGL((conv3_k<BN_, ST_, STATS_, ZB_>), dim3(nmb * (int)(N / BN_)), dim3(C3_NT), 0, st, (const bf16*)A, \

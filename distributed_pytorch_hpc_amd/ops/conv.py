@@ -167,6 +167,10 @@ class _Conv1x1Fn(torch.autograd.Function):
         return dx, gw, None, None
 
 
+_CONV3_WGRAD = os.environ.get("DPH_CONV3_WGRAD", "miopen")
+_CONV3X3_DEFAULT = "0"   # DPH_CONV3X3=1: stride-1 3x3 convolutions on csrc/conv3x3.hip
+
+
 def _conv3_stats_ok() -> bool:
     # the BatchNorm-statistics epilogue exists on the LDS-DMA kernel only (csrc/conv3x3.hip)
     return os.environ.get("DPH_CONV3_KERNEL", "dma")[:1] != "t"
@@ -216,7 +220,14 @@ class _Conv3x3Fn(torch.autograd.Function):
             # dX = conv3x3(dY, W') with W'[ci, (kh, kw), co] = W[co, ci, 2 - kh, 2 - kw]
             wf = wb.flip(2, 3).permute(1, 2, 3, 0).reshape(C, 9 * cout)
             dx = _lib.ops().ts_gemm_nt(dy2, wf, H, W).view(B, H, W, C).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and _CONV3_WGRAD != "dph":
+            # weight gradient on MIOpen: 1.0-1.5x the split-pixel kernel on the ResNet-50 shapes
+            # (profiles/r3/conv3_bench_oob.json: 318-485 vs 302-321 TFLOP/s); DPH_CONV3_WGRAD=dph selects the kernel
+            x4 = x2.view(B, H, W, C).permute(0, 3, 1, 2)
+            dy4 = dy2.view(B, H, W, cout).permute(0, 3, 1, 2)
+            gw = torch.ops.aten.convolution_backward(dy4, x4, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1].to(ctx.wdtype)
+        elif ctx.needs_input_grad[1]:
             w = ctx.param
             mg = _main_grad_cl(w, cout, 9 * C)
             if mg is not None:   # straight into the engine's bucket (channels-last weight = [Cout, (kh, kw, Cin)])
@@ -234,7 +245,7 @@ class _Conv3x3Fn(torch.autograd.Function):
 
 
 def conv3x3_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    if os.environ.get("DPH_CONV3X3", "0") != "1" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
+    if os.environ.get("DPH_CONV3X3", _CONV3X3_DEFAULT) != "1" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
         return False
     if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)):
         return False

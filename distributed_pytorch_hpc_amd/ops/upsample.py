@@ -5,11 +5,12 @@ The reference decoder (scripts/01_data_parallel_ddp/multinode_ddp_unet.py:180-18
 181-row grid makes the sizes differ, and ``torch.cat([up, skip], dim=1)``: three passes over the up-sampled map (four
 under bf16 autocast, which runs the resize in fp32 and promotes the cat).  Here:
 
-* forward: ``Y' = X Wr`` on hipBLASLt (channels-last X viewed as [N*H*W, Cin]; ``Wr`` = the weight as
-  [Cin, (i, j, Cout)]), then ``upcat_fwd`` writes the concatenated decoder input directly: the bilinear sample of the
+* forward: ``Y' = X Wr`` on the tall-skinny GEMM of csrc/conv1x1.hip (channels-last X viewed as [N*H*W, Cin];
+  ``Wr`` = the weight as [Cin, (i, j, Cout)]; hipBLASLt when the channel counts are not multiples of 64), then ``upcat_fwd`` writes the concatenated decoder input directly: the bilinear sample of the
   pixel-shuffled Y' + bias in channels [0, Cout), the skip in [Cout, Cout + Cs);
 * backward: ``upcat_bwd`` turns d(cat) into dY' (pixel-unshuffled bilinear adjoint, a deterministic gather) and the
-  dense skip gradient in one launch; dX = dY' Wr^T and dWr = X^T dY' on hipBLASLt; the bias gradient is the channel
+  dense skip gradient in one launch; dX = dY' Wr^T and dWr = X^T dY' on the same tall-skinny kernels (the weight
+  gradient split over pixel chunks with fp32 partials, deterministic); the bias gradient is the channel
   sum of dY' (the bilinear weights of every output pixel sum to one).
 
 ``up_concat(up, x, skip)`` takes the fused path for an ``nn.ConvTranspose2d(Cin, Cout, 2, 2)`` on channels-last GPU
@@ -58,6 +59,10 @@ def up_concat_native_ok(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> b
             and h <= ho <= 4 * h and w <= wo <= 4 * w)
 
 
+def _tall_skinny_ok(cin: int, co: int) -> bool:
+    return cin % 64 == 0 and (4 * co) % 64 == 0 and os.environ.get("DPH_UPCAT_GEMM", "ts") == "ts"
+
+
 class _UpConcatFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, skip):
@@ -65,11 +70,16 @@ class _UpConcatFn(torch.autograd.Function):
         co = weight.shape[1]
         x2 = x.permute(0, 2, 3, 1).reshape(n * h * w, cin)          # channels-last: a view
         wr = weight.permute(0, 2, 3, 1).reshape(cin, 4 * co)        # (ci) x (i, j, co)
-        y2 = torch.matmul(x2, wr)
+        ts = _tall_skinny_ok(cin, co)
+        wrt = wr.t().contiguous() if ts else None                   # [(i, j, co), ci]
+        # the [pixels, Cin] x [Cin, 4 Cout] GEMM on the tall-skinny kernels of csrc/conv1x1.hip when the channel
+        # counts allow (they are written for M >> N, K), hipBLASLt otherwise
+        y2 = _lib.ops().ts_gemm_nt(x2, wrt) if ts else torch.matmul(x2, wr)
         out = _lib.ops().upcat_fwd(y2, bias, skip, h, w)
         ctx.save_for_backward(x2, wr)
         ctx.dims = (n, cin, h, w, co)
         ctx.has_bias = bias is not None
+        ctx.ts = ts
         return out
 
     @staticmethod
@@ -80,9 +90,16 @@ class _UpConcatFn(torch.autograd.Function):
         dy2, dskip = _lib.ops().upcat_bwd(dcat, h, w, co)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.matmul(dy2, wr.t()).view(n, h, w, cin).permute(0, 3, 1, 2)
+            dx2 = _lib.ops().ts_gemm_nt(dy2, wr) if ctx.ts else torch.matmul(dy2, wr.t())
+            dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
-            dw = torch.matmul(x2.t(), dy2).view(cin, 2, 2, co).permute(0, 3, 1, 2).contiguous()
+            if ctx.ts:   # dWr[ci, (i, j, co)] = X^T dY' over all pixels (split-pixel kernel, deterministic)
+                dwr = torch.empty((cin, 4 * co), device=x2.device, dtype=torch.float32)
+                _lib.ops().ts_gemm_tn_(dwr, x2, dy2, False)
+                dwr = dwr.to(x2.dtype)
+            else:
+                dwr = torch.matmul(x2.t(), dy2)
+            dw = dwr.view(cin, 2, 2, co).permute(0, 3, 1, 2).contiguous()
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = _lib.ops().channel_sum(dy2.view(-1, co), torch.float32)
         return dx, dw, db, dskip
