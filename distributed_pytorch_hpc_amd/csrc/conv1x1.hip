@@ -333,6 +333,141 @@ __global__ __launch_bounds__(256) void ts_tn_k(const bf16* __restrict__ A, const
     out[(int64_t)(n0 + wi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * K + k0 + wj * 32 + (lane & 31)] = acc[r];
 }
 
+// ---- 3x3 weight gradient with an LDS-DMA pipeline: P[s][co][k'] = sum_{m in chunk s} dY[m][co] X_tap(k')[m][ci(k')]
+// Output tile TCO (64 | 128) output channels x 192 k' (three 64-channel slabs of the tap-major K' = 9 Cin, each slab
+// with its own tap), 4 waves as 2 (co) x 2 (k'), wave tile TCO/2 x 96 = (TCO/64) x 3 MFMA 32x32x16 tiles.
+// Pixel steps of 64 rows: the dY slab(s) and the three tap-shifted X slabs go global -> LDS by range-checked buffer
+// LDS-DMA (rows past the chunk and padding taps land as zeros, no masking anywhere), 2-stage ring, one barrier per
+// step, MFMA operands by ds_read_b64_tr_b16 from the ts_tn_k image layout (128-B rows, XOR-swizzled by bit 1 of the
+// row).  fp32 partials per pixel chunk, summed by ts_reduce_k.
+constexpr int C3W_TK = 192, C3W_SLABS = 3, C3W_SLAB = 64 * TW_ROWB;   // 8 KB per [64 px][64 ch] slab
+
+// q = r / d, m = r % d for 0 <= r < 2^24 through the fp32 reciprocal (error < 1 before the correction steps)
+__device__ __forceinline__ void fdivmod(int r, int d, float inv, int& q, int& m) {
+  q = (int)((float)r * inv);
+  m = r - q * d;
+  if (m < 0) { --q; m += d; }
+  if (m >= d) { ++q; m -= d; }
+}
+
+template <int TCO>
+__global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                float* __restrict__ P, int M, int N, int K, int64_t lda,
+                                                int64_t ldb, int chunk, int H, int W, int Cin) {
+  constexpr int AS = TCO / 64;                       // dY slabs per step
+  constexpr int STG = (AS + C3W_SLABS) * C3W_SLAB;   // one stage
+  constexpr int PCS = (AS + C3W_SLABS) * 8 / 4;      // 1-KB DMA pieces per wave per step
+  constexpr int TI = TCO / 64;                       // co MFMA tiles per wave (wave covers TCO / 2 channels)
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int cw = wid >> 1, kw = wid & 1;
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, h = lane >> 5;
+  const int tn = N / TCO, tk = K / C3W_TK, ntile = tn * tk;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int s = lin / ntile, tile = lin % ntile;    // the tiles of one pixel chunk run together (same XCD, same rows)
+  const int n0 = (tile / tk) * TCO, k0 = (tile % tk) * C3W_TK;
+  const int mbeg = s * chunk, mend = min(M, mbeg + chunk);
+
+  const float invW = 1.f / (float)W, invH = 1.f / (float)H;
+  const dph_rsrc ra = make_rsrc(A, (unsigned)((int64_t)M * lda * 2));
+  const dph_rsrc rb = make_rsrc(B, (unsigned)((int64_t)M * ldb * 2));
+  const unsigned lds0 = lds_addr(smem);
+  const int wid_u = __builtin_amdgcn_readfirstlane(wid);
+  // DMA lanes: piece i (of AS*8 + 24 per step) = slab i / 8, rows 8 (i % 8) + prow, LDS slot lane % 8
+  const int prow = lane >> 3, sch = (lane & 7) ^ tw_swz(prow);
+  int bdy[C3W_SLABS], bdx[C3W_SLABS], bcb[C3W_SLABS];
+#pragma unroll
+  for (int sb = 0; sb < C3W_SLABS; ++sb) {
+    const int kk = k0 + sb * 64, tap = kk / Cin;
+    bcb[sb] = kk - tap * Cin;
+    bdy[sb] = tap / 3 - 1;
+    bdx[sb] = tap - (tap / 3) * 3 - 1;
+  }
+  auto issue = [&](int m, int stage) {
+#pragma unroll
+    for (int j = 0; j < PCS; ++j) {
+      const int i = wid_u * PCS + j;                 // wave-uniform piece index
+      const int slab = i >> 3, prc = i & 7;
+      const int r = m + 8 * prc + prow;              // pixel row of this lane
+      const unsigned dst = lds0 + stage * STG + i * 1024;
+      if (slab < AS) {
+        const unsigned off = (unsigned)(((int64_t)r * lda + n0 + slab * 64 + sch * 8) * 2);
+        lds_dma16_buf(ra, r < mend ? off : 0x80000000u, dst);
+      } else {
+        const int sb = slab - AS;
+        int yq, xw, yh, nq;
+        fdivmod(r, W, invW, yq, xw);                 // pixel -> (image row, column), then image row -> y
+        fdivmod(yq, H, invH, nq, yh);
+        const bool ok = r < mend && (unsigned)(yh + bdy[sb]) < (unsigned)H && (unsigned)(xw + bdx[sb]) < (unsigned)W;
+        const unsigned off =
+            (unsigned)(((int64_t)(r + bdy[sb] * W + bdx[sb]) * ldb + bcb[sb] + sch * 8) * 2);
+        lds_dma16_buf(rb, ok ? off : 0x80000000u, dst);
+      }
+    }
+  };
+
+  // transposed-read offsets (ts_tn_k's layout): 32-column operand at 32-column offset c32 of a slab
+  const int hh = g >> 1, tch = 2 * (g & 1) + (p >> 1), tin = 8 * (p & 1);
+  auto toff = [&](int c32) { return (8 * hh + q) * TW_ROWB + (((c32 * 4 + tch) ^ tw_swz(q)) << 4) + tin; };
+  int aoff[TI], boff[3];
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int co = cw * (TCO / 2) + i * 32;          // within the tile
+    aoff[i] = (co >> 6) * C3W_SLAB + toff((co >> 5) & 1);
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int kc = kw * 96 + j * 32;
+    boff[j] = (AS + (kc >> 6)) * C3W_SLAB + toff((kc >> 5) & 1);
+  }
+
+  f32x16 acc[TI][3];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nsteps = (mend - mbeg + 63) / 64;
+  if (nsteps > 0) issue(mbeg, 0);
+  for (int st = 0; st < nsteps; ++st) {
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (st + 1 < nsteps) issue(mbeg + (st + 1) * 64, (st + 1) & 1);
+    const char* base = smem + (st & 1) * STG;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {                 // 16-pixel MFMA k-steps
+      const int ro = 16 * kk * TW_ROWB;
+      bf16x8 af[TI], bfr[3];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const bf16x4 lo = tr_read(base + aoff[i] + ro), hi = tr_read(base + aoff[i] + ro + 4 * TW_ROWB);
+        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const bf16x4 lo = tr_read(base + boff[j] + ro), hi = tr_read(base + boff[j] + ro + 4 * TW_ROWB);
+        bfr[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
+    }
+  }
+  // register r of tile (i, j): P[n0 + cw*TCO/2 + i*32 + (r&3) + 8(r>>2) + 4h][k0 + kw*96 + j*32 + (lane & 31)]
+  float* out = P + (int64_t)s * N * K;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        out[(int64_t)(n0 + cw * (TCO / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * K + k0 + kw * 96 + j * 32 +
+            (lane & 31)] = acc[i][j][r];
+}
+
 // dW = sum_s P[s] (+ dW).  A workgroup = 16 float4 output columns x 16 split groups; each thread sums every
 // 16th split of its float4 (independent loads in flight), then the 16 partial sums meet in LDS in a fixed order.
 template <typename T, bool ACC>
@@ -449,12 +584,41 @@ int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K) {
   return (int)best_s;
 }
 
+bool c3w_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
+  static const bool off = [] {
+    const char* e = getenv("DPH_CONV3W_KERNEL");
+    return e && e[0] == 't';
+  }();
+  // 32-bit buffer offsets below the 0x80000000 "padding" sentinel; fp32 row division exact below 2^24 pixels
+  return !off && N % 64 == 0 && K % C3W_TK == 0 && M * lda * 2 < (int64_t(1) << 31) &&
+         M * ldb * 2 < (int64_t(1) << 31) && M < (int64_t(1) << 24);
+}
+
+int c3w_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tco = N % 128 == 0 ? 128 : 64;
+  const int64_t tiles = (N / tco) * (K / C3W_TK);
+  // one resident round of 2 workgroups per CU (the fp32 partials grow with the split), chunks of >= 512 rows
+  int64_t s = cdiv(512, tiles);
+  s = std::max<int64_t>(1, std::min<int64_t>(s, M / 512));
+  return (int)s;
+}
+
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
                 int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t st, int H, int W) {
   const int64_t tiles = (N / 64) * (K / 64);
   int64_t chunk = cdiv(M, nsplit);
   chunk = cdiv(chunk, 64) * 64;
-  if (H > 0)
+  if (H > 0 && c3w_supported(M, N, K, lda, ldb)) {   // the LDS-DMA 3x3 kernel (nsplit from c3w_splits)
+    const int cin = (int)(K / 9);
+    if (N % 128 == 0)
+      hipLaunchKernelGGL((c3w_k<128>), dim3((int)((N / 128) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,
+                         (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, H, W,
+                         cin);
+    else
+      hipLaunchKernelGGL((c3w_k<64>), dim3((int)((N / 64) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,
+                         (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, H, W,
+                         cin);
+  } else if (H > 0)
     hipLaunchKernelGGL((ts_tn_k<true>), dim3((int)(tiles * nsplit)), dim3(256), 0, st, (const bf16*)A,
                        (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, H, W, (int)(K / 9));
   else

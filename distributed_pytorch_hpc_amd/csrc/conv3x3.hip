@@ -266,8 +266,9 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
 
 bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
   // 32-bit DMA source offsets: the whole input and weight must lie within 4 GiB of their bases
-  return M > 0 && N % 64 == 0 && K % (9 * 64) == 0 && M * lda * 2 < (int64_t(1) << 32) &&
-         N * ldb * 2 < (int64_t(1) << 32);
+  // (and below the 0x80000000 offset the range-checked DMA uses for padding rows)
+  return M > 0 && N % 64 == 0 && K % (9 * 64) == 0 && M * lda * 2 < (int64_t(1) << 31) &&
+         N * ldb * 2 < (int64_t(1) << 31);
 }
 
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,

@@ -161,6 +161,9 @@ bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, int H, int W, hipStream_t stream, float* stats = nullptr, const float* bias = nullptr);
 int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K);
+// 3x3 weight gradient on the LDS-DMA kernel (conv1x1.hip c3w_k): supported shapes and its pixel-chunk count
+bool c3w_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
+int c3w_splits(int64_t M, int64_t N, int64_t K);
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
                 int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t stream, int H = 0,
                 int W = 0);

@@ -830,6 +830,28 @@ def test_bias_conv3x3_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W):
     assert rel_err(conv.bias.grad, br.grad) < 1e-3
 
 
+@pytest.mark.parametrize("N_img,C,Co,H,W", [(3, 64, 64, 10, 11), (2, 128, 128, 28, 28), (1, 64, 192, 7, 9),
+                                             (4, 256, 128, 14, 14), (2, 64, 256, 56, 56)])
+def test_conv3x3_weight_gradient_kernel(dph_native, N_img, C, Co, H, W):
+    """ts_gemm_tn_ on the 3x3 path (the LDS-DMA split-pixel kernel, padding taps zero-filled by the DMA) vs the fp32
+    weight gradient of F.conv2d on the same bf16 operands; [Cout, (kh, kw, Cin)] layout."""
+    from distributed_pytorch_hpc_amd.ops import _lib
+
+    torch.manual_seed(7)
+    x = torch.randn(N_img, C, H, W, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    gy = torch.randn(N_img, Co, H, W, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x2 = x.permute(0, 2, 3, 1).reshape(-1, C)
+    g2 = gy.permute(0, 2, 3, 1).reshape(-1, Co)
+    gk = torch.empty(Co, 9 * C, device=DEV, dtype=torch.float32)
+    _lib.ops().ts_gemm_tn_(gk, g2, x2, False, H, W)
+    ref = torch.nn.grad.conv2d_weight(x.float(), (Co, C, 3, 3), gy.float(), padding=1)
+    got = gk.view(Co, 3, 3, C).permute(0, 3, 1, 2)
+    assert rel_err(got, ref) < 2e-3
+    gk2 = gk.clone()
+    _lib.ops().ts_gemm_tn_(gk2, g2, x2, True, H, W)          # accumulate
+    assert rel_err(gk2, 2 * gk) < 1e-5
+
+
 @pytest.mark.parametrize("M_img,C,Co,H,W", [(3, 64, 128, 10, 11), (2, 128, 64, 28, 28)])
 def test_conv3x3_stats_epilogue(dph_native, M_img, C, Co, H, W):
     """ts_gemm_nt_stats on the 3x3 path: the per-128-row-block [mean | M2 | rows] partials of the bf16 output."""
