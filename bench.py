@@ -82,6 +82,8 @@ def parse(argv=None):
                     help="process-group backend (default: nccl = RCCL on GPU); gloo lets several ranks share one GPU "
                          "to rehearse the N > 1 path (tests/test_bench_gpu.py)")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each step as one HIP graph after the warm-up (runtime/graphs.py; one rank only)")
     ap.add_argument("--fp8", action="store_true",
                     help="opt-in FP8 GEMMs for the projections (ops/fp8.py; e4m3 activations/weights, e5m2 gradients, "
                          "LM head bf16). Reported with dtype 'bf16+fp8-gemm' -- not the bf16 headline number")
@@ -158,6 +160,21 @@ def main(argv=None):
             _fail(3, f"rank {rank}: collective self-test failed: {e}")
 
     wl = BUILDERS[args.layout](args, rank, world, dev, log)
+    graph_info = {}
+    if args.graph:
+        if world > 1 or cpu:
+            _fail(2, "--graph: whole-step graph capture is a one-rank GPU option")
+        import types
+
+        from distributed_pytorch_hpc_amd.runtime.graphs import GraphedStep
+
+        eager_step = wl.step
+        runner = GraphedStep(lambda: eager_step(0), optimizer=types.SimpleNamespace(engine=wl.engine),
+                             warmup=max(1, args.warmup - 1))
+        wl.step = lambda i: runner()
+        graph_info = {"graph": "whole step replayed as one HIP graph (captured during the warm-up)"}
+        if args.warmup < 2:
+            _fail(2, "--graph needs --warmup >= 2 (eager warm-up + capture)")
 
     def sync_all():
         sync()
@@ -233,7 +250,7 @@ def main(argv=None):
             "world": world,
             "process_group": dist.get_backend() if dist.is_initialized() else None,
             "rccl_version": preflight.rccl_version() if not cpu else None,
-            **pre, **replica, **wl.extra,
+            **pre, **replica, **wl.extra, **graph_info,
         }
         if wl.flops_per_item:
             rec["mfu_vs_2.5PF_bf16_dense"] = round(rate / world * wl.flops_per_item / 2.5e15, 4)

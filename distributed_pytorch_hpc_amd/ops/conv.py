@@ -10,13 +10,15 @@ of its convolution time, benchmarks/conv_bench.py).  Strided convolutions and th
 (or bf16-autocast) channels-last inputs on the GPU with channel counts that are multiples of 64, and falls back
 to ``F.conv2d`` otherwise.  ``DPH_CONV1X1=0`` disables the kernel path (A/B runs).
 
-``Conv3x3`` does the same for stride-1 / padding-1 3x3 convolutions as implicit GEMMs (K = 9 * Cin, tap-major,
-input rows shifted per tap with zero padding in the kernel): forward and input gradient on the same kernel
-(the input gradient is a 3x3 convolution of dY with the spatially flipped, channel-transposed weight), weight
-gradient on the split-pixel kernel with the input shifted per output tap.  It is opt-in (``DPH_CONV3X3=1``):
-measured 0.51-0.63 ms vs MIOpen's 0.38-0.53 ms per ResNet-50 shape (fwd + bwd, B=256,
-profiles/conv_bench_with_3x3.json) -- the one-barrier-per-K-step structure tops out near 0.5 PFLOP/s on these
-compute-heavier shapes, so MIOpen keeps the 3x3 convolutions by default.
+``Conv3x3`` does the same for stride-1 / padding-1 3x3 convolutions as implicit GEMMs (K = 9 * Cin, tap-major):
+forward and input gradient on the LDS-DMA kernel of csrc/conv3x3.hip (the input gradient is a 3x3 convolution of dY
+with the spatially flipped, channel-transposed weight; padding taps are zero-filled by range-checked buffer DMA; an
+epilogue emits the following BatchNorm's statistics or adds a bias): 440-810 TFLOP/s vs MIOpen's 370-780 on the
+ResNet-50 / SimpleUNet shapes (profiles/r3/conv3_bench_oob.json), on by default (``DPH_CONV3X3=0``: MIOpen).  The
+weight gradient runs on MIOpen by default (318-491 TFLOP/s vs 241-357 for the LDS-DMA split-pixel kernel and 302-324 for
+the older register-staged one, profiles/r3/conv3_bench_c3w_wgrad.json / _tsw_wgrad.json); ``DPH_CONV3_WGRAD=dph``
+selects the kernel.  Round 2's register-staged forward (``DPH_CONV3_KERNEL=ts``) measured 0.51-0.63 ms vs MIOpen's
+0.38-0.53 ms per shape and stayed off.
 """
 from __future__ import annotations
 
@@ -168,7 +170,9 @@ class _Conv1x1Fn(torch.autograd.Function):
 
 
 _CONV3_WGRAD = os.environ.get("DPH_CONV3_WGRAD", "miopen")
-_CONV3X3_DEFAULT = "0"   # DPH_CONV3X3=1: stride-1 3x3 convolutions on csrc/conv3x3.hip
+# stride-1 3x3 convolutions on csrc/conv3x3.hip by default: ResNet-50 FSDP bf16 B=256 9 472 / 9 513 vs 9 258 / 9 278
+# img/s on MIOpen (interleaved A/B on one MI355X, profiles/r3/ab_conv3x3/); DPH_CONV3X3=0 = MIOpen
+_CONV3X3_DEFAULT = "1"
 
 
 def _conv3_stats_ok() -> bool:
