@@ -169,7 +169,9 @@ def main(argv=None):
         from distributed_pytorch_hpc_amd.runtime.graphs import GraphedStep
 
         eager_step = wl.step
-        runner = GraphedStep(lambda: eager_step(0), optimizer=types.SimpleNamespace(engine=wl.engine),
+        # the captured step returns a detached loss: an autograd graph kept alive across the capture (the loss of
+        # the previous step) makes AccumulateGrad run on the wrong stream
+        runner = GraphedStep(lambda: eager_step(0).detach(), optimizer=types.SimpleNamespace(engine=wl.engine),
                              warmup=max(1, args.warmup - 1))
         wl.step = lambda i: runner()
         graph_info = {"graph": "whole step replayed as one HIP graph (captured during the warm-up)"}

@@ -278,7 +278,9 @@ void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     const char* e = getenv("DPH_CONV3_BN");
     return e ? atoi(e) : 0;
   }();
-  const bool wide = N % 128 == 0 && force_bn != 64;
+  // 128-wide tiles unless that leaves fewer than ~1.5 workgroups per CU (SimpleUNet's 22 x 45 bottleneck at B=4:
+  // 124 tiles of 128 vs 248 of 64)
+  const bool wide = N % 128 == 0 && force_bn != 64 && (force_bn == 128 || (int64_t)nmb * (N / 128) >= 384);
   // padding by range-checked buffer DMA (default: 1.0-1.2x the register-zeroing form on every ResNet-50 / UNet shape,
   // profiles/r3/conv3_bench_*.json); DPH_CONV3_ZERO=mask selects the register form
   static const bool zb = [] {
