@@ -468,7 +468,7 @@ void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const 
   else if (rdt == kBF16) DPH_BN_FIN(float, bf16);
   else DPH_BN_FIN(float, float);
 #undef DPH_BN_FIN
-  bn_apply(x, res, scale, shift, y, M, C, relu, dt, st, relu_mask);
+  if (y != nullptr) bn_apply(x, res, scale, shift, y, M, C, relu, dt, st, relu_mask);   // null: folded into the consumer
 }
 
 void bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int64_t M, int64_t C,

@@ -49,18 +49,38 @@ constexpr int TS_KF = TS_BK / 16;   // MFMA k-steps (A fragments) per K-step
 // mb and column n, stats[mb * N + n] = mean, stats[nmb * N + mb * N + n] = M2 (sum of squared deviations),
 // stats[2 * nmb * N + mb] = rows -- the partial layout bn_finalize_k merges (Chan), so the BN that follows a
 // 1x1 convolution skips its own statistics pass over the activation.
-template <int BN, bool C3, bool ADD = false, bool STATS = false>
+// PRO: the A operand is the raw input of a training-mode BatchNorm + ReLU (the bottleneck's bn2 -> conv3): every A
+// element is replaced by relu(a * scale[k] + shift[k]) (pro_ss = fp32 [scale K | shift K], the BatchNorm's forward
+// coefficients) after it lands in registers, so the normalised activation is never written to HBM.
+template <int BN, bool C3, bool ADD = false, bool STATS = false, bool PRO = false>
 __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                  bf16* __restrict__ C, int M, int N, int K, int64_t lda,
                                                  int64_t ldb, int64_t ldc, int H, int W, int Cin,
                                                  const bf16* __restrict__ D = nullptr,
-                                                 float* __restrict__ stats = nullptr) {
+                                                 float* __restrict__ stats = nullptr,
+                                                 const float* __restrict__ pro_ss = nullptr) {
   constexpr int NT = BN / 32;                        // 32-column tiles per wave
   constexpr int BCH = BN * (TS_BK / 8) / TS_NT;      // 16-B B chunks per thread per K-step (BN=128: 4)
   constexpr int CROW = BN + 8;                       // epilogue LDS row (bf16)
   constexpr int LDS_B = 2 * BN * TS_BROW * 2, LDS_C = TS_BM * CROW * 2 + (STATS ? 4 * BN * 4 : 0);
   __shared__ __attribute__((aligned(16))) char smem[LDS_B > LDS_C ? LDS_B : LDS_C];
+  __shared__ __attribute__((aligned(16))) float pss[PRO ? 2 * 2048 : 4];   // [scale K | shift K] (K <= 2048)
   bf16* Bs = reinterpret_cast<bf16*>(smem);
+  if constexpr (PRO) {
+    for (int i = threadIdx.x; i < 2 * K; i += TS_NT) pss[i] = pro_ss[i];   // visible after the first barrier
+  }
+  // relu(a * scale + shift) of the 8 consecutive channels k0.. of an A fragment, from the LDS copy
+  auto pro = [&](bf16x8 v, int k0) -> bf16x8 {
+    const f32x4 s0 = *reinterpret_cast<const f32x4*>(pss + k0), s1 = *reinterpret_cast<const f32x4*>(pss + k0 + 4);
+    const f32x4 t0 = *reinterpret_cast<const f32x4*>(pss + K + k0), t1 = *reinterpret_cast<const f32x4*>(pss + K + k0 + 4);
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[i] = (bf16)fmaxf(fmaf((float)v[i], s0[i], t0[i]), 0.f);
+      o[i + 4] = (bf16)fmaxf(fmaf((float)v[i + 4], s1[i], t1[i]), 0.f);
+    }
+    return o;
+  };
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l32 = lane & 31, h = lane >> 5;
   const int ntn = N / BN, nmb = (M + TS_BM - 1) / TS_BM;
@@ -129,6 +149,10 @@ __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, con
       for (int c = 0; c < BCH; ++c) bst[c] = *reinterpret_cast<const bf16x8*>(bp[c] + ko);
     }
     const bf16* bs = Bs + cur * BN * TS_BROW;
+    if constexpr (PRO) {   // this K-step's fragments have landed (the MFMAs below consume them anyway)
+#pragma unroll
+      for (int f = 0; f < TS_KF; ++f) a[f] = pro(a[f], ks * TS_BK + 16 * f + 8 * h);
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const bf16* br = bs + (t * 32 + l32) * TS_BROW + 8 * h;
@@ -235,10 +259,15 @@ __device__ __forceinline__ bf16x4 tr_read(const char* p) {
 
 // C3: 3x3 weight gradient, K = 9 * Cin tap-major; B rows (input pixels) are shifted by the output tile's tap and
 // zero outside the image, A (output-gradient) rows are not shifted.
-template <bool C3>
+// PRO (1x1 only): B is the raw input of a training-mode BatchNorm + ReLU; each staged B element becomes
+// relu(b * scale[k] + shift[k]) (pro_ss = [scale K | shift K]) on its way into LDS.  A thread's B columns are fixed for
+// the whole loop, so its 8 scales / shifts live in registers.  Rows past the chunk keep dY = 0, so their transformed
+// B values contribute nothing.
+template <bool C3, bool PRO = false>
 __global__ __launch_bounds__(256) void ts_tn_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                float* __restrict__ P, int M, int N, int K, int64_t lda,
-                                               int64_t ldb, int chunk, int H, int W, int Cin) {
+                                               int64_t ldb, int chunk, int H, int W, int Cin,
+                                               const float* __restrict__ pro_ss = nullptr) {
   constexpr int TP = 64;   // pixels per step (rows of the staged slabs)
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * TP * TW_ROWB];   // [buf][A|B][64 rows][128 B]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -296,11 +325,24 @@ __global__ __launch_bounds__(256) void ts_tn_k(const bf16* __restrict__ A, const
       }
     }
   };
+  float psc[8], psh[8];
+  if constexpr (PRO) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      psc[i] = pro_ss[bcol + sch * 8 + i];
+      psh[i] = pro_ss[K + bcol + sch * 8 + i];
+    }
+  }
   auto stage = [&](char* base, const bf16x8 (&va)[2], const bf16x8 (&vb)[2]) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       *reinterpret_cast<bf16x8*>(base + sdst + 32 * u * TW_ROWB) = va[u];
-      *reinterpret_cast<bf16x8*>(base + TP * TW_ROWB + sdst + 32 * u * TW_ROWB) = vb[u];
+      bf16x8 b = vb[u];
+      if constexpr (PRO) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) b[i] = (bf16)fmaxf(fmaf((float)b[i], psc[i], psh[i]), 0.f);
+      }
+      *reinterpret_cast<bf16x8*>(base + TP * TW_ROWB + sdst + 32 * u * TW_ROWB) = b;
     }
   };
   bf16x8 va[2], vb[2];
@@ -502,10 +544,26 @@ bool conv1x1_supported(int64_t M, int64_t N, int64_t K) {
 }
 
 void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, hipStream_t st, int H, int W, const void* D, float* stats) {
+                int64_t ldc, hipStream_t st, int H, int W, const void* D, float* stats, const float* pro_ss) {
   const int nmb = (int)cdiv(M, TS_BM);
   const bool c3 = H > 0;
   const int cin = c3 ? (int)(K / 9) : 0;
+  if (pro_ss != nullptr) {   // BatchNorm-apply + ReLU prologue on A (1x1 only, K <= 2048; host-checked)
+    const bool w128 = N % 128 == 0;
+#define DPH_TS_PRO(BN_, ST_)                                                                                     \
+    hipLaunchKernelGGL((ts_nt_k<BN_, false, false, ST_, true>), dim3(nmb * (int)(N / BN_)), dim3(TS_NT), 0, st,    \
+                       (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, 0, 0, 0,     \
+                       (const bf16*)nullptr, stats, pro_ss)
+    if (stats) {
+      if (w128) DPH_TS_PRO(128, true);
+      else DPH_TS_PRO(64, true);
+    } else {
+      if (w128) DPH_TS_PRO(128, false);
+      else DPH_TS_PRO(64, false);
+    }
+#undef DPH_TS_PRO
+    return;
+  }
 #define DPH_TS_NT(BN_, C3_)                                                                                     \
   hipLaunchKernelGGL((ts_nt_k<BN_, C3_>), dim3(nmb * (int)(N / BN_)), dim3(TS_NT), 0, st, (const bf16*)A,       \
                      (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin)
@@ -604,7 +662,8 @@ int c3w_splits(int64_t M, int64_t N, int64_t K) {
 }
 
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
-                int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t st, int H, int W) {
+                int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t st, int H, int W,
+                const float* pro_ss) {
   const int64_t tiles = (N / 64) * (K / 64);
   int64_t chunk = cdiv(M, nsplit);
   chunk = cdiv(chunk, 64) * 64;
@@ -618,6 +677,9 @@ void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M
       hipLaunchKernelGGL((c3w_k<64>), dim3((int)((N / 64) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,
                          (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, H, W,
                          cin);
+  } else if (pro_ss != nullptr && H == 0) {
+    hipLaunchKernelGGL((ts_tn_k<false, true>), dim3((int)(tiles * nsplit)), dim3(256), 0, st, (const bf16*)A,
+                       (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0, 0, pro_ss);
   } else if (H > 0)
     hipLaunchKernelGGL((ts_tn_k<true>), dim3((int)(tiles * nsplit)), dim3(256), 0, st, (const bf16*)A,
                        (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, H, W, (int)(K / 9));

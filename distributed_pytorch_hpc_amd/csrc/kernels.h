@@ -153,9 +153,11 @@ void gemm_nt_set_variant(int v);
 // fp32 partials over nsplit pixel chunks (partial: nsplit * N * K floats; ts_gemm_tn_splits picks nsplit).
 bool conv1x1_supported(int64_t M, int64_t N, int64_t K);
 // H, W > 0: 3x3 / stride-1 / pad-1 implicit GEMM over a channels-last [M = n*H*W, K/9] input (K tap-major).
+// pro_ss (1x1 only): fp32 [scale K | shift K]; A (nt) / B (tn) elements enter the product as relu(v * scale + shift)
+// -- a training-mode BatchNorm + ReLU folded into the convolution's operand load.
 void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, hipStream_t stream, int H = 0, int W = 0,
-                const void* D = nullptr, float* stats = nullptr);
+                const void* D = nullptr, float* stats = nullptr, const float* pro_ss = nullptr);
 // 3x3 implicit GEMM with an LDS-DMA pipeline (csrc/conv3x3.hip); ts_gemm_nt's H, W > 0 path when supported.
 bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
@@ -166,7 +168,7 @@ bool c3w_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 int c3w_splits(int64_t M, int64_t N, int64_t K);
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
                 int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t stream, int H = 0,
-                int W = 0);
+                int W = 0, const float* pro_ss = nullptr);
 
 // Fused BatchNorm(train) [+ residual] [+ ReLU] on channels-last [M, C] activations (C power of two, 8..2048).
 // Workspaces (fp32): forward 2*G*C + G, backward 2*G*C + 3*C floats with G = bn_partial_blocks(M, C).

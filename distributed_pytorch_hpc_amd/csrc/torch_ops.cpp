@@ -638,8 +638,18 @@ std::vector<int64_t> gemm_tn_plan_info(int64_t M, int64_t N, int64_t K) {
 // H, W > 0: 3x3 / stride-1 / pad-1 convolution as implicit GEMM, A = channels-last input [n*H*W, Cin],
 // B = weights [Cout, 9 * Cin] (tap-major).
 // add (optional): C = A B^T + add, add [M, N] bf16 row-major (a residual branch's gradient merged in the epilogue)
+// BatchNorm + ReLU prologue coefficients of a 1x1 convolution's input: fp32 [scale K | shift K], K <= 2048
+const float* pro_ptr(const c10::optional<Tensor>& pro_ss, int64_t K, int64_t H, const Tensor& like) {
+  if (!pro_ss.has_value()) return nullptr;
+  TORCH_CHECK(H == 0 && K <= 2048, "ts_gemm: the BatchNorm prologue is a 1x1 (H = 0), K <= 2048 feature");
+  TORCH_CHECK(pro_ss->scalar_type() == at::kFloat && pro_ss->is_contiguous() && pro_ss->numel() == 2 * K &&
+                  pro_ss->device() == like.device(),
+              "ts_gemm: pro_ss must be a contiguous fp32 [2 * K] tensor ([scale | shift])");
+  return pro_ss->data_ptr<float>();
+}
+
 Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W, const c10::optional<Tensor>& add,
-                  const c10::optional<Tensor>& bias) {
+                  const c10::optional<Tensor>& bias, const c10::optional<Tensor>& pro_ss) {
   check_cuda(A, "A");
   c10::DeviceGuard g(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2, "ts_gemm_nt: 2-D operands required");
@@ -673,13 +683,16 @@ Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W, const 
                     (int)H, (int)W, cur_stream(), nullptr, bias->data_ptr<float>());
     return C;
   }
+  const float* pro = pro_ptr(pro_ss, K, H, A);
+  TORCH_CHECK(pro == nullptr || D == nullptr, "ts_gemm_nt: add and pro_ss are exclusive");
   dph::ts_gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
-                  cur_stream(), (int)H, (int)W, D);
+                  cur_stream(), (int)H, (int)W, D, nullptr, pro);
   return C;
 }
 
 // C = A B^T plus the BatchNorm statistics partials of C per 128-row block ([mean | M2 | rows], see conv1x1.hip).
-std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B, int64_t H, int64_t W) {
+std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B, int64_t H, int64_t W,
+                                            const c10::optional<Tensor>& pro_ss) {
   check_cuda(A, "A");
   c10::DeviceGuard g(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
@@ -698,13 +711,14 @@ std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B, in
   Tensor C = at::empty({M, N}, A.options());
   Tensor st = at::empty({2 * nmb * N + nmb}, A.options().dtype(at::kFloat));
   dph::ts_gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
-                  cur_stream(), (int)H, (int)W, nullptr, st.data_ptr<float>());
+                  cur_stream(), (int)H, (int)W, nullptr, st.data_ptr<float>(), pro_ptr(pro_ss, K, H, A));
   return {C, st};
 }
 
 // C[N, K] (+)= A[M, N]^T B[M, K] (1x1 convolution weight gradient, split over pixel chunks).
 // H, W > 0: 3x3 weight gradient, C [N, 9 * K_in] tap-major, B = channels-last input [n*H*W, K_in].
-void ts_gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate, int64_t H, int64_t W) {
+void ts_gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate, int64_t H, int64_t W,
+                 const c10::optional<Tensor>& pro_ss) {
   check_cuda(A, "A");
   c10::DeviceGuard g(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "ts_gemm_tn: 2-D operands required");
@@ -722,7 +736,7 @@ void ts_gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate, in
                                                                                   : dph::ts_gemm_tn_splits(M, N, K);
   Tensor part = at::empty({(int64_t)ns * N * K}, A.options().dtype(at::kFloat));
   dph::ts_gemm_tn(A.data_ptr(), B.data_ptr(), part.data_ptr<float>(), C.data_ptr(), M, N, K, A.stride(0),
-                  B.stride(0), ns, dt_code(C), accumulate, cur_stream(), (int)H, (int)W);
+                  B.stride(0), ns, dt_code(C), accumulate, cur_stream(), (int)H, (int)W, pro_ptr(pro_ss, K, H, A));
 }
 
 // Select the wgrad kernel's MFMA shape (16 or 32; anything else re-reads DPH_WGRAD_MFMA); returns the active shape.
@@ -874,7 +888,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
                                               double momentum, double eps, bool relu,
                                               const c10::optional<Tensor>& pre_stats,
                                               const c10::optional<Tensor>& num_batches_tracked,
-                                              const c10::optional<Tensor>& relu_mask_out) {
+                                              const c10::optional<Tensor>& relu_mask_out, bool apply) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
   const int64_t C = bn_channels(x), M = x.numel() / C;
@@ -886,7 +900,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
                                     rmean->scalar_type() == rvar->scalar_type()),
               "bn_act: running stats [C] (both or none)");
   auto fopt = x.options().dtype(at::kFloat);
-  auto y = at::empty_like(x);
+  // apply = false: statistics, running-stat update and [scale | shift] only -- the consumer folds the apply into its
+  // operand load (ts_gemm_nt / ts_gemm_tn_ pro_ss)
+  TORCH_CHECK(apply || (!res.has_value() && !relu_mask_out.has_value()), "bn_act_fwd: apply=False takes no residual");
+  auto y = apply ? at::empty_like(x) : at::empty({0}, x.options());
   auto mean = at::empty({C}, fopt), invstd = at::empty({C}, fopt);
   auto ss = at::empty({2 * C}, fopt);   // [scale | shift]: the backward recomputes the ReLU mask from them
   const Tensor* pre = pre_stats.has_value() ? &*pre_stats : nullptr;
@@ -918,7 +935,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
   auto ws = at::empty({2 * (int64_t)G * C + G}, fopt);
   const int pdt = w ? dt_code(*w) : (b ? dt_code(*b) : dph::kF32);
   const int rdt = rmean ? dt_code(*rmean) : dph::kF32;
-  dph::bn_fwd_train(x.data_ptr(), res ? res->data_ptr() : nullptr, y.data_ptr(), w ? w->data_ptr() : nullptr,
+  dph::bn_fwd_train(x.data_ptr(), res ? res->data_ptr() : nullptr, apply ? y.data_ptr() : nullptr,
+                    w ? w->data_ptr() : nullptr,
                     b ? b->data_ptr() : nullptr, rmean ? rmean->data_ptr() : nullptr,
                     rvar ? rvar->data_ptr() : nullptr, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                     ss.data_ptr<float>(), ss.data_ptr<float>() + C, ws.data_ptr<float>(), M, C, (float)momentum,
@@ -1238,9 +1256,10 @@ TORCH_LIBRARY(dph, m) {
   m.def("gemm_tn_tail_(int cus) -> ()", &gemm_tn_tail_);                          // catch-all kernels
   m.def("gemm_tn_plan_info(int M, int N, int K) -> int[]", &gemm_tn_plan_info);
   m.def("gemm_tn_mfma_(int shape) -> int", &gemm_tn_mfma_);   // no tensor argument: catch-all kernel
-  m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0, Tensor? add=None, Tensor? bias=None) -> Tensor");
-  m.def("ts_gemm_nt_stats(Tensor A, Tensor B, int H=0, int W=0) -> (Tensor, Tensor)");
-  m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0) -> ()");
+  m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0, Tensor? add=None, Tensor? bias=None, Tensor? pro_ss=None) "
+        "-> Tensor");
+  m.def("ts_gemm_nt_stats(Tensor A, Tensor B, int H=0, int W=0, Tensor? pro_ss=None) -> (Tensor, Tensor)");
+  m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0, Tensor? pro_ss=None) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
@@ -1249,7 +1268,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("upcat_bwd(Tensor dcat, int H, int W, int Co) -> (Tensor, Tensor)");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
         "float momentum, float eps, bool relu, Tensor? pre_stats=None, Tensor(c!)? num_batches_tracked=None, "
-        "Tensor(d!)? relu_mask_out=None) "
+        "Tensor(d!)? relu_mask_out=None, bool apply=True) "
         "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "

@@ -19,6 +19,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.batchnorm import bn_relu_conv1x1, bn_relu_conv1x1_ok
 from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot, StemConv2d, grad_tap
 from ..ops.pool import MaxPool2d
 
@@ -80,12 +81,15 @@ class Bottleneck(nn.Module):
             # conv1's: the tap parks the branch's gradient of x for conv1's dgrad epilogue (no separate add over x)
             tapped = grad_tap(x, slot) if slot is not None and slot.consumer else x
             idt, res_slot = self.downsample(tapped), None
-        if isinstance(self.conv2, Conv3x3):
-            s2 = StatsSlot() if self.bn2.training else None
-            out = self.bn2(self.conv2(out, stats_slot=s2), stats_slot=s2)
+        s2 = StatsSlot() if isinstance(self.conv2, Conv3x3) and self.bn2.training else None
+        out = self.conv2(out, stats_slot=s2) if s2 is not None else self.conv2(out)
+        if bn_relu_conv1x1_ok(self.bn2, self.conv3, out):
+            # bn2's apply + ReLU folded into conv3's operand loads (forward and weight gradient): the normalised
+            # activation is never written (ops.batchnorm._BNReLUConv1x1Fn)
+            out = bn_relu_conv1x1(self.bn2, self.conv3, out, s2, s3)
         else:
-            out = self.bn2(self.conv2(out))
-        return self.bn3(self.conv3(out, stats_slot=s3), idt, residual_grad_slot=res_slot, stats_slot=s3)
+            out = self.conv3(self.bn2(out, stats_slot=s2), stats_slot=s3)
+        return self.bn3(out, idt, residual_grad_slot=res_slot, stats_slot=s3)
 
 
 class ResNet(nn.Module):

@@ -75,9 +75,9 @@ def _sumsq(x, out):
 
 @register_fake("dph::bn_act_fwd")
 def _bn_act_fwd(x, res, w, b, rm, rv, momentum, eps, relu, pre_stats=None, num_batches_tracked=None,
-                relu_mask_out=None):
+                relu_mask_out=None, apply=True):
     c = x.shape[1]
-    return (torch.empty_like(x), x.new_empty((c,), dtype=torch.float32), x.new_empty((c,), dtype=torch.float32),
+    return (torch.empty_like(x) if apply else x.new_empty((0,)), x.new_empty((c,), dtype=torch.float32), x.new_empty((c,), dtype=torch.float32),
             x.new_empty((2 * c,), dtype=torch.float32))
 
 
@@ -177,19 +177,19 @@ def _gemm_tn(C, A, B, accumulate):
 
 
 @register_fake("dph::ts_gemm_nt")
-def _ts_gemm_nt(A, B, H=0, W=0, add=None, bias=None):
+def _ts_gemm_nt(A, B, H=0, W=0, add=None, bias=None, pro_ss=None):
     return A.new_empty((A.shape[0], B.shape[0]))
 
 
 @register_fake("dph::ts_gemm_nt_stats")
-def _ts_gemm_nt_stats(A, B, H=0, W=0):
+def _ts_gemm_nt_stats(A, B, H=0, W=0, pro_ss=None):
     M, N = A.shape[0], B.shape[0]
     nmb = (M + 127) // 128
     return A.new_empty((M, N)), A.new_empty((2 * nmb * N + nmb,), dtype=torch.float32)
 
 
 @register_fake("dph::ts_gemm_tn_")
-def _ts_gemm_tn(C, A, B, accumulate, H=0, W=0):
+def _ts_gemm_tn(C, A, B, accumulate, H=0, W=0, pro_ss=None):
     return None
 
 

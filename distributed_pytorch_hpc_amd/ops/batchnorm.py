@@ -10,6 +10,8 @@ resnet_fsdp_training.py:186-191) whose conv -> BN -> ReLU (+ identity) blocks th
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
@@ -142,3 +144,89 @@ class BatchNormAct2d(nn.BatchNorm2d):
 
     def extra_repr(self):
         return super().extra_repr() + f", act={'relu' if self.act else 'none'}"
+
+
+# ------------------------------------------------------------------------------------------------ BN + ReLU -> 1x1 conv
+_PROLOGUE = os.environ.get("DPH_BN_PROLOGUE", "1") != "0"
+
+
+class _BNReLUConv1x1Fn(torch.autograd.Function):
+    """``conv1x1(relu(bn(x)))`` in training mode with the BatchNorm apply + ReLU folded into the convolution's operand
+    loads (csrc/conv1x1.hip ``pro_ss``): the statistics pass and the running-stat update run as usual, but the
+    normalised activation is never written -- the forward GEMM and the weight-gradient GEMM both read x and apply
+    ``relu(x * scale + shift)`` in registers, and the BatchNorm backward takes its ReLU mask from x."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, w3, momentum, eps, pre_stats, nbt, stats_slot3):
+        _, mean, invstd, ss = _lib.ops().bn_act_fwd(x, None, weight, bias, running_mean, running_var, momentum, eps,
+                                                     True, pre_stats, nbt, None, False)
+        B, C, H, W = x.shape
+        cout = w3.shape[0]
+        x2 = x.permute(0, 2, 3, 1).reshape(-1, C)                   # channels-last: a view
+        w3b = w3.to(torch.bfloat16) if w3.dtype != torch.bfloat16 else w3
+        w2d = w3b.reshape(cout, C)
+        if stats_slot3 is not None:
+            y2, stats_slot3.stats = _lib.ops().ts_gemm_nt_stats(x2, w2d, 0, 0, ss)
+            stats_slot3.rows, stats_slot3.cols = y2.shape
+        else:
+            y2 = _lib.ops().ts_gemm_nt(x2, w2d, 0, 0, None, None, ss)
+        ctx.save_for_backward(x, ss, mean, invstd, weight, w2d)
+        ctx.params = (weight, bias, w3)
+        ctx.w3dtype = w3.dtype
+        return y2.view(B, H, W, cout).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .conv import _nhwc2d, _wgrad_into_main
+
+        x, ss, mean, invstd, weight, w2d = ctx.saved_tensors
+        wp, bp, w3 = ctx.params
+        B, C, H, W = x.shape
+        cout = w2d.shape[0]
+        x2 = x.permute(0, 2, 3, 1).reshape(-1, C)
+        dy2 = _nhwc2d(dy.to(torch.bfloat16))
+        gw3 = None
+        if ctx.needs_input_grad[5]:
+            def launch(out, acc):
+                _lib.ops().ts_gemm_tn_(out, dy2, x2, acc, 0, 0, ss)   # dW3 = dY^T relu(bn(x))
+
+            if not _wgrad_into_main(w3, (cout, C), launch):
+                gw3 = torch.empty((cout, C), dtype=ctx.w3dtype, device=dy.device)
+                launch(gw3, False)
+                gw3 = gw3.view(cout, C, 1, 1)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dyb = _lib.ops().ts_gemm_nt(dy2, w2d.t().contiguous())   # gradient of relu(bn(x)), [M, C]
+            dyb = dyb.view(B, H, W, C).permute(0, 3, 1, 2)
+            need_wb = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+            direct = (need_wb and bp is not None and _DIRECT and all(
+                getattr(p, "main_grad", None) is not None and not getattr(p, "_dph_accum", True)
+                and p.main_grad.is_contiguous() and p.main_grad.dtype == p.dtype for p in (wp, bp)))
+            dx, _, dw, db = _lib.ops().bn_act_bwd(dyb, x, x, mean, invstd, weight, True, False, need_wb, ss,
+                                                  wp.main_grad if direct else None, bp.main_grad if direct else None,
+                                                  None)
+            if direct:
+                for p in (wp, bp):
+                    p._dph_accum = True
+                    p._dph_grad_ready()
+                dw = db = None
+            if not need_wb:
+                dw = db = None
+        return dx, dw, db, None, None, gw3, None, None, None, None, None
+
+
+def bn_relu_conv1x1_ok(bn: "BatchNormAct2d", conv, x: torch.Tensor) -> bool:
+    from .conv import Conv1x1, conv1x1_native_ok
+
+    return (_PROLOGUE and isinstance(conv, Conv1x1) and bn.training and bn.track_running_stats and bn.act
+            and bn.momentum is not None and bn.affine and x.dtype == torch.bfloat16 and x.shape[1] <= 2048
+            and _native_ok(x, None) and conv1x1_native_ok(x, conv.weight) and torch.is_grad_enabled())
+
+
+def bn_relu_conv1x1(bn: "BatchNormAct2d", conv, x: torch.Tensor, stats_slot=None, out_stats_slot=None):
+    """``conv(bn(x))`` for a training-mode ``BatchNormAct2d`` (ReLU) followed by a stride-1 ``Conv1x1``, the apply
+    folded into the convolution (see _BNReLUConv1x1Fn); ``stats_slot`` holds x's statistics from its producer's
+    epilogue, ``out_stats_slot`` receives the convolution output's statistics for the next BatchNorm."""
+    pre = stats_slot.take(x.numel() // x.shape[1], x.shape[1]) if stats_slot is not None else None
+    return _BNReLUConv1x1Fn.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, conv.weight, bn.momentum,
+                                  bn.eps, pre, bn.num_batches_tracked, out_stats_slot)

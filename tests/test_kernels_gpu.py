@@ -852,6 +852,57 @@ def test_conv3x3_weight_gradient_kernel(dph_native, N_img, C, Co, H, W):
     assert rel_err(gk2, 2 * gk) < 1e-5
 
 
+@pytest.mark.parametrize("M,K,N", [(1000, 64, 256), (4096, 128, 512), (777, 512, 128)])
+def test_tall_skinny_bn_prologue(dph_native, M, K, N):
+    """ts_gemm_nt / ts_gemm_tn_ with the BatchNorm-apply + ReLU prologue (pro_ss) vs materialising relu(x s + t)."""
+    from distributed_pytorch_hpc_amd.ops import _lib
+
+    torch.manual_seed(8)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.1).to(torch.bfloat16)
+    ss = torch.cat([torch.rand(K, device=DEV) + 0.5, torch.randn(K, device=DEV) * 0.3])
+    xa = torch.relu(x.float() * ss[:K] + ss[K:]).to(torch.bfloat16)       # what the unfused BN apply writes
+    y = _lib.ops().ts_gemm_nt(x, w, 0, 0, None, None, ss)
+    assert rel_err(y, _lib.ops().ts_gemm_nt(xa, w)) < 2e-3   # fused fma vs torch's mul + add: rare 1-ulp operand diffs
+    y2, st = _lib.ops().ts_gemm_nt_stats(x, w, 0, 0, ss)
+    assert torch.equal(y2, y)
+    dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    g = torch.zeros(N, K, device=DEV)
+    _lib.ops().ts_gemm_tn_(g, dy, x, False, 0, 0, ss)
+    ref = dy.float().t() @ xa.float()
+    assert rel_err(g, ref) < 2e-3
+
+
+def test_bottleneck_bn_prologue_matches_unfused(dph_native, monkeypatch):
+    """Bottleneck training step with bn2's apply folded into conv3 vs the unfused modules: output, every parameter
+    gradient and bn2's running statistics."""
+    from distributed_pytorch_hpc_amd.models.resnet import Bottleneck
+    from distributed_pytorch_hpc_amd.ops import batchnorm as bnmod
+
+    torch.manual_seed(9)
+    block = Bottleneck(256, 64).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x0 = torch.randn(4, 256, 28, 28, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    state0 = {k: v.clone() for k, v in block.state_dict().items()}
+
+    def run(fused):
+        monkeypatch.setattr(bnmod, "_PROLOGUE", fused)
+        block.load_state_dict(state0)
+        block.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        y = block(x)
+        y.float().pow(2).mean().backward()
+        return (y.float().clone(), x.grad.float().clone(), {n: p.grad.float().clone() for n, p in block.named_parameters()},
+                block.bn2.running_mean.float().clone(), block.bn2.running_var.float().clone(),
+                int(block.bn2.num_batches_tracked))
+
+    y0, gx0, g0, rm0, rv0, n0 = run(False)
+    y1, gx1, g1, rm1, rv1, n1 = run(True)
+    assert rel_err(y1, y0) < 1e-2 and rel_err(gx1, gx0) < 3e-2
+    for n in g0:
+        assert rel_err(g1[n], g0[n]) < 5e-2, n
+    assert rel_err(rm1, rm0) < 1e-3 and rel_err(rv1, rv0) < 1e-3 and n1 == n0
+
+
 @pytest.mark.parametrize("M_img,C,Co,H,W", [(3, 64, 128, 10, 11), (2, 128, 64, 28, 28)])
 def test_conv3x3_stats_epilogue(dph_native, M_img, C, Co, H, W):
     """ts_gemm_nt_stats on the 3x3 path: the per-128-row-block [mean | M2 | rows] partials of the bf16 output."""
