@@ -10,16 +10,18 @@
 //
 // Structure (replaces the register-staged ts_nt_k<.., C3> path of conv1x1.hip, which tops out near 0.5 PFLOP/s with
 // one K-step in flight and A straight from L2 into registers):
-//   * 128 x BN output tile per workgroup (BN = 64 | 128), 4 waves as 2 (M) x 2 (N), wave tile 64 x BN/2,
-//     v_mfma_f32_32x32x16_bf16 with the pixel rows as the A operand;
-//   * K-steps of 64 channels of one tap; both operands staged global -> LDS by LDS-DMA (global_load_lds_dwordx4,
-//     16 B per lane, one 1-KiB piece = 8 rows of 128 B per wave-instruction) into a STAGES-deep ring of XOR-swizzled
-//     images (slot = chunk ^ ((row >> 1) & 7): conflict-free ds_read_b128 fragment reads); the A gather is just the
-//     per-lane DMA source address (the row shifted by the tap); rows whose tap falls outside the image are fetched
-//     from the row itself and their fragments zeroed in registers (v_cndmask), so no padded copy of the input exists;
+//   * 64 WM x BN output tile per workgroup (BN = 64 | 128; WM = 2: 4 waves, two workgroups per CU; WM = 4: 8 waves,
+//     one workgroup per CU), waves as WM (M) x 2 (N), wave tile 64 x BN/2, v_mfma_f32_32x32x16_bf16 with the pixel
+//     rows as the A operand;
+//   * K-steps of 64 channels of one tap; both operands staged global -> LDS by LDS-DMA (16 B per lane, one 1-KiB
+//     piece = 8 rows of 128 B per wave-instruction) into a STAGES-deep ring of XOR-swizzled images
+//     (slot = chunk ^ ((row >> 1) & 7): conflict-free ds_read_b128 fragment reads); the A gather is just the per-lane
+//     DMA source address (the row shifted by the tap), and rows whose tap falls outside the image (or past M) are
+//     zero-filled by the DMA itself -- a range-checked buffer load with an out-of-range offset -- so neither a padded
+//     copy of the input nor any register masking exists;
 //   * one raw s_barrier per K-step, counted vmcnt: STAGES - 1 K-steps stay in flight behind the MFMAs;
 //   * C tile through LDS, written as whole 16-B row segments; workgroups remapped XCD-aware with the N-tiles of one
-//     row block adjacent (they read the same shifted input rows from one L2).
+//     row block adjacent (they read the same shifted input rows from one L2); epilogues: + bias, BN statistics.
 #include "dph_common.h"
 #include "kernels.h"
 
@@ -27,7 +29,8 @@ namespace dph {
 
 namespace {
 
-constexpr int C3_BM = 128, C3_BK = 64, C3_NT = 256;
+constexpr int C3_BK = 64;
+constexpr int kConv3DefaultWm = 2;   // A/B: DPH_CONV3_WM
 constexpr int C3_ROWB = 128;   // LDS image row: 64 bf16
 
 __device__ __forceinline__ f32x16 c3_mfma(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -38,55 +41,59 @@ __device__ __forceinline__ f32x16 c3_mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 __device__ __forceinline__ int c3_off(int r, int c) { return r * C3_ROWB + ((c ^ ((r >> 1) & 7)) << 4); }
 
 // STATS: also the per-128-row-block BatchNorm partials of the bf16 output (the layout of conv1x1.hip's ts_nt_k
-// STATS epilogue: stats[mb * N + n] = mean, stats[nmb * N + mb * N + n] = M2, stats[2 * nmb * N + mb] = rows), so
-// the BatchNorm after the 3x3 convolution skips its statistics pass.
-// ZB: padding taps / rows past M zero-filled by the DMA itself (buffer_load ... lds with an out-of-range offset),
-// instead of fetching the row and zeroing the fragment registers (the default; DPH_CONV3_ZERO=mask for the latter).
-template <int BN, int STAGES, bool STATS = false, bool ZB = false>
-__global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, const bf16* __restrict__ B,
-                                                   bf16* __restrict__ C, int M, int N, int K, int64_t ldx,
-                                                   int64_t ldb, int64_t ldc, int H, int W, int Cin,
-                                                   float* __restrict__ stats, const float* __restrict__ bias) {
-  constexpr int AIMG = C3_BM * C3_ROWB, BIMG = BN * C3_ROWB, STG = AIMG + BIMG;
-  constexpr int AI = C3_BM / 8 / 4;        // A DMA pieces (8 rows) per wave per K-step
-  constexpr int BI = BN / 8 / 4;           // B DMA pieces per wave per K-step
-  static_assert(AI % 2 == 0 && BI % 2 == 0, "piece parity = j parity");
+// STATS epilogue: stats[mb * N + n] = mean, stats[nmb * N + mb * N + n] = M2, stats[2 * nmb * N + mb] = rows, with
+// 128-row blocks mb whatever the tile height), so the BatchNorm after the 3x3 convolution skips its statistics pass.
+// WM: waves along M (2 waves along N): WM = 2 is a 128-row tile of 4 waves (two workgroups per CU), WM = 4 a 256-row
+// tile of 8 waves (one workgroup per CU, 3-stage ring, the weight slab shared by twice the rows).
+// Padding taps and rows past M are zero-filled by the DMA itself (buffer_load ... lds with an out-of-range offset);
+// round 3 measured that 1.0-1.2x faster than fetching the row and zeroing the fragment registers.
+template <int BN, int STAGES, int WM, bool STATS = false>
+__global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16* __restrict__ X,
+                                                                   const bf16* __restrict__ B, bf16* __restrict__ C,
+                                                                   int M, int N, int K, int64_t ldx, int64_t ldb,
+                                                                   int64_t ldc, int H, int W, int Cin,
+                                                                   float* __restrict__ stats,
+                                                                   const float* __restrict__ bias) {
+  constexpr int NWV = 2 * WM, NTH = 64 * NWV, BM = 64 * WM;
+  constexpr int AIMG = BM * C3_ROWB, BIMG = BN * C3_ROWB, STG = AIMG + BIMG;
+  constexpr int AI = BM / 8 / NWV;         // A DMA pieces (8 rows) per wave per K-step (4)
+  constexpr int BI = BN / 8 / NWV;         // B DMA pieces per wave per K-step (1, 2 or 4)
+  static_assert(AI >= 1 && BI >= 1, "DMA pieces");
   constexpr int PER = AI + BI;             // DMA instructions per thread per K-step
   constexpr int WN = BN / 2, NTW = WN / 32;   // wave tile columns, 32-column MFMA tiles per wave
   constexpr int CROW = BN + 8;             // epilogue LDS row (bf16)
-  constexpr int LDS_C = C3_BM * CROW * 2 + (STATS ? 2 * BN * 4 : 0);
+  constexpr int LDS_C = BM * CROW * 2 + (STATS ? 2 * WM * BN * 4 : 0);
   constexpr int LDS = STAGES * STG > LDS_C ? STAGES * STG : LDS_C;
   __shared__ __attribute__((aligned(1024))) char smem[LDS];
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l32 = lane & 31, h = lane >> 5;
   const int wm = wid >> 1, wn = wid & 1;
-  const int ntn = N / BN, nmb = (M + C3_BM - 1) / C3_BM;
+  const int ntn = N / BN, nmb = (M + BM - 1) / BM;
   const int lin = xcd_remap(blockIdx.x, nmb * ntn);
   const int mb = lin / ntn, n0 = (lin % ntn) * BN;
-  const int m0 = mb * C3_BM;
-  const int HW = H * W;
+  const int m0 = mb * BM;
 
-  // ---- DMA lanes: piece j of this wave covers image rows (wid * AI + j) * 8 + lane / 8, slot lane % 8 ----
+  // ---- DMA lanes: piece q = wid * AI + j covers image rows 8 q + lane / 8, LDS slot lane % 8.  Image row 8 q + prow
+  // has (row >> 1) & 7 = (4 q + (prow >> 1)) & 7: the lane's source chunk depends on the parity of q ----
   const int prow = lane >> 3, pslot = lane & 7;
-  int ay[AI], ax[AI], am[AI];
+  const int chunk0 = pslot ^ ((prow >> 1) & 7), chunk1 = pslot ^ (((prow >> 1) + 4) & 7);
+  int ay[AI], ax[AI], am[AI], ach[AI];
   bool arow_in[AI];
 #pragma unroll
   for (int j = 0; j < AI; ++j) {
-    const int r = (wid * AI + j) * 8 + prow;
+    const int q = wid * AI + j, r = q * 8 + prow;
     const int m = min(m0 + r, M - 1);
     arow_in[j] = m0 + r < M;
     am[j] = m;
     ax[j] = m % W;
     ay[j] = (m / W) % H;
+    ach[j] = (q & 1) ? chunk1 : chunk0;
   }
-  // source chunk of a piece's lane: image row r = 8 q + prow has (r >> 1) & 7 = (4 q + (prow >> 1)) & 7, so the chunk
-  // depends on the parity of the piece index q (AI and BI are even: q's parity is j's)
-  const int chunk0 = pslot ^ ((prow >> 1) & 7), chunk1 = pslot ^ (((prow >> 1) + 4) & 7);
   unsigned boff[BI];
 #pragma unroll
   for (int j = 0; j < BI; ++j) {
-    const int r = (wid * BI + j) * 8 + prow;
-    boff[j] = (unsigned)(((int64_t)(n0 + r) * ldb + ((j & 1) ? chunk1 : chunk0) * 8) * 2);
+    const int q = wid * BI + j, r = q * 8 + prow;
+    boff[j] = (unsigned)(((int64_t)(n0 + r) * ldb + ((q & 1) ? chunk1 : chunk0) * 8) * 2);
   }
   const unsigned lds0 = lds_addr(smem);
   const dph_rsrc xres = make_rsrc(X, (unsigned)((int64_t)M * ldx * 2));
@@ -99,14 +106,9 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
     const unsigned sa = lds0 + stage * STG + wid_u * AI * 1024;
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
-      const bool ok = (unsigned)(ay[j] + dy) < (unsigned)H && (unsigned)(ax[j] + dx) < (unsigned)W;
-      if constexpr (ZB) {
-        const unsigned off = (unsigned)(((int64_t)(am[j] + dy * W + dx) * ldx + cb + ((j & 1) ? chunk1 : chunk0) * 8) * 2);
-        lds_dma16_buf(xres, (ok && arow_in[j]) ? off : 0x80000000u, sa + j * 1024);
-      } else {
-        const int src = ok ? am[j] + dy * W + dx : am[j];
-        lds_dma16(X, (unsigned)(((int64_t)src * ldx + cb + ((j & 1) ? chunk1 : chunk0) * 8) * 2), sa + j * 1024);
-      }
+      const bool ok = arow_in[j] && (unsigned)(ay[j] + dy) < (unsigned)H && (unsigned)(ax[j] + dx) < (unsigned)W;
+      const unsigned off = (unsigned)(((int64_t)(am[j] + dy * W + dx) * ldx + cb + ach[j] * 8) * 2);
+      lds_dma16_buf(xres, ok ? off : 0x80000000u, sa + j * 1024);
     }
     const unsigned sb = lds0 + stage * STG + AIMG + wid_u * BI * 1024;
 #pragma unroll
@@ -114,16 +116,6 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
   };
 
   // ---- fragment readers: A rows wm*64 + i*32 + l32 (i < 2), B rows wn*WN + j*32 + l32 ----
-  int fy[2], fx[2];
-  bool fin[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m = m0 + wm * 64 + i * 32 + l32;
-    fin[i] = m < M;
-    const int mm = min(m, M - 1);
-    fx[i] = mm % W;
-    fy[i] = (mm / W) % H;
-  }
   int aoff[2][4], bofs[NTW][4];
 #pragma unroll
   for (int f = 0; f < 4; ++f) {
@@ -154,12 +146,6 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
     // the stage refilled now was read in step ks - 1, which every wave finished before the barrier
     if (ks + STAGES - 1 < nks) issue(ks + STAGES - 1, (ks + STAGES - 1) % STAGES);
     const char* st = smem + (ks % STAGES) * STG;
-    const int tap = ks * C3_BK / Cin;
-    const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-    bool ok[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      ok[i] = fin[i] && (unsigned)(fy[i] + dy) < (unsigned)H && (unsigned)(fx[i] + dx) < (unsigned)W;
     // all fragments of the K-step are read first (one LDS round trip per K-step, consumed in issue order by
     // counted lgkmcnt waits), then the 8 * NTW MFMAs
     bf16x8 a[4][2], b[4][NTW];
@@ -171,14 +157,11 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
       for (int j = 0; j < NTW; ++j) b[f][j] = *reinterpret_cast<const bf16x8*>(st + bofs[j][f]);
     }
 #pragma unroll
-    for (int f = 0; f < 4; ++f) {
+    for (int f = 0; f < 4; ++f)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const bf16x8 av = (ZB || ok[i]) ? a[f][i] : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) acc[i][j] = c3_mfma(av, b[f][j], acc[i][j]);
-      }
-    }
+        for (int j = 0; j < NTW; ++j) acc[i][j] = c3_mfma(a[f][i], b[f][j], acc[i][j]);
   }
   __syncthreads();
   if (bias != nullptr) {   // per-output-channel bias (fp32) on the accumulators: C and its statistics include it
@@ -203,18 +186,22 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
         Cs[(wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CROW + wn * WN + j * 32 + l32] = (bf16)acc[i][j][r];
   __syncthreads();
   constexpr int CPR = BN / 8;
-  for (int i = threadIdx.x; i < C3_BM * CPR; i += C3_NT) {
+  for (int i = threadIdx.x; i < BM * CPR; i += NTH) {
     const int row = i / CPR, ch = i % CPR;
     if (m0 + row < M)
       *reinterpret_cast<bf16x8*>(C + (int64_t)(m0 + row) * ldc + n0 + ch * 8) =
           *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
   }
   if constexpr (STATS) {
-    // pass 1 column sums, pass 2 squared deviations from the block mean, of the bf16-rounded outputs; lane halves meet
-    // by a cross-half shuffle, the two M-waves of a column in a [2][BN] LDS block behind the C tile
-    float* sred = reinterpret_cast<float*>(smem + C3_BM * CROW * 2);
-    const int valid = min(C3_BM, M - m0);
-    const float inv_n = 1.f / (float)valid;
+    // per 128-row block g (waves 2g, 2g+1): pass 1 column sums, pass 2 squared deviations from the block mean, of the
+    // bf16-rounded outputs; lane halves meet by a cross-half shuffle, the waves in [WM][BN] LDS blocks behind the tile
+    constexpr int G = WM / 2;
+    float* ssum = reinterpret_cast<float*>(smem + BM * CROW * 2);
+    float* sm2 = ssum + WM * BN;
+    const int nmb128 = (M + 127) / 128;
+    const int g = wm >> 1;
+    const int valid = max(0, min(128, M - m0 - 128 * g));
+    const float inv_n = valid > 0 ? 1.f / (float)valid : 0.f;
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       float sm = 0.f;
@@ -222,44 +209,40 @@ __global__ __launch_bounds__(C3_NT, 2) void conv3_k(const bf16* __restrict__ X, 
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int row = (wm & 1) * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;   // within the 128-row block
           sm += row < valid ? (float)(bf16)acc[i][j][r] : 0.f;
         }
       sm += __shfl_xor(sm, 32);
-      if (h == 0) sred[wm * BN + wn * WN + j * 32 + l32] = sm;
+      if (h == 0) ssum[wm * BN + wn * WN + j * 32 + l32] = sm;
     }
     __syncthreads();
-    float mean_t[NTW];
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       const int col = wn * WN + j * 32 + l32;
-      mean_t[j] = (sred[col] + sred[BN + col]) * inv_n;
-    }
-    const float mean_w = threadIdx.x < BN ? (sred[threadIdx.x] + sred[BN + threadIdx.x]) * inv_n : 0.f;
-    __syncthreads();   // every wave has read the sums before the M2 partials overwrite them
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
+      const float mean = (ssum[2 * g * BN + col] + ssum[(2 * g + 1) * BN + col]) * inv_n;
       float m2 = 0.f;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          const float d = (float)(bf16)acc[i][j][r] - mean_t[j];
+          const int row = (wm & 1) * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float d = (float)(bf16)acc[i][j][r] - mean;
           m2 += row < valid ? d * d : 0.f;
         }
       m2 += __shfl_xor(m2, 32);
-      if (h == 0) sred[wm * BN + wn * WN + j * 32 + l32] = m2;
+      if (h == 0) sm2[wm * BN + col] = m2;
     }
     __syncthreads();
-    if (threadIdx.x < BN) {
-      const int col = threadIdx.x;
-      stats[(int64_t)mb * N + n0 + col] = mean_w;
-      stats[(int64_t)nmb * N + (int64_t)mb * N + n0 + col] = sred[col] + sred[BN + col];
-      if (col == 0 && n0 == 0) stats[2 * (int64_t)nmb * N + mb] = (float)valid;
+    for (int i = threadIdx.x; i < G * BN; i += NTH) {
+      const int gg = i / BN, col = i % BN;
+      const int blk = mb * G + gg;
+      const int vg = min(128, M - m0 - 128 * gg);
+      if (vg <= 0 || blk >= nmb128) continue;
+      stats[(int64_t)blk * N + n0 + col] = (ssum[2 * gg * BN + col] + ssum[(2 * gg + 1) * BN + col]) / (float)vg;
+      stats[(int64_t)nmb128 * N + (int64_t)blk * N + n0 + col] = sm2[2 * gg * BN + col] + sm2[(2 * gg + 1) * BN + col];
+      if (col == 0 && n0 == 0) stats[2 * (int64_t)nmb128 * N + blk] = (float)vg;
     }
   }
-  (void)HW;
 }
 
 }  // namespace
@@ -273,37 +256,41 @@ bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) 
 
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, int H, int W, hipStream_t st, float* stats, const float* bias) {
-  const int nmb = (int)cdiv(M, C3_BM), cin = (int)(K / 9);
+  const int cin = (int)(K / 9);
   static const int force_bn = [] {
     const char* e = getenv("DPH_CONV3_BN");
     return e ? atoi(e) : 0;
   }();
+  static const int force_wm = [] {
+    const char* e = getenv("DPH_CONV3_WM");
+    return e ? atoi(e) : 0;
+  }();
+  // 256-row tiles of 8 waves when that still gives >= 1 workgroup per CU (DPH_CONV3_WM=2 | 4 forces one form)
+  const int64_t t256 = cdiv(M, 256) * (N / (N % 128 == 0 ? 128 : 64));
+  const int wm = force_wm == 2 || force_wm == 4 ? force_wm : (t256 >= 256 ? kConv3DefaultWm : 2);
+  const int nmb = (int)cdiv(M, 64 * wm);
   // 128-wide tiles unless that leaves fewer than ~1.5 workgroups per CU (SimpleUNet's 22 x 45 bottleneck at B=4:
   // 124 tiles of 128 vs 248 of 64)
-  const bool wide = N % 128 == 0 && force_bn != 64 && (force_bn == 128 || (int64_t)nmb * (N / 128) >= 384);
-  // padding by range-checked buffer DMA (default: 1.0-1.2x the register-zeroing form on every ResNet-50 / UNet shape,
-  // profiles/r3/conv3_bench_*.json); DPH_CONV3_ZERO=mask selects the register form
-  static const bool zb = [] {
-    const char* e = getenv("DPH_CONV3_ZERO");
-    return !(e && e[0] == 'm');
-  }();
-#define DPH_C3(BN_, ST_, STATS_, ZB_)                                                                                 \
-  hipLaunchKernelGGL((conv3_k<BN_, ST_, STATS_, ZB_>), dim3(nmb * (int)(N / BN_)), dim3(C3_NT), 0, st, (const bf16*)A, \
-                     (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, stats, bias)
-  if (zb) {
+  const bool wide = N % 128 == 0 && force_bn != 64 &&
+                    (force_bn == 128 || (int64_t)nmb * (N / 128) * (wm == 4 ? 2 : 1) >= 384);
+#define DPH_C3(BN_, ST_, WM_, STATS_)                                                                            \
+  hipLaunchKernelGGL((conv3_k<BN_, ST_, WM_, STATS_>), dim3(nmb * (int)(N / BN_)), dim3(128 * WM_), 0, st,    \
+                     (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin,  \
+                     stats, bias)
+  if (wm == 4) {
     if (stats) {
-      if (wide) DPH_C3(128, 2, true, true);
-      else DPH_C3(64, 3, true, true);
+      if (wide) DPH_C3(128, 3, 4, true);
+      else DPH_C3(64, 3, 4, true);
     } else {
-      if (wide) DPH_C3(128, 2, false, true);
-      else DPH_C3(64, 3, false, true);
+      if (wide) DPH_C3(128, 3, 4, false);
+      else DPH_C3(64, 3, 4, false);
     }
   } else if (stats) {
-    if (wide) DPH_C3(128, 2, true, false);
-    else DPH_C3(64, 3, true, false);
+    if (wide) DPH_C3(128, 2, 2, true);
+    else DPH_C3(64, 3, 2, true);
   } else {
-    if (wide) DPH_C3(128, 2, false, false);
-    else DPH_C3(64, 3, false, false);
+    if (wide) DPH_C3(128, 2, 2, false);
+    else DPH_C3(64, 3, 2, false);
   }
 #undef DPH_C3
 }

@@ -14,7 +14,8 @@ to ``F.conv2d`` otherwise.  ``DPH_CONV1X1=0`` disables the kernel path (A/B runs
 forward and input gradient on the LDS-DMA kernel of csrc/conv3x3.hip (the input gradient is a 3x3 convolution of dY
 with the spatially flipped, channel-transposed weight; padding taps are zero-filled by range-checked buffer DMA; an
 epilogue emits the following BatchNorm's statistics or adds a bias): 440-810 TFLOP/s vs MIOpen's 370-780 on the
-ResNet-50 / SimpleUNet shapes (profiles/r3/conv3_bench_oob.json), on by default (``DPH_CONV3X3=0``: MIOpen).  The
+ResNet-50 / SimpleUNet shapes (profiles/r3/conv3_bench_oob.json), on by default (``DPH_CONV3X3=0``: MIOpen;
+``DPH_CONV3_WM=2|4`` picks the 4- or 8-wave tile).  The
 weight gradient runs on MIOpen by default (318-491 TFLOP/s vs 241-357 for the LDS-DMA split-pixel kernel and 302-324 for
 the older register-staged one, profiles/r3/conv3_bench_c3w_wgrad.json / _tsw_wgrad.json); ``DPH_CONV3_WGRAD=dph``
 selects the kernel.  Round 2's register-staged forward (``DPH_CONV3_KERNEL=ts``) measured 0.51-0.63 ms vs MIOpen's
