@@ -133,3 +133,23 @@ def test_llama_fused_blocks_match_unfused(dph_native, which):
     assert abs(l0 - l1) < 1e-2 * abs(l0)
     for n in g0:
         assert rel_err(g1[n], g0[n]) < 3e-2, n
+
+
+@pytest.mark.parametrize("variant", [1])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 192), (768, 512, 320), (256, 1024, 4096)])
+def test_gemm_nt_pipeline_variants_bitwise(dph_native, variant, M, N, K):
+    """Every pipeline variant (csrc/gemm_nt.hip LOOK) accumulates the same products in the same order as variant 0:
+    bitwise-equal outputs, for one, odd and even K-tile counts, in the plain and the fused SwiGLU modes."""
+    a, b = _rnd(M, K, seed=11), _rnd(N, K, seed=12)
+    try:
+        dph_native.gemm_nt_variant_(0)
+        c0 = dph_native.gemm_nt(a, b)
+        s0 = dph_native.gemm_nt_swiglu(a, b)
+        dph_native.gemm_nt_variant_(variant)
+        c1 = dph_native.gemm_nt(a, b)
+        s1 = dph_native.gemm_nt_swiglu(a, b)
+    finally:
+        dph_native.gemm_nt_variant_(-1)
+    assert torch.equal(c0, c1)
+    assert torch.equal(s0[0], s1[0]) and torch.equal(s0[1], s1[1])
+    assert rel_err(c1, a.float() @ b.float().t()) < 5e-3
