@@ -533,10 +533,7 @@ __global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ o, 
 // dV^T += dO^T P and dK^T += Q^T dS: no LDS round trip, no atomics.
 // VAR (A/B knob, DPH_ATTN_BWD_VAR): bit 0 = row constants as the initial S / dP accumulators (no dropout), bit 1 =
 // the dV / dK transposed reads software-pipelined one step ahead, the first step issued before the softmax.
-// DSO: dS (bf16, the value the dQ product consumes) is also written to the P.ds workspace, one 32-key x 32-query block
-// per wave and query tile (4 coalesced 8-B stores per lane; blocks a causal wave skips are written as zeros), for
-// attn_bwd_dq_ds_k -- the dQ pass then needs no S / dP recompute.
-template <int HD, bool CAUSAL, int NW, bool DROP = false, int VAR = 0, bool DSO = false>
+template <int HD, bool CAUSAL, int NW, bool DROP = false, int VAR = 0>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams P) {
   constexpr int NT = 64 * NW, BNK = 32 * NW, BMQ = 32, NC = HD / 8, KS = HD / 16, DT = HD / 32;
   constexpr bool RINIT = !DROP && (VAR & 1);
@@ -671,28 +668,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
   wait_vmcnt<0>();
   __syncthreads();
 
-  // DSO: this wave's dS block (key block key0 / 32, query block qt0 / 32) of query head hq; piece c4 holds queries
-  // 8 c4 .. 8 c4 + 7 of the block as [key][8], and lane (key l32, h) owns queries 8 c4 + 4 h .. + 3 of it
-  // Buffer stores: the head's dS (nb32^2 blocks) as the resource, the block as the scalar offset, the lane's 8-B slot
-  // as the one VGPR offset and the piece as the immediate -- no 64-bit per-lane address in this register-bound kernel.
-  const int nb32 = p.Sq >> 5;
-  const int ds_lane = l32 * 16 + h * 8;
-  auto ds_store = [&](int hq_t, int qt0_t, const bf16x8& lo, const bf16x8& hi) {
-    const char* head = (const char*)P.ds + (int64_t)(b * p.Hq + hq_t) * nb32 * nb32 * 2048;
-    const __amdgpu_buffer_rsrc_t r =
-        __builtin_amdgcn_make_buffer_rsrc((void*)head, (short)0, nb32 * nb32 * 2048, 0x00020000);
-    const int soff = __builtin_amdgcn_readfirstlane(((key0 >> 5) * nb32 + (qt0_t >> 5)) * 2048);
-    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-    const u32x2 w0 = __builtin_bit_cast(u32x2, __builtin_shufflevector(lo, lo, 0, 1, 2, 3));
-    const u32x2 w1 = __builtin_bit_cast(u32x2, __builtin_shufflevector(lo, lo, 4, 5, 6, 7));
-    const u32x2 w2 = __builtin_bit_cast(u32x2, __builtin_shufflevector(hi, hi, 0, 1, 2, 3));
-    const u32x2 w3 = __builtin_bit_cast(u32x2, __builtin_shufflevector(hi, hi, 4, 5, 6, 7));
-    __builtin_amdgcn_raw_buffer_store_b64(w0, r, ds_lane, soff, 0);
-    __builtin_amdgcn_raw_buffer_store_b64(w1, r, ds_lane + 512, soff, 0);
-    __builtin_amdgcn_raw_buffer_store_b64(w2, r, ds_lane + 1024, soff, 0);
-    __builtin_amdgcn_raw_buffer_store_b64(w3, r, ds_lane + 1536, soff, 0);
-  };
-
   for (int it = 0; it < total; ++it) {
     const int buf = it & 1;
     const int qt0 = qstart + (it % nqt_head) * BMQ;
@@ -700,10 +675,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
     const char* Ql = Qbuf + buf * 2 * QIMG;
     const char* Ol = Ql + QIMG;
     // a wave whose 32 keys are all hidden from this query tile by the causal mask skips the tile
-    if (CAUSAL && key0 > qt0 + BMQ - 1 + off) {
-      if constexpr (DSO) ds_store(hk * grp + it / nqt_head, qt0, zero8(), zero8());   // the dQ pass stages whole
-                                                                                    // tiles: masked blocks read 0
-    } else {
+    if (!(CAUSAL && key0 > qt0 + BMQ - 1 + off)) {
       const float* ls = lse_s + buf * BMQ;
       const float* ds = del_s + buf * BMQ;
       f32x16 s = mfma32(lds_b128(Ql, qro[0]), lds_b128(Kimg, kofs(0)), RINIT ? row_init(ls) : zacc);
@@ -755,8 +727,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
           pb[ks][j] = (bf16)s[8 * ks + j];
           sb[ks][j] = (bf16)dp[8 * ks + j];
         }
-      // sb[ks][j] = dS of query (j & 3) + 8 (2 ks + (j >> 2)) + 4 h: piece c4 = 2 ks + (j >> 2), slot 4 h + (j & 3)
-      if constexpr (DSO) ds_store(hk * grp + it / nqt_head, qt0, sb[0], sb[1]);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (TRPIPE) {
         // step i = (ks, dt): its operands were read one step earlier; each step issues the next step's 4 reads
@@ -786,10 +756,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
       }
     }
     if (it + 1 < total) stage_scalars(buf ^ 1);
-    // DSO: both branches issued exactly 4 dS stores after the Q / dO prefetch; vmcnt retires in issue order, so
-    // vmcnt(4) lands the prefetch and leaves the stores in flight (the next tile's wait retires them)
-    if constexpr (DSO) wait_vmcnt<4>();
-    else wait_vmcnt<0>();
+    wait_vmcnt<0>();
     __syncthreads();
   }
 
@@ -960,180 +927,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
   }
 }
 
-// ---- dQ from a handed-off dS (P.ds, written by attn_bwd_dkdv_k<.., DSO>): dQ^T += K^T dS^T only -- one MFMA product
-// per tile instead of three (no S / dP recompute, no Q / dO / lse / delta reads).  The dQ kernel's structure and
-// epilogue (scale, inverse RoPE) with V's LDS image replaced by the dS tile: 64 keys x 128 queries, staged by LDS-DMA
-// straight from the block layout (a DMA lane's 16-B chunk = queries 8c .. 8c + 7 of one key = one piece row) into the
-// same swizzled image geometry as K, so the B operand is the same transposed read as K^T's A operand with this wave's
-// 32 queries as the column block -- both operands carry the same key order by construction.  HD == 32 NW (the dS
-// image then has K's row width); S % 128 == 0, Sq == Sk, no dropout (flash_attn_ds_eligible).
-template <int HD, bool CAUSAL, int NW>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_ds_k(AttnBwdParams P) {
-  using Plan = KVTilePlan<HD, 64 * NW>;
-  constexpr int BM = 32 * NW, BN = Plan::BN, DT = Plan::DT, TILE = Plan::TILE, NS = Plan::NS;
-  static_assert(BM == HD, "the dS image must have K's geometry");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const AttnParams& p = P.f;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
-  const int nqb = p.Sq / BM;
-  int bx, hq, b;
-  xcd_block(nqb, p.Hq, bx, hq, b, nqb * p.Hq * p.B);
-  const int qb = CAUSAL ? nqb - 1 - bx : bx;   // heaviest causal blocks first
-  const int hk = hq / (p.Hq / p.Hkv);
-  const int q0 = qb * BM, q0w = q0 + wid * 32;
-  const int myq = q0w + l32;
-  const int nb32 = p.Sq >> 5;
-
-  const bf16* kp = (const bf16*)p.k + (int64_t)b * p.k_sb + (int64_t)hk * p.k_sh;
-  const char* dsh = (const char*)((const bf16*)P.ds + (int64_t)(b * p.Hq + hq) * nb32 * nb32 * 1024);
-
-  const int ntiles = CAUSAL ? (q0 + BM) / BN : p.Sk / BN;
-  const int wtiles = wave_tile_count<CAUSAL>(ntiles, q0w, 0);
-
-  Plan plan;
-  plan.init(lane, p.k_ss);
-  plan.init_async();
-  // per-lane dS source offsets (bytes) at tile 0: image row rho = key, chunk c = queries q0 + 8c .. + 7 ->
-  // block (rho >> 5, q0 / 32 + c / 4), piece c % 4, row rho % 32; tile t adds 2 t block rows
-  unsigned dso[NS];
-#pragma unroll
-  for (int i = 0; i < NS; ++i) {
-    const int rho = plan.prow[i], c = plan.pch[i] >> 3;
-    dso[i] = (unsigned)(((((rho >> 5) * nb32 + (q0 >> 5) + (c >> 2)) * 1024) + (c & 3) * 256 + (rho & 31) * 8) * 2);
-  }
-  const unsigned lds_w = lds_addr(smem + wid * 64 * 16);
-  auto stage = [&](int t, int buf) {
-    const unsigned l = lds_w + buf * 2 * TILE;
-    const bf16* kt = kp + (int64_t)t * BN * p.k_ss;
-#pragma unroll
-    for (int i = 0; i < NS; ++i)
-      lds_dma16(kt, (unsigned)(((int64_t)plan.prow[i] * p.k_ss + plan.pch[i]) * 2), l + 64 * NW * i * 16);
-    const char* dt_ = dsh + (int64_t)t * 2 * nb32 * 2048;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) lds_dma16(dt_, dso[i], l + TILE + 64 * NW * i * 16);
-  };
-
-  f32x16 dq[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
-
-  if (ntiles > 0) stage(0, 0);
-  wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
-    if (t < wtiles) {
-      const char* Kl = smem + buf * 2 * TILE;
-      const char* Dl = Kl + TILE;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 sfr = lds_tr2(Dl, plan.tr(ks, wid, 0), plan.tr(ks, wid, 1));
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-          dq[dt] = mfma32(lds_tr2(Kl, plan.tr(ks, dt, 0), plan.tr(ks, dt, 1)), sfr, dq[dt]);
-      }
-    }
-    wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-  }
-
-  bf16* dqp = (bf16*)P.dq + (int64_t)b * P.dq_sb + (int64_t)myq * P.dq_ss + (int64_t)hq * P.dq_sh;
-  store_rows_bf16<DT>(dqp, dq, p.scale, h, myq, P.rope_cos, P.rope_sin, P.rope_off);
-}
-
-// The same product at 8 waves = 256 queries per workgroup with a 3-stage ring (K 16 KB + dS 32 KB per stage, 144 KB):
-// the pass is bound by the dS read (every block is read once), and two stages in flight per CU (64 KB of dS) are what
-// keeps HBM busy where the double-buffered 4-wave form (16 KB per workgroup in flight) ran latency-bound.  The dS image
-// is 64 keys x 256 queries (32 chunks per row) read through its own plan; its transposed-read rows (the key order)
-// are the K plan's, so the two operands agree.  Blocks the dK/dV pass never visits (keys of the second 128-key half x
-// queries of the first) land in LDS but only under waves whose causal range ends before those keys.
-template <bool CAUSAL>
-__global__ __launch_bounds__(512, 1) void attn_bwd_dq_ds8_k(AttnBwdParams P) {
-  using KPlan = KVTilePlan<128, 512>;
-  using DPlan = KVTilePlan<256, 512>;
-  constexpr int BM = 256, BN = 64, DT = 4, KTILE = KPlan::TILE, DTILE = DPlan::TILE, STAGE = KTILE + DTILE, NSTG = 3;
-  constexpr int KNS = KPlan::NS, DNS = DPlan::NS, NDMA = KNS + DNS;
-  __shared__ __attribute__((aligned(1024))) char smem[NSTG * STAGE];
-
-  const AttnParams& p = P.f;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
-  const int nqb = p.Sq / BM;
-  int bx, hq, b;
-  xcd_block(nqb, p.Hq, bx, hq, b, nqb * p.Hq * p.B);
-  const int qb = CAUSAL ? nqb - 1 - bx : bx;   // heaviest causal blocks first
-  const int hk = hq / (p.Hq / p.Hkv);
-  const int q0 = qb * BM, q0w = q0 + wid * 32;
-  const int myq = q0w + l32;
-  const int nb32 = p.Sq >> 5;
-
-  const bf16* kp = (const bf16*)p.k + (int64_t)b * p.k_sb + (int64_t)hk * p.k_sh;
-  const char* dsh = (const char*)((const bf16*)P.ds + (int64_t)(b * p.Hq + hq) * nb32 * nb32 * 1024);
-  const int ntiles = CAUSAL ? (q0 + BM) / BN : p.Sk / BN;
-  const int wtiles = wave_tile_count<CAUSAL>(ntiles, q0w, 0);
-
-  KPlan kplan;
-  kplan.init(lane, p.k_ss);
-  kplan.init_async();
-  DPlan dplan;
-  dplan.init(lane, p.k_ss);
-  dplan.init_async();
-  unsigned kso[KNS], dso[DNS];
-#pragma unroll
-  for (int i = 0; i < KNS; ++i) kso[i] = (unsigned)(((int64_t)kplan.prow[i] * p.k_ss + kplan.pch[i]) * 2);
-#pragma unroll
-  for (int i = 0; i < DNS; ++i) {
-    const int rho = dplan.prow[i], c = dplan.pch[i] >> 3;
-    dso[i] = (unsigned)(((((rho >> 5) * nb32 + (q0 >> 5) + (c >> 2)) * 1024) + (c & 3) * 256 + (rho & 31) * 8) * 2);
-  }
-  const unsigned lds_w = lds_addr(smem + wid * 64 * 16);
-  auto stage = [&](int t) {
-    const unsigned l = lds_w + (t % NSTG) * STAGE;
-    const bf16* kt = kp + (int64_t)t * BN * p.k_ss;
-#pragma unroll
-    for (int i = 0; i < KNS; ++i) lds_dma16(kt, kso[i], l + 512 * i * 16);
-    const char* dt_ = dsh + (int64_t)t * 2 * nb32 * 2048;
-#pragma unroll
-    for (int i = 0; i < DNS; ++i) lds_dma16(dt_, dso[i], l + KTILE + 512 * i * 16);
-  };
-
-  f32x16 dq[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
-
-  if (ntiles > 0) stage(0);
-  if (ntiles > 1) stage(1);
-  if (ntiles > 1) wait_vmcnt<NDMA>();
-  else wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-  for (int t = 0; t < ntiles; ++t) {
-    const bool more = t + 2 < ntiles;
-    if (more) stage(t + 2);
-    if (t < wtiles) {
-      const char* Kl = smem + (t % NSTG) * STAGE;
-      const char* Dl = Kl + KTILE;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 sfr = lds_tr2(Dl, dplan.tr(ks, wid, 0), dplan.tr(ks, wid, 1));
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
-          dq[dt] = mfma32(lds_tr2(Kl, kplan.tr(ks, dt, 0), kplan.tr(ks, dt, 1)), sfr, dq[dt]);
-      }
-    }
-    if (more) wait_vmcnt<NDMA>();   // tile t+1 landed, t+2 in flight
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-  }
-
-  bf16* dqp = (bf16*)P.dq + (int64_t)b * P.dq_sb + (int64_t)myq * P.dq_ss + (int64_t)hq * P.dq_sh;
-  store_rows_bf16<DT>(dqp, dq, p.scale, h, myq, P.rope_cos, P.rope_sin, P.rope_off);
-}
-
 // ==================================================================================================
 // Waves per workgroup (4 or 8; DPH_ATTN_WAVES overrides, for A/B runs).  8 waves = 256 query rows (or keys) share
 // every staged K/V (or Q/dO) tile: half the LDS fill traffic per MFMA of 4 waves, one workgroup per CU.
@@ -1197,13 +990,6 @@ static void dkdv_launch(const AttnBwdParams& P, hipStream_t st) {
   constexpr int BNK = 32 * NW;
   const size_t lds_kv = BNK * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
   const dim3 grid_kv((unsigned)((p.Sk + BNK - 1) / BNK * p.Hkv * p.B));
-  if (P.ds) {
-    if constexpr (HD == 32 * NW) {
-      if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, NW, false, VAR, true>), grid_kv, dim3(64 * NW), lds_kv, st, P);
-      else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, NW, false, VAR, true>), grid_kv, dim3(64 * NW), lds_kv, st, P);
-    }
-    return;
-  }
   if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, NW, false, VAR>), grid_kv, dim3(64 * NW), lds_kv, st, P);
   else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, NW, false, VAR>), grid_kv, dim3(64 * NW), lds_kv, st, P);
 }
@@ -1219,23 +1005,6 @@ static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
   }
   const size_t lds_q = 2 * 2 * 64 * HD * 2;
   const dim3 grid_q((unsigned)((p.Sq + 32 * NW - 1) / (32 * NW) * p.Hq * p.B));
-  if (P.ds) {
-    if constexpr (HD == 128) {
-      static const int dsw = [] {   // DPH_ATTN_DS_WAVES=4: the double-buffered 4-wave dQ pass (A/B runs)
-        const char* e = getenv("DPH_ATTN_DS_WAVES");
-        return e && atoi(e) == 4 ? 4 : 8;
-      }();
-      if (dsw == 8) {
-        const dim3 g8((unsigned)(p.Sq / 256 * p.Hq * p.B));
-        if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_ds8_k<true>), g8, dim3(512), 0, st, P);
-        else hipLaunchKernelGGL((attn_bwd_dq_ds8_k<false>), g8, dim3(512), 0, st, P);
-      } else if constexpr (HD == 32 * NW) {
-        if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_ds_k<HD, true, NW>), grid_q, dim3(64 * NW), lds_q, st, P);
-        else hipLaunchKernelGGL((attn_bwd_dq_ds_k<HD, false, NW>), grid_q, dim3(64 * NW), lds_q, st, P);
-      }
-    }
-    return;
-  }
   static const bool dq_pf = [] {
     const char* e = getenv("DPH_ATTN_DQ_VAR");
     return e ? atoi(e) == 1 : kAttnDqDefaultPf;
@@ -1269,27 +1038,7 @@ static void bwd_launch(const AttnBwdParams& P, hipStream_t st) {
   bwd_launch_nw<HD, 4>(P, st);
 }
 
-namespace {
-int g_attn_ds = -1;   // -1: unresolved (env DPH_ATTN_DS, default kAttnDsDefault)
-constexpr int kAttnDsDefault = 0;
-}
-
-int flash_attn_ds_mode(int v) {
-  if (v >= 0) g_attn_ds = v ? 1 : 0;
-  if (v == -2 || g_attn_ds < 0) {
-    const char* e = getenv("DPH_ATTN_DS");
-    g_attn_ds = e ? (atoi(e) ? 1 : 0) : kAttnDsDefault;
-  }
-  return g_attn_ds;
-}
-
-bool flash_attn_ds_eligible(const AttnParams& p) {
-  return flash_attn_ds_mode(-1) == 1 && p.drop_p == 0.f && p.D == 128 && p.Sq == p.Sk && p.Sq % 256 == 0 && p.Sq > 0 && attn_waves(4) == 4;
-}
-
-void flash_attn_bwd(const AttnBwdParams& Pin, hipStream_t st) {
-  AttnBwdParams P = Pin;
-  if (P.ds && !flash_attn_ds_eligible(P.f)) P.ds = nullptr;   // the host op sized it; the shapes decide
+void flash_attn_bwd(const AttnBwdParams& P, hipStream_t st) {
   const AttnParams& p = P.f;
   if (p.B == 0 || p.Sq == 0) return;
   const int64_t rows = (int64_t)p.B * p.Hq * p.Sq;

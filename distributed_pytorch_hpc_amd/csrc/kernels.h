@@ -88,11 +88,6 @@ struct AttnBwdParams {
   AttnParams f;
   const void* dout; int64_t do_sb, do_ss, do_sh;
   float* delta;          // fp32 [B, Hq, Sq] workspace: rowsum(dO * O)
-  // Optional bf16 dS workspace [B * Hq][S / 32][S / 32] blocks of 32 keys x 32 queries, each stored as 4 pieces
-  // [query chunk c4][key][8 queries] (2 KB per block).  Set (flash_attn_ds_eligible) when the dK/dV kernel can hand
-  // dS = P (dP - delta) to a dQ kernel that only multiplies dQ = dS K -- no S / dP recompute; nullptr: the dQ kernel
-  // recomputes S and dP from Q, K, V, dO, lse and delta.
-  void* ds;
   void* dq; void* dk; void* dv;   // bf16 [B,S,H,D] at the strides below; dk/dv per KV head (GQA summed)
   int64_t dq_sb, dq_ss, dq_sh, dk_sb, dk_ss, dk_sh, dv_sb, dv_ss, dv_sh;
   // optional fused inverse RoPE of dq / dk (interleaved pairs, fp32 tables [max_pos, D / 2], position = row +
@@ -101,11 +96,6 @@ struct AttnBwdParams {
   const float* rope_cos; const float* rope_sin; int rope_off;
 };
 void flash_attn_bwd(const AttnBwdParams& p, hipStream_t stream);
-// shapes for which flash_attn_bwd can use the dS hand-off (AttnBwdParams::ds): no dropout, head_dim 128, Sq == Sk,
-// S % 256 == 0, 4-wave kernels
-bool flash_attn_ds_eligible(const AttnParams& p);
-// dS hand-off switch: v = 0 / 1 sets it, -1 queries, -2 re-reads DPH_ATTN_DS; returns the active mode
-int flash_attn_ds_mode(int v);
 
 // ---- Embedding gather / scatter-add backward (vocab-sharded friendly: out-of-range ids -> zero row) ----
 void embedding_fwd(const int64_t* ids, const void* table, void* out, int64_t n, int64_t dim, int64_t vocab_start,

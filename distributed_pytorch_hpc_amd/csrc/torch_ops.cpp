@@ -307,20 +307,6 @@ void flash_attn_bwd_impl(const Tensor& dout, const Tensor& q, const Tensor& k, c
   P.f = make_params(q, k, v, o, lse_c, scale, causal, dropout_p, seed);
   P.dout = dout.data_ptr(); P.do_sb = dout.stride(0); P.do_ss = dout.stride(1); P.do_sh = dout.stride(2);
   P.delta = delta.data_ptr<float>();
-  // dS hand-off workspace (bf16, B * Hq * Sq^2 elements: 8.6 GB for Llama-2-7B at B 8 x S 4096; one layer's backward
-  // at a time), within a size cap (DPH_ATTN_DS_MAX_GB, default 24)
-  Tensor ds;
-  if (dph::flash_attn_ds_eligible(P.f)) {
-    static const double cap_gb = [] {
-      const char* e = getenv("DPH_ATTN_DS_MAX_GB");
-      return e ? atof(e) : 24.0;
-    }();
-    const double bytes = 2.0 * (double)B * (double)Hq * (double)Sq * (double)Sq;
-    if (bytes <= cap_gb * 1e9) {
-      ds = at::empty({B * Hq * Sq * Sq}, q.options());
-      P.ds = ds.data_ptr();
-    }
-  }
   P.dq = dq.data_ptr(); P.dk = dk.data_ptr(); P.dv = dv.data_ptr();
   P.dq_sb = dq.stride(0); P.dq_ss = dq.stride(1); P.dq_sh = dq.stride(2);
   P.dk_sb = dk.stride(0); P.dk_ss = dk.stride(1); P.dk_sh = dk.stride(2);
@@ -1123,9 +1109,6 @@ std::vector<int64_t> out_sizes(const Tensor& x, int64_t n) {
 }  // namespace
 
 // select the gemm_nt pipeline variant (v < 0: back to the env / default); returns the active one
-// dS hand-off of the attention backward on / off (v = 0 / 1), query (-1) or back to DPH_ATTN_DS (-2)
-int64_t attn_ds_mode_(int64_t v) { return dph::flash_attn_ds_mode((int)v); }
-
 int64_t gemm_nt_variant_(int64_t v) {
   dph::gemm_nt_set_variant((int)v);
   return dph::gemm_nt_variant();
@@ -1265,7 +1248,6 @@ TORCH_LIBRARY(dph, m) {
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
   m.def("gemm_nt(Tensor A, Tensor B) -> Tensor");
   m.def("gemm_nt_variant_(int v) -> int", &gemm_nt_variant_);   // no tensor argument: catch-all kernel
-  m.def("attn_ds_mode_(int v) -> int", &attn_ds_mode_);         // no tensor argument: catch-all kernel
   m.def("gemm_nt_swiglu(Tensor x, Tensor w13) -> (Tensor, Tensor)");
   m.def("gemm_nt_dswiglu(Tensor dy, Tensor w2t, Tensor x13) -> Tensor");
   m.def("gemm_nt_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int S, int hd, int n_rot, int pos_off) -> Tensor");
