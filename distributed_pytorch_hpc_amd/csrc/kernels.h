@@ -143,7 +143,7 @@ struct GemmNtParams {
 bool gemm_nt_supported(int mode, int64_t M, int64_t N, int64_t K);
 void gemm_nt(int mode, const GemmNtParams& p, hipStream_t stream);
 // pipeline variant of gemm_nt_k (0: 12/4/8/0 fragment reads per phase, 1: lookahead B0 reads, 8/4/8/0)
-constexpr int kGemmNtDefaultVariant = 0;
+constexpr int kGemmNtDefaultVariant = 1;   // 0.92-1.02x hipBLASLt vs 0.91-1.00x for 0 (profiles/r3/rejected/gemm_nt_2phase_*)
 int gemm_nt_variant();
 void gemm_nt_set_variant(int v);
 

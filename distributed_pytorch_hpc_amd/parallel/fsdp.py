@@ -23,6 +23,7 @@ Create the optimizer with ``fsdp.make_optimizer("adamw", lr=...)`` (fused CDNA4 
 from __future__ import annotations
 
 import contextlib
+import os
 from enum import Enum
 from functools import partial
 from typing import Callable, Iterable, Optional
@@ -146,6 +147,10 @@ class ZeRO3Engine:
         self.shard_total = soff
         self.param_shard = torch.zeros(soff, dtype=self.param_dtype, device=self.device)
         self.grad_shard = torch.zeros(soff, dtype=self.grad_dtype, device=self.device)
+        # A shard group of one: a unit's gathered parameters / full gradient ARE its shard, so they alias the shard
+        # buffers -- the all-gather, reduce-scatter and free of the general path degenerate to nothing instead of a
+        # copy each (3 per unit per step) and an allocator round trip.  Same engine, same update order as world > 1.
+        self._alias = self.world == 1 and os.environ.get("DPH_FSDP_ALIAS", "1") != "0"   # (=0: A/B runs)
         self._unit_of = {}
         with torch.no_grad():
             for u in self.units:
@@ -159,8 +164,11 @@ class ZeRO3Engine:
                     src = dist.get_global_rank(process_group, 0) if process_group is not None else 0
                     dist.broadcast(full, src=src, group=process_group)
                 self.shard_view(u).copy_(full[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel])
-                u.full = full
-                u.grad_full = torch.zeros(u.numel, dtype=self.grad_dtype, device=self.device)
+                if self._alias:
+                    u.full, u.grad_full = self.shard_view(u), self.grad_shard_view(u)
+                else:
+                    u.full = full
+                    u.grad_full = torch.zeros(u.numel, dtype=self.grad_dtype, device=self.device)
                 o = 0
                 for p in u.params:
                     n = p.numel()
@@ -206,6 +214,9 @@ class ZeRO3Engine:
     def _start_gather(self, u):
         if u.gathered or u.ag_work is not None:
             return
+        if self._alias:
+            u.gathered = True
+            return
         _alloc(u.full)
         if self.world == 1:
             u.full.copy_(self.shard_view(u))
@@ -224,7 +235,7 @@ class ZeRO3Engine:
         u.gathered = True
 
     def _release(self, u):
-        if u is self.units[-1] and not self.reshard:
+        if self._alias or (u is self.units[-1] and not self.reshard):
             return
         if u.ag_work is not None:
             u.ag_work.wait()
@@ -245,7 +256,8 @@ class ZeRO3Engine:
 
     def _pre_backward(self, u, module, grad_out):
         self._gather(u)
-        _alloc(u.grad_full)
+        if not self._alias:
+            _alloc(u.grad_full)
         if not any(p._dph_accum for p in u.params):
             u.grad_full.zero_()
         if self.prefetch and u.idx >= 1 and u.idx - 1 < len(self.units) - 1:
@@ -256,7 +268,8 @@ class ZeRO3Engine:
         if g is None:
             return
         u = self._unit_of[id(p)]
-        _alloc(u.grad_full)
+        if not self._alias:
+            _alloc(u.grad_full)
         with torch.no_grad():
             if p._dph_accum:
                 p.main_grad.add_(g)
@@ -289,7 +302,9 @@ class ZeRO3Engine:
             for p in u.params:
                 if not p._dph_accum:
                     p.main_grad.zero_()
-        if self.world == 1:
+        if self._alias:
+            pass   # the full gradient is the shard
+        elif self.world == 1:
             self.grad_shard_view(u).copy_(u.grad_full)
         else:
             u.rs_work = dist.reduce_scatter_tensor(self.grad_shard_view(u), u.grad_full, op=dist.ReduceOp.SUM,
@@ -304,16 +319,19 @@ class ZeRO3Engine:
             for u in self.units:
                 u.n_ready = 0
             return
-        _alloc(self.units[-1].grad_full)
+        if not self._alias:
+            _alloc(self.units[-1].grad_full)
         for u in self.units:
             if not u.launched:
-                _alloc(u.grad_full)
+                if not self._alias:
+                    _alloc(u.grad_full)
                 self._launch(u)
         for u in self.units:
             if u.rs_work is not None:
                 u.rs_work.wait()
                 u.rs_work = None
-            _free(u.grad_full)
+            if not self._alias:
+                _free(u.grad_full)
         if self.replicate_group is not None:
             dist.all_reduce(self.grad_shard, group=self.replicate_group)
 

@@ -13,7 +13,8 @@ Weight gradients take the same route as every other linear layer of the framewor
 ``weight_grad`` writes them straight into the data-parallel engine's bucket and notifies it), so the engines'
 overlapped reduce-scatter / all-reduce see no difference.  The fused paths are taken for plain (not tensor-parallel,
 not FP8) bf16 projections whose shapes the kernel tiles (rows % 256, features % 256, K % 64); everything else runs
-the unfused modules.  ``DPH_FUSED_MLP=0`` / ``DPH_FUSED_QKV=0`` turn them off (A/B runs).
+the unfused modules.  ``DPH_FUSED_MLP=0`` / ``DPH_FUSED_QKV=0`` turn them off (A/B runs); by default only the MLP's
+backward fusion is on.
 """
 from __future__ import annotations
 
@@ -27,8 +28,10 @@ from ..ops import fp8 as _fp8
 from .linear import _dgrad, weight_grad
 
 # DPH_FUSED_MLP: "1" = SwiGLU in the w13 GEMM epilogue AND dSwiGLU in w2's input-gradient epilogue; "bwd" = only the
-# backward fusion (forward: library GEMM + swiglu_fwd); "0" = unfused modules
-_FUSED_MLP = os.environ.get("DPH_FUSED_MLP", "0")
+# backward fusion (forward: library GEMM + swiglu_fwd); "0" = unfused modules.  Default "bwd": +0.3-0.4 % tokens/s on
+# the Llama-2-7B step (interleaved A/B on one MI355X, profiles/r3/ab_fused_mlp_bwd/); the forward fusion measured
+# -0.6 % (the CDNA4 forward GEMM is 0.95x the library on w13, more than the saved swiglu_fwd pass).
+_FUSED_MLP = os.environ.get("DPH_FUSED_MLP", "bwd")
 _FUSED_MLP = False if _FUSED_MLP == "0" else ("bwd" if _FUSED_MLP == "bwd" else True)
 _FUSED_QKV = os.environ.get("DPH_FUSED_QKV", "0") != "0"
 # DPH_GEMM_NT: which forward / input-gradient GEMMs run on the CDNA4 kernel instead of hipBLASLt:

@@ -84,3 +84,48 @@ def test_hybrid_shard_4ranks():
             assert abs(a - b) < 3e-5 * max(1, abs(a))
         for k, v in ref_sd.items():
             assert torch.allclose(v, sd[k], atol=3e-5), k
+
+
+@pytest.mark.parametrize("policy", ["block", "size"])
+def test_full_shard_world1_aliased_matches_single_process(policy):
+    """A shard group of one aliases each unit's gathered parameters / full gradient to its shard (no gather, scatter
+    or free): same losses and parameters as plain AdamW, checkpoint consolidation included."""
+    ref_losses, ref_sd = _reference()
+    (losses, sd), = run_distributed(_worker, 1, "FULL_SHARD", policy)
+    for a, b in zip(ref_losses, losses):
+        assert abs(a - b) < 3e-5 * max(1, abs(a)), (ref_losses, losses)
+    for k, v in ref_sd.items():
+        assert torch.allclose(v, sd[k], atol=3e-5), k
+
+
+def _worker_replicate_only(rank, world):
+    """HYBRID with shard groups of one (aliased units) and gradients all-reduced over the replicate group."""
+    from distributed_pytorch_hpc_amd.models.llama2 import TransformerBlock
+    from distributed_pytorch_hpc_amd.parallel.fsdp import FSDP, ModuleWrapPolicy
+
+    m = _model()
+    singles = [dist.new_group([r]) for r in range(world)]
+    f = FSDP(m, sharding_strategy="HYBRID_SHARD", auto_wrap_policy=ModuleWrapPolicy({TransformerBlock}),
+             process_group=singles[rank], replicate_group=dist.new_group(list(range(world))))
+    assert f.engine._alias
+    opt = f.make_optimizer("adamw", lr=1e-2, weight_decay=0.1)
+    losses = []
+    for t in _batches():
+        local = t.chunk(world, 0)[rank]
+        loss = f(local[:, :-1], local[:, 1:])
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+        lt = loss.detach().clone()
+        dist.all_reduce(lt)
+        losses.append(lt.item() / world)
+    return losses, f.full_state_dict(rank0_only=False)
+
+
+def test_hybrid_shard_groups_of_one():
+    ref_losses, ref_sd = _reference()
+    for losses, sd in run_distributed(_worker_replicate_only, 2):
+        for a, b in zip(ref_losses, losses):
+            assert abs(a - b) < 3e-5 * max(1, abs(a))
+        for k, v in ref_sd.items():
+            assert torch.allclose(v, sd[k], atol=3e-5), k
