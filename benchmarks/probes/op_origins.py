@@ -33,7 +33,8 @@ def main():
         wl.step(i)
     torch.cuda.synchronize()
     want = set(a.ops.split(","))
-    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU], with_stack=True) as prof:
+    with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CPU], with_stack=True,
+                                record_shapes=True) as prof:
         for i in range(a.steps):
             wl.step(3 + i)
         torch.cuda.synchronize()
@@ -41,8 +42,16 @@ def main():
     for ev in prof.events():
         if ev.name not in want:
             continue
-        frames = [f for f in (ev.stack or []) if "distributed_pytorch_hpc_amd" in f or "bench" in f]
-        key = " <- ".join(f.split(ROOT + "/")[-1] for f in frames[:3]) or "(no framework frame)"
+        # nested ops (copy_ under aten::to / contiguous, or under an autograd node) carry no stack themselves: walk
+        # up the parents, keeping their names, to the first one that has framework frames
+        chain, e, frames = [], ev, []
+        while e is not None and not frames:
+            frames = [f for f in (e.stack or []) if "distributed_pytorch_hpc_amd" in f or "bench" in f]
+            if not frames:
+                chain.append(e.name)
+                e = e.cpu_parent
+        key = " < ".join(chain[1:4]) + (" | " if chain[1:] else "") + \
+            (" <- ".join(f.split(ROOT + "/")[-1] for f in frames[:3]) or "(no framework frame)")
         by[ev.name][key] += 1
     for name, c in by.items():
         print(f"== {name}: {sum(c.values()) / a.steps:.1f} per step")

@@ -436,18 +436,33 @@ void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const 
   const float* pmean = workspace;
   const float* pm2 = workspace + (int64_t)G * C;
   const float* pn = workspace + 2 * (int64_t)G * C;
-  if (pre_stats) {   // partials from the producing 1x1 convolution's epilogue, merged down to <= G segments
-    const int S = std::min(G, 64);
-    float* om = workspace;
-    float* o2 = workspace + (int64_t)S * C;
-    float* on = workspace + 2 * (int64_t)S * C;
-    hipLaunchKernelGGL(bn_merge_k, dim3((unsigned)(C / 8), (unsigned)S), dim3(FIN_NT), 0, st, pre_stats,
-                       pre_stats + (int64_t)pre_groups * C, pre_stats + 2 * (int64_t)pre_groups * C, pre_groups,
-                       (int)C, om, o2, on);
-    G = S;
-    pmean = om;
-    pm2 = o2;
-    pn = on;
+  if (pre_stats) {   // partials from the producing convolution's epilogue (one per 128-row block)
+    // Merged first into S segments of >= 4 partials per thread (FIN_GROUPS row groups per block); with a few hundred
+    // partials or fewer bn_finalize_k takes them directly.  (S = 64 for every shape -- up to 16 384 mostly idle
+    // 1024-thread blocks at 2048 channels -- measured 16 us per merge.)
+    static const bool legacy = [] {   // DPH_BN_MERGE_LEGACY=1: 64 segments for every shape (A/B runs)
+      const char* e = getenv("DPH_BN_MERGE_LEGACY");
+      return e && atoi(e) == 1;
+    }();
+    const int S = legacy ? std::min(G, 64)
+                         : std::min(std::min(G, 64), (pre_groups + 4 * FIN_GROUPS - 1) / (4 * FIN_GROUPS));
+    if (S <= 1) {
+      G = pre_groups;
+      pmean = pre_stats;
+      pm2 = pre_stats + (int64_t)pre_groups * C;
+      pn = pre_stats + 2 * (int64_t)pre_groups * C;
+    } else {
+      float* om = workspace;
+      float* o2 = workspace + (int64_t)S * C;
+      float* on = workspace + 2 * (int64_t)S * C;
+      hipLaunchKernelGGL(bn_merge_k, dim3((unsigned)(C / 8), (unsigned)S), dim3(FIN_NT), 0, st, pre_stats,
+                         pre_stats + (int64_t)pre_groups * C, pre_stats + 2 * (int64_t)pre_groups * C, pre_groups,
+                         (int)C, om, o2, on);
+      G = S;
+      pmean = om;
+      pm2 = o2;
+      pn = on;
+    }
   } else {
     const size_t shs = 3 * BN_NT * 8 * sizeof(float);
     DPH_DISPATCH_FLOAT(dt, T, {

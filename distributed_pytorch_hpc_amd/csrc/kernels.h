@@ -215,6 +215,9 @@ void chsum(const void* x, float* part, void* out, int64_t M, int64_t C, int dtyp
 // dst[C, R] = src[R, C]^T (bf16, row-major, leading dims in elements; vector path needs 16-B aligned rows).
 void transpose2d(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_src, int64_t ld_dst,
                  hipStream_t stream);
+// 3x3 convolution input-gradient weight: channels-last w [cout][3][3][cin] -> out [cin][9 taps][cout], taps reversed
+// (the flipped, channel-transposed weight of dX = conv(dY, flip(W)^T)), one launch
+void conv3x3_dgrad_weight(const void* w, void* out, int64_t cout, int64_t cin, hipStream_t stream);
 
 void cast_copy(const void* src, void* dst, int64_t n, int src_dtype, int dst_dtype, float scale, hipStream_t stream);
 

@@ -861,6 +861,21 @@ Tensor transpose2d(const Tensor& x) {
   return out;
 }
 
+// [cout, cin, 3, 3] channels-last bf16 weight -> [cin, 9 * cout]: the flipped, channel-transposed weight of the 3x3
+// convolution's input gradient (what w.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, 9 * cout) copies element-wise)
+Tensor conv3x3_dgrad_weight(const Tensor& w) {
+  c10::DeviceGuard g(w.device());
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3 && w.scalar_type() == at::kBFloat16 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv3x3_dgrad_weight: channels-last bf16 [cout, cin, 3, 3]");
+  const int64_t cout = w.size(0), cin = w.size(1);
+  TORCH_CHECK(cout % 8 == 0 && cin % 8 == 0, "conv3x3_dgrad_weight: channels must be multiples of 8");
+  check_align16(w, "w");
+  auto out = at::empty({cin, 9 * cout}, w.options().memory_format(at::MemoryFormat::Contiguous));
+  dph::conv3x3_dgrad_weight(w.data_ptr(), out.data_ptr(), cout, cin, cur_stream());
+  return out;
+}
+
 // ------------------------------------------------------------------------------------------------ BatchNorm+act
 // x: channels-last [N, C, H, W] (or contiguous [M, C]); statistics over everything but C.
 int64_t bn_channels(const Tensor& x) {
@@ -1259,6 +1274,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("ts_gemm_nt_stats(Tensor A, Tensor B, int H=0, int W=0, Tensor? pro_ss=None) -> (Tensor, Tensor)");
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0, Tensor? pro_ss=None) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
+  m.def("conv3x3_dgrad_weight(Tensor w) -> Tensor");
   m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
   m.def("maxpool_s2_bwd(Tensor dy, Tensor tap, int H, int W, int k) -> Tensor");
@@ -1321,6 +1337,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("ts_gemm_nt_stats", &ts_gemm_nt_stats);
   m.impl("ts_gemm_tn_", &ts_gemm_tn_);
   m.impl("transpose2d", &transpose2d);
+  m.impl("conv3x3_dgrad_weight", &conv3x3_dgrad_weight);
   m.impl("maxpool_s2_fwd", &maxpool_s2_fwd);
   m.impl("channel_sum", &channel_sum);
   m.impl("maxpool_s2_bwd", &maxpool_s2_bwd);

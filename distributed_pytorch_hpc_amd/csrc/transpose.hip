@@ -11,9 +11,14 @@ namespace dph {
 namespace {
 constexpr int TT = 64, PITCH = 66;
 
+// gridDim.z > 1: a batch of transposes, matrix z read at src + (REV ? nz - 1 - z : z) * sz, written at dst + z * dz.
 __global__ __launch_bounds__(256) void transpose_k(const bf16* __restrict__ src, bf16* __restrict__ dst, int64_t R,
-                                                   int64_t C, int64_t lds_src, int64_t ld_dst) {
+                                                   int64_t C, int64_t lds_src, int64_t ld_dst, int64_t sz = 0,
+                                                   int64_t dz = 0, bool rev = false) {
   __shared__ bf16 tile[TT * PITCH];
+  const int z = blockIdx.z, nz = gridDim.z;
+  src += (rev ? nz - 1 - z : z) * sz;
+  dst += z * dz;
   const int64_t r0 = (int64_t)blockIdx.y * TT, c0 = (int64_t)blockIdx.x * TT;
   const int t = threadIdx.x;
   // load: 64 rows x 8 chunks of 8 elements; 2 chunks per thread
@@ -54,7 +59,16 @@ __global__ __launch_bounds__(256) void transpose_k(const bf16* __restrict__ src,
 void transpose2d(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_src, int64_t ld_dst, hipStream_t st) {
   if (R == 0 || C == 0) return;
   const dim3 grid((unsigned)((C + TT - 1) / TT), (unsigned)((R + TT - 1) / TT));
-  hipLaunchKernelGGL(transpose_k, grid, dim3(256), 0, st, (const bf16*)src, (bf16*)dst, R, C, ld_src, ld_dst);
+  hipLaunchKernelGGL(transpose_k, grid, dim3(256), 0, st, (const bf16*)src, (bf16*)dst, R, C, ld_src, ld_dst,
+                     (int64_t)0, (int64_t)0, false);
+}
+
+void conv3x3_dgrad_weight(const void* w, void* out, int64_t cout, int64_t cin, hipStream_t st) {
+  // w: channels-last [cout][3][3][cin]; out[c][t][co] = w[co][8 - t][c] -- nine [cout, cin] transposes, taps reversed
+  if (cout == 0 || cin == 0) return;
+  const dim3 grid((unsigned)((cin + TT - 1) / TT), (unsigned)((cout + TT - 1) / TT), 9u);
+  hipLaunchKernelGGL(transpose_k, grid, dim3(256), 0, st, (const bf16*)w, (bf16*)out, cout, cin, 9 * cin, 9 * cout,
+                     cin, cout, true);
 }
 
 }  // namespace dph

@@ -100,6 +100,11 @@ def _transpose2d(x):
     return x.new_empty((x.shape[1], x.shape[0]))
 
 
+@register_fake("dph::conv3x3_dgrad_weight")
+def _conv3x3_dgrad_weight(w):
+    return w.new_empty((w.shape[1], 9 * w.shape[0]), memory_format=torch.contiguous_format)
+
+
 def _pool_out(n, k):
     return (n - 1) // 2 + 1 if k == 3 else n // 2
 

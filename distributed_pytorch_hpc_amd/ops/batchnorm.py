@@ -17,7 +17,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
-from .conv import _DIRECT
+from .conv import _DIRECT, weight_t
 
 
 def _pow2_channels(c: int) -> bool:
@@ -196,7 +196,7 @@ class _BNReLUConv1x1Fn(torch.autograd.Function):
                 gw3 = gw3.view(cout, C, 1, 1)
         dx = dw = db = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
-            dyb = _lib.ops().ts_gemm_nt(dy2, w2d.t().contiguous())   # gradient of relu(bn(x)), [M, C]
+            dyb = _lib.ops().ts_gemm_nt(dy2, weight_t(w2d))   # gradient of relu(bn(x)), [M, C]
             dyb = dyb.view(B, H, W, C).permute(0, 3, 1, 2)
             need_wb = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
             direct = (need_wb and bp is not None and _DIRECT and all(

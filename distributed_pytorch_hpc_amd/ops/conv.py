@@ -48,6 +48,18 @@ def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1).contiguous().view(-1, t.shape[1])
 
 
+_HIP_WT = os.environ.get("DPH_CONV_WT", "hip") != "aten"   # input-gradient weight copies: HIP kernels or ATen (A/B)
+
+
+def weight_t(w2: torch.Tensor) -> torch.Tensor:
+    """[Cout, Cin] -> [Cin, Cout] for an input-gradient GEMM: the HIP tile transpose (csrc/transpose.hip) instead of
+    ATen's element-wise strided copy."""
+    if _HIP_WT and w2.is_cuda and w2.dtype == torch.bfloat16 and w2.stride(1) == 1 and w2.stride(0) % 8 == 0 and \
+            w2.shape[0] % 8 == 0 and w2.data_ptr() % 16 == 0:
+        return _lib.ops().transpose2d(w2)
+    return w2.t().contiguous()
+
+
 def _main_grad_target(w: torch.Tensor, shape):
     """The engine-owned gradient buffer of parameter ``w`` viewed as ``shape`` (parallel/data_parallel.py keeps
     ``main_grad`` views into its flat bucket), or None when the weight gradient has to be returned to autograd."""
@@ -159,7 +171,7 @@ class _Conv1x1Fn(torch.autograd.Function):
                     raise RuntimeError("Conv1x1: residual gradient slot armed but empty (backward order)")
                 add = _nhwc2d(slot.t.to(torch.bfloat16))
                 slot.t = None
-            dx2 = _lib.ops().ts_gemm_nt(dy2, w2.t().contiguous(), 0, 0, add)    # [M, Cin] (+ residual grad)
+            dx2 = _lib.ops().ts_gemm_nt(dy2, weight_t(w2), 0, 0, add)    # [M, Cin] (+ residual grad)
             dx = dx2.view(B, H, W, C).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             cout = w2.shape[0]
@@ -223,7 +235,10 @@ class _Conv3x3Fn(torch.autograd.Function):
         dx = gw = None
         if ctx.needs_input_grad[0]:
             # dX = conv3x3(dY, W') with W'[ci, (kh, kw), co] = W[co, ci, 2 - kh, 2 - kw]
-            wf = wb.flip(2, 3).permute(1, 2, 3, 0).reshape(C, 9 * cout)
+            if _HIP_WT and wb.is_contiguous(memory_format=torch.channels_last) and cout % 8 == 0 and C % 8 == 0:
+                wf = _lib.ops().conv3x3_dgrad_weight(wb)                  # one launch, HBM-speed tiles
+            else:
+                wf = wb.flip(2, 3).permute(1, 2, 3, 0).reshape(C, 9 * cout)
             dx = _lib.ops().ts_gemm_nt(dy2, wf, H, W).view(B, H, W, C).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] and _CONV3_WGRAD != "dph":
             # weight gradient on MIOpen: 1.0-1.5x the split-pixel kernel on the ResNet-50 shapes

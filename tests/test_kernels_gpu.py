@@ -1160,3 +1160,16 @@ def test_stem_conv_channel_padding_matches_conv2d(dph_native, autocast):
     yb.float().backward(g)
     assert new.weight.grad.shape == (64, 3, 7, 7)
     assert rel_err(new.weight.grad, ref.weight.grad) < tol
+
+
+@pytest.mark.parametrize("cout,cin", [(64, 64), (128, 256), (520, 72)])
+def test_conv3x3_dgrad_weight_and_weight_t(dph_native, cout, cin):
+    """The 3x3 input-gradient weight (nine tap-reversed transposes in one launch) and the 1x1 weight transpose equal
+    ATen's element-wise copies bitwise."""
+    from distributed_pytorch_hpc_amd.ops.conv import weight_t
+
+    w = torch.randn(cout, cin, 3, 3, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ref = w.flip(2, 3).permute(1, 2, 3, 0).reshape(cin, 9 * cout)
+    assert torch.equal(dph_native.conv3x3_dgrad_weight(w), ref)
+    w2 = torch.randn(cout, cin, device=DEV).to(torch.bfloat16)
+    assert torch.equal(weight_t(w2), w2.t().contiguous())
