@@ -256,10 +256,13 @@ class ZeRO3Engine:
 
     def _pre_backward(self, u, module, grad_out):
         self._gather(u)
+        # a freshly allocated full gradient holds garbage (its padding included); an aliased one is the shard, whose
+        # padding was zeroed at construction and is never written, and every parameter slice in it is either written
+        # by this backward or zeroed in _launch -- so only the non-aliased buffer needs the fill
         if not self._alias:
             _alloc(u.grad_full)
-        if not any(p._dph_accum for p in u.params):
-            u.grad_full.zero_()
+            if not any(p._dph_accum for p in u.params):
+                u.grad_full.zero_()
         if self.prefetch and u.idx >= 1 and u.idx - 1 < len(self.units) - 1:
             self._start_gather(self.units[u.idx - 1])
 
