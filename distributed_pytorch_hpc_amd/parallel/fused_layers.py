@@ -33,6 +33,9 @@ from .linear import _dgrad, weight_grad
 # -0.6 % (the CDNA4 forward GEMM is 0.95x the library on w13, more than the saved swiglu_fwd pass).
 _FUSED_MLP = os.environ.get("DPH_FUSED_MLP", "bwd")
 _FUSED_MLP = False if _FUSED_MLP == "0" else ("bwd" if _FUSED_MLP == "bwd" else True)
+# DPH_FUSED_QKV=1: RoPE in the wqkv GEMM's epilogue -- off: -0.4 % in-step even on the lookahead NT variant
+# (27 763 / 27 719 vs 27 664 / 27 597 tokens/s, profiles/r3/ab_fused_qkv_v1/): the kernel's 0.95x on wqkv outweighs
+# the saved rope pass
 _FUSED_QKV = os.environ.get("DPH_FUSED_QKV", "0") != "0"
 # DPH_GEMM_NT: which forward / input-gradient GEMMs run on the CDNA4 kernel instead of hipBLASLt:
 # "fused" (default: only those with a fused epilogue), "all", or "0" (none -- also disables the fused paths)
