@@ -71,7 +71,7 @@ __device__ __forceinline__ void wait_vm() { wait_vmcnt<N>(); }
 // is a compile-time constant.
 #define DPH_GEMM_REGIONS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
 
-template <typename OutT, bool ACCUM>
+template <typename OutT, bool ACCUM, bool LDS_EPI = true>
 __global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                      OutT* __restrict__ C, int M, int N, int K, int64_t lda,
                                                      int64_t ldb, int64_t ldc, int64_t cstride) {
@@ -223,21 +223,53 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, 
 #undef DPH_S
 
   // ---- epilogue: register i of tile (mt, nt) holds C[row (i&3) + 8(i>>2) + 4h][col l32] ----
+  if constexpr (!ACCUM && LDS_EPI) {
+    // Through LDS (free after the main loop): the tile goes out as 16-B row segments -- 16 (bf16) / 32 (fp32, two
+    // 128-row passes) vector stores per thread instead of 128 scalar 2- / 4-byte stores per lane, which left the
+    // epilogue store-issue-bound.  (ACCUM keeps the scalar path: one rounding of old + acc.)
+    constexpr int VE = 16 / (int)sizeof(OutT);                 // elements per 16-B segment
+    constexpr int PR = (int)(sizeof(OutT) == 2 ? 256 : 128);   // rows per pass (128 KB of LDS)
+    constexpr int NPASS = 256 / PR, SPR = 256 / VE;            // passes, segments per row
+    OutT* ct = reinterpret_cast<OutT*>(lds);
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+    for (int pass = 0; pass < NPASS; ++pass) {
+      __syncthreads();   // the main loop's / previous pass's LDS reads are done
+      if (NPASS == 1 || wm == pass) {
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const int col = n0 + wn * 64 + nt * 32 + l32;
+        for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int row = m0 + wm * 128 + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (row >= M || col >= N) continue;
-        OutT* p = C + (int64_t)row * ldc + col;
-        float v = acc[mt][nt][i];
-        if (ACCUM) v += (float)*p;
-        *p = (OutT)v;
+          for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int r = (NPASS == 1 ? wm * 128 : 0) + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+              ct[r * 256 + wn * 64 + nt * 32 + l32] = (OutT)acc[mt][nt][i];
+            }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int c = threadIdx.x; c < PR * SPR; c += GNT) {
+        const int r = c / SPR, seg = c % SPR;
+        const int row = m0 + pass * PR + r, col = n0 + seg * VE;
+        if (row < M && col < N)   // N % 8 == 0: a segment is all in or all out
+          *reinterpret_cast<u32x4*>(C + (int64_t)row * ldc + col) =
+              *reinterpret_cast<const u32x4*>(ct + r * 256 + seg * VE);
       }
     }
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int col = n0 + wn * 64 + nt * 32 + l32;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = m0 + wm * 128 + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (row >= M || col >= N) continue;
+          OutT* p = C + (int64_t)row * ldc + col;
+          *p = (OutT)(ACCUM ? acc[mt][nt][i] + (float)*p : acc[mt][nt][i]);
+        }
+      }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -561,6 +593,10 @@ void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_
              int64_t ldc, int out_dtype, bool accumulate, hipStream_t st, const GemmTnPlan* plan,
              float* workspace) {
   const bool m16 = gemm_tn_mfma() == 16;
+  static const bool lds_epi = [] {   // DPH_WGRAD_EPI=scalar: per-element epilogue stores (A/B runs)
+    const char* e = getenv("DPH_WGRAD_EPI");
+    return !(e && e[0] == 's');
+  }();
   const size_t lds = 0;   // static: 8 x 16 KB regions
   const dim3 block(GNT);
   auto launch = [&](const bf16* a, const bf16* b, void* c, int64_t m, int64_t n, int64_t k, int64_t ldc_, int S,
@@ -570,6 +606,9 @@ void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_
   do {                                                                                                         \
     if (m16)                                                                                                   \
       hipLaunchKernelGGL((gemm_tn16_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,     \
+                         lda, ldb, ldc_, cstride);                                                             \
+    else if (!lds_epi)                                                                                         \
+      hipLaunchKernelGGL((gemm_tn_k<T, ACC, false>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,  \
                          lda, ldb, ldc_, cstride);                                                             \
     else                                                                                                       \
       hipLaunchKernelGGL((gemm_tn_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k, lda,  \
