@@ -62,7 +62,11 @@ __device__ __forceinline__ float nt_sigmoid(float x) { return 1.f / (1.f + __exp
 // segment (interleaved with its MFMAs) into the B register set phase 4 does not use, so the four read segments
 // carry 8 / 4 / 8 / 0 ds_read_b128 instead of 12 / 4 / 8 / 0.  Reading in an MFMA segment needs the data retired one
 // phase earlier under the stagger, so three quarters stay in flight (vmcnt(6)) instead of four.
-template <int MODE, int LOOK>
+// LEPI (every mode): the epilogue goes through LDS -- dh / C rounded to bf16 into a 256 x 256 image (16-B chunks
+// XOR-swizzled by the row, conflict-free 8-B writes from the accumulators), then whole 16-B row segments: one vector
+// load per operand and one store per output (DSWIGLU: x13's gate / up in, d13's dgate / dup out) instead of 8-B
+// accesses at 16 rows per instruction.  Same rounding and math as the register epilogue, so bitwise-equal output.
+template <int MODE, int LOOK, bool LEPI = false>
 __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
   constexpr int VMC = LOOK ? 6 : 8;
   __shared__ __attribute__((aligned(1024))) char lds[2 * BUFB];
@@ -256,6 +260,109 @@ __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
   wait_vmcnt<0>();                            // the clamped tail DMAs must land before the workgroup exits
 
   // ---- epilogue: acc[mb][nb][j] = C[token m0 + 128 wm + 16 mb + r16][feature col(nb) + 4 kq + j] ----
+  if constexpr (LEPI && MODE == kNtSwiglu) {
+    // the tile's 128 gate units | their 128 up units, as image columns 0..127 | 128..255
+    __syncthreads();
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int row = 128 * wm + 16 * mb + r16, col = (nb >> 1) * 128 + 32 * wn + 16 * (nb & 1) + 4 * kq;
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[mb][nb][j];
+        *reinterpret_cast<bf16x4*>(lds + row * 512 + (((col >> 3) ^ (row & 15)) << 4) + (col & 7) * 2) = o;
+      }
+    __syncthreads();
+    const int c = tid & 15;                       // gate chunk c (units 8c ..) and its up chunk 16 + c
+    const int64_t u0 = (int64_t)tn * 128 + c * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int row = (tid >> 4) + 32 * k;
+      const bf16x8 g = *reinterpret_cast<const bf16x8*>(lds + row * 512 + ((c ^ (row & 15)) << 4));
+      const bf16x8 up = *reinterpret_cast<const bf16x8*>(lds + row * 512 + (((16 + c) ^ (row & 15)) << 4));
+      bf16x8 hv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gf = (float)g[j];   // exactly swiglu_fwd_k's math on the rounded gate / up
+        hv[j] = (bf16)(gf * nt_sigmoid(gf) * (float)up[j]);
+      }
+      const int64_t t = (int64_t)m0 + row;
+      *reinterpret_cast<bf16x8*>((bf16*)p.C + t * p.ldc + u0) = g;
+      *reinterpret_cast<bf16x8*>((bf16*)p.C + t * p.ldc + p.H + u0) = up;
+      *reinterpret_cast<bf16x8*>((bf16*)p.C2 + t * p.ldc2 + u0) = hv;
+    }
+    return;
+  }
+  if constexpr (LEPI && (MODE == kNtStore || MODE == kNtDswiglu || MODE == kNtRope)) {
+    __syncthreads();   // every wave is past its last fragment read
+    // image byte offset of (row, 16-B chunk c, byte b): row * 512 + ((c ^ (row & 15)) << 4) + b
+#pragma unroll
+    for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        const int row = 128 * wm + 16 * mb + r16, col = 64 * wn + 16 * nb + 4 * kq;
+        f32x4 v = acc[mb][nb];
+        if constexpr (MODE == kNtRope) {   // rotated on the fp32 accumulators (one rounding), as the register path
+          const int n = tn * NBN + col;
+          if (n < p.n_rot) {
+            const int64_t t = (int64_t)m0 + row;
+            const int pos = (int)(t % p.S) + p.pos_off, i0 = (n % p.hd) >> 1;
+            const float* ct = p.rope_cos + (int64_t)pos * (p.hd >> 1) + i0;
+            const float* st = p.rope_sin + (int64_t)pos * (p.hd >> 1) + i0;
+            const float c0 = ct[0], c1 = ct[1], s0 = st[0], s1 = st[1];
+            const float a0 = v[0], b0 = v[1], a1 = v[2], b1 = v[3];
+            v[0] = a0 * c0 - b0 * s0;
+            v[1] = a0 * s0 + b0 * c0;
+            v[2] = a1 * c1 - b1 * s1;
+            v[3] = a1 * s1 + b1 * c1;
+          }
+        }
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+        *reinterpret_cast<bf16x4*>(lds + row * 512 + (((col >> 3) ^ (row & 15)) << 4) + (col & 7) * 2) = o;
+      }
+    __syncthreads();
+    const int c = tid & 31;                       // this thread's 16-B column chunk (512 threads, 32 per row)
+    const int64_t n0c = (int64_t)tn * NBN + c * 8;
+    constexpr int BATCH = 4;
+#pragma unroll
+    for (int k0 = 0; k0 < 16; k0 += BATCH) {      // rows tid / 32 + 16 k
+      bf16x8 dh[BATCH], gv[BATCH], uv[BATCH];
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int row = (tid >> 5) + 16 * (k0 + k);
+        dh[k] = *reinterpret_cast<const bf16x8*>(lds + row * 512 + ((c ^ (row & 15)) << 4));
+        if constexpr (MODE == kNtDswiglu) {
+          const int64_t t = (int64_t)m0 + row;
+          gv[k] = *reinterpret_cast<const bf16x8*>((const bf16*)p.X + t * p.ldx + n0c);
+          uv[k] = *reinterpret_cast<const bf16x8*>((const bf16*)p.X + t * p.ldx + p.H + n0c);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        const int64_t t = (int64_t)m0 + (tid >> 5) + 16 * (k0 + k);
+        bf16* out = (bf16*)p.C + t * p.ldc + n0c;
+        if constexpr (MODE == kNtDswiglu) {
+          bf16x8 dg, du;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float d = (float)dh[k][j];
+            const float g = (float)gv[k][j], u = (float)uv[k][j];
+            const float sg = nt_sigmoid(g);
+            du[j] = (bf16)(d * (g * sg));
+            dg[j] = (bf16)(d * u * sg * (1.f + g * (1.f - sg)));
+          }
+          *reinterpret_cast<bf16x8*>(out) = dg;
+          *reinterpret_cast<bf16x8*>(out + p.H) = du;
+        } else {
+          *reinterpret_cast<bf16x8*>(out) = dh[k];
+        }
+      }
+    }
+    return;
+  }
   const int64_t tok0 = (int64_t)m0 + 128 * wm + r16;
   if constexpr (MODE == kNtSwiglu) {
     // gate units u = 128 tn + 32 wn + 16 nb + 4 kq + j (nb < 2); acc[.][nb + 2] holds the matching up values
@@ -369,16 +476,32 @@ void gemm_nt(int mode, const GemmNtParams& prm, hipStream_t st) {
   p.tiles_n = mode == kNtSwiglu ? p.N / 128 : p.N / NBN;
   const dim3 grid((unsigned)((p.M / NBM) * p.tiles_n)), block(NNT);
   const bool look = gemm_nt_variant() == 1;
-#define DPH_NT_LAUNCH(MD)                                                                     \
+  static const bool lepi = [] {   // DPH_NT_EPI=reg: the register epilogue for every mode (A/B runs)
+    const char* e = getenv("DPH_NT_EPI");
+    return !(e && e[0] == 'r');
+  }();
+#define DPH_NT_LAUNCH(MD, LE)                                                                 \
   do {                                                                                        \
-    if (look) hipLaunchKernelGGL((gemm_nt_k<MD, 1>), grid, block, 0, st, p);                 \
-    else hipLaunchKernelGGL((gemm_nt_k<MD, 0>), grid, block, 0, st, p);                      \
+    if (look) hipLaunchKernelGGL((gemm_nt_k<MD, 1, LE>), grid, block, 0, st, p);             \
+    else hipLaunchKernelGGL((gemm_nt_k<MD, 0, LE>), grid, block, 0, st, p);                  \
   } while (0)
   switch (mode) {
-    case kNtSwiglu: DPH_NT_LAUNCH(kNtSwiglu); break;
-    case kNtDswiglu: DPH_NT_LAUNCH(kNtDswiglu); break;
-    case kNtRope: DPH_NT_LAUNCH(kNtRope); break;
-    default: DPH_NT_LAUNCH(kNtStore); break;
+    case kNtSwiglu:
+      if (lepi) DPH_NT_LAUNCH(kNtSwiglu, true);
+      else DPH_NT_LAUNCH(kNtSwiglu, false);
+      break;
+    case kNtDswiglu:
+      if (lepi) DPH_NT_LAUNCH(kNtDswiglu, true);
+      else DPH_NT_LAUNCH(kNtDswiglu, false);
+      break;
+    case kNtRope:
+      if (lepi) DPH_NT_LAUNCH(kNtRope, true);
+      else DPH_NT_LAUNCH(kNtRope, false);
+      break;
+    default:
+      if (lepi) DPH_NT_LAUNCH(kNtStore, true);
+      else DPH_NT_LAUNCH(kNtStore, false);
+      break;
   }
 #undef DPH_NT_LAUNCH
 }

@@ -153,3 +153,21 @@ def test_gemm_nt_pipeline_variants_bitwise(dph_native, variant, M, N, K):
     assert torch.equal(c0, c1)
     assert torch.equal(s0[0], s1[0]) and torch.equal(s0[1], s1[1])
     assert rel_err(c1, a.float() @ b.float().t()) < 5e-3
+
+
+def test_gemm_nt_epilogue_forms_bitwise(dph_native):
+    """The LDS-staged epilogue (default for STORE / DSWIGLU) and the register epilogue (DPH_NT_EPI=reg) produce
+    bitwise-identical outputs (same bf16 rounding of dh, same SwiGLU-backward math); run in child processes because
+    the form is read once per process."""
+    import os
+    import subprocess
+    import sys
+
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "nt_epi_check.py")
+    outs = []
+    for form in ("reg", "lds"):
+        env = dict(os.environ, DPH_NT_EPI=form)
+        p = subprocess.run([sys.executable, script], env=env, capture_output=True, text=True, timeout=110)
+        assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+        outs.append(p.stdout.strip().splitlines()[-1])
+    assert outs[0] == outs[1]
