@@ -13,8 +13,8 @@ Weight gradients take the same route as every other linear layer of the framewor
 ``weight_grad`` writes them straight into the data-parallel engine's bucket and notifies it), so the engines'
 overlapped reduce-scatter / all-reduce see no difference.  The fused paths are taken for plain (not tensor-parallel,
 not FP8) bf16 projections whose shapes the kernel tiles (rows % 256, features % 256, K % 64); everything else runs
-the unfused modules.  ``DPH_FUSED_MLP=0`` / ``DPH_FUSED_QKV=0`` turn them off (A/B runs); by default only the MLP's
-backward fusion is on.
+the unfused modules.  ``DPH_FUSED_MLP=0`` / ``DPH_FUSED_QKV=1`` switch them (A/B runs); by default the MLP's
+fusions are on and the QKV + RoPE one is off.
 """
 from __future__ import annotations
 
@@ -28,14 +28,15 @@ from ..ops import fp8 as _fp8
 from .linear import _dgrad, weight_grad
 
 # DPH_FUSED_MLP: "1" = SwiGLU in the w13 GEMM epilogue AND dSwiGLU in w2's input-gradient epilogue; "bwd" = only the
-# backward fusion (forward: library GEMM + swiglu_fwd); "0" = unfused modules.  Default "bwd": +0.3-0.4 % tokens/s on
-# the Llama-2-7B step (interleaved A/B on one MI355X, profiles/r3/ab_fused_mlp_bwd/); the forward fusion measured
-# -0.6 % (the CDNA4 forward GEMM is 0.95x the library on w13, more than the saved swiglu_fwd pass).
-_FUSED_MLP = os.environ.get("DPH_FUSED_MLP", "bwd")
+# backward fusion (forward: library GEMM + swiglu_fwd); "0" = unfused modules.  Default "1": the backward fusion
+# measured +0.4 % on the Llama-2-7B step (profiles/r3/ab_fused_mlp_bwd/); the forward fusion, -0.6 % with the register
+# epilogue, is +0.2 % since the GEMM's epilogue goes through LDS (w13 + SwiGLU 4.15 ms vs 4.24 for the library GEMM +
+# swiglu_fwd; 28 128 / 28 070 vs 28 095 / 27 996 tokens/s, profiles/r3/ab_fused_mlp_fwd_lds/).
+_FUSED_MLP = os.environ.get("DPH_FUSED_MLP", "1")
 _FUSED_MLP = False if _FUSED_MLP == "0" else ("bwd" if _FUSED_MLP == "bwd" else True)
-# DPH_FUSED_QKV=1: RoPE in the wqkv GEMM's epilogue -- off: -0.4 % in-step even on the lookahead NT variant
-# (27 763 / 27 719 vs 27 664 / 27 597 tokens/s, profiles/r3/ab_fused_qkv_v1/): the kernel's 0.95x on wqkv outweighs
-# the saved rope pass
+# DPH_FUSED_QKV=1: RoPE in the wqkv GEMM's epilogue -- off: -0.4 % in-step on the lookahead NT variant
+# (profiles/r3/ab_fused_qkv_v1/) and -0.5 % still with the LDS epilogue (27 954 / 27 914 vs 28 128 / 28 070,
+# profiles/r3/ab_fused_mlp_fwd_lds/): the kernel's 0.97x on wqkv outweighs the saved rope pass
 _FUSED_QKV = os.environ.get("DPH_FUSED_QKV", "0") != "0"
 # DPH_GEMM_NT: which forward / input-gradient GEMMs run on the CDNA4 kernel instead of hipBLASLt:
 # "fused" (default: only those with a fused epilogue), "all", or "0" (none -- also disables the fused paths)
