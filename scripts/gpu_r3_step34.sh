@@ -11,3 +11,5 @@ for rep in 1 2; do
   DPH_FUSED_MLP=1 DPH_FUSED_QKV=0 run r3_s34_bench_mlp_rep$rep 400 python -u bench.py --steps 10 --warmup 3 || exit 1
   DPH_FUSED_MLP=1 DPH_FUSED_QKV=1 run r3_s34_bench_mlpqkv_rep$rep 400 python -u bench.py --steps 10 --warmup 3 || exit 1
 done
+run r3_s34_ntbench_all 600 python -u benchmarks/gemm_nt_bench.py --variants 1 --rounds 3 || exit 1
+grep -h "TF\|SwiGLU" $O/r3_s34_ntbench_all.log
