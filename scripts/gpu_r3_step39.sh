@@ -1,0 +1,12 @@
+#!/usr/bin/env bash
+# round 3 step 39: tree check after the attention LDS epilogues -- GPU tier, smoke, bench x2, 7B kernel-trace profile, ResNet
+export TMPDIR=/tmp
+O=gpurun_out
+mkdir -p $O
+run() { local name=$1; local t=$2; shift 2; timeout -k 10 $t "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc $(grep -o '"value": [0-9.]*' $O/$name.log | tail -1)"; return $rc; }
+run r3_s39_tier 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/ -m gpu || exit 1
+run r3_s39_smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1
+run r3_s39_bench1 400 python -u bench.py --steps 20 --warmup 5 || exit 1
+run r3_s39_bench2 400 python -u bench.py --steps 20 --warmup 5 || exit 1
+timeout -k 10 700 bash scripts/prof_bench.sh $O/r3_s39_prof7b > $O/r3_s39_prof7b.log 2>&1; echo "prof7b rc=$?"
+run r3_s39_resnet 400 python -u bench.py --layout resnet-fsdp --steps 20 --warmup 5 || exit 1
