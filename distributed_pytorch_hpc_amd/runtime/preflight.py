@@ -17,7 +17,6 @@ by a timeout, and run on the job's own process group.
 from __future__ import annotations
 
 import datetime
-import time
 from dataclasses import asdict
 
 import torch
@@ -145,14 +144,19 @@ def probe_alpha_beta(group=None, device=None, sizes_mib=(4, 16, 64, 256), dtype=
     stop the sweep (slow backends, e.g. gloo on CPU: the fit then uses the smaller sizes)."""
     world = dist.get_world_size(group)
     fits = {}
-    t_start = time.perf_counter()
+    # The stop decision must be identical on every rank (a rank that skips a size while the others enter its
+    # collective deadlocks the job), so it is taken on the measured times -- measure() returns the slowest rank's
+    # time, the same value everywhere -- never on a rank-local wall clock.
+    spent = 0.0
     for op in ("reduce_scatter", "all_gather"):
         samples = []
         for mib in sizes_mib:
-            if samples and time.perf_counter() - t_start > budget_s:
+            if samples and spent > budget_s:
                 break
-            samples += cost_model.measure(op, [int(mib * 2 ** 20)], group=group, device=device, dtype=dtype,
-                                          iters=iters, warmup=1)
+            got = cost_model.measure(op, [int(mib * 2 ** 20)], group=group, device=device, dtype=dtype,
+                                     iters=iters, warmup=1)
+            spent += sum(t for _, t in got) * (iters + 1)
+            samples += got
         if len(samples) < 2:   # need two points for a slope; fall back to the smallest extra size
             samples += cost_model.measure(op, [int(2 * sizes_mib[0] * 2 ** 20)], group=group, device=device,
                                           dtype=dtype, iters=iters, warmup=1)

@@ -202,3 +202,23 @@ def test_alpha_beta_probe_and_bucket_choice():
     for a, b in fits.values():
         assert a >= 0 and b > 0
     assert 1.0 <= mib <= 64.0
+
+
+def _probe_skew_worker(rank, world):
+    import time
+
+    from distributed_pytorch_hpc_amd.runtime import preflight
+
+    # rank 1 arrives late: a stop rule on each rank's own wall clock would let rank 0 quit the sweep while rank 1
+    # enters the next size's collective (deadlock); the rule on the max-reduced measured times is the same everywhere
+    if rank == 1:
+        time.sleep(1.0)
+    fits = preflight.probe_alpha_beta(None, None, sizes_mib=(0.0625, 0.125, 0.25), budget_s=0.5)
+    return {k: (v.alpha_s, v.beta_bus_Bps, v.source) for k, v in fits.items()}
+
+
+def test_alpha_beta_probe_stop_rule_is_rank_consistent():
+    from dist_utils import run_distributed
+
+    outs = run_distributed(_probe_skew_worker, 2)
+    assert outs[0] == outs[1], outs
