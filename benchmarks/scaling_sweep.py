@@ -2,7 +2,8 @@
 """Weak-scaling sweep of bench.py on one node: N = 1, 2, 4, 8 ranks back to back, one rank per GPU over RCCL.
 
 Each N runs ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py
---gpus N ...`` (N = 1 runs bench.py directly, the single-GPU engine), reads bench.py's JSON line and reports
+--gpus N ...`` (N = 1 runs bench.py directly: the same sharded engine in an RCCL world of one), reads bench.py's
+JSON line and reports
 
     tokens/s (whole job), per GPU, ms/step, and scaling efficiency E(N) = value(N) / (N * value(1))
 
