@@ -19,12 +19,10 @@ through csrc/decode.hip), driven by ``inference.Generator``.
 """
 from __future__ import annotations
 
-import math
-from dataclasses import dataclass, field, replace
+from dataclasses import dataclass, replace
 from typing import Optional
 
 import torch
-import torch.nn.functional as F
 from torch import nn
 
 from .. import ops

@@ -13,7 +13,7 @@ available (as torchvision).  ``BatchNormAct2d`` subclasses ``nn.BatchNorm2d``, s
 """
 from __future__ import annotations
 
-from typing import Optional, Type, Union
+from typing import Type, Union
 
 import torch
 from torch import nn

@@ -13,7 +13,7 @@ The reference never checkpoints activations.  On MI355X the default is to keep e
 """
 from __future__ import annotations
 
-from typing import Callable, Optional
+from typing import Callable
 
 import torch
 from torch import nn

@@ -35,7 +35,7 @@ import torch.distributed as dist
 from .. import ops
 from ..comm import functional as cf
 from ..ops import _lib
-from ..ops.rope import rope_, rope_reference
+from ..ops.rope import rope_reference
 
 
 def _ws(g):

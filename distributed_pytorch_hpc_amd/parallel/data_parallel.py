@@ -26,11 +26,10 @@ resnet_fsdp_training.py:193-212).  The design here is MI355X-first rather than a
 from __future__ import annotations
 
 import contextlib
-import math
 import os
 from dataclasses import dataclass
 from functools import partial
-from typing import Iterable, Optional
+from typing import Optional
 
 import torch
 import torch.distributed as dist

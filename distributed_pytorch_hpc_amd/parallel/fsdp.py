@@ -36,7 +36,7 @@ from ..ops import _lib
 from ..train import optim as optim_ref
 from ..utils.flat import ALIGN, align_up, flat_order, flat_order_like, param_view
 from .data_parallel import DataParallelEngine, MixedPrecision, OptimConfig, _EngineOptimizer, _hyper_for
-from .linear import convert_linears_, join_wgrad_stream, wgrad_stream
+from .linear import convert_linears_, join_wgrad_stream
 
 
 class ShardingStrategy(Enum):

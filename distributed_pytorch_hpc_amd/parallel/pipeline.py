@@ -17,7 +17,7 @@ MI355X node); opposite-direction transfers of the steady 1F1B phase are posted t
 from __future__ import annotations
 
 import contextlib
-from typing import Callable, Optional, Sequence
+from typing import Callable, Optional
 
 import torch
 import torch.distributed as dist

@@ -34,7 +34,6 @@ from typing import Callable, Optional
 
 import torch
 import torch.distributed as dist
-import torch.nn.functional as F
 from torch import nn
 
 from .. import ops

@@ -10,7 +10,6 @@ import sys
 
 import pytest
 import torch
-import torch.distributed as dist
 
 from distributed_pytorch_hpc_amd.runtime.env import free_port
 

@@ -1,5 +1,4 @@
 """Domain parallelism: a conv-BN-ReLU stack on a latitude-sharded field equals the unsharded model (gloo)."""
-import copy
 
 import pytest
 import torch

@@ -35,8 +35,7 @@ def _reference():
 
 def _worker(rank, world, strategy, policy_kind):
     from distributed_pytorch_hpc_amd.models.llama2 import TransformerBlock
-    from distributed_pytorch_hpc_amd.parallel.fsdp import (FSDP, ModuleWrapPolicy, ShardingStrategy,
-                                                           size_based_auto_wrap_policy)
+    from distributed_pytorch_hpc_amd.parallel.fsdp import FSDP, ModuleWrapPolicy, size_based_auto_wrap_policy
 
     m = _model()
     policy = {"block": ModuleWrapPolicy({TransformerBlock}), "size": size_based_auto_wrap_policy(5000),
