@@ -15,6 +15,11 @@ export TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC=${TORCH_NCCL_HEARTBEAT_TIMEOUT_SEC:-600}
 export NCCL_DEBUG=${NCCL_DEBUG:-VERSION}
 
 # ---- knobs to sweep on the box (leave unset for RCCL's own topology-aware defaults) ----
+# benchmarks/rccl_sweep.py measures them and writes the winning exports for bucket-sized traffic; picked up here
+# when present (DPH_RCCL_ENV overrides the path)
+_dph_rccl_env=${DPH_RCCL_ENV:-$(dirname "${BASH_SOURCE[0]}")/../results/rccl_sweep/rccl_env.sh}
+[ -f "$_dph_rccl_env" ] && . "$_dph_rccl_env"
+unset _dph_rccl_env
 # export NCCL_MIN_NCHANNELS=32          # more channels -> more xGMI links busy per collective
 # export NCCL_MAX_NCHANNELS=64
 # export NCCL_ALGO=Ring                 # Ring | Tree (direct/one-shot variants are chosen by RCCL per size)
