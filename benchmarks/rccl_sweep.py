@@ -106,6 +106,28 @@ def summarise(runs: list[dict], min_gain: float = 1.03) -> dict:
             "recommended": rec, "failed": [{"name": r["name"], "rc": r["rc"]} for r in runs if not r["ok"]]}
 
 
+def write_env_file(out: str, rec, nproc: int, scores: dict, backend=None) -> str | None:
+    """Write ``rccl_env.sh`` for the recommended variant, or remove a stale one.  A gloo rehearsal measures noise (gloo
+    ignores every RCCL knob) and a sweep without a winner ("base" or none) must not leave an older recommendation for
+    scripts/env_mi355x.sh to pick up.  Each export only fills a knob the user left unset, and the file records the
+    rank count it was measured at (env_mi355x.sh skips it for another)."""
+    env_path = os.path.join(out, "rccl_env.sh")
+    if backend == "gloo" or rec in (None, "base") or not VARIANTS.get(rec):
+        if os.path.exists(env_path):
+            os.remove(env_path)
+        why = "gloo rehearsal" if backend == "gloo" else "no variant beat RCCL's defaults"
+        print(f"[sweep] no export file written ({why})")
+        return None
+    with open(env_path, "w") as fh:
+        fh.write(f"# benchmarks/rccl_sweep.py: best variant for 32-512 MiB reduce-scatter / all-gather on "
+                 f"{nproc} ranks (x{scores.get(rec, float('nan')):.3f} vs RCCL defaults)\n")
+        fh.write(f"DPH_RCCL_SWEEP_NPROC={nproc}\n")
+        for k, v in VARIANTS[rec].items():
+            fh.write(f": ${{{k}:={v}}}; export {k}\n")
+    print(f"[sweep] recommended for bucket traffic: {rec} {VARIANTS[rec]} -> {env_path}")
+    return env_path
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--nproc", type=int, default=8)
@@ -139,14 +161,8 @@ def main(argv=None):
     for row in summ["best_per_size"]:
         print(f"{row['op']:15s} {row['bytes'] / 2 ** 20:10.3f} MiB  best {row['best']:10s} "
               f"{row['busbw_GBps']:8.2f} GB/s  (base {row['base_busbw_GBps']}, x{row['speedup_vs_base']})")
-    rec = summ["recommended"]
-    if rec is not None:
-        with open(os.path.join(args.out, "rccl_env.sh"), "w") as fh:
-            fh.write(f"# benchmarks/rccl_sweep.py: best variant for 32-512 MiB reduce-scatter / all-gather on "
-                     f"{args.nproc} ranks (x{summ['bucket_traffic_score_vs_base'][rec]:.3f} vs RCCL defaults)\n")
-            for k, v in VARIANTS[rec].items():
-                fh.write(f"export {k}={v}\n")
-        print(f"[sweep] recommended for bucket traffic: {rec} {VARIANTS[rec]} -> {args.out}/rccl_env.sh")
+    write_env_file(args.out, summ["recommended"], args.nproc, summ.get("bucket_traffic_score_vs_base", {}),
+                   args.backend)
     return summ
 
 

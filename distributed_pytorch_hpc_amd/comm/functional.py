@@ -187,6 +187,10 @@ def _a2a(x: torch.Tensor, scatter_dim: int, gather_dim: int, group) -> torch.Ten
     ws = _ws(group)
     if ws == 1:
         return x
+    # normalise negative dims first: unflatten / movedim / flatten below index the ORIGINAL rank of x, and the
+    # unflattened tensor has one more dimension (-1 would name the chunk, not the rank, dimension)
+    scatter_dim %= x.dim()
+    gather_dim %= x.dim()
     n = x.shape[scatter_dim]
     assert n % ws == 0, f"all_to_all: dim {scatter_dim} ({n}) not divisible by the group size {ws}"
     inp = x.unflatten(scatter_dim, (ws, n // ws)).movedim(scatter_dim, 0).contiguous()

@@ -602,12 +602,16 @@ void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_
   auto launch = [&](const bf16* a, const bf16* b, void* c, int64_t m, int64_t n, int64_t k, int64_t ldc_, int S,
                     bool f32_out, bool acc, int64_t cstride) {
     const dim3 grid((unsigned)(((m + GBM - 1) / GBM) * ((n + GBN - 1) / GBN)), (unsigned)S);
+    // the LDS epilogue stores 16-B row segments: C's base and row pitch must be 16-B aligned (an offset view of C
+    // falls back to the per-element epilogue)
+    const int64_t esz_c = (!f32_out && out_dtype == kBF16) ? 2 : 4;
+    const bool vec_c = ((uintptr_t)c & 15) == 0 && ((ldc_ * esz_c) & 15) == 0;
 #define DPH_GEMM_LAUNCH(T, ACC)                                                                                \
   do {                                                                                                         \
     if (m16)                                                                                                   \
       hipLaunchKernelGGL((gemm_tn16_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,     \
                          lda, ldb, ldc_, cstride);                                                             \
-    else if (!lds_epi)                                                                                         \
+    else if (!lds_epi || !vec_c)                                                                               \
       hipLaunchKernelGGL((gemm_tn_k<T, ACC, false>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,  \
                          lda, ldb, ldc_, cstride);                                                             \
     else                                                                                                       \

@@ -57,26 +57,49 @@ def collective_selftest(group=None, device=None, timeout_s: float = 120.0, numel
         device = torch.device("cpu")   # gloo's transport is host memory (and its P2P takes CPU tensors only)
     report = {"world": world, "checked": []}
     n = max(world, numel // world * world)
+    idx = torch.arange(n, device=device)
     for dtype in (torch.float32, torch.bfloat16):
         tag = str(dtype).replace("torch.", "")
-        # all-reduce: rank r contributes (r + 1) * (1 + i % 4)  ->  sum = W(W+1)/2 * (1 + i % 4)  (<= 36 * 4)
-        pattern = (torch.arange(n, device=device) % 4 + 1).to(dtype)
-        x = pattern * (rank + 1)
+        exact_sum = dtype == torch.float32
+        if exact_sum:
+            # all-reduce: rank r contributes (r + 1) * (1 + i % 4)  ->  sum = W(W+1)/2 * (1 + i % 4): exact in fp32 for
+            # any realistic world (< 2^24), and it pins every rank's identity and the SUM reduction
+            pattern = (idx % 4 + 1).to(dtype)
+            x = pattern * (rank + 1)
+            want = pattern * (world * (world + 1) // 2)
+        else:
+            # bf16: RCCL keeps partial sums in bf16 between hops, so only sums whose every partial sum has <= 8
+            # significant bits are exact at any world size.  Element i gets a = 1 + i % 4 from rank i % W and 8 from
+            # rank (i + 1) % W (zeros elsewhere): every partial sum is 0, a, 8 or a + 8, and SUM (not max / any single
+            # contribution) is still what makes the total a + 8.
+            a = (idx % 4 + 1).to(dtype)
+            x = torch.where(idx % world == rank, a, torch.zeros_like(a)) + \
+                torch.where((idx + 1) % world == rank, torch.full_like(a, 8), torch.zeros_like(a))
+            want = a + 8
         _wait(dist.all_reduce(x, group=group, async_op=True), timeout_s, f"all_reduce[{tag}]")
         _dev_sync(device)
-        want = pattern * (world * (world + 1) // 2)
         if not torch.equal(x, want):
             bad = int((x != want).nonzero()[0])
             raise PreflightError(f"all_reduce[{tag}] mismatch on rank {rank}: element {bad} = {float(x[bad])}, "
                                  f"expected {float(want[bad])}")
         report["checked"].append(f"all_reduce[{tag}]")
-        # reduce-scatter: input chunk c of rank r = (r + 1) * (c + 1)  ->  output of rank r = W(W+1)/2 * (r + 1)
         k = n // world
-        inp = (torch.arange(world, device=device).repeat_interleave(k) + 1).to(dtype) * (rank + 1)
+        chunk = torch.arange(world, device=device).repeat_interleave(k)
+        if exact_sum:
+            # reduce-scatter: input chunk c of rank r = (r + 1) * (c + 1)  ->  output of rank r = W(W+1)/2 * (r + 1)
+            inp = (chunk + 1).to(dtype) * (rank + 1)
+            want = torch.full((k,), float(world * (world + 1) // 2 * (rank + 1)), dtype=dtype, device=device)
+        else:
+            # bf16: chunk c gets 1 + (j + c) % 7 (element j) from rank c and 8 from rank (c + 1) % W: exact partial
+            # sums, and the chunk -> rank order shows in the phase of the pattern
+            j = torch.arange(n, device=device) % k
+            inp = torch.where(chunk == rank, ((j + chunk) % 7 + 1).to(dtype), torch.zeros(n, dtype=dtype, device=device))
+            inp = inp + torch.where((chunk + 1) % world == rank, torch.full((n,), 8.0, dtype=dtype, device=device),
+                                    torch.zeros(n, dtype=dtype, device=device))
+            want = ((torch.arange(k, device=device) + rank) % 7 + 9).to(dtype)
         out = torch.empty(k, dtype=dtype, device=device)
         _wait(dist.reduce_scatter_tensor(out, inp, group=group, async_op=True), timeout_s, f"reduce_scatter[{tag}]")
         _dev_sync(device)
-        want = torch.full((k,), float(world * (world + 1) // 2 * (rank + 1)), dtype=dtype, device=device)
         if not torch.equal(out, want):
             raise PreflightError(f"reduce_scatter[{tag}] mismatch on rank {rank}: got {float(out[0])} ... "
                                  f"expected {float(want[0])} (wrong rank order or reduction?)")

@@ -16,10 +16,18 @@ export NCCL_DEBUG=${NCCL_DEBUG:-VERSION}
 
 # ---- knobs to sweep on the box (leave unset for RCCL's own topology-aware defaults) ----
 # benchmarks/rccl_sweep.py measures them and writes the winning exports for bucket-sized traffic; picked up here
-# when present (DPH_RCCL_ENV overrides the path)
+# when present (DPH_RCCL_ENV overrides the path) and measured at this job's rank count (DPH_NPROC, default 8);
+# the file only fills knobs the user left unset
 _dph_rccl_env=${DPH_RCCL_ENV:-$(dirname "${BASH_SOURCE[0]}")/../results/rccl_sweep/rccl_env.sh}
-[ -f "$_dph_rccl_env" ] && . "$_dph_rccl_env"
-unset _dph_rccl_env
+if [ -f "$_dph_rccl_env" ]; then
+  _dph_sweep_n=$(sed -n 's/^DPH_RCCL_SWEEP_NPROC=//p' "$_dph_rccl_env")
+  if [ "${_dph_sweep_n:-0}" = "${DPH_NPROC:-8}" ]; then
+    . "$_dph_rccl_env"
+  else
+    echo "env_mi355x.sh: ignoring $_dph_rccl_env (swept at ${_dph_sweep_n:-?} ranks, job has ${DPH_NPROC:-8})" >&2
+  fi
+fi
+unset _dph_rccl_env _dph_sweep_n
 # export NCCL_MIN_NCHANNELS=32          # more channels -> more xGMI links busy per collective
 # export NCCL_MAX_NCHANNELS=64
 # export NCCL_ALGO=Ring                 # Ring | Tree (direct/one-shot variants are chosen by RCCL per size)

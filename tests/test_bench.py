@@ -222,3 +222,18 @@ def test_alpha_beta_probe_stop_rule_is_rank_consistent():
 
     outs = run_distributed(_probe_skew_worker, 2)
     assert outs[0] == outs[1], outs
+
+
+def _selftest_worker(rank, world):
+    from distributed_pytorch_hpc_amd.runtime import preflight
+
+    return preflight.collective_selftest(None, None, numel=1 << 12)["checked"]
+
+
+def test_preflight_selftest_exact_at_world_16():
+    """The bf16 self-test values stay exact past 8 ranks (two-node jobs): every partial sum has <= 8 significant
+    bits whatever the reduction order (3 * (1 + ... + 13) = 273 needs 9)."""
+    from dist_utils import run_distributed
+
+    outs = run_distributed(_selftest_worker, 16, timeout=400)
+    assert all("all_reduce[bfloat16]" in o and "reduce_scatter[bfloat16]" in o for o in outs), outs

@@ -143,3 +143,29 @@ def test_llama_zigzag_ring_matches_single():
     for lt, gw in outs:
         assert abs(lt - loss.item()) < 1e-5
         assert torch.allclose(gw, m.layers[0].attention.wqkv.weight.grad, atol=1e-5)
+
+
+def _a2a_negative_dims_worker(rank, world):
+    import torch
+
+    from distributed_pytorch_hpc_amd.comm import functional as F
+
+    torch.manual_seed(0)
+    full = torch.randn(3, 4 * world, 6 * world, requires_grad=True)   # identical on every rank
+    x = full.detach().chunk(world, 1)[rank].clone().requires_grad_()   # [3, 4, 6W]: sharded on dim 1
+    out = {}
+    for sd, gd in ((2, 1), (-1, -2), (-1, 1), (2, -2)):
+        y = F.all_to_all(x, sd, gd, None)                              # -> [3, 4W, 6]: sharded on dim 2
+        want = full.detach().chunk(world, 2)[rank]
+        out[(sd, gd)] = bool(torch.equal(y, want))
+        (g,) = torch.autograd.grad((y * y).sum(), x)
+        out[(sd, gd, "grad")] = bool(torch.allclose(g, 2 * x.detach()))
+    return out
+
+
+def test_all_to_all_negative_dims():
+    """all_to_all accepts negative scatter / gather dims (forward and backward) exactly like positive ones."""
+    from dist_utils import run_distributed
+
+    for res in run_distributed(_a2a_negative_dims_worker, 2):
+        assert all(res.values()), res

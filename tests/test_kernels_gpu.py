@@ -366,6 +366,20 @@ def test_gemm_tn_wgrad_ragged_edge_tiles(dph_native, K, M, N, mfma):
     assert (big[M:] == 7.0).all() and (big[:, N:] == 7.0).all()
 
 
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+def test_gemm_tn_misaligned_output_view(dph_native, out_dtype):
+    """C as an offset column view (base not 16-B aligned, odd row pitch): the 16-B LDS epilogue would store
+    misaligned, so the host falls back to the per-element epilogue; neighbours of the view stay untouched."""
+    torch.manual_seed(6)
+    a = torch.randn(128, 256, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(128, 264, device=DEV, dtype=torch.bfloat16)
+    big = torch.full((256, 264 + 11), 3.0, device=DEV, dtype=out_dtype)
+    c = big[:, 1:265]
+    torch.ops.dph.gemm_tn_(c, a, b, False)
+    assert rel_err(c, a.float().t() @ b.float()) < (1e-5 if out_dtype == torch.float32 else 8e-3)
+    assert (big[:, 0] == 3.0).all() and (big[:, 265:] == 3.0).all()
+
+
 def test_gemm_tn_strided_operands(dph_native):
     """Operands that are column slices of wider activations (packed projections)."""
     torch.manual_seed(1)

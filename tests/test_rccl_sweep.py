@@ -42,3 +42,38 @@ def test_sweep_driver_gloo(tmp_path):
     with open(os.path.join(out, "summary.json")) as fh:
         assert json.load(fh)["nproc"] == 2
     assert os.path.exists(os.path.join(out, "base.json")) and os.path.exists(os.path.join(out, "ch16.json"))
+
+
+def test_env_file_only_for_real_winners(tmp_path):
+    import subprocess
+
+    out = str(tmp_path)
+    p = rccl_sweep.write_env_file(out, "ch32", 8, {"ch32": 1.2})
+    text = open(p).read()
+    assert "DPH_RCCL_SWEEP_NPROC=8" in text
+    k, v = next(iter(rccl_sweep.VARIANTS["ch32"].items()))
+    assert f": ${{{k}:={v}}}; export {k}" in text
+    # a user's explicit value survives sourcing; an unset knob takes the sweep's value
+    r = subprocess.run(["bash", "-c", f"export {k}=user; . {p}; echo ${k}"], capture_output=True, text=True)
+    assert r.stdout.strip() == "user"
+    r = subprocess.run(["bash", "-c", f"unset {k}; . {p}; echo ${k}"], capture_output=True, text=True)
+    assert r.stdout.strip() == str(v)
+    # gloo rehearsals and no-winner sweeps remove a stale file
+    assert rccl_sweep.write_env_file(out, "ch32", 8, {"ch32": 1.2}, backend="gloo") is None
+    assert not os.path.exists(p)
+    rccl_sweep.write_env_file(out, "ch32", 8, {"ch32": 1.2})
+    assert rccl_sweep.write_env_file(out, "base", 8, {}) is None and not os.path.exists(p)
+
+
+def test_env_script_checks_rank_count(tmp_path):
+    import subprocess
+
+    p = rccl_sweep.write_env_file(str(tmp_path), "ch32", 2, {"ch32": 1.2})
+    k, v = next(iter(rccl_sweep.VARIANTS["ch32"].items()))
+    script = os.path.join(ROOT, "scripts", "env_mi355x.sh")
+    r = subprocess.run(["bash", "-c", f"unset {k}; DPH_RCCL_ENV={p} DPH_NPROC=8 . {script}; echo ${k}"],
+                       capture_output=True, text=True)
+    assert r.stdout.strip() == "" and "ignoring" in r.stderr
+    r = subprocess.run(["bash", "-c", f"unset {k}; DPH_RCCL_ENV={p} DPH_NPROC=2 . {script}; echo ${k}"],
+                       capture_output=True, text=True)
+    assert r.stdout.strip() == str(v)
