@@ -59,6 +59,19 @@ def local_report() -> dict:
     elif shutil.which("rocm-smi"):
         r["xgmi_topology"] = _run(["rocm-smi", "--showtopotype"])[:4000]
     r["env"] = {k: v for k, v in os.environ.items() if k.startswith(("NCCL_", "RCCL_", "HSA_", "HIP_", "ROCR_"))}
+    # rank -> GPU -> NUMA -> CPU map the launcher applies (runtime/device.py), plus this process's actual affinity
+    from distributed_pytorch_hpc_amd.runtime import device
+
+    nproc = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "0")) or 0) or \
+        max(1, len(device.gpus()))
+    r["gpu_numa"] = [{"gpu": g.index, "pci": g.bdf, "numa": g.numa_node, "local_cpus": len(g.local_cpus)}
+                     for g in device.gpus()]
+    r["cpu_binding_plan"] = device.describe(device.plan(nproc)).splitlines()
+    try:
+        r["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        r["affinity"] = None
+    r["cpu_bind_env"] = os.environ.get("DPH_CPU_BIND")
     return r
 
 
@@ -77,6 +90,7 @@ def main():
         rank, world, local = rt.init_distributed(verbose=False)
         infos = [None] * world
         dist.all_gather_object(infos, {"rank": rank, "host": rep["host"], "local_rank": local,
+                                       "numa": os.environ.get("DPH_NUMA_NODE"), "cpus": rep["affinity"],
                                        "device": torch.cuda.current_device() if torch.cuda.is_available() else "cpu"})
         dev = rt.device_for(local)
         t = torch.tensor([float(rank)], device=dev)

@@ -12,6 +12,9 @@ rank that exits non-zero (or a --timeout) tears the whole gang down (SIGTERM to 
 after a grace period) -- no rank is left blocked in a collective -- and, while restarts remain, relaunches on a
 fresh port; training scripts resume from their latest checkpoint (utils.checkpointing.ShardedCheckpointer).
 ``--log-dir`` writes rank{r}.out / rank{r}.err per rank (utils/redirect.py semantics at the process level).
+``--cpu-bind numa`` (default) pins each rank to its share of the cores local to its GPU's NUMA node
+(runtime/device.py; set in the child before it execs Python, so before any GPU call) and sizes OMP_NUM_THREADS
+to that share; ``--cpu-bind none`` reproduces the reference's unbound ranks (run_fsdp.sh:64).
 """
 from __future__ import annotations
 
@@ -22,11 +25,29 @@ import subprocess
 import sys
 import time
 
+from . import device
 from .env import free_port
+
+
+def _bind(cpus):
+    """preexec_fn: runs in the forked child before exec -- pins the rank's CPU set (no GPU state exists yet)."""
+    def fn():
+        if cpus:
+            os.sched_setaffinity(0, cpus)
+    return fn
+
+
+def bindings(args):
+    if getattr(args, "cpu_bind", "numa") != "numa":
+        return None
+    return device.plan(args.nproc, omp_threads=args.omp_threads)
 
 
 def _spawn(args, attempt: int, port: int):
     procs = []
+    binds = bindings(args)
+    if binds and attempt == 0:
+        print("[dph.launch] CPU binding:\n" + device.describe(binds), file=sys.stderr, flush=True)
     for r in range(args.nproc):
         env = dict(os.environ)
         env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.nproc), LOCAL_WORLD_SIZE=str(args.nproc),
@@ -34,8 +55,14 @@ def _spawn(args, attempt: int, port: int):
                    DPH_RESTART_COUNT=str(attempt))
         if args.backend:
             env["DPH_BACKEND"] = args.backend
+        b = binds[r] if binds else None
+        if b is not None:
+            env["DPH_CPU_BIND"] = ",".join(map(str, b.cpus)) if b.cpus else "none"
+            env["DPH_NUMA_NODE"] = str(b.numa_node)
         if args.omp_threads:
             env["OMP_NUM_THREADS"] = str(args.omp_threads)
+        elif b is not None and b.cpus and "OMP_NUM_THREADS" not in os.environ:
+            env["OMP_NUM_THREADS"] = str(b.omp_threads)
         elif "OMP_NUM_THREADS" not in env:   # ranks split the cores instead of oversubscribing them
             try:
                 cores = len(os.sched_getaffinity(0))
@@ -48,7 +75,8 @@ def _spawn(args, attempt: int, port: int):
             out = open(os.path.join(args.log_dir, f"rank{r}.out"), "a")
             err = open(os.path.join(args.log_dir, f"rank{r}.err"), "a")
         cmd = [sys.executable, "-u", args.script] + args.script_args
-        p = subprocess.Popen(cmd, env=env, stdout=out, stderr=err, start_new_session=True)
+        p = subprocess.Popen(cmd, env=env, stdout=out, stderr=err, start_new_session=True,
+                             preexec_fn=_bind(b.cpus) if b is not None and b.cpus else None)
         procs.append((p, out, err))
     return procs
 
@@ -118,6 +146,8 @@ def main(argv=None):
     ap.add_argument("--timeout", type=float, default=0.0, help="seconds; 0 = none")
     ap.add_argument("--grace", type=float, default=10.0)
     ap.add_argument("--omp-threads", type=int, default=0)
+    ap.add_argument("--cpu-bind", choices=["numa", "none"], default="numa",
+                    help="numa: pin each rank to its share of its GPU's NUMA-local cores; none: no binding")
     ap.add_argument("script")
     ap.add_argument("script_args", nargs=argparse.REMAINDER)
     args = ap.parse_args(argv)
