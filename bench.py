@@ -60,8 +60,10 @@ def parse(argv=None):
     ap.add_argument("--tp", type=int, default=None, help="tp / hybrid layouts: tensor-parallel degree")
     ap.add_argument("--async-tp", type=int, default=2, help="tp / hybrid: micro-collectives per SP collective")
     ap.add_argument("--pp", type=int, default=None, help="pp layout: pipeline stages (default 4)")
-    ap.add_argument("--microbatches", type=int, default=8, help="pp layout: micro-batches per step")
-    ap.add_argument("--schedule", choices=["1f1b", "gpipe"], default="1f1b")
+    ap.add_argument("--microbatches", type=int, default=16, help="pp layout: micro-batches per step")
+    ap.add_argument("--schedule", choices=["auto", "1f1b", "gpipe", "interleaved"], default="auto",
+                    help="pp layout: auto = interleaved 1F1B with --virtual-stages chunks per rank where it applies")
+    ap.add_argument("--virtual-stages", type=int, default=2, help="pp layout: model chunks per rank (interleaved)")
     ap.add_argument("--parallel", choices=["auto", "fsdp", "ddp"], default="auto",
                     help="dp layout: auto = the sharded (FSDP / ZeRO-2) engine; ddp = replicated optimizer state")
     ap.add_argument("--bucket-mb", default="calibrate",

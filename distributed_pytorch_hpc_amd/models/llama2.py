@@ -79,6 +79,7 @@ PRESETS = {
     "tiny": ModelArgs(dim=128, n_layers=2, n_heads=4, vocab_size=512, max_seq_len=512),
     # heads, FFN (352), vocab and layers divisible by 8 / 4: rehearses the BASELINE meshes (tp8, dp2 x tp4, pp4 x dp2)
     "tiny8": ModelArgs(dim=128, n_layers=4, n_heads=8, vocab_size=512, multiple_of=32, max_seq_len=512),
+    "tiny8-deep": ModelArgs(dim=128, n_layers=8, n_heads=8, vocab_size=512, multiple_of=32, max_seq_len=512),
     "llama2-1b": ModelArgs(dim=2048, n_layers=16, n_heads=16, vocab_size=32000, max_seq_len=4096),
     "llama2-7b": ModelArgs(dim=4096, n_layers=32, n_heads=32, vocab_size=32000, max_seq_len=4096),
     "llama2-13b": ModelArgs(dim=5120, n_layers=40, n_heads=40, vocab_size=32000, max_seq_len=4096),

@@ -191,10 +191,37 @@ def build_hybrid(args, rank, world, dev, log) -> Workload:
     return _tp_hybrid(args, rank, world, dev, log, args.tp or (4 if world % 4 == 0 else world), "hybrid")
 
 
+class _EngineSet:
+    """The per-chunk data-parallel engines of an interleaved pipeline rank, driven as one."""
+
+    def __init__(self, engines):
+        self.engines = list(engines)
+
+    def synchronize(self):
+        for e in self.engines:
+            e.synchronize()
+
+    def step(self):
+        for e in self.engines:
+            e.step()
+
+    def zero_grad(self):
+        for e in self.engines:
+            e.zero_grad()
+
+    @property
+    def bucket_cap_mb(self):
+        return self.engines[0].bucket_cap_mb
+
+    @property
+    def flat_param(self):
+        return torch.cat([e.flat_param.reshape(-1) for e in self.engines])
+
+
 def build_pp(args, rank, world, dev, log) -> Workload:
     from ..comm.mesh import Mesh
     from ..parallel.data_parallel import DataParallelEngine, MixedPrecision, OptimConfig
-    from ..parallel.pipeline import PipelineSchedule, make_lm_loss, split_llama
+    from ..parallel.pipeline import PipelineSchedule, make_lm_loss, split_llama, split_llama_virtual
 
     pp = args.pp or (4 if world % 4 == 0 else world)
     assert world % pp == 0, f"world {world} is not divisible by pp {pp}"
@@ -209,21 +236,38 @@ def build_pp(args, rank, world, dev, log) -> Workload:
         stage = dp_rank = 0
         pp_group = dp_group = None
     margs, model = _llama(args, dev, dtype)
-    assert margs.n_layers >= pp
-    stage_mod = split_llama(model, pp, stage)
-    del model
-    reduce_dtype = torch.bfloat16 if not cpu else torch.float32
-    grad_bytes = sum(p.numel() for p in stage_mod.parameters()) * torch.empty((), dtype=reduce_dtype).element_size()
-    bucket_mb, binfo = _bucket(args, dp, grad_bytes, dp > 1, dp_group, dev, log)
-    engine = DataParallelEngine(stage_mod, dp_group, shard=dp > 1,
-                                mixed_precision=MixedPrecision(param_dtype=dtype, reduce_dtype=reduce_dtype),
-                                bucket_cap_mb=bucket_mb)
-    engine.configure_optimizer(OptimConfig(name="adamw", lr=args.lr, betas=(0.9, 0.95), weight_decay=0.1))
     M = args.microbatches
     B, S = args.micro_batch, args.seq_len
     assert B % M == 0, f"--micro-batch {B} (sequences per dp replica) must be divisible by --microbatches {M}"
-    sched = PipelineSchedule(stage_mod, stage, pp, M, loss_fn=make_lm_loss(None), group=pp_group,
-                             schedule=args.schedule, device=dev, dp_engine=engine)
+    # interleaved 1F1B (v model chunks per rank) where it applies: >= 3 stages, M % pp == 0, a layer per chunk
+    schedule, v = args.schedule, max(1, args.virtual_stages)
+    if schedule == "auto":
+        ok = pp >= 3 and M % pp == 0 and margs.n_layers >= pp * v and v > 1
+        schedule, v = ("interleaved", v) if ok else ("1f1b", 1)
+    if schedule != "interleaved":
+        v = 1
+    assert margs.n_layers >= pp * v
+    # stages split by modelled cost (embedding on the first, norm + LM head + loss on the last)
+    if schedule == "interleaved":
+        chunks = split_llama_virtual(model, pp, v, stage, seq_len=S)
+    else:
+        chunks = [split_llama(model, pp, stage, seq_len=S)]
+    del model
+    reduce_dtype = torch.bfloat16 if not cpu else torch.float32
+    grad_bytes = sum(p.numel() for c in chunks for p in c.parameters()) * \
+        torch.empty((), dtype=reduce_dtype).element_size()
+    bucket_mb, binfo = _bucket(args, dp, grad_bytes, dp > 1, dp_group, dev, log)
+    engines = []
+    for c in chunks:
+        e = DataParallelEngine(c, dp_group, shard=dp > 1,
+                               mixed_precision=MixedPrecision(param_dtype=dtype, reduce_dtype=reduce_dtype),
+                               bucket_cap_mb=bucket_mb)
+        e.configure_optimizer(OptimConfig(name="adamw", lr=args.lr, betas=(0.9, 0.95), weight_decay=0.1))
+        engines.append(e)
+    engine = engines[0] if len(engines) == 1 else _EngineSet(engines)
+    sched = PipelineSchedule(chunks[0] if v == 1 else chunks, stage, pp, M, loss_fn=make_lm_loss(None),
+                             group=pp_group, schedule=schedule, device=dev,
+                             dp_engine=engines[0] if v == 1 else engines)
     batches = _tokens(margs, B, S, dev, 1000 + dp_rank)
     first, last = stage == 0, stage == pp - 1
 
@@ -234,9 +278,10 @@ def build_pp(args, rank, world, dev, log) -> Workload:
         engine.zero_grad()
         return torch.stack(losses).mean() if losses else None
 
+    layers = [sum(len(c.layers) for c in chunks)]
     cfg = {"model": _model_name(args), "global_batch": dp * B, "seq_len": S, "parallelism": f"pp{pp}xddp{dp}",
-           "pp": pp, "dp": dp, "microbatches": M, "schedule": args.schedule,
-           "bubble_fraction": round(sched.bubble, 4), "tokens_per_step": dp * B * S,
+           "pp": pp, "dp": dp, "microbatches": M, "schedule": schedule, "virtual_stages": v,
+           "layers_on_rank0": layers[0], "bubble_fraction": round(sched.bubble, 4), "tokens_per_step": dp * B * S,
            "bucket_mb": round(engine.bucket_cap_mb, 1), **binfo}
     return Workload(step, engine, "tokens/sec, Llama-2 7B PP 4 stages x DDP 2 (1F1B send/recv pipeline)",
                     "tokens/s", dp * B * S, "weak", cfg, replica_group=dp_group,

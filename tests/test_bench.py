@@ -76,7 +76,7 @@ ARGS8 = ["--device", "cpu", "--model", "tiny8", "--seq-len", "64", "--steps", "2
 @pytest.mark.parametrize("layout,extra,par,scaling,batch", [
     ("tp", ["--micro-batch", "4"], "tp8", "strong", 4),
     ("hybrid", ["--micro-batch", "4"], "fsdp2xtp4", "weak", 8),
-    ("pp", ["--micro-batch", "8", "--microbatches", "4"], "pp4xddp2", "weak", 16),
+    ("pp", ["--micro-batch", "8", "--microbatches", "4", "--model", "tiny8-deep"], "pp4xddp2", "weak", 16),
 ])
 def test_bench_baseline_layouts_world8(layout, extra, par, scaling, batch, tmp_path):
     """BASELINE configs 3-5 (TP=8, FSDP(2) x TP(4), PP4 x DDP2) under bench.py's JSON contract at world 8 (gloo)."""
@@ -95,6 +95,9 @@ def test_bench_baseline_layouts_world8(layout, extra, par, scaling, batch, tmp_p
     assert r["preflight_ok"] is True
     if layout != "tp":   # replicas exist only over a dp dimension
         assert r["param_checksum_ok"] is True
+    if layout == "pp":   # default schedule: interleaved 1F1B, 2 chunks per rank
+        assert r["config"]["schedule"] == "interleaved" and r["config"]["virtual_stages"] == 2
+        assert abs(r["config"]["bubble_fraction"] - round(3 / (2 * 4 + 3), 4)) < 1e-9
     assert abs(r["value"] - batch * 64 * 2 / (r["ms_per_step"] * 2 / 1000)) / r["value"] < 1e-3
 
 

@@ -156,6 +156,63 @@ def test_pp4_x_ddp2_1f1b_matches_single_process():
     assert len(last) == 4 and abs(sum(last) / 4 - ref_loss) < 1e-5
 
 
+def _model_l8():
+    from distributed_pytorch_hpc_amd.models.llama2 import ModelArgs, build_llama
+
+    return build_llama(ModelArgs(**dict(PRESET8, n_layers=8)), device="cpu", dtype=torch.float32, seed=7)
+
+
+def _ipp_worker(rank, world, pp, v, m_micro):
+    from distributed_pytorch_hpc_amd.comm.mesh import Mesh
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine
+    from distributed_pytorch_hpc_amd.parallel.pipeline import PipelineSchedule, lm_loss, split_llama_virtual
+
+    dp = world // pp
+    mesh = Mesh((pp, dp), ("pp", "dp"))
+    stage, dpr = mesh.local_rank("pp"), mesh.local_rank("dp")
+    model = _model_l8()
+    names = {id(p): n for n, p in model.named_parameters()}
+    chunks = split_llama_virtual(model, pp, v, stage)
+    engines = [DataParallelEngine(c, mesh.group("dp"), shard=False, bucket_cap_mb=0.05) for c in chunks]
+    sched = PipelineSchedule(chunks, stage, pp, m_micro, loss_fn=lm_loss, group=mesh.group("pp"),
+                             schedule="interleaved", dp_engine=engines)
+    t = _batches(global_b=16)[0]
+    x, y = t[:, :-1].chunk(dp)[dpr], t[:, 1:].chunk(dp)[dpr]
+    losses = sched.step(inputs=x if stage == 0 else None, target=y if stage == pp - 1 else None)
+    grads = {}
+    for e, c in zip(engines, chunks):
+        e.synchronize()
+        grads.update({names[id(p)]: p.main_grad.detach().clone() / dp for p in c.parameters()})
+    return [float(l) for l in losses], stage, grads, sched.bubble
+
+
+def test_pp4_x_ddp2_interleaved_matches_single_process():
+    """BASELINE config 5 with the interleaved schedule: 4 ranks x 2 model chunks of one layer each, one
+    data-parallel engine per chunk (each chunk's gradients reduce at its own last backward), 8 micro-batches per dp
+    replica -- the same micro-batch partition (16 of 1 sequence) as the single-process reference."""
+    from distributed_pytorch_hpc_amd.parallel.pipeline import lm_loss
+
+    m = _model_l8()
+    t = _batches(global_b=16)[0]
+    x, y = t[:, :-1], t[:, 1:]
+    ref_loss = 0.0
+    for xm, ym in zip(x.chunk(16), y.chunk(16)):
+        loss = lm_loss(m(xm), ym) / 16
+        loss.backward()
+        ref_loss += loss.item()
+    ref_g = {n: p.grad.clone() for n, p in m.named_parameters()}
+    outs = run_distributed(_ipp_worker, 8, 4, 2, 8, timeout=400)
+    seen = set()
+    for losses, stage, grads, bub in outs:
+        assert abs(bub - 3 / (2 * 8 + 3)) < 1e-12
+        for n, g in grads.items():
+            assert torch.allclose(g, ref_g[n], atol=1e-5, rtol=1e-4), (stage, n)
+            seen.add(n)
+    assert seen == set(ref_g)
+    last = [v for lo, st, _, _ in outs if st == 3 for v in lo]
+    assert len(last) == 16 and abs(sum(last) / 16 - ref_loss) < 1e-5
+
+
 # ---------------------------------------------------------------------------------------------- CP = 8
 def _qkv(b=1, s=64, h=8, d=16, seed=0):
     g = torch.Generator().manual_seed(seed)
