@@ -205,6 +205,7 @@ class DataParallelEngine:
                     p._dph_accum = False
                     p._dph_grad_ready = partial(self._on_grad_ready, p)
                     self._bucket_of[id(p)] = b
+                    p._dph_flat_off = o
                     o += align_up(n)
         self._hooks = [p.register_post_accumulate_grad_hook(self._post_accumulate) for p in params]
         if broadcast_from_rank0 and self.world > 1:
@@ -227,6 +228,7 @@ class DataParallelEngine:
         self._next_launch = 0
         self._callback_queued = False
         self._gscale = torch.full((1,), 1.0 / self.world, dtype=torch.float32, device=self.device)
+        self._init_tp_partial()
 
         # Opt-in (overlap_step=True / DPH_OVERLAP_STEP=1): each bucket's update runs on a side stream in forward
         # order and the next forward waits per module for its bucket only, so the HBM-bound AdamW / SGD sweep can
@@ -246,6 +248,45 @@ class DataParallelEngine:
             if ids:
                 self._fwd_hooks.append(m.register_forward_pre_hook(partial(self._wait_ag, sorted(ids))))
         self._fwd_hooks.append(module.register_forward_hook(lambda *_: self._join_opt_stream()))
+
+    # ------------------------------------------------------------------------------------------ TP-partial grads
+    def _init_tp_partial(self):
+        """Sequence-parallel parameters (norm weights that run on a sequence shard, tensor_parallel.py
+        mark_sequence_parallel) hold gradients that are partial over the TP group.  Instead of one latency-bound
+        all-reduce per parameter from a backward hook (65 per Llama-2-7B backward), the engine takes them over: the
+        data-parallel reduction runs as usual (a sum, so the order of the two reductions does not matter) and
+        ``step`` completes them with ONE all-reduce over the TP group of every such element this rank holds (the
+        flat / sharded layouts are identical across TP ranks: equal shard shapes).  SURVEY.md C9."""
+        groups = {}
+        for p in self.params:
+            g = getattr(p, "_dph_sp_group", None)
+            if getattr(p, "_dph_sequence_parallel", False) and g is not None and dist.is_initialized() and \
+                    dist.get_world_size(g) > 1:
+                groups.setdefault(id(g), (g, []))[1].append(p)
+        self._tp_partial = []
+        for g, ps in groups.values():
+            idx = []
+            for p in ps:
+                p._dph_tp_batched = True
+                b, o, n = self._bucket_of[id(p)], p._dph_flat_off, p.numel()
+                if not self.shard:
+                    idx.append(torch.arange(o, o + n, dtype=torch.int64))
+                    continue
+                lo = b.offset + self.rank * b.shard_numel           # this rank's shard of the bucket
+                s0, s1 = max(o, lo), min(o + n, lo + b.shard_numel)
+                if s0 < s1:
+                    idx.append(torch.arange(s0 - lo, s1 - lo, dtype=torch.int64) + b.shard_offset)
+            cat = torch.cat(idx) if idx else torch.zeros(0, dtype=torch.int64)
+            self._tp_partial.append((g, cat.to(self.device)))
+
+    def _reduce_tp_partial(self):
+        red = self.grad_shard if self.shard else self.flat_grad
+        for g, idx in self._tp_partial:
+            # every rank of the TP group joins the collective, even one whose shard holds none of the elements
+            buf = red.index_select(0, idx) if idx.numel() else torch.zeros(1, dtype=red.dtype, device=red.device)
+            dist.all_reduce(buf, group=g)
+            if idx.numel():
+                red.index_copy_(0, idx, buf)
 
     # ------------------------------------------------------------------------------------------ views
     def grad_view(self, b: _Bucket) -> torch.Tensor:
@@ -402,6 +443,10 @@ class DataParallelEngine:
         if not self._sync_enabled:
             raise RuntimeError("optimizer step inside no_sync()")
         self.step_count += 1
+        if self._tp_partial:
+            for b in self.buckets:
+                self._wait_reduce(b)
+            self._reduce_tp_partial()
         if cfg.max_grad_norm is not None:
             norm = self._global_sumsq().sqrt()
             self._gscale.copy_(torch.clamp(cfg.max_grad_norm / (norm + 1e-6), max=1.0) / self.world)

@@ -143,12 +143,16 @@ class VocabParallelEmbedding(nn.Module):
 
 
 def mark_sequence_parallel(module: nn.Module, group):
-    """Replicated params of a module that runs on a sequence shard: all-reduce their grads over TP."""
+    """Replicated params of a module that runs on a sequence shard: their grads are partial over TP.  A
+    data-parallel engine that owns them (parallel/data_parallel.py) completes ALL of them with one all-reduce per
+    step after its own reduction (``_dph_tp_batched``); without an engine a backward hook all-reduces each one."""
     if _ws(group) == 1:
         return module
     for p in module.parameters(recurse=False):
-        p.register_hook(lambda g, grp=group: cf.all_reduce_(g.contiguous().clone(), grp))
         p._dph_sequence_parallel = True
+        p._dph_sp_group = group
+        p.register_hook(lambda g, grp=group, prm=p: g if getattr(prm, "_dph_tp_batched", False)
+                        else cf.all_reduce_(g.contiguous().clone(), grp))
     return module
 
 

@@ -358,3 +358,49 @@ def test_run_config_llama2_7b_world8(cfg, extra, tmp_path):
                        env=dict(os.environ, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1"))
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
     assert any(ln.startswith("{") for ln in p.stdout.splitlines()), p.stdout[-2000:]
+
+
+def _sp_count_worker(rank, world):
+    from distributed_pytorch_hpc_amd.comm import functional as cf
+    from distributed_pytorch_hpc_amd.comm.mesh import DeviceMesh2D
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig
+    from distributed_pytorch_hpc_amd.parallel.tensor_parallel import parallelize_llama
+
+    mesh = DeviceMesh2D(1, world)
+    m = _model()
+    parallelize_llama(m, mesh.tp_group, sequence_parallel=True, loss_parallel=True)
+    eng = DataParallelEngine(m, process_group=mesh.dp_group, shard=False, bucket_cap_mb=0.05)
+    eng.configure_optimizer(OptimConfig(lr=1e-2))
+    calls = {"hook": 0, "batched": 0}
+    real_ar, real_batched = cf.all_reduce_, eng._reduce_tp_partial
+
+    def counting_hook_ar(t, g, **kw):
+        if t.shape == (PRESET8["dim"],) and not kw:   # a norm weight's gradient
+            calls["hook"] += 1
+        return real_ar(t, g, **kw)
+
+    def counting_batched():
+        calls["batched"] += 1
+        return real_batched()
+
+    cf.all_reduce_ = counting_hook_ar
+    eng._reduce_tp_partial = counting_batched
+    try:
+        t = _batches()[0][:, :13]   # 8 x 12 tokens: divisible by tp, and 96 != dim
+        loss = m(t[:, :-1], t[:, 1:])
+        loss.backward()
+        eng.step()
+    finally:
+        cf.all_reduce_ = real_ar
+    assert len(eng._tp_partial) == 1
+    n_sp = sum(1 for p in m.parameters() if getattr(p, "_dph_sequence_parallel", False))
+    return calls, n_sp
+
+
+def test_sp_norm_grads_one_batched_all_reduce():
+    """With the data-parallel engine owning them, the sequence-parallel norm weights' TP-partial gradients cost ONE
+    all-reduce per step (engine.step), not one per parameter from a backward hook."""
+    outs = run_distributed(_sp_count_worker, 4)
+    for calls, n_sp in outs:
+        assert n_sp == 2 * PRESET8["n_layers"] + 1
+        assert calls == {"hook": 0, "batched": 1}, calls
