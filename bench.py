@@ -52,8 +52,9 @@ def parse(argv=None):
     ap.add_argument("--arch", default="resnet50", help="resnet-fsdp layout: ResNet depth")
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--image-size", type=int, default=224)
-    ap.add_argument("--unet-precision", choices=["bf16", "fp32"], default="bf16",
-                    help="unet-ddp layout: bf16 autocast over fp32 weights, or the reference's fp32")
+    ap.add_argument("--unet-precision", choices=["bf16", "bf16-autocast", "fp32"], default="bf16",
+                    help="unet-ddp layout: bf16 parameters + fp32 master weights in the engine (default), bf16 "
+                         "autocast over fp32 weights, or the reference's fp32")
     ap.add_argument("--micro-batch", type=int, default=None,
                     help="sequences (images) per GPU / per dp replica per step; default 8 (dp, tp, hybrid), 16 (pp), "
                          "256 (resnet-fsdp).  8 x 4096 tokens: ~249 GB peak on one 288 GB MI355X")
@@ -80,6 +81,9 @@ def parse(argv=None):
                     help="N = 1 without a process group (the engine is the same; no RCCL communicator)")
     ap.add_argument("--force-dist", action="store_true", help=argparse.SUPPRESS)   # the default now; kept for scripts
     ap.add_argument("--no-preflight", action="store_true", help="skip the collective self-test and replica check")
+    ap.add_argument("--xgmi-probe", type=int, default=1,
+                    help="multi-GPU layouts with all-reducing groups (tp, hybrid, unet-ddp): time the direct-peer "
+                         "xGMI all-reduce against RCCL and route messages below the crossover to it (0: RCCL only)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default=None,
                     help="process-group backend (default: nccl = RCCL on GPU); gloo lets several ranks share one GPU "
                          "to rehearse the N > 1 path (tests/test_bench_gpu.py)")
@@ -162,6 +166,19 @@ def main(argv=None):
             _fail(3, f"rank {rank}: collective self-test failed: {e}")
 
     wl = BUILDERS[args.layout](args, rank, world, dev, log)
+    # ---- direct-peer all-reduce: measured crossover per all-reducing group (small messages, RCCL above) ----
+    xgmi = {}
+    if world > 1 and not cpu and not args.no_preflight and args.xgmi_probe and wl.ar_groups and \
+            dist.get_backend() == "nccl":
+        from distributed_pytorch_hpc_amd.comm import custom_allreduce as car_mod
+
+        for name, grp in wl.ar_groups:
+            res = car_mod.probe_crossover(grp)
+            car_mod.set_policy(grp, res["crossover_bytes"])
+            xgmi[name] = {"crossover_bytes": res["crossover_bytes"], "verified": res["verified"],
+                          "samples_us": [(b, round(1e6 * tr, 1), None if tx is None else round(1e6 * tx, 1))
+                                         for b, tr, tx in res["samples"]]}
+            log(f"[bench] xGMI all-reduce vs RCCL on {name}: crossover {res['crossover_bytes']} B")
     graph_info = {}
     if args.graph:
         if world > 1 or cpu:
@@ -255,6 +272,7 @@ def main(argv=None):
             "process_group": dist.get_backend() if dist.is_initialized() else None,
             "rccl_version": preflight.rccl_version() if not cpu else None,
             **pre, **replica, **wl.extra, **graph_info,
+            **({"xgmi_allreduce": xgmi} if xgmi else {}),
         }
         if wl.flops_per_item:
             rec["mfu_vs_2.5PF_bf16_dense"] = round(rate / world * wl.flops_per_item / 2.5e15, 4)

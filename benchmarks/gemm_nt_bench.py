@@ -19,6 +19,9 @@ from distributed_pytorch_hpc_amd.ops import _lib  # noqa: E402
 FWD = {"wqkv": (12288, 4096), "wo": (4096, 4096), "w13": (22016, 4096), "w2": (4096, 11008), "output": (32000, 4096)}
 DGRAD = {"wqkv.dgrad": (4096, 12288), "wo.dgrad": (4096, 4096), "w13.dgrad": (4096, 22016),
          "w2.dgrad": (11008, 4096), "output.dgrad": (4096, 32000)}
+# one tensor-parallel rank's shards at tp = 8 (ragged for the 256 / 64 tile grid)
+TP8 = {"wqkv.tp8": (1536, 4096), "w13.tp8": (2752, 4096), "w2.tp8": (4096, 1376), "output.tp8": (4000, 4096),
+       "w13.dgrad.tp8": (4096, 2752), "w2.dgrad.tp8": (1376, 4096), "wo.dgrad.tp8": (512, 4096)}
 
 
 def timeit(fn, iters):
@@ -39,14 +42,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--json", default=None)
     ap.add_argument("--shapes", default=",".join(list(FWD) + list(DGRAD)))
-    ap.add_argument("--variants", default="0,1", help="gemm_nt pipeline variants to A/B (csrc/gemm_nt.hip LOOK)")
+    ap.add_argument("--variants", default="1,3", help="gemm_nt variants to A/B (bit 0 LOOK, bit 1 32x32x16 MFMA)")
     ap.add_argument("--no-fused", action="store_true")
     a = ap.parse_args()
     _lib.require()
     ops = torch.ops.dph
     T = a.tokens
     res = {}
-    shapes = {**FWD, **DGRAD}
+    shapes = {**FWD, **DGRAD, **TP8}
     for name in a.shapes.split(","):
         N, K = shapes[name]
         x = torch.randn(T, K, device="cuda").to(torch.bfloat16)

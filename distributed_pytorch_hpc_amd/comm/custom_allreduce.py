@@ -17,9 +17,17 @@ Use::
     car.all_reduce(t)                     # in place, SUM (op="avg" divides by the group size)
 
 ``get_custom_allreduce(group)`` returns a cached instance, or ``None`` when the group is not eligible (CPU/gloo,
-more than 8 ranks, ranks on several hosts, native extension missing).  ``comm.functional.all_reduce_`` routes
-eligible messages here when ``DPH_CUSTOM_ALLREDUCE=1`` (off by default; ``benchmarks/comm_bench.py --custom``
-measures both paths so the threshold can be set from data on the target node).
+more than 8 ranks, ranks on several hosts, native extension missing).
+
+Which path a message takes is decided from data (reference: the timing loop of tests/torch_comm_bench.py:62-116):
+``probe_crossover(group)`` times RCCL's all-reduce and this one at 4 KiB .. 16 MiB on the job's own group (slowest
+rank's time, so every rank decides alike), and ``choose_crossover`` turns the samples into the largest message
+size up to which the direct-peer path wins at every measured size (0 when RCCL wins already at the smallest).
+``set_policy(group, crossover)`` records it; ``comm.functional.all_reduce_`` -- which the TP row-parallel
+all-reduce, the sequence-parallel norm-gradient reduction and the loss-parallel reductions go through -- and the
+data-parallel engine's buckets then route SUM messages up to the crossover here.  ``DPH_CUSTOM_ALLREDUCE=1`` forces
+the path up to ``DPH_CUSTOM_ALLREDUCE_MAX_BYTES`` (8 MiB), ``=0`` disables it; unset = the measured policy (none
+recorded: RCCL).
 """
 from __future__ import annotations
 
@@ -108,6 +116,14 @@ class XgmiAllReduce:
 _CACHE: dict = {}
 
 
+_POLICY: dict = {}        # group key -> crossover bytes (messages <= it take the direct-peer path)
+_ANY_BACKEND: set = set()  # group keys allowed on a non-RCCL group (tests: gloo ranks sharing one GPU)
+
+
+def _key(group):
+    return id(group) if group is not None else "world"
+
+
 def custom_allreduce_enabled() -> bool:
     return os.environ.get("DPH_CUSTOM_ALLREDUCE", "0") == "1"
 
@@ -116,14 +132,113 @@ def custom_allreduce_max_bytes() -> int:
     return int(os.environ.get("DPH_CUSTOM_ALLREDUCE_MAX_BYTES", str(8 << 20)))
 
 
+def set_policy(group, crossover_bytes: int, allow_any_backend: bool = False) -> None:
+    """Record the measured crossover for ``group`` (0 = always RCCL).  ``allow_any_backend``: also on a non-RCCL
+    group whose tensors live on GPUs (processes sharing one GPU in tests)."""
+    _POLICY[_key(group)] = int(crossover_bytes)
+    if allow_any_backend:
+        _ANY_BACKEND.add(_key(group))
+
+
+def clear_policy(group=None) -> None:
+    _POLICY.pop(_key(group), None)
+    _ANY_BACKEND.discard(_key(group))
+
+
+def policy_max_bytes(group) -> int:
+    """Largest message (bytes) the direct-peer path takes on ``group``: the env override, else the measured
+    crossover, else 0."""
+    env = os.environ.get("DPH_CUSTOM_ALLREDUCE")
+    if env == "1":
+        return custom_allreduce_max_bytes()
+    if env == "0":
+        return 0
+    return _POLICY.get(_key(group), 0)
+
+
+def use_custom(t: torch.Tensor, group) -> Optional["XgmiAllReduce"]:
+    """The XgmiAllReduce to run this SUM all-reduce on, or None for RCCL.  Rank-invariant: the decision depends on
+    the message size, the recorded policy and the group only."""
+    limit = policy_max_bytes(group)
+    if limit <= 0 or not t.is_cuda or t.numel() * t.element_size() > limit:
+        return None
+    car = get_custom_allreduce(group)
+    return car if car is not None and car.supports(t) else None
+
+
+def choose_crossover(samples: list) -> int:
+    """samples: [(bytes, t_rccl_s, t_xgmi_s)] -> the largest size up to which the direct-peer path is faster at EVERY
+    measured size (sizes above the first loss go to RCCL), 0 if RCCL wins at the smallest size."""
+    best = 0
+    for nbytes, t_rccl, t_xgmi in sorted(samples):
+        if t_xgmi is None or not (t_xgmi < t_rccl):
+            break
+        best = int(nbytes)
+    return best
+
+
+def probe_crossover(group=None, sizes=(4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20),
+                    iters: int = 10, warmup: int = 3, dtype=torch.bfloat16) -> dict:
+    """Time RCCL's all-reduce and the direct-peer one on ``group`` at ``sizes`` bytes; every rank gets the same
+    (max over ranks) times and the same crossover.  Collective.  Returns {"samples": [...], "crossover_bytes": n}."""
+    car = get_custom_allreduce(group)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    world = dist.get_world_size(group)
+    samples = []
+    ok = torch.ones(1, dtype=torch.float64, device=dev)
+    for nbytes in sizes:
+        n = max(8, nbytes // torch.empty((), dtype=dtype).element_size())
+        x = torch.ones(n, dtype=dtype, device=dev)
+        times = []
+        for path in ("rccl", "xgmi"):
+            if path == "xgmi" and (car is None or not car.supports(x)):
+                times.append(None)
+                continue
+
+            def run():
+                if path == "rccl":
+                    dist.all_reduce(x, group=group)
+                else:
+                    car.all_reduce(x)
+
+            for _ in range(warmup):
+                run()
+            torch.cuda.synchronize(dev)
+            dist.barrier(group=group)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(iters):
+                x.fill_(1.0)
+                run()
+            e.record()
+            e.synchronize()
+            if path == "xgmi" and not (torch.all(x == world) and car.errors() == 0):
+                ok.zero_()      # wrong sums or barrier timeouts: never route traffic to this path
+            x.fill_(1.0)
+            t = torch.tensor([s.elapsed_time(e) / iters / 1e3], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            times.append(float(t.item()))
+        samples.append((int(nbytes), times[0], times[1]))
+    # whether the xgmi arm exists is itself rank-invariant (every rank constructs or fails alike); correctness is
+    # agreed on (MIN over ranks) so a path that failed anywhere is off everywhere
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+    verified = bool(ok.item() == 1.0)
+    return {"samples": samples, "verified": verified,
+            "crossover_bytes": choose_crossover(samples) if verified else 0}
+
+
 def get_custom_allreduce(group=None) -> Optional[XgmiAllReduce]:
     """Cached XgmiAllReduce for ``group`` or None if the group cannot use it (collective on first call)."""
-    if not dist.is_initialized() or dist.get_backend(group) != "nccl":
+    if not dist.is_initialized():
         return None
-    key = id(group) if group is not None else "world"
+    if dist.get_backend(group) != "nccl" and _key(group) not in _ANY_BACKEND:
+        return None
+    key = _key(group)
     if key not in _CACHE:
         try:
-            _CACHE[key] = XgmiAllReduce(group, max_bytes=max(custom_allreduce_max_bytes(), 1 << 20))
+            # staging sized for the probe's largest message (16 MiB) or a larger forced / recorded limit
+            _CACHE[key] = XgmiAllReduce(group, max_bytes=max(custom_allreduce_max_bytes(), _POLICY.get(key, 0),
+                                                             16 << 20))
         except (ValueError, RuntimeError):
             _CACHE[key] = None
     return _CACHE[key]

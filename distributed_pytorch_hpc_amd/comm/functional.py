@@ -19,9 +19,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from .custom_allreduce import custom_allreduce_enabled as _custom_ar_enabled
-from .custom_allreduce import custom_allreduce_max_bytes as _custom_ar_max_bytes
-from .custom_allreduce import get_custom_allreduce as _get_custom_ar
+from .custom_allreduce import use_custom as _use_custom
 
 
 def _ws(group) -> int:
@@ -68,14 +66,13 @@ def split_dim(x: torch.Tensor, dim: int, group) -> torch.Tensor:
 
 
 def all_reduce_(x: torch.Tensor, group, op=dist.ReduceOp.SUM) -> torch.Tensor:
-    """In-place all-reduce.  With ``DPH_CUSTOM_ALLREDUCE=1``, SUM messages up to
-    ``DPH_CUSTOM_ALLREDUCE_MAX_BYTES`` on a single-node RCCL group take the direct-peer-read xGMI kernel
-    (comm/custom_allreduce.py); everything else goes to RCCL."""
+    """In-place all-reduce.  SUM messages up to the group's measured crossover (comm/custom_allreduce.py
+    probe_crossover / set_policy; ``DPH_CUSTOM_ALLREDUCE=1`` forces it up to ``DPH_CUSTOM_ALLREDUCE_MAX_BYTES``) take
+    the direct-peer-read xGMI kernel; everything else goes to RCCL."""
     if _ws(group) > 1:
-        if op == dist.ReduceOp.SUM and x.is_cuda and _custom_ar_enabled() and \
-                x.numel() * x.element_size() <= _custom_ar_max_bytes():
-            car = _get_custom_ar(group)
-            if car is not None and car.supports(x):
+        if op == dist.ReduceOp.SUM and x.is_cuda:
+            car = _use_custom(x, group)
+            if car is not None:
                 car.all_reduce(x)
                 return x
         dist.all_reduce(x, op=op, group=group)

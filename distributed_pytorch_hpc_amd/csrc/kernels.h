@@ -140,9 +140,12 @@ struct GemmNtParams {
   int S, hd, n_rot, pos_off;
   int tiles_n;          // set by gemm_nt
 };
+// rows % 256, N (SWIGLU: H) % 8, K % 8; shapes off the 256 / 64 grid (gemm_nt_ragged) run the ragged-edge kernel
 bool gemm_nt_supported(int mode, int64_t M, int64_t N, int64_t K);
+bool gemm_nt_ragged(int mode, int64_t N, int64_t K);
 void gemm_nt(int mode, const GemmNtParams& p, hipStream_t stream);
-// pipeline variant of gemm_nt_k (0: 12/4/8/0 fragment reads per phase, 1: lookahead B0 reads, 8/4/8/0)
+// pipeline variant: bit 0 = lookahead B0 reads (8/4/8/0 fragment reads per phase instead of 12/4/8/0), bit 1 = the
+// v_mfma_f32_32x32x16_bf16 kernel (gemm_nt32_k) instead of 16x16x32 (gemm_nt_k).  Ragged shapes always take bit 1.
 constexpr int kGemmNtDefaultVariant = 1;   // 0.92-1.02x hipBLASLt vs 0.91-1.00x for 0 (profiles/r3/rejected/gemm_nt_2phase_*)
 int gemm_nt_variant();
 void gemm_nt_set_variant(int v);

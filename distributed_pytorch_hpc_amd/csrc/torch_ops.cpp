@@ -1136,7 +1136,7 @@ Tensor gemm_nt(const Tensor& A, const Tensor& B) {
   const Tensor a = rows2d(A, "gemm_nt A"), b = rows2d(B, "gemm_nt B");
   TORCH_CHECK(B.dim() == 2 && b.size(1) == a.size(1), "gemm_nt: B must be [N, K] with A's K");
   TORCH_CHECK(dph::gemm_nt_supported(dph::kNtStore, a.size(0), b.size(0), a.size(1)),
-              "gemm_nt: need rows % 256, N % 256, K % 64 (got ", a.size(0), ", ", b.size(0), ", ", a.size(1), ")");
+              "gemm_nt: need rows % 256, N % 8, K % 8 (got ", a.size(0), ", ", b.size(0), ", ", a.size(1), ")");
   Tensor C = at::empty(out_sizes(A, b.size(0)), A.options());
   auto p = nt_params(a, b);
   p.N = (int)b.size(0);
@@ -1154,7 +1154,7 @@ std::tuple<Tensor, Tensor> gemm_nt_swiglu(const Tensor& x, const Tensor& w13) {
   TORCH_CHECK(w13.dim() == 2 && b.size(1) == a.size(1) && b.size(0) % 2 == 0, "gemm_nt_swiglu: w13 [2H, K]");
   const int64_t H = b.size(0) / 2;
   TORCH_CHECK(dph::gemm_nt_supported(dph::kNtSwiglu, a.size(0), H, a.size(1)),
-              "gemm_nt_swiglu: need rows % 256, H % 128, K % 64 (got ", a.size(0), ", ", H, ", ", a.size(1), ")");
+              "gemm_nt_swiglu: need rows % 256, H % 8, K % 8 (got ", a.size(0), ", ", H, ", ", a.size(1), ")");
   Tensor x13 = at::empty(out_sizes(x, 2 * H), x.options());
   Tensor h = at::empty(out_sizes(x, H), x.options());
   auto p = nt_params(a, b);
@@ -1178,7 +1178,7 @@ Tensor gemm_nt_dswiglu(const Tensor& dy, const Tensor& w2t, const Tensor& x13) {
   TORCH_CHECK(w2t.dim() == 2 && b.size(1) == a.size(1) && xr.size(0) == a.size(0) && xr.size(1) == 2 * H,
               "gemm_nt_dswiglu: w2t [H, K], x13 [rows, 2H]");
   TORCH_CHECK(dph::gemm_nt_supported(dph::kNtDswiglu, a.size(0), H, a.size(1)),
-              "gemm_nt_dswiglu: need rows % 256, H % 256, K % 64 (got ", a.size(0), ", ", H, ", ", a.size(1), ")");
+              "gemm_nt_dswiglu: need rows % 256, H % 8, K % 8 (got ", a.size(0), ", ", H, ", ", a.size(1), ")");
   Tensor d13 = at::empty(out_sizes(dy, 2 * H), dy.options());
   auto p = nt_params(a, b);
   p.N = (int)H;
@@ -1204,7 +1204,7 @@ Tensor gemm_nt_rope(const Tensor& x, const Tensor& w, const Tensor& cos_t, const
   TORCH_CHECK(n_rot % hd == 0 && n_rot <= b.size(0) && S > 0 && a.size(0) % S == 0 &&
                   cos_t.size(0) >= S + pos_off, "gemm_nt_rope: bad rotary layout");
   TORCH_CHECK(dph::gemm_nt_supported(dph::kNtRope, a.size(0), b.size(0), a.size(1)),
-              "gemm_nt_rope: need rows % 256, N % 256, K % 64");
+              "gemm_nt_rope: need rows % 256, N % 8, K % 8");
   Tensor C = at::empty(out_sizes(x, b.size(0)), x.options());
   auto p = nt_params(a, b);
   p.N = (int)b.size(0);

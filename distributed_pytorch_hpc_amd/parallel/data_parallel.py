@@ -35,6 +35,7 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
+from ..comm.custom_allreduce import use_custom as use_custom_allreduce
 from ..ops import _lib
 from ..train import optim as optim_ref
 from ..utils.flat import ALIGN, align_up, param_view
@@ -280,11 +281,14 @@ class DataParallelEngine:
             self._tp_partial.append((g, cat.to(self.device)))
 
     def _reduce_tp_partial(self):
+        from ..comm.functional import all_reduce_
+
         red = self.grad_shard if self.shard else self.flat_grad
         for g, idx in self._tp_partial:
-            # every rank of the TP group joins the collective, even one whose shard holds none of the elements
-            buf = red.index_select(0, idx) if idx.numel() else torch.zeros(1, dtype=red.dtype, device=red.device)
-            dist.all_reduce(buf, group=g)
+            # every rank of the TP group joins the collective, even one whose shard holds none of the elements; the
+            # message is small, so below the measured crossover it takes the direct-peer path (all_reduce_)
+            buf = red.index_select(0, idx) if idx.numel() else torch.zeros(8, dtype=red.dtype, device=red.device)
+            all_reduce_(buf, g)
             if idx.numel():
                 red.index_copy_(0, idx, buf)
 
@@ -364,7 +368,14 @@ class DataParallelEngine:
                 b.work = dist.reduce_scatter_tensor(self.grad_shard_view(b), g, op=dist.ReduceOp.SUM,
                                                     group=self.group, async_op=True)
             else:
-                b.work = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                # a bucket below the group's measured crossover (typically the small tail bucket) takes the
+                # direct-peer xGMI all-reduce on the stream (comm/custom_allreduce.py); the rest RCCL
+                car = use_custom_allreduce(g, self.group)
+                if car is not None:
+                    car.all_reduce(g)
+                    b.work = None
+                else:
+                    b.work = dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def _join_wgrad_stream(self):
         join_wgrad_stream(self.device)

@@ -11,9 +11,12 @@
 
 Weight gradients take the same route as every other linear layer of the framework (parallel/linear.py:
 ``weight_grad`` writes them straight into the data-parallel engine's bucket and notifies it), so the engines'
-overlapped reduce-scatter / all-reduce see no difference.  The fused paths are taken for plain (not tensor-parallel,
-not FP8) bf16 projections whose shapes the kernel tiles (rows % 256, features % 256, K % 64); everything else runs
-the unfused modules.  ``DPH_FUSED_MLP=0`` / ``DPH_FUSED_QKV=1`` switch them (A/B runs); by default the MLP's
+overlapped reduce-scatter / all-reduce see no difference.  The fused paths are taken for bf16 projections whose
+shapes the kernel tiles (rows % 256, features % 8, K % 8 -- shapes off the 256 / 64 grid run its ragged edge tiles),
+plain or tensor-parallel: a ColwiseParallelLinear w13 / wqkv with a RowwiseParallelLinear w2 / wo (Megatron pair,
+fsdp_tp/fsdp_tp_example.py:165-176) runs the same fused local computation between the pair's sequence all-gather
+(or copy-to-group) and reduce-scatter (or all-reduce) -- at tp = 8 the 7B shards (SwiGLU H = 1376, w2's K = 1376)
+tile as edge tiles.  FP8 and async-TP (pipelined micro-collectives) keep the unfused modules.  ``DPH_FUSED_MLP=0`` / ``DPH_FUSED_QKV=1`` switch them (A/B runs); by default the MLP's
 fusions are on and the QKV + RoPE one is off.
 """
 from __future__ import annotations
@@ -62,6 +65,49 @@ def _plain_weight(mod) -> bool:
     return isinstance(mod, nn.Linear) and mod.bias is None and not getattr(mod.weight, "_dph_tp", False)
 
 
+def _tp_col(mod) -> bool:
+    from .tensor_parallel import ColwiseParallelLinear
+
+    return (isinstance(mod, ColwiseParallelLinear) and mod.bias is None and not mod.gather_output and
+            mod.seq_dim == 1 and not mod.async_chunks)
+
+
+def _tp_row(mod) -> bool:
+    from .tensor_parallel import RowwiseParallelLinear
+
+    return (isinstance(mod, RowwiseParallelLinear) and mod.bias is None and mod.input_is_parallel and
+            mod.seq_dim == 1 and not mod.async_chunks)
+
+
+def _tp_pair(col, row) -> bool:
+    return _tp_col(col) and _tp_row(row) and col.group is row.group and col.sp == row.sp
+
+
+def _tp_world(mod) -> int:
+    import torch.distributed as dist
+
+    return dist.get_world_size(mod.group) if dist.is_initialized() else 1
+
+
+def _tp_input(col, x):
+    """The column-parallel layer's input as its local GEMM sees it: sequence-gathered (SP) or copied to the group."""
+    from ..comm import functional as cf
+
+    return cf.gather_along_dim(x, 1, col.group) if col.sp else cf.copy_to_group(x, col.group)
+
+
+def _tp_output(row, y):
+    from ..comm import functional as cf
+
+    return cf.reduce_scatter_along_dim(y, 1, row.group) if row.sp else cf.reduce_from_group(y, row.group)
+
+
+def _nt_ok(rows: int, n: int, k: int) -> bool:
+    """Shapes the CDNA4 NT kernel tiles (csrc/gemm_nt.hip gemm_nt_supported): rows % 256, N % 8, K % 8, 32-bit
+    offsets."""
+    return rows > 0 and rows % 256 == 0 and n % 8 == 0 and k % 8 == 0 and n * k * 2 < (1 << 31)
+
+
 def _native_bf16(*ts) -> bool:
     return all(t.is_cuda and t.dtype == torch.bfloat16 for t in ts) and not _lib.reference_mode() and \
         _lib.use_native(ts[0])
@@ -71,17 +117,23 @@ def _rows_ok(t: torch.Tensor) -> bool:
     return t.stride(-1) == 1 and t.is_contiguous() and t.data_ptr() % 16 == 0
 
 
+def nt_enabled() -> bool:
+    """Every forward / input-gradient GEMM of the framework's linear layers on the CDNA4 NT kernel (DPH_GEMM_NT=all)."""
+    return _GEMM_NT == "all"
+
+
 def nt_matmul(a2: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
     """a2 [M, K] @ b[N, K]^T on the CDNA4 kernel when enabled for all GEMMs and tileable, else hipBLASLt."""
-    if _GEMM_NT == "all" and _native_bf16(a2, b) and a2.shape[0] % 256 == 0 and b.shape[0] % 256 == 0 and \
-            a2.shape[1] % 64 == 0 and _rows_ok(a2) and b.is_contiguous():
+    if _GEMM_NT == "all" and _native_bf16(a2, b) and _nt_ok(a2.shape[0], b.shape[0], a2.shape[1]) and \
+            _rows_ok(a2) and b.is_contiguous():
         return _lib.ops().gemm_nt(a2, b)
     return torch.matmul(a2, b.t())
 
 
 def _dgrad_nt(g2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dX = dY W for a [N, K] weight: the library path of parallel/linear.py, or the CDNA4 kernel on W^T."""
-    if _GEMM_NT == "all" and g2.shape[0] % 256 == 0 and w.shape[1] % 256 == 0 and w.shape[0] % 64 == 0:
+    if _GEMM_NT == "all" and _native_bf16(g2, w) and _nt_ok(g2.shape[0], w.shape[1], w.shape[0]) and \
+            _rows_ok(g2) and w.is_contiguous():
         return _lib.ops().gemm_nt(g2, _lib.ops().transpose2d(w))
     return _dgrad(g2, w)
 
@@ -121,17 +173,30 @@ class _SwiGLUMLPFn(torch.autograd.Function):
 
 
 def swiglu_mlp_ok(x: torch.Tensor, w13_mod, w2_mod) -> bool:
-    if not (_FUSED_MLP and _GEMM_NT != "0" and _plain_weight(w13_mod) and _plain_weight(w2_mod)):
+    if not (_FUSED_MLP and _GEMM_NT != "0"):
+        return False
+    tp = _tp_pair(w13_mod, w2_mod)
+    if not (tp or (_plain_weight(w13_mod) and _plain_weight(w2_mod))):
         return False
     if _fp8.fp8_enabled() or not _native_bf16(x, w13_mod.weight, w2_mod.weight) or not _rows_ok(x):
         return False
     rows, k = x.numel() // x.shape[-1], x.shape[-1]
+    if tp and w13_mod.sp:
+        if x.dim() != 3:
+            return False
+        rows *= _tp_world(w13_mod)            # the local GEMMs see the sequence-gathered activations
     h2 = w13_mod.weight.shape[0]
-    return (rows % 256 == 0 and k % 64 == 0 and h2 % 512 == 0 and w2_mod.weight.shape[1] == h2 // 2
-            and w2_mod.weight.shape[0] % 256 == 0 and w13_mod.weight.is_contiguous() and w2_mod.weight.is_contiguous())
+    h, d_out = h2 // 2, w2_mod.weight.shape[0]
+    return (h2 % 2 == 0 and w2_mod.weight.shape[1] == h and _nt_ok(rows, h2, k) and _nt_ok(rows, d_out, h)
+            and _nt_ok(rows, h, d_out) and w13_mod.weight.is_contiguous() and w2_mod.weight.is_contiguous())
 
 
 def swiglu_mlp(x: torch.Tensor, w13_mod, w2_mod) -> torch.Tensor:
+    if _tp_pair(w13_mod, w2_mod):
+        # Megatron pair: the local fused MLP between the column layer's input collective and the row layer's output
+        # collective (their autograd adjoints give the backward's reduce-scatter / all-gather)
+        y = _SwiGLUMLPFn.apply(_tp_input(w13_mod, x), w13_mod.weight, w2_mod.weight, _FUSED_MLP is True)
+        return _tp_output(w2_mod, y)
     return _SwiGLUMLPFn.apply(x, w13_mod.weight, w2_mod.weight, _FUSED_MLP is True)
 
 
@@ -178,16 +243,21 @@ class _QKVRopeAttnFn(torch.autograd.Function):
 
 
 def qkv_rope_attention_ok(x: torch.Tensor, wqkv_mod, hd: int) -> bool:
-    if not (_FUSED_QKV and _GEMM_NT != "0" and _plain_weight(wqkv_mod)) or x.dim() != 3:
+    tp = _tp_col(wqkv_mod)
+    if not (_FUSED_QKV and _GEMM_NT != "0" and (tp or _plain_weight(wqkv_mod))) or x.dim() != 3:
         return False
     if _fp8.fp8_enabled() or not _native_bf16(x, wqkv_mod.weight) or not _rows_ok(x):
         return False
     b, s, k = x.shape
+    if tp and wqkv_mod.sp:
+        s *= _tp_world(wqkv_mod)
     n = wqkv_mod.weight.shape[0]
-    return ((b * s) % 256 == 0 and k % 64 == 0 and n % 256 == 0 and hd in (64, 128) and
-            wqkv_mod.weight.is_contiguous())
+    return _nt_ok(b * s, n, k) and hd in (64, 128) and wqkv_mod.weight.is_contiguous()
 
 
 def qkv_rope_attention(x, wqkv_mod, cos, sin, n_heads: int, n_kv_heads: int, head_dim: int,
                        pos_offset: int = 0) -> torch.Tensor:
+    """n_heads / n_kv_heads: the LOCAL head counts (tensor-parallel: this rank's heads of the column shard)."""
+    if _tp_col(wqkv_mod):
+        x = _tp_input(wqkv_mod, x)
     return _QKVRopeAttnFn.apply(x, wqkv_mod.weight, cos, sin, n_heads, n_kv_heads, head_dim, pos_offset)

@@ -75,16 +75,47 @@ def _native_wgrad(out: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor, accumul
     return True
 
 
+def _nt_ok(a: torch.Tensor, w: torch.Tensor) -> bool:
+    """a [..., K] @ w[N, K]^T can run on the CDNA4 NT kernel (csrc/gemm_nt.hip) and DPH_GEMM_NT=all asks for it."""
+    from . import fused_layers
+
+    if not fused_layers.nt_enabled():
+        return False
+    if not (a.is_cuda and a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.dim() == 2):
+        return False
+    from ..ops import _lib
+
+    if _lib.reference_mode() or not _lib.use_native(a):
+        return False
+    K = a.shape[-1]
+    rows = a.numel() // K if K else 0
+    if not fused_layers._nt_ok(rows, w.shape[0], K) or w.shape[1] != K or not w.is_contiguous():
+        return False
+    return a.is_contiguous() and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0
+
+
+def _fwd_gemm(x: torch.Tensor, w: torch.Tensor, b=None) -> torch.Tensor:
+    """y = x W^T (+ b): the CDNA4 NT kernel when enabled and tileable, else hipBLASLt (F.linear)."""
+    if b is None and _nt_ok(x, w):
+        from ..ops import _lib
+
+        return _lib.ops().gemm_nt(x, w)
+    return F.linear(x, w, b)
+
+
 def _dgrad(gy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """dX = dY W.  hipBLASLt runs this 10-15 % faster with a K-contiguous W^T operand (mm(dY, W^T.t()):
     profiles/gemm_layout_*.json); the HIP transpose makes that copy at HBM speed (~0.04-0.07 ms for 7B weights)
-    and it is freed right after the GEMM."""
+    and it is freed right after the GEMM.  With DPH_GEMM_NT=all the same W^T feeds the CDNA4 NT kernel."""
     if (gy.is_cuda and w.dtype == torch.bfloat16 and gy.dtype == torch.bfloat16 and w.dim() == 2
             and w.is_contiguous() and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and w.numel() >= (1 << 22)):
         from ..ops import _lib
 
         if not _lib.reference_mode():
             wt = _lib.ops().transpose2d(w)
+            gyc = gy.contiguous()
+            if _nt_ok(gyc, wt):
+                return _lib.ops().gemm_nt(gyc, wt)
             return torch.matmul(gy, wt.t())
     return torch.matmul(gy, w)
 
@@ -171,7 +202,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
         with torch.autocast(x.device.type, enabled=False):
-            return F.linear(x, w, b)
+            return _fwd_gemm(x, w, b)
 
     @staticmethod
     def backward(ctx, gy):

@@ -39,6 +39,9 @@ class Workload:
     replica_flat: Optional[torch.Tensor] = None
     flops_per_item: float = 0.0
     extra: dict = field(default_factory=dict)
+    # (name, group) pairs whose all-reduces may take the direct-peer xGMI path below a measured crossover
+    # (bench.py probes each before timing; comm/custom_allreduce.py)
+    ar_groups: list = field(default_factory=list)
 
 
 def _bucket(args, world_dp: int, grad_bytes: float, sharded: bool, group, dev, log) -> tuple[float, dict]:
@@ -180,7 +183,8 @@ def _tp_hybrid(args, rank, world, dev, log, tp: int, layout: str) -> Workload:
     # strong scaling for pure TP (the batch is fixed as N grows), weak over the dp dimension for the hybrid
     return Workload(step, engine, metric, "tokens/s", dp * B * S, "strong" if layout == "tp" else "weak", cfg,
                     replica_group=dp_group, replica_flat=engine.flat_param if dp > 1 else None,
-                    flops_per_item=margs.flops_per_token(S))
+                    flops_per_item=margs.flops_per_token(S),
+                    ar_groups=[("tp", mesh.tp_group)] if tp > 1 else [])
 
 
 def build_tp(args, rank, world, dev, log) -> Workload:
@@ -332,11 +336,13 @@ def build_resnet_fsdp(args, rank, world, dev, log) -> Workload:
 def build_unet_ddp(args, rank, world, dev, log) -> Workload:
     """SimpleUNet data-parallel training on ERA5-shaped fields (scripts/01_data_parallel_ddp/multinode_ddp_unet.py:
     B = 4 per GPU, AdamW lr 1e-4 wd 1e-5, latitude-weighted MSE, 65 channels on the 181 x 360 grid).  MI355X path:
-    channels-last activations, bf16 autocast over fp32 master weights (``--unet-precision fp32`` = the reference's
-    fp32), DDP engine with one gradient bucket all-reduced during backward."""
+    channels-last activations and the engine's mixed precision -- bf16 parameters / activations / gradient
+    buckets with the fp32 master weights and AdamW state in the fused optimizer (as the ResNet FSDP path), so no
+    per-step cast or layout-flip kernels run (``--unet-precision bf16-autocast`` = bf16 autocast over fp32 weights,
+    ``fp32`` = the reference's precision); DDP engine with one gradient bucket all-reduced during backward."""
     from ..models.unet import SimpleUNet, to_channels_last
     from ..ops.loss import latitude_weighted_mse
-    from ..parallel.data_parallel import DDP
+    from ..parallel.data_parallel import DDP, MixedPrecision
 
     cpu = dev.type == "cpu"
     C = 65 if not cpu else 5
@@ -346,21 +352,26 @@ def build_unet_ddp(args, rank, world, dev, log) -> Workload:
     torch.manual_seed(1234)
     model = to_channels_last(SimpleUNet(C, C, base).to(dev))
     n_params = sum(p.numel() for p in model.parameters())
-    grad_bytes = n_params * 4
+    prec = args.unet_precision if not cpu else "fp32"
+    mp = MixedPrecision(torch.bfloat16, torch.bfloat16, torch.bfloat16) if prec == "bf16" else None
+    grad_bytes = n_params * (2 if mp is not None else 4)
     bucket_mb, binfo = _bucket(args, world, grad_bytes, False, None, dev, log)
-    ddp = DDP(model, bucket_cap_mb=bucket_mb)
+    ddp = DDP(model, bucket_cap_mb=bucket_mb, mixed_precision=mp)
     opt = ddp.make_optimizer("adamw", lr=1e-4, weight_decay=1e-5)
     B = args.micro_batch
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     x = torch.randn(B, C, lat, lon, device=dev, generator=g).contiguous(memory_format=torch.channels_last)
     y = (x + 0.1 * torch.randn(B, C, lat, lon, device=dev, generator=g)).contiguous(memory_format=torch.channels_last)
-    amp = (not cpu) and args.unet_precision == "bf16"
+    if mp is not None:   # the data loader hands bf16 fields over (one cast per batch, outside the step)
+        x = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        y = y.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    amp = prec == "bf16-autocast"
 
     def step(i):
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             out = ddp(x)
-        loss = latitude_weighted_mse(out.float() if out.dtype != torch.float32 else out, y)
+        loss = latitude_weighted_mse(out, y)
         loss.backward()
         opt.step()
         opt.zero_grad()
@@ -368,11 +379,14 @@ def build_unet_ddp(args, rank, world, dev, log) -> Workload:
 
     cfg = {"model": "SimpleUNet (7,742,849 params)" if not cpu else f"SimpleUNet-mini ({n_params} params)",
            "global_batch": world * B, "grid": f"{C} x {lat} x {lon}", "parallelism": f"ddp{world}",
-           "micro_batch_per_gpu": B, "precision": "bf16 autocast, fp32 master weights" if amp else "fp32",
+           "micro_batch_per_gpu": B,
+           "precision": {"bf16": "bf16 params / activations / grads, fp32 master weights + AdamW",
+                         "bf16-autocast": "bf16 autocast over fp32 weights", "fp32": "fp32"}[prec],
            "channels_last": True, "optimizer": "AdamW lr 1e-4 wd 1e-5 (multinode_ddp_unet.py:316)",
            "loss": "latitude-weighted MSE", "bucket_mb": round(bucket_mb, 1)}
     return Workload(step, ddp.engine, "samples/sec, SimpleUNet DDP ERA5 65x181x360", "samples/s", world * B,
-                    "weak", cfg, replica_group=None, replica_flat=ddp.engine.flat_param, extra=binfo)
+                    "weak", cfg, replica_group=None, replica_flat=ddp.engine.flat_param, extra=binfo,
+                    ar_groups=[("world", None)] if world > 1 else [])
 
 
 BUILDERS = {"dp": build_dp, "tp": build_tp, "hybrid": build_hybrid, "pp": build_pp, "resnet-fsdp": build_resnet_fsdp,

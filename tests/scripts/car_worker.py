@@ -26,6 +26,61 @@ def expected(xs, scale):
     return (acc * scale).to(xs[0].dtype)
 
 
+def engine_routed(rank, world):
+    """The replicated data-parallel engine with a recorded crossover: buckets up to it go through the direct-peer
+    all-reduce (counted), larger ones through the collective backend; parameters after 3 AdamW steps match the run
+    with no crossover recorded (everything on the backend) and every replica agrees bitwise."""
+    from distributed_pytorch_hpc_amd.comm import custom_allreduce as C
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, MixedPrecision, OptimConfig
+
+    def run(crossover):
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.GELU(), torch.nn.Linear(512, 64)).cuda()
+        if crossover:
+            C.set_policy(None, crossover, allow_any_backend=True)
+        else:
+            C.clear_policy(None)
+        eng = DataParallelEngine(m, shard=False, bucket_cap_mb=0.25,
+                                 mixed_precision=MixedPrecision(reduce_dtype=torch.float32))
+        eng.configure_optimizer(OptimConfig(lr=1e-2))
+        calls = {"n": 0}
+        real = C.XgmiAllReduce.all_reduce
+
+        def counted(self, t, *a, **kw):
+            calls["n"] += 1
+            return real(self, t, *a, **kw)
+
+        C.XgmiAllReduce.all_reduce = counted
+        try:
+            for step in range(3):
+                g = torch.Generator().manual_seed(100 * step + rank)
+                x = torch.randn(32, 256, generator=g).cuda()
+                m(x).square().mean().backward()
+                eng.step()
+                eng.zero_grad()
+            eng.synchronize()
+            torch.cuda.synchronize()
+        finally:
+            C.XgmiAllReduce.all_reduce = real
+            C.clear_policy(None)
+        return eng.flat_param.float().cpu(), calls["n"], len(eng.buckets)
+
+    fails = []
+    p0, n0, nb = run(0)
+    p1, n1, _ = run(256 << 10)          # the 256 KiB crossover: the small buckets go direct-peer
+    if n0 != 0:
+        fails.append(f"engine: {n0} direct-peer calls without a recorded crossover")
+    if not (0 < n1 < 3 * nb):
+        fails.append(f"engine: {n1} direct-peer calls for {nb} buckets x 3 steps (want some, not all)")
+    if not torch.allclose(p0, p1, atol=1e-6, rtol=1e-5):
+        fails.append(f"engine: params differ by {(p0 - p1).abs().max().item()}")
+    got = [None] * world
+    dist.all_gather_object(got, p1)
+    if any(not torch.equal(got[0], g) for g in got):
+        fails.append("engine: replicas diverged")
+    return fails
+
+
 def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -73,6 +128,7 @@ def main():
     if err:
         fails.append(f"{err} barrier timeouts")
     car.close()
+    fails += engine_routed(rank, world)
     flags = [None] * world
     dist.all_gather_object(flags, fails)
     if rank == 0:

@@ -37,3 +37,37 @@ def test_custom_allreduce_not_used_on_cpu(monkeypatch):
     assert get_custom_allreduce(None) is None          # no process group
     x = torch.ones(16)
     assert F.all_reduce_(x, None) is x                 # world 1: untouched
+
+
+def test_choose_crossover_rule():
+    from distributed_pytorch_hpc_amd.comm.custom_allreduce import choose_crossover
+
+    KiB = 1 << 10
+    # direct-peer wins up to 256 KiB, then RCCL: the crossover is the last winning size
+    s = [(4 * KiB, 20e-6, 8e-6), (64 * KiB, 22e-6, 10e-6), (256 * KiB, 30e-6, 25e-6), (1 << 20, 40e-6, 45e-6),
+         (4 << 20, 80e-6, 70e-6)]
+    assert choose_crossover(s) == 256 * KiB          # a later win after a loss does not count
+    assert choose_crossover(list(reversed(s))) == 256 * KiB
+    assert choose_crossover([(4 * KiB, 5e-6, 9e-6)]) == 0          # RCCL wins from the start: nothing changes
+    assert choose_crossover([(4 * KiB, 5e-6, None)]) == 0          # no direct-peer arm on this group
+    assert choose_crossover([]) == 0
+
+
+def test_policy_routing_is_size_and_env_driven(monkeypatch):
+    from distributed_pytorch_hpc_amd.comm import custom_allreduce as C
+
+    monkeypatch.delenv("DPH_CUSTOM_ALLREDUCE", raising=False)
+    C.clear_policy(None)
+    assert C.policy_max_bytes(None) == 0                       # no measurement: RCCL
+    C.set_policy(None, 1 << 20)
+    try:
+        assert C.policy_max_bytes(None) == 1 << 20
+        monkeypatch.setenv("DPH_CUSTOM_ALLREDUCE", "0")
+        assert C.policy_max_bytes(None) == 0                   # forced off
+        monkeypatch.setenv("DPH_CUSTOM_ALLREDUCE", "1")
+        monkeypatch.setenv("DPH_CUSTOM_ALLREDUCE_MAX_BYTES", str(4 << 20))
+        assert C.policy_max_bytes(None) == 4 << 20             # forced on
+        monkeypatch.delenv("DPH_CUSTOM_ALLREDUCE")
+        assert C.use_custom(torch.ones(16), None) is None      # CPU tensors never take the IPC path
+    finally:
+        C.clear_policy(None)

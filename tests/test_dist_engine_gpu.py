@@ -56,3 +56,50 @@ def test_sharded_engine_matches_ddp_two_ranks_one_gpu():
             assert torch.equal(v, ddp_sd[k]), k                      # replicas bitwise identical
             torch.testing.assert_close(sd_sh[k], v, atol=2e-3, rtol=2e-2, msg=k)
     assert ddp_l[-1] < ddp_l[0]
+
+
+# ---- tensor-parallel pair on the fused CDNA4 paths (ragged shard shapes), two TP ranks on one GPU ----
+TP_PRESET = dict(dim=512, n_layers=2, n_heads=4, vocab_size=512, max_seq_len=256, multiple_of=32)   # H 1376 -> 688
+
+
+def _tp_fused_run(rank, world, fused):
+    from distributed_pytorch_hpc_amd.models.llama2 import ModelArgs, build_llama
+    from distributed_pytorch_hpc_amd.ops import _lib
+    from distributed_pytorch_hpc_amd.parallel import fused_layers
+    from distributed_pytorch_hpc_amd.parallel.tensor_parallel import parallelize_llama
+
+    _lib.require()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    old = fused_layers.set_enabled(mlp=fused, qkv=fused, gemm_nt="all" if fused else "0")
+    try:
+        m = build_llama(ModelArgs(**TP_PRESET), device=dev, dtype=torch.bfloat16, seed=3)
+        parallelize_llama(m, dist.group.WORLD, sequence_parallel=True, loss_parallel=True)
+        ff, at = m.layers[0].feed_forward, m.layers[0].attention
+        assert ff.w13.weight.shape[0] == 2 * 688                # ragged for the 128-unit SwiGLU tile
+        x = torch.zeros(2, 256 // world, 512, device=dev, dtype=torch.bfloat16)
+        assert fused_layers.swiglu_mlp_ok(x, ff.w13, ff.w2) == fused
+        assert fused_layers.qkv_rope_attention_ok(x, at.wqkv, at.head_dim) == fused
+        g = torch.Generator().manual_seed(9)
+        t = torch.randint(0, TP_PRESET["vocab_size"], (2, 257), generator=g).to(dev)
+        loss = m(t[:, :-1], t[:, 1:])
+        loss.backward()
+        torch.cuda.synchronize()
+        return loss.item(), {n: p.grad.float().cpu() for n, p in m.named_parameters()}
+    finally:
+        fused_layers.set_enabled(*old)
+
+
+def _tp_fused_worker(rank, world):
+    return _tp_fused_run(rank, world, False), _tp_fused_run(rank, world, True)
+
+
+def test_tp_fused_mlp_qkv_match_unfused_two_ranks_one_gpu():
+    """A Megatron column / row pair (SP, loss-parallel, tp = 2) through the fused SwiGLU-MLP and QKV+RoPE paths on
+    the NT kernel (ragged shard: SwiGLU H = 688) gives the loss and every gradient of the unfused modules."""
+    outs = run_distributed(_tp_fused_worker, 2, timeout=110.0)
+    for (l0, g0), (l1, g1) in outs:
+        assert abs(l0 - l1) < 1e-2 * abs(l0)
+        for n in g0:
+            err = ((g1[n] - g0[n]).norm() / (g0[n].norm() + 1e-12)).item()
+            assert err < 3e-2, (n, err)
