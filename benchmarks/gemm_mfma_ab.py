@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--variants", default="32,16")
+    ap.add_argument("--variants", default="32,33,16")
     ap.add_argument("--shapes", default=",".join(SHAPES))
     a = ap.parse_args()
     variants = [int(v) for v in a.variants.split(",")]

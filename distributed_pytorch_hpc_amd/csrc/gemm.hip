@@ -273,6 +273,198 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, 
 }
 
 // ------------------------------------------------------------------------------------------------------------------
+// Staggered variant of gemm_tn_k (DPH_WGRAD_MFMA=33 / gemm_tn_set_mfma(33)).  Waves 4..7 run one barrier behind
+// waves 0..3, so on every SIMD one wave issues its slot's MFMAs while its partner waits at the barrier, issues its
+// DMA pair and transposed reads (the ping-pong of gemm_nt.hip); in lockstep both waves of a SIMD reach the barrier
+// together and the matrix pipe idles while they wait (PMC on the w13 shape: SQ_WAIT_ANY 40 % of wave cycles, MFMA
+// busy 0.74).  The stagger makes an early wave's read of region S+1 at its slot S race the LATE waves' share of that
+// region's DMA, so the pipeline is one pair deeper: slot S retires pair S+2 (not S+1) before its barrier and issues
+// pair S+5 (not S+4); regions in use at once: S..S+5 = 6 of the 8.  WAR: pair S+5 overwrites pair S-3's region,
+// whose last reader (a late wave, in its slot S-4 = the early waves' slot S-3) is two barriers back.
+// No tail code: a pair index past the last one re-loads the last pair (finite data) into a region whose contents are
+// never multiplied, so every slot has the same DMA / counted wait / read and the loop body is one 8-slot block (plus
+// one 4-slot block for an odd K-tile count) -- the tail sequences of gemm_tn_k cost ~400 VGPR spills and a
+// vmcnt(0) drain per iteration where the waitcnt pass merged the spill reloads into the loop.
+template <typename OutT, bool ACCUM>
+__global__ __launch_bounds__(GNT, 1) void gemm_tn_stag_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                         OutT* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                         int64_t ldb, int64_t ldc, int64_t cstride) {
+  A += (int64_t)blockIdx.y * K * lda;
+  B += (int64_t)blockIdx.y * K * ldb;
+  C += (int64_t)blockIdx.y * cstride;
+  __shared__ __attribute__((aligned(1024))) char lds[8 * 16384];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int h = lane >> 5, l32 = lane & 31;
+  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
+
+  const int tiles_m = (M + GBM - 1) / GBM, tiles_n = (N + GBN - 1) / GBN, nwg = tiles_m * tiles_n;
+  int tm, tn;
+  grouped_tile(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * GBM, n0 = tn * GBN;
+
+  const int x = 2 * (g & 1) + (tp >> 1);
+  const int krow = 4 * (g >> 1) + tq;
+  const int base = krow * ROWB + 8 * (tp & 1);
+  int aoff[4], boff[2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) aoff[mt] = base + (wm << 8) + ((4 * (mt ^ tq) + x) << 4);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+    boff[nt] = 8192 + base + ((wn >> 1) << 8) + ((4 * ((((wn & 1) << 1) | nt) ^ tq) + x) << 4);
+
+  const int srow = threadIdx.x >> 5, lr = (threadIdx.x >> 4) & 1, sslot = threadIdx.x & 15;
+  const int sch = (lr << 4) | (sslot ^ ((srow & 3) << 2));
+  const int colA = min(sch * 8, M - 8 - m0), colB = min(sch * 8, N - 8 - n0);
+  const unsigned voffA = (unsigned)((srow * lda + colA) * 2), voffB = (unsigned)((srow * ldb + colB) * 2);
+  const char* Ag = reinterpret_cast<const char*>(A + m0);
+  const char* Bg = reinterpret_cast<const char*>(B + n0);
+  const int64_t stepA = 16 * lda * 2, stepB = 16 * ldb * 2;
+  const unsigned lds_wave = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds + (threadIdx.x >> 6) * 1024);
+
+  auto region = [&](auto RI) -> char* { return lds + decltype(RI)::value * 16384; };
+  const int NP = (K / GBK) * 4;
+  auto dma_pair = [&](int P, auto RI) {
+    const unsigned d = lds_wave + decltype(RI)::value * 16384;
+    const int Pc = min(P, NP - 1);   // past the end: the last pair again, into a region nobody multiplies
+    glds16(Ag + Pc * stepA, voffA, d);
+    glds16(Bg + Pc * stepB, voffB, d + 8192);
+  };
+  auto read_phase = [&](auto RI, bf16x8 (&af)[4], bf16x8 (&bfr)[2]) {
+    const char* rg = region(RI);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) af[mt] = tr2(rg, aoff[mt], aoff[mt] + 8 * ROWB);
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) bfr[nt] = tr2(rg, boff[nt], boff[nt] + 8 * ROWB);
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.f;
+
+  auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[2]) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  // prologue: pairs 0..4 (regions 0..4), then pairs 0 and 1 retired by every wave before the common barrier
+  dma_pair(0, I0{});
+  dma_pair(1, I1{});
+  dma_pair(2, I2{});
+  dma_pair(3, I3{});
+  dma_pair(4, I4{});
+  wait_vm<6>();
+  __builtin_amdgcn_s_barrier();
+  bf16x8 af0[4], bf0[2], af1[4], bf1[2];
+  read_phase(I0{}, af0, bf0);
+  const bool late = __builtin_amdgcn_readfirstlane(wid) >= 4;
+  if (late) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+
+  // slot S (region S & 7): retire pair S+2 (vmcnt 4: pairs S+3, S+4 stay in flight) -> barrier -> DMA pair S+5 ->
+  // reads of region S+1 into the other register set interleaved with the 8 MFMAs of region S
+  auto slot = [&](int P0, auto SI, bf16x8 (&afc)[4], bf16x8 (&bfc)[2], bf16x8 (&afn)[4], bf16x8 (&bfn)[2]) {
+    constexpr int S = decltype(SI)::value;
+    wait_vm<4>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    dma_pair(P0 + S + 5, std::integral_constant<int, (S + 5) & 7>{});
+    __builtin_amdgcn_s_setprio(1);
+    read_phase(std::integral_constant<int, (S + 1) & 7>{}, afn, bfn);
+    mma(afc, bfc);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+#define DPH_S(i) std::integral_constant<int, i>{}
+  int P0 = 0;
+  for (; P0 + 8 <= NP; P0 += 8) {
+    slot(P0, DPH_S(0), af0, bf0, af1, bf1);
+    slot(P0, DPH_S(1), af1, bf1, af0, bf0);
+    slot(P0, DPH_S(2), af0, bf0, af1, bf1);
+    slot(P0, DPH_S(3), af1, bf1, af0, bf0);
+    slot(P0, DPH_S(4), af0, bf0, af1, bf1);
+    slot(P0, DPH_S(5), af1, bf1, af0, bf0);
+    slot(P0, DPH_S(6), af0, bf0, af1, bf1);
+    slot(P0, DPH_S(7), af1, bf1, af0, bf0);
+  }
+  if (P0 < NP) {   // odd number of K-tiles: the last one (regions 0..3)
+    slot(P0, DPH_S(0), af0, bf0, af1, bf1);
+    slot(P0, DPH_S(1), af1, bf1, af0, bf0);
+    slot(P0, DPH_S(2), af0, bf0, af1, bf1);
+    slot(P0, DPH_S(3), af1, bf1, af0, bf0);
+  }
+#undef DPH_S
+  if (!late) __builtin_amdgcn_s_barrier();   // balance the stagger
+  wait_vm<0>();
+
+  // ---- epilogue: as gemm_tn_k (LDS-staged 16-B row segments; ACCUM: per element) ----
+  if constexpr (!ACCUM) {
+    constexpr int VE = 16 / (int)sizeof(OutT);
+    constexpr int PR = (int)(sizeof(OutT) == 2 ? 256 : 128);
+    constexpr int NPASS = 256 / PR, SPR = 256 / VE;
+    OutT* ct = reinterpret_cast<OutT*>(lds);
+#pragma unroll
+    for (int pass = 0; pass < NPASS; ++pass) {
+      __syncthreads();
+      if (NPASS == 1 || wm == pass) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int r = (NPASS == 1 ? wm * 128 : 0) + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+              ct[r * 256 + wn * 64 + nt * 32 + l32] = (OutT)acc[mt][nt][i];
+            }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int c = threadIdx.x; c < PR * SPR; c += GNT) {
+        const int r = c / SPR, seg = c % SPR;
+        const int row = m0 + pass * PR + r, col = n0 + seg * VE;
+        if (row < M && col < N)
+          *reinterpret_cast<u32x4*>(C + (int64_t)row * ldc + col) =
+              *reinterpret_cast<const u32x4*>(ct + r * 256 + seg * VE);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int col = n0 + wn * 64 + nt * 32 + l32;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int row = m0 + wm * 128 + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (row >= M || col >= N) continue;
+          OutT* pp = C + (int64_t)row * ldc + col;
+          *pp = (OutT)(acc[mt][nt][i] + (float)*pp);
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
 // The same pipeline on v_mfma_f32_16x16x32_bf16.  The chip holds a higher clock on the 16x16x32 shape than on
 // 32x32x16 at equal cycles per FLOP (MI355X_MICROARCH.md 'DVFS give-back' item 7, cdna_hip_programming.md rule 28),
 // so the same output tile per wave (128 x 64 = 8 x 4 tiles of 16 x 16, 128 accumulator VGPRs) is built on both and
@@ -528,12 +720,13 @@ int gemm_tn_cus() {
 int gemm_tn_mfma() {
   if (g_gemm_tn_mfma == 0) {
     const char* e = getenv("DPH_WGRAD_MFMA");
-    g_gemm_tn_mfma = (e && atoi(e) == 32) ? 32 : (e && atoi(e) == 16) ? 16 : kGemmTnDefaultMfma;
+    const int v = e ? atoi(e) : 0;
+    g_gemm_tn_mfma = (v == 32 || v == 16 || v == 33) ? v : kGemmTnDefaultMfma;
   }
   return g_gemm_tn_mfma;
 }
 
-void gemm_tn_set_mfma(int shape) { g_gemm_tn_mfma = (shape == 16 || shape == 32) ? shape : 0; }
+void gemm_tn_set_mfma(int shape) { g_gemm_tn_mfma = (shape == 16 || shape == 32 || shape == 33) ? shape : 0; }
 
 void gemm_tn_set_tail(int cus) { g_gemm_tn_tail = cus; }
 
@@ -552,7 +745,7 @@ GemmTnPlan gemm_tn_plan(int64_t M, int64_t N, int64_t K) {
     const char* e = getenv("DPH_WGRAD_TAIL");
     return e && atoi(e) == 0;
   }();
-  if (g_gemm_tn_tail < 0 || (env_off && g_gemm_tn_tail == 0) || gemm_tn_mfma() != 32) return pl;
+  if (g_gemm_tn_tail < 0 || (env_off && g_gemm_tn_tail == 0) || gemm_tn_mfma() == 16) return pl;
   if (M % GBM || N % GBN) return pl;   // ragged edge tiles: one launch
   const int cus = gemm_tn_cus();
   const int64_t tm = M / GBM, tn = N / GBN, T = tm * tn;
@@ -592,7 +785,7 @@ GemmTnPlan gemm_tn_plan(int64_t M, int64_t N, int64_t K) {
 void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
              int64_t ldc, int out_dtype, bool accumulate, hipStream_t st, const GemmTnPlan* plan,
              float* workspace) {
-  const bool m16 = gemm_tn_mfma() == 16;
+  const bool m16 = gemm_tn_mfma() == 16, stag = gemm_tn_mfma() == 33;
   static const bool lds_epi = [] {   // DPH_WGRAD_EPI=scalar: per-element epilogue stores (A/B runs)
     const char* e = getenv("DPH_WGRAD_EPI");
     return !(e && e[0] == 's');
@@ -610,6 +803,9 @@ void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_
   do {                                                                                                         \
     if (m16)                                                                                                   \
       hipLaunchKernelGGL((gemm_tn16_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,     \
+                         lda, ldb, ldc_, cstride);                                                             \
+    else if (stag && (ACC || (lds_epi && vec_c)))                                                              \
+      hipLaunchKernelGGL((gemm_tn_stag_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,  \
                          lda, ldb, ldc_, cstride);                                                             \
     else if (!lds_epi || !vec_c)                                                                               \
       hipLaunchKernelGGL((gemm_tn_k<T, ACC, false>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,  \

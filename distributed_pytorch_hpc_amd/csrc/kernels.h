@@ -107,7 +107,7 @@ void embedding_bwd(const int64_t* sorted_ids, const int64_t* perm, const void* d
 // C[M, N] (+)= A^T B, A [K, M] / B [K, N] bf16 row-major (weight gradient); C bf16 or fp32.
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K);
 // MFMA shape of the wgrad kernel: 16 (v_mfma_f32_16x16x32_bf16) or 32 (v_mfma_f32_32x32x16_bf16); env DPH_WGRAD_MFMA
-constexpr int kGemmTnDefaultMfma = 32;
+constexpr int kGemmTnDefaultMfma = 33;   // 33 = gemm_tn_stag_k (staggered 32x32x16), +1-2 % isolated, +0.5 % in-step (profiles/r4/wgrad_stagger)
 int gemm_tn_mfma();
 void gemm_tn_set_mfma(int shape);
 // Partial-last-wave plan (csrc/gemm.hip gemm_tn_plan): compute the tile band that would run as a partial wave with K

@@ -301,7 +301,7 @@ def test_embedding(dph_native):
                          [(512, 256, 256, torch.float32, False), (1024, 512, 768, torch.bfloat16, False),
                           (2048, 768, 512, torch.bfloat16, True), (64, 256, 512, torch.float32, True),
                           (192, 256, 256, torch.float32, False), (128, 512, 256, torch.float32, True)])
-@pytest.mark.parametrize("mfma,tail", [(16, 0), (32, 0), (32, 3), (32, 8)])
+@pytest.mark.parametrize("mfma,tail", [(16, 0), (32, 0), (32, 3), (32, 8), (33, 0), (33, 3), (33, 8)])
 def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate, mfma, tail):
     """C (+)= A^T B with token-major A [K, M], B [K, N] (weight gradient dW = dY^T X), both MFMA-shape kernels
     (K = 64 / 128 / 192 exercise the one- and two-K-step tails of the pipeline).  tail > 0 plans the partial-last-
@@ -347,7 +347,7 @@ def test_gemm_tn_tail_band(dph_native, M, N, dim, out_dtype, accumulate):
 
 @pytest.mark.parametrize("K,M,N", [(256, 2752 // 4, 4096 // 8), (128, 264, 520), (192, 4000 // 10, 1376 // 4),
                                    (64, 8, 256), (512, 1000, 24)])
-@pytest.mark.parametrize("mfma", [16, 32])
+@pytest.mark.parametrize("mfma", [16, 32, 33])
 def test_gemm_tn_wgrad_ragged_edge_tiles(dph_native, K, M, N, mfma):
     """Tensor-parallel shard shapes (M, N % 8 but not % 256: w13 / w2 / vocab-head shards at tp=8) as partial edge
     tiles: every in-bounds element matches the fp32 reference and nothing past the matrix edge is written."""
