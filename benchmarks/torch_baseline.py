@@ -41,6 +41,10 @@ def main(argv=None):
     ap.add_argument("--adamw", choices=["fused", "foreach"], default="fused")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--params", choices=["fp32", "bf16"], default="fp32",
+                    help="fp32 = fp32 parameters + bf16 autocast (default); bf16 = bf16 parameters, no autocast, "
+                         "fused AdamW on the bf16 parameters (its states in bf16: lighter than the framework's fp32 "
+                         "master + states, so B = 8 fits)")
     args = ap.parse_args(argv)
 
     from distributed_pytorch_hpc_amd.models.llama2 import build_llama, get_preset
@@ -60,7 +64,8 @@ def main(argv=None):
     sync = (lambda: None) if cpu else torch.cuda.synchronize
 
     margs = get_preset(args.model, max_seq_len=max(args.seq_len, 4096))
-    model = build_llama(margs, device=dev, dtype=torch.float32, seed=1234)
+    model = build_llama(margs, device=dev, dtype=torch.bfloat16 if args.params == "bf16" else torch.float32,
+                        seed=1234)
     if world > 1:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=None if cpu else [local])
     opt = torch.optim.AdamW(model.parameters(), lr=3e-4, betas=(0.9, 0.95), weight_decay=0.1,
@@ -69,7 +74,7 @@ def main(argv=None):
     g = torch.Generator(device=dev)
     g.manual_seed(1000 + rank)
     batches = [torch.randint(0, margs.vocab_size, (B, S + 1), device=dev, generator=g) for _ in range(4)]
-    amp = torch.autocast(device_type=dev.type, dtype=torch.bfloat16)
+    amp = torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=args.params == "fp32")
 
     def step(i):
         t = batches[i % len(batches)]
@@ -103,12 +108,13 @@ def main(argv=None):
     if rank == 0:
         rec = {"metric": "tokens/sec, stock PyTorch-ROCm comparator (BASELINE.md)", "value": round(tps, 2),
                "unit": "tokens/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True, "dtype": "bf16 autocast",
+               "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
+               "dtype": "bf16 autocast" if args.params == "fp32" else "bf16",
                "data": "synthetic (random tokens, random-init weights)",
                "config": {"model": "Llama-2-7B" if args.model == "llama2-7b" else args.model,
                           "global_batch": world * B, "seq_len": S,
                           "parallelism": f"torch-ddp{world}" if world > 1 else "single",
-                          "optimizer": f"torch.optim.AdamW({args.adamw})", "params": "fp32"},
+                          "optimizer": f"torch.optim.AdamW({args.adamw})", "params": args.params},
                "tokens_per_sec_per_gpu": round(tps / world, 2),
                "peak_hbm_gb": 0.0 if cpu else round(torch.cuda.max_memory_allocated() / 1e9, 2),
                "loss_first_warmup": round(first, 4), "loss_last": round(float(loss.detach()), 4)}
