@@ -326,7 +326,13 @@ __device__ __forceinline__ int wave_tile_count(int ntiles, int q0w, int off) {
 // tile max exceeds it by more than RESCALE_THR (FA4-style lazy rescaling): p is then bounded by 2^THR,
 // harmless for the bf16 P operand and the fp32 accumulators, and the exact result is recovered by the
 // final 1/l.  The rescale branch is wave-uniform (ballot), so steady-state tiles skip 16*DT multiplies.
-template <int HD, bool CAUSAL, int NW, bool DROP = false>
+// STG (8 waves, DPH_ATTN_WAVES=9): waves 4..7 run one barrier behind waves 0..3, so on every SIMD one wave's QK^T /
+// PV MFMAs overlap its partner's softmax VALU work instead of both waves hitting the exp chain at once.  The K/V
+// ring is 4 tiles deep with the DMA two tiles ahead: an early wave reads tile t after its barrier t-1, which the late
+// waves pass only after retiring THEIR share of tile t (issued two iterations earlier); the slot a DMA overwrites
+// (tile t-2's) was last read by a late wave two barriers back.  Every iteration drains its own DMA (vmcnt(0)): one
+// tile of compute hides it.
+template <int HD, bool CAUSAL, int NW, bool DROP = false, bool STG = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
   using Plan = KVTilePlan<HD, 64 * NW>;
   constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
@@ -375,8 +381,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
   const unsigned dthr = DROP ? attn_drop_thr(p.drop_p) : 0u;
 
   if (ntiles > 0) plan.stage_async(lds_w, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
+  if (STG && ntiles > 1) plan.stage_async(lds_w + 2 * TILE, kp, vp, p.k_ss, p.v_ss, BN, p.Sk);
   wait_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
+  const bool late = STG && __builtin_amdgcn_readfirstlane(wid) >= 4;
+  if (late) __builtin_amdgcn_s_barrier();
 
   auto tile = [&](const char* Kl, const char* Vl, int k0, bool need_mask) {
     // ---- S^T = K Q^T for two 32-key sub-tiles ----
@@ -457,17 +466,22 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
   };
 
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles)
+    const int buf = STG ? (t & 3) : (t & 1);
+    if (STG) {
+      if (t + 2 < ntiles)
+        plan.stage_async(lds_w + ((t + 2) & 3) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 2) * BN, p.Sk);
+    } else if (t + 1 < ntiles) {
       plan.stage_async(lds_w + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
+    }
     const char* Kl = smem + buf * 2 * TILE;
     if (t < wtiles) {
       const int k0 = t * BN;
       tile(Kl, Kl + TILE, k0, (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0w + off)));
     }
-    wait_vmcnt<0>();   // this wave's share of tile t+1 has landed ...
+    wait_vmcnt<0>();   // this wave's share of tile t+1 (STG: t+2) has landed ...
     __builtin_amdgcn_s_barrier();   // ... and every wave's, and nobody reads tile t's images any more
   }
+  if (STG && !late) __builtin_amdgcn_s_barrier();   // balance the stagger
 
   // ---- epilogue: O = O^T / l, lse ----
   lsum = half_sum(lsum);
@@ -957,15 +971,15 @@ static int attn_waves(int fallback) {
     const char* e = getenv("DPH_ATTN_WAVES");
     return e ? atoi(e) : 0;
   }();
-  return (w == 4 || w == 8) ? w : fallback;
+  return (w == 4 || w == 8 || w == 9) ? w : fallback;
 }
 
-template <int HD, int NW>
+template <int HD, int NW, bool STG = false>
 static void fwd_launch_nw(const AttnParams& p, hipStream_t st) {
   const dim3 grid((unsigned)((p.Sq + 32 * NW - 1) / (32 * NW) * p.Hq * p.B));   // 1-D: xcd_block() maps it
-  const size_t lds = 2 * 2 * 64 * HD * 2;
-  if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, NW>), grid, dim3(64 * NW), lds, st, p);
-  else hipLaunchKernelGGL((attn_fwd_k<HD, false, NW>), grid, dim3(64 * NW), lds, st, p);
+  const size_t lds = (STG ? 4 : 2) * 2 * 64 * HD * 2;
+  if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, NW, false, STG>), grid, dim3(64 * NW), lds, st, p);
+  else hipLaunchKernelGGL((attn_fwd_k<HD, false, NW, false, STG>), grid, dim3(64 * NW), lds, st, p);
 }
 
 template <int HD>
@@ -979,6 +993,7 @@ static void fwd_launch(const AttnParams& p, hipStream_t st) {
   }
   if constexpr (HD >= 64) {   // a 64-key tile of HD = 32 has fewer 16-B chunks than 8 waves have lanes
     if (attn_waves(4) == 8) return fwd_launch_nw<HD, 8>(p, st);
+    if (attn_waves(4) == 9) return fwd_launch_nw<HD, 8, true>(p, st);   // 8 waves, staggered
   }
   fwd_launch_nw<HD, 4>(p, st);
 }

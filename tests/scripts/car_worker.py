@@ -72,7 +72,7 @@ def engine_routed(rank, world):
         fails.append(f"engine: {n0} direct-peer calls without a recorded crossover")
     if not (0 < n1 < 3 * nb):
         fails.append(f"engine: {n1} direct-peer calls for {nb} buckets x 3 steps (want some, not all)")
-    if not torch.allclose(p0, p1, atol=1e-6, rtol=1e-5):
+    if not torch.allclose(p0, p1, atol=2e-5, rtol=1e-4):   # sum order differs (AdamW normalises tiny grad diffs)
         fails.append(f"engine: params differ by {(p0 - p1).abs().max().item()}")
     got = [None] * world
     dist.all_gather_object(got, p1)

@@ -234,14 +234,16 @@ def test_flash_attention_long_sequence(dph_native):
     assert rel_err(q.grad, qr.grad) < 3e-2 and rel_err(k.grad, kr.grad) < 3e-2 and rel_err(v.grad, vr.grad) < 3e-2
 
 
-def test_flash_attention_eight_wave_variant(dph_native):
-    """The opt-in 8-wave workgroups (DPH_ATTN_WAVES=8, read once per process) in a child process."""
+@pytest.mark.parametrize("waves", ["8", "9"])
+def test_flash_attention_eight_wave_variant(dph_native, waves):
+    """The opt-in 8-wave workgroups (DPH_ATTN_WAVES=8; 9 = 8 waves with the staggered forward), read once per
+    process, in a child process."""
     import os
     import subprocess
     import sys
 
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "attn_check.py")
-    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_ATTN_WAVES="8"), capture_output=True,
+    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_ATTN_WAVES=waves), capture_output=True,
                        text=True, timeout=100)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
     assert '"ok": true' in p.stdout
