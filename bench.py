@@ -52,10 +52,10 @@ def parse(argv=None):
     ap.add_argument("--arch", default="resnet50", help="resnet-fsdp layout: ResNet depth")
     ap.add_argument("--seq-len", type=int, default=4096)
     ap.add_argument("--image-size", type=int, default=224)
-    ap.add_argument("--unet-precision", choices=["bf16", "bf16-autocast", "fp32"], default="bf16-autocast",
-                    help="unet-ddp layout: bf16 autocast over fp32 weights (default: 911 vs 795 samples/s for the "
-                         "engine's bf16 parameters, profiles/r4/tp_pp/unet_*.log), bf16 parameters + fp32 master "
-                         "weights in the engine, or the reference's fp32")
+    ap.add_argument("--unet-precision", choices=["bf16", "bf16-autocast", "fp32"], default="bf16",
+                    help="unet-ddp layout: bf16 parameters / activations / gradients with fp32 master weights in the "
+                         "engine (default: 834 / 927 vs 796 / 799 samples/s for bf16 autocast over fp32 weights in "
+                         "alternating runs on one box, profiles/r4/unet/), or the reference's fp32")
     ap.add_argument("--micro-batch", type=int, default=None,
                     help="sequences (images) per GPU / per dp replica per step; default 8 (dp, tp, hybrid), 16 (pp), "
                          "256 (resnet-fsdp).  8 x 4096 tokens: ~249 GB peak on one 288 GB MI355X")
