@@ -66,8 +66,11 @@ __device__ __forceinline__ float nt_sigmoid(float x) { return 1.f / (1.f + __exp
 // XOR-swizzled by the row, conflict-free 8-B writes from the accumulators), then whole 16-B row segments: one vector
 // load per operand and one store per output (DSWIGLU: x13's gate / up in, d13's dgate / dup out) instead of 8-B
 // accesses at 16 rows per instruction.  Same rounding and math as the register epilogue, so bitwise-equal output.
-template <int MODE, int LOOK, bool LEPI = false>
+// RAG (LEPI only): ragged N / H and K as in gemm_nt32_k below -- clamped weight rows, a zero-filled partial last K-tile
+// by range-checked buffer DMA, epilogue stores masked to whole 8-column segments below N.
+template <int MODE, int LOOK, bool LEPI = false, bool RAG = false>
 __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
+  static_assert(!RAG || LEPI, "ragged edges need the LDS epilogue");
   constexpr int VMC = LOOK ? 6 : 8;
   __shared__ __attribute__((aligned(1024))) char lds[2 * BUFB];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -92,36 +95,53 @@ __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
   }
 
   // ---- per-lane LDS-DMA source offsets (bytes, relative to the quarter's row-0 pointer at k-tile 0) ----
-  unsigned voff[4][2];
+  const int nk = RAG ? (p.K + NBK - 1) / NBK : p.K / NBK;
+  unsigned voff[4][2], vtail[4][2];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = i * NNT + tid, rho = c >> 3, kc = (c & 7) ^ ((rho >> 1) & 7);
-      int row;
+      int64_t row;
       if (q < 2) row = 128 * (rho >> 6) + (rho & 63);            // Q_A1's base pointer carries the +64
       else if (MODE == kNtSwiglu) row = rho;
       else row = 64 * (rho >> 5) + (rho & 31);                    // Q_B1's base pointer carries the +32
+      if constexpr (RAG) {   // weight quarters: absolute rows from the operand's base, clamped to the last valid one
+        if (q >= 2) {
+          const int64_t nb = q == Q_B0 ? nbase0 : nbase1;
+          int64_t lim;
+          if constexpr (MODE == kNtSwiglu) lim = q == Q_B0 ? p.H : 2 * (int64_t)p.H;
+          else lim = p.N;
+          row = min(nb + row, lim - 1);
+        }
+      }
       const int64_t ld = q < 2 ? p.lda : p.ldb;
       voff[q][i] = (unsigned)(row * ld * 2 + kc * 16);
+      vtail[q][i] = ((nk - 1) * NBK + kc * 8 < p.K) ? voff[q][i] : 0x80000000u;
     }
   const char* qptr[4];
   const bf16* Ap = reinterpret_cast<const bf16*>(p.A);
   const bf16* Bp = reinterpret_cast<const bf16*>(p.B);
   qptr[Q_A0] = reinterpret_cast<const char*>(Ap + (int64_t)m0 * p.lda);
   qptr[Q_A1] = reinterpret_cast<const char*>(Ap + (int64_t)(m0 + 64) * p.lda);
-  qptr[Q_B0] = reinterpret_cast<const char*>(Bp + nbase0 * p.ldb);
-  qptr[Q_B1] = reinterpret_cast<const char*>(Bp + nbase1 * p.ldb);
+  qptr[Q_B0] = reinterpret_cast<const char*>(RAG ? Bp : Bp + nbase0 * p.ldb);
+  qptr[Q_B1] = reinterpret_cast<const char*>(RAG ? Bp : Bp + nbase1 * p.ldb);
   const unsigned lds_w = lds_addr(lds + wid * 1024);
-  const int nk = p.K / NBK;
+  const bool ktail = RAG && (p.K % NBK) != 0;
 
   auto dma = [&](auto QI, int kt, auto BI) {
     constexpr int Q = decltype(QI)::value, BUF = decltype(BI)::value;
     const int ktc = min(kt, nk - 1);   // past the end: re-load the last tile into a slot nobody reads again
     const char* src = qptr[Q] + (int64_t)ktc * (NBK * 2);
     const unsigned d = lds_w + BUF * BUFB + Q * QB;
-    lds_dma16(src, voff[Q][0], d);
-    lds_dma16(src, voff[Q][1], d + NNT * 16);
+    if (RAG && ktail && ktc == nk - 1) {   // wave-uniform: the partial last K-tile, zero-filled past K
+      const dph_rsrc rs = make_rsrc(src, 0x7fffffffu);
+      lds_dma16_buf(rs, vtail[Q][0], d);
+      lds_dma16_buf(rs, vtail[Q][1], d + NNT * 16);
+    } else {
+      lds_dma16(src, voff[Q][0], d);
+      lds_dma16(src, voff[Q][1], d + NNT * 16);
+    }
   };
 
   // ---- per-lane fragment read offsets: row r16 of a 16-row block, logical chunk 4 s + kq ----
@@ -276,6 +296,7 @@ __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
     __syncthreads();
     const int c = tid & 15;                       // gate chunk c (units 8c ..) and its up chunk 16 + c
     const int64_t u0 = (int64_t)tn * 128 + c * 8;
+    if (RAG && u0 >= p.H) return;                 // whole 8-unit segment past H (H % 8 == 0)
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int row = (tid >> 4) + 32 * k;
@@ -326,6 +347,7 @@ __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
     __syncthreads();
     const int c = tid & 31;                       // this thread's 16-B column chunk (512 threads, 32 per row)
     const int64_t n0c = (int64_t)tn * NBN + c * 8;
+    if (RAG && n0c >= p.N) return;
     constexpr int BATCH = 4;
 #pragma unroll
     for (int k0 = 0; k0 < 16; k0 += BATCH) {      // rows tid / 32 + 16 k
@@ -795,7 +817,22 @@ void gemm_nt(int mode, const GemmNtParams& prm, hipStream_t st) {
   const int var = gemm_nt_variant();
   const bool look = (var & 1) != 0;
   const bool rag = gemm_nt_ragged(mode, p.N, p.K);
-  if ((var & 2) || rag) {   // 32x32x16 kernel (ragged shapes always)
+  if (rag && !(var & 2)) {   // ragged shapes on the 16x16x32 kernel's edge tiles (LDS epilogue)
+#define DPH_NT16R(MD)                                                                             \
+  do {                                                                                            \
+    if (look) hipLaunchKernelGGL((gemm_nt_k<MD, 1, true, true>), grid, block, 0, st, p);         \
+    else hipLaunchKernelGGL((gemm_nt_k<MD, 0, true, true>), grid, block, 0, st, p);              \
+  } while (0)
+    switch (mode) {
+      case kNtSwiglu: DPH_NT16R(kNtSwiglu); break;
+      case kNtDswiglu: DPH_NT16R(kNtDswiglu); break;
+      case kNtRope: DPH_NT16R(kNtRope); break;
+      default: DPH_NT16R(kNtStore); break;
+    }
+#undef DPH_NT16R
+    return;
+  }
+  if (var & 2) {   // 32x32x16 kernel
 #define DPH_NT32(MD)                                                                                      \
   do {                                                                                                    \
     if (rag) {                                                                                            \

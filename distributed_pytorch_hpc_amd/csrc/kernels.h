@@ -145,7 +145,7 @@ bool gemm_nt_supported(int mode, int64_t M, int64_t N, int64_t K);
 bool gemm_nt_ragged(int mode, int64_t N, int64_t K);
 void gemm_nt(int mode, const GemmNtParams& p, hipStream_t stream);
 // pipeline variant: bit 0 = lookahead B0 reads (8/4/8/0 fragment reads per phase instead of 12/4/8/0), bit 1 = the
-// v_mfma_f32_32x32x16_bf16 kernel (gemm_nt32_k) instead of 16x16x32 (gemm_nt_k).  Ragged shapes always take bit 1.
+// v_mfma_f32_32x32x16_bf16 kernel (gemm_nt32_k) instead of 16x16x32 (gemm_nt_k); both take ragged shapes.
 constexpr int kGemmNtDefaultVariant = 1;   // 0.92-1.02x hipBLASLt vs 0.91-1.00x for 0 (profiles/r3/rejected/gemm_nt_2phase_*)
 int gemm_nt_variant();
 void gemm_nt_set_variant(int v);

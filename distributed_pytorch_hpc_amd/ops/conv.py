@@ -16,9 +16,10 @@ with the spatially flipped, channel-transposed weight; padding taps are zero-fil
 epilogue emits the following BatchNorm's statistics or adds a bias): 440-810 TFLOP/s vs MIOpen's 370-780 on the
 ResNet-50 / SimpleUNet shapes (profiles/r3/conv3_bench_oob.json), on by default (``DPH_CONV3X3=0``: MIOpen;
 ``DPH_CONV3_WM=2|4`` picks the 4- or 8-wave tile).  The
-weight gradient runs on MIOpen by default (318-491 TFLOP/s vs 241-357 for the LDS-DMA split-pixel kernel and 302-324 for
-the older register-staged one, profiles/r3/conv3_bench_c3w_wgrad.json / _tsw_wgrad.json); ``DPH_CONV3_WGRAD=dph``
-selects the kernel.  Round 2's register-staged forward (``DPH_CONV3_KERNEL=ts``) measured 0.51-0.63 ms vs MIOpen's
+weight gradient of the ResNet ``Conv3x3`` runs on MIOpen by default (318-491 TFLOP/s vs 241-357 for the LDS-DMA
+split-pixel kernel and 302-324 for the older register-staged one, profiles/r3/conv3_bench_c3w_wgrad.json /
+_tsw_wgrad.json; ResNet-50 in-step -2.4 % with the kernel); the SimpleUNet's biased 3x3 convolutions (``BiasConv2d``)
+take the kernel (+19 % in-step, profiles/r4/conv_wgrad/).  ``DPH_CONV3_WGRAD=miopen|dph`` overrides both.  Round 2's register-staged forward (``DPH_CONV3_KERNEL=ts``) measured 0.51-0.63 ms vs MIOpen's
 0.38-0.53 ms per shape and stayed off.
 """
 from __future__ import annotations
@@ -182,7 +183,13 @@ class _Conv1x1Fn(torch.autograd.Function):
         return dx, gw, None, None
 
 
-_CONV3_WGRAD = os.environ.get("DPH_CONV3_WGRAD", "miopen")
+def _conv3_wgrad(default: str) -> str:
+    """Which kernel runs a 3x3 weight gradient: DPH_CONV3_WGRAD (miopen | dph) overrides the module's measured default.
+    Conv3x3 (ResNet bottlenecks) keeps MIOpen: ResNet-50 FSDP bf16 B=256 10 068 / 10 079 img/s vs 9 835 / 9 833 with
+    the split-pixel kernel; BiasConv2d (SimpleUNet) takes the kernel: 1 005 / 984 vs 848 / 826 samples/s eager, the
+    UNet step being host-bound and the MIOpen call the heavier launch (interleaved A/B on one MI355X each,
+    profiles/r4/conv_wgrad/)."""
+    return os.environ.get("DPH_CONV3_WGRAD", default)
 # stride-1 3x3 convolutions on csrc/conv3x3.hip by default: ResNet-50 FSDP bf16 B=256 9 472 / 9 513 vs 9 258 / 9 278
 # img/s on MIOpen (interleaved A/B on one MI355X, profiles/r3/ab_conv3x3/); DPH_CONV3X3=0 = MIOpen
 _CONV3X3_DEFAULT = "1"
@@ -205,7 +212,7 @@ def _main_grad_cl(w: torch.Tensor, cout: int, k: int):
 
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stats_slot=None, bias=None):
+    def forward(ctx, x, w, stats_slot=None, bias=None, wgrad="miopen"):
         wdtype = w.dtype
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -222,6 +229,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         else:
             y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W)
         ctx.has_bias = bias is not None
+        ctx.wgrad = wgrad
         ctx.save_for_backward(x2, wb)
         ctx.shape, ctx.wdtype, ctx.param = (B, C, H, W), wdtype, w
         return y2.view(B, H, W, cout).permute(0, 3, 1, 2)
@@ -240,9 +248,9 @@ class _Conv3x3Fn(torch.autograd.Function):
             else:
                 wf = wb.flip(2, 3).permute(1, 2, 3, 0).reshape(C, 9 * cout)
             dx = _lib.ops().ts_gemm_nt(dy2, wf, H, W).view(B, H, W, C).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1] and _CONV3_WGRAD != "dph":
+        if ctx.needs_input_grad[1] and ctx.wgrad != "dph":
             # weight gradient on MIOpen: 1.0-1.5x the split-pixel kernel on the ResNet-50 shapes
-            # (profiles/r3/conv3_bench_oob.json: 318-485 vs 302-321 TFLOP/s); DPH_CONV3_WGRAD=dph selects the kernel
+            # (profiles/r3/conv3_bench_oob.json: 318-485 vs 302-321 TFLOP/s); see _conv3_wgrad
             x4 = x2.view(B, H, W, C).permute(0, 3, 1, 2)
             dy4 = dy2.view(B, H, W, cout).permute(0, 3, 1, 2)
             gw = torch.ops.aten.convolution_backward(dy4, x4, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
@@ -261,7 +269,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         db = None
         if ctx.has_bias and ctx.needs_input_grad[3]:
             db = _lib.ops().channel_sum(dy2, torch.float32)
-        return dx, gw, None, db
+        return dx, gw, None, db, None
 
 
 def conv3x3_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -283,7 +291,8 @@ class Conv3x3(nn.Conv2d):
     def forward(self, x, stats_slot: StatsSlot | None = None):
         if conv3x3_native_ok(x, self.weight):
             _lib.require()
-            return _Conv3x3Fn.apply(x, self.weight, stats_slot if _conv3_stats_ok() else None)
+            return _Conv3x3Fn.apply(x, self.weight, stats_slot if _conv3_stats_ok() else None, None,
+                                    _conv3_wgrad("miopen"))
         return F.conv2d(x, self.weight, padding=1)
 
 
@@ -373,7 +382,7 @@ class BiasConv2d(nn.Conv2d):
         if _bias_conv3x3_ok(self, x):
             _lib.require()
             b = self.bias if self.bias.dtype == torch.float32 else self.bias.float()
-            return _Conv3x3Fn.apply(x, self.weight, None, b)
+            return _Conv3x3Fn.apply(x, self.weight, None, b, _conv3_wgrad("dph"))
         if _bias_conv_ok(self, x):
             return _bias_conv(self, x, False, (0, 0))
         return super().forward(x)

@@ -24,7 +24,7 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
-from .linear import _dgrad, weight_grad
+from .linear import weight_grad
 
 
 def _ws(group) -> int:
@@ -69,24 +69,43 @@ def _seq_major(t: torch.Tensor) -> torch.Tensor:
     return t.permute(2, 1, 0, 3, 4).reshape(B, P * k * m, X)
 
 
+def _k_major(w: torch.Tensor, transpose_w: bool) -> torch.Tensor:
+    """The K-contiguous [N, K] operand of ``x @ op(w)`` (op(w) = w^T: w itself; op(w) = w: its transpose, made ONCE per
+    call -- HIP tile transpose on the GPU -- instead of once per micro-GEMM; hipBLASLt prefers this layout,
+    parallel/linear.py _dgrad)."""
+    if transpose_w:
+        return w
+    if w.is_cuda and w.dtype == torch.bfloat16 and w.dim() == 2 and w.is_contiguous() and w.shape[0] % 8 == 0 \
+            and w.shape[1] % 8 == 0:
+        from ..ops import _lib
+
+        if not _lib.reference_mode():
+            return _lib.ops().transpose2d(w)
+    return w.t().contiguous()
+
+
 def _ag_matmul(x: torch.Tensor, w: torch.Tensor, group, k: int, transpose_w: bool):
     """AG(x) @ op(w) with k pipelined micro all-gathers; x [B, Sl, D].  Returns (y [B, S, N], gathered [k,P,B,m,D]).
 
-    The micro all-gathers land in slots of ONE chunk-major buffer (kept for the weight gradient: no stack), and each
-    micro-GEMM's [P, B, m, N] result is copied once into its rank-major sequence positions of y (one copy, overlapping
-    the next micro all-gather; no stack + permute)."""
+    The micro all-gathers land in slots of ONE chunk-major buffer (kept for the weight gradient: no stack).  With one
+    sequence per rank (B = 1) micro-GEMM i writes its [P, m, N] result straight into its rank-major sequence rows of
+    y -- one strided-batched GEMM whose output batch stride is k m N, no copy; otherwise its [P, B, m, N] result is
+    copied once into place (overlapping the next micro all-gather)."""
     B, Sl, D = x.shape
     P = _ws(group)
     m = Sl // k
     xg = torch.empty((k, P * B, m, D), dtype=x.dtype, device=x.device)
     pend = [_ag_async(x[:, i * m:(i + 1) * m].contiguous(), group, xg[i]) for i in range(k)]
-    N = w.shape[0] if transpose_w else w.shape[1]
+    wk = _k_major(w, transpose_w)                                          # [N, D]
+    N = wk.shape[0]
     y = torch.empty((B, P * Sl, N), dtype=x.dtype, device=x.device)
     yv = y.view(B, P, k, m, N)
     for i, (g, work) in enumerate(pend):
         work.wait()
-        yi = torch.matmul(g, w.t()) if transpose_w else _dgrad(g, w)         # [P, B, m, N]
-        yv[:, :, i].copy_(yi.permute(1, 0, 2, 3))
+        if B == 1:
+            torch.bmm(g.view(P, m, D), wk.t().expand(P, D, N), out=yv[0, :, i])
+        else:
+            yv[:, :, i].copy_(torch.matmul(g, wk.t()).permute(1, 0, 2, 3))   # [P, B, m, N] -> sequence order
     return y, xg.view(k, P, B, m, D)
 
 
@@ -95,11 +114,12 @@ def _matmul_rs(x_cm: torch.Tensor, w: torch.Tensor, group, transpose_w: bool) ->
     chunk-major.  Returns [B, Sl, N] (this rank's sequence shard); with one sequence per rank (B = 1) the micro
     reduce-scatters write straight into their slice of it."""
     k, _, B, m, _ = x_cm.shape
-    N = w.shape[0] if transpose_w else w.shape[1]
+    wk = _k_major(w, transpose_w)
+    N = wk.shape[0]
     y = torch.empty((B, k * m, N), dtype=x_cm.dtype, device=x_cm.device) if B == 1 else None
     pend = []
     for i in range(k):
-        part = torch.matmul(x_cm[i], w.t()) if transpose_w else _dgrad(x_cm[i], w)
+        part = torch.matmul(x_cm[i], wk.t())
         pend.append(_rs_async(part, group, y[:, i * m:(i + 1) * m] if y is not None else None))
     outs = []
     for o, work in pend:

@@ -173,7 +173,7 @@ def test_gemm_nt_epilogue_forms_bitwise(dph_native):
     assert outs[0] == outs[1]
 
 
-# ---- the 32x32x16 kernel (variant bit 1) and its ragged edge tiles (tensor-parallel shard shapes) ----
+# ---- both MFMA shapes (variants 0/1: 16x16x32, 2/3: 32x32x16) on ragged edge tiles (tensor-parallel shards) ----
 def _with_variant(dph_native, v, fn):
     try:
         dph_native.gemm_nt_variant_(v)
@@ -187,7 +187,7 @@ def _check_store(c, ref):
     assert ((c.float() - ref).abs() <= 1e-2 * ref.abs() + 2e-2 * ref.abs().mean()).all()
 
 
-@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 192), (768, 512, 320), (256, 1024, 4096),
                                    # ragged: tp8 / tp4 shards of Llama-2-7B (w13 2752, head 4000, w2's K 1376),
                                    # a partial single K-tile, the smallest N
@@ -208,7 +208,7 @@ def test_gemm_nt32_asymmetric_identity(dph_native):
     assert torch.equal(c, b.t().contiguous())
 
 
-@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,H,K", [(256, 128, 64), (512, 384, 256), (256, 1376, 256), (256, 2752, 136),
                                    (256, 40, 64)])
 def test_gemm_nt32_swiglu(dph_native, variant, M, H, K):
@@ -222,7 +222,7 @@ def test_gemm_nt32_swiglu(dph_native, variant, M, H, K):
     assert torch.equal(h, dph_native.swiglu_fwd(x13))
 
 
-@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,H,K", [(256, 256, 64), (512, 768, 128), (256, 1376, 512), (256, 2752, 200)])
 def test_gemm_nt32_dswiglu(dph_native, variant, M, H, K):
     dy, w2t = _rnd(M, K, seed=27), _rnd(H, K, seed=28, scale=0.5)
@@ -236,7 +236,7 @@ def test_gemm_nt32_dswiglu(dph_native, variant, M, H, K):
     assert rel_err(d13, ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("S,hd,heads,K", [(256, 64, 4, 256), (512, 128, 2, 256), (256, 128, 4, 1376)])
 def test_gemm_nt32_rope(dph_native, variant, S, hd, heads, K):
     from distributed_pytorch_hpc_amd.models.llama2 import rope_tables
