@@ -36,6 +36,7 @@ CATEGORIES = [
     ("rccl", re.compile(r"ncclDevKernel|rccl|nccl", re.I)),
     ("batchnorm(dph)", re.compile(r"bn_(stats|apply|finalize|merge|bwd)")),
     ("conv1x1(dph)", re.compile(r"ts_nt_k|ts_tn_k|ts_reduce|conv1x1")),
+    ("conv3x3(dph)", re.compile(r"conv3_k|c3w_k|conv3x3|conv3_dgrad_w|conv_s2")),
     ("copy/fill", re.compile(r"copy|fill|FillFunctor|direct_copy", re.I)),
     ("elementwise(aten)", re.compile(r"elementwise|vectorized|reduce_kernel", re.I)),
 ]
@@ -76,7 +77,7 @@ def load_events(path: str):
     return ev
 
 
-def summarise(events, last_ms: float | None = None, steps: int = 1):
+def summarise(events, last_ms: float | None = None, steps: int = 1, top: int = 80):
     if not events:
         raise SystemExit("no kernel events found")
     events.sort(key=lambda e: e[1])
@@ -93,7 +94,10 @@ def summarise(events, last_ms: float | None = None, steps: int = 1):
         per_k[k][1] += d
         per_c[category(name)] += d
     busy = sum(per_c.values())
+    launches = sum(c for c, _ in per_k.values())
     return {
+        "launches_per_step": round(launches / steps, 2),
+        "idle_pct": round(100 * max(0.0, span - busy) / span, 2) if span > 0 else 0.0,
         "steps": steps,
         "span_ms_per_step": round(span / steps, 3),
         "kernel_busy_ms_per_step": round(busy / steps, 3),
@@ -101,7 +105,7 @@ def summarise(events, last_ms: float | None = None, steps: int = 1):
         "top_kernels": [
             {"name": k, "calls_per_step": round(c / steps, 2), "ms_per_step": round(t / steps, 3),
              "pct": round(100 * t / busy, 2)}
-            for k, (c, t) in sorted(per_k.items(), key=lambda x: -x[1][1])[:40]
+            for k, (c, t) in sorted(per_k.items(), key=lambda x: -x[1][1])[:top]
         ],
     }
 
@@ -112,13 +116,15 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=1, help="divide totals by this many steps")
     ap.add_argument("--last-ms", type=float, default=None, help="only the last N ms of GPU activity")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--top", type=int, default=25, help="kernels printed (the JSON keeps up to 80)")
     args = ap.parse_args(argv)
     out = summarise(load_events(args.path), args.last_ms, args.steps)
-    print(f"span/step {out['span_ms_per_step']} ms, kernel busy/step {out['kernel_busy_ms_per_step']} ms")
+    print(f"span/step {out['span_ms_per_step']} ms, kernel busy/step {out['kernel_busy_ms_per_step']} ms, "
+          f"idle {out['idle_pct']} %, {out['launches_per_step']} launches/step")
     for c, v in out["categories_ms_per_step"].items():
         print(f"  {c:22s} {v:10.3f} ms")
     print("top kernels:")
-    for k in out["top_kernels"][:25]:
+    for k in out["top_kernels"][:args.top]:
         print(f"  {k['ms_per_step']:9.3f} ms {k['pct']:6.2f}% x{k['calls_per_step']:<7} {k['name'][:90]}")
     if args.json:
         with open(args.json, "w") as fh:

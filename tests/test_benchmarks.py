@@ -65,3 +65,19 @@ def test_torch_baseline_comparator_gloo(tmp_path):
     rec = json.loads((tmp_path / "t.json").read_text())
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "torch-ddp2" and rec["value"] > 0
     assert sum(ln.startswith("{") for ln in out.splitlines()) == 1   # rank 0 only
+
+
+def test_prof_summary_idle_launches_categories():
+    """benchmarks/prof_summary.py: per-category time, launches per step and idle share of the span."""
+    sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+    import prof_summary
+
+    ms = 1_000_000
+    ev = [("void dph::conv3_k<64, 3, 2, false>(...)", 0, 2 * ms),          # 2 ms
+          ("igemm_wrw_gtcx35_nhwc_bf16", 3 * ms, 4 * ms),                  # 1 ms after 1 ms idle
+          ("dph::bn_apply_k<...>", 4 * ms, 5 * ms)]
+    out = prof_summary.summarise(ev, steps=1)
+    assert out["launches_per_step"] == 3
+    assert abs(out["idle_pct"] - 20.0) < 1e-6
+    cats = out["categories_ms_per_step"]
+    assert cats["conv3x3(dph)"] == 2.0 and cats["conv(miopen/ck)"] == 1.0 and cats["batchnorm(dph)"] == 1.0
