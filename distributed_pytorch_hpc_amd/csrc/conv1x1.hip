@@ -392,10 +392,12 @@ __device__ __forceinline__ void fdivmod(int r, int d, float inv, int& q, int& m)
   if (m >= d) { ++q; m -= d; }
 }
 
-template <int TCO>
+// GEN: the X rows are gathered by kernels.h ConvGeo (strided convolutions): output row r = (n, oy, ox) over Ho x Wo,
+// tap t's source pixel (n Hs + sy oy + by + tdy[t]) Ws + sx ox + bx + tdx[t] of the [src_rows, Cin] input.
+template <int TCO, bool GEN = false>
 __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                 float* __restrict__ P, int M, int N, int K, int64_t lda,
-                                                int64_t ldb, int chunk, int H, int W, int Cin) {
+                                                int64_t ldb, int chunk, int H, int W, int Cin, ConvGeo geo) {
   constexpr int AS = TCO / 64;                       // dY slabs per step
   constexpr int STG = (AS + C3W_SLABS) * C3W_SLAB;   // one stage
   constexpr int PCS = (AS + C3W_SLABS) * 8 / 4;      // 1-KB DMA pieces per wave per step
@@ -410,9 +412,10 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
   const int n0 = (tile / tk) * TCO, k0 = (tile % tk) * C3W_TK;
   const int mbeg = s * chunk, mend = min(M, mbeg + chunk);
 
-  const float invW = 1.f / (float)W, invH = 1.f / (float)H;
+  const int Wr = GEN ? geo.Wo : W, Hr = GEN ? geo.Ho : H;   // the row space's grid
+  const float invW = 1.f / (float)Wr, invH = 1.f / (float)Hr;
   const dph_rsrc ra = make_rsrc(A, (unsigned)((int64_t)M * lda * 2));
-  const dph_rsrc rb = make_rsrc(B, (unsigned)((int64_t)M * ldb * 2));
+  const dph_rsrc rb = make_rsrc(B, (unsigned)((GEN ? geo.src_rows : (int64_t)M) * ldb * 2));
   const unsigned lds0 = lds_addr(smem);
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
   // DMA lanes: piece i (of AS*8 + 24 per step) = slab i / 8, rows 8 (i % 8) + prow, LDS slot lane % 8
@@ -422,8 +425,19 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
   for (int sb = 0; sb < C3W_SLABS; ++sb) {
     const int kk = k0 + sb * 64, tap = kk / Cin;
     bcb[sb] = kk - tap * Cin;
-    bdy[sb] = tap / 3 - 1;
-    bdx[sb] = tap - (tap / 3) * 3 - 1;
+    if constexpr (GEN) {   // tap table lookup by selects (tap is uniform over the workgroup)
+      bdy[sb] = geo.tdy[0];
+      bdx[sb] = geo.tdx[0];
+#pragma unroll
+      for (int t = 1; t < 9; ++t)
+        if (tap == t) {
+          bdy[sb] = geo.tdy[t];
+          bdx[sb] = geo.tdx[t];
+        }
+    } else {
+      bdy[sb] = tap / 3 - 1;
+      bdx[sb] = tap - (tap / 3) * 3 - 1;
+    }
   }
   auto issue = [&](int m, int stage) {
 #pragma unroll
@@ -438,11 +452,19 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
       } else {
         const int sb = slab - AS;
         int yq, xw, yh, nq;
-        fdivmod(r, W, invW, yq, xw);                 // pixel -> (image row, column), then image row -> y
-        fdivmod(yq, H, invH, nq, yh);
-        const bool ok = r < mend && (unsigned)(yh + bdy[sb]) < (unsigned)H && (unsigned)(xw + bdx[sb]) < (unsigned)W;
-        const unsigned off =
-            (unsigned)(((int64_t)(r + bdy[sb] * W + bdx[sb]) * ldb + bcb[sb] + sch * 8) * 2);
+        fdivmod(r, Wr, invW, yq, xw);                // pixel -> (image row, column), then image row -> y
+        fdivmod(yq, Hr, invH, nq, yh);
+        bool ok;
+        int64_t src;
+        if constexpr (GEN) {
+          const int ay = geo.sy * yh + geo.by + bdy[sb], ax = geo.sx * xw + geo.bx + bdx[sb];
+          ok = r < mend && (unsigned)ay < (unsigned)geo.Hs && (unsigned)ax < (unsigned)geo.Ws;
+          src = ((int64_t)nq * geo.Hs + ay) * geo.Ws + ax;
+        } else {
+          ok = r < mend && (unsigned)(yh + bdy[sb]) < (unsigned)H && (unsigned)(xw + bdx[sb]) < (unsigned)W;
+          src = r + bdy[sb] * W + bdx[sb];
+        }
+        const unsigned off = (unsigned)((src * ldb + bcb[sb] + sch * 8) * 2);
         lds_dma16_buf(rb, ok ? off : 0x80000000u, dst);
       }
     }
@@ -661,6 +683,18 @@ int c3w_splits(int64_t M, int64_t N, int64_t K) {
   return (int)s;
 }
 
+static void ts_reduce(const float* partial, void* C, int64_t nk, int nsplit, int out_dtype, bool accumulate,
+                      hipStream_t st) {
+  const dim3 grid((int)cdiv(nk / 4, 16));
+  if (out_dtype == kBF16) {
+    if (accumulate) hipLaunchKernelGGL((ts_reduce_k<bf16, true>), grid, dim3(256), 0, st, partial, (bf16*)C, nk, nsplit);
+    else hipLaunchKernelGGL((ts_reduce_k<bf16, false>), grid, dim3(256), 0, st, partial, (bf16*)C, nk, nsplit);
+  } else {
+    if (accumulate) hipLaunchKernelGGL((ts_reduce_k<float, true>), grid, dim3(256), 0, st, partial, (float*)C, nk, nsplit);
+    else hipLaunchKernelGGL((ts_reduce_k<float, false>), grid, dim3(256), 0, st, partial, (float*)C, nk, nsplit);
+  }
+}
+
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
                 int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t st, int H, int W,
                 const float* pro_ss) {
@@ -672,11 +706,11 @@ void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M
     if (N % 128 == 0)
       hipLaunchKernelGGL((c3w_k<128>), dim3((int)((N / 128) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,
                          (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, H, W,
-                         cin);
+                         cin, ConvGeo{});
     else
       hipLaunchKernelGGL((c3w_k<64>), dim3((int)((N / 64) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,
                          (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, H, W,
-                         cin);
+                         cin, ConvGeo{});
   } else if (pro_ss != nullptr && H == 0) {
     hipLaunchKernelGGL((ts_tn_k<false, true>), dim3((int)(tiles * nsplit)), dim3(256), 0, st, (const bf16*)A,
                        (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0, 0, pro_ss);
@@ -686,15 +720,30 @@ void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M
   else
     hipLaunchKernelGGL((ts_tn_k<false>), dim3((int)(tiles * nsplit)), dim3(256), 0, st, (const bf16*)A,
                        (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0, 0);
-  const int64_t nk = N * K;
-  const dim3 grid((int)cdiv(nk / 4, 16));
-  if (out_dtype == kBF16) {
-    if (accumulate) hipLaunchKernelGGL((ts_reduce_k<bf16, true>), grid, dim3(256), 0, st, partial, (bf16*)C, nk, nsplit);
-    else hipLaunchKernelGGL((ts_reduce_k<bf16, false>), grid, dim3(256), 0, st, partial, (bf16*)C, nk, nsplit);
-  } else {
-    if (accumulate) hipLaunchKernelGGL((ts_reduce_k<float, true>), grid, dim3(256), 0, st, partial, (float*)C, nk, nsplit);
-    else hipLaunchKernelGGL((ts_reduce_k<float, false>), grid, dim3(256), 0, st, partial, (float*)C, nk, nsplit);
-  }
+  ts_reduce(partial, C, N * K, nsplit, out_dtype, accumulate, st);
+}
+
+bool c3wg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g) {
+  // c3w_k tiles: 192 k' (three 64-channel slabs of one tap each); fp32 row division exact below 2^24 rows
+  return g.ntaps >= 1 && g.ntaps <= 9 && N % 64 == 0 && K % C3W_TK == 0 && K % g.ntaps == 0 &&
+         (K / g.ntaps) % 64 == 0 && M * lda * 2 < (int64_t(1) << 31) && g.src_rows * ldb * 2 < (int64_t(1) << 31) &&
+         M < (int64_t(1) << 24);
+}
+
+void ts_gemm_tn_geo(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
+                    int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, const ConvGeo& g,
+                    hipStream_t st) {
+  int64_t chunk = cdiv(cdiv(M, nsplit), 64) * 64;
+  const int cin = (int)(K / g.ntaps);
+  if (N % 128 == 0)
+    hipLaunchKernelGGL((c3w_k<128, true>), dim3((int)((N / 128) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,
+                       (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0,
+                       cin, g);
+  else
+    hipLaunchKernelGGL((c3w_k<64, true>), dim3((int)((N / 64) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,
+                       (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0,
+                       cin, g);
+  ts_reduce(partial, C, N * K, nsplit, out_dtype, accumulate, st);
 }
 
 }  // namespace dph

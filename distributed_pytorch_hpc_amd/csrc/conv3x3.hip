@@ -47,13 +47,16 @@ __device__ __forceinline__ int c3_off(int r, int c) { return r * C3_ROWB + ((c ^
 // tile of 8 waves (one workgroup per CU, 3-stage ring, the weight slab shared by twice the rows).
 // Padding taps and rows past M are zero-filled by the DMA itself (buffer_load ... lds with an out-of-range offset);
 // round 3 measured that 1.0-1.2x faster than fetching the row and zeroing the fragment registers.
-template <int BN, int STAGES, int WM, bool STATS = false>
+// GEN: the gathered geometry of kernels.h ConvGeo (strided forward, the parity classes of a strided input gradient):
+// per-lane source pixels from g, the K-step's tap offsets from g's tap table, rows stored to g's destination rows.
+// GEN = false is the stride-1 3x3 path (H, W, the fixed 3x3 taps, identity stores).
+template <int BN, int STAGES, int WM, bool STATS = false, bool GEN = false>
 __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16* __restrict__ X,
                                                                    const bf16* __restrict__ B, bf16* __restrict__ C,
                                                                    int M, int N, int K, int64_t ldx, int64_t ldb,
                                                                    int64_t ldc, int H, int W, int Cin,
                                                                    float* __restrict__ stats,
-                                                                   const float* __restrict__ bias) {
+                                                                   const float* __restrict__ bias, ConvGeo g) {
   constexpr int NWV = 2 * WM, NTH = 64 * NWV, BM = 64 * WM;
   constexpr int AIMG = BM * C3_ROWB, BIMG = BN * C3_ROWB, STG = AIMG + BIMG;
   constexpr int AI = BM / 8 / NWV;         // A DMA pieces (8 rows) per wave per K-step (4)
@@ -84,9 +87,16 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16*
     const int q = wid * AI + j, r = q * 8 + prow;
     const int m = min(m0 + r, M - 1);
     arow_in[j] = m0 + r < M;
-    am[j] = m;
-    ax[j] = m % W;
-    ay[j] = (m / W) % H;
+    if constexpr (GEN) {   // output row (n, oy, ox) -> its source base pixel (sy oy + by, sx ox + bx) of image n
+      const int hw = g.Ho * g.Wo, n = m / hw, rem = m - n * hw, oy = rem / g.Wo, ox = rem - oy * g.Wo;
+      ay[j] = g.sy * oy + g.by;
+      ax[j] = g.sx * ox + g.bx;
+      am[j] = (n * g.Hs + ay[j]) * g.Ws + ax[j];
+    } else {
+      am[j] = m;
+      ax[j] = m % W;
+      ay[j] = (m / W) % H;
+    }
     ach[j] = (q & 1) ? chunk1 : chunk0;
   }
   unsigned boff[BI];
@@ -96,18 +106,32 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16*
     boff[j] = (unsigned)(((int64_t)(n0 + r) * ldb + ((q & 1) ? chunk1 : chunk0) * 8) * 2);
   }
   const unsigned lds0 = lds_addr(smem);
-  const dph_rsrc xres = make_rsrc(X, (unsigned)((int64_t)M * ldx * 2));
+  const dph_rsrc xres = make_rsrc(X, (unsigned)((GEN ? g.src_rows : (int64_t)M) * ldx * 2));
+  const int Hs = GEN ? g.Hs : H, Ws = GEN ? g.Ws : W;
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);   // the DMA destination (M0) must be provably wave-uniform
 
   auto issue = [&](int ks, int stage) {
     const int k0 = ks * C3_BK;
     const int tap = k0 / Cin, cb = k0 - tap * Cin;
-    const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+    int dy, dx;
+    if constexpr (GEN) {   // wave-uniform table lookup by selects (no dynamically indexed kernel-argument array)
+      dy = g.tdy[0];
+      dx = g.tdx[0];
+#pragma unroll
+      for (int t = 1; t < 9; ++t)
+        if (tap == t) {
+          dy = g.tdy[t];
+          dx = g.tdx[t];
+        }
+    } else {
+      dy = tap / 3 - 1;
+      dx = tap - (tap / 3) * 3 - 1;
+    }
     const unsigned sa = lds0 + stage * STG + wid_u * AI * 1024;
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
-      const bool ok = arow_in[j] && (unsigned)(ay[j] + dy) < (unsigned)H && (unsigned)(ax[j] + dx) < (unsigned)W;
-      const unsigned off = (unsigned)(((int64_t)(am[j] + dy * W + dx) * ldx + cb + ach[j] * 8) * 2);
+      const bool ok = arow_in[j] && (unsigned)(ay[j] + dy) < (unsigned)Hs && (unsigned)(ax[j] + dx) < (unsigned)Ws;
+      const unsigned off = (unsigned)(((int64_t)(am[j] + dy * Ws + dx) * ldx + cb + ach[j] * 8) * 2);
       lds_dma16_buf(xres, ok ? off : 0x80000000u, sa + j * 1024);
     }
     const unsigned sb = lds0 + stage * STG + AIMG + wid_u * BI * 1024;
@@ -188,9 +212,14 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16*
   constexpr int CPR = BN / 8;
   for (int i = threadIdx.x; i < BM * CPR; i += NTH) {
     const int row = i / CPR, ch = i % CPR;
-    if (m0 + row < M)
-      *reinterpret_cast<bf16x8*>(C + (int64_t)(m0 + row) * ldc + n0 + ch * 8) =
-          *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
+    if (m0 + row < M) {
+      int64_t drow = m0 + row;
+      if constexpr (GEN) {
+        const int m = m0 + row, hw = g.Ho * g.Wo, n = m / hw, rem = m - n * hw, oy = rem / g.Wo, ox = rem - oy * g.Wo;
+        drow = ((int64_t)n * g.Hd + g.ty * oy + g.tby) * g.Wd + g.tx * ox + g.tbx;
+      }
+      *reinterpret_cast<bf16x8*>(C + drow * ldc + n0 + ch * 8) = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
+    }
   }
   if constexpr (STATS) {
     // per 128-row block g (waves 2g, 2g+1): pass 1 column sums, pass 2 squared deviations from the block mean, of the
@@ -276,7 +305,7 @@ void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 #define DPH_C3(BN_, ST_, WM_, STATS_)                                                                            \
   hipLaunchKernelGGL((conv3_k<BN_, ST_, WM_, STATS_>), dim3(nmb * (int)(N / BN_)), dim3(128 * WM_), 0, st,    \
                      (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin,  \
-                     stats, bias)
+                     stats, bias, ConvGeo{})
   if (wm == 4) {
     if (stats) {
       if (wide) DPH_C3(128, 3, 4, true);
@@ -293,6 +322,33 @@ void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     else DPH_C3(64, 3, 2, false);
   }
 #undef DPH_C3
+}
+
+bool convg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g) {
+  // whole 64-channel K-steps of one tap; 32-bit DMA offsets below the padding sentinel; int row arithmetic
+  return M > 0 && g.ntaps >= 1 && g.ntaps <= 9 && N % 64 == 0 && K % g.ntaps == 0 && (K / g.ntaps) % 64 == 0 &&
+         g.src_rows * lda * 2 < (int64_t(1) << 31) && N * ldb * 2 < (int64_t(1) << 31) && M < (int64_t(1) << 31) &&
+         (int64_t)g.Hd * g.Wd * (M / ((int64_t)g.Ho * g.Wo) + 1) < (int64_t(1) << 31);
+}
+
+void convg_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                int64_t ldc, const ConvGeo& g, hipStream_t st, float* stats) {
+  const int cin = (int)(K / g.ntaps);
+  // the stride-1 kernel's tile choice: 128-row tiles of 4 waves, 128 columns unless that leaves < 1.5 WG per CU
+  const int nmb = (int)cdiv(M, 128);
+  const bool wide = N % 128 == 0 && (int64_t)nmb * (N / 128) >= 384;
+#define DPH_CG(BN_, ST_, STATS_)                                                                                  \
+  hipLaunchKernelGGL((conv3_k<BN_, ST_, 2, STATS_, true>), dim3(nmb * (int)(N / BN_)), dim3(256), 0, st,        \
+                     (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, 0, 0, cin,   \
+                     stats, (const float*)nullptr, g)
+  if (stats) {
+    if (wide) DPH_CG(128, 2, true);
+    else DPH_CG(64, 3, true);
+  } else {
+    if (wide) DPH_CG(128, 2, false);
+    else DPH_CG(64, 3, false);
+  }
+#undef DPH_CG
 }
 
 }  // namespace dph

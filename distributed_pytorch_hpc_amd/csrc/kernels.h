@@ -164,6 +164,27 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, int H, int W, hipStream_t stream, float* stats = nullptr, const float* bias = nullptr);
+// Gathered implicit GEMM: strided and parity-class (strided-dgrad) convolutions on the same LDS-DMA kernels.
+// GEMM rows m = (n, oy, ox) over an Ho x Wo grid.  The gathered operand's row for output row m and tap t is the pixel
+//   (n Hs + sy oy + by + tdy[t]) Ws + sx ox + bx + tdx[t]     -- zero-filled when outside the Hs x Ws image --
+// of a channels-last [src_rows, Cin] tensor, K = ntaps * Cin tap-major; the forward / input-gradient kernel stores row m
+// to destination row (n Hd + ty oy + tby) Wd + tx ox + tbx (a scatter for the parity classes of a strided dgrad).
+struct ConvGeo {
+  int Hs, Ws, Ho, Wo;
+  int sy, sx, by, bx;
+  int Hd, Wd, ty, tx, tby, tbx;
+  int ntaps;
+  int tdy[9], tdx[9];
+  int64_t src_rows;
+};
+bool convg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g);
+void convg_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                int64_t ldc, const ConvGeo& g, hipStream_t stream, float* stats = nullptr);
+// weight gradient C[N, K] (+)= dY[M, N]^T X_gathered[M, K] on c3w_k (K = ntaps * Cin, a multiple of 192)
+bool c3wg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g);
+void ts_gemm_tn_geo(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
+                    int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, const ConvGeo& g,
+                    hipStream_t stream);
 int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K);
 // 3x3 weight gradient on the LDS-DMA kernel (conv1x1.hip c3w_k): supported shapes and its pixel-chunk count
 bool c3w_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);

@@ -737,6 +737,95 @@ void ts_gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate, in
                   B.stride(0), ns, dt_code(C), accumulate, cur_stream(), (int)H, (int)W, pro_ptr(pro_ss, K, H, A));
 }
 
+// ---------------------------------------------------------------- gathered implicit GEMM (strided convolutions)
+// geo = [Hs, Ws, Ho, Wo, sy, sx, by, bx, Hd, Wd, ty, tx, tby, tbx, ntaps, tdy[0..8], tdx[0..8]] (kernels.h ConvGeo)
+dph::ConvGeo make_geo(at::IntArrayRef geo, int64_t src_rows) {
+  TORCH_CHECK(geo.size() == 15 + 18, "conv geometry: 33 integers expected");
+  dph::ConvGeo g{};
+  int* f[15] = {&g.Hs, &g.Ws, &g.Ho, &g.Wo, &g.sy, &g.sx, &g.by, &g.bx, &g.Hd, &g.Wd, &g.ty, &g.tx, &g.tby, &g.tbx, &g.ntaps};
+  for (int i = 0; i < 15; ++i) *f[i] = (int)geo[i];
+  for (int t = 0; t < 9; ++t) {
+    g.tdy[t] = (int)geo[15 + t];
+    g.tdx[t] = (int)geo[24 + t];
+  }
+  g.src_rows = src_rows;
+  TORCH_CHECK(g.Hs > 0 && g.Ws > 0 && g.Ho > 0 && g.Wo > 0 && g.Hd > 0 && g.Wd > 0 && g.ntaps >= 1 && g.ntaps <= 9,
+              "conv geometry: positive grids and 1..9 taps required");
+  TORCH_CHECK(src_rows % ((int64_t)g.Hs * g.Ws) == 0, "conv geometry: source rows must be whole Hs x Ws images");
+  // every destination row of every image must land inside the Hd x Wd grid (scatter bound, checked on the host)
+  const int64_t ymax = (int64_t)g.ty * (g.Ho - 1) + g.tby, xmax = (int64_t)g.tx * (g.Wo - 1) + g.tbx;
+  TORCH_CHECK(g.tby >= 0 && g.tbx >= 0 && ymax < g.Hd && xmax < g.Wd, "conv geometry: destination outside the grid");
+  return g;
+}
+
+// C[rows(g), N] (rows stored per g's destination map) = A_gathered[M, K] B[N, K]^T; M = images * Ho * Wo.
+// out (optional): the destination tensor (parity classes of one input gradient share it); stats: BatchNorm partials.
+std::vector<Tensor> convg_nt(const Tensor& A, const Tensor& B, at::IntArrayRef geo, const c10::optional<Tensor>& out,
+                             bool stats) {
+  check_cuda(A, "A");
+  c10::DeviceGuard dg(A.device());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
+              "convg_nt: bf16 2-D operands");
+  const dph::ConvGeo g = make_geo(geo, A.size(0));
+  const int64_t imgs = A.size(0) / ((int64_t)g.Hs * g.Ws);
+  const int64_t M = imgs * g.Ho * g.Wo, N = B.size(0), K = B.size(1);
+  TORCH_CHECK(K == g.ntaps * A.size(1), "convg_nt: B must be [N, ntaps * Cin]");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
+              "convg_nt: row-major operands with 16-B aligned rows required");
+  TORCH_CHECK(dph::convg_supported(M, N, K, A.stride(0), B.stride(0), g),
+              "convg_nt: unsupported shape (N % 64, Cin % 64, 32-bit offsets)");
+  check_align16(A, "A");
+  check_align16(B, "B");
+  const int64_t rows = imgs * g.Hd * g.Wd;
+  Tensor C;
+  if (out.has_value()) {
+    C = *out;
+    TORCH_CHECK(C.scalar_type() == at::kBFloat16 && C.dim() == 2 && C.size(0) == rows && C.size(1) == N &&
+                    C.stride(1) == 1 && C.stride(0) % 8 == 0 && C.device() == A.device(),
+                "convg_nt: out must be a bf16 [images * Hd * Wd, N] row-major tensor");
+    check_align16(C, "out");
+  } else {
+    C = at::empty({rows, N}, A.options());
+  }
+  std::vector<Tensor> res{C};
+  float* sp = nullptr;
+  if (stats) {
+    TORCH_CHECK(rows == M, "convg_nt: statistics need the identity destination map");
+    const int64_t nmb = (M + 127) / 128;
+    Tensor st = at::empty({2 * nmb * N + nmb}, A.options().dtype(at::kFloat));
+    sp = st.data_ptr<float>();
+    res.push_back(st);
+  }
+  dph::convg_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0), g,
+                  cur_stream(), sp);
+  return res;
+}
+
+// C[N, ntaps * Cin] (+)= dY[M, N]^T X_gathered[M, ntaps * Cin]; X = the [images * Hs * Ws, Cin] input.
+void convg_tn_(Tensor C, const Tensor& A, const Tensor& B, at::IntArrayRef geo, bool accumulate) {
+  check_cuda(A, "A");
+  c10::DeviceGuard dg(A.device());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.scalar_type() == at::kBFloat16 &&
+                  B.scalar_type() == at::kBFloat16,
+              "convg_tn_: bf16 2-D operands");
+  const dph::ConvGeo g = make_geo(geo, B.size(0));
+  const int64_t imgs = B.size(0) / ((int64_t)g.Hs * g.Ws);
+  const int64_t M = A.size(0), N = A.size(1), K = g.ntaps * B.size(1);
+  TORCH_CHECK(M == imgs * g.Ho * g.Wo, "convg_tn_: dY rows must be images * Ho * Wo");
+  TORCH_CHECK(C.size(0) == N && C.size(1) == K && C.is_contiguous(), "convg_tn_: C must be [N, ntaps * Cin]");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
+              "convg_tn_: row-major operands with 16-B aligned rows required");
+  TORCH_CHECK(dph::c3wg_supported(M, N, K, A.stride(0), B.stride(0), g),
+              "convg_tn_: unsupported shape (N % 64, ntaps * Cin % 192, Cin % 64)");
+  TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "convg_tn_: C bf16 or fp32");
+  check_align16(A, "A");
+  check_align16(B, "B");
+  const int ns = dph::c3w_splits(M, N, K);
+  Tensor part = at::empty({(int64_t)ns * N * K}, A.options().dtype(at::kFloat));
+  dph::ts_gemm_tn_geo(A.data_ptr(), B.data_ptr(), part.data_ptr<float>(), C.data_ptr(), M, N, K, A.stride(0),
+                      B.stride(0), ns, dt_code(C), accumulate, g, cur_stream());
+}
+
 // Select the wgrad kernel's MFMA shape (16 or 32; anything else re-reads DPH_WGRAD_MFMA); returns the active shape.
 int64_t gemm_tn_mfma_(int64_t shape) {
   if (shape != -1) dph::gemm_tn_set_mfma((int)shape);
@@ -1275,6 +1364,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0, Tensor? pro_ss=None) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("conv3x3_dgrad_weight(Tensor w) -> Tensor");
+  m.def("convg_nt(Tensor A, Tensor B, int[] geo, Tensor? out=None, bool stats=False) -> Tensor[]");
+  m.def("convg_tn_(Tensor(a!) C, Tensor A, Tensor B, int[] geo, bool accumulate) -> ()");
   m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
   m.def("maxpool_s2_bwd(Tensor dy, Tensor tap, int H, int W, int k) -> Tensor");
@@ -1338,6 +1429,8 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("ts_gemm_tn_", &ts_gemm_tn_);
   m.impl("transpose2d", &transpose2d);
   m.impl("conv3x3_dgrad_weight", &conv3x3_dgrad_weight);
+  m.impl("convg_nt", &convg_nt);
+  m.impl("convg_tn_", &convg_tn_);
   m.impl("maxpool_s2_fwd", &maxpool_s2_fwd);
   m.impl("channel_sum", &channel_sum);
   m.impl("maxpool_s2_bwd", &maxpool_s2_bwd);

@@ -20,18 +20,19 @@ from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.batchnorm import bn_relu_conv1x1, bn_relu_conv1x1_ok
-from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot, StemConv2d, grad_tap
+from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot, StemConv2d, StridedConv2d, grad_tap
 from ..ops.pool import MaxPool2d
 
 
 def conv3x3(cin, cout, stride=1):
-    # stride 1: channels-last implicit-GEMM kernel path (ops/conv.py); strided 3x3 convolutions stay on MIOpen
-    return Conv3x3(cin, cout) if stride == 1 else nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+    # channels-last implicit-GEMM kernel paths (ops/conv.py): stride 1 Conv3x3, strided the gathered-row kernels
+    return Conv3x3(cin, cout) if stride == 1 else StridedConv2d(cin, cout, 3, stride, 1, bias=False)
 
 
 def conv1x1(cin, cout, stride=1):
-    # stride 1: nn.Conv2d-compatible module that runs channels-last bf16 on the CDNA4 GEMM kernels (ops/conv.py)
-    return Conv1x1(cin, cout) if stride == 1 else nn.Conv2d(cin, cout, 1, stride, bias=False)
+    # nn.Conv2d-compatible modules that run channels-last bf16 on the CDNA4 GEMM kernels (ops/conv.py); the strided
+    # 1x1 (the downsample of layers 2-4) gathers every s-th pixel in its operand load
+    return Conv1x1(cin, cout) if stride == 1 else StridedConv2d(cin, cout, 1, stride, 0, bias=False)
 
 
 class BasicBlock(nn.Module):
@@ -81,7 +82,7 @@ class Bottleneck(nn.Module):
             # conv1's: the tap parks the branch's gradient of x for conv1's dgrad epilogue (no separate add over x)
             tapped = grad_tap(x, slot) if slot is not None and slot.consumer else x
             idt, res_slot = self.downsample(tapped), None
-        s2 = StatsSlot() if isinstance(self.conv2, Conv3x3) and self.bn2.training else None
+        s2 = StatsSlot() if isinstance(self.conv2, (Conv3x3, StridedConv2d)) and self.bn2.training else None
         out = self.conv2(out, stats_slot=s2) if s2 is not None else self.conv2(out)
         if bn_relu_conv1x1_ok(self.bn2, self.conv3, out):
             # bn2's apply + ReLU folded into conv3's operand loads (forward and weight gradient): the normalised

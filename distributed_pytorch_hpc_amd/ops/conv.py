@@ -296,6 +296,161 @@ class Conv3x3(nn.Conv2d):
         return F.conv2d(x, self.weight, padding=1)
 
 
+# ------------------------------------------------------------------------------------------------ strided convolutions
+def conv_geo(Hs, Ws, Ho, Wo, sy, sx, by, bx, Hd, Wd, ty, tx, tby, tbx, taps) -> list[int]:
+    """The 33-integer geometry of the gathered implicit GEMM (csrc/kernels.h ConvGeo): rows (n, oy, ox) over Ho x Wo
+    read source pixel (sy oy + by + dy, sx ox + bx + dx) of an Hs x Ws image for tap (dy, dx), and are stored to
+    destination pixel (ty oy + tby, tx ox + tbx) of an Hd x Wd image."""
+    dy = [t[0] for t in taps] + [0] * (9 - len(taps))
+    dx = [t[1] for t in taps] + [0] * (9 - len(taps))
+    return [Hs, Ws, Ho, Wo, sy, sx, by, bx, Hd, Wd, ty, tx, tby, tbx, len(taps)] + dy + dx
+
+
+def strided_out_hw(H, W, k, s, p):
+    return (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+
+
+def strided_fwd_geo(H, W, k, s, p) -> list[int]:
+    Ho, Wo = strided_out_hw(H, W, k, s, p)
+    taps = [(ky - p, kx - p) for ky in range(k) for kx in range(k)]
+    return conv_geo(H, W, Ho, Wo, s, s, 0, 0, Ho, Wo, 1, 1, 0, 0, taps)
+
+
+def strided_dgrad_classes(H, W, k, s, p):
+    """The input gradient of a stride-s convolution as s^2 parity classes: input pixel (s a + py, s b + px) receives
+    dY(a + dy, b + dx) W[ky, kx] for every tap with ky = py + p - s dy (0 <= ky < k).  Yields
+    (geometry, [(ky, kx)...]) per class with at least one tap; classes without taps receive zero."""
+    Ho, Wo = strided_out_hw(H, W, k, s, p)
+    for py in range(s):
+        for px in range(s):
+            Hc, Wc = len(range(py, H, s)), len(range(px, W, s))
+            if Hc == 0 or Wc == 0:
+                continue
+            ys = [((py + p - ky) // s, ky) for ky in range(k) if (py + p - ky) % s == 0]
+            xs = [((px + p - kx) // s, kx) for kx in range(k) if (px + p - kx) % s == 0]
+            taps = [(dy, dx) for dy, _ in ys for dx, _ in xs]
+            if not taps:
+                continue
+            yield (conv_geo(Ho, Wo, Hc, Wc, 1, 1, 0, 0, H, W, s, s, py, px, taps),
+                   [(ky, kx) for _, ky in ys for _, kx in xs])
+
+
+def strided_dgrad_covers_all(H, W, k, s, p) -> bool:
+    """True when every input pixel belongs to a parity class with taps (no zero-fill needed)."""
+    return sum(g[2] * g[3] for g, _ in strided_dgrad_classes(H, W, k, s, p)) == H * W
+
+
+def convg_reference(A: torch.Tensor, B: torch.Tensor, geo: list, out: torch.Tensor | None = None) -> torch.Tensor:
+    """fp32 PyTorch model of ``convg_nt`` (the gathered implicit GEMM) for tests: A [imgs * Hs * Ws, Cin],
+    B [N, ntaps * Cin] -> rows per the destination map."""
+    Hs, Ws, Ho, Wo, sy, sx, by, bx, Hd, Wd, ty, tx, tby, tbx, nt = geo[:15]
+    tdy, tdx = geo[15:15 + nt], geo[24:24 + nt]
+    imgs, cin = A.shape[0] // (Hs * Ws), A.shape[1]
+    img = A.float().view(imgs, Hs, Ws, cin)
+    oy = torch.arange(Ho, device=A.device)
+    ox = torch.arange(Wo, device=A.device)
+    acc = torch.zeros(imgs, Ho, Wo, B.shape[0], device=A.device)
+    for t in range(nt):
+        yy, xx = sy * oy + by + tdy[t], sx * ox + bx + tdx[t]
+        vy, vx = (yy >= 0) & (yy < Hs), (xx >= 0) & (xx < Ws)
+        g = img[:, yy.clamp(0, Hs - 1)][:, :, xx.clamp(0, Ws - 1)]
+        g = g * (vy[None, :, None, None] & vx[None, None, :, None])
+        acc += g @ B.float()[:, t * cin:(t + 1) * cin].t()
+    if out is None:
+        out = torch.zeros(imgs * Hd * Wd, B.shape[0], device=A.device)
+    dst = out.view(imgs, Hd, Wd, -1)
+    dst[:, ty * oy[:, None] + tby, tx * ox[None, :] + tbx] = acc.to(out.dtype)
+    return out
+
+
+class _StridedConvFn(torch.autograd.Function):
+    """Strided, bias-free k x k convolution (ResNet's stride-2 3x3 conv2 and 1x1 downsample) on the gathered implicit
+    GEMM: forward = per-lane strided source pixels (csrc/conv3x3.hip conv3_k GEN), input gradient = one GEMM per
+    parity class of input pixels with only the taps that reach it, scattered to its pixels, weight gradient = the
+    LDS-DMA 3x3 weight-gradient kernel with strided gathered rows (c3w_k GEN; 1x1: the dense 1x1 kernel over the
+    strided sub-image)."""
+
+    @staticmethod
+    def forward(ctx, x, w, k, s, p, stats_slot=None):
+        wdtype = w.dtype
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        wb = w.to(torch.bfloat16)
+        B, C, H, W = x.shape
+        cout = wb.shape[0]
+        Ho, Wo = strided_out_hw(H, W, k, s, p)
+        x2 = _nhwc2d(x)
+        wk = wb.permute(0, 2, 3, 1).reshape(cout, k * k * C)          # [Cout, (kh, kw, Cin)]
+        geo = strided_fwd_geo(H, W, k, s, p)
+        if stats_slot is not None:
+            y2, stats_slot.stats = _lib.ops().convg_nt(x2, wk, geo, None, True)
+            stats_slot.rows, stats_slot.cols = y2.shape
+        else:
+            y2 = _lib.ops().convg_nt(x2, wk, geo, None, False)[0]
+        ctx.save_for_backward(x2, wb)
+        ctx.cfg = (B, C, H, W, k, s, p, Ho, Wo)
+        ctx.wdtype, ctx.param = wdtype, w
+        return y2.view(B, Ho, Wo, cout).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wb = ctx.saved_tensors
+        B, C, H, W, k, s, p, Ho, Wo = ctx.cfg
+        cout = wb.shape[0]
+        dy2 = _nhwc2d(dy.to(torch.bfloat16))
+        dx = gw = None
+        if ctx.needs_input_grad[0]:
+            full = strided_dgrad_covers_all(H, W, k, s, p)
+            dx2 = (torch.empty if full else torch.zeros)((B * H * W, C), dtype=torch.bfloat16, device=dy.device)
+            wp = wb.permute(1, 2, 3, 0)                                   # [Cin, kh, kw, Cout]
+            for geo, kt in strided_dgrad_classes(H, W, k, s, p):
+                bk = torch.stack([wp[:, ky, kx, :] for ky, kx in kt], 1).reshape(C, len(kt) * cout)
+                _lib.ops().convg_nt(dy2, bk, geo, dx2, False)
+            dx = dx2.view(B, H, W, C).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            w = ctx.param
+            mg = _main_grad_cl(w, cout, k * k * C)
+            tgt = mg if mg is not None else torch.empty((cout, k * k * C), dtype=ctx.wdtype, device=dy.device)
+            acc = bool(getattr(w, "_dph_accum", False)) if mg is not None else False
+            if k == 1:   # 1x1: the dense weight-gradient kernel over the strided sub-image
+                xs = x2.view(B, H, W, C)[:, ::s, ::s].reshape(B * Ho * Wo, C)
+                _lib.ops().ts_gemm_tn_(tgt, dy2, xs, acc)
+            else:
+                _lib.ops().convg_tn_(tgt, dy2, x2, strided_fwd_geo(H, W, k, s, p), acc)
+            if mg is not None:
+                w._dph_accum = True
+                w._dph_grad_ready()
+            else:
+                gw = tgt.view(cout, k, k, C).permute(0, 3, 1, 2).contiguous()
+        return dx, gw, None, None, None, None
+
+
+def strided_native_ok(x: torch.Tensor, m: nn.Conv2d) -> bool:
+    if os.environ.get("DPH_CONV_STRIDED", "0") == "0" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
+        return False
+    if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)):
+        return False
+    k, s, p = m.kernel_size[0], m.stride[0], m.padding[0]
+    cout, cin = m.weight.shape[0], m.weight.shape[1]
+    return (x.dim() == 4 and m.kernel_size == (k, k) and m.stride == (s, s) and m.padding == (p, p)
+            and m.dilation == (1, 1) and m.groups == 1 and m.bias is None and k in (1, 3) and s > 1
+            and cin % 64 == 0 and cout % 64 == 0 and x.is_contiguous(memory_format=torch.channels_last)
+            and x.data_ptr() % 16 == 0)
+
+
+class StridedConv2d(nn.Conv2d):
+    """Bias-free strided 1x1 / 3x3 ``nn.Conv2d`` (same parameters and state dict) on the framework's gathered
+    implicit-GEMM kernels for channels-last bf16 inputs with 64-multiple channels; MIOpen otherwise
+    (``DPH_CONV_STRIDED=0`` forces MIOpen)."""
+
+    def forward(self, x, stats_slot: StatsSlot | None = None):
+        if strided_native_ok(x, self):
+            _lib.require()
+            return _StridedConvFn.apply(x, self.weight, self.kernel_size[0], self.stride[0], self.padding[0],
+                                        stats_slot if _conv3_stats_ok() else None)
+        return F.conv2d(x, self.weight, None, self.stride, self.padding)
+
+
 def conv1x1_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     if os.environ.get("DPH_CONV1X1", "1") == "0" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
         return False
