@@ -52,7 +52,9 @@ constexpr int TS_KF = TS_BK / 16;   // MFMA k-steps (A fragments) per K-step
 // PRO: the A operand is the raw input of a training-mode BatchNorm + ReLU (the bottleneck's bn2 -> conv3): every A
 // element is replaced by relu(a * scale[k] + shift[k]) (pro_ss = fp32 [scale K | shift K], the BatchNorm's forward
 // coefficients) after it lands in registers, so the normalised activation is never written to HBM.
-template <int BN, bool C3, bool ADD = false, bool STATS = false, bool PRO = false>
+// ADDS = s > 1 (with ADD): D is the gradient of the stride-s sub-image (a strided 1x1 downsample's input gradient,
+// [n * ceil(H/s) * ceil(W/s), N]) and is added only at the pixels (y, x) with y % s == x % s == 0 of the H x W grid.
+template <int BN, bool C3, bool ADD = false, bool STATS = false, bool PRO = false, int ADDS = 0>
 __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                  bf16* __restrict__ C, int M, int N, int K, int64_t lda,
                                                  int64_t ldb, int64_t ldc, int H, int W, int Cin,
@@ -185,7 +187,16 @@ __global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, con
     if (m0 + row < M) {
       const int64_t o = (int64_t)(m0 + row) * ldc + nt0 + ch * 8;
       bf16x8 v = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
-      if constexpr (ADD) {
+      if constexpr (ADD && ADDS > 1) {
+        const int m = m0 + row, x = m % W, t = m / W, y = t % H, n = t / H;
+        if (x % ADDS == 0 && y % ADDS == 0) {
+          const int Ho = (H - 1) / ADDS + 1, Wo = (W - 1) / ADDS + 1;
+          const int64_t dr = ((int64_t)n * Ho + y / ADDS) * Wo + x / ADDS;
+          const bf16x8 d = *reinterpret_cast<const bf16x8*>(D + dr * ldc + nt0 + ch * 8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)d[j]);
+        }
+      } else if constexpr (ADD) {
         const bf16x8 d = *reinterpret_cast<const bf16x8*>(D + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)d[j]);
@@ -633,6 +644,20 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     else DPH_TS_NT(64, false);
   }
 #undef DPH_TS_NT
+}
+
+void ts_gemm_nt_add_sub(const void* A, const void* B, void* C, const void* D, int64_t M, int64_t N, int64_t K,
+                        int64_t lda, int64_t ldb, int64_t ldc, int H, int W, int s, hipStream_t st) {
+  const int nmb = (int)cdiv(M, TS_BM);
+  if (N % 128 == 0)
+    hipLaunchKernelGGL((ts_nt_k<128, false, true, false, false, 2>), dim3(nmb * (int)(N / 128)), dim3(TS_NT), 0, st,
+                       (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, 0,
+                       (const bf16*)D);
+  else
+    hipLaunchKernelGGL((ts_nt_k<64, false, true, false, false, 2>), dim3(nmb * (int)(N / 64)), dim3(TS_NT), 0, st,
+                       (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, 0,
+                       (const bf16*)D);
+  (void)s;
 }
 
 int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K) {

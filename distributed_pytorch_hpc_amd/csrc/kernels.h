@@ -160,6 +160,10 @@ bool conv1x1_supported(int64_t M, int64_t N, int64_t K);
 void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, hipStream_t stream, int H = 0, int W = 0,
                 const void* D = nullptr, float* stats = nullptr, const float* pro_ss = nullptr);
+// 1x1 input gradient plus the stride-2 sub-image gradient D [n * ceil(H/2) * ceil(W/2), N] added at the even pixels of
+// the H x W grid (a strided 1x1 downsample's input gradient merged into the block's conv1 dgrad; s must be 2).
+void ts_gemm_nt_add_sub(const void* A, const void* B, void* C, const void* D, int64_t M, int64_t N, int64_t K,
+                        int64_t lda, int64_t ldb, int64_t ldc, int H, int W, int s, hipStream_t stream);
 // 3x3 implicit GEMM with an LDS-DMA pipeline (csrc/conv3x3.hip); ts_gemm_nt's H, W > 0 path when supported.
 bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,

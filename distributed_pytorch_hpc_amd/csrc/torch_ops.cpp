@@ -688,6 +688,31 @@ Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W, const 
   return C;
 }
 
+// 1x1 input gradient C = A B^T with a stride-2 sub-image gradient added at the even pixels of the H x W grid.
+Tensor ts_gemm_nt_add_sub(const Tensor& A, const Tensor& B, const Tensor& add, int64_t H, int64_t W, int64_t s) {
+  check_cuda(A, "A");
+  c10::DeviceGuard g(A.device());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
+              "ts_gemm_nt_add_sub: bf16 2-D operands");
+  TORCH_CHECK(s == 2, "ts_gemm_nt_add_sub: stride 2 only");
+  const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+  TORCH_CHECK(B.size(1) == K && H > 0 && W > 0 && M % (H * W) == 0, "ts_gemm_nt_add_sub: shape mismatch");
+  const int64_t Ho = (H - 1) / s + 1, Wo = (W - 1) / s + 1;
+  TORCH_CHECK(add.scalar_type() == at::kBFloat16 && add.dim() == 2 && add.size(0) == (M / (H * W)) * Ho * Wo &&
+                  add.size(1) == N && add.is_contiguous() && add.device() == A.device(),
+              "ts_gemm_nt_add_sub: add must be a contiguous bf16 [n * ceil(H/2) * ceil(W/2), N] tensor");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
+              "ts_gemm_nt_add_sub: row-major operands with 16-B aligned rows required");
+  TORCH_CHECK(dph::conv1x1_supported(M, N, K), "ts_gemm_nt_add_sub: need N, K % 64 == 0");
+  check_align16(A, "A");
+  check_align16(B, "B");
+  check_align16(add, "add");
+  Tensor C = at::empty({M, N}, A.options());
+  dph::ts_gemm_nt_add_sub(A.data_ptr(), B.data_ptr(), C.data_ptr(), add.data_ptr(), M, N, K, A.stride(0),
+                          B.stride(0), C.stride(0), (int)H, (int)W, (int)s, cur_stream());
+  return C;
+}
+
 // C = A B^T plus the BatchNorm statistics partials of C per 128-row block ([mean | M2 | rows], see conv1x1.hip).
 std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B, int64_t H, int64_t W,
                                             const c10::optional<Tensor>& pro_ss) {
@@ -1366,6 +1391,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("conv3x3_dgrad_weight(Tensor w) -> Tensor");
   m.def("convg_nt(Tensor A, Tensor B, int[] geo, Tensor? out=None, bool stats=False) -> Tensor[]");
   m.def("convg_tn_(Tensor(a!) C, Tensor A, Tensor B, int[] geo, bool accumulate) -> ()");
+  m.def("ts_gemm_nt_add_sub(Tensor A, Tensor B, Tensor add, int H, int W, int s) -> Tensor");
   m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
   m.def("maxpool_s2_bwd(Tensor dy, Tensor tap, int H, int W, int k) -> Tensor");
@@ -1431,6 +1457,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("conv3x3_dgrad_weight", &conv3x3_dgrad_weight);
   m.impl("convg_nt", &convg_nt);
   m.impl("convg_tn_", &convg_tn_);
+  m.impl("ts_gemm_nt_add_sub", &ts_gemm_nt_add_sub);
   m.impl("maxpool_s2_fwd", &maxpool_s2_fwd);
   m.impl("channel_sum", &channel_sum);
   m.impl("maxpool_s2_bwd", &maxpool_s2_bwd);

@@ -20,7 +20,7 @@ from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.batchnorm import bn_relu_conv1x1, bn_relu_conv1x1_ok
-from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot, StemConv2d, StridedConv2d, grad_tap
+from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot, StemConv2d, StridedConv2d, grad_tap, strided_native_ok
 from ..ops.pool import MaxPool2d
 
 
@@ -80,8 +80,17 @@ class Bottleneck(nn.Module):
         else:
             # built after conv1 / bn1, so autograd runs the downsample branch's backward (ending in the tap) before
             # conv1's: the tap parks the branch's gradient of x for conv1's dgrad epilogue (no separate add over x)
-            tapped = grad_tap(x, slot) if slot is not None and slot.consumer else x
-            idt, res_slot = self.downsample(tapped), None
+            ds = self.downsample[0]
+            if (slot is not None and slot.consumer and isinstance(ds, StridedConv2d) and ds.kernel_size == (1, 1)
+                    and ds.stride == (2, 2) and strided_native_ok(x, ds)):
+                # strided 1x1 downsample: its sub-image input gradient goes to conv1's epilogue (added at the even
+                # pixels), so no zero-filled full-size gradient of x is ever written
+                slot.armed = True
+                idt = self.downsample[1](ds(x, grad_slot=slot))
+            else:
+                tapped = grad_tap(x, slot) if slot is not None and slot.consumer else x
+                idt = self.downsample(tapped)
+            res_slot = None
         s2 = StatsSlot() if isinstance(self.conv2, (Conv3x3, StridedConv2d)) and self.bn2.training else None
         out = self.conv2(out, stats_slot=s2) if s2 is not None else self.conv2(out)
         if bn_relu_conv1x1_ok(self.bn2, self.conv3, out):

@@ -4,7 +4,8 @@
 In NHWC a stride-1, bias-free 1x1 convolution is ``Y[M, Cout] = X[M, Cin] W[Cout, Cin]^T`` with M = N*H*W, and
 its two gradients are ``dX = dY W`` and ``dW = dY^T X`` -- no im2col, no layout change: the channels-last tensor
 IS the row-major [M, C] matrix.  ResNet-50's bottleneck convolutions conv1 / conv3 are of this kind (about 2/3
-of its convolution time, benchmarks/conv_bench.py).  Strided convolutions and the 7x7 stem keep MIOpen.
+of its convolution time, benchmarks/conv_bench.py).  Strided 1x1 / 3x3 convolutions run on the gathered implicit GEMM
+(``StridedConv2d``, below); the 7x7 stem keeps MIOpen.
 
 ``Conv1x1`` is a drop-in ``nn.Conv2d`` (same parameter, same state dict) that takes the kernel path for bf16
 (or bf16-autocast) channels-last inputs on the GPU with channel counts that are multiples of 64, and falls back
@@ -91,9 +92,10 @@ class GradSlot:
     residual gradient in ``t`` -- bn3's backward runs before conv1's -- and conv1's dgrad kernel adds it in its
     epilogue (``ts_gemm_nt(..., add=)``), so x receives one gradient."""
 
-    __slots__ = ("consumer", "armed", "t")
+    __slots__ = ("consumer", "armed", "t", "sub")
 
     def __init__(self):
+        self.sub = None      # (s, H, W): t is the gradient of the stride-s sub-image of an H x W input
         self.consumer = False
         self.armed = False
         self.t = None
@@ -170,9 +172,15 @@ class _Conv1x1Fn(torch.autograd.Function):
             if slot is not None and slot.armed:
                 if slot.t is None:
                     raise RuntimeError("Conv1x1: residual gradient slot armed but empty (backward order)")
-                add = _nhwc2d(slot.t.to(torch.bfloat16))
+                add = slot.t
                 slot.t = None
-            dx2 = _lib.ops().ts_gemm_nt(dy2, weight_t(w2), 0, 0, add)    # [M, Cin] (+ residual grad)
+            if add is not None and slot.sub is not None:   # a strided 1x1 downsample's sub-image gradient
+                s_, h_, w_ = slot.sub
+                dx2 = _lib.ops().ts_gemm_nt_add_sub(dy2, weight_t(w2), add.to(torch.bfloat16), h_, w_, s_)
+            else:
+                if add is not None:
+                    add = _nhwc2d(add.to(torch.bfloat16))
+                dx2 = _lib.ops().ts_gemm_nt(dy2, weight_t(w2), 0, 0, add)    # [M, Cin] (+ residual grad)
             dx = dx2.view(B, H, W, C).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             cout = w2.shape[0]
@@ -363,6 +371,10 @@ def convg_reference(A: torch.Tensor, B: torch.Tensor, geo: list, out: torch.Tens
     return out
 
 
+def _strided_wgrad() -> str:
+    return os.environ.get("DPH_CONV_STRIDED_WGRAD", "miopen")
+
+
 class _StridedConvFn(torch.autograd.Function):
     """Strided, bias-free k x k convolution (ResNet's stride-2 3x3 conv2 and 1x1 downsample) on the gathered implicit
     GEMM: forward = per-lane strided source pixels (csrc/conv3x3.hip conv3_k GEN), input gradient = one GEMM per
@@ -371,7 +383,7 @@ class _StridedConvFn(torch.autograd.Function):
     strided sub-image)."""
 
     @staticmethod
-    def forward(ctx, x, w, k, s, p, stats_slot=None):
+    def forward(ctx, x, w, k, s, p, stats_slot=None, grad_slot=None):
         wdtype = w.dtype
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -389,7 +401,7 @@ class _StridedConvFn(torch.autograd.Function):
             y2 = _lib.ops().convg_nt(x2, wk, geo, None, False)[0]
         ctx.save_for_backward(x2, wb)
         ctx.cfg = (B, C, H, W, k, s, p, Ho, Wo)
-        ctx.wdtype, ctx.param = wdtype, w
+        ctx.wdtype, ctx.param, ctx.grad_slot = wdtype, w, grad_slot
         return y2.view(B, Ho, Wo, cout).permute(0, 3, 1, 2)
 
     @staticmethod
@@ -399,7 +411,13 @@ class _StridedConvFn(torch.autograd.Function):
         cout = wb.shape[0]
         dy2 = _nhwc2d(dy.to(torch.bfloat16))
         dx = gw = None
-        if ctx.needs_input_grad[0]:
+        slot = ctx.grad_slot
+        if slot is not None and slot.armed:
+            # 1x1 / stride 2 feeding a GradSlot: the sub-image gradient (one dense GEMM over the strided pixels) goes to
+            # the block's conv1, whose dgrad epilogue adds it at the even pixels -- no zero-filled full-size tensor
+            slot.t = _lib.ops().ts_gemm_nt(dy2, weight_t(wb.view(cout, C)))
+            slot.sub = (s, H, W)
+        elif ctx.needs_input_grad[0]:
             full = strided_dgrad_covers_all(H, W, k, s, p)
             dx2 = (torch.empty if full else torch.zeros)((B * H * W, C), dtype=torch.bfloat16, device=dy.device)
             wp = wb.permute(1, 2, 3, 0)                                   # [Cin, kh, kw, Cout]
@@ -407,7 +425,14 @@ class _StridedConvFn(torch.autograd.Function):
                 bk = torch.stack([wp[:, ky, kx, :] for ky, kx in kt], 1).reshape(C, len(kt) * cout)
                 _lib.ops().convg_nt(dy2, bk, geo, dx2, False)
             dx = dx2.view(B, H, W, C).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and _strided_wgrad() != "dph":
+            # MIOpen's weight gradient: 1.0-1.4x the gathered c3w_k / sub-image 1x1 kernel on ResNet-50's six strided
+            # shapes (profiles/r4/strided_conv/strided.log); DPH_CONV_STRIDED_WGRAD=dph selects the kernels
+            x4 = x2.view(B, H, W, C).permute(0, 3, 1, 2)
+            dy4 = dy2.view(B, Ho, Wo, cout).permute(0, 3, 1, 2)
+            gw = torch.ops.aten.convolution_backward(dy4, x4, wb, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1].to(ctx.wdtype)
+        elif ctx.needs_input_grad[1]:
             w = ctx.param
             mg = _main_grad_cl(w, cout, k * k * C)
             tgt = mg if mg is not None else torch.empty((cout, k * k * C), dtype=ctx.wdtype, device=dy.device)
@@ -422,11 +447,11 @@ class _StridedConvFn(torch.autograd.Function):
                 w._dph_grad_ready()
             else:
                 gw = tgt.view(cout, k, k, C).permute(0, 3, 1, 2).contiguous()
-        return dx, gw, None, None, None, None
+        return dx, gw, None, None, None, None, None
 
 
 def strided_native_ok(x: torch.Tensor, m: nn.Conv2d) -> bool:
-    if os.environ.get("DPH_CONV_STRIDED", "0") == "0" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
+    if os.environ.get("DPH_CONV_STRIDED", "1") == "0" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
         return False
     if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)):
         return False
@@ -441,13 +466,19 @@ def strided_native_ok(x: torch.Tensor, m: nn.Conv2d) -> bool:
 class StridedConv2d(nn.Conv2d):
     """Bias-free strided 1x1 / 3x3 ``nn.Conv2d`` (same parameters and state dict) on the framework's gathered
     implicit-GEMM kernels for channels-last bf16 inputs with 64-multiple channels; MIOpen otherwise
-    (``DPH_CONV_STRIDED=0`` forces MIOpen)."""
+    (``DPH_CONV_STRIDED=0`` forces MIOpen).  ResNet-50 FSDP bf16 B=256: 10 066 / 10 106 vs 10 037 / 10 020 img/s
+    (profiles/r4/strided_conv/final/)."""
 
-    def forward(self, x, stats_slot: StatsSlot | None = None):
+    def forward(self, x, stats_slot: StatsSlot | None = None, grad_slot: GradSlot | None = None):
+        """``grad_slot`` (1x1 / stride 2 only, armed by the caller): the input gradient is handed to the slot's
+        consumer as the stride-2 sub-image gradient instead of being returned (ResNet downsample, models/resnet.py)."""
         if strided_native_ok(x, self):
             _lib.require()
+            gs = grad_slot if (grad_slot is not None and self.kernel_size[0] == 1 and self.stride[0] == 2) else None
             return _StridedConvFn.apply(x, self.weight, self.kernel_size[0], self.stride[0], self.padding[0],
-                                        stats_slot if _conv3_stats_ok() else None)
+                                        stats_slot if _conv3_stats_ok() else None, gs)
+        if grad_slot is not None:
+            raise RuntimeError("StridedConv2d: grad_slot needs the kernel path (check strided_native_ok first)")
         return F.conv2d(x, self.weight, None, self.stride, self.padding)
 
 

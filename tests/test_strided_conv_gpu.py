@@ -24,9 +24,11 @@ def rel_err(a, b):
                                           (3, 3, 256, 256, 14, 14), (1, 2, 256, 512, 14, 14), (1, 2, 64, 128, 7, 9),
                                           (1, 1, 512, 1024, 28, 28)])
 @pytest.mark.parametrize("autocast", [False, True])
-def test_strided_conv_matches_conv2d(dph_native, k, B, C, Co, H, W, autocast):
+@pytest.mark.parametrize("wgrad", ["dph", "miopen"])
+def test_strided_conv_matches_conv2d(dph_native, monkeypatch, k, B, C, Co, H, W, autocast, wgrad):
     from distributed_pytorch_hpc_amd.ops.conv import StridedConv2d, strided_native_ok
 
+    monkeypatch.setenv("DPH_CONV_STRIDED_WGRAD", wgrad)
     torch.manual_seed(7)
     p = k // 2
     conv = StridedConv2d(C, Co, k, 2, p, bias=False).to(DEV).to(memory_format=torch.channels_last)
@@ -49,11 +51,12 @@ def test_strided_conv_matches_conv2d(dph_native, k, B, C, Co, H, W, autocast):
     assert rel_err(conv.weight.grad, wr.grad) < 1e-2
 
 
-def test_strided_conv_stats_epilogue_and_main_grad(dph_native):
+def test_strided_conv_stats_epilogue_and_main_grad(dph_native, monkeypatch):
     """The BatchNorm partials from the strided forward equal the output's own statistics; with an engine-owned
-    channels-last main_grad the weight gradient is written (then accumulated) into it directly."""
+    channels-last main_grad the weight-gradient kernel writes (then accumulates) into it directly."""
     from distributed_pytorch_hpc_amd.ops.conv import StatsSlot, StridedConv2d
 
+    monkeypatch.setenv("DPH_CONV_STRIDED_WGRAD", "dph")
     torch.manual_seed(3)
     conv = StridedConv2d(128, 128, 3, 2, 1, bias=False).to(DEV).to(torch.bfloat16).to(
         memory_format=torch.channels_last)
@@ -110,3 +113,45 @@ def test_downsample_bottleneck_strided_path_matches_miopen(dph_native, monkeypat
     assert rel_err(gx1, gx0) < 3e-2
     for n in g0:
         assert rel_err(g1[n], g0[n]) < 5e-2, n
+
+
+@pytest.mark.parametrize("n,H,W,K,N", [(2, 14, 14, 128, 256), (1, 7, 9, 64, 128), (3, 28, 28, 256, 64)])
+def test_ts_gemm_nt_add_sub(dph_native, n, H, W, K, N):
+    """1x1 dgrad + a stride-2 sub-image gradient added at the even pixels (the strided downsample's hand-off)."""
+    torch.manual_seed(n * H + W)
+    a = torch.randn(n * H * W, K, device=DEV, dtype=torch.bfloat16)
+    b = (0.1 * torch.randn(N, K, device=DEV)).to(torch.bfloat16)
+    Ho, Wo = (H + 1) // 2, (W + 1) // 2
+    d = torch.randn(n * Ho * Wo, N, device=DEV, dtype=torch.bfloat16)
+    c = torch.ops.dph.ts_gemm_nt_add_sub(a, b, d, H, W, 2)
+    ref = (a.float() @ b.float().t()).view(n, H, W, N)
+    ref[:, ::2, ::2] += d.float().view(n, Ho, Wo, N)
+    assert rel_err(c, ref.view(-1, N)) < 5e-3
+
+
+def test_downsample_hands_sub_gradient_to_conv1(dph_native, monkeypatch):
+    """The strided 1x1 downsample parks its sub-image gradient in conv1's GradSlot (no full-size dX of its own)."""
+    import importlib
+
+    from distributed_pytorch_hpc_amd.ops.conv import GradSlot
+
+    resnet_mod = importlib.import_module("distributed_pytorch_hpc_amd.models.resnet")
+    made = []
+
+    class _Spy(GradSlot):
+        __slots__ = ()
+
+        def __init__(self):
+            super().__init__()
+            made.append(self)
+
+    monkeypatch.setattr(resnet_mod, "GradSlot", _Spy)
+    torch.manual_seed(1)
+    down = torch.nn.Sequential(resnet_mod.conv1x1(256, 512, 2),
+                               resnet_mod.BatchNormAct2d(512, act=False))
+    block = resnet_mod.Bottleneck(256, 128, 2, down).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(2, 256, 14, 14, device=DEV, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+    block(x).float().pow(2).mean().backward()
+    assert made and made[0].armed and made[0].sub == (2, 14, 14) and made[0].t is None
+    assert x.grad is not None and torch.isfinite(x.grad.float()).all()
