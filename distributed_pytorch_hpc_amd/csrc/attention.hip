@@ -806,7 +806,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
 // are one scalar per lane), then dQ^T += K^T dS^T with dS^T consumed straight from the accumulator.
 // PF (A/B knob, DPH_ATTN_DQ_VAR=1): the dQ product's transposed K reads software-pipelined one MFMA ahead, the first
 // issued before the last sub-tile's softmax.
-template <int HD, bool CAUSAL, int NW, bool DROP = false, bool PF = false>
+// KQ: K / V fragments read KS / KQ k-steps ahead of their MFMAs (2 = half a sub-tile; 4 = a quarter, 16 fewer VGPRs:
+// the KQ = 2 form spills 3 registers at 256).
+template <int HD, bool CAUSAL, int NW, bool DROP = false, bool PF = false, int KQ = 2>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P) {
   using Plan = KVTilePlan<HD, 64 * NW>;
   constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
@@ -875,10 +877,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
     for (int sub = 0; sub < 2; ++sub) {
       // K and V fragments are read a half sub-tile (KH k-steps) ahead of their MFMAs with counted lgkmcnt waits
       // (one read + wait + multiply at a time exposed an LDS round trip per MFMA; all KS at once spills)
-      constexpr int KH = KS / 2;
+      constexpr int NQ = KS >= KQ ? KQ : KS, KH = KS / NQ;
       f32x16 s = zacc, dp = zacc;
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
+      for (int half = 0; half < NQ; ++half) {
         bf16x8 kf[KH], vf[KH];
 #pragma unroll
         for (int j = 0; j < KH; ++j) {
@@ -1040,11 +1042,14 @@ static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
   }
   const size_t lds_q = 2 * 2 * 64 * HD * 2;
   const dim3 grid_q((unsigned)((p.Sq + 32 * NW - 1) / (32 * NW) * p.Hq * p.B));
-  static const bool dq_pf = [] {
+  static const int dq_var = [] {
     const char* e = getenv("DPH_ATTN_DQ_VAR");
-    return e ? atoi(e) == 1 : kAttnDqDefaultPf;
+    return e ? atoi(e) : (kAttnDqDefaultPf ? 1 : 0);
   }();
-  if (dq_pf) {
+  if (dq_var == 2) {   // quarter-sub-tile K / V read-ahead (no spills)
+    if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW, false, false, 4>), grid_q, dim3(64 * NW), lds_q, st, P);
+    else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW, false, false, 4>), grid_q, dim3(64 * NW), lds_q, st, P);
+  } else if (dq_var == 1) {
     if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW, false, true>), grid_q, dim3(64 * NW), lds_q, st, P);
     else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW, false, true>), grid_q, dim3(64 * NW), lds_q, st, P);
   } else {

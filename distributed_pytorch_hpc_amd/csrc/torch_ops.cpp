@@ -715,7 +715,7 @@ Tensor ts_gemm_nt_add_sub(const Tensor& A, const Tensor& B, const Tensor& add, i
 
 // C = A B^T plus the BatchNorm statistics partials of C per 128-row block ([mean | M2 | rows], see conv1x1.hip).
 std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B, int64_t H, int64_t W,
-                                            const c10::optional<Tensor>& pro_ss) {
+                                            const c10::optional<Tensor>& pro_ss, const c10::optional<Tensor>& bias) {
   check_cuda(A, "A");
   c10::DeviceGuard g(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
@@ -733,6 +733,15 @@ std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B, in
   const int64_t nmb = (M + 127) / 128;
   Tensor C = at::empty({M, N}, A.options());
   Tensor st = at::empty({2 * nmb * N + nmb}, A.options().dtype(at::kFloat));
+  if (bias.has_value()) {   // 3x3 LDS-DMA kernel: fp32 bias on the accumulators, statistics of the biased output
+    TORCH_CHECK(H > 0 && !pro_ss.has_value(), "ts_gemm_nt_stats: bias is a 3x3 (H > 0) feature");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous() &&
+                    bias->device() == A.device(),
+                "ts_gemm_nt_stats: bias must be a contiguous fp32 [N] tensor");
+    dph::conv3_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
+                    (int)H, (int)W, cur_stream(), st.data_ptr<float>(), bias->data_ptr<float>());
+    return {C, st};
+  }
   dph::ts_gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
                   cur_stream(), (int)H, (int)W, nullptr, st.data_ptr<float>(), pro_ptr(pro_ss, K, H, A));
   return {C, st};
@@ -1385,7 +1394,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("gemm_tn_mfma_(int shape) -> int", &gemm_tn_mfma_);   // no tensor argument: catch-all kernel
   m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0, Tensor? add=None, Tensor? bias=None, Tensor? pro_ss=None) "
         "-> Tensor");
-  m.def("ts_gemm_nt_stats(Tensor A, Tensor B, int H=0, int W=0, Tensor? pro_ss=None) -> (Tensor, Tensor)");
+  m.def("ts_gemm_nt_stats(Tensor A, Tensor B, int H=0, int W=0, Tensor? pro_ss=None, Tensor? bias=None) -> (Tensor, Tensor)");
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0, Tensor? pro_ss=None) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("conv3x3_dgrad_weight(Tensor w) -> Tensor");

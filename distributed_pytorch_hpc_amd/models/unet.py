@@ -10,19 +10,35 @@ swaps the 3x3 convolutions for halo-exchanging ones when the latitude axis is sh
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import BiasConv2d, BiasConvTranspose2d
+from ..ops.conv import BiasConv2d, BiasConvTranspose2d, StatsSlot
 from ..ops.pool import MaxPool2d
 from ..ops.upsample import up_concat
 
 
+_CONV_STATS = os.environ.get("DPH_UNET_CONV_STATS", "1") != "0"   # A/B knob: BN statistics from the conv epilogue
+
+
+class ConvBlock(nn.Sequential):
+    """conv -> BN -> ReLU twice, as the reference's ``conv_block``; BN + ReLU run as one fused channels-last op
+    (BatchNormAct2d, a BatchNorm2d subclass: same state-dict keys; the ReLU slots stay as Identity so the indices are
+    unchanged), and a training-mode BN takes its batch statistics from the 3x3 convolution's epilogue (StatsSlot)
+    instead of a statistics pass over the activation."""
+
+    def forward(self, x):
+        for conv, bn in ((self[0], self[1]), (self[3], self[4])):
+            slot = StatsSlot() if bn.training and _CONV_STATS else None
+            x = bn(conv(x, stats_slot=slot), stats_slot=slot)
+        return x
+
+
 def conv_block(in_ch: int, out_ch: int) -> nn.Sequential:
-    # conv -> BN -> ReLU twice, as the reference; BN + ReLU run as one fused channels-last op (BatchNormAct2d, a
-    # BatchNorm2d subclass: same state-dict keys; the ReLU slots stay as Identity so the indices are unchanged)
-    return nn.Sequential(
+    return ConvBlock(
         BiasConv2d(in_ch, out_ch, 3, padding=1), BatchNormAct2d(out_ch), nn.Identity(),
         BiasConv2d(out_ch, out_ch, 3, padding=1), BatchNormAct2d(out_ch), nn.Identity(),
     )

@@ -187,7 +187,7 @@ def _ts_gemm_nt(A, B, H=0, W=0, add=None, bias=None, pro_ss=None):
 
 
 @register_fake("dph::ts_gemm_nt_stats")
-def _ts_gemm_nt_stats(A, B, H=0, W=0, pro_ss=None):
+def _ts_gemm_nt_stats(A, B, H=0, W=0, pro_ss=None, bias=None):
     M, N = A.shape[0], B.shape[0]
     nmb = (M + 127) // 128
     return A.new_empty((M, N)), A.new_empty((2 * nmb * N + nmb,), dtype=torch.float32)
@@ -196,6 +196,29 @@ def _ts_gemm_nt_stats(A, B, H=0, W=0, pro_ss=None):
 @register_fake("dph::ts_gemm_tn_")
 def _ts_gemm_tn(C, A, B, accumulate, H=0, W=0, pro_ss=None):
     return None
+
+
+@register_fake("dph::convg_nt")
+def _convg_nt(A, B, geo, out=None, stats=False):
+    Hs, Ws, Ho, Wo, Hd, Wd = geo[0], geo[1], geo[2], geo[3], geo[8], geo[9]
+    imgs = A.shape[0] // (Hs * Ws)
+    N = B.shape[0]
+    res = [out if out is not None else A.new_empty((imgs * Hd * Wd, N))]
+    if stats:
+        M = imgs * Ho * Wo
+        nmb = (M + 127) // 128
+        res.append(A.new_empty((2 * nmb * N + nmb,), dtype=torch.float32))
+    return res
+
+
+@register_fake("dph::convg_tn_")
+def _convg_tn(C, A, B, geo, accumulate):
+    return None
+
+
+@register_fake("dph::ts_gemm_nt_add_sub")
+def _ts_gemm_nt_add_sub(A, B, add, H, W, s):
+    return A.new_empty((A.shape[0], B.shape[0]))
 
 
 @register_fake("dph::latmse_fwd")

@@ -229,11 +229,11 @@ class _Conv3x3Fn(torch.autograd.Function):
         cout = wb.shape[0]
         x2 = _nhwc2d(x)
         wk = wb.permute(0, 2, 3, 1).reshape(cout, 9 * C)             # [Cout, (kh, kw, Cin)]
-        if bias is not None:   # fp32 bias in the epilogue (SimpleUNet's biased 3x3 convolutions)
-            y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W, None, bias)
-        elif stats_slot is not None:
-            y2, stats_slot.stats = _lib.ops().ts_gemm_nt_stats(x2, wk, H, W)   # + BN partials of the output
+        if stats_slot is not None:   # + BN partials of the output (of the biased output when there is a bias)
+            y2, stats_slot.stats = _lib.ops().ts_gemm_nt_stats(x2, wk, H, W, None, bias)
             stats_slot.rows, stats_slot.cols = y2.shape
+        elif bias is not None:   # fp32 bias in the epilogue (SimpleUNet's biased 3x3 convolutions)
+            y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W, None, bias)
         else:
             y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W)
         ctx.has_bias = bias is not None
@@ -564,11 +564,13 @@ class BiasConv2d(nn.Conv2d):
     kernel of csrc/conv3x3.hip with the bias in its epilogue (when the 3x3 path is on), everything else the stock
     MIOpen convolution."""
 
-    def forward(self, x):
+    def forward(self, x, stats_slot: StatsSlot | None = None):
+        """``stats_slot``: on the 3x3 kernel path the following BatchNorm's statistics come from this convolution's
+        epilogue (SimpleUNet's conv -> BN blocks, models/unet.py); otherwise the slot stays empty."""
         if _bias_conv3x3_ok(self, x):
             _lib.require()
             b = self.bias if self.bias.dtype == torch.float32 else self.bias.float()
-            return _Conv3x3Fn.apply(x, self.weight, None, b, _conv3_wgrad("dph"))
+            return _Conv3x3Fn.apply(x, self.weight, stats_slot, b, _conv3_wgrad("dph"))
         if _bias_conv_ok(self, x):
             return _bias_conv(self, x, False, (0, 0))
         return super().forward(x)

@@ -249,6 +249,21 @@ def test_flash_attention_eight_wave_variant(dph_native, waves):
     assert '"ok": true' in p.stdout
 
 
+@pytest.mark.parametrize("dq_var", ["1", "2"])
+def test_flash_attention_dq_variants(dph_native, dq_var):
+    """dQ kernel variants (DPH_ATTN_DQ_VAR: 1 = transposed-K read ring, 2 = quarter-sub-tile K / V read-ahead without
+    register spills), read once per process, in a child process against the fp32 reference."""
+    import os
+    import subprocess
+    import sys
+
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "attn_check.py")
+    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_ATTN_DQ_VAR=dq_var), capture_output=True,
+                       text=True, timeout=100)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    assert '"ok": true' in p.stdout
+
+
 def test_flash_attention_padded_head_dim(dph_native):
     torch.manual_seed(10)
     q, k, v = (torch.randn(2, 64, 4, 16, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
@@ -844,6 +859,40 @@ def test_bias_conv3x3_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W):
     assert rel_err(x.grad, xr.grad) < 1e-2
     assert rel_err(conv.weight.grad, wr.grad) < 1e-2
     assert rel_err(conv.bias.grad, br.grad) < 1e-3
+
+
+def test_unet_conv_block_stats_from_conv_epilogue(dph_native):
+    """SimpleUNet's ConvBlock: each training-mode BN takes its batch statistics (of the biased output) from the 3x3
+    convolution's epilogue; output, running statistics and gradients equal the path where BN runs its own pass."""
+    from distributed_pytorch_hpc_amd.models.unet import conv_block
+
+    torch.manual_seed(4)
+    blk = conv_block(64, 128).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        blk[0].bias.uniform_(-1, 1)
+        blk[3].bias.uniform_(-1, 1)
+    ref = conv_block(64, 128).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    ref.load_state_dict(blk.state_dict())
+    x = torch.randn(2, 64, 20, 23, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xa, xb = x.clone().requires_grad_(), x.clone().requires_grad_()
+    ya = blk(xa)
+    yb = x.new_empty(0)
+    h = xb
+    for i in (0, 3):                      # the plain Sequential order: BN computes its own statistics
+        h = ref[i + 1](ref[i](h))
+    yb = h
+    assert rel_err(ya, yb) < 1e-2
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    assert rel_err(xa.grad, xb.grad) < 2e-2
+    for (n, pa), (_, pb) in zip(blk.named_parameters(), ref.named_parameters()):
+        if n in ("0.bias", "3.bias"):     # a bias before training-mode BN has gradient 0 up to rounding noise
+            assert pa.grad.float().abs().max() < 5e-2 * blk[0].weight.grad.float().abs().max() + 1e-2, n
+            continue
+        assert rel_err(pa.grad, pb.grad) < 5e-2, n
+    assert rel_err(blk[1].running_mean, ref[1].running_mean) < 1e-2
+    assert rel_err(blk[4].running_var, ref[4].running_var) < 1e-2
 
 
 @pytest.mark.parametrize("N_img,C,Co,H,W", [(3, 64, 64, 10, 11), (2, 128, 128, 28, 28), (1, 64, 192, 7, 9),
