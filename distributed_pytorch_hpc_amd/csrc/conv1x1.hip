@@ -405,22 +405,25 @@ __device__ __forceinline__ void fdivmod(int r, int d, float inv, int& q, int& m)
 
 // GEN: the X rows are gathered by kernels.h ConvGeo (strided convolutions): output row r = (n, oy, ox) over Ho x Wo,
 // tap t's source pixel (n Hs + sy oy + by + tdy[t]) Ws + sx ox + bx + tdx[t] of the [src_rows, Cin] input.
-template <int TCO, bool GEN = false>
+// SL: X slabs (64 k' each) per output tile: 3 for the 3x3 kernels (192 k', one tap per slab), 1 or 2 for the 1x1
+// weight gradient (GEN with the identity geometry).
+template <int TCO, bool GEN = false, int SL = C3W_SLABS>
 __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                 float* __restrict__ P, int M, int N, int K, int64_t lda,
                                                 int64_t ldb, int chunk, int H, int W, int Cin, ConvGeo geo) {
   constexpr int AS = TCO / 64;                       // dY slabs per step
-  constexpr int STG = (AS + C3W_SLABS) * C3W_SLAB;   // one stage
-  constexpr int PCS = (AS + C3W_SLABS) * 8 / 4;      // 1-KB DMA pieces per wave per step
+  constexpr int TK = 64 * SL, WK = TK / 2;            // k' per tile, per wave
+  constexpr int STG = (AS + SL) * C3W_SLAB;           // one stage
+  constexpr int PCS = (AS + SL) * 8 / 4;              // 1-KB DMA pieces per wave per step
   constexpr int TI = TCO / 64;                       // co MFMA tiles per wave (wave covers TCO / 2 channels)
   __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int cw = wid >> 1, kw = wid & 1;
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, h = lane >> 5;
-  const int tn = N / TCO, tk = K / C3W_TK, ntile = tn * tk;
+  const int tn = N / TCO, tk = K / TK, ntile = tn * tk;
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int s = lin / ntile, tile = lin % ntile;    // the tiles of one pixel chunk run together (same XCD, same rows)
-  const int n0 = (tile / tk) * TCO, k0 = (tile % tk) * C3W_TK;
+  const int n0 = (tile / tk) * TCO, k0 = (tile % tk) * TK;
   const int mbeg = s * chunk, mend = min(M, mbeg + chunk);
 
   const int Wr = GEN ? geo.Wo : W, Hr = GEN ? geo.Ho : H;   // the row space's grid
@@ -431,9 +434,9 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
   const int wid_u = __builtin_amdgcn_readfirstlane(wid);
   // DMA lanes: piece i (of AS*8 + 24 per step) = slab i / 8, rows 8 (i % 8) + prow, LDS slot lane % 8
   const int prow = lane >> 3, sch = (lane & 7) ^ tw_swz(prow);
-  int bdy[C3W_SLABS], bdx[C3W_SLABS], bcb[C3W_SLABS];
+  int bdy[SL], bdx[SL], bcb[SL];
 #pragma unroll
-  for (int sb = 0; sb < C3W_SLABS; ++sb) {
+  for (int sb = 0; sb < SL; ++sb) {
     const int kk = k0 + sb * 64, tap = kk / Cin;
     bcb[sb] = kk - tap * Cin;
     if constexpr (GEN) {   // tap table lookup by selects (tap is uniform over the workgroup)
@@ -461,7 +464,7 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
         const unsigned off = (unsigned)(((int64_t)r * lda + n0 + slab * 64 + sch * 8) * 2);
         lds_dma16_buf(ra, r < mend ? off : 0x80000000u, dst);
       } else {
-        const int sb = slab - AS;
+        const int sb = SL == 1 ? 0 : slab - AS;   // (SL = 1: a constant index, no private-memory array)
         int yq, xw, yh, nq;
         fdivmod(r, Wr, invW, yq, xw);                // pixel -> (image row, column), then image row -> y
         fdivmod(yq, Hr, invH, nq, yh);
@@ -484,23 +487,23 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
   // transposed-read offsets (ts_tn_k's layout): 32-column operand at 32-column offset c32 of a slab
   const int hh = g >> 1, tch = 2 * (g & 1) + (p >> 1), tin = 8 * (p & 1);
   auto toff = [&](int c32) { return (8 * hh + q) * TW_ROWB + (((c32 * 4 + tch) ^ tw_swz(q)) << 4) + tin; };
-  int aoff[TI], boff[3];
+  int aoff[TI], boff[SL];
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
     const int co = cw * (TCO / 2) + i * 32;          // within the tile
     aoff[i] = (co >> 6) * C3W_SLAB + toff((co >> 5) & 1);
   }
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int kc = kw * 96 + j * 32;
+  for (int j = 0; j < SL; ++j) {
+    const int kc = kw * WK + j * 32;
     boff[j] = (AS + (kc >> 6)) * C3W_SLAB + toff((kc >> 5) & 1);
   }
 
-  f32x16 acc[TI][3];
+  f32x16 acc[TI][SL];
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < SL; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -514,21 +517,21 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {                 // 16-pixel MFMA k-steps
       const int ro = 16 * kk * TW_ROWB;
-      bf16x8 af[TI], bfr[3];
+      bf16x8 af[TI], bfr[SL];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const bf16x4 lo = tr_read(base + aoff[i] + ro), hi = tr_read(base + aoff[i] + ro + 4 * TW_ROWB);
         af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < SL; ++j) {
         const bf16x4 lo = tr_read(base + boff[j] + ro), hi = tr_read(base + boff[j] + ro + 4 * TW_ROWB);
         bfr[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < SL; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
     }
   }
   // register r of tile (i, j): P[n0 + cw*TCO/2 + i*32 + (r&3) + 8(r>>2) + 4h][k0 + kw*96 + j*32 + (lane & 31)]
@@ -536,10 +539,10 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < SL; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        out[(int64_t)(n0 + cw * (TCO / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * K + k0 + kw * 96 + j * 32 +
+        out[(int64_t)(n0 + cw * (TCO / 2) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * K + k0 + kw * WK + j * 32 +
             (lane & 31)] = acc[i][j][r];
 }
 
@@ -699,9 +702,29 @@ bool c3w_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
          M * ldb * 2 < (int64_t(1) << 31) && M < (int64_t(1) << 24);
 }
 
+static int64_t c3w_tiles(int64_t N, int64_t K, int64_t tk) { return (N / (N % 128 == 0 ? 128 : 64)) * (K / tk); }
+
+// 1x1 weight gradient on the LDS-DMA kernel (c3w_k with one tap, identity rows): k' tiles of 128 (64 when K % 128)
+static int w1_tk(int64_t K) { return K % 128 == 0 ? 128 : 64; }
+
+bool w1_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
+  static const bool on = [] {   // A/B knob: DPH_W1_KERNEL=0 keeps the register-staged ts_tn_k
+    const char* e = getenv("DPH_W1_KERNEL");
+    return !(e && e[0] == '0');
+  }();
+  return on && N % 64 == 0 && K % 64 == 0 && M * lda * 2 < (int64_t(1) << 31) && M * ldb * 2 < (int64_t(1) << 31) &&
+         M < (int64_t(1) << 24);
+}
+
+int w1_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = c3w_tiles(N, K, w1_tk(K));
+  int64_t s = cdiv(512, tiles);   // one resident round of 2 workgroups per CU, chunks of >= 512 rows
+  s = std::max<int64_t>(1, std::min<int64_t>(s, M / 512));
+  return (int)s;
+}
+
 int c3w_splits(int64_t M, int64_t N, int64_t K) {
-  const int64_t tco = N % 128 == 0 ? 128 : 64;
-  const int64_t tiles = (N / tco) * (K / C3W_TK);
+  const int64_t tiles = c3w_tiles(N, K, C3W_TK);
   // one resident round of 2 workgroups per CU (the fp32 partials grow with the split), chunks of >= 512 rows
   int64_t s = cdiv(512, tiles);
   s = std::max<int64_t>(1, std::min<int64_t>(s, M / 512));
@@ -726,7 +749,27 @@ void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M
   const int64_t tiles = (N / 64) * (K / 64);
   int64_t chunk = cdiv(M, nsplit);
   chunk = cdiv(chunk, 64) * 64;
-  if (H > 0 && c3w_supported(M, N, K, lda, ldb)) {   // the LDS-DMA 3x3 kernel (nsplit from c3w_splits)
+  if (H == 0 && pro_ss == nullptr && w1_supported(M, N, K, lda, ldb)) {   // LDS-DMA 1x1 (nsplit from w1_splits)
+    ConvGeo g{};
+    g.Hs = g.Ho = g.Hd = 1;
+    g.Ws = g.Wo = g.Wd = (int)M;
+    g.sy = g.sx = g.ty = g.tx = 1;
+    g.ntaps = 1;
+    g.src_rows = M;
+    const int tk = w1_tk(K);
+#define DPH_W1(TCO_, SL_)                                                                                      \
+  hipLaunchKernelGGL((c3w_k<TCO_, true, SL_>), dim3((int)((N / TCO_) * (K / tk) * nsplit)), dim3(256), 0, st,   \
+                     (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0,   \
+                     (int)K, g)
+    if (N % 128 == 0) {
+      if (tk == 128) DPH_W1(128, 2);
+      else DPH_W1(128, 1);
+    } else {
+      if (tk == 128) DPH_W1(64, 2);
+      else DPH_W1(64, 1);
+    }
+#undef DPH_W1
+  } else if (H > 0 && c3w_supported(M, N, K, lda, ldb)) {   // the LDS-DMA 3x3 kernel (nsplit from c3w_splits)
     const int cin = (int)(K / 9);
     if (N % 128 == 0)
       hipLaunchKernelGGL((c3w_k<128>), dim3((int)((N / 128) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,

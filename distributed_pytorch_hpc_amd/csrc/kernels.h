@@ -193,6 +193,9 @@ int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K);
 // 3x3 weight gradient on the LDS-DMA kernel (conv1x1.hip c3w_k): supported shapes and its pixel-chunk count
 bool c3w_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 int c3w_splits(int64_t M, int64_t N, int64_t K);
+// 1x1 weight gradient on the same LDS-DMA kernel (ts_gemm_tn's H = 0 path without pro_ss when supported)
+bool w1_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
+int w1_splits(int64_t M, int64_t N, int64_t K);
 void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
                 int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, hipStream_t stream, int H = 0,
                 int W = 0, const float* pro_ss = nullptr);

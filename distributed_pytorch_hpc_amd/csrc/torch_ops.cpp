@@ -764,7 +764,9 @@ void ts_gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate, in
   TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "ts_gemm_tn: C bf16 or fp32");
   check_align16(A, "A");
   check_align16(B, "B");
+  const bool w1 = H == 0 && !pro_ss.has_value() && dph::w1_supported(M, N, K, A.stride(0), B.stride(0));
   const int ns = (H > 0 && dph::c3w_supported(M, N, K, A.stride(0), B.stride(0))) ? dph::c3w_splits(M, N, K)
+                 : w1                                                              ? dph::w1_splits(M, N, K)
                                                                                   : dph::ts_gemm_tn_splits(M, N, K);
   Tensor part = at::empty({(int64_t)ns * N * K}, A.options().dtype(at::kFloat));
   dph::ts_gemm_tn(A.data_ptr(), B.data_ptr(), part.data_ptr<float>(), C.data_ptr(), M, N, K, A.stride(0),
