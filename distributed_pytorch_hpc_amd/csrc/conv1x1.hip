@@ -407,7 +407,8 @@ __device__ __forceinline__ void fdivmod(int r, int d, float inv, int& q, int& m)
 // tap t's source pixel (n Hs + sy oy + by + tdy[t]) Ws + sx ox + bx + tdx[t] of the [src_rows, Cin] input.
 // SL: X slabs (64 k' each) per output tile: 3 for the 3x3 kernels (192 k', one tap per slab), 1 or 2 for the 1x1
 // weight gradient (GEN with the identity geometry).
-template <int TCO, bool GEN = false, int SL = C3W_SLABS>
+// GEN = 2: chunk taps (the 7x7 RGB stem, conv3x3.hip conv3_k GEN = 2): every 16-B chunk of an X slab is its own tap.
+template <int TCO, int GEN = 0, int SL = C3W_SLABS>
 __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                 float* __restrict__ P, int M, int N, int K, int64_t lda,
                                                 int64_t ldb, int chunk, int H, int W, int Cin, ConvGeo geo) {
@@ -470,7 +471,13 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
         fdivmod(yq, Hr, invH, nq, yh);
         bool ok;
         int64_t src;
-        if constexpr (GEN) {
+        unsigned col = (unsigned)(bcb[sb] + sch * 8);
+        if constexpr (GEN == 2) {   // this lane's chunk is tap t: the whole 8-element source row
+          const int t = min((k0 + sb * 64) / 8 + sch, geo.ntaps - 1), ty = t / geo.tdx[0], tx = t - ty * geo.tdx[0];
+          ok = r < mend;
+          src = ((int64_t)nq * geo.Hs + geo.sy * yh + geo.by + ty) * geo.Ws + geo.sx * xw + geo.bx + tx;
+          col = 0;
+        } else if constexpr (GEN) {
           const int ay = geo.sy * yh + geo.by + bdy[sb], ax = geo.sx * xw + geo.bx + bdx[sb];
           ok = r < mend && (unsigned)ay < (unsigned)geo.Hs && (unsigned)ax < (unsigned)geo.Ws;
           src = ((int64_t)nq * geo.Hs + ay) * geo.Ws + ax;
@@ -478,7 +485,7 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
           ok = r < mend && (unsigned)(yh + bdy[sb]) < (unsigned)H && (unsigned)(xw + bdx[sb]) < (unsigned)W;
           src = r + bdy[sb] * W + bdx[sb];
         }
-        const unsigned off = (unsigned)((src * ldb + bcb[sb] + sch * 8) * 2);
+        const unsigned off = (unsigned)((src * ldb + col) * 2);
         lds_dma16_buf(rb, ok ? off : 0x80000000u, dst);
       }
     }
@@ -791,17 +798,39 @@ void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M
   ts_reduce(partial, C, N * K, nsplit, out_dtype, accumulate, st);
 }
 
-bool c3wg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g) {
+bool c3wg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g, bool chunk_taps) {
+  if (chunk_taps)   // 128-wide k' tiles of 16 chunk taps each
+    return N % 64 == 0 && K % 128 == 0 && ldb == 8 && g.ntaps >= 1 && g.ntaps <= K / 8 && g.tdx[0] > 0 &&
+           M * lda * 2 < (int64_t(1) << 31) && g.src_rows * ldb * 2 < (int64_t(1) << 31) && M < (int64_t(1) << 24);
   // c3w_k tiles: 192 k' (three 64-channel slabs of one tap each); fp32 row division exact below 2^24 rows
   return g.ntaps >= 1 && g.ntaps <= 9 && N % 64 == 0 && K % C3W_TK == 0 && K % g.ntaps == 0 &&
          (K / g.ntaps) % 64 == 0 && M * lda * 2 < (int64_t(1) << 31) && g.src_rows * ldb * 2 < (int64_t(1) << 31) &&
          M < (int64_t(1) << 24);
 }
 
+int c3wg_splits(int64_t M, int64_t N, int64_t K, bool chunk_taps) {
+  if (!chunk_taps) return c3w_splits(M, N, K);
+  const int64_t tiles = c3w_tiles(N, K, 128);
+  int64_t s = cdiv(512, tiles);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, M / 512));
+}
+
 void ts_gemm_tn_geo(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
                     int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, const ConvGeo& g,
-                    hipStream_t st) {
+                    hipStream_t st, bool chunk_taps) {
   int64_t chunk = cdiv(cdiv(M, nsplit), 64) * 64;
+  if (chunk_taps) {   // the RGB stem's weight gradient: 64 output channels x 128-wide k' tiles
+    if (N % 128 == 0)
+      hipLaunchKernelGGL((c3w_k<128, 2, 2>), dim3((int)((N / 128) * (K / 128) * nsplit)), dim3(256), 0, st,
+                         (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0,
+                         8, g);
+    else
+      hipLaunchKernelGGL((c3w_k<64, 2, 2>), dim3((int)((N / 64) * (K / 128) * nsplit)), dim3(256), 0, st,
+                         (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0,
+                         8, g);
+    ts_reduce(partial, C, N * K, nsplit, out_dtype, accumulate, st);
+    return;
+  }
   const int cin = (int)(K / g.ntaps);
   if (N % 128 == 0)
     hipLaunchKernelGGL((c3w_k<128, true>), dim3((int)((N / 128) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,

@@ -49,8 +49,11 @@ __device__ __forceinline__ int c3_off(int r, int c) { return r * C3_ROWB + ((c ^
 // round 3 measured that 1.0-1.2x faster than fetching the row and zeroing the fragment registers.
 // GEN: the gathered geometry of kernels.h ConvGeo (strided forward, the parity classes of a strided input gradient):
 // per-lane source pixels from g, the K-step's tap offsets from g's tap table, rows stored to g's destination rows.
-// GEN = false is the stride-1 3x3 path (H, W, the fixed 3x3 taps, identity stores).
-template <int BN, int STAGES, int WM, bool STATS = false, bool GEN = false>
+// GEN = 2 (chunk taps, the 7x7 RGB stem): every 16-B chunk of a K-step is its own tap -- K-step ks, chunk c is tap
+// t = 8 ks + c of g.ntaps, source row (base + (t / g.tdx[0]) Ws + t % g.tdx[0]) of an [src_rows, 8] operand (pairs of
+// 4-channel pixels of a zero-padded image, so no bounds checks); taps past ntaps read tap ntaps - 1 (zero weights).
+// GEN = 0 is the stride-1 3x3 path (H, W, the fixed 3x3 taps, identity stores).
+template <int BN, int STAGES, int WM, bool STATS = false, int GEN = 0>
 __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16* __restrict__ X,
                                                                    const bf16* __restrict__ B, bf16* __restrict__ C,
                                                                    int M, int N, int K, int64_t ldx, int64_t ldb,
@@ -128,11 +131,20 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16*
       dx = tap - (tap / 3) * 3 - 1;
     }
     const unsigned sa = lds0 + stage * STG + wid_u * AI * 1024;
+    if constexpr (GEN == 2) {
 #pragma unroll
-    for (int j = 0; j < AI; ++j) {
-      const bool ok = arow_in[j] && (unsigned)(ay[j] + dy) < (unsigned)Hs && (unsigned)(ax[j] + dx) < (unsigned)Ws;
-      const unsigned off = (unsigned)(((int64_t)(am[j] + dy * Ws + dx) * ldx + cb + ach[j] * 8) * 2);
-      lds_dma16_buf(xres, ok ? off : 0x80000000u, sa + j * 1024);
+      for (int j = 0; j < AI; ++j) {
+        const int t = min(ks * 8 + ach[j], g.ntaps - 1), ty = t / g.tdx[0], tx = t - ty * g.tdx[0];
+        const unsigned off = (unsigned)((int64_t)(am[j] + ty * Ws + tx) * ldx * 2);
+        lds_dma16_buf(xres, arow_in[j] ? off : 0x80000000u, sa + j * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < AI; ++j) {
+        const bool ok = arow_in[j] && (unsigned)(ay[j] + dy) < (unsigned)Hs && (unsigned)(ax[j] + dx) < (unsigned)Ws;
+        const unsigned off = (unsigned)(((int64_t)(am[j] + dy * Ws + dx) * ldx + cb + ach[j] * 8) * 2);
+        lds_dma16_buf(xres, ok ? off : 0x80000000u, sa + j * 1024);
+      }
     }
     const unsigned sb = lds0 + stage * STG + AIMG + wid_u * BI * 1024;
 #pragma unroll
@@ -324,7 +336,10 @@ void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 #undef DPH_C3
 }
 
-bool convg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g) {
+bool convg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g, bool chunk_taps) {
+  if (chunk_taps)   // 8-element rows, one tap per 16-B chunk, K = whole 64-element steps covering ntaps chunks
+    return M > 0 && N % 64 == 0 && lda == 8 && K % 64 == 0 && g.ntaps >= 1 && g.ntaps <= K / 8 && g.tdx[0] > 0 &&
+           g.src_rows * lda * 2 < (int64_t(1) << 31) && N * ldb * 2 < (int64_t(1) << 31) && M < (int64_t(1) << 31);
   // whole 64-channel K-steps of one tap; 32-bit DMA offsets below the padding sentinel; int row arithmetic
   return M > 0 && g.ntaps >= 1 && g.ntaps <= 9 && N % 64 == 0 && K % g.ntaps == 0 && (K / g.ntaps) % 64 == 0 &&
          g.src_rows * lda * 2 < (int64_t(1) << 31) && N * ldb * 2 < (int64_t(1) << 31) && M < (int64_t(1) << 31) &&
@@ -332,21 +347,24 @@ bool convg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, 
 }
 
 void convg_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, const ConvGeo& g, hipStream_t st, float* stats) {
-  const int cin = (int)(K / g.ntaps);
+                int64_t ldc, const ConvGeo& g, hipStream_t st, float* stats, bool chunk_taps) {
+  const int cin = chunk_taps ? 8 : (int)(K / g.ntaps);
   // the stride-1 kernel's tile choice: 128-row tiles of 4 waves, 128 columns unless that leaves < 1.5 WG per CU
   const int nmb = (int)cdiv(M, 128);
   const bool wide = N % 128 == 0 && (int64_t)nmb * (N / 128) >= 384;
-#define DPH_CG(BN_, ST_, STATS_)                                                                                  \
-  hipLaunchKernelGGL((conv3_k<BN_, ST_, 2, STATS_, true>), dim3(nmb * (int)(N / BN_)), dim3(256), 0, st,        \
+#define DPH_CG(BN_, ST_, STATS_, G_)                                                                              \
+  hipLaunchKernelGGL((conv3_k<BN_, ST_, 2, STATS_, G_>), dim3(nmb * (int)(N / BN_)), dim3(256), 0, st,          \
                      (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, 0, 0, cin,   \
                      stats, (const float*)nullptr, g)
-  if (stats) {
-    if (wide) DPH_CG(128, 2, true);
-    else DPH_CG(64, 3, true);
+  if (chunk_taps) {   // the RGB stem: 64 output channels
+    if (stats) DPH_CG(64, 3, true, 2);
+    else DPH_CG(64, 3, false, 2);
+  } else if (stats) {
+    if (wide) DPH_CG(128, 2, true, 1);
+    else DPH_CG(64, 3, true, 1);
   } else {
-    if (wide) DPH_CG(128, 2, false);
-    else DPH_CG(64, 3, false);
+    if (wide) DPH_CG(128, 2, false, 1);
+    else DPH_CG(64, 3, false, 1);
   }
 #undef DPH_CG
 }

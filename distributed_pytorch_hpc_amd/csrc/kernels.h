@@ -181,14 +181,19 @@ struct ConvGeo {
   int tdy[9], tdx[9];
   int64_t src_rows;
 };
-bool convg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g);
+// chunk_taps (the 7x7 RGB stem): every 16-B chunk of the operand's K is its own tap t < ntaps at source row offset
+// (t / tdx[0]) Ws + t % tdx[0] of an [src_rows, 8] operand (pairs of 4-channel pixels of a zero-padded image).
+bool convg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g,
+                     bool chunk_taps = false);
 void convg_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, const ConvGeo& g, hipStream_t stream, float* stats = nullptr);
+                int64_t ldc, const ConvGeo& g, hipStream_t stream, float* stats = nullptr, bool chunk_taps = false);
 // weight gradient C[N, K] (+)= dY[M, N]^T X_gathered[M, K] on c3w_k (K = ntaps * Cin, a multiple of 192)
-bool c3wg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g);
+bool c3wg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g,
+                    bool chunk_taps = false);
+int c3wg_splits(int64_t M, int64_t N, int64_t K, bool chunk_taps);
 void ts_gemm_tn_geo(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
                     int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, const ConvGeo& g,
-                    hipStream_t stream);
+                    hipStream_t stream, bool chunk_taps = false);
 int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K);
 // 3x3 weight gradient on the LDS-DMA kernel (conv1x1.hip c3w_k): supported shapes and its pixel-chunk count
 bool c3w_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);

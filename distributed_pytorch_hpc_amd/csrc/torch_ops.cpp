@@ -797,7 +797,7 @@ dph::ConvGeo make_geo(at::IntArrayRef geo, int64_t src_rows) {
 // C[rows(g), N] (rows stored per g's destination map) = A_gathered[M, K] B[N, K]^T; M = images * Ho * Wo.
 // out (optional): the destination tensor (parity classes of one input gradient share it); stats: BatchNorm partials.
 std::vector<Tensor> convg_nt(const Tensor& A, const Tensor& B, at::IntArrayRef geo, const c10::optional<Tensor>& out,
-                             bool stats) {
+                             bool stats, bool chunk_taps) {
   check_cuda(A, "A");
   c10::DeviceGuard dg(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
@@ -805,10 +805,11 @@ std::vector<Tensor> convg_nt(const Tensor& A, const Tensor& B, at::IntArrayRef g
   const dph::ConvGeo g = make_geo(geo, A.size(0));
   const int64_t imgs = A.size(0) / ((int64_t)g.Hs * g.Ws);
   const int64_t M = imgs * g.Ho * g.Wo, N = B.size(0), K = B.size(1);
-  TORCH_CHECK(K == g.ntaps * A.size(1), "convg_nt: B must be [N, ntaps * Cin]");
+  TORCH_CHECK(chunk_taps ? (A.size(1) == 8 && K % 64 == 0) : K == g.ntaps * A.size(1),
+              "convg_nt: B must be [N, ntaps * Cin] (chunk taps: A [rows, 8], K a multiple of 64)");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
               "convg_nt: row-major operands with 16-B aligned rows required");
-  TORCH_CHECK(dph::convg_supported(M, N, K, A.stride(0), B.stride(0), g),
+  TORCH_CHECK(dph::convg_supported(M, N, K, A.stride(0), B.stride(0), g, chunk_taps),
               "convg_nt: unsupported shape (N % 64, Cin % 64, 32-bit offsets)");
   check_align16(A, "A");
   check_align16(B, "B");
@@ -833,12 +834,12 @@ std::vector<Tensor> convg_nt(const Tensor& A, const Tensor& B, at::IntArrayRef g
     res.push_back(st);
   }
   dph::convg_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0), g,
-                  cur_stream(), sp);
+                  cur_stream(), sp, chunk_taps);
   return res;
 }
 
 // C[N, ntaps * Cin] (+)= dY[M, N]^T X_gathered[M, ntaps * Cin]; X = the [images * Hs * Ws, Cin] input.
-void convg_tn_(Tensor C, const Tensor& A, const Tensor& B, at::IntArrayRef geo, bool accumulate) {
+void convg_tn_(Tensor C, const Tensor& A, const Tensor& B, at::IntArrayRef geo, bool accumulate, bool chunk_taps) {
   check_cuda(A, "A");
   c10::DeviceGuard dg(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.scalar_type() == at::kBFloat16 &&
@@ -846,20 +847,21 @@ void convg_tn_(Tensor C, const Tensor& A, const Tensor& B, at::IntArrayRef geo, 
               "convg_tn_: bf16 2-D operands");
   const dph::ConvGeo g = make_geo(geo, B.size(0));
   const int64_t imgs = B.size(0) / ((int64_t)g.Hs * g.Ws);
-  const int64_t M = A.size(0), N = A.size(1), K = g.ntaps * B.size(1);
+  const int64_t M = A.size(0), N = A.size(1), K = chunk_taps ? C.size(1) : g.ntaps * B.size(1);
+  TORCH_CHECK(!chunk_taps || B.size(1) == 8, "convg_tn_: chunk taps need an [rows, 8] input");
   TORCH_CHECK(M == imgs * g.Ho * g.Wo, "convg_tn_: dY rows must be images * Ho * Wo");
   TORCH_CHECK(C.size(0) == N && C.size(1) == K && C.is_contiguous(), "convg_tn_: C must be [N, ntaps * Cin]");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
               "convg_tn_: row-major operands with 16-B aligned rows required");
-  TORCH_CHECK(dph::c3wg_supported(M, N, K, A.stride(0), B.stride(0), g),
+  TORCH_CHECK(dph::c3wg_supported(M, N, K, A.stride(0), B.stride(0), g, chunk_taps),
               "convg_tn_: unsupported shape (N % 64, ntaps * Cin % 192, Cin % 64)");
   TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "convg_tn_: C bf16 or fp32");
   check_align16(A, "A");
   check_align16(B, "B");
-  const int ns = dph::c3w_splits(M, N, K);
+  const int ns = dph::c3wg_splits(M, N, K, chunk_taps);
   Tensor part = at::empty({(int64_t)ns * N * K}, A.options().dtype(at::kFloat));
   dph::ts_gemm_tn_geo(A.data_ptr(), B.data_ptr(), part.data_ptr<float>(), C.data_ptr(), M, N, K, A.stride(0),
-                      B.stride(0), ns, dt_code(C), accumulate, g, cur_stream());
+                      B.stride(0), ns, dt_code(C), accumulate, g, cur_stream(), chunk_taps);
 }
 
 // Select the wgrad kernel's MFMA shape (16 or 32; anything else re-reads DPH_WGRAD_MFMA); returns the active shape.
@@ -1400,8 +1402,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0, Tensor? pro_ss=None) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("conv3x3_dgrad_weight(Tensor w) -> Tensor");
-  m.def("convg_nt(Tensor A, Tensor B, int[] geo, Tensor? out=None, bool stats=False) -> Tensor[]");
-  m.def("convg_tn_(Tensor(a!) C, Tensor A, Tensor B, int[] geo, bool accumulate) -> ()");
+  m.def("convg_nt(Tensor A, Tensor B, int[] geo, Tensor? out=None, bool stats=False, bool chunk_taps=False) -> Tensor[]");
+  m.def("convg_tn_(Tensor(a!) C, Tensor A, Tensor B, int[] geo, bool accumulate, bool chunk_taps=False) -> ()");
   m.def("ts_gemm_nt_add_sub(Tensor A, Tensor B, Tensor add, int H, int W, int s) -> Tensor");
   m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");

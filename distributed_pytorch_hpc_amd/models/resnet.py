@@ -144,7 +144,12 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.bn1(self.conv1(x)))
+        if isinstance(self.conv1, StemConv2d) and self.bn1.training:
+            # the stem's GEMM epilogue hands bn1 its batch statistics (no statistics pass over the 112^2 activation)
+            s = StatsSlot()
+            x = self.maxpool(self.bn1(self.conv1(x, stats_slot=s), stats_slot=s))
+        else:
+            x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

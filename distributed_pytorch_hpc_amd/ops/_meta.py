@@ -199,7 +199,7 @@ def _ts_gemm_tn(C, A, B, accumulate, H=0, W=0, pro_ss=None):
 
 
 @register_fake("dph::convg_nt")
-def _convg_nt(A, B, geo, out=None, stats=False):
+def _convg_nt(A, B, geo, out=None, stats=False, chunk_taps=False):
     Hs, Ws, Ho, Wo, Hd, Wd = geo[0], geo[1], geo[2], geo[3], geo[8], geo[9]
     imgs = A.shape[0] // (Hs * Ws)
     N = B.shape[0]
@@ -212,7 +212,7 @@ def _convg_nt(A, B, geo, out=None, stats=False):
 
 
 @register_fake("dph::convg_tn_")
-def _convg_tn(C, A, B, geo, accumulate):
+def _convg_tn(C, A, B, geo, accumulate, chunk_taps=False):
     return None
 
 

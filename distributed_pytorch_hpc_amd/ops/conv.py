@@ -586,6 +586,81 @@ class BiasConvTranspose2d(nn.ConvTranspose2d):
 
 
 # ------------------------------------------------------------------------------------------------ RGB stem
+def stem_geometry(H, W, k, p, cin=4):
+    """The k x k / stride-2 stem as a chunk-tap implicit GEMM (csrc/conv3x3.hip conv3_k GEN = 2): the input is
+    zero-padded by p and stored as pairs of 4-channel pixels (16-B rows of 8 bf16), so output pixel (oy, ox) and kernel
+    tap (ky, kx = 2 kxp + px) read pair row (2 oy + ky, ox + kxp); every 16-B chunk of the GEMM's K is one (ky, kxp)
+    tap.  Returns (Hp, Wq, Ho, Wo, kxp, ntaps, K, geo)."""
+    Hp, Wp = H + 2 * p, W + 2 * p
+    Wp += Wp % 2
+    Wq = Wp // 2
+    Ho, Wo = (H + 2 * p - k) // 2 + 1, (W + 2 * p - k) // 2 + 1
+    kxp = (k + 1) // 2
+    ntaps = k * kxp
+    K = -(-ntaps * 8 // 128) * 128
+    geo = conv_geo(Hp, Wq, Ho, Wo, 2, 1, 0, 0, Ho, Wo, 1, 1, 0, 0, [(0, kxp)])
+    geo[14] = ntaps
+    return Hp, Wq, Ho, Wo, kxp, ntaps, K, geo
+
+
+def stem_weight(w: torch.Tensor, kxp: int, K: int) -> torch.Tensor:
+    """[Cout, C <= 4, k, k] -> the chunk-tap operand [Cout, K]: column (ky kxp + j) 8 + 4 px + c = w[co, c, ky, 2j + px]
+    (zero for the 4th channel, kx = k and the K padding)."""
+    co, c, k, _ = w.shape
+    w4 = F.pad(w, (0, 2 * kxp - k, 0, 0, 0, 4 - c))                 # [Cout, 4, k, 2 kxp]
+    wk = w4.view(co, 4, k, kxp, 2).permute(0, 2, 3, 4, 1).reshape(co, k * kxp * 8)
+    return F.pad(wk, (0, K - wk.shape[1])).contiguous()
+
+
+class _StemConvFn(torch.autograd.Function):
+    """The RGB stem (k x k / stride 2, 3 -> Cout channels, no bias) on the framework's chunk-tap implicit GEMM:
+    forward (with the following BatchNorm's statistics when asked) and weight gradient (c3w_k GEN = 2) from one padded
+    pair-pixel copy of the image; the image itself gets no gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, k, p, stats_slot=None):
+        B, C, H, W = x.shape
+        Hp, Wq, Ho, Wo, kxp, ntaps, K, geo = stem_geometry(H, W, k, p)
+        xp = torch.zeros((B, Hp, 2 * Wq, 4), device=x.device, dtype=torch.bfloat16)
+        xp[:, p:p + H, p:p + W, :C] = x.permute(0, 2, 3, 1)
+        a = xp.view(B * Hp * Wq, 8)
+        cout = w.shape[0]
+        wk = stem_weight(w.to(torch.bfloat16), kxp, K)
+        if stats_slot is not None:
+            y2, stats_slot.stats = _lib.ops().convg_nt(a, wk, geo, None, True, True)
+            stats_slot.rows, stats_slot.cols = y2.shape
+        else:
+            y2 = _lib.ops().convg_nt(a, wk, geo, None, False, True)[0]
+        ctx.save_for_backward(a)
+        ctx.cfg = (B, C, H, W, k, p, Ho, Wo, kxp, K, geo, w.shape, w.dtype)
+        return y2.view(B, Ho, Wo, cout).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (a,) = ctx.saved_tensors
+        B, C, H, W, k, p, Ho, Wo, kxp, K, geo, wshape, wdtype = ctx.cfg
+        gw = None
+        if ctx.needs_input_grad[1]:
+            cout = wshape[0]
+            dy2 = _nhwc2d(dy.to(torch.bfloat16))
+            gk = torch.empty((cout, K), device=dy.device, dtype=torch.float32)
+            _lib.ops().convg_tn_(gk, dy2, a, geo, False, True)
+            g5 = gk[:, :k * kxp * 8].view(cout, k, kxp, 2, 4).permute(0, 4, 1, 2, 3).reshape(cout, 4, k, 2 * kxp)
+            gw = g5[:, :C, :, :k].to(wdtype).contiguous(memory_format=torch.channels_last)
+        return None, gw, None, None, None
+
+
+def stem_native_ok(x: torch.Tensor, m: nn.Conv2d) -> bool:
+    if os.environ.get("DPH_STEM_KERNEL", "1") == "0" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
+        return False
+    if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)) or x.requires_grad:
+        return False
+    k = m.kernel_size[0]
+    return (x.dim() == 4 and m.in_channels <= 4 and m.kernel_size == (k, k) and k % 2 == 1 and m.stride == (2, 2)
+            and m.padding == (m.padding[0],) * 2 and m.dilation == (1, 1) and m.groups == 1 and m.bias is None
+            and m.padding_mode == "zeros" and m.out_channels % 64 == 0)
+
+
 class StemConv2d(nn.Conv2d):
     """``nn.Conv2d`` for a 3-channel (RGB) image stem whose channels-last GPU path zero-pads the input channels to 4.
 
@@ -596,7 +671,11 @@ class StemConv2d(nn.Conv2d):
     exactly the 3-channel one; the parameter keeps its [Cout, 3, k, k] shape (state dicts unchanged) and receives
     the gradient of its own 3 channels."""
 
-    def forward(self, x):
+    def forward(self, x, stats_slot: StatsSlot | None = None):
+        if stem_native_ok(x, self):
+            _lib.require()
+            return _StemConvFn.apply(x, self.weight, self.kernel_size[0], self.padding[0],
+                                     stats_slot if _conv3_stats_ok() else None)
         if not (self.in_channels == 3 and self.groups == 1 and x.is_cuda and x.dim() == 4
                 and self.padding_mode == "zeros" and not isinstance(self.padding, str)
                 and x.is_contiguous(memory_format=torch.channels_last) and _lib.use_native(x)):

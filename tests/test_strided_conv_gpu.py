@@ -155,3 +155,37 @@ def test_downsample_hands_sub_gradient_to_conv1(dph_native, monkeypatch):
     block(x).float().pow(2).mean().backward()
     assert made and made[0].armed and made[0].sub == (2, 14, 14) and made[0].t is None
     assert x.grad is not None and torch.isfinite(x.grad.float()).all()
+
+
+@pytest.mark.parametrize("B,H,W,Co,k,p", [(2, 224, 224, 64, 7, 3), (3, 37, 50, 64, 7, 3), (2, 32, 32, 128, 5, 2)])
+@pytest.mark.parametrize("autocast", [False, True])
+def test_stem_conv_matches_conv2d(dph_native, B, H, W, Co, k, p, autocast):
+    """The RGB stem on the chunk-tap implicit GEMM (forward + weight gradient) vs F.conv2d in fp32, with the
+    following BatchNorm's statistics from the epilogue."""
+    from distributed_pytorch_hpc_amd.ops.conv import StatsSlot, StemConv2d, stem_native_ok
+
+    torch.manual_seed(2)
+    conv = StemConv2d(3, Co, k, 2, p, bias=False).to(DEV).to(memory_format=torch.channels_last)
+    if not autocast:
+        conv = conv.to(torch.bfloat16)
+    x = torch.randn(B, 3, H, W, device=DEV, dtype=torch.float32 if autocast else torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    slot = StatsSlot()
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        assert stem_native_ok(x, conv)
+        y = conv(x, stats_slot=slot)
+    g = torch.randn_like(y.float())
+    y.float().backward(g)
+    xr = x.detach().to(torch.bfloat16).float()
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_()
+    yr = torch.nn.functional.conv2d(xr, wr, stride=2, padding=p)
+    yr.backward(g)
+    assert y.shape == yr.shape
+    assert rel_err(y, yr) < 8e-3
+    assert rel_err(conv.weight.grad, wr.grad) < 1e-2
+    y2 = y.permute(0, 2, 3, 1).reshape(-1, Co).float()
+    nmb = (y2.shape[0] + 127) // 128
+    st = slot.stats
+    rows = st[2 * nmb * Co:]
+    mean = (st[:nmb * Co].view(nmb, Co) * rows[:, None]).sum(0) / rows.sum()
+    assert rel_err(mean, y2.mean(0)) < 1e-3
