@@ -59,7 +59,8 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16*
                                                                    int M, int N, int K, int64_t ldx, int64_t ldb,
                                                                    int64_t ldc, int H, int W, int Cin,
                                                                    float* __restrict__ stats,
-                                                                   const float* __restrict__ bias, ConvGeo g) {
+                                                                   const void* __restrict__ bias, ConvGeo g,
+                                                                   bool bias_bf16) {
   constexpr int NWV = 2 * WM, NTH = 64 * NWV, BM = 64 * WM;
   constexpr int AIMG = BM * C3_ROWB, BIMG = BN * C3_ROWB, STG = AIMG + BIMG;
   constexpr int AI = BM / 8 / NWV;         // A DMA pieces (8 rows) per wave per K-step (4)
@@ -200,10 +201,11 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16*
         for (int j = 0; j < NTW; ++j) acc[i][j] = c3_mfma(a[f][i], b[f][j], acc[i][j]);
   }
   __syncthreads();
-  if (bias != nullptr) {   // per-output-channel bias (fp32) on the accumulators: C and its statistics include it
+  if (bias != nullptr) {   // per-output-channel bias (fp32 or bf16) on the accumulators: C and its statistics include it
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
-      const float bj = bias[n0 + wn * WN + j * 32 + l32];
+      const int bc = n0 + wn * WN + j * 32 + l32;
+      const float bj = bias_bf16 ? (float)reinterpret_cast<const bf16*>(bias)[bc] : reinterpret_cast<const float*>(bias)[bc];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -296,7 +298,7 @@ bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) 
 }
 
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, int H, int W, hipStream_t st, float* stats, const float* bias) {
+                int64_t ldc, int H, int W, hipStream_t st, float* stats, const void* bias, bool bias_bf16) {
   const int cin = (int)(K / 9);
   static const int force_bn = [] {
     const char* e = getenv("DPH_CONV3_BN");
@@ -317,7 +319,7 @@ void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 #define DPH_C3(BN_, ST_, WM_, STATS_)                                                                            \
   hipLaunchKernelGGL((conv3_k<BN_, ST_, WM_, STATS_>), dim3(nmb * (int)(N / BN_)), dim3(128 * WM_), 0, st,    \
                      (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin,  \
-                     stats, bias, ConvGeo{})
+                     stats, bias, ConvGeo{}, bias_bf16)
   if (wm == 4) {
     if (stats) {
       if (wide) DPH_C3(128, 3, 4, true);
@@ -355,7 +357,7 @@ void convg_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 #define DPH_CG(BN_, ST_, STATS_, G_)                                                                              \
   hipLaunchKernelGGL((conv3_k<BN_, ST_, 2, STATS_, G_>), dim3(nmb * (int)(N / BN_)), dim3(256), 0, st,          \
                      (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, 0, 0, cin,   \
-                     stats, (const float*)nullptr, g)
+                     stats, (const void*)nullptr, g, false)
   if (chunk_taps) {   // the RGB stem: 64 output channels
     if (stats) DPH_CG(64, 3, true, 2);
     else DPH_CG(64, 3, false, 2);

@@ -167,7 +167,8 @@ void ts_gemm_nt_add_sub(const void* A, const void* B, void* C, const void* D, in
 // 3x3 implicit GEMM with an LDS-DMA pipeline (csrc/conv3x3.hip); ts_gemm_nt's H, W > 0 path when supported.
 bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, int H, int W, hipStream_t stream, float* stats = nullptr, const float* bias = nullptr);
+                int64_t ldc, int H, int W, hipStream_t stream, float* stats = nullptr, const void* bias = nullptr,
+                bool bias_bf16 = false);
 // Gathered implicit GEMM: strided and parity-class (strided-dgrad) convolutions on the same LDS-DMA kernels.
 // GEMM rows m = (n, oy, ox) over an Ho x Wo grid.  The gathered operand's row for output row m and tap t is the pixel
 //   (n Hs + sy oy + by + tdy[t]) Ws + sx ox + bx + tdx[t]     -- zero-filled when outside the Hs x Ws image --

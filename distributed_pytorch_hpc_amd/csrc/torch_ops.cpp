@@ -674,11 +674,11 @@ Tensor ts_gemm_nt(const Tensor& A, const Tensor& B, int64_t H, int64_t W, const 
   if (bias.has_value()) {   // 3x3 with a per-output-channel fp32 bias in the LDS-DMA kernel's epilogue
     TORCH_CHECK(H > 0 && !add.has_value() && dph::conv3_supported(M, N, K, A.stride(0), B.stride(0)),
                 "ts_gemm_nt: bias is supported on the 3x3 LDS-DMA path only");
-    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous() &&
-                    bias->device() == A.device(),
-                "ts_gemm_nt: bias must be a contiguous fp32 [N] tensor");
+    TORCH_CHECK((bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16) && bias->numel() == N &&
+                    bias->is_contiguous() && bias->device() == A.device(),
+                "ts_gemm_nt: bias must be a contiguous fp32 / bf16 [N] tensor");
     dph::conv3_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
-                    (int)H, (int)W, cur_stream(), nullptr, bias->data_ptr<float>());
+                    (int)H, (int)W, cur_stream(), nullptr, bias->data_ptr(), bias->scalar_type() == at::kBFloat16);
     return C;
   }
   const float* pro = pro_ptr(pro_ss, K, H, A);
@@ -735,11 +735,12 @@ std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B, in
   Tensor st = at::empty({2 * nmb * N + nmb}, A.options().dtype(at::kFloat));
   if (bias.has_value()) {   // 3x3 LDS-DMA kernel: fp32 bias on the accumulators, statistics of the biased output
     TORCH_CHECK(H > 0 && !pro_ss.has_value(), "ts_gemm_nt_stats: bias is a 3x3 (H > 0) feature");
-    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous() &&
-                    bias->device() == A.device(),
-                "ts_gemm_nt_stats: bias must be a contiguous fp32 [N] tensor");
+    TORCH_CHECK((bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16) && bias->numel() == N &&
+                    bias->is_contiguous() && bias->device() == A.device(),
+                "ts_gemm_nt_stats: bias must be a contiguous fp32 / bf16 [N] tensor");
     dph::conv3_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),
-                    (int)H, (int)W, cur_stream(), st.data_ptr<float>(), bias->data_ptr<float>());
+                    (int)H, (int)W, cur_stream(), st.data_ptr<float>(), bias->data_ptr(),
+                    bias->scalar_type() == at::kBFloat16);
     return {C, st};
   }
   dph::ts_gemm_nt(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0),

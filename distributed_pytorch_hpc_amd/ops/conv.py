@@ -237,6 +237,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         else:
             y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W)
         ctx.has_bias = bias is not None
+        ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.wgrad = wgrad
         ctx.save_for_backward(x2, wb)
         ctx.shape, ctx.wdtype, ctx.param = (B, C, H, W), wdtype, w
@@ -276,7 +277,7 @@ class _Conv3x3Fn(torch.autograd.Function):
                 gw = gk.view(cout, 3, 3, C).permute(0, 3, 1, 2).contiguous()
         db = None
         if ctx.has_bias and ctx.needs_input_grad[3]:
-            db = _lib.ops().channel_sum(dy2, torch.float32)
+            db = _lib.ops().channel_sum(dy2, ctx.bias_dtype)   # in the bias's own dtype: no cast kernel
         return dx, gw, None, db, None
 
 
@@ -569,7 +570,7 @@ class BiasConv2d(nn.Conv2d):
         epilogue (SimpleUNet's conv -> BN blocks, models/unet.py); otherwise the slot stays empty."""
         if _bias_conv3x3_ok(self, x):
             _lib.require()
-            b = self.bias if self.bias.dtype == torch.float32 else self.bias.float()
+            b = self.bias if self.bias.dtype in (torch.float32, torch.bfloat16) else self.bias.float()
             return _Conv3x3Fn.apply(x, self.weight, stats_slot, b, _conv3_wgrad("dph"))
         if _bias_conv_ok(self, x):
             return _bias_conv(self, x, False, (0, 0))
