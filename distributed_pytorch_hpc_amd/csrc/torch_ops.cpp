@@ -776,7 +776,7 @@ void ts_gemm_tn_(Tensor C, const Tensor& A, const Tensor& B, bool accumulate, in
 
 // ---------------------------------------------------------------- gathered implicit GEMM (strided convolutions)
 // geo = [Hs, Ws, Ho, Wo, sy, sx, by, bx, Hd, Wd, ty, tx, tby, tbx, ntaps, tdy[0..8], tdx[0..8]] (kernels.h ConvGeo)
-dph::ConvGeo make_geo(at::IntArrayRef geo, int64_t src_rows) {
+dph::ConvGeo make_geo(at::IntArrayRef geo, int64_t src_rows, bool chunk_taps = false) {
   TORCH_CHECK(geo.size() == 15 + 18, "conv geometry: 33 integers expected");
   dph::ConvGeo g{};
   int* f[15] = {&g.Hs, &g.Ws, &g.Ho, &g.Wo, &g.sy, &g.sx, &g.by, &g.bx, &g.Hd, &g.Wd, &g.ty, &g.tx, &g.tby, &g.tbx, &g.ntaps};
@@ -786,8 +786,9 @@ dph::ConvGeo make_geo(at::IntArrayRef geo, int64_t src_rows) {
     g.tdx[t] = (int)geo[24 + t];
   }
   g.src_rows = src_rows;
-  TORCH_CHECK(g.Hs > 0 && g.Ws > 0 && g.Ho > 0 && g.Wo > 0 && g.Hd > 0 && g.Wd > 0 && g.ntaps >= 1 && g.ntaps <= 9,
-              "conv geometry: positive grids and 1..9 taps required");
+  TORCH_CHECK(g.Hs > 0 && g.Ws > 0 && g.Ho > 0 && g.Wo > 0 && g.Hd > 0 && g.Wd > 0 && g.ntaps >= 1 &&
+                  (chunk_taps ? g.tdx[0] > 0 : g.ntaps <= 9),
+              "conv geometry: positive grids and 1..9 taps required (chunk taps: any count, tdx[0] taps per row)");
   TORCH_CHECK(src_rows % ((int64_t)g.Hs * g.Ws) == 0, "conv geometry: source rows must be whole Hs x Ws images");
   // every destination row of every image must land inside the Hd x Wd grid (scatter bound, checked on the host)
   const int64_t ymax = (int64_t)g.ty * (g.Ho - 1) + g.tby, xmax = (int64_t)g.tx * (g.Wo - 1) + g.tbx;
@@ -803,7 +804,7 @@ std::vector<Tensor> convg_nt(const Tensor& A, const Tensor& B, at::IntArrayRef g
   c10::DeviceGuard dg(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
               "convg_nt: bf16 2-D operands");
-  const dph::ConvGeo g = make_geo(geo, A.size(0));
+  const dph::ConvGeo g = make_geo(geo, A.size(0), chunk_taps);
   const int64_t imgs = A.size(0) / ((int64_t)g.Hs * g.Ws);
   const int64_t M = imgs * g.Ho * g.Wo, N = B.size(0), K = B.size(1);
   TORCH_CHECK(chunk_taps ? (A.size(1) == 8 && K % 64 == 0) : K == g.ntaps * A.size(1),
@@ -846,7 +847,7 @@ void convg_tn_(Tensor C, const Tensor& A, const Tensor& B, at::IntArrayRef geo, 
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.scalar_type() == at::kBFloat16 &&
                   B.scalar_type() == at::kBFloat16,
               "convg_tn_: bf16 2-D operands");
-  const dph::ConvGeo g = make_geo(geo, B.size(0));
+  const dph::ConvGeo g = make_geo(geo, B.size(0), chunk_taps);
   const int64_t imgs = B.size(0) / ((int64_t)g.Hs * g.Ws);
   const int64_t M = A.size(0), N = A.size(1), K = chunk_taps ? C.size(1) : g.ntaps * B.size(1);
   TORCH_CHECK(!chunk_taps || B.size(1) == 8, "convg_tn_: chunk taps need an [rows, 8] input");
