@@ -32,8 +32,11 @@ class ConvBlock(nn.Sequential):
 
     def forward(self, x):
         for conv, bn in ((self[0], self[1]), (self[3], self[4])):
-            slot = StatsSlot() if bn.training and _CONV_STATS else None
-            x = bn(conv(x, stats_slot=slot), stats_slot=slot)
+            if isinstance(conv, BiasConv2d) and isinstance(bn, BatchNormAct2d) and bn.training and _CONV_STATS:
+                slot = StatsSlot()
+                x = bn(conv(x, stats_slot=slot), stats_slot=slot)
+            else:   # modules swapped in by a wrapper (e.g. the halo convolutions of parallel/domain.py)
+                x = bn(conv(x))
         return x
 
 
