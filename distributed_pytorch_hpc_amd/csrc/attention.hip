@@ -1042,9 +1042,11 @@ static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
   }
   const size_t lds_q = 2 * 2 * 64 * HD * 2;
   const dim3 grid_q((unsigned)((p.Sq + 32 * NW - 1) / (32 * NW) * p.Hq * p.B));
+  // default 2 (no register spills): backward 682.5 / 681.6 / 679.8 vs 677.1 / 680.1 / 679.2 TFLOP/s with 0, interleaved
+  // on one MI355X (profiles/r4/attn_dq/)
   static const int dq_var = [] {
     const char* e = getenv("DPH_ATTN_DQ_VAR");
-    return e ? atoi(e) : (kAttnDqDefaultPf ? 1 : 0);
+    return e ? atoi(e) : (kAttnDqDefaultPf ? 1 : 2);
   }();
   if (dq_var == 2) {   // quarter-sub-tile K / V read-ahead (no spills)
     if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW, false, false, 4>), grid_q, dim3(64 * NW), lds_q, st, P);

@@ -715,9 +715,11 @@ static int64_t c3w_tiles(int64_t N, int64_t K, int64_t tk) { return (N / (N % 12
 static int w1_tk(int64_t K) { return K % 128 == 0 ? 128 : 64; }
 
 bool w1_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
-  static const bool on = [] {   // A/B knob: DPH_W1_KERNEL=0 keeps the register-staged ts_tn_k
+  // opt-in (DPH_W1_KERNEL=1): on ResNet-50's twelve 1x1 shapes it is 0.87-1.16x the register-staged ts_tn_k, 2.609 vs
+  // 2.535 ms per step in total (both ahead of MIOpen's 3.139; profiles/r4/conv1x1_wgrad/)
+  static const bool on = [] {
     const char* e = getenv("DPH_W1_KERNEL");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on && N % 64 == 0 && K % 64 == 0 && M * lda * 2 < (int64_t(1) << 31) && M * ldb * 2 < (int64_t(1) << 31) &&
          M < (int64_t(1) << 24);
