@@ -889,6 +889,22 @@ Tensor channel_sum(const Tensor& x, at::ScalarType out_dtype) {
   return out;
 }
 
+// channel_sum written into an existing [C] buffer (a parameter's gradient-bucket view: no separate copy)
+void channel_sum_into_(const Tensor& x, Tensor out) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK((x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast)) || (x.dim() == 2 && x.is_contiguous()),
+              "channel_sum_into_: channels-last [N, C, H, W] or contiguous [M, C]");
+  const int64_t C = x.size(1), M = C ? x.numel() / C : 0;
+  TORCH_CHECK(out.numel() == C && out.is_contiguous() && out.device() == x.device() &&
+                  (out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16),
+              "channel_sum_into_: out must be a contiguous fp32 / bf16 tensor of C elements");
+  if (C == 0) return;
+  auto part = at::empty({(int64_t)dph::chsum_partial_blocks(M, C) * C}, x.options().dtype(at::kFloat));
+  dph::chsum(x.data_ptr(), part.data_ptr<float>(), out.data_ptr(), M, C, dt_code(x),
+             out.scalar_type() == at::kBFloat16 ? dph::kBF16 : dph::kF32, cur_stream());
+}
+
 // ------------------------------------------------------------------------------------------------ max pooling
 // x: channels-last [N, C, H, W], C % 8 == 0; k = 3 (3x3 / 2 / 1) or 2 (2x2 / 2 / 0).
 // Returns (y channels-last [N, C, Ho, Wo], tap uint8 [N, Ho, Wo, C]).
@@ -1409,6 +1425,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("ts_gemm_nt_add_sub(Tensor A, Tensor B, Tensor add, int H, int W, int s) -> Tensor");
   m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
+  m.def("channel_sum_into_(Tensor x, Tensor(a!) out) -> ()");
   m.def("maxpool_s2_bwd(Tensor dy, Tensor tap, int H, int W, int k) -> Tensor");
   m.def("upcat_fwd(Tensor y2, Tensor? bias, Tensor skip, int H, int W) -> Tensor");
   m.def("upcat_bwd(Tensor dcat, int H, int W, int Co) -> (Tensor, Tensor)");
@@ -1475,6 +1492,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("ts_gemm_nt_add_sub", &ts_gemm_nt_add_sub);
   m.impl("maxpool_s2_fwd", &maxpool_s2_fwd);
   m.impl("channel_sum", &channel_sum);
+  m.impl("channel_sum_into_", &channel_sum_into_);
   m.impl("maxpool_s2_bwd", &maxpool_s2_bwd);
   m.impl("upcat_fwd", &upcat_fwd);
   m.impl("upcat_bwd", &upcat_bwd);

@@ -302,3 +302,8 @@ def _gemm_nt_rope(x, w, cos, sin, S, hd, n_rot, pos_off):
 @register_fake("dph::flash_attn_fwd_merge_")
 def _flash_attn_fwd_merge(q, k, v, scale, causal, acc_o, acc_lse):
     return None
+
+
+@register_fake("dph::channel_sum_into_")
+def _channel_sum_into(x, out):
+    return None

@@ -71,6 +71,19 @@ def _main_grad_target(w: torch.Tensor, shape):
     return mg.view(shape)
 
 
+def bias_grad(param, dy2: torch.Tensor, dtype):
+    """Per-channel sum of dy (a convolution's bias gradient), written straight into the engine-owned gradient bucket
+    view of ``param`` when there is one (engine notified, None returned), else returned in ``dtype``."""
+    mg = getattr(param, "main_grad", None) if param is not None else None
+    if (mg is not None and _DIRECT and not getattr(param, "_dph_accum", False) and mg.is_contiguous()
+            and mg.dtype in (torch.float32, torch.bfloat16)):
+        _lib.ops().channel_sum_into_(dy2, mg.view(-1))
+        param._dph_accum = True
+        param._dph_grad_ready()
+        return None
+    return _lib.ops().channel_sum(dy2, dtype)   # in the bias's own dtype: no cast kernel
+
+
 def _wgrad_into_main(w: torch.Tensor, shape, launch) -> bool:
     """Run ``launch(out, accumulate)`` straight into the engine's gradient bucket and notify the engine (no
     autograd gradient, no post-accumulate copy).  False when ``w`` has no engine-owned buffer."""
@@ -238,6 +251,7 @@ class _Conv3x3Fn(torch.autograd.Function):
             y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W)
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.bias_param = bias if isinstance(bias, nn.Parameter) else None
         ctx.wgrad = wgrad
         ctx.save_for_backward(x2, wb)
         ctx.shape, ctx.wdtype, ctx.param = (B, C, H, W), wdtype, w
@@ -277,7 +291,7 @@ class _Conv3x3Fn(torch.autograd.Function):
                 gw = gk.view(cout, 3, 3, C).permute(0, 3, 1, 2).contiguous()
         db = None
         if ctx.has_bias and ctx.needs_input_grad[3]:
-            db = _lib.ops().channel_sum(dy2, ctx.bias_dtype)   # in the bias's own dtype: no cast kernel
+            db = bias_grad(ctx.bias_param, dy2, ctx.bias_dtype)
         return dx, gw, None, db, None
 
 
@@ -520,6 +534,7 @@ class _ConvBiasFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.cfg = (stride, padding, dilation, transposed, output_padding, groups)
         ctx.bdtype = b.dtype
+        ctx.bias_param = b if isinstance(b, nn.Parameter) else None
         return y
 
     @staticmethod
@@ -533,7 +548,7 @@ class _ConvBiasFn(torch.autograd.Function):
             dx, dw, _ = torch.ops.aten.convolution_backward(dy, x, w, None, stride, padding, dilation, transposed,
                                                             output_padding, groups, [nx, nw, False])
         if nb:
-            db = _lib.ops().channel_sum(dy, ctx.bdtype)
+            db = bias_grad(ctx.bias_param, dy, ctx.bdtype)
         return dx, dw, db, None, None, None, None, None, None
 
 

@@ -861,6 +861,29 @@ def test_bias_conv3x3_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W):
     assert rel_err(conv.bias.grad, br.grad) < 1e-3
 
 
+@pytest.mark.parametrize("k", [3, 1])
+def test_bias_conv_bias_grad_into_bucket(dph_native, k):
+    """With an engine-owned main_grad the bias gradient (per-channel sum of dY) is written straight into the bucket
+    view (3x3 kernel path and the MIOpen path of other convolutions alike): no autograd gradient, engine notified."""
+    from distributed_pytorch_hpc_amd.ops.conv import BiasConv2d
+
+    torch.manual_seed(6)
+    conv = BiasConv2d(64, 128 if k == 3 else 65, k, padding=k // 2).to(DEV).to(torch.bfloat16).to(
+        memory_format=torch.channels_last)
+    b = conv.bias
+    b.main_grad = torch.zeros(b.shape, device=DEV, dtype=torch.bfloat16)
+    calls = []
+    b._dph_grad_ready = lambda: calls.append(1)
+    b._dph_accum = False
+    x = torch.randn(2, 64, 12, 13, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = conv(x)
+    g = torch.randn_like(y)
+    y.backward(g)
+    assert b.grad is None and calls == [1]
+    ref = g.float().sum((0, 2, 3))
+    assert rel_err(b.main_grad, ref) < 1e-2
+
+
 def test_unet_conv_block_stats_from_conv_epilogue(dph_native):
     """SimpleUNet's ConvBlock: each training-mode BN takes its batch statistics (of the biased output) from the 3x3
     convolution's epilogue; output, running statistics and gradients equal the path where BN runs its own pass."""
