@@ -205,9 +205,11 @@ def main(argv=None):
         sync()
 
     loss = None
+    log(f"[bench] {args.layout}: workload built, {args.warmup} warm-up + {args.steps} timed steps")
     for i in range(args.warmup):
         loss = wl.step(i)
     first_loss = float(loss.detach()) if loss is not None else None
+    log(f"[bench] warm-up done (loss {first_loss})")
     wl.engine.synchronize()
     sync_all()
     # ---- replicas must hold bitwise-identical parameters after the warm-up updates ----

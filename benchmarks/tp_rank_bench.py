@@ -76,8 +76,11 @@ def main(argv=None):
         engine.step()
         engine.zero_grad()
 
-    for _ in range(a.warmup):
+    print(f"[tp_rank] model built and sharded (tp {a.tp}): {info}", flush=True)
+    for i in range(a.warmup):
         step()
+        torch.cuda.synchronize()
+        print(f"[tp_rank] warm-up step {i} done", flush=True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
