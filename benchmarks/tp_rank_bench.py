@@ -47,6 +47,10 @@ def main(argv=None):
     from distributed_pytorch_hpc_amd.parallel.tensor_parallel import parallelize_llama
 
     _lib.require()
+    if os.environ.get("DPH_STACK_DUMP_S"):   # diagnostics: the Python stack of every thread every N seconds
+        import faulthandler
+
+        faulthandler.dump_traceback_later(int(os.environ["DPH_STACK_DUMP_S"]), repeat=True, file=sys.stderr)
     if a.gemm_nt is not None or a.fused_qkv is not None:
         fused_layers.set_enabled(gemm_nt=a.gemm_nt, qkv=None if a.fused_qkv is None else bool(a.fused_qkv))
     dist.init_process_group("fake", store=FakeStore(), rank=0, world_size=a.tp)
@@ -70,10 +74,20 @@ def main(argv=None):
     g = torch.Generator(device=dev).manual_seed(0)
     t = torch.randint(0, margs.vocab_size, (a.batch, a.seq + 1), device=dev, generator=g)
 
+    debug = bool(os.environ.get("DPH_STACK_DUMP_S"))
+
+    def mark(what):
+        if debug:
+            torch.cuda.synchronize()
+            print(f"[tp_rank] {what} done", flush=True)
+
     def step():
         loss = model(t[:, :-1], t[:, 1:])
+        mark("forward")
         loss.backward()
+        mark("backward")
         engine.step()
+        mark("optimizer step")
         engine.zero_grad()
 
     print(f"[tp_rank] model built and sharded (tp {a.tp}): {info}", flush=True)
