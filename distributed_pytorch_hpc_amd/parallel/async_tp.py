@@ -87,10 +87,10 @@ def _k_major(w: torch.Tensor, transpose_w: bool) -> torch.Tensor:
 def _ag_matmul(x: torch.Tensor, w: torch.Tensor, group, k: int, transpose_w: bool):
     """AG(x) @ op(w) with k pipelined micro all-gathers; x [B, Sl, D].  Returns (y [B, S, N], gathered [k,P,B,m,D]).
 
-    The micro all-gathers land in slots of ONE chunk-major buffer (kept for the weight gradient: no stack).  With one
-    sequence per rank (B = 1) micro-GEMM i writes its [P, m, N] result straight into its rank-major sequence rows of
-    y -- one strided-batched GEMM whose output batch stride is k m N, no copy; otherwise its [P, B, m, N] result is
-    copied once into place (overlapping the next micro all-gather)."""
+    The micro all-gathers land in slots of ONE chunk-major buffer (kept for the weight gradient: no stack); each
+    micro-GEMM is one 2-D GEMM whose [P, B, m, N] result is copied once into its rank-major sequence rows (overlapping
+    the next micro all-gather).  A strided-batched GEMM writing those rows directly would need the weight broadcast at
+    batch stride 0, which hipBLASLt on this stack rejects (parallel/linear.py _mm2d)."""
     B, Sl, D = x.shape
     P = _ws(group)
     m = Sl // k
@@ -102,10 +102,8 @@ def _ag_matmul(x: torch.Tensor, w: torch.Tensor, group, k: int, transpose_w: boo
     yv = y.view(B, P, k, m, N)
     for i, (g, work) in enumerate(pend):
         work.wait()
-        if B == 1:
-            torch.bmm(g.view(P, m, D), wk.t().expand(P, D, N), out=yv[0, :, i])
-        else:
-            yv[:, :, i].copy_(torch.matmul(g, wk.t()).permute(1, 0, 2, 3))   # [P, B, m, N] -> sequence order
+        yi = torch.mm(g.reshape(-1, D), wk.t()).view(P, B, m, N)   # one 2-D GEMM (no batch-stride-0 broadcast)
+        yv[:, :, i].copy_(yi.permute(1, 0, 2, 3))                   # [P, B, m, N] -> rank-major sequence order
     return y, xg.view(k, P, B, m, D)
 
 
@@ -119,7 +117,7 @@ def _matmul_rs(x_cm: torch.Tensor, w: torch.Tensor, group, transpose_w: bool) ->
     y = torch.empty((B, k * m, N), dtype=x_cm.dtype, device=x_cm.device) if B == 1 else None
     pend = []
     for i in range(k):
-        part = torch.matmul(x_cm[i], wk.t())
+        part = torch.mm(x_cm[i].reshape(-1, x_cm.shape[-1]), wk.t()).view(*x_cm.shape[1:-1], N)
         pend.append(_rs_async(part, group, y[:, i * m:(i + 1) * m] if y is not None else None))
     outs = []
     for o, work in pend:

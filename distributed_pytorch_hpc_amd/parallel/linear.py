@@ -100,6 +100,8 @@ def _fwd_gemm(x: torch.Tensor, w: torch.Tensor, b=None) -> torch.Tensor:
         from ..ops import _lib
 
         return _lib.ops().gemm_nt(x, w)
+    if x.dim() > 2 and not x.is_contiguous():
+        x = x.contiguous()   # F.linear folds a contiguous input into one 2-D GEMM (see _mm2d)
     return F.linear(x, w, b)
 
 
@@ -116,8 +118,19 @@ def _dgrad(gy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
             gyc = gy.contiguous()
             if _nt_ok(gyc, wt):
                 return _lib.ops().gemm_nt(gyc, wt)
-            return torch.matmul(gy, wt.t())
-    return torch.matmul(gy, w)
+            return _mm2d(gyc, wt.t())
+    return _mm2d(gy, w)
+
+
+def _mm2d(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a [..., K] @ b [K, N] as ONE 2-D GEMM over the folded leading dims.  torch.matmul of a non-contiguous 3-D
+    ``a`` (e.g. a sequence-parallel all-gather's view) with a 2-D ``b`` becomes a batched GEMM with ``b`` broadcast
+    at batch stride 0, which hipBLASLt on this stack rejects (HIPBLAS_STATUS_INTERNAL_ERROR) and whose rocBLAS
+    fallback faulted the GPU (illegal address) on the tensor-parallel w2 input gradient."""
+    if a.dim() == 2:
+        return torch.mm(a, b)
+    lead = a.shape[:-1]
+    return torch.mm(a.reshape(-1, a.shape[-1]), b).view(*lead, b.shape[-1])
 
 
 def weight_grad(w: torch.Tensor, g2: torch.Tensor, x2: torch.Tensor):
@@ -225,6 +238,8 @@ def linear(x, w, b=None):
         return _fp8.fp8_linear(x, w)   # opt-in FP8 GEMMs (ops/fp8.py)
     if getattr(w, "main_grad", None) is not None and torch.is_grad_enabled() and w.requires_grad:
         return _LinearFn.apply(x, w, b)
+    if x.is_cuda and x.dim() > 2 and not x.is_contiguous():
+        x = x.contiguous()   # one folded 2-D GEMM, not a batched GEMM with the weight broadcast (see _mm2d)
     return F.linear(x, w, b)
 
 

@@ -48,3 +48,21 @@ def test_ag_matmul_rank_major_rows(monkeypatch, B, k, transpose_w):
     # the gathered buffer is chunk-major [k, P, B, m, D] (the weight gradient's operand)
     m = Sl // k
     assert torch.equal(xg[1, 3], (x[:, m:2 * m] + 3))
+
+
+def test_dgrad_of_noncontiguous_3d_grad_is_one_2d_gemm(dph_native):
+    """The input gradient of a linear layer whose incoming gradient is a non-contiguous 3-D view (the adjoint of a
+    sequence-parallel reduce-scatter): folded into one 2-D GEMM (torch.matmul would broadcast the weight at batch
+    stride 0, which hipBLASLt on this stack rejects and whose fallback faulted the GPU at the TP = 8 w2 shape)."""
+    from distributed_pytorch_hpc_amd.parallel.linear import _dgrad
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    base = torch.randn(1024, 4, 4096, device=dev, generator=g).to(torch.bfloat16)
+    gy = base.transpose(0, 1)                                       # [4, 1024, 4096]: leading dims not foldable
+    assert not gy.is_contiguous()
+    w = (0.02 * torch.randn(4096, 1376, device=dev, generator=g)).to(torch.bfloat16)
+    dx = _dgrad(gy, w)
+    ref = gy.float() @ w.float()
+    assert dx.shape == (4, 1024, 1376)
+    assert ((dx.float() - ref).norm() / ref.norm()).item() < 5e-3
