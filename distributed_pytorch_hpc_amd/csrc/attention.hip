@@ -561,7 +561,9 @@ __global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ o, 
 // S and dP are computed with the key on the lane, so P and dS are directly the B operands of
 // dV^T += dO^T P and dK^T += Q^T dS: no LDS round trip, no atomics.
 // VAR (A/B knob, DPH_ATTN_BWD_VAR): bit 0 = row constants as the initial S / dP accumulators (no dropout), bit 1 =
-// the dV / dK transposed reads software-pipelined one step ahead, the first step issued before the softmax.
+// the dV / dK transposed reads software-pipelined one step ahead, the first step issued before the softmax, bit 2 =
+// issue priority 1 while a wave is in its MFMA chains (S / dP, then dV / dK) and 0 in its softmax, so the partner
+// wave on the SIMD (the other workgroup's) fills the chains' gaps with its softmax instead of competing for issue.
 template <int HD, bool CAUSAL, int NW, bool DROP = false, int VAR = 0>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams P) {
   constexpr int NT = 64 * NW, BNK = 32 * NW, BMQ = 32, NC = HD / 8, KS = HD / 16, DT = HD / 32;
@@ -707,6 +709,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
     if (!(CAUSAL && key0 > qt0 + BMQ - 1 + off)) {
       const float* ls = lse_s + buf * BMQ;
       const float* ds = del_s + buf * BMQ;
+      if constexpr ((VAR & 4) != 0) __builtin_amdgcn_s_setprio(1);
       f32x16 s = mfma32(lds_b128(Ql, qro[0]), lds_b128(Kimg, kofs(0)), RINIT ? row_init(ls) : zacc);
       f32x16 dp = mfma32(lds_b128(Ol, qro[0]), vf[0], RINIT ? row_init(ds) : zacc);
 #pragma unroll
@@ -714,6 +717,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
         s = mfma32(lds_b128(Ql, qro[kk]), lds_b128(Kimg, kofs(kk)), s);
         dp = mfma32(lds_b128(Ol, qro[kk]), vf[kk], dp);
       }
+      if constexpr ((VAR & 4) != 0) __builtin_amdgcn_s_setprio(0);
       // wave-uniform: only diagonal / ragged tiles pay for the selects (masked scores -> -inf -> P = 0)
       if ((qt0 + BMQ > p.Sq) || (key0 + 32 > p.Sk) || (CAUSAL && key0 + 31 > qt0 + off)) {
 #pragma unroll
@@ -757,6 +761,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
           sb[ks][j] = (bf16)dp[8 * ks + j];
         }
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr ((VAR & 4) != 0) __builtin_amdgcn_s_setprio(1);
       if constexpr (TRPIPE) {
         // step i = (ks, dt): its operands were read one step earlier; each step issues the next step's 4 reads
         // ahead of its own 2 MFMAs
@@ -783,6 +788,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
             dk[dt] = mfma32(lds_tr2(Ql, o0, o1), sb[ks], dk[dt]);
           }
       }
+      if constexpr ((VAR & 4) != 0) __builtin_amdgcn_s_setprio(0);
     }
     if (it + 1 < total) stage_scalars(buf ^ 1);
     wait_vmcnt<0>();
@@ -1016,7 +1022,7 @@ static int attn_bwd_var() {
   static const int v = [] {
     const char* e = getenv("DPH_ATTN_BWD_VAR");
     const int x = e ? atoi(e) : kAttnBwdDefaultVar;
-    return (x >= 0 && x <= 3) ? x : kAttnBwdDefaultVar;
+    return (x >= 0 && x <= 3) || x == 6 ? x : kAttnBwdDefaultVar;
   }();
   return v;
 }
@@ -1038,6 +1044,7 @@ static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
     case 1: dkdv_launch<HD, NW, 1>(P, st); break;
     case 2: dkdv_launch<HD, NW, 2>(P, st); break;
     case 3: dkdv_launch<HD, NW, 3>(P, st); break;
+    case 6: dkdv_launch<HD, NW, 6>(P, st); break;
     default: dkdv_launch<HD, NW, 0>(P, st); break;
   }
   const size_t lds_q = 2 * 2 * 64 * HD * 2;

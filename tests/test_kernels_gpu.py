@@ -249,6 +249,21 @@ def test_flash_attention_eight_wave_variant(dph_native, waves):
     assert '"ok": true' in p.stdout
 
 
+@pytest.mark.parametrize("bwd_var", ["6"])
+def test_flash_attention_dkdv_priority_variant(dph_native, bwd_var):
+    """dK/dV kernel with issue priority raised over its MFMA chains (DPH_ATTN_BWD_VAR=6), in a child process against
+    the fp32 reference."""
+    import os
+    import subprocess
+    import sys
+
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "attn_check.py")
+    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_ATTN_BWD_VAR=bwd_var), capture_output=True,
+                       text=True, timeout=100)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    assert '"ok": true' in p.stdout
+
+
 @pytest.mark.parametrize("dq_var", ["1", "2"])
 def test_flash_attention_dq_variants(dph_native, dq_var):
     """dQ kernel variants (DPH_ATTN_DQ_VAR: 1 = transposed-K read ring, 2 = quarter-sub-tile K / V read-ahead without
