@@ -333,7 +333,8 @@ __device__ __forceinline__ int wave_tile_count(int ntiles, int q0w, int off) {
 // (tile t-2's) was last read by a late wave two barriers back.  Every iteration drains its own DMA (vmcnt(0)): one
 // tile of compute hides it.  Measured on B 8, H 32, S 4096, D 128 causal (profiles/r4/attn_stagger/): 809-814
 // TFLOP/s vs 819-822 for 8 waves and 834-838 for the default 4 waves -- kept opt-in.
-template <int HD, bool CAUSAL, int NW, bool DROP = false, bool STG = false>
+// PRIO: issue priority 1 over the S and O MFMA chains, 0 in the softmax (as the dK/dV kernel's VAR bit 2).
+template <int HD, bool CAUSAL, int NW, bool DROP = false, bool STG = false, bool PRIO = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
   using Plan = KVTilePlan<HD, 64 * NW>;
   constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
@@ -398,6 +399,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) kf[sub][kk] = lds_b128(Kl, plan.row(sub, kk));
     f32x16 s[2];
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       s[sub] = mfma32(kf[sub][0], qf[0], zacc);
@@ -408,6 +410,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);   // ... then the MFMAs
     // phase fences keep the scheduler from hoisting the next phase's LDS reads into this one's live range
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if (need_mask) {  // wave-uniform: only diagonal / ragged tiles pay for the selects
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
@@ -459,11 +462,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
     // (+2 % forward TFLOP/s at B 8, H 32, S 4096, D 128; the backward kernels keep their fences: -2 % without them)
 
     // ---- O^T += V^T P^T ----
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
         o[dt] = mfma32(lds_tr2(Vl, plan.tr(ks, dt, 0), plan.tr(ks, dt, 1)), pf[ks], o[dt]);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   for (int t = 0; t < ntiles; ++t) {
@@ -814,7 +819,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
 // issued before the last sub-tile's softmax.
 // KQ: K / V fragments read KS / KQ k-steps ahead of their MFMAs (2 = half a sub-tile; 4 = a quarter, 16 fewer VGPRs:
 // the KQ = 2 form spills 3 registers at 256).
-template <int HD, bool CAUSAL, int NW, bool DROP = false, bool PF = false, int KQ = 2>
+// PRIO: issue priority 1 over the S^T / dP^T and dQ MFMA chains, 0 in the softmax (as the dK/dV kernel's VAR bit 2).
+template <int HD, bool CAUSAL, int NW, bool DROP = false, bool PF = false, int KQ = 2, bool PRIO = false>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P) {
   using Plan = KVTilePlan<HD, 64 * NW>;
   constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
@@ -884,6 +890,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
       // K and V fragments are read a half sub-tile (KH k-steps) ahead of their MFMAs with counted lgkmcnt waits
       // (one read + wait + multiply at a time exposed an LDS round trip per MFMA; all KS at once spills)
       constexpr int NQ = KS >= KQ ? KQ : KS, KH = KS / NQ;
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
       f32x16 s = zacc, dp = zacc;
 #pragma unroll
       for (int half = 0; half < NQ; ++half) {
@@ -907,6 +914,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       if (need_mask) {  // wave-uniform; masked scores -> -inf -> p = 0
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -931,6 +939,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
       __builtin_amdgcn_sched_barrier(0);
     }
     // dQ^T += K^T dS^T
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
     if constexpr (PF) {
 #pragma unroll
       for (int i = 0; i < 4 * DT; ++i) {
@@ -946,6 +955,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
         for (int dt = 0; dt < DT; ++dt)
           dq[dt] = mfma32(lds_tr2(Kl, plan.tr(ks, dt, 0), plan.tr(ks, dt, 1)), sf[ks], dq[dt]);
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   for (int t = 0; t < ntiles; ++t) {
@@ -973,6 +983,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
 // Waves per workgroup (4 or 8; DPH_ATTN_WAVES overrides, for A/B runs).  8 waves = 256 query rows (or keys) share
 // every staged K/V (or Q/dO) tile: half the LDS fill traffic per MFMA of 4 waves, one workgroup per CU.
 constexpr bool kAttnDqDefaultPf = false;
+constexpr bool kAttnFwdDefaultPrio = false;
 constexpr int kAttnBwdDefaultVar = 2;   // A/B on one MI355X: 0 -> 659/663, 1 -> 645/650, 2 -> 673/672, 3 -> 664/660 TF
 
 static int attn_waves(int fallback) {
@@ -983,10 +994,23 @@ static int attn_waves(int fallback) {
   return (w == 4 || w == 8 || w == 9) ? w : fallback;
 }
 
+static bool attn_fwd_prio() {   // DPH_ATTN_FWD_PRIO=1: issue priority over the forward's MFMA chains (A/B)
+  static const bool v = [] {
+    const char* e = getenv("DPH_ATTN_FWD_PRIO");
+    return e ? atoi(e) == 1 : kAttnFwdDefaultPrio;
+  }();
+  return v;
+}
+
 template <int HD, int NW, bool STG = false>
 static void fwd_launch_nw(const AttnParams& p, hipStream_t st) {
   const dim3 grid((unsigned)((p.Sq + 32 * NW - 1) / (32 * NW) * p.Hq * p.B));   // 1-D: xcd_block() maps it
   const size_t lds = (STG ? 4 : 2) * 2 * 64 * HD * 2;
+  if (!STG && attn_fwd_prio()) {
+    if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, NW, false, false, true>), grid, dim3(64 * NW), lds, st, p);
+    else hipLaunchKernelGGL((attn_fwd_k<HD, false, NW, false, false, true>), grid, dim3(64 * NW), lds, st, p);
+    return;
+  }
   if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, NW, false, STG>), grid, dim3(64 * NW), lds, st, p);
   else hipLaunchKernelGGL((attn_fwd_k<HD, false, NW, false, STG>), grid, dim3(64 * NW), lds, st, p);
 }
@@ -1055,7 +1079,10 @@ static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
     const char* e = getenv("DPH_ATTN_DQ_VAR");
     return e ? atoi(e) : (kAttnDqDefaultPf ? 1 : 2);
   }();
-  if (dq_var == 2) {   // quarter-sub-tile K / V read-ahead (no spills)
+  if (dq_var == 3) {   // quarter-sub-tile read-ahead + issue priority over the MFMA chains
+    if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW, false, false, 4, true>), grid_q, dim3(64 * NW), lds_q, st, P);
+    else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW, false, false, 4, true>), grid_q, dim3(64 * NW), lds_q, st, P);
+  } else if (dq_var == 2) {   // quarter-sub-tile K / V read-ahead (no spills)
     if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW, false, false, 4>), grid_q, dim3(64 * NW), lds_q, st, P);
     else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW, false, false, 4>), grid_q, dim3(64 * NW), lds_q, st, P);
   } else if (dq_var == 1) {

@@ -249,16 +249,17 @@ def test_flash_attention_eight_wave_variant(dph_native, waves):
     assert '"ok": true' in p.stdout
 
 
-@pytest.mark.parametrize("bwd_var", ["6"])
-def test_flash_attention_dkdv_priority_variant(dph_native, bwd_var):
-    """dK/dV kernel with issue priority raised over its MFMA chains (DPH_ATTN_BWD_VAR=6), in a child process against
-    the fp32 reference."""
+@pytest.mark.parametrize("knob,val", [("DPH_ATTN_BWD_VAR", "6"), ("DPH_ATTN_DQ_VAR", "3"), ("DPH_ATTN_FWD_PRIO", "1"),
+                                      ("DPH_ATTN_FWD_PRIO", "0")])
+def test_flash_attention_priority_variants(dph_native, knob, val):
+    """The attention kernels with issue priority raised over their MFMA chains (dK/dV DPH_ATTN_BWD_VAR=6, dQ
+    DPH_ATTN_DQ_VAR=3, forward DPH_ATTN_FWD_PRIO=1) and without, in a child process against the fp32 reference."""
     import os
     import subprocess
     import sys
 
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "attn_check.py")
-    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_ATTN_BWD_VAR=bwd_var), capture_output=True,
+    p = subprocess.run([sys.executable, script], env=dict(os.environ, **{knob: val}), capture_output=True,
                        text=True, timeout=100)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
     assert '"ok": true' in p.stdout
