@@ -984,7 +984,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
 // every staged K/V (or Q/dO) tile: half the LDS fill traffic per MFMA of 4 waves, one workgroup per CU.
 constexpr bool kAttnDqDefaultPf = false;
 constexpr bool kAttnFwdDefaultPrio = false;
-constexpr int kAttnBwdDefaultVar = 2;   // A/B on one MI355X: 0 -> 659/663, 1 -> 645/650, 2 -> 673/672, 3 -> 664/660 TF
+// A/B on one MI355X: 0 -> 659/663, 1 -> 645/650, 2 -> 673/672, 3 -> 664/660 TF (round 3); 6 (2 + issue priority over
+// the MFMA chains) -> 691.4 / 690.3 / 686.3 vs 2 -> 681.7 / 684.7 / 685.5 TF, interleaved (round 4, profiles/r4/attn_prio/)
+constexpr int kAttnBwdDefaultVar = 6;
 
 static int attn_waves(int fallback) {
   static const int w = [] {
