@@ -5,6 +5,13 @@ Reads either rocprofv3's SQLite output (``<dir>/<name>_results.db``, the default
 kernel trace (``--output-format csv`` -> ``*_kernel_trace.csv``).  Optionally restricts to the last
 ``--last-ms`` of GPU activity (the timed steps of a bench run) and divides by ``--steps``.
 
+A time window mis-counts steps when tracing slows a host-bound step down (an eager SimpleUNet step runs ~25 % longer
+under rocprofv3, so "the last 4 x ms_per_step" held about 3 steps and every per-step figure read 25 % low).
+``--step-marker NAME --run-steps N`` counts steps instead: the marker kernel's launches per step are its total count
+over the N steps the traced run executed, and the window is the last ``--steps`` steps' worth of its launches.
+``--step-ms`` (the un-traced bench's ms/step) adds ``idle_vs_step_pct`` = 1 - kernel busy / step time, the host gap
+share of the real step rather than of the traced one.
+
     python benchmarks/prof_summary.py gpurun_out/prof3 --steps 2 --json profiles/x.json
 """
 from __future__ import annotations
@@ -77,11 +84,29 @@ def load_events(path: str):
     return ev
 
 
-def summarise(events, last_ms: float | None = None, steps: int = 1, top: int = 80):
+def marker_window(events, marker: str, run_steps: int, steps: int):
+    """Events from the end of the marker launch that closes step (run_steps - steps) on, or None without markers.
+    `events` sorted by start."""
+    idx = [i for i, e in enumerate(events) if marker in e[0]]
+    if not idx or run_steps <= 0:
+        return None
+    per_step = max(1, round(len(idx) / run_steps))
+    keep = steps * per_step
+    if len(idx) <= keep:
+        return events
+    t0 = events[idx[-keep - 1]][2]   # end of the previous step's last marker launch
+    return [e for e in events if e[1] >= t0]
+
+
+def summarise(events, last_ms: float | None = None, steps: int = 1, top: int = 80, marker: str | None = None,
+              run_steps: int = 0, step_ms: float | None = None):
     if not events:
         raise SystemExit("no kernel events found")
     events.sort(key=lambda e: e[1])
-    if last_ms:
+    win = marker_window(events, marker, run_steps, steps) if marker else None
+    if win is not None:
+        events = win
+    elif last_ms:
         t_end = max(e[2] for e in events)
         events = [e for e in events if e[1] >= t_end - last_ms * 1e6]
     span = (max(e[2] for e in events) - min(e[1] for e in events)) / 1e6
@@ -95,7 +120,8 @@ def summarise(events, last_ms: float | None = None, steps: int = 1, top: int = 8
         per_c[category(name)] += d
     busy = sum(per_c.values())
     launches = sum(c for c, _ in per_k.values())
-    return {
+    out = {
+        "window": "marker" if win is not None else ("last_ms" if last_ms else "all"),
         "launches_per_step": round(launches / steps, 2),
         "idle_pct": round(100 * max(0.0, span - busy) / span, 2) if span > 0 else 0.0,
         "steps": steps,
@@ -108,6 +134,10 @@ def summarise(events, last_ms: float | None = None, steps: int = 1, top: int = 8
             for k, (c, t) in sorted(per_k.items(), key=lambda x: -x[1][1])[:top]
         ],
     }
+    if step_ms:
+        out["step_ms"] = step_ms
+        out["idle_vs_step_pct"] = round(100 * max(0.0, step_ms - busy / steps) / step_ms, 2)
+    return out
 
 
 def main(argv=None):
@@ -117,10 +147,16 @@ def main(argv=None):
     ap.add_argument("--last-ms", type=float, default=None, help="only the last N ms of GPU activity")
     ap.add_argument("--json", default=None)
     ap.add_argument("--top", type=int, default=25, help="kernels printed (the JSON keeps up to 80)")
+    ap.add_argument("--step-marker", default=None, help="kernel-name substring launched a fixed number of times per "
+                    "step (e.g. adamw_k): count steps by it instead of a time window")
+    ap.add_argument("--run-steps", type=int, default=0, help="steps the traced run executed (warm-up + timed)")
+    ap.add_argument("--step-ms", type=float, default=None, help="un-traced ms/step: report idle vs the real step")
     args = ap.parse_args(argv)
-    out = summarise(load_events(args.path), args.last_ms, args.steps)
+    out = summarise(load_events(args.path), args.last_ms, args.steps, marker=args.step_marker,
+                    run_steps=args.run_steps, step_ms=args.step_ms)
+    extra = f", idle vs the un-traced {out['step_ms']} ms step {out['idle_vs_step_pct']} %" if "step_ms" in out else ""
     print(f"span/step {out['span_ms_per_step']} ms, kernel busy/step {out['kernel_busy_ms_per_step']} ms, "
-          f"idle {out['idle_pct']} %, {out['launches_per_step']} launches/step")
+          f"idle {out['idle_pct']} %, {out['launches_per_step']} launches/step ({out['window']} window){extra}")
     for c, v in out["categories_ms_per_step"].items():
         print(f"  {c:22s} {v:10.3f} ms")
     print("top kernels:")

@@ -17,6 +17,9 @@ timeout -k 10 300 rocprofv3 --kernel-trace -d "$raw" -o p -- python bench.py --s
 db=$(find "$raw" -name "*results.db" -print -quit)
 # the last 4 steps of GPU activity: 4 x the un-profiled ms/step, slightly trimmed
 ms=$(python -c "import json,sys; print(4 * 0.99 * json.loads([l for l in open(sys.argv[1]) if l.startswith('{\"metric')][0])['ms_per_step'])" "$out/bench.log")
-python benchmarks/prof_summary.py "$db" --steps 4 --last-ms "$ms" --json "$out/summary.json" > "$out/summary.txt"
+step_ms=$(python -c "import json,sys; print(json.loads([l for l in open(sys.argv[1]) if l.startswith('{\"metric')][0])['ms_per_step'])" "$out/bench.log")
+# steps counted by the optimizer kernel (a fixed number of launches per step; 6 steps traced), time window otherwise
+python benchmarks/prof_summary.py "$db" --steps 4 --last-ms "$ms" --step-marker "${PROF_STEP_MARKER:-adamw_k}" \
+  --run-steps "${PROF_RUN_STEPS:-6}" --step-ms "$step_ms" --json "$out/summary.json" > "$out/summary.txt"
 head -n 16 "$out/summary.txt"
 rm -rf "$raw"

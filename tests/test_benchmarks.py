@@ -81,3 +81,23 @@ def test_prof_summary_idle_launches_categories():
     assert abs(out["idle_pct"] - 20.0) < 1e-6
     cats = out["categories_ms_per_step"]
     assert cats["conv3x3(dph)"] == 2.0 and cats["conv(miopen/ck)"] == 1.0 and cats["batchnorm(dph)"] == 1.0
+
+
+def test_prof_summary_step_marker_window():
+    """Steps counted by a per-step marker kernel, not a time window: a traced run of 6 steps whose last steps are
+    slower than the un-traced step still yields exactly the last 2 steps' kernels, and idle vs the un-traced step."""
+    sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+    import prof_summary
+
+    ms = 1_000_000
+    ev, t = [], 0
+    for step in range(6):
+        for name in ("dph::conv3_k<64>", "dph::c3w_k<128>", "dph::adamw_k<bf16>", "dph::adamw_k<bf16>"):
+            ev.append((name, t, t + ms))
+            t += 2 * ms   # 1 ms busy + 1 ms gap per kernel
+    out = prof_summary.summarise(list(ev), last_ms=3.0, steps=2, marker="adamw_k", run_steps=6, step_ms=6.0)
+    assert out["window"] == "marker"
+    assert out["launches_per_step"] == 4 and out["kernel_busy_ms_per_step"] == 4.0
+    assert abs(out["idle_vs_step_pct"] - 100 * 2 / 6) < 0.01
+    # without the marker the 3 ms window holds only part of a step
+    assert prof_summary.summarise(list(ev), last_ms=3.0, steps=2)["launches_per_step"] < 4
