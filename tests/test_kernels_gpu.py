@@ -280,6 +280,36 @@ def test_flash_attention_dq_variants(dph_native, dq_var):
     assert '"ok": true' in p.stdout
 
 
+@pytest.mark.parametrize("kernel,stages", [("0", "2"), ("1", "2"), ("1", "3"), ("1", "4"), ("1", "5")])
+def test_conv1x1_wgrad_variants(dph_native, kernel, stages):
+    """1x1 weight gradient: register-staged ts_tn_k (DPH_W1_KERNEL=0) and the LDS-DMA c3w_k form with 2..5 ring stages
+    (DPH_W1_STAGES; counted vmcnt, ragged last chunk drains), in a child process against the fp32 reference."""
+    import os
+    import subprocess
+    import sys
+
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "w1_check.py")
+    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_W1_KERNEL=kernel, DPH_W1_STAGES=stages),
+                       capture_output=True, text=True, timeout=100)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    assert '"ok": true' in p.stdout
+
+
+@pytest.mark.parametrize("stages", ["2", "3", "4", "5"])
+def test_conv3x3_wgrad_ring_variants(dph_native, stages):
+    """3x3 (stride 1 and gathered strided) and stem weight gradients on c3w_k with 2..5 LDS ring stages
+    (DPH_C3W_STAGES, capped at what fits 160 KiB), in a child process against F.conv2d in fp32."""
+    import os
+    import subprocess
+    import sys
+
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "c3w_check.py")
+    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_C3W_STAGES=stages), capture_output=True,
+                       text=True, timeout=100)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    assert '"ok": true' in p.stdout
+
+
 def test_flash_attention_padded_head_dim(dph_native):
     torch.manual_seed(10)
     q, k, v = (torch.randn(2, 64, 4, 16, device=DEV, dtype=torch.bfloat16, requires_grad=True) for _ in range(3))
