@@ -87,7 +87,8 @@ def load_events(path: str):
 def marker_window(events, marker: str, run_steps: int, steps: int):
     """Events from the end of the marker launch that closes step (run_steps - steps) on, or None without markers.
     `events` sorted by start."""
-    idx = [i for i, e in enumerate(events) if marker in e[0]]
+    names = marker.split("|")
+    idx = [i for i, e in enumerate(events) if any(n in e[0] for n in names)]
     if not idx or run_steps <= 0:
         return None
     per_step = max(1, round(len(idx) / run_steps))
@@ -147,8 +148,8 @@ def main(argv=None):
     ap.add_argument("--last-ms", type=float, default=None, help="only the last N ms of GPU activity")
     ap.add_argument("--json", default=None)
     ap.add_argument("--top", type=int, default=25, help="kernels printed (the JSON keeps up to 80)")
-    ap.add_argument("--step-marker", default=None, help="kernel-name substring launched a fixed number of times per "
-                    "step (e.g. adamw_k): count steps by it instead of a time window")
+    ap.add_argument("--step-marker", default=None, help="kernel-name substring(s), '|'-separated, launched a fixed "
+                    "number of times per step (e.g. adamw_k|sgd_k): count steps by it instead of a time window")
     ap.add_argument("--run-steps", type=int, default=0, help="steps the traced run executed (warm-up + timed)")
     ap.add_argument("--step-ms", type=float, default=None, help="un-traced ms/step: report idle vs the real step")
     args = ap.parse_args(argv)

@@ -408,8 +408,12 @@ __device__ __forceinline__ void fdivmod(int r, int d, float inv, int& q, int& m)
 // SL: X slabs (64 k' each) per output tile: 3 for the 3x3 kernels (192 k', one tap per slab), 1 or 2 for the 1x1
 // weight gradient (GEN with the identity geometry).
 // GEN = 2: chunk taps (the 7x7 RGB stem, conv3x3.hip conv3_k GEN = 2): every 16-B chunk of an X slab is its own tap.
-template <int TCO, int GEN = 0, int SL = C3W_SLABS>
-__global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
+// GEN = 3: identity rows (the stride-1 1x1 weight gradient): X row = dY row, no pixel -> (n, y, x) division per piece.
+// NS: ring stages.  2 = the next step's DMA in flight while one step computes (two workgroups per CU); deeper rings
+// (1x1 weight gradient, one workgroup per CU) keep NS - 1 steps in flight behind a counted vmcnt: at 16 MFMAs per wave
+// and step the two-stage ring waits on every step's DMA round trip (1024->512 @ 14: ~22 % MFMA busy).
+template <int TCO, int GEN = 0, int SL = C3W_SLABS, int NS = 2>
+__global__ __launch_bounds__(256, NS > 2 ? 1 : 2) void c3w_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                 float* __restrict__ P, int M, int N, int K, int64_t lda,
                                                 int64_t ldb, int chunk, int H, int W, int Cin, ConvGeo geo) {
   constexpr int AS = TCO / 64;                       // dY slabs per step
@@ -417,7 +421,7 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
   constexpr int STG = (AS + SL) * C3W_SLAB;           // one stage
   constexpr int PCS = (AS + SL) * 8 / 4;              // 1-KB DMA pieces per wave per step
   constexpr int TI = TCO / 64;                       // co MFMA tiles per wave (wave covers TCO / 2 channels)
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STG];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int cw = wid >> 1, kw = wid & 1;
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3, h = lane >> 5;
@@ -454,7 +458,23 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
       bdx[sb] = tap - (tap / 3) * 3 - 1;
     }
   }
-  auto issue = [&](int m, int stage) {
+  // Pixel coordinates (column, image row, image) of each piece's X row, advanced incrementally by the 64 rows of a
+  // step instead of two float divisions per piece and step (that arithmetic sat in front of every step's MFMAs: the
+  // identity-row 1x1 form without it measured 1.94 vs 2.45 ms per ResNet-50 step).  A piece is an X piece for the
+  // whole loop or never (its slab depends on the wave only).
+  constexpr bool INCR = GEN != 3;
+  int pxw[PCS], pyh[PCS], pnq[PCS];
+  const int adv_x = 64 % Wr, adv_q = 64 / Wr, adv_y = adv_q % Hr, adv_n = adv_q / Hr;
+  if constexpr (INCR) {
+#pragma unroll
+    for (int j = 0; j < PCS; ++j) {
+      int yq;
+      fdivmod(mbeg + 8 * ((wid_u * PCS + j) & 7) + prow, Wr, invW, yq, pxw[j]);
+      fdivmod(yq, Hr, invH, pnq[j], pyh[j]);
+    }
+  }
+  // `adv`: rows moved on by one step since the previous call (every call but the first)
+  auto issue = [&](int m, int stage, bool adv) {
 #pragma unroll
     for (int j = 0; j < PCS; ++j) {
       const int i = wid_u * PCS + j;                 // wave-uniform piece index
@@ -466,13 +486,23 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
         lds_dma16_buf(ra, r < mend ? off : 0x80000000u, dst);
       } else {
         const int sb = SL == 1 ? 0 : slab - AS;   // (SL = 1: a constant index, no private-memory array)
-        int yq, xw, yh, nq;
-        fdivmod(r, Wr, invW, yq, xw);                // pixel -> (image row, column), then image row -> y
-        fdivmod(yq, Hr, invH, nq, yh);
+        if (INCR && adv) {
+          pxw[j] += adv_x;
+          const int cx = pxw[j] >= Wr;
+          pxw[j] -= cx ? Wr : 0;
+          pyh[j] += adv_y + cx;
+          const int cy = pyh[j] >= Hr;
+          pyh[j] -= cy ? Hr : 0;
+          pnq[j] += adv_n + cy;
+        }
+        const int xw = INCR ? pxw[j] : 0, yh = INCR ? pyh[j] : 0, nq = INCR ? pnq[j] : 0;
         bool ok;
         int64_t src;
         unsigned col = (unsigned)(bcb[sb] + sch * 8);
-        if constexpr (GEN == 2) {   // this lane's chunk is tap t: the whole 8-element source row
+        if constexpr (GEN == 3) {
+          ok = r < mend;
+          src = r;
+        } else if constexpr (GEN == 2) {   // this lane's chunk is tap t: the whole 8-element source row
           const int t = min((k0 + sb * 64) / 8 + sch, geo.ntaps - 1), ty = t / geo.tdx[0], tx = t - ty * geo.tdx[0];
           ok = r < mend;
           src = ((int64_t)nq * geo.Hs + geo.sy * yh + geo.by + ty) * geo.Ws + geo.sx * xw + geo.bx + tx;
@@ -515,30 +545,49 @@ __global__ __launch_bounds__(256, 2) void c3w_k(const bf16* __restrict__ A, cons
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int nsteps = (mend - mbeg + 63) / 64;
-  if (nsteps > 0) issue(mbeg, 0);
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nsteps) issue(mbeg + i * 64, i, i > 0);
   for (int st = 0; st < nsteps; ++st) {
-    wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    if (st + 1 < nsteps) issue(mbeg + (st + 1) * 64, (st + 1) & 1);
-    const char* base = smem + (st & 1) * STG;
+    // this wave's pieces of step st have landed: the NS - 2 later steps issued so far may stay in flight (each wave
+    // issues PCS pieces per step); near the end fewer were issued, so drain
+    if (NS > 2 && st + NS - 2 < nsteps) wait_vmcnt<(NS > 2 ? (NS - 2) * PCS : 0)>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();   // ... every wave's, and nobody reads step st - 1's slot any more
+    const char* base = smem + (st % NS) * STG;
+    // every operand of the step is read before its MFMAs (LDS returns in order, so the first k-step's products wait
+    // only for their own reads): one exposed LDS round trip per step instead of one per 16-pixel k-step
+    bf16x8 af[4][TI], bfr[4][SL];
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {                 // 16-pixel MFMA k-steps
+      // the next DMA goes out behind k-step 0's reads: its address arithmetic overlaps their LDS round trip
+      if (kk == 1 && st + NS - 1 < nsteps) issue(mbeg + (st + NS - 1) * 64, (st + NS - 1) % NS, true);
       const int ro = 16 * kk * TW_ROWB;
-      bf16x8 af[TI], bfr[SL];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const bf16x4 lo = tr_read(base + aoff[i] + ro), hi = tr_read(base + aoff[i] + ro + 4 * TW_ROWB);
-        af[i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        af[kk][i] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
 #pragma unroll
       for (int j = 0; j < SL; ++j) {
         const bf16x4 lo = tr_read(base + boff[j] + ro), hi = tr_read(base + boff[j] + ro + 4 * TW_ROWB);
-        bfr[j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        bfr[kk][j] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < SL; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < SL; ++j) acc[i][j] = mfma32(af[kk][i], bfr[kk][j], acc[i][j]);
+    // schedule: the reads run one k-step ahead of the MFMAs -- reads(0), reads(1), MFMAs(0), reads(2), MFMAs(1), ...
+    // (left alone, hipcc reuses one fragment set and issues k-step kk + 1's reads only after k-step kk's MFMAs, so
+    // each k-step's first MFMA waits out an LDS round trip)
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * (TI + SL), 0);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      if (kk < 3) __builtin_amdgcn_sched_group_barrier(0x100, 2 * (TI + SL), 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, TI * SL, 0);
     }
   }
   // register r of tile (i, j): P[n0 + cw*TCO/2 + i*32 + (r&3) + 8(r>>2) + 4h][k0 + kw*96 + j*32 + (lane & 31)]
@@ -711,6 +760,44 @@ bool c3w_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
 
 static int64_t c3w_tiles(int64_t N, int64_t K, int64_t tk) { return (N / (N % 128 == 0 ? 128 : 64)) * (K / tk); }
 
+// LDS ring depth of c3w_k: DPH_W1_STAGES for the 1x1 weight gradient, DPH_C3W_STAGES for the 3x3 / strided / stem ones
+// (2..5; a launch caps it at what fits 160 KiB of LDS).  More than 2 stages = one workgroup per CU.
+static int env_stages(const char* name, int dflt) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : dflt;
+  return v < 2 ? 2 : (v > 5 ? 5 : v);
+}
+static int w1_stages() {
+  static const int ns = env_stages("DPH_W1_STAGES", 2);
+  return ns;
+}
+static int c3w_stages() {
+  static const int ns = env_stages("DPH_C3W_STAGES", 2);
+  return ns;
+}
+
+template <int TCO, int GEN, int SL, int NS>
+static void c3w_go(unsigned nblk, hipStream_t st, const void* A, const void* B, float* P, int64_t M, int64_t N,
+                   int64_t K, int64_t lda, int64_t ldb, int64_t chunk, int H, int W, int cin, const ConvGeo& g) {
+  hipLaunchKernelGGL((c3w_k<TCO, GEN, SL, NS>), dim3(nblk), dim3(256), 0, st, (const bf16*)A, (const bf16*)B, P,
+                     (int)M, (int)N, (int)K, lda, ldb, (int)chunk, H, W, cin, g);
+}
+// c3w_k with `ns` ring stages, capped at the deepest ring that fits 160 KiB
+template <int TCO, int GEN, int SL>
+static void c3w_launch(int ns, unsigned nblk, hipStream_t st, const void* A, const void* B, float* P, int64_t M,
+                       int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t chunk, int H, int W, int cin,
+                       const ConvGeo& g) {
+  constexpr int STG = (TCO / 64 + SL) * C3W_SLAB, LDS = 160 * 1024;
+  if constexpr (5 * STG <= LDS)
+    if (ns >= 5) return c3w_go<TCO, GEN, SL, 5>(nblk, st, A, B, P, M, N, K, lda, ldb, chunk, H, W, cin, g);
+  if constexpr (4 * STG <= LDS)
+    if (ns >= 4) return c3w_go<TCO, GEN, SL, 4>(nblk, st, A, B, P, M, N, K, lda, ldb, chunk, H, W, cin, g);
+  if (ns >= 3) return c3w_go<TCO, GEN, SL, 3>(nblk, st, A, B, P, M, N, K, lda, ldb, chunk, H, W, cin, g);
+  c3w_go<TCO, GEN, SL, 2>(nblk, st, A, B, P, M, N, K, lda, ldb, chunk, H, W, cin, g);
+}
+// resident workgroups per round: 2 per CU with the two-stage ring, 1 with a deeper one
+static int64_t c3w_round(int ns) { return ns > 2 ? 256 : 512; }
+
 // 1x1 weight gradient on the LDS-DMA kernel (c3w_k with one tap, identity rows): k' tiles of 128 (64 when K % 128)
 static int w1_tk(int64_t K) { return K % 128 == 0 ? 128 : 64; }
 
@@ -727,15 +814,16 @@ bool w1_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
 
 int w1_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = c3w_tiles(N, K, w1_tk(K));
-  int64_t s = cdiv(512, tiles);   // one resident round of 2 workgroups per CU, chunks of >= 512 rows
+  // one resident round (2 workgroups per CU with the two-stage ring, 1 with a deeper one), chunks of >= 512 rows
+  int64_t s = cdiv(c3w_round(w1_stages()), tiles);
   s = std::max<int64_t>(1, std::min<int64_t>(s, M / 512));
   return (int)s;
 }
 
 int c3w_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = c3w_tiles(N, K, C3W_TK);
-  // one resident round of 2 workgroups per CU (the fp32 partials grow with the split), chunks of >= 512 rows
-  int64_t s = cdiv(512, tiles);
+  // one resident round of workgroups (the fp32 partials grow with the split), chunks of >= 512 rows
+  int64_t s = cdiv(c3w_round(c3w_stages()), tiles);
   s = std::max<int64_t>(1, std::min<int64_t>(s, M / 512));
   return (int)s;
 }
@@ -766,28 +854,24 @@ void ts_gemm_tn(const void* A, const void* B, float* partial, void* C, int64_t M
     g.ntaps = 1;
     g.src_rows = M;
     const int tk = w1_tk(K);
-#define DPH_W1(TCO_, SL_)                                                                                      \
-  hipLaunchKernelGGL((c3w_k<TCO_, true, SL_>), dim3((int)((N / TCO_) * (K / tk) * nsplit)), dim3(256), 0, st,   \
-                     (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0,   \
-                     (int)K, g)
+    const unsigned nblk = (unsigned)((N / (N % 128 == 0 ? 128 : 64)) * (K / tk) * nsplit);
+    const int ns = w1_stages();
     if (N % 128 == 0) {
-      if (tk == 128) DPH_W1(128, 2);
-      else DPH_W1(128, 1);
+      if (tk == 128) c3w_launch<128, 3, 2>(ns, nblk, st, A, B, partial, M, N, K, lda, ldb, chunk, 0, 0, (int)K, g);
+      else c3w_launch<128, 3, 1>(ns, nblk, st, A, B, partial, M, N, K, lda, ldb, chunk, 0, 0, (int)K, g);
     } else {
-      if (tk == 128) DPH_W1(64, 2);
-      else DPH_W1(64, 1);
+      if (tk == 128) c3w_launch<64, 3, 2>(ns, nblk, st, A, B, partial, M, N, K, lda, ldb, chunk, 0, 0, (int)K, g);
+      else c3w_launch<64, 3, 1>(ns, nblk, st, A, B, partial, M, N, K, lda, ldb, chunk, 0, 0, (int)K, g);
     }
-#undef DPH_W1
   } else if (H > 0 && c3w_supported(M, N, K, lda, ldb)) {   // the LDS-DMA 3x3 kernel (nsplit from c3w_splits)
     const int cin = (int)(K / 9);
+    const int ns = c3w_stages();
     if (N % 128 == 0)
-      hipLaunchKernelGGL((c3w_k<128>), dim3((int)((N / 128) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,
-                         (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, H, W,
-                         cin, ConvGeo{});
+      c3w_launch<128, 0, C3W_SLABS>(ns, (unsigned)((N / 128) * (K / C3W_TK) * nsplit), st, A, B, partial, M, N, K, lda,
+                                    ldb, chunk, H, W, cin, ConvGeo{});
     else
-      hipLaunchKernelGGL((c3w_k<64>), dim3((int)((N / 64) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,
-                         (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, H, W,
-                         cin, ConvGeo{});
+      c3w_launch<64, 0, C3W_SLABS>(ns, (unsigned)((N / 64) * (K / C3W_TK) * nsplit), st, A, B, partial, M, N, K, lda,
+                                   ldb, chunk, H, W, cin, ConvGeo{});
   } else if (pro_ss != nullptr && H == 0) {
     hipLaunchKernelGGL((ts_tn_k<false, true>), dim3((int)(tiles * nsplit)), dim3(256), 0, st, (const bf16*)A,
                        (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0, 0, pro_ss);
@@ -813,7 +897,7 @@ bool c3wg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, c
 int c3wg_splits(int64_t M, int64_t N, int64_t K, bool chunk_taps) {
   if (!chunk_taps) return c3w_splits(M, N, K);
   const int64_t tiles = c3w_tiles(N, K, 128);
-  int64_t s = cdiv(512, tiles);
+  int64_t s = cdiv(c3w_round(c3w_stages()), tiles);
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, M / 512));
 }
 
@@ -821,27 +905,24 @@ void ts_gemm_tn_geo(const void* A, const void* B, float* partial, void* C, int64
                     int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, const ConvGeo& g,
                     hipStream_t st, bool chunk_taps) {
   int64_t chunk = cdiv(cdiv(M, nsplit), 64) * 64;
+  const int ns = c3w_stages();
   if (chunk_taps) {   // the RGB stem's weight gradient: 64 output channels x 128-wide k' tiles
     if (N % 128 == 0)
-      hipLaunchKernelGGL((c3w_k<128, 2, 2>), dim3((int)((N / 128) * (K / 128) * nsplit)), dim3(256), 0, st,
-                         (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0,
-                         8, g);
+      c3w_launch<128, 2, 2>(ns, (unsigned)((N / 128) * (K / 128) * nsplit), st, A, B, partial, M, N, K, lda, ldb,
+                            chunk, 0, 0, 8, g);
     else
-      hipLaunchKernelGGL((c3w_k<64, 2, 2>), dim3((int)((N / 64) * (K / 128) * nsplit)), dim3(256), 0, st,
-                         (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0,
-                         8, g);
+      c3w_launch<64, 2, 2>(ns, (unsigned)((N / 64) * (K / 128) * nsplit), st, A, B, partial, M, N, K, lda, ldb,
+                           chunk, 0, 0, 8, g);
     ts_reduce(partial, C, N * K, nsplit, out_dtype, accumulate, st);
     return;
   }
   const int cin = (int)(K / g.ntaps);
   if (N % 128 == 0)
-    hipLaunchKernelGGL((c3w_k<128, true>), dim3((int)((N / 128) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,
-                       (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0,
-                       cin, g);
+    c3w_launch<128, 1, C3W_SLABS>(ns, (unsigned)((N / 128) * (K / C3W_TK) * nsplit), st, A, B, partial, M, N, K, lda,
+                                  ldb, chunk, 0, 0, cin, g);
   else
-    hipLaunchKernelGGL((c3w_k<64, true>), dim3((int)((N / 64) * (K / C3W_TK) * nsplit)), dim3(256), 0, st,
-                       (const bf16*)A, (const bf16*)B, partial, (int)M, (int)N, (int)K, lda, ldb, (int)chunk, 0, 0,
-                       cin, g);
+    c3w_launch<64, 1, C3W_SLABS>(ns, (unsigned)((N / 64) * (K / C3W_TK) * nsplit), st, A, B, partial, M, N, K, lda,
+                                 ldb, chunk, 0, 0, cin, g);
   ts_reduce(partial, C, N * K, nsplit, out_dtype, accumulate, st);
 }
 

@@ -19,7 +19,7 @@ db=$(find "$raw" -name "*results.db" -print -quit)
 ms=$(python -c "import json,sys; print(4 * 0.99 * json.loads([l for l in open(sys.argv[1]) if l.startswith('{\"metric')][0])['ms_per_step'])" "$out/bench.log")
 step_ms=$(python -c "import json,sys; print(json.loads([l for l in open(sys.argv[1]) if l.startswith('{\"metric')][0])['ms_per_step'])" "$out/bench.log")
 # steps counted by the optimizer kernel (a fixed number of launches per step; 6 steps traced), time window otherwise
-python benchmarks/prof_summary.py "$db" --steps 4 --last-ms "$ms" --step-marker "${PROF_STEP_MARKER:-adamw_k}" \
+python benchmarks/prof_summary.py "$db" --steps 4 --last-ms "$ms" --step-marker "${PROF_STEP_MARKER:-adamw_k|sgd_k}" \
   --run-steps "${PROF_RUN_STEPS:-6}" --step-ms "$step_ms" --json "$out/summary.json" > "$out/summary.txt"
 head -n 16 "$out/summary.txt"
 rm -rf "$raw"
