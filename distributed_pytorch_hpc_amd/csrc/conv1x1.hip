@@ -797,35 +797,34 @@ static void c3w_launch(int ns, unsigned nblk, hipStream_t st, const void* A, con
 }
 // resident workgroups per round: 2 per CU with the two-stage ring, 1 with a deeper one
 static int64_t c3w_round(int ns) { return ns > 2 ? 256 : 512; }
+// pixel-chunk splits: as many as fill ONE resident round (floor -- rounding up, e.g. 22 x 24 tiles = 528 workgroups
+// for 512 slots, started a second round that cost a whole workgroup's time for 16 workgroups), chunks >= 512 rows
+static int64_t c3w_split_count(int64_t M, int64_t tiles, int ns) {
+  const int64_t s = std::max<int64_t>(1, c3w_round(ns) / tiles);
+  return std::max<int64_t>(1, std::min<int64_t>(s, M / 512));
+}
 
 // 1x1 weight gradient on the LDS-DMA kernel (c3w_k with one tap, identity rows): k' tiles of 128 (64 when K % 128)
 static int w1_tk(int64_t K) { return K % 128 == 0 ? 128 : 64; }
 
 bool w1_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
-  // opt-in (DPH_W1_KERNEL=1): on ResNet-50's twelve 1x1 shapes it is 0.87-1.16x the register-staged ts_tn_k, 2.609 vs
-  // 2.535 ms per step in total (both ahead of MIOpen's 3.139; profiles/r4/conv1x1_wgrad/)
+  // default since the identity-row form (GEN 3, no per-piece divisions): 1.94-2.06 ms per ResNet-50 step over its
+  // twelve 1x1 shapes vs 2.50 for the register-staged ts_tn_k and 3.26 for MIOpen (profiles/r4/c3w_incr/,
+  // profiles/r4/c3w_ring/identity_rows/); DPH_W1_KERNEL=0 keeps ts_tn_k.  The BatchNorm-prologue form stays on ts_tn_k.
   static const bool on = [] {
     const char* e = getenv("DPH_W1_KERNEL");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on && N % 64 == 0 && K % 64 == 0 && M * lda * 2 < (int64_t(1) << 31) && M * ldb * 2 < (int64_t(1) << 31) &&
          M < (int64_t(1) << 24);
 }
 
 int w1_splits(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = c3w_tiles(N, K, w1_tk(K));
-  // one resident round (2 workgroups per CU with the two-stage ring, 1 with a deeper one), chunks of >= 512 rows
-  int64_t s = cdiv(c3w_round(w1_stages()), tiles);
-  s = std::max<int64_t>(1, std::min<int64_t>(s, M / 512));
-  return (int)s;
+  return (int)c3w_split_count(M, c3w_tiles(N, K, w1_tk(K)), w1_stages());
 }
 
 int c3w_splits(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = c3w_tiles(N, K, C3W_TK);
-  // one resident round of workgroups (the fp32 partials grow with the split), chunks of >= 512 rows
-  int64_t s = cdiv(c3w_round(c3w_stages()), tiles);
-  s = std::max<int64_t>(1, std::min<int64_t>(s, M / 512));
-  return (int)s;
+  return (int)c3w_split_count(M, c3w_tiles(N, K, C3W_TK), c3w_stages());
 }
 
 static void ts_reduce(const float* partial, void* C, int64_t nk, int nsplit, int out_dtype, bool accumulate,
@@ -896,9 +895,7 @@ bool c3wg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, c
 
 int c3wg_splits(int64_t M, int64_t N, int64_t K, bool chunk_taps) {
   if (!chunk_taps) return c3w_splits(M, N, K);
-  const int64_t tiles = c3w_tiles(N, K, 128);
-  int64_t s = cdiv(c3w_round(c3w_stages()), tiles);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(s, M / 512));
+  return (int)c3w_split_count(M, c3w_tiles(N, K, 128), c3w_stages());
 }
 
 void ts_gemm_tn_geo(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,

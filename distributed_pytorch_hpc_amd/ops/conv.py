@@ -17,10 +17,10 @@ with the spatially flipped, channel-transposed weight; padding taps are zero-fil
 epilogue emits the following BatchNorm's statistics or adds a bias): 440-810 TFLOP/s vs MIOpen's 370-780 on the
 ResNet-50 / SimpleUNet shapes (profiles/r3/conv3_bench_oob.json), on by default (``DPH_CONV3X3=0``: MIOpen;
 ``DPH_CONV3_WM=2|4`` picks the 4- or 8-wave tile).  The
-weight gradient of the ResNet ``Conv3x3`` runs on MIOpen by default (318-491 TFLOP/s vs 241-357 for the LDS-DMA
-split-pixel kernel and 302-324 for the older register-staged one, profiles/r3/conv3_bench_c3w_wgrad.json /
-_tsw_wgrad.json; ResNet-50 in-step -2.4 % with the kernel); the SimpleUNet's biased 3x3 convolutions (``BiasConv2d``)
-take the kernel (+19 % in-step, profiles/r4/conv_wgrad/).  ``DPH_CONV3_WGRAD=miopen|dph`` overrides both.  Round 2's register-staged forward (``DPH_CONV3_KERNEL=ts``) measured 0.51-0.63 ms vs MIOpen's
+weight gradients run on the LDS-DMA split-pixel kernel (``c3w_k``) by default: 1.20-1.42x MIOpen per shape since round
+4 removed its per-piece address divisions and its second, nearly empty round of split-K workgroups (round 3 measured it
+at 241-357 TFLOP/s vs MIOpen's 318-491 and kept MIOpen for ResNet, profiles/r3/conv3_bench_c3w_wgrad.json).
+``DPH_CONV3_WGRAD=miopen|dph`` overrides.  Round 2's register-staged forward (``DPH_CONV3_KERNEL=ts``) measured 0.51-0.63 ms vs MIOpen's
 0.38-0.53 ms per shape and stayed off.
 """
 from __future__ import annotations
@@ -205,11 +205,11 @@ class _Conv1x1Fn(torch.autograd.Function):
 
 
 def _conv3_wgrad(default: str) -> str:
-    """Which kernel runs a 3x3 weight gradient: DPH_CONV3_WGRAD (miopen | dph) overrides the module's measured default.
-    Conv3x3 (ResNet bottlenecks) keeps MIOpen: ResNet-50 FSDP bf16 B=256 10 068 / 10 079 img/s vs 9 835 / 9 833 with
-    the split-pixel kernel; BiasConv2d (SimpleUNet) takes the kernel: 1 005 / 984 vs 848 / 826 samples/s eager, the
-    UNet step being host-bound and the MIOpen call the heavier launch (interleaved A/B on one MI355X each,
-    profiles/r4/conv_wgrad/)."""
+    """Which kernel runs a 3x3 weight gradient: DPH_CONV3_WGRAD (miopen | dph) overrides the module's default, which is
+    the c3w_k kernel everywhere since its DMA addresses advance incrementally and its split-K fills exactly one resident
+    round: 1.20-1.42x MIOpen on the ResNet-50 / SimpleUNet shapes (profiles/r4/c3w_rounds/c3.log).  Before
+    that, Conv3x3 (ResNet bottlenecks) kept MIOpen (10 068 / 10 079 img/s vs 9 835 / 9 833 with the kernel) while
+    BiasConv2d (SimpleUNet) already took the kernel (1 005 / 984 vs 848 / 826 samples/s, profiles/r4/conv_wgrad/)."""
     return os.environ.get("DPH_CONV3_WGRAD", default)
 # stride-1 3x3 convolutions on csrc/conv3x3.hip by default: ResNet-50 FSDP bf16 B=256 9 472 / 9 513 vs 9 258 / 9 278
 # img/s on MIOpen (interleaved A/B on one MI355X, profiles/r3/ab_conv3x3/); DPH_CONV3X3=0 = MIOpen
@@ -315,7 +315,7 @@ class Conv3x3(nn.Conv2d):
         if conv3x3_native_ok(x, self.weight):
             _lib.require()
             return _Conv3x3Fn.apply(x, self.weight, stats_slot if _conv3_stats_ok() else None, None,
-                                    _conv3_wgrad("miopen"))
+                                    _conv3_wgrad("dph"))
         return F.conv2d(x, self.weight, padding=1)
 
 
@@ -387,7 +387,10 @@ def convg_reference(A: torch.Tensor, B: torch.Tensor, geo: list, out: torch.Tens
 
 
 def _strided_wgrad() -> str:
-    return os.environ.get("DPH_CONV_STRIDED_WGRAD", "miopen")
+    """Strided weight gradients on c3w_k by default since its DMA addresses advance incrementally: 0.90-1.46x MIOpen
+    per shape (profiles/r4/c3w_incr/str_ns2.log) and, with the 1x1 identity-row kernel, ResNet-50 10 042 / 10 056 vs
+    9 912 / 9 927 img/s (profiles/r4/resnet_wgrad_ab/); DPH_CONV_STRIDED_WGRAD=miopen keeps MIOpen's."""
+    return os.environ.get("DPH_CONV_STRIDED_WGRAD", "dph")
 
 
 class _StridedConvFn(torch.autograd.Function):
@@ -441,8 +444,8 @@ class _StridedConvFn(torch.autograd.Function):
                 _lib.ops().convg_nt(dy2, bk, geo, dx2, False)
             dx = dx2.view(B, H, W, C).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] and _strided_wgrad() != "dph":
-            # MIOpen's weight gradient: 1.0-1.4x the gathered c3w_k / sub-image 1x1 kernel on ResNet-50's six strided
-            # shapes (profiles/r4/strided_conv/strided.log); DPH_CONV_STRIDED_WGRAD=dph selects the kernels
+            # MIOpen's weight gradient (DPH_CONV_STRIDED_WGRAD=miopen; the gathered c3w_k / sub-image 1x1 kernels are
+            # the default, see _strided_wgrad)
             x4 = x2.view(B, H, W, C).permute(0, 3, 1, 2)
             dy4 = dy2.view(B, Ho, Wo, cout).permute(0, 3, 1, 2)
             gw = torch.ops.aten.convolution_backward(dy4, x4, wb, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
