@@ -112,10 +112,20 @@ def build(jobs: int | None = None, verbose: bool = False, resource_usage: bool =
     if ninja is None:
         raise RuntimeError("ninja not found")
     jobs = jobs or min(8, os.cpu_count() or 4)
+    if os.environ.get("DPH_BUILD_CLEAN", "0") == "1":   # force every object to recompile (a from-scratch build check)
+        subprocess.run([ninja, "-f", ninja_file, "-t", "clean"], check=True, cwd=build_dir, stdout=subprocess.DEVNULL)
     cmd = [ninja, "-f", ninja_file, "-j", str(jobs)]
     if verbose:
         cmd.append("-v")
-    subprocess.run(cmd, check=True, cwd=build_dir)
+    res = subprocess.run(cmd, check=True, cwd=build_dir, stdout=subprocess.PIPE, text=True)
+    sys.stdout.write(res.stdout)
+    # what this call actually compiled: ninja prints one "[i/n] ..." line per edge it ran, nothing when up to date
+    ran = [ln for ln in res.stdout.splitlines() if ln.startswith("[")]
+    n_hip = sum(1 for f in os.listdir(HERE) if f.endswith(".hip"))
+    n_cpp = sum(1 for f in os.listdir(HERE) if f.endswith(".cpp"))
+    compiled = sum(1 for ln in ran if "HIPCC" in ln or "CXX" in ln)
+    print(f"[build] gfx950: {compiled} of {n_hip} .hip + {n_cpp} .cpp sources compiled this call"
+          f"{' (rest up to date)' if compiled < n_hip + n_cpp else ''}; linked: {any('LINK' in ln for ln in ran)}")
     return OUT
 
 
