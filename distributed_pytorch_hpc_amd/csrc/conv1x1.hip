@@ -54,8 +54,12 @@ constexpr int TS_KF = TS_BK / 16;   // MFMA k-steps (A fragments) per K-step
 // coefficients) after it lands in registers, so the normalised activation is never written to HBM.
 // ADDS = s > 1 (with ADD): D is the gradient of the stride-s sub-image (a strided 1x1 downsample's input gradient,
 // [n * ceil(H/s) * ceil(W/s), N]) and is added only at the pixels (y, x) with y % s == x % s == 0 of the H x W grid.
-template <int BN, bool C3, bool ADD = false, bool STATS = false, bool PRO = false, int ADDS = 0>
-__global__ __launch_bounds__(TS_NT) void ts_nt_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
+// Occupancy: the plain / ADD forms fit 128 VGPRs for 4 workgroups per CU (LDS 36 KiB each); at 132 they ran 3, and
+// ResNet-50's 392-row-block layers (14 x 14 at B = 256) then launch 784 workgroups for 768 slots -- a second round for
+// 16 of them (benchmarks/probes/grid_tail.py: +23 % time for +2 % rows there, profiles/r4/grid_tail/).
+// MINB = 4 (the default; DPH_TS_NT_OCC=3 selects 1, the compiler's own budget) for the 128-VGPR build.
+template <int BN, bool C3, bool ADD = false, bool STATS = false, bool PRO = false, int ADDS = 0, int MINB = 4>
+__global__ __launch_bounds__(TS_NT, PRO ? 1 : MINB) void ts_nt_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                  bf16* __restrict__ C, int M, int N, int K, int64_t lda,
                                                  int64_t ldb, int64_t ldc, int H, int W, int Cin,
                                                  const bf16* __restrict__ D = nullptr,
@@ -631,6 +635,27 @@ __global__ __launch_bounds__(256) void ts_reduce_k(const float* __restrict__ P, 
 
 }  // namespace
 
+static bool ts_nt_occ4() {
+  static const bool on = [] {
+    const char* e = getenv("DPH_TS_NT_OCC");
+    return !(e && e[0] == '3');
+  }();
+  return on;
+}
+template <int BN, bool C3, bool ADD = false, bool STATS = false, bool PRO = false, int ADDS = 0>
+static void ts_nt_launch(int nblk, hipStream_t st, const void* A, const void* B, void* C, int64_t M, int64_t N,
+                         int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int H, int W, int cin, const void* D,
+                         float* stats, const float* pro_ss) {
+  if (ts_nt_occ4())
+    hipLaunchKernelGGL((ts_nt_k<BN, C3, ADD, STATS, PRO, ADDS, 4>), dim3(nblk), dim3(TS_NT), 0, st, (const bf16*)A,
+                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, (const bf16*)D,
+                       stats, pro_ss);
+  else
+    hipLaunchKernelGGL((ts_nt_k<BN, C3, ADD, STATS, PRO, ADDS, 1>), dim3(nblk), dim3(TS_NT), 0, st, (const bf16*)A,
+                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, (const bf16*)D,
+                       stats, pro_ss);
+}
+
 bool conv1x1_supported(int64_t M, int64_t N, int64_t K) {
   return M > 0 && N % 64 == 0 && K % 64 == 0 && N >= 64 && K >= 64;
 }
@@ -643,9 +668,8 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
   if (pro_ss != nullptr) {   // BatchNorm-apply + ReLU prologue on A (1x1 only, K <= 2048; host-checked)
     const bool w128 = N % 128 == 0;
 #define DPH_TS_PRO(BN_, ST_)                                                                                     \
-    hipLaunchKernelGGL((ts_nt_k<BN_, false, false, ST_, true>), dim3(nmb * (int)(N / BN_)), dim3(TS_NT), 0, st,    \
-                       (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, 0, 0, 0,     \
-                       (const bf16*)nullptr, stats, pro_ss)
+    ts_nt_launch<BN_, false, false, ST_, true>(nmb * (int)(N / BN_), st, A, B, C, M, N, K, lda, ldb, ldc, 0, 0, 0,   \
+                                               nullptr, stats, pro_ss)
     if (stats) {
       if (w128) DPH_TS_PRO(128, true);
       else DPH_TS_PRO(64, true);
@@ -657,8 +681,8 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     return;
   }
 #define DPH_TS_NT(BN_, C3_)                                                                                     \
-  hipLaunchKernelGGL((ts_nt_k<BN_, C3_>), dim3(nmb * (int)(N / BN_)), dim3(TS_NT), 0, st, (const bf16*)A,       \
-                     (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin)
+  ts_nt_launch<BN_, C3_>(nmb * (int)(N / BN_), st, A, B, C, M, N, K, lda, ldb, ldc, H, W, cin, nullptr, nullptr,   \
+                         nullptr)
   // 128-wide column tiles whenever N allows: 64-wide tiles double the workgroup count of the short-grid 14x14 / 7x7
   // layers but measured 1.1-1.4x slower there too (profiles/conv_nt_bn_ab.log).  DPH_TS_NT_BN=64 forces them.
   static const int force_bn = [] {
@@ -677,22 +701,20 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
   }
   if (stats != nullptr && !c3) {   // BatchNorm statistics of the output (1x1 forward only)
     if (wide)
-      hipLaunchKernelGGL((ts_nt_k<128, false, false, true>), dim3(nmb * (int)(N / 128)), dim3(TS_NT), 0, st,
-                         (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin,
-                         (const bf16*)nullptr, stats);
+      ts_nt_launch<128, false, false, true>(nmb * (int)(N / 128), st, A, B, C, M, N, K, lda, ldb, ldc, H, W, cin,
+                                            nullptr, stats, nullptr);
     else
-      hipLaunchKernelGGL((ts_nt_k<64, false, false, true>), dim3(nmb * (int)(N / 64)), dim3(TS_NT), 0, st,
-                         (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin,
-                         (const bf16*)nullptr, stats);
+      ts_nt_launch<64, false, false, true>(nmb * (int)(N / 64), st, A, B, C, M, N, K, lda, ldb, ldc, H, W, cin,
+                                           nullptr, stats, nullptr);
     return;
   }
   if (D != nullptr && !c3) {   // fused residual-gradient add (1x1 only)
     if (wide)
-      hipLaunchKernelGGL((ts_nt_k<128, false, true>), dim3(nmb * (int)(N / 128)), dim3(TS_NT), 0, st, (const bf16*)A,
-                         (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, (const bf16*)D);
+      ts_nt_launch<128, false, true>(nmb * (int)(N / 128), st, A, B, C, M, N, K, lda, ldb, ldc, H, W, cin, D, nullptr,
+                                     nullptr);
     else
-      hipLaunchKernelGGL((ts_nt_k<64, false, true>), dim3(nmb * (int)(N / 64)), dim3(TS_NT), 0, st, (const bf16*)A,
-                         (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, (const bf16*)D);
+      ts_nt_launch<64, false, true>(nmb * (int)(N / 64), st, A, B, C, M, N, K, lda, ldb, ldc, H, W, cin, D, nullptr,
+                                    nullptr);
     return;
   }
   if (wide) {
@@ -709,13 +731,11 @@ void ts_gemm_nt_add_sub(const void* A, const void* B, void* C, const void* D, in
                         int64_t lda, int64_t ldb, int64_t ldc, int H, int W, int s, hipStream_t st) {
   const int nmb = (int)cdiv(M, TS_BM);
   if (N % 128 == 0)
-    hipLaunchKernelGGL((ts_nt_k<128, false, true, false, false, 2>), dim3(nmb * (int)(N / 128)), dim3(TS_NT), 0, st,
-                       (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, 0,
-                       (const bf16*)D);
+    ts_nt_launch<128, false, true, false, false, 2>(nmb * (int)(N / 128), st, A, B, C, M, N, K, lda, ldb, ldc, H, W, 0,
+                                                    D, nullptr, nullptr);
   else
-    hipLaunchKernelGGL((ts_nt_k<64, false, true, false, false, 2>), dim3(nmb * (int)(N / 64)), dim3(TS_NT), 0, st,
-                       (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, 0,
-                       (const bf16*)D);
+    ts_nt_launch<64, false, true, false, false, 2>(nmb * (int)(N / 64), st, A, B, C, M, N, K, lda, ldb, ldc, H, W, 0,
+                                                   D, nullptr, nullptr);
   (void)s;
 }
 
