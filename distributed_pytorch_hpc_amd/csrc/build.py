@@ -117,8 +117,10 @@ def build(jobs: int | None = None, verbose: bool = False, resource_usage: bool =
     cmd = [ninja, "-f", ninja_file, "-j", str(jobs)]
     if verbose:
         cmd.append("-v")
-    res = subprocess.run(cmd, check=True, cwd=build_dir, stdout=subprocess.PIPE, text=True)
-    sys.stdout.write(res.stdout)
+    res = subprocess.run(cmd, cwd=build_dir, stdout=subprocess.PIPE, text=True)
+    sys.stdout.write(res.stdout)   # ninja's log, compiler diagnostics included
+    if res.returncode != 0:
+        raise subprocess.CalledProcessError(res.returncode, cmd)
     # what this call actually compiled: ninja prints one "[i/n] ..." line per edge it ran, nothing when up to date
     ran = [ln for ln in res.stdout.splitlines() if ln.startswith("[")]
     n_hip = sum(1 for f in os.listdir(HERE) if f.endswith(".hip"))
