@@ -42,7 +42,9 @@ __device__ __forceinline__ void store4<bf16>(bf16* p, const float (&o)[4]) {
 }
 
 // NT (DPH_ADAMW_VAR=1): every stream is touched once per step, so loads and stores carry the non-temporal hint (no
-// L2 / Infinity-Cache allocation for data that will not be re-read before it is evicted).
+// L2 / Infinity-Cache allocation for data that will not be re-read before it is evicted).  Measured slower: 4 257 /
+// 4 270 vs 4 352 / 4 334 GB/s at 2^28 parameters, 7B 28 330 / 28 282 vs 28 367 / 28 323 tokens/s, bitwise equal
+// results (profiles/r4/rejected_adamw_nt/) -- kept off.
 typedef unsigned u32x2_nt __attribute__((ext_vector_type(2)));
 template <typename T>
 __device__ __forceinline__ T ld_nt(const T* p) { return __builtin_nontemporal_load(p); }
