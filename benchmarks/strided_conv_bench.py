@@ -74,12 +74,8 @@ def main():
 
         gk = torch.empty(cout, k * k * cin, device="cuda", dtype=torch.float32)
 
-        def wgrad():
-            if k == 1:
-                xs = x2.view(B, H, H, cin)[:, ::s, ::s].reshape(B * Ho * Wo, cin)
-                ops.ts_gemm_tn_(gk, dy2, xs, False)
-            else:
-                ops.convg_tn_(gk, dy2, x2, geo, False)
+        def wgrad():   # gathered rows for 1x1 and 3x3 alike (ops/conv.py _StridedConvFn)
+            ops.convg_tn_(gk, dy2, x2, geo, False)
 
         ours = {"fwd": timeit(lambda: ops.convg_nt(x2, wk, geo, None, False)), "dgrad": timeit(dgrad),
                 "wgrad": timeit(wgrad)}

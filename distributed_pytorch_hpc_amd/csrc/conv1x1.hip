@@ -907,13 +907,17 @@ bool c3wg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, c
   if (chunk_taps)   // 128-wide k' tiles of 16 chunk taps each
     return N % 64 == 0 && K % 128 == 0 && ldb == 8 && g.ntaps >= 1 && g.ntaps <= K / 8 && g.tdx[0] > 0 &&
            M * lda * 2 < (int64_t(1) << 31) && g.src_rows * ldb * 2 < (int64_t(1) << 31) && M < (int64_t(1) << 24);
+  if (g.ntaps == 1)   // a strided 1x1: the 1x1 tiles (64 / 128-wide k', no tap) over the gathered rows
+    return N % 64 == 0 && K % 64 == 0 && M * lda * 2 < (int64_t(1) << 31) &&
+           g.src_rows * ldb * 2 < (int64_t(1) << 31) && M < (int64_t(1) << 24);
   // c3w_k tiles: 192 k' (three 64-channel slabs of one tap each); fp32 row division exact below 2^24 rows
   return g.ntaps >= 1 && g.ntaps <= 9 && N % 64 == 0 && K % C3W_TK == 0 && K % g.ntaps == 0 &&
          (K / g.ntaps) % 64 == 0 && M * lda * 2 < (int64_t(1) << 31) && g.src_rows * ldb * 2 < (int64_t(1) << 31) &&
          M < (int64_t(1) << 24);
 }
 
-int c3wg_splits(int64_t M, int64_t N, int64_t K, bool chunk_taps) {
+int c3wg_splits(int64_t M, int64_t N, int64_t K, bool chunk_taps, bool one_tap) {
+  if (one_tap && !chunk_taps) return w1_splits(M, N, K);
   if (!chunk_taps) return c3w_splits(M, N, K);
   return (int)c3w_split_count(M, c3w_tiles(N, K, 128), c3w_stages());
 }
@@ -930,6 +934,19 @@ void ts_gemm_tn_geo(const void* A, const void* B, float* partial, void* C, int64
     else
       c3w_launch<64, 2, 2>(ns, (unsigned)((N / 64) * (K / 128) * nsplit), st, A, B, partial, M, N, K, lda, ldb,
                            chunk, 0, 0, 8, g);
+    ts_reduce(partial, C, N * K, nsplit, out_dtype, accumulate, st);
+    return;
+  }
+  if (g.ntaps == 1) {   // strided 1x1: the 1x1 weight-gradient tiles over the gathered X rows (no slice copy)
+    const int tk = w1_tk(K), ns1 = w1_stages();
+    const unsigned nblk = (unsigned)((N / (N % 128 == 0 ? 128 : 64)) * (K / tk) * nsplit);
+    if (N % 128 == 0) {
+      if (tk == 128) c3w_launch<128, 1, 2>(ns1, nblk, st, A, B, partial, M, N, K, lda, ldb, chunk, 0, 0, (int)K, g);
+      else c3w_launch<128, 1, 1>(ns1, nblk, st, A, B, partial, M, N, K, lda, ldb, chunk, 0, 0, (int)K, g);
+    } else {
+      if (tk == 128) c3w_launch<64, 1, 2>(ns1, nblk, st, A, B, partial, M, N, K, lda, ldb, chunk, 0, 0, (int)K, g);
+      else c3w_launch<64, 1, 1>(ns1, nblk, st, A, B, partial, M, N, K, lda, ldb, chunk, 0, 0, (int)K, g);
+    }
     ts_reduce(partial, C, N * K, nsplit, out_dtype, accumulate, st);
     return;
   }

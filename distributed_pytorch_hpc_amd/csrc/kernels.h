@@ -191,7 +191,7 @@ void convg_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 // weight gradient C[N, K] (+)= dY[M, N]^T X_gathered[M, K] on c3w_k (K = ntaps * Cin, a multiple of 192)
 bool c3wg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g,
                     bool chunk_taps = false);
-int c3wg_splits(int64_t M, int64_t N, int64_t K, bool chunk_taps);
+int c3wg_splits(int64_t M, int64_t N, int64_t K, bool chunk_taps, bool one_tap = false);
 void ts_gemm_tn_geo(const void* A, const void* B, float* partial, void* C, int64_t M, int64_t N, int64_t K,
                     int64_t lda, int64_t ldb, int nsplit, int out_dtype, bool accumulate, const ConvGeo& g,
                     hipStream_t stream, bool chunk_taps = false);

@@ -856,11 +856,11 @@ void convg_tn_(Tensor C, const Tensor& A, const Tensor& B, at::IntArrayRef geo, 
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
               "convg_tn_: row-major operands with 16-B aligned rows required");
   TORCH_CHECK(dph::c3wg_supported(M, N, K, A.stride(0), B.stride(0), g, chunk_taps),
-              "convg_tn_: unsupported shape (N % 64, ntaps * Cin % 192, Cin % 64)");
+              "convg_tn_: unsupported shape (N % 64, ntaps * Cin % 192, Cin % 64; one tap: Cin % 64)");
   TORCH_CHECK(C.scalar_type() == at::kBFloat16 || C.scalar_type() == at::kFloat, "convg_tn_: C bf16 or fp32");
   check_align16(A, "A");
   check_align16(B, "B");
-  const int ns = dph::c3wg_splits(M, N, K, chunk_taps);
+  const int ns = dph::c3wg_splits(M, N, K, chunk_taps, g.ntaps == 1);
   Tensor part = at::empty({(int64_t)ns * N * K}, A.options().dtype(at::kFloat));
   dph::ts_gemm_tn_geo(A.data_ptr(), B.data_ptr(), part.data_ptr<float>(), C.data_ptr(), M, N, K, A.stride(0),
                       B.stride(0), ns, dt_code(C), accumulate, g, cur_stream(), chunk_taps);

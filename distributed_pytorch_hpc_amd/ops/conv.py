@@ -455,10 +455,10 @@ class _StridedConvFn(torch.autograd.Function):
             mg = _main_grad_cl(w, cout, k * k * C)
             tgt = mg if mg is not None else torch.empty((cout, k * k * C), dtype=ctx.wdtype, device=dy.device)
             acc = bool(getattr(w, "_dph_accum", False)) if mg is not None else False
-            if k == 1:   # 1x1: the dense weight-gradient kernel over the strided sub-image
+            if k == 1 and os.environ.get("DPH_STRIDED1_COPY", "0") == "1":   # A/B: sub-image copy + dense kernel
                 xs = x2.view(B, H, W, C)[:, ::s, ::s].reshape(B * Ho * Wo, C)
                 _lib.ops().ts_gemm_tn_(tgt, dy2, xs, acc)
-            else:
+            else:   # 1x1 included: the weight-gradient kernel gathers the strided rows itself (no sub-image copy)
                 _lib.ops().convg_tn_(tgt, dy2, x2, strided_fwd_geo(H, W, k, s, p), acc)
             if mg is not None:
                 w._dph_accum = True
