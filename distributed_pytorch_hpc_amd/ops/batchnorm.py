@@ -147,7 +147,11 @@ class BatchNormAct2d(nn.BatchNorm2d):
 
 
 # ------------------------------------------------------------------------------------------------ BN + ReLU -> 1x1 conv
-_PROLOGUE = os.environ.get("DPH_BN_PROLOGUE", "1") != "0"
+# Off by default since round 4: with bn2 applied by its own pass, conv3's weight gradient runs on the plain 1x1 kernel
+# (c3w_k identity rows), which beats the prologue form's register-staged ts_tn_k by more than the extra activation
+# write / read costs -- ResNet-50 10 435 / 10 453 / 10 491 vs 10 318 / 10 323 / 10 345 img/s, interleaved
+# (profiles/r4/bn_prologue_ab/).  DPH_BN_PROLOGUE=1 restores the fused form.
+_PROLOGUE = os.environ.get("DPH_BN_PROLOGUE", "0") == "1"
 
 
 class _BNReLUConv1x1Fn(torch.autograd.Function):
