@@ -89,6 +89,8 @@ def parse(argv=None):
                     help="process-group backend (default: nccl = RCCL on GPU); gloo lets several ranks share one GPU "
                          "to rehearse the N > 1 path (tests/test_bench_gpu.py)")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--no-telemetry", action="store_true",
+                    help="do not sample GPU clock / power / temperature (amdsmi host thread) during the run")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step as one HIP graph after the warm-up (runtime/graphs.py; one rank only)")
     ap.add_argument("--fp8", action="store_true",
@@ -204,6 +206,12 @@ def main(argv=None):
             rt.barrier()
         sync()
 
+    # clock / power / temperature of this rank's GPU on a host thread (amdsmi; never touches a stream)
+    tel = None
+    if not cpu and not args.no_telemetry:
+        from distributed_pytorch_hpc_amd.utils.telemetry import GpuTelemetry
+
+        tel = GpuTelemetry(torch.cuda.current_device())
     loss = None
     log(f"[bench] {args.layout}: workload built, {args.warmup} warm-up + {args.steps} timed steps")
     for i in range(args.warmup):
@@ -226,6 +234,8 @@ def main(argv=None):
     # per-step device-time marks: events recorded between steps (no host synchronisation inside the timed region)
     marks = [] if cpu else [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     host_marks = []
+    if tel is not None:
+        tel.mark("timed_start")
     t0 = time.perf_counter()
     for i in range(args.steps):
         if marks:
@@ -239,6 +249,18 @@ def main(argv=None):
     host_marks.append(time.perf_counter())
     sync_all()
     elapsed = time.perf_counter() - t0
+    telem = {}
+    if tel is not None:
+        tel.mark("timed_end")
+        tel.stop()
+        flops = (wl.flops_per_item or 0) * wl.items_per_step * args.steps / max(world, 1)
+        telem = tel.summary("timed_start", "timed_end", flops=flops or None)
+        if dist.is_initialized() and world > 1:
+            per_rank = [None] * world
+            dist.all_gather_object(per_rank, {k: telem.get(k) for k in ("sclk_mhz", "power_w", "energy_j")})
+            telem["per_rank"] = [{"sclk_median": (r.get("sclk_mhz") or {}).get("median"),
+                                  "power_median": (r.get("power_w") or {}).get("median"),
+                                  "energy_j": r.get("energy_j")} for r in per_rank]
     step_ms = ([marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)] if marks else
                [1000.0 * (host_marks[i + 1] - host_marks[i]) for i in range(args.steps)])
     last_loss = float(loss.detach()) if loss is not None else None
@@ -276,6 +298,7 @@ def main(argv=None):
             "rccl_version": preflight.rccl_version() if not cpu else None,
             **pre, **replica, **wl.extra, **graph_info,
             **({"xgmi_allreduce": xgmi} if xgmi else {}),
+            **telem,
         }
         if wl.flops_per_item:
             rec["mfu_vs_2.5PF_bf16_dense"] = round(rate / world * wl.flops_per_item / 2.5e15, 4)

@@ -70,14 +70,14 @@ def main():
         def dgrad():
             dx2 = (torch.empty if full else torch.zeros)((B * H * H, cin), dtype=torch.bfloat16, device="cuda")
             for g, bk in classes:
-                ops.convg_nt(dy2, bk, g, dx2, False)
+                ops.convg_nt_out_(dy2, bk, g, dx2)
 
         gk = torch.empty(cout, k * k * cin, device="cuda", dtype=torch.float32)
 
         def wgrad():   # gathered rows for 1x1 and 3x3 alike (ops/conv.py _StridedConvFn)
             ops.convg_tn_(gk, dy2, x2, geo, False)
 
-        ours = {"fwd": timeit(lambda: ops.convg_nt(x2, wk, geo, None, False)), "dgrad": timeit(dgrad),
+        ours = {"fwd": timeit(lambda: ops.convg_nt(x2, wk, geo, False)), "dgrad": timeit(dgrad),
                 "wgrad": timeit(wgrad)}
         r = {"shape": f"{k}x{k}/2 {cin}->{cout} @{H}", "miopen": mi, "dph": ours}
         rows.append(r)

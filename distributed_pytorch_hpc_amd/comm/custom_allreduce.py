@@ -49,7 +49,8 @@ def _group_ranks(group):
 
 
 class XgmiAllReduce:
-    def __init__(self, group=None, max_bytes: int = 64 << 20, timeout_s: float = 10.0, max_blocks: int = 64):
+    def __init__(self, group=None, max_bytes: int = 64 << 20, timeout_s: float = None, max_blocks: int = 64):
+        timeout_s = _TIMEOUT_S if timeout_s is None else timeout_s
         if not dist.is_initialized():
             raise RuntimeError("XgmiAllReduce needs an initialised process group")
         _lib.require()
@@ -98,7 +99,8 @@ class XgmiAllReduce:
         return out
 
     def errors(self) -> int:
-        """Number of barrier timeouts recorded on this rank (0 when healthy)."""
+        """Non-zero once a barrier of this rank's kernels timed out (0 when healthy).  No device synchronisation:
+        the kernel writes a host-mapped word, so a kernel still in flight reports on a later call."""
         return int(self._ops.car_status(self.ctx))
 
     def close(self):
@@ -225,6 +227,30 @@ def probe_crossover(group=None, sizes=(4 << 10, 16 << 10, 64 << 10, 256 << 10, 1
     verified = bool(ok.item() == 1.0)
     return {"samples": samples, "verified": verified,
             "crossover_bytes": choose_crossover(samples) if verified else 0}
+
+
+class XgmiAllReduceError(RuntimeError):
+    """A direct-peer all-reduce barrier timed out: its sums may hold a peer's stale staging data."""
+
+
+def check_health() -> None:
+    """Raise XgmiAllReduceError if any cached direct-peer all-reduce recorded a barrier timeout, after turning the
+    path off for that group (RCCL takes every later message).  A timed-out barrier lets the kernel finish with
+    whatever the late peer's staging buffer held, so the affected step's sums are not trustworthy: the engines call
+    this once per optimizer step (host-memory read, no device sync) and stop instead of training on them."""
+    bad = []
+    for key, car in list(_CACHE.items()):
+        if car is not None and car.errors():
+            bad.append(key)
+            _POLICY.pop(key, None)
+    if bad:
+        raise XgmiAllReduceError(
+            f"direct-peer xGMI all-reduce barrier timed out on {len(bad)} group(s) (a peer stalled > "
+            f"{_TIMEOUT_S:.0f} s); gradients / activations reduced through it in this step may be wrong. The path is "
+            "now disabled for those groups.")
+
+
+_TIMEOUT_S = 10.0
 
 
 def get_custom_allreduce(group=None) -> Optional[XgmiAllReduce]:

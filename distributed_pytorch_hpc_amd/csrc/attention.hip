@@ -26,6 +26,8 @@
 // dropped, rescaled P for dV and dS = P (Z dP / (1-p) - delta) for dK; dQ the same dS.  This is the
 // nn.MultiheadAttention(dropout=...) path of the pipeline transformer (03_pipeline_training.py:57-58,70).
 #include <cstdlib>
+#include <string>
+#include <type_traits>
 
 #include "dph_common.h"
 #include "kernels.h"
@@ -248,27 +250,54 @@ struct KVTilePlan {
   // drains the in-flight prefetch (vmcnt(0)) before the first ds_read of the CURRENT tile's V image (it cannot prove
   // the two images disjoint).  The caller retires it with wait_vmcnt<0>() + s_barrier before reading `img`.
   // `lds_w` is this wave's byte address of the image pair (lds_addr(img + wave * 1 KiB)).
-  int prow[NS], pch[NS];
+  // Instruction i of a lane copies chunk L = tid + NT i; with NT a multiple of 256 the swizzle of its 256-B line is that
+  // of i = 0, so its source row is prow + i NT / NC and its chunk column pch: ONE row / column pair per lane (a per-i
+  // table is spilled around the tile loop at high register pressure, and hipcc's vmcnt(0) for the reload would drain
+  // the in-flight DMA).
+  static_assert(NT % 256 == 0, "stage_async assumes whole 16-line swizzle periods per instruction");
+  static constexpr int RSTEP = NT / NC;   // rows between a lane's consecutive instructions
+  int prow, pch;
   __device__ __forceinline__ void init_async() {
-#pragma unroll
-    for (int i = 0; i < NS; ++i) {
-      const int L = threadIdx.x + NT * i, line = L >> 4, slot = L & 15;
-      const int F = (line << 4) + (slot ^ (((line & 3) << 2) | ((line >> 2) & 3)));
-      prow[i] = F / NC;
-      pch[i] = (F % NC) * 8;
-    }
+    const int L = threadIdx.x, line = L >> 4, slot = L & 15;
+    const int F = (line << 4) + (slot ^ (((line & 3) << 2) | ((line >> 2) & 3)));
+    prow = F / NC;
+    pch = (F % NC) * 8;
   }
   __device__ __forceinline__ void stage_async(unsigned lds_w, const bf16* kp, const bf16* vp, int64_t k_ss,
                                               int64_t v_ss, int k0, int Sk) const {
-    const int rmax = Sk - 1 - k0;   // ragged last tile: rows past the end re-read the last valid row
-    const bf16* kt = kp + (int64_t)k0 * k_ss;
-    const bf16* vt = vp + (int64_t)k0 * v_ss;
+    // wave-uniform by construction; readfirstlane keeps the bases in SGPRs inside divergent callers
+    const bf16* kt = uniform_ptr(kp + (int64_t)k0 * k_ss);
+    const bf16* vt = uniform_ptr(vp + (int64_t)k0 * v_ss);
+    if (k0 + BN <= Sk) {   // full tile: byte offsets step by a wave-uniform constant
+      const unsigned ok = (unsigned)((prow * k_ss + pch) * 2), ov = (unsigned)((prow * v_ss + pch) * 2);
+      const unsigned sk = (unsigned)(RSTEP * k_ss * 2), sv = (unsigned)(RSTEP * v_ss * 2);
 #pragma unroll
-    for (int i = 0; i < NS; ++i)
-      lds_dma16(kt, (unsigned)(((int64_t)min(prow[i], rmax) * k_ss + pch[i]) * 2), lds_w + NT * i * 16);
+      for (int i = 0; i < NS; ++i) lds_dma16(kt, ok + i * sk, lds_w + NT * i * 16);
 #pragma unroll
-    for (int i = 0; i < NS; ++i)
-      lds_dma16(vt, (unsigned)(((int64_t)min(prow[i], rmax) * v_ss + pch[i]) * 2), lds_w + TILE + NT * i * 16);
+      for (int i = 0; i < NS; ++i) lds_dma16(vt, ov + i * sv, lds_w + TILE + NT * i * 16);
+    } else {                // ragged last tile: rows past the end re-read the last valid row
+      const int rmax = Sk - 1 - k0;
+#pragma unroll
+      for (int i = 0; i < NS; ++i) {
+        const int r = min(prow + i * RSTEP, rmax);
+        lds_dma16(kt, (unsigned)((r * k_ss + pch) * 2), lds_w + NT * i * 16);
+        lds_dma16(vt, (unsigned)((r * v_ss + pch) * 2), lds_w + TILE + NT * i * 16);
+      }
+    }
+  }
+  // One image (K or V) of tile [k0, k0 + 64) -> `lds_w` (this wave's 1 KiB share of the image), same rules.
+  __device__ __forceinline__ void stage_one_async(unsigned lds_w, const bf16* xp, int64_t x_ss, int k0, int Sk) const {
+    const bf16* xt = uniform_ptr(xp + (int64_t)k0 * x_ss);
+    if (k0 + BN <= Sk) {
+      const unsigned o = (unsigned)((prow * x_ss + pch) * 2), st = (unsigned)(RSTEP * x_ss * 2);
+#pragma unroll
+      for (int i = 0; i < NS; ++i) lds_dma16(xt, o + i * st, lds_w + NT * i * 16);
+    } else {
+      const int rmax = Sk - 1 - k0;
+#pragma unroll
+      for (int i = 0; i < NS; ++i)
+        lds_dma16(xt, (unsigned)((min(prow + i * RSTEP, rmax) * x_ss + pch) * 2), lds_w + NT * i * 16);
+    }
   }
 };
 
@@ -291,7 +320,7 @@ struct RowStagePlan {
   __device__ __forceinline__ void stage(unsigned lds_w, const bf16* base, int64_t rstride, int row0,
                                         int nvalid) const {
     const int rmax = nvalid - 1 - row0;
-    const bf16* t = base + (int64_t)row0 * rstride;
+    const bf16* t = uniform_ptr(base + (int64_t)row0 * rstride);   // wave-uniform: keep it in SGPRs
 #pragma unroll
     for (int i = 0; i < NI; ++i)
       if (CHUNKS % NT == 0 || (int)threadIdx.x + NT * i < CHUNKS)
@@ -529,6 +558,238 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
       p.lse[((int64_t)b * p.Hq + hq) * p.Sq + myq] =
           lsum > 0.f ? (m + __log2f(lsum)) * 0.6931471805599453f : -INFINITY;
   }
+}
+
+// ==================================================================================================
+// Forward, software-pipelined (default for HD 64 / 128 without dropout or ring merge)
+// ==================================================================================================
+// The geometry of attn_fwd_k (4 waves = 128 query rows per workgroup, 32 rows per wave, two workgroups per CU so the
+// two waves on a SIMD belong to independent workgroups), with the tile loop run over 32-key SUB-tiles u so that
+// inside ONE wave the matrix pipe and the VALU always have independent work:
+//   sub-iteration u (S_u = raw scores of sub-tile u, computed in sub-iteration u-1):
+//     [odd u = 2t+1: wait + barrier; LDS-DMA of V tile t+1 and K tile t+2]
+//     BB_a   O += V_{u-1}^T P_{u-1}^T (8 MFMA)   beside   row max of S_u, rescale test
+//            [rare, wave-uniform: rescale O, l and S_u]
+//     BB_b   S_{u+1} = K_{u+1} Q^T (8 MFMA)     beside   exp2 / row sum / bf16 pack of S_u -> P_u
+// attn_fwd_k runs S -> softmax -> PV as one dependent chain per tile, so a wave's VALU and MFMA phases never overlap
+// and only the partner wave on the SIMD can fill them (PMC round 4: MFMA busy 0.46, issue stalls 41 %).  32-key
+// sub-tiles keep two score tiles, the P tile and O within the 256-register budget (64-key sub-tiles spill).
+// K and V have separate 2-slot rings (64 KB per workgroup, two workgroups per CU): V of a tile is read two
+// sub-iterations after its K, so at the barrier of u = 2t+1 the slots of V_{t-1} and K_t are free, V_{t+1} and K_{t+2}
+// are issued into them, and each DMA has a whole tile of compute to land before the barrier that waits for it.
+// No VALU pass for the softmax bookkeeping: Q is prescaled by scale * log2(e) when loaded and every S accumulator
+// starts at -m (the running max, log2 units) -- or at -inf where the causal / ragged mask hides the key -- so the MFMA
+// chain leaves s * scale * log2e - m and p = exp2 of it directly.  m is raised only when a lane's max exceeds it by
+// more than RESCALE_THR (lazy rescaling: p <= 2^THR in between, exact after the final 1 / l); sub-tile 0 always sets it.
+template <int HD, bool CAUSAL, int VAR = 0>
+__global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(AttnParams p) {
+  constexpr int NW = 4;
+  using Plan = KVTilePlan<HD, 64 * NW>;
+  constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
+  constexpr float RESCALE_THR = 8.f;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  // wid through readfirstlane: provably wave-uniform, so the per-wave tile count and the body selection are scalar
+  // branches and the DMA operands stay in SGPRs
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5,
+            l32 = lane & 31;
+  const int nqb = (p.Sq + BM - 1) / BM;
+  int bx, hq, b;
+  xcd_block(nqb, p.Hq, bx, hq, b, nqb * p.Hq * p.B);
+  const int qb = CAUSAL ? nqb - 1 - bx : bx;   // heaviest causal blocks first
+  const int hk = hq / (p.Hq / p.Hkv);
+  const int q0 = qb * BM, q0w = q0 + 32 * wid;
+  const int myq = q0w + l32;
+  const int off = p.Sk - p.Sq;
+
+  const bf16* qp = (const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
+  const bf16* kp = (const bf16*)p.k + (int64_t)b * p.k_sb + (int64_t)hk * p.k_sh;
+  const bf16* vp = (const bf16*)p.v + (int64_t)b * p.v_sb + (int64_t)hk * p.v_sh;
+
+  // Q^T fragments (B operand of S^T = K Q^T), prescaled by c = scale * log2(e) in fp32, rounded once to bf16
+  const float c = p.scale * 1.4426950408889634f;
+  bf16x8 qf[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    bf16x8 x = myq < p.Sq ? *reinterpret_cast<const bf16x8*>(qp + (int64_t)myq * p.q_ss + kk * 16 + 8 * h) : zero8();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * c);
+    qf[kk] = x;
+  }
+
+  int kv_end = p.Sk;
+  if (CAUSAL) kv_end = min(p.Sk, q0 + BM + off);
+  const int ntiles = __builtin_amdgcn_readfirstlane(kv_end > 0 ? (kv_end + BN - 1) / BN : 0);
+  // sub-tiles (32 keys) with a key visible to this wave; the workgroup still walks all ntiles for the shared staging
+  int wsub = 2 * ntiles;
+  if (CAUSAL) {
+    const int last = q0w + 31 + off;
+    wsub = last < 0 ? 0 : min(2 * ntiles, last / 32 + 1);
+  }
+  wsub = __builtin_amdgcn_readfirstlane(min(wsub, (p.Sk + 31) / 32));   // scalar loop bounds (uniform branches)
+
+  Plan plan;
+  plan.init(lane, p.k_ss);
+  plan.init_async();
+  const unsigned lds_w = lds_addr(smem + wid * 64 * 16);
+
+  f32x16 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float m = 0.f, lsum = 0.f;   // running max (log2 units) / this half-wave's partial row sum
+
+  // LDS: K slots 0 / 1 | V slots 0 / 1 (tile t in slot t & 1)
+  if (ntiles > 0) {
+    plan.stage_one_async(lds_w, kp, p.k_ss, 0, p.Sk);
+    plan.stage_one_async(lds_w + 2 * TILE, vp, p.v_ss, 0, p.Sk);
+    plan.stage_one_async(lds_w + TILE, kp, p.k_ss, min(1, ntiles - 1) * BN, p.Sk);
+  }
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+
+  auto kslot = [&](int u) { return smem + ((u >> 1) & 1) * TILE; };
+  auto vslot = [&](int u) { return smem + 2 * TILE + ((u >> 1) & 1) * TILE; };
+  auto needs_mask = [&](int u) { return u * 32 + 32 > p.Sk || (CAUSAL && u * 32 + 31 > q0w + off); };
+  // visible keys of this lane's query: key <= lim
+  const int lim = CAUSAL ? min(myq + off, p.Sk - 1) : p.Sk - 1;
+  // S_u = K_u Q^T - m (-inf where masked) for sub-tile u, K fragments straight from the swizzled LDS image.  The
+  // masked start values are a wave-uniform branch ahead of the MFMA chain, so the chain and the VALU work placed
+  // beside it stay one basic block.
+  auto kread = [&](int u, bf16x8 (&kf)[KS]) {
+    const char* Kl = kslot(u);
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) kf[kk] = lds_b128(Kl, plan.row(u & 1, kk));
+  };
+  auto qk_f = [&](int u, const bf16x8 (&kf)[KS]) {
+    f32x16 a;
+    if (needs_mask(u)) {
+      const int d = u * 32 + 4 * h - lim;   // key(r) - lim = acc_row(r, 0) + d
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a[r] = acc_row(r, 0) + d <= 0 ? -m : -INFINITY;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) a[r] = -m;
+    }
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) a = mfma32(kf[kk], qf[kk], a);
+    return a;
+  };
+  auto qk = [&](int u) {
+    bf16x8 kf[KS];
+    kread(u, kf);
+    return qk_f(u, kf);
+  };
+  // O += V_u^T P_u^T: the sub-tile's two 16-key k-steps of the V image
+  auto pv = [&](int u, const bf16x8 (&pf)[2]) {
+    const char* Vl = vslot(u);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int ks = 2 * (u & 1) + j;
+        o[dt] = mfma32(lds_tr2(Vl, plan.tr(ks, dt, 0), plan.tr(ks, dt, 1)), pf[j], o[dt]);
+      }
+  };
+  // row max of S_u (both half-waves) and the lazy rescale (wave-uniform branch, rare after sub-tile 0)
+  auto rescale = [&](f32x16& s, bool first) {
+    float mx = fmaxf(fmaxf(s[0], s[1]), s[2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) mx = fmaxf(mx, fmaxf(s[r], s[r + 1]));
+    mx = fmaxf(mx, s[15]);
+    mx = half_max(mx);
+    if (first || __ballot(mx > RESCALE_THR)) {
+      const float d = first ? (mx == -INFINITY ? 0.f : mx) : fmaxf(mx, 0.f);
+      const float alpha = exp2_(-d);
+      lsum *= alpha;
+      m += d;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] -= d;
+    }
+  };
+  auto expsum = [&](f32x16& s, bf16x8 (&pf)[2]) {
+    float ls0 = 0.f, ls1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      s[r] = exp2_(s[r]);
+      s[r + 1] = exp2_(s[r + 1]);
+      ls0 += s[r];
+      ls1 += s[r + 1];
+    }
+    lsum += ls0 + ls1;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pf[j][i] = (bf16)s[8 * j + i];
+  };
+  // u = 2t+1: wait for V_t and K_{t+1} (issued one tile ago), barrier, then LDS-DMA of V_{t+1} and K_{t+2} into the
+  // slots of V_{t-1} and K_t, whose last reads (PV_{2t-1}, S_{2t+1}) every wave has made before this barrier.  Past the
+  // last tile the DMA re-reads the last tile (stage_one_async's row clamp needs k0 < Sk) into a free slot, so every
+  // workgroup-wide step is the same in every iteration.
+  auto sync = [&](int t) {
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    plan.stage_one_async(lds_w + 2 * TILE + ((t + 1) & 1) * TILE, vp, p.v_ss, min(t + 1, ntiles - 1) * BN, p.Sk);
+    plan.stage_one_async(lds_w + (t & 1) * TILE, kp, p.k_ss, min(t + 2, ntiles - 1) * BN, p.Sk);
+  };
+
+  // One body for every sub-tile (several specialised bodies spill at this register budget): sub-tile 0 multiplies a
+  // zero P with V_0 (adds exactly 0: V_0 is finite staged data), and the wave's last sub-tile computes an S_{u+1}
+  // that is dropped (its K slot holds staged data) and finishes its own PV at once, before its V slot is recycled.
+  f32x16 s = {};
+  bf16x8 pf[2] = {zero8(), zero8()};
+  if (wsub > 0) s = qk(0);
+  for (int u = 0; u < 2 * ntiles; ++u) {
+    if (u & 1) sync(u >> 1);
+    if (u < wsub) {
+      // ---- BB_a: PV_{u-1} beside max(S_u) ----
+      bf16x8 kf[KS];
+      if constexpr ((VAR & 1) != 0) kread(u + 1, kf);   // K of S_{u+1} in flight during PV_{u-1}
+      pv(max(u - 1, 0), pf);
+      if constexpr ((VAR & 2) != 0) {
+        __builtin_amdgcn_sched_group_barrier(0x100, (VAR & 1) ? 12 : 4, 0);
+#pragma unroll
+        for (int i = 0; i < 2 * DT; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (i + 2 < 2 * DT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        }
+      }
+      rescale(s, u == 0);
+      // ---- BB_b: S_{u+1} beside exp(S_u) ----
+      if constexpr ((VAR & 1) == 0) kread(u + 1, kf);
+      const f32x16 sn = qk_f(u + 1, kf);
+      expsum(s, pf);
+      if constexpr ((VAR & 2) != 0) {
+        if constexpr ((VAR & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 4, 1);
+#pragma unroll
+        for (int i = 0; i < KS; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+          if ((VAR & 1) == 0 && i + 4 < KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+          __builtin_amdgcn_sched_group_barrier(0x002, 8, 1);
+        }
+      }
+      s = sn;
+      if (u == wsub - 1) pv(u, pf);
+    }
+  }
+  wait_vmcnt<0>();   // the last iterations' DMA must land before the slabs reuse the ring
+  __syncthreads();
+
+  // ---- epilogue: O = O^T / l through this wave's LDS slab, lse ----
+  lsum = half_sum(lsum);
+  static_assert(NW * 32 * HD * 2 <= 4 * TILE, "epilogue slabs exceed the forward kernel's LDS");
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  bf16* o0 = (bf16*)p.o + (int64_t)b * p.o_sb + (int64_t)q0w * p.o_ss + (int64_t)hq * p.o_sh;
+  store_rows_lds<DT>(smem + wid * (32 * HD * 2), o0, p.o_ss, min(32, p.Sq - q0w), o, inv, h, l32, 0, nullptr, nullptr,
+                     0);
+  if (myq < p.Sq && h == 0 && p.lse)
+    p.lse[((int64_t)b * p.Hq + hq) * p.Sq + myq] = lsum > 0.f ? (m + __log2f(lsum)) * 0.6931471805599453f : -INFINITY;
 }
 
 // ==================================================================================================
@@ -1017,8 +1278,46 @@ static void fwd_launch_nw(const AttnParams& p, hipStream_t st) {
   else hipLaunchKernelGGL((attn_fwd_k<HD, false, NW, false, STG>), grid, dim3(64 * NW), lds, st, p);
 }
 
+// DPH_ATTN_FWD=pipe: the software-pipelined forward (attn_fwd_pipe_k) instead of attn_fwd_k (A/B; slower so far:
+// 734 vs 788 TFLOP/s on B 8, H 32, S 4096, D 128 causal, profiles/r5/attn_fwd_pipe/)
+static bool attn_fwd_legacy() {
+  static const bool v = [] {
+    const char* e = getenv("DPH_ATTN_FWD");
+    return !(e && std::string(e) == "pipe");
+  }();
+  return v;
+}
+
 template <int HD>
 static void fwd_launch(const AttnParams& p, hipStream_t st) {
+  if constexpr (HD >= 64) {
+    if (p.drop_p == 0.f && !p.acc_o && !attn_fwd_legacy()) {
+      const dim3 grid((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));   // 1-D: xcd_block() maps it
+      const size_t lds = 4 * 64 * HD * 2;
+      static const int var = [] {
+        const char* e = getenv("DPH_ATTN_FWD_VAR");
+        return e ? atoi(e) : 0;
+      }();
+      switch (var) {
+        case 1:
+          if (p.causal) hipLaunchKernelGGL((attn_fwd_pipe_k<HD, true, 1>), grid, dim3(256), lds, st, p);
+          else hipLaunchKernelGGL((attn_fwd_pipe_k<HD, false, 1>), grid, dim3(256), lds, st, p);
+          break;
+        case 2:
+          if (p.causal) hipLaunchKernelGGL((attn_fwd_pipe_k<HD, true, 2>), grid, dim3(256), lds, st, p);
+          else hipLaunchKernelGGL((attn_fwd_pipe_k<HD, false, 2>), grid, dim3(256), lds, st, p);
+          break;
+        case 3:
+          if (p.causal) hipLaunchKernelGGL((attn_fwd_pipe_k<HD, true, 3>), grid, dim3(256), lds, st, p);
+          else hipLaunchKernelGGL((attn_fwd_pipe_k<HD, false, 3>), grid, dim3(256), lds, st, p);
+          break;
+        default:
+          if (p.causal) hipLaunchKernelGGL((attn_fwd_pipe_k<HD, true>), grid, dim3(256), lds, st, p);
+          else hipLaunchKernelGGL((attn_fwd_pipe_k<HD, false>), grid, dim3(256), lds, st, p);
+      }
+      return;
+    }
+  }
   if (p.drop_p > 0.f) {   // dropout: 4-wave instantiations only
     const dim3 grid((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
     const size_t lds = 2 * 2 * 64 * HD * 2;

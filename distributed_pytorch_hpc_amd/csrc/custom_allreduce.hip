@@ -47,6 +47,7 @@ constexpr size_t CAR_SIG_BYTES = (sizeof(CarSignal) + 4095) / 4096 * 4096;
 
 struct CarPeers {
   char* base[CAR_MAX_RANKS];
+  uint32_t* err_host;   // device view of a pinned, host-mapped word: the host reads timeouts without a device sync
 };
 
 #define DPH_HIP_OK(expr)                                                                          \
@@ -74,6 +75,7 @@ __device__ __forceinline__ void car_barrier(const CarPeers& p, int rank, int wor
     while ((int)(__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       if (wall_clock64() - t0 > timeout_ticks) {
         __hip_atomic_fetch_add(&sig(p, rank)->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(p.err_host, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -202,6 +204,7 @@ struct CarContext {
   int rank = 0, world = 1, device = 0;
   size_t max_bytes = 0;
   char* local = nullptr;
+  uint32_t* err_host = nullptr;   // pinned host memory (mapped into the device's address space)
   CarPeers peers{};
   bool opened[CAR_MAX_RANKS] = {};
   uint64_t timeout_ticks = 0;
@@ -224,6 +227,13 @@ int64_t car_create(int rank, int world, int64_t max_bytes, double timeout_s) {
   DPH_HIP_OK(hipDeviceSynchronize());
   c->local = static_cast<char*>(p);
   c->peers.base[rank] = c->local;
+  void* hp = nullptr;
+  DPH_HIP_OK(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  c->err_host = static_cast<uint32_t*>(hp);
+  *c->err_host = 0u;
+  void* dp = nullptr;
+  DPH_HIP_OK(hipHostGetDevicePointer(&dp, hp, 0));
+  c->peers.err_host = static_cast<uint32_t*>(dp);
   int khz = 0;
   DPH_HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
   c->timeout_ticks = (uint64_t)(timeout_s * (double)khz * 1000.0);
@@ -299,11 +309,12 @@ void car_allreduce(int64_t ctx, const void* in, void* out, int64_t bytes, int dt
 #undef DPH_CAR_LAUNCH
 }
 
+// Non-zero once any barrier of this rank's kernels timed out.  Reads the host-mapped word the kernel stores to at
+// system scope: no device synchronisation, so the training engines can check it every step (a kernel still in
+// flight reports on a later check).
 int64_t car_status(int64_t ctx) {
   auto* c = reinterpret_cast<CarContext*>(ctx);
-  uint32_t err = 0;
-  DPH_HIP_OK(hipMemcpy(&err, c->local + offsetof(CarSignal, err), sizeof(err), hipMemcpyDeviceToHost));
-  return err;
+  return (int64_t)__atomic_load_n(c->err_host, __ATOMIC_ACQUIRE);
 }
 
 void car_destroy(int64_t ctx) {
@@ -313,6 +324,7 @@ void car_destroy(int64_t ctx) {
   for (int r = 0; r < c->world; ++r)
     if (c->opened[r]) (void)hipIpcCloseMemHandle(c->peers.base[r]);
   if (c->local) (void)hipFree(c->local);
+  if (c->err_host) (void)hipHostFree(c->err_host);
   delete c;
 }
 

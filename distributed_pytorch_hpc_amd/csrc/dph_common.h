@@ -118,6 +118,14 @@ __device__ __forceinline__ int xcd_remap(int bid, int n) {
   return xcd * (n >> 3) + min(xcd, n & 7) + (bid >> 3);
 }
 
+// A pointer the caller knows to be wave-uniform, forced into SGPRs (lds_dma16's `sbase` operand must be scalar).
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (T*)(((unsigned long long)hi << 32) | lo);
+}
+
 // Wave-uniform LDS byte address of a __shared__ pointer (for lds_dma16's M0 operand).
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return __builtin_amdgcn_readfirstlane(

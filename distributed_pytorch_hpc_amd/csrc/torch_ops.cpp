@@ -840,6 +840,14 @@ std::vector<Tensor> convg_nt(const Tensor& A, const Tensor& B, at::IntArrayRef g
   return res;
 }
 
+std::vector<Tensor> convg_nt_fresh(const Tensor& A, const Tensor& B, at::IntArrayRef geo, bool stats, bool chunk_taps) {
+  return convg_nt(A, B, geo, c10::nullopt, stats, chunk_taps);
+}
+
+void convg_nt_out_(const Tensor& A, const Tensor& B, at::IntArrayRef geo, Tensor out) {
+  (void)convg_nt(A, B, geo, out, false, false);
+}
+
 // C[N, ntaps * Cin] (+)= dY[M, N]^T X_gathered[M, ntaps * Cin]; X = the [images * Hs * Ws, Cin] input.
 void convg_tn_(Tensor C, const Tensor& A, const Tensor& B, at::IntArrayRef geo, bool accumulate, bool chunk_taps) {
   check_cuda(A, "A");
@@ -1420,7 +1428,9 @@ TORCH_LIBRARY(dph, m) {
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0, Tensor? pro_ss=None) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
   m.def("conv3x3_dgrad_weight(Tensor w) -> Tensor");
-  m.def("convg_nt(Tensor A, Tensor B, int[] geo, Tensor? out=None, bool stats=False, bool chunk_taps=False) -> Tensor[]");
+  m.def("convg_nt(Tensor A, Tensor B, int[] geo, bool stats=False, bool chunk_taps=False) -> Tensor[]");
+  // the parity classes of one strided input gradient write disjoint rows of one shared dx: an in-place op
+  m.def("convg_nt_out_(Tensor A, Tensor B, int[] geo, Tensor(a!) out) -> ()");
   m.def("convg_tn_(Tensor(a!) C, Tensor A, Tensor B, int[] geo, bool accumulate, bool chunk_taps=False) -> ()");
   m.def("ts_gemm_nt_add_sub(Tensor A, Tensor B, Tensor add, int H, int W, int s) -> Tensor");
   m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");
@@ -1487,7 +1497,8 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("ts_gemm_tn_", &ts_gemm_tn_);
   m.impl("transpose2d", &transpose2d);
   m.impl("conv3x3_dgrad_weight", &conv3x3_dgrad_weight);
-  m.impl("convg_nt", &convg_nt);
+  m.impl("convg_nt", &convg_nt_fresh);
+  m.impl("convg_nt_out_", &convg_nt_out_);
   m.impl("convg_tn_", &convg_tn_);
   m.impl("ts_gemm_nt_add_sub", &ts_gemm_nt_add_sub);
   m.impl("maxpool_s2_fwd", &maxpool_s2_fwd);

@@ -199,16 +199,21 @@ def _ts_gemm_tn(C, A, B, accumulate, H=0, W=0, pro_ss=None):
 
 
 @register_fake("dph::convg_nt")
-def _convg_nt(A, B, geo, out=None, stats=False, chunk_taps=False):
+def _convg_nt(A, B, geo, stats=False, chunk_taps=False):
     Hs, Ws, Ho, Wo, Hd, Wd = geo[0], geo[1], geo[2], geo[3], geo[8], geo[9]
     imgs = A.shape[0] // (Hs * Ws)
     N = B.shape[0]
-    res = [out if out is not None else A.new_empty((imgs * Hd * Wd, N))]
+    res = [A.new_empty((imgs * Hd * Wd, N))]
     if stats:
         M = imgs * Ho * Wo
         nmb = (M + 127) // 128
         res.append(A.new_empty((2 * nmb * N + nmb,), dtype=torch.float32))
     return res
+
+
+@register_fake("dph::convg_nt_out_")
+def _convg_nt_out(A, B, geo, out):
+    return None
 
 
 @register_fake("dph::convg_tn_")

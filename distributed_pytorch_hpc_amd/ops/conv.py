@@ -413,10 +413,10 @@ class _StridedConvFn(torch.autograd.Function):
         wk = wb.permute(0, 2, 3, 1).reshape(cout, k * k * C)          # [Cout, (kh, kw, Cin)]
         geo = strided_fwd_geo(H, W, k, s, p)
         if stats_slot is not None:
-            y2, stats_slot.stats = _lib.ops().convg_nt(x2, wk, geo, None, True)
+            y2, stats_slot.stats = _lib.ops().convg_nt(x2, wk, geo, True)
             stats_slot.rows, stats_slot.cols = y2.shape
         else:
-            y2 = _lib.ops().convg_nt(x2, wk, geo, None, False)[0]
+            y2 = _lib.ops().convg_nt(x2, wk, geo, False)[0]
         ctx.save_for_backward(x2, wb)
         ctx.cfg = (B, C, H, W, k, s, p, Ho, Wo)
         ctx.wdtype, ctx.param, ctx.grad_slot = wdtype, w, grad_slot
@@ -441,7 +441,7 @@ class _StridedConvFn(torch.autograd.Function):
             wp = wb.permute(1, 2, 3, 0)                                   # [Cin, kh, kw, Cout]
             for geo, kt in strided_dgrad_classes(H, W, k, s, p):
                 bk = torch.stack([wp[:, ky, kx, :] for ky, kx in kt], 1).reshape(C, len(kt) * cout)
-                _lib.ops().convg_nt(dy2, bk, geo, dx2, False)
+                _lib.ops().convg_nt_out_(dy2, bk, geo, dx2)
             dx = dx2.view(B, H, W, C).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] and _strided_wgrad() != "dph":
             # MIOpen's weight gradient (DPH_CONV_STRIDED_WGRAD=miopen; the gathered c3w_k / sub-image 1x1 kernels are
@@ -646,10 +646,10 @@ class _StemConvFn(torch.autograd.Function):
         cout = w.shape[0]
         wk = stem_weight(w.to(torch.bfloat16), kxp, K)
         if stats_slot is not None:
-            y2, stats_slot.stats = _lib.ops().convg_nt(a, wk, geo, None, True, True)
+            y2, stats_slot.stats = _lib.ops().convg_nt(a, wk, geo, True, True)
             stats_slot.rows, stats_slot.cols = y2.shape
         else:
-            y2 = _lib.ops().convg_nt(a, wk, geo, None, False, True)[0]
+            y2 = _lib.ops().convg_nt(a, wk, geo, False, True)[0]
         ctx.save_for_backward(a)
         ctx.cfg = (B, C, H, W, k, p, Ho, Wo, kxp, K, geo, w.shape, w.dtype)
         return y2.view(B, Ho, Wo, cout).permute(0, 3, 1, 2)

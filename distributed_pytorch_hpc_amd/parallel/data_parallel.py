@@ -35,6 +35,7 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
+from ..comm.custom_allreduce import check_health as check_xgmi_health
 from ..comm.custom_allreduce import use_custom as use_custom_allreduce
 from ..ops import _lib
 from ..train import optim as optim_ref
@@ -280,6 +281,18 @@ class DataParallelEngine:
             cat = torch.cat(idx) if idx else torch.zeros(0, dtype=torch.int64)
             self._tp_partial.append((g, cat.to(self.device)))
 
+    def finish_grad_sync(self):
+        """The one place gradient synchronisation completes: wait for every bucket's data-parallel reduction, then
+        (once per reduction round) finish the sequence-parallel gradients over the TP group.  ``synchronize`` and
+        ``step`` both call it, so ``main_grad`` read after ``synchronize()`` -- grad-norm logging, gradient checks,
+        external optimizers -- is already complete over TP."""
+        for b in self.buckets:
+            self._wait_reduce(b)
+        if self._tp_partial and not getattr(self, "_tp_done", False):
+            self._reduce_tp_partial()
+            self._tp_done = True
+        check_xgmi_health()
+
     def _reduce_tp_partial(self):
         from ..comm.functional import all_reduce_
 
@@ -352,6 +365,7 @@ class DataParallelEngine:
 
     def _launch(self, b: _Bucket):
         b.launched = True
+        self._tp_done = False   # new data-parallel sums: the TP completion of SP gradients is due again
         if self.world == 1:
             return
         g = self.grad_view(b)
@@ -455,9 +469,9 @@ class DataParallelEngine:
             raise RuntimeError("optimizer step inside no_sync()")
         self.step_count += 1
         if self._tp_partial:
-            for b in self.buckets:
-                self._wait_reduce(b)
-            self._reduce_tp_partial()
+            self.finish_grad_sync()
+        else:
+            check_xgmi_health()   # a stalled direct-peer all-reduce must stop training, not feed the update
         if cfg.max_grad_norm is not None:
             norm = self._global_sumsq().sqrt()
             self._gscale.copy_(torch.clamp(cfg.max_grad_norm / (norm + 1e-6), max=1.0) / self.world)
@@ -545,8 +559,7 @@ class DataParallelEngine:
 
     def synchronize(self):
         """Wait for every outstanding collective (end of step / before checkpointing or evaluation)."""
-        for b in self.buckets:
-            self._wait_reduce(b)
+        self.finish_grad_sync()
         self._wait_ag(range(len(self.buckets)))
         self._join_opt_stream()
 

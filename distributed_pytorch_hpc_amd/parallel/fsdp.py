@@ -32,6 +32,7 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
+from ..comm.custom_allreduce import check_health as check_xgmi_health
 from ..ops import _lib
 from ..train import optim as optim_ref
 from ..utils.flat import ALIGN, align_up, flat_order, flat_order_like, param_view
@@ -368,6 +369,7 @@ class ZeRO3Engine:
         if lr is not None:
             cfg.lr = lr
         self.step_count += 1
+        check_xgmi_health()   # TP / SP all-reduces of this step may have used the direct-peer path
         if cfg.max_grad_norm is not None:
             sq = optim_ref.global_grad_norm([self.grad_shard]) ** 2
             if self.world > 1:

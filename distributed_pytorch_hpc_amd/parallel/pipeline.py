@@ -320,6 +320,7 @@ class PipelineSchedule:
         outputs of all micro-batches, other stages None.  Interleaved: chunk by chunk, every micro-batch of chunk
         c before chunk c + 1 (the ring order is the same on every rank, so blocking transfers cannot cycle)."""
         mbs = self._split(inputs, "inputs") if self.is_first else [None] * self.m
+        self._reset_meta()
         outs, sends = [], []
         for c in range(self.v):
             for i in range(self.m):
@@ -342,6 +343,12 @@ class PipelineSchedule:
         return torch.cat(outs, 0) if self.is_last else None
 
     # ---- transport of the plan executor (ring neighbours, grouped, waits deferred to the consumer) ----
+    def _reset_meta(self) -> None:
+        # every call (step / forward) re-announces the boundary shape on its first linear-edge send: a later call
+        # may run another sequence length or batch size, and receivers must not post buffers of the old shape
+        self._act_meta = None
+        self._meta_sent = False
+
     def _needs_header(self) -> bool:
         # only the linear edges stage -> stage + 1 carry the one-time shape header: rank 0 knows the boundary shape
         # from its own first forward before anything arrives over the ring's wrap edge (last rank -> rank 0)
@@ -364,7 +371,7 @@ class PipelineSchedule:
         return x
 
     def _send_header(self, y, peer):
-        # the first boundary tensor of this schedule object: its shape / dtype, once (all boundaries share them)
+        # the first boundary tensor of this call: its shape / dtype, once (all boundaries of one call share them)
         dist.send(self.p2p._header(y), peer, group=self.group)
         self._meta_sent = True
         if self._act_meta is None:
@@ -429,6 +436,7 @@ class PipelineSchedule:
         """1F1B / interleaved 1F1B from ``schedule_plan``: forwards, backwards and grouped neighbour exchanges in
         the plan's order; a received tensor is waited for only when its forward / backward starts."""
         P, v, M, r = self.n_stages, self.v, self.m, self.stage
+        self._reset_meta()
         fin = [collections.deque() for _ in range(v)]
         gin = [collections.deque() for _ in range(v)]
         saved = [collections.deque() for _ in range(v)]

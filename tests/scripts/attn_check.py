@@ -22,6 +22,11 @@ CASES = [  # B, Sq, Sk, Hq, Hkv, D, causal -- d >= 64 (the 8-wave variants), rag
     (2, 200, 200, 8, 2, 64, True),
     (1, 64, 192, 2, 2, 64, True),
     (1, 520, 520, 2, 1, 128, True),
+    (2, 1000, 1000, 4, 2, 128, True),
+    (1, 192, 64, 2, 2, 128, True),
+    (1, 300, 77, 2, 2, 64, False),
+    (1, 77, 300, 2, 1, 128, True),
+    (1, 2048, 2048, 2, 2, 128, True),   # with spiked keys: forces the lazy-rescale branch mid-sequence
 ]
 
 
@@ -38,6 +43,12 @@ def main():
         q = torch.randn(B, Sq, Hq, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
         k = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
         v = torch.randn(B, Sk, Hkv, D, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+        if Sq == 2048:
+            with torch.no_grad():
+                dirn = q.float().mean(1)
+                dirn = dirn / dirn.norm(dim=-1, keepdim=True)
+                k[:, 700] = (dirn * 30).to(torch.bfloat16)
+                k[:, 1500] = (dirn * 60).to(torch.bfloat16)
         o = ops.flash_attention(q, k, v, causal=causal)
         qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
         orf = attn_mod.attention_reference(qr, kr, vr, causal, 1.0 / math.sqrt(D))

@@ -82,3 +82,27 @@ def test_verify_min_gpu_count_without_gpus():
 def test_shell_scripts_parse(script):
     p = subprocess.run(["bash", "-n", script], capture_output=True, text=True, timeout=30)
     assert p.returncode == 0, p.stderr
+
+
+def test_gpu_telemetry_summary_without_device(monkeypatch):
+    """bench.py's clock / power sampler: spreads over the samples inside the timed marks, energy from the accumulator
+    delta, throttle residency as a fraction of the SMU accumulation counter.  Fed synthetic readings (no GPU here)."""
+    from distributed_pytorch_hpc_amd.utils import telemetry as tm
+
+    t = tm.GpuTelemetry.__new__(tm.GpuTelemetry)
+    t.samples, t.marks, t.error, t._smi = [], {}, None, object()
+    t.marks["a"] = {"t": 0.0, "energy_j": 100.0, "accumulation_counter": 1000, "ppt_residency_acc": 500}
+    t.marks["b"] = {"t": 2.0, "energy_j": 2900.0, "accumulation_counter": 3000, "ppt_residency_acc": 2300}
+    for i, (clk, pw) in enumerate([(1700, 1390), (1750, 1395), (1800, 1380), (2400, 200)]):
+        t.samples.append({"t": 0.5 * i if i < 3 else 5.0, "sclk": clk, "sclk_min_xcd": clk - 50, "power": pw,
+                          "temp_hot": 60, "temp_mem": 50})
+    out = t.summary("a", "b", flops=2.8e15)
+    assert out["sclk_mhz"]["median"] == 1750 and out["sclk_mhz"]["n"] == 3   # the idle sample after "b" is excluded
+    assert out["power_w"]["max"] == 1395
+    assert out["energy_j"] == 2800.0 and out["avg_power_w"] == 1400.0
+    assert abs(out["tflop_per_joule"] - 1.0) < 1e-9
+    assert out["ppt_limited_frac"] == 0.9
+    # no amdsmi / no GPU: the bench line says so instead of failing
+    u = tm.GpuTelemetry.__new__(tm.GpuTelemetry)
+    u._smi, u.error = None, "ImportError: x"
+    assert "unavailable" in u.summary("a", "b")["telemetry"]

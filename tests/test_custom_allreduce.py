@@ -71,3 +71,44 @@ def test_policy_routing_is_size_and_env_driven(monkeypatch):
         assert C.use_custom(torch.ones(16), None) is None      # CPU tensors never take the IPC path
     finally:
         C.clear_policy(None)
+
+
+def test_check_health_raises_and_disables_path(monkeypatch):
+    """Advisor r4: a timed-out direct-peer barrier must stop training at the next step boundary (not leave wrong
+    sums in the gradients) and turn the path off for that group."""
+    from distributed_pytorch_hpc_amd.comm import custom_allreduce as car
+
+    class _Fake:
+        def __init__(self, err):
+            self.err = err
+
+        def errors(self):
+            return self.err
+
+    monkeypatch.setattr(car, "_CACHE", {"world": _Fake(0), 123: _Fake(1)})
+    monkeypatch.setattr(car, "_POLICY", {"world": 1 << 20, 123: 1 << 20})
+    with pytest.raises(car.XgmiAllReduceError):
+        car.check_health()
+    assert 123 not in car._POLICY and car._POLICY["world"] == 1 << 20
+    car._CACHE[123].err = 0
+    car.check_health()   # healthy groups: no error
+
+
+def test_engine_step_checks_xgmi_health(monkeypatch):
+    from distributed_pytorch_hpc_amd.comm import custom_allreduce as car
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig
+
+    m = torch.nn.Linear(8, 8)
+    eng = DataParallelEngine(m, shard=False)
+    eng.configure_optimizer(OptimConfig(lr=1e-3))
+    m(torch.randn(4, 8)).sum().backward()
+    eng.synchronize()
+
+    class _Bad:
+        def errors(self):
+            return 1
+
+    monkeypatch.setattr(car, "_CACHE", {"world": _Bad()})
+    monkeypatch.setattr(car, "_POLICY", {})
+    with pytest.raises(car.XgmiAllReduceError):
+        eng.step()

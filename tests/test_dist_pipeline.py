@@ -324,3 +324,49 @@ def test_interleaved_matches_single_process(pp, v, m_micro):
     assert seen == set(ref_g)
     for step_losses in outs[pp - 1][0]:
         assert len(step_losses) == m_micro and abs(sum(step_losses) / m_micro - ref_loss) < 1e-5
+
+
+def _varying_shape_worker(rank, world, pp, v, schedule, m_micro):
+    from distributed_pytorch_hpc_amd.parallel.pipeline import (PipelineSchedule, lm_loss, split_llama,
+                                                                split_llama_virtual)
+
+    model = _model8()
+    names = {id(p): n for n, p in model.named_parameters()}
+    chunks = split_llama_virtual(model, pp, v, rank) if v > 1 else split_llama(model, pp, rank)
+    sched = PipelineSchedule(chunks, rank, pp, m_micro, loss_fn=lm_loss, schedule=schedule)
+    out = []
+    for s in (16, 8, 24):   # sequence length changes every step: each call must re-announce the boundary shape
+        x, y = _data(b=12, s=s)
+        for p in chunks.parameters():
+            p.grad = None
+        losses = sched.step(inputs=x if rank == 0 else None, target=y if rank == pp - 1 else None)
+        out.append(([float(l) for l in losses], {names[id(p)]: p.grad.clone() for p in chunks.parameters()}))
+    # forward-only pass at yet another length
+    x, _ = _data(b=12, s=12)
+    logits = sched.forward(x if rank == 0 else None)
+    return out, None if logits is None else tuple(logits.shape)
+
+
+@pytest.mark.parametrize("pp,v,schedule", [(2, 1, "1f1b"), (3, 2, "interleaved")])
+def test_pipeline_shape_changes_between_steps(pp, v, schedule):
+    """Advisor r4: the boundary shape header was sent once per schedule object, so a later step with another
+    sequence length posted receive buffers of the old shape.  Every step must match its own single-process run."""
+    from distributed_pytorch_hpc_amd.parallel.pipeline import lm_loss
+
+    m_micro = 3
+    outs = run_distributed(_varying_shape_worker, pp, pp, v, schedule, m_micro)
+    for step, s in enumerate((16, 8, 24)):
+        m = _model8()
+        x, y = _data(b=12, s=s)
+        total = 0.0
+        for xm, ym in zip(x.chunk(m_micro), y.chunk(m_micro)):
+            loss = lm_loss(m(xm), ym) / m_micro
+            loss.backward()
+            total += loss.item()
+        ref_g = {n: p.grad for n, p in m.named_parameters()}
+        last_losses = outs[pp - 1][0][step][0]
+        assert abs(sum(last_losses) / m_micro - total) < 1e-5, (step, s)
+        for r in range(pp):
+            for n, g in outs[r][0][step][1].items():
+                assert torch.allclose(g, ref_g[n], atol=1e-5, rtol=1e-4), (step, r, n)
+    assert outs[pp - 1][1] is not None and outs[pp - 1][1][1] == 12

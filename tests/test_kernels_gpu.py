@@ -196,6 +196,11 @@ CASES = [
     (1, 130, 130, 2, 2, 32, True),
     (1, 64, 192, 2, 2, 64, True),
     (1, 520, 520, 2, 1, 128, True),
+    # software-pipelined forward (256-row workgroups): ragged tails, Sq > Sk (rows with no visible key), Sk % 32 != 0
+    (2, 1000, 1000, 4, 2, 128, True),
+    (1, 192, 64, 2, 2, 128, True),
+    (1, 300, 77, 2, 2, 64, False),
+    (1, 77, 300, 2, 1, 128, True),
 ]
 
 
@@ -215,6 +220,35 @@ def test_flash_attention(dph_native, B, Sq, Sk, Hq, Hkv, D, causal):
     assert rel_err(q.grad, qr.grad) < 3e-2
     assert rel_err(k.grad, kr.grad) < 3e-2
     assert rel_err(v.grad, vr.grad) < 3e-2
+
+
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_forced_rescale(dph_native, causal):
+    """The lazy-rescale branch (running max raised only when a tile's max exceeds it by RESCALE_THR) is rare on
+    random data, so force it (cdna_hip_programming.md rule 26): key rows 700 and 1500 are aligned with every query and
+    scaled so their scores jump by ~40 in log2 units mid-sequence, and one query row gets large logits everywhere."""
+    torch.manual_seed(21)
+    B, S, H, D = 1, 2048, 2, 128
+    q = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    dirn = q.float().mean(1, keepdim=True)
+    dirn = dirn / dirn.norm(dim=-1, keepdim=True)
+    k[:, 700] = (dirn[:, 0] * 30).to(torch.bfloat16)
+    k[:, 1500] = (dirn[:, 0] * 60).to(torch.bfloat16)
+    q[:, 1800] = q[:, 1800] * 8
+    o, lse = ops.flash_fwd(q, k, v, 1.0 / math.sqrt(D), causal)
+    qr, kr, vr = (t.float() for t in (q, k, v))
+    orf = attn_mod.attention_reference(qr, kr, vr, causal, 1.0 / math.sqrt(D))
+    assert torch.isfinite(o).all()
+    assert rel_err(o, orf) < 2e-2
+    # per-row check: the rows right after a spike are where a wrong rescale shows
+    err = (o.float() - orf).abs().amax(dim=(0, 2, 3))
+    assert err.max().item() < 0.15, int(err.argmax())
+    s = torch.einsum("bqhd,bkhd->bhqk", qr, kr) / math.sqrt(D)
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, device=DEV, dtype=torch.bool).triu(1), float("-inf"))
+    assert (lse - torch.logsumexp(s, -1)).abs().max().item() < 5e-2
 
 
 def test_flash_attention_long_sequence(dph_native):
@@ -245,6 +279,21 @@ def test_flash_attention_eight_wave_variant(dph_native, waves):
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "attn_check.py")
     p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_ATTN_WAVES=waves), capture_output=True,
                        text=True, timeout=100)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    assert '"ok": true' in p.stdout
+
+
+@pytest.mark.parametrize("var", ["0", "1", "2", "3"])
+def test_flash_attention_pipelined_forward(dph_native, var):
+    """The software-pipelined forward (DPH_ATTN_FWD=pipe, schedule variant DPH_ATTN_FWD_VAR), read once per process,
+    in a child process: ragged / Sq > Sk / Sk % 32 != 0 shapes and a spiked-key case that forces the rescale branch."""
+    import os
+    import subprocess
+    import sys
+
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "attn_check.py")
+    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_ATTN_FWD="pipe", DPH_ATTN_FWD_VAR=var),
+                       capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
     assert '"ok": true' in p.stdout
 
