@@ -36,6 +36,9 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--gemm-nt", default=None, choices=["fused", "all", "0"])
     ap.add_argument("--fused-qkv", type=int, default=None)
+    ap.add_argument("--torch-profile", action="store_true",
+                    help="after the timed steps, profile one step with torch.profiler and print where device memcpys "
+                         "and copy kernels come from (Python call sites)")
     a = ap.parse_args(argv)
 
     from torch.testing._internal.distributed.fake_pg import FakeStore
@@ -103,9 +106,46 @@ def main(argv=None):
     ms = (time.perf_counter() - t0) * 1000 / a.steps
     info.update(ms_per_step=round(ms, 2), tokens_per_s_tp_group_no_comm=round(a.batch * a.seq / (ms / 1000), 1),
                 peak_gb=round(torch.cuda.max_memory_allocated() / 1e9, 1))
+    if a.torch_profile:
+        _copy_sites(step)
     print(json.dumps(info), flush=True)
     dist.destroy_process_group()
     return info
+
+
+def _copy_sites(step):
+    """Which Python call sites issue copy kernels / device memcpys in one step (TorchDispatchMode: every copy-like
+    ATen op with its innermost framework frame, counted with its bytes)."""
+    import collections
+    import traceback
+
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    cnt, nbytes = collections.Counter(), collections.Counter()
+    names = ("copy_", "clone", "contiguous", "_to_copy", "cat.", "index_copy", "fill_", "zero_", "empty_like")
+
+    class _M(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            out = func(*args, **(kwargs or {}))
+            n = str(func)
+            if any(x in n for x in names):
+                st = [f for f in traceback.extract_stack() if "distributed_pytorch_hpc_amd" in f.filename
+                      or "benchmarks" in f.filename]
+                where = f"{st[-1].filename.rsplit('/', 2)[-2]}/{st[-1].filename.rsplit('/', 1)[-1]}:{st[-1].lineno}" \
+                    if st else "?"
+                cnt[(n, where)] += 1
+                o = out if isinstance(out, torch.Tensor) else (args[0] if args and isinstance(args[0], torch.Tensor)
+                                                               else None)
+                if o is not None:
+                    nbytes[(n, where)] += o.numel() * o.element_size()
+            return out
+
+    with _M():
+        step()
+    torch.cuda.synchronize()
+    print("[tp_rank] copy-like ops in one step (calls, MB, op, call site):", flush=True)
+    for key in sorted(cnt, key=lambda k: -nbytes[k])[:30]:
+        print(f"  {cnt[key]:6d} {nbytes[key] / 1e6:10.1f}  {key[0]}  {key[1]}", flush=True)
 
 
 if __name__ == "__main__":

@@ -13,6 +13,15 @@ Here each redistribution is one explicit RCCL call with its exact adjoint in bac
 
 All collectives run on contiguous buffers (a transpose+contiguous at most) so RCCL moves one large
 message per call; on gloo (CPU tests) the same code runs unchanged.
+
+Sequence parallelism shards TOKENS, not the sequence dimension (``dim=TOKENS``).  An activation [B, S, D] is the
+contiguous token matrix [B S, D]; rank r holds its share of the flat tokens and presents it as [B, S / tp, D].  Only
+token-wise work (norms, residual adds) runs on the shard, so which tokens a rank holds is free, and choosing whole
+runs of the flat order makes every gather / reduce-scatter a dim-0 collective on contiguous memory: no transpose
+before it and no non-contiguous view after it (dim-1 sharding of [B, S, D] cost one full-size copy per collective
+and another in the consumer -- 92 ms of a TP = 8 Llama-2-7B rank's 238 ms step, profiles/r5/tp_rank/).  With
+``set_sp_chunks(group, k)`` (async TP) the flat tokens are dealt in k rounds of tp runs, so the k micro-collectives of
+parallel/async_tp.py each fill one contiguous slice of the gathered tensor.
 """
 from __future__ import annotations
 
@@ -31,7 +40,91 @@ def _rank(group) -> int:
 
 
 # ------------------------------------------------------------------------------------------- raw helpers
-def all_gather_dim(x: torch.Tensor, dim: int, group) -> torch.Tensor:
+TOKENS = "tokens"      # the ``dim`` of a token-sharded (sequence-parallel) activation, see the module docstring
+_SP_CHUNKS: dict = {}  # group key -> k (rounds of the token deal; 1 = one contiguous run per rank)
+
+
+def _gkey(group):
+    return id(group) if group is not None else "world"
+
+
+def set_sp_chunks(group, k: int) -> None:
+    """Token layout of ``group``'s sequence-parallel activations: k rounds (async TP's micro-collective count)."""
+    _SP_CHUNKS[_gkey(group)] = max(1, int(k))
+
+
+def sp_chunks(group, n_local: int = 0) -> int:
+    """Rounds of the token deal for a shard of ``n_local`` tokens: the configured k, or its largest divisor of
+    n_local (a function of (k, n_local) only, so every collective of a step -- all see the same token count -- and
+    every rank agree on the layout)."""
+    k = _SP_CHUNKS.get(_gkey(group), 1)
+    if n_local > 0:
+        k = max(1, min(k, n_local))
+        while n_local % k:
+            k -= 1
+    return k
+
+
+def _tok_shape(x: torch.Tensor, factor_num: int, factor_den: int = 1):
+    assert x.dim() >= 2, "token-sharded tensors are [..., tokens, D] with at least two dims"
+    shp = list(x.shape)
+    shp[1] = shp[1] * factor_num // factor_den
+    return shp
+
+
+def tok_all_gather(x: torch.Tensor, group) -> torch.Tensor:
+    """[B, Sl, D] token shard -> [B, Sl * tp, D] (natural token order), k dim-0 all-gathers into contiguous slots."""
+    ws = _ws(group)
+    if ws == 1:
+        return x
+    x = x.contiguous()
+    d = x.shape[-1]
+    n = x.numel() // d
+    k = sp_chunks(group, n)
+    m = n // k
+    out = torch.empty((ws * n, d), dtype=x.dtype, device=x.device)
+    xv, ov = x.view(k, m, d), out.view(k, ws * m, d)
+    for c in range(k):
+        dist.all_gather_into_tensor(ov[c], xv[c], group=group)
+    return out.view(_tok_shape(x, ws))
+
+
+def tok_reduce_scatter(x: torch.Tensor, group) -> torch.Tensor:
+    """[B, S, D] partial sums -> this rank's [B, S / tp, D] token shard, k dim-0 reduce-scatters of contiguous slots."""
+    ws = _ws(group)
+    if ws == 1:
+        return x
+    x = x.contiguous()
+    d = x.shape[-1]
+    t = x.numel() // d
+    assert x.shape[1] % ws == 0, f"reduce_scatter: {x.shape[1]} positions do not split over {ws} ranks"
+    k = sp_chunks(group, t // ws)
+    m = t // (ws * k)
+    out = torch.empty((k * m, d), dtype=x.dtype, device=x.device)
+    xv, ov = x.view(k, ws * m, d), out.view(k, m, d)
+    for c in range(k):
+        dist.reduce_scatter_tensor(ov[c], xv[c], op=dist.ReduceOp.SUM, group=group)
+    return out.view(_tok_shape(x, 1, ws))
+
+
+def tok_split(x: torch.Tensor, group) -> torch.Tensor:
+    """This rank's token shard of a replicated [B, S, D] (no communication)."""
+    ws = _ws(group)
+    if ws == 1:
+        return x
+    r = _rank(group)
+    x = x.contiguous()
+    d = x.shape[-1]
+    t = x.numel() // d
+    assert x.shape[1] % ws == 0, f"split: {x.shape[1]} positions do not split over {ws} ranks"
+    k = sp_chunks(group, t // ws)
+    m = t // (ws * k)
+    return x.view(k, ws, m, d)[:, r].contiguous().view(_tok_shape(x, 1, ws))
+
+
+def all_gather_dim(x: torch.Tensor, dim, group) -> torch.Tensor:
+    if dim == TOKENS:
+        return tok_all_gather(x, group)
     ws = _ws(group)
     if ws == 1:
         return x
@@ -46,7 +139,9 @@ def all_gather_dim(x: torch.Tensor, dim: int, group) -> torch.Tensor:
     return out.movedim(0, dim)
 
 
-def reduce_scatter_dim(x: torch.Tensor, dim: int, group) -> torch.Tensor:
+def reduce_scatter_dim(x: torch.Tensor, dim, group) -> torch.Tensor:
+    if dim == TOKENS:
+        return tok_reduce_scatter(x, group)
     ws = _ws(group)
     if ws == 1:
         return x
@@ -57,7 +152,9 @@ def reduce_scatter_dim(x: torch.Tensor, dim: int, group) -> torch.Tensor:
     return out.movedim(0, dim)
 
 
-def split_dim(x: torch.Tensor, dim: int, group) -> torch.Tensor:
+def split_dim(x: torch.Tensor, dim, group) -> torch.Tensor:
+    if dim == TOKENS:
+        return tok_split(x, group)
     ws = _ws(group)
     if ws == 1:
         return x

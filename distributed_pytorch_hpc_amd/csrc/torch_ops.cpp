@@ -1321,6 +1321,58 @@ std::tuple<Tensor, Tensor> gemm_nt_swiglu(const Tensor& x, const Tensor& w13) {
   return {x13, h};
 }
 
+// gemm_nt_swiglu into caller-owned row blocks (x13_out [rows, 2H], h_out [rows, H], row-major, 16-B aligned rows):
+// async tensor parallelism writes each round of the token deal straight into its slice of the full activations
+void gemm_nt_swiglu_into(const Tensor& x, const Tensor& w13, Tensor x13_out, Tensor h_out) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  const Tensor a = rows2d(x, "gemm_nt_swiglu_into x"), b = rows2d(w13, "gemm_nt_swiglu_into w13");
+  TORCH_CHECK(w13.dim() == 2 && b.size(1) == a.size(1) && b.size(0) % 2 == 0, "gemm_nt_swiglu_into: w13 [2H, K]");
+  const int64_t H = b.size(0) / 2;
+  TORCH_CHECK(dph::gemm_nt_supported(dph::kNtSwiglu, a.size(0), H, a.size(1)),
+              "gemm_nt_swiglu_into: need rows % 256, H % 8, K % 8");
+  TORCH_CHECK(x13_out.scalar_type() == at::kBFloat16 && h_out.scalar_type() == at::kBFloat16 && x13_out.dim() == 2 &&
+                  h_out.dim() == 2 && x13_out.size(0) == a.size(0) && x13_out.size(1) == 2 * H &&
+                  h_out.size(0) == a.size(0) && h_out.size(1) == H && x13_out.stride(1) == 1 && h_out.stride(1) == 1 &&
+                  x13_out.stride(0) % 8 == 0 && h_out.stride(0) % 8 == 0,
+              "gemm_nt_swiglu_into: outputs must be bf16 [rows, 2H] / [rows, H] with unit column stride");
+  check_align16(x13_out, "x13_out");
+  check_align16(h_out, "h_out");
+  auto p = nt_params(a, b);
+  p.N = (int)H;
+  p.H = (int)H;
+  p.C = x13_out.data_ptr();
+  p.ldc = x13_out.stride(0);
+  p.C2 = h_out.data_ptr();
+  p.ldc2 = h_out.stride(0);
+  dph::gemm_nt(dph::kNtSwiglu, p, cur_stream());
+}
+
+// gemm_nt_dswiglu into a caller-owned row block d13_out [rows, 2H]
+void gemm_nt_dswiglu_into(const Tensor& dy, const Tensor& w2t, const Tensor& x13, Tensor d13_out) {
+  check_cuda(dy, "dy");
+  c10::DeviceGuard g(dy.device());
+  const Tensor a = rows2d(dy, "gemm_nt_dswiglu_into dy"), b = rows2d(w2t, "gemm_nt_dswiglu_into w2t");
+  const Tensor xr = rows2d(x13, "gemm_nt_dswiglu_into x13");
+  const int64_t H = b.size(0);
+  TORCH_CHECK(w2t.dim() == 2 && b.size(1) == a.size(1) && xr.size(0) == a.size(0) && xr.size(1) == 2 * H,
+              "gemm_nt_dswiglu_into: w2t [H, K], x13 [rows, 2H]");
+  TORCH_CHECK(dph::gemm_nt_supported(dph::kNtDswiglu, a.size(0), H, a.size(1)),
+              "gemm_nt_dswiglu_into: need rows % 256, H % 8, K % 8");
+  TORCH_CHECK(d13_out.scalar_type() == at::kBFloat16 && d13_out.dim() == 2 && d13_out.size(0) == a.size(0) &&
+                  d13_out.size(1) == 2 * H && d13_out.stride(1) == 1 && d13_out.stride(0) % 8 == 0,
+              "gemm_nt_dswiglu_into: d13_out must be bf16 [rows, 2H] with unit column stride");
+  check_align16(d13_out, "d13_out");
+  auto p = nt_params(a, b);
+  p.N = (int)H;
+  p.H = (int)H;
+  p.C = d13_out.data_ptr();
+  p.ldc = d13_out.stride(0);
+  p.X = xr.data_ptr();
+  p.ldx = xr.stride(0);
+  dph::gemm_nt(dph::kNtDswiglu, p, cur_stream());
+}
+
 // d13 = SwiGLU-backward(dh = dy W2, x13): dy [..., K], w2t = W2^T [H, K], x13 [..., 2H] -> [..., 2H]
 Tensor gemm_nt_dswiglu(const Tensor& dy, const Tensor& w2t, const Tensor& x13) {
   check_cuda(dy, "dy");
@@ -1417,6 +1469,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("gemm_nt(Tensor A, Tensor B) -> Tensor");
   m.def("gemm_nt_variant_(int v) -> int", &gemm_nt_variant_);   // no tensor argument: catch-all kernel
   m.def("gemm_nt_swiglu(Tensor x, Tensor w13) -> (Tensor, Tensor)");
+  m.def("gemm_nt_swiglu_into(Tensor x, Tensor w13, Tensor(a!) x13_out, Tensor(b!) h_out) -> ()");
+  m.def("gemm_nt_dswiglu_into(Tensor dy, Tensor w2t, Tensor x13, Tensor(a!) d13_out) -> ()");
   m.def("gemm_nt_dswiglu(Tensor dy, Tensor w2t, Tensor x13) -> Tensor");
   m.def("gemm_nt_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int S, int hd, int n_rot, int pos_off) -> Tensor");
   m.def("gemm_tn_tail_(int cus) -> ()", &gemm_tn_tail_);                          // catch-all kernels
@@ -1490,6 +1544,8 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("gemm_tn_", &gemm_tn_);
   m.impl("gemm_nt", &gemm_nt);
   m.impl("gemm_nt_swiglu", &gemm_nt_swiglu);
+  m.impl("gemm_nt_swiglu_into", &gemm_nt_swiglu_into);
+  m.impl("gemm_nt_dswiglu_into", &gemm_nt_dswiglu_into);
   m.impl("gemm_nt_dswiglu", &gemm_nt_dswiglu);
   m.impl("gemm_nt_rope", &gemm_nt_rope);
   m.impl("ts_gemm_nt", &ts_gemm_nt);

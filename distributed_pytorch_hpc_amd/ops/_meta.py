@@ -211,6 +211,16 @@ def _convg_nt(A, B, geo, stats=False, chunk_taps=False):
     return res
 
 
+@register_fake("dph::gemm_nt_swiglu_into")
+def _gemm_nt_swiglu_into(x, w13, x13_out, h_out):
+    return None
+
+
+@register_fake("dph::gemm_nt_dswiglu_into")
+def _gemm_nt_dswiglu_into(dy, w2t, x13, d13_out):
+    return None
+
+
 @register_fake("dph::convg_nt_out_")
 def _convg_nt_out(A, B, geo, out):
     return None

@@ -12,9 +12,16 @@ collective i+1 (forward and backward, both directions):
 
 Every micro-collective is a full RCCL all-gather / reduce-scatter over the TP group -- on the fully connected xGMI
 mesh RCCL drives several links per collective, which a hand-rolled send/recv ring (one link per step) would not --
-and the micro-chunks stay large (T D / (tp k) elements) so each keeps its plateau bandwidth.  The gathered
-activations needed for dW are kept chunk-major ([k, tp, B, m, D]) so dW is ONE GEMM over all tokens, routed into the
-data-parallel engine's flat gradient buffer when present (parallel/linear.py weight_grad).
+and the micro-chunks stay large (T D / (tp k) elements) so each keeps its plateau bandwidth.
+
+Layout: the sequence-parallel activations are token-sharded with the tokens dealt in k rounds
+(comm/functional.py TOKENS, ``set_sp_chunks(group, k)``): round c of every rank's shard is one contiguous run of m
+tokens, and the k x tp runs in (round, rank) order are the natural token order.  So micro-collective c gathers into
+(or reduce-scatters out of) ONE contiguous slice [c tp m, (c+1) tp m) of the full [T, D] activation, every
+micro-GEMM reads and writes contiguous rows, and the gathered activations needed for dW are the full tensor in
+natural order -- dW is ONE GEMM, routed into the data-parallel engine's flat gradient buffer when present
+(parallel/linear.py weight_grad).  No permute / copy anywhere (the round-4 form reordered every micro-GEMM's rows and
+made chunk-major copies of x and dy).
 
 Equivalent math to parallel/tensor_parallel.py's SP layers (gloo parity tests: tests/test_dist_llama.py::test_async_tp_*).  The
 reference has no async-TP (its SP plan is plain DTensor redistribution, fsdp_tp/fsdp_tp_example.py:146-177).
@@ -31,42 +38,10 @@ def _ws(group) -> int:
     return dist.get_world_size(group) if dist.is_initialized() else 1
 
 
-def _chunks_for(seq_local: int, chunks: int) -> int:
-    k = max(1, min(chunks, seq_local))
-    while seq_local % k:
-        k -= 1
-    return k
+def _rounds(group, n_local: int) -> int:
+    from ..comm.functional import sp_chunks
 
-
-def _ag_async(x: torch.Tensor, group, out: torch.Tensor | None = None):
-    """all-gather of a contiguous [B, m, D] micro-chunk -> ([P, B, m, D] buffer, work); ``out`` (contiguous
-    [P * B, m, D]) lets the caller gather straight into a slot of a larger buffer."""
-    P = _ws(group)
-    if out is None:
-        out = torch.empty((P * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)   # dim-0 concatenation
-    work = dist.all_gather_into_tensor(out, x, group=group, async_op=True)
-    return out.view(P, *x.shape), work
-
-
-def _rs_async(x: torch.Tensor, group, out: torch.Tensor | None = None):
-    """reduce-scatter of a contiguous [P, B, m, D] partial -> ([B, m, D] buffer, work); ``out`` may be a contiguous
-    slot of the caller's output (no concatenation afterwards)."""
-    if out is None:
-        out = torch.empty(x.shape[1:], dtype=x.dtype, device=x.device)
-    inp = x.reshape(x.shape[0] * x.shape[1], *x.shape[2:])                              # dim-0 concatenation
-    return out, dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group, async_op=True)
-
-
-def _chunk_major(t: torch.Tensor, P: int, k: int) -> torch.Tensor:
-    """[B, S, X] (S = P * k * m, rank-major sequence) -> contiguous [k, P, B, m, X]."""
-    B, S, X = t.shape
-    return t.reshape(B, P, k, S // (P * k), X).permute(2, 1, 0, 3, 4).contiguous()
-
-
-def _seq_major(t: torch.Tensor) -> torch.Tensor:
-    """[k, P, B, m, X] -> [B, S, X] (inverse of _chunk_major)."""
-    k, P, B, m, X = t.shape
-    return t.permute(2, 1, 0, 3, 4).reshape(B, P * k * m, X)
+    return sp_chunks(group, n_local)
 
 
 def _k_major(w: torch.Tensor, transpose_w: bool) -> torch.Tensor:
@@ -84,107 +59,109 @@ def _k_major(w: torch.Tensor, transpose_w: bool) -> torch.Tensor:
     return w.t().contiguous()
 
 
-def _ag_matmul(x: torch.Tensor, w: torch.Tensor, group, k: int, transpose_w: bool):
-    """AG(x) @ op(w) with k pipelined micro all-gathers; x [B, Sl, D].  Returns (y [B, S, N], gathered [k,P,B,m,D]).
-
-    The micro all-gathers land in slots of ONE chunk-major buffer (kept for the weight gradient: no stack); each
-    micro-GEMM is one 2-D GEMM whose [P, B, m, N] result is copied once into its rank-major sequence rows (overlapping
-    the next micro all-gather).  A strided-batched GEMM writing those rows directly would need the weight broadcast at
-    batch stride 0, which hipBLASLt on this stack rejects (parallel/linear.py _mm2d)."""
-    B, Sl, D = x.shape
+def _ag_matmul(x2: torch.Tensor, w: torch.Tensor, group, k: int, transpose_w: bool):
+    """AG(x) @ op(w) with k pipelined micro all-gathers; x2 = this rank's [n, D] token shard.  Returns
+    (y [P n, N], gathered x [P n, D]), both in natural token order: round c's all-gather lands in rows
+    [c P m, (c+1) P m) of the gathered buffer and its GEMM writes the same rows of y."""
     P = _ws(group)
-    m = Sl // k
-    xg = torch.empty((k, P * B, m, D), dtype=x.dtype, device=x.device)
-    pend = [_ag_async(x[:, i * m:(i + 1) * m].contiguous(), group, xg[i]) for i in range(k)]
+    n, D = x2.shape
+    m = n // k
+    xg = torch.empty((P * n, D), dtype=x2.dtype, device=x2.device)
+    xs, gs = x2.view(k, m, D), xg.view(k, P * m, D)
+    pend = [dist.all_gather_into_tensor(gs[c], xs[c], group=group, async_op=True) for c in range(k)]
     wk = _k_major(w, transpose_w)                                          # [N, D]
-    N = wk.shape[0]
-    y = torch.empty((B, P * Sl, N), dtype=x.dtype, device=x.device)
-    yv = y.view(B, P, k, m, N)
-    for i, (g, work) in enumerate(pend):
+    y = torch.empty((P * n, wk.shape[0]), dtype=x2.dtype, device=x2.device)
+    ys = y.view(k, P * m, wk.shape[0])
+    for c, work in enumerate(pend):
         work.wait()
-        yi = torch.mm(g.reshape(-1, D), wk.t()).view(P, B, m, N)   # one 2-D GEMM (no batch-stride-0 broadcast)
-        yv[:, :, i].copy_(yi.permute(1, 0, 2, 3))                   # [P, B, m, N] -> rank-major sequence order
-    return y, xg.view(k, P, B, m, D)
+        torch.mm(gs[c], wk.t(), out=ys[c])
+    return y, xg
 
 
-def _matmul_rs(x_cm: torch.Tensor, w: torch.Tensor, group, transpose_w: bool) -> torch.Tensor:
-    """RS(x @ op(w)) with the GEMM of micro-chunk i+1 overlapping the reduce-scatter of i; x_cm [k, P, B, m, F]
-    chunk-major.  Returns [B, Sl, N] (this rank's sequence shard); with one sequence per rank (B = 1) the micro
-    reduce-scatters write straight into their slice of it."""
-    k, _, B, m, _ = x_cm.shape
+def _matmul_rs(x2: torch.Tensor, w: torch.Tensor, group, k: int, transpose_w: bool) -> torch.Tensor:
+    """RS(x @ op(w)) with the GEMM of round c+1 overlapping the reduce-scatter of round c; x2 [P n, F] in natural
+    token order.  Returns this rank's [n, N] token shard."""
+    P = _ws(group)
+    T, F = x2.shape
+    m = T // (P * k)
     wk = _k_major(w, transpose_w)
     N = wk.shape[0]
-    y = torch.empty((B, k * m, N), dtype=x_cm.dtype, device=x_cm.device) if B == 1 else None
+    y = torch.empty((k * m, N), dtype=x2.dtype, device=x2.device)
+    xs, ys = x2.view(k, P * m, F), y.view(k, m, N)
     pend = []
-    for i in range(k):
-        part = torch.mm(x_cm[i].reshape(-1, x_cm.shape[-1]), wk.t()).view(*x_cm.shape[1:-1], N)
-        pend.append(_rs_async(part, group, y[:, i * m:(i + 1) * m] if y is not None else None))
-    outs = []
-    for o, work in pend:
+    for c in range(k):
+        part = torch.mm(xs[c], wk.t())
+        pend.append((part, dist.reduce_scatter_tensor(ys[c], part, op=dist.ReduceOp.SUM, group=group,
+                                                      async_op=True)))
+    for _, work in pend:
         work.wait()
-        outs.append(o)
-    return y if y is not None else torch.cat(outs, 1)
+    return y
 
 
 class _AGMatmulFn(torch.autograd.Function):
-    """Column-parallel projection with a sequence-sharded input: y = AG_seq(x) W^T (+ b)."""
+    """Column-parallel projection with a token-sharded input: y = AG_tokens(x) W^T (+ b)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, group, chunks):
-        k = _chunks_for(x.shape[1], chunks)
-        y, xg = _ag_matmul(x.contiguous(), w, group, k, transpose_w=True)
+    def forward(ctx, x, w, b, group, k):
+        P = _ws(group)
+        x = x.contiguous()
+        y, xg = _ag_matmul(x.view(-1, x.shape[-1]), w, group, k, transpose_w=True)
         if b is not None:
             y = y + b
         ctx.save_for_backward(xg, w)
-        ctx.group, ctx.k, ctx.has_bias = group, k, b is not None
-        return y
+        ctx.group, ctx.k, ctx.has_bias, ctx.xshape = group, k, b is not None, x.shape
+        shp = list(x.shape)
+        shp[1] *= P
+        shp[-1] = y.shape[-1]
+        return y.view(shp)
 
     @staticmethod
     def backward(ctx, dy):
         xg, w = ctx.saved_tensors
-        P, k = _ws(ctx.group), ctx.k
-        dy_cm = _chunk_major(dy.contiguous(), P, k)                           # [k, P, B, m, N]
-        dx = _matmul_rs(dy_cm, w, ctx.group, transpose_w=False) if ctx.needs_input_grad[0] else None
-        gw = None
-        if ctx.needs_input_grad[1]:
-            gw = weight_grad(w, dy_cm.reshape(-1, dy_cm.shape[-1]), xg.reshape(-1, xg.shape[-1]))
-        gb = dy.reshape(-1, dy.shape[-1]).sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        dy2 = dy.contiguous().view(-1, dy.shape[-1])
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _matmul_rs(dy2, w, ctx.group, ctx.k, transpose_w=False).view(ctx.xshape)
+        gw = weight_grad(w, dy2, xg) if ctx.needs_input_grad[1] else None
+        gb = dy2.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return dx, gw, gb, None, None
 
 
 class _MatmulRSFn(torch.autograd.Function):
-    """Row-parallel projection producing a sequence-sharded output: y = RS_seq(x W^T); x [B, S, F_local]."""
+    """Row-parallel projection producing a token-sharded output: y = RS_tokens(x W^T); x [B, S, F_local]."""
 
     @staticmethod
-    def forward(ctx, x, w, group, chunks):
+    def forward(ctx, x, w, group, k):
         P = _ws(group)
-        k = _chunks_for(x.shape[1] // P, chunks)
-        x_cm = _chunk_major(x.contiguous(), P, k)                             # [k, P, B, m, F]
-        y = _matmul_rs(x_cm, w, group, transpose_w=True)
-        ctx.save_for_backward(x_cm, w)
-        ctx.group, ctx.k = group, k
-        return y
+        x = x.contiguous()
+        x2 = x.view(-1, x.shape[-1])
+        y = _matmul_rs(x2, w, group, k, transpose_w=True)
+        ctx.save_for_backward(x2, w)
+        ctx.group, ctx.k, ctx.xshape = group, k, x.shape
+        shp = list(x.shape)
+        shp[1] //= P
+        shp[-1] = y.shape[-1]
+        return y.view(shp)
 
     @staticmethod
     def backward(ctx, dy):
-        x_cm, w = ctx.saved_tensors
-        dyc = dy.contiguous()
-        dx, dyg = _ag_matmul(dyc, w, ctx.group, ctx.k, transpose_w=False)   # dyg [k, P, B, m, D] chunk-major
-        gw = None
-        if ctx.needs_input_grad[1]:
-            gw = weight_grad(w, dyg.reshape(-1, dyg.shape[-1]), x_cm.reshape(-1, x_cm.shape[-1]))
-        return (dx if ctx.needs_input_grad[0] else None), gw, None, None
+        x2, w = ctx.saved_tensors
+        dy2 = dy.contiguous().view(-1, dy.shape[-1])
+        dx, dyg = _ag_matmul(dy2, w, ctx.group, ctx.k, transpose_w=False)   # dyg: the gathered dy, natural order
+        gw = weight_grad(w, dyg, x2) if ctx.needs_input_grad[1] else None
+        return (dx.view(ctx.xshape) if ctx.needs_input_grad[0] else None), gw, None, None
 
 
 def ag_matmul(x, w, b, group, chunks: int = 2):
-    """y = all_gather_seq(x) @ w^T (+ b), x [B, S/tp, D] -> y [B, S, N_local]."""
+    """y = all_gather_tokens(x) @ w^T (+ b), x [B, S/tp, D] -> y [B, S, N_local].  The micro-collective count is the
+    group's token layout (comm.functional.sp_chunks; parallelize_llama sets it from the layers' ``chunks``)."""
     if _ws(group) == 1:
         return torch.nn.functional.linear(x, w, b)
-    return _AGMatmulFn.apply(x, w, b, group, chunks)
+    return _AGMatmulFn.apply(x, w, b, group, _rounds(group, x.numel() // x.shape[-1]))
 
 
 def matmul_reduce_scatter(x, w, group, chunks: int = 2):
-    """y = reduce_scatter_seq(x @ w^T), x [B, S, F_local] -> y [B, S/tp, D]."""
+    """y = reduce_scatter_tokens(x @ w^T), x [B, S, F_local] -> y [B, S/tp, D]."""
     if _ws(group) == 1:
         return torch.nn.functional.linear(x, w)
-    return _MatmulRSFn.apply(x, w, group, chunks)
+    return _MatmulRSFn.apply(x, w, group, _rounds(group, x.numel() // x.shape[-1] // _ws(group)))

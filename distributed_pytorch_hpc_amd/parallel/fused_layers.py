@@ -59,28 +59,37 @@ def set_enabled(mlp: bool | None = None, qkv: bool | None = None, gemm_nt: str |
     return old
 
 
+_TOKENS = "tokens"   # comm.functional.TOKENS (the sequence-parallel token sharding)
+
+
 def _plain_weight(mod) -> bool:
     from torch import nn
 
     return isinstance(mod, nn.Linear) and mod.bias is None and not getattr(mod.weight, "_dph_tp", False)
 
 
-def _tp_col(mod) -> bool:
+def _tp_col(mod, allow_async: bool = False) -> bool:
     from .tensor_parallel import ColwiseParallelLinear
 
     return (isinstance(mod, ColwiseParallelLinear) and mod.bias is None and not mod.gather_output and
-            mod.seq_dim == 1 and not mod.async_chunks)
+            mod.seq_dim == _TOKENS and (allow_async or not mod.async_chunks))
 
 
-def _tp_row(mod) -> bool:
+def _tp_row(mod, allow_async: bool = False) -> bool:
     from .tensor_parallel import RowwiseParallelLinear
 
     return (isinstance(mod, RowwiseParallelLinear) and mod.bias is None and mod.input_is_parallel and
-            mod.seq_dim == 1 and not mod.async_chunks)
+            mod.seq_dim == _TOKENS and (allow_async or not mod.async_chunks))
 
 
-def _tp_pair(col, row) -> bool:
-    return _tp_col(col) and _tp_row(row) and col.group is row.group and col.sp == row.sp
+def _tp_pair(col, row, allow_async: bool = False) -> bool:
+    return (_tp_col(col, allow_async) and _tp_row(row, allow_async) and col.group is row.group and col.sp == row.sp
+            and bool(col.async_chunks) == bool(row.async_chunks))
+
+
+def _async_pair(col, row) -> bool:
+    """Both halves of the MLP pipelined against their sequence-parallel collectives (parallel/async_tp.py)."""
+    return _tp_pair(col, row, allow_async=True) and col.sp and bool(col.async_chunks) and _tp_world(col) > 1
 
 
 def _tp_world(mod) -> int:
@@ -93,13 +102,13 @@ def _tp_input(col, x):
     """The column-parallel layer's input as its local GEMM sees it: sequence-gathered (SP) or copied to the group."""
     from ..comm import functional as cf
 
-    return cf.gather_along_dim(x, 1, col.group) if col.sp else cf.copy_to_group(x, col.group)
+    return cf.gather_along_dim(x, cf.TOKENS, col.group) if col.sp else cf.copy_to_group(x, col.group)
 
 
 def _tp_output(row, y):
     from ..comm import functional as cf
 
-    return cf.reduce_scatter_along_dim(y, 1, row.group) if row.sp else cf.reduce_from_group(y, row.group)
+    return cf.reduce_scatter_along_dim(y, cf.TOKENS, row.group) if row.sp else cf.reduce_from_group(y, row.group)
 
 
 def _nt_ok(rows: int, n: int, k: int) -> bool:
@@ -175,7 +184,7 @@ class _SwiGLUMLPFn(torch.autograd.Function):
 def swiglu_mlp_ok(x: torch.Tensor, w13_mod, w2_mod) -> bool:
     if not (_FUSED_MLP and _GEMM_NT != "0"):
         return False
-    tp = _tp_pair(w13_mod, w2_mod)
+    tp = _tp_pair(w13_mod, w2_mod, allow_async=True)
     if not (tp or (_plain_weight(w13_mod) and _plain_weight(w2_mod))):
         return False
     if _fp8.fp8_enabled() or not _native_bf16(x, w13_mod.weight, w2_mod.weight) or not _rows_ok(x):
@@ -185,13 +194,97 @@ def swiglu_mlp_ok(x: torch.Tensor, w13_mod, w2_mod) -> bool:
         if x.dim() != 3:
             return False
         rows *= _tp_world(w13_mod)            # the local GEMMs see the sequence-gathered activations
+        if _async_pair(w13_mod, w2_mod):      # ... one round of the token deal at a time
+            from ..comm.functional import sp_chunks
+
+            rows //= sp_chunks(w13_mod.group, x.numel() // x.shape[-1])
     h2 = w13_mod.weight.shape[0]
     h, d_out = h2 // 2, w2_mod.weight.shape[0]
     return (h2 % 2 == 0 and w2_mod.weight.shape[1] == h and _nt_ok(rows, h2, k) and _nt_ok(rows, d_out, h)
             and _nt_ok(rows, h, d_out) and w13_mod.weight.is_contiguous() and w2_mod.weight.is_contiguous())
 
 
+class _SwiGLUMLPAsyncFn(torch.autograd.Function):
+    """The fused tensor-parallel SwiGLU MLP with both sequence-parallel collectives pipelined (async TP): round c of
+    the token deal is all-gathered while the fused w13 + SwiGLU GEMM of round c-1 runs, and the w2 GEMM of round c
+    overlaps the reduce-scatter of round c-1.  Backward mirrors it (all-gather of dy feeding the fused w2-dgrad +
+    SwiGLU-backward GEMM, w13 dgrad feeding the reduce-scatter of dx); the weight gradients are one GEMM each over all
+    tokens (natural order, comm/functional.py TOKENS)."""
+
+    @staticmethod
+    def forward(ctx, x, w13, w2, group, k):
+        import torch.distributed as dist
+
+        P = dist.get_world_size(group)
+        x = x.contiguous()
+        d = x.shape[-1]
+        n = x.numel() // d
+        m = n // k
+        x2 = x.view(n, d)
+        xg = torch.empty((P * n, d), dtype=x.dtype, device=x.device)
+        xs, gs = x2.view(k, m, d), xg.view(k, P * m, d)
+        pend = [dist.all_gather_into_tensor(gs[c], xs[c], group=group, async_op=True) for c in range(k)]
+        h2, hl, dout = w13.shape[0], w13.shape[0] // 2, w2.shape[0]
+        x13 = torch.empty((P * n, h2), dtype=x.dtype, device=x.device)
+        h = torch.empty((P * n, hl), dtype=x.dtype, device=x.device)
+        x13s, hs = x13.view(k, P * m, h2), h.view(k, P * m, hl)
+        y = torch.empty((n, dout), dtype=x.dtype, device=x.device)
+        ys = y.view(k, m, dout)
+        rs = []
+        for c, work in enumerate(pend):
+            work.wait()
+            _lib.ops().gemm_nt_swiglu_into(gs[c], w13, x13s[c], hs[c])
+            part = nt_matmul(hs[c], w2)
+            rs.append((part, dist.reduce_scatter_tensor(ys[c], part, op=dist.ReduceOp.SUM, group=group,
+                                                        async_op=True)))
+        for _, work in rs:
+            work.wait()
+        ctx.save_for_backward(xg, w13, x13, h, w2)
+        ctx.group, ctx.k, ctx.shape = group, k, x.shape
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        import torch.distributed as dist
+
+        xg, w13, x13, h, w2 = ctx.saved_tensors
+        group, k = ctx.group, ctx.k
+        P = dist.get_world_size(group)
+        dy = dy.contiguous()
+        dout = dy.shape[-1]
+        n = dy.numel() // dout
+        m = n // k
+        dyg = torch.empty((P * n, dout), dtype=dy.dtype, device=dy.device)
+        dys, gs = dy.view(k, m, dout), dyg.view(k, P * m, dout)
+        pend = [dist.all_gather_into_tensor(gs[c], dys[c], group=group, async_op=True) for c in range(k)]
+        w2t = _lib.ops().transpose2d(w2)
+        h2 = x13.shape[1]
+        d13 = torch.empty((P * n, h2), dtype=dy.dtype, device=dy.device)
+        d13s, x13s = d13.view(k, P * m, h2), x13.view(k, P * m, h2)
+        d = xg.shape[1]
+        dx = torch.empty((n, d), dtype=dy.dtype, device=dy.device)
+        dxs = dx.view(k, m, d)
+        rs = []
+        for c, work in enumerate(pend):
+            work.wait()
+            _lib.ops().gemm_nt_dswiglu_into(gs[c], w2t, x13s[c], d13s[c])
+            part = _dgrad_nt(d13s[c], w13)
+            rs.append((part, dist.reduce_scatter_tensor(dxs[c], part, op=dist.ReduceOp.SUM, group=group,
+                                                        async_op=True)))
+        del w2t
+        gw2 = weight_grad(w2, dyg, h) if ctx.needs_input_grad[2] else None
+        gw13 = weight_grad(w13, d13, xg) if ctx.needs_input_grad[1] else None
+        for _, work in rs:
+            work.wait()
+        return dx.view(ctx.shape), gw13, gw2, None, None
+
+
 def swiglu_mlp(x: torch.Tensor, w13_mod, w2_mod) -> torch.Tensor:
+    if _async_pair(w13_mod, w2_mod):
+        from ..comm.functional import sp_chunks
+
+        return _SwiGLUMLPAsyncFn.apply(x, w13_mod.weight, w2_mod.weight, w13_mod.group,
+                                       sp_chunks(w13_mod.group, x.numel() // x.shape[-1]))
     if _tp_pair(w13_mod, w2_mod):
         # Megatron pair: the local fused MLP between the column layer's input collective and the row layer's output
         # collective (their autograd adjoints give the backward's reduce-scatter / all-gather)

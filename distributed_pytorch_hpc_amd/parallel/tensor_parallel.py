@@ -76,7 +76,7 @@ def _carry_flags(src: torch.Tensor, dst: torch.Tensor) -> None:
 
 class ColwiseParallelLinear(nn.Module):
     def __init__(self, lin: nn.Linear, group, sequence_parallel: bool = False, gather_output: bool = False,
-                 shard_fn: Optional[Callable] = None, seq_dim: int = 1):
+                 shard_fn: Optional[Callable] = None, seq_dim=cf.TOKENS):
         super().__init__()
         self.group, self.sp, self.gather_output, self.seq_dim = group, sequence_parallel, gather_output, seq_dim
         w = lin.weight.detach()
@@ -90,7 +90,7 @@ class ColwiseParallelLinear(nn.Module):
         self.async_chunks = 0   # > 0: sequence all-gather pipelined against the GEMM (parallel/async_tp.py)
 
     def forward(self, x):
-        if self.sp and self.async_chunks and self.seq_dim == 1 and x.dim() == 3 and _ws(self.group) > 1:
+        if self.sp and self.async_chunks and self.seq_dim == cf.TOKENS and x.dim() == 3 and _ws(self.group) > 1:
             y = ag_matmul(x, self.weight, self.bias, self.group, self.async_chunks)
         else:
             x = cf.gather_along_dim(x, self.seq_dim, self.group) if self.sp else cf.copy_to_group(x, self.group)
@@ -102,7 +102,7 @@ class ColwiseParallelLinear(nn.Module):
 
 class RowwiseParallelLinear(nn.Module):
     def __init__(self, lin: nn.Linear, group, sequence_parallel: bool = False, shard_fn: Optional[Callable] = None,
-                 input_is_parallel: bool = True, seq_dim: int = 1):
+                 input_is_parallel: bool = True, seq_dim=cf.TOKENS):
         super().__init__()
         self.group, self.sp, self.input_is_parallel, self.seq_dim = group, sequence_parallel, input_is_parallel, seq_dim
         w = lin.weight.detach()
@@ -116,7 +116,7 @@ class RowwiseParallelLinear(nn.Module):
     def forward(self, x):
         if not self.input_is_parallel:
             x = cf.split_along_dim(x, x.dim() - 1, self.group)
-        if self.sp and self.async_chunks and self.seq_dim == 1 and x.dim() == 3 and _ws(self.group) > 1:
+        if self.sp and self.async_chunks and self.seq_dim == cf.TOKENS and x.dim() == 3 and _ws(self.group) > 1:
             y = matmul_reduce_scatter(x, self.weight, self.group, self.async_chunks)
         else:
             y = _linear(x, self.weight, None)
@@ -128,7 +128,7 @@ class RowwiseParallelLinear(nn.Module):
 
 
 class VocabParallelEmbedding(nn.Module):
-    def __init__(self, emb: nn.Embedding, group, sequence_parallel: bool = False, seq_dim: int = 1):
+    def __init__(self, emb: nn.Embedding, group, sequence_parallel: bool = False, seq_dim=cf.TOKENS):
         super().__init__()
         self.group, self.sp, self.seq_dim = group, sequence_parallel, seq_dim
         ws, r = _ws(group), _rank(group)
@@ -210,6 +210,9 @@ def parallelize_llama(model, tp_group, sequence_parallel: bool = True, loss_para
     hd, nh, nkv = args.head_dim, args.n_heads, args.kv_heads
     assert nh % tp == 0 and nkv % tp == 0, f"heads ({nh}, kv {nkv}) must divide by tp={tp}"
     sp = sequence_parallel
+    # token layout of the sequence-parallel activations: async TP deals the tokens in `async_tp` rounds so each of
+    # its micro-collectives fills one contiguous slice (comm/functional.py TOKENS)
+    cf.set_sp_chunks(tp_group, async_tp if (sp and async_tp) else 1)
     qkv_sizes = [nh * hd, nkv * hd, nkv * hd]
     f = args.ffn_hidden
     assert f % tp == 0, f"ffn hidden {f} must divide by tp={tp}"
