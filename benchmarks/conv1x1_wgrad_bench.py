@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """ResNet-50's stride-1 1x1 weight gradients (B=256, bf16, channels-last): the framework's kernel (``ts_gemm_tn_``:
-the LDS-DMA c3w_k form, or with DPH_W1_KERNEL=0 the register-staged ts_tn_k -- the knob is read once per process)
-vs MIOpen, per shape in ms, plus the per-step total weighted by how often each shape occurs.
+the LDS-DMA c3w_k form) vs MIOpen, per shape in ms, plus the per-step total weighted by how often each shape occurs.
 
     python benchmarks/conv1x1_wgrad_bench.py [--batch 256] [--json out.json]
 """
@@ -42,7 +41,7 @@ def main():
 
     _lib.require()
     torch.backends.cudnn.benchmark = True
-    kern = "ts_tn_k" if os.environ.get("DPH_W1_KERNEL", "1") == "0" else "c3w_k(1x1)"
+    kern = "c3w_k(1x1)"
     rows, tot, tot_mi = [], 0.0, 0.0
     for cin, cout, H, cnt in SHAPES:
         M = a.batch * H * H

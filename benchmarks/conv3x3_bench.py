@@ -2,7 +2,7 @@
 """Stride-1 3x3 convolutions of ResNet-50 (B=256, bf16, channels-last) and SimpleUNet (B=4, 181 x 360): MIOpen vs the
 framework's implicit-GEMM kernels, per pass (forward / input gradient / weight gradient), with TFLOP/s.
 
-    python benchmarks/conv3x3_bench.py [--json out.json]          # DPH_CONV3_KERNEL=ts: the older register-staged path
+    python benchmarks/conv3x3_bench.py [--json out.json]
 """
 import argparse
 import json
@@ -93,7 +93,7 @@ def main():
         tot["dph"] += cnt * d_all
         rows.append(r)
         print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}), flush=True)
-    res = {"kernel": os.environ.get("DPH_CONV3_KERNEL", "conv3 (LDS-DMA)"), "weighted_ms": tot, "shapes": rows}
+    res = {"kernel": "conv3 (LDS-DMA)", "weighted_ms": tot, "shapes": rows}
     print(json.dumps({k: v for k, v in res.items() if k != "shapes"}))
     if a.json:
         with open(a.json, "w") as fh:

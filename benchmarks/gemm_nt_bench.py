@@ -42,7 +42,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--json", default=None)
     ap.add_argument("--shapes", default=",".join(list(FWD) + list(DGRAD)))
-    ap.add_argument("--variants", default="1,3", help="gemm_nt variants to A/B (bit 0 LOOK, bit 1 32x32x16 MFMA)")
     ap.add_argument("--no-fused", action="store_true")
     a = ap.parse_args()
     _lib.require()
@@ -55,28 +54,20 @@ def main():
         x = torch.randn(T, K, device="cuda").to(torch.bfloat16)
         w = (0.02 * torch.randn(N, K, device="cuda")).to(torch.bfloat16)
         flop = 2.0 * T * N * K
-        variants = [int(v) for v in a.variants.split(",")]
-        t = {"blaslt": [], **{f"dph_v{v}": [] for v in variants}}
+        t = {"blaslt": [], "dph": []}
         ref = x.float() @ w.float().t()
-        errs = {}
-        for v in variants:
-            ops.gemm_nt_variant_(v)
-            errs[v] = ((ops.gemm_nt(x, w).float() - ref).norm() / ref.norm()).item()
+        err = ((ops.gemm_nt(x, w).float() - ref).norm() / ref.norm()).item()
         del ref
         for _ in range(a.rounds):
             t["blaslt"].append(timeit(lambda: torch.matmul(x, w.t()), a.iters))
-            for v in variants:
-                ops.gemm_nt_variant_(v)
-                t[f"dph_v{v}"].append(timeit(lambda: ops.gemm_nt(x, w), a.iters))
-        ops.gemm_nt_variant_(-1)
+            t["dph"].append(timeit(lambda: ops.gemm_nt(x, w), a.iters))
         row = {k: {"ms_min": min(v), "ms_med": sorted(v)[len(v) // 2], "tflops_max": flop / min(v) / 1e9}
                for k, v in t.items()}
-        row["relerr"] = errs
+        row["relerr"] = err
         res[name] = row
-        bl = row["blaslt"]["tflops_max"]
-        print(f"{name:14s} N={N:6d} K={K:6d}  blaslt {bl:7.1f} TF  " + "  ".join(
-            f"v{v} {row[f'dph_v{v}']['tflops_max']:7.1f} ({row[f'dph_v{v}']['tflops_max'] / bl:.3f})" for v in variants)
-            + f"  relerr {max(errs.values()):.2e}", flush=True)
+        bl, dp = row["blaslt"]["tflops_max"], row["dph"]["tflops_max"]
+        print(f"{name:14s} N={N:6d} K={K:6d}  blaslt {bl:7.1f} TF  dph {dp:7.1f} ({dp / bl:.3f})  relerr {err:.2e}",
+              flush=True)
         del x, w
     if a.no_fused:
         if a.json:

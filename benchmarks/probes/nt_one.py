@@ -17,14 +17,11 @@ def main():
     ap.add_argument("--n", type=int, default=12288)
     ap.add_argument("--k", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--variant", type=int, default=-1, help="gemm_nt variant (-1 default)")
     ap.add_argument("--hipblaslt", action="store_true")
     a = ap.parse_args()
     _lib.require()
     x = torch.randn(a.m, a.k, device="cuda").to(torch.bfloat16)
     w = (0.02 * torch.randn(a.n, a.k, device="cuda")).to(torch.bfloat16)
-    if a.variant >= 0:
-        torch.ops.dph.gemm_nt_variant_(a.variant)
     for _ in range(a.iters):
         if a.hipblaslt:
             torch.matmul(x, w.t())

@@ -39,6 +39,8 @@ def main(argv=None):
     ap.add_argument("--torch-profile", action="store_true",
                     help="after the timed steps, profile one step with torch.profiler and print where device memcpys "
                          "and copy kernels come from (Python call sites)")
+    ap.add_argument("--stack-dump", type=int, default=0, metavar="S",
+                    help="diagnostics: dump every thread's Python stack each S seconds and mark each phase")
     a = ap.parse_args(argv)
 
     from torch.testing._internal.distributed.fake_pg import FakeStore
@@ -50,10 +52,10 @@ def main(argv=None):
     from distributed_pytorch_hpc_amd.parallel.tensor_parallel import parallelize_llama
 
     _lib.require()
-    if os.environ.get("DPH_STACK_DUMP_S"):   # diagnostics: the Python stack of every thread every N seconds
+    if a.stack_dump:   # diagnostics: the Python stack of every thread every S seconds
         import faulthandler
 
-        faulthandler.dump_traceback_later(int(os.environ["DPH_STACK_DUMP_S"]), repeat=True, file=sys.stderr)
+        faulthandler.dump_traceback_later(a.stack_dump, repeat=True, file=sys.stderr)
     if a.gemm_nt is not None or a.fused_qkv is not None:
         fused_layers.set_enabled(gemm_nt=a.gemm_nt, qkv=None if a.fused_qkv is None else bool(a.fused_qkv))
     dist.init_process_group("fake", store=FakeStore(), rank=0, world_size=a.tp)
@@ -77,7 +79,7 @@ def main(argv=None):
     g = torch.Generator(device=dev).manual_seed(0)
     t = torch.randint(0, margs.vocab_size, (a.batch, a.seq + 1), device=dev, generator=g)
 
-    debug = bool(os.environ.get("DPH_STACK_DUMP_S"))
+    debug = bool(a.stack_dump)
 
     def mark(what):
         if debug:

@@ -285,20 +285,6 @@ struct KVTilePlan {
       }
     }
   }
-  // One image (K or V) of tile [k0, k0 + 64) -> `lds_w` (this wave's 1 KiB share of the image), same rules.
-  __device__ __forceinline__ void stage_one_async(unsigned lds_w, const bf16* xp, int64_t x_ss, int k0, int Sk) const {
-    const bf16* xt = uniform_ptr(xp + (int64_t)k0 * x_ss);
-    if (k0 + BN <= Sk) {
-      const unsigned o = (unsigned)((prow * x_ss + pch) * 2), st = (unsigned)(RSTEP * x_ss * 2);
-#pragma unroll
-      for (int i = 0; i < NS; ++i) lds_dma16(xt, o + i * st, lds_w + NT * i * 16);
-    } else {
-      const int rmax = Sk - 1 - k0;
-#pragma unroll
-      for (int i = 0; i < NS; ++i)
-        lds_dma16(xt, (unsigned)((min(prow + i * RSTEP, rmax) * x_ss + pch) * 2), lds_w + NT * i * 16);
-    }
-  }
 };
 
 // glds_stage issued through lds_dma16 (see KVTilePlan::stage_async) with the per-lane swizzled source row/chunk
@@ -355,16 +341,13 @@ __device__ __forceinline__ int wave_tile_count(int ntiles, int q0w, int off) {
 // tile max exceeds it by more than RESCALE_THR (FA4-style lazy rescaling): p is then bounded by 2^THR,
 // harmless for the bf16 P operand and the fp32 accumulators, and the exact result is recovered by the
 // final 1/l.  The rescale branch is wave-uniform (ballot), so steady-state tiles skip 16*DT multiplies.
-// STG (8 waves, DPH_ATTN_WAVES=9): waves 4..7 run one barrier behind waves 0..3, so on every SIMD one wave's QK^T /
-// PV MFMAs overlap its partner's softmax VALU work instead of both waves hitting the exp chain at once.  The K/V
-// ring is 4 tiles deep with the DMA two tiles ahead: an early wave reads tile t after its barrier t-1, which the late
-// waves pass only after retiring THEIR share of tile t (issued two iterations earlier); the slot a DMA overwrites
-// (tile t-2's) was last read by a late wave two barriers back.  Every iteration drains its own DMA (vmcnt(0)): one
-// tile of compute hides it.  Measured on B 8, H 32, S 4096, D 128 causal (profiles/r4/attn_stagger/): 809-814
-// TFLOP/s vs 819-822 for 8 waves and 834-838 for the default 4 waves -- kept opt-in.
-// PRIO: issue priority 1 over the S and O MFMA chains, 0 in the softmax (as the dK/dV kernel's VAR bit 2).
-template <int HD, bool CAUSAL, int NW, bool DROP = false, bool STG = false, bool PRIO = false>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
+// Rejected round-4/5 variants of this kernel (evidence kept under profiles/): 8-wave workgroups (819-822 vs 834-838
+// TFLOP/s), waves 4..7 staggered one barrier behind (809-814), issue priority over the MFMA chains (within noise),
+// and a software-pipelined body that overlaps each wave's softmax with its own next QK^T (754-788 vs 831-833,
+// profiles/r5/attn_fwd_pipe/).
+template <int HD, bool CAUSAL, bool DROP = false>
+__global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
+  constexpr int NW = 4;
   using Plan = KVTilePlan<HD, 64 * NW>;
   constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
   constexpr float RESCALE_THR = 8.f;
@@ -412,11 +395,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
   const unsigned dthr = DROP ? attn_drop_thr(p.drop_p) : 0u;
 
   if (ntiles > 0) plan.stage_async(lds_w, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
-  if (STG && ntiles > 1) plan.stage_async(lds_w + 2 * TILE, kp, vp, p.k_ss, p.v_ss, BN, p.Sk);
   wait_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
-  const bool late = STG && __builtin_amdgcn_readfirstlane(wid) >= 4;
-  if (late) __builtin_amdgcn_s_barrier();
 
   auto tile = [&](const char* Kl, const char* Vl, int k0, bool need_mask) {
     // ---- S^T = K Q^T for two 32-key sub-tiles ----
@@ -428,7 +408,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
 #pragma unroll
       for (int kk = 0; kk < KS; ++kk) kf[sub][kk] = lds_b128(Kl, plan.row(sub, kk));
     f32x16 s[2];
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       s[sub] = mfma32(kf[sub][0], qf[0], zacc);
@@ -439,7 +418,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
     __builtin_amdgcn_sched_group_barrier(0x008, 2 * KS, 0);   // ... then the MFMAs
     // phase fences keep the scheduler from hoisting the next phase's LDS reads into this one's live range
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     if (need_mask) {  // wave-uniform: only diagonal / ragged tiles pay for the selects
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
@@ -491,32 +469,24 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
     // (+2 % forward TFLOP/s at B 8, H 32, S 4096, D 128; the backward kernels keep their fences: -2 % without them)
 
     // ---- O^T += V^T P^T ----
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt)
         o[dt] = mfma32(lds_tr2(Vl, plan.tr(ks, dt, 0), plan.tr(ks, dt, 1)), pf[ks], o[dt]);
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = STG ? (t & 3) : (t & 1);
-    if (STG) {
-      if (t + 2 < ntiles)
-        plan.stage_async(lds_w + ((t + 2) & 3) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 2) * BN, p.Sk);
-    } else if (t + 1 < ntiles) {
-      plan.stage_async(lds_w + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
-    }
+    const int buf = t & 1;
+    if (t + 1 < ntiles) plan.stage_async(lds_w + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
     const char* Kl = smem + buf * 2 * TILE;
     if (t < wtiles) {
       const int k0 = t * BN;
       tile(Kl, Kl + TILE, k0, (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0w + off)));
     }
-    wait_vmcnt<0>();   // this wave's share of tile t+1 (STG: t+2) has landed ...
+    wait_vmcnt<0>();   // this wave's share of tile t+1 has landed ...
     __builtin_amdgcn_s_barrier();   // ... and every wave's, and nobody reads tile t's images any more
   }
-  if (STG && !late) __builtin_amdgcn_s_barrier();   // balance the stagger
 
   // ---- epilogue: O = O^T / l, lse ----
   lsum = half_sum(lsum);
@@ -561,238 +531,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_fwd_k(AttnParams p) {
 }
 
 // ==================================================================================================
-// Forward, software-pipelined (default for HD 64 / 128 without dropout or ring merge)
-// ==================================================================================================
-// The geometry of attn_fwd_k (4 waves = 128 query rows per workgroup, 32 rows per wave, two workgroups per CU so the
-// two waves on a SIMD belong to independent workgroups), with the tile loop run over 32-key SUB-tiles u so that
-// inside ONE wave the matrix pipe and the VALU always have independent work:
-//   sub-iteration u (S_u = raw scores of sub-tile u, computed in sub-iteration u-1):
-//     [odd u = 2t+1: wait + barrier; LDS-DMA of V tile t+1 and K tile t+2]
-//     BB_a   O += V_{u-1}^T P_{u-1}^T (8 MFMA)   beside   row max of S_u, rescale test
-//            [rare, wave-uniform: rescale O, l and S_u]
-//     BB_b   S_{u+1} = K_{u+1} Q^T (8 MFMA)     beside   exp2 / row sum / bf16 pack of S_u -> P_u
-// attn_fwd_k runs S -> softmax -> PV as one dependent chain per tile, so a wave's VALU and MFMA phases never overlap
-// and only the partner wave on the SIMD can fill them (PMC round 4: MFMA busy 0.46, issue stalls 41 %).  32-key
-// sub-tiles keep two score tiles, the P tile and O within the 256-register budget (64-key sub-tiles spill).
-// K and V have separate 2-slot rings (64 KB per workgroup, two workgroups per CU): V of a tile is read two
-// sub-iterations after its K, so at the barrier of u = 2t+1 the slots of V_{t-1} and K_t are free, V_{t+1} and K_{t+2}
-// are issued into them, and each DMA has a whole tile of compute to land before the barrier that waits for it.
-// No VALU pass for the softmax bookkeeping: Q is prescaled by scale * log2(e) when loaded and every S accumulator
-// starts at -m (the running max, log2 units) -- or at -inf where the causal / ragged mask hides the key -- so the MFMA
-// chain leaves s * scale * log2e - m and p = exp2 of it directly.  m is raised only when a lane's max exceeds it by
-// more than RESCALE_THR (lazy rescaling: p <= 2^THR in between, exact after the final 1 / l); sub-tile 0 always sets it.
-template <int HD, bool CAUSAL, int VAR = 0>
-__global__ __launch_bounds__(256, 2) void attn_fwd_pipe_k(AttnParams p) {
-  constexpr int NW = 4;
-  using Plan = KVTilePlan<HD, 64 * NW>;
-  constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
-  constexpr float RESCALE_THR = 8.f;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  // wid through readfirstlane: provably wave-uniform, so the per-wave tile count and the body selection are scalar
-  // branches and the DMA operands stay in SGPRs
-  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5,
-            l32 = lane & 31;
-  const int nqb = (p.Sq + BM - 1) / BM;
-  int bx, hq, b;
-  xcd_block(nqb, p.Hq, bx, hq, b, nqb * p.Hq * p.B);
-  const int qb = CAUSAL ? nqb - 1 - bx : bx;   // heaviest causal blocks first
-  const int hk = hq / (p.Hq / p.Hkv);
-  const int q0 = qb * BM, q0w = q0 + 32 * wid;
-  const int myq = q0w + l32;
-  const int off = p.Sk - p.Sq;
-
-  const bf16* qp = (const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
-  const bf16* kp = (const bf16*)p.k + (int64_t)b * p.k_sb + (int64_t)hk * p.k_sh;
-  const bf16* vp = (const bf16*)p.v + (int64_t)b * p.v_sb + (int64_t)hk * p.v_sh;
-
-  // Q^T fragments (B operand of S^T = K Q^T), prescaled by c = scale * log2(e) in fp32, rounded once to bf16
-  const float c = p.scale * 1.4426950408889634f;
-  bf16x8 qf[KS];
-#pragma unroll
-  for (int kk = 0; kk < KS; ++kk) {
-    bf16x8 x = myq < p.Sq ? *reinterpret_cast<const bf16x8*>(qp + (int64_t)myq * p.q_ss + kk * 16 + 8 * h) : zero8();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = (bf16)((float)x[j] * c);
-    qf[kk] = x;
-  }
-
-  int kv_end = p.Sk;
-  if (CAUSAL) kv_end = min(p.Sk, q0 + BM + off);
-  const int ntiles = __builtin_amdgcn_readfirstlane(kv_end > 0 ? (kv_end + BN - 1) / BN : 0);
-  // sub-tiles (32 keys) with a key visible to this wave; the workgroup still walks all ntiles for the shared staging
-  int wsub = 2 * ntiles;
-  if (CAUSAL) {
-    const int last = q0w + 31 + off;
-    wsub = last < 0 ? 0 : min(2 * ntiles, last / 32 + 1);
-  }
-  wsub = __builtin_amdgcn_readfirstlane(min(wsub, (p.Sk + 31) / 32));   // scalar loop bounds (uniform branches)
-
-  Plan plan;
-  plan.init(lane, p.k_ss);
-  plan.init_async();
-  const unsigned lds_w = lds_addr(smem + wid * 64 * 16);
-
-  f32x16 o[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-  float m = 0.f, lsum = 0.f;   // running max (log2 units) / this half-wave's partial row sum
-
-  // LDS: K slots 0 / 1 | V slots 0 / 1 (tile t in slot t & 1)
-  if (ntiles > 0) {
-    plan.stage_one_async(lds_w, kp, p.k_ss, 0, p.Sk);
-    plan.stage_one_async(lds_w + 2 * TILE, vp, p.v_ss, 0, p.Sk);
-    plan.stage_one_async(lds_w + TILE, kp, p.k_ss, min(1, ntiles - 1) * BN, p.Sk);
-  }
-  wait_vmcnt<0>();
-  __builtin_amdgcn_s_barrier();
-
-  auto kslot = [&](int u) { return smem + ((u >> 1) & 1) * TILE; };
-  auto vslot = [&](int u) { return smem + 2 * TILE + ((u >> 1) & 1) * TILE; };
-  auto needs_mask = [&](int u) { return u * 32 + 32 > p.Sk || (CAUSAL && u * 32 + 31 > q0w + off); };
-  // visible keys of this lane's query: key <= lim
-  const int lim = CAUSAL ? min(myq + off, p.Sk - 1) : p.Sk - 1;
-  // S_u = K_u Q^T - m (-inf where masked) for sub-tile u, K fragments straight from the swizzled LDS image.  The
-  // masked start values are a wave-uniform branch ahead of the MFMA chain, so the chain and the VALU work placed
-  // beside it stay one basic block.
-  auto kread = [&](int u, bf16x8 (&kf)[KS]) {
-    const char* Kl = kslot(u);
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) kf[kk] = lds_b128(Kl, plan.row(u & 1, kk));
-  };
-  auto qk_f = [&](int u, const bf16x8 (&kf)[KS]) {
-    f32x16 a;
-    if (needs_mask(u)) {
-      const int d = u * 32 + 4 * h - lim;   // key(r) - lim = acc_row(r, 0) + d
-#pragma unroll
-      for (int r = 0; r < 16; ++r) a[r] = acc_row(r, 0) + d <= 0 ? -m : -INFINITY;
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) a[r] = -m;
-    }
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) a = mfma32(kf[kk], qf[kk], a);
-    return a;
-  };
-  auto qk = [&](int u) {
-    bf16x8 kf[KS];
-    kread(u, kf);
-    return qk_f(u, kf);
-  };
-  // O += V_u^T P_u^T: the sub-tile's two 16-key k-steps of the V image
-  auto pv = [&](int u, const bf16x8 (&pf)[2]) {
-    const char* Vl = vslot(u);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) {
-        const int ks = 2 * (u & 1) + j;
-        o[dt] = mfma32(lds_tr2(Vl, plan.tr(ks, dt, 0), plan.tr(ks, dt, 1)), pf[j], o[dt]);
-      }
-  };
-  // row max of S_u (both half-waves) and the lazy rescale (wave-uniform branch, rare after sub-tile 0)
-  auto rescale = [&](f32x16& s, bool first) {
-    float mx = fmaxf(fmaxf(s[0], s[1]), s[2]);
-#pragma unroll
-    for (int r = 3; r < 15; r += 2) mx = fmaxf(mx, fmaxf(s[r], s[r + 1]));
-    mx = fmaxf(mx, s[15]);
-    mx = half_max(mx);
-    if (first || __ballot(mx > RESCALE_THR)) {
-      const float d = first ? (mx == -INFINITY ? 0.f : mx) : fmaxf(mx, 0.f);
-      const float alpha = exp2_(-d);
-      lsum *= alpha;
-      m += d;
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[r] -= d;
-    }
-  };
-  auto expsum = [&](f32x16& s, bf16x8 (&pf)[2]) {
-    float ls0 = 0.f, ls1 = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      s[r] = exp2_(s[r]);
-      s[r + 1] = exp2_(s[r + 1]);
-      ls0 += s[r];
-      ls1 += s[r + 1];
-    }
-    lsum += ls0 + ls1;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) pf[j][i] = (bf16)s[8 * j + i];
-  };
-  // u = 2t+1: wait for V_t and K_{t+1} (issued one tile ago), barrier, then LDS-DMA of V_{t+1} and K_{t+2} into the
-  // slots of V_{t-1} and K_t, whose last reads (PV_{2t-1}, S_{2t+1}) every wave has made before this barrier.  Past the
-  // last tile the DMA re-reads the last tile (stage_one_async's row clamp needs k0 < Sk) into a free slot, so every
-  // workgroup-wide step is the same in every iteration.
-  auto sync = [&](int t) {
-    wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    plan.stage_one_async(lds_w + 2 * TILE + ((t + 1) & 1) * TILE, vp, p.v_ss, min(t + 1, ntiles - 1) * BN, p.Sk);
-    plan.stage_one_async(lds_w + (t & 1) * TILE, kp, p.k_ss, min(t + 2, ntiles - 1) * BN, p.Sk);
-  };
-
-  // One body for every sub-tile (several specialised bodies spill at this register budget): sub-tile 0 multiplies a
-  // zero P with V_0 (adds exactly 0: V_0 is finite staged data), and the wave's last sub-tile computes an S_{u+1}
-  // that is dropped (its K slot holds staged data) and finishes its own PV at once, before its V slot is recycled.
-  f32x16 s = {};
-  bf16x8 pf[2] = {zero8(), zero8()};
-  if (wsub > 0) s = qk(0);
-  for (int u = 0; u < 2 * ntiles; ++u) {
-    if (u & 1) sync(u >> 1);
-    if (u < wsub) {
-      // ---- BB_a: PV_{u-1} beside max(S_u) ----
-      bf16x8 kf[KS];
-      if constexpr ((VAR & 1) != 0) kread(u + 1, kf);   // K of S_{u+1} in flight during PV_{u-1}
-      pv(max(u - 1, 0), pf);
-      if constexpr ((VAR & 2) != 0) {
-        __builtin_amdgcn_sched_group_barrier(0x100, (VAR & 1) ? 12 : 4, 0);
-#pragma unroll
-        for (int i = 0; i < 2 * DT; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          if (i + 2 < 2 * DT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-        }
-      }
-      rescale(s, u == 0);
-      // ---- BB_b: S_{u+1} beside exp(S_u) ----
-      if constexpr ((VAR & 1) == 0) kread(u + 1, kf);
-      const f32x16 sn = qk_f(u + 1, kf);
-      expsum(s, pf);
-      if constexpr ((VAR & 2) != 0) {
-        if constexpr ((VAR & 1) == 0) __builtin_amdgcn_sched_group_barrier(0x100, 4, 1);
-#pragma unroll
-        for (int i = 0; i < KS; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-          if ((VAR & 1) == 0 && i + 4 < KS) __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
-          __builtin_amdgcn_sched_group_barrier(0x002, 8, 1);
-        }
-      }
-      s = sn;
-      if (u == wsub - 1) pv(u, pf);
-    }
-  }
-  wait_vmcnt<0>();   // the last iterations' DMA must land before the slabs reuse the ring
-  __syncthreads();
-
-  // ---- epilogue: O = O^T / l through this wave's LDS slab, lse ----
-  lsum = half_sum(lsum);
-  static_assert(NW * 32 * HD * 2 <= 4 * TILE, "epilogue slabs exceed the forward kernel's LDS");
-  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-  bf16* o0 = (bf16*)p.o + (int64_t)b * p.o_sb + (int64_t)q0w * p.o_ss + (int64_t)hq * p.o_sh;
-  store_rows_lds<DT>(smem + wid * (32 * HD * 2), o0, p.o_ss, min(32, p.Sq - q0w), o, inv, h, l32, 0, nullptr, nullptr,
-                     0);
-  if (myq < p.Sq && h == 0 && p.lse)
-    p.lse[((int64_t)b * p.Hq + hq) * p.Sq + myq] = lsum > 0.f ? (m + __log2f(lsum)) * 0.6931471805599453f : -INFINITY;
-}
-
-// ==================================================================================================
 // Backward
 // ==================================================================================================
 // delta[b, h, q] = sum_d dO[b,q,h,d] * O[b,q,h,d] (fp32).  TPR = D/8 lanes per row, 8 elements per lane;
@@ -826,15 +564,16 @@ __global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ o, 
 // of the GQA group x 32-row query tiles (double-buffered Q / dO LDS images, one barrier per tile).
 // S and dP are computed with the key on the lane, so P and dS are directly the B operands of
 // dV^T += dO^T P and dK^T += Q^T dS: no LDS round trip, no atomics.
-// VAR (A/B knob, DPH_ATTN_BWD_VAR): bit 0 = row constants as the initial S / dP accumulators (no dropout), bit 1 =
-// the dV / dK transposed reads software-pipelined one step ahead, the first step issued before the softmax, bit 2 =
-// issue priority 1 while a wave is in its MFMA chains (S / dP, then dV / dK) and 0 in its softmax, so the partner
-// wave on the SIMD (the other workgroup's) fills the chains' gaps with its softmax instead of competing for issue.
-template <int HD, bool CAUSAL, int NW, bool DROP = false, int VAR = 0>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams P) {
+// The dV / dK transposed reads are software-pipelined one step ahead (the first step issued before the softmax), and a
+// wave runs at issue priority 1 while in its MFMA chains (S / dP, then dV / dK) and 0 in its softmax, so the partner
+// wave on the SIMD (the other workgroup's) fills the chains' gaps with its softmax instead of competing for issue
+// (round 3/4 A/B: +2 % and +1 %; row constants as the initial S / dP accumulators measured -2 % and were removed).
+template <int HD, bool CAUSAL, bool DROP = false>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
+  constexpr int NW = 4;
   constexpr int NT = 64 * NW, BNK = 32 * NW, BMQ = 32, NC = HD / 8, KS = HD / 16, DT = HD / 32;
-  constexpr bool RINIT = !DROP && (VAR & 1);
-  constexpr bool TRPIPE = (VAR & 2) != 0;
+  constexpr bool RINIT = false;
+  constexpr bool TRPIPE = true;
   constexpr int QIMG = BMQ * HD * 2;        // Q / dO tile image [32 q][HD]
   constexpr int KIMG = BNK * HD * 2;        // K image [128 keys][HD] (B operand of S = Q K^T)
   // img_off's line permutation repeats every 16 lines.  For NC >= 8, rows r and r + 32 are a multiple of 16
@@ -975,7 +714,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
     if (!(CAUSAL && key0 > qt0 + BMQ - 1 + off)) {
       const float* ls = lse_s + buf * BMQ;
       const float* ds = del_s + buf * BMQ;
-      if constexpr ((VAR & 4) != 0) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
       f32x16 s = mfma32(lds_b128(Ql, qro[0]), lds_b128(Kimg, kofs(0)), RINIT ? row_init(ls) : zacc);
       f32x16 dp = mfma32(lds_b128(Ol, qro[0]), vf[0], RINIT ? row_init(ds) : zacc);
 #pragma unroll
@@ -983,7 +722,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
         s = mfma32(lds_b128(Ql, qro[kk]), lds_b128(Kimg, kofs(kk)), s);
         dp = mfma32(lds_b128(Ol, qro[kk]), vf[kk], dp);
       }
-      if constexpr ((VAR & 4) != 0) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
       // wave-uniform: only diagonal / ragged tiles pay for the selects (masked scores -> -inf -> P = 0)
       if ((qt0 + BMQ > p.Sq) || (key0 + 32 > p.Sk) || (CAUSAL && key0 + 31 > qt0 + off)) {
 #pragma unroll
@@ -1027,7 +766,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
           sb[ks][j] = (bf16)dp[8 * ks + j];
         }
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr ((VAR & 4) != 0) __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_s_setprio(1);
       if constexpr (TRPIPE) {
         // step i = (ks, dt): its operands were read one step earlier; each step issues the next step's 4 reads
         // ahead of its own 2 MFMAs
@@ -1054,7 +793,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
             dk[dt] = mfma32(lds_tr2(Ql, o0, o1), sb[ks], dk[dt]);
           }
       }
-      if constexpr ((VAR & 4) != 0) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_setprio(0);
     }
     if (it + 1 < total) stage_scalars(buf ^ 1);
     wait_vmcnt<0>();
@@ -1076,13 +815,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dkdv_k(AttnBwdParams
 // query (lane & 31).  Per 64-key tile: S^T = K Q^T and dP^T = V dO^T (A = K / V rows from LDS, B = Q^T / dO^T
 // fragments in registers), P^T = exp2(S^T c - lse) and dS^T = P^T (dP^T - delta) lane-locally (lse and delta
 // are one scalar per lane), then dQ^T += K^T dS^T with dS^T consumed straight from the accumulator.
-// PF (A/B knob, DPH_ATTN_DQ_VAR=1): the dQ product's transposed K reads software-pipelined one MFMA ahead, the first
-// issued before the last sub-tile's softmax.
-// KQ: K / V fragments read KS / KQ k-steps ahead of their MFMAs (2 = half a sub-tile; 4 = a quarter, 16 fewer VGPRs:
-// the KQ = 2 form spills 3 registers at 256).
-// PRIO: issue priority 1 over the S^T / dP^T and dQ MFMA chains, 0 in the softmax (as the dK/dV kernel's VAR bit 2).
-template <int HD, bool CAUSAL, int NW, bool DROP = false, bool PF = false, int KQ = 2, bool PRIO = false>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P) {
+// K / V fragments are read a quarter sub-tile ahead of their MFMAs (KQ = 4: no register spills; the half-sub-tile form
+// spilled 3 registers).  Rejected A/B variants (profiles/r4/attn_dq/, attn_prio/): the dQ product's transposed K reads
+// software-pipelined one MFMA ahead, and issue priority over the MFMA chains.
+template <int HD, bool CAUSAL, bool DROP = false>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
+  constexpr int NW = 4, KQ = 4;
+  constexpr bool PF = false, PRIO = false;
   using Plan = KVTilePlan<HD, 64 * NW>;
   constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1241,95 +980,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_dq_k(AttnBwdParams P
 }
 
 // ==================================================================================================
-// Waves per workgroup (4 or 8; DPH_ATTN_WAVES overrides, for A/B runs).  8 waves = 256 query rows (or keys) share
-// every staged K/V (or Q/dO) tile: half the LDS fill traffic per MFMA of 4 waves, one workgroup per CU.
-constexpr bool kAttnDqDefaultPf = false;
-constexpr bool kAttnFwdDefaultPrio = false;
-// A/B on one MI355X: 0 -> 659/663, 1 -> 645/650, 2 -> 673/672, 3 -> 664/660 TF (round 3); 6 (2 + issue priority over
-// the MFMA chains) -> 691.4 / 690.3 / 686.3 vs 2 -> 681.7 / 684.7 / 685.5 TF, interleaved (round 4, profiles/r4/attn_prio/)
-constexpr int kAttnBwdDefaultVar = 6;
-
-static int attn_waves(int fallback) {
-  static const int w = [] {
-    const char* e = getenv("DPH_ATTN_WAVES");
-    return e ? atoi(e) : 0;
-  }();
-  return (w == 4 || w == 8 || w == 9) ? w : fallback;
-}
-
-static bool attn_fwd_prio() {   // DPH_ATTN_FWD_PRIO=1: issue priority over the forward's MFMA chains (A/B)
-  static const bool v = [] {
-    const char* e = getenv("DPH_ATTN_FWD_PRIO");
-    return e ? atoi(e) == 1 : kAttnFwdDefaultPrio;
-  }();
-  return v;
-}
-
-template <int HD, int NW, bool STG = false>
-static void fwd_launch_nw(const AttnParams& p, hipStream_t st) {
-  const dim3 grid((unsigned)((p.Sq + 32 * NW - 1) / (32 * NW) * p.Hq * p.B));   // 1-D: xcd_block() maps it
-  const size_t lds = (STG ? 4 : 2) * 2 * 64 * HD * 2;
-  if (!STG && attn_fwd_prio()) {
-    if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, NW, false, false, true>), grid, dim3(64 * NW), lds, st, p);
-    else hipLaunchKernelGGL((attn_fwd_k<HD, false, NW, false, false, true>), grid, dim3(64 * NW), lds, st, p);
-    return;
-  }
-  if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, NW, false, STG>), grid, dim3(64 * NW), lds, st, p);
-  else hipLaunchKernelGGL((attn_fwd_k<HD, false, NW, false, STG>), grid, dim3(64 * NW), lds, st, p);
-}
-
-// DPH_ATTN_FWD=pipe: the software-pipelined forward (attn_fwd_pipe_k) instead of attn_fwd_k (A/B; slower so far:
-// 734 vs 788 TFLOP/s on B 8, H 32, S 4096, D 128 causal, profiles/r5/attn_fwd_pipe/)
-static bool attn_fwd_legacy() {
-  static const bool v = [] {
-    const char* e = getenv("DPH_ATTN_FWD");
-    return !(e && std::string(e) == "pipe");
-  }();
-  return v;
-}
-
+// One geometry for every kernel: 4 waves = 128 query rows (or keys) per workgroup, two workgroups per CU.
 template <int HD>
 static void fwd_launch(const AttnParams& p, hipStream_t st) {
-  if constexpr (HD >= 64) {
-    if (p.drop_p == 0.f && !p.acc_o && !attn_fwd_legacy()) {
-      const dim3 grid((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));   // 1-D: xcd_block() maps it
-      const size_t lds = 4 * 64 * HD * 2;
-      static const int var = [] {
-        const char* e = getenv("DPH_ATTN_FWD_VAR");
-        return e ? atoi(e) : 0;
-      }();
-      switch (var) {
-        case 1:
-          if (p.causal) hipLaunchKernelGGL((attn_fwd_pipe_k<HD, true, 1>), grid, dim3(256), lds, st, p);
-          else hipLaunchKernelGGL((attn_fwd_pipe_k<HD, false, 1>), grid, dim3(256), lds, st, p);
-          break;
-        case 2:
-          if (p.causal) hipLaunchKernelGGL((attn_fwd_pipe_k<HD, true, 2>), grid, dim3(256), lds, st, p);
-          else hipLaunchKernelGGL((attn_fwd_pipe_k<HD, false, 2>), grid, dim3(256), lds, st, p);
-          break;
-        case 3:
-          if (p.causal) hipLaunchKernelGGL((attn_fwd_pipe_k<HD, true, 3>), grid, dim3(256), lds, st, p);
-          else hipLaunchKernelGGL((attn_fwd_pipe_k<HD, false, 3>), grid, dim3(256), lds, st, p);
-          break;
-        default:
-          if (p.causal) hipLaunchKernelGGL((attn_fwd_pipe_k<HD, true>), grid, dim3(256), lds, st, p);
-          else hipLaunchKernelGGL((attn_fwd_pipe_k<HD, false>), grid, dim3(256), lds, st, p);
-      }
-      return;
-    }
+  const dim3 grid((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));   // 1-D: xcd_block() maps it
+  const size_t lds = 2 * 2 * 64 * HD * 2;
+  if (p.drop_p > 0.f) {
+    if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, true>), grid, dim3(256), lds, st, p);
+    else hipLaunchKernelGGL((attn_fwd_k<HD, false, true>), grid, dim3(256), lds, st, p);
+  } else {
+    if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true>), grid, dim3(256), lds, st, p);
+    else hipLaunchKernelGGL((attn_fwd_k<HD, false>), grid, dim3(256), lds, st, p);
   }
-  if (p.drop_p > 0.f) {   // dropout: 4-wave instantiations only
-    const dim3 grid((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
-    const size_t lds = 2 * 2 * 64 * HD * 2;
-    if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, 4, true>), grid, dim3(256), lds, st, p);
-    else hipLaunchKernelGGL((attn_fwd_k<HD, false, 4, true>), grid, dim3(256), lds, st, p);
-    return;
-  }
-  if constexpr (HD >= 64) {   // a 64-key tile of HD = 32 has fewer 16-B chunks than 8 waves have lanes
-    if (attn_waves(4) == 8) return fwd_launch_nw<HD, 8>(p, st);
-    if (attn_waves(4) == 9) return fwd_launch_nw<HD, 8, true>(p, st);   // 8 waves, staggered
-  }
-  fwd_launch_nw<HD, 4>(p, st);
 }
 
 void flash_attn_fwd(const AttnParams& p, hipStream_t st) {
@@ -1342,77 +1004,23 @@ void flash_attn_fwd(const AttnParams& p, hipStream_t st) {
   }
 }
 
-// dK/dV kernel variant (template VAR of attn_bwd_dkdv_k); DPH_ATTN_BWD_VAR overrides, for A/B runs
-static int attn_bwd_var() {
-  static const int v = [] {
-    const char* e = getenv("DPH_ATTN_BWD_VAR");
-    const int x = e ? atoi(e) : kAttnBwdDefaultVar;
-    return (x >= 0 && x <= 3) || x == 6 ? x : kAttnBwdDefaultVar;
-  }();
-  return v;
-}
-
-template <int HD, int NW, int VAR>
-static void dkdv_launch(const AttnBwdParams& P, hipStream_t st) {
+template <int HD, bool DROP>
+static void bwd_launch_t(const AttnBwdParams& P, hipStream_t st) {
   const AttnParams& p = P.f;
-  constexpr int BNK = 32 * NW;
-  const size_t lds_kv = BNK * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
-  const dim3 grid_kv((unsigned)((p.Sk + BNK - 1) / BNK * p.Hkv * p.B));
-  if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, NW, false, VAR>), grid_kv, dim3(64 * NW), lds_kv, st, P);
-  else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, NW, false, VAR>), grid_kv, dim3(64 * NW), lds_kv, st, P);
-}
-
-template <int HD, int NW>
-static void bwd_launch_nw(const AttnBwdParams& P, hipStream_t st) {
-  const AttnParams& p = P.f;
-  switch (attn_bwd_var()) {
-    case 1: dkdv_launch<HD, NW, 1>(P, st); break;
-    case 2: dkdv_launch<HD, NW, 2>(P, st); break;
-    case 3: dkdv_launch<HD, NW, 3>(P, st); break;
-    case 6: dkdv_launch<HD, NW, 6>(P, st); break;
-    default: dkdv_launch<HD, NW, 0>(P, st); break;
-  }
+  const size_t lds_kv = 128 * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
+  const dim3 grid_kv((unsigned)((p.Sk + 127) / 128 * p.Hkv * p.B));
+  if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, DROP>), grid_kv, dim3(256), lds_kv, st, P);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, DROP>), grid_kv, dim3(256), lds_kv, st, P);
   const size_t lds_q = 2 * 2 * 64 * HD * 2;
-  const dim3 grid_q((unsigned)((p.Sq + 32 * NW - 1) / (32 * NW) * p.Hq * p.B));
-  // default 2 (no register spills): backward 682.5 / 681.6 / 679.8 vs 677.1 / 680.1 / 679.2 TFLOP/s with 0, interleaved
-  // on one MI355X (profiles/r4/attn_dq/)
-  static const int dq_var = [] {
-    const char* e = getenv("DPH_ATTN_DQ_VAR");
-    return e ? atoi(e) : (kAttnDqDefaultPf ? 1 : 2);
-  }();
-  if (dq_var == 3) {   // quarter-sub-tile read-ahead + issue priority over the MFMA chains
-    if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW, false, false, 4, true>), grid_q, dim3(64 * NW), lds_q, st, P);
-    else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW, false, false, 4, true>), grid_q, dim3(64 * NW), lds_q, st, P);
-  } else if (dq_var == 2) {   // quarter-sub-tile K / V read-ahead (no spills)
-    if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW, false, false, 4>), grid_q, dim3(64 * NW), lds_q, st, P);
-    else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW, false, false, 4>), grid_q, dim3(64 * NW), lds_q, st, P);
-  } else if (dq_var == 1) {
-    if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW, false, true>), grid_q, dim3(64 * NW), lds_q, st, P);
-    else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW, false, true>), grid_q, dim3(64 * NW), lds_q, st, P);
-  } else {
-    if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, NW>), grid_q, dim3(64 * NW), lds_q, st, P);
-    else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, NW>), grid_q, dim3(64 * NW), lds_q, st, P);
-  }
+  const dim3 grid_q((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
+  if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, DROP>), grid_q, dim3(256), lds_q, st, P);
+  else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, DROP>), grid_q, dim3(256), lds_q, st, P);
 }
 
 template <int HD>
 static void bwd_launch(const AttnBwdParams& P, hipStream_t st) {
-  const AttnParams& p = P.f;
-  if (p.drop_p > 0.f) {   // dropout: 4-wave instantiations only
-    const size_t lds_kv = 128 * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
-    const dim3 grid_kv((unsigned)((p.Sk + 127) / 128 * p.Hkv * p.B));
-    if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, 4, true>), grid_kv, dim3(256), lds_kv, st, P);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, 4, true>), grid_kv, dim3(256), lds_kv, st, P);
-    const size_t lds_q = 2 * 2 * 64 * HD * 2;
-    const dim3 grid_q((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
-    if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, 4, true>), grid_q, dim3(256), lds_q, st, P);
-    else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, 4, true>), grid_q, dim3(256), lds_q, st, P);
-    return;
-  }
-  if constexpr (HD >= 64) {
-    if (attn_waves(4) == 8) return bwd_launch_nw<HD, 8>(P, st);
-  }
-  bwd_launch_nw<HD, 4>(P, st);
+  if (P.f.drop_p > 0.f) bwd_launch_t<HD, true>(P, st);
+  else bwd_launch_t<HD, false>(P, st);
 }
 
 void flash_attn_bwd(const AttnBwdParams& P, hipStream_t st) {

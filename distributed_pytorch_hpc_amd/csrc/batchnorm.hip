@@ -40,7 +40,7 @@ __device__ __forceinline__ Stat chan_merge(Stat a, Stat b) {
 }
 
 // Per-block statistics: block b covers rows [b*rows_per_block, ...).  Partials: mean/m2 [G][C], n [G].
-template <typename T, bool TREE>
+template <typename T>
 __global__ __launch_bounds__(BN_NT) void bn_stats_k(const T* __restrict__ x, float* __restrict__ pmean,
                                                     float* __restrict__ pm2, float* __restrict__ pn, int64_t M,
                                                     int C, int64_t rows_per_block) {
@@ -79,43 +79,27 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_k(const T* __restrict__ x, flo
     shq[threadIdx.x * 8 + i] = n > 0.f ? fmaxf(ss[i] - s[i] * mean_d, 0.f) : 0.f;
   }
   __syncthreads();
-  if (TREE) {
-    // log2(rpi) merge rounds with every row lane of the lower half active (rpi is a power of two), instead of
-    // rpi - 1 serial merges by the ch8 lanes of row group 0 (rpi = 32 at C = 64)
-    for (int half = rpi >> 1; half > 0; half >>= 1) {
-      if (r0 < half) {
-        const int t = (r0 + half) * ch8 + cc;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const Stat a = {shn[threadIdx.x * 8 + i], shm[threadIdx.x * 8 + i], shq[threadIdx.x * 8 + i]};
-          const Stat m = chan_merge(a, {shn[t * 8 + i], shm[t * 8 + i], shq[t * 8 + i]});
-          shn[threadIdx.x * 8 + i] = m.n;
-          shm[threadIdx.x * 8 + i] = m.mean;
-          shq[threadIdx.x * 8 + i] = m.m2;
-        }
-      }
-      __syncthreads();
-    }
-    if (r0 == 0) {
+  // log2(rpi) merge rounds with every row lane of the lower half active (rpi is a power of two), instead of
+  // rpi - 1 serial merges by the ch8 lanes of row group 0 (rpi = 32 at C = 64)
+  for (int half = rpi >> 1; half > 0; half >>= 1) {
+    if (r0 < half) {
+      const int t = (r0 + half) * ch8 + cc;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        pmean[(int64_t)blockIdx.x * C + cc * 8 + i] = shm[threadIdx.x * 8 + i];
-        pm2[(int64_t)blockIdx.x * C + cc * 8 + i] = shq[threadIdx.x * 8 + i];
+        const Stat a = {shn[threadIdx.x * 8 + i], shm[threadIdx.x * 8 + i], shq[threadIdx.x * 8 + i]};
+        const Stat m = chan_merge(a, {shn[t * 8 + i], shm[t * 8 + i], shq[t * 8 + i]});
+        shn[threadIdx.x * 8 + i] = m.n;
+        shm[threadIdx.x * 8 + i] = m.mean;
+        shq[threadIdx.x * 8 + i] = m.m2;
       }
-      if (cc == 0) pn[blockIdx.x] = (float)(end > beg ? end - beg : 0);
     }
-    return;
+    __syncthreads();
   }
   if (r0 == 0) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      Stat acc = {shn[threadIdx.x * 8 + i], shm[threadIdx.x * 8 + i], shq[threadIdx.x * 8 + i]};
-      for (int g = 1; g < rpi; ++g) {
-        const int t = g * ch8 + cc;
-        acc = chan_merge(acc, {shn[t * 8 + i], shm[t * 8 + i], shq[t * 8 + i]});
-      }
-      pmean[(int64_t)blockIdx.x * C + cc * 8 + i] = acc.mean;
-      pm2[(int64_t)blockIdx.x * C + cc * 8 + i] = acc.m2;
+      pmean[(int64_t)blockIdx.x * C + cc * 8 + i] = shm[threadIdx.x * 8 + i];
+      pm2[(int64_t)blockIdx.x * C + cc * 8 + i] = shq[threadIdx.x * 8 + i];
     }
     if (cc == 0) pn[blockIdx.x] = (float)(end > beg ? end - beg : 0);
   }
@@ -397,17 +381,9 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_dx_k(const T* __restrict__ dy, c
   }
 }
 
-// Block-level Chan merge of the statistics kernel's row-lane partials as an LDS tree (default; 25.0 -> 19.7 ms of
-// bn_stats_k over benchmarks/bn_bench.py, profiles/r2s3/ab_bn_tree/) or serially by row group 0 (DPH_BN_TREE=0,
-// the previous form, kept for A/B runs: scripts/ab_bn_stats.sh).  The backward reduction's plain sums gained
-// nothing from the same tree (16.1 / 14.7 vs 16.3 / 14.8 ms) and stay serial.
-bool bn_tree() {
-  static const bool tree = [] {
-    const char* e = getenv("DPH_BN_TREE");
-    return !(e && e[0] == '0');
-  }();
-  return tree;
-}
+// The statistics kernel merges its row-lane partials as an LDS tree (25.0 -> 19.7 ms of bn_stats_k over
+// benchmarks/bn_bench.py against a serial merge by row group 0, profiles/r2s3/ab_bn_tree/).  The backward
+// reduction's plain sums gained nothing from the same tree (16.1 / 14.7 vs 16.3 / 14.8 ms) and stay serial.
 
 int stats_grid(int64_t M, int C, int64_t* rows_per_block) {
   const int rpi = BN_NT / (C / 8);
@@ -440,12 +416,7 @@ void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const 
     // Merged first into S segments of >= 4 partials per thread (FIN_GROUPS row groups per block); with a few hundred
     // partials or fewer bn_finalize_k takes them directly.  (S = 64 for every shape -- up to 16 384 mostly idle
     // 1024-thread blocks at 2048 channels -- measured 16 us per merge.)
-    static const bool legacy = [] {   // DPH_BN_MERGE_LEGACY=1: 64 segments for every shape (A/B runs)
-      const char* e = getenv("DPH_BN_MERGE_LEGACY");
-      return e && atoi(e) == 1;
-    }();
-    const int S = legacy ? std::min(G, 64)
-                         : std::min(std::min(G, 64), (pre_groups + 4 * FIN_GROUPS - 1) / (4 * FIN_GROUPS));
+    const int S = std::min(std::min(G, 64), (pre_groups + 4 * FIN_GROUPS - 1) / (4 * FIN_GROUPS));
     if (S <= 1) {
       G = pre_groups;
       pmean = pre_stats;
@@ -466,12 +437,8 @@ void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const 
   } else {
     const size_t shs = 3 * BN_NT * 8 * sizeof(float);
     DPH_DISPATCH_FLOAT(dt, T, {
-      if (bn_tree())
-        hipLaunchKernelGGL((bn_stats_k<T, true>), dim3(G), dim3(BN_NT), shs, st, (const T*)x, workspace,
-                           workspace + (int64_t)G * C, workspace + 2 * (int64_t)G * C, M, (int)C, rpb);
-      else
-        hipLaunchKernelGGL((bn_stats_k<T, false>), dim3(G), dim3(BN_NT), shs, st, (const T*)x, workspace,
-                           workspace + (int64_t)G * C, workspace + 2 * (int64_t)G * C, M, (int)C, rpb);
+      hipLaunchKernelGGL((bn_stats_k<T>), dim3(G), dim3(BN_NT), shs, st, (const T*)x, workspace,
+                         workspace + (int64_t)G * C, workspace + 2 * (int64_t)G * C, M, (int)C, rpb);
     });
   }
   const dim3 fg((unsigned)(C / 8));

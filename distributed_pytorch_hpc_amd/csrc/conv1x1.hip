@@ -57,7 +57,7 @@ constexpr int TS_KF = TS_BK / 16;   // MFMA k-steps (A fragments) per K-step
 // Occupancy: the plain / ADD forms fit 128 VGPRs for 4 workgroups per CU (LDS 36 KiB each); at 132 they ran 3, and
 // ResNet-50's 392-row-block layers (14 x 14 at B = 256) then launch 784 workgroups for 768 slots -- a second round for
 // 16 of them (benchmarks/probes/grid_tail.py: +23 % time for +2 % rows there, profiles/r4/grid_tail/).
-// MINB = 4 (the default; DPH_TS_NT_OCC=3 selects 1, the compiler's own budget) for the 128-VGPR build.
+// MINB = 4 forces the 128-VGPR build (MINB = 1, the compiler's own budget, measured slower: profiles/r4/grid_tail/).
 template <int BN, bool C3, bool ADD = false, bool STATS = false, bool PRO = false, int ADDS = 0, int MINB = 4>
 __global__ __launch_bounds__(TS_NT, PRO ? 1 : MINB) void ts_nt_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                  bf16* __restrict__ C, int M, int N, int K, int64_t lda,
@@ -635,25 +635,15 @@ __global__ __launch_bounds__(256) void ts_reduce_k(const float* __restrict__ P, 
 
 }  // namespace
 
-static bool ts_nt_occ4() {
-  static const bool on = [] {
-    const char* e = getenv("DPH_TS_NT_OCC");
-    return !(e && e[0] == '3');
-  }();
-  return on;
-}
 template <int BN, bool C3, bool ADD = false, bool STATS = false, bool PRO = false, int ADDS = 0>
 static void ts_nt_launch(int nblk, hipStream_t st, const void* A, const void* B, void* C, int64_t M, int64_t N,
                          int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int H, int W, int cin, const void* D,
                          float* stats, const float* pro_ss) {
-  if (ts_nt_occ4())
-    hipLaunchKernelGGL((ts_nt_k<BN, C3, ADD, STATS, PRO, ADDS, 4>), dim3(nblk), dim3(TS_NT), 0, st, (const bf16*)A,
-                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, (const bf16*)D,
-                       stats, pro_ss);
-  else
-    hipLaunchKernelGGL((ts_nt_k<BN, C3, ADD, STATS, PRO, ADDS, 1>), dim3(nblk), dim3(TS_NT), 0, st, (const bf16*)A,
-                       (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, (const bf16*)D,
-                       stats, pro_ss);
+  // built for 4 workgroups per CU (128 VGPRs, no scratch): +0.5 % in-step over the compiler's budget of 3
+  // (profiles/r4/ts_nt_occ/)
+  hipLaunchKernelGGL((ts_nt_k<BN, C3, ADD, STATS, PRO, ADDS, 4>), dim3(nblk), dim3(TS_NT), 0, st, (const bf16*)A,
+                     (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin, (const bf16*)D,
+                     stats, pro_ss);
 }
 
 bool conv1x1_supported(int64_t M, int64_t N, int64_t K) {
@@ -684,18 +674,10 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
   ts_nt_launch<BN_, C3_>(nmb * (int)(N / BN_), st, A, B, C, M, N, K, lda, ldb, ldc, H, W, cin, nullptr, nullptr,   \
                          nullptr)
   // 128-wide column tiles whenever N allows: 64-wide tiles double the workgroup count of the short-grid 14x14 / 7x7
-  // layers but measured 1.1-1.4x slower there too (profiles/conv_nt_bn_ab.log).  DPH_TS_NT_BN=64 forces them.
-  static const int force_bn = [] {
-    const char* e = getenv("DPH_TS_NT_BN");
-    return e ? atoi(e) : 0;
-  }();
-  const bool wide = N % 128 == 0 && force_bn != 64;
-  // 3x3: the LDS-DMA implicit GEMM of conv3x3.hip (DPH_CONV3_KERNEL=ts keeps this file's register-staged C3 path)
-  static const bool c3_ts = [] {
-    const char* e = getenv("DPH_CONV3_KERNEL");
-    return e && e[0] == 't';
-  }();
-  if (c3 && D == nullptr && !c3_ts && conv3_supported(M, N, K, lda, ldb)) {
+  // layers but measured 1.1-1.4x slower there too (profiles/conv_nt_bn_ab.log).
+  const bool wide = N % 128 == 0;
+  // 3x3: the LDS-DMA implicit GEMM of conv3x3.hip where it tiles; this file's register-staged C3 path otherwise
+  if (c3 && D == nullptr && conv3_supported(M, N, K, lda, ldb)) {
     conv3_gemm(A, B, C, M, N, K, lda, ldb, ldc, H, W, st, stats);   // (+ BatchNorm partials of the output)
     return;
   }
@@ -746,11 +728,8 @@ int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K) {
   // runs a second, nearly empty round -- measured 1.4x slower than 1017), +2 steps of per-workgroup prologue /
   // epilogue, and the fp32 partials written here and re-read by ts_reduce_k (~1.5 us per 8 MB at the measured
   // 1.47 us per step).  Chunks of at least 1024 rows, partial buffers of at most max(256 splits, 64 MB).
-  // DPH_TS_TN_WGS overrides R.
-  static const int R = [] {
-    const char* e = getenv("DPH_TS_TN_WGS");
-    return e ? atoi(e) : 256 * 4;
-  }();
+  // (Modelling R = 1024 resident workgroups measured as well as any other value: profiles/r4/rejected_ts_tn_wgs/.)
+  constexpr int R = 256 * 4;
   const int64_t tiles = (N / 64) * (K / 64);
   const int64_t smax = std::max<int64_t>(1, std::min<int64_t>(M / 1024,
                                                               std::max<int64_t>(256, (int64_t(64) << 20) / (N * K * 4))));
@@ -769,32 +748,17 @@ int ts_gemm_tn_splits(int64_t M, int64_t N, int64_t K) {
 }
 
 bool c3w_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
-  static const bool off = [] {
-    const char* e = getenv("DPH_CONV3W_KERNEL");
-    return e && e[0] == 't';
-  }();
   // 32-bit buffer offsets below the 0x80000000 "padding" sentinel; fp32 row division exact below 2^24 pixels
-  return !off && N % 64 == 0 && K % C3W_TK == 0 && M * lda * 2 < (int64_t(1) << 31) &&
+  return N % 64 == 0 && K % C3W_TK == 0 && M * lda * 2 < (int64_t(1) << 31) &&
          M * ldb * 2 < (int64_t(1) << 31) && M < (int64_t(1) << 24);
 }
 
 static int64_t c3w_tiles(int64_t N, int64_t K, int64_t tk) { return (N / (N % 128 == 0 ? 128 : 64)) * (K / tk); }
 
-// LDS ring depth of c3w_k: DPH_W1_STAGES for the 1x1 weight gradient, DPH_C3W_STAGES for the 3x3 / strided / stem ones
-// (2..5; a launch caps it at what fits 160 KiB of LDS).  More than 2 stages = one workgroup per CU.
-static int env_stages(const char* name, int dflt) {
-  const char* e = getenv(name);
-  const int v = e ? atoi(e) : dflt;
-  return v < 2 ? 2 : (v > 5 ? 5 : v);
-}
-static int w1_stages() {
-  static const int ns = env_stages("DPH_W1_STAGES", 2);
-  return ns;
-}
-static int c3w_stages() {
-  static const int ns = env_stages("DPH_C3W_STAGES", 2);
-  return ns;
-}
+// LDS ring depth of c3w_k: 2 stages, two workgroups per CU (3-5 stages = one workgroup per CU measured slower,
+// profiles/r4/c3w_ring/).
+static int w1_stages() { return 2; }
+static int c3w_stages() { return 2; }
 
 template <int TCO, int GEN, int SL, int NS>
 static void c3w_go(unsigned nblk, hipStream_t st, const void* A, const void* B, float* P, int64_t M, int64_t N,
@@ -807,12 +771,7 @@ template <int TCO, int GEN, int SL>
 static void c3w_launch(int ns, unsigned nblk, hipStream_t st, const void* A, const void* B, float* P, int64_t M,
                        int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t chunk, int H, int W, int cin,
                        const ConvGeo& g) {
-  constexpr int STG = (TCO / 64 + SL) * C3W_SLAB, LDS = 160 * 1024;
-  if constexpr (5 * STG <= LDS)
-    if (ns >= 5) return c3w_go<TCO, GEN, SL, 5>(nblk, st, A, B, P, M, N, K, lda, ldb, chunk, H, W, cin, g);
-  if constexpr (4 * STG <= LDS)
-    if (ns >= 4) return c3w_go<TCO, GEN, SL, 4>(nblk, st, A, B, P, M, N, K, lda, ldb, chunk, H, W, cin, g);
-  if (ns >= 3) return c3w_go<TCO, GEN, SL, 3>(nblk, st, A, B, P, M, N, K, lda, ldb, chunk, H, W, cin, g);
+  (void)ns;
   c3w_go<TCO, GEN, SL, 2>(nblk, st, A, B, P, M, N, K, lda, ldb, chunk, H, W, cin, g);
 }
 // resident workgroups per round: 2 per CU with the two-stage ring, 1 with a deeper one
@@ -830,12 +789,8 @@ static int w1_tk(int64_t K) { return K % 128 == 0 ? 128 : 64; }
 bool w1_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
   // default since the identity-row form (GEN 3, no per-piece divisions): 1.94-2.06 ms per ResNet-50 step over its
   // twelve 1x1 shapes vs 2.50 for the register-staged ts_tn_k and 3.26 for MIOpen (profiles/r4/c3w_incr/,
-  // profiles/r4/c3w_ring/identity_rows/); DPH_W1_KERNEL=0 keeps ts_tn_k.  The BatchNorm-prologue form stays on ts_tn_k.
-  static const bool on = [] {
-    const char* e = getenv("DPH_W1_KERNEL");
-    return !(e && e[0] == '0');
-  }();
-  return on && N % 64 == 0 && K % 64 == 0 && M * lda * 2 < (int64_t(1) << 31) && M * ldb * 2 < (int64_t(1) << 31) &&
+  // profiles/r4/c3w_ring/identity_rows/).  The BatchNorm-prologue form stays on ts_tn_k.
+  return N % 64 == 0 && K % 64 == 0 && M * lda * 2 < (int64_t(1) << 31) && M * ldb * 2 < (int64_t(1) << 31) &&
          M < (int64_t(1) << 24);
 }
 

@@ -30,7 +30,7 @@ namespace dph {
 namespace {
 
 constexpr int C3_BK = 64;
-constexpr int kConv3DefaultWm = 2;   // A/B: DPH_CONV3_WM
+constexpr int kConv3DefaultWm = 2;   // 4-wave tile (the 8-wave WM = 4 tile measured slower)
 constexpr int C3_ROWB = 128;   // LDS image row: 64 bf16
 
 __device__ __forceinline__ f32x16 c3_mfma(bf16x8 a, bf16x8 b, f32x16 c) {
@@ -300,22 +300,13 @@ bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) 
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 int64_t ldc, int H, int W, hipStream_t st, float* stats, const void* bias, bool bias_bf16) {
   const int cin = (int)(K / 9);
-  static const int force_bn = [] {
-    const char* e = getenv("DPH_CONV3_BN");
-    return e ? atoi(e) : 0;
-  }();
-  static const int force_wm = [] {
-    const char* e = getenv("DPH_CONV3_WM");
-    return e ? atoi(e) : 0;
-  }();
-  // 256-row tiles of 8 waves when that still gives >= 1 workgroup per CU (DPH_CONV3_WM=2 | 4 forces one form)
+  // 256-row tiles of 8 waves when that still gives >= 1 workgroup per CU
   const int64_t t256 = cdiv(M, 256) * (N / (N % 128 == 0 ? 128 : 64));
-  const int wm = force_wm == 2 || force_wm == 4 ? force_wm : (t256 >= 256 ? kConv3DefaultWm : 2);
+  const int wm = t256 >= 256 ? kConv3DefaultWm : 2;
   const int nmb = (int)cdiv(M, 64 * wm);
   // 128-wide tiles unless that leaves fewer than ~1.5 workgroups per CU (SimpleUNet's 22 x 45 bottleneck at B=4:
   // 124 tiles of 128 vs 248 of 64)
-  const bool wide = N % 128 == 0 && force_bn != 64 &&
-                    (force_bn == 128 || (int64_t)nmb * (N / 128) * (wm == 4 ? 2 : 1) >= 384);
+  const bool wide = N % 128 == 0 && (int64_t)nmb * (N / 128) * (wm == 4 ? 2 : 1) >= 384;
 #define DPH_C3(BN_, ST_, WM_, STATS_)                                                                            \
   hipLaunchKernelGGL((conv3_k<BN_, ST_, WM_, STATS_>), dim3(nmb * (int)(N / BN_)), dim3(128 * WM_), 0, st,    \
                      (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin,  \

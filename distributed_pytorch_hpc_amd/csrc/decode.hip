@@ -318,7 +318,7 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 }
 
 // default K split (workgroup = SG_WAVES waves) and unroll: the best of the (waves x unroll) sweep on every 7B
-// decode projection (profiles/serving/skinny_sweep/); DPH_SKINNY_CFG="waves,unroll" overrides
+// decode projection (profiles/serving/skinny_sweep/)
 constexpr int SG_WAVES = 4, SG_UNROLL = 4;
 
 template <int MT, int U, int NWV = SG_WAVES>
@@ -583,33 +583,8 @@ void skinny_gemm(const void* x, int64_t ldx, const void* w, int64_t ldw, void* y
     gemv(a, GX_PLAIN, st);
     return;
   }
-  // DPH_SKINNY_CFG="waves,unroll" (A/B runs of benchmarks/skinny_gemm_bench.py): waves in {2, 4, 8}, unroll in {4, 8}
-  static int cfg_w = -1, cfg_u = -1;
-  if (cfg_w < 0) {
-    cfg_w = SG_WAVES; cfg_u = 0;
-    if (const char* e = getenv("DPH_SKINNY_CFG")) {
-      int a = 0, b = 0;
-      if (sscanf(e, "%d,%d", &a, &b) == 2 && (a == 2 || a == 4 || a == 8) && (b == 4 || b == 8)) { cfg_w = a; cfg_u = b; }
-    }
-  }
+  // (waves, unroll) sweeps of benchmarks/skinny_gemm_bench.py picked SG_WAVES / SG_UNROLL (profiles/r3/skinny_*)
   const int mt = (M + 15) / 16;
-  if (cfg_u != 0 && K % (32 * cfg_w) == 0) {
-    const dim3 blk(64 * cfg_w);
-#define DPH_SK(MT_, U_, W_) hipLaunchKernelGGL((skinny_gemm_k<MT_, U_, W_>), grid, blk, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K)
-#define DPH_SK_MT(U_, W_)                          \
-  do {                                             \
-    if (mt == 1) DPH_SK(1, U_, W_);                \
-    else if (mt == 2) DPH_SK(2, U_, W_);           \
-    else if (mt == 3) DPH_SK(3, 4, W_);            \
-    else DPH_SK(4, 4, W_);                         \
-  } while (0)
-    if (cfg_w == 2) { if (cfg_u == 4) DPH_SK_MT(4, 2); else DPH_SK_MT(8, 2); }
-    else if (cfg_w == 4) { if (cfg_u == 4) DPH_SK_MT(4, 4); else DPH_SK_MT(8, 4); }
-    else { if (cfg_u == 4) DPH_SK_MT(4, 8); else DPH_SK_MT(8, 8); }
-#undef DPH_SK_MT
-#undef DPH_SK
-    return;
-  }
   switch (mt) {
     case 1: hipLaunchKernelGGL((skinny_gemm_k<1, SG_UNROLL>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;
     case 2: hipLaunchKernelGGL((skinny_gemm_k<2, SG_UNROLL>), grid, block, 0, st, xb, ldx, wb, ldw, yb, ldy, M, K); break;

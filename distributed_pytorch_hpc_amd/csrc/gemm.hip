@@ -273,7 +273,7 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, 
 }
 
 // ------------------------------------------------------------------------------------------------------------------
-// Staggered variant of gemm_tn_k (DPH_WGRAD_MFMA=33 / gemm_tn_set_mfma(33)).  Waves 4..7 run one barrier behind
+// Staggered variant of gemm_tn_k (gemm_tn_set_mfma(33)).  Waves 4..7 run one barrier behind
 // waves 0..3, so on every SIMD one wave issues its slot's MFMAs while its partner waits at the barrier, issues its
 // DMA pair and transposed reads (the ping-pong of gemm_nt.hip); in lockstep both waves of a SIMD reach the barrier
 // together and the matrix pipe idles while they wait (PMC on the w13 shape: SQ_WAIT_ANY 40 % of wave cycles, MFMA
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_stag_k(const bf16* __restrict_
 // The same pipeline on v_mfma_f32_16x16x32_bf16.  The chip holds a higher clock on the 16x16x32 shape than on
 // 32x32x16 at equal cycles per FLOP (MI355X_MICROARCH.md 'DVFS give-back' item 7, cdna_hip_programming.md rule 28),
 // so the same output tile per wave (128 x 64 = 8 x 4 tiles of 16 x 16, 128 accumulator VGPRs) is built on both and
-// the faster one by wall time on random data is the default (gemm_tn_set_mfma / DPH_WGRAD_MFMA).  Measured on the
+// the faster one by wall time on random data is the default (gemm_tn_set_mfma).  Measured on the
 // Llama-2-7B wgrad shapes (benchmarks/gemm_mfma_ab.py, profiles/gemm_wgrad_mfma16_vs_32.json): 16x16x32 runs
 // 1045-1260 TF vs 1287-1432 TF for 32x32x16 -- twice the MFMA issues and 12 region-address VALU ops per slot
 // (LDS offsets >= 64 KB do not fit the ds_read immediate) outweigh the clock gain here, so 32 stays the default.
@@ -490,195 +490,8 @@ __device__ __forceinline__ bf16x4 tr1(const char* p) {
   return __builtin_bit_cast(bf16x4, v);
 }
 
-template <typename OutT, bool ACCUM>
-__global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                      OutT* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                      int64_t ldb, int64_t ldc, int64_t cstride) {
-  // split-K (gridDim.y > 1): slice blockIdx.y reduces rows [y*K, (y+1)*K) of A / B into its own C slab
-  A += (int64_t)blockIdx.y * K * lda;
-  B += (int64_t)blockIdx.y * K * ldb;
-  C += (int64_t)blockIdx.y * cstride;
-  __shared__ __attribute__((aligned(1024))) char lds[8 * 16384];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid >> 2, wn = wid & 3;                          // 2 x 4 waves
-  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
-
-  // ---- XCD-aware, grouped tile order (as gemm_tn_k) ----
-  const int tiles_m = (M + GBM - 1) / GBM, tiles_n = (N + GBN - 1) / GBN, nwg = tiles_m * tiles_n;
-  int tm, tn;
-  grouped_tile(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * GBM, n0 = tn * GBN;
-
-  // ---- per-lane transposed-read offsets within a region: row 4g + tq, chunk (logical) c -> slot c ^ f(row) ----
-  const int rrow = 4 * g + tq;
-  const int fx = (rrow & 7) << 1;
-  auto slot_off = [&](int c) { return rrow * ROWB + (((c & 16) | ((c & 15) ^ fx)) << 4) + 8 * (tp & 1); };
-  int aoff[8], boff[4];
-#pragma unroll
-  for (int mb = 0; mb < 8; ++mb) aoff[mb] = slot_off(wm * 16 + 2 * mb + (tp >> 1));
-#pragma unroll
-  for (int nb = 0; nb < 4; ++nb) boff[nb] = 8192 + slot_off(wn * 8 + 2 * nb + (tp >> 1));
-
-  // ---- per-lane DMA source offsets: row tid/32 of the region, physical slot tid & 31 ----
-  const int srow = threadIdx.x >> 5, lr = (threadIdx.x >> 4) & 1, sslot = threadIdx.x & 15;
-  const int sch = (lr << 4) | (sslot ^ ((srow & 7) << 1));
-  // edge tiles: a chunk past M / N re-reads the last valid chunk (its columns are never stored)
-  const int colA = min(sch * 8, M - 8 - m0), colB = min(sch * 8, N - 8 - n0);
-  const unsigned voffA = (unsigned)((srow * lda + colA) * 2), voffB = (unsigned)((srow * ldb + colB) * 2);
-  const char* Ag = reinterpret_cast<const char*>(A + m0);        // uniform
-  const char* Bg = reinterpret_cast<const char*>(B + n0);
-  const int64_t stepA = 16 * lda * 2, stepB = 16 * ldb * 2;       // bytes per 16-row region
-  const unsigned lds_wave = __builtin_amdgcn_readfirstlane(
-      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds + (threadIdx.x >> 6) * 1024);
-
-  auto dma_pair = [&](int P, auto RI) {
-    const unsigned d = lds_wave + decltype(RI)::value * 16384;
-    glds16(Ag + P * stepA, voffA, d);
-    glds16(Bg + P * stepB, voffB, d + 8192);
-  };
-
-  // fragment sets: fa[p][mb], fb[p][nb] with p = (region >> 1) & 1; region R fills the low (R even) or high
-  // (R odd) 4 elements of its pair's fragments
-  bf16x8 fa[2][8], fb[2][4];
-  auto read_region = [&](auto RI, auto PI, auto HI) {
-    constexpr int RG = decltype(RI)::value, PS = decltype(PI)::value, HF = decltype(HI)::value;
-    const char* rg = lds + RG * 16384;
-#pragma unroll
-    for (int mb = 0; mb < 8; ++mb) {
-      const bf16x4 v = tr1(rg + aoff[mb]);
-      const bf16x8 w = __builtin_shufflevector(v, v, 0, 1, 2, 3, 0, 1, 2, 3);
-      fa[PS][mb] = HF ? __builtin_shufflevector(fa[PS][mb], w, 0, 1, 2, 3, 12, 13, 14, 15)
-                      : __builtin_shufflevector(fa[PS][mb], w, 8, 9, 10, 11, 4, 5, 6, 7);
-    }
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-      const bf16x4 v = tr1(rg + boff[nb]);
-      const bf16x8 w = __builtin_shufflevector(v, v, 0, 1, 2, 3, 0, 1, 2, 3);
-      fb[PS][nb] = HF ? __builtin_shufflevector(fb[PS][nb], w, 0, 1, 2, 3, 12, 13, 14, 15)
-                      : __builtin_shufflevector(fb[PS][nb], w, 8, 9, 10, 11, 4, 5, 6, 7);
-    }
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // pair set 1 stands for pair -1 (regions -2, -1): the second-half MFMAs of slot 0 multiply zeros
-#pragma unroll
-  for (int mb = 0; mb < 8; ++mb) fa[1][mb] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-  for (int nb = 0; nb < 4; ++nb) fb[1][nb] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-
-  // 16 MFMAs of the pair in set PS: m-blocks [MB0, MB0 + 4) x all 4 n-blocks
-  auto mma_half = [&](auto PI, auto MB0I) {
-    constexpr int PS = decltype(PI)::value, MB0 = decltype(MB0I)::value;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-        acc[MB0 + i][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[PS][MB0 + i], fb[PS][nb], acc[MB0 + i][nb],
-                                                                   0, 0, 0);
-  };
-
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  const int NP = (K / GBK) * 4;   // 16-row regions
-  // prologue: the first tile (regions 0..3), then region 0's halves
-  dma_pair(0, I0{});
-  dma_pair(1, I1{});
-  dma_pair(2, I2{});
-  dma_pair(3, I3{});
-  wait_vm<6>();
-  __builtin_amdgcn_s_barrier();
-  read_region(I0{}, I0{}, I0{});
-
-  // Slot S of a two-tile super-step (region R = P0 + S; P0 % 8 == 0 so R & 3 == S & 3).
-  //   WAIT: vmcnt (-1: none), DMA: issue region R+4, READ: halves of region R+1, MF: 1 = first half of pair
-  //   (R-1, R) (R odd), 2 = second half of pair (R-2, R-1) (R even), 0 = none.
-  auto slot = [&](int P0, auto SI, auto WAITI, auto DMAI, auto READI, auto MFI) {
-    constexpr int S = decltype(SI)::value, WAIT = decltype(WAITI)::value, MF = decltype(MFI)::value;
-    constexpr bool DMA = decltype(DMAI)::value, READ = decltype(READI)::value;
-    if constexpr (WAIT >= 0) {
-      wait_vm<(WAIT >= 0 ? WAIT : 0)>();
-      __builtin_amdgcn_s_barrier();
-    }
-    if constexpr (DMA) dma_pair(P0 + S + 4, std::integral_constant<int, (S + 4) & 7>{});
-    if constexpr (READ)
-      read_region(std::integral_constant<int, (S + 1) & 7>{}, std::integral_constant<int, ((S + 1) >> 1) & 1>{},
-                  std::integral_constant<int, (S + 1) & 1>{});
-    if constexpr (MF == 1) mma_half(std::integral_constant<int, (S >> 1) & 1>{}, I0{});   // pair (S-1, S)
-    if constexpr (MF == 2)                                                                 // pair (S-2, S-1)
-      mma_half(std::integral_constant<int, ((S + 2) >> 1) & 1>{}, std::integral_constant<int, 4>{});
-    if constexpr (READ && MF != 0) {
-#pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  using W4 = std::integral_constant<int, 4>;
-  using W2 = std::integral_constant<int, 2>;
-  using W0 = std::integral_constant<int, 0>;
-  using WN = std::integral_constant<int, -1>;
-  using M0_ = std::integral_constant<int, 0>;
-  using M1_ = std::integral_constant<int, 1>;
-  using M2_ = std::integral_constant<int, 2>;
-#define DPH_S(i) std::integral_constant<int, i>{}
-  int P0 = 0;
-  for (; P0 + 12 <= NP; P0 += 8) {
-    slot(P0, DPH_S(0), W4{}, T_{}, T_{}, M2_{});
-    slot(P0, DPH_S(1), W4{}, T_{}, T_{}, M1_{});
-    slot(P0, DPH_S(2), W4{}, T_{}, T_{}, M2_{});
-    slot(P0, DPH_S(3), W4{}, T_{}, T_{}, M1_{});
-    slot(P0, DPH_S(4), W4{}, T_{}, T_{}, M2_{});
-    slot(P0, DPH_S(5), W4{}, T_{}, T_{}, M1_{});
-    slot(P0, DPH_S(6), W4{}, T_{}, T_{}, M2_{});
-    slot(P0, DPH_S(7), W4{}, T_{}, T_{}, M1_{});
-  }
-  if (NP - P0 == 8) {
-    slot(P0, DPH_S(0), W4{}, T_{}, T_{}, M2_{});
-    slot(P0, DPH_S(1), W4{}, T_{}, T_{}, M1_{});
-    slot(P0, DPH_S(2), W4{}, T_{}, T_{}, M2_{});
-    slot(P0, DPH_S(3), W4{}, T_{}, T_{}, M1_{});
-    slot(P0, DPH_S(4), W4{}, F_{}, T_{}, M2_{});
-    slot(P0, DPH_S(5), W2{}, F_{}, T_{}, M1_{});
-    slot(P0, DPH_S(6), W0{}, F_{}, T_{}, M2_{});
-    slot(P0, DPH_S(7), WN{}, F_{}, F_{}, M1_{});
-    slot(P0, DPH_S(8), WN{}, F_{}, F_{}, M2_{});
-  } else {
-    slot(P0, DPH_S(0), W4{}, F_{}, T_{}, M2_{});
-    slot(P0, DPH_S(1), W2{}, F_{}, T_{}, M1_{});
-    slot(P0, DPH_S(2), W0{}, F_{}, T_{}, M2_{});
-    slot(P0, DPH_S(3), WN{}, F_{}, F_{}, M1_{});
-    slot(P0, DPH_S(4), WN{}, F_{}, F_{}, M2_{});
-  }
-#undef DPH_S
-
-  // ---- epilogue: register i of tile (mb, nb) holds C[row 4 * (lane >> 4) + i][col lane & 15] ----
-#pragma unroll
-  for (int mb = 0; mb < 8; ++mb)
-#pragma unroll
-    for (int nb = 0; nb < 4; ++nb) {
-      const int col = n0 + wn * 64 + nb * 16 + (lane & 15);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = m0 + wm * 128 + mb * 16 + 4 * g + i;
-        if (row >= M || col >= N) continue;
-        OutT* p = C + (int64_t)row * ldc + col;
-        float v = acc[mb][nb][i];
-        if (ACCUM) v += (float)*p;
-        *p = (OutT)v;
-      }
-    }
-}
+// Rejected: a 16x16x32 form of this kernel (32x32x16 and its staggered form were faster in-step,
+// profiles/gemm_wgrad_mfma16_vs_32.json, profiles/r4/wgrad_stagger/).
 
 // fp32 split-K slabs W[S][Mb][Nb] -> C band (+ C when accumulating), in C's dtype.  Fixed summation order.
 template <typename OutT, bool ACCUM>
@@ -700,7 +513,7 @@ __global__ __launch_bounds__(256) void gemm_split_reduce_k(const float* __restri
   }
 }
 
-int g_gemm_tn_mfma = 0;   // 0: not yet resolved from DPH_WGRAD_MFMA
+int g_gemm_tn_mfma = 0;   // 0: the default (kGemmTnDefaultMfma); tests force 32 / 33 through gemm_tn_set_mfma
 int g_gemm_tn_tail = 0;   // tail split: 0 = device CU count, > 0 = that many CUs (tests), < 0 = off
 
 int gemm_tn_cus() {
@@ -717,16 +530,9 @@ int gemm_tn_cus() {
 
 }  // namespace
 
-int gemm_tn_mfma() {
-  if (g_gemm_tn_mfma == 0) {
-    const char* e = getenv("DPH_WGRAD_MFMA");
-    const int v = e ? atoi(e) : 0;
-    g_gemm_tn_mfma = (v == 32 || v == 16 || v == 33) ? v : kGemmTnDefaultMfma;
-  }
-  return g_gemm_tn_mfma;
-}
+int gemm_tn_mfma() { return g_gemm_tn_mfma ? g_gemm_tn_mfma : kGemmTnDefaultMfma; }
 
-void gemm_tn_set_mfma(int shape) { g_gemm_tn_mfma = (shape == 16 || shape == 32 || shape == 33) ? shape : 0; }
+void gemm_tn_set_mfma(int shape) { g_gemm_tn_mfma = (shape == 32 || shape == 33) ? shape : 0; }
 
 void gemm_tn_set_tail(int cus) { g_gemm_tn_tail = cus; }
 
@@ -741,11 +547,7 @@ bool gemm_tn_supported(int64_t M, int64_t N, int64_t K) {
 // the band then costs ceil(band * S / CU) / S waves instead of ceil(band / CU).
 GemmTnPlan gemm_tn_plan(int64_t M, int64_t N, int64_t K) {
   GemmTnPlan pl{};
-  static const bool env_off = [] {   // DPH_WGRAD_TAIL=0: no tail split (A/B runs)
-    const char* e = getenv("DPH_WGRAD_TAIL");
-    return e && atoi(e) == 0;
-  }();
-  if (g_gemm_tn_tail < 0 || (env_off && g_gemm_tn_tail == 0) || gemm_tn_mfma() == 16) return pl;
+  if (g_gemm_tn_tail < 0) return pl;
   if (M % GBM || N % GBN) return pl;   // ragged edge tiles: one launch
   const int cus = gemm_tn_cus();
   const int64_t tm = M / GBM, tn = N / GBN, T = tm * tn;
@@ -785,11 +587,7 @@ GemmTnPlan gemm_tn_plan(int64_t M, int64_t N, int64_t K) {
 void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
              int64_t ldc, int out_dtype, bool accumulate, hipStream_t st, const GemmTnPlan* plan,
              float* workspace) {
-  const bool m16 = gemm_tn_mfma() == 16, stag = gemm_tn_mfma() == 33;
-  static const bool lds_epi = [] {   // DPH_WGRAD_EPI=scalar: per-element epilogue stores (A/B runs)
-    const char* e = getenv("DPH_WGRAD_EPI");
-    return !(e && e[0] == 's');
-  }();
+  const bool stag = gemm_tn_mfma() == 33;
   const size_t lds = 0;   // static: 8 x 16 KB regions
   const dim3 block(GNT);
   auto launch = [&](const bf16* a, const bf16* b, void* c, int64_t m, int64_t n, int64_t k, int64_t ldc_, int S,
@@ -801,13 +599,10 @@ void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_
     const bool vec_c = ((uintptr_t)c & 15) == 0 && ((ldc_ * esz_c) & 15) == 0;
 #define DPH_GEMM_LAUNCH(T, ACC)                                                                                \
   do {                                                                                                         \
-    if (m16)                                                                                                   \
-      hipLaunchKernelGGL((gemm_tn16_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,     \
-                         lda, ldb, ldc_, cstride);                                                             \
-    else if (stag && (ACC || (lds_epi && vec_c)))                                                              \
+    if (stag && (ACC || vec_c))                                                                                \
       hipLaunchKernelGGL((gemm_tn_stag_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,  \
                          lda, ldb, ldc_, cstride);                                                             \
-    else if (!lds_epi || !vec_c)                                                                               \
+    else if (!vec_c)                                                                                           \
       hipLaunchKernelGGL((gemm_tn_k<T, ACC, false>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,  \
                          lda, ldb, ldc_, cstride);                                                             \
     else                                                                                                       \

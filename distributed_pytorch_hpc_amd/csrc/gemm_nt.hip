@@ -472,317 +472,10 @@ __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
   }
 }
 
-// ------------------------------------------------------------------------------------------------------------------
-// The same pipeline on v_mfma_f32_32x32x16_bf16 (gemm_nt32_k), plus ragged edges.
-//
-// Same LDS images, DMA schedule, phases, stagger and vmcnt counts as gemm_nt_k -- only the fragment shape changes.
-// A quadrant of the wave tile is 2 token blocks x 1 feature block of 32, so a phase is 8 MFMAs of 32x32x16 (K = 64 as
-// 4 k-steps of 16) instead of 16 of 16x16x32: the same FLOP, LDS bytes and ds_read_b128 count (lane l reads row l & 31,
-// logical chunk 2 s + (l >> 5) of k-step s; the row-pair XOR swizzle keeps every 16-lane group conflict-free), half the
-// MFMA issues.  The weights stay the MFMA A operand, so a lane's 16 accumulators of a 32 x 32 tile are 4 runs of 4
-// CONSECUTIVE features ((i & 3) + 8 (i >> 2) + 4 (l >> 5)) of one token (l & 31): RoPE pairs remain lane-local.  The
-// wgrad kernel measured 32x32x16 13-23 % faster than 16x16x32 at an equal wave tile (profiles/gemm_wgrad_mfma16_vs_32.json).
-//
-// RAG (ragged edges, the tensor-parallel shards of Llama-2-7B: w13 2752 / 5504 rows, SwiGLU H = 1376 / 2752, w2's
-// K = 1376, the vocab-sharded head 4000 / 8000): N (H for SWIGLU) % 8 and K % 8 instead of % 256 (% 128) and % 64.
-//   * weight rows past the edge are clamped to the last valid row at DMA-offset setup (finite data, never stored);
-//   * the last K-tile's 16-B chunks past K are range-checked buffer_load ... lds with an out-of-range offset, which
-//     write zeros to LDS (both operands: no garbage, no read past an allocation);
-//   * the epilogue stores only columns < N (whole 8-column segments, N % 8 == 0).
-template <int MODE, int LOOK, bool RAG>
-__global__ __launch_bounds__(NNT, 1) void gemm_nt32_k(GemmNtParams p) {
-  constexpr int VMC = LOOK ? 6 : 8;
-  __shared__ __attribute__((aligned(1024))) char lds[2 * BUFB];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
-  const int r32 = lane & 31, hk = lane >> 5;
-
-  const int tiles_m = p.M / NBM, tiles_n = p.tiles_n;
-  int tm, tn;
-  nt_grouped_tile(xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * NBM;
-  int64_t nbase0, nbase1;
-  if constexpr (MODE == kNtSwiglu) {
-    nbase0 = (int64_t)tn * 128;
-    nbase1 = (int64_t)p.H + (int64_t)tn * 128;
-  } else {
-    nbase0 = (int64_t)tn * NBN;
-    nbase1 = nbase0 + 32;
-  }
-  const int nk = (p.K + NBK - 1) / NBK;
-
-  // ---- per-lane LDS-DMA source offsets (bytes from the quarter's base pointer at k-tile 0) ----
-  // RAG: the weight quarters use the operand's base and absolute (clamped) rows; vtail = the last K-tile's offsets
-  // with chunks past K replaced by the out-of-range sentinel.
-  unsigned voff[4][2], vtail[4][2];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = i * NNT + tid, rho = c >> 3, kc = (c & 7) ^ ((rho >> 1) & 7);
-      int64_t row;
-      if (q < 2) row = 128 * (rho >> 6) + (rho & 63);
-      else if (MODE == kNtSwiglu) row = rho;
-      else row = 64 * (rho >> 5) + (rho & 31);
-      if constexpr (RAG) {
-        if (q >= 2) {
-          const int64_t nb = q == Q_B0 ? nbase0 : nbase1;
-          int64_t lim;
-          if constexpr (MODE == kNtSwiglu) lim = q == Q_B0 ? p.H : 2 * (int64_t)p.H;
-          else lim = p.N;
-          row = min(nb + row, lim - 1);
-        }
-      }
-      const int64_t ld = q < 2 ? p.lda : p.ldb;
-      voff[q][i] = (unsigned)(row * ld * 2 + kc * 16);
-      vtail[q][i] = ((nk - 1) * NBK + kc * 8 < p.K) ? voff[q][i] : 0x80000000u;
-    }
-  const char* qptr[4];
-  const bf16* Ap = reinterpret_cast<const bf16*>(p.A);
-  const bf16* Bp = reinterpret_cast<const bf16*>(p.B);
-  qptr[Q_A0] = reinterpret_cast<const char*>(Ap + (int64_t)m0 * p.lda);
-  qptr[Q_A1] = reinterpret_cast<const char*>(Ap + (int64_t)(m0 + 64) * p.lda);
-  qptr[Q_B0] = reinterpret_cast<const char*>(RAG ? Bp : Bp + nbase0 * p.ldb);
-  qptr[Q_B1] = reinterpret_cast<const char*>(RAG ? Bp : Bp + nbase1 * p.ldb);
-  const unsigned lds_w = lds_addr(lds + wid * 1024);
-  const bool ktail = RAG && (p.K % NBK) != 0;
-
-  auto dma = [&](auto QI, int kt, auto BI) {
-    constexpr int Q = decltype(QI)::value, BUF = decltype(BI)::value;
-    const int ktc = min(kt, nk - 1);   // past the end: re-load the last tile into a slot nobody reads again
-    const char* src = qptr[Q] + (int64_t)ktc * (NBK * 2);
-    const unsigned d = lds_w + BUF * BUFB + Q * QB;
-    if (RAG && ktail && ktc == nk - 1) {   // wave-uniform: the partial last K-tile, zero-filled past K
-      const dph_rsrc rs = make_rsrc(src, 0x7fffffffu);
-      lds_dma16_buf(rs, vtail[Q][0], d);
-      lds_dma16_buf(rs, vtail[Q][1], d + NNT * 16);
-    } else {
-      lds_dma16(src, voff[Q][0], d);
-      lds_dma16(src, voff[Q][1], d + NNT * 16);
-    }
-  };
-
-  // ---- per-lane fragment read offsets: row r32 of a 32-row block, logical chunk 2 s + hk of k-step s ----
-  const int xsw = (r32 >> 1) & 7;
-  int offk[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) offk[s] = r32 * 128 + (((2 * s + hk) ^ xsw) << 4);
-  const char* a_img = lds + wm * 8192;    // + Q * QB + buf * BUFB, + mb * 4096
-  const char* b_img = lds + wn * 4096;    // + Q * QB + buf * BUFB
-
-  bf16x8 fa[2][4], fb0[4], fb1[4];
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-  auto read_a = [&](auto QI, auto BI) {
-    constexpr int Q = decltype(QI)::value, BUF = decltype(BI)::value;
-    const char* base = a_img + BUF * BUFB + Q * QB;
-#pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) fa[mb][s] = *reinterpret_cast<const bf16x8*>(base + mb * 4096 + offk[s]);
-  };
-  auto read_b = [&](auto QI, auto BI, bf16x8 (&fb)[4]) {
-    constexpr int Q = decltype(QI)::value, BUF = decltype(BI)::value;
-    const char* base = b_img + BUF * BUFB + Q * QB;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) fb[s] = *reinterpret_cast<const bf16x8*>(base + offk[s]);
-  };
-  // quadrant (a-half AH, b-half BH): 2 token blocks x 1 feature block x 4 k-steps of 16
-  auto mma = [&](auto AHI, auto BHI, const bf16x8 (&fb)[4]) {
-    constexpr int AH = decltype(AHI)::value, BH = decltype(BHI)::value;
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int mb = 0; mb < 2; ++mb)
-        acc[2 * AH + mb][BH] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s], fa[mb][s], acc[2 * AH + mb][BH], 0, 0, 0);
-  };
-
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using IA0 = std::integral_constant<int, Q_A0>;
-  using IA1 = std::integral_constant<int, Q_A1>;
-  using IB0 = std::integral_constant<int, Q_B0>;
-  using IB1 = std::integral_constant<int, Q_B1>;
-
-  // one phase, exactly gemm_nt_k's (reads -> one quarter of DMA -> vmcnt -> barrier -> 8 MFMAs -> barrier)
-  auto phase = [&](auto PI, auto CI, int kt) {
-    constexpr int P = decltype(PI)::value, CUR = decltype(CI)::value;
-    using ICUR = std::integral_constant<int, CUR>;
-    using INXT = std::integral_constant<int, CUR ^ 1>;
-    constexpr bool SW = LOOK && CUR == 1;
-    auto& fB0 = SW ? fb1 : fb0;
-    auto& fB1 = SW ? fb0 : fb1;
-    if constexpr (P == 0) {
-      if constexpr (!LOOK) read_b(IB0{}, ICUR{}, fB0);
-      read_a(IA0{}, ICUR{});
-    }
-    if constexpr (P == 1) read_b(IB1{}, ICUR{}, fB1);
-    if constexpr (P == 2) read_a(IA1{}, ICUR{});
-    if constexpr (P == 0) dma(IB1{}, kt + 1, INXT{});
-    if constexpr (P == 1) dma(IA1{}, kt + 1, INXT{});
-    if constexpr (P == 2) dma(IA0{}, kt + 2, ICUR{});
-    if constexpr (P == 3) dma(IB0{}, kt + 2, ICUR{});
-    wait_vmcnt<VMC>();
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-    if constexpr (P == 0) mma(I0{}, I0{}, fB0);
-    if constexpr (P == 1) mma(I0{}, I1{}, fB1);
-    if constexpr (P == 2) mma(I1{}, I1{}, fB1);
-    if constexpr (P == 3) {
-      mma(I1{}, I0{}, fB0);
-      if constexpr (LOOK) {   // next tile's B0 (retired by phase 3's wait) into the idle set, between the MFMAs
-        read_b(IB0{}, INXT{}, fB1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // 2 MFMAs
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 DS read
-        }
-      }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  dma(IA0{}, 0, I0{});
-  dma(IB0{}, 0, I0{});
-  dma(IB1{}, 0, I0{});
-  dma(IA1{}, 0, I0{});
-  dma(IA0{}, 1, I1{});
-  dma(IB0{}, 1, I1{});
-  wait_vmcnt<8>();
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  if constexpr (LOOK) read_b(IB0{}, I0{}, fb0);
-  const bool late = __builtin_amdgcn_readfirstlane(wid) >= 4;
-  if (late) __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-
-  int kt = 0;
-  for (; kt + 2 <= nk; kt += 2) {
-    phase(I0{}, I0{}, kt);
-    phase(I1{}, I0{}, kt);
-    phase(std::integral_constant<int, 2>{}, I0{}, kt);
-    phase(std::integral_constant<int, 3>{}, I0{}, kt);
-    phase(I0{}, I1{}, kt + 1);
-    phase(I1{}, I1{}, kt + 1);
-    phase(std::integral_constant<int, 2>{}, I1{}, kt + 1);
-    phase(std::integral_constant<int, 3>{}, I1{}, kt + 1);
-  }
-  if (kt < nk) {
-    phase(I0{}, I0{}, kt);
-    phase(I1{}, I0{}, kt);
-    phase(std::integral_constant<int, 2>{}, I0{}, kt);
-    phase(std::integral_constant<int, 3>{}, I0{}, kt);
-  }
-  if (!late) __builtin_amdgcn_s_barrier();
-  wait_vmcnt<0>();
-
-  // ---- epilogue through LDS: acc[mt][nb][i] = C[token 128 wm + 32 mt + r32][feature row (i&3) + 8 (i>>2) + 4 hk of
-  // feature block nb]; rounded to bf16 into a 256 x 256 image (16-B chunks XOR-swizzled by row & 15) ----
-  __syncthreads();
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int row = 128 * wm + 32 * mt + r32;
-        const int f = 8 * g + 4 * hk;                       // feature offset within the 32-block
-        // image column: SWIGLU gate units | up units at 0..127 | 128..255; else the tile's feature column
-        const int col = MODE == kNtSwiglu ? nb * 128 + 32 * wn + f : 64 * wn + 32 * nb + f;
-        f32x4 v = {acc[mt][nb][4 * g], acc[mt][nb][4 * g + 1], acc[mt][nb][4 * g + 2], acc[mt][nb][4 * g + 3]};
-        if constexpr (MODE == kNtRope) {
-          const int n = tn * NBN + col;
-          if (n < p.n_rot) {
-            const int64_t t = (int64_t)m0 + row;
-            const int pos = (int)(t % p.S) + p.pos_off, i0 = (n % p.hd) >> 1;
-            const float* ct = p.rope_cos + (int64_t)pos * (p.hd >> 1) + i0;
-            const float* st = p.rope_sin + (int64_t)pos * (p.hd >> 1) + i0;
-            const float c0 = ct[0], c1 = ct[1], s0 = st[0], s1 = st[1];
-            const float a0 = v[0], b0 = v[1], a1 = v[2], b1 = v[3];
-            v[0] = a0 * c0 - b0 * s0;
-            v[1] = a0 * s0 + b0 * c0;
-            v[2] = a1 * c1 - b1 * s1;
-            v[3] = a1 * s1 + b1 * c1;
-          }
-        }
-        bf16x4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
-        *reinterpret_cast<bf16x4*>(lds + row * 512 + (((col >> 3) ^ (row & 15)) << 4) + (col & 7) * 2) = o;
-      }
-  __syncthreads();
-  if constexpr (MODE == kNtSwiglu) {
-    const int c = tid & 15;                       // gate chunk c (units 8c ..) and its up chunk 16 + c
-    const int64_t u0 = (int64_t)tn * 128 + c * 8;
-    if (RAG && u0 >= p.H) return;                 // whole 8-unit segment past H (H % 8 == 0)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int row = (tid >> 4) + 32 * k;
-      const bf16x8 g = *reinterpret_cast<const bf16x8*>(lds + row * 512 + ((c ^ (row & 15)) << 4));
-      const bf16x8 up = *reinterpret_cast<const bf16x8*>(lds + row * 512 + (((16 + c) ^ (row & 15)) << 4));
-      bf16x8 hv;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float gf = (float)g[j];
-        hv[j] = (bf16)(gf * nt_sigmoid(gf) * (float)up[j]);
-      }
-      const int64_t t = (int64_t)m0 + row;
-      *reinterpret_cast<bf16x8*>((bf16*)p.C + t * p.ldc + u0) = g;
-      *reinterpret_cast<bf16x8*>((bf16*)p.C + t * p.ldc + p.H + u0) = up;
-      *reinterpret_cast<bf16x8*>((bf16*)p.C2 + t * p.ldc2 + u0) = hv;
-    }
-  } else {
-    const int c = tid & 31;
-    const int64_t n0c = (int64_t)tn * NBN + c * 8;
-    if (RAG && n0c >= p.N) return;
-    constexpr int BATCH = 4;
-#pragma unroll
-    for (int k0 = 0; k0 < 16; k0 += BATCH) {
-      bf16x8 dh[BATCH], gv[BATCH], uv[BATCH];
-#pragma unroll
-      for (int k = 0; k < BATCH; ++k) {
-        const int row = (tid >> 5) + 16 * (k0 + k);
-        dh[k] = *reinterpret_cast<const bf16x8*>(lds + row * 512 + ((c ^ (row & 15)) << 4));
-        if constexpr (MODE == kNtDswiglu) {
-          const int64_t t = (int64_t)m0 + row;
-          gv[k] = *reinterpret_cast<const bf16x8*>((const bf16*)p.X + t * p.ldx + n0c);
-          uv[k] = *reinterpret_cast<const bf16x8*>((const bf16*)p.X + t * p.ldx + p.H + n0c);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < BATCH; ++k) {
-        const int64_t t = (int64_t)m0 + (tid >> 5) + 16 * (k0 + k);
-        bf16* out = (bf16*)p.C + t * p.ldc + n0c;
-        if constexpr (MODE == kNtDswiglu) {
-          bf16x8 dg, du;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float d = (float)dh[k][j];
-            const float g = (float)gv[k][j], u = (float)uv[k][j];
-            const float sg = nt_sigmoid(g);
-            du[j] = (bf16)(d * (g * sg));
-            dg[j] = (bf16)(d * u * sg * (1.f + g * (1.f - sg)));
-          }
-          *reinterpret_cast<bf16x8*>(out) = dg;
-          *reinterpret_cast<bf16x8*>(out + p.H) = du;
-        } else {
-          *reinterpret_cast<bf16x8*>(out) = dh[k];
-        }
-      }
-    }
-  }
-}
+// Rejected variants (code removed; evidence kept): the same pipeline on v_mfma_f32_32x32x16_bf16 (0.86-0.96x this
+// kernel, profiles/r4/nt_mfma32/; at the 1400 W package limit it delivers 0.98-1.00 TFLOP/J against 1.06-1.09 here
+// and 1.10-1.14 for hipBLASLt, profiles/r5/gemm_power/), the two-phase form without the B0 look-ahead (LOOK = 0,
+// profiles/r3/rejected/gemm_nt_2phase_*) and the register epilogue (bitwise equal, slower: profiles/r3/ab_fused_mlp_fwd_lds/).
 
 }  // namespace
 
@@ -796,88 +489,21 @@ bool gemm_nt_ragged(int mode, int64_t N, int64_t K) {
   return K % NBK != 0 || (mode == kNtSwiglu ? N % 128 : N % NBN) != 0;
 }
 
-namespace {
-int g_nt_variant = -1;   // -1: unresolved (env DPH_GEMM_NT_VARIANT, default kGemmNtDefaultVariant)
-}
-
-int gemm_nt_variant() {
-  if (g_nt_variant < 0) {
-    const char* e = getenv("DPH_GEMM_NT_VARIANT");
-    g_nt_variant = e ? (atoi(e) & 3) : kGemmNtDefaultVariant;
-  }
-  return g_nt_variant;
-}
-
-void gemm_nt_set_variant(int v) { g_nt_variant = v < 0 ? -1 : (v & 3); }
-
 void gemm_nt(int mode, const GemmNtParams& prm, hipStream_t st) {
   GemmNtParams p = prm;
   p.tiles_n = mode == kNtSwiglu ? (p.N + 127) / 128 : (p.N + NBN - 1) / NBN;
   const dim3 grid((unsigned)((p.M / NBM) * p.tiles_n)), block(NNT);
-  const int var = gemm_nt_variant();
-  const bool look = (var & 1) != 0;
   const bool rag = gemm_nt_ragged(mode, p.N, p.K);
-  if (rag && !(var & 2)) {   // ragged shapes on the 16x16x32 kernel's edge tiles (LDS epilogue)
-#define DPH_NT16R(MD)                                                                             \
-  do {                                                                                            \
-    if (look) hipLaunchKernelGGL((gemm_nt_k<MD, 1, true, true>), grid, block, 0, st, p);         \
-    else hipLaunchKernelGGL((gemm_nt_k<MD, 0, true, true>), grid, block, 0, st, p);              \
-  } while (0)
-    switch (mode) {
-      case kNtSwiglu: DPH_NT16R(kNtSwiglu); break;
-      case kNtDswiglu: DPH_NT16R(kNtDswiglu); break;
-      case kNtRope: DPH_NT16R(kNtRope); break;
-      default: DPH_NT16R(kNtStore); break;
-    }
-#undef DPH_NT16R
-    return;
-  }
-  if (var & 2) {   // 32x32x16 kernel
-#define DPH_NT32(MD)                                                                                      \
-  do {                                                                                                    \
-    if (rag) {                                                                                            \
-      if (look) hipLaunchKernelGGL((gemm_nt32_k<MD, 1, true>), grid, block, 0, st, p);                   \
-      else hipLaunchKernelGGL((gemm_nt32_k<MD, 0, true>), grid, block, 0, st, p);                        \
-    } else {                                                                                              \
-      if (look) hipLaunchKernelGGL((gemm_nt32_k<MD, 1, false>), grid, block, 0, st, p);                  \
-      else hipLaunchKernelGGL((gemm_nt32_k<MD, 0, false>), grid, block, 0, st, p);                       \
-    }                                                                                                     \
-  } while (0)
-    switch (mode) {
-      case kNtSwiglu: DPH_NT32(kNtSwiglu); break;
-      case kNtDswiglu: DPH_NT32(kNtDswiglu); break;
-      case kNtRope: DPH_NT32(kNtRope); break;
-      default: DPH_NT32(kNtStore); break;
-    }
-#undef DPH_NT32
-    return;
-  }
-  static const bool lepi = [] {   // DPH_NT_EPI=reg: the register epilogue for every mode (A/B runs)
-    const char* e = getenv("DPH_NT_EPI");
-    return !(e && e[0] == 'r');
-  }();
-#define DPH_NT_LAUNCH(MD, LE)                                                                 \
-  do {                                                                                        \
-    if (look) hipLaunchKernelGGL((gemm_nt_k<MD, 1, LE>), grid, block, 0, st, p);             \
-    else hipLaunchKernelGGL((gemm_nt_k<MD, 0, LE>), grid, block, 0, st, p);                  \
+#define DPH_NT_LAUNCH(MD)                                                                    \
+  do {                                                                                       \
+    if (rag) hipLaunchKernelGGL((gemm_nt_k<MD, 1, true, true>), grid, block, 0, st, p);      \
+    else hipLaunchKernelGGL((gemm_nt_k<MD, 1, true>), grid, block, 0, st, p);                \
   } while (0)
   switch (mode) {
-    case kNtSwiglu:
-      if (lepi) DPH_NT_LAUNCH(kNtSwiglu, true);
-      else DPH_NT_LAUNCH(kNtSwiglu, false);
-      break;
-    case kNtDswiglu:
-      if (lepi) DPH_NT_LAUNCH(kNtDswiglu, true);
-      else DPH_NT_LAUNCH(kNtDswiglu, false);
-      break;
-    case kNtRope:
-      if (lepi) DPH_NT_LAUNCH(kNtRope, true);
-      else DPH_NT_LAUNCH(kNtRope, false);
-      break;
-    default:
-      if (lepi) DPH_NT_LAUNCH(kNtStore, true);
-      else DPH_NT_LAUNCH(kNtStore, false);
-      break;
+    case kNtSwiglu: DPH_NT_LAUNCH(kNtSwiglu); break;
+    case kNtDswiglu: DPH_NT_LAUNCH(kNtDswiglu); break;
+    case kNtRope: DPH_NT_LAUNCH(kNtRope); break;
+    default: DPH_NT_LAUNCH(kNtStore); break;
   }
 #undef DPH_NT_LAUNCH
 }

@@ -106,7 +106,7 @@ void embedding_bwd(const int64_t* sorted_ids, const int64_t* perm, const void* d
 // ---- cast / scale helpers ----
 // C[M, N] (+)= A^T B, A [K, M] / B [K, N] bf16 row-major (weight gradient); C bf16 or fp32.
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K);
-// MFMA shape of the wgrad kernel: 16 (v_mfma_f32_16x16x32_bf16) or 32 (v_mfma_f32_32x32x16_bf16); env DPH_WGRAD_MFMA
+// Pipeline of the wgrad kernel (v_mfma_f32_32x32x16_bf16): 32 = gemm_tn_k, 33 = its staggered form (tests force one)
 constexpr int kGemmTnDefaultMfma = 33;   // 33 = gemm_tn_stag_k (staggered 32x32x16), +1-2 % isolated, +0.5 % in-step (profiles/r4/wgrad_stagger)
 int gemm_tn_mfma();
 void gemm_tn_set_mfma(int shape);
@@ -146,9 +146,6 @@ bool gemm_nt_ragged(int mode, int64_t N, int64_t K);
 void gemm_nt(int mode, const GemmNtParams& p, hipStream_t stream);
 // pipeline variant: bit 0 = lookahead B0 reads (8/4/8/0 fragment reads per phase instead of 12/4/8/0), bit 1 = the
 // v_mfma_f32_32x32x16_bf16 kernel (gemm_nt32_k) instead of 16x16x32 (gemm_nt_k); both take ragged shapes.
-constexpr int kGemmNtDefaultVariant = 1;   // 0.92-1.02x hipBLASLt vs 0.91-1.00x for 0 (profiles/r3/rejected/gemm_nt_2phase_*)
-int gemm_nt_variant();
-void gemm_nt_set_variant(int v);
 
 // 1x1 convolution on channels-last activations as tall-skinny GEMMs (csrc/conv1x1.hip).  bf16 operands.
 // ts_gemm_nt: C[M, N] = A[M, K] B[N, K]^T (N, K % 64 == 0).  ts_gemm_tn: C[N, K] (+)= A[M, N]^T B[M, K] through

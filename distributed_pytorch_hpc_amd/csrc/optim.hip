@@ -41,42 +41,9 @@ __device__ __forceinline__ void store4<bf16>(bf16* p, const float (&o)[4]) {
   *reinterpret_cast<bf16x4*>(p) = v;
 }
 
-// NT (DPH_ADAMW_VAR=1): every stream is touched once per step, so loads and stores carry the non-temporal hint (no
-// L2 / Infinity-Cache allocation for data that will not be re-read before it is evicted).  Measured slower: 4 257 /
-// 4 270 vs 4 352 / 4 334 GB/s at 2^28 parameters, 7B 28 330 / 28 282 vs 28 367 / 28 323 tokens/s, bitwise equal
-// results (profiles/r4/rejected_adamw_nt/) -- kept off.
-typedef unsigned u32x2_nt __attribute__((ext_vector_type(2)));
-template <typename T>
-__device__ __forceinline__ T ld_nt(const T* p) { return __builtin_nontemporal_load(p); }
-template <typename T>
-__device__ __forceinline__ void st_nt(T v, T* p) { __builtin_nontemporal_store(v, p); }
-
-template <typename G, bool NT>
-__device__ __forceinline__ void load4g(const G* p, float (&o)[4]) {
-  if constexpr (!NT) {
-    load4<G>(p, o);
-  } else if constexpr (sizeof(G) == 4) {
-    const f32x4 v = ld_nt(reinterpret_cast<const f32x4*>(p));
-    o[0] = v[0]; o[1] = v[1]; o[2] = v[2]; o[3] = v[3];
-  } else {
-    const u32x2_nt u = ld_nt(reinterpret_cast<const u32x2_nt*>(p));
-    const bf16x4 v = __builtin_bit_cast(bf16x4, u);
-    o[0] = (float)v[0]; o[1] = (float)v[1]; o[2] = (float)v[2]; o[3] = (float)v[3];
-  }
-}
-template <typename T, bool NT>
-__device__ __forceinline__ void store4g(T* p, const float (&o)[4]) {
-  if constexpr (!NT) {
-    store4<T>(p, o);
-  } else if constexpr (sizeof(T) == 4) {
-    st_nt(f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<f32x4*>(p));
-  } else {
-    const bf16x4 v = {(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]};
-    st_nt(__builtin_bit_cast(u32x2_nt, v), reinterpret_cast<u32x2_nt*>(p));
-  }
-}
-
-template <typename G, typename P, bool HAS_OUT, bool NT = false>
+// Rejected: non-temporal loads / stores on the five streams (4 257 / 4 270 vs 4 352 / 4 334 GB/s at 2^28 parameters,
+// 7B 28 330 / 28 282 vs 28 367 / 28 323 tokens/s; profiles/r4/rejected_adamw_nt/).
+template <typename G, typename P, bool HAS_OUT>
 __global__ __launch_bounds__(256) void adamw_k(float* __restrict__ master, float* __restrict__ m,
                                                float* __restrict__ v, const G* __restrict__ grad,
                                                P* __restrict__ pout, int64_t n, float lr, float b1, float b2,
@@ -94,10 +61,10 @@ __global__ __launch_bounds__(256) void adamw_k(float* __restrict__ master, float
   const int64_t n4 = n >> 2;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     float p[4], mm[4], vv[4], g[4];
-    load4g<float, NT>(master + i * 4, p);
-    load4g<float, NT>(m + i * 4, mm);
-    load4g<float, NT>(v + i * 4, vv);
-    load4g<G, NT>(grad + i * 4, g);
+    load4<float>(master + i * 4, p);
+    load4<float>(m + i * 4, mm);
+    load4<float>(v + i * 4, vv);
+    load4<G>(grad + i * 4, g);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float gk = g[k] * gs;
@@ -107,10 +74,10 @@ __global__ __launch_bounds__(256) void adamw_k(float* __restrict__ master, float
       const float denom = sqrtf(vv[k]) * inv_bc2_sqrt + eps;
       p[k] = p[k] - step_size * mm[k] / denom;
     }
-    store4g<float, NT>(master + i * 4, p);
-    store4g<float, NT>(m + i * 4, mm);
-    store4g<float, NT>(v + i * 4, vv);
-    if (HAS_OUT) store4g<P, NT>(pout + i * 4, p);
+    store4<float>(master + i * 4, p);
+    store4<float>(m + i * 4, mm);
+    store4<float>(v + i * 4, vv);
+    if (HAS_OUT) store4<P>(pout + i * 4, p);
   }
   // tail (n % 4)
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
@@ -175,19 +142,9 @@ void adamw_step(float* master, float* m, float* v, const void* grad, void* param
                 const float* hyper, int grad_dtype, int param_dtype, hipStream_t stream) {
   if (n == 0) return;
   const int grid = stream_grid((n + 3) / 4, 256);
-  static const bool nt = [] {
-    const char* e = getenv("DPH_ADAMW_VAR");
-    return e && e[0] == '1';
-  }();
 #define AD(G, P, OUT)                                                                                              \
-  do {                                                                                                             \
-    if (nt)                                                                                                        \
-      hipLaunchKernelGGL((adamw_k<G, P, OUT, true>), dim3(grid), dim3(256), 0, stream, master, m, v, (const G*)grad, \
-                         (P*)param_out, n, lr, beta1, beta2, eps, wd, bc1, bc2, gscale, hyper);                    \
-    else                                                                                                           \
-      hipLaunchKernelGGL((adamw_k<G, P, OUT>), dim3(grid), dim3(256), 0, stream, master, m, v, (const G*)grad,    \
-                         (P*)param_out, n, lr, beta1, beta2, eps, wd, bc1, bc2, gscale, hyper);                    \
-  } while (0)
+  hipLaunchKernelGGL((adamw_k<G, P, OUT>), dim3(grid), dim3(256), 0, stream, master, m, v, (const G*)grad,        \
+                     (P*)param_out, n, lr, beta1, beta2, eps, wd, bc1, bc2, gscale, hyper)
   if (grad_dtype == kBF16) {
     if (!param_out) AD(bf16, bf16, false);
     else if (param_dtype == kBF16) AD(bf16, bf16, true);

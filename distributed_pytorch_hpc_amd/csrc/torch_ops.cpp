@@ -874,7 +874,7 @@ void convg_tn_(Tensor C, const Tensor& A, const Tensor& B, at::IntArrayRef geo, 
                       B.stride(0), ns, dt_code(C), accumulate, g, cur_stream(), chunk_taps);
 }
 
-// Select the wgrad kernel's MFMA shape (16 or 32; anything else re-reads DPH_WGRAD_MFMA); returns the active shape.
+// Select the wgrad kernel's MFMA form (32 = 32x32x16, 33 = its staggered form; -1 = query only); returns the active one.
 int64_t gemm_tn_mfma_(int64_t shape) {
   if (shape != -1) dph::gemm_tn_set_mfma((int)shape);
   return dph::gemm_tn_mfma();
@@ -1277,10 +1277,6 @@ std::vector<int64_t> out_sizes(const Tensor& x, int64_t n) {
 }  // namespace
 
 // select the gemm_nt pipeline variant (v < 0: back to the env / default); returns the active one
-int64_t gemm_nt_variant_(int64_t v) {
-  dph::gemm_nt_set_variant((int)v);
-  return dph::gemm_nt_variant();
-}
 
 // C = A B^T (A [..., K], B [N, K]) -> [..., N]
 Tensor gemm_nt(const Tensor& A, const Tensor& B) {
@@ -1467,7 +1463,6 @@ TORCH_LIBRARY(dph, m) {
   m.def("embedding_bwd(Tensor ids, Tensor dout, int vocab_local, int vocab_start) -> Tensor");
   m.def("gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate) -> ()");
   m.def("gemm_nt(Tensor A, Tensor B) -> Tensor");
-  m.def("gemm_nt_variant_(int v) -> int", &gemm_nt_variant_);   // no tensor argument: catch-all kernel
   m.def("gemm_nt_swiglu(Tensor x, Tensor w13) -> (Tensor, Tensor)");
   m.def("gemm_nt_swiglu_into(Tensor x, Tensor w13, Tensor(a!) x13_out, Tensor(b!) h_out) -> ()");
   m.def("gemm_nt_dswiglu_into(Tensor dy, Tensor w2t, Tensor x13, Tensor(a!) d13_out) -> ()");

@@ -21,9 +21,6 @@ from ..ops.pool import MaxPool2d
 from ..ops.upsample import up_concat
 
 
-_CONV_STATS = os.environ.get("DPH_UNET_CONV_STATS", "1") != "0"   # A/B knob: BN statistics from the conv epilogue
-
-
 class ConvBlock(nn.Sequential):
     """conv -> BN -> ReLU twice, as the reference's ``conv_block``; BN + ReLU run as one fused channels-last op
     (BatchNormAct2d, a BatchNorm2d subclass: same state-dict keys; the ReLU slots stay as Identity so the indices are
@@ -32,7 +29,7 @@ class ConvBlock(nn.Sequential):
 
     def forward(self, x):
         for conv, bn in ((self[0], self[1]), (self[3], self[4])):
-            if isinstance(conv, BiasConv2d) and isinstance(bn, BatchNormAct2d) and bn.training and _CONV_STATS:
+            if isinstance(conv, BiasConv2d) and isinstance(bn, BatchNormAct2d) and bn.training:
                 slot = StatsSlot()
                 x = bn(conv(x, stats_slot=slot), stats_slot=slot)
             else:   # modules swapped in by a wrapper (e.g. the halo convolutions of parallel/domain.py)

@@ -27,8 +27,8 @@ from . import _lib
 from .rope import rope_, rope_reference
 
 _NATIVE_D = (32, 64, 128)
-# DPH_FUSED_ROPE_BWD=0: separate inverse-RoPE pass over dq / dk instead of the fused kernel epilogue (A/B runs)
-_FUSED_ROPE_BWD = os.environ.get("DPH_FUSED_ROPE_BWD", "1") != "0"
+# inverse RoPE of dq / dk in the backward kernels' epilogue (the separate pass stays for non-native shapes)
+_FUSED_ROPE_BWD = True
 _warned = set()
 
 

@@ -5,23 +5,27 @@ In NHWC a stride-1, bias-free 1x1 convolution is ``Y[M, Cout] = X[M, Cin] W[Cout
 its two gradients are ``dX = dY W`` and ``dW = dY^T X`` -- no im2col, no layout change: the channels-last tensor
 IS the row-major [M, C] matrix.  ResNet-50's bottleneck convolutions conv1 / conv3 are of this kind (about 2/3
 of its convolution time, benchmarks/conv_bench.py).  Strided 1x1 / 3x3 convolutions run on the gathered implicit GEMM
-(``StridedConv2d``, below); the 7x7 stem keeps MIOpen.
+(``StridedConv2d``, below), the 7x7 stride-2 stem on the same gathered kernel (``StemConv2d``).
+
+One switch covers every convolution here: ``DPH_CONV=miopen`` sends all of them (forward and both gradients) to
+ATen / MIOpen -- the comparator of the A/B runs quoted below; the default ``dph`` takes the HIP kernels wherever the
+shape qualifies.
 
 ``Conv1x1`` is a drop-in ``nn.Conv2d`` (same parameter, same state dict) that takes the kernel path for bf16
 (or bf16-autocast) channels-last inputs on the GPU with channel counts that are multiples of 64, and falls back
-to ``F.conv2d`` otherwise.  ``DPH_CONV1X1=0`` disables the kernel path (A/B runs).
+to ``F.conv2d`` otherwise.
 
 ``Conv3x3`` does the same for stride-1 / padding-1 3x3 convolutions as implicit GEMMs (K = 9 * Cin, tap-major):
 forward and input gradient on the LDS-DMA kernel of csrc/conv3x3.hip (the input gradient is a 3x3 convolution of dY
 with the spatially flipped, channel-transposed weight; padding taps are zero-filled by range-checked buffer DMA; an
 epilogue emits the following BatchNorm's statistics or adds a bias): 440-810 TFLOP/s vs MIOpen's 370-780 on the
-ResNet-50 / SimpleUNet shapes (profiles/r3/conv3_bench_oob.json), on by default (``DPH_CONV3X3=0``: MIOpen;
-``DPH_CONV3_WM=2|4`` picks the 4- or 8-wave tile).  The
+ResNet-50 / SimpleUNet shapes (profiles/r3/conv3_bench_oob.json).  The
 weight gradients run on the LDS-DMA split-pixel kernel (``c3w_k``) by default: 1.20-1.42x MIOpen per shape since round
 4 removed its per-piece address divisions and its second, nearly empty round of split-K workgroups (round 3 measured it
 at 241-357 TFLOP/s vs MIOpen's 318-491 and kept MIOpen for ResNet, profiles/r3/conv3_bench_c3w_wgrad.json).
-``DPH_CONV3_WGRAD=miopen|dph`` overrides.  Round 2's register-staged forward (``DPH_CONV3_KERNEL=ts``) measured 0.51-0.63 ms vs MIOpen's
-0.38-0.53 ms per shape and stayed off.
+Rejected variants (removed from the tree in round 5; their A/B evidence stays under profiles/): round 2's
+register-staged 3x3 forward (0.51-0.63 ms vs MIOpen's 0.38-0.53 ms per shape), the 8-wave 3x3 tile, the sub-image copy
+for strided 1x1 weight gradients, and ATen copies for the input-gradient weight transposes.
 """
 from __future__ import annotations
 
@@ -33,12 +37,13 @@ from torch import nn
 
 from . import _lib
 
-# DPH_DIRECT_MAIN_GRAD=0: return weight gradients to autograd (engine copies them) instead of writing the bucket
-_DIRECT = os.environ.get("DPH_DIRECT_MAIN_GRAD", "1") != "0"
+# weight gradients go straight into the data-parallel engine's bucket (main_grad) when it exposes one
+_DIRECT = True
 
-# Set by runtime/graphs.GraphedStep (DPH_GRAPH_SAFE_CONV=1 only, an investigation knob): convolutions take MIOpen
-# inside whole-step HIP graphs.
-_GRAPHED_STEP = False
+
+def _miopen() -> bool:
+    """DPH_CONV=miopen: every convolution on ATen / MIOpen (A/B comparator); default dph = the HIP kernels."""
+    return os.environ.get("DPH_CONV", "dph").lower() == "miopen"
 
 
 def _autocast_bf16(t: torch.Tensor) -> bool:
@@ -50,13 +55,10 @@ def _nhwc2d(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1).contiguous().view(-1, t.shape[1])
 
 
-_HIP_WT = os.environ.get("DPH_CONV_WT", "hip") != "aten"   # input-gradient weight copies: HIP kernels or ATen (A/B)
-
-
 def weight_t(w2: torch.Tensor) -> torch.Tensor:
     """[Cout, Cin] -> [Cin, Cout] for an input-gradient GEMM: the HIP tile transpose (csrc/transpose.hip) instead of
     ATen's element-wise strided copy."""
-    if _HIP_WT and w2.is_cuda and w2.dtype == torch.bfloat16 and w2.stride(1) == 1 and w2.stride(0) % 8 == 0 and \
+    if w2.is_cuda and w2.dtype == torch.bfloat16 and w2.stride(1) == 1 and w2.stride(0) % 8 == 0 and \
             w2.shape[0] % 8 == 0 and w2.data_ptr() % 16 == 0:
         return _lib.ops().transpose2d(w2)
     return w2.t().contiguous()
@@ -204,21 +206,13 @@ class _Conv1x1Fn(torch.autograd.Function):
         return dx, gw, None, None
 
 
-def _conv3_wgrad(default: str) -> str:
-    """Which kernel runs a 3x3 weight gradient: DPH_CONV3_WGRAD (miopen | dph) overrides the module's default, which is
-    the c3w_k kernel everywhere since its DMA addresses advance incrementally and its split-K fills exactly one resident
-    round: 1.20-1.42x MIOpen on the ResNet-50 / SimpleUNet shapes (profiles/r4/c3w_rounds/c3.log).  Before
-    that, Conv3x3 (ResNet bottlenecks) kept MIOpen (10 068 / 10 079 img/s vs 9 835 / 9 833 with the kernel) while
-    BiasConv2d (SimpleUNet) already took the kernel (1 005 / 984 vs 848 / 826 samples/s, profiles/r4/conv_wgrad/)."""
-    return os.environ.get("DPH_CONV3_WGRAD", default)
-# stride-1 3x3 convolutions on csrc/conv3x3.hip by default: ResNet-50 FSDP bf16 B=256 9 472 / 9 513 vs 9 258 / 9 278
-# img/s on MIOpen (interleaved A/B on one MI355X, profiles/r3/ab_conv3x3/); DPH_CONV3X3=0 = MIOpen
-_CONV3X3_DEFAULT = "1"
-
-
-def _conv3_stats_ok() -> bool:
-    # the BatchNorm-statistics epilogue exists on the LDS-DMA kernel only (csrc/conv3x3.hip)
-    return os.environ.get("DPH_CONV3_KERNEL", "dma")[:1] != "t"
+# 3x3 weight gradients on the c3w_k kernel (wgrad="dph") since its DMA addresses advance incrementally and its split-K
+# fills exactly one resident round: 1.20-1.42x MIOpen on the ResNet-50 / SimpleUNet shapes (profiles/r4/c3w_rounds/
+# c3.log).  Before that, Conv3x3 (ResNet bottlenecks) kept MIOpen (10 068 / 10 079 img/s vs 9 835 / 9 833 with the
+# kernel) while BiasConv2d (SimpleUNet) already took the kernel (1 005 / 984 vs 848 / 826 samples/s,
+# profiles/r4/conv_wgrad/).  wgrad="miopen" keeps MIOpen's (comparisons).
+# stride-1 3x3 convolutions on csrc/conv3x3.hip: ResNet-50 FSDP bf16 B=256 9 472 / 9 513 vs 9 258 / 9 278 img/s on
+# MIOpen (interleaved A/B on one MI355X, profiles/r3/ab_conv3x3/)
 
 
 def _main_grad_cl(w: torch.Tensor, cout: int, k: int):
@@ -233,7 +227,7 @@ def _main_grad_cl(w: torch.Tensor, cout: int, k: int):
 
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stats_slot=None, bias=None, wgrad="miopen"):
+    def forward(ctx, x, w, stats_slot=None, bias=None, wgrad="dph"):
         wdtype = w.dtype
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -266,14 +260,14 @@ class _Conv3x3Fn(torch.autograd.Function):
         dx = gw = None
         if ctx.needs_input_grad[0]:
             # dX = conv3x3(dY, W') with W'[ci, (kh, kw), co] = W[co, ci, 2 - kh, 2 - kw]
-            if _HIP_WT and wb.is_contiguous(memory_format=torch.channels_last) and cout % 8 == 0 and C % 8 == 0:
+            if wb.is_contiguous(memory_format=torch.channels_last) and cout % 8 == 0 and C % 8 == 0:
                 wf = _lib.ops().conv3x3_dgrad_weight(wb)                  # one launch, HBM-speed tiles
             else:
                 wf = wb.flip(2, 3).permute(1, 2, 3, 0).reshape(C, 9 * cout)
             dx = _lib.ops().ts_gemm_nt(dy2, wf, H, W).view(B, H, W, C).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] and ctx.wgrad != "dph":
             # weight gradient on MIOpen: 1.0-1.5x the split-pixel kernel on the ResNet-50 shapes
-            # (profiles/r3/conv3_bench_oob.json: 318-485 vs 302-321 TFLOP/s); see _conv3_wgrad
+            # (profiles/r3/conv3_bench_oob.json: 318-485 vs 302-321 TFLOP/s, before round 4's c3w_k rework)
             x4 = x2.view(B, H, W, C).permute(0, 3, 1, 2)
             dy4 = dy2.view(B, H, W, cout).permute(0, 3, 1, 2)
             gw = torch.ops.aten.convolution_backward(dy4, x4, wb, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
@@ -296,7 +290,7 @@ class _Conv3x3Fn(torch.autograd.Function):
 
 
 def conv3x3_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    if os.environ.get("DPH_CONV3X3", _CONV3X3_DEFAULT) != "1" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
+    if _miopen() or not x.is_cuda or _lib.reference_mode():
         return False
     if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)):
         return False
@@ -314,8 +308,7 @@ class Conv3x3(nn.Conv2d):
     def forward(self, x, stats_slot: StatsSlot | None = None):
         if conv3x3_native_ok(x, self.weight):
             _lib.require()
-            return _Conv3x3Fn.apply(x, self.weight, stats_slot if _conv3_stats_ok() else None, None,
-                                    _conv3_wgrad("dph"))
+            return _Conv3x3Fn.apply(x, self.weight, stats_slot)
         return F.conv2d(x, self.weight, padding=1)
 
 
@@ -386,11 +379,9 @@ def convg_reference(A: torch.Tensor, B: torch.Tensor, geo: list, out: torch.Tens
     return out
 
 
-def _strided_wgrad() -> str:
-    """Strided weight gradients on c3w_k by default since its DMA addresses advance incrementally: 0.90-1.46x MIOpen
-    per shape (profiles/r4/c3w_incr/str_ns2.log) and, with the 1x1 identity-row kernel, ResNet-50 10 042 / 10 056 vs
-    9 912 / 9 927 img/s (profiles/r4/resnet_wgrad_ab/); DPH_CONV_STRIDED_WGRAD=miopen keeps MIOpen's."""
-    return os.environ.get("DPH_CONV_STRIDED_WGRAD", "dph")
+# Strided weight gradients on c3w_k since its DMA addresses advance incrementally: 0.90-1.46x MIOpen per shape
+# (profiles/r4/c3w_incr/str_ns2.log) and, with the 1x1 identity-row kernel, ResNet-50 10 042 / 10 056 vs 9 912 / 9 927
+# img/s (profiles/r4/resnet_wgrad_ab/).
 
 
 class _StridedConvFn(torch.autograd.Function):
@@ -443,23 +434,13 @@ class _StridedConvFn(torch.autograd.Function):
                 bk = torch.stack([wp[:, ky, kx, :] for ky, kx in kt], 1).reshape(C, len(kt) * cout)
                 _lib.ops().convg_nt_out_(dy2, bk, geo, dx2)
             dx = dx2.view(B, H, W, C).permute(0, 3, 1, 2)
-        if ctx.needs_input_grad[1] and _strided_wgrad() != "dph":
-            # MIOpen's weight gradient (DPH_CONV_STRIDED_WGRAD=miopen; the gathered c3w_k / sub-image 1x1 kernels are
-            # the default, see _strided_wgrad)
-            x4 = x2.view(B, H, W, C).permute(0, 3, 1, 2)
-            dy4 = dy2.view(B, Ho, Wo, cout).permute(0, 3, 1, 2)
-            gw = torch.ops.aten.convolution_backward(dy4, x4, wb, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
-                                                     [False, True, False])[1].to(ctx.wdtype)
-        elif ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1]:
             w = ctx.param
             mg = _main_grad_cl(w, cout, k * k * C)
             tgt = mg if mg is not None else torch.empty((cout, k * k * C), dtype=ctx.wdtype, device=dy.device)
             acc = bool(getattr(w, "_dph_accum", False)) if mg is not None else False
-            if k == 1 and os.environ.get("DPH_STRIDED1_COPY", "0") == "1":   # A/B: sub-image copy + dense kernel
-                xs = x2.view(B, H, W, C)[:, ::s, ::s].reshape(B * Ho * Wo, C)
-                _lib.ops().ts_gemm_tn_(tgt, dy2, xs, acc)
-            else:   # 1x1 included: the weight-gradient kernel gathers the strided rows itself (no sub-image copy)
-                _lib.ops().convg_tn_(tgt, dy2, x2, strided_fwd_geo(H, W, k, s, p), acc)
+            # 1x1 included: the weight-gradient kernel gathers the strided rows itself (no sub-image copy)
+            _lib.ops().convg_tn_(tgt, dy2, x2, strided_fwd_geo(H, W, k, s, p), acc)
             if mg is not None:
                 w._dph_accum = True
                 w._dph_grad_ready()
@@ -469,7 +450,7 @@ class _StridedConvFn(torch.autograd.Function):
 
 
 def strided_native_ok(x: torch.Tensor, m: nn.Conv2d) -> bool:
-    if os.environ.get("DPH_CONV_STRIDED", "1") == "0" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
+    if _miopen() or not x.is_cuda or _lib.reference_mode():
         return False
     if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)):
         return False
@@ -484,7 +465,7 @@ def strided_native_ok(x: torch.Tensor, m: nn.Conv2d) -> bool:
 class StridedConv2d(nn.Conv2d):
     """Bias-free strided 1x1 / 3x3 ``nn.Conv2d`` (same parameters and state dict) on the framework's gathered
     implicit-GEMM kernels for channels-last bf16 inputs with 64-multiple channels; MIOpen otherwise
-    (``DPH_CONV_STRIDED=0`` forces MIOpen).  ResNet-50 FSDP bf16 B=256: 10 066 / 10 106 vs 10 037 / 10 020 img/s
+    (``DPH_CONV=miopen`` forces MIOpen).  ResNet-50 FSDP bf16 B=256: 10 066 / 10 106 vs 10 037 / 10 020 img/s
     (profiles/r4/strided_conv/final/)."""
 
     def forward(self, x, stats_slot: StatsSlot | None = None, grad_slot: GradSlot | None = None):
@@ -494,14 +475,14 @@ class StridedConv2d(nn.Conv2d):
             _lib.require()
             gs = grad_slot if (grad_slot is not None and self.kernel_size[0] == 1 and self.stride[0] == 2) else None
             return _StridedConvFn.apply(x, self.weight, self.kernel_size[0], self.stride[0], self.padding[0],
-                                        stats_slot if _conv3_stats_ok() else None, gs)
+                                        stats_slot, gs)
         if grad_slot is not None:
             raise RuntimeError("StridedConv2d: grad_slot needs the kernel path (check strided_native_ok first)")
         return F.conv2d(x, self.weight, None, self.stride, self.padding)
 
 
 def conv1x1_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    if os.environ.get("DPH_CONV1X1", "1") == "0" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
+    if _miopen() or not x.is_cuda or _lib.reference_mode():
         return False
     if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)):
         return False
@@ -574,7 +555,7 @@ def _bias_conv(m: nn.Module, x: torch.Tensor, transposed: bool, output_padding) 
 def _bias_conv3x3_ok(m: nn.Module, x: torch.Tensor) -> bool:
     return (tuple(m.kernel_size) == (3, 3) and tuple(m.stride) == (1, 1) and tuple(m.padding) == (1, 1)
             and tuple(m.dilation) == (1, 1) and m.groups == 1 and m.padding_mode == "zeros" and m.bias is not None
-            and _conv3_stats_ok() and conv3x3_native_ok(x, m.weight))
+            and conv3x3_native_ok(x, m.weight))
 
 
 class BiasConv2d(nn.Conv2d):
@@ -589,7 +570,7 @@ class BiasConv2d(nn.Conv2d):
         if _bias_conv3x3_ok(self, x):
             _lib.require()
             b = self.bias if self.bias.dtype in (torch.float32, torch.bfloat16) else self.bias.float()
-            return _Conv3x3Fn.apply(x, self.weight, stats_slot, b, _conv3_wgrad("dph"))
+            return _Conv3x3Fn.apply(x, self.weight, stats_slot, b)
         if _bias_conv_ok(self, x):
             return _bias_conv(self, x, False, (0, 0))
         return super().forward(x)
@@ -670,7 +651,7 @@ class _StemConvFn(torch.autograd.Function):
 
 
 def stem_native_ok(x: torch.Tensor, m: nn.Conv2d) -> bool:
-    if os.environ.get("DPH_STEM_KERNEL", "1") == "0" or _GRAPHED_STEP or not x.is_cuda or _lib.reference_mode():
+    if _miopen() or not x.is_cuda or _lib.reference_mode():
         return False
     if not (x.dtype == torch.bfloat16 or _autocast_bf16(x)) or x.requires_grad:
         return False
@@ -694,7 +675,7 @@ class StemConv2d(nn.Conv2d):
         if stem_native_ok(x, self):
             _lib.require()
             return _StemConvFn.apply(x, self.weight, self.kernel_size[0], self.padding[0],
-                                     stats_slot if _conv3_stats_ok() else None)
+                                     stats_slot)
         if not (self.in_channels == 3 and self.groups == 1 and x.is_cuda and x.dim() == 4
                 and self.padding_mode == "zeros" and not isinstance(self.padding, str)
                 and x.is_contiguous(memory_format=torch.channels_last) and _lib.use_native(x)):

@@ -27,9 +27,6 @@ from torch import nn
 
 from . import _lib
 
-_ENABLED = os.environ.get("DPH_FUSED_UPCAT", "1") != "0"    # A/B knob: 0 = the reference three-op sequence
-
-
 def _pair(v):
     return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
 
@@ -41,8 +38,6 @@ def _compute_dtype(x: torch.Tensor) -> torch.dtype:
 
 
 def up_concat_native_ok(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> bool:
-    if not _ENABLED:
-        return False
     if not (isinstance(up, nn.ConvTranspose2d) and _pair(up.kernel_size) == (2, 2) and _pair(up.stride) == (2, 2)
             and _pair(up.padding) == (0, 0) and _pair(up.output_padding) == (0, 0) and _pair(up.dilation) == (1, 1)
             and up.groups == 1):
@@ -60,7 +55,7 @@ def up_concat_native_ok(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> b
 
 
 def _tall_skinny_ok(cin: int, co: int) -> bool:
-    return cin % 64 == 0 and (4 * co) % 64 == 0 and os.environ.get("DPH_UPCAT_GEMM", "ts") == "ts"
+    return cin % 64 == 0 and (4 * co) % 64 == 0
 
 
 class _UpConcatFn(torch.autograd.Function):

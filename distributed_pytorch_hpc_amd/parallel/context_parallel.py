@@ -120,8 +120,7 @@ def _attn_bwd(do, q, k, v, o, lse, causal, scale):
 
 def _fused_merge_ok(q) -> bool:
     """The flash forward can merge into the ring accumulators in its epilogue (bf16 CUDA operands, native head dim)."""
-    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (32, 64, 128) and _lib.use_native(q)
-            and os.environ.get("DPH_RING_FUSED_MERGE", "1") != "0")
+    return (q.is_cuda and q.dtype == torch.bfloat16 and q.shape[-1] in (32, 64, 128) and _lib.use_native(q))
 
 
 def _merge(o, lse, o2, lse2):

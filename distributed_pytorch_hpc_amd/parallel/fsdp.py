@@ -151,7 +151,7 @@ class ZeRO3Engine:
         # A shard group of one: a unit's gathered parameters / full gradient ARE its shard, so they alias the shard
         # buffers -- the all-gather, reduce-scatter and free of the general path degenerate to nothing instead of a
         # copy each (3 per unit per step) and an allocator round trip.  Same engine, same update order as world > 1.
-        self._alias = self.world == 1 and os.environ.get("DPH_FSDP_ALIAS", "1") != "0"   # (=0: A/B runs)
+        self._alias = self.world == 1
         self._unit_of = {}
         with torch.no_grad():
             for u in self.units:

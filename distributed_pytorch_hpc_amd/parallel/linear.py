@@ -29,7 +29,7 @@ _WGRAD_STREAMS: dict = {}
 # the caching allocator from recycling multi-GB blocks and drives it into synchronising cudaFree/retry cycles
 # near the 288 GB limit) and the compute stream waits for the oldest once more than _WGRAD_LAG are in flight.
 _WGRAD_PENDING: list = []
-_WGRAD_LAG = int(os.environ.get("DPH_WGRAD_LAG", "1"))
+_WGRAD_LAG = 1
 
 
 def join_wgrad_stream(device: torch.device):

@@ -23,8 +23,8 @@ next replay): consume or clone it before the next call.
 Multi-rank steps would capture their RCCL collectives into the graph too; that path is off unless
 ``allow_collectives=True`` (not exercised on the 1-GPU test box).
 
-Warm-up runs on the current stream by default; ``DPH_GRAPH_WARMUP_SIDE=1`` warms up on a side stream (the usual
-capture recipe).  Round 2 reported replayed ResNet-50 steps diverging with side-stream warm-up; round 3 re-examined
+Warm-up runs on the current stream (``warmup_side_stream=True`` warms up on a side stream, the usual capture
+recipe).  Round 2 reported replayed ResNet-50 steps diverging with side-stream warm-up; round 3 re-examined
 it with ``scripts/diag_graph_side_stream.py`` under MIOpen's deterministic algorithms (two eager runs bitwise equal):
 side- and current-stream warm-up, with fresh allocations + writes, in-place writes, or host-synchronised work between
 replays, with and without the 1x1 convolution kernels, at 32 px and at 224 px (the 14 x 14 layers) -- every replayed
@@ -33,13 +33,10 @@ MIOpen's non-deterministic bf16 solvers, where two EAGER runs already differed b
 (``profiles/diag_nondeterminism_resnet*.log``), so its "divergence" had no bitwise baseline; the one blow-up recorded
 then (``gpu_tests_intermittent_resnet50_graph_fail.log``) happened with current-stream warm-up, i.e. it was not
 tied to the warm-up stream.  ``tests/test_graphs.py::test_graph_warmup_stream_and_interference_bitwise`` keeps both
-warm-up modes bitwise-checked against eager with unrelated GPU work between replays.  ``DPH_GRAPH_SAFE_CONV=1``
-routes convolutions to MIOpen inside graphed steps (investigation knob).
+warm-up modes bitwise-checked against eager with unrelated GPU work between replays.
 """
 from __future__ import annotations
 
-import contextlib
-import os
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -50,23 +47,11 @@ def _engine_of(optimizer):
     return getattr(optimizer, "engine", None)
 
 
-@contextlib.contextmanager
-def _graph_safe_ops():
-    from ..ops import conv
-
-    old = conv._GRAPHED_STEP
-    conv._GRAPHED_STEP = os.environ.get("DPH_GRAPH_SAFE_CONV", "0") == "1"   # investigation knob
-    try:
-        yield
-    finally:
-        conv._GRAPHED_STEP = old
-
-
 class GraphedStep:
     """Capture ``step_fn(*tensors) -> loss`` into a HIP graph after ``warmup`` eager calls, then replay it."""
 
     def __init__(self, step_fn: Callable[..., torch.Tensor], *, optimizer=None, warmup: int = 3,
-                 pool=None, allow_collectives: bool = False):
+                 pool=None, allow_collectives: bool = False, warmup_side_stream: bool = False):
         if not torch.cuda.is_available():
             raise RuntimeError("GraphedStep needs a GPU (HIP graphs)")
         if dist.is_initialized() and dist.get_world_size() > 1 and not allow_collectives:
@@ -88,6 +73,7 @@ class GraphedStep:
         self.static_in: list[torch.Tensor] = []
         self.static_out = None
         self._side = torch.cuda.Stream()
+        self.warmup_side_stream = warmup_side_stream
 
     # ---------------------------------------------------------------------------------------------- internals
     def _stage(self, args: Sequence[torch.Tensor]):
@@ -120,9 +106,9 @@ class GraphedStep:
                 self.optimizer.param_groups[0]["lr"] = lr
         self._set_lr(lr)
         cur = torch.cuda.current_stream()
-        side = self._side if os.environ.get("DPH_GRAPH_WARMUP_SIDE", "0") == "1" else cur
+        side = self._side if self.warmup_side_stream else cur
         side.wait_stream(cur)
-        with torch.cuda.stream(side), _graph_safe_ops():
+        with torch.cuda.stream(side):
             out = self.step_fn(*self.static_in)
         cur.wait_stream(side)
         return out
@@ -133,7 +119,7 @@ class GraphedStep:
         saved = self.engine.step_count if self.engine is not None else None
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with _graph_safe_ops(), torch.cuda.graph(self.graph, pool=self.pool):
+        with torch.cuda.graph(self.graph, pool=self.pool):
             self.static_out = self.step_fn(*self.static_in)
         if self.engine is not None:
             self.engine.step_count = saved

@@ -4,7 +4,7 @@
 Runs ResNet (FSDP units, bf16, channels-last) with MIOpen's deterministic algorithms so two eager runs agree
 bitwise, then replays a captured step under combinations of:
 
-  * warm-up stream: current (default) / side (DPH_GRAPH_WARMUP_SIDE=1, the configuration that diverged);
+  * warm-up stream: current (default) / side (GraphedStep(warmup_side_stream=True), the configuration that diverged);
   * interference between replays: none / "alloc" (fresh allocations of assorted sizes + GPU writes into them, the
     caching allocator may hand out any block it considers free) / "noalloc" (the same writes into ONE buffer
     allocated before the run -- no allocator traffic) / "sync" (alloc, but the host synchronises first);
@@ -42,7 +42,6 @@ def run(arch, batches, graphed, interference, side, extra_env=None):
     from distributed_pytorch_hpc_amd.parallel.fsdp import FSDP
     from distributed_pytorch_hpc_amd.runtime import graphs
 
-    os.environ["DPH_GRAPH_WARMUP_SIDE"] = "1" if side else "0"
     for k, v in (extra_env or {}).items():
         os.environ[k] = v
     dev = torch.device("cuda")
@@ -57,7 +56,7 @@ def run(arch, batches, graphed, interference, side, extra_env=None):
         opt.step()
         return loss.detach()
 
-    runner = graphs.GraphedStep(step_fn, optimizer=opt, warmup=2) if graphed else None
+    runner = graphs.GraphedStep(step_fn, optimizer=opt, warmup=2, warmup_side_stream=side) if graphed else None
     scratch = torch.empty(64 << 20, dtype=torch.uint8, device=dev)   # "noalloc" interference target
     g = torch.Generator(device=dev).manual_seed(77)
     losses = []
@@ -106,7 +105,7 @@ def main():
     res = {"eager": ref, "eager_reproducible": bool(torch.equal(ref_t, ref2_t)), "cases": {}}
     print(f"eager losses {ref}; second eager run bitwise equal: {res['eager_reproducible']}", flush=True)
     cases = [("current", "none", {}), ("current", "alloc", {}), ("side", "none", {}), ("side", "alloc", {}),
-             ("side", "noalloc", {}), ("side", "sync", {}), ("side", "alloc", {"DPH_CONV1X1": "0"})]
+             ("side", "noalloc", {}), ("side", "sync", {}), ("side", "alloc", {"DPH_CONV": "miopen"})]
     refs = {}
     for side, inter, env in cases:
         name = f"warmup={side} interference={inter}" + (f" {env}" if env else "")

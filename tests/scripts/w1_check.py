@@ -1,6 +1,5 @@
 """1x1 weight-gradient GEMM (ts_gemm_tn_: dW = dY^T X over channels-last pixels) against an fp32 reference, in a
-fresh process: the kernel choice (DPH_W1_KERNEL) and its LDS ring depth (DPH_W1_STAGES) are read once per process,
-so tests/test_kernels_gpu.py runs this script as a child to cover each variant.  Shapes cover both output tile widths,
+child process of tests/test_kernels_gpu.py (a kernel fault ends the child, not the test session).  Shapes cover both output tile widths,
 64- and 128-wide k' tiles, a pixel count that leaves a ragged last chunk / step, and accumulation into bf16 and fp32.
 Prints one JSON line; exits 1 on a tolerance miss."""
 import json
@@ -38,8 +37,7 @@ def main():
         worst = max(worst, err / (1e-2 if dt == torch.bfloat16 else 1e-4))
         print(json.dumps({"M": M, "N": N, "K": K, "dtype": str(dt), "acc": acc, "rel_err": err}), flush=True)
     ok = worst <= 1.0
-    print(json.dumps({"ok": ok, "worst_over_tol": worst, "w1": os.environ.get("DPH_W1_KERNEL"),
-                      "stages": os.environ.get("DPH_W1_STAGES")}))
+    print(json.dumps({"ok": ok, "worst_over_tol": worst}))
     sys.exit(0 if ok else 1)
 
 

@@ -135,85 +135,36 @@ def test_llama_fused_blocks_match_unfused(dph_native, which):
         assert rel_err(g1[n], g0[n]) < 3e-2, n
 
 
-@pytest.mark.parametrize("variant", [1])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 192), (768, 512, 320), (256, 1024, 4096)])
-def test_gemm_nt_pipeline_variants_bitwise(dph_native, variant, M, N, K):
-    """Every pipeline variant (csrc/gemm_nt.hip LOOK) accumulates the same products in the same order as variant 0:
-    bitwise-equal outputs, for one, odd and even K-tile counts, in the plain and the fused SwiGLU modes."""
-    a, b = _rnd(M, K, seed=11), _rnd(N, K, seed=12)
-    try:
-        dph_native.gemm_nt_variant_(0)
-        c0 = dph_native.gemm_nt(a, b)
-        s0 = dph_native.gemm_nt_swiglu(a, b)
-        dph_native.gemm_nt_variant_(variant)
-        c1 = dph_native.gemm_nt(a, b)
-        s1 = dph_native.gemm_nt_swiglu(a, b)
-    finally:
-        dph_native.gemm_nt_variant_(-1)
-    assert torch.equal(c0, c1)
-    assert torch.equal(s0[0], s1[0]) and torch.equal(s0[1], s1[1])
-    assert rel_err(c1, a.float() @ b.float().t()) < 5e-3
-
-
-def test_gemm_nt_epilogue_forms_bitwise(dph_native):
-    """The LDS-staged epilogue (default for STORE / DSWIGLU) and the register epilogue (DPH_NT_EPI=reg) produce
-    bitwise-identical outputs (same bf16 rounding of dh, same SwiGLU-backward math); run in child processes because
-    the form is read once per process."""
-    import os
-    import subprocess
-    import sys
-
-    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "nt_epi_check.py")
-    outs = []
-    for form in ("reg", "lds"):
-        env = dict(os.environ, DPH_NT_EPI=form)
-        p = subprocess.run([sys.executable, script], env=env, capture_output=True, text=True, timeout=110)
-        assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
-        outs.append(p.stdout.strip().splitlines()[-1])
-    assert outs[0] == outs[1]
-
-
-# ---- both MFMA shapes (variants 0/1: 16x16x32, 2/3: 32x32x16) on ragged edge tiles (tensor-parallel shards) ----
-def _with_variant(dph_native, v, fn):
-    try:
-        dph_native.gemm_nt_variant_(v)
-        return fn()
-    finally:
-        dph_native.gemm_nt_variant_(-1)
-
-
 def _check_store(c, ref):
     assert rel_err(c, ref) < 5e-3
     assert ((c.float() - ref).abs() <= 1e-2 * ref.abs() + 2e-2 * ref.abs().mean()).all()
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 192), (768, 512, 320), (256, 1024, 4096),
                                    # ragged: tp8 / tp4 shards of Llama-2-7B (w13 2752, head 4000, w2's K 1376),
                                    # a partial single K-tile, the smallest N
                                    (256, 2752, 256), (512, 4000, 128), (256, 4096, 1376), (256, 520, 40),
                                    (256, 8, 72), (512, 1000, 200)])
-def test_gemm_nt32_store(dph_native, variant, M, N, K):
+def test_gemm_nt_ragged_store(dph_native, M, N, K):
     a, b = _rnd(M, K, seed=21), _rnd(N, K, seed=22)
-    c = _with_variant(dph_native, variant, lambda: dph_native.gemm_nt(a, b))
+    c = (dph_native.gemm_nt(a, b))
     assert c.shape == (M, N)
     _check_store(c, a.float() @ b.float().t())
 
 
-def test_gemm_nt32_asymmetric_identity(dph_native):
+def test_gemm_nt_ragged_asymmetric_identity(dph_native):
     M = N = K = 256
     a = torch.eye(M, K, device=DEV, dtype=torch.bfloat16)
     b = (torch.arange(N * K, device=DEV) % 251).reshape(N, K).to(torch.bfloat16)
-    c = _with_variant(dph_native, 3, lambda: dph_native.gemm_nt(a, b))
+    c = (dph_native.gemm_nt(a, b))
     assert torch.equal(c, b.t().contiguous())
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,H,K", [(256, 128, 64), (512, 384, 256), (256, 1376, 256), (256, 2752, 136),
                                    (256, 40, 64)])
-def test_gemm_nt32_swiglu(dph_native, variant, M, H, K):
+def test_gemm_nt_ragged_swiglu(dph_native, M, H, K):
     x, w13 = _rnd(M, K, seed=25), _rnd(2 * H, K, seed=26, scale=0.5)
-    x13, h = _with_variant(dph_native, variant, lambda: dph_native.gemm_nt_swiglu(x, w13))
+    x13, h = (dph_native.gemm_nt_swiglu(x, w13))
     ref13 = x.float() @ w13.float().t()
     assert x13.shape == (M, 2 * H) and h.shape == (M, H)
     assert rel_err(x13, ref13) < 5e-3
@@ -222,12 +173,11 @@ def test_gemm_nt32_swiglu(dph_native, variant, M, H, K):
     assert torch.equal(h, dph_native.swiglu_fwd(x13))
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("M,H,K", [(256, 256, 64), (512, 768, 128), (256, 1376, 512), (256, 2752, 200)])
-def test_gemm_nt32_dswiglu(dph_native, variant, M, H, K):
+def test_gemm_nt_ragged_dswiglu(dph_native, M, H, K):
     dy, w2t = _rnd(M, K, seed=27), _rnd(H, K, seed=28, scale=0.5)
     x13 = _rnd(M, 2 * H, seed=29, scale=2.0)
-    d13 = _with_variant(dph_native, variant, lambda: dph_native.gemm_nt_dswiglu(dy, w2t, x13))
+    d13 = (dph_native.gemm_nt_dswiglu(dy, w2t, x13))
     dh = dy.float() @ w2t.float().t()
     g, u = x13[:, :H].float(), x13[:, H:].float()
     s = torch.sigmoid(g)
@@ -236,17 +186,15 @@ def test_gemm_nt32_dswiglu(dph_native, variant, M, H, K):
     assert rel_err(d13, ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("S,hd,heads,K", [(256, 64, 4, 256), (512, 128, 2, 256), (256, 128, 4, 1376)])
-def test_gemm_nt32_rope(dph_native, variant, S, hd, heads, K):
+def test_gemm_nt_ragged_rope(dph_native, S, hd, heads, K):
     from distributed_pytorch_hpc_amd.models.llama2 import rope_tables
 
     B = 2
     N = 3 * heads * hd
     x, w = _rnd(B * S, K, seed=30), _rnd(N, K, seed=31, scale=0.2)
     cos, sin = rope_tables(hd, 2 * S, 10000.0, torch.device(DEV))
-    y = _with_variant(dph_native, variant,
-                      lambda: dph_native.gemm_nt_rope(x, w, cos, sin, S, hd, 2 * heads * hd, 3))
+    y = dph_native.gemm_nt_rope(x, w, cos, sin, S, hd, 2 * heads * hd, 3)
     ref = x.float() @ w.float().t()
     pos = torch.arange(B * S, device=DEV) % S + 3
     c, s = cos[pos][:, None, :], sin[pos][:, None, :]
@@ -254,12 +202,3 @@ def test_gemm_nt32_rope(dph_native, variant, S, hd, heads, K):
     a, b = rot[..., 0], rot[..., 1]
     rot = torch.stack([a * c - b * s, a * s + b * c], -1).reshape(B * S, -1)
     assert rel_err(y, torch.cat([rot, ref[:, 2 * heads * hd:]], 1)) < 5e-3
-
-
-@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 192), (768, 512, 320)])
-def test_gemm_nt32_lookahead_bitwise(dph_native, M, N, K):
-    """The lookahead variant of the 32x32 kernel accumulates in the same order: bitwise equal to variant 2."""
-    a, b = _rnd(M, K, seed=32), _rnd(N, K, seed=33)
-    c2 = _with_variant(dph_native, 2, lambda: dph_native.gemm_nt(a, b))
-    c3 = _with_variant(dph_native, 3, lambda: dph_native.gemm_nt(a, b))
-    assert torch.equal(c2, c3)

@@ -292,7 +292,6 @@ def test_graph_warmup_stream_and_interference_bitwise(dph_native, side, interfer
     d.CIFAR_STEM = False
     det, bench = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
     torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
-    old = os.environ.get("DPH_GRAPH_WARMUP_SIDE")
     try:
         torch.manual_seed(3)
         batches = [(torch.randn(8, 3, 224, 224, device=DEV, dtype=torch.bfloat16).contiguous(
@@ -301,8 +300,4 @@ def test_graph_warmup_stream_and_interference_bitwise(dph_native, side, interfer
         got, _ = d.run("resnet50", batches, True, interference, side == "side")
     finally:
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = det, bench
-        if old is None:
-            os.environ.pop("DPH_GRAPH_WARMUP_SIDE", None)
-        else:
-            os.environ["DPH_GRAPH_WARMUP_SIDE"] = old
     assert got == ref, (got, ref)

@@ -268,92 +268,29 @@ def test_flash_attention_long_sequence(dph_native):
     assert rel_err(q.grad, qr.grad) < 3e-2 and rel_err(k.grad, kr.grad) < 3e-2 and rel_err(v.grad, vr.grad) < 3e-2
 
 
-@pytest.mark.parametrize("waves", ["8", "9"])
-def test_flash_attention_eight_wave_variant(dph_native, waves):
-    """The opt-in 8-wave workgroups (DPH_ATTN_WAVES=8; 9 = 8 waves with the staggered forward), read once per
-    process, in a child process."""
-    import os
-    import subprocess
-    import sys
-
-    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "attn_check.py")
-    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_ATTN_WAVES=waves), capture_output=True,
-                       text=True, timeout=100)
-    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
-    assert '"ok": true' in p.stdout
-
-
-@pytest.mark.parametrize("var", ["0", "1", "2", "3"])
-def test_flash_attention_pipelined_forward(dph_native, var):
-    """The software-pipelined forward (DPH_ATTN_FWD=pipe, schedule variant DPH_ATTN_FWD_VAR), read once per process,
-    in a child process: ragged / Sq > Sk / Sk % 32 != 0 shapes and a spiked-key case that forces the rescale branch."""
-    import os
-    import subprocess
-    import sys
-
-    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "attn_check.py")
-    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_ATTN_FWD="pipe", DPH_ATTN_FWD_VAR=var),
-                       capture_output=True, text=True, timeout=110)
-    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
-    assert '"ok": true' in p.stdout
-
-
-@pytest.mark.parametrize("knob,val", [("DPH_ATTN_BWD_VAR", "6"), ("DPH_ATTN_DQ_VAR", "3"), ("DPH_ATTN_FWD_PRIO", "1"),
-                                      ("DPH_ATTN_FWD_PRIO", "0")])
-def test_flash_attention_priority_variants(dph_native, knob, val):
-    """The attention kernels with issue priority raised over their MFMA chains (dK/dV DPH_ATTN_BWD_VAR=6, dQ
-    DPH_ATTN_DQ_VAR=3, forward DPH_ATTN_FWD_PRIO=1) and without, in a child process against the fp32 reference."""
-    import os
-    import subprocess
-    import sys
-
-    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "attn_check.py")
-    p = subprocess.run([sys.executable, script], env=dict(os.environ, **{knob: val}), capture_output=True,
-                       text=True, timeout=100)
-    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
-    assert '"ok": true' in p.stdout
-
-
-@pytest.mark.parametrize("dq_var", ["1", "2"])
-def test_flash_attention_dq_variants(dph_native, dq_var):
-    """dQ kernel variants (DPH_ATTN_DQ_VAR: 1 = transposed-K read ring, 2 = quarter-sub-tile K / V read-ahead without
-    register spills), read once per process, in a child process against the fp32 reference."""
-    import os
-    import subprocess
-    import sys
-
-    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "attn_check.py")
-    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_ATTN_DQ_VAR=dq_var), capture_output=True,
-                       text=True, timeout=100)
-    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
-    assert '"ok": true' in p.stdout
-
-
-@pytest.mark.parametrize("kernel,stages", [("0", "2"), ("1", "2"), ("1", "3"), ("1", "4"), ("1", "5")])
-def test_conv1x1_wgrad_variants(dph_native, kernel, stages):
-    """1x1 weight gradient: register-staged ts_tn_k (DPH_W1_KERNEL=0) and the LDS-DMA c3w_k form with 2..5 ring stages
-    (DPH_W1_STAGES; counted vmcnt, ragged last chunk drains), in a child process against the fp32 reference."""
+def test_conv1x1_wgrad(dph_native):
+    """1x1 weight gradient on the LDS-DMA c3w_k form (2-stage ring, counted vmcnt, ragged last chunk drains), in a
+    child process against the fp32 reference."""
     import os
     import subprocess
     import sys
 
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "w1_check.py")
-    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_W1_KERNEL=kernel, DPH_W1_STAGES=stages),
+    p = subprocess.run([sys.executable, script], env=dict(os.environ),
                        capture_output=True, text=True, timeout=100)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
     assert '"ok": true' in p.stdout
 
 
-@pytest.mark.parametrize("stages", ["2", "3", "4", "5"])
-def test_conv3x3_wgrad_ring_variants(dph_native, stages):
-    """3x3 (stride 1 and gathered strided) and stem weight gradients on c3w_k with 2..5 LDS ring stages
-    (DPH_C3W_STAGES, capped at what fits 160 KiB), in a child process against F.conv2d in fp32."""
+def test_conv3x3_wgrad_c3w(dph_native):
+    """3x3 (stride 1 and gathered strided) and stem weight gradients on c3w_k, in a child process against F.conv2d in
+    fp32."""
     import os
     import subprocess
     import sys
 
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "scripts", "c3w_check.py")
-    p = subprocess.run([sys.executable, script], env=dict(os.environ, DPH_C3W_STAGES=stages), capture_output=True,
+    p = subprocess.run([sys.executable, script], env=dict(os.environ), capture_output=True,
                        text=True, timeout=100)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
     assert '"ok": true' in p.stdout
@@ -413,7 +350,7 @@ def test_embedding(dph_native):
                          [(512, 256, 256, torch.float32, False), (1024, 512, 768, torch.bfloat16, False),
                           (2048, 768, 512, torch.bfloat16, True), (64, 256, 512, torch.float32, True),
                           (192, 256, 256, torch.float32, False), (128, 512, 256, torch.float32, True)])
-@pytest.mark.parametrize("mfma,tail", [(16, 0), (32, 0), (32, 3), (32, 8), (33, 0), (33, 3), (33, 8)])
+@pytest.mark.parametrize("mfma,tail", [(32, 0), (32, 3), (32, 8), (33, 0), (33, 3), (33, 8)])
 def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate, mfma, tail):
     """C (+)= A^T B with token-major A [K, M], B [K, N] (weight gradient dW = dY^T X), both MFMA-shape kernels
     (K = 64 / 128 / 192 exercise the one- and two-K-step tails of the pipeline).  tail > 0 plans the partial-last-
@@ -430,7 +367,7 @@ def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate, mfma, tail):
             assert torch.ops.dph.gemm_tn_plan_info(M, N, K)[0] > 0 or K < 128
         torch.ops.dph.gemm_tn_(c, a, b, accumulate)
     finally:
-        torch.ops.dph.gemm_tn_mfma_(0)   # back to the default / DPH_WGRAD_MFMA
+        torch.ops.dph.gemm_tn_mfma_(0)   # back to the default
         torch.ops.dph.gemm_tn_tail_(0)
     ref = a.float().t() @ b.float() + (c0.float() if accumulate else 0)
     assert rel_err(c, ref) < (1e-5 if out_dtype == torch.float32 else 8e-3)
@@ -459,7 +396,7 @@ def test_gemm_tn_tail_band(dph_native, M, N, dim, out_dtype, accumulate):
 
 @pytest.mark.parametrize("K,M,N", [(256, 2752 // 4, 4096 // 8), (128, 264, 520), (192, 4000 // 10, 1376 // 4),
                                    (64, 8, 256), (512, 1000, 24)])
-@pytest.mark.parametrize("mfma", [16, 32, 33])
+@pytest.mark.parametrize("mfma", [32, 33])
 def test_gemm_tn_wgrad_ragged_edge_tiles(dph_native, K, M, N, mfma):
     """Tensor-parallel shard shapes (M, N % 8 but not % 256: w13 / w2 / vocab-head shards at tp=8) as partial edge
     tiles: every in-bounds element matches the fp32 reference and nothing past the matrix edge is written."""
@@ -817,7 +754,7 @@ def test_bottleneck_conv1x1_path_matches_miopen_gradients(dph_native, monkeypatc
     x = torch.randn(8, 256, 16, 16, device=DEV).contiguous(memory_format=torch.channels_last)
 
     def grads(flag, amp=True):
-        monkeypatch.setenv("DPH_CONV1X1", flag)
+        monkeypatch.setenv("DPH_CONV", "dph" if flag == "1" else "miopen")
         model.zero_grad(set_to_none=True)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             loss = model(x).float().pow(2).mean()
@@ -884,7 +821,7 @@ def test_bottleneck_residual_grad_slot(dph_native, monkeypatch):
         memory_format=torch.channels_last).requires_grad_()
 
     def run(flag):
-        monkeypatch.setenv("DPH_CONV1X1", flag)
+        monkeypatch.setenv("DPH_CONV", "dph" if flag == "1" else "miopen")
         block.zero_grad(set_to_none=True)
         x.grad = None
         made.clear()
@@ -907,7 +844,7 @@ def test_conv3x3_module_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W, 
     input gradient and weight gradient; images smaller than a 128-row tile and non-square."""
     from distributed_pytorch_hpc_amd.ops.conv import Conv3x3, conv3x3_native_ok
 
-    monkeypatch.setenv("DPH_CONV3X3", "1")   # opt-in path
+    monkeypatch.setenv("DPH_CONV", "dph")
     torch.manual_seed(5)
     conv = Conv3x3(C, Co).to(DEV)
     if not autocast:
@@ -934,7 +871,7 @@ def test_bias_conv3x3_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W):
     vs F.conv2d in fp32 on the same bf16-rounded operands."""
     from distributed_pytorch_hpc_amd.ops.conv import BiasConv2d, _bias_conv3x3_ok
 
-    monkeypatch.setenv("DPH_CONV3X3", "1")
+    monkeypatch.setenv("DPH_CONV", "dph")
     torch.manual_seed(3)
     conv = BiasConv2d(C, Co, 3, padding=1).to(DEV).to(memory_format=torch.channels_last)
     with torch.no_grad():
@@ -1117,7 +1054,7 @@ def test_resnet_bottleneck_conv3x3_path_matches_miopen(dph_native, monkeypatch):
     x0 = torch.randn(4, 256, 14, 14, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
 
     def run(flag):
-        monkeypatch.setenv("DPH_CONV3X3", flag)
+        monkeypatch.setenv("DPH_CONV", "dph" if flag == "1" else "miopen")
         block.zero_grad(set_to_none=True)
         x = x0.clone().requires_grad_()
         block(x).float().pow(2).mean().backward()
@@ -1208,7 +1145,7 @@ def test_bottleneck_downsample_grad_tap(dph_native, monkeypatch, inplanes, plane
         memory_format=torch.channels_last).requires_grad_()
 
     def run(flag):
-        monkeypatch.setenv("DPH_CONV1X1", flag)
+        monkeypatch.setenv("DPH_CONV", "dph" if flag == "1" else "miopen")
         block.zero_grad(set_to_none=True)
         x.grad = None
         made.clear()

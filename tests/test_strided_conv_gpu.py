@@ -12,7 +12,7 @@ DEV = "cuda"
 
 @pytest.fixture(autouse=True)
 def _strided_on(monkeypatch):
-    monkeypatch.setenv("DPH_CONV_STRIDED", "1")
+    monkeypatch.setenv("DPH_CONV", "dph")
 
 
 def rel_err(a, b):
@@ -24,11 +24,9 @@ def rel_err(a, b):
                                           (3, 3, 256, 256, 14, 14), (1, 2, 256, 512, 14, 14), (1, 2, 64, 128, 7, 9),
                                           (1, 1, 512, 1024, 28, 28)])
 @pytest.mark.parametrize("autocast", [False, True])
-@pytest.mark.parametrize("wgrad", ["dph", "miopen"])
-def test_strided_conv_matches_conv2d(dph_native, monkeypatch, k, B, C, Co, H, W, autocast, wgrad):
+def test_strided_conv_matches_conv2d(dph_native, k, B, C, Co, H, W, autocast):
     from distributed_pytorch_hpc_amd.ops.conv import StridedConv2d, strided_native_ok
 
-    monkeypatch.setenv("DPH_CONV_STRIDED_WGRAD", wgrad)
     torch.manual_seed(7)
     p = k // 2
     conv = StridedConv2d(C, Co, k, 2, p, bias=False).to(DEV).to(memory_format=torch.channels_last)
@@ -56,7 +54,6 @@ def test_strided_conv_stats_epilogue_and_main_grad(dph_native, monkeypatch):
     channels-last main_grad the weight-gradient kernel writes (then accumulates) into it directly."""
     from distributed_pytorch_hpc_amd.ops.conv import StatsSlot, StridedConv2d
 
-    monkeypatch.setenv("DPH_CONV_STRIDED_WGRAD", "dph")
     torch.manual_seed(3)
     conv = StridedConv2d(128, 128, 3, 2, 1, bias=False).to(DEV).to(torch.bfloat16).to(
         memory_format=torch.channels_last)
@@ -100,15 +97,15 @@ def test_downsample_bottleneck_strided_path_matches_miopen(dph_native, monkeypat
         memory_format=torch.channels_last).requires_grad_()
 
     def run(flag):
-        monkeypatch.setenv("DPH_CONV_STRIDED", flag)
+        monkeypatch.setenv("DPH_CONV", flag)
         block.zero_grad(set_to_none=True)
         x.grad = None
         y = block(x)
         y.float().pow(2).mean().backward()
         return y.float().clone(), x.grad.float().clone(), {n: p.grad.float().clone() for n, p in block.named_parameters()}
 
-    y1, gx1, g1 = run("1")
-    y0, gx0, g0 = run("0")
+    y1, gx1, g1 = run("dph")
+    y0, gx0, g0 = run("miopen")
     assert rel_err(y1, y0) < 2e-2
     assert rel_err(gx1, gx0) < 3e-2
     for n in g0:

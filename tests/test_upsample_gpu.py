@@ -103,15 +103,16 @@ def test_unet_fused_up_path_step_matches_reference():
 
     def run(fused, amp=True):
         m.zero_grad(set_to_none=True)
-        old = upsample._ENABLED
-        upsample._ENABLED = fused
+        old = upsample.up_concat_native_ok
+        if not fused:   # the reference three-op sequence
+            upsample.up_concat_native_ok = lambda *a: False
         try:
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
                 out = m(x)
             loss = latitude_weighted_mse(out.float(), y)
             loss.backward()
         finally:
-            upsample._ENABLED = old
+            upsample.up_concat_native_ok = old
         return loss.item(), {k: p.grad.float().clone() for k, p in m.named_parameters()}
 
     l32, g32 = run(False, amp=False)           # fp32 everywhere: the yardstick for both bf16 paths
