@@ -16,6 +16,7 @@ replicas of the same flat parameters (checked bitwise after warm-up), the work p
 """
 from __future__ import annotations
 
+import copy
 from dataclasses import dataclass, field
 from typing import Callable, Optional
 
@@ -307,6 +308,7 @@ def build_resnet_fsdp(args, rank, world, dev, log) -> Workload:
     torch.manual_seed(1234)
     model = resnet(arch, num_classes=1000).to(dev).to(memory_format=torch.channels_last)
     mp = MixedPrecision(torch.bfloat16, torch.bfloat16, torch.bfloat16) if not cpu else None
+    model32 = copy.deepcopy(model) if not cpu else None   # the witness's fp32 reference (freed after it)
     wrapped = FSDP(model, mixed_precision=mp, auto_wrap_policy=ModuleWrapPolicy({BasicBlock, Bottleneck}))
     opt = wrapped.make_optimizer("sgd", lr=0.1, momentum=0.9, weight_decay=1e-5)
     B, R = args.micro_batch, args.image_size
@@ -315,6 +317,8 @@ def build_resnet_fsdp(args, rank, world, dev, log) -> Workload:
     x = torch.rand(B, 3, R, R, device=dev, generator=g, dtype=torch.float32 if cpu else torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (B,), device=dev, generator=g)
+    witness = _first_step_witness(wrapped, model32, x, y) if not cpu else "n/a (CPU)"
+    del model32
 
     def step(i):
         out = wrapped(x)
@@ -330,7 +334,38 @@ def build_resnet_fsdp(args, rank, world, dev, log) -> Workload:
            "optimizer": "SGD m=0.9 wd=1e-5 (scripts/main.py)"}
     return Workload(step, wrapped.engine, "images/sec, ResNet-50 FSDP bf16 on 8 x MI355X", "images/s", world * B,
                     "weak", cfg, replica_group=None, replica_flat=None,
-                    extra={"replica_check": "n/a (FULL_SHARD: no replicated parameters)"})
+                    extra={"replica_check": "n/a (FULL_SHARD: no replicated parameters)",
+                           "first_step_witness": witness})
+
+
+def _first_step_witness(wrapped, model32, x, y) -> dict:
+    """The untrained model's first forward on the benchmark batch three ways, same weights: the framework's bf16
+    kernels, stock ATen / MIOpen in bf16 (reference mode) and stock ATen in fp32.  The loss after many lr-0.1 steps
+    on one batch is chaotic (it moves by whole units between equivalent runs); this is not.  A random-init
+    ResNet-50 in training-mode BatchNorm amplifies rounding (the two bf16 paths each land ~0.1 rel L2 from fp32 in
+    the logits), so the witness is differential: a broken bf16 conv / BN kernel shows up as ``dph_vs_fp32`` well
+    above ``aten_bf16_vs_fp32``.  BatchNorm running statistics take three extra updates (never read in training
+    mode)."""
+    import torch.nn.functional as F
+
+    from ..ops import _lib
+
+    def rel(a, b):
+        return round(((a - b).norm() / b.norm().clamp_min(1e-20)).item(), 5)
+
+    with torch.no_grad():
+        out_dph = wrapped(x).float()
+        _lib.set_reference_mode(True)
+        try:
+            out_bf = wrapped(x).float()
+            out_32 = model32(x.float()).float()
+        finally:
+            _lib.set_reference_mode(False)
+        return {"loss_dph": round(F.cross_entropy(out_dph, y).item(), 5),
+                "loss_aten_bf16": round(F.cross_entropy(out_bf, y).item(), 5),
+                "loss_aten_fp32": round(F.cross_entropy(out_32, y).item(), 5),
+                "logits_dph_vs_fp32": rel(out_dph, out_32), "logits_aten_bf16_vs_fp32": rel(out_bf, out_32),
+                "logits_dph_vs_aten_bf16": rel(out_dph, out_bf)}
 
 
 def build_unet_ddp(args, rank, world, dev, log) -> Workload:
