@@ -6,6 +6,11 @@ the fraction of the window the package power limit (PPT) was active.  Interleave
 (cdna_hip_programming.md rule 24); random operands (rule 25).
 
     python benchmarks/probes/gemm_power.py [--shapes w13,w2,wqkv,w13.dgrad] [--seconds 2] [--rounds 2]
+    python benchmarks/probes/gemm_power.py --shapes w13.wgrad,w2.wgrad --arms tn,blaslt,blaslt_kc
+
+A ``.wgrad`` shape is the weight gradient dW[N, K] = dY^T X over the tokens (dY [T, N], X [T, K]): ``tn`` = the
+framework's CDNA4 kernel (csrc/gemm.hip, bf16 out), ``blaslt`` = hipBLASLt on the same token-major operands,
+``blaslt_kc`` = hipBLASLt on pre-transposed K-contiguous copies (the transposes not counted).
 """
 import argparse
 import json
@@ -21,6 +26,8 @@ from distributed_pytorch_hpc_amd.utils.telemetry import GpuTelemetry  # noqa: E4
 
 SHAPES = {"wqkv": (12288, 4096), "wo": (4096, 4096), "w13": (22016, 4096), "w2": (4096, 11008),
           "output": (32000, 4096), "w13.dgrad": (4096, 22016), "w2.dgrad": (11008, 4096)}
+for _n in ("wqkv", "wo", "w13", "w2", "output"):
+    SHAPES[_n + ".wgrad"] = SHAPES[_n]
 
 
 def main():
@@ -38,12 +45,23 @@ def main():
     out = []
     for name in a.shapes.split(","):
         N, K = SHAPES[name]
+        wg = name.endswith(".wgrad")
         x = torch.randn(a.tokens, K, device="cuda").to(torch.bfloat16)
         w = (0.02 * torch.randn(N, K, device="cuda")).to(torch.bfloat16)
+        if wg:
+            dy = torch.randn(a.tokens, N, device="cuda").to(torch.bfloat16)
+            c = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
+            dyT, xT = dy.t().contiguous(), x.t().contiguous()
         flop = 2.0 * a.tokens * N * K
         for rnd in range(a.rounds):
             for arm in a.arms.split(","):
-                if arm == "blaslt":
+                if wg and arm == "tn":
+                    fn = lambda: ops.gemm_tn_(c, dy, x, False)  # noqa: E731
+                elif wg and arm == "blaslt":
+                    fn = lambda: torch.matmul(dy.t(), x)  # noqa: E731
+                elif wg and arm == "blaslt_kc":
+                    fn = lambda: torch.matmul(dyT, xT.t())  # noqa: E731
+                elif arm == "blaslt":
                     fn = lambda: torch.matmul(x, w.t())  # noqa: E731
                 else:   # the CDNA4 NT kernel (16x16x32; the 32x32x16 form measured in round 5 was removed)
                     fn = lambda: ops.gemm_nt(x, w)  # noqa: E731
@@ -72,6 +90,8 @@ def main():
                 out.append(row)
                 print(json.dumps(row), flush=True)
         del x, w
+        if wg:
+            del dy, c, dyT, xT
     tel.stop()
     if a.json:
         with open(a.json, "w") as fh:
