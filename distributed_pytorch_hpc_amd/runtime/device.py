@@ -9,8 +9,11 @@ those cores are split between the ranks that share the node, so eight ranks neve
 Only sysfs is read (no HIP call): the plan is computed in the launcher process and applied in the spawned child
 before it execs Python (``preexec_fn``), i.e. before anything touches the GPU.
 
-* ``gpus(sysfs)`` -- the node's AMD GPUs in PCI-bus order (the order HIP enumerates them), each with its NUMA node
-  and the CPUs sysfs lists as local to it.
+* ``gpus(sysfs)`` -- the node's AMD GPUs in PCI-bus order (the order HIP enumerates them), each with its NUMA node,
+  the CPUs sysfs lists as local to it and whether this process can open its render node.  A container given a
+  subset of the cards through device cgroups still sees every card in sysfs; HIP enumerates only the cards whose
+  ``/dev/dri/renderD*`` node is present and openable, so those are the ones device ordinals (and
+  *_VISIBLE_DEVICES) index.
 * ``visible_indices(env)`` -- HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES as physical indices.
 * ``plan(nproc, ...)`` -- rank r -> (physical GPU, NUMA node, disjoint CPU set, OMP thread count).
 
@@ -32,6 +35,7 @@ class GpuInfo:
     bdf: str                  # PCI address, e.g. 0000:05:00.0
     numa_node: int            # -1 when the platform reports none
     local_cpus: list = field(default_factory=list)
+    accessible: bool | None = None   # render node present and openable; None: unknown (no /dev/dri to check)
 
 
 @dataclass
@@ -45,6 +49,26 @@ class RankBinding:
 
 def _root(sysfs: str | None) -> str:
     return sysfs or os.environ.get("DPH_SYSFS_ROOT", "/sys")
+
+
+def _devroot(sysfs: str | None) -> str:
+    """/dev for the real sysfs; a fake tree (tests) keeps its device nodes in a sibling ``dev`` directory."""
+    root = _root(sysfs)
+    return "/dev" if os.path.abspath(root) == "/sys" else os.path.join(os.path.dirname(os.path.abspath(root)), "dev")
+
+
+def _render_access(dev: str, devroot: str) -> bool | None:
+    """Whether one of the card's render nodes (``<device>/drm/renderD*``) exists and opens read-write under
+    ``devroot/dri``; None when there is nothing to check against."""
+    dri = os.path.join(devroot, "dri")
+    try:
+        nodes = [n for n in os.listdir(os.path.join(dev, "drm")) if n.startswith("renderD")]
+    except OSError:
+        return None
+    if not nodes or not os.path.isdir(dri):
+        return None
+    return any(os.path.exists(os.path.join(dri, n)) and os.access(os.path.join(dri, n), os.R_OK | os.W_OK)
+               for n in nodes)
 
 
 def _read(path: str, default: str = "") -> str:
@@ -74,6 +98,7 @@ def gpus(sysfs: str | None = None) -> list:
     """AMD GPUs found under <sysfs>/class/drm/card*/device, in PCI-bus order, de-duplicated by PCI address."""
     root = _root(sysfs)
     drm = os.path.join(root, "class", "drm")
+    devroot = _devroot(sysfs)
     seen = {}
     try:
         cards = sorted(c for c in os.listdir(drm) if c.startswith("card") and c[4:].isdigit())
@@ -95,8 +120,8 @@ def gpus(sysfs: str | None = None) -> list:
         cpus = parse_cpulist(_read(os.path.join(dev, "local_cpulist")))
         if not cpus and node >= 0:
             cpus = parse_cpulist(_read(os.path.join(root, "devices", "system", "node", f"node{node}", "cpulist")))
-        seen[bdf] = (node, cpus)
-    return [GpuInfo(i, bdf, n, c) for i, (bdf, (n, c)) in enumerate(sorted(seen.items()))]
+        seen[bdf] = (node, cpus, _render_access(dev, devroot))
+    return [GpuInfo(i, bdf, n, c, a) for i, (bdf, (n, c, a)) in enumerate(sorted(seen.items()))]
 
 
 def visible_indices(env: dict | None = None, n_physical: int | None = None) -> list | None:
@@ -130,8 +155,10 @@ def plan(nproc: int, sysfs: str | None = None, env: dict | None = None, allowed:
             allowed = list(range(os.cpu_count() or 1))
     allowed_set = set(allowed)
     devs = gpus(sysfs)
-    vis = visible_indices(env, len(devs)) if devs else None
-    phys = vis if vis is not None else list(range(len(devs)))
+    # the cards HIP can enumerate: those whose render node this process can open (all of them when unknown)
+    usable = [g.index for g in devs if g.accessible is not False]
+    vis = visible_indices(env, len(usable)) if usable else None
+    phys = [usable[i] for i in vis] if vis is not None else usable
     out = []
     if not devs or len(phys) < nproc:
         share = max(1, len(allowed) // max(nproc, 1))

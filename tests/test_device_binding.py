@@ -114,3 +114,27 @@ def test_launcher_pins_each_rank(tmp_path):
     assert p.returncode == 0, p.stderr
     out = json.loads((tmp_path / "l2" / "rank1.out").read_text().strip().splitlines()[-1])
     assert out["aff"] == sorted(os.sched_getaffinity(0))
+
+
+def test_plan_skips_cards_whose_render_node_is_not_exposed(tmp_path):
+    """A container given GPUs 2 and 5 of 8 through device cgroups (no *_VISIBLE_DEVICES): sysfs lists all eight,
+    /dev/dri holds only two render nodes, and HIP's ordinals 0 / 1 are those two cards."""
+    root = fake_sysfs(tmp_path, TWO_SOCKET)
+    drm = os.path.join(root, "class", "drm")
+    cards = sorted(os.listdir(drm), key=lambda c: os.path.realpath(os.path.join(drm, c, "device")))
+    dri = tmp_path / "dev" / "dri"
+    dri.mkdir(parents=True)
+    for i, c in enumerate(cards):   # PCI order i -> render node renderD(128 + i)
+        (tmp_path / "sys" / "class" / "drm" / c / "device" / "drm" / f"renderD{128 + i}").mkdir(parents=True)
+    for i in (2, 5):
+        (dri / f"renderD{128 + i}").write_text("")
+    g = device.gpus(root)
+    assert [x.accessible for x in g] == [i in (2, 5) for i in range(8)]
+    b = device.plan(2, sysfs=root, env={}, allowed=list(range(8)))
+    assert [x.gpu for x in b] == [2, 5] and [x.numa_node for x in b] == [0, 1]
+    # HIP_VISIBLE_DEVICES indexes the cards the process can open
+    b = device.plan(1, sysfs=root, env={"HIP_VISIBLE_DEVICES": "1"}, allowed=list(range(8)))
+    assert [x.gpu for x in b] == [5]
+    # more ranks than exposed cards: nothing is bound
+    b = device.plan(4, sysfs=root, env={}, allowed=list(range(8)))
+    assert all(x.cpus == [] for x in b)
