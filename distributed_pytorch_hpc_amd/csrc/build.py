@@ -128,7 +128,7 @@ def build(jobs: int | None = None, verbose: bool = False, resource_usage: bool =
     n_hip = sum(1 for f in os.listdir(HERE) if f.endswith(".hip"))
     n_cpp = sum(1 for f in os.listdir(HERE) if f.endswith(".cpp"))
     compiled = sum(1 for ln in ran if "HIPCC" in ln or "CXX" in ln)
-    print(f"[build] gfx950: {compiled} of {n_hip} .hip + {n_cpp} .cpp sources compiled this call"
+    print(f"[build] {ARCH}: {compiled} of {n_hip + n_cpp} sources ({n_hip} .hip + {n_cpp} .cpp) compiled this call"
           f"{' (rest up to date)' if compiled < n_hip + n_cpp else ''}; linked: {any('LINK' in ln for ln in ran)}")
     return OUT
 

@@ -340,7 +340,8 @@ bool convg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, 
 }
 
 void convg_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, const ConvGeo& g, hipStream_t st, float* stats, bool chunk_taps) {
+                int64_t ldc, const ConvGeo& g, hipStream_t st, float* stats, bool chunk_taps, const void* bias,
+                bool bias_bf16) {
   const int cin = chunk_taps ? 8 : (int)(K / g.ntaps);
   // the stride-1 kernel's tile choice: 128-row tiles of 4 waves, 128 columns unless that leaves < 1.5 WG per CU
   const int nmb = (int)cdiv(M, 128);
@@ -348,7 +349,7 @@ void convg_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 #define DPH_CG(BN_, ST_, STATS_, G_)                                                                              \
   hipLaunchKernelGGL((conv3_k<BN_, ST_, 2, STATS_, G_>), dim3(nmb * (int)(N / BN_)), dim3(256), 0, st,          \
                      (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, 0, 0, cin,   \
-                     stats, (const void*)nullptr, g, false)
+                     stats, bias, g, bias_bf16)
   if (chunk_taps) {   // the RGB stem: 64 output channels
     if (stats) DPH_CG(64, 3, true, 2);
     else DPH_CG(64, 3, false, 2);

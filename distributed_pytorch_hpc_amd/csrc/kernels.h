@@ -184,7 +184,8 @@ struct ConvGeo {
 bool convg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g,
                      bool chunk_taps = false);
 void convg_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
-                int64_t ldc, const ConvGeo& g, hipStream_t stream, float* stats = nullptr, bool chunk_taps = false);
+                int64_t ldc, const ConvGeo& g, hipStream_t stream, float* stats = nullptr, bool chunk_taps = false,
+                const void* bias = nullptr, bool bias_bf16 = false);
 // weight gradient C[N, K] (+)= dY[M, N]^T X_gathered[M, K] on c3w_k (K = ntaps * Cin, a multiple of 192)
 bool c3wg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g,
                     bool chunk_taps = false);
@@ -247,6 +248,7 @@ int chsum_partial_blocks(int64_t M, int64_t C);
 void chsum(const void* x, float* part, void* out, int64_t M, int64_t C, int dtype, int out_dtype, hipStream_t stream);
 
 // dst[C, R] = src[R, C]^T (bf16, row-major, leading dims in elements; vector path needs 16-B aligned rows).
+void pad_cols(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_src, int64_t Cp, hipStream_t stream);
 void transpose2d(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_src, int64_t ld_dst,
                  hipStream_t stream);
 // 3x3 convolution input-gradient weight: channels-last w [cout][3][3][cin] -> out [cin][9 taps][cout], taps reversed

@@ -797,9 +797,10 @@ dph::ConvGeo make_geo(at::IntArrayRef geo, int64_t src_rows, bool chunk_taps = f
 }
 
 // C[rows(g), N] (rows stored per g's destination map) = A_gathered[M, K] B[N, K]^T; M = images * Ho * Wo.
-// out (optional): the destination tensor (parity classes of one input gradient share it); stats: BatchNorm partials.
+// out (optional): the destination tensor (parity classes of one input gradient share it); stats: BatchNorm partials;
+// bias (optional): a per-output-channel fp32 / bf16 bias added in the epilogue (before the statistics).
 std::vector<Tensor> convg_nt(const Tensor& A, const Tensor& B, at::IntArrayRef geo, const c10::optional<Tensor>& out,
-                             bool stats, bool chunk_taps) {
+                             bool stats, bool chunk_taps, const c10::optional<Tensor>& bias = c10::nullopt) {
   check_cuda(A, "A");
   c10::DeviceGuard dg(A.device());
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
@@ -835,13 +836,21 @@ std::vector<Tensor> convg_nt(const Tensor& A, const Tensor& B, at::IntArrayRef g
     sp = st.data_ptr<float>();
     res.push_back(st);
   }
+  const void* bp = nullptr;
+  if (bias.has_value()) {
+    TORCH_CHECK((bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16) && bias->numel() == N &&
+                    bias->is_contiguous() && bias->device() == A.device(),
+                "convg_nt: bias must be a contiguous fp32 / bf16 [N] tensor");
+    bp = bias->data_ptr();
+  }
   dph::convg_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), C.stride(0), g,
-                  cur_stream(), sp, chunk_taps);
+                  cur_stream(), sp, chunk_taps, bp, bias.has_value() && bias->scalar_type() == at::kBFloat16);
   return res;
 }
 
-std::vector<Tensor> convg_nt_fresh(const Tensor& A, const Tensor& B, at::IntArrayRef geo, bool stats, bool chunk_taps) {
-  return convg_nt(A, B, geo, c10::nullopt, stats, chunk_taps);
+std::vector<Tensor> convg_nt_fresh(const Tensor& A, const Tensor& B, at::IntArrayRef geo, bool stats, bool chunk_taps,
+                                   const c10::optional<Tensor>& bias) {
+  return convg_nt(A, B, geo, c10::nullopt, stats, chunk_taps, bias);
 }
 
 void convg_nt_out_(const Tensor& A, const Tensor& B, at::IntArrayRef geo, Tensor out) {
@@ -1001,6 +1010,17 @@ std::tuple<Tensor, Tensor> upcat_bwd(const Tensor& dcat, int64_t H, int64_t W, i
 }
 
 // ------------------------------------------------------------------------------------------------ transpose
+// [R, C] bf16 rows (any row stride) -> [R, cols] with zero columns C..cols-1 (cols % 8 == 0)
+Tensor pad_cols(const Tensor& x, int64_t cols) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kBFloat16 && x.stride(1) == 1, "pad_cols: bf16 [R, C] rows");
+  TORCH_CHECK(cols % 8 == 0 && cols >= x.size(1), "pad_cols: cols must be a multiple of 8 and >= C");
+  auto out = at::empty({x.size(0), cols}, x.options());
+  dph::pad_cols(x.data_ptr(), out.data_ptr(), x.size(0), x.size(1), x.stride(0), cols, cur_stream());
+  return out;
+}
+
 Tensor transpose2d(const Tensor& x) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
@@ -1476,8 +1496,9 @@ TORCH_LIBRARY(dph, m) {
   m.def("ts_gemm_nt_stats(Tensor A, Tensor B, int H=0, int W=0, Tensor? pro_ss=None, Tensor? bias=None) -> (Tensor, Tensor)");
   m.def("ts_gemm_tn_(Tensor(a!) C, Tensor A, Tensor B, bool accumulate, int H=0, int W=0, Tensor? pro_ss=None) -> ()");
   m.def("transpose2d(Tensor x) -> Tensor");
+  m.def("pad_cols(Tensor x, int cols) -> Tensor");
   m.def("conv3x3_dgrad_weight(Tensor w) -> Tensor");
-  m.def("convg_nt(Tensor A, Tensor B, int[] geo, bool stats=False, bool chunk_taps=False) -> Tensor[]");
+  m.def("convg_nt(Tensor A, Tensor B, int[] geo, bool stats=False, bool chunk_taps=False, Tensor? bias=None) -> Tensor[]");
   // the parity classes of one strided input gradient write disjoint rows of one shared dx: an in-place op
   m.def("convg_nt_out_(Tensor A, Tensor B, int[] geo, Tensor(a!) out) -> ()");
   m.def("convg_tn_(Tensor(a!) C, Tensor A, Tensor B, int[] geo, bool accumulate, bool chunk_taps=False) -> ()");
@@ -1547,6 +1568,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("ts_gemm_nt_stats", &ts_gemm_nt_stats);
   m.impl("ts_gemm_tn_", &ts_gemm_tn_);
   m.impl("transpose2d", &transpose2d);
+  m.impl("pad_cols", &pad_cols);
   m.impl("conv3x3_dgrad_weight", &conv3x3_dgrad_weight);
   m.impl("convg_nt", &convg_nt_fresh);
   m.impl("convg_nt_out_", &convg_nt_out_);

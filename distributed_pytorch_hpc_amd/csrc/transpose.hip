@@ -3,6 +3,8 @@
 // dX = dY W reads W^T: profiles/gemm_layout_*.json), where torch's strided copy reaches ~1 TB/s.
 // 64 x 64 tiles through LDS (row pitch 66 elements: 33 dwords, so the column-wise reads of the store phase
 // hit 32 different banks); 16-B vector loads and stores on both global sides.
+#include <algorithm>
+
 #include "dph_common.h"
 #include "kernels.h"
 
@@ -54,7 +56,33 @@ __global__ __launch_bounds__(256) void transpose_k(const bf16* __restrict__ src,
     }
   }
 }
+
+// dst[r, 0:C] = src[r, 0:C], dst[r, C:Cp] = 0: one 16-B output chunk per thread (Cp % 8 == 0), source rows of any
+// length and stride (SimpleUNet's 65-channel pixels -> 128-channel rows for the 64-multiple conv kernels).
+__global__ __launch_bounds__(256) void pad_cols_k(const bf16* __restrict__ src, bf16* __restrict__ dst, int64_t R,
+                                                  int64_t C, int64_t ld_src, int64_t Cp) {
+  const int64_t chunks = Cp / 8;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < R * chunks; idx += (int64_t)gridDim.x * 256) {
+    const int64_t r = idx / chunks, c = (idx % chunks) * 8;
+    const bf16* s = src + r * ld_src + c;
+    bf16x8 v;
+    if (c + 8 <= C && ((ld_src | c) & 7) == 0) {
+      v = *reinterpret_cast<const bf16x8*>(s);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = c + j < C ? s[j] : (bf16)0.f;
+    }
+    *reinterpret_cast<bf16x8*>(dst + r * Cp + c) = v;
+  }
+}
 }  // namespace
+
+void pad_cols(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_src, int64_t Cp, hipStream_t st) {
+  if (R == 0) return;
+  const int64_t work = R * (Cp / 8);
+  const unsigned blocks = (unsigned)std::min<int64_t>((work + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(pad_cols_k, dim3(blocks), dim3(256), 0, st, (const bf16*)src, (bf16*)dst, R, C, ld_src, Cp);
+}
 
 void transpose2d(const void* src, void* dst, int64_t R, int64_t C, int64_t ld_src, int64_t ld_dst, hipStream_t st) {
   if (R == 0 || C == 0) return;

@@ -95,6 +95,11 @@ def _bn_act_bwd(dy, y, x, mean, invstd, w, relu, need_dres, need_dwb, xmask_ss=N
             x.new_empty((c,) if need_dwb else (0,), dtype=pdt), x.new_empty((c,) if need_dwb else (0,), dtype=pdt))
 
 
+@register_fake("dph::pad_cols")
+def _pad_cols(x, cols):
+    return x.new_empty((x.shape[0], cols))
+
+
 @register_fake("dph::transpose2d")
 def _transpose2d(x):
     return x.new_empty((x.shape[1], x.shape[0]))
@@ -199,7 +204,7 @@ def _ts_gemm_tn(C, A, B, accumulate, H=0, W=0, pro_ss=None):
 
 
 @register_fake("dph::convg_nt")
-def _convg_nt(A, B, geo, stats=False, chunk_taps=False):
+def _convg_nt(A, B, geo, stats=False, chunk_taps=False, bias=None):
     Hs, Ws, Ho, Wo, Hd, Wd = geo[0], geo[1], geo[2], geo[3], geo[8], geo[9]
     imgs = A.shape[0] // (Hs * Ws)
     N = B.shape[0]

@@ -86,6 +86,20 @@ def bias_grad(param, dy2: torch.Tensor, dtype):
     return _lib.ops().channel_sum(dy2, dtype)   # in the bias's own dtype: no cast kernel
 
 
+def zero_bias_grad(param, n: int, dtype, device):
+    """The gradient of a bias that a following training-mode BatchNorm cancels: exactly zero, so no channel sum runs
+    (SimpleUNet's 14 conv biases: 28 reduction launches per step).  Written into the engine's bucket view when
+    there is one (one fill, engine notified, None returned)."""
+    mg = getattr(param, "main_grad", None) if param is not None else None
+    if mg is not None and _DIRECT:
+        if not getattr(param, "_dph_accum", False):
+            mg.zero_()
+            param._dph_accum = True
+        param._dph_grad_ready()
+        return None
+    return torch.zeros(n, dtype=dtype, device=device)
+
+
 def _wgrad_into_main(w: torch.Tensor, shape, launch) -> bool:
     """Run ``launch(out, accumulate)`` straight into the engine's gradient bucket and notify the engine (no
     autograd gradient, no post-accumulate copy).  False when ``w`` has no engine-owned buffer."""
@@ -143,7 +157,9 @@ def grad_tap(x: torch.Tensor, slot: GradSlot) -> torch.Tensor:
 class StatsSlot:
     """BatchNorm statistics of a 1x1 convolution's output, computed in the convolution's epilogue
     (``ts_gemm_nt_stats``: per-128-row-block [mean | M2 | rows] partials) and consumed by the BatchNorm that
-    follows, which then skips its own statistics pass over the activation."""
+    follows, which then skips its own statistics pass over the activation.  Passing a slot declares that consumer: a
+    training-mode BatchNorm applied directly to this output, so a convolution bias cancels in it and gets an exactly
+    zero gradient (``zero_bias_grad``)."""
 
     __slots__ = ("stats", "rows", "cols")
 
@@ -244,6 +260,9 @@ class _Conv3x3Fn(torch.autograd.Function):
         else:
             y2 = _lib.ops().ts_gemm_nt(x2, wk, H, W)
         ctx.has_bias = bias is not None
+        # a stats slot means a training-mode BatchNorm normalises this output with its own batch statistics: a
+        # per-channel constant (the bias) cancels in BN(y + b) = BN(y), so the bias gradient is exactly zero
+        ctx.bias_cancels = bias is not None and stats_slot is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.bias_param = bias if isinstance(bias, nn.Parameter) else None
         ctx.wgrad = wgrad
@@ -285,7 +304,8 @@ class _Conv3x3Fn(torch.autograd.Function):
                 gw = gk.view(cout, 3, 3, C).permute(0, 3, 1, 2).contiguous()
         db = None
         if ctx.has_bias and ctx.needs_input_grad[3]:
-            db = bias_grad(ctx.bias_param, dy2, ctx.bias_dtype)
+            db = (zero_bias_grad(ctx.bias_param, cout, ctx.bias_dtype, dy.device) if ctx.bias_cancels
+                  else bias_grad(ctx.bias_param, dy2, ctx.bias_dtype))
         return dx, gw, None, db, None
 
 
@@ -558,11 +578,101 @@ def _bias_conv3x3_ok(m: nn.Module, x: torch.Tensor) -> bool:
             and conv3x3_native_ok(x, m.weight))
 
 
+def _edge_conv_input_ok(x: torch.Tensor) -> bool:
+    return (not _miopen() and x.is_cuda and not _lib.reference_mode() and x.dim() == 4
+            and (x.dtype == torch.bfloat16 or _autocast_bf16(x))
+            and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0)
+
+
+def _bias_conv3x3_padded_ok(m: nn.Module, x: torch.Tensor) -> bool:
+    """A stride-1 3x3 biased convolution whose input channel count is not a multiple of 64 (SimpleUNet's 65-channel
+    ERA5 input) on the implicit-GEMM kernel, through a zero-padded copy of the input."""
+    return (tuple(m.kernel_size) == (3, 3) and tuple(m.stride) == (1, 1) and tuple(m.padding) == (1, 1)
+            and tuple(m.dilation) == (1, 1) and m.groups == 1 and m.padding_mode == "zeros" and m.bias is not None
+            and m.in_channels % 64 != 0 and m.in_channels <= 512 and m.out_channels % 64 == 0
+            and _edge_conv_input_ok(x))
+
+
+def _bias_conv1x1_ok(m: nn.Module, x: torch.Tensor) -> bool:
+    return (tuple(m.kernel_size) == (1, 1) and tuple(m.stride) == (1, 1) and tuple(m.padding) == (0, 0)
+            and tuple(m.dilation) == (1, 1) and m.groups == 1 and m.bias is not None and m.in_channels % 64 == 0
+            and not isinstance(m, nn.ConvTranspose2d) and _edge_conv_input_ok(x))
+
+
+class _PadChannelsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cp):
+        B, C, H, W = x.shape
+        xb = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
+        ctx.c, ctx.dtype = C, x.dtype
+        x2 = xb.permute(0, 2, 3, 1).contiguous().view(-1, C)   # a view for channels-last input
+        return _lib.ops().pad_cols(x2, cp).view(B, H, W, cp).permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g[:, :ctx.c].to(ctx.dtype), None
+
+
+def pad_channels(x: torch.Tensor, cp: int) -> torch.Tensor:
+    """Channels-last [B, C, H, W] -> a bf16 channels-last [B, cp, H, W] copy whose channels C..cp-1 are zero (one
+    HIP pass, csrc/transpose.hip pad_cols_k); the gradient is the first C channels of the padded one."""
+    return _PadChannelsFn.apply(x, cp)
+
+
+class _BiasConv1x1Fn(torch.autograd.Function):
+    """Stride-1 1x1 convolution with a bias and any output-channel count (SimpleUNet's 64 -> 65 ``out``) on the
+    gathered implicit GEMM (one tap, bias in the epilogue, csrc/conv3x3.hip): the weight is zero-padded to a multiple
+    of 64 rows and the result is the first Cout columns of the [pixels, Np] product, returned as a strided
+    channels-last view (no slicing copy).  The backward pads dY the same way, so the input gradient (K = Np) and the
+    weight gradient (``ts_gemm_tn_``) run on the 1x1 kernels and the bias gradient is one channel sum."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias):
+        B, C, H, W = x.shape
+        cout = w.shape[0]
+        npad = -(-cout // 64) * 64
+        xb = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
+        x2 = _nhwc2d(xb)
+        w2 = F.pad(w.reshape(cout, C).to(torch.bfloat16), (0, 0, 0, npad - cout))
+        bp = F.pad(bias.float(), (0, npad - cout))
+        y2 = _lib.ops().convg_nt(x2, w2, strided_fwd_geo(H, W, 1, 1, 0), False, False, bp)[0]
+        ctx.save_for_backward(x2, w2)
+        ctx.cfg = (B, C, H, W, cout, npad, w.dtype, bias.dtype)
+        ctx.bias_param = bias if isinstance(bias, nn.Parameter) else None
+        return y2.view(B, H, W, npad)[..., :cout].permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w2 = ctx.saved_tensors
+        B, C, H, W, cout, npad, wdt, bdt = ctx.cfg
+        dy2 = _lib.ops().pad_cols(_nhwc2d(dy.to(torch.bfloat16)), npad)   # [pixels, npad], zero columns past Cout
+        dx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            dx = _lib.ops().ts_gemm_nt(dy2, weight_t(w2)).view(B, H, W, C).permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            gk = torch.empty((npad, C), device=dy.device, dtype=torch.float32)
+            _lib.ops().ts_gemm_tn_(gk, dy2, x2, False)
+            gw = gk[:cout].to(wdt).view(cout, C, 1, 1)
+        if ctx.needs_input_grad[2]:
+            gb = _lib.ops().channel_sum(dy2, torch.float32)[:cout]
+            p = ctx.bias_param
+            mg = getattr(p, "main_grad", None) if p is not None else None
+            if mg is not None and _DIRECT and not getattr(p, "_dph_accum", False) and mg.is_contiguous():
+                mg.view(-1).copy_(gb)   # straight into the engine's bucket (as bias_grad does)
+                p._dph_accum = True
+                p._dph_grad_ready()
+                gb = None
+            else:
+                gb = gb.to(bdt)
+        return dx, gw, gb
+
+
 class BiasConv2d(nn.Conv2d):
     """``nn.Conv2d`` (same parameters and state dict) whose channels-last GPU path computes the bias gradient with
-    the per-channel sum kernel; stride-1 3x3 convolutions with 64-multiple channel counts take the implicit-GEMM
-    kernel of csrc/conv3x3.hip with the bias in its epilogue (when the 3x3 path is on), everything else the stock
-    MIOpen convolution."""
+    the per-channel sum kernel; stride-1 3x3 convolutions take the implicit-GEMM kernel of csrc/conv3x3.hip with the
+    bias in its epilogue (input channels that are not a multiple of 64 through a zero-padded input copy), stride-1 1x1
+    ones the gathered one-tap GEMM (output channels padded to a multiple of 64), everything else the stock MIOpen
+    convolution."""
 
     def forward(self, x, stats_slot: StatsSlot | None = None):
         """``stats_slot``: on the 3x3 kernel path the following BatchNorm's statistics come from this convolution's
@@ -571,6 +681,17 @@ class BiasConv2d(nn.Conv2d):
             _lib.require()
             b = self.bias if self.bias.dtype in (torch.float32, torch.bfloat16) else self.bias.float()
             return _Conv3x3Fn.apply(x, self.weight, stats_slot, b)
+        if _bias_conv3x3_padded_ok(self, x):
+            # SimpleUNet's 65-channel input conv: MIOpen's igemm_fwd / igemm_wrw before (0.117 + 0.095 ms per step,
+            # profiles/r4/unet_c3w_default/); the padded K costs 2x the MFMAs but keeps the BN-statistics epilogue
+            _lib.require()
+            cp = -(-self.in_channels // 64) * 64
+            b = self.bias if self.bias.dtype in (torch.float32, torch.bfloat16) else self.bias.float()
+            wp = F.pad(self.weight, (0, 0, 0, 0, 0, cp - self.in_channels))
+            return _Conv3x3Fn.apply(pad_channels(x, cp), wp, stats_slot, b)
+        if _bias_conv1x1_ok(self, x):
+            _lib.require()
+            return _BiasConv1x1Fn.apply(x, self.weight, self.bias)
         if _bias_conv_ok(self, x):
             return _bias_conv(self, x, False, (0, 0))
         return super().forward(x)

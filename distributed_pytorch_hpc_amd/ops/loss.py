@@ -93,8 +93,12 @@ def latitude_weighted_mse(pred: torch.Tensor, target: torch.Tensor, n_lat_global
     n = n_lat_global or pred.shape[-2]
     if (pred.dim() == 4 and _lib.use_native(pred) and pred.dtype in (torch.bfloat16, torch.float32)
             and target.dtype == pred.dtype and target.shape == pred.shape):
-        fmt = (torch.channels_last if pred.is_contiguous(memory_format=torch.channels_last)
-               and not pred.is_contiguous() else torch.contiguous_format)
+        # channels-last when either operand is laid out channel-innermost (a channels-last tensor, or a strided
+        # channels-last view such as the first Cout columns of a padded 1x1 convolution's output): one compaction
+        # copy at most, never an NHWC <-> NCHW transpose of both fields
+        cl = (pred.is_contiguous(memory_format=torch.channels_last) and not pred.is_contiguous()) or (
+            pred.stride(1) == 1 and pred.shape[1] > 1 and target.is_contiguous(memory_format=torch.channels_last))
+        fmt = torch.channels_last if cl else torch.contiguous_format
         p, t = pred.contiguous(memory_format=fmt), target.contiguous(memory_format=fmt)
         p = p if p.data_ptr() % 16 == 0 else p.clone(memory_format=fmt)
         t = t if t.data_ptr() % 16 == 0 else t.clone(memory_format=fmt)

@@ -893,6 +893,53 @@ def test_bias_conv3x3_matches_conv2d(dph_native, monkeypatch, B, C, Co, H, W):
     assert rel_err(conv.bias.grad, br.grad) < 1e-3
 
 
+@pytest.mark.parametrize("C,Co,k", [(65, 64, 3), (3, 64, 3), (64, 65, 1), (128, 3, 1), (64, 64, 1)])
+@pytest.mark.parametrize("autocast", [False, True])
+def test_bias_conv_edge_channels_match_conv2d(dph_native, monkeypatch, C, Co, k, autocast):
+    """SimpleUNet's edge convolutions off MIOpen: a 3x3 whose input channels are not a multiple of 64 (65-channel
+    ERA5 input: zero-padded input copy + the LDS-DMA kernel with its bias / BN-statistics epilogue) and a biased 1x1
+    with any output-channel count (64 -> 65 ``out``: the one-tap gathered GEMM with the bias in its epilogue, padded
+    weight rows, a strided channels-last result) vs F.conv2d in fp32 on the same bf16-rounded operands."""
+    from distributed_pytorch_hpc_amd.ops.conv import (BiasConv2d, StatsSlot, _bias_conv1x1_ok,
+                                                      _bias_conv3x3_padded_ok)
+
+    monkeypatch.setenv("DPH_CONV", "dph")
+    torch.manual_seed(C + Co + k)
+    conv = BiasConv2d(C, Co, k, padding=k // 2).to(DEV).to(memory_format=torch.channels_last)
+    if not autocast:
+        conv = conv.to(torch.bfloat16)
+    with torch.no_grad():
+        conv.bias.uniform_(-1, 1)
+    x = torch.randn(2, C, 13, 17, device=DEV, dtype=torch.float32 if autocast else torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last).requires_grad_()
+    slot = StatsSlot() if k == 3 else None
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+        assert (_bias_conv3x3_padded_ok if k == 3 else _bias_conv1x1_ok)(conv, x)
+        y = conv(x, stats_slot=slot) if k == 3 else conv(x)
+    g = torch.randn_like(y.float())
+    y.float().backward(g)
+    xr = x.detach().to(torch.bfloat16).float().requires_grad_()
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_()
+    br = conv.bias.detach().float().clone().requires_grad_()
+    yr = torch.nn.functional.conv2d(xr, wr, br, padding=k // 2)
+    yr.backward(g.to(torch.bfloat16).float())
+    assert y.shape == yr.shape
+    assert rel_err(y, yr) < 8e-3
+    assert rel_err(x.grad, xr.grad) < 1e-2
+    assert rel_err(conv.weight.grad, wr.grad) < 1e-2
+    if k == 3:
+        # a stats slot declares a training-mode BN consumer, which cancels the bias: its gradient is exactly zero
+        assert torch.count_nonzero(conv.bias.grad) == 0
+    else:
+        assert rel_err(conv.bias.grad, br.grad) < 1e-2
+    if k == 3:   # the following BatchNorm's statistics from the epilogue: per-channel mean of the biased output
+        st = slot.stats
+        nmb = (y.numel() // Co + 127) // 128
+        rows = st[2 * nmb * Co:]
+        mean = (st[:nmb * Co].view(nmb, Co) * rows[:, None]).sum(0) / rows.sum()
+        assert rel_err(mean, yr.detach().mean((0, 2, 3))) < 1e-2
+
+
 @pytest.mark.parametrize("k", [3, 1])
 def test_bias_conv_bias_grad_into_bucket(dph_native, k):
     """With an engine-owned main_grad the bias gradient (per-channel sum of dY) is written straight into the bucket
