@@ -464,34 +464,10 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_stag_k(const bf16* __restrict_
   }
 }
 
-// ------------------------------------------------------------------------------------------------------------------
-// The same pipeline on v_mfma_f32_16x16x32_bf16.  The chip holds a higher clock on the 16x16x32 shape than on
-// 32x32x16 at equal cycles per FLOP (MI355X_MICROARCH.md 'DVFS give-back' item 7, cdna_hip_programming.md rule 28),
-// so the same output tile per wave (128 x 64 = 8 x 4 tiles of 16 x 16, 128 accumulator VGPRs) is built on both and
-// the faster one by wall time on random data is the default (gemm_tn_set_mfma).  Measured on the
-// Llama-2-7B wgrad shapes (benchmarks/gemm_mfma_ab.py, profiles/gemm_wgrad_mfma16_vs_32.json): 16x16x32 runs
-// 1045-1260 TF vs 1287-1432 TF for 32x32x16 -- twice the MFMA issues and 12 region-address VALU ops per slot
-// (LDS offsets >= 64 KB do not fit the ds_read immediate) outweigh the clock gain here, so 32 stays the default.
-//
-// One 16x16x32 MFMA consumes 32 k-rows = TWO 16-row LDS regions, while DMA, waits and barriers keep the 16-row
-// region granularity of gemm_tn_k (same lead time, same counted vmcnt).  The k order inside an MFMA is free as long
-// as A and B agree, so operand element j < 4 of 16-lane group g comes from row 4g + j of the pair's first region and
-// element j >= 4 from row 4g + j - 4 of its second: each region contributes one ds_read_b64_tr_b16 per fragment
-// (a half-fragment, 4 bf16).  Region R's halves are read in slot R - 1; pair t = regions (2t, 2t+1) runs its 32
-// MFMAs as two halves of 16 (m-blocks 0..3, then 4..7) in slots 2t+1 and 2t+2, so every slot carries 16 MFMAs and
-// 12 transposed reads like gemm_tn_k.  Pair t's fragments live in register set t & 1 (region R writes the low
-// (R even) or high (R odd) half of each).
-//
-// LDS image: 16-B slot s of row r holds logical chunk s ^ ((r & 7) << 1) (low 4 bits; the 256-B half is kept).  A
-// half-wave's transposed read covers rows 4g..4g+3 of two groups (8 consecutive rows) x 2 adjacent chunks: the XOR
-// with distinct even values for the 8 rows maps those 16 (row, chunk) pairs onto 16 distinct bank slots.
-__device__ __forceinline__ bf16x4 tr1(const char* p) {
-  i16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4_g*)p);
-  return __builtin_bit_cast(bf16x4, v);
-}
-
-// Rejected: a 16x16x32 form of this kernel (32x32x16 and its staggered form were faster in-step,
-// profiles/gemm_wgrad_mfma16_vs_32.json, profiles/r4/wgrad_stagger/).
+// Rejected (round 2-4, code removed in round 5): the same pipeline on v_mfma_f32_16x16x32_bf16 (same 128 x 64 tile
+// per wave as 8 x 4 tiles of 16 x 16, pairs of 16-row regions per MFMA): 1045-1260 TF vs 1287-1432 TF for the
+// 32x32x16 kernel on the 7B shapes -- twice the MFMA issues and 12 region-address VALU ops per slot outweighed the
+// higher clock the chip holds on the 16x16x32 shape (profiles/gemm_wgrad_mfma16_vs_32.json, profiles/r4/wgrad_stagger/).
 
 // fp32 split-K slabs W[S][Mb][Nb] -> C band (+ C when accumulating), in C's dtype.  Fixed summation order.
 template <typename OutT, bool ACCUM>
