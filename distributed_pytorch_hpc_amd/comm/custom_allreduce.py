@@ -225,8 +225,22 @@ def probe_crossover(group=None, sizes=(4 << 10, 16 << 10, 64 << 10, 256 << 10, 1
     # agreed on (MIN over ranks) so a path that failed anywhere is off everywhere
     dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
     verified = bool(ok.item() == 1.0)
+    if not verified:
+        drop(group)
     return {"samples": samples, "verified": verified,
             "crossover_bytes": choose_crossover(samples) if verified else 0}
+
+
+def drop(group=None) -> None:
+    """Forget ``group``'s direct-peer instance (after a failed probe; every rank calls it alike): nothing is ever
+    routed to it again, and a barrier timeout it recorded does not surface later as a training-step
+    XgmiAllReduceError (check_health)."""
+    key = _key(group)
+    car = _CACHE.get(key)
+    _CACHE[key] = None
+    _POLICY.pop(key, None)
+    if car is not None:
+        car.close()
 
 
 class XgmiAllReduceError(RuntimeError):

@@ -112,3 +112,26 @@ def test_engine_step_checks_xgmi_health(monkeypatch):
     monkeypatch.setattr(car, "_POLICY", {})
     with pytest.raises(car.XgmiAllReduceError):
         eng.step()
+
+
+def test_failed_probe_drops_the_instance(monkeypatch):
+    """A direct-peer path that fails the crossover probe (wrong sums or a barrier timeout; probe_crossover calls
+    drop() on every rank) is never used again, and its recorded timeout does not stop training at the first engine
+    step."""
+    from distributed_pytorch_hpc_amd.comm import custom_allreduce as car
+
+    class _Bad:
+        closed = False
+
+        def errors(self):
+            return 1
+
+        def close(self):
+            _Bad.closed = True
+
+    monkeypatch.setattr(car, "_CACHE", {"world": _Bad()})
+    monkeypatch.setattr(car, "_POLICY", {"world": 1 << 20})
+    car.drop(None)
+    assert car._CACHE["world"] is None and "world" not in car._POLICY and _Bad.closed
+    car.check_health()   # no error: the failed instance is gone
+    assert car.get_custom_allreduce(None) is None   # cached as unusable (no process group here either)
