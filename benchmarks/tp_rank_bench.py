@@ -26,6 +26,23 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+class _Done:
+    def wait(self, *a, **kw):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+def _null_collectives():
+    def null(*args, async_op=False, **kw):
+        return _Done() if async_op else None
+
+    for name in ("all_gather_into_tensor", "reduce_scatter_tensor", "all_reduce", "all_to_all_single",
+                 "broadcast", "all_gather"):
+        setattr(dist, name, null)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama2-7b")
@@ -39,6 +56,9 @@ def main(argv=None):
     ap.add_argument("--torch-profile", action="store_true",
                     help="after the timed steps, profile one step with torch.profiler and print where device memcpys "
                          "and copy kernels come from (Python call sites)")
+    ap.add_argument("--fake-pg-copies", action="store_true",
+                    help="keep the fake process group's own all-gather (a device memcpy per rank slot) instead of the "
+                         "null collectives that return without touching data")
     ap.add_argument("--stack-dump", type=int, default=0, metavar="S",
                     help="diagnostics: dump every thread's Python stack each S seconds and mark each phase")
     a = ap.parse_args(argv)
@@ -59,6 +79,11 @@ def main(argv=None):
     if a.gemm_nt is not None or a.fused_qkv is not None:
         fused_layers.set_enabled(gemm_nt=a.gemm_nt, qkv=None if a.fused_qkv is None else bool(a.fused_qkv))
     dist.init_process_group("fake", store=FakeStore(), rank=0, world_size=a.tp)
+    if not a.fake_pg_copies:
+        # torch's fake backend implements all_gather_into_tensor as one device memcpy per rank slot
+        # (benchmarks/probes/fake_pg_copies.py): 1 413 copy launches / 13.9 ms per TP = 8 step that a real rank runs
+        # as RCCL kernels instead.  Null collectives keep the timed step to the rank's own compute.
+        _null_collectives()
     tp_group = dist.new_group(list(range(a.tp)))
     dp_group = dist.new_group([0])
     dev = torch.device("cuda", 0)

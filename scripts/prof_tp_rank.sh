@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
-out=$R/gpurun_out/r5/tp_rank
+out=$R/gpurun_out/r5/${TP_OUT:-tp_rank}
 mkdir -p $out
 for tp in 8 4; do
   timeout -k 10 240 python3 -u $R/benchmarks/tp_rank_bench.py --tp $tp --steps 5 > $out/tp${tp}_bench.log 2>&1 || exit 1
