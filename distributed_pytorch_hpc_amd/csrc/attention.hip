@@ -183,6 +183,15 @@ __device__ __forceinline__ void store_rows_lds(char* slab, bf16* base, int64_t r
 // ds_read_b64_tr_b16 transposed reads, and the LDS-DMA source offsets of the staging loads.  Computed once
 // per kernel so the tile loop issues loads with immediate offsets instead of recomputing the XOR swizzle.
 // Row offsets repeat with period KP sub-tiles (32 rows) and tr offsets with period TRP k-steps (16 rows):
+// Lane id as a value the compiler must treat as redefined here: what is derived from it is recomputed at the use
+// instead of being hoisted out of the tile loop and kept live (at 256 VGPRs such hoisted lane constants were spilled,
+// and the reload's compiler-inserted vmcnt(0) drained the in-flight LDS-DMA prefetch right after it was issued).
+__device__ __forceinline__ int opaque_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 // img_off's line permutation depends on (line & 15) only, so advancing 16 lines is a pure byte offset.
 template <int HD, int NT_ = 256>
 struct KVTilePlan {
@@ -254,17 +263,24 @@ struct KVTilePlan {
   // of i = 0, so its source row is prow + i NT / NC and its chunk column pch: ONE row / column pair per lane (a per-i
   // table is spilled around the tile loop at high register pressure, and hipcc's vmcnt(0) for the reload would drain
   // the in-flight DMA).
+  // RECOMPUTE: the row / column pair is recomputed from an opaque lane id per call (a few VALU) rather than kept
+  // live across the tile loop -- the dQ kernel spilled the hoisted per-instruction offsets and each reload's vmcnt(0)
+  // drained the DMA issued just before it; the forward (no spills) keeps the pair from init_async().
   static_assert(NT % 256 == 0, "stage_async assumes whole 16-line swizzle periods per instruction");
   static constexpr int RSTEP = NT / NC;   // rows between a lane's consecutive instructions
-  int prow, pch;
-  __device__ __forceinline__ void init_async() {
-    const int L = threadIdx.x, line = L >> 4, slot = L & 15;
+  int prow0 = 0, pch0 = 0;
+  __device__ __forceinline__ static void lane_chunk(int L, int& prow, int& pch) {
+    const int line = L >> 4, slot = L & 15;
     const int F = (line << 4) + (slot ^ (((line & 3) << 2) | ((line >> 2) & 3)));
     prow = F / NC;
     pch = (F % NC) * 8;
   }
+  __device__ __forceinline__ void init_async() { lane_chunk(threadIdx.x, prow0, pch0); }
+  template <bool RECOMPUTE = false>
   __device__ __forceinline__ void stage_async(unsigned lds_w, const bf16* kp, const bf16* vp, int64_t k_ss,
                                               int64_t v_ss, int k0, int Sk) const {
+    int prow = prow0, pch = pch0;
+    if constexpr (RECOMPUTE) lane_chunk(opaque_tid(), prow, pch);
     // wave-uniform by construction; readfirstlane keeps the bases in SGPRs inside divergent callers
     const bf16* kt = uniform_ptr(kp + (int64_t)k0 * k_ss);
     const bf16* vt = uniform_ptr(vp + (int64_t)k0 * v_ss);
@@ -287,30 +303,26 @@ struct KVTilePlan {
   }
 };
 
-// glds_stage issued through lds_dma16 (see KVTilePlan::stage_async) with the per-lane swizzled source row/chunk
-// hoisted out of the tile loop: ROWS x NC chunks of rows [row0, row0 + ROWS) of a strided tile, rows past `nvalid`
-// re-reading the last valid one.  `lds_w` = lds_addr(img + wave * 1 KiB).
+// glds_stage issued through lds_dma16 (see KVTilePlan::stage_async): ROWS x NC chunks of rows [row0, row0 + ROWS) of a
+// strided tile, rows past `nvalid` re-reading the last valid one.  `lds_w` = lds_addr(img + wave * 1 KiB).  A lane's
+// source row / chunk are recomputed from an opaque lane id per call (a few VALU) instead of a hoisted per-lane table;
+// with NT a multiple of 256 instruction i's chunk lies 16 image lines (RSTEP rows) below instruction 0's.
 template <int NC, int ROWS, int NT>
 struct RowStagePlan {
-  static constexpr int CHUNKS = ROWS * NC, NI = (CHUNKS + NT - 1) / NT;
-  int prow[NI], pch[NI];
-  __device__ __forceinline__ void init() {
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int L = threadIdx.x + NT * i, line = L >> 4, slot = L & 15;
-      const int F = (line << 4) + (slot ^ (((line & 3) << 2) | ((line >> 2) & 3)));
-      prow[i] = F / NC;
-      pch[i] = (F % NC) * 8;
-    }
-  }
+  static constexpr int CHUNKS = ROWS * NC, NI = (CHUNKS + NT - 1) / NT, RSTEP = NT / NC;
+  static_assert(NT % 256 == 0, "RowStagePlan assumes whole 16-line swizzle periods per instruction");
+  __device__ __forceinline__ void init() {}
   __device__ __forceinline__ void stage(unsigned lds_w, const bf16* base, int64_t rstride, int row0,
                                         int nvalid) const {
+    const int tid = opaque_tid(), line = tid >> 4, slot = tid & 15;
+    const int F = (line << 4) + (slot ^ (((line & 3) << 2) | ((line >> 2) & 3)));
+    const int prow = F / NC, pch = (F % NC) * 8;
     const int rmax = nvalid - 1 - row0;
     const bf16* t = uniform_ptr(base + (int64_t)row0 * rstride);   // wave-uniform: keep it in SGPRs
 #pragma unroll
     for (int i = 0; i < NI; ++i)
-      if (CHUNKS % NT == 0 || (int)threadIdx.x + NT * i < CHUNKS)
-        lds_dma16(t, (unsigned)(((int64_t)min(prow[i], rmax) * rstride + pch[i]) * 2), lds_w + NT * i * 16);
+      if (CHUNKS % NT == 0 || tid + NT * i < CHUNKS)
+        lds_dma16(t, (unsigned)(((int64_t)min(prow + i * RSTEP, rmax) * rstride + pch) * 2), lds_w + NT * i * 16);
   }
 };
 
@@ -616,24 +628,40 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
     for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
   const f32x16 zacc = {};
 
-  // hoisted per-lane LDS offsets
-  int qro[KS];
+  // per-lane LDS offsets.  For HD = 128 (NC = 16, one 256-B image line per row) every offset is one per-lane base
+  // XOR / plus compile-time constants: the row read of chunk 2kk + h is qb ^ (kk << 5), and the transposed read of
+  // (dt, hi) is tb ^ (dt << 6) ^ (hi << 5) + hi * 2048 (img_off's swizzle f(row) XORs bits 4-7 only, and row + 8
+  // flips bit 1 of f).  Two registers instead of 16 (at 256 VGPRs the tables were spilled around the tile loop).
+  // The two bases are recomputed from an opaque lane id at the top of every tile (a few VALU), so they are not
+  // carried across the loop at all.
+  constexpr bool XOFS = NC == 16;
+  int qro[XOFS ? 1 : KS];
 #pragma unroll
-  for (int kk = 0; kk < KS; ++kk) qro[kk] = img_off<NC>(l32, kk * 2 + h);
+  for (int kk = 0; kk < (XOFS ? 1 : KS); ++kk) qro[kk] = img_off<NC>(l32, kk * 2 + h);
+  auto qofs = [&](int kk) { return XOFS ? qro[0] ^ (kk << 5) : qro[kk]; };
+
   auto kofs = [&](int kk) {
-    return KSHARE ? qro[kk] + wid * 32 * NC * 16 : img_off<NC>(wid * 32 + l32, kk * 2 + h);
+    return KSHARE ? qofs(kk) + wid * 32 * NC * 16 : img_off<NC>(wid * 32 + l32, kk * 2 + h);
   };
-  int tro[TRADD ? 1 : 2][DT][2];
+  int tro[XOFS ? 1 : (TRADD ? 1 : 2)][XOFS ? 1 : DT][XOFS ? 1 : 2];
 #pragma unroll
-  for (int ks = 0; ks < (TRADD ? 1 : 2); ++ks)
+  for (int ks = 0; ks < (XOFS ? 1 : (TRADD ? 1 : 2)); ++ks)
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
+    for (int dt = 0; dt < (XOFS ? 1 : DT); ++dt)
 #pragma unroll
-      for (int hi = 0; hi < 2; ++hi)
+      for (int hi = 0; hi < (XOFS ? 1 : 2); ++hi)
         tro[ks][dt][hi] = img_off<NC>(ks * 16 + 4 * (g >> 1) + tq + 8 * hi, dt * 4 + 2 * (g & 1) + (tp >> 1)) +
                           8 * (tp & 1);
   auto trofs = [&](int ks, int dt, int hi) {
+    if constexpr (XOFS) return (tro[0][0][0] ^ (dt << 6) ^ (hi << 5)) + hi * 2048 + ks * 16 * NC * 16;
     return TRADD ? tro[0][dt][hi] + ks * 16 * NC * 16 : tro[ks][dt][hi];
+  };
+  auto rebase = [&]() {
+    if constexpr (XOFS) {
+      const int ln = opaque_tid() & 63, lh = ln >> 5, lg = ln >> 4, ltq = (ln & 15) >> 2, ltp = ln & 3;
+      qro[0] = img_off<NC>(ln & 31, lh);
+      tro[0][0][0] = img_off<NC>(4 * (lg >> 1) + ltq, 2 * (lg & 1) + (ltp >> 1)) + 8 * (ltp & 1);
+    }
   };
 
   int qstart = 0;
@@ -651,6 +679,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
   const unsigned lds_q = lds_addr(Qbuf + wid * 64 * 16);
   float st_lse = 0.f, st_del = 0.f;
   unsigned st_rk = 0u;
+  // lse / delta rows of this (batch, kv head)'s GQA group: grp * Sq floats from the group's first query head
+  const int64_t grow = ((int64_t)b * p.Hq + (int64_t)hk * grp) * p.Sq;
+  const auto lse_rs = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(p.lse + grow), 0, grp * p.Sq * 4, 0x00020000);
+  const auto del_rs = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(P.delta + grow), 0, grp * p.Sq * 4, 0x00020000);
   const unsigned dthr = DROP ? attn_drop_thr(p.drop_p) : 0u;
   const float drs = DROP ? 1.f / (1.f - p.drop_p) : 1.f;
   auto stage = [&](int it, int buf) {
@@ -661,12 +693,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
     const unsigned ql = lds_q + buf * 2 * QIMG;
     qplan.stage(ql, qp, p.q_ss, qt0, p.Sq);
     qplan.stage(ql + QIMG, dop, P.do_ss, qt0, p.Sq);
-    if (threadIdx.x < BMQ) {
-      const int q = min(qt0 + (int)threadIdx.x, p.Sq - 1);   // rows past Sq: finite, masked by the caller
-      const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + q;
-      st_lse = p.lse[idx];
-      st_del = P.delta[idx];
-      if constexpr (DROP) st_rk = attn_row_key(p.drop_seed, (unsigned)(b * p.Hq + hq), (unsigned)(qt0 + threadIdx.x));
+    const int tid = opaque_tid();
+    if (tid < BMQ) {
+      // buffer loads off the GQA group's lse / delta rows (scalar resources built once, below): only the 32-bit lane
+      // offset is a VGPR (a per-lane 64-bit address was spilled and its reload drained the Q / dO prefetch above)
+      const int q = min(qt0 + tid, p.Sq - 1);   // rows past Sq: finite, masked by the caller
+      const int o = ((it / nqt_head) * p.Sq + q) * 4;
+      st_lse = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(lse_rs, o, 0, 0));
+      st_del = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(del_rs, o, 0, 0));
+      if constexpr (DROP) st_rk = attn_row_key(p.drop_seed, (unsigned)(b * p.Hq + hq), (unsigned)(qt0 + tid));
     }
   };
   // Row constants: without dropout they become the INITIAL accumulators of the S and dP chains (S' = Q K^T - lse/scale,
@@ -714,13 +749,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
     if (!(CAUSAL && key0 > qt0 + BMQ - 1 + off)) {
       const float* ls = lse_s + buf * BMQ;
       const float* ds = del_s + buf * BMQ;
+      rebase();
       __builtin_amdgcn_s_setprio(1);
-      f32x16 s = mfma32(lds_b128(Ql, qro[0]), lds_b128(Kimg, kofs(0)), RINIT ? row_init(ls) : zacc);
-      f32x16 dp = mfma32(lds_b128(Ol, qro[0]), vf[0], RINIT ? row_init(ds) : zacc);
+      f32x16 s = mfma32(lds_b128(Ql, qofs(0)), lds_b128(Kimg, kofs(0)), RINIT ? row_init(ls) : zacc);
+      f32x16 dp = mfma32(lds_b128(Ol, qofs(0)), vf[0], RINIT ? row_init(ds) : zacc);
 #pragma unroll
       for (int kk = 1; kk < KS; ++kk) {
-        s = mfma32(lds_b128(Ql, qro[kk]), lds_b128(Kimg, kofs(kk)), s);
-        dp = mfma32(lds_b128(Ol, qro[kk]), vf[kk], dp);
+        s = mfma32(lds_b128(Ql, qofs(kk)), lds_b128(Kimg, kofs(kk)), s);
+        dp = mfma32(lds_b128(Ol, qofs(kk)), vf[kk], dp);
       }
       __builtin_amdgcn_s_setprio(0);
       // wave-uniform: only diagonal / ragged tiles pay for the selects (masked scores -> -inf -> P = 0)
@@ -877,7 +913,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
     for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
   const f32x16 zacc = {};
 
-  if (ntiles > 0) plan.stage_async(lds_w, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
+  if (ntiles > 0) plan.template stage_async<true>(lds_w, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
   wait_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
 
@@ -961,7 +997,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < ntiles)
-      plan.stage_async(lds_w + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
+      plan.template stage_async<true>(lds_w + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
     const char* Kl = smem + buf * 2 * TILE;
     if (t < wtiles) {
       const int k0 = t * BN;

@@ -58,234 +58,26 @@ __device__ __forceinline__ void glds16(const char* sbase, unsigned voff, unsigne
 template <int N>
 __device__ __forceinline__ void wait_vm() { wait_vmcnt<N>(); }
 
-// Pipeline: one K-step (64 tokens) = 4 phases of 16 k-rows.  Phase P's operands live in LDS region
-// R = P & 7 (tile parity x 16-row region; A rows at +0, B rows at +8 KB of a 16-KB region) and are filled by DMA
-// "pair P" (one 16-B global_load_lds per thread per operand, inline asm: see glds16).  In slot P every wave
-//   1. waits (counted vmcnt) for its share of pair P+1 and meets the others at a raw s_barrier,
-//   2. issues pair P+4 (same region of the next tile; that region was last read in phase P-4),
-//   3. issues the transposed LDS reads of phase P+1 into the other fragment register set,
-//   4. runs the 8 MFMAs of phase P (operands read one slot earlier) -- the LDS latency of step 3 and the DMA
-//      latency of step 2 hide behind them.
-// DMA pairs are issued in phase order, so the pairs allowed in flight at step 1 are the ones issued after
-// pair P+1: min(NP - P - 2, 2) of them.  Slots are unrolled 8 at a time (two K-steps) so every region index
-// is a compile-time constant.
-#define DPH_GEMM_REGIONS(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
-
-template <typename OutT, bool ACCUM, bool LDS_EPI = true>
-__global__ __launch_bounds__(GNT, 1) void gemm_tn_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                     OutT* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                     int64_t ldb, int64_t ldc, int64_t cstride) {
-  // split-K (gridDim.y > 1): slice blockIdx.y reduces rows [y*K, (y+1)*K) of A / B into its own C slab
-  A += (int64_t)blockIdx.y * K * lda;
-  B += (int64_t)blockIdx.y * K * ldb;
-  C += (int64_t)blockIdx.y * cstride;
-  __shared__ __attribute__((aligned(1024))) char lds[8 * 16384];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm = wid >> 2, wn = wid & 3;                          // 2 x 4 waves
-  const int h = lane >> 5, l32 = lane & 31;
-  const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
-
-  // ---- XCD-aware, grouped tile order ----
-  const int tiles_m = (M + GBM - 1) / GBM, tiles_n = (N + GBN - 1) / GBN, nwg = tiles_m * tiles_n;
-  int tm, tn;
-  grouped_tile(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
-  const int m0 = tm * GBM, n0 = tn * GBN;
-
-  // ---- per-lane transposed-read offsets within a region (hi half = +8 rows = +4096 bytes) ----
-  const int x = 2 * (g & 1) + (tp >> 1);
-  const int krow = 4 * (g >> 1) + tq;                             // krow & 3 == tq
-  const int base = krow * ROWB + 8 * (tp & 1);
-  int aoff[4], boff[2];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt) aoff[mt] = base + (wm << 8) + ((4 * (mt ^ tq) + x) << 4);
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
-    boff[nt] = 8192 + base + ((wn >> 1) << 8) + ((4 * ((((wn & 1) << 1) | nt) ^ tq) + x) << 4);
-
-  // ---- per-lane DMA source offsets: chunk tid of a 16-row region (row tid/32, swizzled slot) ----
-  const int srow = threadIdx.x >> 5, lr = (threadIdx.x >> 4) & 1, sslot = threadIdx.x & 15;
-  const int sch = (lr << 4) | (sslot ^ ((srow & 3) << 2));
-  // edge tiles: a chunk past M / N re-reads the last valid chunk (its columns are never stored)
-  const int colA = min(sch * 8, M - 8 - m0), colB = min(sch * 8, N - 8 - n0);
-  const unsigned voffA = (unsigned)((srow * lda + colA) * 2), voffB = (unsigned)((srow * ldb + colB) * 2);
-  const char* Ag = reinterpret_cast<const char*>(A + m0);        // uniform
-  const char* Bg = reinterpret_cast<const char*>(B + n0);
-  const int64_t stepA = 16 * lda * 2, stepB = 16 * ldb * 2;       // bytes per 16-row region
-  const unsigned lds_wave = __builtin_amdgcn_readfirstlane(
-      (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds + (threadIdx.x >> 6) * 1024);
-
-  auto region = [&](auto RI) -> char* { return lds + decltype(RI)::value * 16384; };
-  auto dma_pair = [&](int P, auto RI) {
-    const unsigned d = lds_wave + decltype(RI)::value * 16384;
-    glds16(Ag + P * stepA, voffA, d);
-    glds16(Bg + P * stepB, voffB, d + 8192);
-  };
-  auto read_phase = [&](auto RI, bf16x8 (&af)[4], bf16x8 (&bfr)[2]) {
-    const char* rg = region(RI);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) af[mt] = tr2(rg, aoff[mt], aoff[mt] + 8 * ROWB);
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) bfr[nt] = tr2(rg, boff[nt], boff[nt] + 8 * ROWB);
-  };
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.f;
-
-  auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[2]) {
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
-  };
-
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  const int NP = (K / GBK) * 4;
-  // prologue: the first tile (pairs 0..3 -> regions 0..3), then phase 0's fragments
-  dma_pair(0, I0{});
-  dma_pair(1, I1{});
-  dma_pair(2, I2{});
-  dma_pair(3, I3{});
-  wait_vm<6>();
-  __builtin_amdgcn_s_barrier();
-  bf16x8 af0[4], bf0[2], af1[4], bf1[2];
-  read_phase(I0{}, af0, bf0);
-
-  // Slot S of a two-tile super-step (phase P = P0 + S, region S, operands in register set S & 1).  Every
-  // flag is a compile-time constant so the loop body has no branches (the waitcnt pass would otherwise
-  // merge states pessimistically at the joins and wait lgkmcnt(0) before the MFMAs).
-  //   WAIT: vmcnt to wait for (-1: none, last phase), DMA: issue pair P+4, READ: prefetch phase P+1.
-  auto slot = [&](int P0, auto SI, auto WAITI, auto DMAI, auto READI, bf16x8 (&afc)[4], bf16x8 (&bfc)[2],
-                  bf16x8 (&afn)[4], bf16x8 (&bfn)[2]) {
-    constexpr int S = decltype(SI)::value, WAIT = decltype(WAITI)::value;
-    constexpr bool DMA = decltype(DMAI)::value, READ = decltype(READI)::value;
-    if constexpr (WAIT >= 0) {
-      wait_vm<(WAIT >= 0 ? WAIT : 0)>();
-      __builtin_amdgcn_s_barrier();
-    }
-    if constexpr (DMA) dma_pair(P0 + S + 4, std::integral_constant<int, (S + 4) & 7>{});
-    if constexpr (READ) read_phase(std::integral_constant<int, (S + 1) & 7>{}, afn, bfn);
-    mma(afc, bfc);
-    if constexpr (READ) {
-      // interleave the 12 prefetch reads with the 8 MFMAs (2 reads per MFMA) instead of issuing all reads
-      // first: a burst of 12 ds_reads from 8 waves backs up the LDS issue queue and delays the MFMAs
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // 2 DS reads
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);   // keep the next slot's reads out of this slot (register pressure)
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  using W4 = std::integral_constant<int, 4>;
-  using W2 = std::integral_constant<int, 2>;
-  using W0 = std::integral_constant<int, 0>;
-  using WN = std::integral_constant<int, -1>;
-#define DPH_S(i) std::integral_constant<int, i>{}
-  int P0 = 0;
-  // steady state: all 8 slots issue their DMA pair (P + 4 < NP) and keep two pairs in flight
-  for (; P0 + 12 <= NP; P0 += 8) {
-    slot(P0, DPH_S(0), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
-    slot(P0, DPH_S(1), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
-    slot(P0, DPH_S(2), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
-    slot(P0, DPH_S(3), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
-    slot(P0, DPH_S(4), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
-    slot(P0, DPH_S(5), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
-    slot(P0, DPH_S(6), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
-    slot(P0, DPH_S(7), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
-  }
-  if (NP - P0 == 8) {   // last two K-steps: DMA only for the final tile, then drain
-    slot(P0, DPH_S(0), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
-    slot(P0, DPH_S(1), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
-    slot(P0, DPH_S(2), W4{}, T_{}, T_{}, af0, bf0, af1, bf1);
-    slot(P0, DPH_S(3), W4{}, T_{}, T_{}, af1, bf1, af0, bf0);
-    slot(P0, DPH_S(4), W4{}, F_{}, T_{}, af0, bf0, af1, bf1);
-    slot(P0, DPH_S(5), W2{}, F_{}, T_{}, af1, bf1, af0, bf0);
-    slot(P0, DPH_S(6), W0{}, F_{}, T_{}, af0, bf0, af1, bf1);
-    slot(P0, DPH_S(7), WN{}, F_{}, F_{}, af1, bf1, af0, bf0);
-  } else {              // last K-step
-    slot(P0, DPH_S(0), W4{}, F_{}, T_{}, af0, bf0, af1, bf1);
-    slot(P0, DPH_S(1), W2{}, F_{}, T_{}, af1, bf1, af0, bf0);
-    slot(P0, DPH_S(2), W0{}, F_{}, T_{}, af0, bf0, af1, bf1);
-    slot(P0, DPH_S(3), WN{}, F_{}, F_{}, af1, bf1, af0, bf0);
-  }
-#undef DPH_S
-
-  // ---- epilogue: register i of tile (mt, nt) holds C[row (i&3) + 8(i>>2) + 4h][col l32] ----
-  if constexpr (!ACCUM && LDS_EPI) {
-    // Through LDS (free after the main loop): the tile goes out as 16-B row segments -- 16 (bf16) / 32 (fp32, two
-    // 128-row passes) vector stores per thread instead of 128 scalar 2- / 4-byte stores per lane, which left the
-    // epilogue store-issue-bound.  (ACCUM keeps the scalar path: one rounding of old + acc.)
-    constexpr int VE = 16 / (int)sizeof(OutT);                 // elements per 16-B segment
-    constexpr int PR = (int)(sizeof(OutT) == 2 ? 256 : 128);   // rows per pass (128 KB of LDS)
-    constexpr int NPASS = 256 / PR, SPR = 256 / VE;            // passes, segments per row
-    OutT* ct = reinterpret_cast<OutT*>(lds);
-#pragma unroll
-    for (int pass = 0; pass < NPASS; ++pass) {
-      __syncthreads();   // the main loop's / previous pass's LDS reads are done
-      if (NPASS == 1 || wm == pass) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const int r = (NPASS == 1 ? wm * 128 : 0) + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-              ct[r * 256 + wn * 64 + nt * 32 + l32] = (OutT)acc[mt][nt][i];
-            }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int c = threadIdx.x; c < PR * SPR; c += GNT) {
-        const int r = c / SPR, seg = c % SPR;
-        const int row = m0 + pass * PR + r, col = n0 + seg * VE;
-        if (row < M && col < N)   // N % 8 == 0: a segment is all in or all out
-          *reinterpret_cast<u32x4*>(C + (int64_t)row * ldc + col) =
-              *reinterpret_cast<const u32x4*>(ct + r * 256 + seg * VE);
-      }
-    }
-  } else {
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int col = n0 + wn * 64 + nt * 32 + l32;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int row = m0 + wm * 128 + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (row >= M || col >= N) continue;
-          OutT* p = C + (int64_t)row * ldc + col;
-          *p = (OutT)(ACCUM ? acc[mt][nt][i] + (float)*p : acc[mt][nt][i]);
-        }
-      }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------------------------
-// Staggered variant of gemm_tn_k (gemm_tn_set_mfma(33)).  Waves 4..7 run one barrier behind
-// waves 0..3, so on every SIMD one wave issues its slot's MFMAs while its partner waits at the barrier, issues its
-// DMA pair and transposed reads (the ping-pong of gemm_nt.hip); in lockstep both waves of a SIMD reach the barrier
-// together and the matrix pipe idles while they wait (PMC on the w13 shape: SQ_WAIT_ANY 40 % of wave cycles, MFMA
-// busy 0.74).  The stagger makes an early wave's read of region S+1 at its slot S race the LATE waves' share of that
-// region's DMA, so the pipeline is one pair deeper: slot S retires pair S+2 (not S+1) before its barrier and issues
-// pair S+5 (not S+4); regions in use at once: S..S+5 = 6 of the 8.  WAR: pair S+5 overwrites pair S-3's region,
-// whose last reader (a late wave, in its slot S-4 = the early waves' slot S-3) is two barriers back.
+// Pipeline: one K-step (64 tokens) = 4 phases of 16 k-rows.  Phase P's operands live in LDS region R = P & 7 (tile
+// parity x 16-row region; A rows at +0, B rows at +8 KB of a 16-KB region) and are filled by DMA "pair P" (one 16-B
+// global_load_lds per thread per operand, inline asm: see glds16).  In slot S every wave retires its share of pair
+// S+2 (counted vmcnt), meets the others at a raw s_barrier, issues pair S+5, and runs the 8 MFMAs of region S while the
+// transposed reads of region S+1 go to the other fragment register set.
+//
+// Waves 4..7 run one barrier behind waves 0..3, so on every SIMD one wave issues its slot's MFMAs while its partner
+// waits at the barrier, issues its DMA pair and transposed reads (the ping-pong of gemm_nt.hip); in lockstep (the
+// round-2..4 gemm_tn_k, deleted in round 5) both waves of a SIMD reached the barrier together and the matrix pipe idled
+// while they waited (PMC on the w13 shape: SQ_WAIT_ANY 40 % of wave cycles, MFMA busy 0.74 vs 0.79 staggered,
+// profiles/r5/wgrad_power/).  The stagger makes an early wave's read of region S+1 at its slot S race the LATE waves'
+// share of that region's DMA, hence the pipeline depth: slot S retires pair S+2 (not S+1) and issues pair S+5 (not
+// S+4); regions in use at once: S..S+5 = 6 of the 8.  WAR: pair S+5 overwrites pair S-3's region, whose last reader
+// (a late wave, in its slot S-4 = the early waves' slot S-3) is two barriers back.
 // No tail code: a pair index past the last one re-loads the last pair (finite data) into a region whose contents are
 // never multiplied, so every slot has the same DMA / counted wait / read and the loop body is one 8-slot block (plus
-// one 4-slot block for an odd K-tile count) -- the tail sequences of gemm_tn_k cost ~400 VGPR spills and a
+// one 4-slot block for an odd K-tile count) -- tail sequences cost the lockstep kernel ~400 VGPR spills and a
 // vmcnt(0) drain per iteration where the waitcnt pass merged the spill reloads into the loop.
-template <typename OutT, bool ACCUM>
+// LDS_EPI: the 16-B LDS-staged epilogue (C 16-B aligned with a 16-B row pitch); otherwise one store per element.
+template <typename OutT, bool ACCUM, bool LDS_EPI = true>
 __global__ __launch_bounds__(GNT, 1) void gemm_tn_stag_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                          OutT* __restrict__ C, int M, int N, int K, int64_t lda,
                                                          int64_t ldb, int64_t ldc, int64_t cstride) {
@@ -417,8 +209,10 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_stag_k(const bf16* __restrict_
   if (!late) __builtin_amdgcn_s_barrier();   // balance the stagger
   wait_vm<0>();
 
-  // ---- epilogue: as gemm_tn_k (LDS-staged 16-B row segments; ACCUM: per element) ----
-  if constexpr (!ACCUM) {
+  // ---- epilogue: register i of tile (mt, nt) holds C[row (i&3) + 8(i>>2) + 4h][col l32].  Through LDS (free after
+  // the main loop) the tile leaves as 16-B row segments -- 16 (bf16) / 32 (fp32, two 128-row passes) vector stores per
+  // thread instead of 128 scalar stores per lane; ACCUM keeps the per-element path (one rounding of old + acc) ----
+  if constexpr (!ACCUM && LDS_EPI) {
     constexpr int VE = 16 / (int)sizeof(OutT);
     constexpr int PR = (int)(sizeof(OutT) == 2 ? 256 : 128);
     constexpr int NPASS = 256 / PR, SPR = 256 / VE;
@@ -458,7 +252,7 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_stag_k(const bf16* __restrict_
           const int row = m0 + wm * 128 + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
           if (row >= M || col >= N) continue;
           OutT* pp = C + (int64_t)row * ldc + col;
-          *pp = (OutT)(acc[mt][nt][i] + (float)*pp);
+          *pp = (OutT)(ACCUM ? acc[mt][nt][i] + (float)*pp : acc[mt][nt][i]);
         }
       }
   }
@@ -489,7 +283,6 @@ __global__ __launch_bounds__(256) void gemm_split_reduce_k(const float* __restri
   }
 }
 
-int g_gemm_tn_mfma = 0;   // 0: the default (kGemmTnDefaultMfma); tests force 32 / 33 through gemm_tn_set_mfma
 int g_gemm_tn_tail = 0;   // tail split: 0 = device CU count, > 0 = that many CUs (tests), < 0 = off
 
 int gemm_tn_cus() {
@@ -506,9 +299,7 @@ int gemm_tn_cus() {
 
 }  // namespace
 
-int gemm_tn_mfma() { return g_gemm_tn_mfma ? g_gemm_tn_mfma : kGemmTnDefaultMfma; }
 
-void gemm_tn_set_mfma(int shape) { g_gemm_tn_mfma = (shape == 32 || shape == 33) ? shape : 0; }
 
 void gemm_tn_set_tail(int cus) { g_gemm_tn_tail = cus; }
 
@@ -563,7 +354,6 @@ GemmTnPlan gemm_tn_plan(int64_t M, int64_t N, int64_t K) {
 void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
              int64_t ldc, int out_dtype, bool accumulate, hipStream_t st, const GemmTnPlan* plan,
              float* workspace) {
-  const bool stag = gemm_tn_mfma() == 33;
   const size_t lds = 0;   // static: 8 x 16 KB regions
   const dim3 block(GNT);
   auto launch = [&](const bf16* a, const bf16* b, void* c, int64_t m, int64_t n, int64_t k, int64_t ldc_, int S,
@@ -575,15 +365,12 @@ void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_
     const bool vec_c = ((uintptr_t)c & 15) == 0 && ((ldc_ * esz_c) & 15) == 0;
 #define DPH_GEMM_LAUNCH(T, ACC)                                                                                \
   do {                                                                                                         \
-    if (stag && (ACC || vec_c))                                                                                \
+    if (ACC || vec_c)                                                                                          \
       hipLaunchKernelGGL((gemm_tn_stag_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,  \
                          lda, ldb, ldc_, cstride);                                                             \
-    else if (!vec_c)                                                                                           \
-      hipLaunchKernelGGL((gemm_tn_k<T, ACC, false>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,  \
-                         lda, ldb, ldc_, cstride);                                                             \
     else                                                                                                       \
-      hipLaunchKernelGGL((gemm_tn_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k, lda,  \
-                         ldb, ldc_, cstride);                                                                  \
+      hipLaunchKernelGGL((gemm_tn_stag_k<T, false, false>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, \
+                         (int)k, lda, ldb, ldc_, cstride);                                                     \
   } while (0)
     if (!f32_out && out_dtype == kBF16) {
       if (acc) DPH_GEMM_LAUNCH(bf16, true);

@@ -106,10 +106,6 @@ void embedding_bwd(const int64_t* sorted_ids, const int64_t* perm, const void* d
 // ---- cast / scale helpers ----
 // C[M, N] (+)= A^T B, A [K, M] / B [K, N] bf16 row-major (weight gradient); C bf16 or fp32.
 bool gemm_tn_supported(int64_t M, int64_t N, int64_t K);
-// Pipeline of the wgrad kernel (v_mfma_f32_32x32x16_bf16): 32 = gemm_tn_k, 33 = its staggered form (tests force one)
-constexpr int kGemmTnDefaultMfma = 33;   // 33 = gemm_tn_stag_k (staggered 32x32x16), +1-2 % isolated, +0.5 % in-step (profiles/r4/wgrad_stagger)
-int gemm_tn_mfma();
-void gemm_tn_set_mfma(int shape);
 // Partial-last-wave plan (csrc/gemm.hip gemm_tn_plan): compute the tile band that would run as a partial wave with K
 // split `split` ways into fp32 slabs (workspace_floats floats), keeping rows (dim 0) / columns (dim 1) [0, keep) on
 // the plain kernel.  split == 0: one launch.  gemm_tn_set_tail(n): plan for n CUs (tests), 0 = device, < 0 = off.

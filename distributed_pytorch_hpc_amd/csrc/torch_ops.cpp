@@ -883,12 +883,6 @@ void convg_tn_(Tensor C, const Tensor& A, const Tensor& B, at::IntArrayRef geo, 
                       B.stride(0), ns, dt_code(C), accumulate, g, cur_stream(), chunk_taps);
 }
 
-// Select the wgrad kernel's MFMA form (32 = 32x32x16, 33 = its staggered form; -1 = query only); returns the active one.
-int64_t gemm_tn_mfma_(int64_t shape) {
-  if (shape != -1) dph::gemm_tn_set_mfma((int)shape);
-  return dph::gemm_tn_mfma();
-}
-
 // ------------------------------------------------------------------------------------------------ channel sum
 // x channels-last [N, C, H, W] or contiguous [M, C] -> [C] in out_dtype (the convolution bias gradient).
 Tensor channel_sum(const Tensor& x, at::ScalarType out_dtype) {
@@ -1490,7 +1484,6 @@ TORCH_LIBRARY(dph, m) {
   m.def("gemm_nt_rope(Tensor x, Tensor w, Tensor cos, Tensor sin, int S, int hd, int n_rot, int pos_off) -> Tensor");
   m.def("gemm_tn_tail_(int cus) -> ()", &gemm_tn_tail_);                          // catch-all kernels
   m.def("gemm_tn_plan_info(int M, int N, int K) -> int[]", &gemm_tn_plan_info);
-  m.def("gemm_tn_mfma_(int shape) -> int", &gemm_tn_mfma_);   // no tensor argument: catch-all kernel
   m.def("ts_gemm_nt(Tensor A, Tensor B, int H=0, int W=0, Tensor? add=None, Tensor? bias=None, Tensor? pro_ss=None) "
         "-> Tensor");
   m.def("ts_gemm_nt_stats(Tensor A, Tensor B, int H=0, int W=0, Tensor? pro_ss=None, Tensor? bias=None) -> (Tensor, Tensor)");

@@ -350,12 +350,11 @@ def test_embedding(dph_native):
                          [(512, 256, 256, torch.float32, False), (1024, 512, 768, torch.bfloat16, False),
                           (2048, 768, 512, torch.bfloat16, True), (64, 256, 512, torch.float32, True),
                           (192, 256, 256, torch.float32, False), (128, 512, 256, torch.float32, True)])
-@pytest.mark.parametrize("mfma,tail", [(32, 0), (32, 3), (32, 8), (33, 0), (33, 3), (33, 8)])
-def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate, mfma, tail):
-    """C (+)= A^T B with token-major A [K, M], B [K, N] (weight gradient dW = dY^T X), both MFMA-shape kernels
+@pytest.mark.parametrize("tail", [0, 3, 8])
+def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate, tail):
+    """C (+)= A^T B with token-major A [K, M], B [K, N] (weight gradient dW = dY^T X) on the staggered pipeline
     (K = 64 / 128 / 192 exercise the one- and two-K-step tails of the pipeline).  tail > 0 plans the partial-last-
     wave split for that many CUs, so the small shapes take the split-K band + fp32 slab reduction path."""
-    torch.ops.dph.gemm_tn_mfma_(mfma)
     torch.ops.dph.gemm_tn_tail_(tail)
     torch.manual_seed(0)
     a = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
@@ -367,7 +366,6 @@ def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate, mfma, tail):
             assert torch.ops.dph.gemm_tn_plan_info(M, N, K)[0] > 0 or K < 128
         torch.ops.dph.gemm_tn_(c, a, b, accumulate)
     finally:
-        torch.ops.dph.gemm_tn_mfma_(0)   # back to the default
         torch.ops.dph.gemm_tn_tail_(0)
     ref = a.float().t() @ b.float() + (c0.float() if accumulate else 0)
     assert rel_err(c, ref) < (1e-5 if out_dtype == torch.float32 else 8e-3)
@@ -396,20 +394,15 @@ def test_gemm_tn_tail_band(dph_native, M, N, dim, out_dtype, accumulate):
 
 @pytest.mark.parametrize("K,M,N", [(256, 2752 // 4, 4096 // 8), (128, 264, 520), (192, 4000 // 10, 1376 // 4),
                                    (64, 8, 256), (512, 1000, 24)])
-@pytest.mark.parametrize("mfma", [32, 33])
-def test_gemm_tn_wgrad_ragged_edge_tiles(dph_native, K, M, N, mfma):
+def test_gemm_tn_wgrad_ragged_edge_tiles(dph_native, K, M, N):
     """Tensor-parallel shard shapes (M, N % 8 but not % 256: w13 / w2 / vocab-head shards at tp=8) as partial edge
     tiles: every in-bounds element matches the fp32 reference and nothing past the matrix edge is written."""
-    torch.ops.dph.gemm_tn_mfma_(mfma)
-    try:
-        torch.manual_seed(5)
-        a = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
-        b = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
-        big = torch.full((M + 8, N + 16), 7.0, device=DEV, dtype=torch.float32)   # guard rows / columns
-        c = big[:M, :N]
-        torch.ops.dph.gemm_tn_(c, a, b, False)
-    finally:
-        torch.ops.dph.gemm_tn_mfma_(0)
+    torch.manual_seed(5)
+    a = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
+    b = torch.randn(K, N, device=DEV, dtype=torch.bfloat16)
+    big = torch.full((M + 8, N + 16), 7.0, device=DEV, dtype=torch.float32)   # guard rows / columns
+    c = big[:M, :N]
+    torch.ops.dph.gemm_tn_(c, a, b, False)
     ref = a.float().t() @ b.float()
     assert rel_err(c, ref) < 1e-5
     assert (big[M:] == 7.0).all() and (big[:, N:] == 7.0).all()
