@@ -1,0 +1,498 @@
+// Flash attention backward for CDNA4 (gfx950): delta = rowsum(dO * O), the KV-stationary dK/dV kernel, the
+// Q-stationary dQ kernel and their launcher.  Design notes at the top of attention_common.h.
+#include "attention_common.h"
+
+namespace dph {
+
+// ==================================================================================================
+// Backward
+// ==================================================================================================
+// delta[b, h, q] = sum_d dO[b,q,h,d] * O[b,q,h,d] (fp32).  TPR = D/8 lanes per row, 8 elements per lane;
+// rows are enumerated (b, q, h) so a wave reads 64 * 16 contiguous bytes of each [B, S, H, D] operand.
+template <int TPR>
+__global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ o, const bf16* __restrict__ dout,
+                                                    float* __restrict__ delta, int B, int S, int H,
+                                                    int64_t o_sb, int64_t o_ss, int64_t o_sh, int64_t d_sb,
+                                                    int64_t d_ss, int64_t d_sh) {
+  constexpr int RPB = 256 / TPR;  // rows per block-iteration
+  const int sub = threadIdx.x % TPR;
+  const int64_t rows = (int64_t)B * H * S;
+  for (int64_t r = (int64_t)blockIdx.x * RPB + threadIdx.x / TPR; r < rows; r += (int64_t)gridDim.x * RPB) {
+    const int hh = (int)(r % H);
+    const int64_t bq = r / H;
+    const int q = (int)(bq % S), bb = (int)(bq / S);
+    float x[8], y[8];
+    Vec8<bf16>::load(o + bb * o_sb + (int64_t)q * o_ss + hh * o_sh + sub * 8, x);
+    Vec8<bf16>::load(dout + bb * d_sb + (int64_t)q * d_ss + hh * d_sh + sub * 8, y);
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += x[k] * y[k];
+#pragma unroll
+    for (int m = TPR / 2; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
+    if (sub == 0) delta[((int64_t)bb * H + hh) * S + q] = acc;
+  }
+}
+
+// ---- dK / dV: KV-stationary.  One workgroup = 4 waves = 128 keys of one (batch, kv head); one wave =
+// 32 keys whose K^T / V^T B-operand fragments stay in registers.  The workgroup sweeps every query head
+// of the GQA group x 32-row query tiles (double-buffered Q / dO LDS images, one barrier per tile).
+// S and dP are computed with the key on the lane, so P and dS are directly the B operands of
+// dV^T += dO^T P and dK^T += Q^T dS: no LDS round trip, no atomics.
+// The dV / dK transposed reads are software-pipelined one step ahead (the first step issued before the softmax), and a
+// wave runs at issue priority 1 while in its MFMA chains (S / dP, then dV / dK) and 0 in its softmax, so the partner
+// wave on the SIMD (the other workgroup's) fills the chains' gaps with its softmax instead of competing for issue
+// (round 3/4 A/B: +2 % and +1 %; row constants as the initial S / dP accumulators measured -2 % and were removed).
+template <int HD, bool CAUSAL, bool DROP = false>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_k(AttnBwdParams P) {
+  constexpr int NW = 4;
+  constexpr int NT = 64 * NW, BNK = 32 * NW, BMQ = 32, NC = HD / 8, KS = HD / 16, DT = HD / 32;
+  constexpr bool RINIT = false;
+  constexpr bool TRPIPE = true;
+  constexpr int QIMG = BMQ * HD * 2;        // Q / dO tile image [32 q][HD]
+  constexpr int KIMG = BNK * HD * 2;        // K image [128 keys][HD] (B operand of S = Q K^T)
+  // img_off's line permutation repeats every 16 lines.  For NC >= 8, rows r and r + 32 are a multiple of 16
+  // lines apart, so the wave's K rows reuse the Q-image offsets plus a constant.
+  constexpr bool KSHARE = NC >= 8;
+  constexpr bool TRADD = NC >= 16;          // +16 rows is a pure byte offset for the transposed reads
+  // smem: K | Q0 | dO0 | Q1 | dO1 | -lse2[2][32] | delta[2][32] | dropout row keys[2][32]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Kimg = smem;
+  char* Qbuf = smem + KIMG;
+  float* lse_s = reinterpret_cast<float*>(Qbuf + 4 * QIMG);
+  float* del_s = lse_s + 2 * BMQ;
+  unsigned* rk_s = reinterpret_cast<unsigned*>(del_s + 2 * BMQ);
+
+  const AttnParams& p = P.f;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+  const int g = lane >> 4, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  const int nkb = (p.Sk + BNK - 1) / BNK;
+  int kbx, hk, b;
+  xcd_block(nkb, p.Hkv, kbx, hk, b, nkb * p.Hkv * p.B);
+  const int kb0 = kbx * BNK;   // ascending = heaviest causal key blocks first
+  const int grp = p.Hq / p.Hkv;
+  const int off = p.Sk - p.Sq;
+  const int key0 = kb0 + wid * 32;
+  const int mykey = key0 + l32;
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  const bf16* kp = (const bf16*)p.k + (int64_t)b * p.k_sb + (int64_t)hk * p.k_sh;
+  const bf16* vp = (const bf16*)p.v + (int64_t)b * p.v_sb + (int64_t)hk * p.v_sh;
+  glds_stage<NC, BNK, NT>(Kimg, kp, p.k_ss, kb0, p.Sk);
+  bf16x8 vf[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk)
+    vf[kk] = mykey < p.Sk ? *reinterpret_cast<const bf16x8*>(vp + (int64_t)mykey * p.v_ss + kk * 16 + 8 * h)
+                          : zero8();
+  f32x16 dk[DT], dv[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dk[dt][r] = 0.f; dv[dt][r] = 0.f; }
+  const f32x16 zacc = {};
+
+  // hoisted per-lane LDS offsets
+  int qro[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) qro[kk] = img_off<NC>(l32, kk * 2 + h);
+  auto kofs = [&](int kk) {
+    return KSHARE ? qro[kk] + wid * 32 * NC * 16 : img_off<NC>(wid * 32 + l32, kk * 2 + h);
+  };
+  int tro[TRADD ? 1 : 2][DT][2];
+#pragma unroll
+  for (int ks = 0; ks < (TRADD ? 1 : 2); ++ks)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int hi = 0; hi < 2; ++hi)
+        tro[ks][dt][hi] = img_off<NC>(ks * 16 + 4 * (g >> 1) + tq + 8 * hi, dt * 4 + 2 * (g & 1) + (tp >> 1)) +
+                          8 * (tp & 1);
+  auto trofs = [&](int ks, int dt, int hi) {
+    return TRADD ? tro[0][dt][hi] + ks * 16 * NC * 16 : tro[ks][dt][hi];
+  };
+
+  int qstart = 0;
+  if (CAUSAL) qstart = max(0, kb0 - off) / BMQ * BMQ;
+  const int nqt_head = qstart < p.Sq ? (p.Sq - qstart + BMQ - 1) / BMQ : 0;
+  const int total = nqt_head * grp;
+
+  // Q / dO tiles are prefetched by inline-asm LDS-DMA (RowStagePlan), retired by the explicit wait_vmcnt<0>() ahead
+  // of the end-of-tile barrier: with the compiler-visible builtin, hipcc drained the whole prefetch (vmcnt(0))
+  // before the transposed reads of the CURRENT tile.  The lse / delta row scalars are loaded raw and only scaled
+  // when written to LDS at the end of the tile, so their loads are not waited for (and, vmcnt retiring in order,
+  // the DMA behind them with it) at the top of the tile either.
+  RowStagePlan<NC, BMQ, NT> qplan;
+  qplan.init();
+  const unsigned lds_q = lds_addr(Qbuf + wid * 64 * 16);
+  float st_lse = 0.f, st_del = 0.f;
+  unsigned st_rk = 0u;
+  const unsigned dthr = DROP ? attn_drop_thr(p.drop_p) : 0u;
+  const float drs = DROP ? 1.f / (1.f - p.drop_p) : 1.f;
+  auto stage = [&](int it, int buf) {
+    const int hq = hk * grp + it / nqt_head;
+    const int qt0 = qstart + (it % nqt_head) * BMQ;
+    const bf16* qp = (const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
+    const bf16* dop = (const bf16*)P.dout + (int64_t)b * P.do_sb + (int64_t)hq * P.do_sh;
+    const unsigned ql = lds_q + buf * 2 * QIMG;
+    qplan.stage(ql, qp, p.q_ss, qt0, p.Sq);
+    qplan.stage(ql + QIMG, dop, P.do_ss, qt0, p.Sq);
+    if (threadIdx.x < BMQ) {
+      const int q = min(qt0 + (int)threadIdx.x, p.Sq - 1);   // rows past Sq: finite, masked by the caller
+      const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + q;
+      st_lse = p.lse[idx];
+      st_del = P.delta[idx];
+      if constexpr (DROP) st_rk = attn_row_key(p.drop_seed, (unsigned)(b * p.Hq + hq), (unsigned)(qt0 + threadIdx.x));
+    }
+  };
+  // Row constants: without dropout they become the INITIAL accumulators of the S and dP chains (S' = Q K^T - lse/scale,
+  // dP' = dO V^T - delta), so p = exp2(S' scale log2e) and dS = p dP' need no per-element row reads after the chains
+  // (cdna_hip_programming.md 'Row constants as the initial accumulator'); dropout keeps the explicit form.
+  const float inv_scale = 1.f / p.scale;
+  auto stage_scalars = [&](int buf) {
+    if (threadIdx.x < BMQ) {
+      if constexpr (!RINIT) {
+        lse_s[buf * BMQ + threadIdx.x] = -st_lse * 1.4426950408889634f;  // -lse in log2 units
+        del_s[buf * BMQ + threadIdx.x] = st_del;
+        if constexpr (DROP) rk_s[buf * BMQ + threadIdx.x] = st_rk;
+      } else {
+        lse_s[buf * BMQ + threadIdx.x] = -st_lse * inv_scale;
+        del_s[buf * BMQ + threadIdx.x] = -st_del;
+      }
+    }
+  };
+  // accumulator register r holds query row acc_row(r, h) = (r & 3) + 8 (r >> 2) + 4 h: four 16-B row reads
+  auto row_init = [&](const float* rows) {
+    f32x16 a;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(rows + 8 * j + 4 * h);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[4 * j + i] = v[i];
+    }
+    return a;
+  };
+
+  if (total > 0) {
+    stage(0, 0);
+    stage_scalars(0);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  for (int it = 0; it < total; ++it) {
+    const int buf = it & 1;
+    const int qt0 = qstart + (it % nqt_head) * BMQ;
+    if (it + 1 < total) stage(it + 1, buf ^ 1);
+    const char* Ql = Qbuf + buf * 2 * QIMG;
+    const char* Ol = Ql + QIMG;
+    // a wave whose 32 keys are all hidden from this query tile by the causal mask skips the tile
+    if (!(CAUSAL && key0 > qt0 + BMQ - 1 + off)) {
+      const float* ls = lse_s + buf * BMQ;
+      const float* ds = del_s + buf * BMQ;
+      __builtin_amdgcn_s_setprio(1);
+      f32x16 s = mfma32(lds_b128(Ql, qro[0]), lds_b128(Kimg, kofs(0)), RINIT ? row_init(ls) : zacc);
+      f32x16 dp = mfma32(lds_b128(Ol, qro[0]), vf[0], RINIT ? row_init(ds) : zacc);
+#pragma unroll
+      for (int kk = 1; kk < KS; ++kk) {
+        s = mfma32(lds_b128(Ql, qro[kk]), lds_b128(Kimg, kofs(kk)), s);
+        dp = mfma32(lds_b128(Ol, qro[kk]), vf[kk], dp);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      // wave-uniform: only diagonal / ragged tiles pay for the selects (masked scores -> -inf -> P = 0)
+      if ((qt0 + BMQ > p.Sq) || (key0 + 32 > p.Sk) || (CAUSAL && key0 + 31 > qt0 + off)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = qt0 + acc_row(r, h);
+          s[r] = (q >= p.Sq || mykey >= p.Sk || (CAUSAL && mykey > q + off)) ? -INFINITY : s[r];
+        }
+      }
+      // TRPIPE: the first dV / dK step's transposed operands are read now, their latency covered by the softmax
+      bf16x8 tro_o[2], tro_q[2];
+      if constexpr (TRPIPE) {
+        tro_o[0] = lds_tr2(Ol, trofs(0, 0, 0), trofs(0, 0, 1));
+        tro_q[0] = lds_tr2(Ql, trofs(0, 0, 0), trofs(0, 0, 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if constexpr (RINIT) {
+          const float pv = exp2_(s[r] * sl2);
+          s[r] = pv;
+          dp[r] = pv * dp[r];
+        } else if constexpr (DROP) {   // dV from the dropped, rescaled P; dS = P (Z dP / (1-p) - delta)
+          const int qr = acc_row(r, h);
+          const float pv = exp2_(fmaf(s[r], sl2, ls[qr]));
+          const bool keep = attn_keep(rk_s[buf * BMQ + qr], (unsigned)mykey, dthr);
+          s[r] = keep ? pv * drs : 0.f;
+          dp[r] = pv * ((keep ? dp[r] * drs : 0.f) - ds[qr]);
+        } else {
+          const int qr = acc_row(r, h);
+          const float pv = exp2_(fmaf(s[r], sl2, ls[qr]));
+          s[r] = pv;
+          dp[r] = pv * (dp[r] - ds[qr]);
+        }
+      }
+      bf16x8 pb[2], sb[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          pb[ks][j] = (bf16)s[8 * ks + j];
+          sb[ks][j] = (bf16)dp[8 * ks + j];
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      if constexpr (TRPIPE) {
+        // step i = (ks, dt): its operands were read one step earlier; each step issues the next step's 4 reads
+        // ahead of its own 2 MFMAs
+#pragma unroll
+        for (int i = 0; i < 2 * DT; ++i) {
+          const int ks = i / DT, dt = i % DT;
+          if (i + 1 < 2 * DT) {
+            const int k2 = (i + 1) / DT, d2 = (i + 1) % DT;
+            tro_o[(i + 1) & 1] = lds_tr2(Ol, trofs(k2, d2, 0), trofs(k2, d2, 1));
+            tro_q[(i + 1) & 1] = lds_tr2(Ql, trofs(k2, d2, 0), trofs(k2, d2, 1));
+          }
+          dv[dt] = mfma32(tro_o[i & 1], pb[ks], dv[dt]);
+          dk[dt] = mfma32(tro_q[i & 1], sb[ks], dk[dt]);
+          if (i + 1 < 2 * DT) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) {
+            const int o0 = trofs(ks, dt, 0), o1 = trofs(ks, dt, 1);
+            dv[dt] = mfma32(lds_tr2(Ol, o0, o1), pb[ks], dv[dt]);
+            dk[dt] = mfma32(lds_tr2(Ql, o0, o1), sb[ks], dk[dt]);
+          }
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+    if (it + 1 < total) stage_scalars(buf ^ 1);
+    wait_vmcnt<0>();
+    __syncthreads();
+  }
+
+  {   // dK then dV through this wave's LDS slab (the K and Q / dO images are free after the loop's last barrier)
+    static_assert(NW * 32 * HD * 2 <= KIMG + 4 * QIMG, "epilogue slabs exceed the dK/dV kernel's LDS");
+    const int nvalid = min(32, p.Sk - key0);
+    bf16* dk0 = (bf16*)P.dk + (int64_t)b * P.dk_sb + (int64_t)key0 * P.dk_ss + (int64_t)hk * P.dk_sh;
+    bf16* dv0 = (bf16*)P.dv + (int64_t)b * P.dv_sb + (int64_t)key0 * P.dv_ss + (int64_t)hk * P.dv_sh;
+    char* slab = smem + wid * (32 * HD * 2);
+    store_rows_lds<DT>(slab, dk0, P.dk_ss, nvalid, dk, p.scale, h, l32, mykey, P.rope_cos, P.rope_sin, P.rope_off);
+    store_rows_lds<DT>(slab, dv0, P.dv_ss, nvalid, dv, 1.f, h, l32, mykey, nullptr, nullptr, 0);
+  }
+}
+
+// ---- dQ: Q-stationary, the forward's structure.  One workgroup = 4 waves = 128 queries; a lane owns one
+// query (lane & 31).  Per 64-key tile: S^T = K Q^T and dP^T = V dO^T (A = K / V rows from LDS, B = Q^T / dO^T
+// fragments in registers), P^T = exp2(S^T c - lse) and dS^T = P^T (dP^T - delta) lane-locally (lse and delta
+// are one scalar per lane), then dQ^T += K^T dS^T with dS^T consumed straight from the accumulator.
+// K / V fragments are read a quarter sub-tile ahead of their MFMAs (KQ = 4: no register spills; the half-sub-tile form
+// spilled 3 registers).  Rejected A/B variants (profiles/r4/attn_dq/, attn_prio/): the dQ product's transposed K reads
+// software-pipelined one MFMA ahead, and issue priority over the MFMA chains.
+template <int HD, bool CAUSAL, bool DROP = false>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
+  constexpr int NW = 4, KQ = 4;
+  constexpr bool PF = false, PRIO = false;
+  using Plan = KVTilePlan<HD, 64 * NW>;
+  constexpr int BM = 32 * NW, BN = Plan::BN, KS = Plan::KS, DT = Plan::DT, TILE = Plan::TILE;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const AttnParams& p = P.f;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, l32 = lane & 31;
+  const int nqb = (p.Sq + BM - 1) / BM;
+  int bx, hq, b;
+  xcd_block(nqb, p.Hq, bx, hq, b, nqb * p.Hq * p.B);
+  const int qb = CAUSAL ? nqb - 1 - bx : bx;
+  const int hk = hq / (p.Hq / p.Hkv);
+  const int q0 = qb * BM, q0w = q0 + wid * 32;
+  const int myq = q0w + l32;
+  const int off = p.Sk - p.Sq;
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  const bf16* qp = (const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
+  const bf16* dop = (const bf16*)P.dout + (int64_t)b * P.do_sb + (int64_t)hq * P.do_sh;
+  const bf16* kp = (const bf16*)p.k + (int64_t)b * p.k_sb + (int64_t)hk * p.k_sh;
+  const bf16* vp = (const bf16*)p.v + (int64_t)b * p.v_sb + (int64_t)hk * p.v_sh;
+
+  bf16x8 qf[KS], df[KS];
+#pragma unroll
+  for (int kk = 0; kk < KS; ++kk) {
+    const bool ok = myq < p.Sq;
+    qf[kk] = ok ? *reinterpret_cast<const bf16x8*>(qp + (int64_t)myq * p.q_ss + kk * 16 + 8 * h) : zero8();
+    df[kk] = ok ? *reinterpret_cast<const bf16x8*>(dop + (int64_t)myq * P.do_ss + kk * 16 + 8 * h) : zero8();
+  }
+  float nlse2 = 0.f, delta = 0.f;  // -lse in log2 units
+  if (myq < p.Sq) {
+    const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + myq;
+    nlse2 = -p.lse[idx] * 1.4426950408889634f;
+    delta = P.delta[idx];
+  }
+
+  int kv_end = p.Sk;
+  if (CAUSAL) kv_end = min(p.Sk, q0 + BM + off);
+  const int ntiles = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
+  const int wtiles = wave_tile_count<CAUSAL>(ntiles, q0w, off);
+  const unsigned drk = DROP ? attn_row_key(p.drop_seed, (unsigned)(b * p.Hq + hq), (unsigned)myq) : 0u;
+  const unsigned dthr = DROP ? attn_drop_thr(p.drop_p) : 0u;
+  const float drs = DROP ? 1.f / (1.f - p.drop_p) : 1.f;
+
+  Plan plan;
+  plan.init(lane, p.k_ss);
+  plan.init_async();
+  const unsigned lds_w = lds_addr(smem + (threadIdx.x >> 6) * 64 * 16);
+
+  f32x16 dq[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[dt][r] = 0.f;
+  const f32x16 zacc = {};
+
+  if (ntiles > 0) plan.template stage_async<true>(lds_w, kp, vp, p.k_ss, p.v_ss, 0, p.Sk);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+
+  auto tile = [&](const char* Kl, const char* Vl, int k0, bool need_mask) {
+    bf16x8 sf[4];
+    bf16x8 tk[2];   // PF: ring of transposed K operands, step i = (ks, dt) = (i / DT, i % DT)
+    auto tk_read = [&](int i) { return lds_tr2(Kl, plan.tr(i / DT, i % DT, 0), plan.tr(i / DT, i % DT, 1)); };
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      // K and V fragments are read a half sub-tile (KH k-steps) ahead of their MFMAs with counted lgkmcnt waits
+      // (one read + wait + multiply at a time exposed an LDS round trip per MFMA; all KS at once spills)
+      constexpr int NQ = KS >= KQ ? KQ : KS, KH = KS / NQ;
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+      f32x16 s = zacc, dp = zacc;
+#pragma unroll
+      for (int half = 0; half < NQ; ++half) {
+        bf16x8 kf[KH], vf[KH];
+#pragma unroll
+        for (int j = 0; j < KH; ++j) {
+          kf[j] = lds_b128(Kl, plan.row(sub, half * KH + j));
+          vf[j] = lds_b128(Vl, plan.row(sub, half * KH + j));
+        }
+#pragma unroll
+        for (int j = 0; j < KH; ++j) {
+          s = mfma32(kf[j], qf[half * KH + j], s);
+          dp = mfma32(vf[j], df[half * KH + j], dp);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * KH, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * KH, 0);
+      }
+      if constexpr (PF) {
+        if (sub == 1) {
+          tk[0] = tk_read(0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+      if (need_mask) {  // wave-uniform; masked scores -> -inf -> p = 0
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + sub * 32 + acc_row(r, h);
+          s[r] = (key >= p.Sk || (CAUSAL && key > myq + off)) ? -INFINITY : s[r];
+        }
+      }
+      if constexpr (DROP) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool keep = attn_keep(drk, (unsigned)(k0 + sub * 32 + acc_row(r, h)), dthr);
+          s[r] = exp2_(fmaf(s[r], sl2, nlse2)) * ((keep ? dp[r] * drs : 0.f) - delta);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = exp2_(fmaf(s[r], sl2, nlse2)) * (dp[r] - delta);
+      }
+#pragma unroll
+      for (int half = 0; half < 2; ++half)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sf[sub * 2 + half][j] = (bf16)s[8 * half + j];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // dQ^T += K^T dS^T
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PF) {
+#pragma unroll
+      for (int i = 0; i < 4 * DT; ++i) {
+        if (i + 1 < 4 * DT) tk[(i + 1) & 1] = tk_read(i + 1);
+        dq[i % DT] = mfma32(tk[i & 1], sf[i / DT], dq[i % DT]);
+        if (i + 1 < 4 * DT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+          dq[dt] = mfma32(lds_tr2(Kl, plan.tr(ks, dt, 0), plan.tr(ks, dt, 1)), sf[ks], dq[dt]);
+    }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles)
+      plan.template stage_async<true>(lds_w + (buf ^ 1) * 2 * TILE, kp, vp, p.k_ss, p.v_ss, (t + 1) * BN, p.Sk);
+    const char* Kl = smem + buf * 2 * TILE;
+    if (t < wtiles) {
+      const int k0 = t * BN;
+      tile(Kl, Kl + TILE, k0, (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0w + off)));
+    }
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+  }
+
+  {   // dQ through this wave's LDS slab (the K / V images are free after the loop's last barrier)
+    static_assert(NW * 32 * HD * 2 <= 4 * TILE, "epilogue slabs exceed the dQ kernel's LDS");
+    bf16* dq0 = (bf16*)P.dq + (int64_t)b * P.dq_sb + (int64_t)q0w * P.dq_ss + (int64_t)hq * P.dq_sh;
+    store_rows_lds<DT>(smem + wid * (32 * HD * 2), dq0, P.dq_ss, min(32, p.Sq - q0w), dq, p.scale, h, l32, myq,
+                       P.rope_cos, P.rope_sin, P.rope_off);
+  }
+}
+
+template <int HD, bool DROP>
+static void bwd_launch_t(const AttnBwdParams& P, hipStream_t st) {
+  const AttnParams& p = P.f;
+  const size_t lds_kv = 128 * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
+  const dim3 grid_kv((unsigned)((p.Sk + 127) / 128 * p.Hkv * p.B));
+  if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, DROP>), grid_kv, dim3(256), lds_kv, st, P);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, DROP>), grid_kv, dim3(256), lds_kv, st, P);
+  const size_t lds_q = 2 * 2 * 64 * HD * 2;
+  const dim3 grid_q((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
+  if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, DROP>), grid_q, dim3(256), lds_q, st, P);
+  else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, DROP>), grid_q, dim3(256), lds_q, st, P);
+}
+
+template <int HD>
+static void bwd_launch(const AttnBwdParams& P, hipStream_t st) {
+  if (P.f.drop_p > 0.f) bwd_launch_t<HD, true>(P, st);
+  else bwd_launch_t<HD, false>(P, st);
+}
+
+void flash_attn_bwd(const AttnBwdParams& P, hipStream_t st) {
+  const AttnParams& p = P.f;
+  if (p.B == 0 || p.Sq == 0) return;
+  const int64_t rows = (int64_t)p.B * p.Hq * p.Sq;
+  auto delta = [&](auto kern, int tpr) {
+    hipLaunchKernelGGL(kern, dim3(stream_grid(rows, 256 / tpr)), dim3(256), 0, st, (const bf16*)p.o,
+                       (const bf16*)P.dout, P.delta, p.B, p.Sq, p.Hq, p.o_sb, p.o_ss, p.o_sh, P.do_sb, P.do_ss,
+                       P.do_sh);
+  };
+  switch (p.D) {
+    case 32: delta(attn_delta_k<4>, 4); break;
+    case 64: delta(attn_delta_k<8>, 8); break;
+    case 128: delta(attn_delta_k<16>, 16); break;
+    default: return;
+  }
+  switch (p.D) {
+    case 32: bwd_launch<32>(P, st); break;
+    case 64: bwd_launch<64>(P, st); break;
+    case 128: bwd_launch<128>(P, st); break;
+    default: break;
+  }
+}
+
+}  // namespace dph

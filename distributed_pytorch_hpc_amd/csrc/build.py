@@ -24,10 +24,11 @@ BUILD_DIR = os.path.join(PKG, "..", "build", "native")
 OUT = os.path.join(PKG, "_C.so")
 ARCH = os.environ.get("DPH_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
-# attention: no NaN canonicalisation around fmaxf of MFMA outputs (halves the row-max VALU work);
-# infinities stay honoured (masked scores are -inf)
-# attention.hip: no NaN semantics needed (masks are -inf, never NaN), and IEEE mode off so fmaxf on MFMA results is a
-# bare v_max / v_max3 instead of a canonicalising v_max per operand first (the row max of every score tile)
+# attention.hip (the forward): no NaN semantics needed (masks are -inf, never NaN), and IEEE mode off so fmaxf on MFMA
+# results is a bare v_max / v_max3 instead of a canonicalising v_max per operand first (the row max of every score
+# tile): forward 814 -> 836 TFLOP/s.  attention_bwd.hip has no row max and is built WITHOUT them: under these flags
+# the dK/dV kernel's register allocation spills 80 B at 256 VGPRs (the reloads drain the in-flight Q / dO prefetch),
+# backward 702 -> 655 TFLOP/s (profiles/r5/attn_split/).
 PER_FILE_HIP_FLAGS = {"attention.hip": ["-fno-honor-nans", "-mno-amdgpu-ieee"]}
 
 

@@ -1,4 +1,4 @@
-"""Flash attention on CDNA4 (csrc/attention.hip) and the fused RoPE+attention core of the Llama block.
+"""Flash attention on CDNA4 (csrc/attention.hip forward, csrc/attention_bwd.hip backward) and the fused RoPE+attention core of the Llama block.
 
 Layout convention is [B, S, H, D] (sequence-major, heads inner) so that q/k/v are plain strided VIEWS of
 the fused QKV GEMM output [B, S, (Hq + 2 Hkv) * D] -- no transposes, no copies.  The reference calls
@@ -76,7 +76,7 @@ _M32 = 0xFFFFFFFF
 
 
 def _mix(x: torch.Tensor) -> torch.Tensor:
-    """csrc/attention.hip attn_mix on int64 tensors holding uint32 values."""
+    """csrc/attention_common.h attn_mix on int64 tensors holding uint32 values."""
     x = x ^ (x >> 16)
     x = (x * 0x7FEB352D) & _M32
     x = x ^ (x >> 15)

@@ -1,4 +1,4 @@
-"""Attention dropout in the CDNA4 flash kernels (csrc/attention.hip DROP instantiations).
+"""Attention dropout in the CDNA4 flash kernels (csrc/attention.hip / attention_bwd.hip DROP instantiations).
 
 The keep mask is a counter hash the kernels regenerate; ``ops.attention.dropout_mask`` rebuilds it on the host, so
 the kernels are checked against an fp32 PyTorch reference of dropout attention with exactly that mask.
