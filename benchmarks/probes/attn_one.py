@@ -2,6 +2,7 @@
 """Run the flash-attention kernels on one Llama-2-7B shape a few times (for rocprofv3 counter collection)
 and print their TFLOP/s."""
 import argparse
+import json
 import math
 import os
 import sys
@@ -22,6 +23,9 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--which", default="fwd,bwd")
     ap.add_argument("--noncausal", action="store_true")
+    ap.add_argument("--sustain", type=float, default=0.0,
+                    help="also loop each kernel for this many seconds under the GPU telemetry sampler (clock, power, "
+                         "package-power residency, TFLOP/J)")
     a = ap.parse_args()
     _lib.require()
     causal = not a.noncausal
@@ -44,6 +48,20 @@ def main():
         ms = s.elapsed_time(e) / a.iters
         f = flops * (2.5 if which == "bwd" else 1.0)
         print(f"{which}: {ms:.3f} ms  {f / ms / 1e9:.1f} TFLOP/s", flush=True)
+        if a.sustain > 0:
+            from distributed_pytorch_hpc_amd.utils.telemetry import GpuTelemetry
+
+            n = max(1, int(a.sustain * 1e3 / ms))
+            tel = GpuTelemetry(torch.cuda.current_device(), period=0.05)
+            tel.mark("start")
+            for _ in range(n):
+                fn()
+            torch.cuda.synchronize()
+            tel.mark("end")
+            tel.stop()
+            summ = tel.summary("start", "end", flops=f * n)
+            keep = ("sclk_mhz", "power_w", "avg_power_w", "tflop_per_joule", "ppt_limited_frac")
+            print(f"{which} sustained x{n}: " + json.dumps({k: summ.get(k) for k in keep}), flush=True)
 
 
 if __name__ == "__main__":

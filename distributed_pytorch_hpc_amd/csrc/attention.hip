@@ -14,8 +14,10 @@ namespace dph {
 // final 1/l.  The rescale branch is wave-uniform (ballot), so steady-state tiles skip 16*DT multiplies.
 // Rejected round-4/5 variants of this kernel (evidence kept under profiles/): 8-wave workgroups (819-822 vs 834-838
 // TFLOP/s), waves 4..7 staggered one barrier behind (809-814), issue priority over the MFMA chains (within noise),
-// and a software-pipelined body that overlaps each wave's softmax with its own next QK^T (754-788 vs 831-833,
-// profiles/r5/attn_fwd_pipe/).
+// a software-pipelined body that overlaps each wave's softmax with its own next QK^T (754-788 vs 831-833,
+// profiles/r5/attn_fwd_pipe/), and one wave per SIMD with 64 query rows per wave, every K / V fragment feeding two
+// 32-row blocks, the whole 512-entry file (256 VGPR + 256 AGPR, no scratch): 629-630 vs 819 TFLOP/s, the compiler's
+// AGPR form adds ~350 v_accvgpr moves per tile and no second wave hides the barrier (profiles/r5/attn_q2/).
 template <int HD, bool CAUSAL, bool DROP = false>
 __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
   constexpr int NW = 4;
