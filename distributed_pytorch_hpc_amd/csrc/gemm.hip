@@ -4,14 +4,13 @@
 // hipBLASLt runs this "both operands K-strided" pattern at 0.95-1.2 PFLOP/s on the Llama-2-7B shapes while the
 // K-contiguous pattern reaches 1.5-1.6 PFLOP/s (profiles/gemm_layout_*.json); transposing the operands first
 // costs more than it saves.  Here the transposition happens on the LDS -> register path instead:
-//   * 256 x 256 output tile per workgroup, 8 waves as 2 (M) x 4 (N), each wave 128 x 64 = 4 x 2 MFMA
-//     32x32x16 bf16 tiles (128 fp32 accumulator VGPRs);
-//   * K-steps of 64 tokens: the [64][256] A and B tiles are copied global -> LDS by LDS-DMA
-//     (global_load_lds_dwordx4, 16 B per lane, lane-linear destination, swizzle applied to the SOURCE address),
-//     double-buffered so the copy of step t+1 overlaps the MFMAs of step t;
-//   * MFMA operands (8 consecutive k of one m or n column per lane) come from ds_read_b64_tr_b16 transposed
-//     reads; the LDS image XORs each 16-B slot with (row & 3) << 2, which makes the 4-row x 4-chunk footprint of
-//     a half-wave's transposed read cover all 64 banks exactly once;
+//   * 256 x 256 output tile per workgroup, 8 waves as 2 (M) x 4 (N), each wave 128 x 64 = 8 x 4 MFMA
+//     16x16x32 bf16 tiles (128 fp32 accumulator VGPRs);
+//   * slots of 32 tokens: the [32][256] A and B tiles are copied global -> LDS by LDS-DMA (global_load_lds_dwordx4,
+//     16 B per lane, lane-linear destination, swizzle applied to the SOURCE address) into a 5-region ring, the
+//     copies of slots t+2 and t+3 in flight under the MFMAs of slot t;
+//   * MFMA operands (8 k of one m or n column per lane) come from ds_read_b64_tr_b16 transposed reads; the LDS image
+//     XORs each 16-B slot so a half-wave's transposed reads cover all 64 banks exactly once;
 //   * workgroups are remapped so each XCD (blockIdx % 8 under round-robin dispatch) owns a contiguous range of
 //     output tiles, grouped GROUP_M tiles tall, for L2 reuse of the shared A / B column panels.
 // Requirements (checked by the host op): M % 8 == 0, N % 8 == 0, K % 64 == 0, lda / ldb % 8 == 0, 16-B aligned
@@ -32,7 +31,6 @@ typedef __attribute__((address_space(3))) i16x4 lds_i16x4_g;
 
 constexpr int GBM = 256, GBN = 256, GBK = 64, GNT = 512;
 constexpr int ROWB = GBM * 2;              // bytes per LDS image row (256 bf16)
-constexpr int TILEB = GBK * ROWB;          // 32 KB per operand tile
 constexpr int GROUP_M = 8;
 
 // Tile (tm, tn) of logical workgroup lin: columns of GROUP_M-tall tile groups, m fastest, so the workgroups an XCD
@@ -58,36 +56,36 @@ __device__ __forceinline__ void glds16(const char* sbase, unsigned voff, unsigne
 template <int N>
 __device__ __forceinline__ void wait_vm() { wait_vmcnt<N>(); }
 
-// Pipeline: one K-step (64 tokens) = 4 phases of 16 k-rows.  Phase P's operands live in LDS region R = P & 7 (tile
-// parity x 16-row region; A rows at +0, B rows at +8 KB of a 16-KB region) and are filled by DMA "pair P" (one 16-B
-// global_load_lds per thread per operand, inline asm: see glds16).  In slot S every wave retires its share of pair
-// S+2 (counted vmcnt), meets the others at a raw s_barrier, issues pair S+5, and runs the 8 MFMAs of region S while the
-// transposed reads of region S+1 go to the other fragment register set.
-//
-// Waves 4..7 run one barrier behind waves 0..3, so on every SIMD one wave issues its slot's MFMAs while its partner
-// waits at the barrier, issues its DMA pair and transposed reads (the ping-pong of gemm_nt.hip); in lockstep (the
-// round-2..4 gemm_tn_k, deleted in round 5) both waves of a SIMD reached the barrier together and the matrix pipe idled
-// while they waited (PMC on the w13 shape: SQ_WAIT_ANY 40 % of wave cycles, MFMA busy 0.74 vs 0.79 staggered,
-// profiles/r5/wgrad_power/).  The stagger makes an early wave's read of region S+1 at its slot S race the LATE waves'
-// share of that region's DMA, hence the pipeline depth: slot S retires pair S+2 (not S+1) and issues pair S+5 (not
-// S+4); regions in use at once: S..S+5 = 6 of the 8.  WAR: pair S+5 overwrites pair S-3's region, whose last reader
-// (a late wave, in its slot S-4 = the early waves' slot S-3) is two barriers back.
-// No tail code: a pair index past the last one re-loads the last pair (finite data) into a region whose contents are
-// never multiplied, so every slot has the same DMA / counted wait / read and the loop body is one 8-slot block (plus
-// one 4-slot block for an odd K-tile count) -- tail sequences cost the lockstep kernel ~400 VGPR spills and a
-// vmcnt(0) drain per iteration where the waitcnt pass merged the spill reloads into the loop.
-// LDS_EPI: the 16-B LDS-staged epilogue (C 16-B aligned with a 16-B row pitch); otherwise one store per element.
+// ---- The kernel: v_mfma_f32_16x16x32_bf16 (profiles/r5/mfma_power/: 12 % more TFLOP/J and 15 % more TFLOP/s than
+// 32x32x16 on register operands, the clock held 14 % higher) ----
+// Wave tile 128 x 64 = 8 x 4 tiles of 16 x 16 (32 f32x4 accumulators, 128 VGPRs).  A slot is 32 k-rows (one MFMA's
+// K): region R of LDS holds A rows [32][256] at +0 and B rows [32][256] at +16 KB, 5 regions = 160 KB.
+// Fragment of m-tile mt: lane L (m = L & 15, k-group g = L >> 4) reads rows 4g + tq (k 0..15 half) and 16 + 4g + tq
+// (k 16..31 half) with two ds_read_b64_tr_b16 at one lane offset 16 rows apart; the k permutation is the same for the
+// A and B fragments, so the products are exact.  The image swizzle XORs the 16-B slot with ((row & 3) << 2) |
+// (((row >> 2) & 1) << 1): the two 16-lane groups of a half-wave read rows 4 apart, and the extra bit sends them to
+// disjoint slots, so a half-wave's 32 transposed 8-B reads cover all 64 banks once.
+// Pipeline: slot S retires DMA pair S+1 (pairs S+2, S+3 stay in flight: three slots of MFMA work hide each copy),
+// meets the other waves at the barrier, issues pair S+4 into region (S+4) % 5 -- the region pair S-1 left, which every
+// wave finished multiplying before this barrier -- and runs the 32 MFMAs of region S while the fragments of region S+1
+// are read: B into the other B set first, then each A row refilled right after its own 4 MFMAs.  Pairs past the end
+// re-load the last pair into a region nobody multiplies.
+// Measured against the round-2..5 kernel (32x32x16, 128 x 64 wave tile, waves 4..7 one barrier behind; deleted), one
+// box, interleaved (profiles/r5/wgrad16/): w13 / wqkv / w2 1255-1264 / 1296-1301 / 1312-1313 TFLOP/s vs 1202-1206 /
+// 1245-1248 / 1252-1254 at 1.71-1.85 vs 1.60-1.64 GHz, 7B step 28 425-28 436 vs 28 225-28 316 tokens/s.  The same
+// 16x16x32 body with the stagger lost (1224-1260 TFLOP/s): it fits only one slot of DMA latency in 160 KB of LDS.
+constexpr int R16 = 5, REG16 = 32768;
+
 template <typename OutT, bool ACCUM, bool LDS_EPI = true>
-__global__ __launch_bounds__(GNT, 1) void gemm_tn_stag_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
-                                                         OutT* __restrict__ C, int M, int N, int K, int64_t lda,
-                                                         int64_t ldb, int64_t ldc, int64_t cstride) {
+__global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
+                                                      OutT* __restrict__ C, int M, int N, int K, int64_t lda,
+                                                      int64_t ldb, int64_t ldc, int64_t cstride) {
   A += (int64_t)blockIdx.y * K * lda;
   B += (int64_t)blockIdx.y * K * ldb;
   C += (int64_t)blockIdx.y * cstride;
-  __shared__ __attribute__((aligned(1024))) char lds[8 * 16384];
+  __shared__ __attribute__((aligned(1024))) char lds[R16 * REG16];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm = wid >> 2, wn = wid & 3;
-  const int h = lane >> 5, l32 = lane & 31;
   const int g = lane >> 4, tq = (lane & 15) >> 2, tp = lane & 3;
 
   const int tiles_m = (M + GBM - 1) / GBM, tiles_n = (N + GBN - 1) / GBN, nwg = tiles_m * tiles_n;
@@ -95,123 +93,145 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_stag_k(const bf16* __restrict_
   grouped_tile(xcd_remap(blockIdx.x, nwg), tiles_m, tiles_n, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
 
-  const int x = 2 * (g & 1) + (tp >> 1);
-  const int krow = 4 * (g >> 1) + tq;
-  const int base = krow * ROWB + 8 * (tp & 1);
-  int aoff[4], boff[2];
+  // transposed-read offsets (k 0..15 half; the 16..31 half is +16 rows)
+  const int swz = (tq << 2) | ((g & 1) << 1);
+  const int base = (4 * g + tq) * ROWB + 8 * (tp & 1);
+  int aoff[8], boff[4];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) aoff[mt] = base + (wm << 8) + ((4 * (mt ^ tq) + x) << 4);
+  for (int mt = 0; mt < 8; ++mt) aoff[mt] = base + (wm << 8) + (((2 * mt + (tp >> 1)) ^ swz) << 4);
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
-    boff[nt] = 8192 + base + ((wn >> 1) << 8) + ((4 * ((((wn & 1) << 1) | nt) ^ tq) + x) << 4);
+  for (int nt = 0; nt < 4; ++nt)
+    boff[nt] = 16384 + base + ((wn >> 1) << 8) + (((8 * (wn & 1) + 2 * nt + (tp >> 1)) ^ swz) << 4);
 
-  const int srow = threadIdx.x >> 5, lr = (threadIdx.x >> 4) & 1, sslot = threadIdx.x & 15;
-  const int sch = (lr << 4) | (sslot ^ ((srow & 3) << 2));
-  const int colA = min(sch * 8, M - 8 - m0), colB = min(sch * 8, N - 8 - n0);
+  // LDS-DMA: thread t copies chunks t and t + 512 of a [32][32 x 16 B] operand image (rows t >> 5 and 16 + (t >> 5));
+  // the destination is lane-linear, the swizzle goes into the source column
+  const int srow = threadIdx.x >> 5, pslot = threadIdx.x & 31;
+  const int sswz = ((srow & 3) << 2) | (((srow >> 2) & 1) << 1);
+  const int lslot = (pslot & 16) | ((pslot & 15) ^ sswz);
+  const int colA = min(lslot * 8, M - 8 - m0), colB = min(lslot * 8, N - 8 - n0);
   const unsigned voffA = (unsigned)((srow * lda + colA) * 2), voffB = (unsigned)((srow * ldb + colB) * 2);
+  const unsigned hopA = (unsigned)(16 * lda * 2), hopB = (unsigned)(16 * ldb * 2);
   const char* Ag = reinterpret_cast<const char*>(A + m0);
   const char* Bg = reinterpret_cast<const char*>(B + n0);
-  const int64_t stepA = 16 * lda * 2, stepB = 16 * ldb * 2;
+  const int64_t stepA = 32 * lda * 2, stepB = 32 * ldb * 2;
   const unsigned lds_wave = __builtin_amdgcn_readfirstlane(
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds + (threadIdx.x >> 6) * 1024);
 
-  auto region = [&](auto RI) -> char* { return lds + decltype(RI)::value * 16384; };
-  const int NP = (K / GBK) * 4;
+  const int NP = K / 32;
   auto dma_pair = [&](int P, auto RI) {
-    const unsigned d = lds_wave + decltype(RI)::value * 16384;
+    const unsigned d = lds_wave + decltype(RI)::value * REG16;
     const int Pc = min(P, NP - 1);   // past the end: the last pair again, into a region nobody multiplies
-    glds16(Ag + Pc * stepA, voffA, d);
-    glds16(Bg + Pc * stepB, voffB, d + 8192);
+    const char* ga = Ag + Pc * stepA;
+    const char* gb = Bg + Pc * stepB;
+    glds16(ga, voffA, d);
+    glds16(ga, voffA + hopA, d + 8192);
+    glds16(gb, voffB, d + 16384);
+    glds16(gb, voffB + hopB, d + 16384 + 8192);
   };
-  auto read_phase = [&](auto RI, bf16x8 (&af)[4], bf16x8 (&bfr)[2]) {
-    const char* rg = region(RI);
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) af[mt] = tr2(rg, aoff[mt], aoff[mt] + 8 * ROWB);
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) bfr[nt] = tr2(rg, boff[nt], boff[nt] + 8 * ROWB);
+  // region base as an opaque wave-uniform value: the 12 per-lane addresses are formed per slot (12 VALU) instead of
+  // being hoisted out of the loop for all 5 regions (60 live VGPRs)
+  auto region = [&](auto RI) -> const char* {
+    int rb = decltype(RI)::value * REG16;
+    asm volatile("" : "+s"(rb));
+    return lds + rb;
   };
-
-  f32x16 acc[4][2];
+  auto read_b = [&](const char* rg, bf16x8 (&bfr)[4]) {
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+    for (int nt = 0; nt < 4; ++nt) bfr[nt] = tr2(rg, boff[nt], boff[nt] + 16 * ROWB);
+  };
+  auto read_a = [&](const char* rg, bf16x8 (&af)[8]) {
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[mt][nt][i] = 0.f;
-
-  auto mma = [&](const bf16x8 (&af)[4], const bf16x8 (&bfr)[2]) {
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-        acc[mt][nt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
+    for (int mt = 0; mt < 8; ++mt) af[mt] = tr2(rg, aoff[mt], aoff[mt] + 16 * ROWB);
   };
 
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  using I4 = std::integral_constant<int, 4>;
-  // prologue: pairs 0..4 (regions 0..4), then pairs 0 and 1 retired by every wave before the common barrier
-  dma_pair(0, I0{});
-  dma_pair(1, I1{});
-  dma_pair(2, I2{});
-  dma_pair(3, I3{});
-  dma_pair(4, I4{});
-  wait_vm<6>();
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int mt = 0; mt < 8; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // the 32 MFMAs of the current region, row by row; row mt's A fragment is refilled from the next region right after
+  // its 4 MFMAs (one A set, rotated in place; B, used by every row, has two sets)
+  auto mma_refill = [&](bf16x8 (&af)[8], const bf16x8 (&bfr)[4], const char* rn) {
+#pragma unroll
+    for (int mt = 0; mt < 8; ++mt) {
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
+      af[mt] = tr2(rn, aoff[mt], aoff[mt] + 16 * ROWB);
+    }
+  };
+
+  // prologue: pairs 0..3 (regions 0..3), pair 0 retired by every wave before the common barrier
+  dma_pair(0, std::integral_constant<int, 0>{});
+  dma_pair(1, std::integral_constant<int, 1>{});
+  dma_pair(2, std::integral_constant<int, 2>{});
+  dma_pair(3, std::integral_constant<int, 3>{});
+  wait_vm<12>();
   __builtin_amdgcn_s_barrier();
-  bf16x8 af0[4], bf0[2], af1[4], bf1[2];
-  read_phase(I0{}, af0, bf0);
-  const bool late = __builtin_amdgcn_readfirstlane(wid) >= 4;
-  if (late) __builtin_amdgcn_s_barrier();
+  bf16x8 af[8], bf0[4], bf1[4];
+  {
+    const char* r0 = region(std::integral_constant<int, 0>{});
+    read_b(r0, bf0);
+    read_a(r0, af);
+  }
   __builtin_amdgcn_sched_barrier(0);
 
-  // slot S (region S & 7): retire pair S+2 (vmcnt 4: pairs S+3, S+4 stay in flight) -> barrier -> DMA pair S+5 ->
-  // reads of region S+1 into the other register set interleaved with the 8 MFMAs of region S
-  auto slot = [&](int P0, auto SI, bf16x8 (&afc)[4], bf16x8 (&bfc)[2], bf16x8 (&afn)[4], bf16x8 (&bfn)[2]) {
+  auto slot = [&](int P0, auto SI, bf16x8 (&bfc)[4], bf16x8 (&bfn)[4]) {
     constexpr int S = decltype(SI)::value;
-    wait_vm<4>();
+    wait_vm<8>();
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    dma_pair(P0 + S + 5, std::integral_constant<int, (S + 5) & 7>{});
+    dma_pair(P0 + S + 4, std::integral_constant<int, (S + 4) % R16>{});
     __builtin_amdgcn_s_setprio(1);
-    read_phase(std::integral_constant<int, (S + 1) & 7>{}, afn, bfn);
-    mma(afc, bfc);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    const char* rn = region(std::integral_constant<int, (S + 1) % R16>{});
+    read_b(rn, bfn);
+    mma_refill(af, bfc, rn);
+    // B reads (8) then per row 4 MFMAs + its 2 A reads
+    for (int i = 0; i < 8; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   };
 #define DPH_S(i) std::integral_constant<int, i>{}
   int P0 = 0;
-  for (; P0 + 8 <= NP; P0 += 8) {
-    slot(P0, DPH_S(0), af0, bf0, af1, bf1);
-    slot(P0, DPH_S(1), af1, bf1, af0, bf0);
-    slot(P0, DPH_S(2), af0, bf0, af1, bf1);
-    slot(P0, DPH_S(3), af1, bf1, af0, bf0);
-    slot(P0, DPH_S(4), af0, bf0, af1, bf1);
-    slot(P0, DPH_S(5), af1, bf1, af0, bf0);
-    slot(P0, DPH_S(6), af0, bf0, af1, bf1);
-    slot(P0, DPH_S(7), af1, bf1, af0, bf0);
+  for (; P0 + 10 <= NP; P0 += 10) {
+    slot(P0, DPH_S(0), bf0, bf1);
+    slot(P0, DPH_S(1), bf1, bf0);
+    slot(P0, DPH_S(2), bf0, bf1);
+    slot(P0, DPH_S(3), bf1, bf0);
+    slot(P0, DPH_S(4), bf0, bf1);
+    slot(P0, DPH_S(5), bf1, bf0);
+    slot(P0, DPH_S(6), bf0, bf1);
+    slot(P0, DPH_S(7), bf1, bf0);
+    slot(P0, DPH_S(8), bf0, bf1);
+    slot(P0, DPH_S(9), bf1, bf0);
   }
-  if (P0 < NP) {   // odd number of K-tiles: the last one (regions 0..3)
-    slot(P0, DPH_S(0), af0, bf0, af1, bf1);
-    slot(P0, DPH_S(1), af1, bf1, af0, bf0);
-    slot(P0, DPH_S(2), af0, bf0, af1, bf1);
-    slot(P0, DPH_S(3), af1, bf1, af0, bf0);
+  {   // the remaining NP - P0 (< 10) slots, each position compiled once
+    const int rem = NP - P0;
+    if (rem > 0) slot(P0, DPH_S(0), bf0, bf1);
+    if (rem > 1) slot(P0, DPH_S(1), bf1, bf0);
+    if (rem > 2) slot(P0, DPH_S(2), bf0, bf1);
+    if (rem > 3) slot(P0, DPH_S(3), bf1, bf0);
+    if (rem > 4) slot(P0, DPH_S(4), bf0, bf1);
+    if (rem > 5) slot(P0, DPH_S(5), bf1, bf0);
+    if (rem > 6) slot(P0, DPH_S(6), bf0, bf1);
+    if (rem > 7) slot(P0, DPH_S(7), bf1, bf0);
+    if (rem > 8) slot(P0, DPH_S(8), bf0, bf1);
   }
 #undef DPH_S
-  if (!late) __builtin_amdgcn_s_barrier();   // balance the stagger
   wait_vm<0>();
 
-  // ---- epilogue: register i of tile (mt, nt) holds C[row (i&3) + 8(i>>2) + 4h][col l32].  Through LDS (free after
-  // the main loop) the tile leaves as 16-B row segments -- 16 (bf16) / 32 (fp32, two 128-row passes) vector stores per
-  // thread instead of 128 scalar stores per lane; ACCUM keeps the per-element path (one rounding of old + acc) ----
+  // ---- epilogue: register r of tile (mt, nt) holds C[row 16 mt + 4 (lane >> 4) + r][col 16 nt + (lane & 15)] ----
+  const int crow = 4 * g, ccol = lane & 15;
   if constexpr (!ACCUM && LDS_EPI) {
     constexpr int VE = 16 / (int)sizeof(OutT);
     constexpr int PR = (int)(sizeof(OutT) == 2 ? 256 : 128);
@@ -222,13 +242,13 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_stag_k(const bf16* __restrict_
       __syncthreads();
       if (NPASS == 1 || wm == pass) {
 #pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
+        for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-          for (int nt = 0; nt < 2; ++nt)
+          for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const int r = (NPASS == 1 ? wm * 128 : 0) + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-              ct[r * 256 + wn * 64 + nt * 32 + l32] = (OutT)acc[mt][nt][i];
+            for (int r = 0; r < 4; ++r) {
+              const int row = (NPASS == 1 ? wm * 128 : 0) + mt * 16 + crow + r;
+              ct[row * 256 + wn * 64 + nt * 16 + ccol] = (OutT)acc[mt][nt][r];
             }
       }
       __syncthreads();
@@ -243,25 +263,25 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn_stag_k(const bf16* __restrict_
     }
   } else {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < 8; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int col = n0 + wn * 64 + nt * 32 + l32;
+      for (int nt = 0; nt < 4; ++nt) {
+        const int col = n0 + wn * 64 + nt * 16 + ccol;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int row = m0 + wm * 128 + mt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * 128 + mt * 16 + crow + r;
           if (row >= M || col >= N) continue;
           OutT* pp = C + (int64_t)row * ldc + col;
-          *pp = (OutT)(ACCUM ? acc[mt][nt][i] + (float)*pp : acc[mt][nt][i]);
+          *pp = (OutT)(ACCUM ? acc[mt][nt][r] + (float)*pp : acc[mt][nt][r]);
         }
       }
   }
 }
 
-// Rejected (round 2-4, code removed in round 5): the same pipeline on v_mfma_f32_16x16x32_bf16 (same 128 x 64 tile
-// per wave as 8 x 4 tiles of 16 x 16, pairs of 16-row regions per MFMA): 1045-1260 TF vs 1287-1432 TF for the
-// 32x32x16 kernel on the 7B shapes -- twice the MFMA issues and 12 region-address VALU ops per slot outweighed the
-// higher clock the chip holds on the 16x16x32 shape (profiles/gemm_wgrad_mfma16_vs_32.json, profiles/r4/wgrad_stagger/).
+
+// History: a round-2..4 16x16x32 form of the 32x32x16 pipeline (pairs of 16-row regions per MFMA, 12 region-address
+// VALU ops per slot) lost to it, 1045-1260 vs 1287-1432 TF (profiles/gemm_wgrad_mfma16_vs_32.json); the kernel above
+// differs in its 32-row regions, per-slot address formation, in-place A refill and a three-slot DMA lead.
 
 // fp32 split-K slabs W[S][Mb][Nb] -> C band (+ C when accumulating), in C's dtype.  Fixed summation order.
 template <typename OutT, bool ACCUM>
@@ -354,7 +374,7 @@ GemmTnPlan gemm_tn_plan(int64_t M, int64_t N, int64_t K) {
 void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
              int64_t ldc, int out_dtype, bool accumulate, hipStream_t st, const GemmTnPlan* plan,
              float* workspace) {
-  const size_t lds = 0;   // static: 8 x 16 KB regions
+  const size_t lds = 0;   // static: 5 x 32 KB regions
   const dim3 block(GNT);
   auto launch = [&](const bf16* a, const bf16* b, void* c, int64_t m, int64_t n, int64_t k, int64_t ldc_, int S,
                     bool f32_out, bool acc, int64_t cstride) {
@@ -366,10 +386,10 @@ void gemm_tn(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_
 #define DPH_GEMM_LAUNCH(T, ACC)                                                                                \
   do {                                                                                                         \
     if (ACC || vec_c)                                                                                          \
-      hipLaunchKernelGGL((gemm_tn_stag_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,  \
+      hipLaunchKernelGGL((gemm_tn16_k<T, ACC>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, (int)k,     \
                          lda, ldb, ldc_, cstride);                                                             \
     else                                                                                                       \
-      hipLaunchKernelGGL((gemm_tn_stag_k<T, false, false>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n, \
+      hipLaunchKernelGGL((gemm_tn16_k<T, false, false>), grid, block, lds, st, a, b, (T*)c, (int)m, (int)n,    \
                          (int)k, lda, ldb, ldc_, cstride);                                                     \
   } while (0)
     if (!f32_out && out_dtype == kBF16) {

@@ -352,7 +352,7 @@ def test_embedding(dph_native):
                           (192, 256, 256, torch.float32, False), (128, 512, 256, torch.float32, True)])
 @pytest.mark.parametrize("tail", [0, 3, 8])
 def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate, tail):
-    """C (+)= A^T B with token-major A [K, M], B [K, N] (weight gradient dW = dY^T X) on the staggered pipeline
+    """C (+)= A^T B with token-major A [K, M], B [K, N] (weight gradient dW = dY^T X) on the 16x16x32 slot pipeline
     (K = 64 / 128 / 192 exercise the one- and two-K-step tails of the pipeline).  tail > 0 plans the partial-last-
     wave split for that many CUs, so the small shapes take the split-K band + fp32 slab reduction path."""
     torch.ops.dph.gemm_tn_tail_(tail)
