@@ -56,6 +56,14 @@ __device__ __forceinline__ void glds16(const char* sbase, unsigned voff, unsigne
 template <int N>
 __device__ __forceinline__ void wait_vm() { wait_vmcnt<N>(); }
 
+template <int N, typename F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, F, I + 1>(static_cast<F&&>(f));
+  }
+}
+
 // ---- The kernel: v_mfma_f32_16x16x32_bf16 (profiles/r5/mfma_power/: 12 % more TFLOP/J and 15 % more TFLOP/s than
 // 32x32x16 on register operands, the clock held 14 % higher) ----
 // Wave tile 128 x 64 = 8 x 4 tiles of 16 x 16 (32 f32x4 accumulators, 128 VGPRs).  A slot is 32 k-rows (one MFMA's
@@ -66,10 +74,12 @@ __device__ __forceinline__ void wait_vm() { wait_vmcnt<N>(); }
 // (((row >> 2) & 1) << 1): the two 16-lane groups of a half-wave read rows 4 apart, and the extra bit sends them to
 // disjoint slots, so a half-wave's 32 transposed 8-B reads cover all 64 banks once.
 // Pipeline: slot S retires DMA pair S+1 (pairs S+2, S+3 stay in flight: three slots of MFMA work hide each copy),
-// meets the other waves at the barrier, issues pair S+4 into region (S+4) % 5 -- the region pair S-1 left, which every
-// wave finished multiplying before this barrier -- and runs the 32 MFMAs of region S while the fragments of region S+1
-// are read: B into the other B set first, then each A row refilled right after its own 4 MFMAs.  Pairs past the end
-// re-load the last pair into a region nobody multiplies.
+// meets the other waves at the barrier and runs the 32 MFMAs of region S while the fragments of region S+1 are read: B
+// into the other B set first, then each A row refilled right after its own 4 MFMAs.  Pair S+4 goes into region
+// (S+4) % 5 -- the region pair S-1 left, which every wave finished multiplying before this barrier -- one DMA
+// instruction after every other MFMA row (+2-4 % over issuing all four right after the barrier, where each one's M0
+// save / set / restore held the matrix pipe: profiles/r5/wgrad_spread/).  Pairs past the end re-load the last pair into
+// a region nobody multiplies.
 // Measured against the round-2..5 kernel (32x32x16, 128 x 64 wave tile, waves 4..7 one barrier behind; deleted), one
 // box, interleaved (profiles/r5/wgrad16/): w13 / wqkv / w2 1255-1264 / 1296-1301 / 1312-1313 TFLOP/s vs 1202-1206 /
 // 1245-1248 / 1252-1254 at 1.71-1.85 vs 1.60-1.64 GHz, 7B step 28 425-28 436 vs 28 225-28 316 tokens/s.  The same
@@ -118,15 +128,19 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)lds + (threadIdx.x >> 6) * 1024);
 
   const int NP = K / 32;
-  auto dma_pair = [&](int P, auto RI) {
-    const unsigned d = lds_wave + decltype(RI)::value * REG16;
+  // DMA instruction i (< 4) of pair P: A rows 0..15 / 16..31, B rows 0..15 / 16..31
+  auto dma_piece = [&](int P, auto RI, auto II) {
+    constexpr int i = decltype(II)::value;
+    const unsigned d = lds_wave + decltype(RI)::value * REG16 + (i >> 1) * 16384 + (i & 1) * 8192;
     const int Pc = min(P, NP - 1);   // past the end: the last pair again, into a region nobody multiplies
-    const char* ga = Ag + Pc * stepA;
-    const char* gb = Bg + Pc * stepB;
-    glds16(ga, voffA, d);
-    glds16(ga, voffA + hopA, d + 8192);
-    glds16(gb, voffB, d + 16384);
-    glds16(gb, voffB + hopB, d + 16384 + 8192);
+    if constexpr (i < 2) glds16(Ag + Pc * stepA, voffA + (i & 1) * hopA, d);
+    else glds16(Bg + Pc * stepB, voffB + (i & 1) * hopB, d);
+  };
+  auto dma_pair = [&](int P, auto RI) {
+    dma_piece(P, RI, std::integral_constant<int, 0>{});
+    dma_piece(P, RI, std::integral_constant<int, 1>{});
+    dma_piece(P, RI, std::integral_constant<int, 2>{});
+    dma_piece(P, RI, std::integral_constant<int, 3>{});
   };
   // region base as an opaque wave-uniform value: the 12 per-lane addresses are formed per slot (12 VALU) instead of
   // being hoisted out of the loop for all 5 regions (60 live VGPRs)
@@ -152,14 +166,17 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
 
   // the 32 MFMAs of the current region, row by row; row mt's A fragment is refilled from the next region right after
   // its 4 MFMAs (one A set, rotated in place; B, used by every row, has two sets)
-  auto mma_refill = [&](bf16x8 (&af)[8], const bf16x8 (&bfr)[4], const char* rn) {
-#pragma unroll
-    for (int mt = 0; mt < 8; ++mt) {
+  // ... and the next pair's DMA spread over the rows (one instruction after every other row), so no run of DMA issue
+  // (each an M0 save / set / restore) holds the matrix pipe at the start of the slot
+  auto mma_refill = [&](bf16x8 (&af)[8], const bf16x8 (&bfr)[4], const char* rn, int P, auto RI) {
+    static_for<8>([&](auto MI) {
+      constexpr int mt = decltype(MI)::value;
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt)
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
       af[mt] = tr2(rn, aoff[mt], aoff[mt] + 16 * ROWB);
-    }
+      if constexpr (mt & 1) dma_piece(P, RI, std::integral_constant<int, mt / 2>{});
+    });
   };
 
   // prologue: pairs 0..3 (regions 0..3), pair 0 retired by every wave before the common barrier
@@ -183,11 +200,10 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    dma_pair(P0 + S + 4, std::integral_constant<int, (S + 4) % R16>{});
     __builtin_amdgcn_s_setprio(1);
     const char* rn = region(std::integral_constant<int, (S + 1) % R16>{});
     read_b(rn, bfn);
-    mma_refill(af, bfc, rn);
+    mma_refill(af, bfc, rn, P0 + S + 4, std::integral_constant<int, (S + 4) % R16>{});
     // B reads (8) then per row 4 MFMAs + its 2 A reads
     for (int i = 0; i < 8; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -279,6 +295,9 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
 }
 
 
+// Rejected (round 5, profiles/r5/wgrad_w4/): a 4-wave form, one wave per SIMD with a 128 x 128 wave tile (256
+// accumulators in AGPRs, a third less LDS traffic per FLOP): 1272-1275 vs 1296-1302 TFLOP/s on w13 at 1.97 vs 1.78 GHz,
+// MFMA busy 0.65 -- below the power cap, one wave cannot hide its own barrier and read latency.
 // History: a round-2..4 16x16x32 form of the 32x32x16 pipeline (pairs of 16-row regions per MFMA, 12 region-address
 // VALU ops per slot) lost to it, 1045-1260 vs 1287-1432 TF (profiles/gemm_wgrad_mfma16_vs_32.json); the kernel above
 // differs in its 32-row regions, per-slot address formation, in-place A refill and a three-slot DMA lead.
