@@ -472,6 +472,10 @@ __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
   }
 }
 
+// Rejected in round 5 (profiles/r5/nt16_slots/): STORE mode on the weight-gradient kernel's lockstep slot pipeline
+// (32-k slots in a 5-region ring, DMA three slots ahead, one ds_read_b128 per fragment): 1221-1275 TFLOP/s against
+// 1482-1515 for this kernel and 1439-1601 for hipBLASLt on the 7B shapes -- a 32-k slot of a K-contiguous operand is a
+// 64-B piece of every row, half a cache line per DMA lane.
 // Rejected variants (code removed; evidence kept): the same pipeline on v_mfma_f32_32x32x16_bf16 (0.86-0.96x this
 // kernel, profiles/r4/nt_mfma32/; at the 1400 W package limit it delivers 0.98-1.00 TFLOP/J against 1.06-1.09 here
 // and 1.10-1.14 for hipBLASLt, profiles/r5/gemm_power/), the two-phase form without the B0 look-ahead (LOOK = 0,
