@@ -31,7 +31,9 @@ typedef __attribute__((address_space(3))) i16x4 lds_i16x4_g;
 
 constexpr int GBM = 256, GBN = 256, GBK = 64, GNT = 512;
 constexpr int ROWB = GBM * 2;              // bytes per LDS image row (256 bf16)
-constexpr int GROUP_M = 8;
+// 4 tiles tall: w13 / wqkv +1.5-2 %, w2 / wo equal against 8 (16: -4 %; 2, 3, 6 no better than 4), interleaved on one
+// box (profiles/r5/wgrad_tune/)
+constexpr int GROUP_M = 4;
 
 // Tile (tm, tn) of logical workgroup lin: columns of GROUP_M-tall tile groups, m fastest, so the workgroups an XCD
 // runs together share GROUP_M A panels and a few B panels in its L2.
