@@ -1,5 +1,5 @@
-// Flash attention backward for CDNA4 (gfx950): delta = rowsum(dO * O), the KV-stationary dK/dV kernel, the
-// Q-stationary dQ kernel and their launcher.  Design notes at the top of attention_common.h.
+// Flash attention backward for CDNA4 (gfx950): the Q-stationary dQ kernel (which also forms delta = rowsum(dO * O)),
+// the KV-stationary dK/dV kernel and their launcher.  Design notes at the top of attention_common.h.
 #include "attention_common.h"
 
 namespace dph {
@@ -7,32 +7,6 @@ namespace dph {
 // ==================================================================================================
 // Backward
 // ==================================================================================================
-// delta[b, h, q] = sum_d dO[b,q,h,d] * O[b,q,h,d] (fp32).  TPR = D/8 lanes per row, 8 elements per lane;
-// rows are enumerated (b, q, h) so a wave reads 64 * 16 contiguous bytes of each [B, S, H, D] operand.
-template <int TPR>
-__global__ __launch_bounds__(256) void attn_delta_k(const bf16* __restrict__ o, const bf16* __restrict__ dout,
-                                                    float* __restrict__ delta, int B, int S, int H,
-                                                    int64_t o_sb, int64_t o_ss, int64_t o_sh, int64_t d_sb,
-                                                    int64_t d_ss, int64_t d_sh) {
-  constexpr int RPB = 256 / TPR;  // rows per block-iteration
-  const int sub = threadIdx.x % TPR;
-  const int64_t rows = (int64_t)B * H * S;
-  for (int64_t r = (int64_t)blockIdx.x * RPB + threadIdx.x / TPR; r < rows; r += (int64_t)gridDim.x * RPB) {
-    const int hh = (int)(r % H);
-    const int64_t bq = r / H;
-    const int q = (int)(bq % S), bb = (int)(bq / S);
-    float x[8], y[8];
-    Vec8<bf16>::load(o + bb * o_sb + (int64_t)q * o_ss + hh * o_sh + sub * 8, x);
-    Vec8<bf16>::load(dout + bb * d_sb + (int64_t)q * d_ss + hh * d_sh + sub * 8, y);
-    float acc = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc += x[k] * y[k];
-#pragma unroll
-    for (int m = TPR / 2; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
-    if (sub == 0) delta[((int64_t)bb * H + hh) * S + q] = acc;
-  }
-}
-
 // ---- dK / dV: KV-stationary.  One workgroup = 4 waves = 128 keys of one (batch, kv head); one wave =
 // 32 keys whose K^T / V^T B-operand fragments stay in registers.  The workgroup sweeps every query head
 // of the GQA group x 32-row query tiles (double-buffered Q / dO LDS images, one barrier per tile).
@@ -324,11 +298,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
     qf[kk] = ok ? *reinterpret_cast<const bf16x8*>(qp + (int64_t)myq * p.q_ss + kk * 16 + 8 * h) : zero8();
     df[kk] = ok ? *reinterpret_cast<const bf16x8*>(dop + (int64_t)myq * P.do_ss + kk * 16 + 8 * h) : zero8();
   }
+  // delta = rowsum(dO * O) of this lane's query, formed here from the dO fragments already in registers plus the same
+  // slice of O (the two half-waves hold complementary halves of the row), and written out for the dK/dV kernel, which
+  // runs after this one: no separate delta pass over dO and O
   float nlse2 = 0.f, delta = 0.f;  // -lse in log2 units
-  if (myq < p.Sq) {
-    const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + myq;
-    nlse2 = -p.lse[idx] * 1.4426950408889634f;
-    delta = P.delta[idx];
+  {
+    const bf16* opp = (const bf16*)p.o + (int64_t)b * p.o_sb + (int64_t)hq * p.o_sh;
+    float part = 0.f;
+    if (myq < p.Sq) {
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(opp + (int64_t)myq * p.o_ss + kk * 16 + 8 * h);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part += (float)df[kk][j] * (float)ov[j];
+      }
+    }
+    delta = half_sum(part);
+    if (myq < p.Sq) {
+      const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + myq;
+      nlse2 = -p.lse[idx] * 1.4426950408889634f;
+      if (h == 0) P.delta[idx] = delta;
+    }
   }
 
   int kv_end = p.Sk;
@@ -456,14 +446,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
 template <int HD, bool DROP>
 static void bwd_launch_t(const AttnBwdParams& P, hipStream_t st) {
   const AttnParams& p = P.f;
-  const size_t lds_kv = 128 * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
-  const dim3 grid_kv((unsigned)((p.Sk + 127) / 128 * p.Hkv * p.B));
-  if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, DROP>), grid_kv, dim3(256), lds_kv, st, P);
-  else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, DROP>), grid_kv, dim3(256), lds_kv, st, P);
+  // dQ first: it forms delta = rowsum(dO * O) for its rows and writes it for the dK/dV kernel
   const size_t lds_q = 2 * 2 * 64 * HD * 2;
   const dim3 grid_q((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
   if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, DROP>), grid_q, dim3(256), lds_q, st, P);
   else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, DROP>), grid_q, dim3(256), lds_q, st, P);
+  const size_t lds_kv = 128 * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
+  const dim3 grid_kv((unsigned)((p.Sk + 127) / 128 * p.Hkv * p.B));
+  if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, DROP>), grid_kv, dim3(256), lds_kv, st, P);
+  else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, DROP>), grid_kv, dim3(256), lds_kv, st, P);
 }
 
 template <int HD>
@@ -475,18 +466,6 @@ static void bwd_launch(const AttnBwdParams& P, hipStream_t st) {
 void flash_attn_bwd(const AttnBwdParams& P, hipStream_t st) {
   const AttnParams& p = P.f;
   if (p.B == 0 || p.Sq == 0) return;
-  const int64_t rows = (int64_t)p.B * p.Hq * p.Sq;
-  auto delta = [&](auto kern, int tpr) {
-    hipLaunchKernelGGL(kern, dim3(stream_grid(rows, 256 / tpr)), dim3(256), 0, st, (const bf16*)p.o,
-                       (const bf16*)P.dout, P.delta, p.B, p.Sq, p.Hq, p.o_sb, p.o_ss, p.o_sh, P.do_sb, P.do_ss,
-                       P.do_sh);
-  };
-  switch (p.D) {
-    case 32: delta(attn_delta_k<4>, 4); break;
-    case 64: delta(attn_delta_k<8>, 8); break;
-    case 128: delta(attn_delta_k<16>, 16); break;
-    default: return;
-  }
   switch (p.D) {
     case 32: bwd_launch<32>(P, st); break;
     case 64: bwd_launch<64>(P, st); break;

@@ -1,5 +1,5 @@
 // Device-side building blocks shared by the flash-attention kernels (attention.hip: forward; attention_bwd.hip:
-// delta, dK/dV and dQ).  The two kernel families are separate translation units so each is compiled with the flags
+// dQ + delta, then dK/dV).  The two kernel families are separate translation units so each is compiled with the flags
 // that suit it (csrc/build.py PER_FILE_HIP_FLAGS).
 //
 // Flash attention forward + backward for CDNA4 (gfx950), bf16 in / fp32 accumulate, MFMA 32x32x16.
@@ -15,7 +15,7 @@
 // transposed LDS reads.  K/V tiles (64 keys) are register-staged into a double-buffered, XOR-swizzled
 // LDS image (conflict-free for both ds_read_b128 row reads and tr reads), one barrier per tile.
 //
-// Backward (no atomics, no dS round trip through LDS): two kernels after a delta = rowsum(dO*O) pass.
+// Backward (no atomics, no dS round trip through LDS): two kernels; the first (dQ) also forms delta = rowsum(dO*O).
 //   dK/dV kernel, KV-stationary: a wave keeps its 32 keys' K^T / V^T fragments and dK^T / dV^T in registers
 //   while the workgroup sweeps query tiles; S and dP are computed with the key on the lane so P and dS are
 //   directly the B operands of dV^T += dO^T P and dK^T += Q^T dS.
