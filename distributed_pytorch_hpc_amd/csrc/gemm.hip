@@ -299,7 +299,9 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
 
 // Rejected (round 5, profiles/r5/wgrad_w4/): a 4-wave form, one wave per SIMD with a 128 x 128 wave tile (256
 // accumulators in AGPRs, a third less LDS traffic per FLOP): 1272-1275 vs 1296-1302 TFLOP/s on w13 at 1.97 vs 1.78 GHz,
-// MFMA busy 0.65 -- below the power cap, one wave cannot hide its own barrier and read latency.
+// MFMA busy 0.65 -- below the power cap, one wave cannot hide its own barrier and read latency.  With the DMA spread
+// over its rows (offsets recomputed per instruction, no spills in the main loop) it fell to 1011-1074 vs 1363-1429 at
+// 2.2 GHz (profiles/r5/wgrad_w4/spread_*).
 // History: a round-2..4 16x16x32 form of the 32x32x16 pipeline (pairs of 16-row regions per MFMA, 12 region-address
 // VALU ops per slot) lost to it, 1045-1260 vs 1287-1432 TF (profiles/gemm_wgrad_mfma16_vs_32.json); the kernel above
 // differs in its 32-row regions, per-slot address formation, in-place A refill and a three-slot DMA lead.
