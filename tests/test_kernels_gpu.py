@@ -349,12 +349,15 @@ def test_embedding(dph_native):
 @pytest.mark.parametrize("K,M,N,out_dtype,accumulate",
                          [(512, 256, 256, torch.float32, False), (1024, 512, 768, torch.bfloat16, False),
                           (2048, 768, 512, torch.bfloat16, True), (64, 256, 512, torch.float32, True),
-                          (192, 256, 256, torch.float32, False), (128, 512, 256, torch.float32, True)])
+                          (192, 256, 256, torch.float32, False), (128, 512, 256, torch.float32, True),
+                          (256, 256, 512, torch.bfloat16, False), (576, 512, 256, torch.float32, True),
+                          (640, 256, 256, torch.bfloat16, False)])
 @pytest.mark.parametrize("tail", [0, 3, 8])
 def test_gemm_tn_wgrad(dph_native, K, M, N, out_dtype, accumulate, tail):
-    """C (+)= A^T B with token-major A [K, M], B [K, N] (weight gradient dW = dY^T X) on the 16x16x32 slot pipeline
-    (K = 64 / 128 / 192 exercise the one- and two-K-step tails of the pipeline).  tail > 0 plans the partial-last-
-    wave split for that many CUs, so the small shapes take the split-K band + fp32 slab reduction path."""
+    """C (+)= A^T B with token-major A [K, M], B [K, N] (weight gradient dW = dY^T X) on the 16x16x32 slot pipeline.
+    K = 64 ... 640 is 2 ... 20 slots of 32 tokens: every remainder of the 10-slot unrolled loop that K % 64 allows.
+    tail > 0 plans the partial-last-wave split for that many CUs, so the small shapes take the split-K band + fp32
+    slab reduction path."""
     torch.ops.dph.gemm_tn_tail_(tail)
     torch.manual_seed(0)
     a = torch.randn(K, M, device=DEV, dtype=torch.bfloat16)
