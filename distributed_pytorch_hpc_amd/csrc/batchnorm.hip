@@ -361,12 +361,9 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_dx_k(const T* __restrict__ dy, c
     ms[i] = XMASK ? ss[c] : 0.f;
     mb[i] = XMASK ? ss[C + c] : 0.f;
   }
-  for (int64_t v = v0; v < nvec; v += (int64_t)gridDim.x * BN_NT) {
-    float g[8], xv[8], yv[8], o[8];
-    Vec8<T>::load(dy + v * 8, g);
-    Vec8<T>::load(x + v * 8, xv);
-    if (RELU && !XMASK && !BMASK) Vec8<T>::load(y + v * 8, yv);
-    const unsigned bits = BMASK ? bmask[v] : 0u;
+  const int64_t stride = (int64_t)gridDim.x * BN_NT;
+  auto one = [&](int64_t v, float (&g)[8], const float (&xv)[8], const float (&yv)[8], unsigned bits) {
+    float o[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const bool on = BMASK ? ((bits >> i) & 1u) != 0u
@@ -378,6 +375,32 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_dx_k(const T* __restrict__ dy, c
     }
     Vec8<T>::store(dx + v * 8, o);
     if (DRES) Vec8<T>::store(dres + v * 8, g);
+  };
+  // two vectors per iteration, both loads issued before either is used: twice the 16-B loads in flight per thread.
+  // Backward with the ReLU mask from x 5.66-5.75 -> 5.47-5.52 ms per ResNet-50 step of BN layers, the residual form
+  // unchanged (benchmarks/bn_bench.py, profiles/r5/bn_unroll3/); four vectors, and unrolling the apply and reduce
+  // passes the same way, measured no better or worse (profiles/r5/bn_unroll/, bn_unroll2/).
+  int64_t v = v0;
+  for (; v + stride < nvec; v += 2 * stride) {
+    float g[2][8], xv[2][8], yv[2][8];
+    unsigned bits[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t w = v + u * stride;
+      Vec8<T>::load(dy + w * 8, g[u]);
+      Vec8<T>::load(x + w * 8, xv[u]);
+      if (RELU && !XMASK && !BMASK) Vec8<T>::load(y + w * 8, yv[u]);
+      bits[u] = BMASK ? bmask[w] : 0u;
+    }
+    one(v, g[0], xv[0], yv[0], bits[0]);
+    one(v + stride, g[1], xv[1], yv[1], bits[1]);
+  }
+  if (v < nvec) {
+    float g[8], xv[8], yv[8];
+    Vec8<T>::load(dy + v * 8, g);
+    Vec8<T>::load(x + v * 8, xv);
+    if (RELU && !XMASK && !BMASK) Vec8<T>::load(y + v * 8, yv);
+    one(v, g, xv, yv, BMASK ? bmask[v] : 0u);
   }
 }
 
