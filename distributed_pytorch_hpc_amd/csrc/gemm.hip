@@ -168,8 +168,11 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
 
   // the 32 MFMAs of the current region, row by row; row mt's A fragment is refilled from the next region right after
   // its 4 MFMAs (one A set, rotated in place; B, used by every row, has two sets)
-  // ... and the next pair's DMA spread over the rows (one instruction after every other row), so no run of DMA issue
-  // (each an M0 save / set / restore) holds the matrix pipe at the start of the slot
+  // ... and the next pair's DMA issued behind the first two rows (two instructions after row 0, two after row 1): early
+  // enough for the longest latency slack, yet not ahead of the slot's first MFMAs. A/B on one box (profiles/r5/dma_place,
+  // 3 wgrad shapes x 2 rounds): one instruction after every odd row 1 393 / 1 420 / 1 373 TFLOP/s; after rows 0-3
+  // +0.6 %; before rows 0-3 +0.8 %; after rows 1-4 +-0; two after rows 0 and 2 +1.1 %; two after rows 0 and 1 +1.4 %;
+  // all four after row 0 +1.4 %
   auto mma_refill = [&](bf16x8 (&af)[8], const bf16x8 (&bfr)[4], const char* rn, int P, auto RI) {
     static_for<8>([&](auto MI) {
       constexpr int mt = decltype(MI)::value;
@@ -177,7 +180,10 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tn16_k(const bf16* __restrict__ A
       for (int nt = 0; nt < 4; ++nt)
         acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], bfr[nt], acc[mt][nt], 0, 0, 0);
       af[mt] = tr2(rn, aoff[mt], aoff[mt] + 16 * ROWB);
-      if constexpr (mt & 1) dma_piece(P, RI, std::integral_constant<int, mt / 2>{});
+      if constexpr (mt < 2) {
+        dma_piece(P, RI, std::integral_constant<int, 2 * mt>{});
+        dma_piece(P, RI, std::integral_constant<int, 2 * mt + 1>{});
+      }
     });
   };
 
