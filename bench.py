@@ -26,6 +26,10 @@ and spread of rank 0's per-step device times ("step_ms", CUDA events between con
     python bench.py [--gpus N] [--steps K] [--warmup W] [--layout dp|tp|hybrid|pp|resnet-fsdp|unet-ddp]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+
+Ranks: under a launcher (torchrun, runtime/launch.py, mpiexec, srun) its world size must equal --gpus, or the run
+exits 2 before any work.  Without one, --gpus N > 1 starts its own N ranks (runtime/launch.py, one per GPU, before
+this process touches a GPU) and exits non-zero if any rank fails or if fewer than N GPUs are visible for RCCL.
 """
 from __future__ import annotations
 
@@ -127,11 +131,53 @@ def _fail(code: int, msg: str):
     os._exit(code)   # a rank that failed a check must not wait in a collective the others never reach
 
 
+def _self_launch(args, argv) -> int:
+    """``--gpus N > 1`` with no launcher around us: start N fresh ranks through the framework's own launcher.
+
+    This process never touches the GPU (``torch.cuda.device_count()`` does not initialise HIP on this image): it checks
+    that N ranks can each own a device, spawns N children of this same script with the torchrun environment
+    (runtime/launch.py: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free MASTER_PORT, NUMA binding),
+    waits, and returns the gang's exit code -- non-zero as soon as any rank fails (the watchdog tears the others down,
+    so no rank is left in a collective).  Rank 0 prints the one JSON line to the shared stdout.
+    (Reference: scripts/torchrun_multigpu_pbs.sh:152 wraps every multi-GPU run in an external torchrun.)"""
+    import types
+
+    from distributed_pytorch_hpc_amd.runtime import launch
+
+    backend = "gloo" if args.device == "cpu" else (args.backend or "nccl")
+    if args.device != "cpu" and backend == "nccl":
+        visible = torch.cuda.device_count()
+        if visible < args.gpus:
+            _fail(2, f"--gpus {args.gpus}: only {visible} GPU(s) visible; RCCL needs one GPU per rank "
+                     f"(no N=1 number is reported in place of an N={args.gpus} one)")
+    argv = list(sys.argv[1:] if argv is None else argv)
+    largs = types.SimpleNamespace(nproc=args.gpus, master_addr="127.0.0.1", master_port=0, backend=None,
+                                  log_dir=None, max_restarts=0, timeout=0.0, grace=10.0, omp_threads=0,
+                                  cpu_bind="numa" if args.device != "cpu" else "none",
+                                  script=os.path.abspath(__file__), script_args=argv)
+    if not args.quiet:
+        print(f"[bench] launching {args.gpus} ranks (runtime/launch.py, backend {backend})", file=sys.stderr,
+              flush=True)
+    code = launch.run(largs)
+    if code != 0:
+        print(f"[bench] FATAL: the {args.gpus}-rank run failed (exit {code})", file=sys.stderr, flush=True)
+    return code
+
+
 def main(argv=None):
     args = parse(argv)
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     from distributed_pytorch_hpc_amd.runtime import env as rt
     from distributed_pytorch_hpc_amd.runtime import preflight
+
+    info = rt.get_rank_info()
+    if args.gpus < 1:
+        _fail(2, f"--gpus {args.gpus}: need at least one rank")
+    if info.launcher == "single" and args.gpus > 1:
+        sys.exit(_self_launch(args, argv))
+    if info.world_size != args.gpus:
+        # an N=1 number must never be reported as N=8 (nor the reverse): a launcher / flag mismatch is fatal
+        _fail(2, f"--gpus {args.gpus} but the launcher ({info.launcher}) started {info.world_size} rank(s)")
+    world_env = info.world_size
 
     cpu = args.device == "cpu"
     if world_env > 1 or not args.no_dist:
@@ -142,8 +188,8 @@ def main(argv=None):
         rank, world, local = 0, 1, 0
         if not cpu:
             torch.cuda.set_device(0)
-    if world != args.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting n_gpus={world}", file=sys.stderr)
+    if world != args.gpus:
+        _fail(2, f"rank {rank}: --gpus {args.gpus} but the process group has {world} ranks")
     dev = torch.device("cpu") if cpu else torch.device("cuda", torch.cuda.current_device())
     sync = (lambda: None) if cpu else torch.cuda.synchronize
 

@@ -73,6 +73,8 @@ class XgmiAllReduce:
         table = torch.tensor([list(h) for h in handles], dtype=torch.uint8)
         ops.car_open(self.ctx, table.contiguous())
         dist.barrier(group=group)
+        self._flag = None           # int32 [1] device scratch of the step guard (guard_update)
+        self._guard_event = None    # event after the last guard: its verdict is readable once it completes
 
     # ------------------------------------------------------------------------------------------------
     def supports(self, t: torch.Tensor) -> bool:
@@ -102,6 +104,11 @@ class XgmiAllReduce:
         """Non-zero once a barrier of this rank's kernels timed out (0 when healthy).  No device synchronisation:
         the kernel writes a host-mapped word, so a kernel still in flight reports on a later call."""
         return int(self._ops.car_status(self.ctx))
+
+    def agreed_error(self) -> int:
+        """The group-agreed verdict written by the last ``guard_update`` (non-zero: some rank's barrier timed out).
+        Authoritative once that guard's event has completed."""
+        return int(self._ops.car_agreed(self.ctx))
 
     def close(self):
         if getattr(self, "ctx", None):
@@ -147,9 +154,14 @@ def clear_policy(group=None) -> None:
     _ANY_BACKEND.discard(_key(group))
 
 
+_DEAD: set = set()        # group keys whose direct-peer path failed its health check: never used again
+
+
 def policy_max_bytes(group) -> int:
-    """Largest message (bytes) the direct-peer path takes on ``group``: the env override, else the measured
-    crossover, else 0."""
+    """Largest message (bytes) the direct-peer path takes on ``group``: 0 once the group's path failed a health check
+    (whatever the environment says), else the env override, else the measured crossover, else 0."""
+    if _key(group) in _DEAD:
+        return 0
     env = os.environ.get("DPH_CUSTOM_ALLREDUCE")
     if env == "1":
         return custom_allreduce_max_bytes()
@@ -231,6 +243,34 @@ def probe_crossover(group=None, sizes=(4 << 10, 16 << 10, 64 << 10, 256 << 10, 1
             "crossover_bytes": choose_crossover(samples) if verified else 0}
 
 
+def active() -> bool:
+    """True when some group has a live direct-peer instance (the engines then run ``guard_update`` every step)."""
+    return any(car is not None for car in _CACHE.values())
+
+
+def guard_update(gscale: torch.Tensor) -> None:
+    """Stream-ordered health guard: call between a step's last reduction and its optimizer kernels, on the stream
+    that runs them, with the step's device gradient scale.  For every live direct-peer instance (in cache order,
+    which is the same on every rank: instances are created collectively) it copies this rank's barrier-timeout word
+    to the device, MAX-all-reduces it over the instance's group through the process-group backend (never through the
+    possibly broken path itself) and, if any rank of the group timed out, sets ``gscale`` to NaN -- the optimizer
+    kernels then skip the update on every rank of the group alike -- and records the agreed verdict for
+    ``check_health``.  Every rank of every such group must call it (the engines do, once per step).
+    Advisor r5: the host-side check alone ran before the update kernels were queued, so the update of the step whose
+    all-reduce timed out still ran on its sums; and the per-rank word let only the waiting ranks disable the path."""
+    for car in list(_CACHE.values()):
+        if car is None:
+            continue
+        if car._flag is None or car._flag.device != gscale.device:
+            car._flag = torch.zeros(1, dtype=torch.int32, device=gscale.device)
+        car._ops.car_flag(car.ctx, car._flag)
+        dist.all_reduce(car._flag, op=dist.ReduceOp.MAX, group=car.group)
+        car._ops.car_poison(car.ctx, car._flag, gscale)
+        ev = torch.cuda.Event()
+        ev.record()
+        car._guard_event = ev
+
+
 def drop(group=None) -> None:
     """Forget ``group``'s direct-peer instance (after a failed probe; every rank calls it alike): nothing is ever
     routed to it again, and a barrier timeout it recorded does not surface later as a training-step
@@ -248,20 +288,39 @@ class XgmiAllReduceError(RuntimeError):
 
 
 def check_health() -> None:
-    """Raise XgmiAllReduceError if any cached direct-peer all-reduce recorded a barrier timeout, after turning the
-    path off for that group (RCCL takes every later message).  A timed-out barrier lets the kernel finish with
-    whatever the late peer's staging buffer held, so the affected step's sums are not trustworthy: the engines call
-    this once per optimizer step (host-memory read, no device sync) and stop instead of training on them."""
+    """Raise XgmiAllReduceError if a direct-peer all-reduce barrier timed out, after turning the path off for that
+    group for good (``_DEAD``: RCCL takes every later message, ``DPH_CUSTOM_ALLREDUCE=1`` included).
+
+    A timed-out barrier lets the kernel finish with whatever the late peer's staging buffer held.  The update that
+    would consume such sums is already skipped on the device by ``guard_update`` (same step, every rank of the group);
+    this host check reports it.  It reads the group-agreed verdict of the previous step's guard after that guard's
+    event (in steady state it completed long ago: the host is at most one step ahead), so every rank raises at the
+    same step and drops the same groups -- a caller that catches the error keeps routing identically on every rank.
+    The timeout of the current step's reductions is reported at the next step.  An instance that never ran a guard
+    (direct use, inference) falls back to this rank's own timeout word."""
     bad = []
     for key, car in list(_CACHE.items()):
-        if car is not None and car.errors():
+        if car is None:
+            continue
+        if car._guard_event is not None:
+            car._guard_event.synchronize()
+            failed = car.agreed_error()
+        else:
+            failed = car.errors()
+        if failed:
             bad.append(key)
-            _POLICY.pop(key, None)
+    for key in bad:
+        _DEAD.add(key)
+        _POLICY.pop(key, None)
+        car = _CACHE.get(key)
+        _CACHE[key] = None
+        if car is not None:
+            car.close()
     if bad:
         raise XgmiAllReduceError(
             f"direct-peer xGMI all-reduce barrier timed out on {len(bad)} group(s) (a peer stalled > "
-            f"{_TIMEOUT_S:.0f} s); gradients / activations reduced through it in this step may be wrong. The path is "
-            "now disabled for those groups.")
+            f"{_TIMEOUT_S:.0f} s); the optimizer update that would have used those sums was skipped on every rank of "
+            "the group, and the path is now disabled for those groups.")
 
 
 _TIMEOUT_S = 10.0
@@ -274,6 +333,8 @@ def get_custom_allreduce(group=None) -> Optional[XgmiAllReduce]:
     if dist.get_backend(group) != "nccl" and _key(group) not in _ANY_BACKEND:
         return None
     key = _key(group)
+    if key in _DEAD:
+        return None
     if key not in _CACHE:
         try:
             # staging sized for the probe's largest message (16 MiB) or a larger forced / recorded limit

@@ -66,9 +66,11 @@ def sp_chunks(group, n_local: int = 0) -> int:
 
 
 def _tok_shape(x: torch.Tensor, factor_num: int, factor_den: int = 1):
-    assert x.dim() >= 2, "token-sharded tensors are [..., tokens, D] with at least two dims"
+    """Shape of the gathered / scattered token tensor: [B, S, D] scales S (dim 1), [T, D] scales T (dim 0).  The
+    TOKENS layout deals flattened tokens, so only token-wise ops may run on the shard (tensor_parallel.py)."""
+    assert x.dim() in (2, 3), f"token-sharded tensors are [B, S, D] or [T, D], got {list(x.shape)}"
     shp = list(x.shape)
-    shp[1] = shp[1] * factor_num // factor_den
+    shp[-2] = shp[-2] * factor_num // factor_den
     return shp
 
 
@@ -97,7 +99,8 @@ def tok_reduce_scatter(x: torch.Tensor, group) -> torch.Tensor:
     x = x.contiguous()
     d = x.shape[-1]
     t = x.numel() // d
-    assert x.shape[1] % ws == 0, f"reduce_scatter: {x.shape[1]} positions do not split over {ws} ranks"
+    assert x.dim() in (2, 3), f"token-sharded tensors are [B, S, D] or [T, D], got {list(x.shape)}"
+    assert x.shape[-2] % ws == 0, f"reduce_scatter: {x.shape[-2]} positions do not split over {ws} ranks"
     k = sp_chunks(group, t // ws)
     m = t // (ws * k)
     out = torch.empty((k * m, d), dtype=x.dtype, device=x.device)

@@ -230,7 +230,8 @@ int64_t car_create(int rank, int world, int64_t max_bytes, double timeout_s) {
   void* hp = nullptr;
   DPH_HIP_OK(hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent));
   c->err_host = static_cast<uint32_t*>(hp);
-  *c->err_host = 0u;
+  c->err_host[0] = 0u;   // this rank's barrier timeouts
+  c->err_host[1] = 0u;   // the group-agreed verdict of the last guard
   void* dp = nullptr;
   DPH_HIP_OK(hipHostGetDevicePointer(&dp, hp, 0));
   c->peers.err_host = static_cast<uint32_t*>(dp);
@@ -307,6 +308,36 @@ void car_allreduce(int64_t ctx, const void* in, void* out, int64_t bytes, int dt
   }
 #undef DPH_CAR_WORLD
 #undef DPH_CAR_LAUNCH
+}
+
+// ---- stream-ordered health guard (the engines run it between a step's reductions and its optimizer update) ----
+// car_flag copies this rank's timeout word into a device int; the caller MAX-all-reduces it over the group (RCCL);
+// car_poison then turns the step's gradient scale into NaN when any rank of the group timed out -- the optimizer
+// kernels skip their update on a NaN scale (csrc/optim.hip), on every rank alike, so sums that may hold a late peer's
+// stale staging data never reach the weights -- and records the agreed verdict in the second host-mapped word, which
+// the host reads after the guard's event (comm/custom_allreduce.py check_health): same verdict, same step, every rank.
+__global__ void car_flag_k(const uint32_t* err, int* flag) {
+  flag[0] = (int)__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void car_poison_k(const int* flag, float* gscale, uint32_t* agreed) {
+  if (flag[0] != 0) {
+    gscale[0] = __builtin_nanf("");
+    __hip_atomic_store(agreed, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+void car_flag(int64_t ctx, int* flag_dev, hipStream_t st) {
+  auto* c = reinterpret_cast<CarContext*>(ctx);
+  hipLaunchKernelGGL(car_flag_k, dim3(1), dim3(64), 0, st, c->peers.err_host, flag_dev);
+}
+void car_poison(int64_t ctx, const int* flag_dev, float* gscale_dev, hipStream_t st) {
+  auto* c = reinterpret_cast<CarContext*>(ctx);
+  hipLaunchKernelGGL(car_poison_k, dim3(1), dim3(64), 0, st, flag_dev, gscale_dev, c->peers.err_host + 1);
+}
+// The group-agreed verdict of the last guard (0 = healthy); read after the guard's event has completed.
+int64_t car_agreed(int64_t ctx) {
+  auto* c = reinterpret_cast<CarContext*>(ctx);
+  return (int64_t)__atomic_load_n(c->err_host + 1, __ATOMIC_ACQUIRE);
 }
 
 // Non-zero once any barrier of this rank's kernels timed out.  Reads the host-mapped word the kernel stores to at

@@ -326,6 +326,9 @@ int64_t car_max_bytes(int64_t ctx);
 void car_allreduce(int64_t ctx, const void* in, void* out, int64_t bytes, int dtype, int algo, float scale,
                    int max_blocks, hipStream_t stream);
 int64_t car_status(int64_t ctx);
+void car_flag(int64_t ctx, int* flag_dev, hipStream_t st);
+void car_poison(int64_t ctx, const int* flag_dev, float* gscale_dev, hipStream_t st);
+int64_t car_agreed(int64_t ctx);
 void car_destroy(int64_t ctx);
 
 }  // namespace dph

@@ -50,6 +50,7 @@ __global__ __launch_bounds__(256) void adamw_k(float* __restrict__ master, float
                                                float eps, float wd, float bc1, float bc2,
                                                const float* __restrict__ gscale, const float* __restrict__ hyper) {
   const float gs = gscale ? *gscale : 1.f;
+  if (gs != gs) return;   // NaN scale = skip this update (xGMI health guard, comm/custom_allreduce.py; NaN clip norm)
   if (hyper) {
     lr = hyper[0];
     bc1 = 1.f - powf(b1, hyper[1]);
@@ -98,6 +99,7 @@ __global__ __launch_bounds__(256) void sgd_k(float* __restrict__ master, float* 
                                              float mom, float damp, float wd, int nesterov, int first,
                                              const float* __restrict__ gscale, const float* __restrict__ hyper) {
   const float gs = gscale ? *gscale : 1.f;
+  if (gs != gs) return;   // NaN scale = skip this update (xGMI health guard, comm/custom_allreduce.py; NaN clip norm)
   if (hyper) {
     lr = hyper[0];
     first = hyper[1] == 1.f;

@@ -1259,6 +1259,21 @@ void car_allreduce_op(int64_t ctx, const Tensor& inp, Tensor& out, int64_t algo,
                      (int)max_blocks, cur_stream());
 }
 int64_t car_status_op(int64_t ctx) { return dph::car_status(ctx); }
+void car_flag_op(int64_t ctx, Tensor& flag) {
+  check_cuda(flag, "flag");
+  TORCH_CHECK(flag.scalar_type() == at::kInt && flag.numel() >= 1, "car_flag: int32 device tensor");
+  c10::DeviceGuard g(flag.device());
+  dph::car_flag(ctx, flag.data_ptr<int>(), cur_stream());
+}
+void car_poison_op(int64_t ctx, const Tensor& flag, Tensor& gscale) {
+  check_cuda(flag, "flag");
+  check_cuda(gscale, "gscale");
+  TORCH_CHECK(flag.scalar_type() == at::kInt && gscale.scalar_type() == at::kFloat && gscale.numel() >= 1,
+              "car_poison: int32 flag and float32 gscale device tensors");
+  c10::DeviceGuard g(flag.device());
+  dph::car_poison(ctx, flag.data_ptr<int>(), gscale.data_ptr<float>(), cur_stream());
+}
+int64_t car_agreed_op(int64_t ctx) { return dph::car_agreed(ctx); }
 void car_destroy_op(int64_t ctx) { dph::car_destroy(ctx); }
 
 }  // namespace
@@ -1519,6 +1534,9 @@ TORCH_LIBRARY(dph, m) {
   m.def("car_ipc_handle(int ctx) -> Tensor", &car_ipc_handle_op);
   m.def("car_open(int ctx, Tensor handles) -> ()", &car_open_op);
   m.def("car_status(int ctx) -> int", &car_status_op);
+  m.def("car_agreed(int ctx) -> int", &car_agreed_op);
+  m.def("car_flag(int ctx, Tensor(a!) flag) -> ()");
+  m.def("car_poison(int ctx, Tensor flag, Tensor(a!) gscale) -> ()");
   m.def("car_destroy(int ctx) -> ()", &car_destroy_op);
   m.def("car_allreduce(int ctx, Tensor inp, Tensor(a!) out, int algo, float scale, int max_blocks) -> ()");
 }
@@ -1577,6 +1595,8 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("bn_act_apply", &bn_act_apply);
   m.impl("bn_act_bwd", &bn_act_bwd);
   m.impl("car_allreduce", &car_allreduce_op);
+  m.impl("car_flag", &car_flag_op);
+  m.impl("car_poison", &car_poison_op);
   m.impl("latmse_fwd", &latmse_fwd);
   m.impl("latmse_bwd", &latmse_bwd);
 }

@@ -152,15 +152,16 @@ class _MatmulRSFn(torch.autograd.Function):
         return (dx.view(ctx.xshape) if ctx.needs_input_grad[0] else None), gw, None, None
 
 
-def ag_matmul(x, w, b, group, chunks: int = 2):
+def ag_matmul(x, w, b, group):
     """y = all_gather_tokens(x) @ w^T (+ b), x [B, S/tp, D] -> y [B, S, N_local].  The micro-collective count is the
-    group's token layout (comm.functional.sp_chunks; parallelize_llama sets it from the layers' ``chunks``)."""
+    group's token layout (comm.functional.sp_chunks), which every SP collective of the group shares; a layer's
+    ``async_chunks`` assignment sets it (tensor_parallel._AsyncChunks)."""
     if _ws(group) == 1:
         return torch.nn.functional.linear(x, w, b)
     return _AGMatmulFn.apply(x, w, b, group, _rounds(group, x.numel() // x.shape[-1]))
 
 
-def matmul_reduce_scatter(x, w, group, chunks: int = 2):
+def matmul_reduce_scatter(x, w, group):
     """y = reduce_scatter_tokens(x @ w^T), x [B, S, F_local] -> y [B, S/tp, D]."""
     if _ws(group) == 1:
         return torch.nn.functional.linear(x, w)

@@ -35,6 +35,7 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
+from ..comm import custom_allreduce as _car
 from ..comm.custom_allreduce import check_health as check_xgmi_health
 from ..comm.custom_allreduce import use_custom as use_custom_allreduce
 from ..ops import _lib
@@ -227,6 +228,7 @@ class DataParallelEngine:
         self.step_count = 0
         self._hyper: Optional[StepHyper] = None
         self._sync_enabled = True
+        self._tp_due = False
         self._next_launch = 0
         self._callback_queued = False
         self._gscale = torch.full((1,), 1.0 / self.world, dtype=torch.float32, device=self.device)
@@ -288,9 +290,11 @@ class DataParallelEngine:
         external optimizers -- is already complete over TP."""
         for b in self.buckets:
             self._wait_reduce(b)
-        if self._tp_partial and not getattr(self, "_tp_done", False):
+        # only after a reduction round has launched: synchronize() inside no_sync(), or before the first backward,
+        # must not all-reduce partial SP sums that later micro-steps still add to (they would be counted tp times)
+        if self._tp_partial and self._tp_due:
             self._reduce_tp_partial()
-            self._tp_done = True
+            self._tp_due = False
         check_xgmi_health()
 
     def _reduce_tp_partial(self):
@@ -365,7 +369,7 @@ class DataParallelEngine:
 
     def _launch(self, b: _Bucket):
         b.launched = True
-        self._tp_done = False   # new data-parallel sums: the TP completion of SP gradients is due again
+        self._tp_due = True   # new data-parallel sums: the TP completion of SP gradients is due again
         if self.world == 1:
             return
         g = self.grad_view(b)
@@ -477,7 +481,13 @@ class DataParallelEngine:
             self._gscale.copy_(torch.clamp(cfg.max_grad_norm / (norm + 1e-6), max=1.0) / self.world)
             self.last_grad_norm = norm
         else:
-            self._gscale.fill_(1.0 / self.world)   # (a previous step may have clipped)
+            self._gscale.fill_(1.0 / self.world)   # (a previous step may have clipped, or the guard poisoned it)
+        if _car.active():
+            # every reduction of the step (buckets, TP / SP all-reduces) is queued ahead of the guard, which skips the
+            # update on every rank if any direct-peer barrier of the group timed out (comm/custom_allreduce.py)
+            for b in self.buckets:
+                self._wait_reduce(b)
+            _car.guard_update(self._gscale)
         native = _lib.use_native(self.master)
         hyper = _hyper_for(self, native)
         b1, b2 = cfg.betas

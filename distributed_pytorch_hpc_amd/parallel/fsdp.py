@@ -32,6 +32,7 @@ import torch
 import torch.distributed as dist
 from torch import nn
 
+from ..comm import custom_allreduce as _car
 from ..comm.custom_allreduce import check_health as check_xgmi_health
 from ..ops import _lib
 from ..train import optim as optim_ref
@@ -376,6 +377,10 @@ class ZeRO3Engine:
                 dist.all_reduce(sq, group=self.group)
             norm = sq.sqrt() / self._dp_world()
             self._gscale.copy_(torch.clamp(cfg.max_grad_norm / (norm + 1e-6), max=1.0) / self._dp_world())
+        if _car.active():
+            if cfg.max_grad_norm is None:
+                self._gscale.fill_(1.0 / self._dp_world())   # a previous step's guard may have poisoned it
+            _car.guard_update(self._gscale)   # skip the update on every rank if a direct-peer barrier timed out
         native = _lib.use_native(self.master)
         hyper = _hyper_for(self, native)
         b1, b2 = cfg.betas

@@ -10,7 +10,11 @@ HIP kernels see ordinary contiguous buffers.
 Styles (applied by ``parallelize_module(module, tp_group, plan)``):
   ColwiseParallel(sequence_parallel=False, gather_output=False, shard_fn=None)
       weight [out, in] -> rows out/tp.  Input: replicated (copy_to_group: grad all-reduced) or, with
-      sequence_parallel, seq-sharded [B, S/tp, *] all-gathered along dim 1 (grad reduce-scattered).
+      sequence_parallel, token-sharded and all-gathered (grad reduce-scattered).  The default SP layout is TOKENS
+      (comm/functional.py): the [B, S/tp, D] shard is a view of k contiguous runs of the FLATTENED B*S tokens, not of
+      batch rows, so the collectives move contiguous rank slots with no transposes.  Its contract: every module in
+      the SP region must be token-wise (norms, projections, activations); anything per-sample or position-dependent
+      (attention, RoPE) runs after the all-gather on the full sequence.
   RowwiseParallel(sequence_parallel=False, shard_fn=None)
       weight [out, in] -> columns in/tp.  Output: partial sums all-reduced, or reduce-scattered along the
       sequence (SP).  A bias is added once, after the reduction.
@@ -28,6 +32,8 @@ wqkv / w13 projections (sharded per head / per half) and vocab-parallel cross-en
 only [N] all-reduces instead of all-gathering [B, S, V] logits).
 """
 from __future__ import annotations
+
+import warnings
 
 from dataclasses import dataclass
 from typing import Callable, Optional
@@ -89,15 +95,32 @@ class ColwiseParallelLinear(nn.Module):
         self.in_features, self.out_features = lin.in_features, self.weight.shape[0]
         self.async_chunks = 0   # > 0: sequence all-gather pipelined against the GEMM (parallel/async_tp.py)
 
+    async_chunks = property(lambda self: self._async_chunks, lambda self, k: _set_async_chunks(self, k))
+
     def forward(self, x):
         if self.sp and self.async_chunks and self.seq_dim == cf.TOKENS and x.dim() == 3 and _ws(self.group) > 1:
-            y = ag_matmul(x, self.weight, self.bias, self.group, self.async_chunks)
+            y = ag_matmul(x, self.weight, self.bias, self.group)
         else:
             x = cf.gather_along_dim(x, self.seq_dim, self.group) if self.sp else cf.copy_to_group(x, self.group)
             y = _linear(x, self.weight, self.bias)
         if self.gather_output:
             y = cf.gather_replicated_along_dim(y, y.dim() - 1, self.group)
         return y
+
+
+def _set_async_chunks(mod, k) -> None:
+    """``layer.async_chunks = k`` (k > 0) pipelines the layer's SP collective in k micro-collectives.  The count is a
+    property of the TP group's token layout (comm.functional.set_sp_chunks), shared by every SP collective of the
+    group, so assigning it here sets the layout too -- a plan that sets ``async_chunks`` directly gets the overlap it
+    asked for (advisor r5: the count used to be read from the layout only, which only parallelize_llama set)."""
+    k = int(k)
+    object.__setattr__(mod, "_async_chunks", k)
+    if k > 0 and mod.sp:
+        prev = cf.sp_chunks(mod.group)
+        if prev not in (1, k):
+            warnings.warn(f"async_chunks={k} replaces the TP group's SP layout of {prev} rounds for every layer of "
+                          "the group", stacklevel=3)
+        cf.set_sp_chunks(mod.group, k)
 
 
 class RowwiseParallelLinear(nn.Module):
@@ -113,11 +136,13 @@ class RowwiseParallelLinear(nn.Module):
         self.in_features, self.out_features = self.weight.shape[1], lin.out_features
         self.async_chunks = 0   # > 0: GEMM pipelined against the sequence reduce-scatter (parallel/async_tp.py)
 
+    async_chunks = property(lambda self: self._async_chunks, lambda self, k: _set_async_chunks(self, k))
+
     def forward(self, x):
         if not self.input_is_parallel:
             x = cf.split_along_dim(x, x.dim() - 1, self.group)
         if self.sp and self.async_chunks and self.seq_dim == cf.TOKENS and x.dim() == 3 and _ws(self.group) > 1:
-            y = matmul_reduce_scatter(x, self.weight, self.group, self.async_chunks)
+            y = matmul_reduce_scatter(x, self.weight, self.group)
         else:
             y = _linear(x, self.weight, None)
             y = cf.reduce_scatter_along_dim(y, self.seq_dim, self.group) if self.sp else \

@@ -172,7 +172,14 @@ class FusedSGD(torch.optim.Optimizer):
 
 
 # ------------------------------------------------------------------------------------------ references
+def _skip(grad_scale) -> bool:
+    """A NaN gradient scale skips the update, as in the HIP kernels (csrc/optim.hip: the xGMI health guard)."""
+    return torch.is_tensor(grad_scale) and bool(torch.isnan(grad_scale).any())
+
+
 def adamw_reference_(master, m, v, g, lr, b1, b2, eps, wd, bc1, bc2, grad_scale=None):
+    if _skip(grad_scale):
+        return
     gf = g.float()
     if grad_scale is not None:
         gf = gf * grad_scale
@@ -184,6 +191,8 @@ def adamw_reference_(master, m, v, g, lr, b1, b2, eps, wd, bc1, bc2, grad_scale=
 
 
 def sgd_reference_(master, buf, g, lr, momentum, dampening, wd, nesterov, first, grad_scale=None):
+    if _skip(grad_scale):
+        return
     d = g.float()
     if grad_scale is not None:
         d = d * grad_scale

@@ -81,6 +81,61 @@ def engine_routed(rank, world):
     return fails
 
 
+def health_guard(rank, world):
+    """Advisor r5: a direct-peer barrier that times out on SOME ranks must (1) skip the optimizer update of that very
+    step on EVERY rank (stream-ordered guard: agreed flag -> NaN gradient scale -> the AdamW kernel returns) and (2)
+    raise XgmiAllReduceError on every rank at the same check, disabling the path for good (env override included).
+    Rank 1 enters the all-reduce 3 s late against a 0.5 s barrier timeout, so only the early ranks time out."""
+    import time
+
+    from distributed_pytorch_hpc_amd.comm import custom_allreduce as C
+    from distributed_pytorch_hpc_amd.ops import _lib
+
+    fails = []
+    C.set_policy(None, 1 << 20, allow_any_backend=True)
+    car = XgmiAllReduce(None, max_bytes=1 << 20, timeout_s=0.5)
+    C._CACHE[C._key(None)] = car
+    x = torch.ones(4096, device="cuda")
+    torch.cuda.synchronize()
+    dist.barrier()
+    if rank == 1:
+        time.sleep(3.0)
+    car.all_reduce(x)
+    torch.cuda.synchronize()
+    dist.barrier()
+    local = car.errors()
+    master = torch.randn(1024, device="cuda")
+    m, v = torch.zeros_like(master), torch.zeros_like(master)
+    grad = torch.randn(1024, device="cuda")
+    before = master.clone()
+    gscale = torch.ones(1, device="cuda")
+    C.guard_update(gscale)                   # agreed over the group: every rank poisons its scale
+    _lib.ops().adamw_step_(master, m, v, grad, None, 1e-2, 0.9, 0.95, 1e-8, 0.1, 0.1, 0.05, gscale)
+    torch.cuda.synchronize()
+    if not torch.isnan(gscale).all():
+        fails.append(f"guard did not poison the scale (local timeout word {local})")
+    if not torch.equal(master, before) or m.abs().sum() != 0:
+        fails.append("optimizer update ran on a step whose all-reduce timed out")
+    try:
+        C.check_health()
+        fails.append("check_health did not raise")
+    except C.XgmiAllReduceError:
+        pass
+    os.environ["DPH_CUSTOM_ALLREDUCE"] = "1"
+    if C.policy_max_bytes(None) != 0 or C.use_custom(x, None) is not None:
+        fails.append("a failed group's path came back through the env override")
+    del os.environ["DPH_CUSTOM_ALLREDUCE"]
+    C.check_health()                          # dropped: no second raise
+    locals_ = [None] * world
+    dist.all_gather_object(locals_, int(local))
+    if rank == 0 and not (locals_[0] and not locals_[1]):
+        print(f"note: timeout words per rank {locals_} (the test wants rank 0 late-waited, rank 1 clean)")
+    C._DEAD.clear()
+    C.clear_policy(None)
+    C._CACHE.pop(C._key(None), None)
+    return fails
+
+
 def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -129,6 +184,7 @@ def main():
         fails.append(f"{err} barrier timeouts")
     car.close()
     fails += engine_routed(rank, world)
+    fails += health_guard(rank, world)
     flags = [None] * world
     dist.all_gather_object(flags, fails)
     if rank == 0:

@@ -240,3 +240,42 @@ def test_preflight_selftest_exact_at_world_16():
 
     outs = run_distributed(_selftest_worker, 16, timeout=400)
     assert all("all_reduce[bfloat16]" in o and "reduce_scatter[bfloat16]" in o for o in outs), outs
+
+
+def test_bench_self_launches_its_ranks(tmp_path):
+    """`python bench.py --gpus 2` with no launcher starts its own 2 ranks (runtime/launch.py) and reports world 2 --
+    never an N = 1 number labelled N = 2."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="1")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + ARGS
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    recs = _lines(p.stdout)
+    assert len(recs) == 1, p.stdout
+    r = recs[0]
+    assert r["n_gpus"] == 2 and r["world"] == 2 and r["config"]["parallelism"] == "fsdp2"
+    assert r["preflight_ok"] is True and r["param_checksum_ok"] is True
+
+
+def test_bench_rank_count_mismatch_is_fatal(tmp_path):
+    """An external launcher whose world size disagrees with --gpus: exit 2 on every rank, no JSON line."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "4"] + ARGS
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert p.returncode != 0 and not _lines(p.stdout)
+    assert "--gpus 4 but the launcher" in p.stderr
+
+
+def test_bench_too_few_gpus_is_fatal(tmp_path):
+    """--gpus N over RCCL with fewer than N visible GPUs (none here; one on the 1-GPU test box): exit 2 before any
+    rank starts."""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("this machine has enough GPUs")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "tiny", "--quiet"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=env, cwd=str(tmp_path))
+    assert p.returncode == 2 and not _lines(p.stdout), p.stderr[-2000:]
+    assert "RCCL needs one GPU per rank" in p.stderr

@@ -51,3 +51,15 @@ def test_bench_tp_layout_two_ranks_share_one_gpu(tmp_path):
     r = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")][0]
     assert r["config"]["parallelism"] == "tp2" and r["dtype"] == "bf16" and r["value"] > 0
     assert abs(r["loss_last"] - r["loss_first_warmup"]) < 2.0
+
+
+def test_bench_more_gpus_than_visible_fails(tmp_path):
+    """On a box with fewer GPUs than --gpus, bench.py must exit non-zero instead of timing fewer ranks."""
+    import torch
+
+    n = torch.cuda.device_count()
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n + 1), "--model", "tiny", "--quiet"]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=100, cwd=str(tmp_path), env=env)
+    assert p.returncode == 2, p.stderr[-2000:]
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

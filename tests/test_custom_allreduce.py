@@ -79,19 +79,65 @@ def test_check_health_raises_and_disables_path(monkeypatch):
     from distributed_pytorch_hpc_amd.comm import custom_allreduce as car
 
     class _Fake:
+        _guard_event = None   # no engine guard ran: the rank's own timeout word decides
+
         def __init__(self, err):
             self.err = err
+            self.closed = False
 
         def errors(self):
             return self.err
 
-    monkeypatch.setattr(car, "_CACHE", {"world": _Fake(0), 123: _Fake(1)})
+        def close(self):
+            self.closed = True
+
+    bad = _Fake(1)
+    monkeypatch.setattr(car, "_CACHE", {"world": _Fake(0), 123: bad})
     monkeypatch.setattr(car, "_POLICY", {"world": 1 << 20, 123: 1 << 20})
+    monkeypatch.setattr(car, "_DEAD", set())
     with pytest.raises(car.XgmiAllReduceError):
         car.check_health()
     assert 123 not in car._POLICY and car._POLICY["world"] == 1 << 20
-    car._CACHE[123].err = 0
+    assert car._CACHE[123] is None and bad.closed and 123 in car._DEAD
     car.check_health()   # healthy groups: no error
+
+
+def test_check_health_reads_the_agreed_verdict_after_the_guard(monkeypatch):
+    """With an engine guard in flight the host check waits for that guard's event and reads the group-agreed word,
+    not this rank's own one: every rank raises at the same step (advisor r5)."""
+    from distributed_pytorch_hpc_amd.comm import custom_allreduce as car
+
+    class _Ev:
+        waited = False
+
+        def synchronize(self):
+            _Ev.waited = True
+
+    class _Guarded:
+        def __init__(self, own, agreed):
+            self.own, self.agreed = own, agreed
+            self._guard_event = _Ev()
+
+        def errors(self):
+            return self.own
+
+        def agreed_error(self):
+            return self.agreed
+
+        def close(self):
+            pass
+
+    monkeypatch.setattr(car, "_POLICY", {"world": 1 << 20})
+    monkeypatch.setattr(car, "_DEAD", set())
+    monkeypatch.setattr(car, "_CACHE", {"world": _Guarded(own=0, agreed=1)})   # a peer timed out, not this rank
+    with pytest.raises(car.XgmiAllReduceError):
+        car.check_health()
+    assert _Ev.waited and "world" in car._DEAD
+    monkeypatch.setenv("DPH_CUSTOM_ALLREDUCE", "1")
+    assert car.policy_max_bytes(None) == 0          # dead groups stay off, whatever the environment says
+    monkeypatch.setattr(car, "_CACHE", {"world": _Guarded(own=1, agreed=0)})   # own word alone does not raise
+    car._DEAD.clear()
+    car.check_health()
 
 
 def test_engine_step_checks_xgmi_health(monkeypatch):
@@ -105,11 +151,17 @@ def test_engine_step_checks_xgmi_health(monkeypatch):
     eng.synchronize()
 
     class _Bad:
+        _guard_event = None
+
         def errors(self):
             return 1
 
+        def close(self):
+            pass
+
     monkeypatch.setattr(car, "_CACHE", {"world": _Bad()})
     monkeypatch.setattr(car, "_POLICY", {})
+    monkeypatch.setattr(car, "_DEAD", set())
     with pytest.raises(car.XgmiAllReduceError):
         eng.step()
 

@@ -165,3 +165,35 @@ def test_async_tp_single_sequence_matches_single_process():
     ref = _reference(global_b=1)
     outs = run_distributed(_tp_worker, 2, 1, True, True, 2, 1)
     _check_tp(ref, outs, 2)
+
+
+def _tp_accum_worker(rank, world, sync_inside):
+    """TP=2 + SP, two accumulation micro-steps (the first inside no_sync); optionally synchronize() inside no_sync."""
+    from distributed_pytorch_hpc_amd.comm.mesh import DeviceMesh2D
+    from distributed_pytorch_hpc_amd.parallel.data_parallel import DataParallelEngine, OptimConfig
+    from distributed_pytorch_hpc_amd.parallel.tensor_parallel import parallelize_llama
+
+    mesh = DeviceMesh2D(1, world)
+    m = _model()
+    parallelize_llama(m, mesh.tp_group, sequence_parallel=True, loss_parallel=True)
+    eng = DataParallelEngine(m, process_group=mesh.dp_group, shard=False, bucket_cap_mb=0.02)
+    eng.configure_optimizer(OptimConfig(lr=1e-2, weight_decay=0.1))
+    t = _batches()[0]
+    with eng.no_sync():
+        m(t[:2, :-1], t[:2, 1:]).backward()
+        if sync_inside:
+            eng.synchronize()
+    m(t[2:, :-1], t[2:, 1:]).backward()
+    eng.step()
+    eng.synchronize()
+    return {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+def test_synchronize_inside_no_sync_keeps_sp_grads():
+    """Advisor r5: synchronize() inside no_sync() must not TP-all-reduce the partial sequence-parallel norm gradients
+    that the next micro-step still adds to (they were counted tp times)."""
+    plain = run_distributed(_tp_accum_worker, 2, False)
+    synced = run_distributed(_tp_accum_worker, 2, True)
+    for a, b in zip(plain, synced):
+        for k, v in a.items():
+            assert torch.allclose(v, b[k], atol=1e-6, rtol=1e-6), k
