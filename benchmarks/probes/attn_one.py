@@ -23,11 +23,14 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--which", default="fwd,bwd")
     ap.add_argument("--noncausal", action="store_true")
+    ap.add_argument("--variant", type=int, default=0, help="attention kernel A/B (0 = default 16x16x32 forms for D 128, "
+                                                            "1 = the 32x32x16 forms)")
     ap.add_argument("--sustain", type=float, default=0.0,
                     help="also loop each kernel for this many seconds under the GPU telemetry sampler (clock, power, "
                          "package-power residency, TFLOP/J)")
     a = ap.parse_args()
     _lib.require()
+    _lib.ops().attn_variant(a.variant)
     causal = not a.noncausal
     q, k, v = (torch.randn(a.b, a.s, a.h, a.d, device="cuda", dtype=torch.bfloat16) for _ in range(3))
     do = torch.randn_like(q)

@@ -204,6 +204,192 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_k(AttnParams p) {
 }
 
 // ==================================================================================================
+// Forward on v_mfma_f32_16x16x32_bf16 (head dim 128, no dropout, no ring merge): the structure above as 16x16 tiles.
+// A wave owns 32 queries = two 16-query column blocks qb; per 64-key tile:
+//   S^T[kb][qb] = K Q^T      A = K rows (x16 image, b128), B = Q^T fragments (registers)      32 MFMAs
+//   online softmax with the query on the lane: a lane holds 16 of the tile's keys per query (4 per key block), the
+//   row max / sum finish with two lane swaps (permlane16 / permlane32), lazy rescale as above
+//   O^T[db][qb] += V^T P^T   A = x16_tr(V image), B = the P^T pair of key blocks (2 ks, 2 ks + 1)   32 MFMAs
+__device__ __forceinline__ float quad_max(float x) {   // max over lanes l, l ^ 16, l ^ 32, l ^ 48
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
+}
+__device__ __forceinline__ float quad_sum(float x) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto c = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(c[0]) + __uint_as_float(c[1]);
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_fwd16_k(AttnParams p) {
+  constexpr int HD = 128, NW = 4, NT = 64 * NW, BM = 32 * NW, BN = 64;
+  constexpr int TILE = BN * HD * 2;   // one 64-row x16 image; buffer = K | V
+  constexpr float RESCALE_THR = 8.f;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
+  const int nqb = (p.Sq + BM - 1) / BM;
+  int bx, hq, b;
+  xcd_block(nqb, p.Hq, bx, hq, b, nqb * p.Hq * p.B);
+  const int qblk = CAUSAL ? nqb - 1 - bx : bx;  // heaviest causal blocks first
+  const int hk = hq / (p.Hq / p.Hkv);
+  const int q0 = qblk * BM, q0w = q0 + wid * 32;
+  const int off = p.Sk - p.Sq;
+
+  const bf16* qp = (const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
+  const bf16* kp = (const bf16*)p.k + (int64_t)b * p.k_sb + (int64_t)hk * p.k_sh;
+  const bf16* vp = (const bf16*)p.v + (int64_t)b * p.v_sb + (int64_t)hk * p.v_sh;
+
+  bf16x8 qf[2][4];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = q0w + qb * 16 + i16;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      qf[qb][kk] = q < p.Sq ? *reinterpret_cast<const bf16x8*>(qp + (int64_t)q * p.q_ss + kk * 32 + 8 * g) : zero8();
+  }
+  int kv_end = p.Sk;
+  if (CAUSAL) kv_end = min(p.Sk, q0 + BM + off);
+  const int ntiles = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
+  const int wtiles = wave_tile_count<CAUSAL>(ntiles, q0w, off);
+
+  X16Stage<BN, NT> st;
+  st.init();
+  X16Reads rd;
+  rd.init(lane);
+  const unsigned lds_w = lds_addr(smem + wid * 1024);
+
+  f32x4 o[8][2];
+#pragma unroll
+  for (int db = 0; db < 8; ++db)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[db][qb][r] = 0.f;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};   // per query block: running max (log2 units), partial sum
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  if (ntiles > 0) {
+    st.stage(lds_w, kp, p.k_ss, 0, p.Sk);
+    st.stage(lds_w + TILE, vp, p.v_ss, 0, p.Sk);
+  }
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) {
+      const unsigned nb = lds_w + (buf ^ 1) * 2 * TILE;
+      st.stage(nb, kp, p.k_ss, (t + 1) * BN, p.Sk);
+      st.stage(nb + TILE, vp, p.v_ss, (t + 1) * BN, p.Sk);
+    }
+    const char* Kl = smem + buf * 2 * TILE;
+    const char* Vl = Kl + TILE;
+    if (t < wtiles) {
+      const int k0 = t * BN;
+      f32x4 s[4][2];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) s[kb][qb] = z4;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        bf16x8 kf[4];
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) kf[kb] = lds_b128(Kl, rd.row[kk] + (kb << 12));
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+          s[kb][0] = mfma16(kf[kb], qf[0][kk], s[kb][0]);
+          s[kb][1] = mfma16(kf[kb], qf[1][kk], s[kb][1]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if ((k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0w + off))) {   // wave-uniform
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int key = k0 + kb * 16 + 4 * g + r, q = q0w + qb * 16 + i16;
+              s[kb][qb][r] = (key >= p.Sk || (CAUSAL && key > q + off)) ? -INFINITY : s[kb][qb][r];
+            }
+      }
+      bf16x8 pf[2][2];   // [ks][qb]
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float mx = fmaxf(s[0][qb][0], s[1][qb][0]);
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[kb][qb][r]);
+        mx = quad_max(mx) * sl2;
+        if (__ballot(mx > m[qb] + RESCALE_THR)) {
+          const float mn = fmaxf(m[qb], mx);
+          const float alpha = mn == -INFINITY ? 1.f : exp2_(m[qb] - mn);
+          lsum[qb] *= alpha;
+#pragma unroll
+          for (int db = 0; db < 8; ++db)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[db][qb][r] *= alpha;
+          m[qb] = mn;
+        }
+        const float mneg = m[qb] == -INFINITY ? 0.f : -m[qb];
+        float ls = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            s[kb][qb][r] = exp2_(fmaf(s[kb][qb][r], sl2, mneg));
+            ls += s[kb][qb][r];
+          }
+        lsum[qb] += ls;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) pf[ks][qb] = acc_pair_b(s[2 * ks][qb], s[2 * ks + 1][qb]);
+      }
+      // O^T += V^T P^T
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int db = 0; db < 8; ++db) {
+          const bf16x8 vt = x16_tr(Vl, rd.tr[db] + ((ks * 32) << 8));
+          o[db][0] = mfma16(vt, pf[ks][0], o[db][0]);
+          o[db][1] = mfma16(vt, pf[ks][1], o[db][1]);
+        }
+    }
+    wait_vmcnt<0>();   // this wave's share of tile t+1 has landed ...
+    __builtin_amdgcn_s_barrier();   // ... and every wave's, and nobody reads tile t's images any more
+  }
+
+  // ---- epilogue: O = O^T / l, lse ----
+  float inv[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    lsum[qb] = quad_sum(lsum[qb]);
+    inv[qb] = lsum[qb] > 0.f ? 1.f / lsum[qb] : 0.f;
+#pragma unroll
+    for (int db = 0; db < 8; ++db)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[db][qb][r] *= inv[qb];
+  }
+  bf16* o0 = (bf16*)p.o + (int64_t)b * p.o_sb + (int64_t)q0w * p.o_ss + (int64_t)hq * p.o_sh;
+  store_rows16(smem + wid * (32 * HD * 2), o0, p.o_ss, min(32, p.Sq - q0w), o, 1.f, lane, q0w, nullptr, nullptr, 0);
+  if (g == 0 && p.lse) {
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int q = q0w + qb * 16 + i16;
+      if (q < p.Sq)
+        p.lse[((int64_t)b * p.Hq + hq) * p.Sq + q] =
+            lsum[qb] > 0.f ? (m[qb] + __log2f(lsum[qb])) * 0.6931471805599453f : -INFINITY;
+    }
+  }
+}
+
+// ==================================================================================================
 // One geometry for every kernel: 4 waves = 128 query rows (or keys) per workgroup, two workgroups per CU.
 template <int HD>
 static void fwd_launch(const AttnParams& p, hipStream_t st) {
@@ -212,6 +398,9 @@ static void fwd_launch(const AttnParams& p, hipStream_t st) {
   if (p.drop_p > 0.f) {
     if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, true>), grid, dim3(256), lds, st, p);
     else hipLaunchKernelGGL((attn_fwd_k<HD, false, true>), grid, dim3(256), lds, st, p);
+  } else if (HD == 128 && !p.acc_o && attn_get_variant() == 0) {
+    if (p.causal) hipLaunchKernelGGL((attn_fwd16_k<true>), grid, dim3(256), lds, st, p);
+    else hipLaunchKernelGGL((attn_fwd16_k<false>), grid, dim3(256), lds, st, p);
   } else {
     if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true>), grid, dim3(256), lds, st, p);
     else hipLaunchKernelGGL((attn_fwd_k<HD, false>), grid, dim3(256), lds, st, p);

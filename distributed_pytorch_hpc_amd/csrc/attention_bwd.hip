@@ -443,16 +443,396 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
   }
 }
 
+// ---- dK / dV on v_mfma_f32_16x16x32_bf16 (head dim 128, no dropout): the KV-stationary structure above with every
+// product a set of 16x16 tiles.  A wave owns 32 keys = two 16-key column blocks kb; per 32-query tile:
+//   S[qb][kb]  = Q K^T   A = Q rows (x16 image, b128), B = K^T (K image rows, b128)        16 MFMAs
+//   dP[qb][kb] = dO V^T  A = dO rows,                  B = V^T (registers, loaded once)     16 MFMAs
+//   dV^T[db][kb] += dO^T P,  dK^T[db][kb] += Q^T dS:  A = x16_tr (transposed image reads), B = the S / dP accumulator
+//   pair of the key block (acc_pair_b: no lane movement)                                   32 MFMAs
+// The key is on the lane of S / dP (col = lane & 15), so P and dS are B operands as they stand.  LDS traffic per MFMA
+// FLOP is that of the 32x32x16 kernel; the x16 image makes every read conflict-free.
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
+  constexpr int HD = 128, NW = 4, NT = 64 * NW, BNK = 32 * NW, BMQ = 32;
+  constexpr int QIMG = BMQ * HD * 2;        // Q / dO tile image [32 q][128]
+  constexpr int KIMG = BNK * HD * 2;        // K image [128 keys][128]
+  // smem: K | Q0 | dO0 | Q1 | dO1 | -lse2[2][32] | delta[2][32]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Kimg = smem;
+  char* Qbuf = smem + KIMG;
+  float* lse_s = reinterpret_cast<float*>(Qbuf + 4 * QIMG);
+  float* del_s = lse_s + 2 * BMQ;
+
+  const AttnParams& p = P.f;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
+  const int nkb = (p.Sk + BNK - 1) / BNK;
+  int kbx, hk, b;
+  xcd_block(nkb, p.Hkv, kbx, hk, b, nkb * p.Hkv * p.B);
+  const int kb0 = kbx * BNK;   // ascending = heaviest causal key blocks first
+  const int grp = p.Hq / p.Hkv;
+  const int off = p.Sk - p.Sq;
+  const int key0 = kb0 + wid * 32;
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  const bf16* kp = (const bf16*)p.k + (int64_t)b * p.k_sb + (int64_t)hk * p.k_sh;
+  const bf16* vp = (const bf16*)p.v + (int64_t)b * p.v_sb + (int64_t)hk * p.v_sh;
+  {
+    X16Stage<BNK, NT> kst;
+    kst.init();
+    kst.stage(lds_addr(Kimg + wid * 1024), kp, p.k_ss, kb0, p.Sk);
+  }
+  // V^T B fragments of dP = dO V^T: lane (key i, g) holds V[key][32 kk + 8 g .. + 7]
+  bf16x8 vf[2][4];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int key = key0 + kb * 16 + i16;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+      vf[kb][kk] = key < p.Sk ? *reinterpret_cast<const bf16x8*>(vp + (int64_t)key * p.v_ss + kk * 32 + 8 * g)
+                              : zero8();
+  }
+  f32x4 dk[8][2], dv[8][2];
+#pragma unroll
+  for (int db = 0; db < 8; ++db)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { dk[db][kb][r] = 0.f; dv[db][kb][r] = 0.f; }
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+  X16Reads rd;
+  rd.init(lane);
+  const int krow = (wid * 32) << 8;   // this wave's K rows in the K image
+
+  int qstart = 0;
+  if (CAUSAL) qstart = max(0, kb0 - off) / BMQ * BMQ;
+  const int nqt_head = qstart < p.Sq ? (p.Sq - qstart + BMQ - 1) / BMQ : 0;
+  const int total = nqt_head * grp;
+
+  X16Stage<BMQ, NT> qst;
+  qst.init();
+  const unsigned lds_q = lds_addr(Qbuf + wid * 1024);
+  float st_lse = 0.f, st_del = 0.f;
+  auto stage = [&](int it, int buf) {
+    const int hq = hk * grp + it / nqt_head;
+    const int qt0 = qstart + (it % nqt_head) * BMQ;
+    const bf16* qp = (const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
+    const bf16* dop = (const bf16*)P.dout + (int64_t)b * P.do_sb + (int64_t)hq * P.do_sh;
+    const unsigned ql = lds_q + buf * 2 * QIMG;
+    qst.stage(ql, qp, p.q_ss, qt0, p.Sq);
+    qst.stage(ql + QIMG, dop, P.do_ss, qt0, p.Sq);
+    if (threadIdx.x < BMQ) {
+      const int q = min(qt0 + (int)threadIdx.x, p.Sq - 1);   // rows past Sq: finite, masked below
+      const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + q;
+      st_lse = p.lse[idx];
+      st_del = P.delta[idx];
+    }
+  };
+  auto stage_scalars = [&](int buf) {
+    if (threadIdx.x < BMQ) {
+      lse_s[buf * BMQ + threadIdx.x] = -st_lse * 1.4426950408889634f;  // -lse in log2 units
+      del_s[buf * BMQ + threadIdx.x] = st_del;
+    }
+  };
+
+  if (total > 0) {
+    stage(0, 0);
+    stage_scalars(0);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+
+  for (int it = 0; it < total; ++it) {
+    const int buf = it & 1;
+    const int qt0 = qstart + (it % nqt_head) * BMQ;
+    if (it + 1 < total) stage(it + 1, buf ^ 1);
+    const char* Ql = Qbuf + buf * 2 * QIMG;
+    const char* Ol = Ql + QIMG;
+    if (!(CAUSAL && key0 > qt0 + BMQ - 1 + off)) {   // some of this wave's keys are visible to the tile
+      __builtin_amdgcn_s_setprio(1);
+      f32x4 s[2][2], dp[2][2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) { s[qb][kb] = z4; dp[qb][kb] = z4; }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const bf16x8 k0f = lds_b128(Kimg, rd.row[kk] + krow), k1f = lds_b128(Kimg, rd.row[kk] + krow + 4096);
+        const bf16x8 q0f = lds_b128(Ql, rd.row[kk]), q1f = lds_b128(Ql, rd.row[kk] + 4096);
+        const bf16x8 o0f = lds_b128(Ol, rd.row[kk]), o1f = lds_b128(Ol, rd.row[kk] + 4096);
+        s[0][0] = mfma16(q0f, k0f, s[0][0]);
+        s[0][1] = mfma16(q0f, k1f, s[0][1]);
+        s[1][0] = mfma16(q1f, k0f, s[1][0]);
+        s[1][1] = mfma16(q1f, k1f, s[1][1]);
+        dp[0][0] = mfma16(o0f, vf[0][kk], dp[0][0]);
+        dp[0][1] = mfma16(o0f, vf[1][kk], dp[0][1]);
+        dp[1][0] = mfma16(o1f, vf[0][kk], dp[1][0]);
+        dp[1][1] = mfma16(o1f, vf[1][kk], dp[1][1]);
+      }
+      __builtin_amdgcn_s_setprio(0);
+      // wave-uniform: only diagonal / ragged tiles pay for the selects (masked scores -> -inf -> P = 0)
+      if ((qt0 + BMQ > p.Sq) || (key0 + 32 > p.Sk) || (CAUSAL && key0 + 31 > qt0 + off)) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int q = qt0 + qb * 16 + 4 * g + r, key = key0 + kb * 16 + i16;
+              s[qb][kb][r] = (q >= p.Sq || key >= p.Sk || (CAUSAL && key > q + off)) ? -INFINITY : s[qb][kb][r];
+            }
+      }
+      // the first dV / dK step's transposed operands are read now, their latency covered by the softmax
+      bf16x8 tro_o[2], tro_q[2];
+      tro_o[0] = x16_tr(Ol, rd.tr[0]);
+      tro_q[0] = x16_tr(Ql, rd.tr[0]);
+      __builtin_amdgcn_sched_barrier(0);
+      const float* ls = lse_s + buf * BMQ;
+      const float* ds = del_s + buf * BMQ;
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const f32x4 nl = *reinterpret_cast<const f32x4*>(ls + qb * 16 + 4 * g);
+        const f32x4 dl = *reinterpret_cast<const f32x4*>(ds + qb * 16 + 4 * g);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pv = exp2_(fmaf(s[qb][kb][r], sl2, nl[r]));
+            s[qb][kb][r] = pv;
+            dp[qb][kb][r] = pv * (dp[qb][kb][r] - dl[r]);
+          }
+      }
+      bf16x8 pb[2], sb[2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        pb[kb] = acc_pair_b(s[0][kb], s[1][kb]);
+        sb[kb] = acc_pair_b(dp[0][kb], dp[1][kb]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+      // step db: its operands were read one step earlier; each step issues the next step's 4 reads ahead of its MFMAs
+#pragma unroll
+      for (int db = 0; db < 8; ++db) {
+        if (db + 1 < 8) {
+          tro_o[(db + 1) & 1] = x16_tr(Ol, rd.tr[db + 1]);
+          tro_q[(db + 1) & 1] = x16_tr(Ql, rd.tr[db + 1]);
+        }
+        dv[db][0] = mfma16(tro_o[db & 1], pb[0], dv[db][0]);
+        dv[db][1] = mfma16(tro_o[db & 1], pb[1], dv[db][1]);
+        dk[db][0] = mfma16(tro_q[db & 1], sb[0], dk[db][0]);
+        dk[db][1] = mfma16(tro_q[db & 1], sb[1], dk[db][1]);
+        if (db + 1 < 8) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+    if (it + 1 < total) stage_scalars(buf ^ 1);
+    wait_vmcnt<0>();
+    __syncthreads();
+  }
+
+  {   // dK then dV through this wave's 8-KiB LDS slab (the images are free after the loop's last barrier)
+    static_assert(NW * 32 * HD * 2 <= KIMG + 4 * QIMG, "epilogue slabs exceed the dK/dV kernel's LDS");
+    const int nvalid = min(32, p.Sk - key0);
+    bf16* dk0 = (bf16*)P.dk + (int64_t)b * P.dk_sb + (int64_t)key0 * P.dk_ss + (int64_t)hk * P.dk_sh;
+    bf16* dv0 = (bf16*)P.dv + (int64_t)b * P.dv_sb + (int64_t)key0 * P.dv_ss + (int64_t)hk * P.dv_sh;
+    char* slab = smem + wid * (32 * HD * 2);
+    store_rows16(slab, dk0, P.dk_ss, nvalid, dk, p.scale, lane, key0, P.rope_cos, P.rope_sin, P.rope_off);
+    store_rows16(slab, dv0, P.dv_ss, nvalid, dv, 1.f, lane, key0, nullptr, nullptr, 0);
+  }
+}
+
+// ---- dQ on v_mfma_f32_16x16x32_bf16 (head dim 128, no dropout): the Q-stationary structure above as 16x16 tiles.
+// A wave owns 32 queries = two 16-query column blocks qb (Q^T / dO^T B fragments in registers); per 64-key tile, in
+// two 32-key halves h (register budget: one half's S^T / dP^T accumulators live at a time):
+//   S^T[kb][qb] = K Q^T, dP^T[kb][qb] = V dO^T   A = K / V rows (x16 images, b128)          2 x 16 MFMAs
+//   dS^T = P^T (dP^T - delta), P^T = exp2(S^T c - lse): the query is on the lane, row constants are lane scalars
+//   dQ^T[db][qb] += K^T dS^T                       A = x16_tr(K image), B = the half's dS^T pair   16 MFMAs
+// and it forms delta = rowsum(dO * O) for its queries first (written for the dK/dV kernel, which runs after it).
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(AttnBwdParams P) {
+  constexpr int HD = 128, NW = 4, NT = 64 * NW, BM = 32 * NW, BN = 64;
+  constexpr int TILE = BN * HD * 2;   // one 64-row x16 image (16 KiB); buffer = K | V
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const AttnParams& p = P.f;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
+  const int nqb = (p.Sq + BM - 1) / BM;
+  int bx, hq, b;
+  xcd_block(nqb, p.Hq, bx, hq, b, nqb * p.Hq * p.B);
+  const int qblk = CAUSAL ? nqb - 1 - bx : bx;
+  const int hk = hq / (p.Hq / p.Hkv);
+  const int q0 = qblk * BM, q0w = q0 + wid * 32;
+  const int off = p.Sk - p.Sq;
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  const bf16* qp = (const bf16*)p.q + (int64_t)b * p.q_sb + (int64_t)hq * p.q_sh;
+  const bf16* dop = (const bf16*)P.dout + (int64_t)b * P.do_sb + (int64_t)hq * P.do_sh;
+  const bf16* opp = (const bf16*)p.o + (int64_t)b * p.o_sb + (int64_t)hq * p.o_sh;
+  const bf16* kp = (const bf16*)p.k + (int64_t)b * p.k_sb + (int64_t)hk * p.k_sh;
+  const bf16* vp = (const bf16*)p.v + (int64_t)b * p.v_sb + (int64_t)hk * p.v_sh;
+
+  // Q^T / dO^T B fragments: lane (query i, g) holds row q0w + 16 qb + i, columns 32 kk + 8 g .. + 7
+  bf16x8 qf[2][4], df[2][4];
+  float nlse2[2], delta[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = q0w + qb * 16 + i16;
+    const bool ok = q < p.Sq;
+    float part = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int64_t c = kk * 32 + 8 * g;
+      qf[qb][kk] = ok ? *reinterpret_cast<const bf16x8*>(qp + (int64_t)q * p.q_ss + c) : zero8();
+      df[qb][kk] = ok ? *reinterpret_cast<const bf16x8*>(dop + (int64_t)q * P.do_ss + c) : zero8();
+      if (ok) {
+        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(opp + (int64_t)q * p.o_ss + c);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) part += (float)df[qb][kk][j] * (float)ov[j];
+      }
+    }
+    // the four lane groups hold complementary column slices of the row
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    delta[qb] = part;
+    nlse2[qb] = 0.f;
+    if (ok) {
+      const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + q;
+      nlse2[qb] = -p.lse[idx] * 1.4426950408889634f;
+      if (g == 0) P.delta[idx] = part;
+    }
+  }
+
+  int kv_end = p.Sk;
+  if (CAUSAL) kv_end = min(p.Sk, q0 + BM + off);
+  const int ntiles = kv_end > 0 ? (kv_end + BN - 1) / BN : 0;
+  const int wtiles = wave_tile_count<CAUSAL>(ntiles, q0w, off);
+
+  X16Stage<BN, NT> st;
+  st.init();
+  X16Reads rd;
+  rd.init(lane);
+  const unsigned lds_w = lds_addr(smem + wid * 1024);
+
+  f32x4 dq[8][2];
+#pragma unroll
+  for (int db = 0; db < 8; ++db)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dq[db][qb][r] = 0.f;
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+
+  if (ntiles > 0) {
+    st.stage(lds_w, kp, p.k_ss, 0, p.Sk);
+    st.stage(lds_w + TILE, vp, p.v_ss, 0, p.Sk);
+  }
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) {
+      const unsigned nb = lds_w + (buf ^ 1) * 2 * TILE;
+      st.stage(nb, kp, p.k_ss, (t + 1) * BN, p.Sk);
+      st.stage(nb + TILE, vp, p.v_ss, (t + 1) * BN, p.Sk);
+    }
+    const char* Kl = smem + buf * 2 * TILE;
+    const char* Vl = Kl + TILE;
+    if (t < wtiles) {
+      const int k0 = t * BN;
+      const bool need_mask = (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0w + off));
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 sa[2][2], pa[2][2];   // [kb within the half][qb]
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) { sa[a][qb] = z4; pa[a][qb] = z4; }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int r0 = (h * 32) << 8;
+          const bf16x8 k0f = lds_b128(Kl, rd.row[kk] + r0), k1f = lds_b128(Kl, rd.row[kk] + r0 + 4096);
+          const bf16x8 v0f = lds_b128(Vl, rd.row[kk] + r0), v1f = lds_b128(Vl, rd.row[kk] + r0 + 4096);
+          sa[0][0] = mfma16(k0f, qf[0][kk], sa[0][0]);
+          sa[0][1] = mfma16(k0f, qf[1][kk], sa[0][1]);
+          sa[1][0] = mfma16(k1f, qf[0][kk], sa[1][0]);
+          sa[1][1] = mfma16(k1f, qf[1][kk], sa[1][1]);
+          pa[0][0] = mfma16(v0f, df[0][kk], pa[0][0]);
+          pa[0][1] = mfma16(v0f, df[1][kk], pa[0][1]);
+          pa[1][0] = mfma16(v1f, df[0][kk], pa[1][0]);
+          pa[1][1] = mfma16(v1f, df[1][kk], pa[1][1]);
+        }
+        if (need_mask) {   // wave-uniform; masked scores -> -inf -> p = 0
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int key = k0 + h * 32 + a * 16 + 4 * g + r, q = q0w + qb * 16 + i16;
+                sa[a][qb][r] = (key >= p.Sk || (CAUSAL && key > q + off)) ? -INFINITY : sa[a][qb][r];
+              }
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              sa[a][qb][r] = exp2_(fmaf(sa[a][qb][r], sl2, nlse2[qb])) * (pa[a][qb][r] - delta[qb]);
+        bf16x8 dsb[2];
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) dsb[qb] = acc_pair_b(sa[0][qb], sa[1][qb]);
+        __builtin_amdgcn_sched_barrier(0);
+        // dQ^T += K^T dS^T over this half's 32 keys
+#pragma unroll
+        for (int db = 0; db < 8; ++db) {
+          const bf16x8 kt = x16_tr(Kl, rd.tr[db] + ((h * 32) << 8));
+          dq[db][0] = mfma16(kt, dsb[0], dq[db][0]);
+          dq[db][1] = mfma16(kt, dsb[1], dq[db][1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+  }
+
+  {   // dQ through this wave's 8-KiB LDS slab (the K / V images are free after the loop's last barrier)
+    bf16* dq0 = (bf16*)P.dq + (int64_t)b * P.dq_sb + (int64_t)q0w * P.dq_ss + (int64_t)hq * P.dq_sh;
+    store_rows16(smem + wid * (32 * HD * 2), dq0, P.dq_ss, min(32, p.Sq - q0w), dq, p.scale, lane, q0w,
+                 P.rope_cos, P.rope_sin, P.rope_off);
+  }
+}
+
+// A/B switch for the 16x16x32 kernels (benchmarks/probes/attn_one.py --variant): 1 = the 32x32x16 forms for head
+// dim 128 too.  Process-wide, default 0; not read from the environment.
+static int g_attn_variant = 0;
+int attn_set_variant(int v) {
+  const int old = g_attn_variant;
+  g_attn_variant = v;
+  return old;
+}
+int attn_get_variant() { return g_attn_variant; }
+
 template <int HD, bool DROP>
 static void bwd_launch_t(const AttnBwdParams& P, hipStream_t st) {
   const AttnParams& p = P.f;
   // dQ first: it forms delta = rowsum(dO * O) for its rows and writes it for the dK/dV kernel
   const size_t lds_q = 2 * 2 * 64 * HD * 2;
   const dim3 grid_q((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
-  if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, DROP>), grid_q, dim3(256), lds_q, st, P);
+  if (HD == 128 && !DROP && g_attn_variant == 0) {
+    if (p.causal) hipLaunchKernelGGL((attn_bwd_dq16_k<true>), grid_q, dim3(256), lds_q, st, P);
+    else hipLaunchKernelGGL((attn_bwd_dq16_k<false>), grid_q, dim3(256), lds_q, st, P);
+  } else if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, DROP>), grid_q, dim3(256), lds_q, st, P);
   else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, DROP>), grid_q, dim3(256), lds_q, st, P);
   const size_t lds_kv = 128 * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
   const dim3 grid_kv((unsigned)((p.Sk + 127) / 128 * p.Hkv * p.B));
+  if (HD == 128 && !DROP && g_attn_variant == 0) {
+    if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv16_k<true>), grid_kv, dim3(256), lds_kv, st, P);
+    else hipLaunchKernelGGL((attn_bwd_dkdv16_k<false>), grid_kv, dim3(256), lds_kv, st, P);
+    return;
+  }
   if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, true, DROP>), grid_kv, dim3(256), lds_kv, st, P);
   else hipLaunchKernelGGL((attn_bwd_dkdv_k<HD, false, DROP>), grid_kv, dim3(256), lds_kv, st, P);
 }

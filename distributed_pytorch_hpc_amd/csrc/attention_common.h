@@ -351,4 +351,120 @@ __device__ __forceinline__ int wave_tile_count(int ntiles, int q0w, int off) {
   return last < 0 ? 0 : min(ntiles, last / 64 + 1);
 }
 
+// ==================================================================================================
+// 16x16x32 building blocks (head dim 128).  v_mfma_f32_16x16x32_bf16: lane l holds A[row l&15][k 8(l>>4) + j] and
+// B[k 8(l>>4) + j][col l&15] (j < 8), and C/D[row 4(l>>4) + r][col l&15] (r < 4).  In bare loops it sustains 1.12-1.15x
+// the FLOP/s of the 32x32x16 form at equal cycles per FLOP (a higher clock under load, profiles/r5/mfma_power/).
+// ==================================================================================================
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// LDS image of a [rows][128 bf16] tile, one 256-B bank row per tile row, 16-B chunk ch of row r at slot
+// ch ^ 2 (r & 7).  Conflict-free for both reads the 16x16x32 kernels issue (bank rule of MI355X_MICROARCH.md §LDS):
+//  * ds_read_b128 operand rows: lane (i, g) reads row r0 + i, chunk 4 kk + g.  A b128 lane group holds rows
+//    {0-3, 12-15} at chunk a and rows {4-11} at chunk a ^ 1 (or the reverse); their slots a ^ {0,2,..,14} and
+//    a ^ {1,3,..,15} are all 16 distinct;
+//  * ds_read_b64_tr_b16 (T10): a 32-lane half reads 8 consecutive rows x chunks {2 db, 2 db + 1}: the 8 rows' XORs
+//    2 (r & 7) differ above bit 0, so the 16 (row, chunk) pairs take 16 distinct slots.
+// (img_off's swizzle, built for the 32x32x16 pattern, leaves the 16x16x32 row read 2-way conflicted.)
+__device__ __forceinline__ int x16_off(int row, int ch) { return (row << 8) + ((ch ^ ((row & 7) << 1)) << 4); }
+
+// Per-lane offsets of the two operand reads of a 16x16x32 product on an x16 image whose row block starts at a multiple
+// of 16 rows (the block's base is then an immediate).
+struct X16Reads {
+  int row[4];   // ds_read_b128 of k-step kk: row i, chunk 4 kk + g
+  int tr[8];    // ds_read_b64_tr_b16 of 16-column block db, rows 4 g + q (and + 16 rows at tr + 4096)
+  __device__ __forceinline__ void init(int lane) {
+    const int i = lane & 15, g = lane >> 4, q = i >> 2, pp = i & 3;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) row[kk] = x16_off(i, 4 * kk + g);
+#pragma unroll
+    for (int db = 0; db < 8; ++db) tr[db] = x16_off(4 * g + q, 2 * db + (pp >> 1)) + 8 * (pp & 1);
+  }
+};
+
+// A = X^T operand (16 columns of X as rows x 32 rows of X as k) for a 32-row tile: rows {4g..4g+3} and {16+4g..}, the
+// k order in which a 16x16 accumulator pair (row blocks 0 and 1 of the other product) hands over as the B operand.
+__device__ __forceinline__ bf16x8 x16_tr(const char* img, int off) { return lds_tr2(img, off, off + 16 * 256); }
+
+// B operand from two 16x16 accumulators holding rows 4g + r of row blocks 0 and 1 (the x16_tr k order).
+__device__ __forceinline__ bf16x8 acc_pair_b(const f32x4& lo, const f32x4& hi) {
+  bf16x8 b;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    b[j] = (bf16)lo[j];
+    b[4 + j] = (bf16)hi[j];
+  }
+  return b;
+}
+
+// LDS-DMA of ROWS x 128 bf16 rows [row0, row0 + ROWS) of a strided tile into an x16 image (rows past nvalid re-read
+// the last valid row: finite data the caller masks).  A lane's instructions are NT / 16 rows apart, a multiple of 8,
+// so one (row, chunk) pair per lane serves them all.  `lds_w` = lds_addr(img + wave * 1 KiB).
+template <int ROWS, int NT>
+struct X16Stage {
+  static constexpr int NI = ROWS * 16 / NT, RSTEP = NT / 16;
+  static_assert(ROWS * 16 % NT == 0 && RSTEP % 8 == 0, "x16 staging: whole 8-row swizzle periods per instruction");
+  int prow = 0, pch = 0;
+  __device__ __forceinline__ void init() {
+    const int L = threadIdx.x;
+    prow = L >> 4;
+    pch = ((L & 15) ^ ((prow & 7) << 1)) * 8;
+  }
+  __device__ __forceinline__ void stage(unsigned lds_w, const bf16* base, int64_t rstride, int row0,
+                                        int nvalid) const {
+    const bf16* t = uniform_ptr(base + (int64_t)row0 * rstride);
+    const int rmax = nvalid - 1 - row0;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      lds_dma16(t, (unsigned)(((int64_t)min(prow + i * RSTEP, rmax) * rstride + pch) * 2), lds_w + NT * i * 16);
+  }
+};
+
+// Epilogue of a 32-row x 128-column result held as 16x16 accumulators acc[db][rb] (lane: row rb * 16 + (lane & 15),
+// columns 16 db + 4 g .. + 3): scale, optional inverse RoPE of the interleaved pairs (position row + rope_off), bf16,
+// rows [0, nvalid) stored at base + r * rstride as 16-B row segments through this wave's 8-KiB LDS slab.
+__device__ __forceinline__ void store_rows16(char* slab, bf16* base, int64_t rstride, int nvalid,
+                                             const f32x4 (&acc)[8][2], float mul, int lane, int row0,
+                                             const float* rc, const float* rs, int rope_off) {
+  const int i = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int r = rb * 16 + i;
+    const bool ok = r < nvalid;
+    const float* cr = rc && ok ? rc + (int64_t)(row0 + r + rope_off) * 64 : nullptr;
+    const float* sr = rs && ok ? rs + (int64_t)(row0 + r + rope_off) * 64 : nullptr;
+#pragma unroll
+    for (int db = 0; db < 8; ++db) {
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = acc[db][rb][j] * mul;
+      if (cr) {
+        const int i0 = db * 8 + 2 * g;   // pairs (16 db + 4 g, +1) and (+2, +3)
+        const float2 c = *reinterpret_cast<const float2*>(cr + i0);
+        const float2 sn = *reinterpret_cast<const float2*>(sr + i0);
+        const float a0 = v[0], b0 = v[1], a1 = v[2], b1 = v[3];
+        v[0] = fmaf(a0, c.x, b0 * sn.x);
+        v[1] = fmaf(b0, c.x, -a0 * sn.x);
+        v[2] = fmaf(a1, c.y, b1 * sn.y);
+        v[3] = fmaf(b1, c.y, -a1 * sn.y);
+      }
+      bf16x4 w;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = (bf16)v[j];
+      const int ch = 2 * db + (g >> 1);
+      *reinterpret_cast<bf16x4*>(slab + (r << 8) + ((ch ^ (r & 15)) << 4) + 8 * (g & 1)) = w;
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes are done
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int r = it * 4 + (lane >> 4), c = lane & 15;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(slab + (r << 8) + ((c ^ (r & 15)) << 4));
+    if (r < nvalid) *reinterpret_cast<bf16x8*>(base + (int64_t)r * rstride + c * 8) = v;
+  }
+}
+
 }  // namespace dph

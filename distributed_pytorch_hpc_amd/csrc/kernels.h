@@ -96,6 +96,8 @@ struct AttnBwdParams {
   const float* rope_cos; const float* rope_sin; int rope_off;
 };
 void flash_attn_bwd(const AttnBwdParams& p, hipStream_t stream);
+int attn_set_variant(int v);   // A/B of the 16x16x32 attention kernels (0 = default)
+int attn_get_variant();
 
 // ---- Embedding gather / scatter-add backward (vocab-sharded friendly: out-of-range ids -> zero row) ----
 void embedding_fwd(const int64_t* ids, const void* table, void* out, int64_t n, int64_t dim, int64_t vocab_start,

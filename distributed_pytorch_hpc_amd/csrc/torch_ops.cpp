@@ -1274,6 +1274,7 @@ void car_poison_op(int64_t ctx, const Tensor& flag, Tensor& gscale) {
   dph::car_poison(ctx, flag.data_ptr<int>(), gscale.data_ptr<float>(), cur_stream());
 }
 int64_t car_agreed_op(int64_t ctx) { return dph::car_agreed(ctx); }
+int64_t attn_variant_op(int64_t v) { return dph::attn_set_variant((int)v); }
 void car_destroy_op(int64_t ctx) { dph::car_destroy(ctx); }
 
 }  // namespace
@@ -1535,6 +1536,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("car_open(int ctx, Tensor handles) -> ()", &car_open_op);
   m.def("car_status(int ctx) -> int", &car_status_op);
   m.def("car_agreed(int ctx) -> int", &car_agreed_op);
+  m.def("attn_variant(int v) -> int", &attn_variant_op);
   m.def("car_flag(int ctx, Tensor(a!) flag) -> ()");
   m.def("car_poison(int ctx, Tensor flag, Tensor(a!) gscale) -> ()");
   m.def("car_destroy(int ctx) -> ()", &car_destroy_op);

@@ -298,6 +298,16 @@ def _car_allreduce(ctx, inp, out, algo, scale, max_blocks):
     return None
 
 
+@register_fake("dph::car_flag")
+def _car_flag(ctx, flag):
+    return None
+
+
+@register_fake("dph::car_poison")
+def _car_poison(ctx, flag, gscale):
+    return None
+
+
 @register_fake("dph::gemm_nt")
 def _gemm_nt(A, B):
     return A.new_empty((*A.shape[:-1], B.shape[0]))

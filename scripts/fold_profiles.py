@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Fold a finished A/B or measurement directory under profiles/ into one archive file plus its README.
+
+Every round's A/B left dozens of 4-line logs per directory (1,031 tracked files).  This keeps all of the
+evidence -- byte for byte -- but as ONE ``raw_logs.txt`` per directory, each original file introduced by a
+``==== <relative path> (<n> bytes) ====`` header, so a citation ``profiles/r5/dma_place/run3.log`` becomes
+``profiles/r5/dma_place/raw_logs.txt`` section ``run3.log``.  ``README.md`` and ``summary*.txt`` / ``pmc.txt`` (the files
+other documents cite by line number) stay as they are.  Binary files are left alone.
+
+    python scripts/fold_profiles.py profiles/r5/dma_place profiles/r5/wgrad16 ...
+    python scripts/fold_profiles.py --unfold profiles/r5/dma_place      # restore the original files
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+
+KEEP = ("README.md", "pmc.txt")
+ARCHIVE = "raw_logs.txt"
+SEP = "==== "
+
+
+def _keep(name: str) -> bool:
+    return name in KEEP or (name.startswith("summary") and name.endswith(".txt")) or name == ARCHIVE
+
+
+def _text(path: str):
+    with open(path, "rb") as fh:
+        data = fh.read()
+    try:
+        return data.decode("utf-8")
+    except UnicodeDecodeError:
+        return None
+
+
+def fold(d: str) -> int:
+    parts = []
+    for root, _, files in sorted(os.walk(d)):
+        for f in sorted(files):
+            p = os.path.join(root, f)
+            rel = os.path.relpath(p, d)
+            if root == d and _keep(f):
+                continue
+            t = _text(p)
+            if t is None:
+                continue
+            parts.append((rel, p, t))
+    if not parts:
+        return 0
+    arch = os.path.join(d, ARCHIVE)
+    mode = "a" if os.path.exists(arch) else "w"
+    with open(arch, mode) as fh:
+        for rel, _, t in parts:
+            fh.write(f"{SEP}{rel} ({len(t.encode())} bytes) ====\n{t}")
+            if not t.endswith("\n"):
+                fh.write("\n")
+    for _, p, _ in parts:
+        os.remove(p)
+    for root, dirs, files in sorted(os.walk(d, topdown=False)):
+        if root != d and not os.listdir(root):
+            os.rmdir(root)
+    return len(parts)
+
+
+def unfold(d: str) -> int:
+    arch = os.path.join(d, ARCHIVE)
+    with open(arch) as fh:
+        lines = fh.read().split("\n")
+    n, cur, buf = 0, None, []
+
+    def flush():
+        nonlocal n
+        if cur is None:
+            return
+        p = os.path.join(d, cur)
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "w") as out:
+            out.write("\n".join(buf))
+        n += 1
+
+    for ln in lines:
+        if ln.startswith(SEP) and ln.endswith(" bytes) ===="):
+            flush()
+            cur, buf = ln[len(SEP):].rsplit(" (", 1)[0], []
+        else:
+            buf.append(ln)
+    flush()
+    os.remove(arch)
+    return n
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("dirs", nargs="+")
+    ap.add_argument("--unfold", action="store_true")
+    a = ap.parse_args(argv)
+    for d in a.dirs:
+        n = unfold(d) if a.unfold else fold(d)
+        print(f"{d}: {'restored' if a.unfold else 'folded'} {n} file(s)", file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()
