@@ -100,6 +100,9 @@ def parse(argv=None):
     ap.add_argument("--fp8", action="store_true",
                     help="opt-in FP8 GEMMs for the projections (ops/fp8.py; e4m3 activations/weights, e5m2 gradients, "
                          "LM head bf16). Reported with dtype 'bf16+fp8-gemm' -- not the bf16 headline number")
+    ap.add_argument("--attn-variant", type=int, default=0,
+                    help="flash-attention kernels for head dim 128: 0 = 32x32x16 MFMA forms (default), 2 = the "
+                         "16x16x32 forms (faster in isolation, not in the power-limited step: profiles/r6/attn16/)")
     ap.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
                     help="cpu: gloo + eager reference ops (tests of the N > 1 code path with tiny models only)")
     args = ap.parse_args(argv)
@@ -201,6 +204,8 @@ def main(argv=None):
 
     if not cpu:
         _lib.require()
+        if args.attn_variant:
+            _lib.ops().attn_variant(args.attn_variant)
     if args.kernels == "aten":
         _lib.set_reference_mode(True)
 

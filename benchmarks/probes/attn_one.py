@@ -23,8 +23,10 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--which", default="fwd,bwd")
     ap.add_argument("--noncausal", action="store_true")
-    ap.add_argument("--variant", type=int, default=0, help="attention kernel A/B (0 = default 16x16x32 forms for D 128, "
-                                                            "1 = the 32x32x16 forms)")
+    ap.add_argument("--packed", action="store_true",
+                    help="q / k / v as views of one [B, S, 3 H D] projection output (the Llama step's layout)")
+    ap.add_argument("--variant", type=int, default=0, help="attention kernel forms for D 128: 0 = 32x32x16 (default), "
+                                                            "2 = 16x16x32")
     ap.add_argument("--sustain", type=float, default=0.0,
                     help="also loop each kernel for this many seconds under the GPU telemetry sampler (clock, power, "
                          "package-power residency, TFLOP/J)")
@@ -32,8 +34,12 @@ def main():
     _lib.require()
     _lib.ops().attn_variant(a.variant)
     causal = not a.noncausal
-    q, k, v = (torch.randn(a.b, a.s, a.h, a.d, device="cuda", dtype=torch.bfloat16) for _ in range(3))
-    do = torch.randn_like(q)
+    if a.packed:
+        qkv = torch.randn(a.b, a.s, 3 * a.h * a.d, device="cuda", dtype=torch.bfloat16)
+        q, k, v = (qkv[:, :, i * a.h * a.d:(i + 1) * a.h * a.d].view(a.b, a.s, a.h, a.d) for i in range(3))
+    else:
+        q, k, v = (torch.randn(a.b, a.s, a.h, a.d, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+    do = torch.randn(a.b, a.s, a.h, a.d, device="cuda", dtype=torch.bfloat16)
     scale = 1 / math.sqrt(a.d)
     o, lse = ops.flash_fwd(q, k, v, scale, causal)
     flops = 4 * a.b * a.h * a.s * a.s * a.d * (0.5 if causal else 1.0)

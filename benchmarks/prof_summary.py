@@ -28,11 +28,11 @@ from collections import defaultdict
 CATEGORIES = [
     ("conv(miopen/ck)", re.compile(r"igemm_|grouped_conv|naive_conv|MIOpen|miopen|SubTensorOp", re.I)),
     ("gemm", re.compile(r"Cijk_|gemm|Gemm|hipblaslt|_MT\d+x\d+", re.I)),
-    ("attn_fwd", re.compile(r"attn_fwd_k")),
+    ("attn_fwd", re.compile(r"attn_fwd(16)?_k")),
     ("decode_attn", re.compile(r"decode_attn_k|decode_combine_k")),
     ("kv_append", re.compile(r"kv_append_k")),
-    ("attn_bwd_dkdv", re.compile(r"attn_bwd_dkdv_k")),
-    ("attn_bwd_dq", re.compile(r"attn_bwd_dq_k")),
+    ("attn_bwd_dkdv", re.compile(r"attn_bwd_dkdv(16)?_k")),
+    ("attn_bwd_dq", re.compile(r"attn_bwd_dq(16)?_k")),
     ("attn_delta", re.compile(r"attn_delta_k")),
     ("rmsnorm", re.compile(r"rmsnorm|col_reduce")),
     ("swiglu", re.compile(r"swiglu")),

@@ -1,5 +1,7 @@
 // Flash attention forward for CDNA4 (gfx950): the kernel and its launcher.  Design notes for the whole attention
 // family (forward, backward, dropout) are at the top of attention_common.h.
+#include <type_traits>
+
 #include "attention_common.h"
 
 namespace dph {
@@ -257,9 +259,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(AttnParams p) {
   const int wtiles = wave_tile_count<CAUSAL>(ntiles, q0w, off);
 
   X16Stage<BN, NT> st;
-  st.init();
+  st.init(p.k_ss);
   X16Reads rd;
-  rd.init(lane);
+  rd.init(lane, lds_addr(smem));
   const unsigned lds_w = lds_addr(smem + wid * 1024);
 
   f32x4 o[8][2];
@@ -280,15 +282,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(AttnParams p) {
   wait_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
+  // one instantiation of the tile body per image buffer: every LDS read is a per-lane address plus an immediate
+  auto tile = [&](auto BUFC, int t) {
+    constexpr int buf = decltype(BUFC)::value;
+    constexpr unsigned KL = buf * 2 * TILE, VL = KL + TILE;
     if (t + 1 < ntiles) {
       const unsigned nb = lds_w + (buf ^ 1) * 2 * TILE;
       st.stage(nb, kp, p.k_ss, (t + 1) * BN, p.Sk);
       st.stage(nb + TILE, vp, p.v_ss, (t + 1) * BN, p.Sk);
     }
-    const char* Kl = smem + buf * 2 * TILE;
-    const char* Vl = Kl + TILE;
     if (t < wtiles) {
       const int k0 = t * BN;
       f32x4 s[4][2];
@@ -300,7 +302,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(AttnParams p) {
       for (int kk = 0; kk < 4; ++kk) {
         bf16x8 kf[4];
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb) kf[kb] = lds_b128(Kl, rd.row[kk] + (kb << 12));
+        for (int kb = 0; kb < 4; ++kb) kf[kb] = ldsa_b128(rd.row[kk] + KL + (kb << 12));
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb) {
           s[kb][0] = mfma16(kf[kb], qf[0][kk], s[kb][0]);
@@ -309,6 +311,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(AttnParams p) {
       }
       __builtin_amdgcn_sched_barrier(0);
       if ((k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0w + off))) {   // wave-uniform
+        asm volatile("" ::: "memory");   // a real branch: no if-converted selects on every tile
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
@@ -356,13 +359,17 @@ __global__ __launch_bounds__(256, 2) void attn_fwd16_k(AttnParams p) {
       for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
         for (int db = 0; db < 8; ++db) {
-          const bf16x8 vt = x16_tr(Vl, rd.tr[db] + ((ks * 32) << 8));
+          const bf16x8 vt = ldsa_tr(rd.tr[db] + VL + ((ks * 32) << 8));
           o[db][0] = mfma16(vt, pf[ks][0], o[db][0]);
           o[db][1] = mfma16(vt, pf[ks][1], o[db][1]);
         }
     }
     wait_vmcnt<0>();   // this wave's share of tile t+1 has landed ...
     __builtin_amdgcn_s_barrier();   // ... and every wave's, and nobody reads tile t's images any more
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t + 1);
   }
 
   // ---- epilogue: O = O^T / l, lse ----
@@ -398,7 +405,7 @@ static void fwd_launch(const AttnParams& p, hipStream_t st) {
   if (p.drop_p > 0.f) {
     if (p.causal) hipLaunchKernelGGL((attn_fwd_k<HD, true, true>), grid, dim3(256), lds, st, p);
     else hipLaunchKernelGGL((attn_fwd_k<HD, false, true>), grid, dim3(256), lds, st, p);
-  } else if (HD == 128 && !p.acc_o && attn_get_variant() == 0) {
+  } else if (HD == 128 && !p.acc_o && attn_get_variant() == 2) {
     if (p.causal) hipLaunchKernelGGL((attn_fwd16_k<true>), grid, dim3(256), lds, st, p);
     else hipLaunchKernelGGL((attn_fwd16_k<false>), grid, dim3(256), lds, st, p);
   } else {

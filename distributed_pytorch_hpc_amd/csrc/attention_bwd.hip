@@ -1,5 +1,7 @@
 // Flash attention backward for CDNA4 (gfx950): the Q-stationary dQ kernel (which also forms delta = rowsum(dO * O)),
 // the KV-stationary dK/dV kernel and their launcher.  Design notes at the top of attention_common.h.
+#include <type_traits>
+
 #include "attention_common.h"
 
 namespace dph {
@@ -451,8 +453,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_k(AttnBwdParams P) {
 //   pair of the key block (acc_pair_b: no lane movement)                                   32 MFMAs
 // The key is on the lane of S / dP (col = lane & 15), so P and dS are B operands as they stand.  LDS traffic per MFMA
 // FLOP is that of the 32x32x16 kernel; the x16 image makes every read conflict-free.
-template <bool CAUSAL>
+// OPT bits (measured, profiles/r6/attn16/README.md): bit 0 = -delta as the dP chain's initial accumulator, bit 1 = one
+// tile-body instance per image buffer (immediate LDS offsets), bit 2 = no compiler fence in the mask branch.  Per-kernel
+// times under --kernel-trace on one box, dK/dV + dQ per call: OPT 0 2.32 + 1.65 ms, 4 2.29 + 1.63, 3 2.19 + 1.60,
+// 7 2.20 + 1.60; the round-5 32x32x16 kernels 2.23 + 1.65.  Default 3.
+template <bool CAUSAL, int OPT = 3>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
+  constexpr bool RINIT = OPT & 1, UNROLL = OPT & 2;
   constexpr int HD = 128, NW = 4, NT = 64 * NW, BNK = 32 * NW, BMQ = 32;
   constexpr int QIMG = BMQ * HD * 2;        // Q / dO tile image [32 q][128]
   constexpr int KIMG = BNK * HD * 2;        // K image [128 keys][128]
@@ -478,7 +485,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
   const bf16* vp = (const bf16*)p.v + (int64_t)b * p.v_sb + (int64_t)hk * p.v_sh;
   {
     X16Stage<BNK, NT> kst;
-    kst.init();
+    kst.init(p.k_ss);
     kst.stage(lds_addr(Kimg + wid * 1024), kp, p.k_ss, kb0, p.Sk);
   }
   // V^T B fragments of dP = dO V^T: lane (key i, g) holds V[key][32 kk + 8 g .. + 7]
@@ -500,16 +507,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
       for (int r = 0; r < 4; ++r) { dk[db][kb][r] = 0.f; dv[db][kb][r] = 0.f; }
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   X16Reads rd;
-  rd.init(lane);
-  const int krow = (wid * 32) << 8;   // this wave's K rows in the K image
+  rd.init(lane, lds_addr(smem));
+  // image bases relative to smem (immediates in every read): K | Q0 | dO0 | Q1 | dO1
+  const unsigned kro = (wid * 32) << 8;   // this wave's K rows
 
   int qstart = 0;
   if (CAUSAL) qstart = max(0, kb0 - off) / BMQ * BMQ;
   const int nqt_head = qstart < p.Sq ? (p.Sq - qstart + BMQ - 1) / BMQ : 0;
   const int total = nqt_head * grp;
 
-  X16Stage<BMQ, NT> qst;
-  qst.init();
+  X16Stage<BMQ, NT> qst, ost;   // one plan per row stride (Q is often a view of the packed QKV projection, dO is not)
+  qst.init(p.q_ss);
+  ost.init(P.do_ss);
   const unsigned lds_q = lds_addr(Qbuf + wid * 1024);
   float st_lse = 0.f, st_del = 0.f;
   auto stage = [&](int it, int buf) {
@@ -519,7 +528,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
     const bf16* dop = (const bf16*)P.dout + (int64_t)b * P.do_sb + (int64_t)hq * P.do_sh;
     const unsigned ql = lds_q + buf * 2 * QIMG;
     qst.stage(ql, qp, p.q_ss, qt0, p.Sq);
-    qst.stage(ql + QIMG, dop, P.do_ss, qt0, p.Sq);
+    ost.stage(ql + QIMG, dop, P.do_ss, qt0, p.Sq);
     if (threadIdx.x < BMQ) {
       const int q = min(qt0 + (int)threadIdx.x, p.Sq - 1);   // rows past Sq: finite, masked below
       const int64_t idx = ((int64_t)b * p.Hq + hq) * p.Sq + q;
@@ -530,7 +539,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
   auto stage_scalars = [&](int buf) {
     if (threadIdx.x < BMQ) {
       lse_s[buf * BMQ + threadIdx.x] = -st_lse * 1.4426950408889634f;  // -lse in log2 units
-      del_s[buf * BMQ + threadIdx.x] = st_del;
+      del_s[buf * BMQ + threadIdx.x] = RINIT ? -st_del : st_del;   // -delta: the dP chain's initial accumulator
     }
   };
 
@@ -541,24 +550,33 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
   wait_vmcnt<0>();
   __syncthreads();
 
-  for (int it = 0; it < total; ++it) {
-    const int buf = it & 1;
+  // The tile body is instantiated once per image buffer (even / odd tiles), so every LDS address is a per-lane offset
+  // plus an immediate: no per-read address arithmetic on the vector ALU, which this body is bound by.
+  auto tile = [&](auto BUFC, int it) {
+    const int buf = BUFC;
     const int qt0 = qstart + (it % nqt_head) * BMQ;
     if (it + 1 < total) stage(it + 1, buf ^ 1);
-    const char* Ql = Qbuf + buf * 2 * QIMG;
-    const char* Ol = Ql + QIMG;
+    const unsigned QL = KIMG + buf * 2 * QIMG, OL = QL + QIMG;
     if (!(CAUSAL && key0 > qt0 + BMQ - 1 + off)) {   // some of this wave's keys are visible to the tile
+      const float* ls = lse_s + buf * BMQ;
+      const float* ds = del_s + buf * BMQ;
+      // row constants: -delta is the dP chain's initial accumulator (dS = P dP' needs no subtraction afterwards)
+      f32x4 nl[2], ndl[2], s[2][2], dp[2][2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        nl[qb] = *reinterpret_cast<const f32x4*>(ls + qb * 16 + 4 * g);
+        const f32x4 nd = *reinterpret_cast<const f32x4*>(ds + qb * 16 + 4 * g);
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) { s[qb][kb] = z4; dp[qb][kb] = RINIT ? nd : z4; }
+        ndl[qb] = nd;
+      }
       __builtin_amdgcn_s_setprio(1);
-      f32x4 s[2][2], dp[2][2];
-#pragma unroll
-      for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) { s[qb][kb] = z4; dp[qb][kb] = z4; }
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const bf16x8 k0f = lds_b128(Kimg, rd.row[kk] + krow), k1f = lds_b128(Kimg, rd.row[kk] + krow + 4096);
-        const bf16x8 q0f = lds_b128(Ql, rd.row[kk]), q1f = lds_b128(Ql, rd.row[kk] + 4096);
-        const bf16x8 o0f = lds_b128(Ol, rd.row[kk]), o1f = lds_b128(Ol, rd.row[kk] + 4096);
+        const unsigned ka = rd.row[kk] + kro;
+        const bf16x8 k0f = ldsa_b128(ka), k1f = ldsa_b128(ka + 4096);
+        const bf16x8 q0f = ldsa_b128(rd.row[kk] + QL), q1f = ldsa_b128(rd.row[kk] + QL + 4096);
+        const bf16x8 o0f = ldsa_b128(rd.row[kk] + OL), o1f = ldsa_b128(rd.row[kk] + OL + 4096);
         s[0][0] = mfma16(q0f, k0f, s[0][0]);
         s[0][1] = mfma16(q0f, k1f, s[0][1]);
         s[1][0] = mfma16(q1f, k0f, s[1][0]);
@@ -569,8 +587,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
         dp[1][1] = mfma16(o1f, vf[1][kk], dp[1][1]);
       }
       __builtin_amdgcn_s_setprio(0);
-      // wave-uniform: only diagonal / ragged tiles pay for the selects (masked scores -> -inf -> P = 0)
+      // wave-uniform: only diagonal / ragged tiles pay for the selects (masked scores -> -inf -> P = 0); the empty asm
+      // keeps the compiler from if-converting the block into selects that every tile would execute
       if ((qt0 + BMQ > p.Sq) || (key0 + 32 > p.Sk) || (CAUSAL && key0 + 31 > qt0 + off)) {
+        if constexpr (!(OPT & 4)) asm volatile("" ::: "memory");
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
@@ -583,24 +603,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
       }
       // the first dV / dK step's transposed operands are read now, their latency covered by the softmax
       bf16x8 tro_o[2], tro_q[2];
-      tro_o[0] = x16_tr(Ol, rd.tr[0]);
-      tro_q[0] = x16_tr(Ql, rd.tr[0]);
+      tro_o[0] = ldsa_tr(rd.tr[0] + OL);
+      tro_q[0] = ldsa_tr(rd.tr[0] + QL);
       __builtin_amdgcn_sched_barrier(0);
-      const float* ls = lse_s + buf * BMQ;
-      const float* ds = del_s + buf * BMQ;
 #pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        const f32x4 nl = *reinterpret_cast<const f32x4*>(ls + qb * 16 + 4 * g);
-        const f32x4 dl = *reinterpret_cast<const f32x4*>(ds + qb * 16 + 4 * g);
+      for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float pv = exp2_(fmaf(s[qb][kb][r], sl2, nl[r]));
+            const float pv = exp2_(fmaf(s[qb][kb][r], sl2, nl[qb][r]));
             s[qb][kb][r] = pv;
-            dp[qb][kb][r] = pv * (dp[qb][kb][r] - dl[r]);
+            dp[qb][kb][r] = RINIT ? pv * dp[qb][kb][r] : pv * (dp[qb][kb][r] - ndl[qb][r]);
           }
-      }
       bf16x8 pb[2], sb[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -613,8 +628,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
 #pragma unroll
       for (int db = 0; db < 8; ++db) {
         if (db + 1 < 8) {
-          tro_o[(db + 1) & 1] = x16_tr(Ol, rd.tr[db + 1]);
-          tro_q[(db + 1) & 1] = x16_tr(Ql, rd.tr[db + 1]);
+          tro_o[(db + 1) & 1] = ldsa_tr(rd.tr[db + 1] + OL);
+          tro_q[(db + 1) & 1] = ldsa_tr(rd.tr[db + 1] + QL);
         }
         dv[db][0] = mfma16(tro_o[db & 1], pb[0], dv[db][0]);
         dv[db][1] = mfma16(tro_o[db & 1], pb[1], dv[db][1]);
@@ -628,6 +643,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
     if (it + 1 < total) stage_scalars(buf ^ 1);
     wait_vmcnt<0>();
     __syncthreads();
+  };
+  if constexpr (UNROLL) {
+    for (int it = 0; it < total; it += 2) {
+      tile(std::integral_constant<int, 0>{}, it);
+      if (it + 1 < total) tile(std::integral_constant<int, 1>{}, it + 1);
+    }
+  } else {
+    for (int it = 0; it < total; ++it) tile(it & 1, it);
   }
 
   {   // dK then dV through this wave's 8-KiB LDS slab (the images are free after the loop's last barrier)
@@ -648,8 +671,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv16_k(AttnBwdParams P) {
 //   dS^T = P^T (dP^T - delta), P^T = exp2(S^T c - lse): the query is on the lane, row constants are lane scalars
 //   dQ^T[db][qb] += K^T dS^T                       A = x16_tr(K image), B = the half's dS^T pair   16 MFMAs
 // and it forms delta = rowsum(dO * O) for its queries first (written for the dK/dV kernel, which runs after it).
-template <bool CAUSAL>
+template <bool CAUSAL, int OPT = 3>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(AttnBwdParams P) {
+  constexpr bool RINIT = OPT & 1, UNROLL = OPT & 2;
   constexpr int HD = 128, NW = 4, NT = 64 * NW, BM = 32 * NW, BN = 64;
   constexpr int TILE = BN * HD * 2;   // one 64-row x16 image (16 KiB); buffer = K | V
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -708,9 +732,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(AttnBwdParams P) {
   const int wtiles = wave_tile_count<CAUSAL>(ntiles, q0w, off);
 
   X16Stage<BN, NT> st;
-  st.init();
+  st.init(p.k_ss);
   X16Reads rd;
-  rd.init(lane);
+  rd.init(lane, lds_addr(smem));
   const unsigned lds_w = lds_addr(smem + wid * 1024);
 
   f32x4 dq[8][2];
@@ -729,30 +753,35 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(AttnBwdParams P) {
   wait_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
 
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
+  // one instantiation of the tile body per image buffer: every LDS read is a per-lane address plus an immediate
+  f32x4 nd[2];   // -delta of this lane's queries: the dP^T chain's initial accumulator (dS^T = P^T dP^T')
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) nd[qb][r] = -delta[qb];
+  auto tile = [&](auto BUFC, int t) {
+    const int buf = BUFC;
+    const unsigned KL = buf * 2 * TILE, VL = KL + TILE;
     if (t + 1 < ntiles) {
       const unsigned nb = lds_w + (buf ^ 1) * 2 * TILE;
       st.stage(nb, kp, p.k_ss, (t + 1) * BN, p.Sk);
       st.stage(nb + TILE, vp, p.v_ss, (t + 1) * BN, p.Sk);
     }
-    const char* Kl = smem + buf * 2 * TILE;
-    const char* Vl = Kl + TILE;
     if (t < wtiles) {
       const int k0 = t * BN;
       const bool need_mask = (k0 + BN > p.Sk) || (CAUSAL && (k0 + BN - 1 > q0w + off));
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
+        const unsigned R0 = (unsigned)(h * 32) << 8;
         f32x4 sa[2][2], pa[2][2];   // [kb within the half][qb]
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-          for (int qb = 0; qb < 2; ++qb) { sa[a][qb] = z4; pa[a][qb] = z4; }
+          for (int qb = 0; qb < 2; ++qb) { sa[a][qb] = z4; pa[a][qb] = RINIT ? nd[qb] : z4; }
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
-          const int r0 = (h * 32) << 8;
-          const bf16x8 k0f = lds_b128(Kl, rd.row[kk] + r0), k1f = lds_b128(Kl, rd.row[kk] + r0 + 4096);
-          const bf16x8 v0f = lds_b128(Vl, rd.row[kk] + r0), v1f = lds_b128(Vl, rd.row[kk] + r0 + 4096);
+          const bf16x8 k0f = ldsa_b128(rd.row[kk] + KL + R0), k1f = ldsa_b128(rd.row[kk] + KL + R0 + 4096);
+          const bf16x8 v0f = ldsa_b128(rd.row[kk] + VL + R0), v1f = ldsa_b128(rd.row[kk] + VL + R0 + 4096);
           sa[0][0] = mfma16(k0f, qf[0][kk], sa[0][0]);
           sa[0][1] = mfma16(k0f, qf[1][kk], sa[0][1]);
           sa[1][0] = mfma16(k1f, qf[0][kk], sa[1][0]);
@@ -762,7 +791,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(AttnBwdParams P) {
           pa[1][0] = mfma16(v1f, df[0][kk], pa[1][0]);
           pa[1][1] = mfma16(v1f, df[1][kk], pa[1][1]);
         }
-        if (need_mask) {   // wave-uniform; masked scores -> -inf -> p = 0
+        // wave-uniform; masked scores -> -inf -> p = 0.  The empty asm keeps hipcc from if-converting the block into
+        // selects that every tile would execute.
+        if (need_mask) {
+          if constexpr (!(OPT & 4)) asm volatile("" ::: "memory");
 #pragma unroll
           for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -779,7 +811,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(AttnBwdParams P) {
           for (int qb = 0; qb < 2; ++qb)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              sa[a][qb][r] = exp2_(fmaf(sa[a][qb][r], sl2, nlse2[qb])) * (pa[a][qb][r] - delta[qb]);
+              sa[a][qb][r] = exp2_(fmaf(sa[a][qb][r], sl2, nlse2[qb])) * (RINIT ? pa[a][qb][r] : pa[a][qb][r] - delta[qb]);
         bf16x8 dsb[2];
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) dsb[qb] = acc_pair_b(sa[0][qb], sa[1][qb]);
@@ -787,7 +819,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(AttnBwdParams P) {
         // dQ^T += K^T dS^T over this half's 32 keys
 #pragma unroll
         for (int db = 0; db < 8; ++db) {
-          const bf16x8 kt = x16_tr(Kl, rd.tr[db] + ((h * 32) << 8));
+          const bf16x8 kt = ldsa_tr(rd.tr[db] + KL + R0);
           dq[db][0] = mfma16(kt, dsb[0], dq[db][0]);
           dq[db][1] = mfma16(kt, dsb[1], dq[db][1]);
         }
@@ -796,6 +828,14 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(AttnBwdParams P) {
     }
     wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
+  };
+  if constexpr (UNROLL) {
+    for (int t = 0; t < ntiles; t += 2) {
+      tile(std::integral_constant<int, 0>{}, t);
+      if (t + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t + 1);
+    }
+  } else {
+    for (int t = 0; t < ntiles; ++t) tile(t & 1, t);
   }
 
   {   // dQ through this wave's 8-KiB LDS slab (the K / V images are free after the loop's last barrier)
@@ -805,8 +845,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq16_k(AttnBwdParams P) {
   }
 }
 
-// A/B switch for the 16x16x32 kernels (benchmarks/probes/attn_one.py --variant): 1 = the 32x32x16 forms for head
-// dim 128 too.  Process-wide, default 0; not read from the environment.
+// Which flash-attention kernels run for head dim 128 (process-wide, set by the attn_variant op; not read from the
+// environment): 0 (default) = the 32x32x16 kernels, 2 = the 16x16x32 kernels (attn_fwd16_k / attn_bwd_dq16_k /
+// attn_bwd_dkdv16_k).  In isolation the 16x16x32 forms are 1-4 % faster (they hold a 6-11 % higher clock), but in
+// the 7B training step, where the package power limit sets the clock for every kernel, they lose that clock and keep
+// their lower MFMA busy share: 28 650 / 28 507 / 28 706 vs 28 756 / 28 757 / 28 782 tokens/s interleaved on one box,
+// 28 845 / 28 755 vs 29 150 / 29 079 on another (profiles/r6/attn16/README.md).  So the 32x32x16 kernels stay the
+// default.
 static int g_attn_variant = 0;
 int attn_set_variant(int v) {
   const int old = g_attn_variant;
@@ -821,14 +866,14 @@ static void bwd_launch_t(const AttnBwdParams& P, hipStream_t st) {
   // dQ first: it forms delta = rowsum(dO * O) for its rows and writes it for the dK/dV kernel
   const size_t lds_q = 2 * 2 * 64 * HD * 2;
   const dim3 grid_q((unsigned)((p.Sq + 127) / 128 * p.Hq * p.B));
-  if (HD == 128 && !DROP && g_attn_variant == 0) {
+  if (HD == 128 && !DROP && g_attn_variant == 2) {
     if (p.causal) hipLaunchKernelGGL((attn_bwd_dq16_k<true>), grid_q, dim3(256), lds_q, st, P);
     else hipLaunchKernelGGL((attn_bwd_dq16_k<false>), grid_q, dim3(256), lds_q, st, P);
   } else if (p.causal) hipLaunchKernelGGL((attn_bwd_dq_k<HD, true, DROP>), grid_q, dim3(256), lds_q, st, P);
   else hipLaunchKernelGGL((attn_bwd_dq_k<HD, false, DROP>), grid_q, dim3(256), lds_q, st, P);
   const size_t lds_kv = 128 * HD * 2 + 4 * 32 * HD * 2 + 6 * 32 * 4;
   const dim3 grid_kv((unsigned)((p.Sk + 127) / 128 * p.Hkv * p.B));
-  if (HD == 128 && !DROP && g_attn_variant == 0) {
+  if (HD == 128 && !DROP && g_attn_variant == 2) {
     if (p.causal) hipLaunchKernelGGL((attn_bwd_dkdv16_k<true>), grid_kv, dim3(256), lds_kv, st, P);
     else hipLaunchKernelGGL((attn_bwd_dkdv16_k<false>), grid_kv, dim3(256), lds_kv, st, P);
     return;

@@ -370,19 +370,31 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 // (img_off's swizzle, built for the 32x32x16 pattern, leaves the 16x16x32 row read 2-way conflicted.)
 __device__ __forceinline__ int x16_off(int row, int ch) { return (row << 8) + ((ch ^ ((row & 7) << 1)) << 4); }
 
-// Per-lane offsets of the two operand reads of a 16x16x32 product on an x16 image whose row block starts at a multiple
-// of 16 rows (the block's base is then an immediate).
+// Per-lane ABSOLUTE LDS byte addresses of the two operand reads of a 16x16x32 product on an x16 image whose row block
+// starts at a multiple of 16 rows: a read is then `ds_read v_addr offset:<image + block>` with a compile-time
+// immediate.  (Addressed as `smem + offset`, hipcc materialises the dynamic-LDS symbol with one v_add per read: 50
+// vector adds per two tiles of the dK/dV body, which is bound by vector issue.)
 struct X16Reads {
-  int row[4];   // ds_read_b128 of k-step kk: row i, chunk 4 kk + g
-  int tr[8];    // ds_read_b64_tr_b16 of 16-column block db, rows 4 g + q (and + 16 rows at tr + 4096)
-  __device__ __forceinline__ void init(int lane) {
+  unsigned row[4];   // ds_read_b128 of k-step kk: row i, chunk 4 kk + g
+  unsigned tr[8];    // ds_read_b64_tr_b16 of 16-column block db, rows 4 g + q (and + 16 rows at tr + 4096)
+  __device__ __forceinline__ void init(int lane, unsigned base) {
     const int i = lane & 15, g = lane >> 4, q = i >> 2, pp = i & 3;
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) row[kk] = x16_off(i, 4 * kk + g);
+    for (int kk = 0; kk < 4; ++kk) row[kk] = base + x16_off(i, 4 * kk + g);
 #pragma unroll
-    for (int db = 0; db < 8; ++db) tr[db] = x16_off(4 * g + q, 2 * db + (pp >> 1)) + 8 * (pp & 1);
+    for (int db = 0; db < 8; ++db) tr[db] = base + x16_off(4 * g + q, 2 * db + (pp >> 1)) + 8 * (pp & 1);
   }
 };
+
+// Reads at an absolute LDS byte address (the X16Reads forms).
+typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8_c;
+__device__ __forceinline__ bf16x8 ldsa_b128(unsigned a) { return *reinterpret_cast<lds_bf16x8_c*>(a); }
+__device__ __forceinline__ bf16x8 ldsa_tr(unsigned a) {
+  i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(reinterpret_cast<lds_i16x4*>(a));
+  i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(reinterpret_cast<lds_i16x4*>(a + 16 * 256));
+  bf16x4 x = __builtin_bit_cast(bf16x4, lo), y = __builtin_bit_cast(bf16x4, hi);
+  return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
+}
 
 // A = X^T operand (16 columns of X as rows x 32 rows of X as k) for a 32-row tile: rows {4g..4g+3} and {16+4g..}, the
 // k order in which a 16x16 accumulator pair (row blocks 0 and 1 of the other product) hands over as the B operand.
@@ -402,23 +414,34 @@ __device__ __forceinline__ bf16x8 acc_pair_b(const f32x4& lo, const f32x4& hi) {
 // LDS-DMA of ROWS x 128 bf16 rows [row0, row0 + ROWS) of a strided tile into an x16 image (rows past nvalid re-read
 // the last valid row: finite data the caller masks).  A lane's instructions are NT / 16 rows apart, a multiple of 8,
 // so one (row, chunk) pair per lane serves them all.  `lds_w` = lds_addr(img + wave * 1 KiB).
+// Full tiles step the wave-uniform source base by RSTEP rows per instruction (scalar adds) with one per-lane byte
+// offset computed at init; only a ragged last tile clamps rows per instruction.
 template <int ROWS, int NT>
 struct X16Stage {
   static constexpr int NI = ROWS * 16 / NT, RSTEP = NT / 16;
   static_assert(ROWS * 16 % NT == 0 && RSTEP % 8 == 0, "x16 staging: whole 8-row swizzle periods per instruction");
   int prow = 0, pch = 0;
-  __device__ __forceinline__ void init() {
+  unsigned voff = 0;   // (prow * rs0 + pch) * 2
+  int64_t rs0 = 0;     // the row stride voff was computed for (a tile of another stride takes the general path)
+  __device__ __forceinline__ void init(int64_t rstride) {
     const int L = threadIdx.x;
     prow = L >> 4;
     pch = ((L & 15) ^ ((prow & 7) << 1)) * 8;
+    rs0 = rstride;
+    voff = (unsigned)((prow * rstride + pch) * 2);
   }
   __device__ __forceinline__ void stage(unsigned lds_w, const bf16* base, int64_t rstride, int row0,
                                         int nvalid) const {
     const bf16* t = uniform_ptr(base + (int64_t)row0 * rstride);
-    const int rmax = nvalid - 1 - row0;
+    if (row0 + ROWS <= nvalid && rstride == rs0) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i)
-      lds_dma16(t, (unsigned)(((int64_t)min(prow + i * RSTEP, rmax) * rstride + pch) * 2), lds_w + NT * i * 16);
+      for (int i = 0; i < NI; ++i) lds_dma16(t + (int64_t)i * RSTEP * rstride, voff, lds_w + NT * i * 16);
+    } else {
+      const int rmax = nvalid - 1 - row0;
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+        lds_dma16(t, (unsigned)(((int64_t)min(prow + i * RSTEP, rmax) * rstride + pch) * 2), lds_w + NT * i * 16);
+    }
   }
 };
 

@@ -96,7 +96,7 @@ struct AttnBwdParams {
   const float* rope_cos; const float* rope_sin; int rope_off;
 };
 void flash_attn_bwd(const AttnBwdParams& p, hipStream_t stream);
-int attn_set_variant(int v);   // A/B of the 16x16x32 attention kernels (0 = default)
+int attn_set_variant(int v);   // flash-attention kernel forms for head dim 128: 0 = 32x32x16 (default), 2 = 16x16x32
 int attn_get_variant();
 
 // ---- Embedding gather / scatter-add backward (vocab-sharded friendly: out-of-range ids -> zero row) ----

@@ -222,6 +222,32 @@ def test_flash_attention(dph_native, B, Sq, Sk, Hq, Hkv, D, causal):
     assert rel_err(v.grad, vr.grad) < 3e-2
 
 
+@pytest.mark.parametrize("B,Sq,Sk,Hq,Hkv,D,causal", [c for c in CASES if c[5] == 128])
+def test_flash_attention_x16_forms(dph_native, B, Sq, Sk, Hq, Hkv, D, causal):
+    """The 16x16x32-MFMA kernels (attn_variant 2: attn_fwd16_k / attn_bwd_dq16_k / attn_bwd_dkdv16_k, opt-in) against
+    the fp32 reference, with the same shapes, ragged tails and GQA as the default kernels."""
+    prev = dph_native.attn_variant(2)
+    try:
+        test_flash_attention(dph_native, B, Sq, Sk, Hq, Hkv, D, causal)
+        cos, sin = rope_mod.precompute_rope_tables(D, 2048, device=DEV)   # fused inverse-RoPE epilogues
+        qkv = torch.randn(B, Sq, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        if Sq == Sk:
+            o = ops.rope_attention(qkv * 1.0, cos, sin, Hq, Hkv, D, pos_offset=3)
+            x = qkv.detach().float().requires_grad_()
+            q = rope_mod.rope_reference(x[:, :, : Hq * D].view(B, Sq, Hq, D), cos, sin, 3)
+            k = rope_mod.rope_reference(x[:, :, Hq * D:(Hq + Hkv) * D].view(B, Sq, Hkv, D), cos, sin, 3)
+            v = x[:, :, (Hq + Hkv) * D:].view(B, Sq, Hkv, D)
+            orf = attn_mod.attention_reference(q, k, v, causal, 1 / math.sqrt(D)).reshape(B, Sq, -1)
+            if causal:
+                assert rel_err(o, orf) < 2e-2
+                g = torch.randn_like(o)
+                o.backward(g)
+                orf.backward(g.float())
+                assert rel_err(qkv.grad, x.grad) < 3e-2
+    finally:
+        dph_native.attn_variant(prev)
+
+
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_forced_rescale(dph_native, causal):
     """The lazy-rescale branch (running max raised only when a tile's max exceeds it by RESCALE_THR) is rare on
