@@ -3,9 +3,9 @@
 
 Every round's A/B left dozens of 4-line logs per directory (1,031 tracked files).  This keeps all of the
 evidence -- byte for byte -- but as ONE ``raw_logs.txt`` per directory, each original file introduced by a
-``==== <relative path> (<n> bytes) ====`` header, so a citation ``profiles/r5/dma_place/run3.log`` becomes
-``profiles/r5/dma_place/raw_logs.txt`` section ``run3.log``.  ``README.md`` and ``summary*.txt`` / ``pmc.txt`` (the files
-other documents cite by line number) stay as they are.  Binary files are left alone.
+``==== <relative path> (<n> bytes) ====`` header, so ``profiles/r5/dma_place/run3.log`` becomes section ``run3.log`` of
+``profiles/r5/dma_place/raw_logs.txt``.  ``README.md``, ``summary*.txt`` / ``pmc.txt`` and every file some document or
+source cites by path stay as they are.  Binary files are left alone.
 
     python scripts/fold_profiles.py profiles/r5/dma_place profiles/r5/wgrad16 ...
     python scripts/fold_profiles.py --unfold profiles/r5/dma_place      # restore the original files
@@ -34,13 +34,30 @@ def _text(path: str):
         return None
 
 
-def fold(d: str) -> int:
+def cited_paths(roots=("README.md", "BASELINE.md", "SURVEY.md", "docs", "distributed_pytorch_hpc_amd", "benchmarks",
+                        "scripts", "tests", "profiles", "bench.py", "__graft_entry__.py")) -> set:
+    """Every profiles/... path that a document or source file cites: those files stay where they are."""
+    import re
+
+    out = set()
+    for root in roots:
+        walk = os.walk(root) if os.path.isdir(root) else [("", None, [root])]
+        for dp, _, fs in walk:
+            for f in fs:
+                p = os.path.join(dp, f)
+                if p.endswith((".md", ".py", ".hip", ".h", ".cpp", ".sh", ".txt")) and os.path.isfile(p):
+                    with open(p, errors="ignore") as fh:
+                        out.update(c.rstrip("./") for c in re.findall(r"profiles/[A-Za-z0-9_./-]+", fh.read()))
+    return out
+
+
+def fold(d: str, keep: set = frozenset()) -> int:
     parts = []
     for root, _, files in sorted(os.walk(d)):
         for f in sorted(files):
             p = os.path.join(root, f)
             rel = os.path.relpath(p, d)
-            if root == d and _keep(f):
+            if (root == d and _keep(f)) or os.path.normpath(p) in keep:
                 continue
             t = _text(p)
             if t is None:
@@ -95,8 +112,9 @@ def main(argv=None):
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--unfold", action="store_true")
     a = ap.parse_args(argv)
+    keep = set() if a.unfold else {os.path.normpath(c) for c in cited_paths()}
     for d in a.dirs:
-        n = unfold(d) if a.unfold else fold(d)
+        n = unfold(d) if a.unfold else fold(d, keep)
         print(f"{d}: {'restored' if a.unfold else 'folded'} {n} file(s)", file=sys.stderr)
 
 
