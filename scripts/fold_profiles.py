@@ -84,7 +84,7 @@ def unfold(d: str) -> int:
     arch = os.path.join(d, ARCHIVE)
     with open(arch) as fh:
         lines = fh.read().split("\n")
-    n, cur, buf = 0, None, []
+    n, cur, size, buf = 0, None, 0, []
 
     def flush():
         nonlocal n
@@ -92,14 +92,18 @@ def unfold(d: str) -> int:
             return
         p = os.path.join(d, cur)
         os.makedirs(os.path.dirname(p), exist_ok=True)
+        body = "\n".join(buf)
+        if len((body + "\n").encode()) <= size:   # the original ended with a newline (the header records its size)
+            body += "\n"
         with open(p, "w") as out:
-            out.write("\n".join(buf))
+            out.write(body)
         n += 1
 
     for ln in lines:
         if ln.startswith(SEP) and ln.endswith(" bytes) ===="):
             flush()
-            cur, buf = ln[len(SEP):].rsplit(" (", 1)[0], []
+            name, tail = ln[len(SEP):].rsplit(" (", 1)
+            cur, size, buf = name, int(tail.split()[0]), []
         else:
             buf.append(ln)
     flush()
