@@ -95,8 +95,11 @@ def parse(argv=None):
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--no-telemetry", action="store_true",
                     help="do not sample GPU clock / power / temperature (amdsmi host thread) during the run")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay each step as one HIP graph after the warm-up (runtime/graphs.py; one rank only)")
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=None,
+                    help="replay each step as one HIP graph after the warm-up (runtime/graphs.py; one rank only).  "
+                         "Default: on for the one-rank unet-ddp layout, whose eager step is launch-bound (243 launches "
+                         "in 3.25 ms: graph 1 229 / 1 232 samples/s at stdev 0.02 ms vs eager 1 044 / 1 230 at "
+                         "0.13-0.19 ms, profiles/r6/unet_graph/), off otherwise")
     ap.add_argument("--fp8", action="store_true",
                     help="opt-in FP8 GEMMs for the projections (ops/fp8.py; e4m3 activations/weights, e5m2 gradients, "
                          "LM head bf16). Reported with dtype 'bf16+fp8-gemm' -- not the bf16 headline number")
@@ -234,6 +237,8 @@ def main(argv=None):
                                          for b, tr, tx in res["samples"]]}
             log(f"[bench] xGMI all-reduce vs RCCL on {name}: crossover {res['crossover_bytes']} B")
     graph_info = {}
+    if args.graph is None:   # auto: the launch-bound one-rank SimpleUNet step replays as one graph
+        args.graph = args.layout == "unet-ddp" and world == 1 and not cpu and args.warmup >= 2
     if args.graph:
         if world > 1 or cpu:
             _fail(2, "--graph: whole-step graph capture is a one-rank GPU option")
