@@ -63,6 +63,20 @@ def main():
                     fn = lambda: torch.matmul(dyT, xT.t())  # noqa: E731
                 elif arm == "blaslt":
                     fn = lambda: torch.matmul(x, w.t())  # noqa: E731
+                elif arm in ("nt4", "nt4n", "nt4p", "nt4h"):   # 4-wave / 256-AGPR gemm_nt4_k, PIPE 1 / 0 / 2 / 3
+                    v = {"nt4": 5, "nt4n": 4, "nt4p": 6, "nt4h": 7}[arm]
+
+                    def fn(v=v):
+                        old = ops.gemm_nt_variant(v)
+                        y = ops.gemm_nt(x, w)
+                        ops.gemm_nt_variant(old)
+                        return y
+                    if rnd == 0:   # numerics against hipBLASLt on the same operands
+                        ref = torch.matmul(x, w.t()).float()
+                        err = ((fn().float() - ref).norm() / ref.norm()).item()
+                        print(json.dumps({"shape": name, "arm": arm, "rel_err_vs_blaslt": err}), flush=True)
+                        if not err < 1e-2:
+                            raise SystemExit(f"{arm} wrong on {name}: rel err {err}")
                 else:   # the CDNA4 NT kernel (16x16x32; the 32x32x16 form measured in round 5 was removed)
                     fn = lambda: ops.gemm_nt(x, w)  # noqa: E731
                 for _ in range(3):

@@ -18,8 +18,10 @@ def main():
     ap.add_argument("--k", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--hipblaslt", action="store_true")
+    ap.add_argument("--variant", type=int, default=0, help="plain-store GEMM form: 0 = gemm_nt_k, 6 = gemm_nt4_k")
     a = ap.parse_args()
     _lib.require()
+    torch.ops.dph.gemm_nt_variant(a.variant)
     x = torch.randn(a.m, a.k, device="cuda").to(torch.bfloat16)
     w = (0.02 * torch.randn(a.n, a.k, device="cuda")).to(torch.bfloat16)
     for _ in range(a.iters):

@@ -472,6 +472,348 @@ __global__ __launch_bounds__(NNT, 1) void gemm_nt_k(GemmNtParams p) {
   }
 }
 
+// ==================================================================================================
+// gemm_nt4_k: the STORE GEMM in hipBLASLt's workgroup shape -- 4 waves (2 M x 2 N), each owning a 128-token x 128-
+// feature wave tile in 256 ACCUMULATOR registers (one wave per SIMD, the whole 512-entry register file), so a K-step
+// reads 16 fragments for 64 MFMAs (0.25 ds_read_b128 per MFMA, 0.375 in gemm_nt_k's 128 x 64 wave tile).  hipcc
+// keeps 256 accumulators in AGPRs cleanly only when every MFMA names them as asm "+a" operands (the plain-C++ form
+// leaves hundreds of v_accvgpr moves and scratch in the loop: docs/guide/performance.md, round 2 wgrad note), so the
+// MFMAs are inline asm and the compiler only allocates.  Same K-tile images, swizzle and quarter DMA schedule as
+// gemm_nt_k (a quarter = 4 DMA instructions per lane at 256 threads); wave row-group wm owns token rows 128 wm..,
+// wave column-group wn feature rows 128 wn..; Q_B0 / Q_B1 hold the first / second 64 feature rows of each group.
+// Hazards the asm statements need (cdna_hip_programming.md §5.7 item 2): an MFMA chain on one accumulator needs no
+// wait states; the accumulators are zeroed before the prologue's DMA waits (far more than 2 states before the first
+// MFMA) and read only after an explicit 16-state pad behind the last MFMA.
+__device__ __forceinline__ void mfma_acc(f32x4& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+constexpr int N4T = 256;
+
+// PIPE = 1: every fragment a phase needs is read during the PREVIOUS phase's MFMAs (one ds_read between every 2-4
+// MFMAs), so a phase's MFMAs start on registers that are already loaded and the LDS latency hides behind the matrix
+// pipe -- with one wave per SIMD nothing else would hide it.  That needs two A register sets (A0 of tile t+1 is read
+// while phase 4 still multiplies A1 of tile t) and every quarter retired one phase earlier: the wait before phase P's
+// barrier retires what phase P's MFMA section reads (4 quarters stay in flight).  PIPE = 0: the reads before the
+// barrier of the phase that uses them (gemm_nt_k's order without the stagger).
+template <int PIPE>
+__global__ __launch_bounds__(N4T, 1) void gemm_nt4_k(GemmNtParams p) {
+  constexpr int QI = 4;                    // DMA instructions per quarter and lane
+  constexpr int VMC = 4 * QI;
+  __shared__ __attribute__((aligned(1024))) char lds[2 * BUFB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int r16 = lane & 15, kq = lane >> 4;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      asm volatile("" : "=a"(acc[i][j]) : "0"(z));
+    }
+
+  const int tiles_m = p.M / NBM, tiles_n = p.tiles_n;
+  int tm, tn;
+  nt_grouped_tile(xcd_remap(blockIdx.x, tiles_m * tiles_n), tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * NBM;
+  const int64_t n0 = (int64_t)tn * NBN;
+  const int nk = p.K / NBK;
+
+  // per-lane DMA source offsets: instruction i of a quarter copies chunk c = i * 256 + tid -> image row rho = c >> 3
+  // (operand row 128 (rho >> 6) + (rho & 63) relative to the quarter's base row), 16-B chunk kc (source-side swizzle)
+  unsigned voffA[QI], voffB[QI];
+#pragma unroll
+  for (int i = 0; i < QI; ++i) {
+    const int c = i * N4T + tid, rho = c >> 3, kc = (c & 7) ^ ((rho >> 1) & 7);
+    const int64_t row = 128 * (rho >> 6) + (rho & 63);
+    voffA[i] = (unsigned)(row * p.lda * 2 + kc * 16);
+    voffB[i] = (unsigned)(row * p.ldb * 2 + kc * 16);
+  }
+  const bf16* Ap = reinterpret_cast<const bf16*>(p.A);
+  const bf16* Bp = reinterpret_cast<const bf16*>(p.B);
+  const char* qptr[4];
+  qptr[Q_A0] = reinterpret_cast<const char*>(Ap + (int64_t)m0 * p.lda);
+  qptr[Q_A1] = reinterpret_cast<const char*>(Ap + (int64_t)(m0 + 64) * p.lda);
+  qptr[Q_B0] = reinterpret_cast<const char*>(Bp + n0 * p.ldb);
+  qptr[Q_B1] = reinterpret_cast<const char*>(Bp + (n0 + 64) * p.ldb);
+  const unsigned lds_w = lds_addr(lds + wid * 1024);
+
+  auto dma = [&](auto QIc, int kt, auto BI) {
+    constexpr int Q = decltype(QIc)::value, BUF = decltype(BI)::value;
+    const int ktc = min(kt, nk - 1);   // past the end: re-load the last tile into a slot nobody reads again
+    const char* src = uniform_ptr(qptr[Q] + (int64_t)ktc * (NBK * 2));
+    const unsigned d = lds_w + BUF * BUFB + Q * QB;
+#pragma unroll
+    for (int i = 0; i < QI; ++i) lds_dma16(src, Q < 2 ? voffA[i] : voffB[i], d + i * N4T * 16);
+  };
+  // instruction i of a quarter's DMA (PIPE 2 spreads a quarter over a phase's MFMA section)
+  auto dma1 = [&](int Q, int kt, int BUF, int i) {
+    const int ktc = min(kt, nk - 1);
+    const char* src = uniform_ptr(qptr[Q] + (int64_t)ktc * (NBK * 2));
+    lds_dma16(src, Q < 2 ? voffA[i] : voffB[i], lds_w + BUF * BUFB + Q * QB + i * N4T * 16);
+  };
+
+  // fragment reads: row r16 of a 16-row block, logical chunk 4 s + kq (image rows 64 w + 16 b + r16)
+  const int xsw = (r16 >> 1) & 7;
+  const int off_s0 = r16 * 128 + ((kq ^ xsw) << 4);
+  const int off_s1 = r16 * 128 + (((4 + kq) ^ xsw) << 4);
+  const char* a_img = lds + wm * 8192;
+  const char* b_img = lds + wn * 8192;
+  bf16x8 fa0[4][2], fa1[4][2], fb0[4][2], fb1[4][2];
+  auto read4 = [&](const char* img, auto QIc, auto BI, bf16x8 (&f)[4][2]) {
+    constexpr int Q = decltype(QIc)::value, BUF = decltype(BI)::value;
+    const char* base = img + BUF * BUFB + Q * QB;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      f[b][0] = *reinterpret_cast<const bf16x8*>(base + b * 2048 + off_s0);
+      f[b][1] = *reinterpret_cast<const bf16x8*>(base + b * 2048 + off_s1);
+    }
+  };
+  // quadrant (AH, BH): 4 token blocks x 4 feature blocks x 2 k-steps of 32 = 32 MFMAs; `rd(r)` issues the r-th of R
+  // fragment reads for the next phase, one after every 32 / R MFMAs (pinned there by scheduling fences)
+  auto mma = [&](auto AHI, auto BHI, const bf16x8 (&fA)[4][2], const bf16x8 (&fB)[4][2], auto RI, auto&& rd,
+                 auto&& dq) {
+    constexpr int AH = decltype(AHI)::value, BH = decltype(BHI)::value, R = decltype(RI)::value;
+    // 8 reads go out after MFMAs 2, 5, .., 23 (front-loaded: their latency is hidden before the phase ends); 16 reads
+    // after every other MFMA
+    constexpr int EVERY = R == 8 ? 3 : (R ? 32 / (R ? R : 1) : 64);
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      const int s = i >> 4, mb = (i >> 2) & 3, nb = i & 3;
+      mfma_acc(acc[4 * AH + mb][4 * BH + nb], fB[nb][s], fA[mb][s]);
+      if constexpr (R > 0) {
+        if (i % EVERY == EVERY - 1 && i / EVERY < R) {
+          __builtin_amdgcn_sched_barrier(0);
+          rd(i / EVERY);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (i % 8 == 4) {   // PIPE 2: one DMA instruction of the next phase's quarter every 8 MFMAs
+        __builtin_amdgcn_sched_barrier(0);
+        dq(i / 8);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  // one fragment read: r < 8 -> block r / 2, k-step r % 2 of image img (quarter Q, buffer BUF) into f
+  auto rd1 = [&](const char* img, int Q, int BUF, bf16x8 (&f)[4][2], int r) {
+    const char* base = img + BUF * BUFB + Q * QB + (r >> 1) * 2048;
+    f[r >> 1][r & 1] = *reinterpret_cast<const bf16x8*>(base + ((r & 1) ? off_s1 : off_s0));
+  };
+  auto none = [](int) {};
+  auto nodma = [](int) {};
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using IA0 = std::integral_constant<int, Q_A0>;
+  using IA1 = std::integral_constant<int, Q_A1>;
+  using IB0 = std::integral_constant<int, Q_B0>;
+  using IB1 = std::integral_constant<int, Q_B1>;
+
+  auto phase = [&](auto PI, auto CI, int kt) {
+    constexpr int P = decltype(PI)::value, CUR = decltype(CI)::value;
+    using ICUR = std::integral_constant<int, CUR>;
+    using INXT = std::integral_constant<int, CUR ^ 1>;
+    using R0 = std::integral_constant<int, 0>;
+    using R8 = std::integral_constant<int, 8>;
+    using R16 = std::integral_constant<int, 16>;
+    constexpr bool SW = CUR == 1;            // B0 of tile t lives in fb0 for even t, fb1 for odd t
+    auto& fB0 = SW ? fb1 : fb0;
+    auto& fB1 = SW ? fb0 : fb1;
+    if constexpr (!PIPE) {
+      if constexpr (P == 0) {
+        read4(b_img, IB0{}, ICUR{}, fB0);
+        read4(a_img, IA0{}, ICUR{}, fa0);
+      }
+      if constexpr (P == 1) read4(b_img, IB1{}, ICUR{}, fB1);
+      if constexpr (P == 2) read4(a_img, IA1{}, ICUR{}, fa1);
+    }
+    if constexpr (PIPE < 2) {
+      if constexpr (P == 0) dma(IB1{}, kt + 1, INXT{});
+      if constexpr (P == 1) dma(IA1{}, kt + 1, INXT{});
+      if constexpr (P == 2) dma(IA0{}, kt + 2, ICUR{});
+      if constexpr (P == 3) dma(IB0{}, kt + 2, ICUR{});
+    }
+    wait_vmcnt<VMC>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // PIPE 2: the quarter gemm_nt_k issues at the start of phase P + 1 goes out during phase P's MFMAs instead (same
+    // issue order, so the same vmcnt retires the same quarters; every overwritten region was last read >= 2 phases
+    // before and the barrier bounds the skew to one phase)
+    auto dq = [&](int i) {
+      if constexpr (PIPE == 2) {
+        if constexpr (P == 0) dma1(Q_A1, kt + 1, CUR ^ 1, i);
+        if constexpr (P == 1) dma1(Q_A0, kt + 2, CUR, i);
+        if constexpr (P == 2) dma1(Q_B0, kt + 2, CUR, i);
+        if constexpr (P == 3) dma1(Q_B1, kt + 2, CUR, i);
+      }
+    };
+    if constexpr (!PIPE) {
+      if constexpr (P == 0) mma(I0{}, I0{}, fa0, fB0, R0{}, none, nodma);
+      if constexpr (P == 1) mma(I0{}, I1{}, fa0, fB1, R0{}, none, nodma);
+      if constexpr (P == 2) mma(I1{}, I1{}, fa1, fB1, R0{}, none, nodma);
+      if constexpr (P == 3) mma(I1{}, I0{}, fa1, fB0, R0{}, none, nodma);
+    } else {
+      // P0 reads B1(t) for P1, P1 reads A1(t) for P2, P3 reads A0(t+1) and B0(t+1) (into the B set P3 leaves idle)
+      if constexpr (P == 0) mma(I0{}, I0{}, fa0, fB0, R8{}, [&](int r) { rd1(b_img, Q_B1, CUR, fB1, r); }, dq);
+      if constexpr (P == 1) mma(I0{}, I1{}, fa0, fB1, R8{}, [&](int r) { rd1(a_img, Q_A1, CUR, fa1, r); }, dq);
+      if constexpr (PIPE == 1) {
+        if constexpr (P == 2) mma(I1{}, I1{}, fa1, fB1, R0{}, none, dq);
+        if constexpr (P == 3)
+          mma(I1{}, I0{}, fa1, fB0, R16{}, [&](int r) {
+            if (r < 8) rd1(a_img, Q_A0, CUR ^ 1, fa0, r);
+            else rd1(b_img, Q_B0, CUR ^ 1, fB1, r - 8);
+          }, dq);
+      } else {   // PIPE 2: A0(t+1) is retired one phase earlier here, so P2 reads it and P3 only B0(t+1)
+        if constexpr (P == 2) mma(I1{}, I1{}, fa1, fB1, R8{}, [&](int r) { rd1(a_img, Q_A0, CUR ^ 1, fa0, r); }, dq);
+        if constexpr (P == 3) mma(I1{}, I0{}, fa1, fB0, R8{}, [&](int r) { rd1(b_img, Q_B0, CUR ^ 1, fB1, r); }, dq);
+      }
+    }
+    // One barrier per phase is enough under PIPE: every region a DMA overwrites was last read >= 3 phases earlier
+    // and one barrier bounds the skew between waves to one phase; PIPE = 0 keeps the template's second barrier
+    // (its reads sit right before the barrier of the phase that uses them).
+    if constexpr (!PIPE) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  if constexpr (PIPE == 3) {
+    // PIPE 3: two phases per K-tile (64 MFMAs each, one barrier each: half of PIPE 2's barriers).  H0 = A0 x (B0,
+    // B1), H1 = A1 x (B1, B0).  Every fragment is read during the phase before its first use (B1(t) in H0(t)'s first
+    // half, A1(t) in H0(t), A0(t+1) in H1(t), B0(t+1) in H1(t)'s second half into the B set H1's first half is done
+    // with, so the two B sets swap roles every K-tile); a phase's two DMA quarters are the ones the phase after next
+    // reads (issued two phases ahead, 2 quarters in flight at every barrier: vmcnt(8)).  Every DMA target was last
+    // read >= 2 phases before its issue and one barrier per phase bounds the skew between waves to one phase.
+    auto hphase = [&](auto HI, auto CI, int kt) {
+      constexpr int H = decltype(HI)::value, CUR = decltype(CI)::value;
+      constexpr bool SW = CUR == 1;
+      auto& fB0 = SW ? fb1 : fb0;   // B0 of tile kt
+      auto& fB1 = SW ? fb0 : fb1;   // B1 of tile kt (and B0 of tile kt + 1 after H1's first half)
+      wait_vmcnt<2 * QI>();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const int s = (i >> 4) & 1, mb = (i >> 2) & 3, nb = i & 3;
+        if constexpr (H == 0) {
+          if (i < 32) mfma_acc(acc[mb][nb], fB0[nb][s], fa0[mb][s]);
+          else mfma_acc(acc[mb][4 + nb], fB1[nb][s], fa0[mb][s]);
+        } else {
+          if (i < 32) mfma_acc(acc[4 + mb][4 + nb], fB1[nb][s], fa1[mb][s]);
+          else mfma_acc(acc[4 + mb][nb], fB0[nb][s], fa1[mb][s]);
+        }
+        if (i % 2 == 0 && i < 48 && (i < 16 || i >= 32 || H == 0)) {
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (H == 0) {   // B1(t) first (used by this phase's second half), then A1(t)
+            if (i < 16) rd1(b_img, Q_B1, CUR, fB1, i / 2);
+            else if (i < 32) rd1(a_img, Q_A1, CUR, fa1, (i - 16) / 2);
+          } else {                  // A0(t+1), then B0(t+1) once the first half no longer reads fB1
+            if (i < 16) rd1(a_img, Q_A0, CUR ^ 1, fa0, i / 2);
+            else if (i >= 32) rd1(b_img, Q_B0, CUR ^ 1, fB1, (i - 32) / 2);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (i % 8 == 5) {   // 2 quarters = 8 DMA instructions per phase (front-loading them measured 0.6 % slower)
+          __builtin_amdgcn_sched_barrier(0);
+          const int j = i / 8;
+          if constexpr (H == 0) dma1(j < 4 ? Q_A1 : Q_B1, kt + 1, CUR ^ 1, j & 3);
+          else dma1(j < 4 ? Q_A0 : Q_B0, kt + 2, CUR, j & 3);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    };
+    // prologue: A0(0) B0(0) A1(0) B1(0) A0(1) B0(1); tile 0's A0 / B0 into registers
+    dma(IA0{}, 0, I0{});
+    dma(IB0{}, 0, I0{});
+    dma(IA1{}, 0, I0{});
+    dma(IB1{}, 0, I0{});
+    dma(IA0{}, 1, I1{});
+    dma(IB0{}, 1, I1{});
+    wait_vmcnt<4 * QI>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    read4(a_img, IA0{}, I0{}, fa0);
+    read4(b_img, IB0{}, I0{}, fb0);
+    __builtin_amdgcn_sched_barrier(0);
+    int kt = 0;
+    for (; kt + 2 <= nk; kt += 2) {
+      hphase(I0{}, I0{}, kt);
+      hphase(I1{}, I0{}, kt);
+      hphase(I0{}, I1{}, kt + 1);
+      hphase(I1{}, I1{}, kt + 1);
+    }
+    if (kt < nk) {
+      hphase(I0{}, I0{}, kt);
+      hphase(I1{}, I0{}, kt);
+    }
+  } else {
+    // prologue: Q_A0(0) Q_B0(0) Q_B1(0) Q_A1(0) Q_A0(1) Q_B0(1)
+    dma(IA0{}, 0, I0{});
+    dma(IB0{}, 0, I0{});
+    dma(IB1{}, 0, I0{});
+    dma(IA1{}, 0, I0{});
+    dma(IA0{}, 1, I1{});
+    dma(IB0{}, 1, I1{});
+    wait_vmcnt<4 * QI>();   // Q_A0(0), Q_B0(0) landed
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    if constexpr (PIPE) {   // tile 0's A0 / B0, as phase 4 of tile -1 would have read them
+      read4(a_img, IA0{}, I0{}, fa0);
+      read4(b_img, IB0{}, I0{}, fb0);
+    }
+    if constexpr (PIPE == 2) dma(IB1{}, 1, I1{});   // the quarter phase 4 of tile -1 would have issued
+    __builtin_amdgcn_sched_barrier(0);
+
+    int kt = 0;
+    for (; kt + 2 <= nk; kt += 2) {
+      phase(I0{}, I0{}, kt);
+      phase(I1{}, I0{}, kt);
+      phase(std::integral_constant<int, 2>{}, I0{}, kt);
+      phase(std::integral_constant<int, 3>{}, I0{}, kt);
+      phase(I0{}, I1{}, kt + 1);
+      phase(I1{}, I1{}, kt + 1);
+      phase(std::integral_constant<int, 2>{}, I1{}, kt + 1);
+      phase(std::integral_constant<int, 3>{}, I1{}, kt + 1);
+    }
+    if (kt < nk) {
+      phase(I0{}, I0{}, kt);
+      phase(I1{}, I0{}, kt);
+      phase(std::integral_constant<int, 2>{}, I0{}, kt);
+      phase(std::integral_constant<int, 3>{}, I0{}, kt);
+    }
+  }
+  wait_vmcnt<0>();                                  // the clamped tail DMAs land before the images are reused
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // MFMA results -> accumulator reads
+  __syncthreads();
+
+  // epilogue through LDS: acc[mb][nb][j] = C[token m0 + 128 wm + 16 mb + r16][feature n0 + 128 wn + 16 nb + 4 kq + j]
+  // rounded to bf16 into a 256 x 256 image (16-B chunks XOR-swizzled by the row), then whole 16-B row segments
+#pragma unroll
+  for (int mb = 0; mb < 8; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 8; ++nb) {
+      const int row = 128 * wm + 16 * mb + r16, col = 128 * wn + 16 * nb + 4 * kq;
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = (bf16)acc[mb][nb][j];
+      *reinterpret_cast<bf16x4*>(lds + row * 512 + (((col >> 3) ^ (row & 15)) << 4) + (col & 7) * 2) = o;
+    }
+  __syncthreads();
+  const int c = tid & 31;
+  bf16* C = (bf16*)p.C;
+#pragma unroll 4
+  for (int k = 0; k < 32; ++k) {
+    const int row = (tid >> 5) + 8 * k;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + row * 512 + ((c ^ (row & 15)) << 4));
+    *reinterpret_cast<bf16x8*>(C + (int64_t)(m0 + row) * p.ldc + n0 + c * 8) = v;
+  }
+}
+
 // Rejected in round 5 (profiles/r5/nt16_slots/): STORE mode on the weight-gradient kernel's lockstep slot pipeline
 // (32-k slots in a 5-region ring, DMA three slots ahead, one ds_read_b128 per fragment): 1221-1275 TFLOP/s against
 // 1482-1515 for this kernel and 1439-1601 for hipBLASLt on the 7B shapes -- a 32-k slot of a K-contiguous operand is a
@@ -493,11 +835,26 @@ bool gemm_nt_ragged(int mode, int64_t N, int64_t K) {
   return K % NBK != 0 || (mode == kNtSwiglu ? N % 128 : N % NBN) != 0;
 }
 
+// A/B of the plain-store GEMM forms (gemm_nt_variant op): 0 = gemm_nt_k (8 waves), 4 / 5 / 6 / 7 = gemm_nt4_k (PIPE 0 / 1 / 2 / 3)
+static int g_nt_variant = 0;
+int gemm_nt_set_variant(int v) {
+  const int old = g_nt_variant;
+  g_nt_variant = v;
+  return old;
+}
+
 void gemm_nt(int mode, const GemmNtParams& prm, hipStream_t st) {
   GemmNtParams p = prm;
   p.tiles_n = mode == kNtSwiglu ? (p.N + 127) / 128 : (p.N + NBN - 1) / NBN;
   const dim3 grid((unsigned)((p.M / NBM) * p.tiles_n)), block(NNT);
   const bool rag = gemm_nt_ragged(mode, p.N, p.K);
+  if (mode == kNtStore && !rag && g_nt_variant >= 4 && g_nt_variant <= 7) {
+    if (g_nt_variant == 4) hipLaunchKernelGGL((gemm_nt4_k<0>), grid, dim3(N4T), 0, st, p);
+    else if (g_nt_variant == 5) hipLaunchKernelGGL((gemm_nt4_k<1>), grid, dim3(N4T), 0, st, p);
+    else if (g_nt_variant == 6) hipLaunchKernelGGL((gemm_nt4_k<2>), grid, dim3(N4T), 0, st, p);
+    else hipLaunchKernelGGL((gemm_nt4_k<3>), grid, dim3(N4T), 0, st, p);
+    return;
+  }
 #define DPH_NT_LAUNCH(MD)                                                                    \
   do {                                                                                       \
     if (rag) hipLaunchKernelGGL((gemm_nt_k<MD, 1, true, true>), grid, block, 0, st, p);      \

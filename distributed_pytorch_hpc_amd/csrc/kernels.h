@@ -142,6 +142,7 @@ struct GemmNtParams {
 bool gemm_nt_supported(int mode, int64_t M, int64_t N, int64_t K);
 bool gemm_nt_ragged(int mode, int64_t N, int64_t K);
 void gemm_nt(int mode, const GemmNtParams& p, hipStream_t stream);
+int gemm_nt_set_variant(int v);   // plain-store GEMM form (A/B): 0 = 8-wave gemm_nt_k, 4 / 5 = 4-wave gemm_nt4_k
 // pipeline variant: bit 0 = lookahead B0 reads (8/4/8/0 fragment reads per phase instead of 12/4/8/0), bit 1 = the
 // v_mfma_f32_32x32x16_bf16 kernel (gemm_nt32_k) instead of 16x16x32 (gemm_nt_k); both take ragged shapes.
 

@@ -1275,6 +1275,7 @@ void car_poison_op(int64_t ctx, const Tensor& flag, Tensor& gscale) {
 }
 int64_t car_agreed_op(int64_t ctx) { return dph::car_agreed(ctx); }
 int64_t attn_variant_op(int64_t v) { return dph::attn_set_variant((int)v); }
+int64_t gemm_nt_variant_op(int64_t v) { return dph::gemm_nt_set_variant((int)v); }
 void car_destroy_op(int64_t ctx) { dph::car_destroy(ctx); }
 
 }  // namespace
@@ -1537,6 +1538,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("car_status(int ctx) -> int", &car_status_op);
   m.def("car_agreed(int ctx) -> int", &car_agreed_op);
   m.def("attn_variant(int v) -> int", &attn_variant_op);
+  m.def("gemm_nt_variant(int v) -> int", &gemm_nt_variant_op);
   m.def("car_flag(int ctx, Tensor(a!) flag) -> ()");
   m.def("car_poison(int ctx, Tensor flag, Tensor(a!) gscale) -> ()");
   m.def("car_destroy(int ctx) -> ()", &car_destroy_op);

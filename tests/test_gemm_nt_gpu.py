@@ -202,3 +202,25 @@ def test_gemm_nt_ragged_rope(dph_native, S, hd, heads, K):
     a, b = rot[..., 0], rot[..., 1]
     rot = torch.stack([a * c - b * s, a * s + b * c], -1).reshape(B * S, -1)
     assert rel_err(y, torch.cat([rot, ref[:, 2 * heads * hd:]], 1)) < 5e-3
+
+@pytest.mark.parametrize("variant", [4, 5, 6, 7])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 192), (768, 512, 320), (256, 1024, 4096),
+                                   (2048, 256, 128), (1024, 512, 64 * 7)])
+def test_gemm_nt4_store(dph_native, variant, M, N, K):
+    """The 4-wave / 256-AGPR plain GEMM (gemm_nt4_k, every PIPE form): against the fp32 reference, bitwise equal to
+    the 8-wave kernel, odd and even K-tile counts, and the identity check for the row / column map."""
+    a, b = _rnd(M, K, seed=1), _rnd(N, K, seed=2)
+    ref8 = dph_native.gemm_nt(a, b)
+    old = dph_native.gemm_nt_variant(variant)
+    try:
+        c = dph_native.gemm_nt(a, b)
+        eye = torch.eye(256, 256, device=DEV, dtype=torch.bfloat16)
+        asym = (torch.arange(256 * 256, device=DEV) % 251).reshape(256, 256).to(torch.bfloat16)
+        ci = dph_native.gemm_nt(eye, asym)
+    finally:
+        dph_native.gemm_nt_variant(old)
+    ref = a.float() @ b.float().t()
+    assert rel_err(c, ref) < 5e-3
+    assert ((c.float() - ref).abs() <= 1e-2 * ref.abs() + 2e-2 * ref.abs().mean()).all()
+    assert torch.equal(c, ref8)
+    assert torch.equal(ci, asym.t().contiguous())
