@@ -7,6 +7,7 @@
 // 8-channel chunks exactly.  Passes over the activation (A = its size):
 //   forward : stats (read x)  +  apply (read x [+ residual], write y)            = 3A (+A)
 //   backward: reduce (read dy, y, x) + dx (read dy, y, x, write dx [+ dres])      = 7A (+A)
+//             (the reduce pass disappears when the convolution that produced dy ran it in its epilogue: pre_part)
 //             ReLU without residual: the mask [x * scale + shift > 0] is recomputed from x with the forward's
 //             own fp32 scale / shift (bit-identical to y > 0), so y is not read:  5A
 //             ReLU with residual: the forward's apply pass also writes the mask [y > 0] as one BIT per element
@@ -497,17 +498,22 @@ void bn_apply(const void* x, const void* res, const float* scale, const float* s
 
 void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
             void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dt,
-            int pdt, hipStream_t st, const float* xmask_ss, const uint8_t* relu_mask) {
+            int pdt, hipStream_t st, const float* xmask_ss, const uint8_t* relu_mask, const float* pre_part,
+            int pre_groups) {
   const bool bm = relu && relu_mask != nullptr;
   const bool xm = relu && !bm && xmask_ss != nullptr;
   int64_t rpb;
-  const int G = stats_grid(M, (int)C, &rpb);
-  float* part = workspace;                       // [G][2C]
+  int G = stats_grid(M, (int)C, &rpb);
+  const float* part = workspace;                 // [G][2C]
   float* coef = workspace + 2 * (int64_t)G * C;  // [3C]
   const size_t shs = 2 * BN_NT * 8 * sizeof(float);
+  if (pre_part != nullptr) {   // reduced by the input-gradient epilogue that produced dy (kernels.h BnRed)
+    part = pre_part;
+    G = pre_groups;
+  } else {
 #define DPH_BN_RED(R_, X_, B_)                                                                                     \
   hipLaunchKernelGGL((bn_bwd_reduce_k<T, R_, X_, B_>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy, (const T*)y,  \
-                     (const T*)x, mean, invstd, xmask_ss, part, M, (int)C, rpb, relu_mask)
+                     (const T*)x, mean, invstd, xmask_ss, workspace, M, (int)C, rpb, relu_mask)
   DPH_DISPATCH_FLOAT(dt, T, {
     if (bm) DPH_BN_RED(true, false, true);
     else if (xm) DPH_BN_RED(true, true, false);
@@ -515,6 +521,7 @@ void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, con
     else DPH_BN_RED(false, false, false);
   });
 #undef DPH_BN_RED
+  }
   const dim3 fg((unsigned)(C / 8));
   if (pdt == kBF16)
     hipLaunchKernelGGL((bn_bwd_finalize_k<bf16>), fg, dim3(FIN_NT), 0, st, part, G, (int)C, (float)M, (const bf16*)w,

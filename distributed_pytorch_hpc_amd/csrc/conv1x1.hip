@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "bn_epilogue.h"
 #include "dph_common.h"
 #include "kernels.h"
 
@@ -58,13 +59,22 @@ constexpr int TS_KF = TS_BK / 16;   // MFMA k-steps (A fragments) per K-step
 // ResNet-50's 392-row-block layers (14 x 14 at B = 256) then launch 784 workgroups for 768 slots -- a second round for
 // 16 of them (benchmarks/probes/grid_tail.py: +23 % time for +2 % rows there, profiles/r4/grid_tail/).
 // MINB = 4 forces the 128-VGPR build (MINB = 1, the compiler's own budget, measured slower: profiles/r4/grid_tail/).
-template <int BN, bool C3, bool ADD = false, bool STATS = false, bool PRO = false, int ADDS = 0, int MINB = 4>
+// BRED = 1 | 2 (input gradient of a BatchNorm + ReLU output, 1x1 only): the BatchNorm backward's reduction over the
+// stored gradient (kernels.h BnRed, bn_epilogue.h) -- mask from x (1) or from the forward's bits (2).
+// AMASK (with ADD, ADDS = 0): D enters as D * mask, mask = dmask bits (one byte per 8-channel vector of [M, N]) -- the
+// residual gradient of a BatchNorm + residual + ReLU is its output gradient under the ReLU mask, so that BatchNorm's
+// backward hands over dy and its forward's bits instead of writing the masked copy.
+template <int BN, bool C3, bool ADD = false, bool STATS = false, bool PRO = false, int ADDS = 0, int MINB = 4,
+          int BRED = 0, bool AMASK = false>
 __global__ __launch_bounds__(TS_NT, PRO ? 1 : MINB) void ts_nt_k(const bf16* __restrict__ A, const bf16* __restrict__ B,
                                                  bf16* __restrict__ C, int M, int N, int K, int64_t lda,
                                                  int64_t ldb, int64_t ldc, int H, int W, int Cin,
                                                  const bf16* __restrict__ D = nullptr,
                                                  float* __restrict__ stats = nullptr,
-                                                 const float* __restrict__ pro_ss = nullptr) {
+                                                 const float* __restrict__ pro_ss = nullptr, BnRed bnr = {},
+                                                 const uint8_t* __restrict__ dmask = nullptr) {
+  static_assert(!BRED || (!C3 && !STATS && !PRO), "BRED: 1x1 input-gradient forms only");
+  static_assert(!AMASK || (ADD && ADDS == 0), "AMASK: the masked residual-gradient add");
   constexpr int NT = BN / 32;                        // 32-column tiles per wave
   constexpr int BCH = BN * (TS_BK / 8) / TS_NT;      // 16-B B chunks per thread per K-step (BN=128: 4)
   constexpr int CROW = BN + 8;                       // epilogue LDS row (bf16)
@@ -183,11 +193,40 @@ __global__ __launch_bounds__(TS_NT, PRO ? 1 : MINB) void ts_nt_k(const bf16* __r
 #pragma unroll
     for (int r = 0; r < 16; ++r)
       Cs[(wid * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CROW + t * 32 + l32] = (bf16)acc[t][r];
-  __syncthreads();
   constexpr int CPR = BN / 8;   // 16-B chunks per row
+  constexpr int NIT = TS_BM * CPR / TS_NT;   // store iterations per thread (its chunk column is fixed)
+  // HBM operands of the store loop (the residual-gradient add, the BatchNorm input and its mask bits) are fetched PF
+  // iterations ahead, the first PF before the barrier: one exposed load latency per tile instead of one per iteration
+  constexpr bool PDA = ADD && ADDS == 0;
+  constexpr int PF = (PDA || BRED != 0) ? (NIT < 4 ? NIT : 4) : 1;
+  using BRA = BnRedAcc<BRED ? BRED : 1>;
+  [[maybe_unused]] bf16x8 dq[PF], xq[PF];
+  [[maybe_unused]] unsigned mq[PF], aq[PF];
+  auto fetch = [&](int it, int sl) {
+    const int i = threadIdx.x + it * TS_NT, ch = i % CPR;
+    const int64_t r = min(m0 + i / CPR, M - 1);
+    if constexpr (PDA) dq[sl] = *reinterpret_cast<const bf16x8*>(D + r * ldc + nt0 + ch * 8);
+    if constexpr (AMASK) aq[sl] = dmask[r * (N >> 3) + (nt0 >> 3) + ch];
+    if constexpr (BRED != 0) {
+      xq[sl] = BRA::load_x(bnr, r, N, nt0 + ch * 8);
+      mq[sl] = BRA::load_m(bnr, r, N, nt0 + ch * 8);
+    }
+  };
+  if constexpr (PDA || BRED != 0) {
 #pragma unroll
-  for (int i = threadIdx.x; i < TS_BM * CPR; i += TS_NT) {
-    const int row = i / CPR, ch = i % CPR;
+    for (int it = 0; it < PF; ++it) fetch(it, it);
+  }
+  __syncthreads();
+  [[maybe_unused]] BRA bra;
+  if constexpr (BRED != 0) bra.init(bnr, nt0 + (threadIdx.x % CPR) * 8, N);
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = threadIdx.x + it * TS_NT, row = i / CPR, ch = i % CPR, sl = it % PF;
+    [[maybe_unused]] const bf16x8 dv = dq[sl], xv = xq[sl];
+    [[maybe_unused]] const unsigned mv = mq[sl], av = aq[sl];
+    if constexpr (PDA || BRED != 0) {
+      if (it + PF < NIT) fetch(it + PF, sl);
+    }
     if (m0 + row < M) {
       const int64_t o = (int64_t)(m0 + row) * ldc + nt0 + ch * 8;
       bf16x8 v = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
@@ -200,13 +239,20 @@ __global__ __launch_bounds__(TS_NT, PRO ? 1 : MINB) void ts_nt_k(const bf16* __r
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)d[j]);
         }
-      } else if constexpr (ADD) {
-        const bf16x8 d = *reinterpret_cast<const bf16x8*>(D + o);
+      } else if constexpr (AMASK) {   // bitwise the unmasked add of a materialised bf16(dy * mask)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)d[j]);
+        for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (((av >> j) & 1u) ? (float)dv[j] : 0.f));
+      } else if constexpr (ADD) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)v[j] + (float)dv[j]);
       }
       *reinterpret_cast<bf16x8*>(C + o) = v;
+      if constexpr (BRED != 0) bra.add(xv, mv, v);
     }
+  }
+  if constexpr (BRED != 0) {
+    __syncthreads();   // every C-tile read is done: the tile's LDS holds the cross-wave partials
+    bra.finish(reinterpret_cast<float*>(smem), CPR, TS_NT / 64, mb, N, nt0, bnr.part);
   }
   if constexpr (STATS) {
     // from the accumulator registers (rounded to bf16, the values BN will read): register r of tile t is row
@@ -707,6 +753,38 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     else DPH_TS_NT(64, false);
   }
 #undef DPH_TS_NT
+}
+
+void ts_gemm_nt_bnred(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                      int64_t ldb, int64_t ldc, int H, int W, const void* D, int adds, const BnRed& r,
+                      hipStream_t st, const uint8_t* dmask) {
+  if (H > 0 && adds == 0) {   // 3x3 stride-1 input gradient on the LDS-DMA kernel
+    conv3_gemm_bnred(A, B, C, M, N, K, lda, ldb, ldc, H, W, r, st);
+    return;
+  }
+  const int nmb = (int)cdiv(M, TS_BM);
+  const bool wide = N % 128 == 0;
+#define DPH_TS_BR(BN_, ADD_, ADDS_, MODE_, AM_)                                                                    \
+  hipLaunchKernelGGL((ts_nt_k<BN_, false, ADD_, false, false, ADDS_, 4, MODE_, AM_>), dim3(nmb * (int)(N / BN_)),   \
+                     dim3(TS_NT), 0, st, (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, \
+                     ldc, H, W, 0, (const bf16*)D, nullptr, nullptr, r, dmask)
+#define DPH_TS_BR_W(ADD_, ADDS_, MODE_, AM_)         \
+  if (wide) DPH_TS_BR(128, ADD_, ADDS_, MODE_, AM_); \
+  else DPH_TS_BR(64, ADD_, ADDS_, MODE_, AM_)
+  const bool bits = r.bits != nullptr;
+  if (dmask != nullptr) {   // masked residual-gradient add; r.part == nullptr: no BatchNorm reduction
+    if (r.part == nullptr) { DPH_TS_BR_W(true, 0, 0, true); }
+    else if (bits) { DPH_TS_BR_W(true, 0, 2, true); }
+    else { DPH_TS_BR_W(true, 0, 1, true); }
+  } else if (adds == 2) {
+    if (bits) { DPH_TS_BR_W(true, 2, 2, false); } else { DPH_TS_BR_W(true, 2, 1, false); }
+  } else if (D != nullptr) {
+    if (bits) { DPH_TS_BR_W(true, 0, 2, false); } else { DPH_TS_BR_W(true, 0, 1, false); }
+  } else {
+    if (bits) { DPH_TS_BR_W(false, 0, 2, false); } else { DPH_TS_BR_W(false, 0, 1, false); }
+  }
+#undef DPH_TS_BR_W
+#undef DPH_TS_BR
 }
 
 void ts_gemm_nt_add_sub(const void* A, const void* B, void* C, const void* D, int64_t M, int64_t N, int64_t K,

@@ -22,6 +22,7 @@
 //   * one raw s_barrier per K-step, counted vmcnt: STAGES - 1 K-steps stay in flight behind the MFMAs;
 //   * C tile through LDS, written as whole 16-B row segments; workgroups remapped XCD-aware with the N-tiles of one
 //     row block adjacent (they read the same shifted input rows from one L2); epilogues: + bias, BN statistics.
+#include "bn_epilogue.h"
 #include "dph_common.h"
 #include "kernels.h"
 
@@ -53,14 +54,17 @@ __device__ __forceinline__ int c3_off(int r, int c) { return r * C3_ROWB + ((c ^
 // t = 8 ks + c of g.ntaps, source row (base + (t / g.tdx[0]) Ws + t % g.tdx[0]) of an [src_rows, 8] operand (pairs of
 // 4-channel pixels of a zero-padded image, so no bounds checks); taps past ntaps read tap ntaps - 1 (zero weights).
 // GEN = 0 is the stride-1 3x3 path (H, W, the fixed 3x3 taps, identity stores).
-template <int BN, int STAGES, int WM, bool STATS = false, int GEN = 0>
+// BRED = 1 | 2 (GEN = 0, WM = 2: one partial row per 128-row tile): the input gradient of a BatchNorm + ReLU output
+// also emits the BatchNorm backward's reduction partials (kernels.h BnRed, bn_epilogue.h).
+template <int BN, int STAGES, int WM, bool STATS = false, int GEN = 0, int BRED = 0>
 __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16* __restrict__ X,
                                                                    const bf16* __restrict__ B, bf16* __restrict__ C,
                                                                    int M, int N, int K, int64_t ldx, int64_t ldb,
                                                                    int64_t ldc, int H, int W, int Cin,
                                                                    float* __restrict__ stats,
                                                                    const void* __restrict__ bias, ConvGeo g,
-                                                                   bool bias_bf16) {
+                                                                   bool bias_bf16, BnRed bnr) {
+  static_assert(!BRED || (GEN == 0 && WM == 2 && !STATS), "BRED: stride-1 128-row tiles, no statistics");
   constexpr int NWV = 2 * WM, NTH = 64 * NWV, BM = 64 * WM;
   constexpr int AIMG = BM * C3_ROWB, BIMG = BN * C3_ROWB, STG = AIMG + BIMG;
   constexpr int AI = BM / 8 / NWV;         // A DMA pieces (8 rows) per wave per K-step (4)
@@ -170,6 +174,25 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16*
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // BRED: the BatchNorm input / mask bits at the tile's output positions are loaded into registers before the K-loop
+  // (their values do not depend on it), so the epilogue never waits on HBM for them -- fetched at the epilogue instead,
+  // one exposed load latency per tile cost the 56 x 56 layers ~2x the bytes' share (benchmarks/probes/bn_epi_probe.py)
+  constexpr int CPR = BN / 8;
+  constexpr int NIT = BM * CPR / NTH;   // store iterations per thread (its chunk column is fixed)
+  constexpr int PF = BRED != 0 ? NIT : 1;
+  using BRA = BnRedAcc<BRED ? BRED : 1>;
+  [[maybe_unused]] bf16x8 xq[PF];
+  [[maybe_unused]] unsigned mq[PF];
+  if constexpr (BRED != 0) {
+#pragma unroll
+    for (int it = 0; it < PF; ++it) {
+      const int i = threadIdx.x + it * NTH, ch = i % CPR;
+      const int64_t r = min(m0 + i / CPR, M - 1);
+      xq[it] = BRA::load_x(bnr, r, N, n0 + ch * 8);
+      mq[it] = BRA::load_m(bnr, r, N, n0 + ch * 8);
+    }
+  }
+
   const int nks = K / C3_BK;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -223,17 +246,27 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16*
       for (int r = 0; r < 16; ++r)
         Cs[(wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * CROW + wn * WN + j * 32 + l32] = (bf16)acc[i][j][r];
   __syncthreads();
-  constexpr int CPR = BN / 8;
-  for (int i = threadIdx.x; i < BM * CPR; i += NTH) {
-    const int row = i / CPR, ch = i % CPR;
+  [[maybe_unused]] BRA bra;
+  if constexpr (BRED != 0) bra.init(bnr, n0 + (threadIdx.x % CPR) * 8, N);
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = threadIdx.x + it * NTH, row = i / CPR, ch = i % CPR, sl = it % PF;
+    [[maybe_unused]] const bf16x8 xv = xq[sl];
+    [[maybe_unused]] const unsigned mv = mq[sl];
     if (m0 + row < M) {
       int64_t drow = m0 + row;
       if constexpr (GEN) {
         const int m = m0 + row, hw = g.Ho * g.Wo, n = m / hw, rem = m - n * hw, oy = rem / g.Wo, ox = rem - oy * g.Wo;
         drow = ((int64_t)n * g.Hd + g.ty * oy + g.tby) * g.Wd + g.tx * ox + g.tbx;
       }
-      *reinterpret_cast<bf16x8*>(C + drow * ldc + n0 + ch * 8) = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(Cs + row * CROW + ch * 8);
+      *reinterpret_cast<bf16x8*>(C + drow * ldc + n0 + ch * 8) = v;
+      if constexpr (BRED != 0) bra.add(xv, mv, v);
     }
+  }
+  if constexpr (BRED != 0) {
+    __syncthreads();   // every C-tile read is done: the tile's LDS holds the cross-wave partials
+    bra.finish(reinterpret_cast<float*>(smem), CPR, NWV, mb, N, n0, bnr.part);
   }
   if constexpr (STATS) {
     // per 128-row block g (waves 2g, 2g+1): pass 1 column sums, pass 2 squared deviations from the block mean, of the
@@ -310,7 +343,7 @@ void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 #define DPH_C3(BN_, ST_, WM_, STATS_)                                                                            \
   hipLaunchKernelGGL((conv3_k<BN_, ST_, WM_, STATS_>), dim3(nmb * (int)(N / BN_)), dim3(128 * WM_), 0, st,    \
                      (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin,  \
-                     stats, bias, ConvGeo{}, bias_bf16)
+                     stats, bias, ConvGeo{}, bias_bf16, BnRed{})
   if (wm == 4) {
     if (stats) {
       if (wide) DPH_C3(128, 3, 4, true);
@@ -327,6 +360,26 @@ void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     else DPH_C3(64, 3, 2, false);
   }
 #undef DPH_C3
+}
+
+void conv3_gemm_bnred(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                      int64_t ldb, int64_t ldc, int H, int W, const BnRed& r, hipStream_t st) {
+  // conv3_gemm's tile choice at WM = 2 (its only one for these shapes): 128-row tiles = the partial rows
+  const int cin = (int)(K / 9);
+  const int nmb = (int)cdiv(M, 128);
+  const bool wide = N % 128 == 0 && (int64_t)nmb * (N / 128) >= 384;
+#define DPH_C3B(BN_, ST_, MODE_)                                                                                  \
+  hipLaunchKernelGGL((conv3_k<BN_, ST_, 2, false, 0, MODE_>), dim3(nmb * (int)(N / BN_)), dim3(256), 0, st,      \
+                     (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin,  \
+                     nullptr, nullptr, ConvGeo{}, false, r)
+  if (r.bits != nullptr) {
+    if (wide) DPH_C3B(128, 2, 2);
+    else DPH_C3B(64, 3, 2);
+  } else {
+    if (wide) DPH_C3B(128, 2, 1);
+    else DPH_C3B(64, 3, 1);
+  }
+#undef DPH_C3B
 }
 
 bool convg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g, bool chunk_taps) {
@@ -349,7 +402,7 @@ void convg_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 #define DPH_CG(BN_, ST_, STATS_, G_)                                                                              \
   hipLaunchKernelGGL((conv3_k<BN_, ST_, 2, STATS_, G_>), dim3(nmb * (int)(N / BN_)), dim3(256), 0, st,          \
                      (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, 0, 0, cin,   \
-                     stats, bias, g, bias_bf16)
+                     stats, bias, g, bias_bf16, BnRed{})
   if (chunk_taps) {   // the RGB stem: 64 output channels
     if (stats) DPH_CG(64, 3, true, 2);
     else DPH_CG(64, 3, false, 2);

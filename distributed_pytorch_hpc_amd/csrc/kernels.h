@@ -160,6 +160,29 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 // the H x W grid (a strided 1x1 downsample's input gradient merged into the block's conv1 dgrad; s must be 2).
 void ts_gemm_nt_add_sub(const void* A, const void* B, void* C, const void* D, int64_t M, int64_t N, int64_t K,
                         int64_t lda, int64_t ldb, int64_t ldc, int H, int W, int s, hipStream_t stream);
+// BatchNorm backward reduction folded into the input-gradient epilogue that produces the BatchNorm's dy (the consumer
+// convolution's dgrad): for 128-row block g of the bf16 output C [M, N] and column c,
+//   part[g * 2N + c] = sum dz,   part[g * 2N + N + c] = sum dz * (x - mean) * invstd,   dz = C * [ReLU mask],
+// the layout bn_bwd takes as pre_part (its reduction pass over dy, x and the mask is then skipped).  The mask comes
+// from x * scale + shift (ss = the forward's fp32 [scale N | shift N]) or from the forward's bits (one byte per
+// 8-channel vector); x is the BatchNorm's bf16 input with C's layout (leading dimension N).
+struct BnRed {
+  const void* x = nullptr;
+  const float* mean = nullptr;
+  const float* invstd = nullptr;
+  const float* ss = nullptr;
+  const uint8_t* bits = nullptr;
+  float* part = nullptr;
+};
+// C = A B^T [+ D] with the BnRed epilogue: 1x1 (H = W = 0; D the residual gradient [M, N], or with adds = 2 the
+// stride-2 sub-image gradient of ts_gemm_nt_add_sub over an H x W grid) or the 3x3 stride-1 LDS-DMA kernel (H, W > 0,
+// no D).  part must hold cdiv(M, 128) * 2N floats.  dmask (1x1, D [M, N], adds = 0): D is added under these mask bits
+// (one byte per 8-channel vector); then r.part == nullptr means no reduction (the masked add alone).
+void ts_gemm_nt_bnred(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                      int64_t ldb, int64_t ldc, int H, int W, const void* D, int adds, const BnRed& r,
+                      hipStream_t stream, const uint8_t* dmask = nullptr);
+void conv3_gemm_bnred(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
+                      int64_t ldb, int64_t ldc, int H, int W, const BnRed& r, hipStream_t stream);
 // 3x3 implicit GEMM with an LDS-DMA pipeline (csrc/conv3x3.hip); ts_gemm_nt's H, W > 0 path when supported.
 bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
@@ -219,10 +242,11 @@ void bn_apply(const void* x, const void* res, const float* scale, const float* s
               bool relu, int dtype, hipStream_t stream, uint8_t* relu_mask = nullptr);
 // xmask_ss (optional, fp32 [scale | shift] of the forward): ReLU mask from x instead of reading y.
 // relu_mask (optional): the forward's bit mask instead of y (takes precedence over xmask_ss).
+// pre_part (optional): the reduction partials [pre_groups][2C] from the producer's epilogue (BnRed): no reduction pass.
 void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
             void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dtype,
             int param_dtype, hipStream_t stream, const float* xmask_ss = nullptr,
-            const uint8_t* relu_mask = nullptr);
+            const uint8_t* relu_mask = nullptr, const float* pre_part = nullptr, int pre_groups = 0);
 
 // Stride-2 max pooling, channels-last [N, H, W, C] (C % 8 == 0), csrc/pool.hip: k = 3 (padding 1) or 2 (padding 0),
 // floor mode.  tap: one byte per output element, the window position (0..k*k-1) of the max; the backward gathers

@@ -713,6 +713,107 @@ Tensor ts_gemm_nt_add_sub(const Tensor& A, const Tensor& B, const Tensor& add, i
   return C;
 }
 
+// Input gradient C = A B^T [+ add] of a convolution whose input is a training-mode BatchNorm + ReLU output, with the
+// BatchNorm backward's reduction over C in the epilogue (kernels.h BnRed): returns C and the partials
+// [cdiv(M, 128), 2N] that bn_act_bwd takes as pre_part.  H, W > 0 and sub = 0: 3x3 stride-1 (A = dY, B = the flipped
+// weight [N, 9 * Cout]); sub = 2: add is a stride-2 sub-image gradient over the H x W grid (ts_gemm_nt_add_sub);
+// otherwise 1x1 with an optional [M, N] add.  x: the BatchNorm's input ([M, N] rows, channels-last); the ReLU mask
+// comes from ss (fp32 [scale N | shift N]) or from bits (the forward's uint8 [M * N / 8]).
+std::tuple<Tensor, Tensor> ts_gemm_nt_bnred(const Tensor& A, const Tensor& B, int64_t H, int64_t W,
+                                            const c10::optional<Tensor>& add, int64_t sub, const Tensor& x,
+                                            const Tensor& mean, const Tensor& invstd, const c10::optional<Tensor>& ss,
+                                            const c10::optional<Tensor>& bits,
+                                            const c10::optional<Tensor>& add_mask) {
+  check_cuda(A, "A");
+  c10::DeviceGuard g(A.device());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
+              "ts_gemm_nt_bnred: bf16 2-D operands");
+  TORCH_CHECK(sub == 0 || sub == 2, "ts_gemm_nt_bnred: sub must be 0 or 2");
+  const bool c3 = H > 0 && sub == 0;
+  const int64_t M = A.size(0), N = B.size(0), K = c3 ? 9 * A.size(1) : A.size(1);
+  TORCH_CHECK(B.size(1) == K && (H == 0 || (W > 0 && M % (H * W) == 0)), "ts_gemm_nt_bnred: shape mismatch");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
+              "ts_gemm_nt_bnred: row-major operands with 16-B aligned rows required");
+  TORCH_CHECK(dph::conv1x1_supported(M, N, K), "ts_gemm_nt_bnred: need N, K % 64 == 0");
+  TORCH_CHECK(!c3 || (!add.has_value() && dph::conv3_supported(M, N, K, A.stride(0), B.stride(0))),
+              "ts_gemm_nt_bnred: 3x3 needs the LDS-DMA kernel's shapes and no add");
+  TORCH_CHECK(sub == 0 || (add.has_value() && H > 0 && W > 0), "ts_gemm_nt_bnred: sub = 2 needs add and H, W");
+  check_align16(A, "A");
+  check_align16(B, "B");
+  const void* D = nullptr;
+  if (add.has_value()) {
+    const int64_t rows = sub == 2 ? (M / (H * W)) * ((H - 1) / 2 + 1) * ((W - 1) / 2 + 1) : M;
+    TORCH_CHECK(add->scalar_type() == at::kBFloat16 && add->dim() == 2 && add->size(0) == rows &&
+                    add->size(1) == N && add->is_contiguous() && add->device() == A.device(),
+                "ts_gemm_nt_bnred: add must be a contiguous bf16 [rows, N] tensor");
+    check_align16(*add, "add");
+    D = add->data_ptr();
+  }
+  const bool xcl = x.dim() == 4 ? (x.size(1) == N && x.is_contiguous(at::MemoryFormat::ChannelsLast))
+                                : (x.dim() == 2 && x.size(1) == N && x.is_contiguous());
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.numel() == M * N && xcl && x.device() == A.device(),
+              "ts_gemm_nt_bnred: x must be the BatchNorm's bf16 channels-last input with M x N elements");
+  check_align16(x, "x");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && invstd.scalar_type() == at::kFloat && mean.numel() == N &&
+                  invstd.numel() == N && mean.is_contiguous() && invstd.is_contiguous(),
+              "ts_gemm_nt_bnred: fp32 mean / invstd [N]");
+  TORCH_CHECK(ss.has_value() != bits.has_value(), "ts_gemm_nt_bnred: exactly one of ss / bits");
+  dph::BnRed r;
+  r.x = x.data_ptr();
+  r.mean = mean.data_ptr<float>();
+  r.invstd = invstd.data_ptr<float>();
+  if (ss.has_value()) {
+    TORCH_CHECK(ss->scalar_type() == at::kFloat && ss->numel() == 2 * N && ss->is_contiguous(),
+                "ts_gemm_nt_bnred: ss must be fp32 [scale N | shift N]");
+    r.ss = ss->data_ptr<float>();
+  } else {
+    TORCH_CHECK(bits->scalar_type() == at::kByte && bits->numel() == M * N / 8 && bits->is_contiguous(),
+                "ts_gemm_nt_bnred: bits must be the forward's uint8 [M * N / 8]");
+    r.bits = bits->data_ptr<uint8_t>();
+  }
+  const uint8_t* am = nullptr;
+  if (add_mask.has_value()) {
+    TORCH_CHECK(add.has_value() && sub == 0 && !c3 && add_mask->scalar_type() == at::kByte &&
+                    add_mask->numel() == M * N / 8 && add_mask->is_contiguous() && add_mask->device() == A.device(),
+                "ts_gemm_nt_bnred: add_mask must be uint8 [M * N / 8] bits of a 1x1 [M, N] add");
+    am = add_mask->data_ptr<uint8_t>();
+  }
+  Tensor C = at::empty({M, N}, A.options());
+  Tensor part = at::empty({(M + 127) / 128, 2 * N}, A.options().dtype(at::kFloat));
+  r.part = part.data_ptr<float>();
+  dph::ts_gemm_nt_bnred(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), N, (int)H,
+                        (int)W, D, (int)sub, r, cur_stream(), am);
+  return {C, part};
+}
+
+// 1x1 input gradient C = A B^T + add * mask: the residual gradient of a BatchNorm + residual + ReLU handed over as its
+// output gradient ``add`` [M, N] and the forward's ReLU bits ``add_mask`` (uint8 [M * N / 8]), bitwise the plain add
+// of the masked bf16 gradient.
+Tensor ts_gemm_nt_addmask(const Tensor& A, const Tensor& B, const Tensor& add, const Tensor& add_mask) {
+  check_cuda(A, "A");
+  c10::DeviceGuard g(A.device());
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16,
+              "ts_gemm_nt_addmask: bf16 2-D operands");
+  const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+  TORCH_CHECK(B.size(1) == K, "ts_gemm_nt_addmask: K mismatch");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
+              "ts_gemm_nt_addmask: row-major operands with 16-B aligned rows required");
+  TORCH_CHECK(dph::conv1x1_supported(M, N, K), "ts_gemm_nt_addmask: need N, K % 64 == 0");
+  TORCH_CHECK(add.scalar_type() == at::kBFloat16 && add.dim() == 2 && add.size(0) == M && add.size(1) == N &&
+                  add.is_contiguous() && add.device() == A.device(),
+              "ts_gemm_nt_addmask: add must be a contiguous bf16 [M, N] tensor");
+  TORCH_CHECK(add_mask.scalar_type() == at::kByte && add_mask.numel() == M * N / 8 && add_mask.is_contiguous() &&
+                  add_mask.device() == A.device(),
+              "ts_gemm_nt_addmask: add_mask must be uint8 [M * N / 8]");
+  check_align16(A, "A");
+  check_align16(B, "B");
+  check_align16(add, "add");
+  Tensor C = at::empty({M, N}, A.options());
+  dph::ts_gemm_nt_bnred(A.data_ptr(), B.data_ptr(), C.data_ptr(), M, N, K, A.stride(0), B.stride(0), N, 0, 0,
+                        add.data_ptr(), 0, dph::BnRed{}, cur_stream(), add_mask.data_ptr<uint8_t>());
+  return C;
+}
+
 // C = A B^T plus the BatchNorm statistics partials of C per 128-row block ([mean | M2 | rows], see conv1x1.hip).
 std::tuple<Tensor, Tensor> ts_gemm_nt_stats(const Tensor& A, const Tensor& B, int64_t H, int64_t W,
                                             const c10::optional<Tensor>& pro_ss, const c10::optional<Tensor>& bias) {
@@ -1146,7 +1247,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Te
                                                       bool need_dwb, const c10::optional<Tensor>& xmask_ss,
                                                       const c10::optional<Tensor>& dw_out,
                                                       const c10::optional<Tensor>& db_out,
-                                                      const c10::optional<Tensor>& relu_mask) {
+                                                      const c10::optional<Tensor>& relu_mask,
+                                                      const c10::optional<Tensor>& pre_part) {
   check_cuda(x, "x");
   c10::DeviceGuard g(x.device());
   const int64_t C = bn_channels(x), M = x.numel() / C;
@@ -1183,11 +1285,19 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Te
   Tensor db = out_or_new(db_out, "db_out");
   const int G = dph::bn_partial_blocks(M, C);
   auto ws = at::empty({2 * (int64_t)G * C + 3 * C}, fopt);
+  int pre_groups = 0;
+  if (pre_part.has_value()) {   // the producer's epilogue reduced dy (ts_gemm_nt_bnred)
+    TORCH_CHECK(pre_part->scalar_type() == at::kFloat && pre_part->dim() == 2 && pre_part->size(1) == 2 * C &&
+                    pre_part->is_contiguous() && pre_part->device() == x.device() && (bm || xm),
+                "bn_act_bwd: pre_part must be fp32 [G, 2C] partials of a ReLU BatchNorm");
+    pre_groups = (int)pre_part->size(0);
+  }
   dph::bn_bwd(dy.data_ptr(), y.data_ptr(), x.data_ptr(), mean.data_ptr<float>(), invstd.data_ptr<float>(),
               w ? w->data_ptr() : nullptr, dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr,
               need_dwb ? dw.data_ptr() : nullptr, need_dwb ? db.data_ptr() : nullptr, ws.data_ptr<float>(), M, C, relu,
               dt_code(x), w ? dt_code(*w) : dph::kF32, cur_stream(), xm ? xmask_ss->data_ptr<float>() : nullptr,
-              bm ? relu_mask->data_ptr<uint8_t>() : nullptr);
+              bm ? relu_mask->data_ptr<uint8_t>() : nullptr,
+              pre_part.has_value() ? pre_part->data_ptr<float>() : nullptr, pre_groups);
   return {dx, dres, dw, db};
 }
 
@@ -1513,6 +1623,9 @@ TORCH_LIBRARY(dph, m) {
   m.def("convg_nt_out_(Tensor A, Tensor B, int[] geo, Tensor(a!) out) -> ()");
   m.def("convg_tn_(Tensor(a!) C, Tensor A, Tensor B, int[] geo, bool accumulate, bool chunk_taps=False) -> ()");
   m.def("ts_gemm_nt_add_sub(Tensor A, Tensor B, Tensor add, int H, int W, int s) -> Tensor");
+  m.def("ts_gemm_nt_bnred(Tensor A, Tensor B, int H, int W, Tensor? add, int sub, Tensor x, Tensor mean, "
+        "Tensor invstd, Tensor? ss=None, Tensor? bits=None, Tensor? add_mask=None) -> (Tensor, Tensor)");
+  m.def("ts_gemm_nt_addmask(Tensor A, Tensor B, Tensor add, Tensor add_mask) -> Tensor");
   m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
   m.def("channel_sum_into_(Tensor x, Tensor(a!) out) -> ()");
@@ -1526,7 +1639,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "
         "bool need_dwb, Tensor? xmask_ss=None, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, "
-        "Tensor? relu_mask=None) "
+        "Tensor? relu_mask=None, Tensor? pre_part=None) "
         "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("latmse_fwd(Tensor pred, Tensor target, int n_global, int lat_offset) -> Tensor");
   m.def("latmse_bwd(Tensor gloss, Tensor pred, Tensor target, int n_global, int lat_offset, bool need_dtarget) -> "
@@ -1589,6 +1702,8 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("convg_nt_out_", &convg_nt_out_);
   m.impl("convg_tn_", &convg_tn_);
   m.impl("ts_gemm_nt_add_sub", &ts_gemm_nt_add_sub);
+  m.impl("ts_gemm_nt_bnred", &ts_gemm_nt_bnred);
+  m.impl("ts_gemm_nt_addmask", &ts_gemm_nt_addmask);
   m.impl("maxpool_s2_fwd", &maxpool_s2_fwd);
   m.impl("channel_sum", &channel_sum);
   m.impl("channel_sum_into_", &channel_sum_into_);

@@ -20,7 +20,8 @@ from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.batchnorm import bn_relu_conv1x1, bn_relu_conv1x1_ok
-from ..ops.conv import Conv1x1, Conv3x3, GradSlot, StatsSlot, StemConv2d, StridedConv2d, grad_tap, strided_native_ok
+from ..ops.conv import (BnGradSlot, Conv1x1, Conv3x3, GradSlot, StatsSlot, StemConv2d, StridedConv2d, grad_tap,
+                        strided_native_ok)
 from ..ops.pool import MaxPool2d
 
 
@@ -33,6 +34,39 @@ def conv1x1(cin, cout, stride=1):
     # nn.Conv2d-compatible modules that run channels-last bf16 on the CDNA4 GEMM kernels (ops/conv.py); the strided
     # 1x1 (the downsample of layers 2-4) gathers every s-th pixel in its operand load
     return Conv1x1(cin, cout) if stride == 1 else StridedConv2d(cin, cout, 1, stride, 0, bias=False)
+
+
+class BnHandoff:
+    """Hands a block's last BatchNorm slot (ops.conv.BnGradSlot) to the next block's conv1, which consumes that output.
+
+    A tensor attribute would not survive module hooks (full backward hooks hand the next block an alias of the
+    output), so the producing block leaves the slot here with the output's storage key, and the consuming block takes
+    it only when its input has that key (same storage, shape and strides).  Plain object (not a Module): no state."""
+
+    __slots__ = ("slot", "key")
+
+    def __init__(self):
+        self.slot = self.key = None
+
+    @staticmethod
+    def _key(t: torch.Tensor):
+        return (t.data_ptr(), tuple(t.shape), tuple(t.stride()))
+
+    def put(self, y: torch.Tensor, slot):
+        self.slot, self.key = slot, (self._key(y) if slot is not None else None)
+
+    def take(self, x: torch.Tensor):
+        slot, key = self.slot, self.key
+        self.slot = self.key = None
+        return slot if slot is not None and key == self._key(x) else None
+
+
+def link_bn_handoff(blocks) -> None:
+    """Chain consecutive bottleneck blocks (in forward order) through one BnHandoff (ResNet does this for its own)."""
+    h = BnHandoff()
+    for b in blocks:
+        if isinstance(b, Bottleneck):
+            b._dph_handoff = h
 
 
 class BasicBlock(nn.Module):
@@ -48,8 +82,10 @@ class BasicBlock(nn.Module):
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
-        out = self.bn1(self.conv1(x))
-        return self.bn2(self.conv2(out), idt)
+        # bn1's backward reduction runs in conv2's input-gradient epilogue (its only consumer; ops.conv.BnGradSlot)
+        r1 = BnGradSlot() if isinstance(self.conv2, Conv3x3) and self.bn1.training else None
+        out = self.bn1(self.conv1(x), bn_slot=r1)
+        return self.bn2(self.conv2(out, bn_slot=r1), idt)
 
 
 class Bottleneck(nn.Module):
@@ -74,7 +110,16 @@ class Bottleneck(nn.Module):
         # training-mode BN after a 1x1 convolution takes its statistics from the convolution's epilogue
         s1 = StatsSlot() if self.bn1.training and isinstance(self.conv1, Conv1x1) else None
         s3 = StatsSlot() if self.bn3.training and isinstance(self.conv3, Conv1x1) else None
-        out = self.bn1(self.conv1(x, grad_slot=slot, stats_slot=s1), stats_slot=s1)
+        # BatchNorm backward reductions in the consuming convolution's input-gradient epilogue (ops.conv.BnGradSlot):
+        # bn1 -> conv2 (stride-1 3x3), bn2 -> conv3, and the previous block's bn3 -> this conv1 when the GradSlot
+        # carries x's other gradient (identity or downsample) into the same epilogue
+        train = self.bn1.training
+        r1 = BnGradSlot() if train and isinstance(self.conv2, Conv3x3) else None
+        r2 = BnGradSlot() if train and isinstance(self.conv3, Conv1x1) else None
+        r3 = BnGradSlot(sole=False) if self.bn3.training else None
+        hand = getattr(self, "_dph_handoff", None)
+        rin = hand.take(x) if hand is not None and slot is not None else None
+        out = self.bn1(self.conv1(x, grad_slot=slot, stats_slot=s1, bn_slot=rin), stats_slot=s1, bn_slot=r1)
         if self.downsample is None:
             idt, res_slot = x, slot
         else:
@@ -92,14 +137,20 @@ class Bottleneck(nn.Module):
                 idt = self.downsample(tapped)
             res_slot = None
         s2 = StatsSlot() if isinstance(self.conv2, (Conv3x3, StridedConv2d)) and self.bn2.training else None
-        out = self.conv2(out, stats_slot=s2) if s2 is not None else self.conv2(out)
+        if isinstance(self.conv2, Conv3x3):
+            out = self.conv2(out, stats_slot=s2, bn_slot=r1)
+        else:
+            out = self.conv2(out, stats_slot=s2) if s2 is not None else self.conv2(out)
         if bn_relu_conv1x1_ok(self.bn2, self.conv3, out):
             # bn2's apply + ReLU folded into conv3's operand loads (forward and weight gradient): the normalised
             # activation is never written (ops.batchnorm._BNReLUConv1x1Fn)
             out = bn_relu_conv1x1(self.bn2, self.conv3, out, s2, s3)
         else:
-            out = self.conv3(self.bn2(out, stats_slot=s2), stats_slot=s3)
-        return self.bn3(out, idt, residual_grad_slot=res_slot, stats_slot=s3)
+            out = self.conv3(self.bn2(out, stats_slot=s2, bn_slot=r2), stats_slot=s3, bn_slot=r2)
+        y = self.bn3(out, idt, residual_grad_slot=res_slot, stats_slot=s3, bn_slot=r3)
+        if hand is not None:
+            hand.put(y, r3)   # for the next block's conv1
+        return y
 
 
 class ResNet(nn.Module):
@@ -118,6 +169,7 @@ class ResNet(nn.Module):
         self.layer2 = self._make(block, 128, layers[1], 2)
         self.layer3 = self._make(block, 256, layers[2], 2)
         self.layer4 = self._make(block, 512, layers[3], 2)
+        link_bn_handoff([b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer])
         self.avgpool = nn.AdaptiveAvgPool2d((1, 1))
         self.fc = nn.Linear(512 * block.expansion, num_classes)
         for m in self.modules():

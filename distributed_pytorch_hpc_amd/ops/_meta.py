@@ -88,7 +88,7 @@ def _bn_act_apply(x, res, scale, shift, relu):
 
 @register_fake("dph::bn_act_bwd")
 def _bn_act_bwd(dy, y, x, mean, invstd, w, relu, need_dres, need_dwb, xmask_ss=None, dw_out=None, db_out=None,
-                relu_mask=None):
+                relu_mask=None, pre_part=None):
     c = x.shape[1]
     pdt = w.dtype if w is not None else torch.float32
     return (torch.empty_like(x), torch.empty_like(x) if need_dres else x.new_empty((0,)),
@@ -238,6 +238,17 @@ def _convg_tn(C, A, B, geo, accumulate, chunk_taps=False):
 
 @register_fake("dph::ts_gemm_nt_add_sub")
 def _ts_gemm_nt_add_sub(A, B, add, H, W, s):
+    return A.new_empty((A.shape[0], B.shape[0]))
+
+
+@register_fake("dph::ts_gemm_nt_bnred")
+def _ts_gemm_nt_bnred(A, B, H, W, add, sub, x, mean, invstd, ss=None, bits=None, add_mask=None):
+    M, N = A.shape[0], B.shape[0]
+    return A.new_empty((M, N)), A.new_empty(((M + 127) // 128, 2 * N), dtype=torch.float32)
+
+
+@register_fake("dph::ts_gemm_nt_addmask")
+def _ts_gemm_nt_addmask(A, B, add, add_mask):
     return A.new_empty((A.shape[0], B.shape[0]))
 
 

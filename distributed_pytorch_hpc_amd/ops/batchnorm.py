@@ -42,7 +42,7 @@ def _native_ok(x: torch.Tensor, residual) -> bool:
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, slot=None,
-                pre_stats=None, nbt=None):
+                pre_stats=None, nbt=None, bn_slot=None):
         # ReLU without residual: the backward recomputes the mask from x with the forward's scale / shift and
         # never reads y (one activation-sized read less in each backward pass).  ReLU after a residual add: the
         # forward writes [y > 0] as bits (1/16 of y's bytes) and the backward reads those instead of y.
@@ -52,6 +52,11 @@ class _BNActFn(torch.autograd.Function):
         y, mean, invstd, ss = _lib.ops().bn_act_fwd(x, residual, weight, bias, running_mean, running_var, momentum,
                                                     eps, relu, pre_stats, nbt, bits)
         ctx.save_for_backward(x, ss if ctx.xmask else (bits if ctx.bmask else y), mean, invstd, weight)
+        # the consumer convolution may run this BatchNorm's backward reduction in its dgrad epilogue (BnGradSlot)
+        ctx.bn_slot = bn_slot if (bn_slot is not None and (ctx.xmask or ctx.bmask)
+                                  and x.dtype == torch.bfloat16) else None
+        if ctx.bn_slot is not None:
+            bn_slot.fill(x, mean, invstd, ss if ctx.xmask else None, bits if ctx.bmask else None)
         ctx.relu, ctx.has_res = relu, residual is not None
         ctx.has_wb = weight is not None
         ctx.params = (weight, bias)
@@ -61,6 +66,7 @@ class _BNActFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, saved, mean, invstd, weight = ctx.saved_tensors
+        part = ctx.bn_slot.take(dy) if ctx.bn_slot is not None else None   # reduced by the consumer's epilogue
         dy = dy.contiguous(memory_format=torch.channels_last)
         need_wb = ctx.has_wb and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         # y is only read by the kernels when neither mask form applies (no ReLU: it is not read at all)
@@ -73,37 +79,49 @@ class _BNActFn(torch.autograd.Function):
         direct = (need_wb and bp is not None and _DIRECT and all(
             getattr(p, "main_grad", None) is not None and not getattr(p, "_dph_accum", True)
             and p.main_grad.is_contiguous() and p.main_grad.dtype == p.dtype for p in (wp, bp)))
+        # the residual gradient is dy under the ReLU bits: with a consuming 1x1 convolution (GradSlot) hand it dy and
+        # the bits -- its dgrad kernel adds dy * mask -- instead of writing the masked copy (one activation-sized
+        # write less)
+        handoff = (ctx.slot is not None and ctx.has_res and bits is not None and dy.dtype == torch.bfloat16
+                   and os.environ.get("DPH_RES_MASK", "1") != "0")
         dx, dres, dw, db = _lib.ops().bn_act_bwd(dy, y, x, mean, invstd, weight if ctx.has_wb else None, ctx.relu,
-                                                 ctx.has_res, need_wb, ss, wp.main_grad if direct else None,
-                                                 bp.main_grad if direct else None, bits)
+                                                 ctx.has_res and not handoff, need_wb, ss,
+                                                 wp.main_grad if direct else None, bp.main_grad if direct else None,
+                                                 bits, part)
         if direct:
             for p in (wp, bp):
                 p._dph_accum = True
                 p._dph_grad_ready()
             dw = db = None
-        if ctx.slot is not None and ctx.has_res:   # the residual's gradient goes to the consuming 1x1 conv
+        if handoff:
+            ctx.slot.t, ctx.slot.mask = dy, bits
+            dres = None
+        elif ctx.slot is not None and ctx.has_res:   # the residual's gradient goes to the consuming 1x1 conv
             ctx.slot.t = dres
             dres = None
         return (dx, dw if need_wb else None, db if need_wb else None, None, None, dres if ctx.has_res else None,
-                None, None, None, None, None, None)
+                None, None, None, None, None, None, None)
 
 
 def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
                    residual=None, relu: bool = True, residual_grad_slot=None, stats_slot=None,
-                   num_batches_tracked=None):
+                   num_batches_tracked=None, bn_slot=None):
     """act(batch_norm(x) + residual) with the fused kernels when eligible.  ``residual_grad_slot``
-    (ops.conv.GradSlot): hand the residual's gradient to the 1x1 convolution that consumes the same input."""
+    (ops.conv.GradSlot): hand the residual's gradient to the 1x1 convolution that consumes the same input.
+    ``bn_slot`` (ops.conv.BnGradSlot): the convolution consuming the output may run the backward reduction."""
     if _native_ok(x, residual):
         if training:
             # statistics already computed by the producing 1x1 convolution (ops.conv.StatsSlot)
             pre = stats_slot.take(x.numel() // x.shape[1], x.shape[1]) if stats_slot is not None else None
             slot = residual_grad_slot
+            if not torch.is_grad_enabled():
+                bn_slot = None
             if slot is not None and residual is not None and slot.consumer and torch.is_grad_enabled():
                 slot.armed = True
                 return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual.detach(), momentum, eps,
-                                      relu, slot, pre, num_batches_tracked)
+                                      relu, slot, pre, num_batches_tracked, bn_slot)
             return _BNActFn.apply(x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, None,
-                                  pre, num_batches_tracked)
+                                  pre, num_batches_tracked, bn_slot)
         with torch.no_grad():
             inv = torch.rsqrt(running_var.float() + eps)
             scale = inv * (weight.float() if weight is not None else 1.0)
@@ -124,7 +142,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         super().__init__(num_features, eps, momentum, affine, track_running_stats, **kw)
         self.act = act
 
-    def forward(self, x, residual=None, residual_grad_slot=None, stats_slot=None):
+    def forward(self, x, residual=None, residual_grad_slot=None, stats_slot=None, bn_slot=None):
         training = self.training or not self.track_running_stats
         momentum = self.momentum
         nbt = None
@@ -140,7 +158,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         if training and rm is not None and not self.training:
             rm = rv = None
         return batch_norm_act(x, self.weight, self.bias, rm, rv, training, momentum, self.eps, residual, self.act,
-                              residual_grad_slot, stats_slot, nbt)
+                              residual_grad_slot, stats_slot, nbt, bn_slot)
 
     def extra_repr(self):
         return super().extra_repr() + f", act={'relu' if self.act else 'none'}"

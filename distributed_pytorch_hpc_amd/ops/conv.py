@@ -121,13 +121,16 @@ class GradSlot:
     residual gradient in ``t`` -- bn3's backward runs before conv1's -- and conv1's dgrad kernel adds it in its
     epilogue (``ts_gemm_nt(..., add=)``), so x receives one gradient."""
 
-    __slots__ = ("consumer", "armed", "t", "sub")
+    __slots__ = ("consumer", "armed", "t", "sub", "mask")
 
     def __init__(self):
         self.sub = None      # (s, H, W): t is the gradient of the stride-s sub-image of an H x W input
         self.consumer = False
         self.armed = False
         self.t = None
+        # ReLU bits of the BatchNorm that left t: the residual gradient is t under this mask -- bn3 hands over its dy
+        # and its forward's bits instead of writing the masked copy (DPH_RES_MASK=0 restores the copy)
+        self.mask = None
 
 
 class _GradTapFn(torch.autograd.Function):
@@ -172,9 +175,55 @@ class StatsSlot:
         return st if st is not None and (self.rows, self.cols) == (rows, cols) else None
 
 
+class BnGradSlot:
+    """The backward reduction of a training-mode BatchNorm + ReLU, run in the epilogue of the convolution that consumes
+    the BatchNorm's output (``ts_gemm_nt_bnred``; csrc/bn_epilogue.h).
+
+    The BatchNorm backward needs, per channel, sum(dz) and sum(dz * xhat) over its output gradient (dz = dy * ReLU
+    mask) before it can write dx -- a pass that re-reads dy, x and the mask.  dy is written by the consumer
+    convolution's input-gradient kernel, so that kernel reads x and the mask at the rows it stores and emits the
+    per-128-row partials instead (one read of dy fewer, one launch fewer).  The BatchNorm's forward ``fill``s the slot
+    (its saved x, mean, invstd and mask source), the consumer's backward leaves ``part`` and the identity of the
+    gradient it returned, and the BatchNorm's backward ``take``s the partials -- only if the gradient it received is
+    that very tensor, unmodified (``dy_key``): a gradient summed with another consumer's falls back to the reduction
+    pass.  ``sole``: the convolution is the output's only consumer; otherwise (a ResNet block input, also the
+    residual) it uses the slot only when its GradSlot routes the other gradient into the same epilogue."""
+
+    __slots__ = ("x", "mean", "invstd", "ss", "bits", "part", "dy_key", "sole")
+
+    def __init__(self, sole: bool = True):
+        self.sole = sole
+        self.x = self.mean = self.invstd = self.ss = self.bits = self.part = self.dy_key = None
+
+    def fill(self, x, mean, invstd, ss=None, bits=None):
+        self.x, self.mean, self.invstd, self.ss, self.bits = x, mean, invstd, ss, bits
+
+    def usable(self, rows: int, cols: int, armed: bool = False) -> bool:
+        # DPH_BN_EPILOGUE=0: the BatchNorm runs its own reduction pass (A/B comparisons)
+        return (self.x is not None and (self.sole or armed) and self.x.dtype == torch.bfloat16
+                and os.environ.get("DPH_BN_EPILOGUE", "1") != "0"
+                and self.x.numel() == rows * cols and self.x.shape[1] == cols)
+
+    def launch(self, A, B, H=0, W=0, add=None, sub=0):
+        """dX = A B^T (+ add) with the reduction epilogue; keeps the partials, returns dX [rows, cols]."""
+        dx2, self.part = _lib.ops().ts_gemm_nt_bnred(A, B, H, W, add, sub, self.x, self.mean, self.invstd, self.ss,
+                                                     self.bits)
+        return dx2
+
+    def mark(self, dx: torch.Tensor):
+        self.dy_key = (dx.data_ptr(), dx._version, tuple(dx.shape), tuple(dx.stride()))
+
+    def take(self, dy: torch.Tensor):
+        part, key = self.part, self.dy_key
+        self.x = self.mean = self.invstd = self.ss = self.bits = self.part = self.dy_key = None
+        if part is None or key != (dy.data_ptr(), dy._version, tuple(dy.shape), tuple(dy.stride())):
+            return None
+        return part
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, slot=None, stats_slot=None):
+    def forward(ctx, x, w, slot=None, stats_slot=None, bn_slot=None):
         wdtype = w.dtype
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -188,7 +237,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         else:
             y2 = _lib.ops().ts_gemm_nt(x2, w2)                      # [M, Cout]
         ctx.save_for_backward(x2, w2)
-        ctx.shape, ctx.wdtype, ctx.param, ctx.slot = (B, C, H, W), wdtype, w, slot
+        ctx.shape, ctx.wdtype, ctx.param, ctx.slot, ctx.bn_slot = (B, C, H, W), wdtype, w, slot, bn_slot
         return y2.view(B, H, W, -1).permute(0, 3, 1, 2)             # channels-last [B, Cout, H, W]
 
     @staticmethod
@@ -199,27 +248,44 @@ class _Conv1x1Fn(torch.autograd.Function):
         dx = gw = None
         slot = ctx.slot
         if ctx.needs_input_grad[0]:
-            add = None
+            add = amask = None
             if slot is not None and slot.armed:
                 if slot.t is None:
                     raise RuntimeError("Conv1x1: residual gradient slot armed but empty (backward order)")
-                add = slot.t
-                slot.t = None
-            if add is not None and slot.sub is not None:   # a strided 1x1 downsample's sub-image gradient
+                add, amask = slot.t, slot.mask
+                slot.t = slot.mask = None
+            bn = ctx.bn_slot   # x is a BatchNorm + ReLU output: that BatchNorm's reduction in this epilogue
+            bn = bn if bn is not None and bn.usable(B * H * W, C, slot is not None and slot.armed) else None
+            if amask is not None:   # the residual gradient is add under the ReLU bits amask (identity block)
+                add = _nhwc2d(add.to(torch.bfloat16))
+                if bn is not None:
+                    dx2, bn.part = _lib.ops().ts_gemm_nt_bnred(dy2, weight_t(w2), 0, 0, add, 0, bn.x, bn.mean,
+                                                               bn.invstd, bn.ss, bn.bits, amask)
+                else:
+                    dx2 = _lib.ops().ts_gemm_nt_addmask(dy2, weight_t(w2), add, amask)
+            elif add is not None and slot.sub is not None:   # a strided 1x1 downsample's sub-image gradient
                 s_, h_, w_ = slot.sub
-                dx2 = _lib.ops().ts_gemm_nt_add_sub(dy2, weight_t(w2), add.to(torch.bfloat16), h_, w_, s_)
+                if bn is not None:
+                    dx2 = bn.launch(dy2, weight_t(w2), h_, w_, add.to(torch.bfloat16), s_)
+                else:
+                    dx2 = _lib.ops().ts_gemm_nt_add_sub(dy2, weight_t(w2), add.to(torch.bfloat16), h_, w_, s_)
             else:
                 if add is not None:
                     add = _nhwc2d(add.to(torch.bfloat16))
-                dx2 = _lib.ops().ts_gemm_nt(dy2, weight_t(w2), 0, 0, add)    # [M, Cin] (+ residual grad)
+                if bn is not None:
+                    dx2 = bn.launch(dy2, weight_t(w2), 0, 0, add)
+                else:
+                    dx2 = _lib.ops().ts_gemm_nt(dy2, weight_t(w2), 0, 0, add)    # [M, Cin] (+ residual grad)
             dx = dx2.view(B, H, W, C).permute(0, 3, 1, 2)
+            if bn is not None:
+                bn.mark(dx)
         if ctx.needs_input_grad[1]:
             cout = w2.shape[0]
             if not _wgrad_into_main(ctx.param, (cout, C), lambda out, acc: _lib.ops().ts_gemm_tn_(out, dy2, x2, acc)):
                 gw = torch.empty((cout, C), dtype=ctx.wdtype, device=dy.device)
                 _lib.ops().ts_gemm_tn_(gw, dy2, x2, False)
                 gw = gw.view(cout, C, 1, 1)
-        return dx, gw, None, None
+        return dx, gw, None, None, None
 
 
 # 3x3 weight gradients on the c3w_k kernel (wgrad="dph") since its DMA addresses advance incrementally and its split-K
@@ -241,9 +307,14 @@ def _main_grad_cl(w: torch.Tensor, cout: int, k: int):
     return mg.permute(0, 2, 3, 1).view(cout, k)
 
 
+def _conv3_lds_ok(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
+    """csrc/conv3x3.hip conv3_supported: the 3x3 shapes the LDS-DMA kernel (and its BatchNorm epilogue) takes."""
+    return M > 0 and N % 64 == 0 and K % (9 * 64) == 0 and M * lda * 2 < 2 ** 31 and N * ldb * 2 < 2 ** 31
+
+
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stats_slot=None, bias=None, wgrad="dph"):
+    def forward(ctx, x, w, stats_slot=None, bias=None, wgrad="dph", bn_slot=None):
         wdtype = w.dtype
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -266,6 +337,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.bias_param = bias if isinstance(bias, nn.Parameter) else None
         ctx.wgrad = wgrad
+        ctx.bn_slot = bn_slot
         ctx.save_for_backward(x2, wb)
         ctx.shape, ctx.wdtype, ctx.param = (B, C, H, W), wdtype, w
         return y2.view(B, H, W, cout).permute(0, 3, 1, 2)
@@ -283,7 +355,13 @@ class _Conv3x3Fn(torch.autograd.Function):
                 wf = _lib.ops().conv3x3_dgrad_weight(wb)                  # one launch, HBM-speed tiles
             else:
                 wf = wb.flip(2, 3).permute(1, 2, 3, 0).reshape(C, 9 * cout)
-            dx = _lib.ops().ts_gemm_nt(dy2, wf, H, W).view(B, H, W, C).permute(0, 3, 1, 2)
+            bn = ctx.bn_slot   # x is a BatchNorm + ReLU output: that BatchNorm's reduction in this epilogue
+            if (bn is not None and bn.usable(B * H * W, C) and wf.is_contiguous()
+                    and _conv3_lds_ok(B * H * W, C, 9 * cout, dy2.stride(0), wf.stride(0))):
+                dx = bn.launch(dy2, wf, H, W).view(B, H, W, C).permute(0, 3, 1, 2)
+                bn.mark(dx)
+            else:
+                dx = _lib.ops().ts_gemm_nt(dy2, wf, H, W).view(B, H, W, C).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1] and ctx.wgrad != "dph":
             # weight gradient on MIOpen: 1.0-1.5x the split-pixel kernel on the ResNet-50 shapes
             # (profiles/r3/conv3_bench_oob.json: 318-485 vs 302-321 TFLOP/s, before round 4's c3w_k rework)
@@ -306,7 +384,7 @@ class _Conv3x3Fn(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[3]:
             db = (zero_bias_grad(ctx.bias_param, cout, ctx.bias_dtype, dy.device) if ctx.bias_cancels
                   else bias_grad(ctx.bias_param, dy2, ctx.bias_dtype))
-        return dx, gw, None, db, None
+        return dx, gw, None, db, None, None
 
 
 def conv3x3_native_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -325,10 +403,12 @@ class Conv3x3(nn.Conv2d):
     def __init__(self, in_channels: int, out_channels: int):
         super().__init__(in_channels, out_channels, kernel_size=3, stride=1, padding=1, bias=False)
 
-    def forward(self, x, stats_slot: StatsSlot | None = None):
+    def forward(self, x, stats_slot: StatsSlot | None = None, bn_slot: BnGradSlot | None = None):
+        """``bn_slot``: x is the output of a training-mode BatchNorm + ReLU consumed only here; the BatchNorm's backward
+        reduction then runs in this convolution's input-gradient epilogue (BnGradSlot)."""
         if conv3x3_native_ok(x, self.weight):
             _lib.require()
-            return _Conv3x3Fn.apply(x, self.weight, stats_slot)
+            return _Conv3x3Fn.apply(x, self.weight, stats_slot, None, "dph", bn_slot)
         return F.conv2d(x, self.weight, padding=1)
 
 
@@ -517,12 +597,16 @@ class Conv1x1(nn.Conv2d):
     def __init__(self, in_channels: int, out_channels: int):
         super().__init__(in_channels, out_channels, kernel_size=1, stride=1, padding=0, bias=False)
 
-    def forward(self, x, grad_slot: GradSlot | None = None, stats_slot: StatsSlot | None = None):
+    def forward(self, x, grad_slot: GradSlot | None = None, stats_slot: StatsSlot | None = None,
+                bn_slot: BnGradSlot | None = None):
+        """``bn_slot``: x is a training-mode BatchNorm + ReLU output whose backward reduction may run in this
+        convolution's input-gradient epilogue (BnGradSlot: always when the slot is ``sole``, else only when
+        ``grad_slot`` carries x's other gradient into the same epilogue)."""
         if conv1x1_native_ok(x, self.weight):
             _lib.require()
             if grad_slot is not None:
                 grad_slot.consumer = True
-            return _Conv1x1Fn.apply(x, self.weight, grad_slot, stats_slot)
+            return _Conv1x1Fn.apply(x, self.weight, grad_slot, stats_slot, bn_slot)
         return F.conv2d(x, self.weight)
 
 

@@ -1,0 +1,246 @@
+"""BatchNorm backward reduction in the consumer convolution's input-gradient epilogue (ops/conv.py BnGradSlot,
+csrc/bn_epilogue.h, ``ts_gemm_nt_bnred``) against fp64 references of the same sums, and the ResNet blocks / ResNet-50
+with the epilogue on vs off (DPH_BN_EPILOGUE=0: the BatchNorm's own reduction pass)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _kernels_on(monkeypatch):
+    monkeypatch.setenv("DPH_CONV", "dph")
+    monkeypatch.delenv("DPH_BN_EPILOGUE", raising=False)
+
+
+def rel_err(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _mask(x, ss=None, bits=None):
+    M, N = x.shape
+    if bits is not None:
+        return ((bits.long()[:, None] >> torch.arange(8, device=x.device)) & 1).reshape(M, N).bool()
+    # the kernel's test is fmaf(x, scale, shift) > 0: in fp64 the product is exact and the sign of the sum survives
+    return x.double() * ss[:N].double() + ss[N:].double() > 0
+
+
+def _ref_sums(c, x, mean, invstd, mask):
+    dz = c.double() * mask
+    xh = (x.double() - mean.double()) * invstd.double()
+    return dz.sum(0), (dz * xh).sum(0)
+
+
+@pytest.mark.parametrize("form", ["1x1", "1x1_add", "1x1_sub", "3x3"])
+@pytest.mark.parametrize("N", [64, 128, 256])
+@pytest.mark.parametrize("mode", ["ss", "bits"])
+def test_ts_gemm_nt_bnred_matches_fp64(dph_native, form, N, mode):
+    """dX is bitwise the plain kernel's output; the partials sum to fp64 sum(dz) / sum(dz * xhat) over the stored bf16
+    gradient, with a ragged last 128-row block."""
+    torch.manual_seed(N + len(form))
+    ops = torch.ops.dph
+    n_img, H, W = 3, 9, 13                                  # M = 351: two full 128-row blocks + a ragged one
+    M = n_img * H * W
+    K = 128 if form != "3x3" else 64
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    if form == "3x3":
+        b = (torch.randn(N, 9 * K, device=DEV) * 0.05).to(torch.bfloat16)
+        ref = ops.ts_gemm_nt(a, b, H, W)
+        hh, ww, add, sub = H, W, None, 0
+    elif form == "1x1_sub":
+        b = (torch.randn(N, K, device=DEV) * 0.1).to(torch.bfloat16)
+        add = torch.randn(n_img * ((H + 1) // 2) * ((W + 1) // 2), N, device=DEV, dtype=torch.bfloat16)
+        ref = ops.ts_gemm_nt_add_sub(a, b, add, H, W, 2)
+        hh, ww, sub = H, W, 2
+    else:
+        b = (torch.randn(N, K, device=DEV) * 0.1).to(torch.bfloat16)
+        add = torch.randn(M, N, device=DEV, dtype=torch.bfloat16) if form == "1x1_add" else None
+        ref = ops.ts_gemm_nt(a, b, 0, 0, add)
+        hh, ww, sub = 0, 0, 0
+    x = (torch.randn(M, N, device=DEV) * 1.5 + 0.3).to(torch.bfloat16)
+    mean = x.float().mean(0)
+    invstd = torch.rsqrt(x.float().var(0, unbiased=False) + 1e-5)
+    ss = bits = None
+    if mode == "ss":
+        ss = torch.cat([torch.randn(N, device=DEV), torch.randn(N, device=DEV) * 0.5])
+    else:
+        bits = torch.randint(0, 256, (M * N // 8,), device=DEV, dtype=torch.uint8)
+    c, part = ops.ts_gemm_nt_bnred(a, b, hh, ww, add, sub, x, mean, invstd, ss, bits)
+    torch.cuda.synchronize()
+    assert torch.equal(c, ref)
+    assert part.shape == ((M + 127) // 128, 2 * N)
+    sd, sdx = _ref_sums(c, x, mean, invstd, _mask(x, ss, bits))
+    got = part.double().sum(0)
+    assert rel_err(got[:N], sd) < 1e-5
+    assert rel_err(got[N:], sdx) < 1e-5
+
+
+@pytest.mark.parametrize("residual", [False, True])
+def test_bn_act_bwd_pre_part_matches_own_reduction(dph_native, residual):
+    """bn_act_bwd with the epilogue's partials gives the dx / dgamma / dbeta of its own reduction pass (fp32 sums in
+    another order: agreement to fp32 rounding)."""
+    torch.manual_seed(3)
+    ops = torch.ops.dph
+    B, C, H, W = 4, 128, 10, 12
+    x = torch.randn(B, C, H, W, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = torch.randn_like(x) if residual else None
+    w = (1 + 0.1 * torch.randn(C, device=DEV))
+    bias = 0.1 * torch.randn(C, device=DEV)
+    bits = torch.empty(x.numel() // 8, device=DEV, dtype=torch.uint8) if residual else None
+    y, mean, invstd, ss = ops.bn_act_fwd(x, res, w, bias, None, None, 0.1, 1e-5, True, None, None, bits)
+    A = torch.randn(B * H * W, 256, device=DEV, dtype=torch.bfloat16)
+    Bw = (torch.randn(C, 256, device=DEV) * 0.05).to(torch.bfloat16)
+    dy2, part = ops.ts_gemm_nt_bnred(A, Bw, 0, 0, None, 0, x, mean, invstd, None if residual else ss, bits)
+    dy = dy2.view(B, H, W, C).permute(0, 3, 1, 2)
+    saved = bits if residual else None
+    kw = dict(xmask_ss=None if residual else ss, relu_mask=saved)
+    ref = ops.bn_act_bwd(dy, x, x, mean, invstd, w, True, residual, True, **kw)
+    got = ops.bn_act_bwd(dy, x, x, mean, invstd, w, True, residual, True, **kw, pre_part=part)
+    for g_, r_ in zip(got, ref):
+        if r_.numel():
+            assert rel_err(g_, r_) < 1e-4
+
+
+class _Count:
+    def __init__(self, monkeypatch):
+        from distributed_pytorch_hpc_amd.ops import conv as conv_mod
+
+        self.used = 0
+        orig = conv_mod.BnGradSlot.take
+
+        def take(slot, dy):
+            part = orig(slot, dy)
+            self.used += part is not None
+            return part
+
+        monkeypatch.setattr(conv_mod.BnGradSlot, "take", take)
+
+
+def _grads(model, x, monkeypatch, on):
+    monkeypatch.setenv("DPH_BN_EPILOGUE", "1" if on else "0")
+    model.zero_grad(set_to_none=True)
+    x.grad = None
+    torch.manual_seed(11)
+    y = model(x)
+    (y.float() * torch.randn_like(y.float())).sum().backward()
+    torch.cuda.synchronize()
+    return x.grad.double().clone(), {n: p.grad.double().clone() for n, p in model.named_parameters()}
+
+
+@pytest.mark.parametrize("kind", ["identity", "downsample", "basic"])
+def test_blocks_epilogue_on_matches_off(dph_native, monkeypatch, kind):
+    """A ResNet block pair (so the second block's conv1 reduces the first block's bn3): input and parameter gradients
+    with the reductions in the convolution epilogues match the BatchNorms' own reduction passes."""
+    import importlib
+
+    R = importlib.import_module("distributed_pytorch_hpc_amd.models.resnet")
+    torch.manual_seed(0)
+    if kind == "identity":
+        blocks = [R.Bottleneck(256, 64), R.Bottleneck(256, 64)]
+        expect, cin, hw = 5, 256, 14   # bn1 x2 (3x3 consumer), bn2 x2 (conv3), first bn3 (second conv1)
+    elif kind == "downsample":
+        ds = torch.nn.Sequential(R.conv1x1(256, 512, 2), R.BatchNormAct2d(512, act=False))
+        blocks = [R.Bottleneck(256, 64), R.Bottleneck(256, 128, 2, ds)]
+        expect, cin, hw = 4, 256, 14   # bn1 (stride-1 block only), bn2 x2, first bn3 (conv1 + downsample slot)
+    else:
+        blocks = [R.BasicBlock(64, 64), R.BasicBlock(64, 64)]
+        expect, cin, hw = 2, 64, 12    # bn1 x2 (conv2 consumers); bn2 outputs feed the next block's 3x3 conv1
+    R.link_bn_handoff(blocks)
+    model = torch.nn.Sequential(*blocks).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for m in model.modules():   # non-trivial affine parameters
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    x = torch.randn(4, cin, hw, hw, device=DEV, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+    cnt = _Count(monkeypatch)
+    gx0, g0 = _grads(model, x, monkeypatch, False)
+    assert cnt.used == 0
+    gx1, g1 = _grads(model, x, monkeypatch, True)
+    assert cnt.used == expect
+    assert rel_err(gx1, gx0) < 1e-2
+    for n in g0:
+        assert rel_err(g1[n], g0[n]) < 1e-2, n
+
+
+@pytest.mark.parametrize("hooks", [False, True])
+def test_resnet50_epilogue_reductions_all_used(dph_native, monkeypatch, hooks):
+    """ResNet-50 training step: 44 of the 53 BatchNorm backward reductions run in convolution epilogues (bn1 of the
+    13 stride-1 conv2 blocks, every bn2, every bn3 but the last), and the gradients match the unfused reductions.
+    BatchNorm shifts at 3, as in tests/test_whole_net_grad_gpu.py: with the default init a random bf16 ResNet-50
+    amplifies any change of fp32 summation order layer over layer (there: bf16 vs fp32 decorrelate completely).
+    hooks: a full backward pre-hook on every block, as the FSDP engine installs (parallel/fsdp.py) -- the blocks then
+    see aliases of each other's outputs, and the hand-off must still find them (models/resnet.py BnHandoff)."""
+    from distributed_pytorch_hpc_amd.models.resnet import Bottleneck, resnet50
+
+    torch.manual_seed(0)
+    model = resnet50(num_classes=10, channels_last=True).to(DEV).to(torch.bfloat16)
+    if hooks:
+        for m in model.modules():
+            if isinstance(m, Bottleneck):
+                m.register_full_backward_pre_hook(lambda mod, g: None)
+    for m in model.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.bias.data.fill_(3.0)
+    x = torch.randn(2, 3, 64, 64, device=DEV, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+    cnt = _Count(monkeypatch)
+    _, g0 = _grads(model, x, monkeypatch, False)
+    _, g1 = _grads(model, x, monkeypatch, True)
+    assert cnt.used == 44
+    agg = rel_err(torch.cat([g1[n].flatten() for n in g0]), torch.cat([g0[n].flatten() for n in g0]))
+    assert agg < 5e-3, agg
+    for n in g0:
+        if "conv" in n or "downsample.0" in n:
+            assert rel_err(g1[n], g0[n]) < 5e-2, n
+
+
+@pytest.mark.parametrize("N", [64, 256])
+@pytest.mark.parametrize("reduce", [False, True])
+def test_masked_residual_add_is_bitwise_the_materialised_add(dph_native, N, reduce):
+    """ts_gemm_nt_addmask / ts_gemm_nt_bnred(add_mask=): A B^T + add * bits equals the plain add of the materialised
+    bf16 masked gradient bit for bit (and the reduction partials match too)."""
+    torch.manual_seed(N)
+    ops = torch.ops.dph
+    M, K = 333, 128
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = (torch.randn(N, K, device=DEV) * 0.1).to(torch.bfloat16)
+    dy = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    bits = torch.randint(0, 256, (M * N // 8,), device=DEV, dtype=torch.uint8)
+    dres = torch.where(_mask(dy, bits=bits), dy, torch.zeros_like(dy))
+    ref = ops.ts_gemm_nt(a, b, 0, 0, dres)
+    if not reduce:
+        assert torch.equal(ops.ts_gemm_nt_addmask(a, b, dy, bits), ref)
+        return
+    x = torch.randn(M, N, device=DEV, dtype=torch.bfloat16)
+    mean, invstd = x.float().mean(0), torch.rsqrt(x.float().var(0, unbiased=False) + 1e-5)
+    xbits = torch.randint(0, 256, (M * N // 8,), device=DEV, dtype=torch.uint8)
+    c1, p1 = ops.ts_gemm_nt_bnred(a, b, 0, 0, dy, 0, x, mean, invstd, None, xbits, bits)
+    c0, p0 = ops.ts_gemm_nt_bnred(a, b, 0, 0, dres, 0, x, mean, invstd, None, xbits)
+    assert torch.equal(c1, ref) and torch.equal(c0, ref)
+    assert torch.equal(p1, p0)
+
+
+def test_identity_blocks_residual_mask_handoff_bitwise(dph_native, monkeypatch):
+    """bn3 handing conv1 its dy + ReLU bits (DPH_RES_MASK=1, default) instead of the masked copy changes no bit of any
+    gradient."""
+    import importlib
+
+    R = importlib.import_module("distributed_pytorch_hpc_amd.models.resnet")
+    torch.manual_seed(0)
+    blocks = [R.Bottleneck(256, 64), R.Bottleneck(256, 64), R.Bottleneck(256, 64)]
+    R.link_bn_handoff(blocks)
+    model = torch.nn.Sequential(*blocks).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(4, 256, 14, 14, device=DEV, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+    out = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("DPH_RES_MASK", v)
+        out.append(_grads(model, x, monkeypatch, True))
+    (gx0, g0), (gx1, g1) = out
+    assert torch.equal(gx0, gx1)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
