@@ -125,9 +125,9 @@ __global__ __launch_bounds__(FIN_NT) void bn_finalize_k(const float* __restrict_
                                                        float eps, float* __restrict__ mean_out,
                                                        float* __restrict__ invstd_out, float* __restrict__ scale,
                                                        float* __restrict__ shift, int64_t* __restrict__ nbt) {
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;   // num_batches_tracked, one launch fewer
   __shared__ float sh[3][FIN_NT];
   const int c = blockIdx.x * 8 + (threadIdx.x & 7), grp = threadIdx.x >> 3;
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;   // num_batches_tracked, one launch fewer
   Stat acc = {0.f, 0.f, 0.f};
   for (int g0 = grp; g0 < G; g0 += FIN_UNROLL * FIN_GROUPS) {
     Stat st[FIN_UNROLL];
@@ -205,20 +205,33 @@ __global__ __launch_bounds__(FIN_NT) void bn_merge_k(const float* __restrict__ p
 // y = act(x * scale + shift [+ res]).  The grid stride (gridDim.x * 256 vectors) is a multiple of ch8 = C / 8 (a
 // power of two <= 256), so a thread's channel chunk never changes: its 8 scales / shifts are loaded once, into
 // registers, instead of per element from L1.  MASK: also store [y > 0] of the vector's 8 elements as one byte.
-template <typename T, bool RES, bool RELU, bool MASK = false>
+// RESBN: the residual is itself a BatchNorm output, applied here -- res = round(z * rscale + rshift) from the raw z
+// (rss = its [scale | shift]) -- so a projection shortcut's normalised activation is never written (bitwise the
+// unfused pair: the same fmaf and the same rounding to T before the add).
+template <typename T, bool RES, bool RELU, bool MASK = false, bool RESBN = false>
 __global__ __launch_bounds__(BN_NT) void bn_apply_k(const T* __restrict__ x, const T* __restrict__ res,
                                                     const float* __restrict__ scale, const float* __restrict__ shift,
                                                     T* __restrict__ y, int64_t nvec, int ch8,
-                                                    uint8_t* __restrict__ mask = nullptr) {
+                                                    uint8_t* __restrict__ mask = nullptr,
+                                                    const float* __restrict__ rss = nullptr) {
   const int64_t v0 = (int64_t)blockIdx.x * BN_NT + threadIdx.x;
   const int c0 = (int)(v0 % ch8) * 8;
-  float sc[8], sf[8];
+  float sc[8], sf[8], rsc[8], rsf[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { sc[i] = scale[c0 + i]; sf[i] = shift[c0 + i]; }
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = scale[c0 + i];
+    sf[i] = shift[c0 + i];
+    rsc[i] = RESBN ? rss[c0 + i] : 0.f;
+    rsf[i] = RESBN ? rss[ch8 * 8 + c0 + i] : 0.f;
+  }
   for (int64_t v = v0; v < nvec; v += (int64_t)gridDim.x * BN_NT) {
     float a[8], rr[8];
     Vec8<T>::load(x + v * 8, a);
     if (RES) Vec8<T>::load(res + v * 8, rr);
+    if constexpr (RESBN) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rr[i] = (float)from_f32<T>(fmaf(rr[i], rsc[i], rsf[i]));
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float t = fmaf(a[i], sc[i], sf[i]);
@@ -337,6 +350,37 @@ __global__ __launch_bounds__(FIN_NT) void bn_bwd_finalize_k(const float* __restr
   coef[c] = gw * invstd[c];           // dx = coef * (dz - sum_dz / M - xhat * sum_dzx / M)
   coef[C + c] = a / count;
   coef[2 * C + c] = b / count;
+}
+
+// Sum G (thousands of) backward partials [G][2C] into gridDim.y segment rows [S][2C] (block = 8 channels x one
+// segment; 128 thread groups, then an LDS tree): the convolution-epilogue partials come one per 128-row tile, and
+// bn_bwd_finalize_k alone is latency-bound on them (8 blocks at C = 64 walking 6 272 rows: ~10 us per BatchNorm).
+__global__ __launch_bounds__(FIN_NT) void bn_bwd_merge_k(const float* __restrict__ part, int G, int C,
+                                                        float* __restrict__ out) {
+  __shared__ float sh[2][FIN_NT];
+  const int c = blockIdx.x * 8 + (threadIdx.x & 7), grp = threadIdx.x >> 3;
+  const int S = gridDim.y, sgm = blockIdx.y;
+  const int g_beg = (int)((int64_t)G * sgm / S), g_end = (int)((int64_t)G * (sgm + 1) / S);
+  float a = 0.f, b = 0.f;
+  for (int g = g_beg + grp; g < g_end; g += FIN_GROUPS) {
+    a += part[(int64_t)g * 2 * C + c];
+    b += part[(int64_t)g * 2 * C + C + c];
+  }
+  sh[0][threadIdx.x] = a;
+  sh[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int half = FIN_GROUPS / 2; half > 0; half >>= 1) {
+    if (grp < half) {
+      a += sh[0][threadIdx.x + half * 8];
+      b += sh[1][threadIdx.x + half * 8];
+      sh[0][threadIdx.x] = a;
+      sh[1][threadIdx.x] = b;
+    }
+    __syncthreads();
+  }
+  if (grp != 0) return;
+  out[(int64_t)sgm * 2 * C + c] = a;
+  out[(int64_t)sgm * 2 * C + C + c] = b;
 }
 
 template <typename T, bool RELU, bool DRES, bool XMASK, bool BMASK = false>
@@ -496,6 +540,16 @@ void bn_apply(const void* x, const void* res, const float* scale, const float* s
   });
 }
 
+void bn_apply_resbn(const void* x, const void* z, const float* ss, const float* zss, void* y, uint8_t* relu_mask,
+                    int64_t M, int64_t C, int dt, hipStream_t st) {
+  const int64_t nvec = M * C / 8;
+  const dim3 grid(stream_grid(nvec, BN_NT));
+  DPH_DISPATCH_FLOAT(dt, T, {
+    hipLaunchKernelGGL((bn_apply_k<T, true, true, true, true>), grid, dim3(BN_NT), 0, st, (const T*)x, (const T*)z,
+                       ss, ss + C, (T*)y, nvec, (int)(C / 8), relu_mask, zss);
+  });
+}
+
 void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
             void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dt,
             int pdt, hipStream_t st, const float* xmask_ss, const uint8_t* relu_mask, const float* pre_part,
@@ -508,8 +562,17 @@ void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, con
   float* coef = workspace + 2 * (int64_t)G * C;  // [3C]
   const size_t shs = 2 * BN_NT * 8 * sizeof(float);
   if (pre_part != nullptr) {   // reduced by the input-gradient epilogue that produced dy (kernels.h BnRed)
-    part = pre_part;
-    G = pre_groups;
+    // thousands of per-tile rows: merged first into S segment rows (>= 4 rows per thread, as bn_fwd_train does
+    // with the forward's epilogue statistics) in the reduction pass's workspace (G >= S rows of 2C)
+    const int S = std::min(std::min(G, 64), (pre_groups + 4 * FIN_GROUPS - 1) / (4 * FIN_GROUPS));
+    if (S > 1) {
+      hipLaunchKernelGGL(bn_bwd_merge_k, dim3((unsigned)(C / 8), (unsigned)S), dim3(FIN_NT), 0, st, pre_part,
+                         pre_groups, (int)C, workspace);
+      G = S;
+    } else {
+      part = pre_part;
+      G = pre_groups;
+    }
   } else {
 #define DPH_BN_RED(R_, X_, B_)                                                                                     \
   hipLaunchKernelGGL((bn_bwd_reduce_k<T, R_, X_, B_>), dim3(G), dim3(BN_NT), shs, st, (const T*)dy, (const T*)y,  \
@@ -523,12 +586,13 @@ void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, con
 #undef DPH_BN_RED
   }
   const dim3 fg((unsigned)(C / 8));
-  if (pdt == kBF16)
+  if (pdt == kBF16) {
     hipLaunchKernelGGL((bn_bwd_finalize_k<bf16>), fg, dim3(FIN_NT), 0, st, part, G, (int)C, (float)M, (const bf16*)w,
                        invstd, (bf16*)dw, (bf16*)db, coef);
-  else
+  } else {
     hipLaunchKernelGGL((bn_bwd_finalize_k<float>), fg, dim3(FIN_NT), 0, st, part, G, (int)C, (float)M,
                        (const float*)w, invstd, (float*)dw, (float*)db, coef);
+  }
   const int64_t nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, BN_NT));
 #define DPH_BN_DX(R_, D_, X_, B_)                                                                                 \

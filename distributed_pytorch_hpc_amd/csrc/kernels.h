@@ -240,6 +240,11 @@ void bn_fwd_train(const void* x, const void* res, void* y, const void* w, const 
 // relu_mask (optional, ReLU only): also write [y > 0] as bits, one byte per 8-channel vector ([M * C / 8] bytes).
 void bn_apply(const void* x, const void* res, const float* scale, const float* shift, void* y, int64_t M, int64_t C,
               bool relu, int dtype, hipStream_t stream, uint8_t* relu_mask = nullptr);
+// y = relu(x * scale + shift + round(z * zscale + zshift)) and its [y > 0] bits (ss / zss: fp32 [scale C | shift C]):
+// a BatchNorm + ReLU whose residual is another BatchNorm's output (ResNet's projection shortcut), both applied in one
+// pass, bitwise the unfused pair.
+void bn_apply_resbn(const void* x, const void* z, const float* ss, const float* zss, void* y, uint8_t* relu_mask,
+                    int64_t M, int64_t C, int dtype, hipStream_t stream);
 // xmask_ss (optional, fp32 [scale | shift] of the forward): ReLU mask from x instead of reading y.
 // relu_mask (optional): the forward's bit mask instead of y (takes precedence over xmask_ss).
 // pre_part (optional): the reduction partials [pre_groups][2C] from the producer's epilogue (BnRed): no reduction pass.

@@ -1226,6 +1226,25 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_fwd(const Tensor& x, const c10
   return {y, mean, invstd, ss};
 }
 
+// relu(BN_a(x) + BN_b(z)) from both BatchNorms' forward [scale | shift] (bn_act_fwd with apply=False), plus the
+// [y > 0] bits into relu_mask (uint8 [M * C / 8]).
+Tensor bn_act_apply_resbn(const Tensor& x, const Tensor& ss, const Tensor& z, const Tensor& zss, Tensor relu_mask) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  const int64_t C = bn_channels(x), M = x.numel() / C;
+  check_like(z, x, "z");
+  TORCH_CHECK(ss.scalar_type() == at::kFloat && zss.scalar_type() == at::kFloat && ss.numel() == 2 * C &&
+                  zss.numel() == 2 * C && ss.is_contiguous() && zss.is_contiguous(),
+              "bn_act_apply_resbn: fp32 [scale | shift] of 2C each");
+  TORCH_CHECK(relu_mask.scalar_type() == at::kByte && relu_mask.is_contiguous() && relu_mask.numel() == M * C / 8 &&
+                  relu_mask.device() == x.device(),
+              "bn_act_apply_resbn: relu_mask must be a contiguous uint8 [M * C / 8]");
+  auto y = at::empty_like(x);
+  dph::bn_apply_resbn(x.data_ptr(), z.data_ptr(), ss.data_ptr<float>(), zss.data_ptr<float>(), y.data_ptr(),
+                      relu_mask.data_ptr<uint8_t>(), M, C, dt_code(x), cur_stream());
+  return y;
+}
+
 Tensor bn_act_apply(const Tensor& x, const c10::optional<Tensor>& res, const Tensor& scale, const Tensor& shift,
                     bool relu) {
   check_cuda(x, "x");
@@ -1637,6 +1656,7 @@ TORCH_LIBRARY(dph, m) {
         "Tensor(d!)? relu_mask_out=None, bool apply=True) "
         "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
+  m.def("bn_act_apply_resbn(Tensor x, Tensor ss, Tensor z, Tensor zss, Tensor(a!) relu_mask) -> Tensor");
   m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "
         "bool need_dwb, Tensor? xmask_ss=None, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, "
         "Tensor? relu_mask=None, Tensor? pre_part=None) "
@@ -1713,6 +1733,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("bn_act_fwd", &bn_act_fwd);
   m.impl("bn_act_apply", &bn_act_apply);
   m.impl("bn_act_bwd", &bn_act_bwd);
+  m.impl("bn_act_apply_resbn", &bn_act_apply_resbn);
   m.impl("car_allreduce", &car_allreduce_op);
   m.impl("car_flag", &car_flag_op);
   m.impl("car_poison", &car_poison_op);

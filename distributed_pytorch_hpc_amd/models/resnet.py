@@ -19,7 +19,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.batchnorm import bn_relu_conv1x1, bn_relu_conv1x1_ok
+from ..ops.batchnorm import bn_dual_act, bn_relu_conv1x1, bn_relu_conv1x1_ok
 from ..ops.conv import (BnGradSlot, Conv1x1, Conv3x3, GradSlot, StatsSlot, StemConv2d, StridedConv2d, grad_tap,
                         strided_native_ok)
 from ..ops.pool import MaxPool2d
@@ -120,21 +120,30 @@ class Bottleneck(nn.Module):
         hand = getattr(self, "_dph_handoff", None)
         rin = hand.take(x) if hand is not None and slot is not None else None
         out = self.bn1(self.conv1(x, grad_slot=slot, stats_slot=s1, bn_slot=rin), stats_slot=s1, bn_slot=r1)
+        z = dbn = None
         if self.downsample is None:
             idt, res_slot = x, slot
         else:
             # built after conv1 / bn1, so autograd runs the downsample branch's backward (ending in the tap) before
             # conv1's: the tap parks the branch's gradient of x for conv1's dgrad epilogue (no separate add over x)
             ds = self.downsample[0]
+            if (len(self.downsample) == 2 and isinstance(self.downsample[1], BatchNormAct2d)
+                    and isinstance(ds, (Conv1x1, StridedConv2d))):
+                # projection shortcut: the downsample BatchNorm takes its statistics from the convolution's epilogue
+                # and is applied inside bn3's apply pass (ops.batchnorm.bn_dual_act) -- its output never written
+                dbn = self.downsample[1]
+                sds = StatsSlot() if dbn.training else None
             if (slot is not None and slot.consumer and isinstance(ds, StridedConv2d) and ds.kernel_size == (1, 1)
                     and ds.stride == (2, 2) and strided_native_ok(x, ds)):
                 # strided 1x1 downsample: its sub-image input gradient goes to conv1's epilogue (added at the even
                 # pixels), so no zero-filled full-size gradient of x is ever written
                 slot.armed = True
-                idt = self.downsample[1](ds(x, grad_slot=slot))
+                z = ds(x, stats_slot=sds if dbn is not None else None, grad_slot=slot)
             else:
                 tapped = grad_tap(x, slot) if slot is not None and slot.consumer else x
-                idt = self.downsample(tapped)
+                z = ds(tapped, stats_slot=sds) if dbn is not None else ds(tapped)
+            if dbn is None:
+                idt, z = self.downsample[1:](z), None
             res_slot = None
         s2 = StatsSlot() if isinstance(self.conv2, (Conv3x3, StridedConv2d)) and self.bn2.training else None
         if isinstance(self.conv2, Conv3x3):
@@ -147,7 +156,10 @@ class Bottleneck(nn.Module):
             out = bn_relu_conv1x1(self.bn2, self.conv3, out, s2, s3)
         else:
             out = self.conv3(self.bn2(out, stats_slot=s2, bn_slot=r2), stats_slot=s3, bn_slot=r2)
-        y = self.bn3(out, idt, residual_grad_slot=res_slot, stats_slot=s3, bn_slot=r3)
+        if z is not None:
+            y = bn_dual_act(self.bn3, dbn, out, z, s3, sds, r3)
+        else:
+            y = self.bn3(out, idt, residual_grad_slot=res_slot, stats_slot=s3, bn_slot=r3)
         if hand is not None:
             hand.put(y, r3)   # for the next block's conv1
         return y

@@ -86,6 +86,11 @@ def _bn_act_apply(x, res, scale, shift, relu):
     return torch.empty_like(x)
 
 
+@register_fake("dph::bn_act_apply_resbn")
+def _bn_act_apply_resbn(x, ss, z, zss, relu_mask):
+    return torch.empty_like(x)
+
+
 @register_fake("dph::bn_act_bwd")
 def _bn_act_bwd(dy, y, x, mean, invstd, w, relu, need_dres, need_dwb, xmask_ss=None, dw_out=None, db_out=None,
                 relu_mask=None, pre_part=None):

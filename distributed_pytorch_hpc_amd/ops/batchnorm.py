@@ -103,6 +103,89 @@ class _BNActFn(torch.autograd.Function):
                 None, None, None, None, None, None, None)
 
 
+def _direct_pair(wp, bp, need_wb: bool) -> bool:
+    """Write dgamma / dbeta straight into engine-owned gradient buckets (parallel/data_parallel.py main_grad views)
+    on the parameters' first gradient of the step."""
+    return bool(need_wb and wp is not None and bp is not None and _DIRECT and all(
+        getattr(p, "main_grad", None) is not None and not getattr(p, "_dph_accum", True)
+        and p.main_grad.is_contiguous() and p.main_grad.dtype == p.dtype for p in (wp, bp)))
+
+
+def _mark_direct(wp, bp):
+    for p in (wp, bp):
+        p._dph_accum = True
+        p._dph_grad_ready()
+
+
+class _BNDualActFn(torch.autograd.Function):
+    """relu(bn_a(x) + bn_b(z)) for two training-mode BatchNorms: a BatchNorm + residual + ReLU whose residual is itself
+    a BatchNorm's output -- ResNet's projection shortcut, bn3(conv3(.)) + bn(downsample(.)).
+
+    Forward: both BatchNorms' statistics (from the producing convolutions' epilogues when given) and running-stat
+    updates, then ONE apply pass that reads x and z and writes y and its ReLU bits (csrc/batchnorm.hip bn_apply_k
+    RESBN): the shortcut's normalised activation is never written or re-read.  Backward: the gradient reaching both
+    BatchNorm outputs is dy under the ReLU bits, so each BatchNorm's backward takes dy and the bits directly (no
+    masked residual-gradient copy is written); bn_a's reduction may come from the consumer's epilogue (bn_slot)."""
+
+    @staticmethod
+    def forward(ctx, x, z, wa, ba, rma, rva, wb, bb, rmb, rvb, mom_a, eps_a, mom_b, eps_b, pre_a, pre_b, nbt_a, nbt_b,
+                bn_slot):
+        ops = _lib.ops()
+        _, mean_a, inv_a, ss_a = ops.bn_act_fwd(x, None, wa, ba, rma, rva, mom_a, eps_a, True, pre_a, nbt_a, None,
+                                                False)
+        _, mean_b, inv_b, ss_b = ops.bn_act_fwd(z, None, wb, bb, rmb, rvb, mom_b, eps_b, False, pre_b, nbt_b, None,
+                                                False)
+        bits = x.new_empty((x.numel() // 8,), dtype=torch.uint8)
+        y = ops.bn_act_apply_resbn(x, ss_a, z, ss_b, bits)
+        ctx.save_for_backward(x, z, bits, mean_a, inv_a, mean_b, inv_b, wa, wb)
+        ctx.params = (wa, ba, wb, bb)
+        ctx.bn_slot = bn_slot if bn_slot is not None and x.dtype == torch.bfloat16 else None
+        if ctx.bn_slot is not None:
+            bn_slot.fill(x, mean_a, inv_a, None, bits)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, z, bits, mean_a, inv_a, mean_b, inv_b, wa, wb = ctx.saved_tensors
+        part = ctx.bn_slot.take(dy) if ctx.bn_slot is not None else None   # reduced by the consumer's epilogue
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        wpa, bpa, wpb, bpb = ctx.params
+        grads = []
+        for xx, mean, inv, w, wp, bp, pre, gi in ((x, mean_a, inv_a, wa, wpa, bpa, part, 2),
+                                                  (z, mean_b, inv_b, wb, wpb, bpb, None, 6)):
+            need_wb = ctx.needs_input_grad[gi] or ctx.needs_input_grad[gi + 1]
+            direct = _direct_pair(wp, bp, need_wb)
+            dx, _, dw, db = _lib.ops().bn_act_bwd(dy, xx, xx, mean, inv, w, True, False, need_wb, None,
+                                                  wp.main_grad if direct else None, bp.main_grad if direct else None,
+                                                  bits, pre)
+            if direct:
+                _mark_direct(wp, bp)
+                dw = db = None
+            grads.append((dx, dw if need_wb else None, db if need_wb else None))
+        (dxa, dwa, dba), (dxb, dwb, dbb) = grads
+        return (dxa, dxb, dwa, dba, None, None, dwb, dbb, None, None, None, None, None, None, None, None, None, None,
+                None)
+
+
+def bn_dual_act(bn_a: "BatchNormAct2d", bn_b: "BatchNormAct2d", x, z, stats_a=None, stats_b=None, bn_slot=None):
+    """``bn_a(x, residual=bn_b(z))`` with bn_a's ReLU and bn_b without activation (ResNet's projection-shortcut block
+    tail), as one fused op when both are training-mode, tracked, affine BatchNorms on eligible tensors
+    (_BNDualActFn); otherwise exactly the two module calls.  ``stats_a`` / ``stats_b``: statistics from the producing
+    convolutions' epilogues (ops.conv.StatsSlot); ``bn_slot``: bn_a's reduction from its consumer's epilogue."""
+    ok = (all(b.training and b.track_running_stats and b.affine and b.momentum is not None for b in (bn_a, bn_b))
+          and bn_a.act and not bn_b.act and x.shape == z.shape and x.stride() == z.stride() and x.dtype == z.dtype
+          and _native_ok(x, None) and _native_ok(z, None) and os.environ.get("DPH_BN_DUAL", "1") != "0")
+    if not ok:
+        return bn_a(x, bn_b(z, stats_slot=stats_b), stats_slot=stats_a, bn_slot=bn_slot)
+    ch = x.shape[1]
+    pre_a = stats_a.take(x.numel() // ch, ch) if stats_a is not None else None
+    pre_b = stats_b.take(z.numel() // ch, ch) if stats_b is not None else None
+    return _BNDualActFn.apply(x, z, bn_a.weight, bn_a.bias, bn_a.running_mean, bn_a.running_var, bn_b.weight,
+                              bn_b.bias, bn_b.running_mean, bn_b.running_var, bn_a.momentum, bn_a.eps, bn_b.momentum,
+                              bn_b.eps, pre_a, pre_b, bn_a.num_batches_tracked, bn_b.num_batches_tracked,
+                              bn_slot if torch.is_grad_enabled() else None)
+
+
 def batch_norm_act(x, weight, bias, running_mean, running_var, training: bool, momentum: float, eps: float,
                    residual=None, relu: bool = True, residual_grad_slot=None, stats_slot=None,
                    num_batches_tracked=None, bn_slot=None):

@@ -15,8 +15,10 @@ timeout -k 10 400 rocprofv3 --kernel-trace -d "$raw" -o p -- python examples/res
   --arch resnet50 --use-fsdp --amp --channels-last --batch-size "$B" --epochs 2 --steps-syn "$S" \
   > "$out/resnet_under_rocprof.log" 2>&1
 db=$(find "$raw" -name "*results.db" -print -quit)
-# the last epoch: S steps at ~0.1175 ms per image (trimmed so no part of the previous epoch is counted)
-ms=$(python -c "print(0.97 * $S * $B * 0.1135)")
-python benchmarks/prof_summary.py "$db" --steps "$S" --last-ms "$ms" --json "$out/summary.json" > "$out/summary.txt"
+# the last epoch: S steps at ~MS_PER_IMG ms per image (default 0.0905 = 11.05k img/s; trimmed so no part of the
+# previous epoch is counted)
+ms=$(python -c "print(0.97 * $S * $B * ${MS_PER_IMG:-0.0905})")
+python benchmarks/prof_summary.py "$db" --steps "$S" --last-ms "$ms" --step-marker "sgd_k" --run-steps $((2 * S)) \
+  --json "$out/summary.json" > "$out/summary.txt"
 head -n 40 "$out/summary.txt"
 rm -rf "$raw"

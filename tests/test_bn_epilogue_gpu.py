@@ -244,3 +244,84 @@ def test_identity_blocks_residual_mask_handoff_bitwise(dph_native, monkeypatch):
     assert torch.equal(gx0, gx1)
     for n in g0:
         assert torch.equal(g0[n], g1[n]), n
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+def test_projection_shortcut_dual_bn_bitwise(dph_native, monkeypatch, stride):
+    """bn3 + the downsample BatchNorm applied in one pass (ops.batchnorm.bn_dual_act, DPH_BN_DUAL=1 default) and
+    their backward on dy + ReLU bits: output, every gradient, the running statistics and the batch counters are
+    bitwise those of the two module calls (DPH_BN_DUAL=0)."""
+    import copy
+    import importlib
+
+    R = importlib.import_module("distributed_pytorch_hpc_amd.models.resnet")
+    torch.manual_seed(1)
+    cout = 128 * 4
+    ds = torch.nn.Sequential(R.conv1x1(256, cout, stride), R.BatchNormAct2d(cout, act=False))
+    base = R.Bottleneck(256, 128, stride, ds).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for m in base.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    x0 = torch.randn(4, 256, 14, 14, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("DPH_BN_DUAL", v)
+        blk = copy.deepcopy(base)
+        x = x0.clone().requires_grad_()
+        torch.manual_seed(5)
+        y = blk(x)
+        (y.float() * torch.randn_like(y.float())).sum().backward()
+        torch.cuda.synchronize()
+        bufs = {n: b.clone() for n, b in blk.named_buffers()}
+        res.append((y.detach().clone(), x.grad.clone(), {n: p.grad.clone() for n, p in blk.named_parameters()}, bufs))
+    (y0, gx0, g0, b0), (y1, gx1, g1, b1) = res
+    assert torch.equal(y0, y1)
+    assert torch.equal(gx0, gx1)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
+    for n in b0:
+        assert torch.equal(b0[n], b1[n]), n
+
+
+@pytest.mark.parametrize("C", [64, 256])
+def test_segment_merge_large_partial_counts(dph_native, C):
+    """Thousands of per-tile partials are merged into segment rows before the finalize, in both directions
+    (bn_merge_k / bn_bwd_merge_k): forward statistics / running stats / batch counter and backward dx / dgamma / dbeta
+    match the BatchNorm's own passes, and repeated launches agree bit for bit."""
+    torch.manual_seed(C)
+    ops = torch.ops.dph
+    B, H, W = 24, 100, 80                                    # M = 192 000 rows: 1 500 partials of 128 rows
+    M = B * H * W
+    a = torch.randn(M, 128, device=DEV, dtype=torch.bfloat16)
+    wt = (torch.randn(C, 128, device=DEV) * 0.1 + 0.01).to(torch.bfloat16)
+    y2, st = ops.ts_gemm_nt_stats(a, wt)
+    x = y2.view(B, H, W, C).permute(0, 3, 1, 2)
+    w = (1 + 0.1 * torch.randn(C, device=DEV)).to(torch.bfloat16)
+    bias = (0.1 * torch.randn(C, device=DEV)).to(torch.bfloat16)
+    outs = []
+    for pre in (None, st, st):
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        nbt = torch.zeros((), device=DEV, dtype=torch.long)
+        r = ops.bn_act_fwd(x, None, w, bias, rm, rv, 0.1, 1e-5, True, pre, nbt)
+        torch.cuda.synchronize()
+        outs.append((r, rm, rv, nbt))
+    (r0, rm0, rv0, n0), (r1, rm1, rv1, n1), (r2, rm2, rv2, n2) = outs
+    for g_, ref in zip(r1, r0):
+        assert rel_err(g_, ref) < 1e-4
+    assert rel_err(rm1, rm0) < 1e-4 and rel_err(rv1, rv0) < 1e-4 and n1.item() == n0.item() == 1
+    for g_, ref in zip(r2, r1):
+        assert torch.equal(g_, ref)
+    _, mean, invstd, ss = r1
+    A = torch.randn(M, 256, device=DEV, dtype=torch.bfloat16)
+    Bw = (torch.randn(C, 256, device=DEV) * 0.05).to(torch.bfloat16)
+    dy2, part = ops.ts_gemm_nt_bnred(A, Bw, 0, 0, None, 0, x, mean, invstd, ss, None)
+    dy = dy2.view(B, H, W, C).permute(0, 3, 1, 2)
+    ref = ops.bn_act_bwd(dy, x, x, mean, invstd, w, True, False, True, ss)
+    got = [ops.bn_act_bwd(dy, x, x, mean, invstd, w, True, False, True, ss, None, None, None, part) for _ in range(2)]
+    torch.cuda.synchronize()
+    for g_, r_ in zip(got[0], ref):
+        if r_.numel():
+            assert rel_err(g_, r_) < 1e-4
+    for g_, r_ in zip(got[1], got[0]):
+        assert torch.equal(g_, r_)
