@@ -40,6 +40,19 @@ __device__ __forceinline__ Stat chan_merge(Stat a, Stat b) {
   return {n, a.mean + d * f, a.m2 + b.m2 + d * d * a.n * f};
 }
 
+// A wave's lanes hold (row group lane >> 3, channel lane & 7): merge its 8 row groups per channel by an xor butterfly
+// (fixed order: deterministic), no LDS round trip or barrier.
+__device__ __forceinline__ Stat wave_merge_groups(Stat a) {
+  for (int off = 8; off < 64; off <<= 1) a = chan_merge(a, {__shfl_xor(a.n, off), __shfl_xor(a.mean, off),
+                                                            __shfl_xor(a.m2, off)});
+  return a;
+}
+
+__device__ __forceinline__ float wave_sum_groups(float v) {
+  for (int off = 8; off < 64; off <<= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
 // Per-block statistics: block b covers rows [b*rows_per_block, ...).  Partials: mean/m2 [G][C], n [G].
 template <typename T>
 __global__ __launch_bounds__(BN_NT) void bn_stats_k(const T* __restrict__ x, float* __restrict__ pmean,
@@ -111,7 +124,7 @@ __global__ __launch_bounds__(BN_NT) void bn_stats_k(const T* __restrict__ x, flo
 // issued FIN_UNROLL at a time so the chain is not one memory latency per partial), then a fixed-order LDS tree.
 // 1024 threads = 128 row groups of 8 channel lanes per 8-channel chunk: at C = 64 only 8 workgroups exist, so the
 // merge of up to 1024 partials is latency-bound; more groups per workgroup = fewer load rounds per thread.
-constexpr int FIN_NT = 1024;
+constexpr int FIN_NT = 1024;   // 16 waves: the shuffle trees below assume it (16 x 8 = 2 x 64 LDS entries)
 constexpr int FIN_GROUPS = FIN_NT / 8;
 // Partials loaded per group before they are merged: the chain over G <= 1024 partials is latency-bound (a finalize
 // ran ~10 us, most of it load rounds); 8 per round halves the rounds.  Merge order per thread is unchanged.
@@ -139,20 +152,18 @@ __global__ __launch_bounds__(FIN_NT) void bn_finalize_k(const float* __restrict_
 #pragma unroll
     for (int u = 0; u < FIN_UNROLL; ++u) acc = chan_merge(acc, st[u]);
   }
-  sh[0][threadIdx.x] = acc.n;
-  sh[1][threadIdx.x] = acc.mean;
-  sh[2][threadIdx.x] = acc.m2;
-  __syncthreads();
-  for (int half = FIN_GROUPS / 2; half > 0; half >>= 1) {
-    if (grp < half) {
-      const int o = threadIdx.x + half * 8;
-      acc = chan_merge(acc, {sh[0][o], sh[1][o], sh[2][o]});
-      sh[0][threadIdx.x] = acc.n;
-      sh[1][threadIdx.x] = acc.mean;
-      sh[2][threadIdx.x] = acc.m2;
-    }
-    __syncthreads();
+  // the 128 row groups: 8 per wave by shuffles, then the 16 waves' results through LDS (one barrier) into wave 0
+  acc = wave_merge_groups(acc);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane < 8) {
+    sh[0][wid * 8 + lane] = acc.n;
+    sh[1][wid * 8 + lane] = acc.mean;
+    sh[2][wid * 8 + lane] = acc.m2;
   }
+  __syncthreads();
+  if (wid != 0) return;
+  acc = chan_merge({sh[0][lane], sh[1][lane], sh[2][lane]}, {sh[0][64 + lane], sh[1][64 + lane], sh[2][64 + lane]});
+  acc = wave_merge_groups(acc);
   if (grp != 0) return;
   const float var = acc.n > 0.f ? acc.m2 / acc.n : 0.f;
   const float inv = rsqrtf(var + eps);
@@ -182,20 +193,18 @@ __global__ __launch_bounds__(FIN_NT) void bn_merge_k(const float* __restrict__ p
   Stat acc = {0.f, 0.f, 0.f};
   for (int g = g_beg + grp; g < g_end; g += FIN_GROUPS)
     acc = chan_merge(acc, Stat{pn[g], pmean[(int64_t)g * C + c], pm2[(int64_t)g * C + c]});
-  sh[0][threadIdx.x] = acc.n;
-  sh[1][threadIdx.x] = acc.mean;
-  sh[2][threadIdx.x] = acc.m2;
-  __syncthreads();
-  for (int half = FIN_GROUPS / 2; half > 0; half >>= 1) {
-    if (grp < half) {
-      const int o = threadIdx.x + half * 8;
-      acc = chan_merge(acc, {sh[0][o], sh[1][o], sh[2][o]});
-      sh[0][threadIdx.x] = acc.n;
-      sh[1][threadIdx.x] = acc.mean;
-      sh[2][threadIdx.x] = acc.m2;
-    }
-    __syncthreads();
+  // the 128 row groups: 8 per wave by shuffles, then the 16 waves' results through LDS (one barrier) into wave 0
+  acc = wave_merge_groups(acc);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane < 8) {
+    sh[0][wid * 8 + lane] = acc.n;
+    sh[1][wid * 8 + lane] = acc.mean;
+    sh[2][wid * 8 + lane] = acc.m2;
   }
+  __syncthreads();
+  if (wid != 0) return;
+  acc = chan_merge({sh[0][lane], sh[1][lane], sh[2][lane]}, {sh[0][64 + lane], sh[1][64 + lane], sh[2][64 + lane]});
+  acc = wave_merge_groups(acc);
   if (grp != 0) return;
   omean[(int64_t)sgm * C + c] = acc.mean;
   om2[(int64_t)sgm * C + c] = acc.m2;
@@ -331,18 +340,18 @@ __global__ __launch_bounds__(FIN_NT) void bn_bwd_finalize_k(const float* __restr
       b += pb[u];
     }
   }
-  sh[0][threadIdx.x] = a;
-  sh[1][threadIdx.x] = b;
-  __syncthreads();
-  for (int half = FIN_GROUPS / 2; half > 0; half >>= 1) {
-    if (grp < half) {
-      a += sh[0][threadIdx.x + half * 8];
-      b += sh[1][threadIdx.x + half * 8];
-      sh[0][threadIdx.x] = a;
-      sh[1][threadIdx.x] = b;
-    }
-    __syncthreads();
+  // the 128 row groups: 8 per wave by shuffles, then the 16 waves' sums through LDS (one barrier) into wave 0
+  a = wave_sum_groups(a);
+  b = wave_sum_groups(b);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane < 8) {
+    sh[0][wid * 8 + lane] = a;
+    sh[1][wid * 8 + lane] = b;
   }
+  __syncthreads();
+  if (wid != 0) return;
+  a = wave_sum_groups(sh[0][lane] + sh[0][64 + lane]);
+  b = wave_sum_groups(sh[1][lane] + sh[1][64 + lane]);
   if (grp != 0) return;
   if (dw) dw[c] = (PT)b;
   if (db) db[c] = (PT)a;
@@ -366,18 +375,18 @@ __global__ __launch_bounds__(FIN_NT) void bn_bwd_merge_k(const float* __restrict
     a += part[(int64_t)g * 2 * C + c];
     b += part[(int64_t)g * 2 * C + C + c];
   }
-  sh[0][threadIdx.x] = a;
-  sh[1][threadIdx.x] = b;
-  __syncthreads();
-  for (int half = FIN_GROUPS / 2; half > 0; half >>= 1) {
-    if (grp < half) {
-      a += sh[0][threadIdx.x + half * 8];
-      b += sh[1][threadIdx.x + half * 8];
-      sh[0][threadIdx.x] = a;
-      sh[1][threadIdx.x] = b;
-    }
-    __syncthreads();
+  // the 128 row groups: 8 per wave by shuffles, then the 16 waves' sums through LDS (one barrier) into wave 0
+  a = wave_sum_groups(a);
+  b = wave_sum_groups(b);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane < 8) {
+    sh[0][wid * 8 + lane] = a;
+    sh[1][wid * 8 + lane] = b;
   }
+  __syncthreads();
+  if (wid != 0) return;
+  a = wave_sum_groups(sh[0][lane] + sh[0][64 + lane]);
+  b = wave_sum_groups(sh[1][lane] + sh[1][64 + lane]);
   if (grp != 0) return;
   out[(int64_t)sgm * 2 * C + c] = a;
   out[(int64_t)sgm * 2 * C + C + c] = b;

@@ -261,6 +261,11 @@ void maxpool_s2_fwd(const void* x, void* y, uint8_t* tap, int64_t N, int64_t H, 
                     int dtype, hipStream_t stream);
 void maxpool_s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C, int k,
                     int dtype, hipStream_t stream);
+// maxpool_s2_bwd (bf16, C / 8 dividing 256) whose input is a training-mode BatchNorm + ReLU output: also that
+// BatchNorm's backward reduction partials (BnRed, mask from x) into r.part [maxpool_s2_bwd_bnred_blocks(...)][2C].
+int maxpool_s2_bwd_bnred_blocks(int64_t N, int64_t H, int64_t W, int64_t C);
+void maxpool_s2_bwd_bnred(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C,
+                          int k, const BnRed& r, hipStream_t stream);
 
 // SimpleUNet up-path, csrc/upsample.hip.  y: the ConvTranspose2d(2, 2) GEMM output [N*H*W, 4*Co] (columns (i, j, co));
 // skip / out / dcat / dskip channels-last.  out[n, oh, ow, :] = [bilinear(pixel_shuffle(y) + bias)(oh, ow), skip].

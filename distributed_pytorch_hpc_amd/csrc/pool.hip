@@ -14,6 +14,7 @@
 //             pass (rows / columns outside every window get 0).
 // Traffic: forward reads x (the 9-fold reuse stays in L2) and writes y + 1 byte/elem; backward reads dy + taps
 // (each about 2.25x, L2) and writes dx: both run near a device copy of x.
+#include "bn_epilogue.h"
 #include "dph_common.h"
 #include "kernels.h"
 
@@ -71,11 +72,16 @@ __global__ __launch_bounds__(PNT) void maxpool_fwd_k(const T* __restrict__ x, T*
   }
 }
 
-template <typename T, int K, int P>
+// BRED (bf16, the input is a BatchNorm + ReLU output -- the ResNet stem): also the BatchNorm backward's reduction
+// over the written gradient (kernels.h BnRed, mask from x; one partial row per block).  The grid stride is a multiple
+// of C / 8 (PNT % (C / 8) == 0, host-checked), so a thread's channel chunk is fixed.
+template <typename T, int K, int P, bool BRED = false>
 __global__ __launch_bounds__(PNT) void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ tap,
                                                      T* __restrict__ dx, int H, int W, int Ho, int Wo, int C,
-                                                     int64_t total) {
+                                                     int64_t total, BnRed bnr) {
   const int cv = C >> 3;
+  [[maybe_unused]] BnRedAcc<1> bra;
+  if constexpr (BRED) bra.init(bnr, (int)(((int64_t)blockIdx.x * PNT + threadIdx.x) % cv) * 8, C);
   for (int64_t i = (int64_t)blockIdx.x * PNT + threadIdx.x; i < total; i += (int64_t)gridDim.x * PNT) {
     const int c8 = (int)(i % cv);
     const int64_t p = i / cv;                       // input pixel n * H * W + iy * W + ix
@@ -104,6 +110,16 @@ __global__ __launch_bounds__(PNT) void maxpool_bwd_k(const T* __restrict__ dy, c
       }
     }
     Vec8<T>::store(dx + p * C + c8 * 8, acc);
+    if constexpr (BRED) {
+      bf16x8 g;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) g[k] = (bf16)acc[k];
+      bra.add(BnRedAcc<1>::load_x(bnr, p, C, c8 * 8), 0u, g);
+    }
+  }
+  if constexpr (BRED) {
+    __shared__ float red[(PNT / 64) * 64 * 16];   // finish(): nwv * cpr * 16 floats, cpr = C / 8 <= 64
+    bra.finish(red, cv, PNT / 64, blockIdx.x, C, 0, bnr.part);
   }
 }
 
@@ -135,8 +151,22 @@ void maxpool_s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int
   const dim3 grid(stream_grid(total, PNT));
   DPH_DISPATCH_FLOAT(dtype, T, {
     DPH_POOL_KP(k, hipLaunchKernelGGL((maxpool_bwd_k<T, K, P>), grid, dim3(PNT), 0, st, (const T*)dy, tap, (T*)dx,
-                                      (int)H, (int)W, (int)Ho, (int)Wo, (int)C, total));
+                                      (int)H, (int)W, (int)Ho, (int)Wo, (int)C, total, BnRed{}));
   });
+}
+
+int maxpool_s2_bwd_bnred_blocks(int64_t N, int64_t H, int64_t W, int64_t C) {
+  return stream_grid(N * H * W * (C / 8), PNT);
+}
+
+void maxpool_s2_bwd_bnred(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C,
+                          int k, const BnRed& r, hipStream_t st) {
+  const int64_t Ho = maxpool_s2_out(H, k), Wo = maxpool_s2_out(W, k);
+  const int64_t total = N * H * W * (C / 8);
+  if (total <= 0) return;
+  const dim3 grid(stream_grid(total, PNT));
+  DPH_POOL_KP(k, hipLaunchKernelGGL((maxpool_bwd_k<bf16, K, P, true>), grid, dim3(PNT), 0, st, (const bf16*)dy, tap,
+                                    (bf16*)dx, (int)H, (int)W, (int)Ho, (int)Wo, (int)C, total, r));
 }
 #undef DPH_POOL_KP
 

@@ -1057,6 +1057,48 @@ Tensor maxpool_s2_bwd(const Tensor& dy, const Tensor& tap, int64_t H, int64_t W,
   return dx;
 }
 
+// maxpool_s2_bwd whose input x is a training-mode BatchNorm + ReLU output (the ResNet stem): also that BatchNorm's
+// backward reduction partials [blocks, 2C] (mask from x with the forward's ss = [scale | shift]), for bn_act_bwd's
+// pre_part -- the BatchNorm then skips its reduction pass over dx and x.
+std::tuple<Tensor, Tensor> maxpool_s2_bwd_bnred(const Tensor& dy, const Tensor& tap, int64_t H, int64_t W, int64_t k,
+                                                const Tensor& x, const Tensor& mean, const Tensor& invstd,
+                                                const Tensor& ss) {
+  check_cuda(dy, "dy");
+  c10::DeviceGuard g(dy.device());
+  TORCH_CHECK(k == 2 || k == 3, "maxpool_s2_bwd_bnred: kernel 2 or 3");
+  TORCH_CHECK(dy.dim() == 4 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  dy.scalar_type() == at::kBFloat16,
+              "maxpool_s2_bwd_bnred: channels-last bf16 [N, C, Ho, Wo] gradient");
+  const int64_t N = dy.size(0), C = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0 && Ho == dph::maxpool_s2_out(H, (int)k) &&
+                  Wo == dph::maxpool_s2_out(W, (int)k),
+              "maxpool_s2_bwd_bnred: gradient shape / channel count (C / 8 must divide 256)");
+  TORCH_CHECK(tap.scalar_type() == at::kByte && tap.is_contiguous() && tap.dim() == 4 && tap.size(0) == N &&
+                  tap.size(1) == Ho && tap.size(2) == Wo && tap.size(3) == C && tap.device() == dy.device(),
+              "maxpool_s2_bwd_bnred: tap must be the forward's uint8 [N, Ho, Wo, C]");
+  TORCH_CHECK(x.dim() == 4 && x.size(0) == N && x.size(1) == C && x.size(2) == H && x.size(3) == W &&
+                  x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  x.device() == dy.device(),
+              "maxpool_s2_bwd_bnred: x must be the BatchNorm's bf16 channels-last [N, C, H, W] input");
+  TORCH_CHECK(mean.scalar_type() == at::kFloat && invstd.scalar_type() == at::kFloat && ss.scalar_type() == at::kFloat &&
+                  mean.numel() == C && invstd.numel() == C && ss.numel() == 2 * C && mean.is_contiguous() &&
+                  invstd.is_contiguous() && ss.is_contiguous(),
+              "maxpool_s2_bwd_bnred: fp32 mean / invstd [C], ss [2C]");
+  check_align16(dy, "dy");
+  check_align16(x, "x");
+  auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor part = at::empty({dph::maxpool_s2_bwd_bnred_blocks(N, H, W, C), 2 * C}, dy.options().dtype(at::kFloat));
+  dph::BnRed r;
+  r.x = x.data_ptr();
+  r.mean = mean.data_ptr<float>();
+  r.invstd = invstd.data_ptr<float>();
+  r.ss = ss.data_ptr<float>();
+  r.part = part.data_ptr<float>();
+  dph::maxpool_s2_bwd_bnred(dy.data_ptr(), tap.data_ptr<uint8_t>(), dx.data_ptr(), N, H, W, C, (int)k, r,
+                            cur_stream());
+  return {dx, part};
+}
+
 // ------------------------------------------------------------------------------------------------ UNet up-path
 // y2: [N*H*W, 4*Co] ConvTranspose2d(2, 2) GEMM output; skip: channels-last [N, Cs, Ho, Wo].
 // Returns channels-last [N, Co + Cs, Ho, Wo] = cat([bilinear(pixel_shuffle(y2) + bias, (Ho, Wo)), skip]).
@@ -1649,6 +1691,8 @@ TORCH_LIBRARY(dph, m) {
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
   m.def("channel_sum_into_(Tensor x, Tensor(a!) out) -> ()");
   m.def("maxpool_s2_bwd(Tensor dy, Tensor tap, int H, int W, int k) -> Tensor");
+  m.def("maxpool_s2_bwd_bnred(Tensor dy, Tensor tap, int H, int W, int k, Tensor x, Tensor mean, Tensor invstd, "
+        "Tensor ss) -> (Tensor, Tensor)");
   m.def("upcat_fwd(Tensor y2, Tensor? bias, Tensor skip, int H, int W) -> Tensor");
   m.def("upcat_bwd(Tensor dcat, int H, int W, int Co) -> (Tensor, Tensor)");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
@@ -1728,6 +1772,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("channel_sum", &channel_sum);
   m.impl("channel_sum_into_", &channel_sum_into_);
   m.impl("maxpool_s2_bwd", &maxpool_s2_bwd);
+  m.impl("maxpool_s2_bwd_bnred", &maxpool_s2_bwd_bnred);
   m.impl("upcat_fwd", &upcat_fwd);
   m.impl("upcat_bwd", &upcat_bwd);
   m.impl("bn_act_fwd", &bn_act_fwd);

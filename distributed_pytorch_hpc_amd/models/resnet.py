@@ -211,7 +211,9 @@ class ResNet(nn.Module):
         if isinstance(self.conv1, StemConv2d) and self.bn1.training:
             # the stem's GEMM epilogue hands bn1 its batch statistics (no statistics pass over the 112^2 activation)
             s = StatsSlot()
-            x = self.maxpool(self.bn1(self.conv1(x, stats_slot=s), stats_slot=s))
+            r0 = BnGradSlot() if isinstance(self.maxpool, MaxPool2d) else None   # reduction in the pool's gather
+            y = self.bn1(self.conv1(x, stats_slot=s), stats_slot=s, bn_slot=r0)
+            x = self.maxpool(y, bn_slot=r0) if r0 is not None else self.maxpool(y)
         else:
             x = self.maxpool(self.bn1(self.conv1(x)))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))

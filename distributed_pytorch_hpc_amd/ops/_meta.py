@@ -257,6 +257,14 @@ def _ts_gemm_nt_addmask(A, B, add, add_mask):
     return A.new_empty((A.shape[0], B.shape[0]))
 
 
+@register_fake("dph::maxpool_s2_bwd_bnred")
+def _maxpool_s2_bwd_bnred(dy, tap, H, W, k, x, mean, invstd, ss):
+    n, c = dy.shape[0], dy.shape[1]
+    blocks = min(max((n * H * W * (c // 8) + 255) // 256, 1), 2048)   # csrc/dph_common.h stream_grid
+    dx = dy.new_empty((n, c, H, W)).contiguous(memory_format=torch.channels_last)
+    return dx, dy.new_empty((blocks, 2 * c), dtype=torch.float32)
+
+
 @register_fake("dph::latmse_fwd")
 def _latmse_fwd(pred, target, n_global, lat_offset):
     return pred.new_empty((), dtype=torch.float32)

@@ -24,17 +24,25 @@ def maxpool3s2_native_ok(x: torch.Tensor) -> bool:
 
 class _MaxPoolS2Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k):
+    def forward(ctx, x, k, bn_slot=None):
         y, tap = _lib.ops().maxpool_s2_fwd(x, k)
         ctx.save_for_backward(tap)
-        ctx.hw, ctx.k = (x.shape[2], x.shape[3]), k
+        ctx.hw, ctx.k, ctx.bn_slot = (x.shape[2], x.shape[3]), k, bn_slot
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (tap,) = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
-        return _lib.ops().maxpool_s2_bwd(dy, tap, ctx.hw[0], ctx.hw[1], ctx.k), None
+        bn = ctx.bn_slot   # x is a BatchNorm + ReLU output: that BatchNorm's reduction runs in this gather
+        n, c = dy.shape[0], dy.shape[1]
+        if (bn is not None and bn.ss is not None and dy.dtype == torch.bfloat16 and 256 % (c // 8) == 0
+                and bn.usable(n * ctx.hw[0] * ctx.hw[1], c)):
+            dx, bn.part = _lib.ops().maxpool_s2_bwd_bnred(dy, tap, ctx.hw[0], ctx.hw[1], ctx.k, bn.x, bn.mean,
+                                                          bn.invstd, bn.ss)
+            bn.mark(dx)
+            return dx, None, None
+        return _lib.ops().maxpool_s2_bwd(dy, tap, ctx.hw[0], ctx.hw[1], ctx.k), None, None
 
 
 def max_pool3s2(x: torch.Tensor) -> torch.Tensor:
@@ -55,12 +63,14 @@ class MaxPool2d(nn.MaxPool2d):
     """``nn.MaxPool2d`` whose 3x3 / stride 2 / padding 1 and 2x2 / stride 2 cases run the channels-last HIP
     kernels."""
 
-    def forward(self, x):
+    def forward(self, x, bn_slot=None):
+        """``bn_slot`` (ops.conv.BnGradSlot): x is a training-mode BatchNorm + ReLU output consumed only here (the
+        ResNet stem); the BatchNorm's backward reduction then runs in this pooling's gradient gather."""
         k = {(3, 1): 3, (2, 0): 2}.get((_one(self.kernel_size), _one(self.padding)))
         fast = (k is not None and _one(self.stride) == 2 and _one(self.dilation) == 1 and not self.ceil_mode
                 and not self.return_indices)
         if fast and maxpool3s2_native_ok(x) and x.shape[2] >= k - 1 and x.shape[3] >= k - 1:
-            return _MaxPoolS2Fn.apply(x, k)
+            return _MaxPoolS2Fn.apply(x, k, bn_slot)
         return super().forward(x)
 
 

@@ -1,0 +1,20 @@
+#!/bin/bash
+# round 6: shuffle trees in the BatchNorm finalize / merge kernels + the stem BatchNorm's reduction in the max-pool
+# gather -- tests, A/B (v0 = round-6 BatchNorm changes off, v3 = default), kernel profile of the default
+set -o pipefail
+out=gpurun_out/r6bn9
+mkdir -p $out
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_bn_epilogue_gpu.py \
+  tests/test_whole_net_grad_gpu.py tests/test_strided_conv_gpu.py tests/test_kernels_gpu.py \
+  -k "bn or conv or bottleneck or slot or resnet or epilogue or mask or dual or whole or pool or unet" > $out/tests.log 2>&1 \
+  || { echo "tests failed"; grep -E "FAILED|Error|assert" $out/tests.log | head -30; tail -30 $out/tests.log; exit 1; }
+tail -1 $out/tests.log
+for r in 1 2; do
+  for v in 0 3; do
+    f=$([ $v -ge 1 ] && echo 1 || echo 0)
+    DPH_BN_EPILOGUE=$f DPH_RES_MASK=$f DPH_BN_DUAL=$f timeout -k 10 300 python -u bench.py --layout resnet-fsdp --steps 30 --warmup 5 > $out/bench_v${v}_r${r}.log 2>&1 || exit 1
+    echo "v$v r$r $(tail -1 $out/bench_v${v}_r${r}.log | cut -c60-140)"
+  done
+done
+timeout -k 10 500 bash scripts/prof_resnet.sh $out/prof 256 10 > /dev/null 2>&1 || { echo "prof failed"; exit 1; }
+head -12 $out/prof/summary.txt | cut -c1-150

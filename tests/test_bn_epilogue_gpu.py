@@ -168,8 +168,9 @@ def test_blocks_epilogue_on_matches_off(dph_native, monkeypatch, kind):
 
 @pytest.mark.parametrize("hooks", [False, True])
 def test_resnet50_epilogue_reductions_all_used(dph_native, monkeypatch, hooks):
-    """ResNet-50 training step: 44 of the 53 BatchNorm backward reductions run in convolution epilogues (bn1 of the
-    13 stride-1 conv2 blocks, every bn2, every bn3 but the last), and the gradients match the unfused reductions.
+    """ResNet-50 training step: 45 of the 53 BatchNorm backward reductions run in the consumers' gradient kernels (bn1
+    of the 13 stride-1 conv2 blocks, every bn2, every bn3 but the last in convolution epilogues; the stem's in the
+    max-pool gather), and the gradients match the unfused reductions.
     BatchNorm shifts at 3, as in tests/test_whole_net_grad_gpu.py: with the default init a random bf16 ResNet-50
     amplifies any change of fp32 summation order layer over layer (there: bf16 vs fp32 decorrelate completely).
     hooks: a full backward pre-hook on every block, as the FSDP engine installs (parallel/fsdp.py) -- the blocks then
@@ -190,7 +191,7 @@ def test_resnet50_epilogue_reductions_all_used(dph_native, monkeypatch, hooks):
     cnt = _Count(monkeypatch)
     _, g0 = _grads(model, x, monkeypatch, False)
     _, g1 = _grads(model, x, monkeypatch, True)
-    assert cnt.used == 44
+    assert cnt.used == 45
     agg = rel_err(torch.cat([g1[n].flatten() for n in g0]), torch.cat([g0[n].flatten() for n in g0]))
     assert agg < 5e-3, agg
     for n in g0:
@@ -325,3 +326,24 @@ def test_segment_merge_large_partial_counts(dph_native, C):
             assert rel_err(g_, r_) < 1e-4
     for g_, r_ in zip(got[1], got[0]):
         assert torch.equal(g_, r_)
+
+
+def test_stem_maxpool_gather_reduces_bn(dph_native, monkeypatch):
+    """ResNet stem: the max-pool's gradient gather also runs the stem BatchNorm's backward reduction
+    (maxpool_s2_bwd_bnred); dx is bitwise the plain gather and the partials sum to the fp64 reduction."""
+    torch.manual_seed(2)
+    ops = torch.ops.dph
+    N, C, H, W = 4, 64, 30, 26
+    x = (torch.randn(N, C, H, W, device=DEV) * 1.3 + 0.2).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    y, mean, invstd, ss = ops.bn_act_fwd(x, None, None, None, None, None, 0.1, 1e-5, True)
+    p, tap = ops.maxpool_s2_fwd(y, 3)
+    dy = torch.randn_like(p)
+    ref = ops.maxpool_s2_bwd(dy, tap, H, W, 3)
+    dx, part = ops.maxpool_s2_bwd_bnred(dy, tap, H, W, 3, x, mean, invstd, ss)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, ref)
+    x2 = x.permute(0, 2, 3, 1).reshape(-1, C)
+    sd, sdx = _ref_sums(dx.permute(0, 2, 3, 1).reshape(-1, C), x2, mean, invstd, _mask(x2, ss=ss))
+    got = part.double().sum(0)
+    assert rel_err(got[:C], sd) < 1e-5 and rel_err(got[C:], sdx) < 1e-5
