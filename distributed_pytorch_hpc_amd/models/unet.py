@@ -16,7 +16,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import BiasConv2d, BiasConvTranspose2d, StatsSlot
+from ..ops.conv import BiasConv2d, BiasConvTranspose2d, BnGradSlot, StatsSlot
 from ..ops.pool import MaxPool2d
 from ..ops.upsample import up_concat
 
@@ -28,12 +28,18 @@ class ConvBlock(nn.Sequential):
     instead of a statistics pass over the activation."""
 
     def forward(self, x):
-        for conv, bn in ((self[0], self[1]), (self[3], self[4])):
+        # the first BatchNorm's output is consumed only by the second convolution: its backward reduction runs in that
+        # convolution's input-gradient epilogue (ops.conv.BnGradSlot); the second's feeds pooling / skip / up-path
+        red = None
+        for i, (conv, bn) in enumerate(((self[0], self[1]), (self[3], self[4]))):
             if isinstance(conv, BiasConv2d) and isinstance(bn, BatchNormAct2d) and bn.training:
                 slot = StatsSlot()
-                x = bn(conv(x, stats_slot=slot), stats_slot=slot)
+                nxt = BnGradSlot() if i == 0 and isinstance(self[3], BiasConv2d) else None
+                x = bn(conv(x, stats_slot=slot, bn_slot=red), stats_slot=slot, bn_slot=nxt)
+                red = nxt
             else:   # modules swapped in by a wrapper (e.g. the halo convolutions of parallel/domain.py)
                 x = bn(conv(x))
+                red = None
         return x
 
 

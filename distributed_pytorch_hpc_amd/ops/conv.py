@@ -758,13 +758,15 @@ class BiasConv2d(nn.Conv2d):
     ones the gathered one-tap GEMM (output channels padded to a multiple of 64), everything else the stock MIOpen
     convolution."""
 
-    def forward(self, x, stats_slot: StatsSlot | None = None):
+    def forward(self, x, stats_slot: StatsSlot | None = None, bn_slot: BnGradSlot | None = None):
         """``stats_slot``: on the 3x3 kernel path the following BatchNorm's statistics come from this convolution's
-        epilogue (SimpleUNet's conv -> BN blocks, models/unet.py); otherwise the slot stays empty."""
+        epilogue (SimpleUNet's conv -> BN blocks, models/unet.py); otherwise the slot stays empty.  ``bn_slot``: x is
+        a training-mode BatchNorm + ReLU output consumed only here; its backward reduction then runs in this
+        convolution's input-gradient epilogue (3x3 kernel path)."""
         if _bias_conv3x3_ok(self, x):
             _lib.require()
             b = self.bias if self.bias.dtype in (torch.float32, torch.bfloat16) else self.bias.float()
-            return _Conv3x3Fn.apply(x, self.weight, stats_slot, b)
+            return _Conv3x3Fn.apply(x, self.weight, stats_slot, b, "dph", bn_slot)
         if _bias_conv3x3_padded_ok(self, x):
             # SimpleUNet's 65-channel input conv: MIOpen's igemm_fwd / igemm_wrw before (0.117 + 0.095 ms per step,
             # profiles/r4/unet_c3w_default/); the padded K costs 2x the MFMAs but keeps the BN-statistics epilogue

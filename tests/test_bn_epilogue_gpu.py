@@ -347,3 +347,22 @@ def test_stem_maxpool_gather_reduces_bn(dph_native, monkeypatch):
     sd, sdx = _ref_sums(dx.permute(0, 2, 3, 1).reshape(-1, C), x2, mean, invstd, _mask(x2, ss=ss))
     got = part.double().sum(0)
     assert rel_err(got[:C], sd) < 1e-5 and rel_err(got[C:], sdx) < 1e-5
+
+
+def test_unet_conv_block_first_bn_reduced_in_second_conv(dph_native, monkeypatch):
+    """SimpleUNet conv block: the first BatchNorm's backward reduction runs in the second 3x3 convolution's dgrad
+    epilogue (biased conv path); gradients match the BatchNorm's own reduction."""
+    from distributed_pytorch_hpc_amd.models.unet import conv_block
+
+    torch.manual_seed(4)
+    blk = conv_block(64, 128).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    x = torch.randn(2, 64, 24, 40, device=DEV, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+    cnt = _Count(monkeypatch)
+    gx0, g0 = _grads(blk, x, monkeypatch, False)
+    assert cnt.used == 0
+    gx1, g1 = _grads(blk, x, monkeypatch, True)
+    assert cnt.used == 1
+    assert rel_err(gx1, gx0) < 1e-2
+    for n in g0:
+        assert rel_err(g1[n], g0[n]) < 1e-2, n
