@@ -99,7 +99,8 @@ def parse(argv=None):
                     help="replay each step as one HIP graph after the warm-up (runtime/graphs.py; one rank only).  "
                          "Default: on for the one-rank unet-ddp layout, whose eager step is launch-bound (243 launches "
                          "in 3.25 ms: graph 1 229 / 1 232 samples/s at stdev 0.02 ms vs eager 1 044 / 1 230 at "
-                         "0.13-0.19 ms, profiles/r6/unet_graph/), off otherwise")
+                         "0.13-0.19 ms, profiles/r6/unet_graph/) and the one-rank resnet-fsdp layout (575 launches: "
+                         "11 505 / 11 516 vs 11 367 / 11 351 img/s eager, profiles/r6/resnet_graph/), off otherwise")
     ap.add_argument("--fp8", action="store_true",
                     help="opt-in FP8 GEMMs for the projections (ops/fp8.py; e4m3 activations/weights, e5m2 gradients, "
                          "LM head bf16). Reported with dtype 'bf16+fp8-gemm' -- not the bf16 headline number")
@@ -237,8 +238,8 @@ def main(argv=None):
                                          for b, tr, tx in res["samples"]]}
             log(f"[bench] xGMI all-reduce vs RCCL on {name}: crossover {res['crossover_bytes']} B")
     graph_info = {}
-    if args.graph is None:   # auto: the launch-bound one-rank SimpleUNet step replays as one graph
-        args.graph = args.layout == "unet-ddp" and world == 1 and not cpu and args.warmup >= 2
+    if args.graph is None:   # auto: the one-rank SimpleUNet / ResNet steps replay as one graph (fewer launch gaps)
+        args.graph = args.layout in ("unet-ddp", "resnet-fsdp") and world == 1 and not cpu and args.warmup >= 2
     if args.graph:
         if world > 1 or cpu:
             _fail(2, "--graph: whole-step graph capture is a one-rank GPU option")

@@ -63,3 +63,18 @@ def test_bench_more_gpus_than_visible_fails(tmp_path):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=100, cwd=str(tmp_path), env=env)
     assert p.returncode == 2, p.stderr[-2000:]
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.parametrize("layout", ["resnet-fsdp", "unet-ddp"])
+def test_bench_one_rank_conv_layouts_replay_graph(tmp_path, layout):
+    """The one-rank resnet-fsdp / unet-ddp layouts replay each timed step as one HIP graph by default (captured in the
+    warm-up); the loss stays finite and the line says so."""
+    extra = (["--arch", "resnet18", "--image-size", "64", "--micro-batch", "8"] if layout == "resnet-fsdp"
+             else ["--micro-batch", "1"])
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--layout", layout, "--steps", "3", "--warmup", "2",
+           "--quiet", "--no-telemetry"] + extra
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")][0]
+    assert r["n_gpus"] == 1 and r["value"] > 0 and "graph" in r, r
+    assert r["loss_last"] == r["loss_last"]   # not NaN
