@@ -727,6 +727,10 @@ void ts_gemm_nt(const void* A, const void* B, void* C, int64_t M, int64_t N, int
     conv3_gemm(A, B, C, M, N, K, lda, ldb, ldc, H, W, st, stats);   // (+ BatchNorm partials of the output)
     return;
   }
+  if (!c3 && D == nullptr && gemm1_lds_preferred(M, N, K, lda, ldb)) {   // deep-K 1x1: the LDS-DMA pipeline
+    convg_gemm(A, B, C, M, N, K, lda, ldb, ldc, gemm1_identity_geo(M), st, stats);   // (+ BatchNorm partials)
+    return;
+  }
   if (stats != nullptr && !c3) {   // BatchNorm statistics of the output (1x1 forward only)
     if (wide)
       ts_nt_launch<128, false, false, true>(nmb * (int)(N / 128), st, A, B, C, M, N, K, lda, ldb, ldc, H, W, cin,
@@ -760,6 +764,10 @@ void ts_gemm_nt_bnred(const void* A, const void* B, void* C, int64_t M, int64_t 
                       hipStream_t st, const uint8_t* dmask) {
   if (H > 0 && adds == 0) {   // 3x3 stride-1 input gradient on the LDS-DMA kernel
     conv3_gemm_bnred(A, B, C, M, N, K, lda, ldb, ldc, H, W, r, st);
+    return;
+  }
+  if (H == 0 && D == nullptr && dmask == nullptr && r.part != nullptr && gemm1_lds_preferred(M, N, K, lda, ldb)) {
+    conv3_gemm_bnred(A, B, C, M, N, K, lda, ldb, ldc, 0, 0, r, st);   // deep-K 1x1 on the LDS-DMA pipeline
     return;
   }
   const int nmb = (int)cdiv(M, TS_BM);

@@ -22,6 +22,8 @@
 //   * one raw s_barrier per K-step, counted vmcnt: STAGES - 1 K-steps stay in flight behind the MFMAs;
 //   * C tile through LDS, written as whole 16-B row segments; workgroups remapped XCD-aware with the N-tiles of one
 //     row block adjacent (they read the same shifted input rows from one L2); epilogues: + bias, BN statistics.
+#include <cstdlib>
+
 #include "bn_epilogue.h"
 #include "dph_common.h"
 #include "kernels.h"
@@ -64,7 +66,9 @@ __global__ __launch_bounds__(128 * WM, WM == 2 ? 2 : 1) void conv3_k(const bf16*
                                                                    float* __restrict__ stats,
                                                                    const void* __restrict__ bias, ConvGeo g,
                                                                    bool bias_bf16, BnRed bnr) {
-  static_assert(!BRED || (GEN == 0 && WM == 2 && !STATS), "BRED: stride-1 128-row tiles, no statistics");
+  // (GEN = 1 only with an identity destination map -- the one-tap plain GEMM of gemm1_identity_geo -- since the
+  // BatchNorm operands are fetched at the source row before the K-loop)
+  static_assert(!BRED || (GEN != 2 && WM == 2 && !STATS), "BRED: 128-row tiles, no statistics");
   constexpr int NWV = 2 * WM, NTH = 64 * NWV, BM = 64 * WM;
   constexpr int AIMG = BM * C3_ROWB, BIMG = BN * C3_ROWB, STG = AIMG + BIMG;
   constexpr int AI = BM / 8 / NWV;         // A DMA pieces (8 rows) per wave per K-step (4)
@@ -364,22 +368,49 @@ void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int
 
 void conv3_gemm_bnred(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                       int64_t ldb, int64_t ldc, int H, int W, const BnRed& r, hipStream_t st) {
-  // conv3_gemm's tile choice at WM = 2 (its only one for these shapes): 128-row tiles = the partial rows
-  const int cin = (int)(K / 9);
+  // conv3_gemm's tile choice at WM = 2 (its only one for these shapes): 128-row tiles = the partial rows.
+  // H = 0: the plain GEMM C = A B^T on the same kernel (one tap, identity geometry: gemm1_identity_geo).
+  const bool plain = H == 0;
+  const ConvGeo g = plain ? gemm1_identity_geo(M) : ConvGeo{};
+  const int cin = plain ? (int)K : (int)(K / 9);
   const int nmb = (int)cdiv(M, 128);
   const bool wide = N % 128 == 0 && (int64_t)nmb * (N / 128) >= 384;
-#define DPH_C3B(BN_, ST_, MODE_)                                                                                  \
-  hipLaunchKernelGGL((conv3_k<BN_, ST_, 2, false, 0, MODE_>), dim3(nmb * (int)(N / BN_)), dim3(256), 0, st,      \
+#define DPH_C3B(BN_, ST_, GEN_, MODE_)                                                                           \
+  hipLaunchKernelGGL((conv3_k<BN_, ST_, 2, false, GEN_, MODE_>), dim3(nmb * (int)(N / BN_)), dim3(256), 0, st,  \
                      (const bf16*)A, (const bf16*)B, (bf16*)C, (int)M, (int)N, (int)K, lda, ldb, ldc, H, W, cin,  \
-                     nullptr, nullptr, ConvGeo{}, false, r)
-  if (r.bits != nullptr) {
-    if (wide) DPH_C3B(128, 2, 2);
-    else DPH_C3B(64, 3, 2);
+                     nullptr, nullptr, g, false, r)
+#define DPH_C3B_W(GEN_, MODE_)             \
+  if (wide) DPH_C3B(128, 2, GEN_, MODE_); \
+  else DPH_C3B(64, 3, GEN_, MODE_)
+  if (plain) {
+    if (r.bits != nullptr) { DPH_C3B_W(1, 2); } else { DPH_C3B_W(1, 1); }
   } else {
-    if (wide) DPH_C3B(128, 2, 1);
-    else DPH_C3B(64, 3, 1);
+    if (r.bits != nullptr) { DPH_C3B_W(0, 2); } else { DPH_C3B_W(0, 1); }
   }
+#undef DPH_C3B_W
 #undef DPH_C3B
+}
+
+ConvGeo gemm1_identity_geo(int64_t M) {
+  // M images of 1 x 1 pixel, one tap at (0, 0), stored to the same row: the implicit GEMM degenerates to C = A B^T
+  ConvGeo g{};
+  g.Hs = g.Ws = g.Ho = g.Wo = g.Hd = g.Wd = 1;
+  g.sy = g.sx = g.ty = g.tx = 1;
+  g.ntaps = 1;
+  g.src_rows = M;
+  return g;
+}
+
+bool gemm1_lds_preferred(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
+  // ResNet-50's deep 1x1 convolutions (K >= 1024: layers 3-4) on small grids: the LDS-DMA pipeline hides the operand
+  // latency that bounds ts_nt_k there (fwd + stats 10-26 % faster, input gradient 20-27 %; K <= 512 ties or loses,
+  // profiles/r6/conv1x1_probe/probe.log)
+  static const bool off = [] {   // DPH_GEMM1_LDS=0: keep every 1x1 GEMM on ts_nt_k (A/B)
+    const char* e = std::getenv("DPH_GEMM1_LDS");
+    return e != nullptr && e[0] == '0';
+  }();
+  return !off && K >= 1024 && M > 0 && M < (int64_t(1) << 31) &&
+         convg_supported(M, N, K, lda, ldb, gemm1_identity_geo(M));
 }
 
 bool convg_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, const ConvGeo& g, bool chunk_taps) {

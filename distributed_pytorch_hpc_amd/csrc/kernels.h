@@ -183,6 +183,11 @@ void ts_gemm_nt_bnred(const void* A, const void* B, void* C, int64_t M, int64_t 
                       hipStream_t stream, const uint8_t* dmask = nullptr);
 void conv3_gemm_bnred(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda,
                       int64_t ldb, int64_t ldc, int H, int W, const BnRed& r, hipStream_t stream);
+// The one-tap identity geometry (ConvGeo below) that makes the LDS-DMA implicit GEMM a plain C = A B^T, and whether a
+// 1x1 convolution's GEMM runs better there than on ts_nt_k (deep-K shapes).
+struct ConvGeo;
+ConvGeo gemm1_identity_geo(int64_t M);
+bool gemm1_lds_preferred(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 // 3x3 implicit GEMM with an LDS-DMA pipeline (csrc/conv3x3.hip); ts_gemm_nt's H, W > 0 path when supported.
 bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,

@@ -34,7 +34,7 @@ def _ref_sums(c, x, mean, invstd, mask):
     return dz.sum(0), (dz * xh).sum(0)
 
 
-@pytest.mark.parametrize("form", ["1x1", "1x1_add", "1x1_sub", "3x3"])
+@pytest.mark.parametrize("form", ["1x1", "1x1_add", "1x1_sub", "3x3", "1x1_deep"])
 @pytest.mark.parametrize("N", [64, 128, 256])
 @pytest.mark.parametrize("mode", ["ss", "bits"])
 def test_ts_gemm_nt_bnred_matches_fp64(dph_native, form, N, mode):
@@ -44,7 +44,7 @@ def test_ts_gemm_nt_bnred_matches_fp64(dph_native, form, N, mode):
     ops = torch.ops.dph
     n_img, H, W = 3, 9, 13                                  # M = 351: two full 128-row blocks + a ragged one
     M = n_img * H * W
-    K = 128 if form != "3x3" else 64
+    K = {"3x3": 64, "1x1_deep": 1024}.get(form, 128)   # deep K: the LDS-DMA one-tap GEMM (gemm1_lds_preferred)
     a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
     if form == "3x3":
         b = (torch.randn(N, 9 * K, device=DEV) * 0.05).to(torch.bfloat16)
@@ -366,3 +366,23 @@ def test_unet_conv_block_first_bn_reduced_in_second_conv(dph_native, monkeypatch
     assert rel_err(gx1, gx0) < 1e-2
     for n in g0:
         assert rel_err(g1[n], g0[n]) < 1e-2, n
+
+
+@pytest.mark.parametrize("M,K,N", [(50176 // 8, 1024, 256), (12544 // 4 + 37, 2048, 512), (777, 1024, 128)])
+def test_deep_1x1_on_lds_dma_gemm(dph_native, M, K, N):
+    """Deep-K 1x1 GEMMs (K >= 1024) run on the LDS-DMA implicit GEMM with a one-tap identity geometry: the product
+    matches fp32, and the BatchNorm-statistics epilogue drives bn_act_fwd like its own statistics pass."""
+    torch.manual_seed(K + N)
+    ops = torch.ops.dph
+    a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    b = (torch.randn(N, K, device=DEV) * 0.03).to(torch.bfloat16)
+    y = ops.ts_gemm_nt(a, b)
+    ref = a.float() @ b.float().t()
+    assert rel_err(y, ref) < 1e-2
+    y2, st = ops.ts_gemm_nt_stats(a, b)
+    assert torch.equal(y2, y)
+    x = y2.view(1, M, 1, N).permute(0, 3, 1, 2)   # channels-last [1, N, M, 1] view of the [M, N] rows
+    r0 = ops.bn_act_fwd(x, None, None, None, None, None, 0.1, 1e-5, True)
+    r1 = ops.bn_act_fwd(x, None, None, None, None, None, 0.1, 1e-5, True, st)
+    for g_, r_ in zip(r1, r0):
+        assert rel_err(g_, r_) < 1e-4
