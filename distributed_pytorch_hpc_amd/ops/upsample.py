@@ -26,6 +26,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _lib
+from .conv import _main_grad_cl, bias_grad
 
 def _pair(v):
     return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
@@ -58,9 +59,19 @@ def _tall_skinny_ok(cin: int, co: int) -> bool:
     return cin % 64 == 0 and (4 * co) % 64 == 0
 
 
+class _Params:
+    """The module's parameters behind a non-tensor argument (autograd does not track it): the backward writes their
+    gradients straight into the engine's buckets (``main_grad``) instead of returning them."""
+
+    __slots__ = ("weight", "bias")
+
+    def __init__(self, weight, bias):
+        self.weight, self.bias = weight, bias
+
+
 class _UpConcatFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, skip):
+    def forward(ctx, x, weight, bias, skip, params=None):
         n, cin, h, w = x.shape
         co = weight.shape[1]
         x2 = x.permute(0, 2, 3, 1).reshape(n * h * w, cin)          # channels-last: a view
@@ -75,6 +86,7 @@ class _UpConcatFn(torch.autograd.Function):
         ctx.dims = (n, cin, h, w, co)
         ctx.has_bias = bias is not None
         ctx.ts = ts
+        ctx.params = params
         return out
 
     @staticmethod
@@ -87,17 +99,28 @@ class _UpConcatFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx2 = _lib.ops().ts_gemm_nt(dy2, wr) if ctx.ts else torch.matmul(dy2, wr.t())
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+        prm = ctx.params
         if ctx.needs_input_grad[1]:
-            if ctx.ts:   # dWr[ci, (i, j, co)] = X^T dY' over all pixels (split-pixel kernel, deterministic)
-                dwr = torch.empty((cin, 4 * co), device=x2.device, dtype=torch.float32)
-                _lib.ops().ts_gemm_tn_(dwr, x2, dy2, False)
-                dwr = dwr.to(x2.dtype)
+            # a channels-last ConvTranspose2d weight [ci, co, 2, 2] is laid out as [ci, (i, j, co)] = dWr: the engine's
+            # bucket view takes the weight-gradient kernel's output directly (no fp32 copy, permute or accumulate)
+            mg = _main_grad_cl(prm.weight, cin, 4 * co) if (ctx.ts and prm is not None) else None
+            if mg is not None:
+                w = prm.weight
+                _lib.ops().ts_gemm_tn_(mg, x2, dy2, bool(getattr(w, "_dph_accum", False)))
+                w._dph_accum = True
+                w._dph_grad_ready()
             else:
-                dwr = torch.matmul(x2.t(), dy2)
-            dw = dwr.view(cin, 2, 2, co).permute(0, 3, 1, 2).contiguous()
+                if ctx.ts:   # dWr[ci, (i, j, co)] = X^T dY' over all pixels (split-pixel kernel, deterministic)
+                    dwr = torch.empty((cin, 4 * co), device=x2.device, dtype=torch.float32)
+                    _lib.ops().ts_gemm_tn_(dwr, x2, dy2, False)
+                    dwr = dwr.to(x2.dtype)
+                else:
+                    dwr = torch.matmul(x2.t(), dy2)
+                dw = dwr.view(cin, 2, 2, co).permute(0, 3, 1, 2).contiguous()
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = _lib.ops().channel_sum(dy2.view(-1, co), torch.float32)
-        return dx, dw, db, dskip
+            # straight into the bias's bucket view when the engine owns it (bias_grad), else returned in fp32
+            db = bias_grad(prm.bias if prm is not None else None, dy2.view(-1, co), torch.float32)
+        return dx, dw, db, dskip, None
 
 
 def up_concat_reference(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> torch.Tensor:
@@ -117,5 +140,7 @@ def up_concat(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> torch.Tenso
     b = up.bias
     if b is not None and b.dtype != torch.float32:
         b = b.float()
+    # the parameters themselves for the direct bucket writes -- only when the GEMM operand is the weight itself
+    prm = _Params(up.weight, up.bias) if wt is up.weight and os.environ.get("DPH_UPCAT_DIRECT", "1") != "0" else None
     with torch.autocast("cuda", enabled=False):
-        return _UpConcatFn.apply(x if x.dtype == dt else x.to(dt), wt, b, skip)
+        return _UpConcatFn.apply(x if x.dtype == dt else x.to(dt), wt, b, skip, prm)
