@@ -80,6 +80,7 @@ def bias_grad(param, dy2: torch.Tensor, dtype):
     if (mg is not None and _DIRECT and not getattr(param, "_dph_accum", False) and mg.is_contiguous()
             and mg.dtype in (torch.float32, torch.bfloat16)):
         _lib.ops().channel_sum_into_(dy2, mg.view(-1))
+        param._dph_zeroed = False
         param._dph_accum = True
         param._dph_grad_ready()
         return None
@@ -89,11 +90,15 @@ def bias_grad(param, dy2: torch.Tensor, dtype):
 def zero_bias_grad(param, n: int, dtype, device):
     """The gradient of a bias that a following training-mode BatchNorm cancels: exactly zero, so no channel sum runs
     (SimpleUNet's 14 conv biases: 28 reduction launches per step).  Written into the engine's bucket view when
-    there is one (one fill, engine notified, None returned)."""
+    there is one (engine notified, None returned): one fill -- or none when the view lives in a persistent bucket
+    (``_dph_persistent_grad``: parallel/data_parallel.py) that an earlier step zeroed and no writer has touched since
+    (``_dph_zeroed``, cleared by every other write of the parameter's gradient), so it still holds the zeros."""
     mg = getattr(param, "main_grad", None) if param is not None else None
     if mg is not None and _DIRECT:
         if not getattr(param, "_dph_accum", False):
-            mg.zero_()
+            if not (getattr(param, "_dph_persistent_grad", False) and getattr(param, "_dph_zeroed", False)):
+                mg.zero_()
+                param._dph_zeroed = bool(getattr(param, "_dph_persistent_grad", False))
             param._dph_accum = True
         param._dph_grad_ready()
         return None
@@ -743,6 +748,7 @@ class _BiasConv1x1Fn(torch.autograd.Function):
             mg = getattr(p, "main_grad", None) if p is not None else None
             if mg is not None and _DIRECT and not getattr(p, "_dph_accum", False) and mg.is_contiguous():
                 mg.view(-1).copy_(gb)   # straight into the engine's bucket (as bias_grad does)
+                p._dph_zeroed = False
                 p._dph_accum = True
                 p._dph_grad_ready()
                 gb = None

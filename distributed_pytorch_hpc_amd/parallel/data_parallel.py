@@ -204,6 +204,8 @@ class DataParallelEngine:
                     v = param_view(self.flat_param[o:o + n], p)   # channels-last weights stay channels-last
                     v.copy_(p.data)
                     p.main_grad = param_view(self.flat_grad[o:o + n], p)
+                    p._dph_persistent_grad = True   # flat_grad lives as long as the engine (ops.conv.zero_bias_grad)
+                    p._dph_zeroed = False
                     p.data = v
                     p._dph_accum = False
                     p._dph_grad_ready = partial(self._on_grad_ready, p)
@@ -338,6 +340,7 @@ class DataParallelEngine:
         if g is None:
             return
         mg = p.main_grad
+        p._dph_zeroed = False
         with torch.no_grad():
             if p._dph_accum:
                 mg.add_(g)
