@@ -22,8 +22,6 @@
 //   * one raw s_barrier per K-step, counted vmcnt: STAGES - 1 K-steps stay in flight behind the MFMAs;
 //   * C tile through LDS, written as whole 16-B row segments; workgroups remapped XCD-aware with the N-tiles of one
 //     row block adjacent (they read the same shifted input rows from one L2); epilogues: + bias, BN statistics.
-#include <cstdlib>
-
 #include "bn_epilogue.h"
 #include "dph_common.h"
 #include "kernels.h"
@@ -391,6 +389,15 @@ void conv3_gemm_bnred(const void* A, const void* B, void* C, int64_t M, int64_t 
 #undef DPH_C3B
 }
 
+// off (ops/_lib.py applies DPH_GEMM1_LDS=0 through the gemm1_lds op): every 1x1 GEMM stays on ts_nt_k (A/B)
+bool g_gemm1_lds = true;
+
+bool gemm1_lds_set(bool on) {
+  const bool old = g_gemm1_lds;
+  g_gemm1_lds = on;
+  return old;
+}
+
 ConvGeo gemm1_identity_geo(int64_t M) {
   // M images of 1 x 1 pixel, one tap at (0, 0), stored to the same row: the implicit GEMM degenerates to C = A B^T
   ConvGeo g{};
@@ -405,11 +412,7 @@ bool gemm1_lds_preferred(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t l
   // ResNet-50's deep 1x1 convolutions (K >= 1024: layers 3-4) on small grids: the LDS-DMA pipeline hides the operand
   // latency that bounds ts_nt_k there (fwd + stats 10-26 % faster, input gradient 20-27 %; K <= 512 ties or loses,
   // profiles/r6/conv1x1_probe/probe.log)
-  static const bool off = [] {   // DPH_GEMM1_LDS=0: keep every 1x1 GEMM on ts_nt_k (A/B)
-    const char* e = std::getenv("DPH_GEMM1_LDS");
-    return e != nullptr && e[0] == '0';
-  }();
-  return !off && K >= 1024 && M > 0 && M < (int64_t(1) << 31) &&
+  return g_gemm1_lds && K >= 1024 && M > 0 && M < (int64_t(1) << 31) &&
          convg_supported(M, N, K, lda, ldb, gemm1_identity_geo(M));
 }
 

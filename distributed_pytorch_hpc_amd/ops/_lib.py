@@ -49,6 +49,8 @@ def load(build_if_missing: bool = False) -> bool:
             return False
         from . import _meta  # noqa: F401  (fake/meta kernels for the dispatcher ops)
 
+        if os.environ.get("DPH_GEMM1_LDS", "1") == "0":   # deep-K 1x1 GEMMs back on ts_nt_k (A/B, docs/guide/knobs.md)
+            torch.ops.dph.gemm1_lds(0)
         _loaded = True
         return True
 
