@@ -458,6 +458,57 @@ __global__ __launch_bounds__(BN_NT) void bn_bwd_dx_k(const T* __restrict__ dy, c
   }
 }
 
+// Two BatchNorms behind one residual add + ReLU (the projection shortcut: relu(bn_a(x) + bn_b(z)), _BNDualActFn):
+// both see the same output gradient dz = dy * bit, so one pass reads dy, the bits, x and z and writes both input
+// gradients -- the two single passes read dy and the bits once each.  Same per-element arithmetic as bn_bwd_dx_k.
+template <typename T>
+__global__ __launch_bounds__(BN_NT) void bn_bwd_dx2_k(const T* __restrict__ dy, const uint8_t* __restrict__ bmask,
+                                                      const T* __restrict__ x, const T* __restrict__ z,
+                                                      const float* __restrict__ mean_a,
+                                                      const float* __restrict__ invstd_a,
+                                                      const float* __restrict__ coef_a,
+                                                      const float* __restrict__ mean_b,
+                                                      const float* __restrict__ invstd_b,
+                                                      const float* __restrict__ coef_b, T* __restrict__ dx,
+                                                      T* __restrict__ dz_out, int64_t nvec, int ch8) {
+  const int C = ch8 * 8;
+  const int64_t v0 = (int64_t)blockIdx.x * BN_NT + threadIdx.x;
+  const int c0 = (int)(v0 % ch8) * 8;
+  float mua[8], isa[8], ka0[8], ka1[8], ka2[8], mub[8], isb[8], kb0[8], kb1[8], kb2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = c0 + i;
+    mua[i] = mean_a[c];
+    isa[i] = invstd_a[c];
+    ka0[i] = coef_a[c];
+    ka1[i] = coef_a[C + c];
+    ka2[i] = coef_a[2 * C + c];
+    mub[i] = mean_b[c];
+    isb[i] = invstd_b[c];
+    kb0[i] = coef_b[c];
+    kb1[i] = coef_b[C + c];
+    kb2[i] = coef_b[2 * C + c];
+  }
+  const int64_t stride = (int64_t)gridDim.x * BN_NT;
+  for (int64_t v = v0; v < nvec; v += stride) {
+    float g[8], xv[8], zv[8], oa[8], ob[8];
+    Vec8<T>::load(dy + v * 8, g);
+    Vec8<T>::load(x + v * 8, xv);
+    Vec8<T>::load(z + v * 8, zv);
+    const unsigned bits = bmask[v];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float dz = ((bits >> i) & 1u) != 0u ? g[i] : 0.f;
+      const float xa = (xv[i] - mua[i]) * isa[i];
+      const float xb = (zv[i] - mub[i]) * isb[i];
+      oa[i] = ka0[i] * (dz - ka1[i] - xa * ka2[i]);
+      ob[i] = kb0[i] * (dz - kb1[i] - xb * kb2[i]);
+    }
+    Vec8<T>::store(dx + v * 8, oa);
+    Vec8<T>::store(dz_out + v * 8, ob);
+  }
+}
+
 // The statistics kernel merges its row-lane partials as an LDS tree (25.0 -> 19.7 ms of bn_stats_k over
 // benchmarks/bn_bench.py against a serial merge by row group 0, profiles/r2s3/ab_bn_tree/).  The backward
 // reduction's plain sums gained nothing from the same tree (16.1 / 14.7 vs 16.3 / 14.8 ms) and stay serial.
@@ -559,10 +610,12 @@ void bn_apply_resbn(const void* x, const void* z, const float* ss, const float* 
   });
 }
 
-void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
-            void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dt,
-            int pdt, hipStream_t st, const float* xmask_ss, const uint8_t* relu_mask, const float* pre_part,
-            int pre_groups) {
+// The backward's reduction (or the producer's partials, merged) and finalize: dgamma / dbeta and the dx coefficients
+// [3C] in the workspace; returns the coefficients.
+static float* bwd_coef(const void* dy, const void* y, const void* x, const float* mean, const float* invstd,
+                       const void* w, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dt,
+                       int pdt, hipStream_t st, const float* xmask_ss, const uint8_t* relu_mask,
+                       const float* pre_part, int pre_groups) {
   const bool bm = relu && relu_mask != nullptr;
   const bool xm = relu && !bm && xmask_ss != nullptr;
   int64_t rpb;
@@ -602,6 +655,17 @@ void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, con
     hipLaunchKernelGGL((bn_bwd_finalize_k<float>), fg, dim3(FIN_NT), 0, st, part, G, (int)C, (float)M,
                        (const float*)w, invstd, (float*)dw, (float*)db, coef);
   }
+  return coef;
+}
+
+void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
+            void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dt,
+            int pdt, hipStream_t st, const float* xmask_ss, const uint8_t* relu_mask, const float* pre_part,
+            int pre_groups) {
+  const bool bm = relu && relu_mask != nullptr;
+  const bool xm = relu && !bm && xmask_ss != nullptr;
+  const float* coef = bwd_coef(dy, y, x, mean, invstd, w, dw, db, workspace, M, C, relu, dt, pdt, st, xmask_ss,
+                               relu_mask, pre_part, pre_groups);
   const int64_t nvec = M * C / 8;
   const dim3 grid(stream_grid(nvec, BN_NT));
 #define DPH_BN_DX(R_, D_, X_, B_)                                                                                 \
@@ -618,6 +682,22 @@ void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, con
     else DPH_BN_DX(false, false, false, false);
   });
 #undef DPH_BN_DX
+}
+
+void bn_bwd_dual(const void* dy, const uint8_t* relu_mask, const void* x, const void* z, const float* mean_a,
+                 const float* invstd_a, const void* w_a, const float* mean_b, const float* invstd_b, const void* w_b,
+                 void* dx, void* dz, void* dw_a, void* db_a, void* dw_b, void* db_b, float* ws_a, float* ws_b,
+                 int64_t M, int64_t C, int dt, int pdt, hipStream_t st, const float* pre_part_a, int pre_groups_a) {
+  const float* ca = bwd_coef(dy, x, x, mean_a, invstd_a, w_a, dw_a, db_a, ws_a, M, C, true, dt, pdt, st, nullptr,
+                             relu_mask, pre_part_a, pre_groups_a);
+  const float* cb = bwd_coef(dy, z, z, mean_b, invstd_b, w_b, dw_b, db_b, ws_b, M, C, true, dt, pdt, st, nullptr,
+                             relu_mask, nullptr, 0);
+  const int64_t nvec = M * C / 8;
+  const dim3 grid(stream_grid(nvec, BN_NT));
+  DPH_DISPATCH_FLOAT(dt, T, {
+    hipLaunchKernelGGL((bn_bwd_dx2_k<T>), grid, dim3(BN_NT), 0, st, (const T*)dy, relu_mask, (const T*)x,
+                       (const T*)z, mean_a, invstd_a, ca, mean_b, invstd_b, cb, (T*)dx, (T*)dz, nvec, (int)(C / 8));
+  });
 }
 
 }  // namespace dph

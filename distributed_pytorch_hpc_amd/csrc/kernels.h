@@ -253,6 +253,13 @@ void bn_apply_resbn(const void* x, const void* z, const float* ss, const float* 
                     int64_t M, int64_t C, int dtype, hipStream_t stream);
 // xmask_ss (optional, fp32 [scale | shift] of the forward): ReLU mask from x instead of reading y.
 // relu_mask (optional): the forward's bit mask instead of y (takes precedence over xmask_ss).
+// bn_bwd_dual: relu(bn_a(x) + bn_b(z)) with the ReLU bits relu_mask -- both BatchNorms' backward, the dx passes fused
+// into one (dx for x, dz for z); workspaces as bn_bwd's, one each; pre_part_a as bn_bwd's pre_part for bn_a.
+void bn_bwd_dual(const void* dy, const uint8_t* relu_mask, const void* x, const void* z, const float* mean_a,
+                 const float* invstd_a, const void* w_a, const float* mean_b, const float* invstd_b, const void* w_b,
+                 void* dx, void* dz, void* dw_a, void* db_a, void* dw_b, void* db_b, float* ws_a, float* ws_b,
+                 int64_t M, int64_t C, int dtype, int param_dtype, hipStream_t stream, const float* pre_part_a = nullptr,
+                 int pre_groups_a = 0);
 // pre_part (optional): the reduction partials [pre_groups][2C] from the producer's epilogue (BnRed): no reduction pass.
 void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, const float* invstd, const void* w,
             void* dx, void* dres, void* dw, void* db, float* workspace, int64_t M, int64_t C, bool relu, int dtype,

@@ -1362,6 +1362,61 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> bn_act_bwd(const Tensor& dy, const Te
   return {dx, dres, dw, db};
 }
 
+// relu(bn_a(x) + bn_b(z)) backward (the projection shortcut, ops/batchnorm.py _BNDualActFn): both BatchNorms from dy
+// and the forward's ReLU bits, one fused dx pass.  Returns (dx, dz, dw_a, db_a, dw_b, db_b); *_out write the parameter
+// gradients into caller buffers (the engine's buckets), pre_part_a = bn_a's partials from its consumer's epilogue.
+std::vector<Tensor> bn_act_bwd_dual(const Tensor& dy, const Tensor& x, const Tensor& z, const Tensor& relu_mask,
+                                    const Tensor& mean_a, const Tensor& invstd_a, const Tensor& w_a,
+                                    const Tensor& mean_b, const Tensor& invstd_b, const Tensor& w_b, bool need_a,
+                                    bool need_b, const c10::optional<Tensor>& dw_a_out,
+                                    const c10::optional<Tensor>& db_a_out, const c10::optional<Tensor>& dw_b_out,
+                                    const c10::optional<Tensor>& db_b_out, const c10::optional<Tensor>& pre_part_a) {
+  check_cuda(x, "x");
+  c10::DeviceGuard g(x.device());
+  const int64_t C = bn_channels(x), M = x.numel() / C;
+  check_like(dy, x, "dy");
+  check_like(z, x, "z");
+  TORCH_CHECK(relu_mask.scalar_type() == at::kByte && relu_mask.is_contiguous() && relu_mask.numel() == M * C / 8 &&
+                  relu_mask.device() == x.device(),
+              "bn_act_bwd_dual: relu_mask must be the forward's uint8 [M * C / 8] bits");
+  for (const Tensor* t : {&mean_a, &invstd_a, &mean_b, &invstd_b})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == C && t->is_contiguous(), "bn_act_bwd_dual: fp32 [C]");
+  TORCH_CHECK(w_a.numel() == C && w_b.numel() == C && w_a.is_contiguous() && w_b.is_contiguous() &&
+                  w_a.scalar_type() == w_b.scalar_type(),
+              "bn_act_bwd_dual: weights [C] of one dtype");
+  auto fopt = x.options().dtype(at::kFloat);
+  const at::ScalarType pt = w_a.scalar_type();
+  auto out_or_new = [&](bool need, const c10::optional<Tensor>& o, const char* name) {
+    if (!need) return at::empty({0}, fopt);
+    if (o.has_value()) {
+      TORCH_CHECK(o->numel() == C && o->is_contiguous() && o->scalar_type() == pt && o->device() == x.device(),
+                  "bn_act_bwd_dual: ", name, " must be a contiguous [C] tensor of the weight dtype");
+      return *o;
+    }
+    return at::empty({C}, x.options().dtype(pt));
+  };
+  Tensor dwa = out_or_new(need_a, dw_a_out, "dw_a_out"), dba = out_or_new(need_a, db_a_out, "db_a_out");
+  Tensor dwb = out_or_new(need_b, dw_b_out, "dw_b_out"), dbb = out_or_new(need_b, db_b_out, "db_b_out");
+  int pre_groups = 0;
+  if (pre_part_a.has_value()) {
+    TORCH_CHECK(pre_part_a->scalar_type() == at::kFloat && pre_part_a->dim() == 2 && pre_part_a->size(1) == 2 * C &&
+                    pre_part_a->is_contiguous() && pre_part_a->device() == x.device(),
+                "bn_act_bwd_dual: pre_part_a must be fp32 [G, 2C]");
+    pre_groups = (int)pre_part_a->size(0);
+  }
+  const int G = dph::bn_partial_blocks(M, C);
+  auto wsa = at::empty({2 * (int64_t)G * C + 3 * C}, fopt), wsb = at::empty({2 * (int64_t)G * C + 3 * C}, fopt);
+  auto dx = at::empty_like(x), dz = at::empty_like(z);
+  dph::bn_bwd_dual(dy.data_ptr(), relu_mask.data_ptr<uint8_t>(), x.data_ptr(), z.data_ptr(), mean_a.data_ptr<float>(),
+                   invstd_a.data_ptr<float>(), w_a.data_ptr(), mean_b.data_ptr<float>(), invstd_b.data_ptr<float>(),
+                   w_b.data_ptr(), dx.data_ptr(), dz.data_ptr(), need_a ? dwa.data_ptr() : nullptr,
+                   need_a ? dba.data_ptr() : nullptr, need_b ? dwb.data_ptr() : nullptr,
+                   need_b ? dbb.data_ptr() : nullptr, wsa.data_ptr<float>(), wsb.data_ptr<float>(), M, C, dt_code(x),
+                   dt_code(w_a), cur_stream(), pre_part_a.has_value() ? pre_part_a->data_ptr<float>() : nullptr,
+                   pre_groups);
+  return {dx, dz, dwa, dba, dwb, dbb};
+}
+
 // ------------------------------------------------------------------------------ latitude-weighted MSE
 // Row step of the latitude axis in the flat storage order: W (NCHW) or W*C (channels-last).
 int64_t latmse_check(const Tensor& p, const Tensor& t) {
@@ -1702,6 +1757,10 @@ TORCH_LIBRARY(dph, m) {
         "-> (Tensor, Tensor, Tensor, Tensor)");
   m.def("bn_act_apply(Tensor x, Tensor? res, Tensor scale, Tensor shift, bool relu) -> Tensor");
   m.def("bn_act_apply_resbn(Tensor x, Tensor ss, Tensor z, Tensor zss, Tensor(a!) relu_mask) -> Tensor");
+  m.def("bn_act_bwd_dual(Tensor dy, Tensor x, Tensor z, Tensor relu_mask, Tensor mean_a, Tensor invstd_a, "
+        "Tensor w_a, Tensor mean_b, Tensor invstd_b, Tensor w_b, bool need_a, bool need_b, Tensor(a!)? dw_a_out=None, "
+        "Tensor(b!)? db_a_out=None, Tensor(c!)? dw_b_out=None, Tensor(d!)? db_b_out=None, Tensor? pre_part_a=None) "
+        "-> Tensor[]");
   m.def("bn_act_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, Tensor? w, bool relu, bool need_dres, "
         "bool need_dwb, Tensor? xmask_ss=None, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, "
         "Tensor? relu_mask=None, Tensor? pre_part=None) "
@@ -1780,6 +1839,7 @@ TORCH_LIBRARY_IMPL(dph, CUDA, m) {
   m.impl("bn_act_fwd", &bn_act_fwd);
   m.impl("bn_act_apply", &bn_act_apply);
   m.impl("bn_act_bwd", &bn_act_bwd);
+  m.impl("bn_act_bwd_dual", &bn_act_bwd_dual);
   m.impl("bn_act_apply_resbn", &bn_act_apply_resbn);
   m.impl("car_allreduce", &car_allreduce_op);
   m.impl("car_flag", &car_flag_op);

@@ -91,6 +91,17 @@ def _bn_act_apply_resbn(x, ss, z, zss, relu_mask):
     return torch.empty_like(x)
 
 
+@register_fake("dph::bn_act_bwd_dual")
+def _bn_act_bwd_dual(dy, x, z, relu_mask, mean_a, invstd_a, w_a, mean_b, invstd_b, w_b, need_a, need_b, dw_a_out=None,
+                     db_a_out=None, dw_b_out=None, db_b_out=None, pre_part_a=None):
+    c = x.shape[1]
+
+    def pg(need):
+        return x.new_empty((c,) if need else (0,), dtype=w_a.dtype if need else torch.float32)
+
+    return [torch.empty_like(x), torch.empty_like(z), pg(need_a), pg(need_a), pg(need_b), pg(need_b)]
+
+
 @register_fake("dph::bn_act_bwd")
 def _bn_act_bwd(dy, y, x, mean, invstd, w, relu, need_dres, need_dwb, xmask_ss=None, dw_out=None, db_out=None,
                 relu_mask=None, pre_part=None):

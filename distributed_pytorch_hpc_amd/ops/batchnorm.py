@@ -150,21 +150,31 @@ class _BNDualActFn(torch.autograd.Function):
         part = ctx.bn_slot.take(dy) if ctx.bn_slot is not None else None   # reduced by the consumer's epilogue
         dy = dy.contiguous(memory_format=torch.channels_last)
         wpa, bpa, wpb, bpb = ctx.params
-        grads = []
-        for xx, mean, inv, w, wp, bp, pre, gi in ((x, mean_a, inv_a, wa, wpa, bpa, part, 2),
-                                                  (z, mean_b, inv_b, wb, wpb, bpb, None, 6)):
-            need_wb = ctx.needs_input_grad[gi] or ctx.needs_input_grad[gi + 1]
-            direct = _direct_pair(wp, bp, need_wb)
-            dx, _, dw, db = _lib.ops().bn_act_bwd(dy, xx, xx, mean, inv, w, True, False, need_wb, None,
-                                                  wp.main_grad if direct else None, bp.main_grad if direct else None,
-                                                  bits, pre)
-            if direct:
-                _mark_direct(wp, bp)
-                dw = db = None
-            grads.append((dx, dw if need_wb else None, db if need_wb else None))
-        (dxa, dwa, dba), (dxb, dwb, dbb) = grads
-        return (dxa, dxb, dwa, dba, None, None, dwb, dbb, None, None, None, None, None, None, None, None, None, None,
-                None)
+        need_a = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        need_b = ctx.needs_input_grad[6] or ctx.needs_input_grad[7]
+        da, db_ = _direct_pair(wpa, bpa, need_a), _direct_pair(wpb, bpb, need_b)
+        if os.environ.get("DPH_BN_DUAL_DX", "1") != "0":
+            # both BatchNorms' dx in one pass over dy, the bits, x and z (csrc/batchnorm.hip bn_bwd_dx2_k)
+            dxa, dxb, dwa, dba, dwb, dbb = _lib.ops().bn_act_bwd_dual(
+                dy, x, z, bits, mean_a, inv_a, wa, mean_b, inv_b, wb, need_a, need_b,
+                wpa.main_grad if da else None, bpa.main_grad if da else None,
+                wpb.main_grad if db_ else None, bpb.main_grad if db_ else None, part)
+        else:
+            dxa, _, dwa, dba = _lib.ops().bn_act_bwd(dy, x, x, mean_a, inv_a, wa, True, False, need_a, None,
+                                                     wpa.main_grad if da else None, bpa.main_grad if da else None,
+                                                     bits, part)
+            dxb, _, dwb, dbb = _lib.ops().bn_act_bwd(dy, z, z, mean_b, inv_b, wb, True, False, need_b, None,
+                                                     wpb.main_grad if db_ else None, bpb.main_grad if db_ else None,
+                                                     bits, None)
+        if da:
+            _mark_direct(wpa, bpa)
+            dwa = dba = None
+        if db_:
+            _mark_direct(wpb, bpb)
+            dwb = dbb = None
+        return (dxa, dxb, dwa if need_a else None, dba if need_a else None, None, None,
+                dwb if need_b else None, dbb if need_b else None, None, None, None, None, None, None, None, None,
+                None, None, None)
 
 
 def bn_dual_act(bn_a: "BatchNormAct2d", bn_b: "BatchNormAct2d", x, z, stats_a=None, stats_b=None, bn_slot=None):

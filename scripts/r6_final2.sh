@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 6, last tree: the whole GPU tier, smoke(), and the ResNet-50 / SimpleUNet benches
+set -o pipefail
+out=gpurun_out/r6final2
+mkdir -p $out
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests -m gpu > $out/tier.log 2>&1 || { echo "tier failed"; grep -E "FAILED|Error" $out/tier.log | head; tail -40 $out/tier.log; exit 1; }
+tail -1 $out/tier.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
+tail -1 $out/smoke.log
+timeout -k 10 300 python -u bench.py --layout resnet-fsdp --steps 30 --warmup 5 > $out/resnet.log 2>&1 || exit 1
+tail -1 $out/resnet.log | cut -c1-160
+timeout -k 10 300 python -u bench.py --layout unet-ddp --steps 60 --warmup 10 > $out/unet.log 2>&1 || exit 1
+tail -1 $out/unet.log | cut -c1-160

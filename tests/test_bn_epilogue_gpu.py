@@ -386,3 +386,34 @@ def test_deep_1x1_on_lds_dma_gemm(dph_native, M, K, N):
     r1 = ops.bn_act_fwd(x, None, None, None, None, None, 0.1, 1e-5, True, st)
     for g_, r_ in zip(r1, r0):
         assert rel_err(g_, r_) < 1e-4
+
+
+def test_dual_bn_fused_dx_pass_matches_two_passes(dph_native, monkeypatch):
+    """The projection shortcut's backward with both BatchNorms' dx in one pass (bn_bwd_dx2_k, DPH_BN_DUAL_DX=1
+    default) gives the same gradients as two single passes."""
+    import copy
+    import importlib
+
+    R = importlib.import_module("distributed_pytorch_hpc_amd.models.resnet")
+    torch.manual_seed(3)
+    ds = torch.nn.Sequential(R.conv1x1(256, 512, 2), R.BatchNormAct2d(512, act=False))
+    base = R.Bottleneck(256, 128, 2, ds).to(DEV).to(torch.bfloat16).to(memory_format=torch.channels_last)
+    for m in base.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    x0 = torch.randn(4, 256, 14, 14, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    res = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("DPH_BN_DUAL_DX", v)
+        blk = copy.deepcopy(base)
+        x = x0.clone().requires_grad_()
+        torch.manual_seed(5)
+        y = blk(x)
+        (y.float() * torch.randn_like(y.float())).sum().backward()
+        torch.cuda.synchronize()
+        res.append((x.grad.clone(), {n: p.grad.clone() for n, p in blk.named_parameters()}))
+    (gx0, g0), (gx1, g1) = res
+    assert rel_err(gx1, gx0) < 1e-5
+    for n in g0:
+        assert rel_err(g1[n], g0[n]) < 1e-5, n
