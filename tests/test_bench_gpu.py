@@ -78,3 +78,22 @@ def test_bench_one_rank_conv_layouts_replay_graph(tmp_path, layout):
     r = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")][0]
     assert r["n_gpus"] == 1 and r["value"] > 0 and "graph" in r, r
     assert r["loss_last"] == r["loss_last"]   # not NaN
+
+
+def test_bench_resnet50_fsdp_two_ranks_share_one_gpu(tmp_path):
+    """ResNet-50 under the FSDP engine at world 2 (two gloo ranks on one MI355X) with every round-6 BatchNorm path on
+    (reductions in the consumers' epilogues, masked residual hand-off, projection-shortcut dual BatchNorm): the step
+    runs on both ranks and the loss stays finite (the parameters are sharded, so there is no replica checksum)."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--backend", "gloo", "--layout", "resnet-fsdp", "--arch", "resnet50", "--image-size", "64",
+           "--micro-batch", "4", "--steps", "2", "--warmup", "1", "--quiet", "--no-telemetry"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=str(tmp_path),
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")][0]
+    assert r["n_gpus"] == 2 and r["value"] > 0 and r["loss_last"] == r["loss_last"]
+    assert r["config"]["parallelism"] == "fsdp2"
