@@ -27,16 +27,30 @@ class ConvBlock(nn.Sequential):
     unchanged), and a training-mode BN takes its batch statistics from the 3x3 convolution's epilogue (StatsSlot)
     instead of a statistics pass over the activation."""
 
+    def out_slot(self, y: torch.Tensor):
+        """The second BatchNorm's slot (ops.conv.BnGradSlot) if ``y`` is this block's last output -- for a consumer
+        that is the output's only one (the up-path GEMM after the bottleneck and the decoder blocks, the output
+        convolution); the encoder blocks' outputs also feed a skip connection, so nobody takes theirs."""
+        slot, key = getattr(self, "_dph_out", (None, None))
+        self._dph_out = (None, None)
+        if os.environ.get("DPH_UNET_OUT_FOLD", "1") == "0":   # A/B: those BatchNorms run their own reduction pass
+            return None
+        return slot if slot is not None and key == (y.data_ptr(), tuple(y.shape), tuple(y.stride())) else None
+
     def forward(self, x):
         # the first BatchNorm's output is consumed only by the second convolution: its backward reduction runs in that
-        # convolution's input-gradient epilogue (ops.conv.BnGradSlot); the second's feeds pooling / skip / up-path
+        # convolution's input-gradient epilogue (ops.conv.BnGradSlot); the second's is offered to the block's
+        # consumer (out_slot)
         red = None
+        self._dph_out = (None, None)
         for i, (conv, bn) in enumerate(((self[0], self[1]), (self[3], self[4]))):
             if isinstance(conv, BiasConv2d) and isinstance(bn, BatchNormAct2d) and bn.training:
                 slot = StatsSlot()
-                nxt = BnGradSlot() if i == 0 and isinstance(self[3], BiasConv2d) else None
+                nxt = BnGradSlot() if i == 1 or isinstance(self[3], BiasConv2d) else None
                 x = bn(conv(x, stats_slot=slot, bn_slot=red), stats_slot=slot, bn_slot=nxt)
                 red = nxt
+                if i == 1 and nxt is not None:
+                    self._dph_out = (nxt, (x.data_ptr(), tuple(x.shape), tuple(x.stride())))
             else:   # modules swapped in by a wrapper (e.g. the halo convolutions of parallel/domain.py)
                 x = bn(conv(x))
                 red = None
@@ -72,11 +86,18 @@ class SimpleUNet(nn.Module):
         e2 = self.enc2(self.pool(e1))
         e3 = self.enc3(self.pool(e2))
         bt = self.bottleneck(self.pool(e3))
-        # up-sample + resize + concat: one GEMM and one copy kernel per level on the GPU (ops/upsample.py)
-        d3 = self.dec3(up_concat(self.up3, bt, e3))
-        d2 = self.dec2(up_concat(self.up2, d3, e2))
-        d1 = self.dec1(up_concat(self.up1, d2, e1))
+        # up-sample + resize + concat: one GEMM and one copy kernel per level on the GPU (ops/upsample.py); the
+        # bottleneck / decoder outputs feed only the next GEMM, which then runs their last BatchNorm's reduction
+        d3 = self.dec3(up_concat(self.up3, bt, e3, bn_slot=_out_slot(self.bottleneck, bt)))
+        d2 = self.dec2(up_concat(self.up2, d3, e2, bn_slot=_out_slot(self.dec3, d3)))
+        d1 = self.dec1(up_concat(self.up1, d2, e1, bn_slot=_out_slot(self.dec2, d2)))
+        if isinstance(self.out, BiasConv2d):
+            return self.out(d1, bn_slot=_out_slot(self.dec1, d1))
         return self.out(d1)
+
+
+def _out_slot(block, y):
+    return block.out_slot(y) if isinstance(block, ConvBlock) else None
 
 
 def to_channels_last(model: nn.Module) -> nn.Module:

@@ -716,10 +716,11 @@ class _BiasConv1x1Fn(torch.autograd.Function):
     weight gradient (``ts_gemm_tn_``) run on the 1x1 kernels and the bias gradient is one channel sum."""
 
     @staticmethod
-    def forward(ctx, x, w, bias):
+    def forward(ctx, x, w, bias, bn_slot=None):
         B, C, H, W = x.shape
         cout = w.shape[0]
         npad = -(-cout // 64) * 64
+        ctx.bn_slot = bn_slot
         xb = x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)
         x2 = _nhwc2d(xb)
         w2 = F.pad(w.reshape(cout, C).to(torch.bfloat16), (0, 0, 0, npad - cout))
@@ -737,7 +738,12 @@ class _BiasConv1x1Fn(torch.autograd.Function):
         dy2 = _lib.ops().pad_cols(_nhwc2d(dy.to(torch.bfloat16)), npad)   # [pixels, npad], zero columns past Cout
         dx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            dx = _lib.ops().ts_gemm_nt(dy2, weight_t(w2)).view(B, H, W, C).permute(0, 3, 1, 2)
+            bn = ctx.bn_slot   # x is a BatchNorm + ReLU output consumed only here: its reduction in this epilogue
+            if bn is not None and bn.usable(B * H * W, C):
+                dx = bn.launch(dy2, weight_t(w2)).view(B, H, W, C).permute(0, 3, 1, 2)
+                bn.mark(dx)
+            else:
+                dx = _lib.ops().ts_gemm_nt(dy2, weight_t(w2)).view(B, H, W, C).permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
             gk = torch.empty((npad, C), device=dy.device, dtype=torch.float32)
             _lib.ops().ts_gemm_tn_(gk, dy2, x2, False)
@@ -754,7 +760,7 @@ class _BiasConv1x1Fn(torch.autograd.Function):
                 gb = None
             else:
                 gb = gb.to(bdt)
-        return dx, gw, gb
+        return dx, gw, gb, None
 
 
 class BiasConv2d(nn.Conv2d):
@@ -768,7 +774,7 @@ class BiasConv2d(nn.Conv2d):
         """``stats_slot``: on the 3x3 kernel path the following BatchNorm's statistics come from this convolution's
         epilogue (SimpleUNet's conv -> BN blocks, models/unet.py); otherwise the slot stays empty.  ``bn_slot``: x is
         a training-mode BatchNorm + ReLU output consumed only here; its backward reduction then runs in this
-        convolution's input-gradient epilogue (3x3 kernel path)."""
+        convolution's input-gradient epilogue (3x3 and 1x1 kernel paths)."""
         if _bias_conv3x3_ok(self, x):
             _lib.require()
             b = self.bias if self.bias.dtype in (torch.float32, torch.bfloat16) else self.bias.float()
@@ -783,7 +789,7 @@ class BiasConv2d(nn.Conv2d):
             return _Conv3x3Fn.apply(pad_channels(x, cp), wp, stats_slot, b)
         if _bias_conv1x1_ok(self, x):
             _lib.require()
-            return _BiasConv1x1Fn.apply(x, self.weight, self.bias)
+            return _BiasConv1x1Fn.apply(x, self.weight, self.bias, bn_slot)
         if _bias_conv_ok(self, x):
             return _bias_conv(self, x, False, (0, 0))
         return super().forward(x)

@@ -71,7 +71,7 @@ class _Params:
 
 class _UpConcatFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, skip, params=None):
+    def forward(ctx, x, weight, bias, skip, params=None, bn_slot=None):
         n, cin, h, w = x.shape
         co = weight.shape[1]
         x2 = x.permute(0, 2, 3, 1).reshape(n * h * w, cin)          # channels-last: a view
@@ -87,6 +87,7 @@ class _UpConcatFn(torch.autograd.Function):
         ctx.has_bias = bias is not None
         ctx.ts = ts
         ctx.params = params
+        ctx.bn_slot = bn_slot
         return out
 
     @staticmethod
@@ -97,8 +98,15 @@ class _UpConcatFn(torch.autograd.Function):
         dy2, dskip = _lib.ops().upcat_bwd(dcat, h, w, co)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx2 = _lib.ops().ts_gemm_nt(dy2, wr) if ctx.ts else torch.matmul(dy2, wr.t())
+            bn = ctx.bn_slot   # x is a BatchNorm + ReLU output consumed only here: its reduction in this epilogue
+            bn = bn if (bn is not None and ctx.ts and bn.usable(n * h * w, cin)) else None
+            if bn is not None:
+                dx2 = bn.launch(dy2, wr)
+            else:
+                dx2 = _lib.ops().ts_gemm_nt(dy2, wr) if ctx.ts else torch.matmul(dy2, wr.t())
             dx = dx2.view(n, h, w, cin).permute(0, 3, 1, 2)
+            if bn is not None:
+                bn.mark(dx)
         prm = ctx.params
         if ctx.needs_input_grad[1]:
             # a channels-last ConvTranspose2d weight [ci, co, 2, 2] is laid out as [ci, (i, j, co)] = dWr: the engine's
@@ -120,7 +128,7 @@ class _UpConcatFn(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             # straight into the bias's bucket view when the engine owns it (bias_grad), else returned in fp32
             db = bias_grad(prm.bias if prm is not None else None, dy2.view(-1, co), torch.float32)
-        return dx, dw, db, dskip, None
+        return dx, dw, db, dskip, None, None
 
 
 def up_concat_reference(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> torch.Tensor:
@@ -131,8 +139,10 @@ def up_concat_reference(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> t
     return torch.cat([u, skip], dim=1)
 
 
-def up_concat(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> torch.Tensor:
-    """``cat([resize(up(x), skip.shape[2:]), skip], 1)`` -- fused on the GPU when eligible."""
+def up_concat(up: nn.Module, x: torch.Tensor, skip: torch.Tensor, bn_slot=None) -> torch.Tensor:
+    """``cat([resize(up(x), skip.shape[2:]), skip], 1)`` -- fused on the GPU when eligible.  ``bn_slot``
+    (ops.conv.BnGradSlot): x is a BatchNorm + ReLU output consumed only here; its backward reduction then runs in the
+    input-gradient GEMM's epilogue."""
     if not up_concat_native_ok(up, x, skip):
         return up_concat_reference(up, x, skip)
     dt = torch.bfloat16
@@ -143,4 +153,5 @@ def up_concat(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> torch.Tenso
     # the parameters themselves for the direct bucket writes -- only when the GEMM operand is the weight itself
     prm = _Params(up.weight, up.bias) if wt is up.weight and os.environ.get("DPH_UPCAT_DIRECT", "1") != "0" else None
     with torch.autocast("cuda", enabled=False):
-        return _UpConcatFn.apply(x if x.dtype == dt else x.to(dt), wt, b, skip, prm)
+        return _UpConcatFn.apply(x if x.dtype == dt else x.to(dt), wt, b, skip, prm,
+                                 bn_slot if x.dtype == dt else None)

@@ -368,6 +368,27 @@ def test_unet_conv_block_first_bn_reduced_in_second_conv(dph_native, monkeypatch
         assert rel_err(g1[n], g0[n]) < 1e-2, n
 
 
+def test_simple_unet_all_bn_reductions_in_consumers(dph_native, monkeypatch):
+    """Whole SimpleUNet: every block's first BatchNorm reduces in its second convolution (7), and the bottleneck /
+    decoder blocks' last BatchNorm in the up-path GEMM or the output 1x1 convolution (4); gradients match the
+    BatchNorms' own reduction passes."""
+    from distributed_pytorch_hpc_amd.models.unet import SimpleUNet, to_channels_last
+
+    torch.manual_seed(5)
+    net = to_channels_last(SimpleUNet(65, 65, 64).to(DEV).to(torch.bfloat16))
+    x = torch.randn(2, 65, 48, 80, device=DEV, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+    cnt = _Count(monkeypatch)
+    gx0, g0 = _grads(net, x, monkeypatch, False)
+    assert cnt.used == 0
+    gx1, g1 = _grads(net, x, monkeypatch, True)
+    assert cnt.used == 11
+    assert rel_err(gx1, gx0) < 2e-2
+    num = sum((g1[n] - g0[n]).norm() ** 2 for n in g0) ** 0.5
+    den = sum(g0[n].norm() ** 2 for n in g0) ** 0.5
+    assert num / den < 1e-2
+
+
 @pytest.mark.parametrize("M,K,N", [(50176 // 8, 1024, 256), (12544 // 4 + 37, 2048, 512), (777, 1024, 128)])
 def test_deep_1x1_on_lds_dma_gemm(dph_native, M, K, N):
     """Deep-K 1x1 GEMMs (K >= 1024) run on the LDS-DMA implicit GEMM with a one-tap identity geometry: the product
