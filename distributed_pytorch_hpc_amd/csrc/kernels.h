@@ -272,19 +272,21 @@ void bn_bwd(const void* dy, const void* y, const void* x, const float* mean, con
 inline int64_t maxpool_s2_out(int64_t n, int k) { return k == 3 ? (n - 1) / 2 + 1 : n / 2; }
 void maxpool_s2_fwd(const void* x, void* y, uint8_t* tap, int64_t N, int64_t H, int64_t W, int64_t C, int k,
                     int dtype, hipStream_t stream);
+// add (optional): a second gradient of the input, [N, H, W] rows of row stride lda, summed in before the store.
 void maxpool_s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C, int k,
-                    int dtype, hipStream_t stream);
+                    int dtype, hipStream_t stream, const void* add = nullptr, int64_t lda = 0);
 // maxpool_s2_bwd (bf16, C / 8 dividing 256) whose input is a training-mode BatchNorm + ReLU output: also that
 // BatchNorm's backward reduction partials (BnRed, mask from x) into r.part [maxpool_s2_bwd_bnred_blocks(...)][2C].
 int maxpool_s2_bwd_bnred_blocks(int64_t N, int64_t H, int64_t W, int64_t C);
 void maxpool_s2_bwd_bnred(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C,
-                          int k, const BnRed& r, hipStream_t stream);
+                          int k, const BnRed& r, hipStream_t stream, const void* add = nullptr, int64_t lda = 0);
 
 // SimpleUNet up-path, csrc/upsample.hip.  y: the ConvTranspose2d(2, 2) GEMM output [N*H*W, 4*Co] (columns (i, j, co));
 // skip / out / dcat / dskip channels-last.  out[n, oh, ow, :] = [bilinear(pixel_shuffle(y) + bias)(oh, ow), skip].
 // Co, Cs % 8 == 0; bias fp32 or null.
 void upcat_fwd(const void* y, const float* bias, const void* skip, void* out, int64_t N, int64_t H, int64_t W,
                int64_t Co, int64_t Ho, int64_t Wo, int64_t Cs, int dtype, hipStream_t stream);
+// dskip null: only dy (the skip's gradient is read from dcat by its other consumer, maxpool_s2_bwd's add).
 void upcat_bwd(const void* dcat, void* dy, void* dskip, int64_t N, int64_t H, int64_t W, int64_t Co, int64_t Ho,
                int64_t Wo, int64_t Cs, int dtype, hipStream_t stream);
 

@@ -72,13 +72,16 @@ __global__ __launch_bounds__(PNT) void maxpool_fwd_k(const T* __restrict__ x, T*
   }
 }
 
-// BRED (bf16, the input is a BatchNorm + ReLU output -- the ResNet stem): also the BatchNorm backward's reduction
-// over the written gradient (kernels.h BnRed, mask from x; one partial row per block).  The grid stride is a multiple
-// of C / 8 (PNT % (C / 8) == 0, host-checked), so a thread's channel chunk is fixed.
-template <typename T, int K, int P, bool BRED = false>
+// BRED (bf16, the input is a BatchNorm + ReLU output -- the ResNet stem, the SimpleUNet encoder blocks): also the
+// BatchNorm backward's reduction over the written gradient (kernels.h BnRed, mask from x; one partial row per block).
+// The grid stride is a multiple of C / 8 (PNT % (C / 8) == 0, host-checked), so a thread's channel chunk is fixed.
+// ADD: the input's other gradient (SimpleUNet: the skip connection's slice of d(concat), row stride lda) is added
+// before the store -- the sum autograd would otherwise form with a separate kernel.
+template <typename T, int K, int P, bool BRED = false, bool ADD = false>
 __global__ __launch_bounds__(PNT) void maxpool_bwd_k(const T* __restrict__ dy, const uint8_t* __restrict__ tap,
                                                      T* __restrict__ dx, int H, int W, int Ho, int Wo, int C,
-                                                     int64_t total, BnRed bnr) {
+                                                     int64_t total, BnRed bnr, const T* __restrict__ add,
+                                                     int64_t lda) {
   const int cv = C >> 3;
   [[maybe_unused]] BnRedAcc<1> bra;
   if constexpr (BRED) bra.init(bnr, (int)(((int64_t)blockIdx.x * PNT + threadIdx.x) % cv) * 8, C);
@@ -108,6 +111,12 @@ __global__ __launch_bounds__(PNT) void maxpool_bwd_k(const T* __restrict__ dy, c
         for (int k = 0; k < 8; ++k)
           if ((int)((packed >> (8 * k)) & 0xff) == me) acc[k] += g[k];
       }
+    }
+    if constexpr (ADD) {
+      float a[8];
+      Vec8<T>::load(add + p * lda + c8 * 8, a);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] = (float)(T)acc[k] + a[k];   // = the bf16 sum of the two rounded gradients
     }
     Vec8<T>::store(dx + p * C + c8 * 8, acc);
     if constexpr (BRED) {
@@ -144,14 +153,21 @@ void maxpool_s2_fwd(const void* x, void* y, uint8_t* tap, int64_t N, int64_t H, 
 }
 
 void maxpool_s2_bwd(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C, int k,
-                    int dtype, hipStream_t st) {
+                    int dtype, hipStream_t st, const void* add, int64_t lda) {
   const int64_t Ho = maxpool_s2_out(H, k), Wo = maxpool_s2_out(W, k);
   const int64_t total = N * H * W * (C / 8);
   if (total <= 0) return;
   const dim3 grid(stream_grid(total, PNT));
   DPH_DISPATCH_FLOAT(dtype, T, {
-    DPH_POOL_KP(k, hipLaunchKernelGGL((maxpool_bwd_k<T, K, P>), grid, dim3(PNT), 0, st, (const T*)dy, tap, (T*)dx,
-                                      (int)H, (int)W, (int)Ho, (int)Wo, (int)C, total, BnRed{}));
+    if (add) {
+      DPH_POOL_KP(k, hipLaunchKernelGGL((maxpool_bwd_k<T, K, P, false, true>), grid, dim3(PNT), 0, st, (const T*)dy,
+                                        tap, (T*)dx, (int)H, (int)W, (int)Ho, (int)Wo, (int)C, total, BnRed{},
+                                        (const T*)add, lda));
+    } else {
+      DPH_POOL_KP(k, hipLaunchKernelGGL((maxpool_bwd_k<T, K, P>), grid, dim3(PNT), 0, st, (const T*)dy, tap, (T*)dx,
+                                        (int)H, (int)W, (int)Ho, (int)Wo, (int)C, total, BnRed{}, (const T*)nullptr,
+                                        (int64_t)0));
+    }
   });
 }
 
@@ -160,13 +176,20 @@ int maxpool_s2_bwd_bnred_blocks(int64_t N, int64_t H, int64_t W, int64_t C) {
 }
 
 void maxpool_s2_bwd_bnred(const void* dy, const uint8_t* tap, void* dx, int64_t N, int64_t H, int64_t W, int64_t C,
-                          int k, const BnRed& r, hipStream_t st) {
+                          int k, const BnRed& r, hipStream_t st, const void* add, int64_t lda) {
   const int64_t Ho = maxpool_s2_out(H, k), Wo = maxpool_s2_out(W, k);
   const int64_t total = N * H * W * (C / 8);
   if (total <= 0) return;
   const dim3 grid(stream_grid(total, PNT));
-  DPH_POOL_KP(k, hipLaunchKernelGGL((maxpool_bwd_k<bf16, K, P, true>), grid, dim3(PNT), 0, st, (const bf16*)dy, tap,
-                                    (bf16*)dx, (int)H, (int)W, (int)Ho, (int)Wo, (int)C, total, r));
+  if (add) {
+    DPH_POOL_KP(k, hipLaunchKernelGGL((maxpool_bwd_k<bf16, K, P, true, true>), grid, dim3(PNT), 0, st,
+                                      (const bf16*)dy, tap, (bf16*)dx, (int)H, (int)W, (int)Ho, (int)Wo, (int)C, total,
+                                      r, (const bf16*)add, lda));
+  } else {
+    DPH_POOL_KP(k, hipLaunchKernelGGL((maxpool_bwd_k<bf16, K, P, true>), grid, dim3(PNT), 0, st, (const bf16*)dy, tap,
+                                      (bf16*)dx, (int)H, (int)W, (int)Ho, (int)Wo, (int)C, total, r,
+                                      (const bf16*)nullptr, (int64_t)0));
+  }
 }
 #undef DPH_POOL_KP
 

@@ -1038,7 +1038,23 @@ std::tuple<Tensor, Tensor> maxpool_s2_fwd(const Tensor& x, int64_t k) {
   return {y, tap};
 }
 
-Tensor maxpool_s2_bwd(const Tensor& dy, const Tensor& tap, int64_t H, int64_t W, int64_t k) {
+// The optional second gradient of a pooling input: channels [add_off, add_off + C) of a channels-last [N, *, H, W]
+// tensor of dy's dtype (SimpleUNet: the skip connection's slice of d(concat)).  Returns (pointer, row stride).
+static std::pair<const void*, int64_t> pool_add_operand(const c10::optional<Tensor>& add, int64_t add_off,
+                                                        const Tensor& dy, int64_t H, int64_t W, const char* what) {
+  if (!add.has_value()) return {nullptr, 0};
+  const Tensor& a = *add;
+  const int64_t C = dy.size(1);
+  TORCH_CHECK(a.dim() == 4 && a.size(0) == dy.size(0) && a.size(2) == H && a.size(3) == W && add_off >= 0 &&
+                  add_off % 8 == 0 && add_off + C <= a.size(1) && a.scalar_type() == dy.scalar_type() &&
+                  a.device() == dy.device() && a.is_contiguous(at::MemoryFormat::ChannelsLast),
+              what, ": add must be a channels-last [N, >= add_off + C, H, W] tensor of dy's dtype");
+  check_align16(a, "add");
+  return {static_cast<const char*>(a.data_ptr()) + add_off * a.element_size(), a.size(1)};
+}
+
+Tensor maxpool_s2_bwd(const Tensor& dy, const Tensor& tap, int64_t H, int64_t W, int64_t k,
+                      const c10::optional<Tensor>& add, int64_t add_off) {
   check_cuda(dy, "dy");
   c10::DeviceGuard g(dy.device());
   TORCH_CHECK(k == 2 || k == 3, "maxpool_s2_bwd: kernel 2 or 3");
@@ -1051,9 +1067,10 @@ Tensor maxpool_s2_bwd(const Tensor& dy, const Tensor& tap, int64_t H, int64_t W,
                   tap.size(1) == Ho && tap.size(2) == Wo && tap.size(3) == C && tap.device() == dy.device(),
               "maxpool_s2_bwd: tap must be the forward's uint8 [N, Ho, Wo, C]");
   check_align16(dy, "dy");
+  const auto ad = pool_add_operand(add, add_off, dy, H, W, "maxpool_s2_bwd");
   auto dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   dph::maxpool_s2_bwd(dy.data_ptr(), tap.data_ptr<uint8_t>(), dx.data_ptr(), N, H, W, C, (int)k, dt_code(dy),
-                      cur_stream());
+                      cur_stream(), ad.first, ad.second);
   return dx;
 }
 
@@ -1062,7 +1079,8 @@ Tensor maxpool_s2_bwd(const Tensor& dy, const Tensor& tap, int64_t H, int64_t W,
 // pre_part -- the BatchNorm then skips its reduction pass over dx and x.
 std::tuple<Tensor, Tensor> maxpool_s2_bwd_bnred(const Tensor& dy, const Tensor& tap, int64_t H, int64_t W, int64_t k,
                                                 const Tensor& x, const Tensor& mean, const Tensor& invstd,
-                                                const Tensor& ss) {
+                                                const Tensor& ss, const c10::optional<Tensor>& add,
+                                                int64_t add_off) {
   check_cuda(dy, "dy");
   c10::DeviceGuard g(dy.device());
   TORCH_CHECK(k == 2 || k == 3, "maxpool_s2_bwd_bnred: kernel 2 or 3");
@@ -1094,8 +1112,9 @@ std::tuple<Tensor, Tensor> maxpool_s2_bwd_bnred(const Tensor& dy, const Tensor& 
   r.invstd = invstd.data_ptr<float>();
   r.ss = ss.data_ptr<float>();
   r.part = part.data_ptr<float>();
+  const auto ad = pool_add_operand(add, add_off, dy, H, W, "maxpool_s2_bwd_bnred");
   dph::maxpool_s2_bwd_bnred(dy.data_ptr(), tap.data_ptr<uint8_t>(), dx.data_ptr(), N, H, W, C, (int)k, r,
-                            cur_stream());
+                            cur_stream(), ad.first, ad.second);
   return {dx, part};
 }
 
@@ -1131,7 +1150,8 @@ Tensor upcat_fwd(const Tensor& y2, const c10::optional<Tensor>& bias, const Tens
 }
 
 // dcat: channels-last [N, Co + Cs, Ho, Wo]; returns (dy2 [N*H*W, 4*Co], dskip channels-last [N, Cs, Ho, Wo])
-std::tuple<Tensor, Tensor> upcat_bwd(const Tensor& dcat, int64_t H, int64_t W, int64_t Co) {
+// want_skip false: dskip is an empty tensor and the kernel writes only dy2.
+std::tuple<Tensor, Tensor> upcat_bwd(const Tensor& dcat, int64_t H, int64_t W, int64_t Co, bool want_skip) {
   check_cuda(dcat, "dcat");
   c10::DeviceGuard g(dcat.device());
   TORCH_CHECK(dcat.dim() == 4 && dcat.is_contiguous(at::MemoryFormat::ChannelsLast), "upcat_bwd: channels-last dcat");
@@ -1140,9 +1160,10 @@ std::tuple<Tensor, Tensor> upcat_bwd(const Tensor& dcat, int64_t H, int64_t W, i
   TORCH_CHECK(Ho <= 4 * H && Wo <= 4 * W && 4 * Ho >= 2 * H && 4 * Wo >= 2 * W, "upcat_bwd: resize ratio outside [0.5, 2]");
   check_align16(dcat, "dcat");
   auto dy = at::empty({N * H * W, 4 * Co}, dcat.options());
-  auto dskip = at::empty({N, Cs, Ho, Wo}, dcat.options().memory_format(at::MemoryFormat::ChannelsLast));
-  dph::upcat_bwd(dcat.data_ptr(), dy.data_ptr(), dskip.data_ptr(), N, H, W, Co, Ho, Wo, Cs, dt_code(dcat),
-                 cur_stream());
+  auto dskip = want_skip ? at::empty({N, Cs, Ho, Wo}, dcat.options().memory_format(at::MemoryFormat::ChannelsLast))
+                         : at::empty({0}, dcat.options());
+  dph::upcat_bwd(dcat.data_ptr(), dy.data_ptr(), want_skip ? dskip.data_ptr() : nullptr, N, H, W, Co, Ho, Wo, Cs,
+                 dt_code(dcat), cur_stream());
   return {dy, dskip};
 }
 
@@ -1746,11 +1767,11 @@ TORCH_LIBRARY(dph, m) {
   m.def("maxpool_s2_fwd(Tensor x, int k) -> (Tensor, Tensor)");
   m.def("channel_sum(Tensor x, ScalarType out_dtype) -> Tensor");
   m.def("channel_sum_into_(Tensor x, Tensor(a!) out) -> ()");
-  m.def("maxpool_s2_bwd(Tensor dy, Tensor tap, int H, int W, int k) -> Tensor");
+  m.def("maxpool_s2_bwd(Tensor dy, Tensor tap, int H, int W, int k, Tensor? add=None, int add_off=0) -> Tensor");
   m.def("maxpool_s2_bwd_bnred(Tensor dy, Tensor tap, int H, int W, int k, Tensor x, Tensor mean, Tensor invstd, "
-        "Tensor ss) -> (Tensor, Tensor)");
+        "Tensor ss, Tensor? add=None, int add_off=0) -> (Tensor, Tensor)");
   m.def("upcat_fwd(Tensor y2, Tensor? bias, Tensor skip, int H, int W) -> Tensor");
-  m.def("upcat_bwd(Tensor dcat, int H, int W, int Co) -> (Tensor, Tensor)");
+  m.def("upcat_bwd(Tensor dcat, int H, int W, int Co, bool want_skip=True) -> (Tensor, Tensor)");
   m.def("bn_act_fwd(Tensor x, Tensor? res, Tensor? w, Tensor? b, Tensor(a!)? running_mean, Tensor(b!)? running_var, "
         "float momentum, float eps, bool relu, Tensor? pre_stats=None, Tensor(c!)? num_batches_tracked=None, "
         "Tensor(d!)? relu_mask_out=None, bool apply=True) "

@@ -189,7 +189,7 @@ void upcat_fwd(const void* y, const float* bias, const void* skip, void* out, in
 void upcat_bwd(const void* dcat, void* dy, void* dskip, int64_t N, int64_t H, int64_t W, int64_t Co, int64_t Ho,
                int64_t Wo, int64_t Cs, int dtype, hipStream_t st) {
   const int64_t total_y = N * H * W * 4 * (Co / 8);
-  const int64_t total = total_y + N * Ho * Wo * (Cs / 8);
+  const int64_t total = total_y + (dskip ? N * Ho * Wo * (Cs / 8) : 0);
   if (total <= 0) return;
   const UpCatDims d = make_dims(H, W, Co, Ho, Wo, Cs);
   DPH_DISPATCH_FLOAT(dtype, T, {

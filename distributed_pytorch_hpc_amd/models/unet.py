@@ -17,7 +17,7 @@ from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
 from ..ops.conv import BiasConv2d, BiasConvTranspose2d, BnGradSlot, StatsSlot
-from ..ops.pool import MaxPool2d
+from ..ops.pool import MaxPool2d, SkipGradSlot
 from ..ops.upsample import up_concat
 
 
@@ -29,8 +29,9 @@ class ConvBlock(nn.Sequential):
 
     def out_slot(self, y: torch.Tensor):
         """The second BatchNorm's slot (ops.conv.BnGradSlot) if ``y`` is this block's last output -- for a consumer
-        that is the output's only one (the up-path GEMM after the bottleneck and the decoder blocks, the output
-        convolution); the encoder blocks' outputs also feed a skip connection, so nobody takes theirs."""
+        that receives the output's whole gradient: the up-path GEMM after the bottleneck and the decoder blocks, the
+        output convolution, and an encoder block's max pooling when the skip connection's gradient is added in its
+        gather (ops.pool.SkipGradSlot)."""
         slot, key = getattr(self, "_dph_out", (None, None))
         self._dph_out = (None, None)
         if os.environ.get("DPH_UNET_OUT_FOLD", "1") == "0":   # A/B: those BatchNorms run their own reduction pass
@@ -82,18 +83,28 @@ class SimpleUNet(nn.Module):
         self.pool = MaxPool2d(2)   # channels-last HIP kernels (ops/pool.py)
 
     def forward(self, x):
+        # each encoder output feeds the pooling and the skip connection: the skip's gradient is added in the pooling's
+        # gather (ops.pool.SkipGradSlot), which then holds e's whole gradient and so also runs the block's last
+        # BatchNorm reduction
+        fold = self.training and os.environ.get("DPH_UNET_SKIP_FOLD", "1") != "0"
+        s1, s2, s3 = (SkipGradSlot(), SkipGradSlot(), SkipGradSlot()) if fold else (None, None, None)
         e1 = self.enc1(x)
-        e2 = self.enc2(self.pool(e1))
-        e3 = self.enc3(self.pool(e2))
-        bt = self.bottleneck(self.pool(e3))
+        e2 = self.enc2(self._pool(e1, self.enc1, s1))
+        e3 = self.enc3(self._pool(e2, self.enc2, s2))
+        bt = self.bottleneck(self._pool(e3, self.enc3, s3))
         # up-sample + resize + concat: one GEMM and one copy kernel per level on the GPU (ops/upsample.py); the
         # bottleneck / decoder outputs feed only the next GEMM, which then runs their last BatchNorm's reduction
-        d3 = self.dec3(up_concat(self.up3, bt, e3, bn_slot=_out_slot(self.bottleneck, bt)))
-        d2 = self.dec2(up_concat(self.up2, d3, e2, bn_slot=_out_slot(self.dec3, d3)))
-        d1 = self.dec1(up_concat(self.up1, d2, e1, bn_slot=_out_slot(self.dec2, d2)))
+        d3 = self.dec3(up_concat(self.up3, bt, e3, bn_slot=_out_slot(self.bottleneck, bt), skip_slot=s3))
+        d2 = self.dec2(up_concat(self.up2, d3, e2, bn_slot=_out_slot(self.dec3, d3), skip_slot=s2))
+        d1 = self.dec1(up_concat(self.up1, d2, e1, bn_slot=_out_slot(self.dec2, d2), skip_slot=s1))
         if isinstance(self.out, BiasConv2d):
             return self.out(d1, bn_slot=_out_slot(self.dec1, d1))
         return self.out(d1)
+
+    def _pool(self, e, block, skip_slot):
+        if skip_slot is None or not isinstance(self.pool, MaxPool2d):
+            return self.pool(e)
+        return self.pool(e, bn_slot=_out_slot(block, e), skip_slot=skip_slot)
 
 
 def _out_slot(block, y):

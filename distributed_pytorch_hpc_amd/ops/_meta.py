@@ -139,7 +139,7 @@ def _maxpool_s2_fwd(x, k):
 
 
 @register_fake("dph::maxpool_s2_bwd")
-def _maxpool_s2_bwd(dy, tap, H, W, k):
+def _maxpool_s2_bwd(dy, tap, H, W, k, add=None, add_off=0):
     n, c = dy.shape[:2]
     return dy.new_empty((n, c, H, W)).contiguous(memory_format=torch.channels_last)
 
@@ -151,10 +151,11 @@ def _upcat_fwd(y2, bias, skip, H, W):
 
 
 @register_fake("dph::upcat_bwd")
-def _upcat_bwd(dcat, H, W, Co):
+def _upcat_bwd(dcat, H, W, Co, want_skip=True):
     n, ct, ho, wo = dcat.shape
-    return (dcat.new_empty((n * H * W, 4 * Co)),
-            dcat.new_empty((n, ct - Co, ho, wo)).contiguous(memory_format=torch.channels_last))
+    dskip = (dcat.new_empty((n, ct - Co, ho, wo)).contiguous(memory_format=torch.channels_last) if want_skip
+             else dcat.new_empty((0,)))
+    return dcat.new_empty((n * H * W, 4 * Co)), dskip
 
 
 @register_fake("dph::channel_sum")
@@ -269,7 +270,7 @@ def _ts_gemm_nt_addmask(A, B, add, add_mask):
 
 
 @register_fake("dph::maxpool_s2_bwd_bnred")
-def _maxpool_s2_bwd_bnred(dy, tap, H, W, k, x, mean, invstd, ss):
+def _maxpool_s2_bwd_bnred(dy, tap, H, W, k, x, mean, invstd, ss, add=None, add_off=0):
     n, c = dy.shape[0], dy.shape[1]
     blocks = min(max((n * H * W * (c // 8) + 255) // 256, 1), 2048)   # csrc/dph_common.h stream_grid
     dx = dy.new_empty((n, c, H, W)).contiguous(memory_format=torch.channels_last)

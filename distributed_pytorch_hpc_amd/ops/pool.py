@@ -22,27 +22,55 @@ def maxpool3s2_native_ok(x: torch.Tensor) -> bool:
             and x.data_ptr() % 16 == 0)
 
 
+class SkipGradSlot:
+    """Hand-off of a SimpleUNet skip connection's gradient into the max-pooling backward of the same encoder output.
+
+    An encoder output e feeds the pooling and, as the skip, the decoder's up-sample + concat (ops/upsample.py);
+    autograd would sum the two gradients of e with a separate add kernel, after the concat's backward copied the skip's
+    slice out of d(concat).  With a slot, the pooling (on the kernel path) marks itself the ``pool`` in its forward,
+    the concat ``arms`` the slot in its own forward, and its backward -- which runs first -- leaves d(concat) in ``t``
+    (skip channels from ``off``) instead of returning the slice; the pooling's gather adds it before its store
+    (bitwise the bf16 sum autograd would form), so e receives one gradient and the slice is never copied."""
+
+    __slots__ = ("pool", "armed", "t", "off")
+
+    def __init__(self):
+        self.pool = self.armed = False
+        self.t = None
+        self.off = 0
+
+
 class _MaxPoolS2Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k, bn_slot=None):
+    def forward(ctx, x, k, bn_slot=None, skip_slot=None):
         y, tap = _lib.ops().maxpool_s2_fwd(x, k)
         ctx.save_for_backward(tap)
         ctx.hw, ctx.k, ctx.bn_slot = (x.shape[2], x.shape[3]), k, bn_slot
+        ctx.skip_slot = skip_slot
+        if skip_slot is not None:
+            skip_slot.pool = True
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (tap,) = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
+        add, off = None, 0
+        s = ctx.skip_slot
+        if s is not None and s.armed:
+            if s.t is None:
+                raise RuntimeError("MaxPool2d: skip gradient slot armed but empty (backward order)")
+            add, off = s.t, s.off
+            s.t, s.armed = None, False
         bn = ctx.bn_slot   # x is a BatchNorm + ReLU output: that BatchNorm's reduction runs in this gather
         n, c = dy.shape[0], dy.shape[1]
         if (bn is not None and bn.ss is not None and dy.dtype == torch.bfloat16 and 256 % (c // 8) == 0
                 and bn.usable(n * ctx.hw[0] * ctx.hw[1], c)):
             dx, bn.part = _lib.ops().maxpool_s2_bwd_bnred(dy, tap, ctx.hw[0], ctx.hw[1], ctx.k, bn.x, bn.mean,
-                                                          bn.invstd, bn.ss)
+                                                          bn.invstd, bn.ss, add, off)
             bn.mark(dx)
-            return dx, None, None
-        return _lib.ops().maxpool_s2_bwd(dy, tap, ctx.hw[0], ctx.hw[1], ctx.k), None, None
+            return dx, None, None, None
+        return _lib.ops().maxpool_s2_bwd(dy, tap, ctx.hw[0], ctx.hw[1], ctx.k, add, off), None, None, None
 
 
 def max_pool3s2(x: torch.Tensor) -> torch.Tensor:
@@ -63,14 +91,15 @@ class MaxPool2d(nn.MaxPool2d):
     """``nn.MaxPool2d`` whose 3x3 / stride 2 / padding 1 and 2x2 / stride 2 cases run the channels-last HIP
     kernels."""
 
-    def forward(self, x, bn_slot=None):
-        """``bn_slot`` (ops.conv.BnGradSlot): x is a training-mode BatchNorm + ReLU output consumed only here (the
-        ResNet stem); the BatchNorm's backward reduction then runs in this pooling's gradient gather."""
+    def forward(self, x, bn_slot=None, skip_slot=None):
+        """``bn_slot`` (ops.conv.BnGradSlot): x is a training-mode BatchNorm + ReLU output (the ResNet stem, a
+        SimpleUNet encoder block); the BatchNorm's backward reduction then runs in this pooling's gradient gather.
+        ``skip_slot`` (SkipGradSlot): x is also a SimpleUNet skip connection; its gradient is added in the gather."""
         k = {(3, 1): 3, (2, 0): 2}.get((_one(self.kernel_size), _one(self.padding)))
         fast = (k is not None and _one(self.stride) == 2 and _one(self.dilation) == 1 and not self.ceil_mode
                 and not self.return_indices)
         if fast and maxpool3s2_native_ok(x) and x.shape[2] >= k - 1 and x.shape[3] >= k - 1:
-            return _MaxPoolS2Fn.apply(x, k, bn_slot)
+            return _MaxPoolS2Fn.apply(x, k, bn_slot, skip_slot)
         return super().forward(x)
 
 

@@ -71,7 +71,7 @@ class _Params:
 
 class _UpConcatFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, skip, params=None, bn_slot=None):
+    def forward(ctx, x, weight, bias, skip, params=None, bn_slot=None, skip_slot=None):
         n, cin, h, w = x.shape
         co = weight.shape[1]
         x2 = x.permute(0, 2, 3, 1).reshape(n * h * w, cin)          # channels-last: a view
@@ -88,6 +88,10 @@ class _UpConcatFn(torch.autograd.Function):
         ctx.ts = ts
         ctx.params = params
         ctx.bn_slot = bn_slot
+        # the skip's other consumer (the encoder's max pooling, ops.pool.SkipGradSlot) adds its gradient from d(concat)
+        ctx.skip_slot = skip_slot if (skip_slot is not None and skip_slot.pool) else None
+        if ctx.skip_slot is not None:
+            skip_slot.armed = True
         return out
 
     @staticmethod
@@ -95,7 +99,10 @@ class _UpConcatFn(torch.autograd.Function):
         x2, wr = ctx.saved_tensors
         n, cin, h, w, co = ctx.dims
         dcat = dcat.contiguous(memory_format=torch.channels_last)
-        dy2, dskip = _lib.ops().upcat_bwd(dcat, h, w, co)
+        ss = ctx.skip_slot
+        dy2, dskip = _lib.ops().upcat_bwd(dcat, h, w, co, ss is None)
+        if ss is not None:
+            ss.t, ss.off, dskip = dcat, co, None
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             bn = ctx.bn_slot   # x is a BatchNorm + ReLU output consumed only here: its reduction in this epilogue
@@ -128,7 +135,7 @@ class _UpConcatFn(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             # straight into the bias's bucket view when the engine owns it (bias_grad), else returned in fp32
             db = bias_grad(prm.bias if prm is not None else None, dy2.view(-1, co), torch.float32)
-        return dx, dw, db, dskip, None, None
+        return dx, dw, db, dskip, None, None, None
 
 
 def up_concat_reference(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> torch.Tensor:
@@ -139,10 +146,11 @@ def up_concat_reference(up: nn.Module, x: torch.Tensor, skip: torch.Tensor) -> t
     return torch.cat([u, skip], dim=1)
 
 
-def up_concat(up: nn.Module, x: torch.Tensor, skip: torch.Tensor, bn_slot=None) -> torch.Tensor:
+def up_concat(up: nn.Module, x: torch.Tensor, skip: torch.Tensor, bn_slot=None, skip_slot=None) -> torch.Tensor:
     """``cat([resize(up(x), skip.shape[2:]), skip], 1)`` -- fused on the GPU when eligible.  ``bn_slot``
     (ops.conv.BnGradSlot): x is a BatchNorm + ReLU output consumed only here; its backward reduction then runs in the
-    input-gradient GEMM's epilogue."""
+    input-gradient GEMM's epilogue.  ``skip_slot`` (ops.pool.SkipGradSlot): the skip's gradient goes to its max
+    pooling's backward instead of being copied out of d(concat)."""
     if not up_concat_native_ok(up, x, skip):
         return up_concat_reference(up, x, skip)
     dt = torch.bfloat16
@@ -154,4 +162,4 @@ def up_concat(up: nn.Module, x: torch.Tensor, skip: torch.Tensor, bn_slot=None) 
     prm = _Params(up.weight, up.bias) if wt is up.weight and os.environ.get("DPH_UPCAT_DIRECT", "1") != "0" else None
     with torch.autocast("cuda", enabled=False):
         return _UpConcatFn.apply(x if x.dtype == dt else x.to(dt), wt, b, skip, prm,
-                                 bn_slot if x.dtype == dt else None)
+                                 bn_slot if x.dtype == dt else None, skip_slot)

@@ -369,9 +369,10 @@ def test_unet_conv_block_first_bn_reduced_in_second_conv(dph_native, monkeypatch
 
 
 def test_simple_unet_all_bn_reductions_in_consumers(dph_native, monkeypatch):
-    """Whole SimpleUNet: every block's first BatchNorm reduces in its second convolution (7), and the bottleneck /
-    decoder blocks' last BatchNorm in the up-path GEMM or the output 1x1 convolution (4); gradients match the
-    BatchNorms' own reduction passes."""
+    """Whole SimpleUNet: every block's first BatchNorm reduces in its second convolution (7), the bottleneck /
+    decoder blocks' last BatchNorm in the up-path GEMM or the output 1x1 convolution (4), and the encoder blocks' last
+    BatchNorm in the max pooling's gather, which also adds the skip gradient (3); gradients match the BatchNorms' own
+    reduction passes."""
     from distributed_pytorch_hpc_amd.models.unet import SimpleUNet, to_channels_last
 
     torch.manual_seed(5)
@@ -382,11 +383,62 @@ def test_simple_unet_all_bn_reductions_in_consumers(dph_native, monkeypatch):
     gx0, g0 = _grads(net, x, monkeypatch, False)
     assert cnt.used == 0
     gx1, g1 = _grads(net, x, monkeypatch, True)
-    assert cnt.used == 11
+    assert cnt.used == 14
     assert rel_err(gx1, gx0) < 2e-2
     num = sum((g1[n] - g0[n]).norm() ** 2 for n in g0) ** 0.5
     den = sum(g0[n].norm() ** 2 for n in g0) ** 0.5
     assert num / den < 1e-2
+
+
+def test_simple_unet_skip_gradient_in_pool_is_bitwise(dph_native, monkeypatch):
+    """The skip connection's gradient added in the max pooling's gather (ops.pool.SkipGradSlot) instead of autograd's
+    add: with the BatchNorms' own reductions (DPH_BN_EPILOGUE=0) the input and parameter gradients are bitwise the
+    same as with the copy + add."""
+    from distributed_pytorch_hpc_amd.models.unet import SimpleUNet, to_channels_last
+
+    torch.manual_seed(6)
+    net = to_channels_last(SimpleUNet(65, 65, 64).to(DEV).to(torch.bfloat16))
+    x = torch.randn(2, 65, 45, 90, device=DEV, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last).requires_grad_()
+    monkeypatch.setenv("DPH_UNET_SKIP_FOLD", "0")
+    gx0, g0 = _grads(net, x, monkeypatch, False)
+    monkeypatch.setenv("DPH_UNET_SKIP_FOLD", "1")
+    gx1, g1 = _grads(net, x, monkeypatch, False)
+    assert torch.equal(gx1, gx0)
+    for n in g0:
+        assert torch.equal(g1[n], g0[n]), n
+
+
+@pytest.mark.parametrize("k,C,H,W", [(2, 64, 45, 90), (2, 256, 12, 23), (3, 64, 28, 28)])
+def test_maxpool_bwd_add_operand(dph_native, k, C, H, W):
+    """maxpool_s2_bwd / maxpool_s2_bwd_bnred with a second gradient read from a channel slice of a wider tensor:
+    bitwise the bf16 sum of the plain gather and the slice; the BatchNorm partials match a float64 reduction of it."""
+    torch.manual_seed(C + H)
+    ops = torch.ops.dph
+    N, off = 2, 32
+    x = torch.randn(N, C, H, W, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    _, tap = ops.maxpool_s2_fwd(x, k)
+    ho, wo = (H - 1) // 2 + 1 if k == 3 else H // 2, (W - 1) // 2 + 1 if k == 3 else W // 2
+    dy = torch.randn(N, C, ho, wo, device=DEV, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wide = torch.randn(N, off + C + 16, H, W, device=DEV, dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    sl = wide[:, off:off + C]
+    ref = ops.maxpool_s2_bwd(dy, tap, H, W, k) + sl
+    got = ops.maxpool_s2_bwd(dy, tap, H, W, k, wide, off)
+    assert torch.equal(got, ref)
+    mean = torch.randn(C, device=DEV) * 0.1
+    invstd = torch.rand(C, device=DEV) + 0.5
+    ss = torch.cat([torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1])
+    dx, part = ops.maxpool_s2_bwd_bnred(dy, tap, H, W, k, x, mean, invstd, ss, wide, off)
+    assert torch.equal(dx, ref)
+    xf = x.double().permute(0, 2, 3, 1).reshape(-1, C)
+    on = (xf * ss[:C].double() + ss[C:].double()) > 0
+    dz = torch.where(on, dx.double().permute(0, 2, 3, 1).reshape(-1, C), torch.zeros((), device=DEV,
+                                                                                    dtype=torch.float64))
+    xhat = (xf - mean.double()) * invstd.double()
+    p = part.double().sum(0)
+    assert rel_err(p[:C], dz.sum(0)) < 1e-4
+    assert rel_err(p[C:], (dz * xhat).sum(0)) < 1e-4
 
 
 @pytest.mark.parametrize("M,K,N", [(50176 // 8, 1024, 256), (12544 // 4 + 37, 2048, 512), (777, 1024, 128)])
