@@ -61,11 +61,14 @@ def main():
         t_gf = _time(lambda: ops.convg_nt(x, w, geo, True), a.iters)
         t_gd = _time(lambda: ops.convg_nt(dy, wt, geo, False), a.iters)
         t_c = _time(lambda: dst.copy_(src), a.iters) / 2          # read + write of the same byte count
+        # the vendor library on the same products (no statistics epilogue): forward X W^T and dgrad dY W
+        t_bf = _time(lambda: torch.matmul(x, w.t()), a.iters)
+        t_bd = _time(lambda: torch.matmul(dy, w), a.iters)
         gb = M * (cin + cout) * 2 / 1e9
         row = dict(cin=cin, cout=cout, hw=hw, count=cnt, fwd_ms=round(t_f, 4), dgrad_ms=round(t_d, 4),
                    fwd_TBps=round(gb / t_f, 2), dgrad_TBps=round(gb / t_d, 2), copy_TBps=round(gb / t_c, 2),
                    fwd_tflops=round(2 * M * cin * cout / t_f / 1e9, 1), convg_fwd_ms=round(t_gf, 4),
-                   convg_dgrad_ms=round(t_gd, 4))
+                   convg_dgrad_ms=round(t_gd, 4), blas_fwd_ms=round(t_bf, 4), blas_dgrad_ms=round(t_bd, 4))
         print(json.dumps(row), flush=True)
         tot["fwd"] += cnt * t_f
         tot["dgrad"] += cnt * t_d
@@ -73,6 +76,8 @@ def main():
         tot["convg_fwd"] += cnt * t_gf
         tot["convg_dgrad"] += cnt * t_gd
         tot["best"] += cnt * (min(t_f, t_gf) + min(t_d, t_gd))
+        tot["blas_fwd"] = tot.get("blas_fwd", 0.0) + cnt * t_bf
+        tot["blas_dgrad"] = tot.get("blas_dgrad", 0.0) + cnt * t_bd
         del x, w, dy, wt, src, dst
     print(json.dumps({k + "_ms_per_step": round(v, 3) for k, v in tot.items()}))
 
