@@ -861,7 +861,13 @@ static void c3w_launch(int ns, unsigned nblk, hipStream_t st, const void* A, con
   c3w_go<TCO, GEN, SL, 2>(nblk, st, A, B, P, M, N, K, lda, ldb, chunk, H, W, cin, g);
 }
 // resident workgroups per round: 2 per CU with the two-stage ring, 1 with a deeper one
-static int64_t c3w_round(int ns) { return ns > 2 ? 256 : 512; }
+static int64_t g_c3w_round = 512;   // workgroup slots of one round with the two-stage ring (c3w_round_set)
+static int64_t c3w_round(int ns) { return ns > 2 ? g_c3w_round / 2 : g_c3w_round; }
+int64_t c3w_round_set(int64_t slots) {
+  const int64_t prev = g_c3w_round;
+  if (slots > 0) g_c3w_round = slots;
+  return prev;
+}
 // pixel-chunk splits: as many as fill ONE resident round (floor -- rounding up, e.g. 22 x 24 tiles = 528 workgroups
 // for 512 slots, started a second round that cost a whole workgroup's time for 16 workgroups), chunks >= 512 rows
 static int64_t c3w_split_count(int64_t M, int64_t tiles, int ns) {

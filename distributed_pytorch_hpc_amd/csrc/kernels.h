@@ -189,6 +189,9 @@ struct ConvGeo;
 ConvGeo gemm1_identity_geo(int64_t M);
 bool gemm1_lds_preferred(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 bool gemm1_lds_set(bool on);   // returns the previous setting
+// Workgroup slots per round that the LDS-DMA weight-gradient kernels' pixel-chunk split count fills (default 512 = two
+// per CU); slots <= 0 only queries.  Returns the previous value.
+int64_t c3w_round_set(int64_t slots);
 // 3x3 implicit GEMM with an LDS-DMA pipeline (csrc/conv3x3.hip); ts_gemm_nt's H, W > 0 path when supported.
 bool conv3_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 void conv3_gemm(const void* A, const void* B, void* C, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,

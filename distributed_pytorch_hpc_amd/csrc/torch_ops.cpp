@@ -1524,6 +1524,7 @@ int64_t car_agreed_op(int64_t ctx) { return dph::car_agreed(ctx); }
 int64_t attn_variant_op(int64_t v) { return dph::attn_set_variant((int)v); }
 int64_t gemm_nt_variant_op(int64_t v) { return dph::gemm_nt_set_variant((int)v); }
 int64_t gemm1_lds_op(int64_t on) { return dph::gemm1_lds_set(on != 0) ? 1 : 0; }
+int64_t c3w_round_op(int64_t slots) { return dph::c3w_round_set(slots); }
 void car_destroy_op(int64_t ctx) { dph::car_destroy(ctx); }
 
 }  // namespace
@@ -1798,6 +1799,7 @@ TORCH_LIBRARY(dph, m) {
   m.def("attn_variant(int v) -> int", &attn_variant_op);
   m.def("gemm_nt_variant(int v) -> int", &gemm_nt_variant_op);
   m.def("gemm1_lds(int on) -> int", &gemm1_lds_op);
+  m.def("c3w_round(int slots) -> int", &c3w_round_op);
   m.def("car_flag(int ctx, Tensor(a!) flag) -> ()");
   m.def("car_poison(int ctx, Tensor flag, Tensor(a!) gscale) -> ()");
   m.def("car_destroy(int ctx) -> ()", &car_destroy_op);

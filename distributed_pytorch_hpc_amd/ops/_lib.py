@@ -51,6 +51,8 @@ def load(build_if_missing: bool = False) -> bool:
 
         if os.environ.get("DPH_GEMM1_LDS", "1") == "0":   # deep-K 1x1 GEMMs back on ts_nt_k (A/B, docs/guide/knobs.md)
             torch.ops.dph.gemm1_lds(0)
+        if os.environ.get("DPH_C3W_ROUND"):   # weight-gradient split count: workgroup slots per round (A/B)
+            torch.ops.dph.c3w_round(int(os.environ["DPH_C3W_ROUND"]))
         _loaded = True
         return True
 

@@ -7,7 +7,8 @@ from torch._subclasses.fake_tensor import FakeTensorMode
 
 # resource-management / configuration ops with no tensor arguments (catch-all kernels, nothing to trace)
 NO_TENSOR_OPS = {"gemm_tn_tail_", "gemm_tn_plan_info", "car_create", "car_ipc_handle", "car_open",
-                 "car_status", "car_destroy", "car_agreed", "attn_variant", "gemm_nt_variant", "gemm1_lds"}
+                 "car_status", "car_destroy", "car_agreed", "attn_variant", "gemm_nt_variant", "gemm1_lds",
+                 "c3w_round"}
 
 
 @pytest.fixture(scope="module")
