@@ -125,3 +125,37 @@ def test_latitude_weighted_mse_cpu_reference():
     pg, tg = p[:, :, :180], t[:, :, :180]
     wg = latitude_weights(180).view(1, 1, -1, 1)
     torch.testing.assert_close(sum(parts) / 3, (wg * (pg - tg) ** 2).mean())
+
+
+def test_unet_block_output_slot_handoff_cpu(monkeypatch):
+    """ConvBlock.out_slot: the second BatchNorm's slot goes to exactly one taker of exactly that output tensor, and
+    DPH_UNET_OUT_FOLD=0 withholds it.  On the CPU SimpleUNet's gradients are identical with and without the skip
+    slots (they arm only on the GPU kernel paths)."""
+    from distributed_pytorch_hpc_amd.models.unet import SimpleUNet, conv_block
+    from distributed_pytorch_hpc_amd.ops.conv import BnGradSlot
+
+    torch.manual_seed(0)
+    blk = conv_block(8, 16).train()
+    x = torch.randn(2, 8, 6, 10)
+    y = blk(x)
+    other = y.clone()
+    assert blk.out_slot(other) is None          # a different tensor: no slot (and the offer is withdrawn)
+    y = blk(x)
+    s = blk.out_slot(y)
+    assert isinstance(s, BnGradSlot)
+    assert blk.out_slot(y) is None              # taken once
+    monkeypatch.setenv("DPH_UNET_OUT_FOLD", "0")
+    y = blk(x)
+    assert blk.out_slot(y) is None
+    monkeypatch.delenv("DPH_UNET_OUT_FOLD")
+
+    net = SimpleUNet(3, 3, 8).train()
+    inp = torch.randn(2, 3, 12, 20)
+    g = {}
+    for fold in ("1", "0"):
+        monkeypatch.setenv("DPH_UNET_SKIP_FOLD", fold)
+        net.zero_grad(set_to_none=True)
+        net(inp).square().mean().backward()
+        g[fold] = [p.grad.clone() for p in net.parameters()]
+    for a, b in zip(g["1"], g["0"]):
+        assert torch.equal(a, b)
